@@ -1,0 +1,213 @@
+"""Benchmark: valid RRT edge extensions/s (collision + NN), BASELINE.json config 2.
+
+Workload (one "step" = one batched RRT round on the device, motionplanningtoolkit_amd.RRTEngine):
+  blimp agent (blimp.3ds, all 1355 triangles) in the single-room environment (model.dae,
+  316 triangles), tree of 100k synthetic states ~ U(Blimp::getStateVarRanges), K = 65536
+  extensions per round: uniform sample -> exact 1-NN over the 100k-node tree -> randomSteer
+  -> getPoses -> FCL-semantics collision -> ordered append of the collision-free edges.
+  The tree is reset to its 100k base at the start of every round (inside the timed step)
+  so every round does identical work.
+
+Multi-GPU: one process per GPU (torchrun), each rank runs its own seed (independent
+trees, weak scaling); the only collective is the final max/sum reduction of timings and
+counters (RCCL), outside the data path.
+
+Prints ONE JSON line (rank 0).  See DESIGN.md "Measurement" for the roofline definition.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+FP64_PEAK_TFLOPS = 78.6   # MI355X FP64 (vector = matrix), AMD public spec; FMA counted as 2
+HBM_PEAK_GBS = 8000.0     # MI355X_MICROARCH.md: 8.0 TB/s spec
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=65536, help="extensions per round (K)")
+    ap.add_argument("--tree", type=int, default=100_000, help="tree nodes at the start of each round (N0)")
+    ap.add_argument("--seed", type=int, default=1000)
+    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample length")
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--traffic", default=os.path.join(REPO, "profiles", "traffic.json"))
+    return ap.parse_args()
+
+
+def cpu_baseline(sc, tree, K_gpu, seed, target_s):
+    """The oracle (C port of the reference's FCL+FLANN semantics) on the host: the same
+    round on a bounded sample of extensions, 1 thread (the reference is single-threaded),
+    kd-tree NN built once per round (FLANN KDTreeSingleIndex-like), AABB-tree collision."""
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import oracle as orc
+
+    bvh = orc.BVH(sc.env_tris)
+    n0 = tree.shape[0]
+
+    def run(K, threads):
+        nodes = np.zeros((n0 + K, sc.dim))
+        nodes[:n0] = tree
+        par = np.zeros(n0 + K, np.int32)
+        t = time.perf_counter()
+        n, _, _ = orc.engine_step(sc.kind, sc.prm, sc.ranges, sc.steer_dt, sc.cc_dt, seed, 0, K, bvh, sc.env_tf,
+                                  sc.agent_tris, nodes, par, n0, nthreads=threads, use_kdtree=True)
+        return time.perf_counter() - t, n - n0
+
+    t0, _ = run(256, 1)
+    K = int(min(max(256 * target_s / max(t0, 1e-3), 256), K_gpu))
+    t1, valid1 = run(K, 1)
+    threads = os.cpu_count() or 1
+    threads = min(threads, 16)
+    tn, validn = run(K, threads)
+    return {
+        "value": valid1 / t1, "unit": "valid extensions/s", "cores": 1, "kind": "port",
+        "sample": f"{K} extensions of the same blimp round (100k-node tree, kd-tree NN built per round, "
+                  f"AABB-tree + FCL tri-tri SAT), oracle/mpt_oracle.c, {t1:.2f} s",
+        "all_cores": {"value": validn / tn, "cores": threads, "seconds": round(tn, 3)},
+        "cpu": _cpu_model(),
+    }
+
+
+def _cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def main():
+    args = parse()
+    import torch
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    import motionplanningtoolkit_amd as mpt
+    from motionplanningtoolkit_amd import scenes
+
+    mpt.init(local)
+    torch.cuda.set_device(local)
+    stream = torch.cuda.current_stream()
+
+    sc = scenes.blimp_scenario("all")
+    seed = args.seed + rank
+    rng = np.random.default_rng(seed)
+    n0, K = args.tree, args.batch
+    tree = rng.uniform(sc.ranges[:, 0], sc.ranges[:, 1], size=(n0, sc.dim))
+    env = mpt.Environment(sc.env_tris, sc.env_tf)
+    agent = mpt.AgentMesh(sc.agent_tris)
+    eng = mpt.RRTEngine(env, agent, sc.kind, sc.prm, sc.ranges, sc.steer_dt, sc.cc_dt, n0 + K, seed)
+    eng.add_nodes(tree)
+    eng.enable_timing(True)
+
+    def round_():
+        eng.set_size(n0, stream)
+        eng.step(K, stream)
+
+    for _ in range(args.warmup):
+        round_()
+    torch.cuda.synchronize()
+    c0 = eng.counters()
+
+    ktimes = {}
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        round_()
+        for k, v in eng.kernel_times().items():  # hipEvents on the launch stream
+            ktimes[k] = ktimes.get(k, 0.0) + v
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    c1 = eng.counters()
+    valid = c1["valid"] - c0["valid"]
+    checked = c1["checked"] - c0["checked"]
+
+    if dist:
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        s = torch.tensor([valid, checked], dtype=torch.float64, device="cuda")
+        dist.all_reduce(s, op=dist.ReduceOp.SUM)
+        valid, checked = int(s[0].item()), int(s[1].item())
+
+    if rank != 0:
+        if dist:
+            dist.destroy_process_group()
+        return
+
+    steps = args.steps
+    per_launch = {k: v / steps for k, v in ktimes.items()}
+    dominant = max(("nn", "collide", "steer", "append", "sample"), key=lambda k: per_launch.get(k, 0.0))
+    d = sc.dim
+    if dominant == "nn":
+        flops = float(K) * n0 * 3 * d  # 3*d*N FP64 ops per query (sub, mul, add)
+        achieved = flops / (per_launch["nn"] * 1e-3) / 1e12
+        roof = {"bound": "mfma", "achieved": round(achieved, 3), "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
+                "frac": round(achieved / FP64_PEAK_TFLOPS, 4), "traffic": None, "kernel": "k_knn1<7> (+merge)",
+                "note": "FP64 VALU (no MFMA: FLANN's L2 op order is not a dot product); no-FMA ceiling 39.3 TFLOP/s"}
+    else:
+        roof = {"bound": "hbm", "achieved": None, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": None,
+                "traffic": None, "kernel": dominant}
+    try:
+        tr = json.load(open(args.traffic))
+        roof["traffic"] = tr.get(roof["kernel"].split()[0], tr.get("traffic"))
+    except (OSError, ValueError):
+        pass
+
+    out = {
+        "metric": "valid RRT edge extensions/sec (collision+NN) per node, 1/2/4/8 MI355X",
+        "value": valid / elapsed,
+        "unit": "valid extensions/s",
+        "n_gpus": world,
+        "steps": steps,
+        "warmup": args.warmup,
+        "ms_per_step": 1e3 * elapsed / steps,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic (uniform samples and tree states over Blimp::getStateVarRanges; meshes from the reference)",
+        "config": {"workload": "blimp.inst: blimp (1355 tris) vs single-room env (model.dae, 316 tris), "
+                               "batched RRT round over a 100k-node tree",
+                   "tree_nodes": n0, "extensions_per_round": K, "seed_base": args.seed,
+                   "parallelism": f"independent seeds x{world}"},
+        "checked_per_s": checked / elapsed,
+        "valid_fraction": valid / max(checked, 1),
+        "kernel_ms_per_round": {k: round(v, 4) for k, v in per_launch.items() if k != "reserved"},
+        "roofline": roof,
+    }
+    if not args.no_cpu and world == 1:
+        out["cpu_baseline"] = cpu_baseline(sc, tree, K, seed, args.cpu_seconds)
+    else:
+        out["cpu_baseline"] = None
+    print(json.dumps(out))
+    if dist:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,158 @@
+/*
+ * mpt.h -- C ABI of libmpt.so, the MI355X (gfx950) hot path of the RRT/PRM inner loop.
+ *
+ * Drop-in boundary: the reference composes its planner from header-only templates
+ * (main.cpp:38-76) and reaches native code through three seams.  Each entry point
+ * below replaces one of them:
+ *
+ *   collision  MeshHandler::isInCollision            utilities/meshhandler.hpp:187-243
+ *              (via Map3D::safeEdge                  workspaces/map3d.hpp:33-37,
+ *               fcl_helpers::defaultCollisionFunction utilities/fcl_helpers.hpp:52-65)
+ *              StaticEnvironmentMeshHandler ctor     utilities/meshhandler.hpp:18-55
+ *              SimpleAgentMeshHandler ctor           utilities/meshhandler.hpp:114-135
+ *   NN         FLANN_KDTreeWrapper ctor/insertPoint  utilities/flannkdtreewrapper.hpp:21-40
+ *              removePoint                           utilities/flannkdtreewrapper.hpp:42-50
+ *              nearest/kNearest                      utilities/flannkdtreewrapper.hpp:57-89
+ *              kNearestWithin                        utilities/flannkdtreewrapper.hpp:91-117
+ *   RRT loop   RRT::query hot loop                   planners/rrt.hpp:42-94 (batched engine)
+ *
+ * Conventions
+ *   - Plain C types only; `stream` is a hipStream_t passed as void* (NULL = default stream).
+ *   - Functions without a `_device` suffix take HOST pointers, copy in/out and return
+ *     when the results are in host memory.  `_device` variants take DEVICE pointers and
+ *     are asynchronous on `stream` (graph-capturable unless stated otherwise).
+ *   - Every function returns mpt_status (0 = OK); the message of the last failure on the
+ *     calling thread is mpt_last_error().  Nothing throws or exits across the ABI (the
+ *     reference exit()s on bad meshes/keys: meshhandler.hpp:22, instancefilemap.hpp:47).
+ *   - Transforms are 12 doubles: R (3x3 row-major, fcl::Matrix3f(i,j) = R[3i+j]) then T.
+ *   - Triangle soups are [n][9] doubles (three vertices) in the mesh-local frame.
+ *   - NN ids are 1-based in insertion order (FLANN_KDTreeWrapper::currentPointIndex
+ *     starts at 1); squared L2 distances in FLANN L2<double> accumulation order.
+ *
+ * Threading: one handle per host thread; calls on a handle are stream-ordered.
+ */
+#ifndef MPT_H
+#define MPT_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef int32_t mpt_status;
+enum {
+    MPT_OK = 0,
+    MPT_ERR_INVALID = 1,   /* bad argument / shape */
+    MPT_ERR_HIP = 2,       /* HIP runtime error */
+    MPT_ERR_NO_DEVICE = 3, /* no gfx950 device / extension not usable */
+    MPT_ERR_CAPACITY = 4,  /* capacity exceeded */
+    MPT_ERR_INTERNAL = 5
+};
+
+typedef struct mpt_env mpt_env;
+typedef struct mpt_agent mpt_agent;
+typedef struct mpt_nn mpt_nn;
+typedef struct mpt_rrt mpt_rrt;
+
+/* ---- runtime ---- */
+mpt_status mpt_init(int32_t device);
+const char *mpt_last_error(void);
+/* ABI version (major*100 + minor). */
+int32_t mpt_version(void);
+mpt_status mpt_device_synchronize(void);
+
+/* ---- collision: StaticEnvironmentMeshHandler / SimpleAgentMeshHandler / isInCollision ---- */
+/* Environment soup (all submeshes concatenated: they share one transform, meshhandler.hpp:27-49).
+ * tf12 = parseTransform("x y z qw qx qy qz") as R|T (mpt_transform_from_location). */
+mpt_status mpt_env_create(const double *tris, int64_t n_tris, const double tf12[12], mpt_env **out);
+mpt_status mpt_env_destroy(mpt_env *env);
+/* env statistics: [n_tris, n_bvh_nodes, bvh_depth] */
+mpt_status mpt_env_info(const mpt_env *env, int64_t info[3]);
+/* Agent link mesh in its local frame (SimpleAgentMeshHandler keeps ONE submesh). */
+mpt_status mpt_agent_create(const double *tris, int64_t n_tris, mpt_agent **out);
+mpt_status mpt_agent_destroy(mpt_agent *agent);
+/* fcl_helpers::parseTransform: loc7 = {x, y, z, qw, qx, qy, qz} -> tf12 (Quaternion3f::toRotation). */
+mpt_status mpt_transform_from_location(const double loc7[7], double tf12[12]);
+
+/* Batched Map3D::safeEdge / MeshHandler::isInCollision(env, links, poses):
+ *   links[L]            agent mesh of each link (Agent::getMeshes())
+ *   poses               [sum_P][L][12]   (Agent::getPoses(edge, dt) for every edge, concatenated)
+ *   edge_pose_offsets   [E+1]            poses of edge e are [off[e], off[e+1])
+ *   verdict_out         [E]              1 = in collision (safeEdge == false), 0 = safe
+ * An edge with no poses is safe (the reference Blimp case, agents/blimp.hpp:219-223). */
+mpt_status mpt_collide_batch(const mpt_env *env, const mpt_agent *const *links, int32_t L,
+                             const double *poses, const int64_t *edge_pose_offsets, int64_t E,
+                             uint8_t *verdict_out, void *stream);
+/* Device-pointer variant: poses, edge_pose_offsets, verdict_out in device memory;
+ * total_poses = edge_pose_offsets[E] (passed so no device->host read is needed). */
+mpt_status mpt_collide_batch_device(const mpt_env *env, const mpt_agent *const *links, int32_t L,
+                                    const double *d_poses, const int64_t *d_edge_pose_offsets, int64_t E,
+                                    int64_t total_poses, uint8_t *d_verdict_out, void *stream);
+/* Collision statistics of the last collide call on this thread (synchronises):
+ * [units, clusters, bvh node visits, triangle-pair tests]; enabled by mpt_set_stats(1). */
+mpt_status mpt_set_stats(int32_t enable);
+mpt_status mpt_last_collide_stats(uint64_t stats[4]);
+
+/* ---- NN: FLANN_KDTreeWrapper ---- */
+mpt_status mpt_nn_create(int32_t dim, int64_t capacity, mpt_nn **out);
+mpt_status mpt_nn_destroy(mpt_nn *nn);
+/* insertPoint for n points [n][dim]; ids_out[i] = assigned 1-based id (may be NULL). */
+mpt_status mpt_nn_append(mpt_nn *nn, const double *pts, int64_t n, int32_t *ids_out);
+mpt_status mpt_nn_append_device(mpt_nn *nn, const double *d_pts, int64_t n, void *stream);
+/* flann::Index::removePoint(id - 1) for a 1-based id: the point is skipped by queries. */
+mpt_status mpt_nn_remove(mpt_nn *nn, int32_t id);
+mpt_status mpt_nn_size(const mpt_nn *nn, int64_t *n_out);
+/* Device pointer of the [capacity][dim] point array (for zero-copy engines / tests). */
+mpt_status mpt_nn_points_device(const mpt_nn *nn, const double **d_pts);
+/* kNearest / nearest (k = 1): ids [nq][k] (-1 when fewer than k points), d2 [nq][k] (+inf). */
+mpt_status mpt_nn_knn(mpt_nn *nn, const double *q, int64_t nq, int32_t k, int32_t *ids, double *d2,
+                      void *stream);
+mpt_status mpt_nn_knn_device(mpt_nn *nn, const double *d_q, int64_t nq, int32_t k, int32_t *d_ids,
+                             double *d_d2, void *stream);
+/* kNearestWithin: points with d2 < r2 (note: the reference passes `radius` straight to a
+ * squared-distance index, so its argument IS r2), at most max_nb (> 0) nearest per query,
+ * each list sorted by (d2, id).  offsets [nq+1]; ids/d2 written up to cap entries; the
+ * total is offsets[nq].  Synchronises (list sizes are data dependent). */
+mpt_status mpt_nn_radius(mpt_nn *nn, const double *q, int64_t nq, double r2, int32_t max_nb,
+                         int64_t *offsets, int32_t *ids, double *d2, int64_t cap, void *stream);
+
+/* ---- batched RRT engine (planners/rrt.hpp:42-94, K extensions per round) ---- */
+enum { MPT_AGENT_OMNI = 0, MPT_AGENT_BLIMP = 1, MPT_AGENT_SNAKE = 2 };
+/* prm (7 doubles): blimp {length, vmin, vmax, psimin, psimax, vzmin, vzmax};
+ *                  snake {trailerCount, trailerLength, hitchLength, vmin, vmax, psimin, psimax};
+ *                  omni  ignored.
+ * ranges [dim][2] = Agent::getStateVarRanges(Map3D::getBounds()).
+ * The engine holds one tree of up to `capacity` nodes on the device. */
+mpt_status mpt_rrt_create(const mpt_env *env, const mpt_agent *agent, int32_t agent_kind, const double prm[7],
+                          const double *ranges, int32_t dim, double steer_dt, double cc_dt, int64_t capacity,
+                          uint64_t seed, mpt_rrt **out);
+mpt_status mpt_rrt_destroy(mpt_rrt *rrt);
+/* Append n tree nodes [n][dim] with parent ids (NULL = 0). */
+mpt_status mpt_rrt_add_nodes(mpt_rrt *rrt, const double *states, const int32_t *parents, int64_t n);
+/* Set the node count (truncate) without a host sync. */
+mpt_status mpt_rrt_set_size(mpt_rrt *rrt, int64_t n, void *stream);
+/* One batched round: K uniform samples -> exact 1-NN -> randomSteer -> getPoses ->
+ * collision -> ordered append of the collision-free edges.  Asynchronous. */
+mpt_status mpt_rrt_step(mpt_rrt *rrt, int32_t K, void *stream);
+/* counters [8]: rounds, extensions checked, extensions valid, nodes, capacity drops,
+ * pose overflow, reserved, reserved.  Synchronises. */
+mpt_status mpt_rrt_counters(mpt_rrt *rrt, uint64_t counters[8]);
+/* Copy out the first n nodes and parents (1-based parent ids, 0 for roots). Synchronises. */
+mpt_status mpt_rrt_read_tree(mpt_rrt *rrt, double *states, int32_t *parents, int64_t n);
+/* Intermediates of the last round for verification (host copies, synchronises):
+ * samples [K][dim], nn ids [K], ends [K][dim], verdicts [K]; any pointer may be NULL. */
+mpt_status mpt_rrt_last_round(mpt_rrt *rrt, double *samples, int32_t *nn_ids, double *ends, uint8_t *verdicts);
+/* Pose slots of the last round: poses [K][pmax][L][12], pose counts [K]; pmax/L via info. */
+mpt_status mpt_rrt_last_poses(mpt_rrt *rrt, double *poses, int32_t *pose_counts);
+/* [dim, links L, pose slots per edge pmax, capacity] */
+mpt_status mpt_rrt_info(const mpt_rrt *rrt, int64_t info[4]);
+/* Per-kernel device times (ms) of the last round, recorded with hipEvents on the launch
+ * stream when timing is enabled: [sample, nn, nn_merge, steer, collide, append]. */
+mpt_status mpt_rrt_enable_timing(mpt_rrt *rrt, int32_t enable);
+mpt_status mpt_rrt_kernel_times(mpt_rrt *rrt, float ms[6]);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MPT_H */

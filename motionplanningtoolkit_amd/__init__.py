@@ -1,0 +1,32 @@
+"""motionplanningtoolkit_amd -- the RRT/PRM inner loop of csbence/motionplanningtoolkit
+(batched FCL-semantics mesh collision + FLANN-semantics nearest neighbours) as HIP
+kernels for MI355X (gfx950) behind a C ABI (include/mpt.h), with the reference's
+Agent / Sampler / TreeInterface / `.inst` surface kept in C++ (csrc/host/).
+
+See DESIGN.md for the path, the data layout and the kernels.
+"""
+from ._native import LIB_PATH, MptError, build, lib  # noqa: F401
+from .api import (  # noqa: F401
+    AGENT_BLIMP,
+    AGENT_OMNI,
+    AGENT_SNAKE,
+    AgentMesh,
+    Environment,
+    NearestNeighbors,
+    RRTEngine,
+    collide_batch,
+    collide_batch_device,
+    init,
+    last_collide_stats,
+    load_mesh,
+    rrt_inst,
+    set_collide_stats,
+    synchronize,
+    transform_from_location,
+)
+
+__all__ = [
+    "AGENT_OMNI", "AGENT_BLIMP", "AGENT_SNAKE", "AgentMesh", "Environment", "NearestNeighbors", "RRTEngine",
+    "collide_batch", "collide_batch_device", "init", "last_collide_stats", "load_mesh", "rrt_inst",
+    "set_collide_stats", "synchronize", "transform_from_location", "build", "lib", "LIB_PATH", "MptError",
+]

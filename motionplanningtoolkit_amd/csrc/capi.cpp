@@ -1,0 +1,608 @@
+// capi.cpp -- extern "C" boundary (include/mpt.h): handles, host<->device copies, BVH
+// and cluster construction for the environment and agent meshes.
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <mutex>
+#include <numeric>
+#include <string>
+#include <vector>
+
+#include "../../include/mpt.h"
+#include "mpt_internal.h"
+
+namespace mpt {
+
+static thread_local std::string g_last_error;
+std::string &last_error_ref() { return g_last_error; }
+static int g_device = -1;
+static thread_local bool g_stats_enabled = false;
+static thread_local unsigned long long g_last_stats[4] = {0, 0, 0, 0};
+
+void hip_check(hipError_t e, const char *what) {
+    if (e != hipSuccess) throw Error{MPT_ERR_HIP, std::string(what) + ": " + hipGetErrorString(e)};
+}
+
+static void require(bool ok, const char *msg) {
+    if (!ok) throw Error{MPT_ERR_INVALID, msg};
+}
+
+static void ensure_device() {
+    if (g_device < 0) {
+        int n = 0;
+        if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) throw Error{MPT_ERR_NO_DEVICE, "no HIP device"};
+        hip_check(hipGetDevice(&g_device), "hipGetDevice");
+    }
+}
+
+// Growable device buffer (per-thread workspace for the host-pointer entry points).
+struct DevBuf {
+    void *p = nullptr;
+    size_t cap = 0;
+    void *get(size_t bytes) {
+        if (bytes > cap) {
+            if (p) hip_check(hipFree(p), "hipFree");
+            p = nullptr;
+            size_t c = std::max<size_t>(bytes, cap * 2);
+            c = std::max<size_t>(c, 256);
+            hip_check(hipMalloc(&p, c), "hipMalloc workspace");
+            cap = c;
+        }
+        return p;
+    }
+    ~DevBuf() {
+        if (p) (void)hipFree(p);
+    }
+};
+
+struct Workspace {
+    DevBuf poses, pose_edge, verdict, links, q, ids, d2, scratch, offsets, stats;
+};
+static thread_local Workspace g_ws;
+
+}  // namespace mpt
+
+using namespace mpt;
+
+// ---------------------------------------------------------------- handles
+struct mpt_env {
+    EnvDev dev{};
+    EnvTri *d_tris = nullptr;
+    BvhNode *d_nodes = nullptr;
+    int64_t n_tris = 0, n_nodes = 0, depth = 0;
+};
+
+struct mpt_agent {
+    AgentDev dev{};
+    double *d_tris = nullptr;
+    Cluster *d_clusters = nullptr;
+    int64_t n_tris = 0;
+};
+
+struct mpt_nn {
+    int32_t d = 0;
+    int64_t cap = 0, n = 0;
+    double *d_pts = nullptr;
+    uint8_t *d_removed = nullptr;
+};
+
+// ---------------------------------------------------------------- BVH build
+namespace {
+
+struct TriRef {
+    double lo[3], hi[3], c[3];
+    int64_t idx;
+};
+
+// Top-down median split on the widest centroid axis; one triangle per leaf.  Nodes are
+// emitted in pre-order (left child = node + 1).  Boxes come from the exact double
+// vertex bounds, widened outward to float (fcl_math.h widen_*).
+int64_t build_env_bvh(std::vector<TriRef> &refs, int64_t first, int64_t n, std::vector<BvhNode> &nodes,
+                      std::vector<int64_t> &order, int depth, int64_t &max_depth) {
+    const int64_t id = (int64_t)nodes.size();
+    nodes.push_back(BvhNode{});
+    max_depth = std::max<int64_t>(max_depth, depth);
+    double lo[3] = {HUGE_VAL, HUGE_VAL, HUGE_VAL}, hi[3] = {-HUGE_VAL, -HUGE_VAL, -HUGE_VAL};
+    double clo[3] = {HUGE_VAL, HUGE_VAL, HUGE_VAL}, chi[3] = {-HUGE_VAL, -HUGE_VAL, -HUGE_VAL};
+    for (int64_t i = first; i < first + n; ++i)
+        for (int k = 0; k < 3; ++k) {
+            lo[k] = std::min(lo[k], refs[i].lo[k]);
+            hi[k] = std::max(hi[k], refs[i].hi[k]);
+            clo[k] = std::min(clo[k], refs[i].c[k]);
+            chi[k] = std::max(chi[k], refs[i].c[k]);
+        }
+    BvhNode nd{};
+    for (int k = 0; k < 3; ++k) {
+        nd.lo[k] = widen_lo(lo[k]);
+        nd.hi[k] = widen_hi(hi[k]);
+    }
+    if (n == 1) {
+        nd.a = (int32_t)order.size();
+        nd.b = -1;
+        order.push_back(refs[first].idx);
+        nodes[id] = nd;
+        return id;
+    }
+    int ax = 0;
+    for (int k = 1; k < 3; ++k)
+        if (chi[k] - clo[k] > chi[ax] - clo[ax]) ax = k;
+    const int64_t h = n / 2;
+    std::nth_element(refs.begin() + first, refs.begin() + first + h, refs.begin() + first + n,
+                     [ax](const TriRef &x, const TriRef &y) {
+                         return x.c[ax] < y.c[ax] || (x.c[ax] == y.c[ax] && x.idx < y.idx);
+                     });
+    const int64_t l = build_env_bvh(refs, first, h, nodes, order, depth + 1, max_depth);
+    const int64_t r = build_env_bvh(refs, first + h, n - h, nodes, order, depth + 1, max_depth);
+    nd.a = (int32_t)l;
+    nd.b = (int32_t)r;
+    nodes[id] = nd;
+    return id;
+}
+
+// Agent clusters: the same median split, stopping at <= 64 triangles.
+void build_clusters(std::vector<TriRef> &refs, int64_t first, int64_t n, std::vector<std::pair<int64_t, int64_t>> &out) {
+    if (n <= kClusterMax) {
+        out.emplace_back(first, n);
+        return;
+    }
+    double clo[3] = {HUGE_VAL, HUGE_VAL, HUGE_VAL}, chi[3] = {-HUGE_VAL, -HUGE_VAL, -HUGE_VAL};
+    for (int64_t i = first; i < first + n; ++i)
+        for (int k = 0; k < 3; ++k) {
+            clo[k] = std::min(clo[k], refs[i].c[k]);
+            chi[k] = std::max(chi[k], refs[i].c[k]);
+        }
+    int ax = 0;
+    for (int k = 1; k < 3; ++k)
+        if (chi[k] - clo[k] > chi[ax] - clo[ax]) ax = k;
+    // split into multiples of 64 where possible to keep clusters full
+    int64_t h = ((n / 2 + kClusterMax - 1) / kClusterMax) * kClusterMax;
+    if (h >= n) h = n / 2;
+    std::nth_element(refs.begin() + first, refs.begin() + first + h, refs.begin() + first + n,
+                     [ax](const TriRef &x, const TriRef &y) {
+                         return x.c[ax] < y.c[ax] || (x.c[ax] == y.c[ax] && x.idx < y.idx);
+                     });
+    build_clusters(refs, first, h, out);
+    build_clusters(refs, first + h, n - h, out);
+}
+
+std::vector<TriRef> make_refs(const double *tris, int64_t n) {
+    std::vector<TriRef> refs((size_t)n);
+    for (int64_t i = 0; i < n; ++i) {
+        const double *t = tris + 9 * i;
+        for (int k = 0; k < 3; ++k) {
+            refs[i].lo[k] = std::min(t[k], std::min(t[3 + k], t[6 + k]));
+            refs[i].hi[k] = std::max(t[k], std::max(t[3 + k], t[6 + k]));
+            refs[i].c[k] = 0.5 * (refs[i].lo[k] + refs[i].hi[k]);
+        }
+        refs[i].idx = i;
+    }
+    return refs;
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------- runtime
+extern "C" mpt_status mpt_init(int32_t device) {
+    return guarded([&] {
+        int n = 0;
+        if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) throw Error{MPT_ERR_NO_DEVICE, "no HIP device visible"};
+        require(device >= 0 && device < n, "device index out of range");
+        hip_check(hipSetDevice(device), "hipSetDevice");
+        hipDeviceProp_t prop;
+        hip_check(hipGetDeviceProperties(&prop, device), "hipGetDeviceProperties");
+        if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+            throw Error{MPT_ERR_NO_DEVICE, std::string("libmpt is built for gfx950, device is ") + prop.gcnArchName};
+        g_device = device;
+    });
+}
+
+extern "C" const char *mpt_last_error(void) { return g_last_error.c_str(); }
+extern "C" int32_t mpt_version(void) { return 100; }
+
+extern "C" mpt_status mpt_device_synchronize(void) {
+    return guarded([&] { hip_check(hipDeviceSynchronize(), "hipDeviceSynchronize"); });
+}
+
+extern "C" mpt_status mpt_transform_from_location(const double loc7[7], double tf12[12]) {
+    return guarded([&] {
+        require(loc7 && tf12, "null pointer");
+        quat_to_rot(loc7 + 3, tf12);
+        tf12[9] = loc7[0];
+        tf12[10] = loc7[1];
+        tf12[11] = loc7[2];
+    });
+}
+
+// ---------------------------------------------------------------- env / agent
+extern "C" mpt_status mpt_env_create(const double *tris, int64_t n_tris, const double tf12[12], mpt_env **out) {
+    return guarded([&] {
+        require(out && tf12, "null pointer");
+        require(n_tris >= 0 && (n_tris == 0 || tris), "bad triangle soup");
+        require(n_tris < (int64_t(1) << 30), "too many env triangles");
+        ensure_device();
+        auto *env = new mpt_env();
+        try {
+            std::vector<BvhNode> nodes;
+            std::vector<int64_t> order;
+            std::vector<EnvTri> recs;
+            int64_t depth = 0;
+            if (n_tris > 0) {
+                auto refs = make_refs(tris, n_tris);
+                nodes.reserve(2 * n_tris);
+                build_env_bvh(refs, 0, n_tris, nodes, order, 0, depth);
+                if (depth + 1 >= kStackDepth) throw Error{MPT_ERR_INTERNAL, "env BVH too deep"};
+                recs.resize(n_tris);
+                for (int64_t i = 0; i < n_tris; ++i) make_env_tri(tris + 9 * order[i], recs[i]);
+                hip_check(hipMalloc(&env->d_tris, sizeof(EnvTri) * n_tris), "hipMalloc env tris");
+                hip_check(hipMalloc(&env->d_nodes, sizeof(BvhNode) * nodes.size()), "hipMalloc env nodes");
+                hip_check(hipMemcpy(env->d_tris, recs.data(), sizeof(EnvTri) * n_tris, hipMemcpyHostToDevice), "H2D");
+                hip_check(hipMemcpy(env->d_nodes, nodes.data(), sizeof(BvhNode) * nodes.size(), hipMemcpyHostToDevice),
+                          "H2D");
+            }
+            env->n_tris = n_tris;
+            env->n_nodes = (int64_t)nodes.size();
+            env->depth = depth;
+            env->dev.tris = env->d_tris;
+            env->dev.nodes = env->d_nodes;
+            std::memcpy(env->dev.tf, tf12, sizeof(double) * 12);
+            env->dev.n_tris = (int32_t)n_tris;
+            env->dev.n_nodes = (int32_t)nodes.size();
+            *out = env;
+        } catch (...) {
+            mpt_env_destroy(env);
+            throw;
+        }
+    });
+}
+
+extern "C" mpt_status mpt_env_destroy(mpt_env *env) {
+    return guarded([&] {
+        if (!env) return;
+        if (env->d_tris) (void)hipFree(env->d_tris);
+        if (env->d_nodes) (void)hipFree(env->d_nodes);
+        delete env;
+    });
+}
+
+extern "C" mpt_status mpt_env_info(const mpt_env *env, int64_t info[3]) {
+    return guarded([&] {
+        require(env && info, "null pointer");
+        info[0] = env->n_tris;
+        info[1] = env->n_nodes;
+        info[2] = env->depth;
+    });
+}
+
+extern "C" mpt_status mpt_agent_create(const double *tris, int64_t n_tris, mpt_agent **out) {
+    return guarded([&] {
+        require(out, "null pointer");
+        require(n_tris >= 0 && (n_tris == 0 || tris), "bad triangle soup");
+        require(n_tris < (int64_t(1) << 30), "too many agent triangles");
+        ensure_device();
+        auto *ag = new mpt_agent();
+        try {
+            std::vector<double> sorted((size_t)n_tris * 9);
+            std::vector<Cluster> cl;
+            if (n_tris > 0) {
+                auto refs = make_refs(tris, n_tris);
+                std::vector<std::pair<int64_t, int64_t>> ranges;
+                build_clusters(refs, 0, n_tris, ranges);
+                for (auto &r : ranges) {
+                    Cluster c{};
+                    double lo[3] = {HUGE_VAL, HUGE_VAL, HUGE_VAL}, hi[3] = {-HUGE_VAL, -HUGE_VAL, -HUGE_VAL};
+                    for (int64_t i = r.first; i < r.first + r.second; ++i) {
+                        std::memcpy(&sorted[9 * i], tris + 9 * refs[i].idx, 9 * sizeof(double));
+                        for (int k = 0; k < 3; ++k) {
+                            lo[k] = std::min(lo[k], refs[i].lo[k]);
+                            hi[k] = std::max(hi[k], refs[i].hi[k]);
+                        }
+                    }
+                    for (int k = 0; k < 3; ++k) {
+                        c.c[k] = 0.5 * (lo[k] + hi[k]);
+                        // half-extent covering both ends after rounding of the centre
+                        c.e[k] = std::max(hi[k] - c.c[k], c.c[k] - lo[k]) * (1.0 + 1e-12) + 1e-12;
+                    }
+                    c.first = (int32_t)r.first;
+                    c.count = (int32_t)r.second;
+                    cl.push_back(c);
+                }
+                hip_check(hipMalloc(&ag->d_tris, sizeof(double) * 9 * n_tris), "hipMalloc agent tris");
+                hip_check(hipMalloc(&ag->d_clusters, sizeof(Cluster) * cl.size()), "hipMalloc clusters");
+                hip_check(hipMemcpy(ag->d_tris, sorted.data(), sizeof(double) * 9 * n_tris, hipMemcpyHostToDevice),
+                          "H2D");
+                hip_check(hipMemcpy(ag->d_clusters, cl.data(), sizeof(Cluster) * cl.size(), hipMemcpyHostToDevice),
+                          "H2D");
+            }
+            ag->n_tris = n_tris;
+            ag->dev.tris = ag->d_tris;
+            ag->dev.clusters = ag->d_clusters;
+            ag->dev.n_clusters = (int32_t)cl.size();
+            ag->dev.n_tris = (int32_t)n_tris;
+            *out = ag;
+        } catch (...) {
+            mpt_agent_destroy(ag);
+            throw;
+        }
+    });
+}
+
+extern "C" mpt_status mpt_agent_destroy(mpt_agent *ag) {
+    return guarded([&] {
+        if (!ag) return;
+        if (ag->d_tris) (void)hipFree(ag->d_tris);
+        if (ag->d_clusters) (void)hipFree(ag->d_clusters);
+        delete ag;
+    });
+}
+
+// ---------------------------------------------------------------- collide
+namespace mpt {
+// used by the RRT engine as well
+const EnvDev &env_dev(const mpt_env *e) { return e->dev; }
+const AgentDev &agent_dev(const mpt_agent *a) { return a->dev; }
+}  // namespace mpt
+
+static void collide_common(const mpt_env *env, const mpt_agent *const *links, int32_t L, const double *d_poses,
+                           const int32_t *d_pose_edge, int64_t total_poses, int64_t E, uint8_t *d_verdict,
+                           hipStream_t stream) {
+    std::vector<AgentDev> lk((size_t)L);
+    for (int32_t l = 0; l < L; ++l) lk[l] = links[l]->dev;
+    auto *d_links = (AgentDev *)g_ws.links.get(sizeof(AgentDev) * L);
+    hip_check(hipMemcpyAsync(d_links, lk.data(), sizeof(AgentDev) * L, hipMemcpyHostToDevice, stream), "links H2D");
+    hip_check(hipMemsetAsync(d_verdict, 0, (size_t)E, stream), "verdict memset");
+    CollideWork w{};
+    w.poses = d_poses;
+    w.pose_edge = d_pose_edge;
+    w.pcount = nullptr;
+    w.pmax = 1;
+    w.L = L;
+    w.n_units = total_poses * L;
+    w.verdict = d_verdict;
+    w.stats = nullptr;
+    if (g_stats_enabled) {
+        w.stats = (unsigned long long *)g_ws.stats.get(sizeof(unsigned long long) * 4);
+        hip_check(hipMemsetAsync(w.stats, 0, sizeof(unsigned long long) * 4, stream), "stats memset");
+    }
+    launch_collide(env->dev, d_links, w, stream);
+    if (w.stats) {
+        hip_check(hipMemcpyAsync(g_last_stats, w.stats, sizeof(g_last_stats), hipMemcpyDeviceToHost, stream), "stats");
+    }
+}
+
+static void check_links(const mpt_env *env, const mpt_agent *const *links, int32_t L) {
+    require(env != nullptr, "null env");
+    require(L >= 1 && links != nullptr, "need at least one link");
+    for (int32_t l = 0; l < L; ++l) require(links[l] != nullptr, "null link");
+}
+
+extern "C" mpt_status mpt_collide_batch(const mpt_env *env, const mpt_agent *const *links, int32_t L,
+                                        const double *poses, const int64_t *edge_pose_offsets, int64_t E,
+                                        uint8_t *verdict_out, void *stream_) {
+    return guarded([&] {
+        check_links(env, links, L);
+        require(E >= 0 && (E == 0 || (edge_pose_offsets && verdict_out)), "bad edge arrays");
+        if (E == 0) return;
+        require(edge_pose_offsets[0] == 0, "edge_pose_offsets[0] must be 0");
+        for (int64_t e = 0; e < E; ++e) require(edge_pose_offsets[e + 1] >= edge_pose_offsets[e], "offsets not monotone");
+        const int64_t P = edge_pose_offsets[E];
+        require(P == 0 || poses, "null poses");
+        require(P < (int64_t(1) << 31), "too many poses");
+        hipStream_t stream = (hipStream_t)stream_;
+        std::vector<int32_t> pe((size_t)P);
+        for (int64_t e = 0; e < E; ++e)
+            for (int64_t p = edge_pose_offsets[e]; p < edge_pose_offsets[e + 1]; ++p) pe[p] = (int32_t)e;
+        auto *d_poses = (double *)g_ws.poses.get(sizeof(double) * 12 * std::max<int64_t>(P * L, 1));
+        auto *d_pe = (int32_t *)g_ws.pose_edge.get(sizeof(int32_t) * std::max<int64_t>(P, 1));
+        auto *d_v = (uint8_t *)g_ws.verdict.get((size_t)E);
+        if (P > 0) {
+            hip_check(hipMemcpyAsync(d_poses, poses, sizeof(double) * 12 * P * L, hipMemcpyHostToDevice, stream),
+                      "poses H2D");
+            hip_check(hipMemcpyAsync(d_pe, pe.data(), sizeof(int32_t) * P, hipMemcpyHostToDevice, stream), "pe H2D");
+        }
+        collide_common(env, links, L, d_poses, d_pe, P, E, d_v, stream);
+        hip_check(hipMemcpyAsync(verdict_out, d_v, (size_t)E, hipMemcpyDeviceToHost, stream), "verdict D2H");
+        hip_check(hipStreamSynchronize(stream), "collide sync");
+    });
+}
+
+extern "C" mpt_status mpt_collide_batch_device(const mpt_env *env, const mpt_agent *const *links, int32_t L,
+                                               const double *d_poses, const int64_t *d_edge_pose_offsets, int64_t E,
+                                               int64_t total_poses, uint8_t *d_verdict_out, void *stream_) {
+    return guarded([&] {
+        check_links(env, links, L);
+        require(E >= 0 && total_poses >= 0, "bad sizes");
+        if (E == 0) return;
+        require(d_edge_pose_offsets && d_verdict_out && (total_poses == 0 || d_poses), "null pointer");
+        hipStream_t stream = (hipStream_t)stream_;
+        auto *d_pe = (int32_t *)g_ws.pose_edge.get(sizeof(int32_t) * std::max<int64_t>(total_poses, 1));
+        launch_pose_edge(d_edge_pose_offsets, E, d_pe, stream);
+        collide_common(env, links, L, d_poses, d_pe, total_poses, E, d_verdict_out, stream);
+    });
+}
+
+extern "C" mpt_status mpt_set_stats(int32_t enable) {
+    return guarded([&] { g_stats_enabled = enable != 0; });
+}
+
+extern "C" mpt_status mpt_last_collide_stats(uint64_t stats[4]) {
+    return guarded([&] {
+        require(stats, "null pointer");
+        hip_check(hipDeviceSynchronize(), "sync");
+        for (int i = 0; i < 4; ++i) stats[i] = g_last_stats[i];
+    });
+}
+
+// ---------------------------------------------------------------- NN
+static void nn_reserve(mpt_nn *nn, int64_t need) {
+    if (need <= nn->cap) return;
+    int64_t cap = std::max<int64_t>(need, std::max<int64_t>(nn->cap * 2, 1024));
+    double *p = nullptr;
+    hip_check(hipMalloc(&p, sizeof(double) * nn->d * cap), "hipMalloc nn points");
+    if (nn->d_pts) {
+        hip_check(hipMemcpy(p, nn->d_pts, sizeof(double) * nn->d * nn->n, hipMemcpyDeviceToDevice), "nn grow");
+        (void)hipFree(nn->d_pts);
+    }
+    nn->d_pts = p;
+    if (nn->d_removed) {
+        uint8_t *r = nullptr;
+        hip_check(hipMalloc(&r, (size_t)cap), "hipMalloc removed");
+        hip_check(hipMemset(r, 0, (size_t)cap), "memset");
+        hip_check(hipMemcpy(r, nn->d_removed, (size_t)nn->n, hipMemcpyDeviceToDevice), "grow removed");
+        (void)hipFree(nn->d_removed);
+        nn->d_removed = r;
+    }
+    nn->cap = cap;
+}
+
+extern "C" mpt_status mpt_nn_create(int32_t dim, int64_t capacity, mpt_nn **out) {
+    return guarded([&] {
+        require(out, "null pointer");
+        require(dim >= 1 && dim <= 16, "dim must be in [1, 16]");
+        require(capacity >= 0, "bad capacity");
+        ensure_device();
+        auto *nn = new mpt_nn();
+        nn->d = dim;
+        try {
+            nn_reserve(nn, std::max<int64_t>(capacity, 1));
+        } catch (...) {
+            delete nn;
+            throw;
+        }
+        *out = nn;
+    });
+}
+
+extern "C" mpt_status mpt_nn_destroy(mpt_nn *nn) {
+    return guarded([&] {
+        if (!nn) return;
+        if (nn->d_pts) (void)hipFree(nn->d_pts);
+        if (nn->d_removed) (void)hipFree(nn->d_removed);
+        delete nn;
+    });
+}
+
+extern "C" mpt_status mpt_nn_append(mpt_nn *nn, const double *pts, int64_t n, int32_t *ids_out) {
+    return guarded([&] {
+        require(nn && n >= 0 && (n == 0 || pts), "bad arguments");
+        require(nn->n + n < (int64_t(1) << 31) - 1, "id space exhausted");
+        nn_reserve(nn, nn->n + n);
+        if (n > 0)
+            hip_check(hipMemcpy(nn->d_pts + nn->n * nn->d, pts, sizeof(double) * nn->d * n, hipMemcpyHostToDevice),
+                      "nn append");
+        if (ids_out)
+            for (int64_t i = 0; i < n; ++i) ids_out[i] = (int32_t)(nn->n + i + 1);
+        nn->n += n;
+    });
+}
+
+extern "C" mpt_status mpt_nn_append_device(mpt_nn *nn, const double *d_pts, int64_t n, void *stream) {
+    return guarded([&] {
+        require(nn && n >= 0 && (n == 0 || d_pts), "bad arguments");
+        nn_reserve(nn, nn->n + n);
+        if (n > 0)
+            hip_check(hipMemcpyAsync(nn->d_pts + nn->n * nn->d, d_pts, sizeof(double) * nn->d * n,
+                                     hipMemcpyDeviceToDevice, (hipStream_t)stream),
+                      "nn append device");
+        nn->n += n;
+    });
+}
+
+extern "C" mpt_status mpt_nn_remove(mpt_nn *nn, int32_t id) {
+    return guarded([&] {
+        require(nn, "null nn");
+        require(id >= 1 && id <= nn->n, "id out of range");
+        if (!nn->d_removed) {
+            hip_check(hipMalloc(&nn->d_removed, (size_t)nn->cap), "hipMalloc removed");
+            hip_check(hipMemset(nn->d_removed, 0, (size_t)nn->cap), "memset removed");
+        }
+        const uint8_t one = 1;
+        hip_check(hipMemcpy(nn->d_removed + (id - 1), &one, 1, hipMemcpyHostToDevice), "remove");
+    });
+}
+
+extern "C" mpt_status mpt_nn_size(const mpt_nn *nn, int64_t *n_out) {
+    return guarded([&] {
+        require(nn && n_out, "null pointer");
+        *n_out = nn->n;
+    });
+}
+
+extern "C" mpt_status mpt_nn_points_device(const mpt_nn *nn, const double **d_pts) {
+    return guarded([&] {
+        require(nn && d_pts, "null pointer");
+        *d_pts = nn->d_pts;
+    });
+}
+
+static NNWork nn_work(const mpt_nn *nn, const double *d_q, int64_t nq) {
+    NNWork w{};
+    w.pts = nn->d_pts;
+    w.removed = nn->d_removed;
+    w.n = nn->n;
+    w.d = nn->d;
+    w.q = d_q;
+    w.nq = nq;
+    return w;
+}
+
+extern "C" mpt_status mpt_nn_knn_device(mpt_nn *nn, const double *d_q, int64_t nq, int32_t k, int32_t *d_ids,
+                                        double *d_d2, void *stream) {
+    return guarded([&] {
+        require(nn && nq >= 0, "bad arguments");
+        require(k >= 1 && k <= 32, "k must be in [1, 32]");
+        if (nq == 0) return;
+        require(d_q && d_ids && d_d2, "null pointer");
+        const NNWork w = nn_work(nn, d_q, nq);
+        void *scratch = g_ws.scratch.get(nn_knn_scratch_bytes(nq, std::max<int64_t>(nn->n, 1), k));
+        launch_knn(w, k, d_ids, d_d2, scratch, (hipStream_t)stream);
+    });
+}
+
+extern "C" mpt_status mpt_nn_knn(mpt_nn *nn, const double *q, int64_t nq, int32_t k, int32_t *ids, double *d2,
+                                 void *stream_) {
+    return guarded([&] {
+        require(nn && nq >= 0, "bad arguments");
+        require(k >= 1 && k <= 32, "k must be in [1, 32]");
+        if (nq == 0) return;
+        require(q && ids && d2, "null pointer");
+        hipStream_t stream = (hipStream_t)stream_;
+        auto *d_q = (double *)g_ws.q.get(sizeof(double) * nn->d * nq);
+        auto *d_ids = (int32_t *)g_ws.ids.get(sizeof(int32_t) * nq * k);
+        auto *d_d2 = (double *)g_ws.d2.get(sizeof(double) * nq * k);
+        hip_check(hipMemcpyAsync(d_q, q, sizeof(double) * nn->d * nq, hipMemcpyHostToDevice, stream), "q H2D");
+        const NNWork w = nn_work(nn, d_q, nq);
+        void *scratch = g_ws.scratch.get(nn_knn_scratch_bytes(nq, std::max<int64_t>(nn->n, 1), k));
+        launch_knn(w, k, d_ids, d_d2, scratch, stream);
+        hip_check(hipMemcpyAsync(ids, d_ids, sizeof(int32_t) * nq * k, hipMemcpyDeviceToHost, stream), "ids D2H");
+        hip_check(hipMemcpyAsync(d2, d_d2, sizeof(double) * nq * k, hipMemcpyDeviceToHost, stream), "d2 D2H");
+        hip_check(hipStreamSynchronize(stream), "knn sync");
+    });
+}
+
+extern "C" mpt_status mpt_nn_radius(mpt_nn *nn, const double *q, int64_t nq, double r2, int32_t max_nb,
+                                    int64_t *offsets, int32_t *ids, double *d2, int64_t cap, void *stream_) {
+    return guarded([&] {
+        require(nn && nq >= 0 && offsets, "bad arguments");
+        require(cap >= 0 && (cap == 0 || (ids && d2)), "bad output arrays");
+        hipStream_t stream = (hipStream_t)stream_;
+        if (nq == 0) {
+            offsets[0] = 0;
+            return;
+        }
+        require(q, "null queries");
+        auto *d_q = (double *)g_ws.q.get(sizeof(double) * nn->d * nq);
+        auto *d_off = (int64_t *)g_ws.offsets.get(sizeof(int64_t) * (nq + 1));
+        auto *d_ids = (int32_t *)g_ws.ids.get(sizeof(int32_t) * std::max<int64_t>(cap, 1));
+        auto *d_d2 = (double *)g_ws.d2.get(sizeof(double) * std::max<int64_t>(cap, 1));
+        hip_check(hipMemcpyAsync(d_q, q, sizeof(double) * nn->d * nq, hipMemcpyHostToDevice, stream), "q H2D");
+        const NNWork w = nn_work(nn, d_q, nq);
+        const int64_t total = launch_radius(w, r2, max_nb, d_off, d_ids, d_d2, cap, nullptr, 0, stream);
+        hip_check(hipMemcpyAsync(offsets, d_off, sizeof(int64_t) * (nq + 1), hipMemcpyDeviceToHost, stream), "off");
+        const int64_t m = std::min(total, cap);
+        if (m > 0) {
+            hip_check(hipMemcpyAsync(ids, d_ids, sizeof(int32_t) * m, hipMemcpyDeviceToHost, stream), "ids D2H");
+            hip_check(hipMemcpyAsync(d2, d_d2, sizeof(double) * m, hipMemcpyDeviceToHost, stream), "d2 D2H");
+        }
+        hip_check(hipStreamSynchronize(stream), "radius sync");
+    });
+}

@@ -1,0 +1,225 @@
+// fcl_math.h -- FP64 geometry in FCL 0.3.2 operation order, shared by the HIP kernels
+// and the host-side precomputation of environment triangle records.
+//
+// Bit-exactness contract: every expression below is written in the order FCL 0.3.2
+// evaluates it ([upstream] fcl/math/vec_3f.h, matrix_3f.h, intersect.cpp) and the
+// whole library is compiled with -ffp-contract=off, so no a*b+c is fused on either
+// the host (x86-64) or the device (gfx950).  The verdict of tri_intersect() is the
+// AND of the 17 project6() tests, so the tests may run in any order.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <math.h>
+
+#pragma clang fp contract(off)
+
+#define MPT_HD __host__ __device__ __forceinline__
+
+namespace mpt {
+
+struct v3 {
+    double x, y, z;
+};
+
+MPT_HD v3 mk(double x, double y, double z) { return v3{x, y, z}; }
+MPT_HD v3 sub(v3 a, v3 b) { return v3{a.x - b.x, a.y - b.y, a.z - b.z}; }
+// Vec3Data::dot: x*x' + y*y' + z*z' evaluated left to right
+MPT_HD double dot(v3 a, v3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+// Vec3Data::cross
+MPT_HD v3 cross(v3 a, v3 b) {
+    return v3{a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x};
+}
+MPT_HD double dmax(double a, double b) { return a < b ? b : a; }  // std::max
+MPT_HD double dmin(double a, double b) { return b < a ? b : a; }  // std::min
+
+// Matrix3f * Vec3f + T (dotX/dotY/dotZ, then the translation add).
+MPT_HD v3 xform(const double R[9], const double T[3], v3 q) {
+    const double r0 = R[0] * q.x + R[1] * q.y + R[2] * q.z;
+    const double r1 = R[3] * q.x + R[4] * q.y + R[5] * q.z;
+    const double r2 = R[6] * q.x + R[7] * q.y + R[8] * q.z;
+    return v3{r0 + T[0], r1 + T[1], r2 + T[2]};
+}
+
+// fcl::relativeTransform(R1, T1, R2, T2): R = R1^T R2, T = R1^T (T2 - T1).
+MPT_HD void relative_transform(const double R1[9], const double T1[3], const double R2[9],
+                               const double T2[3], double R[9], double T[3]) {
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+        for (int j = 0; j < 3; ++j)
+            R[i * 3 + j] = R1[0 * 3 + i] * R2[0 * 3 + j] + R1[1 * 3 + i] * R2[1 * 3 + j] +
+                           R1[2 * 3 + i] * R2[2 * 3 + j];
+    const double d0 = T2[0] - T1[0], d1 = T2[1] - T1[1], d2 = T2[2] - T1[2];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) T[i] = R1[0 * 3 + i] * d0 + R1[1 * 3 + i] * d1 + R1[2 * 3 + i] * d2;
+}
+
+// Quaternion3f::toRotation, q = {w, x, y, z}.
+MPT_HD void quat_to_rot(const double q[4], double R[9]) {
+    const double w = q[0], x = q[1], y = q[2], z = q[3];
+    const double twoX = 2.0 * x, twoY = 2.0 * y, twoZ = 2.0 * z;
+    const double twoWX = twoX * w, twoWY = twoY * w, twoWZ = twoZ * w;
+    const double twoXX = twoX * x, twoXY = twoY * x, twoXZ = twoZ * x;
+    const double twoYY = twoY * y, twoYZ = twoZ * y, twoZZ = twoZ * z;
+    R[0] = 1.0 - (twoYY + twoZZ); R[1] = twoXY - twoWZ;         R[2] = twoXZ + twoWY;
+    R[3] = twoXY + twoWZ;         R[4] = 1.0 - (twoXX + twoZZ); R[5] = twoYZ - twoWX;
+    R[6] = twoXZ - twoWY;         R[7] = twoYZ + twoWX;         R[8] = 1.0 - (twoXX + twoYY);
+}
+
+// Conservative float bounds: the margin (1e-6 absolute + 4e-7 relative) exceeds both
+// the double->float rounding (<= 6e-8 relative) and the rounding error of the 17-axis
+// test by many orders, so box pruning never removes a pair the all-pairs loop reports.
+MPT_HD float widen_lo(double x) { return (float)(x - (1e-6 + 4e-7 * fabs(x))); }
+MPT_HD float widen_hi(double x) { return (float)(x + (1e-6 + 4e-7 * fabs(x))); }
+
+// Environment triangle record: everything intersect_Triangle derives from P alone,
+// precomputed on the host with the same operations (so bit-identical), 40 doubles.
+struct EnvTri {
+    double P1[3];   // q_i = Q_i' - P1
+    double p2[3];   // p2 = P2 - P1 (= e1, since p1 = P1 - P1 = 0)
+    double p3[3];   // p3 = P3 - P1
+    double e2[3];   // p3 - p2
+    double e3[3];   // p1 - p3
+    double n1[3];   // e1 x e2
+    double g[3][3]; // e_i x n1
+    double nP[2];   // min/max of {p1,p2,p3}.n1 (p1 term is +-0)
+    double gP[3][2];// min/max of {p1,p2,p3}.g_i
+    double pad[5];
+};
+static_assert(sizeof(EnvTri) == 40 * 8, "EnvTri layout");
+
+inline void make_env_tri(const double *t, EnvTri &r) {
+    const v3 P1 = mk(t[0], t[1], t[2]), P2 = mk(t[3], t[4], t[5]), P3 = mk(t[6], t[7], t[8]);
+    const v3 p1 = sub(P1, P1), p2 = sub(P2, P1), p3 = sub(P3, P1);
+    const v3 e1 = sub(p2, p1), e2 = sub(p3, p2), e3 = sub(p1, p3);
+    const v3 n1 = cross(e1, e2);
+    const v3 g[3] = {cross(e1, n1), cross(e2, n1), cross(e3, n1)};
+    r.P1[0] = P1.x; r.P1[1] = P1.y; r.P1[2] = P1.z;
+    r.p2[0] = e1.x; r.p2[1] = e1.y; r.p2[2] = e1.z;
+    r.p3[0] = p3.x; r.p3[1] = p3.y; r.p3[2] = p3.z;
+    r.e2[0] = e2.x; r.e2[1] = e2.y; r.e2[2] = e2.z;
+    r.e3[0] = e3.x; r.e3[1] = e3.y; r.e3[2] = e3.z;
+    r.n1[0] = n1.x; r.n1[1] = n1.y; r.n1[2] = n1.z;
+    auto proj = [&](v3 ax, double *mnmx) {
+        const double a = dot(ax, p1), b = dot(ax, p2), c = dot(ax, p3);
+        mnmx[0] = dmin(a, dmin(b, c));
+        mnmx[1] = dmax(a, dmax(b, c));
+    };
+    proj(n1, r.nP);
+    for (int i = 0; i < 3; ++i) {
+        r.g[i][0] = g[i].x; r.g[i][1] = g[i].y; r.g[i][2] = g[i].z;
+        proj(g[i], r.gP[i]);
+    }
+    for (double &x : r.pad) x = 0.0;
+}
+
+// project6 with the P-side interval known: 0 = separated.
+MPT_HD bool overlap_q(v3 ax, double mn1, double mx1, v3 q1, v3 q2, v3 q3) {
+    const double Q1 = dot(ax, q1), Q2 = dot(ax, q2), Q3 = dot(ax, q3);
+    const double mx2 = dmax(Q1, dmax(Q2, Q3));
+    const double mn2 = dmin(Q1, dmin(Q2, Q3));
+    if (mn1 > mx2) return false;
+    if (mn2 > mx1) return false;
+    return true;
+}
+
+// project6 for an axis depending on Q: P-side = {ax.p1 (= +-0), ax.p2, ax.p3}.
+MPT_HD bool project6_p(v3 ax, v3 p2, v3 p3, v3 q1, v3 q2, v3 q3) {
+    const double P1 = 0.0, P2 = dot(ax, p2), P3 = dot(ax, p3);
+    const double mx1 = dmax(P1, dmax(P2, P3));
+    const double mn1 = dmin(P1, dmin(P2, P3));
+    return overlap_q(ax, mn1, mx1, q1, q2, q3);
+}
+
+// Intersect::intersect_Triangle(P1,P2,P3, Q1',Q2',Q3') with Q' already in the env frame.
+// Returns true when no axis separates (touching counts as intersecting).
+template <class ETri>
+MPT_HD bool tri_intersect(const ETri &E, v3 Q1, v3 Q2, v3 Q3) {
+    const v3 P1 = mk(E.P1[0], E.P1[1], E.P1[2]);
+    const v3 q1 = sub(Q1, P1), q2 = sub(Q2, P1), q3 = sub(Q3, P1);
+    const v3 n1 = mk(E.n1[0], E.n1[1], E.n1[2]);
+    if (!overlap_q(n1, E.nP[0], E.nP[1], q1, q2, q3)) return false;
+    const v3 p2 = mk(E.p2[0], E.p2[1], E.p2[2]);
+    const v3 p3 = mk(E.p3[0], E.p3[1], E.p3[2]);
+    const v3 f1 = sub(q2, q1), f2 = sub(q3, q2), f3 = sub(q1, q3);
+    const v3 m1 = cross(f1, f2);
+    if (!project6_p(m1, p2, p3, q1, q2, q3)) return false;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        const v3 gi = mk(E.g[i][0], E.g[i][1], E.g[i][2]);
+        if (!overlap_q(gi, E.gP[i][0], E.gP[i][1], q1, q2, q3)) return false;
+    }
+    const v3 e1 = p2;
+    const v3 e2 = mk(E.e2[0], E.e2[1], E.e2[2]);
+    const v3 e3 = mk(E.e3[0], E.e3[1], E.e3[2]);
+    if (!project6_p(cross(e1, f1), p2, p3, q1, q2, q3)) return false;
+    if (!project6_p(cross(e1, f2), p2, p3, q1, q2, q3)) return false;
+    if (!project6_p(cross(e1, f3), p2, p3, q1, q2, q3)) return false;
+    if (!project6_p(cross(e2, f1), p2, p3, q1, q2, q3)) return false;
+    if (!project6_p(cross(e2, f2), p2, p3, q1, q2, q3)) return false;
+    if (!project6_p(cross(e2, f3), p2, p3, q1, q2, q3)) return false;
+    if (!project6_p(cross(e3, f1), p2, p3, q1, q2, q3)) return false;
+    if (!project6_p(cross(e3, f2), p2, p3, q1, q2, q3)) return false;
+    if (!project6_p(cross(e3, f3), p2, p3, q1, q2, q3)) return false;
+    if (!project6_p(cross(f1, m1), p2, p3, q1, q2, q3)) return false;
+    if (!project6_p(cross(f2, m1), p2, p3, q1, q2, q3)) return false;
+    if (!project6_p(cross(f3, m1), p2, p3, q1, q2, q3)) return false;
+    return true;
+}
+
+// FLANN 1.8.4 L2<double>::operator() accumulation order: groups of four
+// result += ((d0*d0 + d1*d1) + d2*d2) + d3*d3, then the tail one at a time.
+// The first group is stored instead of added to 0.0 (0.0 + t == t bit for bit, t >= 0).
+template <int D>
+MPT_HD double flann_l2(const double *a, const double *b) {
+    double result = 0.0;
+    int i = 0;
+#pragma unroll
+    for (; i + 3 < D; i += 4) {
+        const double d0 = a[i] - b[i], d1 = a[i + 1] - b[i + 1];
+        const double d2 = a[i + 2] - b[i + 2], d3 = a[i + 3] - b[i + 3];
+        const double t = d0 * d0 + d1 * d1 + d2 * d2 + d3 * d3;
+        result = (i == 0) ? t : result + t;
+    }
+#pragma unroll
+    for (; i < D; ++i) {
+        const double d0 = a[i] - b[i];
+        result += d0 * d0;
+    }
+    return result;
+}
+
+MPT_HD double flann_l2_dyn(const double *a, const double *b, int d) {
+    double result = 0.0;
+    int i = 0;
+    for (; i + 3 < d; i += 4) {
+        const double d0 = a[i] - b[i], d1 = a[i + 1] - b[i + 1];
+        const double d2 = a[i + 2] - b[i + 2], d3 = a[i + 3] - b[i + 3];
+        result += d0 * d0 + d1 * d1 + d2 * d2 + d3 * d3;
+    }
+    for (; i < d; ++i) {
+        const double d0 = a[i] - b[i];
+        result += d0 * d0;
+    }
+    return result;
+}
+
+// (d2, id) lexicographic order of all NN results.
+MPT_HD bool nn_better(double da, int32_t ia, double db, int32_t ib) {
+    return da < db || (da == db && ia < ib);
+}
+
+// Counter-based RNG of the batched engine: splitmix64 finaliser of
+// seed + golden * (counter + 1); top 53 bits -> [0, 1); (u * (b - a)) + a.
+MPT_HD uint64_t mix64(uint64_t z) {
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+    return z ^ (z >> 31);
+}
+MPT_HD double engine_uniform(uint64_t seed, uint64_t counter, double a, double b) {
+    const uint64_t z = mix64(seed + 0x9E3779B97F4A7C15ULL * (counter + 1ULL));
+    const double u = (double)(z >> 11) * (1.0 / 9007199254740992.0);
+    return u * (b - a) + a;
+}
+
+}  // namespace mpt

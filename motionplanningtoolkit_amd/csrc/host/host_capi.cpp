@@ -1,0 +1,57 @@
+// host_capi.cpp -- C entry points into the C++ host planner (for ctypes tests, the
+// Python package and other FFI callers).  Declared in include/mpt_host.h.
+#include <cstring>
+#include <stdexcept>
+#include <string>
+
+#include "../../../include/mpt_host.h"
+#include "compose.hpp"
+
+namespace {
+thread_local std::string g_host_err;
+
+template <class F>
+mpt_status hguard(F &&f) {
+    try {
+        f();
+        return MPT_OK;
+    } catch (const std::exception &e) {
+        g_host_err = e.what();
+        return MPT_ERR_INVALID;
+    } catch (...) {
+        g_host_err = "unknown error";
+        return MPT_ERR_INTERNAL;
+    }
+}
+}  // namespace
+
+extern "C" const char *mpt_host_last_error(void) { return g_host_err.c_str(); }
+
+extern "C" mpt_status mpt_host_load_mesh(const char *path, int32_t which, double *tris, int64_t cap,
+                                         int64_t *n_tris, int32_t *n_submeshes) {
+    return hguard([&] {
+        if (!path || !n_tris) throw std::invalid_argument("null pointer");
+        const auto m = mpt_host::load_mesh(path);
+        if (m.error) throw std::runtime_error(m.message);
+        const std::vector<double> t = which == 1 ? m.last_nonempty() : m.soup();
+        *n_tris = (int64_t)(t.size() / 9);
+        if (n_submeshes) *n_submeshes = (int32_t)m.submeshes.size();
+        if (tris && cap > 0) std::memcpy(tris, t.data(), sizeof(double) * 9 * std::min<int64_t>(cap, *n_tris));
+    });
+}
+
+extern "C" mpt_status mpt_host_rrt_inst(const char *inst_path, int32_t iterations_at_a_time, int64_t cap,
+                                        double *starts, double *ends, int64_t *n_edges, int32_t *dim,
+                                        int32_t *solved) {
+    return hguard([&] {
+        if (!inst_path || !n_edges) throw std::invalid_argument("null pointer");
+        const auto r = mpt_host::run_inst(inst_path, iterations_at_a_time);
+        const int64_t n = r.dim ? (int64_t)(r.ends.size() / r.dim) : 0;
+        *n_edges = n;
+        if (dim) *dim = r.dim;
+        if (solved) *solved = r.solved ? 1 : 0;
+        const int64_t m = std::min<int64_t>(n, cap);
+        if (starts && m > 0) std::memcpy(starts, r.starts.data(), sizeof(double) * r.dim * m);
+        if (ends && m > 0) std::memcpy(ends, r.ends.data(), sizeof(double) * r.dim * m);
+    });
+}

@@ -1,0 +1,127 @@
+// mpt_internal.h -- device data layout in HBM and the internal launch interfaces.
+//
+// Environment (StaticEnvironmentMeshHandler, utilities/meshhandler.hpp:18-55): all
+// submeshes share one transform, so they are merged into one triangle soup, stored
+//   tris  [T] EnvTri (320 B, env-local frame, BVH leaf order)
+//   nodes [2T-1] BvhNode (32 B: float AABB widened outward + children / leaf index)
+// Agent link mesh (SimpleAgentMeshHandler, meshhandler.hpp:112-135):
+//   tris     [T][9] doubles, agent-local frame, grouped in clusters of <= 64
+//   clusters [C] Cluster (local box centre/half-extent + first/count)
+// Tree nodes (FLANN_KDTreeWrapper, utilities/flannkdtreewrapper.hpp): [capacity][d] FP64,
+// id = row + 1 (FLANN ids start at 1, the ctor's dummy point 0 is removed).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <exception>
+#include <string>
+
+#include "fcl_math.h"
+
+namespace mpt {
+
+constexpr int kWave = 64;
+constexpr int kClusterMax = 64;
+constexpr int kStackDepth = 64;
+
+struct BvhNode {
+    float lo[3];
+    int32_t a;   // inner: left child   | leaf: triangle index
+    float hi[3];
+    int32_t b;   // inner: right child  | leaf: -1
+};
+static_assert(sizeof(BvhNode) == 32, "BvhNode layout");
+
+struct Cluster {
+    double c[3];   // local box centre
+    double e[3];   // local half-extent
+    int32_t first; // first triangle
+    int32_t count; // <= 64
+};
+
+struct AgentDev {
+    const double *tris;       // [T][9]
+    const Cluster *clusters;  // [C]
+    int32_t n_clusters;
+    int32_t n_tris;
+};
+
+struct EnvDev {
+    const EnvTri *tris;
+    const BvhNode *nodes;
+    double tf[12];     // R1 (row-major) + T1: parseTransform of "Environment Location"
+    double root_lo[3], root_hi[3];
+    int32_t n_tris;
+    int32_t n_nodes;
+};
+
+// Work description for one collide launch.  Units are (pose, link) pairs.
+//  mode A (host API): pose_edge[p] gives the edge of pose p; units = n_poses * L.
+//  mode B (engine):   edge e owns pose slots [e*pmax, e*pmax + pcount[e]);
+//                     units = n_edges * pmax * L, slots past pcount are skipped.
+struct CollideWork {
+    const double *poses;      // [slots][L][12]
+    const int32_t *pose_edge; // mode A, else nullptr
+    const int32_t *pcount;    // mode B
+    int32_t pmax;             // mode B
+    int32_t L;
+    int64_t n_units;
+    uint8_t *verdict;         // [E], 0-initialised by the launcher, set to 1 on contact
+    unsigned long long *stats; // optional [4]: units run, clusters visited, node visits, SAT tests
+};
+
+void launch_collide(const EnvDev &env, const AgentDev *d_links, const CollideWork &w,
+                    hipStream_t stream);
+void launch_pose_edge(const int64_t *d_offsets, int64_t E, int32_t *d_pose_edge, hipStream_t stream);
+
+// ---------------- NN ----------------
+struct NNWork {
+    const double *pts;       // [n][d]
+    const uint8_t *removed;  // [n] or nullptr
+    int64_t n;
+    int32_t d;
+    const double *q;         // [nq][d]
+    int64_t nq;
+    const int64_t *n_dev;    // optional device-resident point count (<= n); n is then an upper bound
+};
+// 1-NN / kNN (k <= 32): ids [nq][k] 1-based (-1 empty), d2 [nq][k] (+inf empty).
+// scratch must hold nn_knn_scratch_bytes(nq, n, k) bytes.
+size_t nn_knn_scratch_bytes(int64_t nq, int64_t n, int32_t k);
+void launch_knn(const NNWork &w, int32_t k, int32_t *ids, double *d2, void *scratch,
+                hipStream_t stream);
+// radius: counts pass then fill pass; offsets [nq+1] device.  Results per query are
+// sorted by (d2, id) and truncated to max_nb (> 0).  Needs the host to read the total
+// between passes; returns the total.
+int64_t launch_radius(const NNWork &w, double r2, int32_t max_nb, int64_t *d_offsets,
+                      int32_t *d_ids, double *d2, int64_t cap, void *scratch, size_t scratch_bytes,
+                      hipStream_t stream);
+
+// ---------------- error helpers ----------------
+struct Error {
+    int code;
+    std::string msg;
+};
+
+void hip_check(hipError_t e, const char *what);
+// per-thread message returned by mpt_last_error()
+std::string &last_error_ref();
+
+// Run f(), translating exceptions into an mpt_status + last_error message.
+template <class F>
+int32_t guarded(F &&f) {
+    try {
+        f();
+        return 0;
+    } catch (const Error &e) {
+        last_error_ref() = e.msg;
+        return e.code;
+    } catch (const std::exception &e) {
+        last_error_ref() = e.what();
+        return 5;
+    } catch (...) {
+        last_error_ref() = "unknown error";
+        return 5;
+    }
+}
+
+}  // namespace mpt

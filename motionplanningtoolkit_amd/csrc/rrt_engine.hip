@@ -1,0 +1,572 @@
+// rrt_engine.hip -- device-resident batched RRT rounds (throughput mode of planners/rrt.hpp:42-94).
+//
+// The reference loop does one extension per iteration:
+//   sample (UniformSampler::getTreeSample, samplers/uniformsampler.hpp:20-35)
+//   -> nearest (FLANN_KDTreeWrapper::nearest, utilities/flannkdtreewrapper.hpp:57-89)
+//   -> Agent::randomSteer -> Map3D::safeEdge (Agent::getPoses + MeshHandler::isInCollision)
+//   -> TreeInterface::insertIntoTree.
+// A round here performs K such extensions against the tree snapshot taken at the start
+// of the round (new nodes become visible to the next round), entirely on the device:
+//   k_sample -> k_knn1 (+ merge) -> k_steer -> k_collide -> k_count -> k_append -> k_commit
+// No host synchronisation inside a round; the node count lives in device memory.
+// The per-extension randomness comes from a counter-based generator (fcl_math.h
+// engine_uniform): extension g uses counters g*64 + j (sample dims) and g*64 + 32 + j
+// (controls), so results are independent of the launch geometry and of the GPU count.
+// K = 1 reference replay with the reference's own RNG streams is the host planner's job
+// (host/rrt.hpp over the same kernels).
+#include <cstring>
+#include <vector>
+
+#include "../../include/mpt.h"
+#include "mpt_internal.h"
+
+namespace mpt {
+const EnvDev &env_dev(const mpt_env *e);
+const AgentDev &agent_dev(const mpt_agent *a);
+}  // namespace mpt
+
+using namespace mpt;
+
+namespace {
+
+constexpr int kMaxDim = 16;
+
+struct EngineParams {
+    int32_t kind, d, L, pmax;
+    double prm[7];
+    double lo[kMaxDim], hi[kMaxDim];
+    double steer_dt, cc_dt;
+    uint64_t seed;
+};
+
+__device__ __forceinline__ double normalize_theta(double t) {
+    return t - 2 * M_PI * floor((t + M_PI) / (2 * M_PI));
+}
+
+// Blimp::doStep (agents/blimp.hpp:293-317), theta update without dt as written.
+__device__ void blimp_step(const double *prm, const double *s, double a, double w, double z, double dt,
+                           double *out) {
+    double n[7];
+    n[0] = s[0] + cos(s[3]) * s[4] * dt;
+    n[1] = s[1] + sin(s[3]) * s[4] * dt;
+    n[3] = normalize_theta(s[3] + s[4] * tan(s[5]) / prm[0]);
+    n[2] = s[2] + s[6] * dt;
+    n[4] = s[4] + a * dt;
+    n[5] = s[5] + w * dt;
+    n[6] = s[6] + z * dt;
+    if (n[4] > prm[2]) n[4] = prm[2]; else if (n[4] < prm[1]) n[4] = prm[1];
+    if (n[5] > prm[4]) n[5] = prm[4]; else if (n[5] < prm[3]) n[5] = prm[3];
+    if (n[6] > prm[6]) n[6] = prm[6]; else if (n[6] < prm[5]) n[6] = prm[5];
+#pragma unroll
+    for (int i = 0; i < 7; ++i) out[i] = n[i];
+}
+
+// SnakeTrailers::doStep (agents/snake_trailers.hpp:341-369).
+__device__ void snake_step(const double *prm, int T, const double *s, double a, double w, double dt, double *out) {
+    const double Lt = prm[1], Lh = prm[2];
+    double n[kMaxDim];
+    n[0] = s[0] + cos(s[4]) * s[2] * dt;
+    n[1] = s[1] + sin(s[4]) * s[2] * dt;
+    n[4] = normalize_theta(s[4] + s[2] * tan(s[3]) / Lt * dt);
+    n[2] = s[2] + a * dt;
+    n[3] = s[3] + w * dt;
+    if (n[2] > prm[4]) n[2] = prm[4]; else if (n[2] < prm[3]) n[2] = prm[3];
+    if (n[3] > prm[6]) n[3] = prm[6]; else if (n[3] < prm[5]) n[3] = prm[5];
+    double coeff = s[2] / (Lt + Lh);
+    double prev = s[4];
+    for (int i = 1; i < T + 1; ++i) {
+        n[4 + i] = normalize_theta(s[4 + i] + coeff * sin(prev - s[4 + i]) * dt);
+        coeff *= cos(prev - s[4 + i]);
+        prev = s[4 + i];
+    }
+    for (int i = 0; i < 5 + T; ++i) out[i] = n[i];
+}
+
+__device__ __forceinline__ void put_pose(double *p, const double R[9], double x, double y, double z) {
+#pragma unroll
+    for (int i = 0; i < 9; ++i) p[i] = R[i];
+    p[9] = x;
+    p[10] = y;
+    p[11] = z;
+}
+
+// SnakeTrailers::stateToFCLTransforms (agents/snake_trailers.hpp:411-459), verbatim:
+// trailers at (-(Lt + Lh), Y, 0), rotation = rotation * identity (x*1 + y*0 + z*0).
+__device__ void snake_poses(const double *prm, int T, const double *s, double *out /*[L][12]*/) {
+    double R[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1};
+    double sv = sin(s[4]), cv = cos(s[4]);
+    R[0] = cv; R[3] = -sv; R[1] = sv; R[4] = cv;
+    put_pose(out, R, s[0], s[1], 0.0);
+    const double px = -(prm[1] + prm[2]);
+    for (int i = 1; i < T + 1; ++i) {
+        const double t = s[4 + i] - s[4 + i - 1];
+        sv = sin(t); cv = cos(t);
+        R[0] = cv; R[3] = -sv; R[1] = sv; R[4] = cv;
+        double M[9];
+#pragma unroll
+        for (int r = 0; r < 3; ++r)
+#pragma unroll
+            for (int c = 0; c < 3; ++c)
+                M[r * 3 + c] = R[r * 3 + 0] * (c == 0 ? 1.0 : 0.0) + R[r * 3 + 1] * (c == 1 ? 1.0 : 0.0) +
+                               R[r * 3 + 2] * (c == 2 ? 1.0 : 0.0);
+#pragma unroll
+        for (int j = 0; j < 9; ++j) R[j] = M[j];
+        put_pose(out + 12 * i, R, px, s[1], 0.0);
+    }
+}
+
+__global__ void k_sample(EngineParams p, uint64_t ext_base, int32_t K, double *__restrict__ samples) {
+    const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= K) return;
+    const uint64_t g = ext_base + (uint64_t)k;
+    for (int j = 0; j < p.d; ++j) samples[k * p.d + j] = engine_uniform(p.seed, g * 64 + j, p.lo[j], p.hi[j]);
+}
+
+// randomSteer + getPoses per extension.  Writes the end state, the pose slots
+// [k*pmax + i][L][12] and pcount[k].
+__global__ void k_steer(EngineParams p, uint64_t ext_base, int32_t K, const double *__restrict__ nodes,
+                        const int32_t *__restrict__ nn, double *__restrict__ ends, double *__restrict__ poses,
+                        int32_t *__restrict__ pcount, unsigned long long *__restrict__ counters) {
+    const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= K) return;
+    const uint64_t g = ext_base + (uint64_t)k;
+    const int d = p.d;
+    double from[kMaxDim], end[kMaxDim];
+    const int64_t src = nn[k] - 1;  // nn ids are 1-based
+    for (int j = 0; j < d; ++j) from[j] = nodes[src * d + j];
+    double *ps = poses + (int64_t)k * p.pmax * p.L * 12;
+    int32_t P = 0;
+    if (p.kind == MPT_AGENT_OMNI) {
+        // Omnidirectional::randomSteer (agents/omnidirectional.hpp:168-184)
+        const double rx = engine_uniform(p.seed, g * 64 + 32, -1.0, 1.0);
+        const double ry = engine_uniform(p.seed, g * 64 + 33, -1.0, 1.0);
+        const double rz = engine_uniform(p.seed, g * 64 + 34, -1.0, 1.0);
+        const double dist = sqrt(rx * rx + ry * ry + rz * rz);
+        end[0] = from[0] + rx / dist;
+        end[1] = from[1] + ry / dist;
+        end[2] = from[2] + rz / dist;
+        // Omnidirectional::getPoses (agents/omnidirectional.hpp:202-247)
+        const double I[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1};
+        const double dx = end[0] - from[0], dy = end[1] - from[1], dz = end[2] - from[2];
+        const double dd = sqrt(dx * dx + dy * dy + dz * dz);
+        const double qq = dd / p.cc_dt;
+        const unsigned it = (qq >= 4294967296.0 || !(qq >= 0)) ? 0u : (unsigned)qq;
+        if (it < 1) {
+            if (P < p.pmax) put_pose(ps + 12 * P, I, from[0], from[1], from[2]);
+            ++P;
+            if (P < p.pmax) put_pose(ps + 12 * P, I, end[0], end[1], end[2]);
+            ++P;
+        } else {
+            const double step = p.cc_dt / dd;
+            for (unsigned i = 0; i < it; ++i) {
+                const double st = step * (double)i;
+                if (P < p.pmax) put_pose(ps + 12 * P, I, from[0] + st * dx, from[1] + st * dy, from[2] + st * dz);
+                ++P;
+            }
+            if ((double)it * p.cc_dt < dd) {
+                if (P < p.pmax) put_pose(ps + 12 * P, I, end[0], end[1], end[2]);
+                ++P;
+            }
+        }
+    } else if (p.kind == MPT_AGENT_BLIMP) {
+        const double a = engine_uniform(p.seed, g * 64 + 32, -1.0, 1.0);
+        const double w = engine_uniform(p.seed, g * 64 + 33, -0.1745, 0.1745);
+        const double z = engine_uniform(p.seed, g * 64 + 34, -1.0, 1.0);
+        blimp_step(p.prm, from, a, w, z, p.steer_dt, end);
+        // build-defined Blimp::getPoses (reference stub agents/blimp.hpp:219-223 checks nothing):
+        // states after each of max(1, floor(steer_dt / cc_dt)) doStep(cc_dt), end included;
+        // R from theta as Blimp::stateToFCLTransform (agents/blimp.hpp:339-356).
+        const double qq = p.steer_dt / p.cc_dt;
+        unsigned steps = (qq >= 4294967296.0 || !(qq >= 0)) ? 0u : (unsigned)qq;
+        if (steps == 0) steps = 1;
+        double s[7];
+        for (int j = 0; j < 7; ++j) s[j] = from[j];
+        for (unsigned i = 0; i < steps; ++i) {
+            blimp_step(p.prm, s, a, w, z, p.cc_dt, s);
+            const double sv = sin(s[3]), cv = cos(s[3]);
+            const double R[9] = {cv, sv, 0, -sv, cv, 0, 0, 0, 1};
+            if (P < p.pmax) put_pose(ps + 12 * P, R, s[0], s[1], s[2]);
+            ++P;
+        }
+    } else {
+        const int T = (int)p.prm[0];
+        const double a = engine_uniform(p.seed, g * 64 + 32, -0.1, 1.0);
+        const double w = engine_uniform(p.seed, g * 64 + 33, -M_PI / 18., M_PI / 18.);
+        snake_step(p.prm, T, from, a, w, p.steer_dt, end);
+        // SnakeTrailers::getPoses (agents/snake_trailers.hpp:246-268)
+        const double qq = p.steer_dt / p.cc_dt;
+        unsigned steps = (qq >= 4294967296.0 || !(qq >= 0)) ? 0u : (unsigned)qq;
+        if (steps == 0) steps = 1;
+        double s[kMaxDim];
+        for (int j = 0; j < d; ++j) s[j] = from[j];
+        for (unsigned i = 0; i < steps; ++i) {
+            if (P < p.pmax) snake_poses(p.prm, T, s, ps + (int64_t)12 * p.L * P);
+            ++P;
+            snake_step(p.prm, T, s, a, w, p.cc_dt, s);
+        }
+    }
+    if (P > p.pmax) {
+        atomicAdd(counters + 5, 1ull);
+        P = p.pmax;
+    }
+    pcount[k] = P;
+    for (int j = 0; j < d; ++j) ends[k * d + j] = end[j];
+}
+
+// Per 256-extension block: number of collision-free extensions.
+__global__ __launch_bounds__(256) void k_count(const uint8_t *__restrict__ verdict, int32_t K,
+                                               int32_t *__restrict__ bcount) {
+    __shared__ int32_t s[4];
+    const int64_t k = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    const bool ok = k < K && verdict[k] == 0;
+    const int c = __popcll(__ballot(ok));
+    if ((threadIdx.x & 63) == 0) s[threadIdx.x >> 6] = c;
+    __syncthreads();
+    if (threadIdx.x == 0) bcount[blockIdx.x] = s[0] + s[1] + s[2] + s[3];
+}
+
+// Ordered append: extension k lands at n + (number of valid extensions before k).
+__global__ __launch_bounds__(256) void k_append(const uint8_t *__restrict__ verdict, int32_t K, int32_t d,
+                                                const double *__restrict__ ends, const int32_t *__restrict__ nn,
+                                                const int32_t *__restrict__ bcount, const int64_t *__restrict__ n_dev,
+                                                int64_t cap, double *__restrict__ nodes,
+                                                int32_t *__restrict__ parents) {
+    __shared__ int64_t s_red[256];
+    __shared__ int32_t s_wave[4];
+    const int tid = threadIdx.x;
+    int64_t acc = 0;
+    for (int64_t b = tid; b < blockIdx.x; b += 256) acc += bcount[b];
+    s_red[tid] = acc;
+    __syncthreads();
+    for (int st = 128; st > 0; st >>= 1) {
+        if (tid < st) s_red[tid] += s_red[tid + st];
+        __syncthreads();
+    }
+    const int64_t base = *n_dev + s_red[0];
+    const int64_t k = (int64_t)blockIdx.x * 256 + tid;
+    const bool ok = k < K && verdict[k] == 0;
+    const uint64_t m = __ballot(ok);
+    const int lane = tid & 63, wave = tid >> 6;
+    const int before = __popcll(m & ((1ull << lane) - 1ull));
+    if (lane == 0) s_wave[wave] = __popcll(m);
+    __syncthreads();
+    int wbase = 0;
+    for (int w = 0; w < wave; ++w) wbase += s_wave[w];
+    if (!ok) return;
+    const int64_t idx = base + wbase + before;
+    if (idx >= cap) return;
+    for (int j = 0; j < d; ++j) nodes[idx * d + j] = ends[k * d + j];
+    parents[idx] = nn[k];
+}
+
+__global__ void k_commit(const int32_t *__restrict__ bcount, int32_t nblocks, int32_t K, int64_t *__restrict__ n_dev,
+                         int64_t cap, unsigned long long *__restrict__ counters) {
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    int64_t tot = 0;
+    for (int b = 0; b < nblocks; ++b) tot += bcount[b];
+    const int64_t n = *n_dev;
+    const int64_t room = cap - n > 0 ? cap - n : 0;
+    const int64_t add = tot < room ? tot : room;
+    *n_dev = n + add;
+    counters[0] += 1;
+    counters[1] += (unsigned long long)K;
+    counters[2] += (unsigned long long)add;
+    counters[3] = (unsigned long long)(n + add);
+    counters[4] += (unsigned long long)(tot - add);
+}
+
+__global__ void k_set_n(int64_t *n_dev, int64_t n, unsigned long long *counters) {
+    *n_dev = n;
+    counters[3] = (unsigned long long)n;
+}
+
+}  // namespace
+
+struct mpt_rrt {
+    EngineParams p{};
+    EnvDev env{};
+    AgentDev *d_links = nullptr;
+    int64_t cap = 0;
+    int64_t n_upper = 0;  // host-side upper bound of the device node count
+    double *d_nodes = nullptr;
+    int32_t *d_parents = nullptr;
+    int64_t *d_n = nullptr;
+    unsigned long long *d_counters = nullptr;
+    int32_t kcap = 0;
+    double *d_samples = nullptr, *d_ends = nullptr, *d_poses = nullptr, *d_nnd2 = nullptr;
+    int32_t *d_nn = nullptr, *d_pcount = nullptr, *d_bcount = nullptr;
+    uint8_t *d_verdict = nullptr;
+    void *d_scratch = nullptr;
+    size_t scratch_bytes = 0;
+    uint64_t ext_base = 0;
+    int32_t last_K = 0;
+    bool timing = false;
+    hipEvent_t ev[7] = {};
+    float last_ms[6] = {0, 0, 0, 0, 0, 0};
+};
+
+namespace {
+void rfree(mpt_rrt *r) {
+    void *ps[] = {r->d_links, r->d_nodes, r->d_parents, r->d_n, r->d_counters, r->d_samples, r->d_ends,
+                  r->d_poses, r->d_nnd2, r->d_nn, r->d_pcount, r->d_bcount, r->d_verdict, r->d_scratch};
+    for (void *p : ps)
+        if (p) (void)hipFree(p);
+    for (auto &e : r->ev)
+        if (e) (void)hipEventDestroy(e);
+}
+
+void ensure_round_buffers(mpt_rrt *r, int32_t K) {
+    const size_t need_scratch = nn_knn_scratch_bytes(K, std::max<int64_t>(r->cap, 1), 1);
+    if (K > r->kcap) {
+        void *ps[] = {r->d_samples, r->d_ends, r->d_poses, r->d_nnd2, r->d_nn, r->d_pcount, r->d_bcount, r->d_verdict};
+        for (void *p : ps)
+            if (p) hip_check(hipFree(p), "hipFree");
+        const int64_t d = r->p.d;
+        hip_check(hipMalloc(&r->d_samples, sizeof(double) * K * d), "alloc samples");
+        hip_check(hipMalloc(&r->d_ends, sizeof(double) * K * d), "alloc ends");
+        hip_check(hipMalloc(&r->d_poses, sizeof(double) * 12 * (int64_t)K * r->p.pmax * r->p.L), "alloc poses");
+        hip_check(hipMalloc(&r->d_nnd2, sizeof(double) * K), "alloc nnd2");
+        hip_check(hipMalloc(&r->d_nn, sizeof(int32_t) * K), "alloc nn");
+        hip_check(hipMalloc(&r->d_pcount, sizeof(int32_t) * K), "alloc pcount");
+        hip_check(hipMalloc(&r->d_bcount, sizeof(int32_t) * ((K + 255) / 256)), "alloc bcount");
+        hip_check(hipMalloc(&r->d_verdict, (size_t)K), "alloc verdict");
+        r->kcap = K;
+    }
+    // the split count depends on n, so size the NN scratch for the capacity bound
+    if (need_scratch > r->scratch_bytes) {
+        if (r->d_scratch) hip_check(hipFree(r->d_scratch), "hipFree");
+        hip_check(hipMalloc(&r->d_scratch, need_scratch), "alloc nn scratch");
+        r->scratch_bytes = need_scratch;
+    }
+}
+}  // namespace
+
+extern "C" mpt_status mpt_rrt_create(const mpt_env *env, const mpt_agent *agent, int32_t agent_kind,
+                                     const double prm[7], const double *ranges, int32_t dim, double steer_dt,
+                                     double cc_dt, int64_t capacity, uint64_t seed, mpt_rrt **out) {
+    return guarded([&] {
+        if (!env || !agent || !out || !ranges) throw Error{MPT_ERR_INVALID, "null pointer"};
+        if (agent_kind < 0 || agent_kind > 2) throw Error{MPT_ERR_INVALID, "unknown agent kind"};
+        if (capacity < 1 || capacity >= (int64_t(1) << 31) - 1) throw Error{MPT_ERR_INVALID, "bad capacity"};
+        if (!(cc_dt > 0) || !(steer_dt > 0)) throw Error{MPT_ERR_INVALID, "dt must be > 0"};
+        auto *r = new mpt_rrt();
+        try {
+            EngineParams &p = r->p;
+            p.kind = agent_kind;
+            p.d = dim;
+            p.seed = seed;
+            p.steer_dt = steer_dt;
+            p.cc_dt = cc_dt;
+            if (prm) std::memcpy(p.prm, prm, sizeof(p.prm));
+            int expect = 3;
+            if (agent_kind == MPT_AGENT_BLIMP) expect = 7;
+            if (agent_kind == MPT_AGENT_SNAKE) {
+                if (!prm || prm[0] < 0 || prm[0] > kMaxDim - 5) throw Error{MPT_ERR_INVALID, "bad trailer count"};
+                expect = 5 + (int)prm[0];
+            }
+            if (dim != expect) throw Error{MPT_ERR_INVALID, "dim does not match the agent's tree state size"};
+            for (int j = 0; j < dim; ++j) {
+                p.lo[j] = ranges[2 * j];
+                p.hi[j] = ranges[2 * j + 1];
+            }
+            p.L = agent_kind == MPT_AGENT_SNAKE ? (int)prm[0] + 1 : 1;
+            if (agent_kind == MPT_AGENT_OMNI) {
+                // |end - start| = 1 up to rounding: floor(1/dt) poses + the end pose (+1 slack)
+                p.pmax = (int32_t)(1.0 / cc_dt) + 3;
+            } else {
+                const double qq = steer_dt / cc_dt;
+                p.pmax = qq >= 1 ? (int32_t)qq : 1;
+            }
+            if ((int64_t)p.pmax * p.L > 4096) throw Error{MPT_ERR_INVALID, "too many poses per edge"};
+            r->env = env_dev(env);
+            std::vector<AgentDev> links(p.L, agent_dev(agent));
+            hip_check(hipMalloc(&r->d_links, sizeof(AgentDev) * p.L), "alloc links");
+            hip_check(hipMemcpy(r->d_links, links.data(), sizeof(AgentDev) * p.L, hipMemcpyHostToDevice), "links");
+            r->cap = capacity;
+            hip_check(hipMalloc(&r->d_nodes, sizeof(double) * dim * capacity), "alloc nodes");
+            hip_check(hipMalloc(&r->d_parents, sizeof(int32_t) * capacity), "alloc parents");
+            hip_check(hipMalloc(&r->d_n, sizeof(int64_t)), "alloc n");
+            hip_check(hipMemset(r->d_n, 0, sizeof(int64_t)), "memset n");
+            hip_check(hipMalloc(&r->d_counters, sizeof(unsigned long long) * 8), "alloc counters");
+            hip_check(hipMemset(r->d_counters, 0, sizeof(unsigned long long) * 8), "memset counters");
+            for (auto &e : r->ev) hip_check(hipEventCreate(&e), "event");
+        } catch (...) {
+            rfree(r);
+            delete r;
+            throw;
+        }
+        *out = r;
+    });
+}
+
+extern "C" mpt_status mpt_rrt_destroy(mpt_rrt *r) {
+    return guarded([&] {
+        if (!r) return;
+        (void)hipDeviceSynchronize();
+        rfree(r);
+        delete r;
+    });
+}
+
+extern "C" mpt_status mpt_rrt_add_nodes(mpt_rrt *r, const double *states, const int32_t *parents, int64_t n) {
+    return guarded([&] {
+        if (!r || n < 0 || (n > 0 && !states)) throw Error{MPT_ERR_INVALID, "bad arguments"};
+        hip_check(hipDeviceSynchronize(), "sync");
+        int64_t cur = 0;
+        hip_check(hipMemcpy(&cur, r->d_n, sizeof(int64_t), hipMemcpyDeviceToHost), "n D2H");
+        if (cur + n > r->cap) throw Error{MPT_ERR_CAPACITY, "tree capacity exceeded"};
+        const int d = r->p.d;
+        if (n > 0) {
+            hip_check(hipMemcpy(r->d_nodes + cur * d, states, sizeof(double) * d * n, hipMemcpyHostToDevice), "nodes");
+            std::vector<int32_t> par(n, 0);
+            if (parents) std::memcpy(par.data(), parents, sizeof(int32_t) * n);
+            hip_check(hipMemcpy(r->d_parents + cur, par.data(), sizeof(int32_t) * n, hipMemcpyHostToDevice), "par");
+        }
+        const int64_t nn = cur + n;
+        hipLaunchKernelGGL(k_set_n, dim3(1), dim3(1), 0, 0, r->d_n, nn, r->d_counters);
+        hip_check(hipGetLastError(), "k_set_n");
+        hip_check(hipDeviceSynchronize(), "sync");
+        r->n_upper = nn;
+    });
+}
+
+extern "C" mpt_status mpt_rrt_set_size(mpt_rrt *r, int64_t n, void *stream) {
+    return guarded([&] {
+        if (!r || n < 0 || n > r->cap) throw Error{MPT_ERR_INVALID, "bad size"};
+        if (n > r->n_upper) throw Error{MPT_ERR_INVALID, "set_size can only truncate"};
+        hipLaunchKernelGGL(k_set_n, dim3(1), dim3(1), 0, (hipStream_t)stream, r->d_n, n, r->d_counters);
+        hip_check(hipGetLastError(), "k_set_n");
+        r->n_upper = n;
+    });
+}
+
+extern "C" mpt_status mpt_rrt_step(mpt_rrt *r, int32_t K, void *stream_) {
+    return guarded([&] {
+        if (!r || K < 1) throw Error{MPT_ERR_INVALID, "bad arguments"};
+        if (r->n_upper < 1) throw Error{MPT_ERR_INVALID, "tree is empty: add a root first"};
+        hipStream_t stream = (hipStream_t)stream_;
+        ensure_round_buffers(r, K);
+        const EngineParams &p = r->p;
+        const unsigned kb = (unsigned)((K + 255) / 256);
+        auto mark = [&](int i) {
+            if (r->timing) hip_check(hipEventRecord(r->ev[i], stream), "event record");
+        };
+        mark(0);
+        hipLaunchKernelGGL(k_sample, dim3(kb), dim3(256), 0, stream, p, r->ext_base, K, r->d_samples);
+        hip_check(hipGetLastError(), "k_sample");
+        mark(1);
+        NNWork w{};
+        w.pts = r->d_nodes;
+        w.removed = nullptr;
+        w.n = r->n_upper;
+        w.d = p.d;
+        w.q = r->d_samples;
+        w.nq = K;
+        w.n_dev = r->d_n;
+        launch_knn(w, 1, r->d_nn, r->d_nnd2, r->d_scratch, stream);
+        mark(2);
+        mark(3);
+        hipLaunchKernelGGL(k_steer, dim3(kb), dim3(256), 0, stream, p, r->ext_base, K, r->d_nodes, r->d_nn, r->d_ends,
+                           r->d_poses, r->d_pcount, r->d_counters);
+        hip_check(hipGetLastError(), "k_steer");
+        mark(4);
+        hip_check(hipMemsetAsync(r->d_verdict, 0, (size_t)K, stream), "verdict memset");
+        CollideWork cw{};
+        cw.poses = r->d_poses;
+        cw.pose_edge = nullptr;
+        cw.pcount = r->d_pcount;
+        cw.pmax = p.pmax;
+        cw.L = p.L;
+        cw.n_units = (int64_t)K * p.pmax * p.L;
+        cw.verdict = r->d_verdict;
+        cw.stats = nullptr;
+        launch_collide(r->env, r->d_links, cw, stream);
+        mark(5);
+        hipLaunchKernelGGL(k_count, dim3(kb), dim3(256), 0, stream, r->d_verdict, K, r->d_bcount);
+        hipLaunchKernelGGL(k_append, dim3(kb), dim3(256), 0, stream, r->d_verdict, K, p.d, r->d_ends, r->d_nn,
+                           r->d_bcount, r->d_n, r->cap, r->d_nodes, r->d_parents);
+        hipLaunchKernelGGL(k_commit, dim3(1), dim3(64), 0, stream, r->d_bcount, (int32_t)kb, K, r->d_n, r->cap,
+                           r->d_counters);
+        hip_check(hipGetLastError(), "append");
+        mark(6);
+        r->ext_base += (uint64_t)K;
+        r->n_upper = std::min<int64_t>(r->cap, r->n_upper + K);
+        r->last_K = K;
+    });
+}
+
+extern "C" mpt_status mpt_rrt_counters(mpt_rrt *r, uint64_t c[8]) {
+    return guarded([&] {
+        if (!r || !c) throw Error{MPT_ERR_INVALID, "null pointer"};
+        hip_check(hipDeviceSynchronize(), "sync");
+        unsigned long long h[8];
+        hip_check(hipMemcpy(h, r->d_counters, sizeof(h), hipMemcpyDeviceToHost), "counters");
+        for (int i = 0; i < 8; ++i) c[i] = h[i];
+    });
+}
+
+extern "C" mpt_status mpt_rrt_read_tree(mpt_rrt *r, double *states, int32_t *parents, int64_t n) {
+    return guarded([&] {
+        if (!r || n < 0 || n > r->cap) throw Error{MPT_ERR_INVALID, "bad arguments"};
+        hip_check(hipDeviceSynchronize(), "sync");
+        if (states && n) hip_check(hipMemcpy(states, r->d_nodes, sizeof(double) * r->p.d * n, hipMemcpyDeviceToHost), "");
+        if (parents && n) hip_check(hipMemcpy(parents, r->d_parents, sizeof(int32_t) * n, hipMemcpyDeviceToHost), "");
+    });
+}
+
+extern "C" mpt_status mpt_rrt_last_round(mpt_rrt *r, double *samples, int32_t *nn_ids, double *ends,
+                                         uint8_t *verdicts) {
+    return guarded([&] {
+        if (!r) throw Error{MPT_ERR_INVALID, "null pointer"};
+        hip_check(hipDeviceSynchronize(), "sync");
+        const int64_t K = r->last_K, d = r->p.d;
+        if (K == 0) return;
+        if (samples) hip_check(hipMemcpy(samples, r->d_samples, sizeof(double) * K * d, hipMemcpyDeviceToHost), "");
+        if (nn_ids) hip_check(hipMemcpy(nn_ids, r->d_nn, sizeof(int32_t) * K, hipMemcpyDeviceToHost), "");
+        if (ends) hip_check(hipMemcpy(ends, r->d_ends, sizeof(double) * K * d, hipMemcpyDeviceToHost), "");
+        if (verdicts) hip_check(hipMemcpy(verdicts, r->d_verdict, (size_t)K, hipMemcpyDeviceToHost), "");
+    });
+}
+
+extern "C" mpt_status mpt_rrt_last_poses(mpt_rrt *r, double *poses, int32_t *pose_counts) {
+    return guarded([&] {
+        if (!r) throw Error{MPT_ERR_INVALID, "null pointer"};
+        hip_check(hipDeviceSynchronize(), "sync");
+        const int64_t K = r->last_K;
+        if (K == 0) return;
+        if (poses)
+            hip_check(hipMemcpy(poses, r->d_poses, sizeof(double) * 12 * K * r->p.pmax * r->p.L, hipMemcpyDeviceToHost),
+                      "poses D2H");
+        if (pose_counts)
+            hip_check(hipMemcpy(pose_counts, r->d_pcount, sizeof(int32_t) * K, hipMemcpyDeviceToHost), "pcount D2H");
+    });
+}
+
+extern "C" mpt_status mpt_rrt_info(const mpt_rrt *r, int64_t info[4]) {
+    return guarded([&] {
+        if (!r || !info) throw Error{MPT_ERR_INVALID, "null pointer"};
+        info[0] = r->p.d;
+        info[1] = r->p.L;
+        info[2] = r->p.pmax;
+        info[3] = r->cap;
+    });
+}
+
+extern "C" mpt_status mpt_rrt_enable_timing(mpt_rrt *r, int32_t enable) {
+    return guarded([&] {
+        if (!r) throw Error{MPT_ERR_INVALID, "null pointer"};
+        r->timing = enable != 0;
+    });
+}
+
+extern "C" mpt_status mpt_rrt_kernel_times(mpt_rrt *r, float ms[6]) {
+    return guarded([&] {
+        if (!r || !ms) throw Error{MPT_ERR_INVALID, "null pointer"};
+        if (!r->timing) throw Error{MPT_ERR_INVALID, "timing not enabled"};
+        hip_check(hipEventSynchronize(r->ev[6]), "event sync");
+        // [sample, nn (+merge), (reserved), steer, collide, append]
+        const int a[6] = {0, 1, 2, 3, 4, 5};
+        const int b[6] = {1, 2, 3, 4, 5, 6};
+        for (int i = 0; i < 6; ++i) hip_check(hipEventElapsedTime(&ms[i], r->ev[a[i]], r->ev[b[i]]), "elapsed");
+    });
+}

@@ -1,0 +1,962 @@
+/*
+ * mpt_oracle.c -- TEST INFRASTRUCTURE ONLY (see mpt_oracle.h header).
+ *
+ * CPU restatement of the reference's hot path.  Every function cites the
+ * reference call site it follows (paths relative to the reference root) and,
+ * where the arithmetic lives in FCL 0.3.2 / FLANN 1.8.4 (not vendored, not in
+ * the container), the upstream routine it restates, marked [upstream].
+ *
+ * Build: gcc -O2 -std=c99 -fPIC -ffp-contract=off -fno-fast-math (oracle/Makefile).
+ * FMA contraction must stay off: FCL/FLANN were built for x86-64 SSE2 without FMA.
+ */
+#define _GNU_SOURCE
+#include "mpt_oracle.h"
+
+#include <float.h>
+#include <math.h>
+#include <stdlib.h>
+#include <string.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+
+#ifndef M_PI
+#define M_PI 3.14159265358979323846
+#endif
+
+/* ======================================================================
+ * FCL 0.3.2 math [upstream]: fcl/math/vec_3f.h, matrix_3f.h, transform.cpp
+ * ====================================================================== */
+
+static inline double dot3(const double a[3], const double b[3]) {
+    /* Vec3Data::dot: x*x' + y*y' + z*z' */
+    return a[0] * b[0] + a[1] * b[1] + a[2] * b[2];
+}
+static inline void cross3(const double a[3], const double b[3], double o[3]) {
+    /* Vec3Data::cross */
+    o[0] = a[1] * b[2] - a[2] * b[1];
+    o[1] = a[2] * b[0] - a[0] * b[2];
+    o[2] = a[0] * b[1] - a[1] * b[0];
+}
+static inline void sub3(const double a[3], const double b[3], double o[3]) {
+    o[0] = a[0] - b[0];
+    o[1] = a[1] - b[1];
+    o[2] = a[2] - b[2];
+}
+
+/* Quaternion3f::toRotation [upstream]; used by fcl_helpers::parseTransform
+ * (utilities/fcl_helpers.hpp:16-25) through Transform3f(quaternion, vector). */
+void orc_quat_to_rot(const double q[4], double R[9]) {
+    const double w = q[0], x = q[1], y = q[2], z = q[3];
+    const double twoX = 2.0 * x, twoY = 2.0 * y, twoZ = 2.0 * z;
+    const double twoWX = twoX * w, twoWY = twoY * w, twoWZ = twoZ * w;
+    const double twoXX = twoX * x, twoXY = twoY * x, twoXZ = twoZ * x;
+    const double twoYY = twoY * y, twoYZ = twoZ * y, twoZZ = twoZ * z;
+    R[0] = 1.0 - (twoYY + twoZZ); R[1] = twoXY - twoWZ;         R[2] = twoXZ + twoWY;
+    R[3] = twoXY + twoWZ;         R[4] = 1.0 - (twoXX + twoZZ); R[5] = twoYZ - twoWX;
+    R[6] = twoXZ - twoWY;         R[7] = twoYZ + twoWX;         R[8] = 1.0 - (twoXX + twoYY);
+}
+
+/* fcl::relativeTransform [upstream], called by setupMeshCollisionOrientedNode with
+ * (tf1 = env object, tf2 = agent object) -- the callback order of
+ * envManager->collide(agentManager) at utilities/meshhandler.hpp:229. */
+void orc_relative_transform(const double R1[9], const double T1[3],
+                            const double R2[9], const double T2[3],
+                            double R[9], double T[3]) {
+    /* Matrix3Data::transposeTimes: (R1^T R2)(i,j) = sum_k R1(k,i) R2(k,j), k ascending */
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j)
+            R[i * 3 + j] = R1[0 * 3 + i] * R2[0 * 3 + j] + R1[1 * 3 + i] * R2[1 * 3 + j] +
+                           R1[2 * 3 + i] * R2[2 * 3 + j];
+    double d[3];
+    sub3(T2, T1, d);
+    for (int i = 0; i < 3; ++i) T[i] = R1[0 * 3 + i] * d[0] + R1[1 * 3 + i] * d[1] + R1[2 * 3 + i] * d[2];
+}
+
+/* Matrix3f * Vec3f (dotX/dotY/dotZ) followed by + T. */
+void orc_transform_point(const double R[9], const double T[3], const double q[3], double out[3]) {
+    for (int i = 0; i < 3; ++i) {
+        const double r = R[i * 3 + 0] * q[0] + R[i * 3 + 1] * q[1] + R[i * 3 + 2] * q[2];
+        out[i] = r + T[i];
+    }
+}
+
+/* Intersect::project6 [upstream]: 0 = separated along ax. */
+static inline int project6(const double ax[3], const double p1[3], const double p2[3],
+                           const double p3[3], const double q1[3], const double q2[3],
+                           const double q3[3]) {
+    const double P1 = dot3(ax, p1), P2 = dot3(ax, p2), P3 = dot3(ax, p3);
+    const double Q1 = dot3(ax, q1), Q2 = dot3(ax, q2), Q3 = dot3(ax, q3);
+    const double mx1 = fmax(P1, fmax(P2, P3)), mn1 = fmin(P1, fmin(P2, P3));
+    const double mx2 = fmax(Q1, fmax(Q2, Q3)), mn2 = fmin(Q1, fmin(Q2, Q3));
+    if (mn1 > mx2) return 0;
+    if (mn2 > mx1) return 0;
+    return 1;
+}
+
+/* Intersect::intersect_Triangle(P1,P2,P3,Q1,Q2,Q3) [upstream, FCL 0.3.2 intersect.cpp]:
+ * 17 separating-axis tests (n1, m1, e_i x f_j, e_i x n1, f_j x m1) in the frame
+ * translated to P1.  Touching counts as intersection (strict '>' in project6). */
+int orc_tri_intersect(const double P[9], const double Q[9]) {
+    const double *P1 = P, *P2 = P + 3, *P3 = P + 6;
+    const double *Q1 = Q, *Q2 = Q + 3, *Q3 = Q + 6;
+    double p1[3], p2[3], p3[3], q1[3], q2[3], q3[3];
+    sub3(P1, P1, p1); sub3(P2, P1, p2); sub3(P3, P1, p3);
+    sub3(Q1, P1, q1); sub3(Q2, P1, q2); sub3(Q3, P1, q3);
+    double e1[3], e2[3], e3[3], f1[3], f2[3], f3[3];
+    sub3(p2, p1, e1); sub3(p3, p2, e2); sub3(p1, p3, e3);
+    sub3(q2, q1, f1); sub3(q3, q2, f2); sub3(q1, q3, f3);
+    double n1[3], m1[3], ax[3];
+    cross3(e1, e2, n1);
+    if (!project6(n1, p1, p2, p3, q1, q2, q3)) return 0;
+    cross3(f1, f2, m1);
+    if (!project6(m1, p1, p2, p3, q1, q2, q3)) return 0;
+    const double *E[3] = {e1, e2, e3}, *F[3] = {f1, f2, f3};
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) {
+            cross3(E[i], F[j], ax);
+            if (!project6(ax, p1, p2, p3, q1, q2, q3)) return 0;
+        }
+    for (int i = 0; i < 3; ++i) {
+        cross3(E[i], n1, ax);
+        if (!project6(ax, p1, p2, p3, q1, q2, q3)) return 0;
+    }
+    for (int j = 0; j < 3; ++j) {
+        cross3(F[j], m1, ax);
+        if (!project6(ax, p1, p2, p3, q1, q2, q3)) return 0;
+    }
+    return 1;
+}
+
+static inline void map_tri(const double R[9], const double T[3], const double *Q, double *out) {
+    orc_transform_point(R, T, Q, out);
+    orc_transform_point(R, T, Q + 3, out + 3);
+    orc_transform_point(R, T, Q + 6, out + 6);
+}
+
+/* Intersect::intersect_Triangle(P1..3, Q1..3, R, T) [upstream]: Q_i' = R Q_i + T. */
+int orc_tri_intersect_RT(const double P[9], const double Q[9], const double R[9], const double T[3]) {
+    double Qp[9];
+    map_tri(R, T, Q, Qp);
+    return orc_tri_intersect(P, Qp);
+}
+
+/* ======================================================================
+ * Collision: MeshHandler::isInCollision (utilities/meshhandler.hpp:187-243) +
+ * fcl_helpers::defaultCollisionFunction (utilities/fcl_helpers.hpp:52-65).
+ * Verdict = exists (env tri, agent tri) pair not separated by intersect_Triangle;
+ * FCL's broadphase/OBB tests only prune, so the all-pairs loop is the definition.
+ * ====================================================================== */
+
+static void unit_RT(const double env_tf[12], const double pose[12], double R[9], double T[3]) {
+    orc_relative_transform(env_tf, env_tf + 9, pose, pose + 9, R, T);
+}
+
+int orc_collide_unit(const double *env_tris, int64_t Te, const double env_tf[12],
+                     const double *agent_tris, int64_t Ta, const double pose[12]) {
+    double R[9], T[3], Qp[9];
+    unit_RT(env_tf, pose, R, T);
+    for (int64_t b = 0; b < Ta; ++b) {
+        map_tri(R, T, agent_tris + 9 * b, Qp);
+        for (int64_t a = 0; a < Te; ++a)
+            if (orc_tri_intersect(env_tris + 9 * a, Qp)) return 1;
+    }
+    return 0;
+}
+
+void orc_collide_batch(const double *env_tris, int64_t Te, const double env_tf[12],
+                       const double *agent_tris, const int64_t *link_tri_off, int32_t L,
+                       const double *poses, const int64_t *edge_pose_offsets, int64_t E,
+                       uint8_t *verdict) {
+    for (int64_t e = 0; e < E; ++e) {
+        int hit = 0;
+        for (int64_t p = edge_pose_offsets[e]; p < edge_pose_offsets[e + 1] && !hit; ++p)
+            for (int32_t l = 0; l < L && !hit; ++l)
+                hit = orc_collide_unit(env_tris, Te, env_tf, agent_tris + 9 * link_tri_off[l],
+                                       link_tri_off[l + 1] - link_tri_off[l],
+                                       poses + 12 * (p * L + l));
+        verdict[e] = (uint8_t)hit;
+    }
+}
+
+/* ---------------- AABB tree (speed only; conservative margins) ---------------- */
+struct orc_bvh {
+    int64_t T, nn;
+    double *tris;   /* [T][9], reordered copy */
+    double *lo, *hi; /* [nn][3] */
+    int64_t *left;  /* child index or -1 - first tri for leaf */
+    int64_t *cnt;   /* leaf triangle count, 0 for inner */
+};
+
+/* margin applied to every box comparison: far above the rounding error of the
+ * 17-axis test, so pruning never removes a pair the all-pairs loop would report. */
+static inline double bmargin(double a, double b) { return 1e-9 * (1.0 + fabs(a) + fabs(b)); }
+static inline int box_overlap(const double *alo, const double *ahi, const double *blo, const double *bhi) {
+    for (int k = 0; k < 3; ++k) {
+        if (alo[k] > bhi[k] + bmargin(alo[k], bhi[k])) return 0;
+        if (blo[k] > ahi[k] + bmargin(blo[k], ahi[k])) return 0;
+    }
+    return 1;
+}
+static void tri_box(const double *t, double lo[3], double hi[3]) {
+    for (int k = 0; k < 3; ++k) {
+        lo[k] = fmin(t[k], fmin(t[3 + k], t[6 + k]));
+        hi[k] = fmax(t[k], fmax(t[3 + k], t[6 + k]));
+    }
+}
+
+typedef struct { double c[3]; int64_t idx; } cent_t;
+static int g_axis;
+static int cent_cmp(const void *a, const void *b) {
+    const cent_t *x = (const cent_t *)a, *y = (const cent_t *)b;
+    if (x->c[g_axis] < y->c[g_axis]) return -1;
+    if (x->c[g_axis] > y->c[g_axis]) return 1;
+    return (x->idx < y->idx) ? -1 : (x->idx > y->idx);
+}
+
+static int64_t bvh_rec(orc_bvh *b, cent_t *c, int64_t first, int64_t n, const double *src) {
+    const int64_t node = b->nn++;
+    double lo[3] = {DBL_MAX, DBL_MAX, DBL_MAX}, hi[3] = {-DBL_MAX, -DBL_MAX, -DBL_MAX};
+    double clo[3] = {DBL_MAX, DBL_MAX, DBL_MAX}, chi[3] = {-DBL_MAX, -DBL_MAX, -DBL_MAX};
+    for (int64_t i = first; i < first + n; ++i) {
+        double tl[3], th[3];
+        tri_box(src + 9 * c[i].idx, tl, th);
+        for (int k = 0; k < 3; ++k) {
+            lo[k] = fmin(lo[k], tl[k]); hi[k] = fmax(hi[k], th[k]);
+            clo[k] = fmin(clo[k], c[i].c[k]); chi[k] = fmax(chi[k], c[i].c[k]);
+        }
+    }
+    memcpy(b->lo + 3 * node, lo, sizeof lo);
+    memcpy(b->hi + 3 * node, hi, sizeof hi);
+    if (n <= 2) {
+        b->left[node] = first;
+        b->cnt[node] = n;
+        return node;
+    }
+    int ax = 0;
+    for (int k = 1; k < 3; ++k)
+        if (chi[k] - clo[k] > chi[ax] - clo[ax]) ax = k;
+    g_axis = ax;
+    qsort(c + first, (size_t)n, sizeof(cent_t), cent_cmp);
+    const int64_t h = n / 2;
+    b->cnt[node] = 0;
+    const int64_t l = bvh_rec(b, c, first, h, src);
+    (void)l;
+    const int64_t r = bvh_rec(b, c, first + h, n - h, src);
+    b->left[node] = r; /* left child is node + 1, store the right one */
+    return node;
+}
+
+orc_bvh *orc_bvh_build(const double *tris, int64_t T) {
+    orc_bvh *b = (orc_bvh *)calloc(1, sizeof *b);
+    b->T = T;
+    const int64_t cap = 2 * (T > 0 ? T : 1);
+    b->tris = (double *)malloc(sizeof(double) * 9 * (size_t)(T > 0 ? T : 1));
+    b->lo = (double *)malloc(sizeof(double) * 3 * (size_t)cap);
+    b->hi = (double *)malloc(sizeof(double) * 3 * (size_t)cap);
+    b->left = (int64_t *)malloc(sizeof(int64_t) * (size_t)cap);
+    b->cnt = (int64_t *)malloc(sizeof(int64_t) * (size_t)cap);
+    if (T == 0) return b;
+    cent_t *c = (cent_t *)malloc(sizeof(cent_t) * (size_t)T);
+    for (int64_t i = 0; i < T; ++i) {
+        for (int k = 0; k < 3; ++k) c[i].c[k] = (tris[9 * i + k] + tris[9 * i + 3 + k] + tris[9 * i + 6 + k]) / 3.0;
+        c[i].idx = i;
+    }
+    bvh_rec(b, c, 0, T, tris);
+    for (int64_t i = 0; i < T; ++i) memcpy(b->tris + 9 * i, tris + 9 * c[i].idx, 9 * sizeof(double));
+    free(c);
+    return b;
+}
+
+void orc_bvh_free(orc_bvh *b) {
+    if (!b) return;
+    free(b->tris); free(b->lo); free(b->hi); free(b->left); free(b->cnt);
+    free(b);
+}
+
+int orc_collide_unit_bvh(const orc_bvh *env, const double env_tf[12],
+                         const double *agent_tris, int64_t Ta, const double pose[12],
+                         int64_t *n_tri_tests) {
+    if (env->T == 0) return 0;
+    double R[9], T[3], Qp[9], qlo[3], qhi[3];
+    int64_t stack[128];
+    unit_RT(env_tf, pose, R, T);
+    int64_t tests = 0;
+    for (int64_t b = 0; b < Ta; ++b) {
+        map_tri(R, T, agent_tris + 9 * b, Qp);
+        tri_box(Qp, qlo, qhi);
+        int sp = 0;
+        stack[sp++] = 0;
+        while (sp) {
+            const int64_t nd = stack[--sp];
+            if (!box_overlap(qlo, qhi, env->lo + 3 * nd, env->hi + 3 * nd)) continue;
+            if (env->cnt[nd]) {
+                for (int64_t i = env->left[nd]; i < env->left[nd] + env->cnt[nd]; ++i) {
+                    double tl[3], th[3];
+                    tri_box(env->tris + 9 * i, tl, th);
+                    if (!box_overlap(qlo, qhi, tl, th)) continue;
+                    ++tests;
+                    if (orc_tri_intersect(env->tris + 9 * i, Qp)) {
+                        if (n_tri_tests) *n_tri_tests += tests;
+                        return 1;
+                    }
+                }
+            } else {
+                stack[sp++] = env->left[nd];
+                stack[sp++] = nd + 1;
+            }
+        }
+    }
+    if (n_tri_tests) *n_tri_tests += tests;
+    return 0;
+}
+
+void orc_collide_batch_bvh(const orc_bvh *env, const double env_tf[12],
+                           const double *agent_tris, const int64_t *link_tri_off, int32_t L,
+                           const double *poses, const int64_t *edge_pose_offsets, int64_t E,
+                           uint8_t *verdict, int nthreads) {
+#ifdef _OPENMP
+    if (nthreads < 1) nthreads = 1;
+#pragma omp parallel for schedule(dynamic, 16) num_threads(nthreads)
+#endif
+    for (int64_t e = 0; e < E; ++e) {
+        int hit = 0;
+        for (int64_t p = edge_pose_offsets[e]; p < edge_pose_offsets[e + 1] && !hit; ++p)
+            for (int32_t l = 0; l < L && !hit; ++l)
+                hit = orc_collide_unit_bvh(env, env_tf, agent_tris + 9 * link_tri_off[l],
+                                           link_tri_off[l + 1] - link_tri_off[l],
+                                           poses + 12 * (p * L + l), NULL);
+        verdict[e] = (uint8_t)hit;
+    }
+    (void)nthreads;
+}
+
+/* ======================================================================
+ * FLANN 1.8.4 [upstream]: flann/algorithms/dist.h L2<double>::operator(),
+ * used by FLANN_KDTreeWrapper (utilities/flannkdtreewrapper.hpp:57-117).
+ * ====================================================================== */
+
+double orc_l2(const double *a, const double *b, int32_t d) {
+    double result = 0.0;
+    int32_t i = 0;
+    /* while (a < lastgroup), lastgroup = last - 3: groups of 4 */
+    for (; i + 3 < d; i += 4) {
+        const double d0 = a[i] - b[i], d1 = a[i + 1] - b[i + 1];
+        const double d2 = a[i + 2] - b[i + 2], d3 = a[i + 3] - b[i + 3];
+        result += d0 * d0 + d1 * d1 + d2 * d2 + d3 * d3;
+    }
+    for (; i < d; ++i) {
+        const double d0 = a[i] - b[i];
+        result += d0 * d0;
+    }
+    return result;
+}
+
+/* (d2, id) lexicographic: the canonical order of every NN result in this build
+ * (FLANN's own tie order is traversal order; exact ties are canonicalised to the
+ * lowest id). */
+static inline int better(double da, int32_t ia, double db, int32_t ib) {
+    return da < db || (da == db && ia < ib);
+}
+
+static void topk_insert(double *bd, int32_t *bi, int32_t k, double dd, int32_t id) {
+    if (!better(dd, id, bd[k - 1], bi[k - 1])) return;
+    int32_t j = k - 1;
+    while (j > 0 && better(dd, id, bd[j - 1], bi[j - 1])) {
+        bd[j] = bd[j - 1];
+        bi[j] = bi[j - 1];
+        --j;
+    }
+    bd[j] = dd;
+    bi[j] = id;
+}
+
+void orc_knn(const double *pts, const uint8_t *removed, int64_t n, int32_t d,
+             const double *q, int64_t nq, int32_t k, int32_t *ids, double *d2) {
+    for (int64_t s = 0; s < nq; ++s) {
+        double *bd = d2 + s * k;
+        int32_t *bi = ids + s * k;
+        for (int32_t j = 0; j < k; ++j) { bd[j] = INFINITY; bi[j] = -1; }
+        for (int64_t i = 0; i < n; ++i) {
+            if (removed && removed[i]) continue;
+            topk_insert(bd, bi, k, orc_l2(q + s * d, pts + i * d, d), (int32_t)(i + 1));
+        }
+    }
+}
+
+typedef struct { double d; int32_t id; } did_t;
+static int did_cmp(const void *a, const void *b) {
+    const did_t *x = (const did_t *)a, *y = (const did_t *)b;
+    if (better(x->d, x->id, y->d, y->id)) return -1;
+    if (better(y->d, y->id, x->d, x->id)) return 1;
+    return 0;
+}
+
+int64_t orc_radius(const double *pts, const uint8_t *removed, int64_t n, int32_t d,
+                   const double *q, int64_t nq, double r2, int32_t max_nb,
+                   int64_t *offsets, int32_t *ids, double *d2, int64_t cap) {
+    did_t *buf = (did_t *)malloc(sizeof(did_t) * (size_t)(n > 0 ? n : 1));
+    int64_t total = 0;
+    for (int64_t s = 0; s < nq; ++s) {
+        int64_t m = 0;
+        for (int64_t i = 0; i < n; ++i) {
+            if (removed && removed[i]) continue;
+            const double dd = orc_l2(q + s * d, pts + i * d, d);
+            if (dd < r2) { buf[m].d = dd; buf[m].id = (int32_t)(i + 1); ++m; }
+        }
+        qsort(buf, (size_t)m, sizeof(did_t), did_cmp);
+        if (max_nb > 0 && m > max_nb) m = max_nb;
+        if (offsets) offsets[s] = total;
+        for (int64_t j = 0; j < m; ++j, ++total)
+            if (total < cap) { ids[total] = buf[j].id; d2[total] = buf[j].d; }
+    }
+    if (offsets) offsets[nq] = total;
+    free(buf);
+    return total;
+}
+
+/* ---------------- kd-tree (CPU baseline, KDTreeSingleIndex-like) ---------------- */
+struct orc_kdtree {
+    int64_t n;
+    int32_t d;
+    double *pts;     /* reordered [n][d] */
+    int32_t *ids;    /* 1-based ids in reordered order */
+    int64_t nn;
+    int32_t *dim;    /* split dim, -1 leaf */
+    double *split;
+    int64_t *a, *b; /* inner: left,right ; leaf: first,count */
+};
+
+static const double *g_kd_pts;
+static int32_t g_kd_d, g_kd_dim;
+static int idx_cmp(const void *x, const void *y) {
+    const int64_t i = *(const int64_t *)x, j = *(const int64_t *)y;
+    const double a = g_kd_pts[i * g_kd_d + g_kd_dim], b = g_kd_pts[j * g_kd_d + g_kd_dim];
+    if (a < b) return -1;
+    if (a > b) return 1;
+    return (i < j) ? -1 : (i > j);
+}
+
+static int64_t kd_rec(orc_kdtree *t, int64_t *idx, int64_t first, int64_t n, const double *src) {
+    const int64_t node = t->nn++;
+    if (n <= 8) {
+        t->dim[node] = -1;
+        t->a[node] = first;
+        t->b[node] = n;
+        return node;
+    }
+    int32_t best = 0;
+    double bw = -1;
+    for (int32_t k = 0; k < t->d; ++k) {
+        double lo = DBL_MAX, hi = -DBL_MAX;
+        for (int64_t i = first; i < first + n; ++i) {
+            const double v = src[idx[i] * t->d + k];
+            lo = fmin(lo, v); hi = fmax(hi, v);
+        }
+        if (hi - lo > bw) { bw = hi - lo; best = k; }
+    }
+    g_kd_pts = src; g_kd_d = t->d; g_kd_dim = best;
+    qsort(idx + first, (size_t)n, sizeof(int64_t), idx_cmp);
+    const int64_t h = n / 2;
+    t->dim[node] = best;
+    t->split[node] = src[idx[first + h] * t->d + best];
+    t->a[node] = kd_rec(t, idx, first, h, src);
+    t->b[node] = kd_rec(t, idx, first + h, n - h, src);
+    return node;
+}
+
+orc_kdtree *orc_kdtree_build(const double *pts, int64_t n, int32_t d) {
+    orc_kdtree *t = (orc_kdtree *)calloc(1, sizeof *t);
+    t->n = n; t->d = d;
+    const int64_t cap = 2 * (n / 4 + 2);
+    t->pts = (double *)malloc(sizeof(double) * (size_t)(n * d + 1));
+    t->ids = (int32_t *)malloc(sizeof(int32_t) * (size_t)(n + 1));
+    t->dim = (int32_t *)malloc(sizeof(int32_t) * (size_t)cap);
+    t->split = (double *)malloc(sizeof(double) * (size_t)cap);
+    t->a = (int64_t *)malloc(sizeof(int64_t) * (size_t)cap);
+    t->b = (int64_t *)malloc(sizeof(int64_t) * (size_t)cap);
+    int64_t *idx = (int64_t *)malloc(sizeof(int64_t) * (size_t)(n + 1));
+    for (int64_t i = 0; i < n; ++i) idx[i] = i;
+    if (n > 0) kd_rec(t, idx, 0, n, pts);
+    for (int64_t i = 0; i < n; ++i) {
+        memcpy(t->pts + i * d, pts + idx[i] * d, sizeof(double) * (size_t)d);
+        t->ids[i] = (int32_t)(idx[i] + 1);
+    }
+    free(idx);
+    return t;
+}
+
+void orc_kdtree_free(orc_kdtree *t) {
+    if (!t) return;
+    free(t->pts); free(t->ids); free(t->dim); free(t->split); free(t->a); free(t->b);
+    free(t);
+}
+
+static void kd_search(const orc_kdtree *t, int64_t node, const double *q, int32_t k, double *bd, int32_t *bi) {
+    if (t->dim[node] < 0) {
+        for (int64_t i = t->a[node]; i < t->a[node] + t->b[node]; ++i)
+            topk_insert(bd, bi, k, orc_l2(q, t->pts + i * t->d, t->d), t->ids[i]);
+        return;
+    }
+    const int32_t dm = t->dim[node];
+    const double diff = q[dm] - t->split[node];
+    const int64_t nearc = diff < 0 ? t->a[node] : t->b[node];
+    const int64_t farc = diff < 0 ? t->b[node] : t->a[node];
+    kd_search(t, nearc, q, k, bd, bi);
+    /* Exact pruning: every far-side point p has |q-p|_dm >= |diff| and FLANN's sum of
+     * non-negative terms is monotone, so fl(d2(p)) >= fl(diff*diff).  Strict '>'
+     * keeps exact ties, which the (d2, id) order then resolves. */
+    if (diff * diff > bd[k - 1]) return;
+    kd_search(t, farc, q, k, bd, bi);
+}
+
+void orc_kdtree_knn(const orc_kdtree *t, const double *q, int64_t nq, int32_t k,
+                    int32_t *ids, double *d2, int nthreads) {
+#ifdef _OPENMP
+    if (nthreads < 1) nthreads = 1;
+#pragma omp parallel for schedule(static) num_threads(nthreads)
+#endif
+    for (int64_t s = 0; s < nq; ++s) {
+        double *bd = d2 + s * k;
+        int32_t *bi = ids + s * k;
+        for (int32_t j = 0; j < k; ++j) { bd[j] = INFINITY; bi[j] = -1; }
+        if (t->n > 0) kd_search(t, 0, q + s * t->d, k, bd, bi);
+    }
+    (void)nthreads;
+}
+
+/* ======================================================================
+ * RNG restatements
+ * ====================================================================== */
+
+/* glibc stdlib/random_r.c TYPE_3 (x**31 + x**3 + 1), srandom_r + random_r. */
+void orc_glibc_srand(orc_glibc_rand *s, uint32_t seed) {
+    int32_t *r = s->r;
+    (void)r;
+    int32_t state[31];
+    if (seed == 0) seed = 1;
+    state[0] = (int32_t)seed;
+    int32_t word = (int32_t)seed;
+    for (int i = 1; i < 31; ++i) {
+        /* word = 16807 * hi/lo (Schrage), as srandom_r */
+        const long hi = word / 127773;
+        const long lo = word % 127773;
+        word = (int32_t)(16807 * lo - 2836 * hi);
+        if (word < 0) word += 2147483647;
+        state[i] = word;
+    }
+    memcpy(s->r, state, sizeof state);
+    s->f = 3;   /* fptr = &state[SEP_3] */
+    s->b = 0;   /* rptr = &state[0] */
+    for (int i = 0; i < 310; ++i) (void)orc_glibc_rand_next(s);
+}
+
+int32_t orc_glibc_rand_next(orc_glibc_rand *s) {
+    uint32_t *st = (uint32_t *)s->r;
+    const uint32_t val = (st[s->f] += st[s->b]);
+    const int32_t result = (int32_t)(val >> 1);
+    if (++s->f >= 31) { s->f = 0; ++s->b; }
+    else if (++s->b >= 31) s->b = 0;
+    return result;
+}
+
+/* std::linear_congruential_engine<uint_fast32_t, 16807, 0, 2147483647> */
+void orc_minstd_seed(orc_minstd *g, uint64_t seed) {
+    uint64_t x = seed % 2147483647ULL;
+    g->x = x == 0 ? 1 : x;
+}
+uint64_t orc_minstd_next(orc_minstd *g) {
+    g->x = (g->x * 16807ULL) % 2147483647ULL;
+    return g->x;
+}
+
+/* libstdc++ (GCC 11) std::generate_canonical<double, 53>(minstd_rand0):
+ * R = max - min + 1 = 2147483646, log2R = floor(log2(R)) = 30, m = 2 draws. */
+static double generate_canonical_minstd(orc_minstd *g) {
+    const long double r = 2147483646.0L;
+    double sum = 0.0, tmp = 1.0;
+    for (int k = 2; k != 0; --k) {
+        sum += (double)(orc_minstd_next(g) - 1ULL) * tmp;
+        tmp = (double)((long double)tmp * r);
+    }
+    double ret = sum / tmp;
+    if (ret >= 1.0) ret = nextafter(1.0, 0.0);
+    return ret;
+}
+
+/* uniform_real_distribution<double>::operator(): (canonical * (b - a)) + a */
+double orc_uniform_real(orc_minstd *g, double a, double b) {
+    return generate_canonical_minstd(g) * (b - a) + a;
+}
+
+/* Device engine RNG (the build's, not the reference's): splitmix64 finaliser of
+ * seed ^ golden*counter, top 53 bits -> [0,1), then (u * (b - a)) + a. */
+static inline uint64_t mix64(uint64_t z) {
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+    return z ^ (z >> 31);
+}
+double orc_engine_uniform(uint64_t seed, uint64_t counter, double a, double b) {
+    const uint64_t z = mix64(seed + 0x9E3779B97F4A7C15ULL * (counter + 1ULL));
+    const double u = (double)(z >> 11) * (1.0 / 9007199254740992.0);
+    return u * (b - a) + a;
+}
+
+/* ======================================================================
+ * Agents
+ * ====================================================================== */
+
+static void identity_pose(const double t[3], double *pose) {
+    static const double I[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1};
+    memcpy(pose, I, sizeof I);
+    pose[9] = t[0]; pose[10] = t[1]; pose[11] = t[2];
+}
+
+/* Omnidirectional::randomSteer, agents/omnidirectional.hpp:168-184 */
+static double omni_steer_from(const double r[3], const double start[3], double end[3]) {
+    const double dist = sqrt(r[0] * r[0] + r[1] * r[1] + r[2] * r[2]);
+    end[0] = start[0] + r[0] / dist;
+    end[1] = start[1] + r[1] / dist;
+    end[2] = start[2] + r[2] / dist;
+    return dist;
+}
+double orc_omni_random_steer(orc_glibc_rand *rng, const double start[3], double end[3]) {
+    const double RM = 2147483647.0; /* RAND_MAX */
+    double r[3];
+    for (int i = 0; i < 3; ++i) r[i] = ((double)orc_glibc_rand_next(rng) - (RM / 2)) / (RM / 2);
+    return omni_steer_from(r, start, end);
+}
+
+/* Omnidirectional::getPoses, agents/omnidirectional.hpp:202-247 */
+int32_t orc_omni_get_poses(const double start[3], const double end[3], double dt,
+                           double *poses_out, int32_t maxP) {
+    const double dx = end[0] - start[0], dy = end[1] - start[1], dz = end[2] - start[2];
+    const double dist = sqrt(dx * dx + dy * dy + dz * dz);
+    const double q = dist / dt;
+    const unsigned int iterations = (q >= 4294967296.0 || !(q >= 0)) ? 0u : (unsigned int)q;
+    int32_t P = 0;
+    if (iterations < 1) {
+        if (P < maxP) identity_pose(start, poses_out + 12 * P);
+        ++P;
+        if (P < maxP) identity_pose(end, poses_out + 12 * P);
+        ++P;
+    } else {
+        const double step = dt / dist;
+        for (unsigned int i = 0; i < iterations; ++i) {
+            const double stepSize = step * (double)i;
+            const double t[3] = {start[0] + stepSize * dx, start[1] + stepSize * dy,
+                                 start[2] + stepSize * dz};
+            if (P < maxP) identity_pose(t, poses_out + 12 * P);
+            ++P;
+        }
+        if ((double)iterations * dt < dist) {
+            if (P < maxP) identity_pose(end, poses_out + 12 * P);
+            ++P;
+        }
+    }
+    return P;
+}
+
+static double normalize_theta(double t) {
+    /* Blimp/SnakeTrailers::normalizeTheta */
+    return t - 2 * M_PI * floor((t + M_PI) / (2 * M_PI));
+}
+
+/* Blimp::doStep, agents/blimp.hpp:293-317 (theta update omits dt, as written) */
+void orc_blimp_do_step(const double prm[7], const double s[7], double a, double w, double z,
+                       double dt, double out[7]) {
+    const double L = prm[0], vmin = prm[1], vmax = prm[2], pmin = prm[3], pmax = prm[4];
+    const double zmin = prm[5], zmax = prm[6];
+    double n[7];
+    n[0] = s[0] + cos(s[3]) * s[4] * dt;
+    n[1] = s[1] + sin(s[3]) * s[4] * dt;
+    n[3] = normalize_theta(s[3] + s[4] * tan(s[5]) / L);
+    n[2] = s[2] + s[6] * dt;
+    n[4] = s[4] + a * dt;
+    n[5] = s[5] + w * dt;
+    n[6] = s[6] + z * dt;
+    if (n[4] > vmax) n[4] = vmax; else if (n[4] < vmin) n[4] = vmin;
+    if (n[5] > pmax) n[5] = pmax; else if (n[5] < pmin) n[5] = pmin;
+    if (n[6] > zmax) n[6] = zmax; else if (n[6] < zmin) n[6] = zmin;
+    memcpy(out, n, sizeof n);
+}
+
+/* Blimp::randomSteer, agents/blimp.hpp:179-187: draws a, w, z in that order from
+ * uniform(-1,1), uniform(-0.1745,0.1745), uniform(-1,1) on one default engine. */
+void orc_blimp_random_steer(const double prm[7], orc_minstd *g, const double start[7],
+                            double dt, double end[7], double awz[3]) {
+    awz[0] = orc_uniform_real(g, -1, 1);
+    awz[1] = orc_uniform_real(g, -0.1745, 0.1745);
+    awz[2] = orc_uniform_real(g, -1, 1);
+    orc_blimp_do_step(prm, start, awz[0], awz[1], awz[2], dt, end);
+}
+
+/* Blimp::stateToFCLTransform, agents/blimp.hpp:339-356 */
+static void blimp_pose(const double s[7], double *pose) {
+    const double sv = sin(s[3]), cv = cos(s[3]);
+    const double R[9] = {cv, sv, 0, -sv, cv, 0, 0, 0, 1};
+    memcpy(pose, R, sizeof R);
+    pose[9] = s[0]; pose[10] = s[1]; pose[11] = s[2];
+}
+
+/* Build-defined Blimp::getPoses (the reference's agents/blimp.hpp:219-223 returns one
+ * empty pose list, i.e. never checks): the states after each of the
+ * max(1, floor(edge_dt / dt)) doStep(dt) increments, end state included. */
+int32_t orc_blimp_get_poses(const double prm[7], const double start[7], const double awz[3],
+                            double edge_dt, double dt, double *poses_out, int32_t maxP) {
+    const double q = edge_dt / dt;
+    unsigned int steps = (q >= 4294967296.0 || !(q >= 0)) ? 0u : (unsigned int)q;
+    if (steps == 0) steps = 1;
+    double s[7];
+    memcpy(s, start, sizeof s);
+    for (unsigned int i = 0; i < steps; ++i) {
+        orc_blimp_do_step(prm, s, awz[0], awz[1], awz[2], dt, s);
+        if ((int32_t)i < maxP) blimp_pose(s, poses_out + 12 * i);
+    }
+    return (int32_t)steps;
+}
+
+/* SnakeTrailers::doStep, agents/snake_trailers.hpp:341-369 */
+void orc_snake_do_step(const double prm[7], const double *s, double a, double w, double dt,
+                       double *out) {
+    const int T = (int)prm[0];
+    const double Lt = prm[1], Lh = prm[2], vmin = prm[3], vmax = prm[4], pmin = prm[5], pmax = prm[6];
+    enum { X = 0, Y = 1, V = 2, PSI = 3, THETA = 4 };
+    double n[64];
+    n[X] = s[X] + cos(s[THETA]) * s[V] * dt;
+    n[Y] = s[Y] + sin(s[THETA]) * s[V] * dt;
+    n[THETA] = normalize_theta(s[THETA] + s[V] * tan(s[PSI]) / Lt * dt);
+    n[V] = s[V] + a * dt;
+    n[PSI] = s[PSI] + w * dt;
+    if (n[V] > vmax) n[V] = vmax; else if (n[V] < vmin) n[V] = vmin;
+    if (n[PSI] > pmax) n[PSI] = pmax; else if (n[PSI] < pmin) n[PSI] = pmin;
+    double coeff = s[V] / (Lt + Lh);
+    double prev = s[THETA];
+    for (int i = 1; i < T + 1; ++i) {
+        n[THETA + i] = normalize_theta(s[THETA + i] + coeff * sin(prev - s[THETA + i]) * dt);
+        coeff *= cos(prev - s[THETA + i]);
+        prev = s[THETA + i];
+    }
+    memcpy(out, n, sizeof(double) * (size_t)(5 + T));
+}
+
+/* SnakeTrailers::randomSteer, agents/snake_trailers.hpp:206-213: a ~ U(-0.1, 1),
+ * w ~ U(-pi/18, pi/18) from the agent's default engine. */
+void orc_snake_random_steer(const double prm[7], orc_minstd *g, const double *start, double dt,
+                            double *end, double aw[2]) {
+    aw[0] = orc_uniform_real(g, -0.1, 1);
+    aw[1] = orc_uniform_real(g, -M_PI / 18., M_PI / 18.);
+    orc_snake_do_step(prm, start, aw[0], aw[1], dt, end);
+}
+
+/* SnakeTrailers::stateToFCLTransforms, agents/snake_trailers.hpp:411-459, verbatim:
+ * trailer translations are (-(Lt+Lh), Y, 0), not chained. */
+static void snake_poses(const double prm[7], const double *s, double *poses /*[L][12]*/) {
+    const int T = (int)prm[0];
+    const double Lt = prm[1], Lh = prm[2];
+    enum { X = 0, Y = 1, THETA = 4 };
+    double pose_t[3] = {s[X], s[Y], 0};
+    double R[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1};
+    double sv = sin(s[THETA]), cv = cos(s[THETA]);
+    R[0] = cv; R[3] = -sv; R[1] = sv; R[4] = cv;
+    memcpy(poses, R, sizeof R);
+    memcpy(poses + 9, pose_t, sizeof pose_t);
+    for (int i = 1; i < T + 1; ++i) {
+        pose_t[0] = -(Lt + Lh);
+        const double t = s[THETA + i] - s[THETA + i - 1];
+        sv = sin(t); cv = cos(t);
+        R[0] = cv; R[3] = -sv; R[1] = sv; R[4] = cv;
+        /* rotation = rotation * identity: Matrix3Data::operator* sums x*1 + y*0 + z*0 */
+        double M[9];
+        for (int r = 0; r < 3; ++r)
+            for (int c = 0; c < 3; ++c) {
+                const double I0 = (c == 0), I1 = (c == 1), I2 = (c == 2);
+                M[r * 3 + c] = R[r * 3 + 0] * I0 + R[r * 3 + 1] * I1 + R[r * 3 + 2] * I2;
+            }
+        memcpy(R, M, sizeof M);
+        memcpy(poses + 12 * i, R, sizeof R);
+        memcpy(poses + 12 * i + 9, pose_t, sizeof pose_t);
+    }
+}
+
+/* SnakeTrailers::getPoses, agents/snake_trailers.hpp:246-268 */
+int32_t orc_snake_get_poses(const double prm[7], const double *start, const double aw[2],
+                            double edge_dt, double dt, double *poses_out, int32_t maxP) {
+    const int T = (int)prm[0];
+    const int L = T + 1;
+    const double q = edge_dt / dt;
+    unsigned int steps = (q >= 4294967296.0 || !(q >= 0)) ? 0u : (unsigned int)q;
+    if (steps == 0) steps = 1;
+    double s[64];
+    memcpy(s, start, sizeof(double) * (size_t)(5 + T));
+    for (unsigned int i = 0; i < steps; ++i) {
+        if ((int32_t)i < maxP) snake_poses(prm, s, poses_out + (size_t)12 * L * i);
+        orc_snake_do_step(prm, s, aw[0], aw[1], dt, s);
+    }
+    return (int32_t)steps;
+}
+
+/* ======================================================================
+ * Sequential RRT: planners/rrt.hpp:21-94 with UniformSampler
+ * (samplers/uniformsampler.hpp:20-35), TreeInterface (tree_interfaces/treeinterface.hpp),
+ * FLANN_KDTreeWrapper ids (utilities/flannkdtreewrapper.hpp:21-40) and Map3D::safeEdge
+ * (workspaces/map3d.hpp:33-37).
+ * ====================================================================== */
+
+static int is_goal(int kind, const double *s, const double *g, const double *thr) {
+    if (kind == 2) return fabs(s[0] - g[0]) < thr[0] && fabs(s[1] - g[1]) < thr[1];
+    return fabs(s[0] - g[0]) < thr[0] && fabs(s[1] - g[1]) < thr[1] && fabs(s[2] - g[2]) < thr[2];
+}
+
+#define ORC_MAXP 4096
+
+int64_t orc_rrt_run(int32_t agent_kind, const double *prm, int32_t d, const double *ranges,
+                    const double *start, const double *goal, const double *goal_thr,
+                    double steer_dt, double cc_dt,
+                    const double *env_tris, int64_t Te, const double env_tf[12],
+                    const double *agent_tris, int64_t Ta,
+                    int64_t iterations_at_a_time, int64_t max_nodes,
+                    double *nodes, int32_t *parents, int64_t *solved, int64_t *iters_out) {
+    *solved = -1;
+    *iters_out = 0;
+    /* rrt.hpp:27-30: goal test before anything is inserted */
+    if (is_goal(agent_kind, start, goal, goal_thr)) { *solved = -2; return 0; }
+    orc_minstd sampler;     /* UniformSampler::generator (uniformsampler.hpp:43) */
+    orc_minstd agent_gen;   /* Blimp/SnakeTrailers::generator */
+    orc_glibc_rand crand;   /* glibc rand() for Omnidirectional (never seeded: srand(1)) */
+    orc_minstd_seed(&sampler, 1);
+    orc_minstd_seed(&agent_gen, 1);
+    orc_glibc_srand(&crand, 1);
+    orc_bvh *env = orc_bvh_build(env_tris, Te);
+    const int L = agent_kind == 2 ? (int)prm[0] + 1 : 1;
+    double *poses = (double *)malloc(sizeof(double) * 12 * (size_t)ORC_MAXP * (size_t)L);
+    /* rrt.hpp:32-35: root = Edge(start), inserted first (FLANN id 1) */
+    memcpy(nodes, start, sizeof(double) * (size_t)d);
+    parents[0] = 0;
+    int64_t n = 1;
+    double sample[64], end[64], ctrl[3];
+    unsigned int iterations = 0;
+    const int64_t iat = iterations_at_a_time;
+    int64_t pass;
+    for (pass = 0; pass < 100000000; ++pass) {
+        for (int32_t j = 0; j < d; ++j) sample[j] = orc_uniform_real(&sampler, ranges[2 * j], ranges[2 * j + 1]);
+        /* nearest: exact 1-NN, lowest id on exact ties */
+        int64_t best = 0;
+        double bd = INFINITY;
+        for (int64_t i = 0; i < n; ++i) {
+            const double dd = orc_l2(sample, nodes + i * d, d);
+            if (dd < bd) { bd = dd; best = i; }
+        }
+        const double *from = nodes + best * d;
+        int32_t P;
+        const double edge_dt = steer_dt;  /* Blimp/Snake Edge::dt = cost = steering dt */
+        if (agent_kind == 0) {
+            (void)orc_omni_random_steer(&crand, from, end);
+            P = orc_omni_get_poses(from, end, cc_dt, poses, ORC_MAXP);
+        } else if (agent_kind == 1) {
+            orc_blimp_random_steer(prm, &agent_gen, from, steer_dt, end, ctrl);
+            P = orc_blimp_get_poses(prm, from, ctrl, edge_dt, cc_dt, poses, ORC_MAXP);
+        } else {
+            orc_snake_random_steer(prm, &agent_gen, from, steer_dt, end, ctrl);
+            P = orc_snake_get_poses(prm, from, ctrl, edge_dt, cc_dt, poses, ORC_MAXP);
+        }
+        if (P > ORC_MAXP) P = ORC_MAXP;
+        int hit = 0;
+        for (int32_t p = 0; p < P && !hit; ++p)
+            for (int l = 0; l < L && !hit; ++l)
+                hit = orc_collide_unit_bvh(env, env_tf, agent_tris, Ta, poses + 12 * ((size_t)p * L + l), NULL);
+        if (hit) {  /* rrt.hpp:50-56 (iterations counted twice, as written) */
+            ++iterations;
+            if (iat > 0 && ++iterations > (unsigned int)iat) break;
+            continue;
+        }
+        if (is_goal(agent_kind, end, goal, goal_thr)) { *solved = pass; break; }
+        if (n >= max_nodes) break;
+        memcpy(nodes + n * d, end, sizeof(double) * (size_t)d);
+        parents[n] = (int32_t)(best + 1);
+        ++n;
+        if (iat > 0 && ++iterations > (unsigned int)iat) break;
+    }
+    *iters_out = pass;
+    free(poses);
+    orc_bvh_free(env);
+    return n;
+}
+
+/* ======================================================================
+ * Batched device-engine step (the build's throughput mode; see
+ * motionplanningtoolkit_amd/csrc/rrt_engine.hip): K extensions against the tree
+ * snapshot, collision-free edges appended in extension order.
+ * Counter layout per extension g: dims use counter g*64 + j, controls g*64 + 32 + j.
+ * ====================================================================== */
+
+int64_t orc_engine_step(int32_t agent_kind, const double *prm, int32_t d, const double *ranges,
+                        double steer_dt, double cc_dt, uint64_t seed, uint64_t ext_base,
+                        int32_t K, const orc_bvh *env, const double env_tf[12],
+                        const double *agent_tris, int64_t Ta,
+                        double *nodes, int32_t *parents, int64_t n_nodes, int64_t capacity,
+                        int32_t *nn_out, uint8_t *verdict_out, int nthreads, int use_kdtree) {
+    const int L = agent_kind == 2 ? (int)prm[0] + 1 : 1;
+    double *samples = (double *)malloc(sizeof(double) * (size_t)K * (size_t)d);
+    double *ends = (double *)malloc(sizeof(double) * (size_t)K * (size_t)d);
+    int32_t *ids = nn_out;
+    double *d2 = (double *)malloc(sizeof(double) * (size_t)K);
+    for (int32_t k = 0; k < K; ++k) {
+        const uint64_t g = ext_base + (uint64_t)k;
+        for (int32_t j = 0; j < d; ++j)
+            samples[k * d + j] = orc_engine_uniform(seed, g * 64 + j, ranges[2 * j], ranges[2 * j + 1]);
+    }
+    if (use_kdtree) {
+        orc_kdtree *t = orc_kdtree_build(nodes, n_nodes, d);
+        orc_kdtree_knn(t, samples, K, 1, ids, d2, nthreads);
+        orc_kdtree_free(t);
+    } else {
+        orc_knn(nodes, NULL, n_nodes, d, samples, K, 1, ids, d2);
+    }
+#ifdef _OPENMP
+    if (nthreads < 1) nthreads = 1;
+#pragma omp parallel for schedule(dynamic, 16) num_threads(nthreads)
+#endif
+    for (int32_t k = 0; k < K; ++k) {
+        const uint64_t g = ext_base + (uint64_t)k;
+        const double *from = nodes + (int64_t)(ids[k] - 1) * d;
+        double *end = ends + (size_t)k * d;
+        double poses[12 * 64];
+        int32_t P;
+        if (agent_kind == 0) {
+            double r[3];
+            for (int j = 0; j < 3; ++j) r[j] = orc_engine_uniform(seed, g * 64 + 32 + j, -1.0, 1.0);
+            omni_steer_from(r, from, end);
+            P = orc_omni_get_poses(from, end, cc_dt, poses, 64);
+        } else if (agent_kind == 1) {
+            double awz[3];
+            awz[0] = orc_engine_uniform(seed, g * 64 + 32, -1, 1);
+            awz[1] = orc_engine_uniform(seed, g * 64 + 33, -0.1745, 0.1745);
+            awz[2] = orc_engine_uniform(seed, g * 64 + 34, -1, 1);
+            orc_blimp_do_step(prm, from, awz[0], awz[1], awz[2], steer_dt, end);
+            P = orc_blimp_get_poses(prm, from, awz, steer_dt, cc_dt, poses, 64);
+        } else {
+            double aw[2];
+            aw[0] = orc_engine_uniform(seed, g * 64 + 32, -0.1, 1);
+            aw[1] = orc_engine_uniform(seed, g * 64 + 33, -M_PI / 18., M_PI / 18.);
+            orc_snake_do_step(prm, from, aw[0], aw[1], steer_dt, end);
+            P = orc_snake_get_poses(prm, from, aw, steer_dt, cc_dt, poses, 64 / L);
+        }
+        if (P > 64 / L) P = 64 / L;
+        int hit = 0;
+        for (int32_t p = 0; p < P && !hit; ++p)
+            for (int l = 0; l < L && !hit; ++l)
+                hit = orc_collide_unit_bvh(env, env_tf, agent_tris, Ta, poses + 12 * ((size_t)p * L + l), NULL);
+        verdict_out[k] = (uint8_t)hit;
+    }
+    int64_t n = n_nodes;
+    for (int32_t k = 0; k < K; ++k) {
+        if (verdict_out[k]) continue;
+        if (n >= capacity) break;
+        memcpy(nodes + n * d, ends + (size_t)k * d, sizeof(double) * (size_t)d);
+        parents[n] = ids[k];
+        ++n;
+    }
+    free(samples); free(ends); free(d2);
+    return n;
+}

@@ -1,0 +1,134 @@
+"""GPU parity: batched collision verdicts (k_collide through mpt_collide_batch) against the
+oracle's all-pairs FCL verdicts.  Bar: bit-exact verdicts."""
+import math
+
+import numpy as np
+import pytest
+
+from motionplanningtoolkit_amd import scenes
+
+pytestmark = pytest.mark.gpu
+
+I = np.array([1, 0, 0, 0, 1, 0, 0, 0, 1], np.float64)
+
+
+def pose(t, R=I):
+    return np.r_[np.asarray(R, np.float64).ravel(), np.asarray(t, np.float64)]
+
+
+def rot(ax, a):
+    c, s = math.cos(a), math.sin(a)
+    if ax == 2:
+        return np.array([c, -s, 0, s, c, 0, 0, 0, 1], np.float64)
+    if ax == 1:
+        return np.array([c, 0, s, 0, 1, 0, -s, 0, c], np.float64)
+    return np.array([1, 0, 0, 0, c, -s, 0, s, c], np.float64)
+
+
+def random_rot(rng):
+    R = rot(2, rng.uniform(0, 2 * math.pi)).reshape(3, 3)
+    R = R @ rot(1, rng.uniform(0, 2 * math.pi)).reshape(3, 3)
+    R = R @ rot(0, rng.uniform(0, 2 * math.pi)).reshape(3, 3)
+    return R.ravel()
+
+
+def check(mpt, oracle, env_tris, env_tf, links, poses, off):
+    env = mpt.Environment(env_tris, env_tf)
+    ags = [mpt.AgentMesh(t) for t in links]
+    got = mpt.collide_batch(env, ags, poses, off)
+    ref = oracle.collide_batch(env_tris, env_tf, links, poses, off)
+    assert np.array_equal(got, ref), np.nonzero(got != ref)
+    return got
+
+
+def test_box_box_known_answers(mpt_gpu, oracle):
+    box = scenes.read_obj(scenes.mesh_path("agent_unit_box"), "last")
+    ts = [(0, 0, 0), (0.99, 0, 0), (1.0, 0, 0), (1.01, 0, 0), (0, 0, -1.5), (0.6, 0.6, 0.6), (1.01, 1.01, 1.01)]
+    expect = [1, 1, 1, 0, 0, 1, 0]
+    poses = np.array([pose(t) for t in ts]).reshape(-1, 1, 12)
+    got = check(mpt_gpu, oracle, box, pose([0, 0, 0]), [box], poses, np.arange(len(ts) + 1))
+    assert got.tolist() == expect
+    R = rot(2, math.pi / 4)
+    poses = np.array([pose((1.19, 0, 0), R), pose((1.22, 0, 0), R)]).reshape(-1, 1, 12)
+    got = check(mpt_gpu, oracle, box, pose([0, 0, 0]), [box], poses, np.arange(3))
+    assert got.tolist() == [1, 0]
+
+
+@pytest.mark.parametrize("agent_mode", ["last", "all"])
+def test_blimp_room_random_poses(mpt_gpu, oracle, agent_mode):
+    rng = np.random.default_rng(11 if agent_mode == "all" else 12)
+    env = scenes.read_obj(scenes.mesh_path("env_model"))
+    agent = scenes.read_obj(scenes.mesh_path("agent_blimp"), agent_mode)
+    n = 600
+    poses = np.array([pose(rng.uniform([-10, -10, -10], [185, 145, 120]), random_rot(rng)) for _ in range(n)])
+    got = check(mpt_gpu, oracle, env, pose([0, 0, 0]), [agent], poses.reshape(-1, 1, 12), np.arange(n + 1))
+    assert 0 < got.sum() < n
+
+
+def test_near_contact_poses(mpt_gpu, oracle):
+    """Poses bisected to within ~1e-9 of first contact with the room walls: the pruning
+    margins must never change a verdict."""
+    rng = np.random.default_rng(5)
+    env = scenes.read_obj(scenes.mesh_path("env_model"))
+    agent = scenes.read_obj(scenes.mesh_path("agent_blimp"), "last")
+    tf = pose([0, 0, 0])
+    poses = []
+    for _ in range(60):
+        R = random_rot(rng)
+        a = rng.uniform([20, 20, 20], [150, 110, 90])  # inside the room
+        d = rng.normal(size=3)
+        d /= np.linalg.norm(d)
+        lo, hi = 0.0, 300.0
+        hit = lambda s: oracle.collide_batch(env, tf, [agent], pose(a + s * d, R).reshape(1, 1, 12),
+                                             np.array([0, 1]))[0]
+        if hit(lo) or not hit(hi):
+            continue
+        for _ in range(45):
+            mid = 0.5 * (lo + hi)
+            if hit(mid):
+                hi = mid
+            else:
+                lo = mid
+        poses += [pose(a + lo * d, R), pose(a + hi * d, R)]
+    poses = np.array(poses).reshape(-1, 1, 12)
+    got = check(mpt_gpu, oracle, env, tf, [agent], poses, np.arange(len(poses) + 1))
+    assert got.reshape(-1, 2)[:, 0].sum() == 0 and got.reshape(-1, 2)[:, 1].all()
+
+
+def test_env_transform_and_multi_pose_edges(mpt_gpu, oracle):
+    rng = np.random.default_rng(2)
+    box = scenes.read_obj(scenes.mesh_path("agent_unit_box"), "last")
+    env = scenes.corridor_env(0)
+    tf = np.r_[random_rot(rng), [1.5, -2.0, 0.25]]
+    P = rng.integers(0, 9, size=300)  # ragged, including edges with no poses
+    off = np.r_[0, np.cumsum(P)]
+    poses = np.array([pose(rng.uniform([-6, -50, -1], [6, 50, 1]), random_rot(rng)) for _ in range(off[-1])])
+    got = check(mpt_gpu, oracle, env, tf, [box], poses.reshape(-1, 1, 12), off)
+    assert got[P == 0].sum() == 0
+
+
+def test_snake_links(mpt_gpu, oracle):
+    """11 links per pose (SnakeTrailers::getMeshes), the corridor env."""
+    rng = np.random.default_rng(3)
+    sc = scenes.snake_scenario("corridor")
+    E = 200
+    poses = []
+    for _ in range(E):
+        s = np.array([rng.uniform(lo, hi) for lo, hi in sc.ranges])
+        poses.append(oracle.snake_get_poses(sc.prm, s, [0.3, 0.05], sc.steer_dt, sc.cc_dt))
+    poses = np.concatenate(poses)  # [E][11][12]
+    links = [sc.agent_tris] * sc.links
+    got = check(mpt_gpu, oracle, sc.env_tris, sc.env_tf, links, poses, np.arange(E + 1))
+    assert 0 < got.sum() < E
+
+
+def test_empty_and_degenerate(mpt_gpu, oracle):
+    box = scenes.read_obj(scenes.mesh_path("agent_unit_box"), "last")
+    env = mpt_gpu.Environment(box)
+    ag = mpt_gpu.AgentMesh(box)
+    assert mpt_gpu.collide_batch(env, [ag], np.zeros((0, 1, 12)), np.array([0])).shape == (0,)
+    v = mpt_gpu.collide_batch(env, [ag], pose([0, 0, 0]).reshape(1, 1, 12), np.array([0, 0, 0, 1]))
+    assert v.tolist() == [0, 0, 1]
+    # an empty environment never collides
+    empty = mpt_gpu.Environment(np.zeros((0, 9)))
+    assert mpt_gpu.collide_batch(empty, [ag], pose([0, 0, 0]).reshape(1, 1, 12), np.array([0, 1])).tolist() == [0]

@@ -1,0 +1,124 @@
+"""GPU parity: one batched RRT round of the device engine (k_sample -> k_knn1 -> k_steer ->
+k_collide -> ordered append) checked stage by stage against the oracle.
+
+Bars: samples, NN ids, collision verdicts and the append order are bit-exact; the steer
+and pose stages use device sin/cos/tan (ROCm ocml) where the oracle uses glibc libm, so
+states and poses are compared within 1e-12 relative (they agree to the last ulp or two),
+and verdicts are then checked bit-exactly on the device's own poses."""
+import math
+
+import numpy as np
+import pytest
+
+from motionplanningtoolkit_amd import scenes
+
+pytestmark = pytest.mark.gpu
+
+RTOL = 1e-12
+
+
+def bits(a):
+    return np.ascontiguousarray(a, np.float64).view(np.uint64)
+
+
+def make(mpt, sc, n0, K, seed, cap_extra=None):
+    rng = np.random.default_rng(seed)
+    tree = rng.uniform(sc.ranges[:, 0], sc.ranges[:, 1], size=(n0, sc.dim))
+    env = mpt.Environment(sc.env_tris, sc.env_tf)
+    ag = mpt.AgentMesh(sc.agent_tris)
+    eng = mpt.RRTEngine(env, ag, sc.kind, sc.prm, sc.ranges, sc.steer_dt, sc.cc_dt,
+                        capacity=n0 + (cap_extra if cap_extra is not None else 4 * K), seed=seed)
+    eng.add_nodes(tree)
+    return eng, tree
+
+
+def expected_controls(oracle, sc, seed, g):
+    if sc.kind == 0:
+        return [oracle.engine_uniform(seed, g * 64 + 32 + j, -1.0, 1.0) for j in range(3)]
+    if sc.kind == 1:
+        return [oracle.engine_uniform(seed, g * 64 + 32, -1, 1), oracle.engine_uniform(seed, g * 64 + 33, -0.1745, 0.1745),
+                oracle.engine_uniform(seed, g * 64 + 34, -1, 1)]
+    return [oracle.engine_uniform(seed, g * 64 + 32, -0.1, 1), oracle.engine_uniform(seed, g * 64 + 33, -math.pi / 18,
+                                                                                     math.pi / 18)]
+
+
+def check_round(mpt, oracle, sc, eng, tree, seed, ext_base, K):
+    eng.step(K)
+    samples, nn, ends, verdict = eng.last_round(K)
+    poses, pcount = eng.last_poses(K)
+    inf = eng.info()
+    # 1. samples: pure +,-,* arithmetic on the counter hash -> bit-exact
+    exp_s = np.array([[oracle.engine_uniform(seed, (ext_base + k) * 64 + j, lo, hi)
+                       for j, (lo, hi) in enumerate(sc.ranges)] for k in range(K)])
+    assert np.array_equal(bits(samples), bits(exp_s))
+    # 2. nearest neighbours over the snapshot
+    ri, _ = oracle.knn(tree, samples, 1)
+    assert np.array_equal(nn, ri[:, 0])
+    # 3. steer + poses (transcendentals: tolerance)
+    exp_end = np.zeros_like(ends)
+    for k in range(K):
+        g = ext_base + k
+        frm = tree[nn[k] - 1]
+        c = expected_controls(oracle, sc, seed, g)
+        if sc.kind == 0:
+            r = np.array(c)
+            dist = math.sqrt(r[0] * r[0] + r[1] * r[1] + r[2] * r[2])
+            exp_end[k] = frm + r / dist
+            exp_p = oracle.omni_get_poses(frm, exp_end[k], sc.cc_dt)
+            assert pcount[k] == len(exp_p)
+            assert np.array_equal(bits(ends[k]), bits(exp_end[k]))  # no transcendentals
+            assert np.array_equal(bits(poses[k, :pcount[k], 0]), bits(exp_p))
+        elif sc.kind == 1:
+            exp_end[k] = oracle.blimp_do_step(sc.prm, frm, c[0], c[1], c[2], sc.steer_dt)
+            exp_p = oracle.blimp_get_poses(sc.prm, frm, c, sc.steer_dt, sc.cc_dt)
+            assert pcount[k] == len(exp_p)
+            np.testing.assert_allclose(poses[k, :pcount[k], 0], exp_p, rtol=RTOL, atol=1e-13)
+        else:
+            exp_end[k] = oracle.snake_do_step(sc.prm, frm, c[0], c[1], sc.steer_dt)
+            exp_p = oracle.snake_get_poses(sc.prm, frm, c, sc.steer_dt, sc.cc_dt)
+            assert pcount[k] == len(exp_p)
+            np.testing.assert_allclose(poses[k, :pcount[k]], exp_p, rtol=RTOL, atol=1e-13)
+    np.testing.assert_allclose(ends, exp_end, rtol=RTOL, atol=1e-13)
+    # 4. verdicts on the device's own poses: bit-exact
+    flat = np.concatenate([poses[k, :pcount[k]] for k in range(K)]).reshape(-1, inf["links"], 12)
+    off = np.r_[0, np.cumsum(pcount)]
+    ref_v = oracle.collide_batch(sc.env_tris, sc.env_tf, [sc.agent_tris] * inf["links"], flat, off)
+    assert np.array_equal(verdict, ref_v)
+    # 5. ordered append
+    valid = np.nonzero(verdict == 0)[0]
+    n_new = len(tree) + len(valid)
+    c = eng.counters()
+    assert c["nodes"] == n_new and c["valid"] >= len(valid)
+    t2, par = eng.read_tree(n_new)
+    assert np.array_equal(bits(t2[:len(tree)]), bits(tree))
+    assert np.array_equal(bits(t2[len(tree):]), bits(ends[valid]))
+    assert np.array_equal(par[len(tree):], nn[valid])
+    return t2, verdict
+
+
+@pytest.mark.parametrize("name", ["omni", "blimp", "snake"])
+def test_engine_rounds(mpt_gpu, oracle, name):
+    if name == "omni":
+        sc, n0, K = scenes.omni_scenario(), 3000, 1024
+    elif name == "blimp":
+        sc, n0, K = scenes.blimp_scenario("all"), 5000, 1500
+    else:
+        sc, n0, K = scenes.snake_scenario("corridor"), 3000, 700
+    seed = 1234
+    eng, tree = make(mpt_gpu, sc, n0, K, seed)
+    tree, v1 = check_round(mpt_gpu, oracle, sc, eng, tree, seed, 0, K)
+    assert 0 < v1.sum() < K or name == "snake"
+    # second round sees the first round's nodes
+    tree, _ = check_round(mpt_gpu, oracle, sc, eng, tree, seed, K, K // 2 + 3)
+
+
+def test_engine_set_size_and_capacity(mpt_gpu, oracle):
+    sc = scenes.omni_scenario()
+    eng, tree = make(mpt_gpu, sc, 100, 256, 5, cap_extra=50)
+    eng.step(256)
+    c = eng.counters()
+    assert c["nodes"] == 150 and c["capacity_drops"] > 0
+    eng.set_size(100)
+    assert eng.counters()["nodes"] == 100
+    t, _ = eng.read_tree(100)
+    assert np.array_equal(t, tree)

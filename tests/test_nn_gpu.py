@@ -1,0 +1,106 @@
+"""GPU parity: exact NN (k_knn1 / k_knnk / radius) against the oracle's FLANN-order brute
+force.  Bar: ids exact, squared distances bit-exact."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def bits(a):
+    return np.ascontiguousarray(a, np.float64).view(np.uint64)
+
+
+@pytest.mark.parametrize("d,n,nq", [(3, 1, 5), (3, 5000, 700), (7, 20000, 1024), (15, 3000, 300), (5, 4000, 257)])
+def test_knn1_exact(mpt_gpu, oracle, d, n, nq):
+    rng = np.random.default_rng(d * 1000 + n)
+    pts = rng.uniform(-100, 100, size=(n, d))
+    q = rng.uniform(-100, 100, size=(nq, d))
+    nn = mpt_gpu.NearestNeighbors(d, 16)
+    ids = nn.append(pts)
+    assert ids.tolist() == list(range(1, n + 1))
+    gi, gd = nn.knn(q, 1)
+    ri, rd = oracle.knn(pts, q, 1)
+    assert np.array_equal(gi, ri)
+    assert np.array_equal(bits(gd), bits(rd))
+
+
+@pytest.mark.parametrize("k", [2, 10, 16, 32])
+def test_knn_k_exact(mpt_gpu, oracle, k):
+    rng = np.random.default_rng(k)
+    pts = rng.uniform(-10, 10, size=(6000, 7))
+    q = rng.uniform(-10, 10, size=(500, 7))
+    nn = mpt_gpu.NearestNeighbors(7)
+    nn.append(pts)
+    gi, gd = nn.knn(q, k)
+    ri, rd = oracle.knn(pts, q, k)
+    assert np.array_equal(gi, ri)
+    assert np.array_equal(bits(gd), bits(rd))
+
+
+def test_ties_resolve_to_lowest_id(mpt_gpu, oracle):
+    rng = np.random.default_rng(7)
+    base = rng.integers(-3, 4, size=(500, 3)).astype(np.float64)  # lattice: many exact ties
+    pts = np.concatenate([base, base, base])
+    q = rng.integers(-3, 4, size=(300, 3)).astype(np.float64) + 0.5
+    nn = mpt_gpu.NearestNeighbors(3)
+    nn.append(pts)
+    for k in (1, 4):
+        gi, gd = nn.knn(q, k)
+        ri, rd = oracle.knn(pts, q, k)
+        assert np.array_equal(gi, ri) and np.array_equal(bits(gd), bits(rd))
+
+
+def test_fewer_points_than_k_and_removed(mpt_gpu, oracle):
+    nn = mpt_gpu.NearestNeighbors(2)
+    nn.append([[0.0, 0.0], [1.0, 0.0], [2.0, 0.0]])
+    gi, gd = nn.knn([[0.9, 0.0]], 5)
+    assert gi.tolist() == [[2, 1, 3, -1, -1]] and np.isinf(gd[0, 3:]).all()
+    nn.remove(2)
+    gi, _ = nn.knn([[0.9, 0.0]], 2)
+    assert gi.tolist() == [[1, 3]]
+    assert len(nn) == 3
+
+
+def test_incremental_append_growth(mpt_gpu, oracle):
+    rng = np.random.default_rng(9)
+    nn = mpt_gpu.NearestNeighbors(7, 4)
+    pts = []
+    for _ in range(20):
+        p = rng.uniform(-1, 1, size=(rng.integers(1, 500), 7))
+        nn.append(p)
+        pts.append(p)
+    pts = np.concatenate(pts)
+    q = rng.uniform(-1, 1, size=(200, 7))
+    gi, gd = nn.knn(q, 3)
+    ri, rd = oracle.knn(pts, q, 3)
+    assert np.array_equal(gi, ri) and np.array_equal(bits(gd), bits(rd))
+
+
+@pytest.mark.parametrize("max_nb", [-1, 3])
+def test_radius_exact(mpt_gpu, oracle, max_nb):
+    rng = np.random.default_rng(4)
+    pts = rng.uniform(0, 20, size=(8000, 3))
+    q = rng.uniform(0, 20, size=(300, 3))
+    nn = mpt_gpu.NearestNeighbors(3)
+    nn.append(pts)
+    go, gi, gd = nn.radius(q, 2.0, max_nb)
+    ro, ri, rd = oracle.radius(pts, q, 2.0, max_nb)
+    assert np.array_equal(go, ro)
+    assert np.array_equal(gi, ri)
+    assert np.array_equal(bits(gd), bits(rd))
+
+
+def test_baseline_scale_tree(mpt_gpu, oracle):
+    """BASELINE config 2 scale: 100k-node blimp tree (d = 7), 4096 queries; checked
+    against the kd-tree oracle (itself bit-identical to brute force, test_oracle.py)."""
+    from motionplanningtoolkit_amd import scenes
+
+    rng = np.random.default_rng(100)
+    ranges = scenes.blimp_ranges()
+    pts = rng.uniform(ranges[:, 0], ranges[:, 1], size=(100_000, 7))
+    q = rng.uniform(ranges[:, 0], ranges[:, 1], size=(4096, 7))
+    nn = mpt_gpu.NearestNeighbors(7, 100_000)
+    nn.append(pts)
+    gi, gd = nn.knn(q, 1)
+    ri, rd = oracle.KDTree(pts).knn(q, 1, nthreads=8)
+    assert np.array_equal(gi, ri) and np.array_equal(bits(gd), bits(rd))

@@ -1,0 +1,279 @@
+"""CPU: pin the oracle (oracle/mpt_oracle.c) before trusting it as the checker.
+
+The reference ships no tests or golden vectors and cannot be built here, so the oracle
+is pinned by (1) analytic known answers for the FCL triangle test and mesh verdicts,
+(2) scipy.spatial.cKDTree for nearest-neighbour ids, (3) glibc rand() and libstdc++'s
+std::default_random_engine / uniform_real_distribution for the RNG restatements.
+"""
+import ctypes
+import math
+import os
+import shutil
+import subprocess
+
+import numpy as np
+import pytest
+
+from motionplanningtoolkit_amd import scenes
+
+I = np.array([1, 0, 0, 0, 1, 0, 0, 0, 1], np.float64)
+
+
+def pose(t, R=I):
+    return np.r_[np.asarray(R, np.float64).ravel(), np.asarray(t, np.float64)]
+
+
+def rotz(a):
+    c, s = math.cos(a), math.sin(a)
+    return np.array([c, -s, 0, s, c, 0, 0, 0, 1], np.float64)
+
+
+# ---------------------------------------------------------------- RNG
+def test_glibc_rand_matches_libc(oracle):
+    libc = ctypes.CDLL("libc.so.6")
+    libc.srand(1)
+    r = oracle.GlibcRand(1)
+    for _ in range(5000):
+        assert r.next() == libc.rand()
+
+
+@pytest.mark.skipif(shutil.which("g++") is None, reason="needs g++")
+def test_uniform_real_matches_libstdcxx(oracle, tmp_path):
+    src = tmp_path / "u.cpp"
+    src.write_text(
+        "#include <random>\n#include <cstdio>\n#include <cmath>\n"
+        "int main(){std::default_random_engine g;"
+        "std::uniform_real_distribution<double> a(-100,100), b(0, 2*M_PI), c(-0.1745,0.1745);"
+        "for(int i=0;i<3000;i++){double x=a(g); double y=b(g); double z=c(g); printf(\"%a %a %a\\n\",x,y,z);}}\n")
+    exe = tmp_path / "u"
+    subprocess.run(["g++", "-O2", "-o", str(exe), str(src)], check=True)
+    lines = subprocess.run([str(exe)], check=True, capture_output=True, text=True).stdout.split("\n")
+    g = oracle.Minstd(1)
+    for line in lines[:3000]:
+        x, y, z = (float.fromhex(t) for t in line.split())
+        assert g.uniform(-100, 100) == x
+        assert g.uniform(0, 2 * math.pi) == y
+        assert g.uniform(-0.1745, 0.1745) == z
+
+
+def test_engine_uniform_range(oracle):
+    v = [oracle.engine_uniform(7, c, -2.0, 3.0) for c in range(20000)]
+    assert min(v) >= -2.0 and max(v) < 3.0
+    assert abs(np.mean(v) - 0.5) < 0.05
+
+
+# ---------------------------------------------------------------- FCL triangle test
+P0 = np.array([0, 0, 0, 1, 0, 0, 0, 1, 0], np.float64)
+
+
+@pytest.mark.parametrize("Q,expect", [
+    ([0.2, 0.2, -1, 0.2, 0.2, 1, 0.3, 0.25, 1], 1),         # pierces P
+    ([5, 5, 5, 6, 5, 5, 5, 6, 5], 0),                      # far away
+    ([0.25, 0.25, 0, 0.25, 0.25, 1, 0.5, 0.25, 1], 1),     # vertex touching P: touching counts
+    ([0.25, 0.25, 1e-9, 0.25, 0.25, 1, 0.5, 0.25, 1], 0),  # 1e-9 above
+    ([0.1, 0.1, 0, 0.6, 0.1, 0, 0.1, 0.6, 0], 1),          # coplanar overlap
+    ([2, 0, 0, 3, 0, 0, 2, 1, 0], 0),                      # coplanar disjoint
+    ([0.9, 0.9, -1, 0.9, 0.9, 1, 1.0, 0.95, 0], 0),        # pierces the plane outside P
+])
+def test_tri_intersect_known_answers(oracle, Q, expect):
+    assert oracle.tri_intersect(P0, Q) == bool(expect)
+    assert oracle.tri_intersect(Q, P0) == bool(expect)
+
+
+def test_quat_to_rot(oracle):
+    assert np.array_equal(oracle.quat_to_rot([1, 0, 0, 0]), I)
+    a = 0.7
+    q = [math.cos(a / 2), 0, 0, math.sin(a / 2)]
+    np.testing.assert_allclose(oracle.quat_to_rot(q), rotz(a), atol=1e-15)
+
+
+# ---------------------------------------------------------------- mesh verdicts
+@pytest.fixture(scope="module")
+def unit_box():
+    return scenes.read_obj(scenes.mesh_path("agent_unit_box"), "last")
+
+
+def _box_case(oracle, box, t, R=I):
+    off = np.array([0, 1])
+    return int(oracle.collide_batch(box, pose([0, 0, 0]), [box], pose(t, R).reshape(1, 1, 12), off)[0])
+
+
+@pytest.mark.parametrize("t", [(0, 0, 0), (0.5, 0.3, -0.2), (0.99, 0, 0), (0, -0.99, 0.99), (0.6, 0.6, 0.6)])
+def test_box_box_overlap(oracle, unit_box, t):
+    assert _box_case(oracle, unit_box, t) == 1
+
+
+@pytest.mark.parametrize("t", [(1.01, 0, 0), (0, 0, -1.5), (3, 3, 3), (1.01, 1.01, 1.01)])
+def test_box_box_separated(oracle, unit_box, t):
+    assert _box_case(oracle, unit_box, t) == 0
+
+
+def test_box_box_face_touching_counts(oracle, unit_box):
+    assert _box_case(oracle, unit_box, (1.0, 0, 0)) == 1
+    assert _box_case(oracle, unit_box, (0, 0, -1.0)) == 1
+
+
+def test_box_box_rotated(oracle, unit_box):
+    R = rotz(math.pi / 4)  # x half-extent of the rotated box: sqrt(2)/2
+    assert _box_case(oracle, unit_box, (1.19, 0, 0), R) == 1
+    assert _box_case(oracle, unit_box, (1.22, 0, 0), R) == 0
+
+
+def test_env_transform_is_applied(oracle, unit_box):
+    tf = oracle.env_tf_from_location([5, 0, 0, 1, 0, 0, 0])
+    off = np.array([0, 1])
+    hit = oracle.collide_batch(unit_box, tf, [unit_box], pose([4.5, 0, 0]).reshape(1, 1, 12), off)
+    miss = oracle.collide_batch(unit_box, tf, [unit_box], pose([0, 0, 0]).reshape(1, 1, 12), off)
+    assert hit[0] == 1 and miss[0] == 0
+
+
+def _random_poses(rng, n, lo, hi, rot=True):
+    out = np.zeros((n, 12))
+    for i in range(n):
+        a = rng.uniform(0, 2 * math.pi) if rot else 0.0
+        out[i] = pose(rng.uniform(lo, hi), rotz(a))
+    return out
+
+
+def test_bvh_matches_all_pairs_blimp_room(oracle):
+    rng = np.random.default_rng(1)
+    env = scenes.read_obj(scenes.mesh_path("env_model"))
+    agent = scenes.read_obj(scenes.mesh_path("agent_blimp"), "last")
+    poses = _random_poses(rng, 300, [-10, -10, -10], [185, 145, 120])
+    off = np.arange(301)
+    tf = pose([0, 0, 0])
+    a = oracle.collide_batch(env, tf, [agent], poses.reshape(-1, 1, 12), off)
+    b = oracle.collide_batch_bvh(oracle.BVH(env), tf, [agent], poses.reshape(-1, 1, 12), off)
+    assert np.array_equal(a, b)
+    assert 0 < a.sum() < len(a)
+
+
+def test_edges_with_no_poses_are_safe(oracle, unit_box):
+    off = np.array([0, 0, 1, 1])
+    v = oracle.collide_batch(unit_box, pose([0, 0, 0]), [unit_box], pose([0, 0, 0]).reshape(1, 1, 12), off)
+    assert v.tolist() == [0, 1, 0]
+
+
+# ---------------------------------------------------------------- FLANN L2 / NN
+def test_l2_accumulation_order(oracle):
+    rng = np.random.default_rng(0)
+    for d in (1, 3, 4, 5, 7, 8, 15, 16):
+        a = rng.normal(size=d) * 100
+        b = rng.normal(size=d) * 100
+        r = 0.0
+        i = 0
+        while i + 3 < d:
+            d0, d1, d2, d3 = (float(a[i + k] - b[i + k]) for k in range(4))
+            r += d0 * d0 + d1 * d1 + d2 * d2 + d3 * d3
+            i += 4
+        while i < d:
+            d0 = float(a[i] - b[i])
+            r += d0 * d0
+            i += 1
+        assert oracle.l2(a, b) == r
+
+
+@pytest.mark.parametrize("d", [3, 7, 15])
+def test_knn_matches_ckdtree(oracle, d):
+    from scipy.spatial import cKDTree
+
+    rng = np.random.default_rng(d)
+    pts = rng.uniform(-100, 100, size=(3000, d))
+    q = rng.uniform(-100, 100, size=(200, d))
+    ids, d2 = oracle.knn(pts, q, 5)
+    dist, idx = cKDTree(pts).query(q, 5)
+    assert np.array_equal(ids, idx + 1)
+    np.testing.assert_allclose(d2, dist ** 2, rtol=1e-12)
+
+
+def test_kdtree_matches_bruteforce_bitwise(oracle):
+    rng = np.random.default_rng(5)
+    pts = rng.uniform(-10, 10, size=(5000, 7))
+    pts[100] = pts[50]  # exact duplicate: tie resolves to the lower id
+    q = np.r_[rng.uniform(-10, 10, size=(400, 7)), pts[50:51]]
+    ids, d2 = oracle.knn(pts, q, 3)
+    ids2, d22 = oracle.KDTree(pts).knn(q, 3)
+    assert np.array_equal(ids, ids2)
+    assert np.array_equal(d2.view(np.uint64), d22.view(np.uint64))
+    assert ids[-1, 0] == 51 and ids[-1, 1] == 101
+
+
+def test_radius_matches_ckdtree(oracle):
+    from scipy.spatial import cKDTree
+
+    rng = np.random.default_rng(3)
+    pts = rng.uniform(0, 10, size=(2000, 3))
+    q = rng.uniform(0, 10, size=(100, 3))
+    r2 = 0.8
+    off, ids, d2 = oracle.radius(pts, q, r2)
+    ref = cKDTree(pts).query_ball_point(q, math.sqrt(r2))
+    for i in range(len(q)):
+        got = ids[off[i]:off[i + 1]]
+        assert sorted(got.tolist()) == sorted((np.array(ref[i]) + 1).tolist())
+        assert np.all(np.diff(d2[off[i]:off[i + 1]]) >= 0)
+    off5, ids5, _ = oracle.radius(pts, q, r2, max_nb=5)
+    for i in range(len(q)):
+        full = ids[off[i]:off[i + 1]]
+        assert ids5[off5[i]:off5[i + 1]].tolist() == full[:5].tolist()
+
+
+def test_knn_removed_points(oracle):
+    pts = np.array([[0.0], [1.0], [2.0], [3.0]])
+    ids, _ = oracle.knn(pts, [[1.1]], 2, removed=np.array([0, 1, 0, 0], np.uint8))
+    assert ids.tolist() == [[3, 1]]
+
+
+# ---------------------------------------------------------------- agents
+def test_omni_poses_unit_step(oracle):
+    # |end - start| = 1, dt = 0.1: floor(1 / 0.1) = 10 poses, 10 * 0.1 == 1 so no end pose
+    P = oracle.omni_get_poses([0, 0, 0], [1, 0, 0], 0.1)
+    assert len(P) == 10
+    assert np.allclose(P[:, 9], np.arange(10) * 0.1)
+    # short edge: start and end
+    P = oracle.omni_get_poses([0, 0, 0], [0.05, 0, 0], 0.1)
+    assert len(P) == 2 and P[1, 9] == 0.05
+    # 0.95 / 0.1 -> 9 poses + end
+    P = oracle.omni_get_poses([0, 0, 0], [0.95, 0, 0], 0.1)
+    assert len(P) == 10 and P[-1, 9] == 0.95
+
+
+def test_blimp_step_clamps_and_pose(oracle):
+    prm = scenes.BLIMP_PRM
+    s = np.array([1.0, 2.0, 3.0, 0.5, 4.95, 0.78, 4.99])
+    n = oracle.blimp_do_step(prm, s, 1.0, 0.1745, 1.0, 0.1)
+    assert n[4] == 5.0 and n[5] == 0.785398 and n[6] == 5.0  # clamped
+    assert n[0] == s[0] + math.cos(s[3]) * s[4] * 0.1
+    P = oracle.blimp_get_poses(prm, s, [1.0, 0.1745, 1.0], 0.1, 0.1)
+    assert len(P) == 1 and np.array_equal(P[0, 9:], n[:3])
+    assert P[0, 0] == math.cos(n[3]) and P[0, 1] == math.sin(n[3]) and P[0, 3] == -math.sin(n[3])
+
+
+def test_snake_poses_verbatim(oracle):
+    prm = scenes.SNAKE_PRM
+    s = np.zeros(15)
+    s[0], s[1], s[4], s[5] = 3.0, -2.0, 0.3, 0.5
+    P = oracle.snake_get_poses(prm, s, [0.5, 0.1], 0.25, 1.0)
+    assert P.shape == (1, 11, 12)
+    assert np.array_equal(P[0, 0, 9:], [3.0, -2.0, 0.0])
+    for l in range(1, 11):  # trailers at (-(Lt + Lh), Y, 0), not chained
+        assert np.array_equal(P[0, l, 9:], [-1.25, -2.0, 0.0])
+    assert P[0, 1, 0] == math.cos(0.5 - 0.3)
+
+
+# ---------------------------------------------------------------- sequential RRT
+def test_oracle_rrt_omni_solves_and_is_consistent(oracle):
+    sc = scenes.omni_scenario()
+    nodes, parents, solved, iters = oracle.rrt_run(0, None, sc.ranges, sc.start, sc.goal, sc.goal_thr, 0.1, 0.1,
+                                                   sc.env_tris, sc.env_tf, sc.agent_tris, -1, 200000)
+    assert solved >= 0
+    assert np.array_equal(nodes[0], sc.start)
+    for i in range(1, len(nodes)):
+        step = nodes[i] - nodes[parents[i] - 1]
+        assert abs(np.linalg.norm(step) - 1.0) < 1e-12
+    # every inserted edge's checked poses are collision free.  (Not its end state in
+    # general: Omnidirectional::getPoses adds the end pose only if iterations*dt < dist,
+    # so a unit step with dt = 0.1 may stop at 0.9 -- reference behaviour, kept.)
+    edges = [oracle.omni_get_poses(nodes[parents[i] - 1], nodes[i], 0.1) for i in range(1, len(nodes))]
+    off = np.r_[0, np.cumsum([len(e) for e in edges])]
+    v = oracle.collide_batch(sc.env_tris, sc.env_tf, [sc.agent_tris], np.concatenate(edges).reshape(-1, 1, 12), off)
+    assert v.sum() == 0

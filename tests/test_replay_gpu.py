@@ -1,0 +1,57 @@
+"""GPU parity, end to end: the C++ host planner (instances/*.inst -> Agent / UniformSampler /
+TreeInterface / RRT over GpuNN + GPU collision) replays the reference's sequential RRT
+(planners/rrt.hpp:21-94, K = 1, the reference's own RNG streams) node for node against the
+oracle's restatement.  Bar: identical trees, bit for bit."""
+import os
+
+import numpy as np
+import pytest
+
+from motionplanningtoolkit_amd import scenes
+
+pytestmark = pytest.mark.gpu
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def inst(name):
+    return os.path.join(REPO, "instances", name)
+
+
+def bits(a):
+    return np.ascontiguousarray(a, np.float64).view(np.uint64)
+
+
+def compare(mpt, oracle, inst_name, sc, iat, start=None):
+    starts, ends, solved = mpt.rrt_inst(inst(inst_name), iat)
+    st = sc.start if start is None else start
+    nodes, parents, osolved, _ = oracle.rrt_run(sc.kind, sc.prm, sc.ranges, st, sc.goal, sc.goal_thr, sc.steer_dt,
+                                                sc.cc_dt, sc.env_tris, sc.env_tf, sc.agent_tris, iat, 1 << 20)
+    assert ends.shape == nodes.shape, (ends.shape, nodes.shape)
+    assert np.array_equal(bits(ends), bits(nodes))
+    assert np.array_equal(bits(starts[1:]), bits(nodes[parents[1:] - 1]))
+    assert solved == (osolved >= 0)
+    return nodes
+
+
+def test_replay_omnidirectional(mpt_gpu, oracle):
+    nodes = compare(mpt_gpu, oracle, "omnidirectional.inst", scenes.omni_scenario(), -1)
+    assert len(nodes) > 10
+
+
+def test_replay_blimp(mpt_gpu, oracle):
+    sc = scenes.blimp_scenario("last")
+    start = np.array([-20, -20, -20, 1, 0, 0, 0], np.float64)
+    nodes = compare(mpt_gpu, oracle, "blimp.inst", sc, 1500, start)
+    assert len(nodes) > 100
+
+
+def test_replay_snake_reference_env(mpt_gpu, oracle):
+    sc = scenes.snake_scenario("reference")
+    compare(mpt_gpu, oracle, "snake.inst", sc, 600)
+
+
+def test_replay_snake_corridor(mpt_gpu, oracle):
+    sc = scenes.snake_scenario("corridor")
+    sc.env_tris = scenes.read_obj(scenes.mesh_path("env_corridor"))
+    compare(mpt_gpu, oracle, "snake_corridor.inst", sc, 600)
