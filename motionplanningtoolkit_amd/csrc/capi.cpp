@@ -345,10 +345,21 @@ const AgentDev &agent_dev(const mpt_agent *a) { return a->dev; }
 static void collide_common(const mpt_env *env, const mpt_agent *const *links, int32_t L, const double *d_poses,
                            const int32_t *d_pose_edge, int64_t total_poses, int64_t E, uint8_t *d_verdict,
                            hipStream_t stream) {
+    // The link table lives in a per-thread device buffer that is rewritten only when the
+    // set of links changes; the rewrite waits for in-flight work that may still read it
+    // and copies synchronously, so no pageable staging memory outlives this call.
+    static thread_local std::vector<AgentDev> cached;
     std::vector<AgentDev> lk((size_t)L);
     for (int32_t l = 0; l < L; ++l) lk[l] = links[l]->dev;
-    auto *d_links = (AgentDev *)g_ws.links.get(sizeof(AgentDev) * L);
-    hip_check(hipMemcpyAsync(d_links, lk.data(), sizeof(AgentDev) * L, hipMemcpyHostToDevice, stream), "links H2D");
+    const bool same = cached.size() == lk.size() &&
+                      std::memcmp(cached.data(), lk.data(), sizeof(AgentDev) * lk.size()) == 0 && g_ws.links.p;
+    auto *d_links = (AgentDev *)g_ws.links.p;
+    if (!same) {
+        hip_check(hipDeviceSynchronize(), "sync before link table update");
+        d_links = (AgentDev *)g_ws.links.get(sizeof(AgentDev) * L);
+        hip_check(hipMemcpy(d_links, lk.data(), sizeof(AgentDev) * L, hipMemcpyHostToDevice), "links H2D");
+        cached = lk;
+    }
     hip_check(hipMemsetAsync(d_verdict, 0, (size_t)E, stream), "verdict memset");
     CollideWork w{};
     w.poses = d_poses;

@@ -268,6 +268,7 @@ int64_t launch_radius(const NNWork &w, double r2, int32_t max_nb, int64_t *d_off
     if (nq <= 0) {
         hip_check(hipMemcpyAsync(d_offsets, h_off.data(), sizeof(int64_t), hipMemcpyHostToDevice, stream),
                   "radius offsets");
+        hip_check(hipStreamSynchronize(stream), "radius sync");
         return 0;
     }
     const int64_t S = pick_splits(nq, w.n > 0 ? w.n : 1);
@@ -317,6 +318,8 @@ int64_t launch_radius(const NNWork &w, double r2, int32_t max_nb, int64_t *d_off
     hip_check(hipFreeAsync(d_foff, stream), "free");
     hip_check(hipFreeAsync(fid, stream), "free");
     hip_check(hipFreeAsync(fd2, stream), "free");
+    // the H2D copies above read pageable host vectors owned by this frame: wait for them
+    hip_check(hipStreamSynchronize(stream), "radius sync");
     (void)scratch;
     (void)scratch_bytes;
     return h_off[nq];

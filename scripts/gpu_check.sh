@@ -1,0 +1,19 @@
+#!/bin/bash
+# One GPU session: parity tests, smoke, short bench.  Stops at the first step that ends
+# in a fault/abort/timeout (exit status > 1); test failures (status 1) do not stop it.
+mkdir -p gpurun_out
+run() {  # name timeout cmd...
+  local name=$1 t=$2; shift 2
+  echo "== $name: $*" | tee -a gpurun_out/steps.log
+  timeout -k 10 "$t" "$@" > "gpurun_out/$name.log" 2>&1
+  local rc=$?
+  echo "== $name rc=$rc" | tee -a gpurun_out/steps.log
+  tail -5 "gpurun_out/$name.log"
+  return $rc
+}
+run pytest_gpu 800 python -m pytest tests -m gpu -q -p no:cacheprovider -ra; rc=$?
+[ $rc -gt 1 ] && exit $rc
+run smoke 180 python -c "import __graft_entry__ as g; g.smoke()"; rc=$?
+[ $rc -gt 1 ] && exit $rc
+run bench 400 python bench.py --steps 5 --warmup 2 --cpu-seconds 5; rc=$?
+exit $rc
