@@ -41,7 +41,7 @@ def parse():
     ap.add_argument("--seed", type=int, default=1000)
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample length")
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--traffic", default=os.path.join(REPO, "profiles", "traffic.json"))
+    ap.add_argument("--traffic", default=None, help="pmc_summary.json (default: latest profiles/r*/)")
     return ap.parse_args()
 
 
@@ -77,6 +77,24 @@ def cpu_baseline(sc, tree, K_gpu, seed, target_s):
         "all_cores": {"value": validn / tn, "cores": threads, "seconds": round(tn, 3)},
         "cpu": _cpu_model(),
     }
+
+
+def pmc_traffic(path, kernel):
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary
+    (scripts/profile.sh + scripts/pmc_summary.py), or None."""
+    if not path:
+        import glob
+
+        cands = sorted(glob.glob(os.path.join(REPO, "profiles", "r*", "pmc_summary.json")))
+        path = cands[-1] if cands else None
+    try:
+        summ = json.load(open(path))
+    except (OSError, ValueError, TypeError):
+        return None
+    for name, v in summ.items():
+        if kernel in name:
+            return v["hbm_bytes_per_launch"]
+    return None
 
 
 def _cpu_model():
@@ -172,11 +190,7 @@ def main():
     else:
         roof = {"bound": "hbm", "achieved": None, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": None,
                 "traffic": None, "kernel": dominant}
-    try:
-        tr = json.load(open(args.traffic))
-        roof["traffic"] = tr.get(roof["kernel"].split()[0], tr.get("traffic"))
-    except (OSError, ValueError):
-        pass
+    roof["traffic"] = pmc_traffic(args.traffic, roof["kernel"].split()[0])
 
     out = {
         "metric": "valid RRT edge extensions/sec (collision+NN) per node, 1/2/4/8 MI355X",

@@ -260,29 +260,44 @@ __global__ void k_radius_sort(const int64_t *__restrict__ foff, const int64_t *_
         if (ob + i < cap) { ids[ob + i] = fid[b + i]; d2[ob + i] = fd2[b + i]; }
 }
 
+// Device allocations freed at scope exit (radius search only: it is synchronous).
+struct TmpAllocs {
+    std::vector<void *> p;
+    ~TmpAllocs() {
+        for (void *x : p) (void)hipFree(x);
+    }
+    template <class T>
+    T *alloc(size_t n) {
+        void *x = nullptr;
+        hip_check(hipMalloc(&x, sizeof(T) * (n > 0 ? n : 1)), "radius alloc");
+        p.push_back(x);
+        return (T *)x;
+    }
+};
+
 int64_t launch_radius(const NNWork &w, double r2, int32_t max_nb, int64_t *d_offsets, int32_t *d_ids,
                       double *d_d2, int64_t cap, void *scratch, size_t scratch_bytes, hipStream_t stream) {
+    // Synchronous by contract (list sizes are data dependent): plain allocations and
+    // blocking copies, so no pageable host staging outlives a copy.
     if (w.d > 16) throw Error{1, "radius search supports d <= 16"};
     const int64_t nq = w.nq;
     std::vector<int64_t> h_off(nq + 1, 0);
+    hip_check(hipStreamSynchronize(stream), "radius sync");
     if (nq <= 0) {
-        hip_check(hipMemcpyAsync(d_offsets, h_off.data(), sizeof(int64_t), hipMemcpyHostToDevice, stream),
-                  "radius offsets");
-        hip_check(hipStreamSynchronize(stream), "radius sync");
+        hip_check(hipMemcpy(d_offsets, h_off.data(), sizeof(int64_t), hipMemcpyHostToDevice), "radius offsets");
         return 0;
     }
     const int64_t S = pick_splits(nq, w.n > 0 ? w.n : 1);
     const int64_t chunk = (w.n + S - 1) / S;
     const dim3 grid((unsigned)((nq + kNNBlock - 1) / kNNBlock), (unsigned)S);
-    int32_t *counts = nullptr;
-    hip_check(hipMallocAsync((void **)&counts, sizeof(int32_t) * S * nq, stream), "radius counts");
+    TmpAllocs tmp;
+    int32_t *counts = tmp.alloc<int32_t>(S * nq);
     hipLaunchKernelGGL(k_radius_count, grid, dim3(kNNBlock), 0, stream, w.pts, w.removed, w.n, w.d, w.q, nq,
                        chunk, r2, counts);
     hip_check(hipGetLastError(), "k_radius_count");
-    std::vector<int32_t> h_counts(S * nq);
-    hip_check(hipMemcpyAsync(h_counts.data(), counts, sizeof(int32_t) * S * nq, hipMemcpyDeviceToHost, stream),
-              "radius counts D2H");
     hip_check(hipStreamSynchronize(stream), "radius sync");
+    std::vector<int32_t> h_counts(S * nq);
+    hip_check(hipMemcpy(h_counts.data(), counts, sizeof(int32_t) * S * nq, hipMemcpyDeviceToHost), "counts D2H");
     std::vector<int64_t> soff(S * nq), foff(nq + 1);
     int64_t tot = 0;
     for (int64_t qi = 0; qi < nq; ++qi) {
@@ -296,29 +311,19 @@ int64_t launch_radius(const NNWork &w, double r2, int32_t max_nb, int64_t *d_off
         h_off[qi + 1] = h_off[qi] + kept;
     }
     foff[nq] = tot;
-    int64_t *d_soff = nullptr, *d_foff = nullptr;
-    int32_t *fid = nullptr;
-    double *fd2 = nullptr;
-    hip_check(hipMallocAsync((void **)&d_soff, sizeof(int64_t) * S * nq, stream), "radius soff");
-    hip_check(hipMallocAsync((void **)&d_foff, sizeof(int64_t) * (nq + 1), stream), "radius foff");
-    hip_check(hipMallocAsync((void **)&fid, sizeof(int32_t) * (tot + 1), stream), "radius fid");
-    hip_check(hipMallocAsync((void **)&fd2, sizeof(double) * (tot + 1), stream), "radius fd2");
-    hip_check(hipMemcpyAsync(d_soff, soff.data(), sizeof(int64_t) * S * nq, hipMemcpyHostToDevice, stream), "soff");
-    hip_check(hipMemcpyAsync(d_foff, foff.data(), sizeof(int64_t) * (nq + 1), hipMemcpyHostToDevice, stream), "foff");
-    hip_check(hipMemcpyAsync(d_offsets, h_off.data(), sizeof(int64_t) * (nq + 1), hipMemcpyHostToDevice, stream),
-              "offsets");
+    int64_t *d_soff = tmp.alloc<int64_t>(S * nq);
+    int64_t *d_foff = tmp.alloc<int64_t>(nq + 1);
+    int32_t *fid = tmp.alloc<int32_t>(tot + 1);
+    double *fd2 = tmp.alloc<double>(tot + 1);
+    hip_check(hipMemcpy(d_soff, soff.data(), sizeof(int64_t) * S * nq, hipMemcpyHostToDevice), "soff");
+    hip_check(hipMemcpy(d_foff, foff.data(), sizeof(int64_t) * (nq + 1), hipMemcpyHostToDevice), "foff");
+    hip_check(hipMemcpy(d_offsets, h_off.data(), sizeof(int64_t) * (nq + 1), hipMemcpyHostToDevice), "offsets");
     hipLaunchKernelGGL(k_radius_fill, grid, dim3(kNNBlock), 0, stream, w.pts, w.removed, w.n, w.d, w.q, nq, chunk,
                        r2, d_soff, fid, fd2);
     hip_check(hipGetLastError(), "k_radius_fill");
     hipLaunchKernelGGL(k_radius_sort, dim3((unsigned)((nq + 255) / 256)), dim3(256), 0, stream, d_foff, d_offsets,
                        nq, fid, fd2, d_ids, d_d2, cap);
     hip_check(hipGetLastError(), "k_radius_sort");
-    hip_check(hipFreeAsync(counts, stream), "free");
-    hip_check(hipFreeAsync(d_soff, stream), "free");
-    hip_check(hipFreeAsync(d_foff, stream), "free");
-    hip_check(hipFreeAsync(fid, stream), "free");
-    hip_check(hipFreeAsync(fd2, stream), "free");
-    // the H2D copies above read pageable host vectors owned by this frame: wait for them
     hip_check(hipStreamSynchronize(stream), "radius sync");
     (void)scratch;
     (void)scratch_bytes;

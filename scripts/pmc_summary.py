@@ -1,0 +1,40 @@
+"""Summarise rocprofv3 PMC passes (scripts/profile.sh) into profiles/<tag>/pmc_summary.json.
+
+HBM bytes per launch = (2 * FETCH_SIZE + WRITE_SIZE) * 1024, the correction
+/opt/skills/guides/MI355X_MICROARCH.md (§HBM) prescribes for gfx950: FETCH_SIZE reports
+half the bytes of a wide coalesced read.  The doubling is calibrated for 16-B-per-lane
+vector loads only; kernels whose reads are scalar (s_load) loads are marked as such in
+DESIGN.md.  Usage: python scripts/pmc_summary.py gpurun_out/prof_r01 profiles/r01
+"""
+import collections
+import csv
+import json
+import os
+import shutil
+import sys
+
+
+def main(src, dst):
+    os.makedirs(dst, exist_ok=True)
+    out = {}
+    for tag, cn in (("fetch", "FETCH_SIZE"), ("write", "WRITE_SIZE")):
+        path = os.path.join(src, tag, "run_counter_collection.csv")
+        agg = collections.defaultdict(list)
+        for r in csv.DictReader(open(path)):
+            agg[r["Kernel_Name"]].append(float(r["Counter_Value"]))
+        for k, v in agg.items():
+            out.setdefault(k, {})[cn] = sum(v) / len(v)
+    summ = {}
+    for k, v in out.items():
+        f, w = v.get("FETCH_SIZE", 0.0), v.get("WRITE_SIZE", 0.0)
+        summ[k] = {"FETCH_SIZE_KB": round(f, 3), "WRITE_SIZE_KB": round(w, 3),
+                   "hbm_bytes_per_launch": round((2 * f + w) * 1024)}
+    json.dump(summ, open(os.path.join(dst, "pmc_summary.json"), "w"), indent=1)
+    ks = os.path.join(src, "kt", "run_kernel_stats.csv")
+    if os.path.exists(ks):
+        shutil.copy(ks, os.path.join(dst, "kernel_stats.csv"))
+    print(json.dumps({k[:60]: v["hbm_bytes_per_launch"] for k, v in summ.items()}, indent=1))
+
+
+if __name__ == "__main__":
+    main(sys.argv[1], sys.argv[2])
