@@ -41,6 +41,8 @@ def parse():
     ap.add_argument("--seed", type=int, default=1000)
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample length")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--nn", default="grid", choices=["grid", "brute", "auto"], help="engine NN structure")
+    ap.add_argument("--ppc", type=float, default=2.0, help="grid points per cell")
     ap.add_argument("--traffic", default=None, help="pmc_summary.json (default: latest profiles/r*/)")
     return ap.parse_args()
 
@@ -77,6 +79,35 @@ def cpu_baseline(sc, tree, K_gpu, seed, target_s):
         "all_cores": {"value": validn / tn, "cores": threads, "seconds": round(tn, 3)},
         "cpu": _cpu_model(),
     }
+
+
+def roofline(per_launch, cst, K, n0, d, nn_mode):
+    """Roofline of the round's dominant kernel: achieved = algorithmic work of
+    one launch (SURVEY 8(d) per-unit figures x the units the launch processed) / its
+    hipEvent-measured duration."""
+    dominant = max(("nn_build", "nn_query", "collide", "steer", "append", "sample"),
+                   key=lambda k: per_launch.get(k, 0.0))
+    ms = per_launch[dominant]
+    if dominant == "collide":
+        # bytes per (pose, link) unit = 96 (pose) + 32 per BVH node visit + 144 per triangle-pair test
+        nbytes = 96.0 * cst["units"] + 32.0 * cst["node_visits"] + 144.0 * cst["tri_tests"]
+        flops = 54.0 * 64 * cst["clusters"] + 750.0 * cst["tri_tests"]  # upper bounds (full clusters, all 17 axes)
+        gbs = nbytes / (ms * 1e-3) / 1e9
+        return {"bound": "hbm", "achieved": round(gbs, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(gbs / HBM_PEAK_GBS, 5), "traffic": None, "kernel": "k_collide",
+                "ms_per_launch": round(ms, 4), "work_per_launch": cst,
+                "fp64_tflops_upper": round(flops / (ms * 1e-3) / 1e12, 3),
+                "note": "latency/divergence bound BVH traversal + FP64 SAT; bytes per SURVEY 8(d)"}
+    if dominant == "nn_query" and nn_mode == "brute":
+        flops = float(K) * n0 * 3 * d  # SURVEY 8(d): 3*d*N FP64 ops per query (sub, mul, add)
+        tf = flops / (ms * 1e-3) / 1e12
+        return {"bound": "mfma", "achieved": round(tf, 3), "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
+                "frac": round(tf / FP64_PEAK_TFLOPS, 4), "traffic": None, "kernel": "k_knn1",
+                "ms_per_launch": round(ms, 4),
+                "note": "FP64 VALU (no MFMA: FLANN's L2 op order is not a dot product); no-FMA ceiling 39.3 TFLOP/s"}
+    return {"bound": "hbm", "achieved": None, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": None, "traffic": None,
+            "kernel": {"nn_query": "k_grid_knn", "nn_build": "k_grid"}.get(dominant, dominant),
+            "ms_per_launch": round(ms, 4)}
 
 
 def pmc_traffic(path, kernel):
@@ -136,6 +167,7 @@ def main():
     agent = mpt.AgentMesh(sc.agent_tris)
     eng = mpt.RRTEngine(env, agent, sc.kind, sc.prm, sc.ranges, sc.steer_dt, sc.cc_dt, n0 + K, seed)
     eng.add_nodes(tree)
+    eng.set_nn(args.nn, args.ppc)
     eng.enable_timing(True)
 
     def round_():
@@ -179,18 +211,12 @@ def main():
 
     steps = args.steps
     per_launch = {k: v / steps for k, v in ktimes.items()}
-    dominant = max(("nn", "collide", "steer", "append", "sample"), key=lambda k: per_launch.get(k, 0.0))
-    d = sc.dim
-    if dominant == "nn":
-        flops = float(K) * n0 * 3 * d  # 3*d*N FP64 ops per query (sub, mul, add)
-        achieved = flops / (per_launch["nn"] * 1e-3) / 1e12
-        roof = {"bound": "mfma", "achieved": round(achieved, 3), "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
-                "frac": round(achieved / FP64_PEAK_TFLOPS, 4), "traffic": None, "kernel": "k_knn1<7> (+merge)",
-                "note": "FP64 VALU (no MFMA: FLANN's L2 op order is not a dot product); no-FMA ceiling 39.3 TFLOP/s"}
-    else:
-        roof = {"bound": "hbm", "achieved": None, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": None,
-                "traffic": None, "kernel": dominant}
-    roof["traffic"] = pmc_traffic(args.traffic, roof["kernel"].split()[0])
+    # one more round, outside the timed region, with the collision work counters on
+    eng.collide_stats(True)
+    round_()
+    cst = eng.collide_stats(False)
+    roof = roofline(per_launch, cst, K, n0, sc.dim, args.nn)
+    roof["traffic"] = pmc_traffic(args.traffic, roof["kernel"])
 
     out = {
         "metric": "valid RRT edge extensions/sec (collision+NN) per node, 1/2/4/8 MI355X",
@@ -207,11 +233,11 @@ def main():
         "data": "synthetic (uniform samples and tree states over Blimp::getStateVarRanges; meshes from the reference)",
         "config": {"workload": "blimp.inst: blimp (1355 tris) vs single-room env (model.dae, 316 tris), "
                                "batched RRT round over a 100k-node tree",
-                   "tree_nodes": n0, "extensions_per_round": K, "seed_base": args.seed,
+                   "tree_nodes": n0, "extensions_per_round": K, "seed_base": args.seed, "nn_index": args.nn,
                    "parallelism": f"independent seeds x{world}"},
         "checked_per_s": checked / elapsed,
         "valid_fraction": valid / max(checked, 1),
-        "kernel_ms_per_round": {k: round(v, 4) for k, v in per_launch.items() if k != "reserved"},
+        "kernel_ms_per_round": {k: round(v, 4) for k, v in per_launch.items()},
         "roofline": roof,
     }
     if not args.no_cpu and world == 1:

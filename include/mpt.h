@@ -105,6 +105,11 @@ mpt_status mpt_nn_remove(mpt_nn *nn, int32_t id);
 mpt_status mpt_nn_size(const mpt_nn *nn, int64_t *n_out);
 /* Device pointer of the [capacity][dim] point array (for zero-copy engines / tests). */
 mpt_status mpt_nn_points_device(const mpt_nn *nn, const double **d_pts);
+/* Search structure: AUTO (grid when n >= 4096 and nq >= 32), BRUTE (tiled scan), GRID
+ * (device-built uniform grid over the widest <= 3 dims, rebuilt after appends).  All modes
+ * are exact and return identical results; GRID/AUTO rebuilds synchronise once. */
+enum { MPT_NN_AUTO = 0, MPT_NN_BRUTE = 1, MPT_NN_GRID = 2 };
+mpt_status mpt_nn_set_index(mpt_nn *nn, int32_t mode);
 /* kNearest / nearest (k = 1): ids [nq][k] (-1 when fewer than k points), d2 [nq][k] (+inf). */
 mpt_status mpt_nn_knn(mpt_nn *nn, const double *q, int64_t nq, int32_t k, int32_t *ids, double *d2,
                       void *stream);
@@ -148,8 +153,16 @@ mpt_status mpt_rrt_last_poses(mpt_rrt *rrt, double *poses, int32_t *pose_counts)
 /* [dim, links L, pose slots per edge pmax, capacity] */
 mpt_status mpt_rrt_info(const mpt_rrt *rrt, int64_t info[4]);
 /* Per-kernel device times (ms) of the last round, recorded with hipEvents on the launch
- * stream when timing is enabled: [sample, nn, nn_merge, steer, collide, append]. */
+ * stream when timing is enabled: [sample, nn_build, nn_query, steer, collide, append]
+ * (nn_build = grid index build, 0 in brute-force mode; nn_query includes the merge). */
 mpt_status mpt_rrt_enable_timing(mpt_rrt *rrt, int32_t enable);
+/* NN structure of the rounds: MPT_NN_AUTO / _BRUTE / _GRID, grid occupancy target
+ * (points per cell, <= 0 keeps the current value, default 2).  Results are identical. */
+mpt_status mpt_rrt_set_nn(mpt_rrt *rrt, int32_t mode, double points_per_cell);
+/* Collision work counters accumulated since the previous call (synchronises), then reset;
+ * enable = 1 keeps counting in later rounds (atomics: off for timed runs).
+ * out [4] (may be NULL): (pose, link) units, clusters visited, BVH node visits, triangle tests. */
+mpt_status mpt_rrt_collide_stats(mpt_rrt *rrt, int32_t enable, uint64_t out[4]);
 mpt_status mpt_rrt_kernel_times(mpt_rrt *rrt, float ms[6]);
 
 #ifdef __cplusplus

@@ -48,6 +48,7 @@ SIGNATURES = {
     "mpt_nn_remove": (I32, [P, I32]),
     "mpt_nn_size": (I32, [P, P]),
     "mpt_nn_points_device": (I32, [P, P]),
+    "mpt_nn_set_index": (I32, [P, I32]),
     "mpt_nn_knn": (I32, [P, P, I64, I32, P, P, P]),
     "mpt_nn_knn_device": (I32, [P, P, I64, I32, P, P, P]),
     "mpt_nn_radius": (I32, [P, P, I64, D, I32, P, P, P, I64, P]),
@@ -62,6 +63,8 @@ SIGNATURES = {
     "mpt_rrt_last_poses": (I32, [P, P, P]),
     "mpt_rrt_info": (I32, [P, P]),
     "mpt_rrt_enable_timing": (I32, [P, I32]),
+    "mpt_rrt_set_nn": (I32, [P, I32, D]),
+    "mpt_rrt_collide_stats": (I32, [P, I32, P]),
     "mpt_rrt_kernel_times": (I32, [P, P]),
     "mpt_host_last_error": (C.c_char_p, []),
     "mpt_host_load_mesh": (I32, [C.c_char_p, I32, P, I64, P, P]),

@@ -154,6 +154,10 @@ class NearestNeighbors:
         check(lib().mpt_nn_append(self.handle, _p(pts), pts.shape[0], _p(ids)), "mpt_nn_append")
         return ids
 
+    def set_index(self, mode: str) -> None:
+        """'auto' | 'brute' | 'grid' (all exact, identical results)."""
+        check(lib().mpt_nn_set_index(self.handle, {"auto": 0, "brute": 1, "grid": 2}[mode]), "mpt_nn_set_index")
+
     def remove(self, point_id: int) -> None:
         check(lib().mpt_nn_remove(self.handle, int(point_id)), "mpt_nn_remove")
 
@@ -258,7 +262,18 @@ class RRTEngine:
     def kernel_times(self) -> dict:
         ms = np.zeros(6, np.float32)
         check(lib().mpt_rrt_kernel_times(self.handle, _p(ms)), "mpt_rrt_kernel_times")
-        return dict(zip(["sample", "nn", "reserved", "steer", "collide", "append"], ms.astype(float).tolist()))
+        return dict(zip(["sample", "nn_build", "nn_query", "steer", "collide", "append"], ms.astype(float).tolist()))
+
+    def collide_stats(self, enable: bool) -> dict:
+        """Counters since the last call (then reset); enable keeps counting in later rounds."""
+        out = np.zeros(4, np.uint64)
+        check(lib().mpt_rrt_collide_stats(self.handle, 1 if enable else 0, _p(out)), "mpt_rrt_collide_stats")
+        return {"units": int(out[0]), "clusters": int(out[1]), "node_visits": int(out[2]), "tri_tests": int(out[3])}
+
+    def set_nn(self, mode: str = "auto", points_per_cell: float = 0.0) -> None:
+        """NN structure of the rounds: 'auto' | 'brute' | 'grid' (identical results)."""
+        check(lib().mpt_rrt_set_nn(self.handle, {"auto": 0, "brute": 1, "grid": 2}[mode], points_per_cell),
+              "mpt_rrt_set_nn")
 
     def close(self):
         if getattr(self, "handle", None):

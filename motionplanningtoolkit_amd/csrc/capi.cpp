@@ -8,7 +8,10 @@
 #include <string>
 #include <vector>
 
+#include <memory>
+
 #include "../../include/mpt.h"
+#include "grid_nn.h"
 #include "mpt_internal.h"
 
 namespace mpt {
@@ -84,6 +87,11 @@ struct mpt_nn {
     int64_t cap = 0, n = 0;
     double *d_pts = nullptr;
     uint8_t *d_removed = nullptr;
+    // grid index over the current points, rebuilt lazily after appends (grid_nn.hip)
+    std::unique_ptr<GridIndex> grid;
+    int64_t grid_n = -1;
+    double *d_bbox = nullptr;
+    int32_t mode = MPT_NN_AUTO;
 };
 
 // ---------------------------------------------------------------- BVH build
@@ -488,6 +496,7 @@ extern "C" mpt_status mpt_nn_destroy(mpt_nn *nn) {
         if (!nn) return;
         if (nn->d_pts) (void)hipFree(nn->d_pts);
         if (nn->d_removed) (void)hipFree(nn->d_removed);
+        if (nn->d_bbox) (void)hipFree(nn->d_bbox);
         delete nn;
     });
 }
@@ -556,6 +565,47 @@ static NNWork nn_work(const mpt_nn *nn, const double *d_q, int64_t nq) {
     return w;
 }
 
+// Grid index when it pays (enough points and queries), brute force otherwise; both are exact
+// and return identical results.  A stale grid is rebuilt first (bbox D2H: synchronises).
+static void nn_query(mpt_nn *nn, const double *d_q, int64_t nq, int32_t k, int32_t *d_ids, double *d_d2,
+                     hipStream_t stream) {
+    const bool use_grid = nn->mode == MPT_NN_GRID || (nn->mode == MPT_NN_AUTO && nn->n >= 4096 && nq >= 32);
+    if (!use_grid || nn->n == 0) {
+        const NNWork w = nn_work(nn, d_q, nq);
+        void *scratch = g_ws.scratch.get(nn_knn_scratch_bytes(nq, std::max<int64_t>(nn->n, 1), k));
+        launch_knn(w, k, d_ids, d_d2, scratch, stream);
+        return;
+    }
+    if (!nn->grid) nn->grid.reset(new GridIndex());
+    if (nn->grid_n != nn->n) {
+        if (!nn->d_bbox) hip_check(hipMalloc(&nn->d_bbox, sizeof(double) * 2 * 16), "bbox alloc");
+        launch_bbox(nn->d_pts, nn->n, nn->d, nn->d_bbox, stream);
+        double lohi[32];
+        hip_check(hipMemcpyAsync(lohi, nn->d_bbox, sizeof(double) * 2 * nn->d, hipMemcpyDeviceToHost, stream), "bbox");
+        hip_check(hipStreamSynchronize(stream), "bbox sync");
+        int32_t dims[3];
+        const int32_t gd = choose_grid_dims(nn->d, lohi, dims);
+        double lo[3], hi[3];
+        for (int j = 0; j < gd; ++j) {
+            lo[j] = lohi[2 * dims[j]];
+            hi[j] = lohi[2 * dims[j] + 1];
+        }
+        const GridParams g = make_grid_params(nn->d, dims, gd, lo, hi, nn->n, 2.0);
+        nn->grid->build(nn->d_pts, nn->n, nullptr, nn->d, g, stream);
+        nn->grid_n = nn->n;
+    }
+    GridDev G = nn->grid->dev();
+    G.removed = nn->d_removed;
+    launch_grid_knn(G, nn->d, d_q, nq, k, d_ids, d_d2, stream);
+}
+
+extern "C" mpt_status mpt_nn_set_index(mpt_nn *nn, int32_t mode) {
+    return guarded([&] {
+        require(nn && mode >= MPT_NN_AUTO && mode <= MPT_NN_GRID, "bad arguments");
+        nn->mode = mode;
+    });
+}
+
 extern "C" mpt_status mpt_nn_knn_device(mpt_nn *nn, const double *d_q, int64_t nq, int32_t k, int32_t *d_ids,
                                         double *d_d2, void *stream) {
     return guarded([&] {
@@ -563,9 +613,7 @@ extern "C" mpt_status mpt_nn_knn_device(mpt_nn *nn, const double *d_q, int64_t n
         require(k >= 1 && k <= 32, "k must be in [1, 32]");
         if (nq == 0) return;
         require(d_q && d_ids && d_d2, "null pointer");
-        const NNWork w = nn_work(nn, d_q, nq);
-        void *scratch = g_ws.scratch.get(nn_knn_scratch_bytes(nq, std::max<int64_t>(nn->n, 1), k));
-        launch_knn(w, k, d_ids, d_d2, scratch, (hipStream_t)stream);
+        nn_query(nn, d_q, nq, k, d_ids, d_d2, (hipStream_t)stream);
     });
 }
 
@@ -581,9 +629,7 @@ extern "C" mpt_status mpt_nn_knn(mpt_nn *nn, const double *q, int64_t nq, int32_
         auto *d_ids = (int32_t *)g_ws.ids.get(sizeof(int32_t) * nq * k);
         auto *d_d2 = (double *)g_ws.d2.get(sizeof(double) * nq * k);
         hip_check(hipMemcpyAsync(d_q, q, sizeof(double) * nn->d * nq, hipMemcpyHostToDevice, stream), "q H2D");
-        const NNWork w = nn_work(nn, d_q, nq);
-        void *scratch = g_ws.scratch.get(nn_knn_scratch_bytes(nq, std::max<int64_t>(nn->n, 1), k));
-        launch_knn(w, k, d_ids, d_d2, scratch, stream);
+        nn_query(nn, d_q, nq, k, d_ids, d_d2, stream);
         hip_check(hipMemcpyAsync(ids, d_ids, sizeof(int32_t) * nq * k, hipMemcpyDeviceToHost, stream), "ids D2H");
         hip_check(hipMemcpyAsync(d2, d_d2, sizeof(double) * nq * k, hipMemcpyDeviceToHost, stream), "d2 D2H");
         hip_check(hipStreamSynchronize(stream), "knn sync");

@@ -1,0 +1,59 @@
+// grid_nn.h -- device grid index for exact NN (see grid_nn.hip).
+#pragma once
+#include "mpt_internal.h"
+
+namespace mpt {
+
+struct GridParams {
+    int32_t gd;       // number of grid dims (1..3)
+    int32_t dims[3];  // state dims the grid covers
+    double lo[3];     // grid origin per grid dim
+    double h, inv_h;  // cubic cell side
+    double slack;     // subtracted from ring bounds (covers cell-assignment rounding)
+    int32_t n[3];     // cells per grid dim (1 for unused dims)
+    int64_t ncells;
+};
+
+struct GridDev {
+    GridParams g;
+    const int32_t *cell_start;  // [ncells + 1]
+    const double *pts;          // [n][d] in cell order
+    const int32_t *ids;         // 1-based original ids in cell order
+    const uint8_t *removed;     // by original row, or nullptr
+};
+
+// h chosen for about `ppc` points per cell, capped at 4 cells per point and 2^25 cells.
+GridParams make_grid_params(int32_t d, const int32_t *dims, int32_t gd, const double *lo, const double *hi, int64_t n,
+                            double ppc);
+
+class GridIndex {
+public:
+    ~GridIndex();
+    // Index points [0, min(n_upper, *n_dev)) of pts [.][d]; stream-ordered, no host sync.
+    void build(const double *pts, int64_t n_upper, const int64_t *n_dev, int32_t d, const GridParams &g,
+               hipStream_t stream);
+    GridDev dev() const;
+    const GridParams &params() const { return g; }
+
+private:
+    void reserve(int64_t cap_pts, int32_t d, int64_t ncells);
+    GridParams g{};
+    int64_t n_max = 0, pts_cap = 0, cells_cap = 0;
+    int32_t dim = 0;
+    double *spts = nullptr;
+    int32_t *sids = nullptr, *cell_of = nullptr, *counts = nullptr, *cell_start = nullptr;
+    void *temp = nullptr;
+    size_t temp_bytes = 0;
+};
+
+void launch_grid_knn(const GridDev &G, int32_t d, const double *q, int64_t nq, int32_t k, int32_t *ids, double *d2,
+                     hipStream_t stream);
+
+// Per-dim [min, max] of pts[0, n) into d_out[2*d] (lo0, hi0, lo1, hi1, ...).
+void launch_bbox(const double *pts, int64_t n, int32_t d, double *d_out, hipStream_t stream);
+
+// Grid dims: up to three dims with the largest extents, keeping only those whose extent
+// is at least a quarter of the largest (others would only add empty rings).
+int32_t choose_grid_dims(int32_t d, const double *lohi, int32_t dims[3]);
+
+}  // namespace mpt

@@ -1,0 +1,353 @@
+// grid_nn.hip -- exact nearest-neighbour search through a uniform grid built on the device.
+//
+// Same contract as nn.hip (FLANN L2<double> order, 1-based ids, (d2, id) order), but each
+// query visits only the grid cells that can still hold a better point:
+//   * the grid covers gd <= 3 "spatial" state dims (x, y, z for the omni/blimp agents,
+//     x, y for the snake) with cubic cells of side h (about `ppc` points per cell);
+//   * a query walks Chebyshev rings r = 0, 1, 2, ... of cells around its own cell; after
+//     ring r every unvisited point lies outside the (2r+1)^gd block, so its squared
+//     distance is >= LB^2, LB = distance from the query to the block boundary along the
+//     grid dims (the other dims only add non-negative terms; FLANN's sum of squares is
+//     monotone in each term, so fl(d2) >= fl(LB^2) for the exact LB);
+//   * the walk stops once LB_safe^2 > worst-of-k (strict: exact ties are still visited and
+//     resolved by id), LB_safe = LB minus a slack far above the rounding of the cell
+//     assignment, so the result equals the brute-force result bit for bit.
+// Build per snapshot: cell id per point (atomic histogram) -> exclusive scan (hipcub) ->
+// scatter of coordinates and ids into cell order.  The in-cell order is arbitrary, which
+// cannot change any result (all ties resolve by id).
+#include <algorithm>
+
+#include <hipcub/hipcub.hpp>
+
+#include "grid_nn.h"
+
+namespace mpt {
+
+__device__ __forceinline__ int cell_coord(double x, double lo, double inv_h, int n) {
+    double c = floor((x - lo) * inv_h);
+    c = c < 0.0 ? 0.0 : c;
+    c = c > (double)(n - 1) ? (double)(n - 1) : c;
+    return (int)c;
+}
+
+__global__ void k_grid_count(GridParams g, const double *__restrict__ pts, int32_t d, int64_t n,
+                             const int64_t *__restrict__ n_dev, int32_t *__restrict__ cell_of,
+                             int32_t *__restrict__ counts) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (n_dev) n = *n_dev < n ? *n_dev : n;
+    if (i >= n) return;
+    int c[3] = {0, 0, 0};
+    for (int j = 0; j < g.gd; ++j) c[j] = cell_coord(pts[i * d + g.dims[j]], g.lo[j], g.inv_h, g.n[j]);
+    const int32_t cell = (c[0] * g.n[1] + c[1]) * g.n[2] + c[2];
+    cell_of[i] = cell;
+    atomicAdd(counts + cell, 1);
+}
+
+__global__ void k_grid_scatter(const double *__restrict__ pts, int32_t d, int64_t n, const int64_t *__restrict__ n_dev,
+                               const int32_t *__restrict__ cell_of, const int32_t *__restrict__ cell_start,
+                               int32_t *__restrict__ cursor, double *__restrict__ spts, int32_t *__restrict__ sids) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (n_dev) n = *n_dev < n ? *n_dev : n;
+    if (i >= n) return;
+    const int32_t cell = cell_of[i];
+    const int64_t pos = cell_start[cell] + atomicAdd(cursor + cell, 1);
+    for (int j = 0; j < d; ++j) spts[pos * d + j] = pts[i * d + j];
+    sids[pos] = (int32_t)(i + 1);
+}
+
+template <int KMAX>
+__device__ __forceinline__ void grid_push(double (&bd)[KMAX], int32_t (&bi)[KMAX], int32_t k, double dd, int32_t id) {
+    bool done = false;
+#pragma unroll
+    for (int j = KMAX - 1; j >= 0; --j) {
+        if (j >= k || done) continue;
+        if (j == k - 1) {
+            if (!nn_better(dd, id, bd[j], bi[j])) { done = true; continue; }
+            bd[j] = dd;
+            bi[j] = id;
+        }
+        if (j > 0 && nn_better(bd[j], bi[j], bd[j - 1], bi[j - 1])) {
+            const double td = bd[j]; bd[j] = bd[j - 1]; bd[j - 1] = td;
+            const int32_t ti = bi[j]; bi[j] = bi[j - 1]; bi[j - 1] = ti;
+        } else {
+            done = true;
+        }
+    }
+}
+
+// Lower bound on the distance (along the grid dims) from q to any cell outside the ring-r
+// block; returns -1 when no cell lies outside (every cell visited).
+__device__ __forceinline__ double ring_bound(const GridParams &g, const double *qg, const int *cq, int r) {
+    double lb = __builtin_huge_val();
+    bool more = false;
+    for (int j = 0; j < g.gd; ++j) {
+        if (cq[j] - r > 0) {
+            more = true;
+            const double edge = g.lo[j] + (double)(cq[j] - r) * g.h;
+            lb = fmin(lb, qg[j] - edge);
+        }
+        if (cq[j] + r + 1 < g.n[j]) {
+            more = true;
+            const double edge = g.lo[j] + (double)(cq[j] + r + 1) * g.h;
+            lb = fmin(lb, edge - qg[j]);
+        }
+    }
+    if (!more) return -1.0;
+    lb -= g.slack;
+    return lb > 0.0 ? lb : 0.0;
+}
+
+template <int D, int KMAX>
+__global__ __launch_bounds__(256) void k_grid_knn(GridDev G, int32_t d, const double *__restrict__ q, int64_t nq,
+                                                  int32_t k, int32_t *__restrict__ out_ids, double *__restrict__ out_d2) {
+    constexpr int DD = D > 0 ? D : 16;
+    const int64_t qi = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (qi >= nq) return;
+    const GridParams &g = G.g;
+    const int dim = D > 0 ? D : d;
+    double qq[DD];
+#pragma unroll
+    for (int i = 0; i < DD; ++i) qq[i] = i < dim ? q[qi * dim + i] : 0.0;
+    double qg[3] = {0, 0, 0};
+    int cq[3] = {0, 0, 0};
+    for (int j = 0; j < g.gd; ++j) {
+        const double x = q[qi * dim + g.dims[j]];
+        qg[j] = x;
+        cq[j] = cell_coord(x, g.lo[j], g.inv_h, g.n[j]);
+    }
+    double bd[KMAX];
+    int32_t bi[KMAX];
+#pragma unroll
+    for (int i = 0; i < KMAX; ++i) { bd[i] = __builtin_huge_val(); bi[i] = -1; }
+    const int n1 = g.n[1], n2 = g.n[2];
+    for (int r = 0;; ++r) {
+        for (int dx = -r; dx <= r; ++dx) {
+            const int cx = cq[0] + dx;
+            if (cx < 0 || cx >= g.n[0]) continue;
+            const bool ex = dx == -r || dx == r;
+            for (int dy = -r; dy <= r; ++dy) {
+                const int cy = cq[1] + dy;
+                if (cy < 0 || cy >= n1) continue;
+                const bool ey = ex || dy == -r || dy == r;
+                const int step = ey ? 1 : (r > 0 ? 2 * r : 1);
+                for (int dz = -r; dz <= r; dz += step) {
+                    const int cz = cq[2] + dz;
+                    if (cz < 0 || cz >= n2) continue;
+                    const int32_t cell = (cx * n1 + cy) * n2 + cz;
+                    const int32_t s = G.cell_start[cell], e = G.cell_start[cell + 1];
+                    for (int32_t p = s; p < e; ++p) {
+                        const double dd = D > 0 ? flann_l2<DD>(qq, G.pts + (int64_t)p * DD)
+                                                : flann_l2_dyn(qq, G.pts + (int64_t)p * dim, dim);
+                        const int32_t id = G.ids[p];
+                        if (G.removed && G.removed[id - 1]) continue;
+                        double kd = bd[0];
+                        int32_t ki = bi[0];
+#pragma unroll
+                        for (int i = 0; i < KMAX; ++i)
+                            if (i == k - 1) { kd = bd[i]; ki = bi[i]; }
+                        if (nn_better(dd, id, kd, ki)) grid_push<KMAX>(bd, bi, k, dd, id);
+                    }
+                }
+            }
+        }
+        const double lb = ring_bound(g, qg, cq, r);
+        if (lb < 0.0) break;  // every cell visited
+        double worst = bd[0];
+#pragma unroll
+        for (int i = 0; i < KMAX; ++i)
+            if (i == k - 1) worst = bd[i];
+        if (lb * lb > worst) break;
+    }
+#pragma unroll
+    for (int i = 0; i < KMAX; ++i)
+        if (i < k) {
+            out_ids[qi * k + i] = bi[i];
+            out_d2[qi * k + i] = bd[i];
+        }
+}
+
+GridParams make_grid_params(int32_t d, const int32_t *dims, int32_t gd, const double *lo, const double *hi, int64_t n,
+                            double ppc) {
+    GridParams g{};
+    g.gd = gd;
+    double vol = 1.0, span_max = 0.0;
+    for (int j = 0; j < gd; ++j) {
+        g.dims[j] = dims[j];
+        const double span = hi[j] > lo[j] ? hi[j] - lo[j] : 1.0;
+        vol *= span;
+        span_max = span > span_max ? span : span_max;
+        g.lo[j] = lo[j];
+    }
+    for (int j = gd; j < 3; ++j) {
+        g.dims[j] = 0;
+        g.lo[j] = 0.0;
+        g.n[j] = 1;
+    }
+    const double cells_wanted = n > 0 ? (double)n / ppc : 1.0;
+    double h = pow(vol / (cells_wanted > 1.0 ? cells_wanted : 1.0), 1.0 / gd);
+    // cap the cell count (memory, scan length): at most 4 cells per point and 2^25 total
+    for (;;) {
+        double cells = 1.0;
+        for (int j = 0; j < gd; ++j) {
+            const double span = hi[j] > lo[j] ? hi[j] - lo[j] : 1.0;
+            cells *= ceil(span / h) > 1.0 ? ceil(span / h) : 1.0;
+        }
+        if (cells <= 4.0 * (double)(n > 1 ? n : 1) && cells <= (double)(1 << 25)) break;
+        h *= 1.25;
+    }
+    g.h = h;
+    g.inv_h = 1.0 / h;
+    g.ncells = 1;
+    double coord_max = 0.0;
+    for (int j = 0; j < gd; ++j) {
+        const double span = hi[j] > lo[j] ? hi[j] - lo[j] : 1.0;
+        const double c = ceil(span / h);
+        g.n[j] = c > 1.0 ? (int32_t)c : 1;
+        g.ncells *= g.n[j];
+        coord_max = fmax(coord_max, fabs(lo[j]) + g.n[j] * h);
+    }
+    // slack >> rounding of floor((x - lo) * inv_h) and of the edge coordinates
+    g.slack = 1e-9 * (1.0 + coord_max);
+    (void)d;
+    return g;
+}
+
+void GridIndex::reserve(int64_t cap_pts, int32_t d, int64_t ncells) {
+    if (cap_pts > pts_cap || d != dim) {
+        if (spts) hip_check(hipFree(spts), "free");
+        if (sids) hip_check(hipFree(sids), "free");
+        if (cell_of) hip_check(hipFree(cell_of), "free");
+        const int64_t c = cap_pts > 0 ? cap_pts : 1;
+        hip_check(hipMalloc(&spts, sizeof(double) * c * d), "grid pts");
+        hip_check(hipMalloc(&sids, sizeof(int32_t) * c), "grid ids");
+        hip_check(hipMalloc(&cell_of, sizeof(int32_t) * c), "grid cell_of");
+        pts_cap = c;
+        dim = d;
+    }
+    if (ncells + 1 > cells_cap) {
+        if (counts) hip_check(hipFree(counts), "free");
+        if (cell_start) hip_check(hipFree(cell_start), "free");
+        hip_check(hipMalloc(&counts, sizeof(int32_t) * (ncells + 1)), "grid counts");
+        hip_check(hipMalloc(&cell_start, sizeof(int32_t) * (ncells + 1)), "grid starts");
+        cells_cap = ncells + 1;
+        size_t tb = 0;
+        hip_check(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, counts, cell_start, (int)(ncells + 1)), "scan size");
+        if (tb > temp_bytes) {
+            if (temp) hip_check(hipFree(temp), "free");
+            hip_check(hipMalloc(&temp, tb), "scan temp");
+            temp_bytes = tb;
+        }
+    }
+}
+
+GridIndex::~GridIndex() {
+    void *ps[] = {spts, sids, cell_of, counts, cell_start, temp};
+    for (void *p : ps)
+        if (p) (void)hipFree(p);
+}
+
+void GridIndex::build(const double *pts, int64_t n_upper, const int64_t *n_dev, int32_t d, const GridParams &gp,
+                      hipStream_t stream) {
+    if (gp.ncells >= (int64_t(1) << 31) - 1) throw Error{5, "grid too large"};
+    reserve(n_upper, d, gp.ncells);
+    g = gp;
+    n_max = n_upper;
+    hip_check(hipMemsetAsync(counts, 0, sizeof(int32_t) * (g.ncells + 1), stream), "grid memset");
+    if (n_upper > 0) {
+        const unsigned blocks = (unsigned)((n_upper + 255) / 256);
+        hipLaunchKernelGGL(k_grid_count, dim3(blocks), dim3(256), 0, stream, g, pts, d, n_upper, n_dev, cell_of, counts);
+        hip_check(hipGetLastError(), "k_grid_count");
+    }
+    size_t tb = temp_bytes;
+    hip_check(hipcub::DeviceScan::ExclusiveSum(temp, tb, counts, cell_start, (int)(g.ncells + 1), stream), "scan");
+    if (n_upper > 0) {
+        hip_check(hipMemsetAsync(counts, 0, sizeof(int32_t) * g.ncells, stream), "cursor memset");
+        const unsigned blocks = (unsigned)((n_upper + 255) / 256);
+        hipLaunchKernelGGL(k_grid_scatter, dim3(blocks), dim3(256), 0, stream, pts, d, n_upper, n_dev, cell_of,
+                           cell_start, counts, spts, sids);
+        hip_check(hipGetLastError(), "k_grid_scatter");
+    }
+}
+
+GridDev GridIndex::dev() const {
+    GridDev G;
+    G.g = g;
+    G.cell_start = cell_start;
+    G.pts = spts;
+    G.ids = sids;
+    G.removed = nullptr;
+    return G;
+}
+
+__global__ __launch_bounds__(256) void k_bbox(const double *__restrict__ pts, int64_t n, int32_t d,
+                                              double *__restrict__ out) {
+    __shared__ double slo[256], shi[256];
+    const int j = blockIdx.x;
+    double lo = __builtin_huge_val(), hi = -__builtin_huge_val();
+    for (int64_t i = threadIdx.x; i < n; i += 256) {
+        const double v = pts[i * d + j];
+        lo = fmin(lo, v);
+        hi = fmax(hi, v);
+    }
+    slo[threadIdx.x] = lo;
+    shi[threadIdx.x] = hi;
+    __syncthreads();
+    for (int s = 128; s > 0; s >>= 1) {
+        if (threadIdx.x < s) {
+            slo[threadIdx.x] = fmin(slo[threadIdx.x], slo[threadIdx.x + s]);
+            shi[threadIdx.x] = fmax(shi[threadIdx.x], shi[threadIdx.x + s]);
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        out[2 * j] = slo[0];
+        out[2 * j + 1] = shi[0];
+    }
+}
+
+void launch_bbox(const double *pts, int64_t n, int32_t d, double *d_out, hipStream_t stream) {
+    hipLaunchKernelGGL(k_bbox, dim3((unsigned)d), dim3(256), 0, stream, pts, n, d, d_out);
+    hip_check(hipGetLastError(), "k_bbox");
+}
+
+int32_t choose_grid_dims(int32_t d, const double *lohi, int32_t dims[3]) {
+    int32_t order[16];
+    for (int j = 0; j < d; ++j) order[j] = j;
+    auto ext = [&](int j) { return lohi[2 * j + 1] - lohi[2 * j]; };
+    for (int a = 0; a < d; ++a)
+        for (int b = a + 1; b < d; ++b)
+            if (ext(order[b]) > ext(order[a])) std::swap(order[a], order[b]);
+    const double top = ext(order[0]);
+    int32_t gd = 0;
+    for (int i = 0; i < d && gd < 3; ++i)
+        if (ext(order[i]) >= 0.25 * top && ext(order[i]) > 0) dims[gd++] = order[i];
+    if (gd == 0) dims[gd++] = 0;
+    std::sort(dims, dims + gd);
+    return gd;
+}
+
+template <int D>
+static void grid_knn_d(const GridDev &G, int32_t d, const double *q, int64_t nq, int32_t k, int32_t *ids, double *d2,
+                       hipStream_t stream) {
+    const dim3 grid((unsigned)((nq + 255) / 256));
+    if (k == 1)
+        hipLaunchKernelGGL((k_grid_knn<D, 1>), grid, dim3(256), 0, stream, G, d, q, nq, k, ids, d2);
+    else if (k <= 16)
+        hipLaunchKernelGGL((k_grid_knn<D, 16>), grid, dim3(256), 0, stream, G, d, q, nq, k, ids, d2);
+    else
+        hipLaunchKernelGGL((k_grid_knn<D, 32>), grid, dim3(256), 0, stream, G, d, q, nq, k, ids, d2);
+}
+
+void launch_grid_knn(const GridDev &G, int32_t d, const double *q, int64_t nq, int32_t k, int32_t *ids, double *d2,
+                     hipStream_t stream) {
+    if (nq <= 0) return;
+    switch (d) {
+        case 3: grid_knn_d<3>(G, d, q, nq, k, ids, d2, stream); break;
+        case 7: grid_knn_d<7>(G, d, q, nq, k, ids, d2, stream); break;
+        case 15: grid_knn_d<15>(G, d, q, nq, k, ids, d2, stream); break;
+        default: grid_knn_d<0>(G, d, q, nq, k, ids, d2, stream); break;
+    }
+    hip_check(hipGetLastError(), "k_grid_knn launch");
+}
+
+}  // namespace mpt

@@ -17,7 +17,10 @@
 #include <cstring>
 #include <vector>
 
+#include <memory>
+
 #include "../../include/mpt.h"
+#include "grid_nn.h"
 #include "mpt_internal.h"
 
 namespace mpt {
@@ -303,12 +306,20 @@ struct mpt_rrt {
     bool timing = false;
     hipEvent_t ev[7] = {};
     float last_ms[6] = {0, 0, 0, 0, 0, 0};
+    // NN structure over the round's snapshot (grid_nn.hip), rebuilt every round
+    int32_t nn_mode = MPT_NN_AUTO;
+    std::unique_ptr<GridIndex> grid;
+    int32_t grid_gd = 0, grid_dims[3] = {0, 0, 0};
+    double ppc = 2.0;
+    // optional collision work counters (k_collide atomics): units, clusters, node visits, tri tests
+    bool stats_on = false;
+    unsigned long long *d_cstats = nullptr;
 };
 
 namespace {
 void rfree(mpt_rrt *r) {
-    void *ps[] = {r->d_links, r->d_nodes, r->d_parents, r->d_n, r->d_counters, r->d_samples, r->d_ends,
-                  r->d_poses, r->d_nnd2, r->d_nn, r->d_pcount, r->d_bcount, r->d_verdict, r->d_scratch};
+    void *ps[] = {r->d_links, r->d_nodes, r->d_parents, r->d_n,  r->d_counters, r->d_samples, r->d_ends, r->d_poses,
+                  r->d_nnd2,  r->d_nn,    r->d_pcount,  r->d_bcount, r->d_verdict, r->d_scratch, r->d_cstats};
     for (void *p : ps)
         if (p) (void)hipFree(p);
     for (auto &e : r->ev)
@@ -390,6 +401,9 @@ extern "C" mpt_status mpt_rrt_create(const mpt_env *env, const mpt_agent *agent,
             hip_check(hipMalloc(&r->d_counters, sizeof(unsigned long long) * 8), "alloc counters");
             hip_check(hipMemset(r->d_counters, 0, sizeof(unsigned long long) * 8), "memset counters");
             for (auto &e : r->ev) hip_check(hipEventCreate(&e), "event");
+            r->grid.reset(new GridIndex());
+            r->grid_gd = agent_kind == MPT_AGENT_SNAKE ? 2 : 3;
+            for (int j = 0; j < 3; ++j) r->grid_dims[j] = j;
         } catch (...) {
             rfree(r);
             delete r;
@@ -455,16 +469,32 @@ extern "C" mpt_status mpt_rrt_step(mpt_rrt *r, int32_t K, void *stream_) {
         hipLaunchKernelGGL(k_sample, dim3(kb), dim3(256), 0, stream, p, r->ext_base, K, r->d_samples);
         hip_check(hipGetLastError(), "k_sample");
         mark(1);
-        NNWork w{};
-        w.pts = r->d_nodes;
-        w.removed = nullptr;
-        w.n = r->n_upper;
-        w.d = p.d;
-        w.q = r->d_samples;
-        w.nq = K;
-        w.n_dev = r->d_n;
-        launch_knn(w, 1, r->d_nn, r->d_nnd2, r->d_scratch, stream);
+        const bool use_grid = r->nn_mode == MPT_NN_GRID || (r->nn_mode == MPT_NN_AUTO && r->n_upper >= 4096);
+        if (use_grid) {
+            // spatial dims of the agent's tree state: x, y, z (omni, blimp) or x, y (snake);
+            // the grid spans the sampling ranges, nodes outside fall into the border cells
+            double lo[3], hi[3];
+            for (int j = 0; j < r->grid_gd; ++j) {
+                lo[j] = p.lo[r->grid_dims[j]];
+                hi[j] = p.hi[r->grid_dims[j]];
+            }
+            const GridParams g = make_grid_params(p.d, r->grid_dims, r->grid_gd, lo, hi, r->n_upper, r->ppc);
+            r->grid->build(r->d_nodes, r->n_upper, r->d_n, p.d, g, stream);
+        }
         mark(2);
+        if (use_grid) {
+            launch_grid_knn(r->grid->dev(), p.d, r->d_samples, K, 1, r->d_nn, r->d_nnd2, stream);
+        } else {
+            NNWork w{};
+            w.pts = r->d_nodes;
+            w.removed = nullptr;
+            w.n = r->n_upper;
+            w.d = p.d;
+            w.q = r->d_samples;
+            w.nq = K;
+            w.n_dev = r->d_n;
+            launch_knn(w, 1, r->d_nn, r->d_nnd2, r->d_scratch, stream);
+        }
         mark(3);
         hipLaunchKernelGGL(k_steer, dim3(kb), dim3(256), 0, stream, p, r->ext_base, K, r->d_nodes, r->d_nn, r->d_ends,
                            r->d_poses, r->d_pcount, r->d_counters);
@@ -479,7 +509,7 @@ extern "C" mpt_status mpt_rrt_step(mpt_rrt *r, int32_t K, void *stream_) {
         cw.L = p.L;
         cw.n_units = (int64_t)K * p.pmax * p.L;
         cw.verdict = r->d_verdict;
-        cw.stats = nullptr;
+        cw.stats = r->stats_on ? r->d_cstats : nullptr;
         launch_collide(r->env, r->d_links, cw, stream);
         mark(5);
         hipLaunchKernelGGL(k_count, dim3(kb), dim3(256), 0, stream, r->d_verdict, K, r->d_bcount);
@@ -552,6 +582,32 @@ extern "C" mpt_status mpt_rrt_info(const mpt_rrt *r, int64_t info[4]) {
     });
 }
 
+extern "C" mpt_status mpt_rrt_collide_stats(mpt_rrt *r, int32_t enable, uint64_t out[4]) {
+    return guarded([&] {
+        if (!r) throw Error{MPT_ERR_INVALID, "null pointer"};
+        hip_check(hipDeviceSynchronize(), "sync");
+        if (!r->d_cstats) {
+            hip_check(hipMalloc(&r->d_cstats, sizeof(unsigned long long) * 4), "alloc stats");
+            hip_check(hipMemset(r->d_cstats, 0, sizeof(unsigned long long) * 4), "memset stats");
+        }
+        if (out) {
+            unsigned long long h[4];
+            hip_check(hipMemcpy(h, r->d_cstats, sizeof(h), hipMemcpyDeviceToHost), "stats D2H");
+            for (int i = 0; i < 4; ++i) out[i] = h[i];
+        }
+        hip_check(hipMemset(r->d_cstats, 0, sizeof(unsigned long long) * 4), "memset stats");
+        r->stats_on = enable != 0;
+    });
+}
+
+extern "C" mpt_status mpt_rrt_set_nn(mpt_rrt *r, int32_t mode, double points_per_cell) {
+    return guarded([&] {
+        if (!r || mode < MPT_NN_AUTO || mode > MPT_NN_GRID) throw Error{MPT_ERR_INVALID, "bad arguments"};
+        r->nn_mode = mode;
+        if (points_per_cell > 0) r->ppc = points_per_cell;
+    });
+}
+
 extern "C" mpt_status mpt_rrt_enable_timing(mpt_rrt *r, int32_t enable) {
     return guarded([&] {
         if (!r) throw Error{MPT_ERR_INVALID, "null pointer"};
@@ -564,7 +620,7 @@ extern "C" mpt_status mpt_rrt_kernel_times(mpt_rrt *r, float ms[6]) {
         if (!r || !ms) throw Error{MPT_ERR_INVALID, "null pointer"};
         if (!r->timing) throw Error{MPT_ERR_INVALID, "timing not enabled"};
         hip_check(hipEventSynchronize(r->ev[6]), "event sync");
-        // [sample, nn (+merge), (reserved), steer, collide, append]
+        // [sample, nn_build, nn_query, steer, collide, append]
         const int a[6] = {0, 1, 2, 3, 4, 5};
         const int b[6] = {1, 2, 3, 4, 5, 6};
         for (int i = 0; i < 6; ++i) hip_check(hipEventElapsedTime(&ms[i], r->ev[a[i]], r->ev[b[i]]), "elapsed");

@@ -96,8 +96,9 @@ def check_round(mpt, oracle, sc, eng, tree, seed, ext_base, K):
     return t2, verdict
 
 
+@pytest.mark.parametrize("nn_mode", ["brute", "grid"])
 @pytest.mark.parametrize("name", ["omni", "blimp", "snake"])
-def test_engine_rounds(mpt_gpu, oracle, name):
+def test_engine_rounds(mpt_gpu, oracle, name, nn_mode):
     if name == "omni":
         sc, n0, K = scenes.omni_scenario(), 3000, 1024
     elif name == "blimp":
@@ -106,10 +107,27 @@ def test_engine_rounds(mpt_gpu, oracle, name):
         sc, n0, K = scenes.snake_scenario("corridor"), 3000, 700
     seed = 1234
     eng, tree = make(mpt_gpu, sc, n0, K, seed)
+    eng.set_nn(nn_mode)
     tree, v1 = check_round(mpt_gpu, oracle, sc, eng, tree, seed, 0, K)
     assert 0 < v1.sum() < K or name == "snake"
     # second round sees the first round's nodes
     tree, _ = check_round(mpt_gpu, oracle, sc, eng, tree, seed, K, K // 2 + 3)
+
+
+def test_engine_grid_equals_brute_over_growing_rounds(mpt_gpu, oracle):
+    """A growing tree (no reset) over several rounds: the grid and the brute-force NN
+    engines must build the same tree bit for bit (rounds build the grid from scratch)."""
+    sc = scenes.blimp_scenario("last")
+    trees = []
+    for mode in ("brute", "grid"):
+        eng, tree = make(mpt_gpu, sc, 6000, 4096, 77, cap_extra=5 * 4096)
+        eng.set_nn(mode)
+        for K in (4096, 1000, 4096, 333, 2048):
+            eng.step(K)
+        n = eng.counters()["nodes"]
+        trees.append(eng.read_tree(n))
+    assert np.array_equal(bits(trees[0][0]), bits(trees[1][0]))
+    assert np.array_equal(trees[0][1], trees[1][1])
 
 
 def test_engine_set_size_and_capacity(mpt_gpu, oracle):

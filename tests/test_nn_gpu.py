@@ -10,12 +10,18 @@ def bits(a):
     return np.ascontiguousarray(a, np.float64).view(np.uint64)
 
 
-@pytest.mark.parametrize("d,n,nq", [(3, 1, 5), (3, 5000, 700), (7, 20000, 1024), (15, 3000, 300), (5, 4000, 257)])
-def test_knn1_exact(mpt_gpu, oracle, d, n, nq):
+MODES = ["brute", "grid"]
+
+
+@pytest.mark.parametrize("mode", MODES)
+@pytest.mark.parametrize("d,n,nq", [(3, 1, 5), (3, 5000, 700), (7, 20000, 1024), (15, 3000, 300), (5, 4000, 257),
+                                    (2, 30000, 999)])
+def test_knn1_exact(mpt_gpu, oracle, d, n, nq, mode):
     rng = np.random.default_rng(d * 1000 + n)
     pts = rng.uniform(-100, 100, size=(n, d))
     q = rng.uniform(-100, 100, size=(nq, d))
     nn = mpt_gpu.NearestNeighbors(d, 16)
+    nn.set_index(mode)
     ids = nn.append(pts)
     assert ids.tolist() == list(range(1, n + 1))
     gi, gd = nn.knn(q, 1)
@@ -24,12 +30,14 @@ def test_knn1_exact(mpt_gpu, oracle, d, n, nq):
     assert np.array_equal(bits(gd), bits(rd))
 
 
+@pytest.mark.parametrize("mode", MODES)
 @pytest.mark.parametrize("k", [2, 10, 16, 32])
-def test_knn_k_exact(mpt_gpu, oracle, k):
+def test_knn_k_exact(mpt_gpu, oracle, k, mode):
     rng = np.random.default_rng(k)
     pts = rng.uniform(-10, 10, size=(6000, 7))
     q = rng.uniform(-10, 10, size=(500, 7))
     nn = mpt_gpu.NearestNeighbors(7)
+    nn.set_index(mode)
     nn.append(pts)
     gi, gd = nn.knn(q, k)
     ri, rd = oracle.knn(pts, q, k)
@@ -37,17 +45,39 @@ def test_knn_k_exact(mpt_gpu, oracle, k):
     assert np.array_equal(bits(gd), bits(rd))
 
 
-def test_ties_resolve_to_lowest_id(mpt_gpu, oracle):
+@pytest.mark.parametrize("mode", MODES)
+def test_ties_resolve_to_lowest_id(mpt_gpu, oracle, mode):
     rng = np.random.default_rng(7)
     base = rng.integers(-3, 4, size=(500, 3)).astype(np.float64)  # lattice: many exact ties
     pts = np.concatenate([base, base, base])
-    q = rng.integers(-3, 4, size=(300, 3)).astype(np.float64) + 0.5
+    q = np.r_[rng.integers(-3, 4, size=(300, 3)).astype(np.float64) + 0.5, base[:50]]
     nn = mpt_gpu.NearestNeighbors(3)
+    nn.set_index(mode)
     nn.append(pts)
     for k in (1, 4):
         gi, gd = nn.knn(q, k)
         ri, rd = oracle.knn(pts, q, k)
         assert np.array_equal(gi, ri) and np.array_equal(bits(gd), bits(rd))
+
+
+def test_grid_clustered_and_outside_points(mpt_gpu, oracle):
+    """Non-uniform data (a dense cluster, far outliers, queries outside the data box):
+    the grid must stay exact."""
+    rng = np.random.default_rng(21)
+    pts = np.r_[rng.normal(0, 0.01, size=(6000, 7)), rng.uniform(-1000, 1000, size=(200, 7)),
+                rng.uniform(-5, 5, size=(3000, 7))]
+    q = np.r_[rng.normal(0, 0.02, size=(300, 7)), rng.uniform(-3000, 3000, size=(200, 7))]
+    nn = mpt_gpu.NearestNeighbors(7)
+    nn.set_index("grid")
+    nn.append(pts)
+    for k in (1, 5):
+        gi, gd = nn.knn(q, k)
+        ri, rd = oracle.knn(pts, q, k)
+        assert np.array_equal(gi, ri) and np.array_equal(bits(gd), bits(rd))
+    nn.remove(3)
+    gi, _ = nn.knn(pts[2:3], 1)
+    ri, _ = oracle.knn(pts, pts[2:3], 1, removed=np.r_[0, 0, 1, np.zeros(len(pts) - 3)].astype(np.uint8))
+    assert np.array_equal(gi, ri)
 
 
 def test_fewer_points_than_k_and_removed(mpt_gpu, oracle):
@@ -61,19 +91,20 @@ def test_fewer_points_than_k_and_removed(mpt_gpu, oracle):
     assert len(nn) == 3
 
 
-def test_incremental_append_growth(mpt_gpu, oracle):
+@pytest.mark.parametrize("mode", MODES)
+def test_incremental_append_growth(mpt_gpu, oracle, mode):
     rng = np.random.default_rng(9)
     nn = mpt_gpu.NearestNeighbors(7, 4)
+    nn.set_index(mode)
     pts = []
+    q = rng.uniform(-1, 1, size=(200, 7))
     for _ in range(20):
         p = rng.uniform(-1, 1, size=(rng.integers(1, 500), 7))
         nn.append(p)
         pts.append(p)
-    pts = np.concatenate(pts)
-    q = rng.uniform(-1, 1, size=(200, 7))
-    gi, gd = nn.knn(q, 3)
-    ri, rd = oracle.knn(pts, q, 3)
-    assert np.array_equal(gi, ri) and np.array_equal(bits(gd), bits(rd))
+        gi, gd = nn.knn(q, 3)  # queries interleaved with appends: the index is rebuilt
+        ri, rd = oracle.knn(np.concatenate(pts), q, 3)
+        assert np.array_equal(gi, ri) and np.array_equal(bits(gd), bits(rd))
 
 
 @pytest.mark.parametrize("max_nb", [-1, 3])
