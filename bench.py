@@ -238,6 +238,7 @@ def main():
         "checked_per_s": checked / elapsed,
         "valid_fraction": valid / max(checked, 1),
         "kernel_ms_per_round": {k: round(v, 4) for k, v in per_launch.items()},
+        "collide_work_per_round": cst,
         "roofline": roof,
     }
     if not args.no_cpu and world == 1:

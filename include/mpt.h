@@ -93,6 +93,13 @@ mpt_status mpt_collide_batch_device(const mpt_env *env, const mpt_agent *const *
  * [units, clusters, bvh node visits, triangle-pair tests]; enabled by mpt_set_stats(1). */
 mpt_status mpt_set_stats(int32_t enable);
 mpt_status mpt_last_collide_stats(uint64_t stats[4]);
+/* Collision kernel structure (process-wide, both for mpt_collide_batch* and the RRT
+ * engine): MPT_COLLIDE_SPLIT (default) = broad-phase box traversal writing candidate
+ * triangle pairs, then one exact triangle test per candidate; MPT_COLLIDE_FUSED = one
+ * kernel walking the BVH and testing at the leaves with per-edge early exit.
+ * Verdicts are identical; the choice only changes speed. */
+enum { MPT_COLLIDE_SPLIT = 0, MPT_COLLIDE_FUSED = 1 };
+mpt_status mpt_set_collide_mode(int32_t mode);
 
 /* ---- NN: FLANN_KDTreeWrapper ---- */
 mpt_status mpt_nn_create(int32_t dim, int64_t capacity, mpt_nn **out);
@@ -161,8 +168,9 @@ mpt_status mpt_rrt_enable_timing(mpt_rrt *rrt, int32_t enable);
 mpt_status mpt_rrt_set_nn(mpt_rrt *rrt, int32_t mode, double points_per_cell);
 /* Collision work counters accumulated since the previous call (synchronises), then reset;
  * enable = 1 keeps counting in later rounds (atomics: off for timed runs).
- * out [4] (may be NULL): (pose, link) units, clusters visited, BVH node visits, triangle tests. */
-mpt_status mpt_rrt_collide_stats(mpt_rrt *rrt, int32_t enable, uint64_t out[4]);
+ * out [8] (may be NULL): (pose, link) units, clusters visited, BVH node visits, triangle tests,
+ * max node visits of one unit, max / sum of wave lifetimes (s_memtime ticks), reserved. */
+mpt_status mpt_rrt_collide_stats(mpt_rrt *rrt, int32_t enable, uint64_t out[8]);
 mpt_status mpt_rrt_kernel_times(mpt_rrt *rrt, float ms[6]);
 
 #ifdef __cplusplus

@@ -20,6 +20,7 @@ from .api import (  # noqa: F401
     last_collide_stats,
     load_mesh,
     rrt_inst,
+    set_collide_mode,
     set_collide_stats,
     synchronize,
     transform_from_location,
@@ -28,5 +29,5 @@ from .api import (  # noqa: F401
 __all__ = [
     "AGENT_OMNI", "AGENT_BLIMP", "AGENT_SNAKE", "AgentMesh", "Environment", "NearestNeighbors", "RRTEngine",
     "collide_batch", "collide_batch_device", "init", "last_collide_stats", "load_mesh", "rrt_inst",
-    "set_collide_stats", "synchronize", "transform_from_location", "build", "lib", "LIB_PATH", "MptError",
+    "set_collide_mode", "set_collide_stats", "synchronize", "transform_from_location", "build", "lib", "LIB_PATH", "MptError",
 ]

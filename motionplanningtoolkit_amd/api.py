@@ -129,6 +129,15 @@ def collide_batch_device(env: Environment, links: Sequence[AgentMesh], d_poses, 
                                          total_poses, _p(d_verdict), _stream(stream)), "mpt_collide_batch_device")
 
 
+COLLIDE_MODES = {"split": 0, "fused": 1}
+
+
+def set_collide_mode(mode: str) -> None:
+    """Collision kernel structure: "split" (broad phase -> candidate pairs -> exact test,
+    default) or "fused" (BVH walk with the exact test at the leaves).  Same verdicts."""
+    check(lib().mpt_set_collide_mode(COLLIDE_MODES[mode]), "mpt_set_collide_mode")
+
+
 def set_collide_stats(enable: bool) -> None:
     check(lib().mpt_set_stats(1 if enable else 0), "mpt_set_stats")
 
@@ -266,9 +275,10 @@ class RRTEngine:
 
     def collide_stats(self, enable: bool) -> dict:
         """Counters since the last call (then reset); enable keeps counting in later rounds."""
-        out = np.zeros(4, np.uint64)
+        out = np.zeros(8, np.uint64)
         check(lib().mpt_rrt_collide_stats(self.handle, 1 if enable else 0, _p(out)), "mpt_rrt_collide_stats")
-        return {"units": int(out[0]), "clusters": int(out[1]), "node_visits": int(out[2]), "tri_tests": int(out[3])}
+        return {"units": int(out[0]), "clusters": int(out[1]), "node_visits": int(out[2]), "tri_tests": int(out[3]),
+                "max_unit_node_visits": int(out[4]), "max_wave_ticks": int(out[5]), "sum_wave_ticks": int(out[6])}
 
     def set_nn(self, mode: str = "auto", points_per_cell: float = 0.0) -> None:
         """NN structure of the rounds: 'auto' | 'brute' | 'grid' (identical results)."""

@@ -1,6 +1,7 @@
 // capi.cpp -- extern "C" boundary (include/mpt.h): handles, host<->device copies, BVH
 // and cluster construction for the environment and agent meshes.
 #include <algorithm>
+#include <atomic>
 #include <cmath>
 #include <cstring>
 #include <mutex>
@@ -20,7 +21,9 @@ static thread_local std::string g_last_error;
 std::string &last_error_ref() { return g_last_error; }
 static int g_device = -1;
 static thread_local bool g_stats_enabled = false;
-static thread_local unsigned long long g_last_stats[4] = {0, 0, 0, 0};
+static thread_local unsigned long long g_last_stats[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+static std::atomic<int32_t> g_collide_mode{MPT_COLLIDE_SPLIT};
+int32_t collide_mode() { return g_collide_mode.load(std::memory_order_relaxed); }
 
 void hip_check(hipError_t e, const char *what) {
     if (e != hipSuccess) throw Error{MPT_ERR_HIP, std::string(what) + ": " + hipGetErrorString(e)};
@@ -60,6 +63,7 @@ struct DevBuf {
 
 struct Workspace {
     DevBuf poses, pose_edge, verdict, links, q, ids, d2, scratch, offsets, stats;
+    CollideScratch cs;
 };
 static thread_local Workspace g_ws;
 
@@ -72,6 +76,7 @@ struct mpt_env {
     EnvDev dev{};
     EnvTri *d_tris = nullptr;
     BvhNode *d_nodes = nullptr;
+    Item *d_items = nullptr;
     int64_t n_tris = 0, n_nodes = 0, depth = 0;
 };
 
@@ -145,6 +150,93 @@ int64_t build_env_bvh(std::vector<TriRef> &refs, int64_t first, int64_t n, std::
     nd.b = (int32_t)r;
     nodes[id] = nd;
     return id;
+}
+
+// Level (breadth-first) order: the root and the top levels form a prefix of the array.
+std::vector<BvhNode> bfs_order(const std::vector<BvhNode> &in) {
+    std::vector<BvhNode> out;
+    out.reserve(in.size());
+    std::vector<int32_t> queue;
+    queue.reserve(in.size());
+    queue.push_back(0);
+    for (size_t h = 0; h < queue.size(); ++h) {
+        const BvhNode &n = in[queue[h]];
+        BvhNode m = n;
+        if (n.b >= 0) {
+            m.a = (int32_t)(queue.size());      // children get the next free BFS slots
+            queue.push_back(n.a);
+            m.b = (int32_t)(queue.size());
+            queue.push_back(n.b);
+        }
+        out.push_back(m);
+    }
+    return out;
+}
+
+// Broad-phase 64-ary tree (mpt_internal.h Item) from the pre-order median-split BVH,
+// whose subtrees are contiguous ranges of the leaf order.
+struct Range {
+    int32_t first, count;
+};
+Range subtree_range(const std::vector<BvhNode> &pre, int32_t id, std::vector<Range> &memo) {
+    const BvhNode &n = pre[id];
+    Range r = n.b < 0 ? Range{n.a, 1} : Range{0, 0};
+    if (n.b >= 0) {
+        const Range l = subtree_range(pre, n.a, memo), h = subtree_range(pre, n.b, memo);
+        r = Range{l.first, l.count + h.count};
+    }
+    memo[id] = r;
+    return r;
+}
+void collect_buckets(const std::vector<BvhNode> &pre, int32_t id, const std::vector<Range> &memo,
+                     std::vector<Range> &out) {
+    if (memo[id].count <= kClusterMax) {
+        out.push_back(memo[id]);
+        return;
+    }
+    collect_buckets(pre, pre[id].a, memo, out);
+    collect_buckets(pre, pre[id].b, memo, out);
+}
+Item union_item(const std::vector<Item> &lvl, int32_t first, int32_t count) {
+    Item it{{HUGE_VALF, HUGE_VALF, HUGE_VALF}, first, {-HUGE_VALF, -HUGE_VALF, -HUGE_VALF}, count};
+    for (int32_t i = first; i < first + count; ++i)
+        for (int k = 0; k < 3; ++k) {
+            it.lo[k] = std::min(it.lo[k], lvl[i].lo[k]);
+            it.hi[k] = std::max(it.hi[k], lvl[i].hi[k]);
+        }
+    return it;
+}
+std::vector<Item> wide_tree(const std::vector<BvhNode> &pre, int64_t n_tris, std::vector<int32_t> &lev_off) {
+    std::vector<std::vector<Item>> levels(1);
+    levels[0].resize((size_t)n_tris);
+    for (const BvhNode &n : pre)
+        if (n.b < 0) levels[0][n.a] = Item{{n.lo[0], n.lo[1], n.lo[2]}, n.a, {n.hi[0], n.hi[1], n.hi[2]}, 1};
+    if (n_tris > kClusterMax) {
+        std::vector<Range> memo(pre.size()), buckets;
+        subtree_range(pre, 0, memo);
+        collect_buckets(pre, 0, memo, buckets);
+        std::vector<Item> l1;
+        for (const Range &r : buckets) l1.push_back(union_item(levels[0], r.first, r.count));
+        levels.push_back(std::move(l1));
+    }
+    while (levels.back().size() > (size_t)kClusterMax) {
+        const std::vector<Item> &lo = levels.back();
+        std::vector<Item> up;
+        for (size_t f = 0; f < lo.size(); f += kClusterMax)
+            up.push_back(union_item(lo, (int32_t)f, (int32_t)std::min<size_t>(kClusterMax, lo.size() - f)));
+        levels.push_back(std::move(up));
+    }
+    if ((int)levels.size() > kMaxLevels) throw Error{MPT_ERR_INTERNAL, "env tree too deep"};
+    std::vector<Item> all;
+    lev_off.assign(1, 0);
+    for (size_t l = 0; l < levels.size(); ++l) {
+        for (Item it : levels[l]) {
+            if (l > 0) it.first += lev_off[l - 1];  // children as absolute item indices
+            all.push_back(it);
+        }
+        lev_off.push_back((int32_t)all.size());
+    }
+    return all;
 }
 
 // Agent clusters: the same median split, stopping at <= 64 triangles.
@@ -239,6 +331,14 @@ extern "C" mpt_status mpt_env_create(const double *tris, int64_t n_tris, const d
                 nodes.reserve(2 * n_tris);
                 build_env_bvh(refs, 0, n_tris, nodes, order, 0, depth);
                 if (depth + 1 >= kStackDepth) throw Error{MPT_ERR_INTERNAL, "env BVH too deep"};
+                std::vector<int32_t> lev_off;
+                const std::vector<Item> items = wide_tree(nodes, n_tris, lev_off);
+                hip_check(hipMalloc(&env->d_items, sizeof(Item) * items.size()), "hipMalloc env items");
+                hip_check(hipMemcpy(env->d_items, items.data(), sizeof(Item) * items.size(), hipMemcpyHostToDevice),
+                          "H2D");
+                env->dev.n_levels = (int32_t)lev_off.size() - 1;
+                for (size_t l = 0; l < lev_off.size(); ++l) env->dev.lev_off[l] = lev_off[l];
+                nodes = bfs_order(nodes);  // top levels first: the prefix k_collide stages in LDS
                 recs.resize(n_tris);
                 for (int64_t i = 0; i < n_tris; ++i) make_env_tri(tris + 9 * order[i], recs[i]);
                 hip_check(hipMalloc(&env->d_tris, sizeof(EnvTri) * n_tris), "hipMalloc env tris");
@@ -246,7 +346,12 @@ extern "C" mpt_status mpt_env_create(const double *tris, int64_t n_tris, const d
                 hip_check(hipMemcpy(env->d_tris, recs.data(), sizeof(EnvTri) * n_tris, hipMemcpyHostToDevice), "H2D");
                 hip_check(hipMemcpy(env->d_nodes, nodes.data(), sizeof(BvhNode) * nodes.size(), hipMemcpyHostToDevice),
                           "H2D");
+                for (int k = 0; k < 3; ++k) {
+                    env->dev.root_lo[k] = nodes[0].lo[k];
+                    env->dev.root_hi[k] = nodes[0].hi[k];
+                }
             }
+            env->dev.items = env->d_items;
             env->n_tris = n_tris;
             env->n_nodes = (int64_t)nodes.size();
             env->depth = depth;
@@ -268,6 +373,7 @@ extern "C" mpt_status mpt_env_destroy(mpt_env *env) {
         if (!env) return;
         if (env->d_tris) (void)hipFree(env->d_tris);
         if (env->d_nodes) (void)hipFree(env->d_nodes);
+        if (env->d_items) (void)hipFree(env->d_items);
         delete env;
     });
 }
@@ -379,10 +485,15 @@ static void collide_common(const mpt_env *env, const mpt_agent *const *links, in
     w.verdict = d_verdict;
     w.stats = nullptr;
     if (g_stats_enabled) {
-        w.stats = (unsigned long long *)g_ws.stats.get(sizeof(unsigned long long) * 4);
-        hip_check(hipMemsetAsync(w.stats, 0, sizeof(unsigned long long) * 4, stream), "stats memset");
+        w.stats = (unsigned long long *)g_ws.stats.get(sizeof(unsigned long long) * 8);
+        hip_check(hipMemsetAsync(w.stats, 0, sizeof(unsigned long long) * 8, stream), "stats memset");
     }
-    launch_collide(env->dev, d_links, w, stream);
+    if (collide_mode() == MPT_COLLIDE_FUSED) {
+        launch_collide(env->dev, d_links, w, stream);
+    } else {
+        g_ws.cs.ensure(w.n_units);
+        launch_collide_split(env->dev, d_links, w, g_ws.cs, stream);
+    }
     if (w.stats) {
         hip_check(hipMemcpyAsync(g_last_stats, w.stats, sizeof(g_last_stats), hipMemcpyDeviceToHost, stream), "stats");
     }
@@ -436,6 +547,13 @@ extern "C" mpt_status mpt_collide_batch_device(const mpt_env *env, const mpt_age
         auto *d_pe = (int32_t *)g_ws.pose_edge.get(sizeof(int32_t) * std::max<int64_t>(total_poses, 1));
         launch_pose_edge(d_edge_pose_offsets, E, d_pe, stream);
         collide_common(env, links, L, d_poses, d_pe, total_poses, E, d_verdict_out, stream);
+    });
+}
+
+extern "C" mpt_status mpt_set_collide_mode(int32_t mode) {
+    return guarded([&] {
+        require(mode == MPT_COLLIDE_SPLIT || mode == MPT_COLLIDE_FUSED, "unknown collide mode");
+        g_collide_mode.store(mode, std::memory_order_relaxed);
     });
 }
 

@@ -3,56 +3,73 @@
 // Replaces MeshHandler::isInCollision (utilities/meshhandler.hpp:187-243) and the FCL
 // 0.3.2 path behind it (DynamicAABBTreeCollisionManager broadphase + OBBRSS traversal
 // + Intersect::intersect_Triangle).  Verdict per edge = exists (pose, link, env tri,
-// agent tri) with intersect_Triangle true, i.e. the all-pairs definition; every box
-// test below only prunes, with margins (fcl_math.h widen_*) that keep it conservative.
+// agent tri) whose exact AABBs overlap (fcl_math.h tri_gate: FCL's BV test before the
+// leaf test) and with intersect_Triangle true, i.e. the gated all-pairs definition;
+// every float box test below only prunes, with margins (fcl_math.h widen_*) that keep
+// it conservative.
 //
-// Mapping: one wavefront per (pose, link) unit.  The agent link mesh is stored in
-// clusters of <= 64 triangles (one triangle per lane).  Per unit:
+// Two structures, same verdicts (mpt_set_collide_mode):
+//  * split (default): k_broad -> k_narrow below, the fused kernel only for overflow;
+//  * fused: k_collide, described here.
+// Fused mapping: one wavefront per (pose, link) unit, waves stride over the units (a bounded
+// grid, so the per-workgroup LDS staging below is amortised).  The agent link mesh is
+// stored in clusters of <= 64 triangles (one triangle per lane).  Per unit:
 //   1. R, T = fcl::relativeTransform(env tf, pose)                      (uniform)
 //   2. lanes over clusters: transformed cluster box vs env root box -> ballot mask
 //   3. per surviving cluster: each lane maps its triangle Q_i' = R Q_i + T exactly as
-//      FCL does and takes its float box; the wave then walks the env BVH UNIFORMLY
-//      (one node at a time, stack in LDS, node index in an SGPR so node / triangle
-//      records arrive by scalar loads); at each node the lanes' boxes are tested and
-//      a ballot decides descent, so there is no traversal divergence;
+//      FCL does and takes its float box; the wave walks the env BVH UNIFORMLY (one node
+//      at a time, node index in an SGPR, stack in LDS); the top of the BVH (breadth-first
+//      prefix, up to kLdsNodes nodes -- all of it for the benchmark rooms) is staged in LDS
+//      once per workgroup, deeper nodes come from global memory; at each node a ballot
+//      of the lanes' box tests decides descent, so traversal never diverges;
 //   4. at a leaf, lanes whose box overlaps the env triangle run the 17-axis test;
 //      any hit -> verdict[edge] = 1 and the wave (and later units of that edge) stop.
-#include "mpt_internal.h"
+#include "collide_common.h"
 
 namespace mpt {
+
+constexpr int kCollideWaves = 4;     // waves per workgroup
+constexpr int kLdsNodes = 1024;      // 32 KiB of BVH nodes per workgroup
 
 __device__ __forceinline__ bool box_hit(const float lo[3], const float hi[3], const BvhNode &n) {
     return lo[0] <= n.hi[0] && n.lo[0] <= hi[0] && lo[1] <= n.hi[1] && n.lo[1] <= hi[1] &&
            lo[2] <= n.hi[2] && n.lo[2] <= hi[2];
 }
 
-__device__ __forceinline__ uint8_t load_flag(const uint8_t *p) {
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
 // Uniform walk of the env BVH for one cluster.  Returns true on a contact.
-__device__ bool walk_env(const BvhNode *__restrict__ nodes, const EnvTri *__restrict__ etris,
-                         int32_t *stk, bool act, v3 Q1, v3 Q2, v3 Q3, const float blo[3],
-                         const float bhi[3], uint32_t &n_nodes, uint32_t &n_sat) {
+__device__ bool walk_env(const BvhNode *__restrict__ s_nodes, int32_t n_lds, const BvhNode *__restrict__ nodes,
+                         const EnvTri *__restrict__ etris, int32_t *stk, bool act, v3 Q1, v3 Q2, v3 Q3,
+                         const float blo[3], const float bhi[3], uint32_t &n_nodes, uint32_t &n_sat) {
     int sp = 0;
     int32_t node = 0;
     for (;;) {
-        const BvhNode nd = nodes[node];
+        // node is wave-uniform (SGPR): LDS prefix via ds_read, the rest via global loads
+        BvhNode nd;
+        if (node < n_lds) {
+            nd = s_nodes[node];
+        } else {
+            typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+            const u32x4 *g = reinterpret_cast<const u32x4 *>(nodes + node);
+            const u32x4 a = __builtin_nontemporal_load(g), b = __builtin_nontemporal_load(g + 1);
+            nd.lo[0] = __uint_as_float(a.x); nd.lo[1] = __uint_as_float(a.y); nd.lo[2] = __uint_as_float(a.z);
+            nd.a = (int32_t)a.w;
+            nd.hi[0] = __uint_as_float(b.x); nd.hi[1] = __uint_as_float(b.y); nd.hi[2] = __uint_as_float(b.z);
+            nd.b = (int32_t)b.w;
+        }
         ++n_nodes;
         const bool ov = act && box_hit(blo, bhi, nd);
-        if (__ballot(ov)) {
+        const uint64_t m = __ballot(ov);
+        if (m) {
             if (nd.b < 0) {
-                const EnvTri E = etris[nd.a];
+                const EnvTri &E = etris[nd.a];
                 bool hit = false;
-                if (ov) {
-                    hit = tri_intersect(E, Q1, Q2, Q3);
-                }
-                n_sat += __popcll(__ballot(ov));
+                if (ov) hit = tri_gate(E.lo, E.hi, Q1, Q2, Q3) && tri_intersect(E, Q1, Q2, Q3);
+                n_sat += __popcll(m);
                 if (__ballot(hit)) return true;
             } else {
                 if (sp < kStackDepth) stk[sp] = nd.b;
                 ++sp;
-                node = nd.a;
+                node = __builtin_amdgcn_readfirstlane(nd.a);
                 continue;
             }
         }
@@ -62,25 +79,16 @@ __device__ bool walk_env(const BvhNode *__restrict__ nodes, const EnvTri *__rest
     }
 }
 
-__global__ __launch_bounds__(256) void k_collide(EnvDev env, const AgentDev *__restrict__ links,
-                                                 CollideWork w) {
-    __shared__ int32_t s_stack[4][kStackDepth];
-    const int wave = threadIdx.x >> 6;
-    const int lane = threadIdx.x & 63;
-    const int64_t unit = (int64_t)blockIdx.x * 4 + wave;
-    if (unit >= w.n_units) return;
-
+__device__ void collide_unit(const EnvDev &env, const BvhNode *s_nodes, int32_t n_lds,
+                             const AgentDev *__restrict__ links, const CollideWork &w, int64_t unit, int32_t *stk,
+                             int lane, bool shared_edges, uint32_t &n_clusters, uint32_t &n_nodes,
+                             uint32_t &n_sat, uint32_t &n_units) {
+    int32_t link;
+    int64_t slot, edge;
+    if (!decode_unit(w, unit, link, slot, edge)) return;
     const int32_t L = w.L;
-    const int32_t link = (int32_t)(unit % L);
-    const int64_t slot = unit / L;
-    int64_t edge;
-    if (w.pose_edge) {
-        edge = w.pose_edge[slot];
-    } else {
-        edge = slot / w.pmax;
-        if ((int32_t)(slot % w.pmax) >= w.pcount[edge]) return;
-    }
-    if (load_flag(w.verdict + edge)) return;
+    if (shared_edges && load_flag(w.verdict + edge)) return;
+    ++n_units;
 
     const double *pose = w.poses + (slot * L + link) * 12;
     double R2[9], T2[3], R[9], T[3];
@@ -91,11 +99,9 @@ __global__ __launch_bounds__(256) void k_collide(EnvDev env, const AgentDev *__r
     relative_transform(env.tf, env.tf + 9, R2, T2, R, T);
 
     const AgentDev ag = links[link];
-    const BvhNode root = env.nodes[0];
-    uint32_t n_clusters = 0, n_nodes = 0, n_sat = 0;
-    bool contact = false;
+    const BvhNode root = s_nodes[0];
 
-    for (int32_t cbase = 0; cbase < ag.n_clusters && !contact; cbase += kWave) {
+    for (int32_t cbase = 0; cbase < ag.n_clusters; cbase += kWave) {
         const int32_t ci = cbase + lane;
         bool ok = false;
         if (ci < ag.n_clusters) {
@@ -116,11 +122,8 @@ __global__ __launch_bounds__(256) void k_collide(EnvDev env, const AgentDev *__r
         while (m) {
             const int j = __ffsll((unsigned long long)m) - 1;
             m &= m - 1;
-            if (load_flag(w.verdict + edge)) {
-                m = 0;
-                contact = true;  // another unit of this edge already hit
-                break;
-            }
+            // another unit of this edge may already have found the contact
+            if (shared_edges && load_flag(w.verdict + edge)) return;
             ++n_clusters;
             const Cluster c = ag.clusters[cbase + j];
             const bool act = lane < c.count;
@@ -138,21 +141,55 @@ __global__ __launch_bounds__(256) void k_collide(EnvDev env, const AgentDev *__r
                 bhi[1] = widen_hi(dmax(Q1.y, dmax(Q2.y, Q3.y)));
                 bhi[2] = widen_hi(dmax(Q1.z, dmax(Q2.z, Q3.z)));
             }
-            if (walk_env(env.nodes, env.tris, s_stack[wave], act, Q1, Q2, Q3, blo, bhi, n_nodes,
-                         n_sat)) {
+            if (walk_env(s_nodes, n_lds, env.nodes, env.tris, stk, act, Q1, Q2, Q3, blo, bhi, n_nodes, n_sat)) {
                 if (lane == 0)
-                    __hip_atomic_store(w.verdict + edge, (uint8_t)1, __ATOMIC_RELAXED,
-                                       __HIP_MEMORY_SCOPE_AGENT);
-                contact = true;
-                break;
+                    __hip_atomic_store(w.verdict + edge, (uint8_t)1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                return;
             }
         }
     }
+}
+
+__global__ __launch_bounds__(kCollideWaves * 64) void k_collide(EnvDev env, const AgentDev *__restrict__ links,
+                                                                 CollideWork w) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    // list mode (overflow re-run of the two-phase path): usually empty, leave at once
+    const int64_t n_work = w.unit_list ? (int64_t)*w.unit_list_n : w.n_units;
+    if ((int64_t)blockIdx.x * kCollideWaves >= n_work) return;
+    BvhNode *s_nodes = reinterpret_cast<BvhNode *>(smem);
+    const int32_t n_lds = env.n_nodes < kLdsNodes ? env.n_nodes : kLdsNodes;
+    int32_t *s_stack = reinterpret_cast<int32_t *>(smem + sizeof(BvhNode) * n_lds);
+    // stage the breadth-first prefix of the BVH (16-B pieces, all lanes of the workgroup)
+    {
+        const uint4 *src = reinterpret_cast<const uint4 *>(env.nodes);
+        uint4 *dst = reinterpret_cast<uint4 *>(s_nodes);
+        for (int i = threadIdx.x; i < n_lds * 2; i += blockDim.x) dst[i] = src[i];
+    }
+    __syncthreads();
+
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform for the compiler
+    const int lane = threadIdx.x & 63;
+    int32_t *stk = s_stack + wave * kStackDepth;
+    // several units per edge (links, poses, or host-given pose lists): share early exits
+    const bool shared_edges = w.pose_edge != nullptr || w.L > 1 || w.pmax > 1;
+    uint32_t n_units = 0, n_clusters = 0, n_nodes = 0, n_sat = 0;
+    const int64_t stride = (int64_t)gridDim.x * kCollideWaves;
+    const unsigned long long t0 = w.stats ? __builtin_amdgcn_s_memtime() : 0ull;
+    uint32_t max_nodes = 0;
+    for (int64_t i = (int64_t)blockIdx.x * kCollideWaves + wave; i < n_work; i += stride) {
+        const uint32_t before = n_nodes;
+        const int64_t unit = w.unit_list ? (int64_t)w.unit_list[i] : i;
+        collide_unit(env, s_nodes, n_lds, links, w, unit, stk, lane, shared_edges, n_clusters, n_nodes, n_sat,
+                     n_units);
+        max_nodes = max_nodes > n_nodes - before ? max_nodes : n_nodes - before;
+    }
     if (w.stats && lane == 0) {
-        atomicAdd(w.stats + 0, 1ull);
+        atomicAdd(w.stats + 0, (unsigned long long)n_units);
         atomicAdd(w.stats + 1, (unsigned long long)n_clusters);
         atomicAdd(w.stats + 2, (unsigned long long)n_nodes);
         atomicAdd(w.stats + 3, (unsigned long long)n_sat);
+        atomicMax(w.stats + 4, (unsigned long long)max_nodes);
+        atomicAdd(w.stats + 6, __builtin_amdgcn_s_memtime() - t0);
     }
 }
 
@@ -162,11 +199,21 @@ __global__ void k_pose_edge(const int64_t *__restrict__ off, int64_t E, int32_t 
     for (int64_t p = off[e]; p < off[e + 1]; ++p) pe[p] = (int32_t)e;
 }
 
-void launch_collide(const EnvDev &env, const AgentDev *d_links, const CollideWork &w,
-                    hipStream_t stream) {
+void launch_collide(const EnvDev &env, const AgentDev *d_links, const CollideWork &w, hipStream_t stream) {
     if (w.n_units <= 0 || env.n_tris <= 0) return;
-    const int64_t blocks = (w.n_units + 3) / 4;
-    hipLaunchKernelGGL(k_collide, dim3((unsigned)blocks), dim3(256), 0, stream, env, d_links, w);
+    static int max_blocks = 0;
+    if (max_blocks == 0) {
+        int dev = 0, cus = 256;
+        if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+        int per_cu = 6;  // ~2 workgroups per CU resident (VGPR-limited) x 3 rounds
+        if (const char *s = getenv("MPT_COLLIDE_BLOCKS_PER_CU")) per_cu = atoi(s) > 0 ? atoi(s) : per_cu;
+        max_blocks = cus * per_cu;
+    }
+    const int32_t n_lds = env.n_nodes < kLdsNodes ? env.n_nodes : kLdsNodes;
+    const size_t lds = sizeof(BvhNode) * n_lds + sizeof(int32_t) * kStackDepth * kCollideWaves;
+    int64_t blocks = (w.n_units + kCollideWaves - 1) / kCollideWaves;
+    if (blocks > max_blocks) blocks = max_blocks;
+    hipLaunchKernelGGL(k_collide, dim3((unsigned)blocks), dim3(kCollideWaves * 64), lds, stream, env, d_links, w);
     hip_check(hipGetLastError(), "k_collide launch");
 }
 

@@ -73,7 +73,8 @@ MPT_HD float widen_lo(double x) { return (float)(x - (1e-6 + 4e-7 * fabs(x))); }
 MPT_HD float widen_hi(double x) { return (float)(x + (1e-6 + 4e-7 * fabs(x))); }
 
 // Environment triangle record: everything intersect_Triangle derives from P alone,
-// precomputed on the host with the same operations (so bit-identical), 40 doubles.
+// precomputed on the host with the same operations (so bit-identical), plus the exact
+// vertex box of P that gates the test (see tri_gate), 48 doubles.
 struct EnvTri {
     double P1[3];   // q_i = Q_i' - P1
     double p2[3];   // p2 = P2 - P1 (= e1, since p1 = P1 - P1 = 0)
@@ -84,9 +85,11 @@ struct EnvTri {
     double g[3][3]; // e_i x n1
     double nP[2];   // min/max of {p1,p2,p3}.n1 (p1 term is +-0)
     double gP[3][2];// min/max of {p1,p2,p3}.g_i
-    double pad[5];
+    double lo[3];   // min over P1,P2,P3 (env-local, exact)
+    double hi[3];   // max over P1,P2,P3
+    double pad[7];
 };
-static_assert(sizeof(EnvTri) == 40 * 8, "EnvTri layout");
+static_assert(sizeof(EnvTri) == 48 * 8, "EnvTri layout");
 
 inline void make_env_tri(const double *t, EnvTri &r) {
     const v3 P1 = mk(t[0], t[1], t[2]), P2 = mk(t[3], t[4], t[5]), P3 = mk(t[6], t[7], t[8]);
@@ -110,7 +113,25 @@ inline void make_env_tri(const double *t, EnvTri &r) {
         r.g[i][0] = g[i].x; r.g[i][1] = g[i].y; r.g[i][2] = g[i].z;
         proj(g[i], r.gP[i]);
     }
+    const double *v[3] = {t, t + 3, t + 6};
+    for (int k = 0; k < 3; ++k) {
+        r.lo[k] = dmin(v[0][k], dmin(v[1][k], v[2][k]));
+        r.hi[k] = dmax(v[0][k], dmax(v[1][k], v[2][k]));
+    }
     for (double &x : r.pad) x = 0.0;
+}
+
+// FCL only runs intersect_Triangle on pairs whose leaf bounding volumes overlap
+// (BVHCollisionTraversalNode: BVTesting before leafTesting); the exact closed AABB
+// overlap of P and Q' is that gate here.  It matters for degenerate (collinear / point)
+// triangles, for which intersect_Triangle finds no separating axis against any parallel
+// counterpart however far away.  Every float box test in the kernels is a widened
+// superset of this one, so pruning never changes a verdict.
+MPT_HD bool tri_gate(const double lo[3], const double hi[3], v3 Q1, v3 Q2, v3 Q3) {
+    const double qlo[3] = {dmin(Q1.x, dmin(Q2.x, Q3.x)), dmin(Q1.y, dmin(Q2.y, Q3.y)), dmin(Q1.z, dmin(Q2.z, Q3.z))};
+    const double qhi[3] = {dmax(Q1.x, dmax(Q2.x, Q3.x)), dmax(Q1.y, dmax(Q2.y, Q3.y)), dmax(Q1.z, dmax(Q2.z, Q3.z))};
+    return lo[0] <= qhi[0] && qlo[0] <= hi[0] && lo[1] <= qhi[1] && qlo[1] <= hi[1] && lo[2] <= qhi[2] &&
+           qlo[2] <= hi[2];
 }
 
 // project6 with the P-side interval known: 0 = separated.

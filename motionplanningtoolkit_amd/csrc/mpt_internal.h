@@ -46,13 +46,30 @@ struct AgentDev {
     int32_t n_tris;
 };
 
+// Broad-phase env tree, 64 children per node so one wave tests a node's children with one
+// lane each.  Level 0 = one item per triangle (leaf order, box = the triangle's widened
+// box); level 1 = buckets, the maximal median-split subtrees with <= 64 triangles; each
+// higher level groups <= 64 consecutive items of the level below, up to a top level of
+// <= 64 items (the children of a virtual root).  first/count = children in the level below.
+struct Item {
+    float lo[3];
+    int32_t first;
+    float hi[3];
+    int32_t count;
+};
+static_assert(sizeof(Item) == 32, "Item layout");
+constexpr int kMaxLevels = 8;
+
 struct EnvDev {
     const EnvTri *tris;
     const BvhNode *nodes;
-    double tf[12];     // R1 (row-major) + T1: parseTransform of "Environment Location"
-    double root_lo[3], root_hi[3];
+    const Item *items;    // all levels, level l at [lev_off[l], lev_off[l+1])
+    double tf[12];        // R1 (row-major) + T1: parseTransform of "Environment Location"
+    float root_lo[3], root_hi[3];  // root box (float, widened)
     int32_t n_tris;
     int32_t n_nodes;
+    int32_t n_levels;
+    int32_t lev_off[kMaxLevels + 1];
 };
 
 // Work description for one collide launch.  Units are (pose, link) pairs.
@@ -67,11 +84,45 @@ struct CollideWork {
     int32_t L;
     int64_t n_units;
     uint8_t *verdict;         // [E], 0-initialised by the launcher, set to 1 on contact
-    unsigned long long *stats; // optional [4]: units run, clusters visited, node visits, SAT tests
+    // optional [8]: units run, clusters visited, node visits, SAT tests, max node visits of
+    // one unit, max / sum wave lifetime (s_memtime), broad-phase candidates
+    unsigned long long *stats;
+    // fused kernel only: run just the units listed here (count read on the device)
+    const int32_t *unit_list;
+    const uint32_t *unit_list_n;
 };
 
+// Broad-phase candidate: (unit, agent triangle, env triangle) whose float boxes overlap.
+struct Cand {
+    int32_t unit;
+    int32_t atri;
+    int32_t etri;
+};
+
+// Device scratch of the two-phase collide path: one fixed candidate segment per
+// broad-phase wave (no atomics on the candidate path), a unit work queue and the list
+// of units whose candidates did not fit (re-run by the fused kernel).
+struct CollideScratch {
+    Cand *cand = nullptr;        // [n_waves][seg_cap]
+    uint32_t *seg_count = nullptr;  // [n_waves]
+    uint32_t *ctl = nullptr;     // [0] unit queue, [1] overflow units
+    int32_t *ovf_list = nullptr; // [ovf_cap]
+    int64_t ovf_cap = 0;
+    int32_t n_waves = 0, seg_cap = 0, n_blocks = 0;
+    CollideScratch() = default;
+    CollideScratch(const CollideScratch &) = delete;
+    CollideScratch &operator=(const CollideScratch &) = delete;
+    ~CollideScratch();
+    void ensure(int64_t n_units);  // allocates on first use / growth (not stream-ordered)
+};
+
+// Fused single-kernel path (one wave per unit, BVH walk + SAT at the leaves).
 void launch_collide(const EnvDev &env, const AgentDev *d_links, const CollideWork &w,
                     hipStream_t stream);
+// Two-phase path: k_broad (float box traversal, candidates) -> k_narrow (17-axis SAT per
+// candidate) -> fused kernel over overflowed units.  s.ensure(w.n_units) must have run.
+void launch_collide_split(const EnvDev &env, const AgentDev *d_links, const CollideWork &w, CollideScratch &s,
+                          hipStream_t stream);
 void launch_pose_edge(const int64_t *d_offsets, int64_t E, int32_t *d_pose_edge, hipStream_t stream);
 
 // ---------------- NN ----------------

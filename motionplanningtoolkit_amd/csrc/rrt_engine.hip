@@ -25,6 +25,7 @@
 
 namespace mpt {
 const EnvDev &env_dev(const mpt_env *e);
+int32_t collide_mode();
 const AgentDev &agent_dev(const mpt_agent *a);
 }  // namespace mpt
 
@@ -313,6 +314,7 @@ struct mpt_rrt {
     double ppc = 2.0;
     // optional collision work counters (k_collide atomics): units, clusters, node visits, tri tests
     bool stats_on = false;
+    CollideScratch cscratch;
     unsigned long long *d_cstats = nullptr;
 };
 
@@ -342,6 +344,7 @@ void ensure_round_buffers(mpt_rrt *r, int32_t K) {
         hip_check(hipMalloc(&r->d_bcount, sizeof(int32_t) * ((K + 255) / 256)), "alloc bcount");
         hip_check(hipMalloc(&r->d_verdict, (size_t)K), "alloc verdict");
         r->kcap = K;
+        r->cscratch.ensure((int64_t)K * r->p.pmax * r->p.L);
     }
     // the split count depends on n, so size the NN scratch for the capacity bound
     if (need_scratch > r->scratch_bytes) {
@@ -510,7 +513,11 @@ extern "C" mpt_status mpt_rrt_step(mpt_rrt *r, int32_t K, void *stream_) {
         cw.n_units = (int64_t)K * p.pmax * p.L;
         cw.verdict = r->d_verdict;
         cw.stats = r->stats_on ? r->d_cstats : nullptr;
-        launch_collide(r->env, r->d_links, cw, stream);
+        if (collide_mode() == MPT_COLLIDE_FUSED) {
+            launch_collide(r->env, r->d_links, cw, stream);
+        } else {
+            launch_collide_split(r->env, r->d_links, cw, r->cscratch, stream);
+        }
         mark(5);
         hipLaunchKernelGGL(k_count, dim3(kb), dim3(256), 0, stream, r->d_verdict, K, r->d_bcount);
         hipLaunchKernelGGL(k_append, dim3(kb), dim3(256), 0, stream, r->d_verdict, K, p.d, r->d_ends, r->d_nn,
@@ -582,20 +589,20 @@ extern "C" mpt_status mpt_rrt_info(const mpt_rrt *r, int64_t info[4]) {
     });
 }
 
-extern "C" mpt_status mpt_rrt_collide_stats(mpt_rrt *r, int32_t enable, uint64_t out[4]) {
+extern "C" mpt_status mpt_rrt_collide_stats(mpt_rrt *r, int32_t enable, uint64_t out[8]) {
     return guarded([&] {
         if (!r) throw Error{MPT_ERR_INVALID, "null pointer"};
         hip_check(hipDeviceSynchronize(), "sync");
         if (!r->d_cstats) {
-            hip_check(hipMalloc(&r->d_cstats, sizeof(unsigned long long) * 4), "alloc stats");
-            hip_check(hipMemset(r->d_cstats, 0, sizeof(unsigned long long) * 4), "memset stats");
+            hip_check(hipMalloc(&r->d_cstats, sizeof(unsigned long long) * 8), "alloc stats");
+            hip_check(hipMemset(r->d_cstats, 0, sizeof(unsigned long long) * 8), "memset stats");
         }
         if (out) {
-            unsigned long long h[4];
+            unsigned long long h[8];
             hip_check(hipMemcpy(h, r->d_cstats, sizeof(h), hipMemcpyDeviceToHost), "stats D2H");
-            for (int i = 0; i < 4; ++i) out[i] = h[i];
+            for (int i = 0; i < 8; ++i) out[i] = h[i];
         }
-        hip_check(hipMemset(r->d_cstats, 0, sizeof(unsigned long long) * 4), "memset stats");
+        hip_check(hipMemset(r->d_cstats, 0, sizeof(unsigned long long) * 8), "memset stats");
         r->stats_on = enable != 0;
     });
 }

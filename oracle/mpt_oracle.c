@@ -144,9 +144,23 @@ int orc_tri_intersect_RT(const double P[9], const double Q[9], const double R[9]
 /* ======================================================================
  * Collision: MeshHandler::isInCollision (utilities/meshhandler.hpp:187-243) +
  * fcl_helpers::defaultCollisionFunction (utilities/fcl_helpers.hpp:52-65).
- * Verdict = exists (env tri, agent tri) pair not separated by intersect_Triangle;
- * FCL's broadphase/OBB tests only prune, so the all-pairs loop is the definition.
+ * Verdict = exists (env tri, agent tri) pair whose exact vertex AABBs overlap (closed)
+ * and that intersect_Triangle does not separate.  FCL 0.3.2 only calls
+ * intersect_Triangle on pairs whose leaf bounding volumes overlap
+ * (MeshCollisionTraversalNode::BVTesting before leafTesting); the AABB gate is that
+ * precondition.  Without it, a degenerate (collinear) triangle "intersects" any
+ * parallel one at any distance, since all 17 axes vanish; with it the all-pairs loop
+ * below is the definition and every BVH in this repo only prunes.
  * ====================================================================== */
+
+static int tri_gate(const double *P, const double *Qp) {
+    for (int k = 0; k < 3; ++k) {
+        const double plo = fmin(P[k], fmin(P[3 + k], P[6 + k])), phi = fmax(P[k], fmax(P[3 + k], P[6 + k]));
+        const double qlo = fmin(Qp[k], fmin(Qp[3 + k], Qp[6 + k])), qhi = fmax(Qp[k], fmax(Qp[3 + k], Qp[6 + k]));
+        if (plo > qhi || qlo > phi) return 0;
+    }
+    return 1;
+}
 
 static void unit_RT(const double env_tf[12], const double pose[12], double R[9], double T[3]) {
     orc_relative_transform(env_tf, env_tf + 9, pose, pose + 9, R, T);
@@ -159,7 +173,7 @@ int orc_collide_unit(const double *env_tris, int64_t Te, const double env_tf[12]
     for (int64_t b = 0; b < Ta; ++b) {
         map_tri(R, T, agent_tris + 9 * b, Qp);
         for (int64_t a = 0; a < Te; ++a)
-            if (orc_tri_intersect(env_tris + 9 * a, Qp)) return 1;
+            if (tri_gate(env_tris + 9 * a, Qp) && orc_tri_intersect(env_tris + 9 * a, Qp)) return 1;
     }
     return 0;
 }
@@ -292,9 +306,7 @@ int orc_collide_unit_bvh(const orc_bvh *env, const double env_tf[12],
             if (!box_overlap(qlo, qhi, env->lo + 3 * nd, env->hi + 3 * nd)) continue;
             if (env->cnt[nd]) {
                 for (int64_t i = env->left[nd]; i < env->left[nd] + env->cnt[nd]; ++i) {
-                    double tl[3], th[3];
-                    tri_box(env->tris + 9 * i, tl, th);
-                    if (!box_overlap(qlo, qhi, tl, th)) continue;
+                    if (!tri_gate(env->tris + 9 * i, Qp)) continue;
                     ++tests;
                     if (orc_tri_intersect(env->tris + 9 * i, Qp)) {
                         if (n_tri_tests) *n_tri_tests += tests;

@@ -1,0 +1,11 @@
+#!/bin/bash
+# Collide variants on the bench workload (no CPU leg): per-round kernel times + work stats.
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+mkdir -p $R/gpurun_out
+run() {  # tag env...
+  local tag=$1; shift
+  env "$@" timeout -k 10 240 python3 $R/bench.py --steps 10 --warmup 2 --no-cpu > $R/gpurun_out/diag_$tag.json 2> $R/gpurun_out/diag_$tag.err || exit $?
+}
+run split
+run global MPT_BROAD_GLOBAL=1
+echo ok

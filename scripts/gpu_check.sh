@@ -8,12 +8,14 @@ run() {  # name timeout cmd...
   timeout -k 10 "$t" "$@" > "gpurun_out/$name.log" 2>&1
   local rc=$?
   echo "== $name rc=$rc" | tee -a gpurun_out/steps.log
-  tail -5 "gpurun_out/$name.log"
+  tail -4 "gpurun_out/$name.log"
   return $rc
 }
 run pytest_gpu 800 python -m pytest tests -m gpu -q -p no:cacheprovider -ra; rc=$?
 [ $rc -gt 1 ] && exit $rc
 run smoke 180 python -c "import __graft_entry__ as g; g.smoke()"; rc=$?
 [ $rc -gt 1 ] && exit $rc
-run bench 400 python bench.py --steps 5 --warmup 2 --cpu-seconds 5; rc=$?
+run bench 400 python bench.py --steps 10 --warmup 3 --cpu-seconds 5 ${BENCH_EXTRA}; rc=$?
+[ $rc -gt 1 ] && exit $rc
+[ -n "$BENCH2" ] && { run bench2 400 python bench.py --steps 5 --warmup 2 --no-cpu $BENCH2; rc=$?; }
 exit $rc

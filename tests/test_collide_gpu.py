@@ -12,6 +12,14 @@ pytestmark = pytest.mark.gpu
 I = np.array([1, 0, 0, 0, 1, 0, 0, 0, 1], np.float64)
 
 
+@pytest.fixture(params=["split", "fused"], autouse=True)
+def collide_mode(request, mpt_gpu):
+    """Every case runs through both kernel structures (k_broad + k_narrow, and k_collide)."""
+    mpt_gpu.set_collide_mode(request.param)
+    yield request.param
+    mpt_gpu.set_collide_mode("split")
+
+
 def pose(t, R=I):
     return np.r_[np.asarray(R, np.float64).ravel(), np.asarray(t, np.float64)]
 
@@ -120,6 +128,20 @@ def test_snake_links(mpt_gpu, oracle):
     links = [sc.agent_tris] * sc.links
     got = check(mpt_gpu, oracle, sc.env_tris, sc.env_tf, links, poses, np.arange(E + 1))
     assert 0 < got.sum() < E
+
+
+def test_candidate_overflow(mpt_gpu, oracle, collide_mode):
+    """The blimp against itself: thousands of overlapping triangle boxes per pose, more than
+    one broad-phase segment holds, so the split path hands those poses to the fused kernel."""
+    blimp = scenes.read_obj(scenes.mesh_path("agent_blimp"), "all")
+    rng = np.random.default_rng(9)
+    ps = [pose([0, 0, 0])] + [pose(rng.uniform(-3, 3, 3), random_rot(rng)) for _ in range(5)]
+    ps += [pose([500, 0, 0])]  # far away: safe
+    poses = np.array(ps).reshape(-1, 1, 12)
+    mpt_gpu.set_collide_stats(True)
+    got = check(mpt_gpu, oracle, blimp, pose([0, 0, 0]), [blimp], poses, np.arange(len(ps) + 1))
+    mpt_gpu.set_collide_stats(False)
+    assert got[0] == 1 and got[-1] == 0
 
 
 def test_empty_and_degenerate(mpt_gpu, oracle):

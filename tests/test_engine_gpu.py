@@ -114,6 +114,24 @@ def test_engine_rounds(mpt_gpu, oracle, name, nn_mode):
     tree, _ = check_round(mpt_gpu, oracle, sc, eng, tree, seed, K, K // 2 + 3)
 
 
+@pytest.mark.parametrize("name", ["omni", "blimp", "snake"])
+def test_engine_rounds_fused_collide(mpt_gpu, oracle, name):
+    """The same stage-by-stage parity with the fused collision kernel in the round."""
+    if name == "omni":
+        sc, n0, K = scenes.omni_scenario(), 2000, 800
+    elif name == "blimp":
+        sc, n0, K = scenes.blimp_scenario("all"), 3000, 1200
+    else:
+        sc, n0, K = scenes.snake_scenario("corridor"), 2000, 500
+    mpt_gpu.set_collide_mode("fused")
+    try:
+        eng, tree = make(mpt_gpu, sc, n0, K, 99)
+        eng.set_nn("grid")
+        check_round(mpt_gpu, oracle, sc, eng, tree, 99, 0, K)
+    finally:
+        mpt_gpu.set_collide_mode("split")
+
+
 def test_engine_grid_equals_brute_over_growing_rounds(mpt_gpu, oracle):
     """A growing tree (no reset) over several rounds: the grid and the brute-force NN
     engines must build the same tree bit for bit (rounds build the grid from scratch)."""

@@ -148,6 +148,31 @@ def test_bvh_matches_all_pairs_blimp_room(oracle):
     assert 0 < a.sum() < len(a)
 
 
+def test_degenerate_triangles_are_gated_by_boxes(oracle):
+    """intersect_Triangle finds no separating axis between two parallel collinear
+    (zero-area) triangles however far apart; FCL never asks, because their leaf bounding
+    volumes do not overlap.  The oracle's verdict carries that gate."""
+    seg = np.array([0, 0, 0, 1, 0, 0, 2, 0, 0], np.float64)
+    far = seg + np.tile([0, 50, 0], 3)
+    assert oracle.tri_intersect(seg, far)  # ungated test: "intersects"
+    off = np.array([0, 1, 2])
+    poses = np.array([pose([0, 50, 0]), pose([0.5, 0, 0])]).reshape(2, 1, 12)
+    v = oracle.collide_batch(seg.reshape(1, 9), pose([0, 0, 0]), [seg.reshape(1, 9)], poses, off)
+    assert v.tolist() == [0, 1]
+    b = oracle.collide_batch_bvh(oracle.BVH(seg.reshape(1, 9)), pose([0, 0, 0]), [seg.reshape(1, 9)], poses, off)
+    assert b.tolist() == [0, 1]
+
+
+def test_self_collision_blimp_gated_all_pairs_vs_bvh(oracle):
+    """The blimp (which has zero-area triangles) against itself at far and overlapping poses."""
+    blimp = scenes.read_obj(scenes.mesh_path("agent_blimp"), "all")
+    poses = np.array([pose([0, 0, 0]), pose([500, 0, 0]), pose([0, 30, 0])]).reshape(3, 1, 12)
+    off = np.arange(4)
+    a = oracle.collide_batch(blimp, pose([0, 0, 0]), [blimp], poses, off)
+    b = oracle.collide_batch_bvh(oracle.BVH(blimp), pose([0, 0, 0]), [blimp], poses, off)
+    assert a.tolist() == b.tolist() == [1, 0, 0]
+
+
 def test_edges_with_no_poses_are_safe(oracle, unit_box):
     off = np.array([0, 0, 1, 1])
     v = oracle.collide_batch(unit_box, pose([0, 0, 0]), [unit_box], pose([0, 0, 0]).reshape(1, 1, 12), off)
