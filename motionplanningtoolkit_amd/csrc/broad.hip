@@ -26,26 +26,36 @@ constexpr int kChunk = 4;          // units per queue grab
 constexpr int kSegCap = 1024;      // candidates per wave segment
 constexpr int kLdsItems = 2048;    // whole env tree staged in LDS (64 KiB) when it fits
 
+constexpr int kSpillCap = 1 << 22;  // shared spill list (48 MiB)
+constexpr int kSpillBlocks = 256;   // k_narrow workgroups over the spill list
+
 struct BroadArgs {
     Cand *cand;
     uint32_t *seg_count;
+    Cand *spill;
     uint32_t *ctl;
     int32_t *ovf_list;
     int32_t seg_cap;
     int32_t n_waves;
+    int32_t spill_cap;
 };
 
-// Append the lanes of h (ballot m) as candidates; false if the segment is full.
+// Append the lanes of h (ballot m) as candidates: to the wave's segment, or once that is
+// full to the shared spill list; false if both are full.  Called with all lanes active.
 __device__ __forceinline__ bool emit(bool h, uint64_t m, int32_t unit, int32_t atri, int32_t etri, Cand *seg,
-                                     uint32_t &cnt, uint32_t cap) {
+                                     uint32_t &cnt, uint32_t cap, const BroadArgs &b) {
     const uint32_t n = (uint32_t)__popcll(m);
-    if (cnt + n > cap) return false;
-    if (h) {
-        const uint32_t pos =
-            cnt + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-        seg[pos] = Cand{unit, atri, etri};
+    const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+    if (cnt + n <= cap) {
+        if (h) seg[cnt + rank] = Cand{unit, atri, etri};
+        cnt += n;
+        return true;
     }
-    cnt += n;
+    uint32_t base = 0;
+    if ((threadIdx.x & 63) == 0) base = atomicAdd(b.ctl + 2, n);
+    base = __builtin_amdgcn_readfirstlane(base);
+    if (base + n > (uint32_t)b.spill_cap) return false;
+    if (h) b.spill[base + rank] = Cand{unit, atri, etri};
     return true;
 }
 
@@ -90,8 +100,9 @@ __device__ __forceinline__ float lane_f(float v, int j) {
 // false on segment overflow (the unit is then re-run by the fused kernel)
 template <bool kLds>
 __device__ bool broad_unit(const EnvDev &env, const Item *s_items, const AgentDev *__restrict__ links,
-                           const CollideWork &w, int32_t unit, int lane, Cand *seg, uint32_t &cnt, uint32_t cap,
-                           uint32_t &n_units, uint32_t &n_clusters, uint32_t &n_nodes) {
+                           const CollideWork &w, const BroadArgs &b, int32_t unit, int lane, Cand *seg,
+                           uint32_t &cnt, uint32_t cap, uint32_t &n_units, uint32_t &n_clusters,
+                           uint32_t &n_nodes) {
     int32_t link;
     int64_t slot, edge;
     if (!decode_unit(w, unit, link, slot, edge)) return true;
@@ -145,7 +156,7 @@ __device__ bool broad_unit(const EnvDev &env, const Item *s_items, const AgentDe
                         const float ehi[3] = {lane_f(mine.hi[0], t), lane_f(mine.hi[1], t), lane_f(mine.hi[2], t)};
                         const bool h = act && box_overlap(blo, bhi, elo, ehi);
                         const uint64_t m = __ballot(h);
-                        if (m && !emit(h, m, unit, tfirst + lane, base + t, seg, cnt, cap)) return false;
+                        if (m && !emit(h, m, unit, tfirst + lane, base + t, seg, cnt, cap, b)) return false;
                     }
                 }
                 if (!M) {
@@ -203,7 +214,7 @@ __global__ __launch_bounds__(kBroadWaves * 64) void k_broad(EnvDev env, const Ag
         const int64_t end = base + kChunk < w.n_units ? base + kChunk : w.n_units;
         for (int64_t u = base; u < end; ++u) {
             const uint32_t before = n_nodes;
-            if (!broad_unit<kLds>(env, s_items, links, w, (int32_t)u, lane, seg, cnt, cap, n_units, n_clusters,
+            if (!broad_unit<kLds>(env, s_items, links, w, b, (int32_t)u, lane, seg, cnt, cap, n_units, n_clusters,
                                   n_nodes)) {
                 if (lane == 0) b.ovf_list[atomicAdd(b.ctl + 1, 1u)] = (int32_t)u;
             }
@@ -226,36 +237,48 @@ __global__ __launch_bounds__(kBroadWaves * 64) void k_broad(EnvDev env, const Ag
     }
 }
 
+__device__ __forceinline__ void narrow_one(const EnvDev &env, const AgentDev *__restrict__ links,
+                                           const CollideWork &w, const Cand cd, uint32_t &n_sat) {
+    int32_t link;
+    int64_t slot, edge;
+    decode_unit(w, cd.unit, link, slot, edge);
+    if (load_flag(w.verdict + edge)) return;
+    double R[9], T[3];
+    unit_transform(env, w.poses + (slot * w.L + link) * 12, R, T);
+    const double *t = links[link].tris + (int64_t)cd.atri * 9;
+    const v3 Q1 = xform(R, T, mk(t[0], t[1], t[2]));
+    const v3 Q2 = xform(R, T, mk(t[3], t[4], t[5]));
+    const v3 Q3 = xform(R, T, mk(t[6], t[7], t[8]));
+    const EnvTri &E = env.tris[cd.etri];
+    if (!tri_gate(E.lo, E.hi, Q1, Q2, Q3)) return;
+    ++n_sat;
+    if (tri_intersect(E, Q1, Q2, Q3))
+        __hip_atomic_store(w.verdict + edge, (uint8_t)1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Workgroups [0, n_waves): one broad segment each; the next kSpillBlocks: the spill list.
 __global__ __launch_bounds__(64) void k_narrow(EnvDev env, const AgentDev *__restrict__ links, CollideWork w,
                                                BroadArgs b) {
     const int32_t gw = blockIdx.x;
-    const uint32_t cnt = b.seg_count[gw];
-    const Cand *seg = b.cand + (int64_t)gw * b.seg_cap;
     uint32_t n_sat = 0;
-    for (uint32_t i = threadIdx.x; i < cnt; i += 64) {
-        const Cand cd = seg[i];
-        int32_t link;
-        int64_t slot, edge;
-        decode_unit(w, cd.unit, link, slot, edge);
-        if (load_flag(w.verdict + edge)) continue;
-        double R[9], T[3];
-        unit_transform(env, w.poses + (slot * w.L + link) * 12, R, T);
-        const double *t = links[link].tris + (int64_t)cd.atri * 9;
-        const v3 Q1 = xform(R, T, mk(t[0], t[1], t[2]));
-        const v3 Q2 = xform(R, T, mk(t[3], t[4], t[5]));
-        const v3 Q3 = xform(R, T, mk(t[6], t[7], t[8]));
-        const EnvTri &E = env.tris[cd.etri];
-        if (!tri_gate(E.lo, E.hi, Q1, Q2, Q3)) continue;
-        ++n_sat;
-        if (tri_intersect(E, Q1, Q2, Q3))
-            __hip_atomic_store(w.verdict + edge, (uint8_t)1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (gw < b.n_waves) {
+        const uint32_t cnt = b.seg_count[gw];
+        const Cand *seg = b.cand + (int64_t)gw * b.seg_cap;
+        for (uint32_t i = threadIdx.x; i < cnt; i += 64) narrow_one(env, links, w, seg[i], n_sat);
+    } else {
+        const uint32_t n = b.ctl[2] < (uint32_t)b.spill_cap ? b.ctl[2] : (uint32_t)b.spill_cap;
+        for (uint32_t i = (uint32_t)(gw - b.n_waves) * 64 + threadIdx.x; i < n; i += kSpillBlocks * 64)
+            narrow_one(env, links, w, b.spill[i], n_sat);
     }
     if (w.stats && n_sat) atomicAdd(w.stats + 3, (unsigned long long)n_sat);
-    if (w.stats && gw == 0 && threadIdx.x == 0) atomicAdd(w.stats + 5, (unsigned long long)b.ctl[1]);
+    if (w.stats && gw == 0 && threadIdx.x == 0) {
+        atomicAdd(w.stats + 5, (unsigned long long)b.ctl[1]);
+        atomicAdd(w.stats + 7, (unsigned long long)b.ctl[2]);
+    }
 }
 
 CollideScratch::~CollideScratch() {
-    void *ps[] = {cand, seg_count, ctl, ovf_list};
+    void *ps[] = {cand, seg_count, spill, ctl, ovf_list};
     for (void *p : ps)
         if (p) (void)hipFree(p);
 }
@@ -269,6 +292,8 @@ void CollideScratch::ensure(int64_t n_units) {
         seg_cap = kSegCap;
         hip_check(hipMalloc(&cand, sizeof(Cand) * (size_t)n_waves * seg_cap), "alloc candidates");
         hip_check(hipMalloc(&seg_count, sizeof(uint32_t) * n_waves), "alloc seg counts");
+        spill_cap = kSpillCap;
+        hip_check(hipMalloc(&spill, sizeof(Cand) * (size_t)spill_cap), "alloc spill");
         hip_check(hipMalloc(&ctl, sizeof(uint32_t) * 4), "alloc collide ctl");
     }
     if (n_units > ovf_cap) {
@@ -284,7 +309,7 @@ void launch_collide_split(const EnvDev &env, const AgentDev *d_links, const Coll
     if (w.n_units <= 0 || env.n_tris <= 0) return;
     if (w.n_units >= (int64_t(1) << 31) || w.n_units > s.ovf_cap || !s.cand)
         throw Error{5, "collide scratch not sized for this launch"};
-    BroadArgs b{s.cand, s.seg_count, s.ctl, s.ovf_list, s.seg_cap, s.n_waves};
+    BroadArgs b{s.cand, s.seg_count, s.spill, s.ctl, s.ovf_list, s.seg_cap, s.n_waves, s.spill_cap};
     hip_check(hipMemsetAsync(s.ctl, 0, sizeof(uint32_t) * 4, stream), "collide ctl memset");
     const int32_t n_items = env.lev_off[env.n_levels];
     static const bool force_global = getenv("MPT_BROAD_GLOBAL") != nullptr;  // experiment knob
@@ -295,14 +320,16 @@ void launch_collide_split(const EnvDev &env, const AgentDev *d_links, const Coll
         hipLaunchKernelGGL(k_broad<false>, dim3((unsigned)s.n_blocks), dim3(kBroadWaves * 64), 0, stream, env,
                            d_links, w, b);
     hip_check(hipGetLastError(), "k_broad launch");
-    hipLaunchKernelGGL(k_narrow, dim3((unsigned)s.n_waves), dim3(64), 0, stream, env, d_links, w, b);
+    hipLaunchKernelGGL(k_narrow, dim3((unsigned)(s.n_waves + kSpillBlocks)), dim3(64), 0, stream, env, d_links, w,
+                       b);
     hip_check(hipGetLastError(), "k_narrow launch");
-    // units whose candidates overflowed their segment: fused path, list read on the device
+    // units whose candidates overflowed segment and spill list (none in practice): fused
+    // path, list read on the device, a small grid so the usual empty launch costs little
     CollideWork f = w;
     f.unit_list = s.ovf_list;
     f.unit_list_n = s.ctl + 1;
     f.stats = nullptr;
-    launch_collide(env, d_links, f, stream);
+    launch_collide(env, d_links, f, stream, 64);
 }
 
 }  // namespace mpt

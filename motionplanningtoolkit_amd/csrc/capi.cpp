@@ -714,7 +714,8 @@ static void nn_query(mpt_nn *nn, const double *d_q, int64_t nq, int32_t k, int32
     }
     GridDev G = nn->grid->dev();
     G.removed = nn->d_removed;
-    launch_grid_knn(G, nn->d, d_q, nq, k, d_ids, d_d2, stream);
+    const int32_t *ord = nq >= kSortQueries ? nn->grid->order_queries(d_q, nq, nn->d, stream) : nullptr;
+    launch_grid_knn(G, nn->d, d_q, nq, k, d_ids, d_d2, stream, ord);
 }
 
 extern "C" mpt_status mpt_nn_set_index(mpt_nn *nn, int32_t mode) {

@@ -199,7 +199,8 @@ __global__ void k_pose_edge(const int64_t *__restrict__ off, int64_t E, int32_t 
     for (int64_t p = off[e]; p < off[e + 1]; ++p) pe[p] = (int32_t)e;
 }
 
-void launch_collide(const EnvDev &env, const AgentDev *d_links, const CollideWork &w, hipStream_t stream) {
+void launch_collide(const EnvDev &env, const AgentDev *d_links, const CollideWork &w, hipStream_t stream,
+                    int cap_blocks) {
     if (w.n_units <= 0 || env.n_tris <= 0) return;
     static int max_blocks = 0;
     if (max_blocks == 0) {
@@ -213,6 +214,7 @@ void launch_collide(const EnvDev &env, const AgentDev *d_links, const CollideWor
     const size_t lds = sizeof(BvhNode) * n_lds + sizeof(int32_t) * kStackDepth * kCollideWaves;
     int64_t blocks = (w.n_units + kCollideWaves - 1) / kCollideWaves;
     if (blocks > max_blocks) blocks = max_blocks;
+    if (cap_blocks > 0 && blocks > cap_blocks) blocks = cap_blocks;
     hipLaunchKernelGGL(k_collide, dim3((unsigned)blocks), dim3(kCollideWaves * 64), lds, stream, env, d_links, w);
     hip_check(hipGetLastError(), "k_collide launch");
 }

@@ -55,6 +55,16 @@ __global__ void k_grid_scatter(const double *__restrict__ pts, int32_t d, int64_
     sids[pos] = (int32_t)(i + 1);
 }
 
+__global__ void k_query_cells(GridParams g, const double *__restrict__ q, int32_t d, int64_t nq,
+                              uint32_t *__restrict__ key, int32_t *__restrict__ idx) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= nq) return;
+    int c[3] = {0, 0, 0};
+    for (int j = 0; j < g.gd; ++j) c[j] = cell_coord(q[i * d + g.dims[j]], g.lo[j], g.inv_h, g.n[j]);
+    key[i] = (uint32_t)((c[0] * g.n[1] + c[1]) * g.n[2] + c[2]);
+    idx[i] = (int32_t)i;
+}
+
 template <int KMAX>
 __device__ __forceinline__ void grid_push(double (&bd)[KMAX], int32_t (&bi)[KMAX], int32_t k, double dd, int32_t id) {
     bool done = false;
@@ -99,10 +109,12 @@ __device__ __forceinline__ double ring_bound(const GridParams &g, const double *
 
 template <int D, int KMAX>
 __global__ __launch_bounds__(256) void k_grid_knn(GridDev G, int32_t d, const double *__restrict__ q, int64_t nq,
-                                                  int32_t k, int32_t *__restrict__ out_ids, double *__restrict__ out_d2) {
+                                                  int32_t k, int32_t *__restrict__ out_ids, double *__restrict__ out_d2,
+                                                  const int32_t *__restrict__ order) {
     constexpr int DD = D > 0 ? D : 16;
-    const int64_t qi = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (qi >= nq) return;
+    const int64_t ti = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (ti >= nq) return;
+    const int64_t qi = order ? (int64_t)order[ti] : ti;
     const GridParams &g = G.g;
     const int dim = D > 0 ? D : d;
     double qq[DD];
@@ -241,7 +253,7 @@ void GridIndex::reserve(int64_t cap_pts, int32_t d, int64_t ncells) {
 }
 
 GridIndex::~GridIndex() {
-    void *ps[] = {spts, sids, cell_of, counts, cell_start, temp};
+    void *ps[] = {spts, sids, cell_of, counts, cell_start, temp, qkey, qkey_sorted, qidx, qorder, qtemp};
     for (void *p : ps)
         if (p) (void)hipFree(p);
 }
@@ -328,26 +340,59 @@ int32_t choose_grid_dims(int32_t d, const double *lohi, int32_t dims[3]) {
 
 template <int D>
 static void grid_knn_d(const GridDev &G, int32_t d, const double *q, int64_t nq, int32_t k, int32_t *ids, double *d2,
-                       hipStream_t stream) {
+                       hipStream_t stream, const int32_t *order) {
     const dim3 grid((unsigned)((nq + 255) / 256));
     if (k == 1)
-        hipLaunchKernelGGL((k_grid_knn<D, 1>), grid, dim3(256), 0, stream, G, d, q, nq, k, ids, d2);
+        hipLaunchKernelGGL((k_grid_knn<D, 1>), grid, dim3(256), 0, stream, G, d, q, nq, k, ids, d2, order);
     else if (k <= 16)
-        hipLaunchKernelGGL((k_grid_knn<D, 16>), grid, dim3(256), 0, stream, G, d, q, nq, k, ids, d2);
+        hipLaunchKernelGGL((k_grid_knn<D, 16>), grid, dim3(256), 0, stream, G, d, q, nq, k, ids, d2, order);
     else
-        hipLaunchKernelGGL((k_grid_knn<D, 32>), grid, dim3(256), 0, stream, G, d, q, nq, k, ids, d2);
+        hipLaunchKernelGGL((k_grid_knn<D, 32>), grid, dim3(256), 0, stream, G, d, q, nq, k, ids, d2, order);
 }
 
 void launch_grid_knn(const GridDev &G, int32_t d, const double *q, int64_t nq, int32_t k, int32_t *ids, double *d2,
-                     hipStream_t stream) {
+                     hipStream_t stream, const int32_t *order) {
     if (nq <= 0) return;
     switch (d) {
-        case 3: grid_knn_d<3>(G, d, q, nq, k, ids, d2, stream); break;
-        case 7: grid_knn_d<7>(G, d, q, nq, k, ids, d2, stream); break;
-        case 15: grid_knn_d<15>(G, d, q, nq, k, ids, d2, stream); break;
-        default: grid_knn_d<0>(G, d, q, nq, k, ids, d2, stream); break;
+        case 3: grid_knn_d<3>(G, d, q, nq, k, ids, d2, stream, order); break;
+        case 7: grid_knn_d<7>(G, d, q, nq, k, ids, d2, stream, order); break;
+        case 15: grid_knn_d<15>(G, d, q, nq, k, ids, d2, stream, order); break;
+        default: grid_knn_d<0>(G, d, q, nq, k, ids, d2, stream, order); break;
     }
     hip_check(hipGetLastError(), "k_grid_knn launch");
+}
+
+const int32_t *GridIndex::order_queries(const double *q, int64_t nq, int32_t d, hipStream_t stream) {
+    if (nq <= 0) return nullptr;
+    if (nq >= (int64_t(1) << 31)) throw Error{5, "too many queries"};
+    if (nq > q_cap) {
+        void *ps[] = {qkey, qkey_sorted, qidx, qorder};
+        for (void *p : ps)
+            if (p) hip_check(hipFree(p), "free");
+        hip_check(hipMalloc(&qkey, sizeof(uint32_t) * nq), "qkey");
+        hip_check(hipMalloc(&qkey_sorted, sizeof(uint32_t) * nq), "qkey sorted");
+        hip_check(hipMalloc(&qidx, sizeof(int32_t) * nq), "qidx");
+        hip_check(hipMalloc(&qorder, sizeof(int32_t) * nq), "qorder");
+        q_cap = nq;
+    }
+    int end_bit = 1;
+    while (end_bit < 32 && (int64_t(1) << end_bit) < g.ncells) ++end_bit;
+    size_t tb = 0;
+    hip_check(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, qkey, qkey_sorted, qidx, qorder, (int)nq, 0, end_bit,
+                                                 stream),
+              "sort size");
+    if (tb > qtemp_bytes) {
+        if (qtemp) hip_check(hipFree(qtemp), "free");
+        hip_check(hipMalloc(&qtemp, tb), "sort temp");
+        qtemp_bytes = tb;
+    }
+    hipLaunchKernelGGL(k_query_cells, dim3((unsigned)((nq + 255) / 256)), dim3(256), 0, stream, g, q, d, nq, qkey,
+                       qidx);
+    hip_check(hipGetLastError(), "k_query_cells");
+    hip_check(hipcub::DeviceRadixSort::SortPairs(qtemp, tb, qkey, qkey_sorted, qidx, qorder, (int)nq, 0, end_bit,
+                                                 stream),
+              "sort");
+    return qorder;
 }
 
 }  // namespace mpt

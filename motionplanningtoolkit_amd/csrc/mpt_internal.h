@@ -105,10 +105,11 @@ struct Cand {
 struct CollideScratch {
     Cand *cand = nullptr;        // [n_waves][seg_cap]
     uint32_t *seg_count = nullptr;  // [n_waves]
-    uint32_t *ctl = nullptr;     // [0] unit queue, [1] overflow units
+    Cand *spill = nullptr;       // [spill_cap] shared overflow of full segments (atomic)
+    uint32_t *ctl = nullptr;     // [0] unit queue, [1] overflow units, [2] spill count
     int32_t *ovf_list = nullptr; // [ovf_cap]
     int64_t ovf_cap = 0;
-    int32_t n_waves = 0, seg_cap = 0, n_blocks = 0;
+    int32_t n_waves = 0, seg_cap = 0, n_blocks = 0, spill_cap = 0;
     CollideScratch() = default;
     CollideScratch(const CollideScratch &) = delete;
     CollideScratch &operator=(const CollideScratch &) = delete;
@@ -117,8 +118,9 @@ struct CollideScratch {
 };
 
 // Fused single-kernel path (one wave per unit, BVH walk + SAT at the leaves).
+// max_blocks > 0 caps the grid (list mode re-runs, usually empty).
 void launch_collide(const EnvDev &env, const AgentDev *d_links, const CollideWork &w,
-                    hipStream_t stream);
+                    hipStream_t stream, int max_blocks = 0);
 // Two-phase path: k_broad (float box traversal, candidates) -> k_narrow (17-axis SAT per
 // candidate) -> fused kernel over overflowed units.  s.ensure(w.n_units) must have run.
 void launch_collide_split(const EnvDev &env, const AgentDev *d_links, const CollideWork &w, CollideScratch &s,

@@ -265,9 +265,18 @@ __global__ __launch_bounds__(256) void k_append(const uint8_t *__restrict__ verd
 
 __global__ void k_commit(const int32_t *__restrict__ bcount, int32_t nblocks, int32_t K, int64_t *__restrict__ n_dev,
                          int64_t cap, unsigned long long *__restrict__ counters) {
-    if (threadIdx.x != 0 || blockIdx.x != 0) return;
-    int64_t tot = 0;
-    for (int b = 0; b < nblocks; ++b) tot += bcount[b];
+    // one workgroup of 256: block sum of the per-block valid counts, then thread 0 commits
+    __shared__ int64_t s_red[256];
+    int64_t acc = 0;
+    for (int b = threadIdx.x; b < nblocks; b += 256) acc += bcount[b];
+    s_red[threadIdx.x] = acc;
+    __syncthreads();
+    for (int st = 128; st > 0; st >>= 1) {
+        if ((int)threadIdx.x < st) s_red[threadIdx.x] += s_red[threadIdx.x + st];
+        __syncthreads();
+    }
+    if (threadIdx.x != 0) return;
+    const int64_t tot = s_red[0];
     const int64_t n = *n_dev;
     const int64_t room = cap - n > 0 ? cap - n : 0;
     const int64_t add = tot < room ? tot : room;
@@ -486,7 +495,9 @@ extern "C" mpt_status mpt_rrt_step(mpt_rrt *r, int32_t K, void *stream_) {
         }
         mark(2);
         if (use_grid) {
-            launch_grid_knn(r->grid->dev(), p.d, r->d_samples, K, 1, r->d_nn, r->d_nnd2, stream);
+            // large rounds: answer the samples in cell order (coherent cell walks per wave)
+            const int32_t *ord = K >= kSortQueries ? r->grid->order_queries(r->d_samples, K, p.d, stream) : nullptr;
+            launch_grid_knn(r->grid->dev(), p.d, r->d_samples, K, 1, r->d_nn, r->d_nnd2, stream, ord);
         } else {
             NNWork w{};
             w.pts = r->d_nodes;
@@ -522,7 +533,7 @@ extern "C" mpt_status mpt_rrt_step(mpt_rrt *r, int32_t K, void *stream_) {
         hipLaunchKernelGGL(k_count, dim3(kb), dim3(256), 0, stream, r->d_verdict, K, r->d_bcount);
         hipLaunchKernelGGL(k_append, dim3(kb), dim3(256), 0, stream, r->d_verdict, K, p.d, r->d_ends, r->d_nn,
                            r->d_bcount, r->d_n, r->cap, r->d_nodes, r->d_parents);
-        hipLaunchKernelGGL(k_commit, dim3(1), dim3(64), 0, stream, r->d_bcount, (int32_t)kb, K, r->d_n, r->cap,
+        hipLaunchKernelGGL(k_commit, dim3(1), dim3(256), 0, stream, r->d_bcount, (int32_t)kb, K, r->d_n, r->cap,
                            r->d_counters);
         hip_check(hipGetLastError(), "append");
         mark(6);
