@@ -338,11 +338,97 @@ int32_t choose_grid_dims(int32_t d, const double *lohi, int32_t dims[3]) {
     return gd;
 }
 
+// 1-NN with kGroup lanes per query: the lanes of a group split the cells of each ring (the
+// (2r+1)^gd block, interior cells skipped), keep a private best, and merge it with
+// (d2, id) order by xor-shuffles before the ring bound test, which is group-uniform.
+// Sixteen times more waves than k_grid_knn, so the dependent cell_start -> point loads
+// are hidden by occupancy instead of exposed one query per lane.
+constexpr int kGroup = 16;
+
+template <int D>
+__global__ __launch_bounds__(256) void k_grid_nn1_group(GridDev G, int32_t d, const double *__restrict__ q,
+                                                        int64_t nq, int32_t *__restrict__ out_ids,
+                                                        double *__restrict__ out_d2,
+                                                        const int32_t *__restrict__ order) {
+    constexpr int DD = D > 0 ? D : 16;
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t slot = t / kGroup;
+    const int sub = (int)(t % kGroup);
+    if (slot >= nq) return;  // whole groups leave together (nq is per group)
+    const int64_t qi = order ? (int64_t)order[slot] : slot;
+    const GridParams &g = G.g;
+    const int dim = D > 0 ? D : d;
+    double qq[DD];
+#pragma unroll
+    for (int i = 0; i < DD; ++i) qq[i] = i < dim ? q[qi * dim + i] : 0.0;
+    double qg[3] = {0, 0, 0};
+    int cq[3] = {0, 0, 0};
+    for (int j = 0; j < g.gd; ++j) {
+        const double x = q[qi * dim + g.dims[j]];
+        qg[j] = x;
+        cq[j] = cell_coord(x, g.lo[j], g.inv_h, g.n[j]);
+    }
+    double bd = __builtin_huge_val();
+    int32_t bi = -1;
+    for (int r = 0;; ++r) {
+        const int side = 2 * r + 1;
+        const int cube = g.gd == 3 ? side * side * side : (g.gd == 2 ? side * side : side);
+        for (int c = sub; c < cube; c += kGroup) {
+            int o[3] = {0, 0, 0}, rest = c;
+            for (int j = g.gd - 1; j >= 0; --j) {
+                o[j] = rest % side - r;
+                rest /= side;
+            }
+            const int cheb = max(abs(o[0]), max(abs(o[1]), abs(o[2])));
+            if (cheb != r) continue;  // interior: visited in an earlier ring
+            int cc[3];
+            bool inside = true;
+            for (int j = 0; j < 3; ++j) {
+                cc[j] = cq[j] + o[j];
+                inside = inside && cc[j] >= 0 && cc[j] < g.n[j];
+            }
+            if (!inside) continue;
+            const int32_t cell = (cc[0] * g.n[1] + cc[1]) * g.n[2] + cc[2];
+            const int32_t s = G.cell_start[cell], e = G.cell_start[cell + 1];
+            for (int32_t p = s; p < e; ++p) {
+                const double dd = D > 0 ? flann_l2<DD>(qq, G.pts + (int64_t)p * DD)
+                                        : flann_l2_dyn(qq, G.pts + (int64_t)p * dim, dim);
+                const int32_t id = G.ids[p];
+                if (G.removed && G.removed[id - 1]) continue;
+                if (nn_better(dd, id, bd, bi)) {
+                    bd = dd;
+                    bi = id;
+                }
+            }
+        }
+#pragma unroll
+        for (int off = kGroup / 2; off > 0; off >>= 1) {
+            const double od = __shfl_xor(bd, off, kGroup);
+            const int32_t oi = __shfl_xor(bi, off, kGroup);
+            if (nn_better(od, oi, bd, bi)) {
+                bd = od;
+                bi = oi;
+            }
+        }
+        const double lb = ring_bound(g, qg, cq, r);
+        if (lb < 0.0) break;  // every cell visited
+        if (lb * lb > bd) break;
+    }
+    if (sub == 0) {
+        out_ids[qi] = bi;
+        out_d2[qi] = bd;
+    }
+}
+
 template <int D>
 static void grid_knn_d(const GridDev &G, int32_t d, const double *q, int64_t nq, int32_t k, int32_t *ids, double *d2,
                        hipStream_t stream, const int32_t *order) {
     const dim3 grid((unsigned)((nq + 255) / 256));
-    if (k == 1)
+    static const bool per_lane = getenv("MPT_NN1_PER_LANE") != nullptr;  // experiment knob
+    if (k == 1 && !per_lane)
+        hipLaunchKernelGGL((k_grid_nn1_group<D>), dim3((unsigned)((nq * kGroup + 255) / 256)), dim3(256), 0, stream,
+                           G, d, q, nq, ids, d2, order);
+    else if (k == 1)
         hipLaunchKernelGGL((k_grid_knn<D, 1>), grid, dim3(256), 0, stream, G, d, q, nq, k, ids, d2, order);
     else if (k <= 16)
         hipLaunchKernelGGL((k_grid_knn<D, 16>), grid, dim3(256), 0, stream, G, d, q, nq, k, ids, d2, order);

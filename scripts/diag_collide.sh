@@ -1,5 +1,5 @@
 #!/bin/bash
-# Collide variants on the bench workload (no CPU leg): per-round kernel times + work stats.
+# Bench variants (no CPU leg): per-round kernel times + collide work stats.
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 mkdir -p $R/gpurun_out
 run() {  # tag env...
@@ -7,5 +7,5 @@ run() {  # tag env...
   env "$@" timeout -k 10 240 python3 $R/bench.py --steps 10 --warmup 2 --no-cpu > $R/gpurun_out/diag_$tag.json 2> $R/gpurun_out/diag_$tag.err || exit $?
 }
 run split
-run global MPT_BROAD_GLOBAL=1
+run perlane MPT_NN1_PER_LANE=1
 echo ok
