@@ -22,7 +22,7 @@
 namespace mpt {
 
 constexpr int kBroadWaves = 8;     // waves per workgroup
-constexpr int kChunk = 4;          // units per queue grab
+constexpr int kChunk = 4;          // units per queue grab (one pre-pass lane each)
 constexpr int kSegCap = 1024;      // candidates per wave segment
 constexpr int kLdsItems = 2048;    // whole env tree staged in LDS (64 KiB) when it fits
 
@@ -93,38 +93,115 @@ __device__ __forceinline__ void item_range(const Item *s_items, const Item *__re
     }
 }
 
+// One item, wave-uniform index (LDS broadcast read, or the scalar cache).
+template <bool kLds>
+__device__ __forceinline__ Item load_item_u(const Item *s_items, const Item *__restrict__ items, int32_t idx) {
+    if (kLds) return s_items[idx];
+#if defined(__HIP_DEVICE_COMPILE__)
+    typedef __attribute__((address_space(4))) const Item *cptr;
+    const Item *g = items;
+    return ((cptr)g)[idx];
+#else
+    return items[idx];
+#endif
+}
+
 __device__ __forceinline__ float lane_f(float v, int j) {
     return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), j));
 }
 
-// false on segment overflow (the unit is then re-run by the fused kernel)
+__device__ __forceinline__ float wave_min(float v) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v = fminf(v, __shfl_xor(v, off));
+    return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v)));
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v = fmaxf(v, __shfl_xor(v, off));
+    return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v)));
+}
+
+// One unit whose whole-link box passed the root cull; R, T wave-uniform.  False on
+// candidate overflow (the unit is then re-run by the fused kernel).
 template <bool kLds>
-__device__ bool broad_unit(const EnvDev &env, const Item *s_items, const AgentDev *__restrict__ links,
-                           const CollideWork &w, const BroadArgs &b, int32_t unit, int lane, Cand *seg,
-                           uint32_t &cnt, uint32_t cap, uint32_t &n_units, uint32_t &n_clusters,
-                           uint32_t &n_nodes) {
-    int32_t link;
-    int64_t slot, edge;
-    if (!decode_unit(w, unit, link, slot, edge)) return true;
-    ++n_units;
-    double R[9], T[3];
-    unit_transform(env, w.poses + (slot * w.L + link) * 12, R, T);
-#pragma unroll
-    for (int i = 0; i < 9; ++i) R[i] = uniform_d(R[i]);
-#pragma unroll
-    for (int i = 0; i < 3; ++i) T[i] = uniform_d(T[i]);
-    const AgentDev ag = links[link];
+__device__ bool broad_unit(const EnvDev &env, const Item *s_items, const AgentDev &ag, const double R[9],
+                           const double T[3], const BroadArgs &b, int32_t unit, int lane, Cand *seg,
+                           uint32_t &cnt, uint32_t cap, uint32_t &n_clusters, uint32_t &n_nodes,
+                           uint32_t &n_pairs, uint32_t &n_xf) {
     const int32_t top = env.n_levels - 1;
     const int32_t top_off = env.lev_off[top];
     const int32_t n_top = env.lev_off[top + 1] - top_off;
     for (int32_t cbase = 0; cbase < ag.n_clusters; cbase += kWave) {
         float clo[3] = {0, 0, 0}, chi[3] = {0, 0, 0};
         bool ok = false;
+        int32_t cf = 0, cc = 0;
         if (cbase + lane < ag.n_clusters) {
-            cluster_box(ag.clusters[cbase + lane], R, T, clo, chi);
+            const Cluster &c = ag.clusters[cbase + lane];
+            local_box(c.c, c.e, R, T, clo, chi);
             ok = box_overlap(clo, chi, env.root_lo, env.root_hi);
+            cf = c.first;
+            cc = c.count;
         }
         uint64_t cm = __ballot(ok);
+        if (!cm) continue;
+        if (top == 1) {
+            // Two-level tree (top items = buckets of triangles): lanes = clusters test every
+            // bucket box in one pass (lane keeps a bucket bitmask), then cluster by cluster
+            // the overlapping buckets' triangles, lanes = triangles.
+            uint64_t bm = 0;
+            for (int32_t i = 0; i < n_top; ++i) {
+                const Item t = load_item_u<kLds>(s_items, env.items, top_off + i);
+                bm |= (uint64_t)(ok && box_overlap(clo, chi, t.lo, t.hi)) << i;
+            }
+            n_nodes += (uint32_t)n_top;
+            uint64_t cm2 = __ballot(bm != 0);
+            while (cm2) {
+                const int j = __ffsll((unsigned long long)cm2) - 1;
+                cm2 &= cm2 - 1;
+                ++n_clusters;
+                uint64_t B = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int32_t)(uint32_t)(bm >> 32), j) << 32) |
+                             (uint32_t)__builtin_amdgcn_readlane((int32_t)(uint32_t)bm, j);
+                const float qlo[3] = {lane_f(clo[0], j), lane_f(clo[1], j), lane_f(clo[2], j)};
+                const float qhi[3] = {lane_f(chi[0], j), lane_f(chi[1], j), lane_f(chi[2], j)};
+                const int32_t tfirst = __builtin_amdgcn_readlane(cf, j);
+                const int32_t tcount = __builtin_amdgcn_readlane(cc, j);
+                const bool act = lane < tcount;
+                bool have = false;
+                float blo[3] = {0, 0, 0}, bhi[3] = {0, 0, 0}, tlo[3] = {0, 0, 0}, thi[3] = {0, 0, 0};
+                while (B) {
+                    const int i = __ffsll((unsigned long long)B) - 1;
+                    B &= B - 1;
+                    int32_t first, count;
+                    item_range<kLds>(s_items, env.items, top_off + i, first, count);
+                    Item mine{};
+                    uint64_t M = visit<kLds>(s_items, env.items, first, count, qlo, qhi, lane, mine);
+                    ++n_nodes;
+                    if (!M) continue;
+                    if (!have) {
+                        if (act) agent_tri_box(ag.tris + (int64_t)(tfirst + lane) * 9, R, T, blo, bhi);
+                        have = true;
+                        ++n_xf;
+#pragma unroll
+                        for (int k = 0; k < 3; ++k) {
+                            tlo[k] = wave_min(act ? blo[k] : __builtin_huge_valf());
+                            thi[k] = wave_max(act ? bhi[k] : -__builtin_huge_valf());
+                        }
+                    }
+                    M &= __ballot(box_overlap(tlo, thi, mine.lo, mine.hi));
+                    n_pairs += (uint32_t)__popcll(M);
+                    while (M) {
+                        const int t = __ffsll((unsigned long long)M) - 1;
+                        M &= M - 1;
+                        const float elo[3] = {lane_f(mine.lo[0], t), lane_f(mine.lo[1], t), lane_f(mine.lo[2], t)};
+                        const float ehi[3] = {lane_f(mine.hi[0], t), lane_f(mine.hi[1], t), lane_f(mine.hi[2], t)};
+                        const bool h = act && box_overlap(blo, bhi, elo, ehi);
+                        const uint64_t m = __ballot(h);
+                        if (m && !emit(h, m, unit, tfirst + lane, first + t, seg, cnt, cap, b)) return false;
+                    }
+                }
+            }
+            continue;
+        }
         while (cm) {
             const int j = __ffsll((unsigned long long)cm) - 1;
             cm &= cm - 1;
@@ -136,6 +213,7 @@ __device__ bool broad_unit(const EnvDev &env, const Item *s_items, const AgentDe
             const bool act = lane < tcount;
             bool have = false;  // agent triangle boxes of this cluster computed
             float blo[3] = {0, 0, 0}, bhi[3] = {0, 0, 0};
+            float tlo[3] = {0, 0, 0}, thi[3] = {0, 0, 0};  // their union (tighter than the cluster box)
 
             Item mine{};
             int32_t lv = top, base = top_off;
@@ -148,7 +226,17 @@ __device__ bool broad_unit(const EnvDev &env, const Item *s_items, const AgentDe
                     if (M && !have) {
                         if (act) agent_tri_box(ag.tris + (int64_t)(tfirst + lane) * 9, R, T, blo, bhi);
                         have = true;
+                        ++n_xf;
+#pragma unroll
+                        for (int k = 0; k < 3; ++k) {
+                            tlo[k] = wave_min(act ? blo[k] : __builtin_huge_valf());
+                            thi[k] = wave_max(act ? bhi[k] : -__builtin_huge_valf());
+                        }
                     }
+                    // lanes of the last visit hold these triangles' boxes: drop those that miss
+                    // the union of the agent triangle boxes
+                    if (M) M &= __ballot(box_overlap(tlo, thi, mine.lo, mine.hi));
+                    n_pairs += (uint32_t)__popcll(M);
                     while (M) {
                         const int t = __ffsll((unsigned long long)M) - 1;
                         M &= M - 1;
@@ -201,25 +289,57 @@ __global__ __launch_bounds__(kBroadWaves * 64) void k_broad(EnvDev env, const Ag
         for (int i = threadIdx.x; i < n * 2; i += blockDim.x) dst[i] = src[i];
         __syncthreads();
     }
+    __shared__ double s_rt[kBroadWaves][kChunk][12];  // R, T of the chunk's surviving units
+    __shared__ int32_t s_link[kBroadWaves][kChunk];
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform for the compiler
     const int lane = threadIdx.x & 63;
     const int32_t gw = (int32_t)blockIdx.x * kBroadWaves + wave;
     Cand *seg = b.cand + (int64_t)gw * b.seg_cap;
     const uint32_t cap = (uint32_t)b.seg_cap;
-    uint32_t cnt = 0, n_units = 0, n_clusters = 0, n_nodes = 0, max_nodes = 0;
-    const unsigned long long t0 = w.stats ? __builtin_amdgcn_s_memtime() : 0ull;
+    uint32_t cnt = 0, n_units = 0, n_clusters = 0, n_nodes = 0, n_pairs = 0, n_xf = 0;
     const int64_t n_static = (int64_t)b.n_waves * kChunk;
     int64_t base = (int64_t)gw * kChunk;
     while (base < w.n_units) {
         const int64_t end = base + kChunk < w.n_units ? base + kChunk : w.n_units;
-        for (int64_t u = base; u < end; ++u) {
-            const uint32_t before = n_nodes;
-            if (!broad_unit<kLds>(env, s_items, links, w, b, (int32_t)u, lane, seg, cnt, cap, n_units, n_clusters,
-                                  n_nodes)) {
-                if (lane == 0) b.ovf_list[atomicAdd(b.ctl + 1, 1u)] = (int32_t)u;
+        // lane-parallel pre-pass, one lane per unit of the chunk: decode, FCL relative
+        // transform, whole-link box against the env root box
+        bool live = false, ok = false;
+        if (lane < end - base) {
+            int32_t link;
+            int64_t slot, edge;
+            live = decode_unit(w, base + lane, link, slot, edge);
+            if (live) {
+                double R[9], T[3];
+                unit_transform(env, w.poses + (slot * w.L + link) * 12, R, T);
+                float lo[3], hi[3];
+                local_box(links[link].bc, links[link].be, R, T, lo, hi);
+                ok = box_overlap(lo, hi, env.root_lo, env.root_hi);
+#pragma unroll
+                for (int i = 0; i < 9; ++i) s_rt[wave][lane][i] = R[i];
+#pragma unroll
+                for (int i = 0; i < 3; ++i) s_rt[wave][lane][9 + i] = T[i];
+                s_link[wave][lane] = link;
             }
-            max_nodes = max_nodes > n_nodes - before ? max_nodes : n_nodes - before;
         }
+        n_units += (uint32_t)__popcll(__ballot(live));
+        uint64_t um = __ballot(ok);
+        __builtin_amdgcn_wave_barrier();
+        while (um) {
+            const int j = __ffsll((unsigned long long)um) - 1;
+            um &= um - 1;
+            double R[9], T[3];
+#pragma unroll
+            for (int i = 0; i < 9; ++i) R[i] = uniform_d(s_rt[wave][j][i]);
+#pragma unroll
+            for (int i = 0; i < 3; ++i) T[i] = uniform_d(s_rt[wave][j][9 + i]);
+            const int32_t link = __builtin_amdgcn_readfirstlane(s_link[wave][j]);
+            const int32_t u = (int32_t)(base + j);
+            if (!broad_unit<kLds>(env, s_items, links[link], R, T, b, u, lane, seg, cnt, cap, n_clusters, n_nodes,
+                                  n_pairs, n_xf)) {
+                if (lane == 0) b.ovf_list[atomicAdd(b.ctl + 1, 1u)] = u;
+            }
+        }
+        __builtin_amdgcn_wave_barrier();
         if (n_static >= w.n_units) break;
         uint32_t nb = 0;
         if (lane == 0) nb = atomicAdd(b.ctl, 1u);
@@ -231,8 +351,8 @@ __global__ __launch_bounds__(kBroadWaves * 64) void k_broad(EnvDev env, const Ag
         atomicAdd(w.stats + 0, (unsigned long long)n_units);
         atomicAdd(w.stats + 1, (unsigned long long)n_clusters);
         atomicAdd(w.stats + 2, (unsigned long long)n_nodes);
-        atomicMax(w.stats + 4, (unsigned long long)max_nodes);
-        atomicAdd(w.stats + 6, __builtin_amdgcn_s_memtime() - t0);
+        atomicAdd(w.stats + 4, (unsigned long long)n_pairs);
+        atomicAdd(w.stats + 6, (unsigned long long)n_xf);
         atomicAdd(w.stats + 7, (unsigned long long)cnt);
     }
 }

@@ -211,7 +211,7 @@ std::vector<Item> wide_tree(const std::vector<BvhNode> &pre, int64_t n_tris, std
     levels[0].resize((size_t)n_tris);
     for (const BvhNode &n : pre)
         if (n.b < 0) levels[0][n.a] = Item{{n.lo[0], n.lo[1], n.lo[2]}, n.a, {n.hi[0], n.hi[1], n.hi[2]}, 1};
-    if (n_tris > kClusterMax) {
+    {  // always a bucket level (a single bucket for <= 64 triangles)
         std::vector<Range> memo(pre.size()), buckets;
         subtree_range(pre, 0, memo);
         collect_buckets(pre, 0, memo, buckets);
@@ -432,6 +432,18 @@ extern "C" mpt_status mpt_agent_create(const double *tris, int64_t n_tris, mpt_a
             ag->dev.clusters = ag->d_clusters;
             ag->dev.n_clusters = (int32_t)cl.size();
             ag->dev.n_tris = (int32_t)n_tris;
+            // whole-link box (centre / half-extent) for the per-unit cull of the broad phase
+            double lo[3] = {HUGE_VAL, HUGE_VAL, HUGE_VAL}, hi[3] = {-HUGE_VAL, -HUGE_VAL, -HUGE_VAL};
+            for (int64_t i = 0; i < 3 * n_tris; ++i)
+                for (int k = 0; k < 3; ++k) {
+                    lo[k] = std::min(lo[k], tris[3 * i + k]);
+                    hi[k] = std::max(hi[k], tris[3 * i + k]);
+                }
+            for (int k = 0; k < 3; ++k) {
+                ag->dev.bc[k] = n_tris > 0 ? 0.5 * (lo[k] + hi[k]) : 0.0;
+                ag->dev.be[k] = n_tris > 0 ? std::max(hi[k] - ag->dev.bc[k], ag->dev.bc[k] - lo[k]) * (1.0 + 1e-12) + 1e-12
+                                           : 0.0;
+            }
             *out = ag;
         } catch (...) {
             mpt_agent_destroy(ag);

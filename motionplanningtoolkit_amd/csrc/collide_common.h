@@ -55,14 +55,14 @@ __device__ __forceinline__ void agent_tri_box(const double *__restrict__ t, cons
     bhi[2] = widen_hi(dmax(Q1.z, dmax(Q2.z, Q3.z)));
 }
 
-// Widened float box of an agent cluster (local centre/half-extent) under R, T.
-__device__ __forceinline__ void cluster_box(const Cluster &c, const double R[9], const double T[3], float lo[3],
-                                            float hi[3]) {
-    const v3 cc = xform(R, T, mk(c.c[0], c.c[1], c.c[2]));
+// Widened float box of a local box (centre c, half-extent e) under R, T.
+__device__ __forceinline__ void local_box(const double c[3], const double e[3], const double R[9], const double T[3],
+                                          float lo[3], float hi[3]) {
+    const v3 cc = xform(R, T, mk(c[0], c[1], c[2]));
     const double ccv[3] = {cc.x, cc.y, cc.z};
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
-        const double ex = fabs(R[i * 3 + 0]) * c.e[0] + fabs(R[i * 3 + 1]) * c.e[1] + fabs(R[i * 3 + 2]) * c.e[2];
+        const double ex = fabs(R[i * 3 + 0]) * e[0] + fabs(R[i * 3 + 1]) * e[1] + fabs(R[i * 3 + 2]) * e[2];
         lo[i] = widen_lo(ccv[i] - ex);
         hi[i] = widen_hi(ccv[i] + ex);
     }

@@ -44,6 +44,7 @@ struct AgentDev {
     const Cluster *clusters;  // [C]
     int32_t n_clusters;
     int32_t n_tris;
+    double bc[3], be[3];      // whole-link local box centre / half-extent
 };
 
 // Broad-phase env tree, 64 children per node so one wave tests a node's children with one
