@@ -90,7 +90,7 @@ def roofline(per_launch, cst, K, n0, d, nn_mode):
     ms = per_launch[dominant]
     if dominant == "collide":
         # bytes per (pose, link) unit = 96 (pose) + 32 per BVH node visit + 144 per triangle-pair test
-        nbytes = 96.0 * cst["units"] + 32.0 * cst["node_visits"] + 144.0 * cst["tri_tests"]
+        nbytes = 96.0 * cst["units"] + 32.0 * cst["node_tests"] + 144.0 * cst["tri_tests"]
         flops = 54.0 * 64 * cst["clusters"] + 750.0 * cst["tri_tests"]  # upper bounds (full clusters, all 17 axes)
         gbs = nbytes / (ms * 1e-3) / 1e9
         return {"bound": "hbm", "achieved": round(gbs, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",

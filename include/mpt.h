@@ -168,9 +168,11 @@ mpt_status mpt_rrt_enable_timing(mpt_rrt *rrt, int32_t enable);
 mpt_status mpt_rrt_set_nn(mpt_rrt *rrt, int32_t mode, double points_per_cell);
 /* Collision work counters accumulated since the previous call (synchronises), then reset;
  * enable = 1 keeps counting in later rounds (atomics: off for timed runs).
- * out [8] (may be NULL): (pose, link) units, clusters visited, BVH node visits, triangle tests,
- * max node visits of one unit, max / sum of wave lifetimes (s_memtime ticks), reserved. */
-mpt_status mpt_rrt_collide_stats(mpt_rrt *rrt, int32_t enable, uint64_t out[8]);
+ * out [16] (may be NULL): [0] (pose, link) units, [1] agent clusters past the root cull,
+ * [2] env tree node tests, [3] exact triangle tests, [4] (cluster, env triangle) pair tests,
+ * [5] units re-run by the fused kernel, [6] agent cluster transforms, [7] broad-phase
+ * candidates, [8..15] broad-phase wave time per phase (s_memtime ticks, split path). */
+mpt_status mpt_rrt_collide_stats(mpt_rrt *rrt, int32_t enable, uint64_t out[16]);
 mpt_status mpt_rrt_kernel_times(mpt_rrt *rrt, float ms[6]);
 
 #ifdef __cplusplus

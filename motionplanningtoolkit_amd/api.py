@@ -275,10 +275,13 @@ class RRTEngine:
 
     def collide_stats(self, enable: bool) -> dict:
         """Counters since the last call (then reset); enable keeps counting in later rounds."""
-        out = np.zeros(8, np.uint64)
+        out = np.zeros(16, np.uint64)
         check(lib().mpt_rrt_collide_stats(self.handle, 1 if enable else 0, _p(out)), "mpt_rrt_collide_stats")
-        return {"units": int(out[0]), "clusters": int(out[1]), "node_visits": int(out[2]), "tri_tests": int(out[3]),
-                "max_unit_node_visits": int(out[4]), "max_wave_ticks": int(out[5]), "sum_wave_ticks": int(out[6])}
+        names = ["units", "clusters", "node_tests", "tri_tests", "pair_tests", "fused_reruns", "cluster_transforms",
+                 "candidates"]
+        d = {k: int(v) for k, v in zip(names, out[:8])}
+        d["wave_ticks"] = [int(v) for v in out[8:]]
+        return d
 
     def set_nn(self, mode: str = "auto", points_per_cell: float = 0.0) -> None:
         """NN structure of the rounds: 'auto' | 'brute' | 'grid' (identical results)."""

@@ -1,102 +1,58 @@
 // broad.hip -- the two-phase collision path (default structure, mpt_set_collide_mode).
 //
 // Same verdicts as the fused kernel (collide.hip): exists (pose, link, env tri, agent tri)
-// with overlapping exact boxes (tri_gate) and intersect_Triangle true.  Work is split so
-// that neither phase carries the other's registers:
+// with overlapping exact boxes (tri_gate) and intersect_Triangle true.  The work is done
+// breadth-first, every stage a flat parallel loop over its own items, so no wave carries a
+// long chain of dependent memory accesses (what limits the fused kernel):
 //
-// k_broad  one wave per (pose, link) unit (static first chunk per wave, then an atomic
-//          work queue).  Lanes = agent clusters: each lane maps its cluster's local box
-//          (FP64, R T from fcl::relativeTransform) to a widened float box, culled against
-//          the env root box.  For each surviving cluster the wave walks the 64-ary env
-//          tree (mpt_internal.h Item) with that box: at a node, lane i tests child i, the
-//          ballot is the set of children to enter; the walk state (mask, base, level) is a
-//          few SGPRs with the pending levels in lane-indexed VGPRs.  When a bucket's
-//          triangles overlap the cluster box, lanes = the cluster's agent triangles, each
-//          mapped exactly and boxed once per cluster (lazily), and every (lane, env tri)
-//          box overlap is written as a candidate to the wave's own segment.
-// k_narrow one 64-lane workgroup per segment, one candidate per lane: the exact transform of
-//          the agent triangle, tri_gate, intersect_Triangle; verdict[edge] = 1 on contact.
-// Units whose candidates do not fit their segment are listed and re-run by the fused kernel.
+// k_pairs   one thread per (unit, agent cluster).  FCL relative transform of the unit's pose
+//           (FP64), the cluster's local box mapped to a widened float box, culled by the env
+//           root box, then walked down the 64-ary env tree (mpt_internal.h Item, staged in
+//           LDS when it fits): every env triangle whose box overlaps the cluster box makes a
+//           (unit, cluster, triangle) pair.  Two passes (count, then write) give each thread
+//           a contiguous run of its wave's pair segment and one header; the reservations are
+//           LDS atomics.
+// scan      exclusive sum of the per-segment header counts (hipcub), k_expand writes the
+//           header slots densely.
+// k_cands   one wave per header (grid-stride over the dense list): lanes = the cluster's
+//           agent triangles, mapped exactly (FP64) and boxed; lanes also fetch the header's
+//           env triangle boxes, which are then tested from registers; overlaps become
+//           candidates in the wave's segment (or the spill list).
+// k_narrow  one 64-lane workgroup per candidate segment (plus the spill list), one candidate
+//           per lane: exact transform, tri_gate, intersect_Triangle; verdict[edge] = 1.
+// Units whose pairs overflow a segment are re-run by the fused kernel (list mode).
+#include <hipcub/hipcub.hpp>
+
 #include "collide_common.h"
 
 namespace mpt {
 
-constexpr int kBroadWaves = 8;     // waves per workgroup
-constexpr int kChunk = 4;          // units per queue grab (one pre-pass lane each)
-constexpr int kSegCap = 1024;      // candidates per wave segment
-constexpr int kLdsItems = 2048;    // whole env tree staged in LDS (64 KiB) when it fits
-
+constexpr int kPairThreads = 256;   // k_pairs workgroup (4 waves)
+constexpr int kPairCap = 256;       // env triangles per k_pairs wave segment
+constexpr int kHdrCap = 64;         // headers per segment (one per lane at most)
+constexpr int kCandCap = 512;       // candidates per k_cands wave (then the spill list)
 constexpr int kSpillCap = 1 << 22;  // shared spill list (48 MiB)
 constexpr int kSpillBlocks = 256;   // k_narrow workgroups over the spill list
+constexpr int kLdsItems = 2048;     // env tree staged in LDS by k_pairs up to this size (64 KiB)
+constexpr int kStack = kMaxLevels;  // per-thread walk stack (general trees)
 
-struct BroadArgs {
+struct SplitArgs {
+    int32_t *pairs;
+    PairHdr *hdr;
+    uint32_t *hdr_count;
+    const uint32_t *hdr_off;
+    int32_t *hdr_dense;
     Cand *cand;
-    uint32_t *seg_count;
+    uint32_t *cand_count;
     Cand *spill;
     uint32_t *ctl;
     int32_t *ovf_list;
-    int32_t seg_cap;
-    int32_t n_waves;
-    int32_t spill_cap;
+    int64_t n_seg;
+    int32_t pair_cap, cand_cap, spill_cap, n_clusters, n_cwaves;
 };
 
-// Append the lanes of h (ballot m) as candidates: to the wave's segment, or once that is
-// full to the shared spill list; false if both are full.  Called with all lanes active.
-__device__ __forceinline__ bool emit(bool h, uint64_t m, int32_t unit, int32_t atri, int32_t etri, Cand *seg,
-                                     uint32_t &cnt, uint32_t cap, const BroadArgs &b) {
-    const uint32_t n = (uint32_t)__popcll(m);
-    const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-    if (cnt + n <= cap) {
-        if (h) seg[cnt + rank] = Cand{unit, atri, etri};
-        cnt += n;
-        return true;
-    }
-    uint32_t base = 0;
-    if ((threadIdx.x & 63) == 0) base = atomicAdd(b.ctl + 2, n);
-    base = __builtin_amdgcn_readfirstlane(base);
-    if (base + n > (uint32_t)b.spill_cap) return false;
-    if (h) b.spill[base + rank] = Cand{unit, atri, etri};
-    return true;
-}
-
-// Children [first, first + count) of a node (absolute item indices): lane i tests child i
-// against the query box; returns the ballot, the lane keeps its child's box in `mine`.
-template <bool kLds>
-__device__ __forceinline__ uint64_t visit(const Item *s_items, const Item *__restrict__ items, int32_t first,
-                                          int32_t count, const float qlo[3], const float qhi[3], int lane,
-                                          Item &mine) {
-    bool h = false;
-    if (lane < count) {
-        mine = kLds ? s_items[first + lane] : items[first + lane];
-        h = box_overlap(qlo, qhi, mine.lo, mine.hi);
-    }
-    return __ballot(h);
-}
-
-// (first, count) of one item, wave-uniform index.
-template <bool kLds>
-__device__ __forceinline__ void item_range(const Item *s_items, const Item *__restrict__ items, int32_t idx,
-                                           int32_t &first, int32_t &count) {
-    if (kLds) {
-        first = __builtin_amdgcn_readfirstlane(s_items[idx].first);
-        count = __builtin_amdgcn_readfirstlane(s_items[idx].count);
-    } else {
-#if defined(__HIP_DEVICE_COMPILE__)
-        typedef __attribute__((address_space(4))) const Item *cptr;  // scalar cache, s_load
-        const Item *g = items;
-        first = ((cptr)g)[idx].first;
-        count = ((cptr)g)[idx].count;
-#else
-        first = items[idx].first;
-        count = items[idx].count;
-#endif
-    }
-}
-
-// One item, wave-uniform index (LDS broadcast read, or the scalar cache).
-template <bool kLds>
-__device__ __forceinline__ Item load_item_u(const Item *s_items, const Item *__restrict__ items, int32_t idx) {
-    if (kLds) return s_items[idx];
+// wave-uniform item load through the scalar cache (items are read-only in these kernels)
+__device__ __forceinline__ Item load_item_u(const Item *__restrict__ items, int64_t idx) {
 #if defined(__HIP_DEVICE_COMPILE__)
     typedef __attribute__((address_space(4))) const Item *cptr;
     const Item *g = items;
@@ -104,10 +60,6 @@ __device__ __forceinline__ Item load_item_u(const Item *s_items, const Item *__r
 #else
     return items[idx];
 #endif
-}
-
-__device__ __forceinline__ float lane_f(float v, int j) {
-    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), j));
 }
 
 __device__ __forceinline__ float wave_min(float v) {
@@ -120,238 +72,252 @@ __device__ __forceinline__ float wave_max(float v) {
     for (int off = 32; off > 0; off >>= 1) v = fmaxf(v, __shfl_xor(v, off));
     return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v)));
 }
+__device__ __forceinline__ float lane_f(float v, int j) {
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), j));
+}
 
-// One unit whose whole-link box passed the root cull; R, T wave-uniform.  False on
-// candidate overflow (the unit is then re-run by the fused kernel).
-template <bool kLds>
-__device__ bool broad_unit(const EnvDev &env, const Item *s_items, const AgentDev &ag, const double R[9],
-                           const double T[3], const BroadArgs &b, int32_t unit, int lane, Cand *seg,
-                           uint32_t &cnt, uint32_t cap, uint32_t &n_clusters, uint32_t &n_nodes,
-                           uint32_t &n_pairs, uint32_t &n_xf) {
+// Per-thread walk of the env tree (items from LDS or global) with box (lo, hi);
+// sink(tri) for every overlapping triangle box; returns the number of item tests.
+// Two-level trees (top = buckets of triangles) need no stack; deeper ones keep one
+// (mask, base, level) entry per level in LDS.
+template <bool kTwo, class Sink>
+__device__ __forceinline__ uint32_t walk_tree(const EnvDev &env, const Item *__restrict__ items, const float lo[3],
+                                              const float hi[3], uint4 *stk, Sink &&sink) {
     const int32_t top = env.n_levels - 1;
     const int32_t top_off = env.lev_off[top];
     const int32_t n_top = env.lev_off[top + 1] - top_off;
-    for (int32_t cbase = 0; cbase < ag.n_clusters; cbase += kWave) {
-        float clo[3] = {0, 0, 0}, chi[3] = {0, 0, 0};
-        bool ok = false;
-        int32_t cf = 0, cc = 0;
-        if (cbase + lane < ag.n_clusters) {
-            const Cluster &c = ag.clusters[cbase + lane];
-            local_box(c.c, c.e, R, T, clo, chi);
-            ok = box_overlap(clo, chi, env.root_lo, env.root_hi);
-            cf = c.first;
-            cc = c.count;
+    uint32_t tests = (uint32_t)n_top;
+    auto tri_run = [&](int32_t first, int32_t count) {
+        int32_t k = first;
+        const int32_t end = first + count;
+        for (; k + 4 <= end; k += 4) {  // four independent loads in flight
+            const Item t0 = items[k], t1 = items[k + 1], t2 = items[k + 2], t3 = items[k + 3];
+            if (box_overlap(lo, hi, t0.lo, t0.hi)) sink(k);
+            if (box_overlap(lo, hi, t1.lo, t1.hi)) sink(k + 1);
+            if (box_overlap(lo, hi, t2.lo, t2.hi)) sink(k + 2);
+            if (box_overlap(lo, hi, t3.lo, t3.hi)) sink(k + 3);
         }
-        uint64_t cm = __ballot(ok);
-        if (!cm) continue;
-        if (top == 1) {
-            // Two-level tree (top items = buckets of triangles): lanes = clusters test every
-            // bucket box in one pass (lane keeps a bucket bitmask), then cluster by cluster
-            // the overlapping buckets' triangles, lanes = triangles.
-            uint64_t bm = 0;
-            for (int32_t i = 0; i < n_top; ++i) {
-                const Item t = load_item_u<kLds>(s_items, env.items, top_off + i);
-                bm |= (uint64_t)(ok && box_overlap(clo, chi, t.lo, t.hi)) << i;
-            }
-            n_nodes += (uint32_t)n_top;
-            uint64_t cm2 = __ballot(bm != 0);
-            while (cm2) {
-                const int j = __ffsll((unsigned long long)cm2) - 1;
-                cm2 &= cm2 - 1;
-                ++n_clusters;
-                uint64_t B = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int32_t)(uint32_t)(bm >> 32), j) << 32) |
-                             (uint32_t)__builtin_amdgcn_readlane((int32_t)(uint32_t)bm, j);
-                const float qlo[3] = {lane_f(clo[0], j), lane_f(clo[1], j), lane_f(clo[2], j)};
-                const float qhi[3] = {lane_f(chi[0], j), lane_f(chi[1], j), lane_f(chi[2], j)};
-                const int32_t tfirst = __builtin_amdgcn_readlane(cf, j);
-                const int32_t tcount = __builtin_amdgcn_readlane(cc, j);
-                const bool act = lane < tcount;
-                bool have = false;
-                float blo[3] = {0, 0, 0}, bhi[3] = {0, 0, 0}, tlo[3] = {0, 0, 0}, thi[3] = {0, 0, 0};
-                while (B) {
-                    const int i = __ffsll((unsigned long long)B) - 1;
-                    B &= B - 1;
-                    int32_t first, count;
-                    item_range<kLds>(s_items, env.items, top_off + i, first, count);
-                    Item mine{};
-                    uint64_t M = visit<kLds>(s_items, env.items, first, count, qlo, qhi, lane, mine);
-                    ++n_nodes;
-                    if (!M) continue;
-                    if (!have) {
-                        if (act) agent_tri_box(ag.tris + (int64_t)(tfirst + lane) * 9, R, T, blo, bhi);
-                        have = true;
-                        ++n_xf;
-#pragma unroll
-                        for (int k = 0; k < 3; ++k) {
-                            tlo[k] = wave_min(act ? blo[k] : __builtin_huge_valf());
-                            thi[k] = wave_max(act ? bhi[k] : -__builtin_huge_valf());
-                        }
-                    }
-                    M &= __ballot(box_overlap(tlo, thi, mine.lo, mine.hi));
-                    n_pairs += (uint32_t)__popcll(M);
-                    while (M) {
-                        const int t = __ffsll((unsigned long long)M) - 1;
-                        M &= M - 1;
-                        const float elo[3] = {lane_f(mine.lo[0], t), lane_f(mine.lo[1], t), lane_f(mine.lo[2], t)};
-                        const float ehi[3] = {lane_f(mine.hi[0], t), lane_f(mine.hi[1], t), lane_f(mine.hi[2], t)};
-                        const bool h = act && box_overlap(blo, bhi, elo, ehi);
-                        const uint64_t m = __ballot(h);
-                        if (m && !emit(h, m, unit, tfirst + lane, first + t, seg, cnt, cap, b)) return false;
-                    }
-                }
-            }
+        for (; k < end; ++k) {
+            const Item t = items[k];
+            if (box_overlap(lo, hi, t.lo, t.hi)) sink(k);
+        }
+    };
+    if (kTwo) {
+        for (int32_t i = 0; i < n_top; ++i) {
+            const Item b = items[top_off + i];
+            if (!box_overlap(lo, hi, b.lo, b.hi)) continue;
+            tests += (uint32_t)b.count;
+            tri_run(b.first, b.count);
+        }
+        return tests;
+    }
+    // general: DFS over (level, base, remaining-children mask)
+    uint64_t M = 0;
+    for (int32_t i = 0; i < n_top; ++i) {
+        const Item b = items[top_off + i];
+        if (box_overlap(lo, hi, b.lo, b.hi)) M |= 1ull << i;
+    }
+    int32_t lv = top, base = top_off, sp = 0;
+    for (;;) {
+        if (!M) {
+            if (sp == 0) break;
+            --sp;
+            const uint4 e = stk[sp];
+            M = ((uint64_t)e.y << 32) | e.x;
+            base = (int32_t)e.z;
+            lv = (int32_t)e.w;
             continue;
         }
-        while (cm) {
-            const int j = __ffsll((unsigned long long)cm) - 1;
-            cm &= cm - 1;
-            ++n_clusters;
-            const float qlo[3] = {lane_f(clo[0], j), lane_f(clo[1], j), lane_f(clo[2], j)};
-            const float qhi[3] = {lane_f(chi[0], j), lane_f(chi[1], j), lane_f(chi[2], j)};
-            const int32_t tfirst = __builtin_amdgcn_readfirstlane(ag.clusters[cbase + j].first);
-            const int32_t tcount = __builtin_amdgcn_readfirstlane(ag.clusters[cbase + j].count);
-            const bool act = lane < tcount;
-            bool have = false;  // agent triangle boxes of this cluster computed
-            float blo[3] = {0, 0, 0}, bhi[3] = {0, 0, 0};
-            float tlo[3] = {0, 0, 0}, thi[3] = {0, 0, 0};  // their union (tighter than the cluster box)
-
-            Item mine{};
-            int32_t lv = top, base = top_off;
-            uint64_t M = visit<kLds>(s_items, env.items, top_off, n_top, qlo, qhi, lane, mine);
-            ++n_nodes;
-            int32_t sp = 0, st_mlo = 0, st_mhi = 0, st_base = 0, st_lv = 0;  // lane k = pending entry k
-            for (;;) {
-                if (lv == 0) {
-                    // M = env triangles base + bit overlapping the cluster box
-                    if (M && !have) {
-                        if (act) agent_tri_box(ag.tris + (int64_t)(tfirst + lane) * 9, R, T, blo, bhi);
-                        have = true;
-                        ++n_xf;
-#pragma unroll
-                        for (int k = 0; k < 3; ++k) {
-                            tlo[k] = wave_min(act ? blo[k] : __builtin_huge_valf());
-                            thi[k] = wave_max(act ? bhi[k] : -__builtin_huge_valf());
-                        }
-                    }
-                    // lanes of the last visit hold these triangles' boxes: drop those that miss
-                    // the union of the agent triangle boxes
-                    if (M) M &= __ballot(box_overlap(tlo, thi, mine.lo, mine.hi));
-                    n_pairs += (uint32_t)__popcll(M);
-                    while (M) {
-                        const int t = __ffsll((unsigned long long)M) - 1;
-                        M &= M - 1;
-                        const float elo[3] = {lane_f(mine.lo[0], t), lane_f(mine.lo[1], t), lane_f(mine.lo[2], t)};
-                        const float ehi[3] = {lane_f(mine.hi[0], t), lane_f(mine.hi[1], t), lane_f(mine.hi[2], t)};
-                        const bool h = act && box_overlap(blo, bhi, elo, ehi);
-                        const uint64_t m = __ballot(h);
-                        if (m && !emit(h, m, unit, tfirst + lane, base + t, seg, cnt, cap, b)) return false;
-                    }
-                }
-                if (!M) {
-                    if (sp == 0) break;
-                    --sp;
-                    M = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane(st_mhi, sp) << 32) |
-                        (uint32_t)__builtin_amdgcn_readlane(st_mlo, sp);
-                    base = __builtin_amdgcn_readlane(st_base, sp);
-                    lv = __builtin_amdgcn_readlane(st_lv, sp);
-                    continue;
-                }
-                const int c = __ffsll((unsigned long long)M) - 1;
-                M &= M - 1;
-                int32_t cfirst, ccount;
-                item_range<kLds>(s_items, env.items, base + c, cfirst, ccount);
-                if (M) {  // keep the rest of this node for later
-                    st_mlo = lane == sp ? (int32_t)(uint32_t)M : st_mlo;
-                    st_mhi = lane == sp ? (int32_t)(uint32_t)(M >> 32) : st_mhi;
-                    st_base = lane == sp ? base : st_base;
-                    st_lv = lane == sp ? lv : st_lv;
-                    ++sp;
-                }
-                --lv;
-                base = cfirst;
-                M = visit<kLds>(s_items, env.items, cfirst, ccount, qlo, qhi, lane, mine);
-                ++n_nodes;
-            }
+        const int j = __ffsll((unsigned long long)M) - 1;
+        M &= M - 1;
+        const Item it = items[base + j];
+        tests += (uint32_t)it.count;
+        if (lv == 1) {  // children are triangles
+            tri_run(it.first, it.count);
+            continue;
         }
+        uint64_t Mc = 0;
+        for (int32_t c = 0; c < it.count; ++c) {
+            const Item ch = items[it.first + c];
+            if (box_overlap(lo, hi, ch.lo, ch.hi)) Mc |= 1ull << c;
+        }
+        if (!Mc) continue;
+        if (M) stk[sp++] = make_uint4((uint32_t)M, (uint32_t)(M >> 32), (uint32_t)base, (uint32_t)lv);
+        M = Mc;
+        base = it.first;
+        --lv;
     }
-    return true;
+    return tests;
 }
 
-template <bool kLds>
-__global__ __launch_bounds__(kBroadWaves * 64) void k_broad(EnvDev env, const AgentDev *__restrict__ links,
-                                                             CollideWork w, BroadArgs b) {
+template <bool kTwo, bool kLds>
+__global__ __launch_bounds__(kPairThreads) void k_pairs(EnvDev env, const AgentDev *__restrict__ links,
+                                                       CollideWork w, SplitArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    Item *s_items = reinterpret_cast<Item *>(smem);
+    __shared__ uint32_t s_pc[kPairThreads / 64], s_hc[kPairThreads / 64];
+    __shared__ uint4 s_stk[kTwo ? 1 : kPairThreads * kStack];
+    const Item *items = env.items;
     if (kLds) {
+        Item *s_items = reinterpret_cast<Item *>(smem);
         const int32_t n = env.lev_off[env.n_levels];
         const uint4 *src = reinterpret_cast<const uint4 *>(env.items);
         uint4 *dst = reinterpret_cast<uint4 *>(s_items);
         for (int i = threadIdx.x; i < n * 2; i += blockDim.x) dst[i] = src[i];
-        __syncthreads();
+        items = s_items;
     }
-    __shared__ double s_rt[kBroadWaves][kChunk][12];  // R, T of the chunk's surviving units
-    __shared__ int32_t s_link[kBroadWaves][kChunk];
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform for the compiler
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
-    const int32_t gw = (int32_t)blockIdx.x * kBroadWaves + wave;
-    Cand *seg = b.cand + (int64_t)gw * b.seg_cap;
-    const uint32_t cap = (uint32_t)b.seg_cap;
-    uint32_t cnt = 0, n_units = 0, n_clusters = 0, n_nodes = 0, n_pairs = 0, n_xf = 0;
-    const int64_t n_static = (int64_t)b.n_waves * kChunk;
-    int64_t base = (int64_t)gw * kChunk;
-    while (base < w.n_units) {
-        const int64_t end = base + kChunk < w.n_units ? base + kChunk : w.n_units;
-        // lane-parallel pre-pass, one lane per unit of the chunk: decode, FCL relative
-        // transform, whole-link box against the env root box
-        bool live = false, ok = false;
-        if (lane < end - base) {
-            int32_t link;
-            int64_t slot, edge;
-            live = decode_unit(w, base + lane, link, slot, edge);
-            if (live) {
-                double R[9], T[3];
-                unit_transform(env, w.poses + (slot * w.L + link) * 12, R, T);
-                float lo[3], hi[3];
-                local_box(links[link].bc, links[link].be, R, T, lo, hi);
-                ok = box_overlap(lo, hi, env.root_lo, env.root_hi);
-#pragma unroll
-                for (int i = 0; i < 9; ++i) s_rt[wave][lane][i] = R[i];
-#pragma unroll
-                for (int i = 0; i < 3; ++i) s_rt[wave][lane][9 + i] = T[i];
-                s_link[wave][lane] = link;
-            }
-        }
-        n_units += (uint32_t)__popcll(__ballot(live));
-        uint64_t um = __ballot(ok);
-        __builtin_amdgcn_wave_barrier();
-        while (um) {
-            const int j = __ffsll((unsigned long long)um) - 1;
-            um &= um - 1;
-            double R[9], T[3];
-#pragma unroll
-            for (int i = 0; i < 9; ++i) R[i] = uniform_d(s_rt[wave][j][i]);
-#pragma unroll
-            for (int i = 0; i < 3; ++i) T[i] = uniform_d(s_rt[wave][j][9 + i]);
-            const int32_t link = __builtin_amdgcn_readfirstlane(s_link[wave][j]);
-            const int32_t u = (int32_t)(base + j);
-            if (!broad_unit<kLds>(env, s_items, links[link], R, T, b, u, lane, seg, cnt, cap, n_clusters, n_nodes,
-                                  n_pairs, n_xf)) {
-                if (lane == 0) b.ovf_list[atomicAdd(b.ctl + 1, 1u)] = u;
-            }
-        }
-        __builtin_amdgcn_wave_barrier();
-        if (n_static >= w.n_units) break;
-        uint32_t nb = 0;
-        if (lane == 0) nb = atomicAdd(b.ctl, 1u);
-        nb = __builtin_amdgcn_readfirstlane(nb);
-        base = n_static + (int64_t)nb * kChunk;
+    if (lane == 0) {
+        s_pc[wave] = 0;
+        s_hc[wave] = 0;
     }
-    if (lane == 0) b.seg_count[gw] = cnt;
+    __syncthreads();
+    const int64_t t = (int64_t)blockIdx.x * kPairThreads + threadIdx.x;
+    const int64_t seg = t >> 6;
+    const int64_t unit = t / a.n_clusters;
+    const int32_t c = (int32_t)(t % a.n_clusters);
+    bool live = unit < w.n_units;
+    int32_t link = 0;
+    int64_t slot = 0, edge = 0;
+    if (live) live = decode_unit(w, unit, link, slot, edge);
+    if (live) live = c < links[link].n_clusters;
+    float lo[3] = {0, 0, 0}, hi[3] = {0, 0, 0};
+    int32_t tfirst = 0, tcount = 0;
+    if (live) {
+        double R[9], T[3];
+        unit_transform(env, w.poses + (slot * w.L + link) * 12, R, T);
+        const Cluster &cl = links[link].clusters[c];
+        local_box(cl.c, cl.e, R, T, lo, hi);
+        tfirst = cl.first;
+        tcount = cl.count;
+        live = box_overlap(lo, hi, env.root_lo, env.root_hi);
+    }
+    uint4 *stk = s_stk + (kTwo ? 0 : threadIdx.x * kStack);
+    uint32_t np = 0, tests = 0;
+    if (live) tests = walk_tree<kTwo>(env, items, lo, hi, stk, [&](int32_t) { ++np; });
+    bool ovf = false;
+    if (np > 0) {
+        const uint32_t p0 = atomicAdd(&s_pc[wave], np);
+        if (p0 + np > (uint32_t)a.pair_cap) {
+            ovf = true;
+        } else {
+            int32_t *out = a.pairs + seg * a.pair_cap + p0;
+            uint32_t k = 0;
+            walk_tree<kTwo>(env, items, lo, hi, stk, [&](int32_t tri) { out[k++] = tri; });
+            const uint32_t h = atomicAdd(&s_hc[wave], 1u);
+            a.hdr[seg * kHdrCap + h] =
+                PairHdr{(int32_t)unit, c, (int32_t)(seg * a.pair_cap + p0), (int32_t)np, tfirst, tcount, {0, 0}};
+        }
+    }
+    if (ovf) a.ovf_list[atomicAdd(a.ctl + 1, 1u)] = (int32_t)unit;  // rare: fused re-run
+    __builtin_amdgcn_wave_barrier();
+    if (lane == 0 && seg < a.n_seg) a.hdr_count[seg] = s_hc[wave];
+    if (w.stats) {
+        const uint64_t lm = __ballot(live);
+        uint32_t sum_tests = tests, sum_pairs = np;
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) {
+            sum_tests += __shfl_xor(sum_tests, off);
+            sum_pairs += __shfl_xor(sum_pairs, off);
+        }
+        if (lane == 0) {
+            atomicAdd(w.stats + 1, (unsigned long long)__popcll(lm));
+            atomicAdd(w.stats + 2, (unsigned long long)sum_tests);
+            atomicAdd(w.stats + 4, (unsigned long long)sum_pairs);
+        }
+    }
+}
+
+// header slots in dense order: dense[off[seg] + h] = seg * kHdrCap + h
+__global__ void k_expand(const uint32_t *__restrict__ count, const uint32_t *__restrict__ off, int64_t n_seg,
+                         int32_t *__restrict__ dense) {
+    const int64_t seg = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (seg >= n_seg) return;
+    const uint32_t n = count[seg], o = off[seg];
+    for (uint32_t h = 0; h < n; ++h) dense[o + h] = (int32_t)(seg * kHdrCap + h);
+}
+
+// Append the lanes of h (ballot m) as candidates: to the wave's segment, or once that is
+// full to the shared spill list; false if both are full.  Called with all lanes active.
+__device__ __forceinline__ bool emit(bool h, uint64_t m, int32_t unit, int32_t atri, int32_t etri, Cand *seg,
+                                     uint32_t &cnt, const SplitArgs &a) {
+    const uint32_t n = (uint32_t)__popcll(m);
+    const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+    if (cnt + n <= (uint32_t)a.cand_cap) {
+        if (h) seg[cnt + rank] = Cand{unit, atri, etri};
+        cnt += n;
+        return true;
+    }
+    uint32_t base = 0;
+    if ((threadIdx.x & 63) == 0) base = atomicAdd(a.ctl + 2, n);
+    base = __builtin_amdgcn_readfirstlane(base);
+    if (base + n > (uint32_t)a.spill_cap) return false;
+    if (h) a.spill[base + rank] = Cand{unit, atri, etri};
+    return true;
+}
+
+__global__ __launch_bounds__(256) void k_cands(EnvDev env, const AgentDev *__restrict__ links, CollideWork w,
+                                               SplitArgs a) {
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    const int32_t cw = (int32_t)blockIdx.x * 4 + wave;
+    const uint32_t total = __builtin_amdgcn_readfirstlane(a.hdr_off[a.n_seg]);
+    Cand *cseg = a.cand + (int64_t)cw * a.cand_cap;
+    uint32_t cnt = 0, n_xf = 0;
+    for (uint32_t g = (uint32_t)cw; g < total; g += (uint32_t)a.n_cwaves) {
+        const int32_t slot_h = __builtin_amdgcn_readfirstlane(a.hdr_dense[g]);
+        const PairHdr H = a.hdr[slot_h];
+        const int32_t unit = __builtin_amdgcn_readfirstlane(H.unit);
+        const int32_t p0 = __builtin_amdgcn_readfirstlane(H.p0);
+        const int32_t np = __builtin_amdgcn_readfirstlane(H.n);
+        const int32_t tfirst = __builtin_amdgcn_readfirstlane(H.tfirst);
+        const int32_t tcount = __builtin_amdgcn_readfirstlane(H.tcount);
+        int32_t link;
+        int64_t slot, edge;
+        decode_unit(w, unit, link, slot, edge);
+        const bool act = lane < tcount;
+        const double *tri = links[link].tris + (int64_t)(tfirst + (act ? lane : 0)) * 9;
+        double R[9], T[3];
+        unit_transform(env, w.poses + (slot * w.L + link) * 12, R, T);
+#pragma unroll
+        for (int i = 0; i < 9; ++i) R[i] = uniform_d(R[i]);
+#pragma unroll
+        for (int i = 0; i < 3; ++i) T[i] = uniform_d(T[i]);
+        for (int32_t k0 = 0; k0 < np; k0 += 64) {
+            // lanes fetch up to 64 of the header's env triangle boxes
+            const int32_t nk = np - k0 < 64 ? np - k0 : 64;
+            int32_t etri = 0;
+            Item e{};
+            if (lane < nk) {
+                etri = a.pairs[p0 + k0 + lane];
+                e = env.items[etri];
+            }
+            float blo[3] = {0, 0, 0}, bhi[3] = {0, 0, 0}, tlo[3], thi[3];
+            if (act) agent_tri_box(tri, R, T, blo, bhi);
+            if (k0 == 0) ++n_xf;
+#pragma unroll
+            for (int k = 0; k < 3; ++k) {
+                tlo[k] = wave_min(act ? blo[k] : __builtin_huge_valf());
+                thi[k] = wave_max(act ? bhi[k] : -__builtin_huge_valf());
+            }
+            // env triangles that miss the union of the agent triangle boxes are dropped
+            uint64_t M = __ballot(lane < nk && box_overlap(tlo, thi, e.lo, e.hi));
+            bool ok = true;
+            while (M && ok) {
+                const int j = __ffsll((unsigned long long)M) - 1;
+                M &= M - 1;
+                const float elo[3] = {lane_f(e.lo[0], j), lane_f(e.lo[1], j), lane_f(e.lo[2], j)};
+                const float ehi[3] = {lane_f(e.hi[0], j), lane_f(e.hi[1], j), lane_f(e.hi[2], j)};
+                const int32_t et = __builtin_amdgcn_readlane(etri, j);
+                const bool hh = act && box_overlap(blo, bhi, elo, ehi);
+                const uint64_t m = __ballot(hh);
+                if (m) ok = emit(hh, m, unit, tfirst + lane, et, cseg, cnt, a);
+            }
+            if (!ok && lane == 0) a.ovf_list[atomicAdd(a.ctl + 1, 1u)] = unit;  // spill full: fused re-run
+        }
+    }
+    if (lane == 0 && cw < a.n_cwaves) a.cand_count[cw] = cnt;
     if (w.stats && lane == 0) {
-        atomicAdd(w.stats + 0, (unsigned long long)n_units);
-        atomicAdd(w.stats + 1, (unsigned long long)n_clusters);
-        atomicAdd(w.stats + 2, (unsigned long long)n_nodes);
-        atomicAdd(w.stats + 4, (unsigned long long)n_pairs);
         atomicAdd(w.stats + 6, (unsigned long long)n_xf);
         atomicAdd(w.stats + 7, (unsigned long long)cnt);
     }
@@ -376,74 +342,134 @@ __device__ __forceinline__ void narrow_one(const EnvDev &env, const AgentDev *__
         __hip_atomic_store(w.verdict + edge, (uint8_t)1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// Workgroups [0, n_waves): one broad segment each; the next kSpillBlocks: the spill list.
+// Workgroups [0, n_cwaves): one candidate segment each; the next kSpillBlocks: the spill list.
 __global__ __launch_bounds__(64) void k_narrow(EnvDev env, const AgentDev *__restrict__ links, CollideWork w,
-                                               BroadArgs b) {
+                                               SplitArgs a) {
     const int32_t gw = blockIdx.x;
     uint32_t n_sat = 0;
-    if (gw < b.n_waves) {
-        const uint32_t cnt = b.seg_count[gw];
-        const Cand *seg = b.cand + (int64_t)gw * b.seg_cap;
+    if (gw < a.n_cwaves) {
+        const uint32_t cnt = a.cand_count[gw];
+        const Cand *seg = a.cand + (int64_t)gw * a.cand_cap;
         for (uint32_t i = threadIdx.x; i < cnt; i += 64) narrow_one(env, links, w, seg[i], n_sat);
     } else {
-        const uint32_t n = b.ctl[2] < (uint32_t)b.spill_cap ? b.ctl[2] : (uint32_t)b.spill_cap;
-        for (uint32_t i = (uint32_t)(gw - b.n_waves) * 64 + threadIdx.x; i < n; i += kSpillBlocks * 64)
-            narrow_one(env, links, w, b.spill[i], n_sat);
+        const uint32_t n = a.ctl[2] < (uint32_t)a.spill_cap ? a.ctl[2] : (uint32_t)a.spill_cap;
+        for (uint32_t i = (uint32_t)(gw - a.n_cwaves) * 64 + threadIdx.x; i < n; i += kSpillBlocks * 64)
+            narrow_one(env, links, w, a.spill[i], n_sat);
     }
     if (w.stats && n_sat) atomicAdd(w.stats + 3, (unsigned long long)n_sat);
     if (w.stats && gw == 0 && threadIdx.x == 0) {
-        atomicAdd(w.stats + 5, (unsigned long long)b.ctl[1]);
-        atomicAdd(w.stats + 7, (unsigned long long)b.ctl[2]);
+        atomicAdd(w.stats + 5, (unsigned long long)a.ctl[1]);
+        atomicAdd(w.stats + 7, (unsigned long long)(a.ctl[2] < (uint32_t)a.spill_cap ? a.ctl[2] : a.spill_cap));
     }
 }
 
+// units decoded (stats only; the other stages count their own work)
+__global__ void k_count_units(CollideWork w) {
+    const int64_t u = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    int32_t link;
+    int64_t slot, edge;
+    const bool live = u < w.n_units && decode_unit(w, u, link, slot, edge);
+    const uint64_t m = __ballot(live);
+    if ((threadIdx.x & 63) == 0 && m) atomicAdd(w.stats + 0, (unsigned long long)__popcll(m));
+}
+
 CollideScratch::~CollideScratch() {
-    void *ps[] = {cand, seg_count, spill, ctl, ovf_list};
+    void *ps[] = {pairs, hdr, hdr_count, hdr_off, hdr_dense, scan_tmp, cand, cand_count, spill, ctl, ovf_list};
     for (void *p : ps)
         if (p) (void)hipFree(p);
 }
 
-void CollideScratch::ensure(int64_t n_units) {
-    if (!cand) {
+void CollideScratch::ensure(int64_t n_units, int32_t max_clusters) {
+    if (!ctl) {
         int dev = 0, cus = 256;
         if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-        n_blocks = cus * 4;  // 4 x 8 waves per CU: full occupancy if registers allow
-        n_waves = n_blocks * kBroadWaves;
-        seg_cap = kSegCap;
-        hip_check(hipMalloc(&cand, sizeof(Cand) * (size_t)n_waves * seg_cap), "alloc candidates");
-        hip_check(hipMalloc(&seg_count, sizeof(uint32_t) * n_waves), "alloc seg counts");
+        n_cwaves = cus * 16;  // k_cands: a resident grid striding over the headers
+        cand_cap = kCandCap;
         spill_cap = kSpillCap;
+        hip_check(hipMalloc(&cand, sizeof(Cand) * (size_t)n_cwaves * cand_cap), "alloc candidates");
+        hip_check(hipMalloc(&cand_count, sizeof(uint32_t) * (size_t)n_cwaves), "alloc candidate counts");
         hip_check(hipMalloc(&spill, sizeof(Cand) * (size_t)spill_cap), "alloc spill");
         hip_check(hipMalloc(&ctl, sizeof(uint32_t) * 4), "alloc collide ctl");
+    }
+    const int64_t segs = (n_units * (int64_t)(max_clusters > 0 ? max_clusters : 1) + 63) / 64;
+    if (segs > n_seg) {
+        if (segs * kHdrCap >= (int64_t(1) << 31)) throw Error{5, "collide batch too large"};
+        void *ps[] = {pairs, hdr, hdr_count, hdr_off, hdr_dense, scan_tmp};
+        for (void *p : ps)
+            if (p) hip_check(hipFree(p), "hipFree");
+        scan_tmp = nullptr;
+        pair_cap = kPairCap;
+        hip_check(hipMalloc(&pairs, sizeof(int32_t) * (size_t)segs * pair_cap), "alloc pairs");
+        hip_check(hipMalloc(&hdr, sizeof(PairHdr) * (size_t)segs * kHdrCap), "alloc headers");
+        hip_check(hipMalloc(&hdr_count, sizeof(uint32_t) * (size_t)(segs + 1)), "alloc header counts");
+        hip_check(hipMalloc(&hdr_off, sizeof(uint32_t) * (size_t)(segs + 1)), "alloc header offsets");
+        hip_check(hipMalloc(&hdr_dense, sizeof(int32_t) * (size_t)segs * kHdrCap), "alloc dense headers");
+        hip_check(hipMemset(hdr_count, 0, sizeof(uint32_t) * (size_t)(segs + 1)), "memset header counts");
+        scan_bytes = 0;
+        hip_check(hipcub::DeviceScan::ExclusiveSum(nullptr, scan_bytes, hdr_count, hdr_off, (int)(segs + 1)),
+                  "scan size");
+        hip_check(hipMalloc(&scan_tmp, scan_bytes), "alloc scan temp");
+        n_seg = segs;
     }
     if (n_units > ovf_cap) {
         if (ovf_list) hip_check(hipFree(ovf_list), "hipFree");
         ovf_list = nullptr;
-        hip_check(hipMalloc(&ovf_list, sizeof(int32_t) * (size_t)n_units), "alloc overflow list");
+        // a unit can be listed once per cluster (k_pairs) plus once per header (k_cands)
+        hip_check(hipMalloc(&ovf_list, sizeof(int32_t) * (size_t)n_units * (2 * max_clusters + 1)),
+                  "alloc overflow list");
         ovf_cap = n_units;
     }
 }
 
-void launch_collide_split(const EnvDev &env, const AgentDev *d_links, const CollideWork &w, CollideScratch &s,
-                          hipStream_t stream) {
+void launch_collide_split(const EnvDev &env, const AgentDev *d_links, int32_t max_clusters, const CollideWork &w,
+                          CollideScratch &s, hipStream_t stream) {
     if (w.n_units <= 0 || env.n_tris <= 0) return;
-    if (w.n_units >= (int64_t(1) << 31) || w.n_units > s.ovf_cap || !s.cand)
+    const int32_t C = max_clusters > 0 ? max_clusters : 1;
+    const int64_t threads = w.n_units * C;
+    const int64_t segs = (threads + 63) / 64;
+    if (threads >= (int64_t(1) << 31) || w.n_units > s.ovf_cap || segs > s.n_seg || !s.pairs)
         throw Error{5, "collide scratch not sized for this launch"};
-    BroadArgs b{s.cand, s.seg_count, s.spill, s.ctl, s.ovf_list, s.seg_cap, s.n_waves, s.spill_cap};
+    SplitArgs a{s.pairs, s.hdr,   s.hdr_count, s.hdr_off,   s.hdr_dense, s.cand, s.cand_count, s.spill, s.ctl,
+                s.ovf_list, segs, s.pair_cap, s.cand_cap, s.spill_cap, C,           s.n_cwaves};
     hip_check(hipMemsetAsync(s.ctl, 0, sizeof(uint32_t) * 4, stream), "collide ctl memset");
+    const unsigned pblocks = (unsigned)((threads + kPairThreads - 1) / kPairThreads);
     const int32_t n_items = env.lev_off[env.n_levels];
-    static const bool force_global = getenv("MPT_BROAD_GLOBAL") != nullptr;  // experiment knob
-    if (n_items <= kLdsItems && !force_global)
-        hipLaunchKernelGGL(k_broad<true>, dim3((unsigned)s.n_blocks), dim3(kBroadWaves * 64),
-                           sizeof(Item) * n_items, stream, env, d_links, w, b);
-    else
-        hipLaunchKernelGGL(k_broad<false>, dim3((unsigned)s.n_blocks), dim3(kBroadWaves * 64), 0, stream, env,
-                           d_links, w, b);
-    hip_check(hipGetLastError(), "k_broad launch");
-    hipLaunchKernelGGL(k_narrow, dim3((unsigned)(s.n_waves + kSpillBlocks)), dim3(64), 0, stream, env, d_links, w,
-                       b);
+    const bool lds = n_items <= kLdsItems;
+    const size_t lds_bytes = lds ? sizeof(Item) * n_items : 0;
+    if (env.n_levels <= 2) {
+        if (lds)
+            hipLaunchKernelGGL((k_pairs<true, true>), dim3(pblocks), dim3(kPairThreads), lds_bytes, stream, env,
+                               d_links, w, a);
+        else
+            hipLaunchKernelGGL((k_pairs<true, false>), dim3(pblocks), dim3(kPairThreads), 0, stream, env, d_links, w,
+                               a);
+    } else {
+        if (lds)
+            hipLaunchKernelGGL((k_pairs<false, true>), dim3(pblocks), dim3(kPairThreads), lds_bytes, stream, env,
+                               d_links, w, a);
+        else
+            hipLaunchKernelGGL((k_pairs<false, false>), dim3(pblocks), dim3(kPairThreads), 0, stream, env, d_links,
+                               w, a);
+    }
+    hip_check(hipGetLastError(), "k_pairs launch");
+    // count slot `segs` is the scan's sentinel (a larger earlier launch may have used it)
+    hip_check(hipMemsetAsync(s.hdr_count + segs, 0, sizeof(uint32_t), stream), "sentinel memset");
+    size_t tb = s.scan_bytes;
+    hip_check(hipcub::DeviceScan::ExclusiveSum(s.scan_tmp, tb, s.hdr_count, s.hdr_off, (int)(segs + 1), stream),
+              "header scan");
+    hipLaunchKernelGGL(k_expand, dim3((unsigned)((segs + 255) / 256)), dim3(256), 0, stream, s.hdr_count, s.hdr_off,
+                       segs, s.hdr_dense);
+    hip_check(hipGetLastError(), "k_expand launch");
+    hipLaunchKernelGGL(k_cands, dim3((unsigned)((s.n_cwaves + 3) / 4)), dim3(256), 0, stream, env, d_links, w, a);
+    hip_check(hipGetLastError(), "k_cands launch");
+    hipLaunchKernelGGL(k_narrow, dim3((unsigned)(s.n_cwaves + kSpillBlocks)), dim3(64), 0, stream, env, d_links, w,
+                       a);
     hip_check(hipGetLastError(), "k_narrow launch");
-    // units whose candidates overflowed segment and spill list (none in practice): fused
+    if (w.stats) {
+        hipLaunchKernelGGL(k_count_units, dim3((unsigned)((w.n_units + 255) / 256)), dim3(256), 0, stream, w);
+        hip_check(hipGetLastError(), "k_count_units launch");
+    }
+    // units that overflowed a pair segment or the spill list (none in practice): fused
     // path, list read on the device, a small grid so the usual empty launch costs little
     CollideWork f = w;
     f.unit_list = s.ovf_list;

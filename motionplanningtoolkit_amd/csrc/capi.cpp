@@ -21,7 +21,7 @@ static thread_local std::string g_last_error;
 std::string &last_error_ref() { return g_last_error; }
 static int g_device = -1;
 static thread_local bool g_stats_enabled = false;
-static thread_local unsigned long long g_last_stats[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+static thread_local unsigned long long g_last_stats[kCollideStats] = {};
 static std::atomic<int32_t> g_collide_mode{MPT_COLLIDE_SPLIT};
 int32_t collide_mode() { return g_collide_mode.load(std::memory_order_relaxed); }
 
@@ -188,9 +188,19 @@ Range subtree_range(const std::vector<BvhNode> &pre, int32_t id, std::vector<Ran
     memo[id] = r;
     return r;
 }
+// Bucket size of the broad-phase tree: small buckets keep bucket boxes tight for meshes of
+// large triangles (rooms), where a 64-triangle bucket spans several walls.
+int32_t env_bucket_size() {
+    static const int32_t s = [] {
+        const char *e = getenv("MPT_ENV_BUCKET");  // tuning knob
+        const int v = e ? atoi(e) : 0;
+        return v >= 1 && v <= kClusterMax ? v : kClusterMax;
+    }();
+    return s;
+}
 void collect_buckets(const std::vector<BvhNode> &pre, int32_t id, const std::vector<Range> &memo,
                      std::vector<Range> &out) {
-    if (memo[id].count <= kClusterMax) {
+    if (memo[id].count <= env_bucket_size()) {
         out.push_back(memo[id]);
         return;
     }
@@ -497,14 +507,16 @@ static void collide_common(const mpt_env *env, const mpt_agent *const *links, in
     w.verdict = d_verdict;
     w.stats = nullptr;
     if (g_stats_enabled) {
-        w.stats = (unsigned long long *)g_ws.stats.get(sizeof(unsigned long long) * 8);
-        hip_check(hipMemsetAsync(w.stats, 0, sizeof(unsigned long long) * 8, stream), "stats memset");
+        w.stats = (unsigned long long *)g_ws.stats.get(sizeof(g_last_stats));
+        hip_check(hipMemsetAsync(w.stats, 0, sizeof(g_last_stats), stream), "stats memset");
     }
     if (collide_mode() == MPT_COLLIDE_FUSED) {
         launch_collide(env->dev, d_links, w, stream);
     } else {
-        g_ws.cs.ensure(w.n_units);
-        launch_collide_split(env->dev, d_links, w, g_ws.cs, stream);
+        int32_t max_clusters = 1;
+        for (const AgentDev &a : lk) max_clusters = std::max(max_clusters, a.n_clusters);
+        g_ws.cs.ensure(w.n_units, max_clusters);
+        launch_collide_split(env->dev, d_links, max_clusters, w, g_ws.cs, stream);
     }
     if (w.stats) {
         hip_check(hipMemcpyAsync(g_last_stats, w.stats, sizeof(g_last_stats), hipMemcpyDeviceToHost, stream), "stats");

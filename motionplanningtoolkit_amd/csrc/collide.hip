@@ -174,22 +174,16 @@ __global__ __launch_bounds__(kCollideWaves * 64) void k_collide(EnvDev env, cons
     const bool shared_edges = w.pose_edge != nullptr || w.L > 1 || w.pmax > 1;
     uint32_t n_units = 0, n_clusters = 0, n_nodes = 0, n_sat = 0;
     const int64_t stride = (int64_t)gridDim.x * kCollideWaves;
-    const unsigned long long t0 = w.stats ? __builtin_amdgcn_s_memtime() : 0ull;
-    uint32_t max_nodes = 0;
     for (int64_t i = (int64_t)blockIdx.x * kCollideWaves + wave; i < n_work; i += stride) {
-        const uint32_t before = n_nodes;
         const int64_t unit = w.unit_list ? (int64_t)w.unit_list[i] : i;
         collide_unit(env, s_nodes, n_lds, links, w, unit, stk, lane, shared_edges, n_clusters, n_nodes, n_sat,
                      n_units);
-        max_nodes = max_nodes > n_nodes - before ? max_nodes : n_nodes - before;
     }
     if (w.stats && lane == 0) {
         atomicAdd(w.stats + 0, (unsigned long long)n_units);
         atomicAdd(w.stats + 1, (unsigned long long)n_clusters);
         atomicAdd(w.stats + 2, (unsigned long long)n_nodes);
         atomicAdd(w.stats + 3, (unsigned long long)n_sat);
-        atomicMax(w.stats + 4, (unsigned long long)max_nodes);
-        atomicAdd(w.stats + 6, __builtin_amdgcn_s_memtime() - t0);
     }
 }
 

@@ -21,6 +21,7 @@
 namespace mpt {
 
 constexpr int kWave = 64;
+constexpr int kCollideStats = 16;  // collide work counters (mpt_rrt_collide_stats)
 constexpr int kClusterMax = 64;
 constexpr int kStackDepth = 64;
 
@@ -100,32 +101,52 @@ struct Cand {
     int32_t etri;
 };
 
-// Device scratch of the two-phase collide path: one fixed candidate segment per
-// broad-phase wave (no atomics on the candidate path), a unit work queue and the list
-// of units whose candidates did not fit (re-run by the fused kernel).
+// (unit, agent cluster) whose box overlaps n env triangles' boxes; the triangle indices
+// are pairs[p0, p0 + n) of the same wave segment.
+struct PairHdr {
+    int32_t unit;
+    int32_t cluster;
+    int32_t p0;      // absolute index into pairs
+    int32_t n;
+    int32_t tfirst;  // the cluster's agent triangles
+    int32_t tcount;
+    int32_t pad[2];
+};
+
+// Device scratch of the two-phase collide path (broad.hip).  Every stage writes to fixed
+// per-wave segments (no device-wide atomics on the hot path); what does not fit goes to
+// the shared spill list, and units that overflow even that are re-run by the fused kernel.
 struct CollideScratch {
-    Cand *cand = nullptr;        // [n_waves][seg_cap]
-    uint32_t *seg_count = nullptr;  // [n_waves]
-    Cand *spill = nullptr;       // [spill_cap] shared overflow of full segments (atomic)
-    uint32_t *ctl = nullptr;     // [0] unit queue, [1] overflow units, [2] spill count
-    int32_t *ovf_list = nullptr; // [ovf_cap]
-    int64_t ovf_cap = 0;
-    int32_t n_waves = 0, seg_cap = 0, n_blocks = 0, spill_cap = 0;
+    int32_t *pairs = nullptr;       // [n_seg][pair_cap]   env triangle per (unit, cluster) pair
+    PairHdr *hdr = nullptr;         // [n_seg][64]
+    uint32_t *hdr_count = nullptr;  // [n_seg + 1], exclusive-scanned into hdr_off
+    uint32_t *hdr_off = nullptr;    // [n_seg + 1]
+    int32_t *hdr_dense = nullptr;   // [n_seg * 64] header slots in dense order
+    void *scan_tmp = nullptr;
+    size_t scan_bytes = 0;
+    Cand *cand = nullptr;           // [n_cwaves][cand_cap]
+    uint32_t *cand_count = nullptr; // [n_cwaves]
+    Cand *spill = nullptr;          // [spill_cap] shared overflow of full candidate segments
+    uint32_t *ctl = nullptr;        // [1] overflow units, [2] spill count
+    int32_t *ovf_list = nullptr;    // [ovf_cap]
+    int64_t ovf_cap = 0, n_seg = 0;
+    int32_t pair_cap = 0, cand_cap = 0, spill_cap = 0, n_cwaves = 0;
     CollideScratch() = default;
     CollideScratch(const CollideScratch &) = delete;
     CollideScratch &operator=(const CollideScratch &) = delete;
     ~CollideScratch();
-    void ensure(int64_t n_units);  // allocates on first use / growth (not stream-ordered)
+    // allocates on first use / growth (not stream-ordered); max_clusters over the links
+    void ensure(int64_t n_units, int32_t max_clusters);
 };
 
 // Fused single-kernel path (one wave per unit, BVH walk + SAT at the leaves).
 // max_blocks > 0 caps the grid (list mode re-runs, usually empty).
 void launch_collide(const EnvDev &env, const AgentDev *d_links, const CollideWork &w,
                     hipStream_t stream, int max_blocks = 0);
-// Two-phase path: k_broad (float box traversal, candidates) -> k_narrow (17-axis SAT per
-// candidate) -> fused kernel over overflowed units.  s.ensure(w.n_units) must have run.
-void launch_collide_split(const EnvDev &env, const AgentDev *d_links, const CollideWork &w, CollideScratch &s,
-                          hipStream_t stream);
+// Two-phase path (broad.hip): k_pairs -> k_cands -> k_narrow -> fused kernel over
+// overflowed units.  s.ensure(w.n_units, max_clusters) must have run with the same value.
+void launch_collide_split(const EnvDev &env, const AgentDev *d_links, int32_t max_clusters, const CollideWork &w,
+                          CollideScratch &s, hipStream_t stream);
 void launch_pose_edge(const int64_t *d_offsets, int64_t E, int32_t *d_pose_edge, hipStream_t stream);
 
 // ---------------- NN ----------------

@@ -324,6 +324,7 @@ struct mpt_rrt {
     // optional collision work counters (k_collide atomics): units, clusters, node visits, tri tests
     bool stats_on = false;
     CollideScratch cscratch;
+    int32_t max_clusters = 1;
     unsigned long long *d_cstats = nullptr;
 };
 
@@ -353,7 +354,7 @@ void ensure_round_buffers(mpt_rrt *r, int32_t K) {
         hip_check(hipMalloc(&r->d_bcount, sizeof(int32_t) * ((K + 255) / 256)), "alloc bcount");
         hip_check(hipMalloc(&r->d_verdict, (size_t)K), "alloc verdict");
         r->kcap = K;
-        r->cscratch.ensure((int64_t)K * r->p.pmax * r->p.L);
+        r->cscratch.ensure((int64_t)K * r->p.pmax * r->p.L, r->max_clusters);
     }
     // the split count depends on n, so size the NN scratch for the capacity bound
     if (need_scratch > r->scratch_bytes) {
@@ -403,6 +404,7 @@ extern "C" mpt_status mpt_rrt_create(const mpt_env *env, const mpt_agent *agent,
             if ((int64_t)p.pmax * p.L > 4096) throw Error{MPT_ERR_INVALID, "too many poses per edge"};
             r->env = env_dev(env);
             std::vector<AgentDev> links(p.L, agent_dev(agent));
+            r->max_clusters = std::max(1, agent_dev(agent).n_clusters);
             hip_check(hipMalloc(&r->d_links, sizeof(AgentDev) * p.L), "alloc links");
             hip_check(hipMemcpy(r->d_links, links.data(), sizeof(AgentDev) * p.L, hipMemcpyHostToDevice), "links");
             r->cap = capacity;
@@ -527,7 +529,7 @@ extern "C" mpt_status mpt_rrt_step(mpt_rrt *r, int32_t K, void *stream_) {
         if (collide_mode() == MPT_COLLIDE_FUSED) {
             launch_collide(r->env, r->d_links, cw, stream);
         } else {
-            launch_collide_split(r->env, r->d_links, cw, r->cscratch, stream);
+            launch_collide_split(r->env, r->d_links, r->max_clusters, cw, r->cscratch, stream);
         }
         mark(5);
         hipLaunchKernelGGL(k_count, dim3(kb), dim3(256), 0, stream, r->d_verdict, K, r->d_bcount);
@@ -600,20 +602,20 @@ extern "C" mpt_status mpt_rrt_info(const mpt_rrt *r, int64_t info[4]) {
     });
 }
 
-extern "C" mpt_status mpt_rrt_collide_stats(mpt_rrt *r, int32_t enable, uint64_t out[8]) {
+extern "C" mpt_status mpt_rrt_collide_stats(mpt_rrt *r, int32_t enable, uint64_t out[kCollideStats]) {
     return guarded([&] {
         if (!r) throw Error{MPT_ERR_INVALID, "null pointer"};
         hip_check(hipDeviceSynchronize(), "sync");
         if (!r->d_cstats) {
-            hip_check(hipMalloc(&r->d_cstats, sizeof(unsigned long long) * 8), "alloc stats");
-            hip_check(hipMemset(r->d_cstats, 0, sizeof(unsigned long long) * 8), "memset stats");
+            hip_check(hipMalloc(&r->d_cstats, sizeof(unsigned long long) * kCollideStats), "alloc stats");
+            hip_check(hipMemset(r->d_cstats, 0, sizeof(unsigned long long) * kCollideStats), "memset stats");
         }
         if (out) {
-            unsigned long long h[8];
+            unsigned long long h[kCollideStats];
             hip_check(hipMemcpy(h, r->d_cstats, sizeof(h), hipMemcpyDeviceToHost), "stats D2H");
-            for (int i = 0; i < 8; ++i) out[i] = h[i];
+            for (int i = 0; i < kCollideStats; ++i) out[i] = h[i];
         }
-        hip_check(hipMemset(r->d_cstats, 0, sizeof(unsigned long long) * 8), "memset stats");
+        hip_check(hipMemset(r->d_cstats, 0, sizeof(unsigned long long) * kCollideStats), "memset stats");
         r->stats_on = enable != 0;
     });
 }

@@ -6,6 +6,5 @@ run() {  # tag env...
   local tag=$1; shift
   env "$@" timeout -k 10 240 python3 $R/bench.py --steps 10 --warmup 2 --no-cpu > $R/gpurun_out/diag_$tag.json 2> $R/gpurun_out/diag_$tag.err || exit $?
 }
-run split
-run perlane MPT_NN1_PER_LANE=1
+run ${TAG:-cur}
 echo ok
