@@ -40,6 +40,7 @@ struct SplitArgs {
     int32_t *pairs;
     PairHdr *hdr;
     uint32_t *hdr_count;
+    uint32_t *pair_count;
     const uint32_t *hdr_off;
     int32_t *hdr_dense;
     Cand *cand;
@@ -194,24 +195,29 @@ __global__ __launch_bounds__(kPairThreads) void k_pairs(EnvDev env, const AgentD
     }
     uint4 *stk = s_stk + (kTwo ? 0 : threadIdx.x * kStack);
     uint32_t np = 0, tests = 0;
-    if (live) tests = walk_tree<kTwo>(env, items, lo, hi, stk, [&](int32_t) { ++np; });
     bool ovf = false;
-    if (np > 0) {
-        const uint32_t p0 = atomicAdd(&s_pc[wave], np);
-        if (p0 + np > (uint32_t)a.pair_cap) {
-            ovf = true;
-        } else {
-            int32_t *out = a.pairs + seg * a.pair_cap + p0;
-            uint32_t k = 0;
-            walk_tree<kTwo>(env, items, lo, hi, stk, [&](int32_t tri) { out[k++] = tri; });
-            const uint32_t h = atomicAdd(&s_hc[wave], 1u);
-            a.hdr[seg * kHdrCap + h] =
-                PairHdr{(int32_t)unit, c, (int32_t)(seg * a.pair_cap + p0), (int32_t)np, tfirst, tcount, {0, 0}};
-        }
+    int32_t *out = a.pairs + seg * a.pair_cap;
+    // one pass: each pair takes the next slot of the wave's segment (LDS atomic) as a
+    // (lane, triangle) word; k_cands picks a header's pairs out by lane
+    if (live)
+        tests = walk_tree<kTwo>(env, items, lo, hi, stk, [&](int32_t tri) {
+            const uint32_t pos = atomicAdd(&s_pc[wave], 1u);
+            if (pos < (uint32_t)a.pair_cap)
+                out[pos] = (int32_t)(((uint32_t)lane << kPairTriBits) | (uint32_t)tri);
+            else
+                ovf = true;
+            ++np;
+        });
+    if (np > 0 && !ovf) {
+        const uint32_t h = atomicAdd(&s_hc[wave], 1u);
+        a.hdr[seg * kHdrCap + h] = PairHdr{(int32_t)unit, c, (int32_t)seg, (int32_t)np, tfirst, tcount, lane, 0};
     }
     if (ovf) a.ovf_list[atomicAdd(a.ctl + 1, 1u)] = (int32_t)unit;  // rare: fused re-run
     __builtin_amdgcn_wave_barrier();
-    if (lane == 0 && seg < a.n_seg) a.hdr_count[seg] = s_hc[wave];
+    if (lane == 0 && seg < a.n_seg) {
+        a.hdr_count[seg] = s_hc[wave];
+        a.pair_count[seg] = s_pc[wave] < (uint32_t)a.pair_cap ? s_pc[wave] : (uint32_t)a.pair_cap;
+    }
     if (w.stats) {
         const uint64_t lm = __ballot(live);
         uint32_t sum_tests = tests, sum_pairs = np;
@@ -268,10 +274,12 @@ __global__ __launch_bounds__(256) void k_cands(EnvDev env, const AgentDev *__res
         const int32_t slot_h = __builtin_amdgcn_readfirstlane(a.hdr_dense[g]);
         const PairHdr H = a.hdr[slot_h];
         const int32_t unit = __builtin_amdgcn_readfirstlane(H.unit);
-        const int32_t p0 = __builtin_amdgcn_readfirstlane(H.p0);
-        const int32_t np = __builtin_amdgcn_readfirstlane(H.n);
+        const int32_t hseg = __builtin_amdgcn_readfirstlane(H.seg);
+        const int32_t hlane = __builtin_amdgcn_readfirstlane(H.lane);
         const int32_t tfirst = __builtin_amdgcn_readfirstlane(H.tfirst);
         const int32_t tcount = __builtin_amdgcn_readfirstlane(H.tcount);
+        const int32_t sp = __builtin_amdgcn_readfirstlane(a.pair_count[hseg]);
+        const int32_t *spairs = a.pairs + (int64_t)hseg * a.pair_cap;
         int32_t link;
         int64_t slot, edge;
         decode_unit(w, unit, link, slot, edge);
@@ -283,25 +291,27 @@ __global__ __launch_bounds__(256) void k_cands(EnvDev env, const AgentDev *__res
         for (int i = 0; i < 9; ++i) R[i] = uniform_d(R[i]);
 #pragma unroll
         for (int i = 0; i < 3; ++i) T[i] = uniform_d(T[i]);
-        for (int32_t k0 = 0; k0 < np; k0 += 64) {
-            // lanes fetch up to 64 of the header's env triangle boxes
-            const int32_t nk = np - k0 < 64 ? np - k0 : 64;
+        float blo[3] = {0, 0, 0}, bhi[3] = {0, 0, 0}, tlo[3], thi[3];
+        if (act) agent_tri_box(tri, R, T, blo, bhi);
+        ++n_xf;
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            tlo[k] = wave_min(act ? blo[k] : __builtin_huge_valf());
+            thi[k] = wave_max(act ? bhi[k] : -__builtin_huge_valf());
+        }
+        for (int32_t k0 = 0; k0 < sp; k0 += 64) {
+            // lanes scan 64 words of the segment; this header's are those of its lane
+            bool mine = false;
             int32_t etri = 0;
             Item e{};
-            if (lane < nk) {
-                etri = a.pairs[p0 + k0 + lane];
-                e = env.items[etri];
-            }
-            float blo[3] = {0, 0, 0}, bhi[3] = {0, 0, 0}, tlo[3], thi[3];
-            if (act) agent_tri_box(tri, R, T, blo, bhi);
-            if (k0 == 0) ++n_xf;
-#pragma unroll
-            for (int k = 0; k < 3; ++k) {
-                tlo[k] = wave_min(act ? blo[k] : __builtin_huge_valf());
-                thi[k] = wave_max(act ? bhi[k] : -__builtin_huge_valf());
+            if (k0 + lane < sp) {
+                const uint32_t word = (uint32_t)spairs[k0 + lane];
+                mine = (int32_t)(word >> kPairTriBits) == hlane;
+                etri = (int32_t)(word & ((1u << kPairTriBits) - 1u));
+                if (mine) e = env.items[etri];
             }
             // env triangles that miss the union of the agent triangle boxes are dropped
-            uint64_t M = __ballot(lane < nk && box_overlap(tlo, thi, e.lo, e.hi));
+            uint64_t M = __ballot(mine && box_overlap(tlo, thi, e.lo, e.hi));
             bool ok = true;
             while (M && ok) {
                 const int j = __ffsll((unsigned long long)M) - 1;
@@ -374,7 +384,8 @@ __global__ void k_count_units(CollideWork w) {
 }
 
 CollideScratch::~CollideScratch() {
-    void *ps[] = {pairs, hdr, hdr_count, hdr_off, hdr_dense, scan_tmp, cand, cand_count, spill, ctl, ovf_list};
+    void *ps[] = {pairs, hdr, hdr_count, pair_count, hdr_off, hdr_dense, scan_tmp, cand, cand_count, spill, ctl,
+                  ovf_list};
     for (void *p : ps)
         if (p) (void)hipFree(p);
 }
@@ -394,7 +405,7 @@ void CollideScratch::ensure(int64_t n_units, int32_t max_clusters) {
     const int64_t segs = (n_units * (int64_t)(max_clusters > 0 ? max_clusters : 1) + 63) / 64;
     if (segs > n_seg) {
         if (segs * kHdrCap >= (int64_t(1) << 31)) throw Error{5, "collide batch too large"};
-        void *ps[] = {pairs, hdr, hdr_count, hdr_off, hdr_dense, scan_tmp};
+        void *ps[] = {pairs, hdr, hdr_count, pair_count, hdr_off, hdr_dense, scan_tmp};
         for (void *p : ps)
             if (p) hip_check(hipFree(p), "hipFree");
         scan_tmp = nullptr;
@@ -402,6 +413,7 @@ void CollideScratch::ensure(int64_t n_units, int32_t max_clusters) {
         hip_check(hipMalloc(&pairs, sizeof(int32_t) * (size_t)segs * pair_cap), "alloc pairs");
         hip_check(hipMalloc(&hdr, sizeof(PairHdr) * (size_t)segs * kHdrCap), "alloc headers");
         hip_check(hipMalloc(&hdr_count, sizeof(uint32_t) * (size_t)(segs + 1)), "alloc header counts");
+        hip_check(hipMalloc(&pair_count, sizeof(uint32_t) * (size_t)segs), "alloc pair counts");
         hip_check(hipMalloc(&hdr_off, sizeof(uint32_t) * (size_t)(segs + 1)), "alloc header offsets");
         hip_check(hipMalloc(&hdr_dense, sizeof(int32_t) * (size_t)segs * kHdrCap), "alloc dense headers");
         hip_check(hipMemset(hdr_count, 0, sizeof(uint32_t) * (size_t)(segs + 1)), "memset header counts");
@@ -429,7 +441,8 @@ void launch_collide_split(const EnvDev &env, const AgentDev *d_links, int32_t ma
     const int64_t segs = (threads + 63) / 64;
     if (threads >= (int64_t(1) << 31) || w.n_units > s.ovf_cap || segs > s.n_seg || !s.pairs)
         throw Error{5, "collide scratch not sized for this launch"};
-    SplitArgs a{s.pairs, s.hdr,   s.hdr_count, s.hdr_off,   s.hdr_dense, s.cand, s.cand_count, s.spill, s.ctl,
+    if (env.n_tris >= (1 << kPairTriBits)) throw Error{5, "env too large for the split collide path"};
+    SplitArgs a{s.pairs, s.hdr,   s.hdr_count, s.pair_count, s.hdr_off, s.hdr_dense, s.cand, s.cand_count, s.spill, s.ctl,
                 s.ovf_list, segs, s.pair_cap, s.cand_cap, s.spill_cap, C,           s.n_cwaves};
     hip_check(hipMemsetAsync(s.ctl, 0, sizeof(uint32_t) * 4, stream), "collide ctl memset");
     const unsigned pblocks = (unsigned)((threads + kPairThreads - 1) / kPairThreads);

@@ -103,15 +103,19 @@ struct Cand {
 
 // (unit, agent cluster) whose box overlaps n env triangles' boxes; the triangle indices
 // are pairs[p0, p0 + n) of the same wave segment.
+// Pairs are packed (lane << 26 | env triangle) words in the k_pairs wave's segment, in
+// append order; a header names its lane.
 struct PairHdr {
     int32_t unit;
     int32_t cluster;
-    int32_t p0;      // absolute index into pairs
-    int32_t n;
+    int32_t seg;     // k_pairs wave segment holding the pairs
+    int32_t n;       // pairs of this (unit, cluster)
     int32_t tfirst;  // the cluster's agent triangles
     int32_t tcount;
-    int32_t pad[2];
+    int32_t lane;    // k_pairs lane that made them
+    int32_t pad;
 };
+constexpr int kPairTriBits = 26;  // env triangles per env < 2^26 on the split path
 
 // Device scratch of the two-phase collide path (broad.hip).  Every stage writes to fixed
 // per-wave segments (no device-wide atomics on the hot path); what does not fit goes to
@@ -120,6 +124,7 @@ struct CollideScratch {
     int32_t *pairs = nullptr;       // [n_seg][pair_cap]   env triangle per (unit, cluster) pair
     PairHdr *hdr = nullptr;         // [n_seg][64]
     uint32_t *hdr_count = nullptr;  // [n_seg + 1], exclusive-scanned into hdr_off
+    uint32_t *pair_count = nullptr; // [n_seg] pairs written per segment
     uint32_t *hdr_off = nullptr;    // [n_seg + 1]
     int32_t *hdr_dense = nullptr;   // [n_seg * 64] header slots in dense order
     void *scan_tmp = nullptr;
