@@ -194,7 +194,7 @@ int32_t env_bucket_size() {
     static const int32_t s = [] {
         const char *e = getenv("MPT_ENV_BUCKET");  // tuning knob
         const int v = e ? atoi(e) : 0;
-        return v >= 1 && v <= kClusterMax ? v : kClusterMax;
+        return v >= 1 && v <= kClusterMax ? v : 16;
     }();
     return s;
 }
@@ -738,8 +738,7 @@ static void nn_query(mpt_nn *nn, const double *d_q, int64_t nq, int32_t k, int32
     }
     GridDev G = nn->grid->dev();
     G.removed = nn->d_removed;
-    const int32_t *ord = nq >= kSortQueries ? nn->grid->order_queries(d_q, nq, nn->d, stream) : nullptr;
-    launch_grid_knn(G, nn->d, d_q, nq, k, d_ids, d_d2, stream, ord);
+    launch_grid_knn(G, nn->d, d_q, nq, k, d_ids, d_d2, stream);
 }
 
 extern "C" mpt_status mpt_nn_set_index(mpt_nn *nn, int32_t mode) {

@@ -34,17 +34,9 @@ public:
                hipStream_t stream);
     GridDev dev() const;
     const GridParams &params() const { return g; }
-    // Permutation of queries q [nq][d] sorted by grid cell (radix sort on the cell id), so
-    // that neighbouring lanes of k_grid_knn walk the same cells.  Valid until the next call.
-    const int32_t *order_queries(const double *q, int64_t nq, int32_t d, hipStream_t stream);
 
 private:
     void reserve(int64_t cap_pts, int32_t d, int64_t ncells);
-    int64_t q_cap = 0;
-    uint32_t *qkey = nullptr, *qkey_sorted = nullptr;
-    int32_t *qidx = nullptr, *qorder = nullptr;
-    void *qtemp = nullptr;
-    size_t qtemp_bytes = 0;
     GridParams g{};
     int64_t n_max = 0, pts_cap = 0, cells_cap = 0;
     int32_t dim = 0;
@@ -54,11 +46,8 @@ private:
     size_t temp_bytes = 0;
 };
 
-constexpr int64_t kSortQueries = 4096;  // query batches at least this large are cell-sorted first
-
-// order (optional, from GridIndex::order_queries): thread i answers query order[i].
 void launch_grid_knn(const GridDev &G, int32_t d, const double *q, int64_t nq, int32_t k, int32_t *ids, double *d2,
-                     hipStream_t stream, const int32_t *order = nullptr);
+                     hipStream_t stream);
 
 // Per-dim [min, max] of pts[0, n) into d_out[2*d] (lo0, hi0, lo1, hi1, ...).
 void launch_bbox(const double *pts, int64_t n, int32_t d, double *d_out, hipStream_t stream);

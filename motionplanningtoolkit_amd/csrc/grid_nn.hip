@@ -55,16 +55,6 @@ __global__ void k_grid_scatter(const double *__restrict__ pts, int32_t d, int64_
     sids[pos] = (int32_t)(i + 1);
 }
 
-__global__ void k_query_cells(GridParams g, const double *__restrict__ q, int32_t d, int64_t nq,
-                              uint32_t *__restrict__ key, int32_t *__restrict__ idx) {
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= nq) return;
-    int c[3] = {0, 0, 0};
-    for (int j = 0; j < g.gd; ++j) c[j] = cell_coord(q[i * d + g.dims[j]], g.lo[j], g.inv_h, g.n[j]);
-    key[i] = (uint32_t)((c[0] * g.n[1] + c[1]) * g.n[2] + c[2]);
-    idx[i] = (int32_t)i;
-}
-
 template <int KMAX>
 __device__ __forceinline__ void grid_push(double (&bd)[KMAX], int32_t (&bi)[KMAX], int32_t k, double dd, int32_t id) {
     bool done = false;
@@ -109,12 +99,11 @@ __device__ __forceinline__ double ring_bound(const GridParams &g, const double *
 
 template <int D, int KMAX>
 __global__ __launch_bounds__(256) void k_grid_knn(GridDev G, int32_t d, const double *__restrict__ q, int64_t nq,
-                                                  int32_t k, int32_t *__restrict__ out_ids, double *__restrict__ out_d2,
-                                                  const int32_t *__restrict__ order) {
+                                                  int32_t k, int32_t *__restrict__ out_ids, double *__restrict__ out_d2) {
     constexpr int DD = D > 0 ? D : 16;
     const int64_t ti = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (ti >= nq) return;
-    const int64_t qi = order ? (int64_t)order[ti] : ti;
+    const int64_t qi = ti;
     const GridParams &g = G.g;
     const int dim = D > 0 ? D : d;
     double qq[DD];
@@ -253,7 +242,7 @@ void GridIndex::reserve(int64_t cap_pts, int32_t d, int64_t ncells) {
 }
 
 GridIndex::~GridIndex() {
-    void *ps[] = {spts, sids, cell_of, counts, cell_start, temp, qkey, qkey_sorted, qidx, qorder, qtemp};
+    void *ps[] = {spts, sids, cell_of, counts, cell_start, temp};
     for (void *p : ps)
         if (p) (void)hipFree(p);
 }
@@ -343,19 +332,16 @@ int32_t choose_grid_dims(int32_t d, const double *lohi, int32_t dims[3]) {
 // (d2, id) order by xor-shuffles before the ring bound test, which is group-uniform.
 // Sixteen times more waves than k_grid_knn, so the dependent cell_start -> point loads
 // are hidden by occupancy instead of exposed one query per lane.
-constexpr int kGroup = 16;
-
-template <int D>
+template <int D, int kGroup>
 __global__ __launch_bounds__(256) void k_grid_nn1_group(GridDev G, int32_t d, const double *__restrict__ q,
                                                         int64_t nq, int32_t *__restrict__ out_ids,
-                                                        double *__restrict__ out_d2,
-                                                        const int32_t *__restrict__ order) {
+                                                        double *__restrict__ out_d2) {
     constexpr int DD = D > 0 ? D : 16;
     const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int64_t slot = t / kGroup;
     const int sub = (int)(t % kGroup);
     if (slot >= nq) return;  // whole groups leave together (nq is per group)
-    const int64_t qi = order ? (int64_t)order[slot] : slot;
+    const int64_t qi = slot;
     const GridParams &g = G.g;
     const int dim = D > 0 ? D : d;
     double qq[DD];
@@ -388,6 +374,19 @@ __global__ __launch_bounds__(256) void k_grid_nn1_group(GridDev G, int32_t d, co
                 inside = inside && cc[j] >= 0 && cc[j] < g.n[j];
             }
             if (!inside) continue;
+            if (r > 0) {
+                // skip a cell whose box is farther than the best so far: lb2 sums the
+                // (slack-reduced) gaps along the grid dims; border cells are open outward
+                double lb2 = 0.0;
+                for (int j = 0; j < g.gd; ++j) {
+                    const double clo = cc[j] == 0 ? -__builtin_huge_val() : g.lo[j] + (double)cc[j] * g.h;
+                    const double chi = cc[j] == g.n[j] - 1 ? __builtin_huge_val() : g.lo[j] + (double)(cc[j] + 1) * g.h;
+                    const double gap = fmax(fmax(clo - qg[j], qg[j] - chi), 0.0) - g.slack;
+                    if (gap > 0.0) lb2 += gap * gap;
+                }
+                // the 1e-12 shrink covers the different summation order of FLANN's distance
+                if (lb2 * (1.0 - 1e-12) > bd) continue;
+            }
             const int32_t cell = (cc[0] * g.n[1] + cc[1]) * g.n[2] + cc[2];
             const int32_t s = G.cell_start[cell], e = G.cell_start[cell + 1];
             for (int32_t p = s; p < e; ++p) {
@@ -422,63 +421,41 @@ __global__ __launch_bounds__(256) void k_grid_nn1_group(GridDev G, int32_t d, co
 
 template <int D>
 static void grid_knn_d(const GridDev &G, int32_t d, const double *q, int64_t nq, int32_t k, int32_t *ids, double *d2,
-                       hipStream_t stream, const int32_t *order) {
+                       hipStream_t stream) {
     const dim3 grid((unsigned)((nq + 255) / 256));
     static const bool per_lane = getenv("MPT_NN1_PER_LANE") != nullptr;  // experiment knob
-    if (k == 1 && !per_lane)
-        hipLaunchKernelGGL((k_grid_nn1_group<D>), dim3((unsigned)((nq * kGroup + 255) / 256)), dim3(256), 0, stream,
-                           G, d, q, nq, ids, d2, order);
+    static const int group = getenv("MPT_NN1_GROUP") ? atoi(getenv("MPT_NN1_GROUP")) : 16;
+    if (k == 1 && !per_lane && group == 64)
+        hipLaunchKernelGGL((k_grid_nn1_group<D, 64>), dim3((unsigned)((nq * 64 + 255) / 256)), dim3(256), 0, stream, G,
+                           d, q, nq, ids, d2);
+    else if (k == 1 && !per_lane && group == 32)
+        hipLaunchKernelGGL((k_grid_nn1_group<D, 32>), dim3((unsigned)((nq * 32 + 255) / 256)), dim3(256), 0, stream, G,
+                           d, q, nq, ids, d2);
+    else if (k == 1 && !per_lane && group == 8)
+        hipLaunchKernelGGL((k_grid_nn1_group<D, 8>), dim3((unsigned)((nq * 8 + 255) / 256)), dim3(256), 0, stream, G,
+                           d, q, nq, ids, d2);
+    else if (k == 1 && !per_lane)
+        hipLaunchKernelGGL((k_grid_nn1_group<D, 16>), dim3((unsigned)((nq * 16 + 255) / 256)), dim3(256), 0, stream, G,
+                           d, q, nq, ids, d2);
     else if (k == 1)
-        hipLaunchKernelGGL((k_grid_knn<D, 1>), grid, dim3(256), 0, stream, G, d, q, nq, k, ids, d2, order);
+        hipLaunchKernelGGL((k_grid_knn<D, 1>), grid, dim3(256), 0, stream, G, d, q, nq, k, ids, d2);
     else if (k <= 16)
-        hipLaunchKernelGGL((k_grid_knn<D, 16>), grid, dim3(256), 0, stream, G, d, q, nq, k, ids, d2, order);
+        hipLaunchKernelGGL((k_grid_knn<D, 16>), grid, dim3(256), 0, stream, G, d, q, nq, k, ids, d2);
     else
-        hipLaunchKernelGGL((k_grid_knn<D, 32>), grid, dim3(256), 0, stream, G, d, q, nq, k, ids, d2, order);
+        hipLaunchKernelGGL((k_grid_knn<D, 32>), grid, dim3(256), 0, stream, G, d, q, nq, k, ids, d2);
 }
 
 void launch_grid_knn(const GridDev &G, int32_t d, const double *q, int64_t nq, int32_t k, int32_t *ids, double *d2,
-                     hipStream_t stream, const int32_t *order) {
+                     hipStream_t stream) {
     if (nq <= 0) return;
     switch (d) {
-        case 3: grid_knn_d<3>(G, d, q, nq, k, ids, d2, stream, order); break;
-        case 7: grid_knn_d<7>(G, d, q, nq, k, ids, d2, stream, order); break;
-        case 15: grid_knn_d<15>(G, d, q, nq, k, ids, d2, stream, order); break;
-        default: grid_knn_d<0>(G, d, q, nq, k, ids, d2, stream, order); break;
+        case 3: grid_knn_d<3>(G, d, q, nq, k, ids, d2, stream); break;
+        case 7: grid_knn_d<7>(G, d, q, nq, k, ids, d2, stream); break;
+        case 15: grid_knn_d<15>(G, d, q, nq, k, ids, d2, stream); break;
+        default: grid_knn_d<0>(G, d, q, nq, k, ids, d2, stream); break;
     }
     hip_check(hipGetLastError(), "k_grid_knn launch");
 }
 
-const int32_t *GridIndex::order_queries(const double *q, int64_t nq, int32_t d, hipStream_t stream) {
-    if (nq <= 0) return nullptr;
-    if (nq >= (int64_t(1) << 31)) throw Error{5, "too many queries"};
-    if (nq > q_cap) {
-        void *ps[] = {qkey, qkey_sorted, qidx, qorder};
-        for (void *p : ps)
-            if (p) hip_check(hipFree(p), "free");
-        hip_check(hipMalloc(&qkey, sizeof(uint32_t) * nq), "qkey");
-        hip_check(hipMalloc(&qkey_sorted, sizeof(uint32_t) * nq), "qkey sorted");
-        hip_check(hipMalloc(&qidx, sizeof(int32_t) * nq), "qidx");
-        hip_check(hipMalloc(&qorder, sizeof(int32_t) * nq), "qorder");
-        q_cap = nq;
-    }
-    int end_bit = 1;
-    while (end_bit < 32 && (int64_t(1) << end_bit) < g.ncells) ++end_bit;
-    size_t tb = 0;
-    hip_check(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, qkey, qkey_sorted, qidx, qorder, (int)nq, 0, end_bit,
-                                                 stream),
-              "sort size");
-    if (tb > qtemp_bytes) {
-        if (qtemp) hip_check(hipFree(qtemp), "free");
-        hip_check(hipMalloc(&qtemp, tb), "sort temp");
-        qtemp_bytes = tb;
-    }
-    hipLaunchKernelGGL(k_query_cells, dim3((unsigned)((nq + 255) / 256)), dim3(256), 0, stream, g, q, d, nq, qkey,
-                       qidx);
-    hip_check(hipGetLastError(), "k_query_cells");
-    hip_check(hipcub::DeviceRadixSort::SortPairs(qtemp, tb, qkey, qkey_sorted, qidx, qorder, (int)nq, 0, end_bit,
-                                                 stream),
-              "sort");
-    return qorder;
-}
 
 }  // namespace mpt

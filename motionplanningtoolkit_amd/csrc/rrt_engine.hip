@@ -497,9 +497,7 @@ extern "C" mpt_status mpt_rrt_step(mpt_rrt *r, int32_t K, void *stream_) {
         }
         mark(2);
         if (use_grid) {
-            // large rounds: answer the samples in cell order (coherent cell walks per wave)
-            const int32_t *ord = K >= kSortQueries ? r->grid->order_queries(r->d_samples, K, p.d, stream) : nullptr;
-            launch_grid_knn(r->grid->dev(), p.d, r->d_samples, K, 1, r->d_nn, r->d_nnd2, stream, ord);
+            launch_grid_knn(r->grid->dev(), p.d, r->d_samples, K, 1, r->d_nn, r->d_nnd2, stream);
         } else {
             NNWork w{};
             w.pts = r->d_nodes;
