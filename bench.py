@@ -81,33 +81,61 @@ def cpu_baseline(sc, tree, K_gpu, seed, target_s):
     }
 
 
-def roofline(per_launch, cst, K, n0, d, nn_mode):
-    """Roofline of the round's dominant kernel: achieved = algorithmic work of
-    one launch (SURVEY 8(d) per-unit figures x the units the launch processed) / its
-    hipEvent-measured duration."""
-    dominant = max(("nn_build", "nn_query", "collide", "steer", "append", "sample"),
-                   key=lambda k: per_launch.get(k, 0.0))
-    ms = per_launch[dominant]
-    if dominant == "collide":
-        # bytes per (pose, link) unit = 96 (pose) + 32 per BVH node visit + 144 per triangle-pair test
-        nbytes = 96.0 * cst["units"] + 32.0 * cst["node_tests"] + 144.0 * cst["tri_tests"]
-        flops = 54.0 * 64 * cst["clusters"] + 750.0 * cst["tri_tests"]  # upper bounds (full clusters, all 17 axes)
-        gbs = nbytes / (ms * 1e-3) / 1e9
-        return {"bound": "hbm", "achieved": round(gbs, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(gbs / HBM_PEAK_GBS, 5), "traffic": None, "kernel": "k_collide",
-                "ms_per_launch": round(ms, 4), "work_per_launch": cst,
-                "fp64_tflops_upper": round(flops / (ms * 1e-3) / 1e12, 3),
-                "note": "latency/divergence bound BVH traversal + FP64 SAT; bytes per SURVEY 8(d)"}
+# Stage -> the kernel that does its work (kernel names as rocprofv3 reports them).
+STAGE_KERNEL = {"nn_query": "k_grid_nn1_group", "collide_pairs": "k_pairs", "collide_cands": "k_cands",
+                "collide_narrow": "k_narrow", "nn_build": "k_grid_scatter", "steer": "k_steer",
+                "sample": "k_sample", "append": "k_append"}
+
+
+def stage_bytes(stage, c, K, n0, d, pmax):
+    """Algorithmic bytes one launch of the stage must touch (DESIGN.md "Measurement"): the
+    inputs it reads and outputs it writes, each counted once per use, from the counters
+    of the round (c = RRTEngine.collide_stats)."""
+    if stage == "nn_query":  # queries + results + examined points (coords, id) + cell ranges
+        return K * (8 * d + 12) + c["nn_points"] * (8 * d + 4) + c["nn_cells"] * 8
+    if stage == "collide_pairs":  # poses, cluster records, env tree items tested, pair words
+        return c["units"] * 96 + c["cluster_threads"] * 64 + c["node_tests"] * 32 + c["pair_tests"] * 4
+    if stage == "collide_cands":  # per header: header, pose, 64 agent triangles; pairs; candidates
+        return c["cluster_transforms"] * (32 + 96 + 64 * 72) + c["pair_tests"] * (4 + 32) + c["candidates"] * 12
+    if stage == "collide_narrow":  # per candidate: itself, pose, agent triangle, env triangle record
+        return c["candidates"] * (12 + 96 + 72 + 384)
+    if stage == "nn_build":  # read the tree, write it in cell order with ids, cell counts
+        return n0 * (2 * 8 * d + 12)
+    if stage == "steer":  # nn id, tree node, end state, poses
+        return K * (4 + 16 * d + 96 * pmax + 4)
+    if stage == "sample":
+        return K * 8 * d
+    if stage == "append":
+        return K * (1 + 8 * d + 4) * 2
+    return None
+
+
+def roofline(per_launch, cst, K, n0, d, pmax, nn_mode, traffic_path):
+    """Roofline of the round's dominant kernel: achieved = its algorithmic bytes per launch
+    / its hipEvent-measured duration (per-stage events on the engine's stream); every
+    stage's figure is listed under `stages`."""
+    stages = {}
+    for s in STAGE_KERNEL:
+        ms = per_launch.get(s, 0.0)
+        b = stage_bytes(s, cst, K, n0, d, pmax)
+        if ms <= 0 or b is None:
+            continue
+        gbs = b / (ms * 1e-3) / 1e9
+        stages[s] = {"kernel": STAGE_KERNEL[s], "ms": round(ms, 4), "bytes": int(b), "achieved_gbs": round(gbs, 1),
+                     "frac": round(gbs / HBM_PEAK_GBS, 4)}
+    dominant = max(stages, key=lambda s: stages[s]["ms"])
+    st = stages[dominant]
+    traffic = pmc_traffic(traffic_path, st["kernel"])
+    out = {"bound": "hbm", "achieved": st["achieved_gbs"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
+           "frac": st["frac"], "traffic": traffic, "kernel": st["kernel"], "stage": dominant,
+           "ms_per_launch": st["ms"], "algorithmic_bytes": st["bytes"], "stages": stages, "work_per_round": cst}
     if dominant == "nn_query" and nn_mode == "brute":
         flops = float(K) * n0 * 3 * d  # SURVEY 8(d): 3*d*N FP64 ops per query (sub, mul, add)
-        tf = flops / (ms * 1e-3) / 1e12
-        return {"bound": "mfma", "achieved": round(tf, 3), "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
-                "frac": round(tf / FP64_PEAK_TFLOPS, 4), "traffic": None, "kernel": "k_knn1",
-                "ms_per_launch": round(ms, 4),
-                "note": "FP64 VALU (no MFMA: FLANN's L2 op order is not a dot product); no-FMA ceiling 39.3 TFLOP/s"}
-    return {"bound": "hbm", "achieved": None, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": None, "traffic": None,
-            "kernel": {"nn_query": "k_grid_knn", "nn_build": "k_grid"}.get(dominant, dominant),
-            "ms_per_launch": round(ms, 4)}
+        tf = flops / (st["ms"] * 1e-3) / 1e12
+        out.update({"bound": "mfma", "achieved": round(tf, 3), "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
+                    "frac": round(tf / FP64_PEAK_TFLOPS, 4), "kernel": "k_knn1",
+                    "note": "FP64 VALU (FLANN's L2 op order is not a dot product, so no MFMA)"})
+    return out
 
 
 def pmc_traffic(path, kernel):
@@ -215,8 +243,7 @@ def main():
     eng.collide_stats(True)
     round_()
     cst = eng.collide_stats(False)
-    roof = roofline(per_launch, cst, K, n0, sc.dim, args.nn)
-    roof["traffic"] = pmc_traffic(args.traffic, roof["kernel"])
+    roof = roofline(per_launch, cst, K, n0, sc.dim, eng.info()["pmax"], args.nn, args.traffic)
 
     out = {
         "metric": "valid RRT edge extensions/sec (collision+NN) per node, 1/2/4/8 MI355X",
@@ -238,7 +265,6 @@ def main():
         "checked_per_s": checked / elapsed,
         "valid_fraction": valid / max(checked, 1),
         "kernel_ms_per_round": {k: round(v, 4) for k, v in per_launch.items()},
-        "collide_work_per_round": cst,
         "roofline": roof,
     }
     if not args.no_cpu and world == 1:

@@ -171,9 +171,13 @@ mpt_status mpt_rrt_set_nn(mpt_rrt *rrt, int32_t mode, double points_per_cell);
  * out [16] (may be NULL): [0] (pose, link) units, [1] agent clusters past the root cull,
  * [2] env tree node tests, [3] exact triangle tests, [4] (cluster, env triangle) pair tests,
  * [5] units re-run by the fused kernel, [6] agent cluster transforms, [7] broad-phase
- * candidates, [8..15] broad-phase wave time per phase (s_memtime ticks, split path). */
+ * candidates, [8] grid NN points examined, [9] grid NN cells visited, [10] (unit, cluster)
+ * broad-phase threads, [11..15] reserved. */
 mpt_status mpt_rrt_collide_stats(mpt_rrt *rrt, int32_t enable, uint64_t out[16]);
-mpt_status mpt_rrt_kernel_times(mpt_rrt *rrt, float ms[6]);
+/* hipEvent times (ms) of the last round's stages, after mpt_rrt_enable_timing(1):
+ * [sample, nn_build, nn_query, steer, collide_pairs, collide_cands, collide_narrow,
+ *  collide_rest (memsets, fused re-run; the whole collide stage in fused mode), append]. */
+mpt_status mpt_rrt_kernel_times(mpt_rrt *rrt, float ms[9]);
 
 #ifdef __cplusplus
 }

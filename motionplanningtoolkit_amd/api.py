@@ -269,19 +269,21 @@ class RRTEngine:
         check(lib().mpt_rrt_enable_timing(self.handle, 1 if on else 0), "mpt_rrt_enable_timing")
 
     def kernel_times(self) -> dict:
-        ms = np.zeros(6, np.float32)
+        ms = np.zeros(9, np.float32)
         check(lib().mpt_rrt_kernel_times(self.handle, _p(ms)), "mpt_rrt_kernel_times")
-        return dict(zip(["sample", "nn_build", "nn_query", "steer", "collide", "append"], ms.astype(float).tolist()))
+        names = ["sample", "nn_build", "nn_query", "steer", "collide_pairs", "collide_cands", "collide_narrow",
+                 "collide_rest", "append"]
+        t = dict(zip(names, ms.astype(float).tolist()))
+        t["collide"] = t["collide_pairs"] + t["collide_cands"] + t["collide_narrow"] + t["collide_rest"]
+        return t
 
     def collide_stats(self, enable: bool) -> dict:
         """Counters since the last call (then reset); enable keeps counting in later rounds."""
         out = np.zeros(16, np.uint64)
         check(lib().mpt_rrt_collide_stats(self.handle, 1 if enable else 0, _p(out)), "mpt_rrt_collide_stats")
         names = ["units", "clusters", "node_tests", "tri_tests", "pair_tests", "fused_reruns", "cluster_transforms",
-                 "candidates"]
-        d = {k: int(v) for k, v in zip(names, out[:8])}
-        d["wave_ticks"] = [int(v) for v in out[8:]]
-        return d
+                 "candidates", "nn_points", "nn_cells", "cluster_threads"]
+        return {k: int(v) for k, v in zip(names, out[:11])}
 
     def set_nn(self, mode: str = "auto", points_per_cell: float = 0.0) -> None:
         """NN structure of the rounds: 'auto' | 'brute' | 'grid' (identical results)."""

@@ -182,6 +182,7 @@ __global__ __launch_bounds__(kPairThreads) void k_pairs(EnvDev env, const AgentD
     int64_t slot = 0, edge = 0;
     if (live) live = decode_unit(w, unit, link, slot, edge);
     if (live) live = c < links[link].n_clusters;
+    const bool decoded = live;
     float lo[3] = {0, 0, 0}, hi[3] = {0, 0, 0};
     int32_t tfirst = 0, tcount = 0;
     if (live) {
@@ -220,6 +221,7 @@ __global__ __launch_bounds__(kPairThreads) void k_pairs(EnvDev env, const AgentD
     }
     if (w.stats) {
         const uint64_t lm = __ballot(live);
+        const uint64_t dm = __ballot(decoded);
         uint32_t sum_tests = tests, sum_pairs = np;
 #pragma unroll
         for (int off = 32; off > 0; off >>= 1) {
@@ -228,6 +230,7 @@ __global__ __launch_bounds__(kPairThreads) void k_pairs(EnvDev env, const AgentD
         }
         if (lane == 0) {
             atomicAdd(w.stats + 1, (unsigned long long)__popcll(lm));
+            atomicAdd(w.stats + 10, (unsigned long long)__popcll(dm));
             atomicAdd(w.stats + 2, (unsigned long long)sum_tests);
             atomicAdd(w.stats + 4, (unsigned long long)sum_pairs);
         }
@@ -434,8 +437,14 @@ void CollideScratch::ensure(int64_t n_units, int32_t max_clusters) {
 }
 
 void launch_collide_split(const EnvDev &env, const AgentDev *d_links, int32_t max_clusters, const CollideWork &w,
-                          CollideScratch &s, hipStream_t stream) {
-    if (w.n_units <= 0 || env.n_tris <= 0) return;
+                          CollideScratch &s, hipStream_t stream, hipEvent_t *marks) {
+    auto mark = [&](int i) {
+        if (marks) hip_check(hipEventRecord(marks[i], stream), "event record");
+    };
+    if (w.n_units <= 0 || env.n_tris <= 0) {
+        for (int i = 0; i < 3; ++i) mark(i);
+        return;
+    }
     const int32_t C = max_clusters > 0 ? max_clusters : 1;
     const int64_t threads = w.n_units * C;
     const int64_t segs = (threads + 63) / 64;
@@ -465,6 +474,7 @@ void launch_collide_split(const EnvDev &env, const AgentDev *d_links, int32_t ma
                                w, a);
     }
     hip_check(hipGetLastError(), "k_pairs launch");
+    mark(0);
     // count slot `segs` is the scan's sentinel (a larger earlier launch may have used it)
     hip_check(hipMemsetAsync(s.hdr_count + segs, 0, sizeof(uint32_t), stream), "sentinel memset");
     size_t tb = s.scan_bytes;
@@ -475,9 +485,11 @@ void launch_collide_split(const EnvDev &env, const AgentDev *d_links, int32_t ma
     hip_check(hipGetLastError(), "k_expand launch");
     hipLaunchKernelGGL(k_cands, dim3((unsigned)((s.n_cwaves + 3) / 4)), dim3(256), 0, stream, env, d_links, w, a);
     hip_check(hipGetLastError(), "k_cands launch");
+    mark(1);
     hipLaunchKernelGGL(k_narrow, dim3((unsigned)(s.n_cwaves + kSpillBlocks)), dim3(64), 0, stream, env, d_links, w,
                        a);
     hip_check(hipGetLastError(), "k_narrow launch");
+    mark(2);
     if (w.stats) {
         hipLaunchKernelGGL(k_count_units, dim3((unsigned)((w.n_units + 255) / 256)), dim3(256), 0, stream, w);
         hip_check(hipGetLastError(), "k_count_units launch");

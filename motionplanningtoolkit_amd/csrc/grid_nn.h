@@ -20,6 +20,7 @@ struct GridDev {
     const double *pts;          // [n][d] in cell order
     const int32_t *ids;         // 1-based original ids in cell order
     const uint8_t *removed;     // by original row, or nullptr
+    unsigned long long *stats;  // optional [2]: points examined, cells visited (1-NN kernel)
 };
 
 // h chosen for about `ppc` points per cell, capped at 4 cells per point and 2^25 cells.

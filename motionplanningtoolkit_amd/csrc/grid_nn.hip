@@ -277,6 +277,7 @@ GridDev GridIndex::dev() const {
     G.pts = spts;
     G.ids = sids;
     G.removed = nullptr;
+    G.stats = nullptr;
     return G;
 }
 
@@ -356,6 +357,7 @@ __global__ __launch_bounds__(256) void k_grid_nn1_group(GridDev G, int32_t d, co
     }
     double bd = __builtin_huge_val();
     int32_t bi = -1;
+    uint32_t n_pts = 0, n_cells = 0;
     for (int r = 0;; ++r) {
         const int side = 2 * r + 1;
         const int cube = g.gd == 3 ? side * side * side : (g.gd == 2 ? side * side : side);
@@ -389,6 +391,8 @@ __global__ __launch_bounds__(256) void k_grid_nn1_group(GridDev G, int32_t d, co
             }
             const int32_t cell = (cc[0] * g.n[1] + cc[1]) * g.n[2] + cc[2];
             const int32_t s = G.cell_start[cell], e = G.cell_start[cell + 1];
+            ++n_cells;
+            n_pts += (uint32_t)(e - s);
             for (int32_t p = s; p < e; ++p) {
                 const double dd = D > 0 ? flann_l2<DD>(qq, G.pts + (int64_t)p * DD)
                                         : flann_l2_dyn(qq, G.pts + (int64_t)p * dim, dim);
@@ -412,6 +416,17 @@ __global__ __launch_bounds__(256) void k_grid_nn1_group(GridDev G, int32_t d, co
         const double lb = ring_bound(g, qg, cq, r);
         if (lb < 0.0) break;  // every cell visited
         if (lb * lb > bd) break;
+    }
+    if (G.stats) {
+#pragma unroll
+        for (int off = kGroup / 2; off > 0; off >>= 1) {
+            n_pts += __shfl_xor(n_pts, off, kGroup);
+            n_cells += __shfl_xor(n_cells, off, kGroup);
+        }
+        if (sub == 0) {
+            atomicAdd(G.stats + 0, (unsigned long long)n_pts);
+            atomicAdd(G.stats + 1, (unsigned long long)n_cells);
+        }
     }
     if (sub == 0) {
         out_ids[qi] = bi;

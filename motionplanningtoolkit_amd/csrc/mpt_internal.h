@@ -150,8 +150,9 @@ void launch_collide(const EnvDev &env, const AgentDev *d_links, const CollideWor
                     hipStream_t stream, int max_blocks = 0);
 // Two-phase path (broad.hip): k_pairs -> k_cands -> k_narrow -> fused kernel over
 // overflowed units.  s.ensure(w.n_units, max_clusters) must have run with the same value.
+// marks (optional, 3 events): recorded after the pair, candidate and exact-test stages.
 void launch_collide_split(const EnvDev &env, const AgentDev *d_links, int32_t max_clusters, const CollideWork &w,
-                          CollideScratch &s, hipStream_t stream);
+                          CollideScratch &s, hipStream_t stream, hipEvent_t *marks = nullptr);
 void launch_pose_edge(const int64_t *d_offsets, int64_t E, int32_t *d_pose_edge, hipStream_t stream);
 
 // ---------------- NN ----------------

@@ -314,7 +314,7 @@ struct mpt_rrt {
     uint64_t ext_base = 0;
     int32_t last_K = 0;
     bool timing = false;
-    hipEvent_t ev[7] = {};
+    hipEvent_t ev[10] = {};
     float last_ms[6] = {0, 0, 0, 0, 0, 0};
     // NN structure over the round's snapshot (grid_nn.hip), rebuilt every round
     int32_t nn_mode = MPT_NN_AUTO;
@@ -497,7 +497,9 @@ extern "C" mpt_status mpt_rrt_step(mpt_rrt *r, int32_t K, void *stream_) {
         }
         mark(2);
         if (use_grid) {
-            launch_grid_knn(r->grid->dev(), p.d, r->d_samples, K, 1, r->d_nn, r->d_nnd2, stream);
+            GridDev G = r->grid->dev();
+            G.stats = r->stats_on ? r->d_cstats + 8 : nullptr;
+            launch_grid_knn(G, p.d, r->d_samples, K, 1, r->d_nn, r->d_nnd2, stream);
         } else {
             NNWork w{};
             w.pts = r->d_nodes;
@@ -526,17 +528,21 @@ extern "C" mpt_status mpt_rrt_step(mpt_rrt *r, int32_t K, void *stream_) {
         cw.stats = r->stats_on ? r->d_cstats : nullptr;
         if (collide_mode() == MPT_COLLIDE_FUSED) {
             launch_collide(r->env, r->d_links, cw, stream);
+            mark(5);
+            mark(6);
+            mark(7);
         } else {
-            launch_collide_split(r->env, r->d_links, r->max_clusters, cw, r->cscratch, stream);
+            launch_collide_split(r->env, r->d_links, r->max_clusters, cw, r->cscratch, stream,
+                                 r->timing ? r->ev + 5 : nullptr);
         }
-        mark(5);
+        mark(8);
         hipLaunchKernelGGL(k_count, dim3(kb), dim3(256), 0, stream, r->d_verdict, K, r->d_bcount);
         hipLaunchKernelGGL(k_append, dim3(kb), dim3(256), 0, stream, r->d_verdict, K, p.d, r->d_ends, r->d_nn,
                            r->d_bcount, r->d_n, r->cap, r->d_nodes, r->d_parents);
         hipLaunchKernelGGL(k_commit, dim3(1), dim3(256), 0, stream, r->d_bcount, (int32_t)kb, K, r->d_n, r->cap,
                            r->d_counters);
         hip_check(hipGetLastError(), "append");
-        mark(6);
+        mark(9);
         r->ext_base += (uint64_t)K;
         r->n_upper = std::min<int64_t>(r->cap, r->n_upper + K);
         r->last_K = K;
@@ -633,14 +639,13 @@ extern "C" mpt_status mpt_rrt_enable_timing(mpt_rrt *r, int32_t enable) {
     });
 }
 
-extern "C" mpt_status mpt_rrt_kernel_times(mpt_rrt *r, float ms[6]) {
+extern "C" mpt_status mpt_rrt_kernel_times(mpt_rrt *r, float ms[9]) {
     return guarded([&] {
         if (!r || !ms) throw Error{MPT_ERR_INVALID, "null pointer"};
         if (!r->timing) throw Error{MPT_ERR_INVALID, "timing not enabled"};
-        hip_check(hipEventSynchronize(r->ev[6]), "event sync");
-        // [sample, nn_build, nn_query, steer, collide, append]
-        const int a[6] = {0, 1, 2, 3, 4, 5};
-        const int b[6] = {1, 2, 3, 4, 5, 6};
-        for (int i = 0; i < 6; ++i) hip_check(hipEventElapsedTime(&ms[i], r->ev[a[i]], r->ev[b[i]]), "elapsed");
+        hip_check(hipEventSynchronize(r->ev[9]), "event sync");
+        // [sample, nn_build, nn_query, steer, collide_pairs, collide_cands, collide_narrow,
+        //  collide_rest, append]: consecutive event pairs
+        for (int i = 0; i < 9; ++i) hip_check(hipEventElapsedTime(&ms[i], r->ev[i], r->ev[i + 1]), "elapsed");
     });
 }
