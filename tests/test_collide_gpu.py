@@ -130,6 +130,28 @@ def test_snake_links(mpt_gpu, oracle):
     assert 0 < got.sum() < E
 
 
+@pytest.mark.parametrize("nx,ny", [(2, 2), (6, 5)])
+def test_multi_room_env_deep_tree(mpt_gpu, oracle, nx, ny):
+    """Grids of rooms: 1264 triangles (three-level broad-phase tree, staged in LDS) and 9480
+    triangles (three levels, global loads): the general tree walk.  Checked against the
+    oracle's AABB tree (itself pinned to the all-pairs loop by test_oracle)."""
+    env = scenes.rooms_env(nx, ny)
+    agent = scenes.read_obj(scenes.mesh_path("agent_blimp"), "all")
+    info = mpt_gpu.Environment(env).info()
+    assert info["triangles"] == len(env)
+    rng = np.random.default_rng(21)
+    n = 1500
+    lo, hi = np.array([-10, -10, -10]), np.array([nx * 180 + 10, ny * 140 + 10, 125])
+    ts = rng.uniform(lo, hi, size=(n, 3))
+    ts[: n // 3, 2] = rng.choice([0.0, 114.2], size=n // 3) + rng.normal(0, 2, n // 3)  # near floors / ceilings
+    poses = np.array([pose(t, random_rot(rng)) for t in ts]).reshape(-1, 1, 12)
+    off = np.arange(n + 1)
+    ref = oracle.collide_batch_bvh(oracle.BVH(env), pose([0, 0, 0]), [agent], poses, off, nthreads=8)
+    got = mpt_gpu.collide_batch(mpt_gpu.Environment(env), [mpt_gpu.AgentMesh(agent)], poses, off)
+    assert np.array_equal(got, ref), np.nonzero(got != ref)
+    assert 0.1 < ref.mean() < 0.9
+
+
 def test_candidate_overflow(mpt_gpu, oracle, collide_mode):
     """The blimp against itself: thousands of overlapping triangle boxes per pose, more than
     one broad-phase segment holds, so the split path hands those poses to the fused kernel."""
