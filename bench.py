@@ -180,14 +180,14 @@ def main():
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     import motionplanningtoolkit_amd as mpt
-    from motionplanningtoolkit_amd import scenes
+    from motionplanningtoolkit_amd import multiseed, scenes
 
     mpt.init(local)
     torch.cuda.set_device(local)
     stream = torch.cuda.current_stream()
 
     sc = scenes.blimp_scenario("all")
-    seed = args.seed + rank
+    seed = multiseed.rank_seed(args.seed, rank)
     rng = np.random.default_rng(seed)
     n0, K = args.tree, args.batch
     tree = rng.uniform(sc.ranges[:, 0], sc.ranges[:, 1], size=(n0, sc.dim))
@@ -224,13 +224,7 @@ def main():
     valid = c1["valid"] - c0["valid"]
     checked = c1["checked"] - c0["checked"]
 
-    if dist:
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-        s = torch.tensor([valid, checked], dtype=torch.float64, device="cuda")
-        dist.all_reduce(s, op=dist.ReduceOp.SUM)
-        valid, checked = int(s[0].item()), int(s[1].item())
+    elapsed, (valid, checked) = multiseed.reduce_run(dist, elapsed, [valid, checked], "cuda")
 
     if rank != 0:
         if dist:
