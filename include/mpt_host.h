@@ -27,6 +27,18 @@ mpt_status mpt_host_load_mesh(const char *path, int32_t which, double *tris, int
 mpt_status mpt_host_rrt_inst(const char *inst_path, int32_t iterations_at_a_time, int64_t cap, double *starts,
                              double *ends, int64_t *n_edges, int32_t *dim, int32_t *solved);
 
+/* PRM (planners/prm/prm.hpp) with the .inst's agent and workspace.
+ * states != NULL: addMilestone for states[n][dim] in order, `batch` at a time (1 = the
+ *   reference's sequence), and nothing else.
+ * states == NULL: PRM::query(start, goal) repeated (100 sampled milestones per call,
+ *   prm.hpp:207-213) until solved or max_queries calls; then *solved / *cost are set.
+ * Roadmap out: edges[E][2] = (target, source) vertex ids (milestones 0-based in insertion
+ * order), costs[E], comp[n_milestones] = smallest milestone of each component; arrays are
+ * written up to cap edges / comp_cap milestones. */
+mpt_status mpt_host_prm(const char *inst_path, const double *states, int64_t n, int32_t batch, int32_t max_queries,
+                        int64_t cap, int32_t *edges, double *costs, int64_t *n_edges, int64_t comp_cap,
+                        int32_t *comp, int64_t *n_milestones, int32_t *solved, double *cost);
+
 #ifdef __cplusplus
 }
 #endif

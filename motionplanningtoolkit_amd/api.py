@@ -312,6 +312,27 @@ def load_mesh(path: str, which: str = "all") -> np.ndarray:
     return out
 
 
+def prm(path: str, states=None, batch: int = 1, max_queries: int = 50):
+    """PRM (planners/prm/prm.hpp) via the C++ host planner on a .inst file.
+    states given: the roadmap over these milestones only; otherwise PRM::query(start, goal)
+    until solved.  Returns dict(edges [E][2] (target, source), costs [E], comp [n], solved, cost)."""
+    st = None if states is None else np.ascontiguousarray(states, np.float64)
+    n = 0 if st is None else st.shape[0]
+    ne, nm = C.c_int64(), C.c_int64()
+    solved, cost = C.c_int32(), C.c_double()
+    check(lib().mpt_host_prm(path.encode(), _p(st), n, batch, max_queries, 0, None, None, C.byref(ne), 0, None,
+                             C.byref(nm), C.byref(solved), C.byref(cost)), "mpt_host_prm", host=True)
+    # the counts are known now; run again to fill arrays of that size (deterministic)
+    cap, ccap = max(ne.value, 1), max(nm.value, 1)
+    edges = np.zeros((cap, 2), np.int32)
+    costs = np.zeros(cap)
+    comp = np.zeros(ccap, np.int32)
+    check(lib().mpt_host_prm(path.encode(), _p(st), n, batch, max_queries, cap, _p(edges), _p(costs), C.byref(ne),
+                             ccap, _p(comp), C.byref(nm), C.byref(solved), C.byref(cost)), "mpt_host_prm", host=True)
+    return {"edges": edges[: ne.value], "costs": costs[: ne.value], "comp": comp[: nm.value],
+            "solved": bool(solved.value), "cost": cost.value}
+
+
 def rrt_inst(path: str, iterations_at_a_time: int, cap: int = 1 << 16):
     """Run the C++ host planner on a .inst file: returns (starts, ends, solved)."""
     n = C.c_int64()

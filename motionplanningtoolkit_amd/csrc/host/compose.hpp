@@ -9,6 +9,7 @@
 
 #include "agents.hpp"
 #include "planning.hpp"
+#include "prm.hpp"
 
 namespace mpt_host {
 
@@ -46,6 +47,67 @@ RunResult run_rrt(const InstanceFileMap &args, int iterationsAtATime) {
         r.ends.insert(r.ends.end(), t.begin(), t.begin() + r.dim);
     }
     return r;
+}
+
+// PRM roadmap over explicit milestone states (tests / FFI): the .inst's agent, workspace and
+// step sizes, milestones added in order `batch` at a time.
+struct PrmResult {
+    std::vector<int32_t> edges;  // [E][2] (target, source)
+    std::vector<double> costs;   // [E]
+    std::vector<int32_t> comp;   // [n] smallest milestone of each component
+    bool solved = false;
+    double cost = -1;
+    int64_t milestones = 0, queries = 0;
+};
+
+template <class Agent>
+PrmResult run_prm(const InstanceFileMap &args, const double *states, int64_t n, int32_t batch, int32_t max_queries) {
+    typedef Map3D<Agent> Workspace;
+    typedef GpuNN<typename Agent::Edge> KDTree;
+    typedef UniformSampler<Workspace, Agent, KDTree> Sampler;
+    typedef PRM<Workspace, Agent, Sampler> Planner;
+
+    Agent agent(args);
+    Workspace workspace(args);
+    KDTree kdtree(agent.getTreeStateSize());
+    Sampler sampler(workspace, agent, kdtree);
+    Planner prm(workspace, agent, sampler, args, batch);
+    PrmResult r;
+    const unsigned d = agent.getTreeStateSize();
+    if (states) {
+        std::vector<typename Agent::State> ms;
+        for (int64_t i = 0; i < n; ++i) ms.push_back(agent.buildState(StateVars(states + i * d, states + (i + 1) * d)));
+        prm.addMilestones(ms);
+    } else {
+        typename Agent::State start(parse_doubles(args.value("Agent Start Location")));
+        typename Agent::State goal(parse_doubles(args.value("Agent Goal Location")));
+        bool first = true;
+        while (r.queries < max_queries && !prm.query(start, goal, -1, first)) {
+            first = false;
+            ++r.queries;
+        }
+        r.solved = prm.isSolved();
+        r.cost = prm.getSolutionCost();
+    }
+    for (const auto &e : prm.edges()) {
+        r.edges.push_back(e.target);
+        r.edges.push_back(e.source);
+        r.costs.push_back(e.cost);
+    }
+    r.milestones = (int64_t)prm.milestoneCount();
+    for (int64_t v = 0; v < r.milestones; ++v) r.comp.push_back(prm.component((int)v));
+    return r;
+}
+
+inline PrmResult run_prm_inst(const std::string &path, const double *states, int64_t n, int32_t batch,
+                              int32_t max_queries) {
+    InstanceFileMap args(path);
+    srand(1);
+    const std::string type = args.value("Agent Type");
+    if (type == "Omnidirectional") return run_prm<Omnidirectional>(args, states, n, batch, max_queries);
+    if (type == "Blimp") return run_prm<Blimp>(args, states, n, batch, max_queries);
+    if (type == "Snake") return run_prm<SnakeTrailers>(args, states, n, batch, max_queries);
+    throw std::runtime_error("unrecognized Agent Type: " + type);
 }
 
 // main.cpp:192-212 dispatch on "Agent Type".  The reference never seeds rand() or the

@@ -55,3 +55,24 @@ extern "C" mpt_status mpt_host_rrt_inst(const char *inst_path, int32_t iteration
         if (ends && m > 0) std::memcpy(ends, r.ends.data(), sizeof(double) * r.dim * m);
     });
 }
+
+extern "C" mpt_status mpt_host_prm(const char *inst_path, const double *states, int64_t n, int32_t batch,
+                                   int32_t max_queries, int64_t cap, int32_t *edges, double *costs, int64_t *n_edges,
+                                   int64_t comp_cap, int32_t *comp, int64_t *n_milestones, int32_t *solved,
+                                   double *cost) {
+    return hguard([&] {
+        if (!inst_path || !n_edges || !n_milestones) throw std::invalid_argument("null pointer");
+        if (states && n < 0) throw std::invalid_argument("n < 0");
+        const auto r = mpt_host::run_prm_inst(inst_path, states, n, batch, max_queries);
+        const int64_t ne = (int64_t)r.costs.size();
+        *n_edges = ne;
+        *n_milestones = r.milestones;
+        if (solved) *solved = r.solved ? 1 : 0;
+        if (cost) *cost = r.cost;
+        const int64_t m = std::min<int64_t>(ne, cap);
+        if (edges && m > 0) std::memcpy(edges, r.edges.data(), sizeof(int32_t) * 2 * m);
+        if (costs && m > 0) std::memcpy(costs, r.costs.data(), sizeof(double) * m);
+        const int64_t mc = std::min<int64_t>(r.milestones, comp_cap);
+        if (comp && mc > 0) std::memcpy(comp, r.comp.data(), sizeof(int32_t) * mc);
+    });
+}

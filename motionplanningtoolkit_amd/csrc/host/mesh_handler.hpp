@@ -127,6 +127,37 @@ public:
                   "mpt_collide_batch");
         return verdict != 0;
     }
+
+    // isInCollision for many edges in one device call: edges[e] = poses[P_e][L];
+    // returns one verdict per edge (1 = contact).
+    static std::vector<uint8_t> collideEdges(const StaticEnvironmentMeshHandler &environment,
+                                             const std::vector<const SimpleAgentMeshHandler *> &agent,
+                                             const std::vector<std::vector<std::vector<Transform3f>>> &edges) {
+        const int32_t L = (int32_t)agent.size();
+        std::vector<uint8_t> verdict(edges.size(), 0);
+        if (L == 0 || edges.empty()) return verdict;
+        std::vector<double> buf;
+        std::vector<int64_t> off(edges.size() + 1, 0);
+        for (size_t e = 0; e < edges.size(); ++e) {
+            int64_t P = 0;
+            for (const auto &pose : edges[e]) {
+                if (pose.empty()) continue;
+                if ((int32_t)pose.size() != L) throw std::runtime_error("pose/link count mismatch");
+                for (const auto &t : pose) {
+                    buf.insert(buf.end(), t.R.begin(), t.R.end());
+                    buf.insert(buf.end(), t.T.begin(), t.T.end());
+                }
+                ++P;
+            }
+            off[e + 1] = off[e] + P;
+        }
+        std::vector<const mpt_agent *> links(L);
+        for (int32_t l = 0; l < L; ++l) links[l] = agent[l]->handle();
+        mpt_throw(mpt_collide_batch(environment.handle(), links.data(), L, buf.data(), off.data(),
+                                    (int64_t)edges.size(), verdict.data(), nullptr),
+                  "mpt_collide_batch");
+        return verdict;
+    }
 };
 
 }  // namespace mpt_host

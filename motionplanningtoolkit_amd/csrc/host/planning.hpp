@@ -43,6 +43,17 @@ public:
         return !MeshHandler::isInCollision(mesh, agent.getMeshes(), agent.getPoses(edge, dt), checkSelfCollision);
     }
 
+    // safeEdge over many edges in one device call (the batched form PRM construction uses).
+    std::vector<bool> safeEdges(const Agent &agent, const std::vector<Edge> &edges, double dt) const {
+        std::vector<std::vector<std::vector<Transform3f>>> poses;
+        poses.reserve(edges.size());
+        for (const Edge &e : edges) poses.push_back(agent.getPoses(e, dt));
+        const std::vector<uint8_t> v = MeshHandler::collideEdges(mesh, agent.getMeshes(), poses);
+        std::vector<bool> ok(v.size());
+        for (size_t i = 0; i < v.size(); ++i) ok[i] = v[i] == 0;
+        return ok;
+    }
+
     // Map3D::safePoses (map3d.hpp:39-42) as the reference evidently meant it: one pose
     // list per configuration.
     bool safePoses(const Agent &agent, const std::vector<std::vector<Transform3f>> &poses) const {
@@ -107,6 +118,31 @@ public:
             r.distances.push_back(d2[i]);
         }
         return r;
+    }
+
+    // kNearest for many query elements in one device call.
+    std::vector<KNNResult> kNearestBatch(const std::vector<const Element *> &elems, unsigned int k) {
+        if (k == 0) throw std::invalid_argument("kNearestBatch: k > 0");
+        const int64_t nq = (int64_t)elems.size();
+        std::vector<KNNResult> out((size_t)nq);
+        if (nq == 0) return out;
+        std::vector<double> q;
+        q.reserve((size_t)nq * dim_);
+        for (const Element *e : elems) {
+            const std::vector<double> &v = e->getTreeStateVars();
+            q.insert(q.end(), v.begin(), v.begin() + dim_);
+        }
+        std::vector<int32_t> ids((size_t)nq * k);
+        std::vector<double> d2((size_t)nq * k);
+        mpt_throw(mpt_nn_knn(nn_.get(), q.data(), nq, (int32_t)k, ids.data(), d2.data(), nullptr), "mpt_nn_knn");
+        for (int64_t i = 0; i < nq; ++i)
+            for (unsigned j = 0; j < k; ++j) {
+                const int32_t id = ids[i * k + j];
+                if (id < 0) break;
+                out[i].elements.push_back(lookup_.at(id));
+                out[i].distances.push_back(d2[i * k + j]);
+            }
+        return out;
     }
 
     KNNResult kNearestWithin(const Element *elem, double radius, int max_neighbors = -1) const {

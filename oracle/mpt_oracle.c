@@ -972,3 +972,76 @@ int64_t orc_engine_step(int32_t agent_kind, const double *prm, int32_t d, const 
     free(samples); free(ends); free(d2);
     return n;
 }
+
+/* ======================================================================
+ * PRM construction: planners/prm/prm.hpp:334-387 (addMilestone), omnidirectional agent.
+ * Milestones are added in order, `batch` at a time (1 = the reference's sequence); each is
+ * connected to its k nearest earlier milestones (exact kNN over the first 3 state vars,
+ * prm.hpp:155 KDTree(..., 3, 0) and :350 kNearest(.., 10); milestones of one batch do not
+ * see each other) through Omnidirectional::steer(s, t, 1000) (omnidirectional.hpp:144-162:
+ * end = s + (t - s) * min(1, 1000 / |t - s|), cost = |t - s|) and Map3D::safeEdge over
+ * Omnidirectional::getPoses(edge, dt).  A safe edge is recorded as (target, source) with
+ * its cost and unites the two components (prm.hpp:372-376).
+ * ====================================================================== */
+static int32_t uf_find(int32_t *p, int32_t x) {
+    while (p[x] != x) {
+        p[x] = p[p[x]];
+        x = p[x];
+    }
+    return x;
+}
+
+int64_t orc_prm_build(const orc_bvh *env, const double env_tf[12], const double *agent_tris, int64_t Ta,
+                      const double *states, int64_t n, int32_t k, int32_t batch, double cc_dt,
+                      int32_t *edges, double *costs, int64_t cap, int32_t *comp) {
+    if (batch < 1) batch = 1;
+    double *keys = (double *)malloc(sizeof(double) * 3 * (size_t)(n > 0 ? n : 1));
+    int32_t *parent = (int32_t *)malloc(sizeof(int32_t) * (size_t)(n > 0 ? n : 1));
+    int32_t *ids = (int32_t *)malloc(sizeof(int32_t) * (size_t)k);
+    double *d2 = (double *)malloc(sizeof(double) * (size_t)k);
+    int32_t maxP = 1 << 20;
+    double *poses = (double *)malloc(sizeof(double) * 12 * (size_t)maxP);
+    int64_t ne = 0;
+    for (int64_t i = 0; i < n; ++i) {
+        memcpy(keys + 3 * i, states + 3 * i, 3 * sizeof(double));
+        parent[i] = (int32_t)i;
+    }
+    for (int64_t b0 = 0; b0 < n; b0 += batch) {
+        const int64_t b1 = b0 + batch < n ? b0 + batch : n;
+        for (int64_t i = b0; i < b1; ++i) {
+            orc_knn(keys, NULL, b0, 3, keys + 3 * i, 1, k, ids, d2);
+            const double *s = states + 3 * i;
+            for (int32_t j = 0; j < k; ++j) {
+                if (ids[j] < 0) break;
+                const int32_t tgt = ids[j] - 1;
+                const double *t = states + 3 * tgt;
+                const double dx = t[0] - s[0], dy = t[1] - s[1], dz = t[2] - s[2];
+                const double dist = sqrt(dx * dx + dy * dy + dz * dz);
+                double fraction = 1000.0 / dist;
+                if (fraction > 1) fraction = 1;
+                const double end[3] = {s[0] + dx * fraction, s[1] + dy * fraction, s[2] + dz * fraction};
+                const int32_t P = orc_omni_get_poses(s, end, cc_dt, poses, maxP);
+                int hit = 0;
+                for (int32_t p = 0; p < P && p < maxP && !hit; ++p)
+                    hit = orc_collide_unit_bvh(env, env_tf, agent_tris, Ta, poses + 12 * p, NULL);
+                if (hit) continue;
+                if (ne < cap) {
+                    edges[2 * ne] = tgt;
+                    edges[2 * ne + 1] = (int32_t)i;
+                    costs[ne] = dist;
+                }
+                ++ne;
+                const int32_t ra = uf_find(parent, tgt), rb = uf_find(parent, (int32_t)i);
+                if (ra != rb) parent[ra > rb ? ra : rb] = ra < rb ? ra : rb;
+            }
+        }
+    }
+    /* component label = smallest milestone of the component (roots are minimal by construction) */
+    for (int64_t i = 0; i < n; ++i) comp[i] = uf_find(parent, (int32_t)i);
+    free(keys);
+    free(parent);
+    free(ids);
+    free(d2);
+    free(poses);
+    return ne <= cap ? ne : -1;
+}

@@ -144,6 +144,13 @@ int64_t orc_engine_step(int32_t agent_kind, const double *prm, int32_t d, const 
                         double *nodes, int32_t *parents, int64_t n_nodes, int64_t capacity,
                         int32_t *nn_out, uint8_t *verdict_out, int nthreads, int use_kdtree);
 
+/* PRM construction (planners/prm/prm.hpp:334-387) for the omnidirectional agent over
+ * explicit milestones states[n][3]: edges[E][2] = (target, source), costs[E], comp[n] =
+ * smallest milestone of each component.  Returns E, or -1 if E > cap. */
+int64_t orc_prm_build(const orc_bvh *env, const double env_tf[12], const double *agent_tris, int64_t Ta,
+                      const double *states, int64_t n, int32_t k, int32_t batch, double cc_dt,
+                      int32_t *edges, double *costs, int64_t cap, int32_t *comp);
+
 #ifdef __cplusplus
 }
 #endif

@@ -68,6 +68,7 @@ def lib():
             "orc_snake_get_poses": (I32, [P, P, P, D, D, P, I32]),
             "orc_rrt_run": (I64, [I32, P, I32, P, P, P, P, D, D, P, I64, P, P, I64, I64, I64, P, P, P, P]),
             "orc_engine_step": (I64, [I32, P, I32, P, D, D, U64, U64, I32, P, P, P, I64, P, P, I64, I64, P, P, C.c_int, C.c_int]),
+            "orc_prm_build": (I64, [P, P, P, I64, P, I64, I32, I32, D, P, P, I64, P]),
         }
         for name, (res, args) in sig.items():
             f = getattr(L, name)
@@ -285,3 +286,19 @@ def engine_step(kind, prm, ranges, steer_dt, cc_dt, seed, ext_base, K, bvh: BVH,
                               _p(_f64(env_tf)), _p(agent_tris), agent_tris.shape[0], _p(nodes), _p(parents),
                               n_nodes, nodes.shape[0], _p(nn), _p(verdict), nthreads, 1 if use_kdtree else 0)
     return n, nn, verdict
+
+
+def prm_build(bvh: BVH, env_tf, agent_tris, states, k=10, batch=1, cc_dt=0.1):
+    """PRM roadmap over explicit omnidirectional milestones (orc_prm_build): returns
+    (edges [E][2] = (target, source), costs [E], comp [n])."""
+    states = _f64(states).reshape(-1, 3)
+    n = states.shape[0]
+    agent_tris = _f64(agent_tris).reshape(-1, 9)
+    cap = max(1, n * k)
+    edges = np.zeros((cap, 2), np.int32)
+    costs = np.zeros(cap)
+    comp = np.zeros(n, np.int32)
+    ne = lib().orc_prm_build(bvh.ptr, _p(_f64(env_tf)), _p(agent_tris), agent_tris.shape[0], _p(states), n, k, batch,
+                             cc_dt, _p(edges), _p(costs), cap, _p(comp))
+    assert ne >= 0
+    return edges[:ne], costs[:ne], comp

@@ -302,3 +302,32 @@ def test_oracle_rrt_omni_solves_and_is_consistent(oracle):
     off = np.r_[0, np.cumsum([len(e) for e in edges])]
     v = oracle.collide_batch(sc.env_tris, sc.env_tf, [sc.agent_tris], np.concatenate(edges).reshape(-1, 1, 12), off)
     assert v.sum() == 0
+
+
+def test_oracle_prm_roadmap_is_consistent(oracle):
+    """orc_prm_build (prm.hpp:334-387 restated): every edge joins a milestone to one of its k
+    nearest predecessors, costs are the L2 lengths, components are the graph's."""
+    from scipy.sparse import coo_matrix
+    from scipy.sparse.csgraph import connected_components
+    from scipy.spatial import cKDTree
+
+    sc = scenes.omni_scenario()
+    bvh = oracle.BVH(sc.env_tris)
+    states = np.random.default_rng(3).uniform(-10, 10, (200, 3))
+    edges, costs, comp = oracle.prm_build(bvh, sc.env_tf, sc.agent_tris, states, k=10, batch=1, cc_dt=sc.cc_dt)
+    assert len(edges) > 500
+    tgt, src = edges[:, 0], edges[:, 1]
+    assert np.all(tgt < src)
+    assert np.allclose(costs, np.linalg.norm(states[tgt] - states[src], axis=1), rtol=0, atol=1e-12)
+    for s in np.unique(src):
+        _, nn = cKDTree(states[:s]).query(states[s], k=min(10, s))
+        assert set(tgt[src == s]) <= set(np.atleast_1d(nn))
+    n = len(states)
+    g = coo_matrix((np.ones(len(edges)), (tgt, src)), shape=(n, n))
+    _, lab = connected_components(g, directed=False)
+    for c in np.unique(lab):
+        members = np.flatnonzero(lab == c)
+        assert np.all(comp[members] == members.min())
+    # batched: each milestone only sees the milestones before its batch
+    e64, _, _ = oracle.prm_build(bvh, sc.env_tf, sc.agent_tris, states, k=10, batch=64, cc_dt=sc.cc_dt)
+    assert np.all(e64[:, 0] < (e64[:, 1] // 64) * 64)
