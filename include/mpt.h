@@ -101,6 +101,19 @@ mpt_status mpt_last_collide_stats(uint64_t stats[4]);
 enum { MPT_COLLIDE_SPLIT = 0, MPT_COLLIDE_FUSED = 1 };
 mpt_status mpt_set_collide_mode(int32_t mode);
 
+/* ---- distance: fcl::distance through fcl_helpers::defaultDistanceFunction ----
+ * (utilities/fcl_helpers.hpp:67-84, DistanceData :35-42; no caller in the reference) over
+ * the same object sets as mpt_collide_batch: dist_out[e] = minimum over the edge's poses,
+ * links and (env, agent) triangle pairs of FCL's TriangleDistance::triDistance; 0 = in
+ * contact (the callback's dist <= 0 stop); DBL_MAX (the initial DistanceResult) for an edge
+ * without poses.  Same arguments as mpt_collide_batch[_device].  mpt_last_collide_stats
+ * then reports [(unit, cluster) waves, env box tests, triangle-distance calls, pair box tests]. */
+mpt_status mpt_distance_batch(const mpt_env *env, const mpt_agent *const *links, int32_t L, const double *poses,
+                              const int64_t *edge_pose_offsets, int64_t E, double *dist_out, void *stream);
+mpt_status mpt_distance_batch_device(const mpt_env *env, const mpt_agent *const *links, int32_t L,
+                                     const double *d_poses, const int64_t *d_edge_pose_offsets, int64_t E,
+                                     int64_t total_poses, double *d_dist_out, void *stream);
+
 /* ---- NN: FLANN_KDTreeWrapper ---- */
 mpt_status mpt_nn_create(int32_t dim, int64_t capacity, mpt_nn **out);
 mpt_status mpt_nn_destroy(mpt_nn *nn);

@@ -41,6 +41,8 @@ SIGNATURES = {
     "mpt_collide_batch_device": (I32, [P, P, I32, P, P, I64, I64, P, P]),
     "mpt_set_stats": (I32, [I32]),
     "mpt_set_collide_mode": (I32, [I32]),
+    "mpt_distance_batch": (I32, [P, P, I32, P, P, I64, P, P]),
+    "mpt_distance_batch_device": (I32, [P, P, I32, P, P, I64, I64, P, P]),
     "mpt_last_collide_stats": (I32, [P]),
     "mpt_nn_create": (I32, [I32, I64, P]),
     "mpt_nn_destroy": (I32, [P]),

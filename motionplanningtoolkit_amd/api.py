@@ -129,6 +129,25 @@ def collide_batch_device(env: Environment, links: Sequence[AgentMesh], d_poses, 
                                          total_poses, _p(d_verdict), _stream(stream)), "mpt_collide_batch_device")
 
 
+def distance_batch(env: Environment, links: Sequence[AgentMesh], poses, edge_offsets, stream=None) -> np.ndarray:
+    """Minimum mesh-vs-mesh distance per edge (fcl::distance through defaultDistanceFunction,
+    utilities/fcl_helpers.hpp:67-84): 0 = contact, DBL_MAX for an edge without poses."""
+    L = len(links)
+    poses = _f64(poses).reshape(-1, L, 12)
+    off = np.ascontiguousarray(edge_offsets, dtype=np.int64)
+    E = off.shape[0] - 1
+    out = np.zeros(max(E, 0), np.float64)
+    check(lib().mpt_distance_batch(env.handle, _links(links), L, _p(poses), _p(off), E, _p(out), _stream(stream)),
+          "mpt_distance_batch")
+    return out
+
+
+def distance_batch_device(env: Environment, links: Sequence[AgentMesh], d_poses, d_offsets, E: int,
+                          total_poses: int, d_dist, stream=None) -> None:
+    check(lib().mpt_distance_batch_device(env.handle, _links(links), len(links), _p(d_poses), _p(d_offsets), E,
+                                          total_poses, _p(d_dist), _stream(stream)), "mpt_distance_batch_device")
+
+
 COLLIDE_MODES = {"split": 0, "fused": 1}
 
 

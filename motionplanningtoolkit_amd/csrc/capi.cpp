@@ -478,12 +478,10 @@ const EnvDev &env_dev(const mpt_env *e) { return e->dev; }
 const AgentDev &agent_dev(const mpt_agent *a) { return a->dev; }
 }  // namespace mpt
 
-static void collide_common(const mpt_env *env, const mpt_agent *const *links, int32_t L, const double *d_poses,
-                           const int32_t *d_pose_edge, int64_t total_poses, int64_t E, uint8_t *d_verdict,
-                           hipStream_t stream) {
-    // The link table lives in a per-thread device buffer that is rewritten only when the
-    // set of links changes; the rewrite waits for in-flight work that may still read it
-    // and copies synchronously, so no pageable staging memory outlives this call.
+// The link table lives in a per-thread device buffer that is rewritten only when the
+// set of links changes; the rewrite waits for in-flight work that may still read it
+// and copies synchronously, so no pageable staging memory outlives the call.
+static const AgentDev *link_table(const mpt_agent *const *links, int32_t L, int32_t *max_clusters) {
     static thread_local std::vector<AgentDev> cached;
     std::vector<AgentDev> lk((size_t)L);
     for (int32_t l = 0; l < L; ++l) lk[l] = links[l]->dev;
@@ -496,6 +494,16 @@ static void collide_common(const mpt_env *env, const mpt_agent *const *links, in
         hip_check(hipMemcpy(d_links, lk.data(), sizeof(AgentDev) * L, hipMemcpyHostToDevice), "links H2D");
         cached = lk;
     }
+    *max_clusters = 1;
+    for (const AgentDev &a : lk) *max_clusters = std::max(*max_clusters, a.n_clusters);
+    return d_links;
+}
+
+static void collide_common(const mpt_env *env, const mpt_agent *const *links, int32_t L, const double *d_poses,
+                           const int32_t *d_pose_edge, int64_t total_poses, int64_t E, uint8_t *d_verdict,
+                           hipStream_t stream) {
+    int32_t max_clusters = 1;
+    const AgentDev *d_links = link_table(links, L, &max_clusters);
     hip_check(hipMemsetAsync(d_verdict, 0, (size_t)E, stream), "verdict memset");
     CollideWork w{};
     w.poses = d_poses;
@@ -513,8 +521,6 @@ static void collide_common(const mpt_env *env, const mpt_agent *const *links, in
     if (collide_mode() == MPT_COLLIDE_FUSED) {
         launch_collide(env->dev, d_links, w, stream);
     } else {
-        int32_t max_clusters = 1;
-        for (const AgentDev &a : lk) max_clusters = std::max(max_clusters, a.n_clusters);
         g_ws.cs.ensure(w.n_units, max_clusters);
         launch_collide_split(env->dev, d_links, max_clusters, w, g_ws.cs, stream);
     }
@@ -571,6 +577,72 @@ extern "C" mpt_status mpt_collide_batch_device(const mpt_env *env, const mpt_age
         auto *d_pe = (int32_t *)g_ws.pose_edge.get(sizeof(int32_t) * std::max<int64_t>(total_poses, 1));
         launch_pose_edge(d_edge_pose_offsets, E, d_pe, stream);
         collide_common(env, links, L, d_poses, d_pe, total_poses, E, d_verdict_out, stream);
+    });
+}
+
+// ---------------------------------------------------------------- distance
+static void distance_common(const mpt_env *env, const mpt_agent *const *links, int32_t L, const double *d_poses,
+                            const int32_t *d_pose_edge, int64_t total_poses, int64_t E, double *d_dist,
+                            hipStream_t stream) {
+    DistWork w{};
+    const AgentDev *d_links = link_table(links, L, &w.max_clusters);
+    w.poses = d_poses;
+    w.pose_edge = d_pose_edge;
+    w.L = L;
+    w.n_units = total_poses * L;
+    w.best = reinterpret_cast<unsigned long long *>(d_dist);  // written as double bit patterns
+    if (g_stats_enabled) {
+        w.stats = (unsigned long long *)g_ws.stats.get(sizeof(g_last_stats));
+        hip_check(hipMemsetAsync(w.stats, 0, sizeof(g_last_stats), stream), "stats memset");
+    }
+    launch_distance(env->dev, d_links, w, E, stream);
+    if (w.stats) {
+        hip_check(hipMemcpyAsync(g_last_stats, w.stats, sizeof(g_last_stats), hipMemcpyDeviceToHost, stream), "stats");
+    }
+}
+
+extern "C" mpt_status mpt_distance_batch(const mpt_env *env, const mpt_agent *const *links, int32_t L,
+                                         const double *poses, const int64_t *edge_pose_offsets, int64_t E,
+                                         double *dist_out, void *stream_) {
+    return guarded([&] {
+        check_links(env, links, L);
+        require(E >= 0 && (E == 0 || (edge_pose_offsets && dist_out)), "bad edge arrays");
+        if (E == 0) return;
+        require(edge_pose_offsets[0] == 0, "edge_pose_offsets[0] must be 0");
+        for (int64_t e = 0; e < E; ++e) require(edge_pose_offsets[e + 1] >= edge_pose_offsets[e], "offsets not monotone");
+        const int64_t P = edge_pose_offsets[E];
+        require(P == 0 || poses, "null poses");
+        require(P < (int64_t(1) << 31), "too many poses");
+        hipStream_t stream = (hipStream_t)stream_;
+        std::vector<int32_t> pe((size_t)P);
+        for (int64_t e = 0; e < E; ++e)
+            for (int64_t p = edge_pose_offsets[e]; p < edge_pose_offsets[e + 1]; ++p) pe[p] = (int32_t)e;
+        auto *d_poses = (double *)g_ws.poses.get(sizeof(double) * 12 * std::max<int64_t>(P * L, 1));
+        auto *d_pe = (int32_t *)g_ws.pose_edge.get(sizeof(int32_t) * std::max<int64_t>(P, 1));
+        auto *d_d = (double *)g_ws.d2.get(sizeof(double) * (size_t)E);
+        if (P > 0) {
+            hip_check(hipMemcpyAsync(d_poses, poses, sizeof(double) * 12 * P * L, hipMemcpyHostToDevice, stream),
+                      "poses H2D");
+            hip_check(hipMemcpyAsync(d_pe, pe.data(), sizeof(int32_t) * P, hipMemcpyHostToDevice, stream), "pe H2D");
+        }
+        distance_common(env, links, L, d_poses, d_pe, P, E, d_d, stream);
+        hip_check(hipMemcpyAsync(dist_out, d_d, sizeof(double) * (size_t)E, hipMemcpyDeviceToHost, stream), "dist D2H");
+        hip_check(hipStreamSynchronize(stream), "distance sync");
+    });
+}
+
+extern "C" mpt_status mpt_distance_batch_device(const mpt_env *env, const mpt_agent *const *links, int32_t L,
+                                                const double *d_poses, const int64_t *d_edge_pose_offsets, int64_t E,
+                                                int64_t total_poses, double *d_dist_out, void *stream_) {
+    return guarded([&] {
+        check_links(env, links, L);
+        require(E >= 0 && total_poses >= 0, "bad sizes");
+        if (E == 0) return;
+        require(d_edge_pose_offsets && d_dist_out && (total_poses == 0 || d_poses), "null pointer");
+        hipStream_t stream = (hipStream_t)stream_;
+        auto *d_pe = (int32_t *)g_ws.pose_edge.get(sizeof(int32_t) * std::max<int64_t>(total_poses, 1));
+        launch_pose_edge(d_edge_pose_offsets, E, d_pe, stream);
+        distance_common(env, links, L, d_poses, d_pe, total_poses, E, d_dist_out, stream);
     });
 }
 

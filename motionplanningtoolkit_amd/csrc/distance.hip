@@ -1,0 +1,246 @@
+// distance.hip -- batched mesh-vs-mesh minimum distance on gfx950.
+//
+// The "distance" half of the reference's FCL layer: fcl::distance between the env objects
+// and the agent's (pose, link) objects, driven by the broadphase callback
+// fcl_helpers::defaultDistanceFunction (utilities/fcl_helpers.hpp:67-84, DistanceData :35-42)
+// over the same object sets as MeshHandler::isInCollision (meshhandler.hpp:187-243).  FCL's
+// MeshDistanceTraversalNode only prunes BV pairs whose lower bound is not below the running
+// minimum, so its answer is the minimum of TriangleDistance::triDistance over all triangle
+// pairs (fcl_math.h tri_distance, with the box-gated overlap answer).  Per edge:
+//   dist[e] = min over its poses, links and (env, agent) triangle pairs; DBL_MAX (FCL's
+//   initial DistanceResult::min_distance) for an edge without poses; 0 = in contact.
+//
+// Mapping: one wavefront per (unit, agent cluster), one agent triangle per lane (mapped
+// Q' = R Q + T exactly as for collision).  The wave walks the 64-ary env tree (EnvDev
+// items) depth first: at each node the lanes test its <= 64 children's float boxes against
+// the cluster's box, the nearest surviving child is entered at once and the others are
+// pushed (with their lower bound) on a per-wave LDS stack; a popped entry is re-tested
+// against the current bound.  At a bucket the lanes run triDistance against each of its
+// env triangles, skipping pairs whose exact box gap exceeds the bound.  The running bound
+// U of the edge is shared by every wave of the edge through a 64-bit atomicMin on the
+// double's bit pattern (non-negative doubles order like their bits); it only prunes, so
+// the result is the exact minimum whatever the interleaving.
+#include <float.h>
+#include <string.h>
+
+#include "../../include/mpt.h"
+#include "collide_common.h"
+
+namespace mpt {
+
+constexpr int kDistWaves = 4;
+constexpr int kDistStack = kMaxLevels * kWave;
+
+__device__ __forceinline__ double read_best(const unsigned long long *p) {
+    return __longlong_as_double((long long)__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+}
+
+// Squared float bound for the widened-box tests: the boxes are widened beyond float
+// rounding (fcl_math.h widen_*), the factor covers the rounding of the float sum.
+__device__ __forceinline__ float prune2(double U) {
+    const float u = (float)(U * (1.0 + 1e-5) + 1e-6);  // DBL_MAX -> inf
+    return u * u;
+}
+
+__device__ __forceinline__ float gap2f(const float alo[3], const float ahi[3], const float *blo, const float *bhi) {
+    float s = 0.f;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        const float g = fmaxf(fmaxf(alo[k] - bhi[k], blo[k] - ahi[k]), 0.f);
+        s += g * g;
+    }
+    return s;
+}
+
+__device__ __forceinline__ double wave_min_d(double v) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v = fmin(v, __shfl_xor(v, off));
+    return v;
+}
+
+struct DistCounters {
+    uint32_t waves = 0, items = 0, tri_calls = 0, pair_tests = 0;
+};
+
+__device__ void distance_wave(const EnvDev &env, const AgentDev *__restrict__ links, const DistWork &w, int64_t unit,
+                              int32_t cl, int lane, int32_t *stk_i, int32_t *stk_l, float *stk_b, DistCounters &cnt) {
+    const int32_t L = w.L;
+    const int32_t link = (int32_t)(unit % L);
+    const int64_t slot = unit / L;
+    const int64_t edge = w.pose_edge[slot];
+    const AgentDev ag = links[link];
+    if (cl >= ag.n_clusters) return;
+    unsigned long long *bp = w.best + edge;
+    double U = read_best(bp);
+    if (U == 0.0) return;  // defaultDistanceFunction stops at dist <= 0
+    ++cnt.waves;
+
+    double R[9], T[3];
+    unit_transform(env, w.poses + (slot * L + link) * 12, R, T);
+#pragma unroll
+    for (int i = 0; i < 9; ++i) R[i] = uniform_d(R[i]);
+#pragma unroll
+    for (int i = 0; i < 3; ++i) T[i] = uniform_d(T[i]);
+    const Cluster c = ag.clusters[cl];
+    float cblo[3], cbhi[3];
+    local_box(c.c, c.e, R, T, cblo, cbhi);
+
+    const bool act = lane < c.count;
+    v3 Q[3] = {mk(0, 0, 0), mk(0, 0, 0), mk(0, 0, 0)};
+    double qlo[3] = {0, 0, 0}, qhi[3] = {0, 0, 0};
+    if (act) {
+        const double *t = ag.tris + (int64_t)(c.first + lane) * 9;
+#pragma unroll
+        for (int v = 0; v < 3; ++v) Q[v] = xform(R, T, mk(t[3 * v], t[3 * v + 1], t[3 * v + 2]));
+        qlo[0] = dmin(Q[0].x, dmin(Q[1].x, Q[2].x));
+        qlo[1] = dmin(Q[0].y, dmin(Q[1].y, Q[2].y));
+        qlo[2] = dmin(Q[0].z, dmin(Q[1].z, Q[2].z));
+        qhi[0] = dmax(Q[0].x, dmax(Q[1].x, Q[2].x));
+        qhi[1] = dmax(Q[0].y, dmax(Q[1].y, Q[2].y));
+        qhi[2] = dmax(Q[0].z, dmax(Q[1].z, Q[2].z));
+    }
+    double lane_best = DBL_MAX;
+
+    int sp = 0;
+    int lev = env.n_levels - 1;
+    int32_t first = env.lev_off[lev];
+    int32_t count = env.lev_off[lev + 1] - first;
+    for (;;) {
+        const float Uf2 = prune2(U);
+        float lb = __builtin_huge_valf();
+        int32_t cf = 0, cc = 0;
+        bool keep = false;
+        if (lane < count) {
+            const Item it = env.items[first + lane];
+            lb = gap2f(cblo, cbhi, it.lo, it.hi);
+            keep = lb <= Uf2;
+            cf = it.first;
+            cc = it.count;
+        }
+        cnt.items += (uint32_t)count;
+        uint64_t m = __ballot(keep);
+        if (lev == 1) {
+            // buckets: exact pairs against each surviving bucket's triangles
+            while (m) {
+                const int j = __ffsll((unsigned long long)m) - 1;
+                m &= m - 1;
+                if (__shfl(lb, j) > prune2(U)) continue;
+                const int32_t bf = __builtin_amdgcn_readfirstlane(__shfl(cf, j));
+                const int32_t bc = __builtin_amdgcn_readfirstlane(__shfl(cc, j));
+                for (int32_t t = bf; t < bf + bc; ++t) {
+                    const EnvTri &E = env.tris[t];
+                    const double bound = dmin(U, lane_best);
+                    const double thr = bound * (1.0 + 1e-9) + 1e-9;
+                    double g2 = 0.0;
+#pragma unroll
+                    for (int k = 0; k < 3; ++k) {
+                        const double g = dmax(dmax(E.lo[k] - qhi[k], qlo[k] - E.hi[k]), 0.0);
+                        g2 += g * g;
+                    }
+                    cnt.pair_tests += act ? 1u : 0u;
+                    if (act && g2 <= thr * thr) {
+                        const v3 S[3] = {mk(E.P1[0], E.P1[1], E.P1[2]), mk(E.P2[0], E.P2[1], E.P2[2]),
+                                         mk(E.P3[0], E.P3[1], E.P3[2])};
+                        const double d = tri_distance(S, E.lo, E.hi, Q);
+                        lane_best = dmin(lane_best, d);
+                        ++cnt.tri_calls;
+                    }
+                }
+                const double wb = wave_min_d(lane_best);
+                if (wb < U) {
+                    if (lane == 0) atomicMin(bp, (unsigned long long)__double_as_longlong(wb));
+                    U = wb;
+                }
+                U = dmin(U, read_best(bp));
+                U = uniform_d(U);
+                if (U == 0.0) return;
+            }
+        } else if (m) {
+            // enter the nearest surviving child now, push the others
+            float v = keep ? lb : __builtin_huge_valf();
+            int idx = lane;
+#pragma unroll
+            for (int off = 32; off > 0; off >>= 1) {
+                const float ov = __shfl_xor(v, off);
+                const int oi = __shfl_xor(idx, off);
+                if (ov < v || (ov == v && oi < idx)) {
+                    v = ov;
+                    idx = oi;
+                }
+            }
+            const int j = __builtin_amdgcn_readfirstlane(idx);
+            const uint64_t rest = m & ~(1ull << j);
+            if (keep && lane != j) {
+                const int pos = sp + (int)__popcll(rest & ((1ull << lane) - 1));
+                stk_i[pos] = first + lane;
+                stk_l[pos] = lev;
+                stk_b[pos] = lb;
+            }
+            sp += (int)__popcll(rest);
+            first = __builtin_amdgcn_readfirstlane(__shfl(cf, j));
+            count = __builtin_amdgcn_readfirstlane(__shfl(cc, j));
+            lev -= 1;
+            continue;
+        }
+        // pop the next pending subtree that can still hold the minimum
+        U = uniform_d(dmin(U, read_best(bp)));
+        if (U == 0.0) return;
+        const float Uf2p = prune2(U);
+        bool found = false;
+        while (sp > 0) {
+            --sp;
+            if (stk_b[sp] <= Uf2p) {
+                const Item it = env.items[stk_i[sp]];
+                first = __builtin_amdgcn_readfirstlane(it.first);
+                count = __builtin_amdgcn_readfirstlane(it.count);
+                lev = __builtin_amdgcn_readfirstlane(stk_l[sp] - 1);
+                found = true;
+                break;
+            }
+        }
+        if (!found) return;
+    }
+}
+
+__global__ __launch_bounds__(kDistWaves * 64) void k_distance(EnvDev env, const AgentDev *__restrict__ links,
+                                                              DistWork w) {
+    __shared__ int32_t s_idx[kDistWaves][kDistStack];
+    __shared__ int32_t s_lev[kDistWaves][kDistStack];
+    __shared__ float s_lb[kDistWaves][kDistStack];
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    const int64_t g = (int64_t)blockIdx.x * kDistWaves + wave;
+    const int64_t unit = g / w.max_clusters;
+    const int32_t cl = (int32_t)(g % w.max_clusters);
+    DistCounters cnt;
+    if (unit < w.n_units)
+        distance_wave(env, links, w, unit, cl, lane, s_idx[wave], s_lev[wave], s_lb[wave], cnt);
+    if (w.stats && lane == 0 && cnt.waves) {
+        atomicAdd(w.stats + 0, (unsigned long long)cnt.waves);
+        atomicAdd(w.stats + 1, (unsigned long long)cnt.items);
+        atomicAdd(w.stats + 2, (unsigned long long)cnt.tri_calls);
+        atomicAdd(w.stats + 3, (unsigned long long)cnt.pair_tests);
+    }
+}
+
+__global__ void k_fill_u64(unsigned long long *p, int64_t n, unsigned long long v) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) p[i] = v;
+}
+
+void launch_distance(const EnvDev &env, const AgentDev *d_links, const DistWork &w, int64_t E, hipStream_t stream) {
+    if (E <= 0) return;
+    const double dmax_v = DBL_MAX;
+    unsigned long long inf_bits;
+    memcpy(&inf_bits, &dmax_v, sizeof inf_bits);
+    hipLaunchKernelGGL(k_fill_u64, dim3((unsigned)((E + 255) / 256)), dim3(256), 0, stream, w.best, E, inf_bits);
+    hip_check(hipGetLastError(), "k_fill_u64 launch");
+    if (w.n_units <= 0 || env.n_tris <= 0) return;
+    const int64_t waves = w.n_units * w.max_clusters;
+    const int64_t blocks = (waves + kDistWaves - 1) / kDistWaves;
+    if (blocks > 0x7fffffff) throw Error{MPT_ERR_INVALID, "distance batch too large"};
+    hipLaunchKernelGGL(k_distance, dim3((unsigned)blocks), dim3(kDistWaves * 64), 0, stream, env, d_links, w);
+    hip_check(hipGetLastError(), "k_distance launch");
+}
+
+}  // namespace mpt

@@ -87,7 +87,9 @@ struct EnvTri {
     double gP[3][2];// min/max of {p1,p2,p3}.g_i
     double lo[3];   // min over P1,P2,P3 (env-local, exact)
     double hi[3];   // max over P1,P2,P3
-    double pad[7];
+    double P2[3];   // the other two vertices as given (triangle distance)
+    double P3[3];
+    double pad[1];
 };
 static_assert(sizeof(EnvTri) == 48 * 8, "EnvTri layout");
 
@@ -117,6 +119,8 @@ inline void make_env_tri(const double *t, EnvTri &r) {
     for (int k = 0; k < 3; ++k) {
         r.lo[k] = dmin(v[0][k], dmin(v[1][k], v[2][k]));
         r.hi[k] = dmax(v[0][k], dmax(v[1][k], v[2][k]));
+        r.P2[k] = t[3 + k];
+        r.P3[k] = t[6 + k];
     }
     for (double &x : r.pad) x = 0.0;
 }
@@ -186,6 +190,142 @@ MPT_HD bool tri_intersect(const ETri &E, v3 Q1, v3 Q2, v3 Q3) {
     if (!project6_p(cross(f2, m1), p2, p3, q1, q2, q3)) return false;
     if (!project6_p(cross(f3, m1), p2, p3, q1, q2, q3)) return false;
     return true;
+}
+
+MPT_HD v3 add(v3 a, v3 b) { return v3{a.x + b.x, a.y + b.y, a.z + b.z}; }
+MPT_HD v3 scale(v3 a, double s) { return v3{a.x * s, a.y * s, a.z * s}; }
+
+// TriangleDistance::segPoints ([upstream] FCL 0.3.2 intersect.cpp, PQP's SegPoints):
+// closest points X on P + t A and Y on Q + u B, and VEC, the direction the caller tests
+// the off-edge vertices against.
+MPT_HD void seg_points(v3 P, v3 A, v3 Q, v3 B, v3 &VEC, v3 &X, v3 &Y) {
+    const v3 T = sub(Q, P);
+    const double AA = dot(A, A), BB = dot(B, B), AB = dot(A, B), AT = dot(A, T), BT = dot(B, T);
+    const double denom = AA * BB - AB * AB;
+    double t = (AT * BB - BT * AB) / denom;
+    if (t < 0 || isnan(t)) t = 0;
+    else if (t > 1) t = 1;
+    const double u = (t * AB - BT) / BB;
+    if (u <= 0 || isnan(u)) {
+        Y = Q;
+        t = AT / AA;
+        if (t <= 0 || isnan(t)) {
+            X = P;
+            VEC = sub(Q, P);
+        } else if (t >= 1) {
+            X = add(P, A);
+            VEC = sub(Q, X);
+        } else {
+            X = add(P, scale(A, t));
+            VEC = cross(A, cross(T, A));
+        }
+    } else if (u >= 1) {
+        Y = add(Q, B);
+        t = (AB + AT) / AA;
+        if (t <= 0 || isnan(t)) {
+            X = P;
+            VEC = sub(Y, P);
+        } else if (t >= 1) {
+            X = add(P, A);
+            VEC = sub(Y, X);
+        } else {
+            X = add(P, scale(A, t));
+            VEC = cross(A, cross(sub(Y, P), A));
+        }
+    } else {
+        Y = add(Q, scale(B, u));
+        if (t <= 0 || isnan(t)) {
+            X = P;
+            VEC = cross(B, cross(T, B));
+        } else if (t >= 1) {
+            X = add(P, A);
+            VEC = cross(B, cross(sub(Q, X), B));
+        } else {
+            X = add(P, scale(A, t));
+            VEC = cross(A, B);
+            if (dot(VEC, T) < 0) VEC = scale(VEC, -1.0);
+        }
+    }
+}
+
+// One triangle's vertex projected onto the other's plane, if it lies inside that face
+// (the "case 1" test of TriangleDistance::triDistance).  Sn = normal of S, Snl = |Sn|^2,
+// Sv = S's edge vectors; Tp[i] = (S0 - T_i).Sn.  Returns true and the distance if found;
+// sets shown_disjoint when Sn separates.
+MPT_HD bool face_vertex(const v3 S[3], const v3 Sv[3], v3 Sn, double Snl, const v3 T[3], bool s_first,
+                        int &shown_disjoint, double &d) {
+    const double Tp[3] = {dot(sub(S[0], T[0]), Sn), dot(sub(S[0], T[1]), Sn), dot(sub(S[0], T[2]), Sn)};
+    int point = -1;
+    if (Tp[0] > 0 && Tp[1] > 0 && Tp[2] > 0) {
+        point = Tp[0] < Tp[1] ? 0 : 1;
+        if (Tp[2] < Tp[point]) point = 2;
+    } else if (Tp[0] < 0 && Tp[1] < 0 && Tp[2] < 0) {
+        point = Tp[0] > Tp[1] ? 0 : 1;
+        if (Tp[2] > Tp[point]) point = 2;
+    }
+    if (point < 0) return false;
+    shown_disjoint = 1;
+    // selects, not T[point] / Tp[point]: a dynamic index would put the arrays in scratch
+    const v3 Tq = point == 0 ? T[0] : (point == 1 ? T[1] : T[2]);
+    const double Tpp = point == 0 ? Tp[0] : (point == 1 ? Tp[1] : Tp[2]);
+    if (!(dot(sub(Tq, S[0]), cross(Sn, Sv[0])) > 0)) return false;
+    if (!(dot(sub(Tq, S[1]), cross(Sn, Sv[1])) > 0)) return false;
+    if (!(dot(sub(Tq, S[2]), cross(Sn, Sv[2])) > 0)) return false;
+    const v3 proj = add(Tq, scale(Sn, Tpp / Snl));
+    // (P - Q).length() with P on S's face, Q the vertex of T
+    const v3 V = s_first ? sub(proj, Tq) : sub(Tq, proj);
+    d = sqrt(dot(V, V));
+    return true;
+}
+
+// TriangleDistance::triDistance(S1..S3, T1..T3) ([upstream] FCL 0.3.2 intersect.cpp, PQP's
+// TriDist) on T already mapped into S's frame (Q' = R Q + T, as for tri_intersect).
+// Build-defined gate, the distance counterpart of tri_gate: the final "no edge pair or face
+// vertex explains the minimum, so the triangles overlap -> 0" answer is given only when the
+// exact boxes of S and T overlap; otherwise the edge-pair minimum is returned.  For
+// non-degenerate triangles the two agree (overlapping triangles have overlapping boxes);
+// for collinear ones FCL's answer is 0 at any distance.
+MPT_HD double tri_distance(const v3 S[3], const double slo[3], const double shi[3], const v3 T[3]) {
+    const v3 Sv[3] = {sub(S[1], S[0]), sub(S[2], S[1]), sub(S[0], S[2])};
+    const v3 Tv[3] = {sub(T[1], T[0]), sub(T[2], T[1]), sub(T[0], T[2])};
+    const v3 D0 = sub(S[0], T[0]);
+    double mindd = dot(D0, D0) + 1;
+    int shown_disjoint = 0;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+            v3 VEC, P, Q;
+            seg_points(S[i], Sv[i], T[j], Tv[j], VEC, P, Q);
+            const v3 V = sub(Q, P);
+            const double dd = dot(V, V);
+            if (dd <= mindd) {
+                mindd = dd;
+                double a = dot(sub(S[(i + 2) % 3], P), VEC);
+                double b = dot(sub(T[(j + 2) % 3], Q), VEC);
+                if (a <= 0 && b >= 0) return sqrt(dd);
+                const double p = dot(V, VEC);
+                if (a < 0) a = 0;
+                if (b > 0) b = 0;
+                if (p - a + b > 0) shown_disjoint = 1;
+            }
+        }
+    }
+    double d;
+    const v3 Sn = cross(Sv[0], Sv[1]);
+    const double Snl = dot(Sn, Sn);
+    if (Snl > 1e-15 && face_vertex(S, Sv, Sn, Snl, T, true, shown_disjoint, d)) return d;
+    const v3 Tn = cross(Tv[0], Tv[1]);
+    const double Tnl = dot(Tn, Tn);
+    if (Tnl > 1e-15 && face_vertex(T, Tv, Tn, Tnl, S, false, shown_disjoint, d)) return d;
+    if (shown_disjoint) return sqrt(mindd);
+    const double tlo[3] = {dmin(T[0].x, dmin(T[1].x, T[2].x)), dmin(T[0].y, dmin(T[1].y, T[2].y)),
+                           dmin(T[0].z, dmin(T[1].z, T[2].z))};
+    const double thi[3] = {dmax(T[0].x, dmax(T[1].x, T[2].x)), dmax(T[0].y, dmax(T[1].y, T[2].y)),
+                           dmax(T[0].z, dmax(T[1].z, T[2].z))};
+    const bool boxes = slo[0] <= thi[0] && tlo[0] <= shi[0] && slo[1] <= thi[1] && tlo[1] <= shi[1] &&
+                       slo[2] <= thi[2] && tlo[2] <= shi[2];
+    return boxes ? 0.0 : sqrt(mindd);
 }
 
 // FLANN 1.8.4 L2<double>::operator() accumulation order: groups of four

@@ -155,6 +155,21 @@ void launch_collide_split(const EnvDev &env, const AgentDev *d_links, int32_t ma
                           CollideScratch &s, hipStream_t stream, hipEvent_t *marks = nullptr);
 void launch_pose_edge(const int64_t *d_offsets, int64_t E, int32_t *d_pose_edge, hipStream_t stream);
 
+// ---------------- distance (distance.hip) ----------------
+// Units are (pose, link) pairs as for collide mode A; best[E] receives the per-edge minimum
+// distance as the bit pattern of a double (DBL_MAX when the edge has no poses).
+struct DistWork {
+    const double *poses;       // [P][L][12]
+    const int32_t *pose_edge;  // [P]
+    int32_t L;
+    int32_t max_clusters;      // over the links
+    int64_t n_units;           // P * L
+    unsigned long long *best;  // [E]
+    // optional [4]: (unit, cluster) waves, env item box tests, triDistance calls, pair box tests
+    unsigned long long *stats;
+};
+void launch_distance(const EnvDev &env, const AgentDev *d_links, const DistWork &w, int64_t E, hipStream_t stream);
+
 // ---------------- NN ----------------
 struct NNWork {
     const double *pts;       // [n][d]

@@ -1045,3 +1045,188 @@ int64_t orc_prm_build(const orc_bvh *env, const double env_tf[12], const double 
     free(poses);
     return ne <= cap ? ne : -1;
 }
+
+/* ======================================================================
+ * Mesh-vs-mesh distance: FCL 0.3.2 TriangleDistance [upstream] (a port of PQP's
+ * TriDist.cpp), called by MeshDistanceTraversalNode leaf tests under fcl::distance, which
+ * utilities/fcl_helpers.hpp:67-84 (defaultDistanceFunction) drives over the broadphase.
+ * ====================================================================== */
+
+static void seg_pts(const double P[3], const double A[3], const double Q[3], const double B[3],
+                    double VEC[3], double X[3], double Y[3]) {
+    double T[3], TMP[3], W[3];
+    int k;
+    sub3(Q, P, T);
+    const double AA = dot3(A, A), BB = dot3(B, B), AB = dot3(A, B), AT = dot3(A, T), BT = dot3(B, T);
+    const double denom = AA * BB - AB * AB;
+    double t = (AT * BB - BT * AB) / denom;
+    if ((t < 0) || isnan(t)) t = 0;
+    else if (t > 1) t = 1;
+    double u = (t * AB - BT) / BB;
+    if ((u <= 0) || isnan(u)) {
+        for (k = 0; k < 3; ++k) Y[k] = Q[k];
+        t = AT / AA;
+        if ((t <= 0) || isnan(t)) {
+            for (k = 0; k < 3; ++k) X[k] = P[k];
+            sub3(Q, P, VEC);
+        } else if (t >= 1) {
+            for (k = 0; k < 3; ++k) X[k] = P[k] + A[k];
+            sub3(Q, X, VEC);
+        } else {
+            for (k = 0; k < 3; ++k) X[k] = P[k] + A[k] * t;
+            cross3(T, A, TMP);
+            cross3(A, TMP, VEC);
+        }
+    } else if (u >= 1) {
+        for (k = 0; k < 3; ++k) Y[k] = Q[k] + B[k];
+        t = (AB + AT) / AA;
+        if ((t <= 0) || isnan(t)) {
+            for (k = 0; k < 3; ++k) X[k] = P[k];
+            sub3(Y, P, VEC);
+        } else if (t >= 1) {
+            for (k = 0; k < 3; ++k) X[k] = P[k] + A[k];
+            sub3(Y, X, VEC);
+        } else {
+            for (k = 0; k < 3; ++k) X[k] = P[k] + A[k] * t;
+            sub3(Y, P, W);
+            cross3(W, A, TMP);
+            cross3(A, TMP, VEC);
+        }
+    } else {
+        for (k = 0; k < 3; ++k) Y[k] = Q[k] + B[k] * u;
+        if ((t <= 0) || isnan(t)) {
+            for (k = 0; k < 3; ++k) X[k] = P[k];
+            cross3(T, B, TMP);
+            cross3(B, TMP, VEC);
+        } else if (t >= 1) {
+            for (k = 0; k < 3; ++k) X[k] = P[k] + A[k];
+            sub3(Q, X, W);
+            cross3(W, B, TMP);
+            cross3(B, TMP, VEC);
+        } else {
+            for (k = 0; k < 3; ++k) X[k] = P[k] + A[k] * t;
+            cross3(A, B, VEC);
+            if (dot3(VEC, T) < 0)
+                for (k = 0; k < 3; ++k) VEC[k] = VEC[k] * -1.0;
+        }
+    }
+}
+
+double orc_tri_distance(const double S_[9], const double T_[9]) {
+    const double *S[3] = {S_, S_ + 3, S_ + 6}, *T[3] = {T_, T_ + 3, T_ + 6};
+    double Sv[3][3], Tv[3][3], VEC[3], P[3], Q[3], V[3], Z[3];
+    int i, j, k, shown_disjoint = 0;
+    for (i = 0; i < 3; ++i) {
+        sub3(S[(i + 1) % 3], S[i], Sv[i]);
+        sub3(T[(i + 1) % 3], T[i], Tv[i]);
+    }
+    sub3(S[0], T[0], V);
+    double mindd = dot3(V, V) + 1; /* first minimum safely high */
+    for (i = 0; i < 3; ++i)
+        for (j = 0; j < 3; ++j) {
+            seg_pts(S[i], Sv[i], T[j], Tv[j], VEC, P, Q);
+            sub3(Q, P, V);
+            const double dd = dot3(V, V);
+            if (dd <= mindd) {
+                mindd = dd;
+                sub3(S[(i + 2) % 3], P, Z);
+                double a = dot3(Z, VEC);
+                sub3(T[(j + 2) % 3], Q, Z);
+                double b = dot3(Z, VEC);
+                if ((a <= 0) && (b >= 0)) return sqrt(dd);
+                const double p = dot3(V, VEC);
+                if (a < 0) a = 0;
+                if (b > 0) b = 0;
+                if ((p - a + b) > 0) shown_disjoint = 1;
+            }
+        }
+    /* case 1: a vertex of one triangle over the face of the other; first T over S */
+    for (int side = 0; side < 2; ++side) {
+        const double *const *A = side == 0 ? S : T, *const *B = side == 0 ? T : S;
+        double (*Av)[3] = side == 0 ? Sv : Tv;
+        double N[3];
+        cross3(Av[0], Av[1], N);
+        const double Nl = dot3(N, N);
+        if (!(Nl > 1e-15)) continue;
+        double Bp[3];
+        for (k = 0; k < 3; ++k) {
+            sub3(A[0], B[k], V);
+            Bp[k] = dot3(V, N);
+        }
+        int point = -1;
+        if ((Bp[0] > 0) && (Bp[1] > 0) && (Bp[2] > 0)) {
+            point = (Bp[0] < Bp[1]) ? 0 : 1;
+            if (Bp[2] < Bp[point]) point = 2;
+        } else if ((Bp[0] < 0) && (Bp[1] < 0) && (Bp[2] < 0)) {
+            point = (Bp[0] > Bp[1]) ? 0 : 1;
+            if (Bp[2] > Bp[point]) point = 2;
+        }
+        if (point < 0) continue;
+        shown_disjoint = 1;
+        int inside = 1;
+        for (k = 0; k < 3 && inside; ++k) {
+            sub3(B[point], A[k], V);
+            cross3(N, Av[k], Z);
+            inside = dot3(V, Z) > 0;
+        }
+        if (!inside) continue;
+        double F[3];
+        for (k = 0; k < 3; ++k) F[k] = B[point][k] + N[k] * (Bp[point] / Nl);
+        sub3(F, B[point], V);
+        return sqrt(dot3(V, V));
+    }
+    if (shown_disjoint) return sqrt(mindd); /* FCL also returns minP / minQ as the points */
+    /* overlap answer, gated on the exact boxes (the build's definition) */
+    return tri_gate(S_, T_) ? 0.0 : sqrt(mindd);
+}
+
+/* exact box gap between two triangles, a lower bound on any distance between them */
+static double tri_gap2(const double *A, const double *B) {
+    double alo[3], ahi[3], blo[3], bhi[3], s = 0;
+    tri_box(A, alo, ahi);
+    tri_box(B, blo, bhi);
+    for (int k = 0; k < 3; ++k) {
+        double g = fmax(fmax(alo[k] - bhi[k], blo[k] - ahi[k]), 0.0);
+        s += g * g;
+    }
+    return s;
+}
+
+double orc_distance_unit(const double *env_tris, int64_t Te, const double env_tf[12],
+                         const double *agent_tris, int64_t Ta, const double pose[12]) {
+    double R[9], T[3], Qp[9];
+    double best = DBL_MAX;
+    unit_RT(env_tf, pose, R, T);
+    for (int64_t b = 0; b < Ta && best > 0; ++b) {
+        map_tri(R, T, agent_tris + 9 * b, Qp);
+        for (int64_t a = 0; a < Te && best > 0; ++a) {
+            /* the gap is a lower bound on the computed distance up to rounding; the slack
+             * keeps every pair that could reach the minimum */
+            const double thr = best * (1 + 1e-9) + 1e-9;
+            if (tri_gap2(env_tris + 9 * a, Qp) > thr * thr) continue;
+            const double d = orc_tri_distance(env_tris + 9 * a, Qp);
+            if (d < best) best = d;
+        }
+    }
+    return best;
+}
+
+void orc_distance_batch(const double *env_tris, int64_t Te, const double env_tf[12],
+                        const double *agent_tris, const int64_t *link_tri_off, int32_t L,
+                        const double *poses, const int64_t *edge_pose_offsets, int64_t E,
+                        double *dist, int nthreads) {
+#ifdef _OPENMP
+#pragma omp parallel for schedule(dynamic, 1) num_threads(nthreads > 0 ? nthreads : 1)
+#endif
+    for (int64_t e = 0; e < E; ++e) {
+        double best = DBL_MAX;
+        for (int64_t p = edge_pose_offsets[e]; p < edge_pose_offsets[e + 1] && best > 0; ++p)
+            for (int32_t l = 0; l < L && best > 0; ++l) {
+                const double d = orc_distance_unit(env_tris, Te, env_tf, agent_tris + 9 * link_tri_off[l],
+                                                   link_tri_off[l + 1] - link_tri_off[l], poses + 12 * (p * L + l));
+                if (d < best) best = d;
+            }
+        dist[e] = best;
+    }
+    (void)nthreads;
+}

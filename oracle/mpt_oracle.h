@@ -151,6 +151,19 @@ int64_t orc_prm_build(const orc_bvh *env, const double env_tf[12], const double 
                       const double *states, int64_t n, int32_t k, int32_t batch, double cc_dt,
                       int32_t *edges, double *costs, int64_t cap, int32_t *comp);
 
+/* Mesh-vs-mesh distance (utilities/fcl_helpers.hpp:67-84 defaultDistanceFunction over the
+ * isInCollision object sets, meshhandler.hpp:187-243): FCL 0.3.2 TriangleDistance::triDistance
+ * [upstream] with the build's box gate on the overlap answer.  T is already in
+ * S's frame.  orc_distance_unit = min over all (env, agent) triangle pairs (exact pruning by
+ * box gaps); orc_distance_batch = per edge, min over its poses and links (DBL_MAX if none). */
+double orc_tri_distance(const double S[9], const double T[9]);
+double orc_distance_unit(const double *env_tris, int64_t Te, const double env_tf[12],
+                         const double *agent_tris, int64_t Ta, const double pose[12]);
+void orc_distance_batch(const double *env_tris, int64_t Te, const double env_tf[12],
+                        const double *agent_tris, const int64_t *link_tri_off, int32_t L,
+                        const double *poses, const int64_t *edge_pose_offsets, int64_t E,
+                        double *dist, int nthreads);
+
 #ifdef __cplusplus
 }
 #endif

@@ -69,6 +69,9 @@ def lib():
             "orc_rrt_run": (I64, [I32, P, I32, P, P, P, P, D, D, P, I64, P, P, I64, I64, I64, P, P, P, P]),
             "orc_engine_step": (I64, [I32, P, I32, P, D, D, U64, U64, I32, P, P, P, I64, P, P, I64, I64, P, P, C.c_int, C.c_int]),
             "orc_prm_build": (I64, [P, P, P, I64, P, I64, I32, I32, D, P, P, I64, P]),
+            "orc_tri_distance": (D, [P, P]),
+            "orc_distance_unit": (D, [P, I64, P, P, I64, P]),
+            "orc_distance_batch": (None, [P, I64, P, P, P, I32, P, P, I64, P, C.c_int]),
         }
         for name, (res, args) in sig.items():
             f = getattr(L, name)
@@ -115,6 +118,26 @@ def collide_batch(env_tris, env_tf, link_tris: list, poses, edge_offsets) -> np.
     out = np.zeros(E, np.uint8)
     lib().orc_collide_batch(_p(env_tris), env_tris.shape[0], _p(_f64(env_tf)), _p(agent), _p(off),
                             len(link_tris), _p(poses), _p(eo), E, _p(out))
+    return out
+
+
+def tri_distance(S, T) -> float:
+    """FCL triDistance (T already in S's frame) with the box-gated overlap answer."""
+    return float(lib().orc_tri_distance(_p(_f64(S)), _p(_f64(T))))
+
+
+def distance_batch(env_tris, env_tf, link_tris: list, poses, edge_offsets, nthreads=1) -> np.ndarray:
+    """Per-edge minimum mesh-vs-mesh distance (DBL_MAX for an edge without poses)."""
+    env_tris = _f64(env_tris).reshape(-1, 9)
+    agent = _f64(np.concatenate([np.asarray(t, np.float64).reshape(-1, 9) for t in link_tris]))
+    off = np.zeros(len(link_tris) + 1, np.int64)
+    off[1:] = np.cumsum([np.asarray(t).reshape(-1, 9).shape[0] for t in link_tris])
+    poses = _f64(poses)
+    eo = np.ascontiguousarray(edge_offsets, np.int64)
+    E = len(eo) - 1
+    out = np.zeros(E)
+    lib().orc_distance_batch(_p(env_tris), env_tris.shape[0], _p(_f64(env_tf)), _p(agent), _p(off),
+                             len(link_tris), _p(poses), _p(eo), E, _p(out), nthreads)
     return out
 
 

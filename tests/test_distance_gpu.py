@@ -1,0 +1,135 @@
+"""GPU parity: batched mesh-vs-mesh minimum distance (k_distance through mpt_distance_batch)
+against the oracle's restatement of FCL's TriangleDistance over all triangle pairs.  The
+result is a minimum of identically computed FP64 values, so the bar is bit-exact."""
+import math
+
+import numpy as np
+import pytest
+
+from motionplanningtoolkit_amd import scenes
+
+pytestmark = pytest.mark.gpu
+
+I = np.array([1, 0, 0, 0, 1, 0, 0, 0, 1], np.float64)
+DBL_MAX = np.finfo(np.float64).max
+
+
+def pose(t, R=I):
+    return np.r_[np.asarray(R, np.float64).ravel(), np.asarray(t, np.float64)]
+
+
+def random_rot(rng):
+    q = rng.normal(size=4)
+    w, x, y, z = q / np.linalg.norm(q)
+    return np.array([1 - 2 * (y * y + z * z), 2 * (x * y - w * z), 2 * (x * z + w * y),
+                     2 * (x * y + w * z), 1 - 2 * (x * x + z * z), 2 * (y * z - w * x),
+                     2 * (x * z - w * y), 2 * (y * z + w * x), 1 - 2 * (x * x + y * y)])
+
+
+def bits(a):
+    return np.ascontiguousarray(a, np.float64).view(np.uint64)
+
+
+def check(mpt, oracle, env_tris, env_tf, links, poses, off, nthreads=8):
+    env = mpt.Environment(env_tris, env_tf)
+    ags = [mpt.AgentMesh(t) for t in links]
+    got = mpt.distance_batch(env, ags, poses, off)
+    ref = oracle.distance_batch(env_tris, env_tf, links, poses, off, nthreads=nthreads)
+    bad = np.nonzero(bits(got) != bits(ref))[0]
+    assert bad.size == 0, (bad[:10], got[bad[:10]], ref[bad[:10]])
+    return got
+
+
+def test_box_box_known_answers(mpt_gpu, oracle):
+    box = scenes.read_obj(scenes.mesh_path("agent_unit_box"), "last")
+    ts = [(3, 0, 0), (2.5, 0, 0), (1.5, 0, 0), (1.0, 0, 0), (0.5, 0, 0), (3, 4, 0), (3, 3, 3), (0, -2, 0.25)]
+    expect = [2.0, 1.5, 0.5, 0.0, 0.0, math.hypot(2, 3), math.sqrt(12), 1.0]
+    poses = np.array([pose(t) for t in ts]).reshape(-1, 1, 12)
+    got = check(mpt_gpu, oracle, box, pose([0, 0, 0]), [box], poses, np.arange(len(ts) + 1))
+    np.testing.assert_allclose(got, expect, rtol=0, atol=1e-12)
+
+
+def test_no_poses_and_empty(mpt_gpu, oracle):
+    box = scenes.read_obj(scenes.mesh_path("agent_unit_box"), "last")
+    env = mpt_gpu.Environment(box)
+    ag = mpt_gpu.AgentMesh(box)
+    poses = np.array([pose((5, 0, 0))]).reshape(-1, 1, 12)
+    got = mpt_gpu.distance_batch(env, [ag], poses, [0, 0, 1, 1])
+    assert got[0] == DBL_MAX and got[2] == DBL_MAX and got[1] == 4.0
+    assert mpt_gpu.distance_batch(env, [ag], np.zeros((0, 1, 12)), [0]).shape == (0,)
+
+
+def test_box_random_rotations(mpt_gpu, oracle):
+    rng = np.random.default_rng(3)
+    box = scenes.read_obj(scenes.mesh_path("agent_unit_box"), "last")
+    n = 2000
+    poses = np.array([pose(rng.uniform(-3, 3, 3), random_rot(rng)) for _ in range(n)]).reshape(-1, 1, 12)
+    got = check(mpt_gpu, oracle, box, pose([0.5, -0.25, 0.1], random_rot(rng)), [box], poses, np.arange(n + 1))
+    assert (got == 0).mean() > 0.05 and (got > 0).mean() > 0.5
+
+
+@pytest.mark.parametrize("agent_mode", ["last", "all"])
+def test_blimp_room_random_poses(mpt_gpu, oracle, agent_mode):
+    rng = np.random.default_rng(31 if agent_mode == "all" else 32)
+    env = scenes.read_obj(scenes.mesh_path("env_model"))
+    agent = scenes.read_obj(scenes.mesh_path("agent_blimp"), agent_mode)
+    n = 300
+    ts = rng.uniform([-30, -30, -30], [205, 165, 140], size=(n, 3))
+    poses = np.array([pose(t, random_rot(rng)) for t in ts]).reshape(-1, 1, 12)
+    got = check(mpt_gpu, oracle, env, pose([0, 0, 0]), [agent], poses, np.arange(n + 1))
+    assert (got == 0).any() and (got > 1).any()
+
+
+def test_edges_min_over_poses(mpt_gpu, oracle):
+    """Several poses per edge: the minimum over the edge, and contact anywhere gives 0."""
+    rng = np.random.default_rng(8)
+    env = scenes.read_obj(scenes.mesh_path("env_model"))
+    agent = scenes.read_obj(scenes.mesh_path("agent_blimp"), "last")
+    counts = rng.integers(0, 6, size=80)
+    off = np.r_[0, np.cumsum(counts)]
+    ts = rng.uniform([-20, -20, -20], [195, 155, 130], size=(off[-1], 3))
+    poses = np.array([pose(t, random_rot(rng)) for t in ts]).reshape(-1, 1, 12)
+    got = check(mpt_gpu, oracle, env, pose([0, 0, 0]), [agent], poses, off)
+    assert np.all(got[counts == 0] == DBL_MAX)
+
+
+def test_snake_links(mpt_gpu, oracle):
+    """Multi-link units (snake, L = 11 copies of the box mesh) in the corridor env."""
+    box = scenes.read_obj(scenes.mesh_path("agent_unit_box"), "last")
+    env = scenes.read_obj(scenes.mesh_path("env_corridor"))
+    rng = np.random.default_rng(4)
+    L, E = 11, 60
+    poses = np.array([pose(rng.uniform([-6, -52, -1], [6, 52, 1]), random_rot(rng)) for _ in range(E * L)])
+    poses[E * L // 2:, 11] += rng.uniform(2, 6, E * L - E * L // 2)  # second half above the walls
+    got = check(mpt_gpu, oracle, env, pose([0, 0, 0]), [box] * L, poses.reshape(E, L, 12), np.arange(E + 1))
+    assert (got == 0).any() and (got > 0).any()
+
+
+@pytest.mark.parametrize("nx,ny", [(2, 2), (4, 3)])
+def test_multi_room_env_deep_tree(mpt_gpu, oracle, nx, ny):
+    """Deeper env trees (three levels): the general depth-first walk and its LDS stack."""
+    env = scenes.rooms_env(nx, ny)
+    agent = scenes.read_obj(scenes.mesh_path("agent_blimp"), "last")
+    rng = np.random.default_rng(23)
+    n = 200
+    ts = rng.uniform([-10, -10, -10], [nx * 180 + 10, ny * 140 + 10, 125], size=(n, 3))
+    poses = np.array([pose(t, random_rot(rng)) for t in ts]).reshape(-1, 1, 12)
+    check(mpt_gpu, oracle, env, pose([0, 0, 0]), [agent], poses, np.arange(n + 1))
+
+
+def test_distance_agrees_with_collision(mpt_gpu):
+    """Size-independent property at a larger batch: a colliding pose is at distance ~0 and a
+    pose at a clear positive distance is collision free."""
+    rng = np.random.default_rng(12)
+    env_t = scenes.read_obj(scenes.mesh_path("env_model"))
+    agent_t = scenes.read_obj(scenes.mesh_path("agent_blimp"), "all")
+    env, ag = mpt_gpu.Environment(env_t), mpt_gpu.AgentMesh(agent_t)
+    n = 8192
+    ts = rng.uniform([-10, -10, -10], [185, 145, 120], size=(n, 3))
+    poses = np.array([pose(t, random_rot(rng)) for t in ts]).reshape(-1, 1, 12)
+    off = np.arange(n + 1)
+    d = mpt_gpu.distance_batch(env, [ag], poses, off)
+    v = mpt_gpu.collide_batch(env, [ag], poses, off)
+    assert np.all(d[v == 1] <= 1e-9)
+    assert np.all(v[d > 1e-6] == 0)
+    assert 0.05 < v.mean() < 0.95

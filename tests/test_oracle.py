@@ -331,3 +331,49 @@ def test_oracle_prm_roadmap_is_consistent(oracle):
     # batched: each milestone only sees the milestones before its batch
     e64, _, _ = oracle.prm_build(bvh, sc.env_tf, sc.agent_tris, states, k=10, batch=64, cc_dt=sc.cc_dt)
     assert np.all(e64[:, 0] < (e64[:, 1] // 64) * 64)
+
+
+def _sampled_tri_distance(S, T, n=60):
+    """Upper bound on the triangle distance from dense barycentric samples (independent of FCL)."""
+    u, v = np.meshgrid(np.linspace(0, 1, n), np.linspace(0, 1, n))
+    m = (u + v) <= 1
+    u, v = u[m], v[m]
+
+    def pts(X):
+        X = X.reshape(3, 3)
+        return X[0] + u[:, None] * (X[1] - X[0]) + v[:, None] * (X[2] - X[0])
+
+    from scipy.spatial import cKDTree
+
+    d, _ = cKDTree(pts(S)).query(pts(T))
+    return d.min()
+
+
+def test_tri_distance_known_answers(oracle):
+    """FCL TriangleDistance restatement: analytic cases for each branch."""
+    S = np.array([0, 0, 0, 1, 0, 0, 0, 1, 0.0])
+    assert oracle.tri_distance(S, S + np.array([0, 0, 2] * 3)) == 2.0          # parallel faces
+    assert oracle.tri_distance(S, np.array([2, 0, 0, 3, 0, 0, 2, 1, 0.0])) == 1.0  # coplanar, edge to vertex
+    # vertex over the face interior: projection case
+    T = np.array([0.2, 0.2, 0.5, 0.3, 0.2, 2, 0.2, 0.3, 2])
+    assert abs(oracle.tri_distance(S, T) - 0.5) < 1e-15
+    # skew edges: (0.5,0,0)-(0.5,0,0) region
+    T = np.array([0.5, -1, 1, 0.5, 1, 1, 0.5, 0, 3.0])
+    assert abs(oracle.tri_distance(S, T) - 1.0) < 1e-15
+    # crossing triangles -> 0
+    T = np.array([0.2, 0.2, -1, 0.2, 0.2, 1, 0.4, 0.1, 0.0])
+    assert oracle.tri_distance(S, T) == 0.0
+    # degenerate (collinear) triangle far away: the box gate keeps the edge distance
+    Tdeg = np.array([0, 0, 5, 1, 0, 5, 2, 0, 5.0])
+    assert abs(oracle.tri_distance(S, Tdeg) - 5.0) < 1e-12
+
+
+def test_tri_distance_matches_sampling(oracle):
+    rng = np.random.default_rng(0)
+    for _ in range(40):
+        S = rng.uniform(-1, 1, 9)
+        T = rng.uniform(-1, 1, 9) + rng.uniform(-1.5, 1.5, 3).repeat(3).reshape(3, 3).T.ravel()
+        d = oracle.tri_distance(S, T)
+        ds = _sampled_tri_distance(S, T)
+        assert d <= ds + 1e-12
+        assert d >= ds - 0.08  # sampling resolution (edge length / 60 across two triangles)
