@@ -107,7 +107,7 @@ mpt_status mpt_set_collide_mode(int32_t mode);
  * links and (env, agent) triangle pairs of FCL's TriangleDistance::triDistance; 0 = in
  * contact (the callback's dist <= 0 stop); DBL_MAX (the initial DistanceResult) for an edge
  * without poses.  Same arguments as mpt_collide_batch[_device].  mpt_last_collide_stats
- * then reports [(unit, cluster) waves, env box tests, triangle-distance calls, pair box tests]. */
+ * then reports [agent clusters walked, env box tests, triangle-distance calls, pair box tests]. */
 mpt_status mpt_distance_batch(const mpt_env *env, const mpt_agent *const *links, int32_t L, const double *poses,
                               const int64_t *edge_pose_offsets, int64_t E, double *dist_out, void *stream);
 mpt_status mpt_distance_batch_device(const mpt_env *env, const mpt_agent *const *links, int32_t L,

@@ -59,49 +59,46 @@ __device__ __forceinline__ double wave_min_d(double v) {
 }
 
 struct DistCounters {
-    uint32_t waves = 0, items = 0, tri_calls = 0, pair_tests = 0;
+    uint32_t clusters = 0, items = 0, tri_calls = 0, pair_tests = 0;
 };
 
-__device__ void distance_wave(const EnvDev &env, const AgentDev *__restrict__ links, const DistWork &w, int64_t unit,
-                              int32_t cl, int lane, int32_t *stk_i, int32_t *stk_l, float *stk_b, DistCounters &cnt) {
-    const int32_t L = w.L;
-    const int32_t link = (int32_t)(unit % L);
-    const int64_t slot = unit / L;
-    const int64_t edge = w.pose_edge[slot];
-    const AgentDev ag = links[link];
-    if (cl >= ag.n_clusters) return;
-    unsigned long long *bp = w.best + edge;
-    double U = read_best(bp);
-    if (U == 0.0) return;  // defaultDistanceFunction stops at dist <= 0
-    ++cnt.waves;
+// Per-wave LDS: the cluster's mapped agent triangles, the pair queue and the DFS stack.
+struct DistLds {
+    double q[kWave][9];        // Q' of the cluster's triangles, by lane
+    int32_t queue[2 * kWave];  // pending (env tri << 6 | agent lane) pairs
+    int32_t stk_i[kDistStack];
+    int32_t stk_l[kDistStack];
+    float stk_b[kDistStack];
+};
 
-    double R[9], T[3];
-    unit_transform(env, w.poses + (slot * L + link) * 12, R, T);
-#pragma unroll
-    for (int i = 0; i < 9; ++i) R[i] = uniform_d(R[i]);
-#pragma unroll
-    for (int i = 0; i < 3; ++i) T[i] = uniform_d(T[i]);
-    const Cluster c = ag.clusters[cl];
-    float cblo[3], cbhi[3];
-    local_box(c.c, c.e, R, T, cblo, cbhi);
-
-    const bool act = lane < c.count;
-    v3 Q[3] = {mk(0, 0, 0), mk(0, 0, 0), mk(0, 0, 0)};
-    double qlo[3] = {0, 0, 0}, qhi[3] = {0, 0, 0};
-    if (act) {
-        const double *t = ag.tris + (int64_t)(c.first + lane) * 9;
-#pragma unroll
-        for (int v = 0; v < 3; ++v) Q[v] = xform(R, T, mk(t[3 * v], t[3 * v + 1], t[3 * v + 2]));
-        qlo[0] = dmin(Q[0].x, dmin(Q[1].x, Q[2].x));
-        qlo[1] = dmin(Q[0].y, dmin(Q[1].y, Q[2].y));
-        qlo[2] = dmin(Q[0].z, dmin(Q[1].z, Q[2].z));
-        qhi[0] = dmax(Q[0].x, dmax(Q[1].x, Q[2].x));
-        qhi[1] = dmax(Q[0].y, dmax(Q[1].y, Q[2].y));
-        qhi[2] = dmax(Q[0].z, dmax(Q[1].z, Q[2].z));
+// Exact triangle distances of the queued pairs, one pair per lane; returns the new bound.
+__device__ __forceinline__ double flush_pairs(const EnvDev &env, DistLds &s, int n, int lane, double U,
+                                              unsigned long long *bp, DistCounters &cnt) {
+    double d = DBL_MAX;
+    if (lane < n) {
+        const int32_t e = s.queue[lane];
+        const double *qa = s.q[e & 63];
+        const v3 Q[3] = {mk(qa[0], qa[1], qa[2]), mk(qa[3], qa[4], qa[5]), mk(qa[6], qa[7], qa[8])};
+        const EnvTri &E = env.tris[e >> 6];
+        const v3 S[3] = {mk(E.P1[0], E.P1[1], E.P1[2]), mk(E.P2[0], E.P2[1], E.P2[2]), mk(E.P3[0], E.P3[1], E.P3[2])};
+        d = tri_distance(S, E.lo, E.hi, Q);
     }
-    double lane_best = DBL_MAX;
+    cnt.tri_calls += (uint32_t)n;
+    const double wb = wave_min_d(d);
+    if (wb < U) {
+        if (lane == 0) atomicMin(bp, (unsigned long long)__double_as_longlong(wb));
+        U = wb;
+    }
+    return uniform_d(dmin(U, read_best(bp)));
+}
 
-    int sp = 0;
+// Depth-first walk of the env tree for one agent cluster (box cblo/cbhi, lane's triangle
+// box qlo/qhi, Q' in s.q), nearest child first; pairs that survive the exact box-gap test
+// are queued and evaluated 64 at a time.  Returns the updated bound.
+__device__ double walk_cluster(const EnvDev &env, DistLds &s, const float cblo[3], const float cbhi[3], bool act,
+                               const double qlo[3], const double qhi[3], int lane, double U,
+                               unsigned long long *bp, DistCounters &cnt) {
+    int sp = 0, qn = 0;
     int lev = env.n_levels - 1;
     int32_t first = env.lev_off[lev];
     int32_t count = env.lev_off[lev + 1] - first;
@@ -120,40 +117,62 @@ __device__ void distance_wave(const EnvDev &env, const AgentDev *__restrict__ li
         cnt.items += (uint32_t)count;
         uint64_t m = __ballot(keep);
         if (lev == 1) {
-            // buckets: exact pairs against each surviving bucket's triangles
             while (m) {
                 const int j = __ffsll((unsigned long long)m) - 1;
                 m &= m - 1;
                 if (__shfl(lb, j) > prune2(U)) continue;
                 const int32_t bf = __builtin_amdgcn_readfirstlane(__shfl(cf, j));
                 const int32_t bc = __builtin_amdgcn_readfirstlane(__shfl(cc, j));
+                int32_t seed_t = -1;
+                if (U == DBL_MAX) {
+                    // first bucket of the edge: bound from one pair per agent triangle, its
+                    // env triangle of smallest box gap, before the gap test can prune anything
+                    double best_g2 = DBL_MAX;
+                    for (int32_t t = bf; t < bf + bc; ++t) {
+                        const EnvTri &E = env.tris[t];
+                        double g2 = 0.0;
+#pragma unroll
+                        for (int k = 0; k < 3; ++k) {
+                            const double g = dmax(dmax(E.lo[k] - qhi[k], qlo[k] - E.hi[k]), 0.0);
+                            g2 += g * g;
+                        }
+                        if (g2 < best_g2) {
+                            best_g2 = g2;
+                            seed_t = t;
+                        }
+                    }
+                    if (!act) seed_t = -1;
+                    const uint64_t pm = __ballot(act);
+                    if (act) s.queue[(int)__popcll(pm & ((1ull << lane) - 1))] = (seed_t << 6) | lane;
+                    U = flush_pairs(env, s, (int)__popcll(pm), lane, U, bp, cnt);
+                    if (U == 0.0) return U;
+                }
                 for (int32_t t = bf; t < bf + bc; ++t) {
                     const EnvTri &E = env.tris[t];
-                    const double bound = dmin(U, lane_best);
-                    const double thr = bound * (1.0 + 1e-9) + 1e-9;
+                    const double thr = U * (1.0 + 1e-9) + 1e-9;
                     double g2 = 0.0;
 #pragma unroll
                     for (int k = 0; k < 3; ++k) {
                         const double g = dmax(dmax(E.lo[k] - qhi[k], qlo[k] - E.hi[k]), 0.0);
                         g2 += g * g;
                     }
-                    cnt.pair_tests += act ? 1u : 0u;
-                    if (act && g2 <= thr * thr) {
-                        const v3 S[3] = {mk(E.P1[0], E.P1[1], E.P1[2]), mk(E.P2[0], E.P2[1], E.P2[2]),
-                                         mk(E.P3[0], E.P3[1], E.P3[2])};
-                        const double d = tri_distance(S, E.lo, E.hi, Q);
-                        lane_best = dmin(lane_best, d);
-                        ++cnt.tri_calls;
+                    const bool pass = act && t != seed_t && g2 <= thr * thr;
+                    const uint64_t pm = __ballot(pass);
+                    if (pass) s.queue[qn + (int)__popcll(pm & ((1ull << lane) - 1))] = (t << 6) | lane;
+                    qn += (int)__popcll(pm);
+                    cnt.pair_tests += (uint32_t)__popcll(__ballot(act));
+                    if (qn >= kWave) {
+                        U = flush_pairs(env, s, kWave, lane, U, bp, cnt);
+                        qn -= kWave;
+                        if (lane < qn) s.queue[lane] = s.queue[kWave + lane];
+                        if (U == 0.0) return U;
                     }
                 }
-                const double wb = wave_min_d(lane_best);
-                if (wb < U) {
-                    if (lane == 0) atomicMin(bp, (unsigned long long)__double_as_longlong(wb));
-                    U = wb;
+                if (qn > 0) {
+                    U = flush_pairs(env, s, qn, lane, U, bp, cnt);
+                    qn = 0;
+                    if (U == 0.0) return U;
                 }
-                U = dmin(U, read_best(bp));
-                U = uniform_d(U);
-                if (U == 0.0) return;
             }
         } else if (m) {
             // enter the nearest surviving child now, push the others
@@ -172,9 +191,9 @@ __device__ void distance_wave(const EnvDev &env, const AgentDev *__restrict__ li
             const uint64_t rest = m & ~(1ull << j);
             if (keep && lane != j) {
                 const int pos = sp + (int)__popcll(rest & ((1ull << lane) - 1));
-                stk_i[pos] = first + lane;
-                stk_l[pos] = lev;
-                stk_b[pos] = lb;
+                s.stk_i[pos] = first + lane;
+                s.stk_l[pos] = lev;
+                s.stk_b[pos] = lb;
             }
             sp += (int)__popcll(rest);
             first = __builtin_amdgcn_readfirstlane(__shfl(cf, j));
@@ -183,40 +202,118 @@ __device__ void distance_wave(const EnvDev &env, const AgentDev *__restrict__ li
             continue;
         }
         // pop the next pending subtree that can still hold the minimum
-        U = uniform_d(dmin(U, read_best(bp)));
-        if (U == 0.0) return;
         const float Uf2p = prune2(U);
         bool found = false;
         while (sp > 0) {
             --sp;
-            if (stk_b[sp] <= Uf2p) {
-                const Item it = env.items[stk_i[sp]];
+            if (s.stk_b[sp] <= Uf2p) {
+                const Item it = env.items[s.stk_i[sp]];
                 first = __builtin_amdgcn_readfirstlane(it.first);
                 count = __builtin_amdgcn_readfirstlane(it.count);
-                lev = __builtin_amdgcn_readfirstlane(stk_l[sp] - 1);
+                lev = __builtin_amdgcn_readfirstlane(s.stk_l[sp] - 1);
                 found = true;
                 break;
             }
         }
-        if (!found) return;
+        if (!found) return U;
+    }
+}
+
+// One wave per (pose, link) unit: clusters in increasing order of their lower bound over
+// the env tree's top level, each walked with the bound the earlier ones left.
+__device__ void distance_unit(const EnvDev &env, const AgentDev *__restrict__ links, const DistWork &w, int64_t unit,
+                              int lane, DistLds &s, DistCounters &cnt) {
+    const int32_t L = w.L;
+    const int32_t link = (int32_t)(unit % L);
+    const int64_t slot = unit / L;
+    const int64_t edge = w.pose_edge[slot];
+    const AgentDev ag = links[link];
+    unsigned long long *bp = w.best + edge;
+    double U = uniform_d(read_best(bp));
+    if (U == 0.0) return;  // defaultDistanceFunction stops at dist <= 0
+
+    double R[9], T[3];
+    unit_transform(env, w.poses + (slot * L + link) * 12, R, T);
+#pragma unroll
+    for (int i = 0; i < 9; ++i) R[i] = uniform_d(R[i]);
+#pragma unroll
+    for (int i = 0; i < 3; ++i) T[i] = uniform_d(T[i]);
+    const int top = env.n_levels - 1;
+    const int32_t tfirst = env.lev_off[top], tcount = env.lev_off[top + 1] - tfirst;
+
+    for (int32_t cbase = 0; cbase < ag.n_clusters; cbase += kWave) {
+        const int32_t ci = cbase + lane;
+        float clo[3] = {0, 0, 0}, chi[3] = {0, 0, 0};
+        float clb = __builtin_huge_valf();
+        if (ci < ag.n_clusters) {
+            const Cluster c = ag.clusters[ci];
+            local_box(c.c, c.e, R, T, clo, chi);
+            for (int32_t i = 0; i < tcount; ++i) {
+                const Item it = env.items[tfirst + i];
+                clb = fminf(clb, gap2f(clo, chi, it.lo, it.hi));
+            }
+        }
+        uint64_t rem = __ballot(ci < ag.n_clusters);
+        while (rem) {
+            // nearest remaining cluster first
+            float v = (rem >> lane) & 1 ? clb : __builtin_huge_valf();
+            int idx = lane;
+#pragma unroll
+            for (int off = 32; off > 0; off >>= 1) {
+                const float ov = __shfl_xor(v, off);
+                const int oi = __shfl_xor(idx, off);
+                if (ov < v || (ov == v && oi < idx)) {
+                    v = ov;
+                    idx = oi;
+                }
+            }
+            const int j = __builtin_amdgcn_readfirstlane(idx);
+            rem &= ~(1ull << j);
+            if (__shfl(clb, j) > prune2(U)) break;  // the rest are farther still
+            ++cnt.clusters;
+            float cblo[3], cbhi[3];
+#pragma unroll
+            for (int k = 0; k < 3; ++k) {
+                cblo[k] = __shfl(clo[k], j);
+                cbhi[k] = __shfl(chi[k], j);
+            }
+            const Cluster c = ag.clusters[cbase + j];
+            const bool act = lane < c.count;
+            double qlo[3] = {0, 0, 0}, qhi[3] = {0, 0, 0};
+            if (act) {
+                const double *t = ag.tris + (int64_t)(c.first + lane) * 9;
+                v3 Q[3];
+#pragma unroll
+                for (int k = 0; k < 3; ++k) Q[k] = xform(R, T, mk(t[3 * k], t[3 * k + 1], t[3 * k + 2]));
+#pragma unroll
+                for (int k = 0; k < 3; ++k) {
+                    s.q[lane][3 * k] = Q[k].x;
+                    s.q[lane][3 * k + 1] = Q[k].y;
+                    s.q[lane][3 * k + 2] = Q[k].z;
+                }
+                qlo[0] = dmin(Q[0].x, dmin(Q[1].x, Q[2].x));
+                qlo[1] = dmin(Q[0].y, dmin(Q[1].y, Q[2].y));
+                qlo[2] = dmin(Q[0].z, dmin(Q[1].z, Q[2].z));
+                qhi[0] = dmax(Q[0].x, dmax(Q[1].x, Q[2].x));
+                qhi[1] = dmax(Q[0].y, dmax(Q[1].y, Q[2].y));
+                qhi[2] = dmax(Q[0].z, dmax(Q[1].z, Q[2].z));
+            }
+            U = walk_cluster(env, s, cblo, cbhi, act, qlo, qhi, lane, U, bp, cnt);
+            if (U == 0.0) return;
+        }
     }
 }
 
 __global__ __launch_bounds__(kDistWaves * 64) void k_distance(EnvDev env, const AgentDev *__restrict__ links,
                                                               DistWork w) {
-    __shared__ int32_t s_idx[kDistWaves][kDistStack];
-    __shared__ int32_t s_lev[kDistWaves][kDistStack];
-    __shared__ float s_lb[kDistWaves][kDistStack];
+    __shared__ DistLds s_lds[kDistWaves];
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
-    const int64_t g = (int64_t)blockIdx.x * kDistWaves + wave;
-    const int64_t unit = g / w.max_clusters;
-    const int32_t cl = (int32_t)(g % w.max_clusters);
+    const int64_t unit = (int64_t)blockIdx.x * kDistWaves + wave;
     DistCounters cnt;
-    if (unit < w.n_units)
-        distance_wave(env, links, w, unit, cl, lane, s_idx[wave], s_lev[wave], s_lb[wave], cnt);
-    if (w.stats && lane == 0 && cnt.waves) {
-        atomicAdd(w.stats + 0, (unsigned long long)cnt.waves);
+    if (unit < w.n_units) distance_unit(env, links, w, unit, lane, s_lds[wave], cnt);
+    if (w.stats && lane == 0 && unit < w.n_units) {
+        atomicAdd(w.stats + 0, (unsigned long long)cnt.clusters);
         atomicAdd(w.stats + 1, (unsigned long long)cnt.items);
         atomicAdd(w.stats + 2, (unsigned long long)cnt.tri_calls);
         atomicAdd(w.stats + 3, (unsigned long long)cnt.pair_tests);
@@ -236,8 +333,7 @@ void launch_distance(const EnvDev &env, const AgentDev *d_links, const DistWork 
     hipLaunchKernelGGL(k_fill_u64, dim3((unsigned)((E + 255) / 256)), dim3(256), 0, stream, w.best, E, inf_bits);
     hip_check(hipGetLastError(), "k_fill_u64 launch");
     if (w.n_units <= 0 || env.n_tris <= 0) return;
-    const int64_t waves = w.n_units * w.max_clusters;
-    const int64_t blocks = (waves + kDistWaves - 1) / kDistWaves;
+    const int64_t blocks = (w.n_units + kDistWaves - 1) / kDistWaves;
     if (blocks > 0x7fffffff) throw Error{MPT_ERR_INVALID, "distance batch too large"};
     hipLaunchKernelGGL(k_distance, dim3((unsigned)blocks), dim3(kDistWaves * 64), 0, stream, env, d_links, w);
     hip_check(hipGetLastError(), "k_distance launch");

@@ -122,7 +122,7 @@ inline void make_env_tri(const double *t, EnvTri &r) {
         r.P2[k] = t[3 + k];
         r.P3[k] = t[6 + k];
     }
-    for (double &x : r.pad) x = 0.0;
+    r.pad[0] = 0.0;
 }
 
 // FCL only runs intersect_Triangle on pairs whose leaf bounding volumes overlap

@@ -165,7 +165,7 @@ struct DistWork {
     int32_t max_clusters;      // over the links
     int64_t n_units;           // P * L
     unsigned long long *best;  // [E]
-    // optional [4]: (unit, cluster) waves, env item box tests, triDistance calls, pair box tests
+    // optional [4]: agent clusters walked, env item box tests, triDistance calls, pair box tests
     unsigned long long *stats;
 };
 void launch_distance(const EnvDev &env, const AgentDev *d_links, const DistWork &w, int64_t E, hipStream_t stream);
