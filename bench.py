@@ -41,9 +41,14 @@ def parse():
     ap.add_argument("--seed", type=int, default=1000)
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample length")
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--nn", default="grid", choices=["grid", "brute", "auto"], help="engine NN structure")
+    ap.add_argument("--nn", default="auto", choices=["grid", "brute", "auto", "tree"], help="engine NN structure")
     ap.add_argument("--ppc", type=float, default=2.0, help="grid points per cell")
     ap.add_argument("--traffic", default=None, help="pmc_summary.json (default: latest profiles/r*/)")
+    ap.add_argument("--seeds", type=int, default=0,
+                    help="config 5: this many independent blimp RRTs (seed_base + i) sharded over the ranks "
+                         "(0 = config 2, one 100k-node tree per rank)")
+    ap.add_argument("--seed-batch", type=int, default=4096, help="config 5: extensions per seed per round")
+    ap.add_argument("--streams", type=int, default=8, help="config 5: HIP streams the seeds' rounds rotate over")
     return ap.parse_args()
 
 
@@ -166,6 +171,100 @@ def _cpu_model():
     return "unknown"
 
 
+def run_seeds(args, world, rank, dist, torch, mpt, multiseed, scenes):
+    """BASELINE config 5: `args.seeds` independent blimp RRTs, each its own engine and tree grown
+    from the blimp start state, `args.seed_batch` extensions per seed per round; rank r runs
+    the contiguous shard multiseed.shard_seeds(seeds, world, r).  Total work is fixed as the
+    GPU count grows (strong scaling).  A seed's tree depends only on its seed (counter-based
+    RNG), so the digest of all trees is the same at every GPU count."""
+    sc = scenes.blimp_scenario("all")
+    env = mpt.Environment(sc.env_tris, sc.env_tf)
+    agent = mpt.AgentMesh(sc.agent_tris)
+    mine = list(multiseed.shard_seeds(args.seeds, world, rank))
+    K = args.seed_batch
+    rounds = args.warmup + args.steps
+    # collision-free start at rest in the middle of the room (model.dae spans (0,0,0)-(177,138,114);
+    # blimp.inst's start (0,0,0) is the room's corner, inside its walls)
+    start = np.array([[88.6, 68.9, 57.1, 0.0, 0.0, 0.0, 0.0]])
+    engines = []
+    for i in mine:
+        e = mpt.RRTEngine(env, agent, sc.kind, sc.prm, sc.ranges, sc.steer_dt, sc.cc_dt, 1 + (rounds + 1) * K,
+                          args.seed + i)
+        e.add_nodes(start)
+        e.set_nn(args.nn, args.ppc)
+        engines.append(e)
+    streams = [torch.cuda.Stream() for _ in range(max(1, min(args.streams, len(engines))))]
+    if engines:
+        engines[0].enable_timing(True)
+
+    def round_():
+        for j, e in enumerate(engines):
+            e.step(K, streams[j % len(streams)])
+
+    for _ in range(args.warmup):
+        round_()
+    torch.cuda.synchronize()
+    c0 = [e.counters() for e in engines]
+    ktimes = {}
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        round_()
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    c1 = [e.counters() for e in engines]
+    valid = sum(b["valid"] - a["valid"] for a, b in zip(c0, c1))
+    checked = sum(b["checked"] - a["checked"] for a, b in zip(c0, c1))
+    elapsed, (valid, checked) = multiseed.reduce_run(dist, elapsed, [valid, checked], "cuda")
+    digests = {}
+    for i, e, c in zip(mine, engines, c1):
+        st, par = e.read_tree(c["nodes"])
+        digests[i] = multiseed.tree_digest(st, par)
+    digests = multiseed.gather_digests(dist, digests)
+    if rank != 0:
+        return None
+    # seed 0's engine: one more round with stage timing and work counters, outside the timed region
+    e0 = engines[0]
+    n_before = e0.counters()["nodes"]
+    e0.collide_stats(True)
+    e0.step(K, streams[0])
+    torch.cuda.synchronize()
+    cst = e0.collide_stats(False)
+    per_launch = e0.kernel_times()
+    roof = roofline(per_launch, cst, K, n_before, sc.dim, e0.info()["pmax"], args.nn, args.traffic)
+    import hashlib
+
+    all_digest = hashlib.sha256("".join(digests[i] for i in sorted(digests)).encode()).hexdigest()
+    return {
+        "metric": "valid RRT edge extensions/sec (collision+NN) per node, 1/2/4/8 MI355X",
+        "value": valid / elapsed,
+        "unit": "valid extensions/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": 1e3 * elapsed / args.steps,
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic (uniform samples over Blimp::getStateVarRanges; meshes from the reference)",
+        "config": {"workload": f"config 5: {args.seeds} independent blimp RRTs (1355-tri blimp vs model.dae) "
+                               f"grown from the start state, {K} extensions per seed per round",
+                   "seeds": args.seeds, "seed_base": args.seed, "extensions_per_seed_round": K,
+                   "rounds_before_timing": args.warmup, "streams_per_gpu": len(streams),
+                   "parallelism": f"seeds sharded over {world} GPU(s)"},
+        "checked_per_s": checked / elapsed,
+        "valid_fraction": valid / max(checked, 1),
+        "seeds_digest": all_digest,
+        "roofline": roof,
+        "cpu_baseline": None,
+    }
+
+
 def main():
     args = parse()
     import torch
@@ -185,6 +284,13 @@ def main():
     mpt.init(local)
     torch.cuda.set_device(local)
     stream = torch.cuda.current_stream()
+    if args.seeds > 0:
+        out = run_seeds(args, world, rank, dist, torch, mpt, multiseed, scenes)
+        if out is not None:
+            print(json.dumps(out))
+        if dist:
+            dist.destroy_process_group()
+        return
 
     sc = scenes.blimp_scenario("all")
     seed = multiseed.rank_seed(args.seed, rank)

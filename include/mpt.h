@@ -128,7 +128,7 @@ mpt_status mpt_nn_points_device(const mpt_nn *nn, const double **d_pts);
 /* Search structure: AUTO (grid when n >= 4096 and nq >= 32), BRUTE (tiled scan), GRID
  * (device-built uniform grid over the widest <= 3 dims, rebuilt after appends).  All modes
  * are exact and return identical results; GRID/AUTO rebuilds synchronise once. */
-enum { MPT_NN_AUTO = 0, MPT_NN_BRUTE = 1, MPT_NN_GRID = 2 };
+enum { MPT_NN_AUTO = 0, MPT_NN_BRUTE = 1, MPT_NN_GRID = 2, MPT_NN_TREE = 3 };
 mpt_status mpt_nn_set_index(mpt_nn *nn, int32_t mode);
 /* kNearest / nearest (k = 1): ids [nq][k] (-1 when fewer than k points), d2 [nq][k] (+inf). */
 mpt_status mpt_nn_knn(mpt_nn *nn, const double *q, int64_t nq, int32_t k, int32_t *ids, double *d2,
@@ -176,8 +176,9 @@ mpt_status mpt_rrt_info(const mpt_rrt *rrt, int64_t info[4]);
  * stream when timing is enabled: [sample, nn_build, nn_query, steer, collide, append]
  * (nn_build = grid index build, 0 in brute-force mode; nn_query includes the merge). */
 mpt_status mpt_rrt_enable_timing(mpt_rrt *rrt, int32_t enable);
-/* NN structure of the rounds: MPT_NN_AUTO / _BRUTE / _GRID, grid occupancy target
- * (points per cell, <= 0 keeps the current value, default 2).  Results are identical. */
+/* NN structure of the rounds: MPT_NN_AUTO / _BRUTE / _GRID / _TREE (packed Morton tree,
+ * for trees that do not fill the sampling box), grid occupancy target (points per cell,
+ * <= 0 keeps the current value, default 2).  Results are identical. */
 mpt_status mpt_rrt_set_nn(mpt_rrt *rrt, int32_t mode, double points_per_cell);
 /* Collision work counters accumulated since the previous call (synchronises), then reset;
  * enable = 1 keeps counting in later rounds (atomics: off for timed runs).

@@ -305,8 +305,8 @@ class RRTEngine:
         return {k: int(v) for k, v in zip(names, out[:11])}
 
     def set_nn(self, mode: str = "auto", points_per_cell: float = 0.0) -> None:
-        """NN structure of the rounds: 'auto' | 'brute' | 'grid' (identical results)."""
-        check(lib().mpt_rrt_set_nn(self.handle, {"auto": 0, "brute": 1, "grid": 2}[mode], points_per_cell),
+        """NN structure of the rounds: 'auto' | 'brute' | 'grid' | 'tree' (identical results)."""
+        check(lib().mpt_rrt_set_nn(self.handle, {"auto": 0, "brute": 1, "grid": 2, "tree": 3}[mode], points_per_cell),
               "mpt_rrt_set_nn")
 
     def close(self):

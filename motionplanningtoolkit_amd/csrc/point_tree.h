@@ -1,0 +1,56 @@
+// point_tree.h -- packed Morton tree for exact NN over a tree snapshot (see point_tree.hip).
+#pragma once
+#include "mpt_internal.h"
+
+namespace mpt {
+
+constexpr int kPtFan = 8;        // children per node, points per leaf
+constexpr int kPtMaxLevels = 10; // 8^10 points
+
+struct PointTreeDev {
+    int32_t d;
+    int32_t n_levels;          // box levels 1..n_levels (level n_levels = the root)
+    int64_t n_upper;           // layout bound: level l holds ceil(n_upper / 8^l) boxes
+    const int64_t *n_dev;      // live point count (<= n_upper)
+    const float *boxes;        // levels 1..n_levels back to back, each box [2d] floats: lo then hi
+    const double *pts;         // [n][d], Morton order
+    const int32_t *ids;        // 1-based original ids
+    unsigned long long *stats; // optional [2]: points examined, boxes tested
+};
+
+class PointTree {
+public:
+    ~PointTree();
+    // Index rows [0, min(n_upper, *n_dev)) of pts [.][d]: Morton codes of the spatial dims
+    // (dims[0..gd), quantised over [lo, hi]), radix sort, boxes bottom-up.  Stream-ordered.
+    void build(const double *pts, int64_t n_upper, const int64_t *n_dev, int32_t d, int32_t gd, const int32_t *dims,
+               const double *lo, const double *hi, hipStream_t stream);
+    PointTreeDev dev() const { return t; }
+
+private:
+    void reserve(int64_t n_upper, int32_t d);
+    PointTreeDev t{};
+    int64_t cap = 0, box_cap = 0;
+    int32_t dim = 0;
+    uint32_t *keys = nullptr, *keys_sorted = nullptr;
+    int32_t *vals = nullptr, *vals_sorted = nullptr, *sids = nullptr;
+    double *spts = nullptr;
+    float *boxes = nullptr;
+    void *temp = nullptr;
+    size_t temp_bytes = 0;
+};
+
+// box level sizes for a layout bound: level l (1-based) has ceil(n / 8^l) boxes
+inline int32_t pt_levels(int64_t n) {
+    int32_t L = 1;
+    int64_t m = (n + kPtFan - 1) / kPtFan;
+    while (m > 1) {
+        m = (m + kPtFan - 1) / kPtFan;
+        ++L;
+    }
+    return L;
+}
+
+void launch_tree_nn1(const PointTreeDev &T, const double *q, int64_t nq, int32_t *ids, double *d2, hipStream_t stream);
+
+}  // namespace mpt

@@ -21,6 +21,7 @@
 
 #include "../../include/mpt.h"
 #include "grid_nn.h"
+#include "point_tree.h"
 #include "mpt_internal.h"
 
 namespace mpt {
@@ -293,6 +294,46 @@ __global__ void k_set_n(int64_t *n_dev, int64_t n, unsigned long long *counters)
     counters[3] = (unsigned long long)n;
 }
 
+// Spread of the live nodes over the spatial dims (for MPT_NN_AUTO): per-dim min / max as
+// order-preserving 64-bit keys, out[0..gd) = min, out[3..3+gd) = max (pre-set to ~0 / 0).
+__device__ __forceinline__ unsigned long long order_key(double x) {
+    const unsigned long long b = (unsigned long long)__double_as_longlong(x);
+    return (b >> 63) ? ~b : (b | 0x8000000000000000ull);
+}
+__global__ __launch_bounds__(256) void k_spread(const double *__restrict__ nodes, const int64_t *__restrict__ n_dev,
+                                                int32_t d, int32_t gd, unsigned long long *__restrict__ out) {
+    __shared__ unsigned long long s_min[3], s_max[3];
+    if (threadIdx.x < 3) {
+        s_min[threadIdx.x] = ~0ull;
+        s_max[threadIdx.x] = 0ull;
+    }
+    __syncthreads();
+    const int64_t n = *n_dev;
+    unsigned long long mn[3] = {~0ull, ~0ull, ~0ull}, mx[3] = {0, 0, 0};
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+        for (int j = 0; j < gd; ++j) {
+            const unsigned long long k = order_key(nodes[i * d + j]);
+            mn[j] = k < mn[j] ? k : mn[j];
+            mx[j] = k > mx[j] ? k : mx[j];
+        }
+    for (int j = 0; j < gd; ++j) {
+        atomicMin(&s_min[j], mn[j]);
+        atomicMax(&s_max[j], mx[j]);
+    }
+    __syncthreads();
+    if (threadIdx.x < (unsigned)gd) {
+        atomicMin(out + threadIdx.x, s_min[threadIdx.x]);
+        atomicMax(out + 3 + threadIdx.x, s_max[threadIdx.x]);
+    }
+}
+
+double key_value(unsigned long long k) {
+    const unsigned long long b = (k >> 63) ? (k & 0x7fffffffffffffffull) : ~k;
+    double x;
+    std::memcpy(&x, &b, sizeof x);
+    return x;
+}
+
 }  // namespace
 
 struct mpt_rrt {
@@ -319,8 +360,15 @@ struct mpt_rrt {
     // NN structure over the round's snapshot (grid_nn.hip), rebuilt every round
     int32_t nn_mode = MPT_NN_AUTO;
     std::unique_ptr<GridIndex> grid;
+    std::unique_ptr<PointTree> ptree;  // MPT_NN_TREE (point_tree.hip)
     int32_t grid_gd = 0, grid_dims[3] = {0, 0, 0};
     double ppc = 2.0;
+    // MPT_NN_AUTO feedback: the live nodes' spatial spread, copied back after each round and
+    // read at a later round once its event has completed (never waited for; the NN choice
+    // changes only speed, results are identical)
+    unsigned long long *d_spread = nullptr, *h_spread = nullptr;
+    hipEvent_t ev_spread = nullptr;
+    bool spread_pending = false, auto_tree = false;
     // optional collision work counters (k_collide atomics): units, clusters, node visits, tri tests
     bool stats_on = false;
     CollideScratch cscratch;
@@ -336,6 +384,9 @@ void rfree(mpt_rrt *r) {
         if (p) (void)hipFree(p);
     for (auto &e : r->ev)
         if (e) (void)hipEventDestroy(e);
+    if (r->d_spread) (void)hipFree(r->d_spread);
+    if (r->h_spread) (void)hipHostFree(r->h_spread);
+    if (r->ev_spread) (void)hipEventDestroy(r->ev_spread);
 }
 
 void ensure_round_buffers(mpt_rrt *r, int32_t K) {
@@ -416,6 +467,7 @@ extern "C" mpt_status mpt_rrt_create(const mpt_env *env, const mpt_agent *agent,
             hip_check(hipMemset(r->d_counters, 0, sizeof(unsigned long long) * 8), "memset counters");
             for (auto &e : r->ev) hip_check(hipEventCreate(&e), "event");
             r->grid.reset(new GridIndex());
+            r->ptree.reset(new PointTree());
             r->grid_gd = agent_kind == MPT_AGENT_SNAKE ? 2 : 3;
             for (int j = 0; j < 3; ++j) r->grid_dims[j] = j;
         } catch (...) {
@@ -483,8 +535,30 @@ extern "C" mpt_status mpt_rrt_step(mpt_rrt *r, int32_t K, void *stream_) {
         hipLaunchKernelGGL(k_sample, dim3(kb), dim3(256), 0, stream, p, r->ext_base, K, r->d_samples);
         hip_check(hipGetLastError(), "k_sample");
         mark(1);
-        const bool use_grid = r->nn_mode == MPT_NN_GRID || (r->nn_mode == MPT_NN_AUTO && r->n_upper >= 4096);
-        if (use_grid) {
+        if (r->nn_mode == MPT_NN_AUTO && r->spread_pending && hipEventQuery(r->ev_spread) == hipSuccess) {
+            // the tree fills less than a quarter of the sampling box: most samples are far
+            // from every node, where the grid walks empty rings and the Morton tree does not
+            double frac = 1.0;
+            for (int j = 0; j < r->grid_gd; ++j) {
+                const int dj = r->grid_dims[j];
+                const double ext = key_value(r->h_spread[3 + j]) - key_value(r->h_spread[j]);
+                const double range = p.hi[dj] - p.lo[dj];
+                frac *= range > 0 ? std::min(1.0, std::max(0.0, ext / range)) : 1.0;
+            }
+            r->auto_tree = frac < 0.25;
+            r->spread_pending = false;
+        }
+        const bool big = r->n_upper >= 4096;
+        const bool use_tree = r->nn_mode == MPT_NN_TREE || (r->nn_mode == MPT_NN_AUTO && big && r->auto_tree);
+        const bool use_grid = !use_tree && (r->nn_mode == MPT_NN_GRID || (r->nn_mode == MPT_NN_AUTO && big));
+        if (use_tree) {
+            double lo[3], hi[3];
+            for (int j = 0; j < r->grid_gd; ++j) {
+                lo[j] = p.lo[r->grid_dims[j]];
+                hi[j] = p.hi[r->grid_dims[j]];
+            }
+            r->ptree->build(r->d_nodes, r->n_upper, r->d_n, p.d, r->grid_gd, r->grid_dims, lo, hi, stream);
+        } else if (use_grid) {
             // spatial dims of the agent's tree state: x, y, z (omni, blimp) or x, y (snake);
             // the grid spans the sampling ranges, nodes outside fall into the border cells
             double lo[3], hi[3];
@@ -496,7 +570,11 @@ extern "C" mpt_status mpt_rrt_step(mpt_rrt *r, int32_t K, void *stream_) {
             r->grid->build(r->d_nodes, r->n_upper, r->d_n, p.d, g, stream);
         }
         mark(2);
-        if (use_grid) {
+        if (use_tree) {
+            PointTreeDev T = r->ptree->dev();
+            T.stats = r->stats_on ? r->d_cstats + 8 : nullptr;
+            launch_tree_nn1(T, r->d_samples, K, r->d_nn, r->d_nnd2, stream);
+        } else if (use_grid) {
             GridDev G = r->grid->dev();
             G.stats = r->stats_on ? r->d_cstats + 8 : nullptr;
             launch_grid_knn(G, p.d, r->d_samples, K, 1, r->d_nn, r->d_nnd2, stream);
@@ -543,6 +621,22 @@ extern "C" mpt_status mpt_rrt_step(mpt_rrt *r, int32_t K, void *stream_) {
                            r->d_counters);
         hip_check(hipGetLastError(), "append");
         mark(9);
+        if (r->nn_mode == MPT_NN_AUTO && !r->spread_pending) {
+            if (!r->d_spread) {
+                hip_check(hipMalloc(&r->d_spread, sizeof(unsigned long long) * 6), "alloc spread");
+                hip_check(hipHostMalloc(&r->h_spread, sizeof(unsigned long long) * 6), "alloc spread");
+                hip_check(hipEventCreateWithFlags(&r->ev_spread, hipEventDisableTiming), "event");
+            }
+            hip_check(hipMemsetAsync(r->d_spread, 0xff, sizeof(unsigned long long) * 3, stream), "spread memset");
+            hip_check(hipMemsetAsync(r->d_spread + 3, 0, sizeof(unsigned long long) * 3, stream), "spread memset");
+            hipLaunchKernelGGL(k_spread, dim3(64), dim3(256), 0, stream, r->d_nodes, r->d_n, p.d, r->grid_gd,
+                               r->d_spread);
+            hip_check(hipGetLastError(), "k_spread");
+            hip_check(hipMemcpyAsync(r->h_spread, r->d_spread, sizeof(unsigned long long) * 6, hipMemcpyDeviceToHost,
+                                     stream), "spread D2H");
+            hip_check(hipEventRecord(r->ev_spread, stream), "spread event");
+            r->spread_pending = true;
+        }
         r->ext_base += (uint64_t)K;
         r->n_upper = std::min<int64_t>(r->cap, r->n_upper + K);
         r->last_K = K;
@@ -626,7 +720,7 @@ extern "C" mpt_status mpt_rrt_collide_stats(mpt_rrt *r, int32_t enable, uint64_t
 
 extern "C" mpt_status mpt_rrt_set_nn(mpt_rrt *r, int32_t mode, double points_per_cell) {
     return guarded([&] {
-        if (!r || mode < MPT_NN_AUTO || mode > MPT_NN_GRID) throw Error{MPT_ERR_INVALID, "bad arguments"};
+        if (!r || mode < MPT_NN_AUTO || mode > MPT_NN_TREE) throw Error{MPT_ERR_INVALID, "bad arguments"};
         r->nn_mode = mode;
         if (points_per_cell > 0) r->ppc = points_per_cell;
     });

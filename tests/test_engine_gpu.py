@@ -96,7 +96,7 @@ def check_round(mpt, oracle, sc, eng, tree, seed, ext_base, K):
     return t2, verdict
 
 
-@pytest.mark.parametrize("nn_mode", ["brute", "grid"])
+@pytest.mark.parametrize("nn_mode", ["brute", "grid", "tree"])
 @pytest.mark.parametrize("name", ["omni", "blimp", "snake"])
 def test_engine_rounds(mpt_gpu, oracle, name, nn_mode):
     if name == "omni":
@@ -137,15 +137,43 @@ def test_engine_grid_equals_brute_over_growing_rounds(mpt_gpu, oracle):
     engines must build the same tree bit for bit (rounds build the grid from scratch)."""
     sc = scenes.blimp_scenario("last")
     trees = []
-    for mode in ("brute", "grid"):
+    for mode in ("brute", "grid", "tree"):
         eng, tree = make(mpt_gpu, sc, 6000, 4096, 77, cap_extra=5 * 4096)
         eng.set_nn(mode)
         for K in (4096, 1000, 4096, 333, 2048):
             eng.step(K)
         n = eng.counters()["nodes"]
         trees.append(eng.read_tree(n))
-    assert np.array_equal(bits(trees[0][0]), bits(trees[1][0]))
-    assert np.array_equal(trees[0][1], trees[1][1])
+    for t in trees[1:]:
+        assert np.array_equal(bits(trees[0][0]), bits(t[0]))
+        assert np.array_equal(trees[0][1], t[1])
+
+
+@pytest.mark.parametrize("name", ["blimp", "snake"])
+def test_engine_tree_from_one_root(mpt_gpu, name):
+    """A tree grown from a single root (the RRT case: nodes clustered around the start,
+    samples all over the sampling box): the Morton-tree and brute-force NN engines build the
+    same tree bit for bit."""
+    if name == "blimp":
+        sc, root = scenes.blimp_scenario("all"), np.array([[88.6, 68.9, 57.1, 0, 0, 0, 0.0]])
+    else:
+        sc = scenes.snake_scenario("corridor")
+        root = np.asarray(sc.start, np.float64).reshape(1, -1)
+    trees = []
+    for mode in ("brute", "tree", "auto"):
+        env = mpt_gpu.Environment(sc.env_tris, sc.env_tf)
+        ag = mpt_gpu.AgentMesh(sc.agent_tris)
+        eng = mpt_gpu.RRTEngine(env, ag, sc.kind, sc.prm, sc.ranges, sc.steer_dt, sc.cc_dt, 1 + 8 * 2048, 5)
+        eng.add_nodes(root)
+        eng.set_nn(mode)
+        for _ in range(8):
+            eng.step(2048)
+        n = eng.counters()["nodes"]
+        trees.append(eng.read_tree(n))
+    assert len(trees[0][0]) > 100
+    for t in trees[1:]:
+        assert np.array_equal(bits(trees[0][0]), bits(t[0]))
+        assert np.array_equal(trees[0][1], t[1])
 
 
 def test_engine_set_size_and_capacity(mpt_gpu, oracle):
