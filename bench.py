@@ -48,7 +48,7 @@ def parse():
                     help="config 5: this many independent blimp RRTs (seed_base + i) sharded over the ranks "
                          "(0 = config 2, one 100k-node tree per rank)")
     ap.add_argument("--seed-batch", type=int, default=4096, help="config 5: extensions per seed per round")
-    ap.add_argument("--streams", type=int, default=8, help="config 5: HIP streams the seeds' rounds rotate over")
+    ap.add_argument("--streams", type=int, default=32, help="config 5: HIP streams the seeds' rounds rotate over")
     return ap.parse_args()
 
 

@@ -35,9 +35,11 @@ public:
                hipStream_t stream);
     GridDev dev() const;
     const GridParams &params() const { return g; }
+    // allocate for up to cap_pts points and ncells cells now (allocation synchronises the
+    // device; engines reserve their capacity once so rounds on several streams overlap)
+    void reserve(int64_t cap_pts, int32_t d, int64_t ncells);
 
 private:
-    void reserve(int64_t cap_pts, int32_t d, int64_t ncells);
     GridParams g{};
     int64_t n_max = 0, pts_cap = 0, cells_cap = 0;
     int32_t dim = 0;

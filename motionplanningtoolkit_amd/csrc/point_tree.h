@@ -26,9 +26,10 @@ public:
     void build(const double *pts, int64_t n_upper, const int64_t *n_dev, int32_t d, int32_t gd, const int32_t *dims,
                const double *lo, const double *hi, hipStream_t stream);
     PointTreeDev dev() const { return t; }
+    // allocate for up to n_upper points now (see GridIndex::reserve)
+    void reserve(int64_t n_upper, int32_t d);
 
 private:
-    void reserve(int64_t n_upper, int32_t d);
     PointTreeDev t{};
     int64_t cap = 0, box_cap = 0;
     int32_t dim = 0;

@@ -557,6 +557,7 @@ extern "C" mpt_status mpt_rrt_step(mpt_rrt *r, int32_t K, void *stream_) {
                 lo[j] = p.lo[r->grid_dims[j]];
                 hi[j] = p.hi[r->grid_dims[j]];
             }
+            r->ptree->reserve(r->cap, p.d);  // once: no allocation (device sync) in later rounds
             r->ptree->build(r->d_nodes, r->n_upper, r->d_n, p.d, r->grid_gd, r->grid_dims, lo, hi, stream);
         } else if (use_grid) {
             // spatial dims of the agent's tree state: x, y, z (omni, blimp) or x, y (snake);
@@ -567,6 +568,8 @@ extern "C" mpt_status mpt_rrt_step(mpt_rrt *r, int32_t K, void *stream_) {
                 hi[j] = p.hi[r->grid_dims[j]];
             }
             const GridParams g = make_grid_params(p.d, r->grid_dims, r->grid_gd, lo, hi, r->n_upper, r->ppc);
+            const GridParams gcap = make_grid_params(p.d, r->grid_dims, r->grid_gd, lo, hi, r->cap, r->ppc);
+            r->grid->reserve(r->cap, p.d, std::max(g.ncells, gcap.ncells));  // once, as for the tree
             r->grid->build(r->d_nodes, r->n_upper, r->d_n, p.d, g, stream);
         }
         mark(2);
