@@ -6,6 +6,7 @@ namespace mpt {
 
 constexpr int kPtFan = 8;        // children per node, points per leaf
 constexpr int kPtMaxLevels = 10; // 8^10 points
+constexpr int kPtMaxDim = 16;
 
 struct PointTreeDev {
     int32_t d;
@@ -21,10 +22,9 @@ struct PointTreeDev {
 class PointTree {
 public:
     ~PointTree();
-    // Index rows [0, min(n_upper, *n_dev)) of pts [.][d]: Morton codes of the spatial dims
-    // (dims[0..gd), quantised over [lo, hi]), radix sort, boxes bottom-up.  Stream-ordered.
-    void build(const double *pts, int64_t n_upper, const int64_t *n_dev, int32_t d, int32_t gd, const int32_t *dims,
-               const double *lo, const double *hi, hipStream_t stream);
+    // Index rows [0, min(n_upper, *n_dev)) of pts [.][d]: bounding box and code plan on the
+    // device, 30-bit codes over all dims, radix sort, boxes bottom-up.  Stream-ordered.
+    void build(const double *pts, int64_t n_upper, const int64_t *n_dev, int32_t d, hipStream_t stream);
     PointTreeDev dev() const { return t; }
     // allocate for up to n_upper points now (see GridIndex::reserve)
     void reserve(int64_t n_upper, int32_t d);
@@ -37,6 +37,8 @@ private:
     int32_t *vals = nullptr, *vals_sorted = nullptr, *sids = nullptr;
     double *spts = nullptr;
     float *boxes = nullptr;
+    unsigned long long *bbox = nullptr;  // [2][kPtMaxDim] order keys
+    struct CodePlan *plan = nullptr;
     void *temp = nullptr;
     size_t temp_bytes = 0;
 };

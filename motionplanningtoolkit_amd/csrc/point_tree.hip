@@ -5,11 +5,11 @@
 // lie far from every node, and a uniform grid over the sampling box walks many empty rings
 // for them.  Here the cost of a query depends on the tree's shape, not on where it lies.
 //
-// Build (every round, stream-ordered, no host sync): 30-bit Morton code of each node's
-// spatial dims (x, y, z; x, y for the snake) quantised over the sampling box -> hipcub
-// radix sort -> coordinates and ids gathered into code order -> leaves of 8 consecutive
-// points and 8-ary levels above them, each box the float-widened bounds over ALL state dims
-// (a lower bound on FLANN's squared L2 over every dim, not just the spatial ones).
+// Build (every round, stream-ordered, no host sync): bounding box of the live nodes ->
+// code plan (below) -> 30-bit interleaved code per node -> hipcub radix sort -> coordinates
+// and ids gathered into code order -> leaves of 8 consecutive points and 8-ary levels above
+// them, each box the float-widened bounds over all state dims (a lower bound on FLANN's
+// squared L2).
 //
 // Query: 8 lanes per query walk the tree with a per-group LDS stack.  At an inner node the
 // lanes test its 8 children's boxes against the best distance so far and push the survivors
@@ -37,31 +37,107 @@ __device__ __forceinline__ int64_t live_n(const PointTreeDev &T) {
     return n < T.n_upper ? n : T.n_upper;
 }
 
-__device__ __forceinline__ uint32_t spread3(uint32_t x) {  // 10 bits -> every third bit
-    x &= 0x3ff;
-    x = (x | (x << 16)) & 0x030000ff;
-    x = (x | (x << 8)) & 0x0300f00f;
-    x = (x | (x << 4)) & 0x030c30c3;
-    x = (x | (x << 2)) & 0x09249249;
-    return x;
-}
-__device__ __forceinline__ uint32_t spread2(uint32_t x) {  // 15 bits -> every second bit
-    x &= 0x7fff;
-    x = (x | (x << 8)) & 0x00ff00ff;
-    x = (x | (x << 4)) & 0x0f0f0f0f;
-    x = (x | (x << 2)) & 0x33333333;
-    x = (x | (x << 1)) & 0x55555555;
-    return x;
-}
+// Codes over ALL state dims with one common quantisation step h (cubic cells in raw state
+// units, the units of FLANN's L2): dim j gets b_j = ceil(log2(extent_j / h)) bits, h the
+// smallest step for which sum b_j <= 30, and bits interleave from the most significant level
+// down, a level taking the dims still wider than it.  Widest dims are split first, as a
+// kd-tree would; leaves then hold points close in every dim, so their boxes prune on the
+// non-spatial dims as well.  The bounding box comes from the device (no host sync).
+constexpr int kCodeBits = 30;
 
-struct MortonArgs {
-    int32_t gd, dims[3];
-    double lo[3], scale[3];
-    uint32_t qmax;
+}  // namespace
+
+struct CodePlan {
+    double lo[kPtMaxDim], scale[kPtMaxDim];
+    uint32_t qmax[kPtMaxDim];
+    int32_t n;                       // code bits used
+    int8_t dim[kCodeBits], bit[kCodeBits];  // MSB first
 };
 
+namespace {
+
+__device__ __forceinline__ unsigned long long order_key_pt(double x) {
+    const unsigned long long b = (unsigned long long)__double_as_longlong(x);
+    return (b >> 63) ? ~b : (b | 0x8000000000000000ull);
+}
+__device__ __forceinline__ double key_value_pt(unsigned long long k) {
+    const unsigned long long b = (k >> 63) ? (k & 0x7fffffffffffffffull) : ~k;
+    return __longlong_as_double((long long)b);
+}
+
+// per-dim min / max of the live points as order keys: box[0..d) min, box[kPtMaxDim..) max
+__global__ __launch_bounds__(256) void k_pt_bbox(const double *__restrict__ pts, int32_t d, int64_t n_upper,
+                                                 const int64_t *__restrict__ n_dev, unsigned long long *__restrict__ box) {
+    __shared__ unsigned long long s_min[kPtMaxDim], s_max[kPtMaxDim];
+    if (threadIdx.x < kPtMaxDim) {
+        s_min[threadIdx.x] = ~0ull;
+        s_max[threadIdx.x] = 0ull;
+    }
+    __syncthreads();
+    const int64_t n = *n_dev < n_upper ? *n_dev : n_upper;
+    for (int j = 0; j < d; ++j) {
+        unsigned long long mn = ~0ull, mx = 0ull;
+        for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+            const unsigned long long k = order_key_pt(pts[i * d + j]);
+            mn = k < mn ? k : mn;
+            mx = k > mx ? k : mx;
+        }
+        atomicMin(&s_min[j], mn);
+        atomicMax(&s_max[j], mx);
+    }
+    __syncthreads();
+    if (threadIdx.x < (unsigned)d) {
+        atomicMin(box + threadIdx.x, s_min[threadIdx.x]);
+        atomicMax(box + kPtMaxDim + threadIdx.x, s_max[threadIdx.x]);
+    }
+}
+
+__global__ void k_pt_plan(int32_t d, const unsigned long long *__restrict__ box, CodePlan *__restrict__ plan) {
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    double lo[kPtMaxDim], ext[kPtMaxDim], emax = 0.0;
+    for (int j = 0; j < d; ++j) {
+        lo[j] = key_value_pt(box[j]);
+        const double hi = key_value_pt(box[kPtMaxDim + j]);
+        ext[j] = hi > lo[j] ? hi - lo[j] : 0.0;
+        emax = ext[j] > emax ? ext[j] : emax;
+    }
+    int32_t b[kPtMaxDim];
+    for (int j = 0; j < d; ++j) b[j] = 0;
+    if (emax > 0.0) {
+        // finest level k (h = emax / 2^k) whose bit total fits the code
+        for (int k = 1; k <= kCodeBits; ++k) {
+            const double h = ldexp(emax, -k);
+            int32_t bt[kPtMaxDim], tot = 0;
+            for (int j = 0; j < d; ++j) {
+                int32_t bj = 0;
+                while (bj < k && ldexp(h, bj) < ext[j]) ++bj;
+                bt[j] = bj;
+                tot += bj;
+            }
+            if (tot > kCodeBits) break;
+            for (int j = 0; j < d; ++j) b[j] = bt[j];
+        }
+    }
+    int32_t bmax = 0;
+    for (int j = 0; j < d; ++j) {
+        plan->lo[j] = lo[j];
+        plan->qmax[j] = b[j] > 0 ? (1u << b[j]) - 1 : 0u;
+        plan->scale[j] = b[j] > 0 ? ldexp(1.0, b[j]) / ext[j] : 0.0;
+        bmax = b[j] > bmax ? b[j] : bmax;
+    }
+    int32_t n = 0;
+    for (int t = bmax - 1; t >= 0; --t)
+        for (int j = 0; j < d; ++j)
+            if (b[j] > t) {
+                plan->dim[n] = (int8_t)j;
+                plan->bit[n] = (int8_t)t;
+                ++n;
+            }
+    plan->n = n;
+}
+
 __global__ void k_pt_morton(const double *__restrict__ pts, int32_t d, int64_t n_upper, const int64_t *__restrict__ n_dev,
-                            MortonArgs a, uint32_t *__restrict__ keys, int32_t *__restrict__ vals) {
+                            const CodePlan *__restrict__ plan, uint32_t *__restrict__ keys, int32_t *__restrict__ vals) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n_upper) return;
     const int64_t n = *n_dev < n_upper ? *n_dev : n_upper;
@@ -70,13 +146,16 @@ __global__ void k_pt_morton(const double *__restrict__ pts, int32_t d, int64_t n
         keys[i] = 0xffffffffu;  // past the live count: sorted to the end
         return;
     }
-    uint32_t q[3] = {0, 0, 0};
-    for (int j = 0; j < a.gd; ++j) {
-        const double u = (pts[i * d + a.dims[j]] - a.lo[j]) * a.scale[j];
-        q[j] = u <= 0.0 ? 0u : (u >= (double)a.qmax ? a.qmax : (uint32_t)u);
+    uint32_t q[kPtMaxDim];
+    for (int j = 0; j < d; ++j) {
+        const double u = (pts[i * d + j] - plan->lo[j]) * plan->scale[j];
+        const uint32_t m = plan->qmax[j];
+        q[j] = u <= 0.0 ? 0u : (u >= (double)m ? m : (uint32_t)u);
     }
-    keys[i] = a.gd == 3 ? (spread3(q[0]) << 2) | (spread3(q[1]) << 1) | spread3(q[2])
-                        : (a.gd == 2 ? (spread2(q[0]) << 1) | spread2(q[1]) : q[0]);
+    uint32_t code = 0;
+    const int32_t nb = plan->n;
+    for (int k = 0; k < nb; ++k) code = (code << 1) | ((q[plan->dim[k]] >> plan->bit[k]) & 1u);
+    keys[i] = code;
 }
 
 __global__ void k_pt_gather(const double *__restrict__ pts, int32_t d, int64_t n_upper, const int64_t *__restrict__ n_dev,
@@ -236,7 +315,7 @@ __global__ __launch_bounds__(256) void k_tree_nn1(PointTreeDev T, const double *
 
 PointTree::~PointTree() {
     for (void *p : {(void *)keys, (void *)keys_sorted, (void *)vals, (void *)vals_sorted, (void *)sids, (void *)spts,
-                    (void *)boxes, temp})
+                    (void *)boxes, temp, (void *)bbox, (void *)plan})
         if (p) (void)hipFree(p);
 }
 
@@ -265,6 +344,10 @@ void PointTree::reserve(int64_t n_upper, int32_t d) {
         }
         box_cap = 0;
     }
+    if (!bbox) {
+        hip_check(hipMalloc(&bbox, sizeof(unsigned long long) * 2 * kPtMaxDim), "pt bbox");
+        hip_check(hipMalloc(&plan, sizeof(CodePlan)), "pt plan");
+    }
     if (nb * 2 * d > box_cap) {
         if (boxes) hip_check(hipFree(boxes), "free");
         box_cap = std::max<int64_t>(nb * 2 * d, 2 * box_cap);
@@ -272,20 +355,10 @@ void PointTree::reserve(int64_t n_upper, int32_t d) {
     }
 }
 
-void PointTree::build(const double *pts, int64_t n_upper, const int64_t *n_dev, int32_t d, int32_t gd,
-                      const int32_t *dims, const double *lo, const double *hi, hipStream_t stream) {
+void PointTree::build(const double *pts, int64_t n_upper, const int64_t *n_dev, int32_t d, hipStream_t stream) {
     if (d != 3 && d != 7 && d != 15) throw Error{1, "point tree: state dim must be 3, 7 or 15"};
     if (n_upper >= (int64_t(1) << 27)) throw Error{1, "point tree: too many points"};
     reserve(n_upper, d);
-    MortonArgs a{};
-    a.gd = gd;
-    a.qmax = gd == 3 ? 1023u : (gd == 2 ? 32767u : (1u << 30) - 1);
-    for (int j = 0; j < gd; ++j) {
-        a.dims[j] = dims[j];
-        a.lo[j] = lo[j];
-        const double ext = hi[j] - lo[j];
-        a.scale[j] = ext > 0 ? (double)(a.qmax + 1) / ext : 0.0;
-    }
     t.d = d;
     t.n_upper = n_upper;
     t.n_levels = pt_levels(n_upper);
@@ -295,7 +368,11 @@ void PointTree::build(const double *pts, int64_t n_upper, const int64_t *n_dev, 
     t.ids = sids;
     if (n_upper <= 0) return;
     const unsigned blocks = (unsigned)((n_upper + 255) / 256);
-    hipLaunchKernelGGL(k_pt_morton, dim3(blocks), dim3(256), 0, stream, pts, d, n_upper, n_dev, a, keys, vals);
+    hip_check(hipMemsetAsync(bbox, 0xff, sizeof(unsigned long long) * kPtMaxDim, stream), "bbox memset");
+    hip_check(hipMemsetAsync(bbox + kPtMaxDim, 0, sizeof(unsigned long long) * kPtMaxDim, stream), "bbox memset");
+    hipLaunchKernelGGL(k_pt_bbox, dim3(64), dim3(256), 0, stream, pts, d, n_upper, n_dev, bbox);
+    hipLaunchKernelGGL(k_pt_plan, dim3(1), dim3(64), 0, stream, d, bbox, plan);
+    hipLaunchKernelGGL(k_pt_morton, dim3(blocks), dim3(256), 0, stream, pts, d, n_upper, n_dev, plan, keys, vals);
     hip_check(hipGetLastError(), "k_pt_morton");
     size_t tb = temp_bytes;
     hip_check(hipcub::DeviceRadixSort::SortPairs(temp, tb, keys, keys_sorted, vals, vals_sorted, (int)n_upper, 0,

@@ -552,13 +552,8 @@ extern "C" mpt_status mpt_rrt_step(mpt_rrt *r, int32_t K, void *stream_) {
         const bool use_tree = r->nn_mode == MPT_NN_TREE || (r->nn_mode == MPT_NN_AUTO && big && r->auto_tree);
         const bool use_grid = !use_tree && (r->nn_mode == MPT_NN_GRID || (r->nn_mode == MPT_NN_AUTO && big));
         if (use_tree) {
-            double lo[3], hi[3];
-            for (int j = 0; j < r->grid_gd; ++j) {
-                lo[j] = p.lo[r->grid_dims[j]];
-                hi[j] = p.hi[r->grid_dims[j]];
-            }
             r->ptree->reserve(r->cap, p.d);  // once: no allocation (device sync) in later rounds
-            r->ptree->build(r->d_nodes, r->n_upper, r->d_n, p.d, r->grid_gd, r->grid_dims, lo, hi, stream);
+            r->ptree->build(r->d_nodes, r->n_upper, r->d_n, p.d, stream);
         } else if (use_grid) {
             // spatial dims of the agent's tree state: x, y, z (omni, blimp) or x, y (snake);
             // the grid spans the sampling ranges, nodes outside fall into the border cells
