@@ -114,6 +114,21 @@ mpt_status mpt_distance_batch_device(const mpt_env *env, const mpt_agent *const 
                                      const double *d_poses, const int64_t *d_edge_pose_offsets, int64_t E,
                                      int64_t total_poses, double *d_dist_out, void *stream);
 
+/* ---- PRM roadmap edges (BASELINE config 4): PRM::addMilestone, planners/prm/prm.hpp:334-387,
+ * with radius neighbours (FLANN_KDTreeWrapper::kNearestWithin, flannkdtreewrapper.hpp:91-117)
+ * in place of the approximate kNN(10).  Milestone i connects to every earlier milestone j < i
+ * whose first three state variables (prm.hpp:155, the NN key) lie at squared L2 < radius2;
+ * the edge is Omnidirectional::steer(key_i, key_j, 1000) checked at getPoses(edge, cc_dt)
+ * poses (translation along the key segment; a blimp mesh keeps milestone i's yaw, R of
+ * Blimp::stateToFCLTransform).  agent_kind / dim: MPT_AGENT_OMNI / 3 or MPT_AGENT_BLIMP / 7.
+ * Out: edges[E][2] = (i, j) sorted by i then j, verdict[E] (1 = in collision), both written
+ * up to cap; *n_edges = E; comp[n] = smallest milestone of each component over the free
+ * edges (may be NULL); ms[4] (may be NULL) = device ms of [neighbours, poses, collision, all].
+ * Synchronous. */
+mpt_status mpt_prm_connect(const mpt_env *env, const mpt_agent *agent, int32_t agent_kind, const double *states,
+                           int64_t n, int32_t dim, double radius2, double cc_dt, int64_t cap, int32_t *edges,
+                           uint8_t *verdict, int64_t *n_edges, int32_t *comp, float ms[4]);
+
 /* ---- NN: FLANN_KDTreeWrapper ---- */
 mpt_status mpt_nn_create(int32_t dim, int64_t capacity, mpt_nn **out);
 mpt_status mpt_nn_destroy(mpt_nn *nn);

@@ -42,6 +42,7 @@ SIGNATURES = {
     "mpt_set_stats": (I32, [I32]),
     "mpt_set_collide_mode": (I32, [I32]),
     "mpt_distance_batch": (I32, [P, P, I32, P, P, I64, P, P]),
+    "mpt_prm_connect": (I32, [P, P, I32, P, I64, I32, D, D, I64, P, P, P, P, P]),
     "mpt_distance_batch_device": (I32, [P, P, I32, P, P, I64, I64, P, P]),
     "mpt_last_collide_stats": (I32, [P]),
     "mpt_nn_create": (I32, [I32, I64, P]),

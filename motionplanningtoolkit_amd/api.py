@@ -148,6 +148,25 @@ def distance_batch_device(env: Environment, links: Sequence[AgentMesh], d_poses,
                                           total_poses, _p(d_dist), _stream(stream)), "mpt_distance_batch_device")
 
 
+def prm_connect(env: Environment, agent: AgentMesh, kind: int, states, radius2: float, cc_dt: float) -> dict:
+    """PRM roadmap with radius neighbours on the device (config 4, include/mpt.h mpt_prm_connect).
+    Returns edges [E][2] = (i, j), verdict [E] (1 = in collision), comp [n], ms (stage times)."""
+    st = _f64(states)
+    n, dim = st.shape
+    ne = C.c_int64()
+    check(lib().mpt_prm_connect(env.handle, agent.handle, kind, _p(st), n, dim, radius2, cc_dt, 0, None, None,
+                                C.byref(ne), None, None), "mpt_prm_connect")
+    E = ne.value
+    edges = np.zeros((max(E, 1), 2), np.int32)
+    verdict = np.zeros(max(E, 1), np.uint8)
+    comp = np.zeros(max(n, 1), np.int32)
+    ms = np.zeros(4, np.float32)
+    check(lib().mpt_prm_connect(env.handle, agent.handle, kind, _p(st), n, dim, radius2, cc_dt, E, _p(edges),
+                                _p(verdict), C.byref(ne), _p(comp), _p(ms)), "mpt_prm_connect")
+    return {"edges": edges[:E], "verdict": verdict[:E], "comp": comp[:n],
+            "ms": dict(zip(["neighbours", "poses", "collision", "total"], ms.tolist()))}
+
+
 COLLIDE_MODES = {"split": 0, "fused": 1}
 
 

@@ -55,5 +55,9 @@ inline int32_t pt_levels(int64_t n) {
 }
 
 void launch_tree_nn1(const PointTreeDev &T, const double *q, int64_t nq, int32_t *ids, double *d2, hipStream_t stream);
+// Radius search (d2 < r2) over 3-dim keys: offsets == nullptr -> counts[qi]; else fill ids /
+// d2 of query qi from offsets[qi] on (traversal order).  below_only: ids <= qi only.
+void launch_tree_radius(const PointTreeDev &T, const double *q, int64_t nq, double r2, bool below_only,
+                        int32_t *counts, const int64_t *offsets, int32_t *ids, double *d2, hipStream_t stream);
 
 }  // namespace mpt

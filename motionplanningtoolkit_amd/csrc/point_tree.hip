@@ -311,6 +311,79 @@ __global__ __launch_bounds__(256) void k_tree_nn1(PointTreeDev T, const double *
     }
 }
 
+// Radius search (FLANN_KDTreeWrapper::kNearestWithin, utilities/flannkdtreewrapper.hpp:91-117:
+// points with squared L2 < r2) over the tree; below_only keeps only ids <= the query's row
+// (the milestones inserted before it).  Count pass (kFill = false) writes counts[qi]; the fill
+// pass writes the ids and d2 of query qi at offsets[qi] in traversal order.
+template <int D, bool kFill>
+__global__ __launch_bounds__(256) void k_tree_radius(PointTreeDev T, const double *__restrict__ q, int64_t nq, double r2,
+                                                     int32_t below_only, int32_t *__restrict__ counts,
+                                                     const int64_t *__restrict__ offsets, int32_t *__restrict__ out_ids,
+                                                     double *__restrict__ out_d2) {
+    __shared__ int32_t s_node[kPtGroupsPerBlock][kPtStack];
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t slot = t / kPtFan;
+    const int sub = (int)(t % kPtFan);
+    const int grp = threadIdx.x / kPtFan;
+    if (slot >= nq) return;
+    double qq[D];
+#pragma unroll
+    for (int i = 0; i < D; ++i) qq[i] = q[slot * D + i];
+    const int64_t n = live_n(T);
+    const int base = (threadIdx.x & 63) & ~(kPtFan - 1);
+    int64_t cursor = kFill ? offsets[slot] : 0;
+    int32_t found = 0;
+    if (n > 0) {
+        int sp = 1;
+        if (sub == 0) s_node[grp][0] = T.n_levels << 27;
+        __builtin_amdgcn_wave_barrier();
+        while (sp > 0) {
+            --sp;
+            const int32_t code = s_node[grp][sp];
+            __builtin_amdgcn_wave_barrier();
+            const int lev = code >> 27;
+            const int64_t idx = code & ((1 << 27) - 1);
+            if (lev == 1) {
+                const int64_t p = idx * kPtFan + sub;
+                bool hit = false;
+                double dd = 0.0;
+                int32_t id = 0;
+                if (p < n) {
+                    dd = flann_l2<D>(qq, T.pts + p * D);
+                    id = T.ids[p];
+                    hit = dd < r2 && (!below_only || (int64_t)id - 1 < slot);
+                }
+                const uint32_t gm = (uint32_t)(__ballot(hit) >> base) & 0xffu;
+                if (kFill && hit) {
+                    const int64_t pos = cursor + __popc(gm & ((1u << sub) - 1));
+                    out_ids[pos] = id;
+                    out_d2[pos] = dd;
+                }
+                cursor += __popc(gm);
+                found += __popc(gm);
+            } else {
+                const int64_t c = idx * kPtFan + sub;
+                bool keep = false;
+                if (c < lvl_size(n, lev - 1)) {
+                    const float *b = T.boxes + (lvl_off(T.n_upper, lev - 1) + c) * 2 * D;
+                    double lb2 = 0.0;
+#pragma unroll
+                    for (int k = 0; k < D; ++k) {
+                        const double g = fmax(fmax((double)b[k] - qq[k], qq[k] - (double)b[D + k]), 0.0);
+                        lb2 += g * g;
+                    }
+                    keep = lb2 * (1.0 - 1e-12) < r2;
+                }
+                const uint32_t gm = (uint32_t)(__ballot(keep) >> base) & 0xffu;
+                if (keep) s_node[grp][sp + __popc(gm & ((1u << sub) - 1))] = ((lev - 1) << 27) | (int32_t)c;
+                sp += __popc(gm);
+                __builtin_amdgcn_wave_barrier();
+            }
+        }
+    }
+    if (!kFill && sub == 0) counts[slot] = found;
+}
+
 }  // namespace
 
 PointTree::~PointTree() {
@@ -389,6 +462,20 @@ void PointTree::build(const double *pts, int64_t n_upper, const int64_t *n_dev, 
         hipLaunchKernelGGL(k_pt_up_boxes, dim3((unsigned)((ml + 255) / 256)), dim3(256), 0, stream, t, l, boxes);
         hip_check(hipGetLastError(), "k_pt_up_boxes");
     }
+}
+
+void launch_tree_radius(const PointTreeDev &T, const double *q, int64_t nq, double r2, bool below_only,
+                        int32_t *counts, const int64_t *offsets, int32_t *ids, double *d2, hipStream_t stream) {
+    if (nq <= 0) return;
+    if (T.d != 3) throw Error{1, "point tree radius: keys must have 3 dims"};
+    const dim3 grid((unsigned)((nq * kPtFan + 255) / 256));
+    if (offsets)
+        hipLaunchKernelGGL((k_tree_radius<3, true>), grid, dim3(256), 0, stream, T, q, nq, r2, (int32_t)below_only,
+                           counts, offsets, ids, d2);
+    else
+        hipLaunchKernelGGL((k_tree_radius<3, false>), grid, dim3(256), 0, stream, T, q, nq, r2, (int32_t)below_only,
+                           counts, offsets, ids, d2);
+    hip_check(hipGetLastError(), "k_tree_radius launch");
 }
 
 void launch_tree_nn1(const PointTreeDev &T, const double *q, int64_t nq, int32_t *ids, double *d2, hipStream_t stream) {

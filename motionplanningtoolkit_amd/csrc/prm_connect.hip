@@ -1,0 +1,309 @@
+// prm_connect.hip -- PRM roadmap edges on the device (BASELINE config 4).
+//
+// PRM::addMilestone (planners/prm/prm.hpp:334-387) per milestone: neighbours from the NN,
+// steer(src, tgt, 1000), Map3D::safeEdge, add_edge + union_set.  Config 4 asks for radius
+// neighbours (FLANN_KDTreeWrapper::kNearestWithin, utilities/flannkdtreewrapper.hpp:91-117:
+// squared L2 < radius) in place of the approximate kNN(10).  With radius neighbours the
+// roadmap does not depend on the insertion batching: milestone i connects to every earlier j
+// within the radius.  So all milestones go through one pipeline:
+//   keys (first three state variables, prm.hpp:155) -> point tree (point_tree.hip) ->
+//   radius count -> scan -> radius fill (j < i) -> per-query sort by j -> per edge
+//   Omnidirectional::steer(i, j, 1000) and getPoses at cc_dt -> pose scan -> poses ->
+//   batched collision (broad.hip split path) -> verdicts; components on the host.
+// Edge poses translate along the key segment (Omnidirectional::getPoses); a blimp mesh keeps
+// the yaw of milestone i (Blimp::stateToFCLTransform's R, cos/sin from the host's libm so the
+// rotation is bit-identical to the oracle's).
+#include <hipcub/hipcub.hpp>
+
+#include <algorithm>
+#include <cmath>
+#include <vector>
+
+#include "../../include/mpt.h"
+#include "mpt_internal.h"
+#include "point_tree.h"
+
+namespace mpt {
+const EnvDev &env_dev(const mpt_env *e);
+const AgentDev &agent_dev(const mpt_agent *a);
+}  // namespace mpt
+
+using namespace mpt;
+
+namespace {
+
+__global__ void k_widen(const int32_t *__restrict__ c, int64_t n, int64_t *__restrict__ out) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) out[i] = c[i];
+    if (i == n) out[i] = 0;
+}
+
+// each query's neighbours by id (ascending), and the edge -> source milestone map
+__global__ void k_sort_segments(const int64_t *__restrict__ off, int64_t nq, int32_t *__restrict__ ids,
+                                int32_t *__restrict__ src) {
+    const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= nq) return;
+    const int64_t a = off[q], b = off[q + 1];
+    for (int64_t i = a + 1; i < b; ++i) {
+        const int32_t v = ids[i];
+        int64_t k = i - 1;
+        while (k >= a && ids[k] > v) {
+            ids[k + 1] = ids[k];
+            --k;
+        }
+        ids[k + 1] = v;
+    }
+    for (int64_t i = a; i < b; ++i) src[i] = (int32_t)q;
+}
+
+// Omnidirectional::steer(start, goal, 1000) (agents/omnidirectional.hpp:186-198, prm.hpp:366)
+__device__ __forceinline__ void steer_end(const double *s, const double *g, double *e) {
+    const double dx = g[0] - s[0], dy = g[1] - s[1], dz = g[2] - s[2];
+    const double dist = sqrt(dx * dx + dy * dy + dz * dz);
+    double fraction = 1000.0 / dist;
+    if (fraction > 1) fraction = 1;
+    e[0] = s[0] + dx * fraction;
+    e[1] = s[1] + dy * fraction;
+    e[2] = s[2] + dz * fraction;
+}
+
+// Omnidirectional::getPoses count (agents/omnidirectional.hpp:202-247)
+__device__ __forceinline__ int64_t omni_pose_count(const double *s, const double *e, double dt, double &dist,
+                                                   unsigned &it) {
+    const double dx = e[0] - s[0], dy = e[1] - s[1], dz = e[2] - s[2];
+    dist = sqrt(dx * dx + dy * dy + dz * dz);
+    const double q = dist / dt;
+    it = (q >= 4294967296.0 || !(q >= 0)) ? 0u : (unsigned)q;
+    if (it < 1) return 2;
+    return (int64_t)it + (((double)it * dt < dist) ? 1 : 0);
+}
+
+__global__ void k_edge_pose_count(const double *__restrict__ keys, const int32_t *__restrict__ src,
+                                  const int32_t *__restrict__ nbr, int64_t E, double dt, int64_t *__restrict__ pc) {
+    const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e > E) return;
+    if (e == E) {
+        pc[e] = 0;
+        return;
+    }
+    const double *s = keys + (int64_t)src[e] * 3;
+    double end[3], dist;
+    unsigned it;
+    steer_end(s, keys + (int64_t)(nbr[e] - 1) * 3, end);
+    pc[e] = omni_pose_count(s, end, dt, dist, it);
+}
+
+__device__ __forceinline__ void put_pose(double *o, const double *cs, double x, double y, double z) {
+    const double c = cs[0], s = cs[1];
+    o[0] = c; o[1] = s; o[2] = 0.0;
+    o[3] = -s; o[4] = c; o[5] = 0.0;
+    o[6] = 0.0; o[7] = 0.0; o[8] = 1.0;
+    o[9] = x; o[10] = y; o[11] = z;
+}
+
+__global__ void k_edge_poses(const double *__restrict__ keys, const double *__restrict__ rot,
+                             const int32_t *__restrict__ src, const int32_t *__restrict__ nbr, int64_t E, double dt,
+                             const int64_t *__restrict__ poff, double *__restrict__ poses, int32_t *__restrict__ pose_edge) {
+    const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= E) return;
+    const double *s = keys + (int64_t)src[e] * 3;
+    const double *cs = rot + (int64_t)src[e] * 2;
+    double end[3], dist;
+    unsigned it;
+    steer_end(s, keys + (int64_t)(nbr[e] - 1) * 3, end);
+    (void)omni_pose_count(s, end, dt, dist, it);
+    int64_t p = poff[e];
+    const double dx = end[0] - s[0], dy = end[1] - s[1], dz = end[2] - s[2];
+    if (it < 1) {
+        put_pose(poses + 12 * p, cs, s[0], s[1], s[2]);
+        pose_edge[p++] = (int32_t)e;
+        put_pose(poses + 12 * p, cs, end[0], end[1], end[2]);
+        pose_edge[p++] = (int32_t)e;
+        return;
+    }
+    const double step = dt / dist;
+    for (unsigned i = 0; i < it; ++i) {
+        const double st = step * (double)i;
+        put_pose(poses + 12 * p, cs, s[0] + st * dx, s[1] + st * dy, s[2] + st * dz);
+        pose_edge[p++] = (int32_t)e;
+    }
+    if ((double)it * dt < dist) {
+        put_pose(poses + 12 * p, cs, end[0], end[1], end[2]);
+        pose_edge[p++] = (int32_t)e;
+    }
+}
+
+template <class T>
+struct DBuf {
+    T *p = nullptr;
+    int64_t cap = 0;
+    T *get(int64_t n) {
+        if (n > cap) {
+            if (p) hip_check(hipFree(p), "free");
+            cap = std::max<int64_t>(n, 2 * cap);
+            hip_check(hipMalloc(&p, sizeof(T) * (size_t)std::max<int64_t>(cap, 1)), "prm buffer");
+        }
+        return p;
+    }
+    ~DBuf() {
+        if (p) (void)hipFree(p);
+    }
+};
+
+struct PrmScratch {
+    PointTree tree;
+    CollideScratch cs;
+    DBuf<double> keys, rot, d2, poses;
+    DBuf<int32_t> counts, nbr, src, pose_edge;
+    DBuf<int64_t> off, poff, n_dev;
+    DBuf<uint8_t> verdict;
+    DBuf<AgentDev> link;
+    DBuf<char> temp;
+};
+
+int64_t scan_total(int64_t *d_in_out, int64_t n_plus_1, DBuf<char> &temp, hipStream_t stream) {
+    size_t tb = 0;
+    hip_check(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, d_in_out, d_in_out, (int)n_plus_1), "scan size");
+    void *t = temp.get((int64_t)tb + 1);
+    hip_check(hipcub::DeviceScan::ExclusiveSum(t, tb, d_in_out, d_in_out, (int)n_plus_1, stream), "scan");
+    int64_t total = 0;
+    hip_check(hipMemcpyAsync(&total, d_in_out + n_plus_1 - 1, sizeof(int64_t), hipMemcpyDeviceToHost, stream), "total");
+    hip_check(hipStreamSynchronize(stream), "scan sync");
+    return total;
+}
+
+int32_t uf_find(std::vector<int32_t> &p, int32_t x) {
+    while (p[x] != x) {
+        p[x] = p[p[x]];
+        x = p[x];
+    }
+    return x;
+}
+
+}  // namespace
+
+extern "C" mpt_status mpt_prm_connect(const mpt_env *env, const mpt_agent *agent, int32_t agent_kind,
+                                      const double *states, int64_t n, int32_t dim, double radius2, double cc_dt,
+                                      int64_t cap, int32_t *edges, uint8_t *verdict, int64_t *n_edges, int32_t *comp,
+                                      float ms[4]) {
+    return guarded([&] {
+        if (!env || !agent || !n_edges || n < 0 || (n > 0 && !states)) throw Error{MPT_ERR_INVALID, "bad arguments"};
+        if (!(agent_kind == MPT_AGENT_OMNI && dim == 3) && !(agent_kind == MPT_AGENT_BLIMP && dim == 7))
+            throw Error{MPT_ERR_INVALID, "mpt_prm_connect: omnidirectional (dim 3) or blimp (dim 7) milestones"};
+        if (!(cc_dt > 0) || !(radius2 >= 0)) throw Error{MPT_ERR_INVALID, "bad radius / dt"};
+        if (n >= (int64_t(1) << 27)) throw Error{MPT_ERR_INVALID, "too many milestones"};
+        static thread_local PrmScratch S;
+        hipStream_t stream = nullptr;
+        hipEvent_t ev[5];
+        for (auto &e : ev) hip_check(hipEventCreate(&e), "event");
+        struct EvGuard {
+            hipEvent_t *e;
+            ~EvGuard() {
+                for (int i = 0; i < 5; ++i) (void)hipEventDestroy(e[i]);
+            }
+        } guard{ev};
+        hip_check(hipEventRecord(ev[0], stream), "event");
+        // keys and yaw on the host (libm cos/sin, as the oracle)
+        std::vector<double> hk((size_t)n * 3), hr((size_t)n * 2);
+        for (int64_t i = 0; i < n; ++i) {
+            for (int k = 0; k < 3; ++k) hk[i * 3 + k] = states[i * dim + k];
+            hr[i * 2] = dim == 7 ? std::cos(states[i * dim + 3]) : 1.0;
+            hr[i * 2 + 1] = dim == 7 ? std::sin(states[i * dim + 3]) : 0.0;
+        }
+        double *d_keys = S.keys.get(n * 3), *d_rot = S.rot.get(n * 2);
+        int64_t *d_n = S.n_dev.get(1);
+        hip_check(hipMemcpy(d_keys, hk.data(), sizeof(double) * n * 3, hipMemcpyHostToDevice), "keys");
+        hip_check(hipMemcpy(d_rot, hr.data(), sizeof(double) * n * 2, hipMemcpyHostToDevice), "rot");
+        hip_check(hipMemcpy(d_n, &n, sizeof(int64_t), hipMemcpyHostToDevice), "n");
+        // neighbours: j < i with squared key distance < radius2, sorted by j
+        int64_t E = 0;
+        int32_t *d_cnt = S.counts.get(n + 1);
+        int64_t *d_off = S.off.get(n + 1);
+        if (n > 0) {
+            S.tree.build(d_keys, n, d_n, 3, stream);
+            const PointTreeDev T = S.tree.dev();
+            launch_tree_radius(T, d_keys, n, radius2, true, d_cnt, nullptr, nullptr, nullptr, stream);
+            hipLaunchKernelGGL(k_widen, dim3((unsigned)((n + 1 + 255) / 256)), dim3(256), 0, stream, d_cnt, n, d_off);
+            E = scan_total(d_off, n + 1, S.temp, stream);
+        }
+        if (E >= (int64_t(1) << 31)) throw Error{MPT_ERR_CAPACITY, "too many roadmap edges"};
+        int32_t *d_nbr = S.nbr.get(E), *d_src = S.src.get(E);
+        double *d_d2 = S.d2.get(E);
+        if (E > 0) {
+            launch_tree_radius(S.tree.dev(), d_keys, n, radius2, true, d_cnt, d_off, d_nbr, d_d2, stream);
+            hipLaunchKernelGGL(k_sort_segments, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, d_off, n, d_nbr,
+                               d_src);
+            hip_check(hipGetLastError(), "k_sort_segments");
+        }
+        hip_check(hipEventRecord(ev[1], stream), "event");
+        // poses of every edge
+        int64_t P = 0;
+        int64_t *d_poff = S.poff.get(E + 1);
+        if (E > 0) {
+            hipLaunchKernelGGL(k_edge_pose_count, dim3((unsigned)((E + 1 + 255) / 256)), dim3(256), 0, stream, d_keys,
+                               d_src, d_nbr, E, cc_dt, d_poff);
+            P = scan_total(d_poff, E + 1, S.temp, stream);
+        }
+        if (P >= (int64_t(1) << 31)) throw Error{MPT_ERR_CAPACITY, "too many edge poses"};
+        double *d_poses = S.poses.get(P * 12);
+        int32_t *d_pe = S.pose_edge.get(P);
+        if (E > 0)
+            hipLaunchKernelGGL(k_edge_poses, dim3((unsigned)((E + 255) / 256)), dim3(256), 0, stream, d_keys, d_rot, d_src,
+                               d_nbr, E, cc_dt, d_poff, d_poses, d_pe);
+        hip_check(hipEventRecord(ev[2], stream), "event");
+        // collision verdicts (two-phase path)
+        uint8_t *d_v = S.verdict.get(E);
+        if (E > 0) {
+            hip_check(hipMemsetAsync(d_v, 0, (size_t)E, stream), "verdict memset");
+            AgentDev *d_link = S.link.get(1);
+            const AgentDev ag = agent_dev(agent);
+            hip_check(hipMemcpy(d_link, &ag, sizeof(AgentDev), hipMemcpyHostToDevice), "link");
+            CollideWork w{};
+            w.poses = d_poses;
+            w.pose_edge = d_pe;
+            w.pmax = 1;
+            w.L = 1;
+            w.n_units = P;
+            w.verdict = d_v;
+            const int32_t mc = std::max(1, ag.n_clusters);
+            S.cs.ensure(P, mc);
+            launch_collide_split(env_dev(env), d_link, mc, w, S.cs, stream);
+        }
+        hip_check(hipEventRecord(ev[3], stream), "event");
+        std::vector<int32_t> h_src((size_t)E), h_nbr((size_t)E);
+        std::vector<uint8_t> h_v((size_t)E);
+        if (E > 0) {
+            hip_check(hipMemcpyAsync(h_src.data(), d_src, sizeof(int32_t) * E, hipMemcpyDeviceToHost, stream), "src");
+            hip_check(hipMemcpyAsync(h_nbr.data(), d_nbr, sizeof(int32_t) * E, hipMemcpyDeviceToHost, stream), "nbr");
+            hip_check(hipMemcpyAsync(h_v.data(), d_v, (size_t)E, hipMemcpyDeviceToHost, stream), "verdict");
+        }
+        hip_check(hipStreamSynchronize(stream), "prm sync");
+        // union-find over the collision-free edges (disjoint_sets, prm.hpp:346,376)
+        std::vector<int32_t> parent((size_t)n);
+        for (int64_t i = 0; i < n; ++i) parent[i] = (int32_t)i;
+        for (int64_t e = 0; e < E; ++e) {
+            if (h_v[e]) continue;
+            const int32_t a = uf_find(parent, h_src[e]), b = uf_find(parent, h_nbr[e] - 1);
+            if (a != b) parent[std::max(a, b)] = std::min(a, b);
+        }
+        hip_check(hipEventRecord(ev[4], stream), "event");
+        hip_check(hipEventSynchronize(ev[4]), "event sync");
+        *n_edges = E;
+        const int64_t m = std::min(E, cap);
+        for (int64_t e = 0; e < m; ++e) {
+            if (edges) {
+                edges[2 * e] = h_src[e];
+                edges[2 * e + 1] = h_nbr[e] - 1;
+            }
+            if (verdict) verdict[e] = h_v[e];
+        }
+        if (comp)
+            for (int64_t i = 0; i < n; ++i) comp[i] = uf_find(parent, (int32_t)i);
+        if (ms) {
+            hip_check(hipEventElapsedTime(&ms[0], ev[0], ev[1]), "elapsed");
+            hip_check(hipEventElapsedTime(&ms[1], ev[1], ev[2]), "elapsed");
+            hip_check(hipEventElapsedTime(&ms[2], ev[2], ev[3]), "elapsed");
+            hip_check(hipEventElapsedTime(&ms[3], ev[0], ev[4]), "elapsed");
+        }
+    });
+}

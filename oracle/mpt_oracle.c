@@ -1230,3 +1230,77 @@ void orc_distance_batch(const double *env_tris, int64_t Te, const double env_tf[
     }
     (void)nthreads;
 }
+
+/* ======================================================================
+ * PRM with radius neighbours (config 4): planners/prm/prm.hpp:334-387 (addMilestone) with
+ * FLANN_KDTreeWrapper::kNearestWithin (utilities/flannkdtreewrapper.hpp:91-117) as the NN.
+ * ====================================================================== */
+int64_t orc_prm_radius(const orc_bvh *env, const double env_tf[12], const double *agent_tris, int64_t Ta,
+                       const double *states, int64_t n, int32_t dim, double r2, double cc_dt,
+                       int32_t *edges, uint8_t *verdict, int64_t cap, int32_t *comp, int nthreads) {
+    /* neighbours of each milestone among the earlier ones, in (i, j) order */
+    int64_t E = 0, ecap = 1024;
+    int32_t *ei = (int32_t *)malloc(sizeof(int32_t) * 2 * (size_t)ecap);
+    for (int64_t i = 0; i < n; ++i) {
+        double ki[3];
+        memcpy(ki, states + i * dim, sizeof ki);
+        for (int64_t j = 0; j < i; ++j) {
+            double kj[3];
+            memcpy(kj, states + j * dim, sizeof kj);
+            if (!(orc_l2(ki, kj, 3) < r2)) continue;
+            if (E == ecap) {
+                ecap *= 2;
+                ei = (int32_t *)realloc(ei, sizeof(int32_t) * 2 * (size_t)ecap);
+            }
+            ei[2 * E] = (int32_t)i;
+            ei[2 * E + 1] = (int32_t)j;
+            ++E;
+        }
+    }
+    uint8_t *v = (uint8_t *)calloc((size_t)(E > 0 ? E : 1), 1);
+#ifdef _OPENMP
+#pragma omp parallel for schedule(dynamic, 16) num_threads(nthreads > 0 ? nthreads : 1)
+#endif
+    for (int64_t e = 0; e < E; ++e) {
+        const double *s = states + (int64_t)ei[2 * e] * dim, *g = states + (int64_t)ei[2 * e + 1] * dim;
+        /* Omnidirectional::steer(start, goal, 1000) */
+        const double dx = g[0] - s[0], dy = g[1] - s[1], dz = g[2] - s[2];
+        const double dist = sqrt(dx * dx + dy * dy + dz * dz);
+        double fraction = 1000.0 / dist;
+        if (fraction > 1) fraction = 1;
+        const double end[3] = {s[0] + dx * fraction, s[1] + dy * fraction, s[2] + dz * fraction};
+        const int32_t P = orc_omni_get_poses(s, end, cc_dt, NULL, 0);
+        double *poses = (double *)malloc(sizeof(double) * 12 * (size_t)(P > 0 ? P : 1));
+        orc_omni_get_poses(s, end, cc_dt, poses, P);
+        if (dim == 7) { /* Blimp::stateToFCLTransform's R from milestone i's yaw */
+            const double c = cos(s[3]), sn = sin(s[3]);
+            for (int32_t p = 0; p < P; ++p) {
+                double *R = poses + 12 * p;
+                R[0] = c; R[1] = sn; R[2] = 0; R[3] = -sn; R[4] = c; R[5] = 0; R[6] = 0; R[7] = 0; R[8] = 1;
+            }
+        }
+        int hit = 0;
+        for (int32_t p = 0; p < P && !hit; ++p) hit = orc_collide_unit_bvh(env, env_tf, agent_tris, Ta, poses + 12 * p, NULL);
+        v[e] = (uint8_t)hit;
+        free(poses);
+    }
+    (void)nthreads;
+    int32_t *parent = (int32_t *)malloc(sizeof(int32_t) * (size_t)(n > 0 ? n : 1));
+    for (int64_t i = 0; i < n; ++i) parent[i] = (int32_t)i;
+    for (int64_t e = 0; e < E; ++e) {
+        if (v[e]) continue;
+        const int32_t a = uf_find(parent, ei[2 * e]), b = uf_find(parent, ei[2 * e + 1]);
+        if (a != b) parent[a > b ? a : b] = a < b ? a : b;
+    }
+    for (int64_t e = 0; e < E && e < cap; ++e) {
+        edges[2 * e] = ei[2 * e];
+        edges[2 * e + 1] = ei[2 * e + 1];
+        verdict[e] = v[e];
+    }
+    if (comp)
+        for (int64_t i = 0; i < n; ++i) comp[i] = uf_find(parent, (int32_t)i);
+    free(ei);
+    free(v);
+    free(parent);
+    return E;
+}

@@ -164,6 +164,15 @@ void orc_distance_batch(const double *env_tris, int64_t Te, const double env_tf[
                         const double *poses, const int64_t *edge_pose_offsets, int64_t E,
                         double *dist, int nthreads);
 
+/* PRM roadmap with radius neighbours (config 4; prm.hpp:334-387 with kNearestWithin):
+ * edges (i, j), j < i, squared L2 of the first three state variables < r2, sorted by (i, j);
+ * verdict per edge over Omnidirectional::steer(key_i, key_j, 1000) + getPoses(cc_dt) with the
+ * blimp yaw of milestone i (dim 7) or identity (dim 3); comp = smallest milestone of each
+ * component over the free edges.  Returns E (arrays written up to cap). */
+int64_t orc_prm_radius(const orc_bvh *env, const double env_tf[12], const double *agent_tris, int64_t Ta,
+                       const double *states, int64_t n, int32_t dim, double r2, double cc_dt,
+                       int32_t *edges, uint8_t *verdict, int64_t cap, int32_t *comp, int nthreads);
+
 #ifdef __cplusplus
 }
 #endif

@@ -70,6 +70,7 @@ def lib():
             "orc_engine_step": (I64, [I32, P, I32, P, D, D, U64, U64, I32, P, P, P, I64, P, P, I64, I64, P, P, C.c_int, C.c_int]),
             "orc_prm_build": (I64, [P, P, P, I64, P, I64, I32, I32, D, P, P, I64, P]),
             "orc_tri_distance": (D, [P, P]),
+            "orc_prm_radius": (I64, [P, P, P, I64, P, I64, I32, D, D, P, P, I64, P, C.c_int]),
             "orc_distance_unit": (D, [P, I64, P, P, I64, P]),
             "orc_distance_batch": (None, [P, I64, P, P, P, I32, P, P, I64, P, C.c_int]),
         }
@@ -119,6 +120,21 @@ def collide_batch(env_tris, env_tf, link_tris: list, poses, edge_offsets) -> np.
     lib().orc_collide_batch(_p(env_tris), env_tris.shape[0], _p(_f64(env_tf)), _p(agent), _p(off),
                             len(link_tris), _p(poses), _p(eo), E, _p(out))
     return out
+
+
+def prm_radius(bvh: BVH, env_tf, agent_tris, states, r2: float, cc_dt: float, nthreads=8):
+    """orc_prm_radius: (edges [E][2] = (i, j), verdict [E], comp [n])."""
+    st = _f64(states)
+    n, dim = st.shape
+    at = _f64(agent_tris).reshape(-1, 9)
+    E = lib().orc_prm_radius(bvh.ptr, _p(_f64(env_tf)), _p(at), at.shape[0], _p(st), n, dim, r2, cc_dt, None, None, 0,
+                             None, nthreads)
+    edges = np.zeros((max(E, 1), 2), np.int32)
+    verdict = np.zeros(max(E, 1), np.uint8)
+    comp = np.zeros(max(n, 1), np.int32)
+    lib().orc_prm_radius(bvh.ptr, _p(_f64(env_tf)), _p(at), at.shape[0], _p(st), n, dim, r2, cc_dt, _p(edges),
+                         _p(verdict), E, _p(comp), nthreads)
+    return edges[:E], verdict[:E], comp[:n]
 
 
 def tri_distance(S, T) -> float:

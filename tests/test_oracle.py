@@ -377,3 +377,26 @@ def test_tri_distance_matches_sampling(oracle):
         ds = _sampled_tri_distance(S, T)
         assert d <= ds + 1e-12
         assert d >= ds - 0.08  # sampling resolution (edge length / 60 across two triangles)
+
+
+def test_oracle_prm_radius_is_consistent(oracle):
+    """orc_prm_radius (config 4): edges are exactly the earlier milestones within the radius,
+    in (i, j) order; components are those of the free edges."""
+    from scipy.sparse import coo_matrix
+    from scipy.sparse.csgraph import connected_components
+
+    sc = scenes.omni_scenario()
+    bvh = oracle.BVH(sc.env_tris)
+    st = np.random.default_rng(4).uniform(-6, 6, (400, 3))
+    r2 = 2.0 ** 2
+    edges, verdict, comp = oracle.prm_radius(bvh, sc.env_tf, sc.agent_tris, st, r2, sc.cc_dt)
+    d2 = ((st[:, None, :] - st[None, :, :]) ** 2).sum(-1)
+    want = [(i, j) for i in range(len(st)) for j in range(i) if d2[i, j] < r2]
+    assert [tuple(e) for e in edges] == want
+    assert 0 < verdict.sum() < len(edges)
+    free = edges[verdict == 0]
+    g = coo_matrix((np.ones(len(free)), (free[:, 0], free[:, 1])), shape=(len(st),) * 2)
+    _, lab = connected_components(g, directed=False)
+    for c in np.unique(lab):
+        m = np.flatnonzero(lab == c)
+        assert np.all(comp[m] == m.min())
