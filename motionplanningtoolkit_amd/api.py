@@ -154,15 +154,18 @@ def prm_connect(env: Environment, agent: AgentMesh, kind: int, states, radius2: 
     st = _f64(states)
     n, dim = st.shape
     ne = C.c_int64()
-    check(lib().mpt_prm_connect(env.handle, agent.handle, kind, _p(st), n, dim, radius2, cc_dt, 0, None, None,
-                                C.byref(ne), None, None), "mpt_prm_connect")
-    E = ne.value
-    edges = np.zeros((max(E, 1), 2), np.int32)
-    verdict = np.zeros(max(E, 1), np.uint8)
-    comp = np.zeros(max(n, 1), np.int32)
-    ms = np.zeros(4, np.float32)
-    check(lib().mpt_prm_connect(env.handle, agent.handle, kind, _p(st), n, dim, radius2, cc_dt, E, _p(edges),
-                                _p(verdict), C.byref(ne), _p(comp), _p(ms)), "mpt_prm_connect")
+    cap = max(64 * n, 1024)  # room for a mean of 64 earlier neighbours; re-run only beyond that
+    while True:
+        edges = np.zeros((cap, 2), np.int32)
+        verdict = np.zeros(cap, np.uint8)
+        comp = np.zeros(max(n, 1), np.int32)
+        ms = np.zeros(4, np.float32)
+        check(lib().mpt_prm_connect(env.handle, agent.handle, kind, _p(st), n, dim, radius2, cc_dt, cap, _p(edges),
+                                    _p(verdict), C.byref(ne), _p(comp), _p(ms)), "mpt_prm_connect")
+        E = ne.value
+        if E <= cap:
+            break
+        cap = E
     return {"edges": edges[:E], "verdict": verdict[:E], "comp": comp[:n],
             "ms": dict(zip(["neighbours", "poses", "collision", "total"], ms.tolist()))}
 

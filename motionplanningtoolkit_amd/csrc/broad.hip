@@ -30,7 +30,8 @@ namespace mpt {
 constexpr int kPairThreads = 256;   // k_pairs workgroup (4 waves)
 constexpr int kPairCap = 256;       // env triangles per k_pairs wave segment
 constexpr int kHdrCap = 64;         // headers per segment (one per lane at most)
-constexpr int kCandCap = 512;       // candidates per k_cands wave (then the spill list)
+constexpr int kCandCap = 2048;      // candidates per k_cands wave (then the spill list)
+constexpr int64_t kSplitChunkUnits = 1 << 18;  // units per launch of the two-phase path
 constexpr int kSpillCap = 1 << 22;  // shared spill list (48 MiB)
 constexpr int kSpillBlocks = 256;   // k_narrow workgroups over the spill list
 constexpr int kLdsItems = 2048;     // env tree staged in LDS by k_pairs up to this size (64 KiB)
@@ -394,6 +395,7 @@ CollideScratch::~CollideScratch() {
 }
 
 void CollideScratch::ensure(int64_t n_units, int32_t max_clusters) {
+    n_units = std::min<int64_t>(n_units, kSplitChunkUnits);  // launch_collide_split runs chunks
     if (!ctl) {
         int dev = 0, cus = 256;
         if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
@@ -436,8 +438,8 @@ void CollideScratch::ensure(int64_t n_units, int32_t max_clusters) {
     }
 }
 
-void launch_collide_split(const EnvDev &env, const AgentDev *d_links, int32_t max_clusters, const CollideWork &w,
-                          CollideScratch &s, hipStream_t stream, hipEvent_t *marks) {
+static void collide_split_chunk(const EnvDev &env, const AgentDev *d_links, int32_t max_clusters,
+                                const CollideWork &w, CollideScratch &s, hipStream_t stream, hipEvent_t *marks) {
     auto mark = [&](int i) {
         if (marks) hip_check(hipEventRecord(marks[i], stream), "event record");
     };
@@ -501,6 +503,35 @@ void launch_collide_split(const EnvDev &env, const AgentDev *d_links, int32_t ma
     f.unit_list_n = s.ctl + 1;
     f.stats = nullptr;
     launch_collide(env, d_links, f, stream, 64);
+}
+
+// Large batches run in chunks of whole edges (mode A: whole poses) of about kSplitChunkUnits
+// units, by offsetting the pointers: the per-launch candidate segments and spill list then
+// hold a chunk's candidates instead of overflowing to the fused kernel (config 4's 21 M
+// poses overflowed 8 M units).  The scratch is sized for one chunk.
+void launch_collide_split(const EnvDev &env, const AgentDev *d_links, int32_t max_clusters, const CollideWork &w,
+                          CollideScratch &s, hipStream_t stream, hipEvent_t *marks) {
+    const int64_t g = w.pose_edge ? (int64_t)w.L : (int64_t)w.pmax * w.L;
+    const int64_t per = std::max<int64_t>(g, (kSplitChunkUnits / g) * g);
+    if (w.n_units <= per) {
+        collide_split_chunk(env, d_links, max_clusters, w, s, stream, marks);
+        return;
+    }
+    for (int64_t u0 = 0; u0 < w.n_units; u0 += per) {
+        CollideWork c = w;
+        c.n_units = std::min(per, w.n_units - u0);
+        if (w.pose_edge) {
+            const int64_t p0 = u0 / w.L;
+            c.poses = w.poses + p0 * w.L * 12;
+            c.pose_edge = w.pose_edge + p0;
+        } else {
+            const int64_t e0 = u0 / g;
+            c.poses = w.poses + e0 * g * 12;
+            c.pcount = w.pcount + e0;
+            c.verdict = w.verdict + e0;
+        }
+        collide_split_chunk(env, d_links, max_clusters, c, s, stream, u0 + per >= w.n_units ? marks : nullptr);
+    }
 }
 
 }  // namespace mpt

@@ -155,6 +155,13 @@ void launch_collide_split(const EnvDev &env, const AgentDev *d_links, int32_t ma
                           CollideScratch &s, hipStream_t stream, hipEvent_t *marks = nullptr);
 void launch_pose_edge(const int64_t *d_offsets, int64_t E, int32_t *d_pose_edge, hipStream_t stream);
 
+// Edges whose poses share one rotation (sweep.hip): poses of edge e are [poff[e], poff[e+1]);
+// one wave per (edge, cluster) of the single link d_link[0]; verdict[E] must be zeroed.
+// stats (optional [4]): waves, env item tests, (pair, pose) gate tests, SAT tests.
+void launch_collide_sweep(const EnvDev &env, const AgentDev *d_link, int32_t n_clusters, const double *poses,
+                          const int64_t *poff, int64_t E, uint8_t *verdict, unsigned long long *stats,
+                          hipStream_t stream);
+
 // ---------------- distance (distance.hip) ----------------
 // Units are (pose, link) pairs as for collide mode A; best[E] receives the per-edge minimum
 // distance as the bit pattern of a double (DBL_MAX when the edge has no poses).

@@ -9,7 +9,8 @@
 //   keys (first three state variables, prm.hpp:155) -> point tree (point_tree.hip) ->
 //   radius count -> scan -> radius fill (j < i) -> per-query sort by j -> per edge
 //   Omnidirectional::steer(i, j, 1000) and getPoses at cc_dt -> pose scan -> poses ->
-//   batched collision (broad.hip split path) -> verdicts; components on the host.
+//   batched collision (sweep.hip: one wave per (edge, agent cluster)) -> verdicts; components
+//   on the host.
 // Edge poses translate along the key segment (Omnidirectional::getPoses); a blimp mesh keeps
 // the yaw of milestone i (Blimp::stateToFCLTransform's R, cos/sin from the host's libm so the
 // rotation is bit-identical to the oracle's).
@@ -17,6 +18,9 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <string>
 #include <vector>
 
 #include "../../include/mpt.h"
@@ -26,6 +30,7 @@
 namespace mpt {
 const EnvDev &env_dev(const mpt_env *e);
 const AgentDev &agent_dev(const mpt_agent *a);
+int32_t collide_mode();
 }  // namespace mpt
 
 using namespace mpt;
@@ -251,7 +256,7 @@ extern "C" mpt_status mpt_prm_connect(const mpt_env *env, const mpt_agent *agent
             hipLaunchKernelGGL(k_edge_poses, dim3((unsigned)((E + 255) / 256)), dim3(256), 0, stream, d_keys, d_rot, d_src,
                                d_nbr, E, cc_dt, d_poff, d_poses, d_pe);
         hip_check(hipEventRecord(ev[2], stream), "event");
-        // collision verdicts (two-phase path)
+        // collision verdicts (sweep path; MPT_PRM_COLLIDE=split|fused selects the per-pose paths)
         uint8_t *d_v = S.verdict.get(E);
         if (E > 0) {
             hip_check(hipMemsetAsync(d_v, 0, (size_t)E, stream), "verdict memset");
@@ -266,8 +271,15 @@ extern "C" mpt_status mpt_prm_connect(const mpt_env *env, const mpt_agent *agent
             w.n_units = P;
             w.verdict = d_v;
             const int32_t mc = std::max(1, ag.n_clusters);
-            S.cs.ensure(P, mc);
-            launch_collide_split(env_dev(env), d_link, mc, w, S.cs, stream);
+            static const char *path = getenv("MPT_PRM_COLLIDE");  // sweep (default) | split | fused
+            if (!path || std::string(path) == "sweep") {
+                launch_collide_sweep(env_dev(env), d_link, mc, d_poses, d_poff, E, d_v, nullptr, stream);
+            } else if (std::string(path) == "fused") {
+                launch_collide(env_dev(env), d_link, w, stream);
+            } else {
+                S.cs.ensure(P, mc);
+                launch_collide_split(env_dev(env), d_link, mc, w, S.cs, stream);
+            }
         }
         hip_check(hipEventRecord(ev[3], stream), "event");
         std::vector<int32_t> h_src((size_t)E), h_nbr((size_t)E);

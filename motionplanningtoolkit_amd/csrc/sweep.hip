@@ -1,0 +1,190 @@
+// sweep.hip -- collision of straight-line edges whose poses share one rotation.
+//
+// Same verdicts as the two-phase and fused paths (verdict[e] = some pose p of edge e, agent
+// triangle a and env triangle t with tri_gate and intersect_Triangle true), organised around
+// the edge instead of the pose.  PRM edges (prm_connect.hip: Omnidirectional::getPoses along
+// the key segment, one yaw per edge) have ~40 poses 0.1 apart that overlap nearly the same env
+// triangles, so per-pose broad phases redo the same work ~40 times.  Here one wave handles one
+// (edge, agent cluster):
+//   1. R, T of the first and last pose (fcl::relativeTransform, uniform); the cluster's box at
+//      both ends -> swept box (every pose's translation lies on the segment between them; the
+//      widened float boxes cover the rounding of the interpolated translations);
+//   2. lanes = the cluster's triangles: R Q once (the rotated vertices; each pose only adds
+//      its T, exactly as xform() orders the operations), swept triangle box;
+//   3. the wave walks the 64-ary env tree against the swept cluster box (lanes = a node's
+//      children, LDS stack); at a bucket, each env triangle whose box meets the swept cluster
+//      box is tested by the lanes whose swept triangle box meets it, over the edge's poses:
+//      Q'_p = R Q + T_p, exact tri_gate, intersect_Triangle; a hit sets verdict[e] and every
+//      wave of the edge stops.
+#include "collide_common.h"
+
+namespace mpt {
+
+constexpr int kSweepWaves = 4;
+constexpr int kSweepStack = kMaxLevels * kWave;
+
+struct SweepCounters {
+    uint32_t waves = 0, items = 0, pair_poses = 0, sat = 0;
+};
+
+__device__ __forceinline__ void sweep_wave(const EnvDev &env, const AgentDev &ag, const double *__restrict__ poses,
+                                           const int64_t *__restrict__ poff, int64_t e, int32_t cl, uint8_t *verdict,
+                                           int lane, int32_t *stk, SweepCounters &cnt) {
+    if (load_flag(verdict + e)) return;
+    const int64_t p0 = poff[e], p1 = poff[e + 1];
+    if (p1 <= p0) return;
+    ++cnt.waves;
+    double R[9], T0[3], TN[3];
+    unit_transform(env, poses + p0 * 12, R, T0);
+    {
+        double R2[9];
+        unit_transform(env, poses + (p1 - 1) * 12, R2, TN);
+    }
+#pragma unroll
+    for (int i = 0; i < 9; ++i) R[i] = uniform_d(R[i]);
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        T0[i] = uniform_d(T0[i]);
+        TN[i] = uniform_d(TN[i]);
+    }
+    const Cluster c = ag.clusters[cl];
+    float clo[3], chi[3];
+    {
+        float alo[3], ahi[3], blo[3], bhi[3];
+        local_box(c.c, c.e, R, T0, alo, ahi);
+        local_box(c.c, c.e, R, TN, blo, bhi);
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            clo[k] = fminf(alo[k], blo[k]);
+            chi[k] = fmaxf(ahi[k], bhi[k]);
+        }
+    }
+    // the lane's triangle rotated once (R Q, xform's products and sums before the + T)
+    const bool act = lane < c.count;
+    v3 RQ[3] = {mk(0, 0, 0), mk(0, 0, 0), mk(0, 0, 0)};
+    float tlo[3] = {0, 0, 0}, thi[3] = {0, 0, 0};
+    if (act) {
+        const double *t = ag.tris + (int64_t)(c.first + lane) * 9;
+#pragma unroll
+        for (int v = 0; v < 3; ++v) {
+            const double x = t[3 * v], y = t[3 * v + 1], z = t[3 * v + 2];
+            RQ[v] = mk(R[0] * x + R[1] * y + R[2] * z, R[3] * x + R[4] * y + R[5] * z, R[6] * x + R[7] * y + R[8] * z);
+        }
+        // swept box of the triangle: its boxes at both ends (translation only in between)
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            const double a0 = (&RQ[0].x)[k], a1 = (&RQ[1].x)[k], a2 = (&RQ[2].x)[k];
+            const double mn = dmin(a0, dmin(a1, a2)), mx = dmax(a0, dmax(a1, a2));
+            tlo[k] = widen_lo(dmin(mn + T0[k], mn + TN[k]));
+            thi[k] = widen_hi(dmax(mx + T0[k], mx + TN[k]));
+        }
+    }
+    int sp = 0;
+    int lev = env.n_levels - 1;
+    int32_t first = env.lev_off[lev];
+    int32_t count = env.lev_off[lev + 1] - first;
+    for (;;) {
+        bool keep = false;
+        int32_t cf = 0, cc = 0;
+        if (lane < count) {
+            const Item it = env.items[first + lane];
+            keep = box_overlap(clo, chi, it.lo, it.hi);
+            cf = it.first;
+            cc = it.count;
+        }
+        cnt.items += (uint32_t)count;
+        uint64_t m = __ballot(keep);
+        if (lev == 0) {
+            // env triangles: lanes whose swept box meets one run its poses
+            while (m) {
+                const int j = __ffsll((unsigned long long)m) - 1;
+                m &= m - 1;
+                const int32_t t = first + j;
+                const Item ti = env.items[t];  // level 0: item index = triangle index
+                const bool near = act && box_overlap(tlo, thi, ti.lo, ti.hi);
+                if (!__ballot(near)) continue;
+                if (load_flag(verdict + e)) return;
+                const EnvTri &E = env.tris[t];
+                bool hit = false;
+                if (near) {
+                    for (int64_t p = p0; p < p1 && !hit; ++p) {
+                        // T of fcl::relativeTransform: R1^T (T2 - T1), as relative_transform()
+                        const double *pt = poses + p * 12 + 9;
+                        const double d0 = pt[0] - env.tf[9], d1 = pt[1] - env.tf[10], d2 = pt[2] - env.tf[11];
+                        double Tp[3];
+#pragma unroll
+                        for (int i = 0; i < 3; ++i)
+                            Tp[i] = env.tf[0 * 3 + i] * d0 + env.tf[1 * 3 + i] * d1 + env.tf[2 * 3 + i] * d2;
+                        const v3 Q1 = mk(RQ[0].x + Tp[0], RQ[0].y + Tp[1], RQ[0].z + Tp[2]);
+                        const v3 Q2 = mk(RQ[1].x + Tp[0], RQ[1].y + Tp[1], RQ[1].z + Tp[2]);
+                        const v3 Q3 = mk(RQ[2].x + Tp[0], RQ[2].y + Tp[1], RQ[2].z + Tp[2]);
+                        ++cnt.pair_poses;
+                        if (!tri_gate(E.lo, E.hi, Q1, Q2, Q3)) continue;
+                        ++cnt.sat;
+                        hit = tri_intersect(E, Q1, Q2, Q3);
+                    }
+                }
+                if (__ballot(hit)) {
+                    if (lane == 0) __hip_atomic_store(verdict + e, (uint8_t)1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    return;
+                }
+            }
+        } else if (m) {
+            // enter the first overlapping child, push the rest
+            const int j = __ffsll((unsigned long long)m) - 1;
+            const uint64_t rest = m & (m - 1);
+            if (keep && lane != j) {
+                const int pos = sp + (int)__popcll(rest & ((1ull << lane) - 1));
+                stk[pos] = ((lev - 1) << 27) | cf;  // the child range: level, first
+                stk[kSweepStack + pos] = cc;
+            }
+            sp += (int)__popcll(rest);
+            first = __builtin_amdgcn_readfirstlane(__shfl(cf, j));
+            count = __builtin_amdgcn_readfirstlane(__shfl(cc, j));
+            lev -= 1;
+            continue;
+        }
+        if (sp == 0) return;
+        --sp;
+        const int32_t code = __builtin_amdgcn_readfirstlane(stk[sp]);
+        count = __builtin_amdgcn_readfirstlane(stk[kSweepStack + sp]);
+        lev = code >> 27;
+        first = code & ((1 << 27) - 1);
+    }
+}
+
+__global__ __launch_bounds__(kSweepWaves * 64) void k_sweep(EnvDev env, const AgentDev *__restrict__ link,
+                                                            const double *__restrict__ poses,
+                                                            const int64_t *__restrict__ poff, int64_t E,
+                                                            int32_t n_clusters, uint8_t *verdict,
+                                                            unsigned long long *stats) {
+    __shared__ int32_t s_stk[kSweepWaves][2 * kSweepStack];
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    const int64_t g = (int64_t)blockIdx.x * kSweepWaves + wave;
+    const int64_t e = g / n_clusters;
+    const int32_t cl = (int32_t)(g % n_clusters);
+    SweepCounters cnt;
+    if (e < E) sweep_wave(env, link[0], poses, poff, e, cl, verdict, lane, s_stk[wave], cnt);
+    if (stats && lane == 0 && e < E) {
+        atomicAdd(stats + 0, (unsigned long long)cnt.waves);
+        atomicAdd(stats + 1, (unsigned long long)cnt.items);
+        atomicAdd(stats + 2, (unsigned long long)cnt.pair_poses);
+        atomicAdd(stats + 3, (unsigned long long)cnt.sat);
+    }
+}
+
+void launch_collide_sweep(const EnvDev &env, const AgentDev *d_link, int32_t n_clusters, const double *poses,
+                          const int64_t *poff, int64_t E, uint8_t *verdict, unsigned long long *stats,
+                          hipStream_t stream) {
+    if (E <= 0 || env.n_tris <= 0) return;
+    if (env.n_tris >= (1 << 27)) throw Error{5, "env too large for the sweep path"};
+    const int64_t waves = E * n_clusters;
+    const int64_t blocks = (waves + kSweepWaves - 1) / kSweepWaves;
+    if (blocks > 0x7fffffff) throw Error{5, "sweep batch too large"};
+    hipLaunchKernelGGL(k_sweep, dim3((unsigned)blocks), dim3(kSweepWaves * 64), 0, stream, env, d_link, poses, poff, E,
+                       n_clusters, verdict, stats);
+    hip_check(hipGetLastError(), "k_sweep launch");
+}
+
+}  // namespace mpt

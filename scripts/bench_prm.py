@@ -1,0 +1,88 @@
+"""BASELINE config 4: PRM construction with radius neighbours over a ~200k-triangle env.
+
+Workload: synthetic env = 25 x 25 copies of the model.dae room (197 500 triangles; the
+reference's apartment.dae is missing), blimp agent (all 1355 triangles of blimp.3ds),
+N milestones ~ U(Blimp::getStateVarRanges) (x, y, z in [-100, 100]), radius chosen for a mean
+of ~10 neighbours per milestone (counting both directions), cc_dt 0.1 (blimp.inst).  One call
+of mpt_prm_connect: point-tree radius search, edge poses, batched collision, components.
+Prints one JSON line: milestones/s, edges checked/s, per-stage device ms, and the oracle's
+single-core rate on a bounded sample of the same roadmap (its first milestones).
+
+  python scripts/bench_prm.py [--n 100000] [--reps 3]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--n", type=int, default=100_000)
+    ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--degree", type=float, default=10.0)
+    ap.add_argument("--rooms", type=int, default=25)
+    ap.add_argument("--cpu-n", type=int, default=3000)
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--collide", default="split", choices=["split", "fused"])
+    a = ap.parse_args()
+
+    import motionplanningtoolkit_amd as mpt
+    from motionplanningtoolkit_amd import scenes
+
+    mpt.init(0)
+    mpt.set_collide_mode(a.collide)
+    sc = scenes.blimp_scenario("all")
+    env_t = scenes.rooms_env(a.rooms, a.rooms)
+    env, ag = mpt.Environment(env_t, sc.env_tf), mpt.AgentMesh(sc.agent_tris)
+    rng = np.random.default_rng(0)
+    st = rng.uniform(sc.ranges[:, 0], sc.ranges[:, 1], size=(a.n, sc.dim))
+    vol = float(np.prod(sc.ranges[:3, 1] - sc.ranges[:3, 0]))
+    r = (a.degree * vol / (a.n * 4.0 / 3.0 * math.pi)) ** (1.0 / 3.0)
+    r2 = r * r
+    mpt.prm_connect(env, ag, 1, st[: min(a.n, 2000)], r2, sc.cc_dt)  # warm-up (allocations)
+    walls, res = [], None
+    for _ in range(a.reps):
+        t0 = time.perf_counter()
+        res = mpt.prm_connect(env, ag, 1, st, r2, sc.cc_dt)
+        walls.append(time.perf_counter() - t0)
+    E = len(res["edges"])
+    ms = res["ms"]
+    wall = min(walls)
+    out = {
+        "metric": "PRM roadmap construction (radius neighbours + edge collision checks), config 4",
+        "value": a.n / wall, "unit": "milestones/s", "edges_checked_per_s": E / wall,
+        "wall_ms": 1e3 * wall, "device_ms": ms, "dtype": "f64", "data": "synthetic milestones",
+        "config": {"workload": f"blimp ({len(sc.agent_tris)} tris) PRM in {a.rooms}x{a.rooms} rooms "
+                               f"({len(env_t)} tris)", "milestones": a.n, "radius": r, "edges": E,
+                   "free_fraction": float(1.0 - res["verdict"].mean()) if E else None,
+                   "components": int(len(np.unique(res["comp"]))), "collide_mode": a.collide},
+    }
+    if not a.no_cpu:
+        sys.path.insert(0, os.path.join(REPO, "oracle"))
+        import oracle as orc
+
+        k = min(a.cpu_n, a.n)
+        bvh = orc.BVH(env_t)
+        t0 = time.perf_counter()
+        e_ref, v_ref, _ = orc.prm_radius(bvh, sc.env_tf, sc.agent_tris, st[:k], r2, sc.cc_dt, nthreads=1)
+        dt = time.perf_counter() - t0
+        sub = mpt.prm_connect(env, ag, 1, st[:k], r2, sc.cc_dt)
+        out["cpu_baseline"] = {"value": len(e_ref) / dt, "unit": "edges checked/s", "cores": 1, "kind": "port",
+                               "sample": f"the roadmap of the first {k} milestones ({len(e_ref)} edges), "
+                                         f"oracle/mpt_oracle.c orc_prm_radius, {dt:.1f} s"}
+        out["parity_sample"] = bool(np.array_equal(sub["edges"], e_ref) and np.array_equal(sub["verdict"], v_ref))
+    print(json.dumps(out))
+
+
+if __name__ == "__main__":
+    main()
