@@ -84,6 +84,13 @@ mpt_status mpt_transform_from_location(const double loc7[7], double tf12[12]);
 mpt_status mpt_collide_batch(const mpt_env *env, const mpt_agent *const *links, int32_t L,
                              const double *poses, const int64_t *edge_pose_offsets, int64_t E,
                              uint8_t *verdict_out, void *stream);
+/* MeshHandler::isInCollision(env, agent, poses, checkSelfCollision) (meshhandler.hpp:187-243):
+ * as mpt_collide_batch, and with check_self != 0 an edge is also in collision when two
+ * distinct links of one of its poses touch (the self-collision branch, :205-219; each link
+ * pair (j < k) is tested with link j as FCL's o1). */
+mpt_status mpt_collide_batch_ex(const mpt_env *env, const mpt_agent *const *links, int32_t L, const double *poses,
+                                const int64_t *edge_pose_offsets, int64_t E, int32_t check_self,
+                                uint8_t *verdict_out, void *stream);
 /* Device-pointer variant: poses, edge_pose_offsets, verdict_out in device memory;
  * total_poses = edge_pose_offsets[E] (passed so no device->host read is needed). */
 mpt_status mpt_collide_batch_device(const mpt_env *env, const mpt_agent *const *links, int32_t L,

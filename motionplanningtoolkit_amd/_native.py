@@ -39,6 +39,7 @@ SIGNATURES = {
     "mpt_transform_from_location": (I32, [P, P]),
     "mpt_collide_batch": (I32, [P, P, I32, P, P, I64, P, P]),
     "mpt_collide_batch_device": (I32, [P, P, I32, P, P, I64, I64, P, P]),
+    "mpt_collide_batch_ex": (I32, [P, P, I32, P, P, I64, I32, P, P]),
     "mpt_set_stats": (I32, [I32]),
     "mpt_set_collide_mode": (I32, [I32]),
     "mpt_distance_batch": (I32, [P, P, I32, P, P, I64, P, P]),

@@ -111,15 +111,17 @@ def _links(links: Sequence[AgentMesh]):
     return arr
 
 
-def collide_batch(env: Environment, links: Sequence[AgentMesh], poses, edge_offsets, stream=None) -> np.ndarray:
-    """Verdicts (1 = collision) for E edges; poses [sum P][L][12], edge_offsets [E+1]."""
+def collide_batch(env: Environment, links: Sequence[AgentMesh], poses, edge_offsets, stream=None,
+                  check_self: bool = False) -> np.ndarray:
+    """Verdicts (1 = collision) for E edges; poses [sum P][L][12], edge_offsets [E+1].
+    check_self: also link-vs-link contacts within a pose (isInCollision's checkSelfCollision)."""
     L = len(links)
     poses = _f64(poses).reshape(-1, L, 12)
     off = np.ascontiguousarray(edge_offsets, dtype=np.int64)
     E = off.shape[0] - 1
     out = np.zeros(max(E, 0), np.uint8)
-    check(lib().mpt_collide_batch(env.handle, _links(links), L, _p(poses), _p(off), E, _p(out), _stream(stream)),
-          "mpt_collide_batch")
+    check(lib().mpt_collide_batch_ex(env.handle, _links(links), L, _p(poses), _p(off), E, int(check_self), _p(out),
+                                     _stream(stream)), "mpt_collide_batch_ex")
     return out
 
 

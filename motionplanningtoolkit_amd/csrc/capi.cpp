@@ -82,6 +82,7 @@ struct mpt_env {
 
 struct mpt_agent {
     AgentDev dev{};
+    EnvTri *d_etris = nullptr;
     double *d_tris = nullptr;
     Cluster *d_clusters = nullptr;
     int64_t n_tris = 0;
@@ -436,7 +437,13 @@ extern "C" mpt_status mpt_agent_create(const double *tris, int64_t n_tris, mpt_a
                           "H2D");
                 hip_check(hipMemcpy(ag->d_clusters, cl.data(), sizeof(Cluster) * cl.size(), hipMemcpyHostToDevice),
                           "H2D");
+                // the same triangles as P-side records, for link-vs-link (self) collision
+                std::vector<EnvTri> rec((size_t)n_tris);
+                for (int64_t i = 0; i < n_tris; ++i) make_env_tri(&sorted[9 * i], rec[i]);
+                hip_check(hipMalloc(&ag->d_etris, sizeof(EnvTri) * n_tris), "hipMalloc agent records");
+                hip_check(hipMemcpy(ag->d_etris, rec.data(), sizeof(EnvTri) * n_tris, hipMemcpyHostToDevice), "H2D");
             }
+            ag->dev.etris = ag->d_etris;
             ag->n_tris = n_tris;
             ag->dev.tris = ag->d_tris;
             ag->dev.clusters = ag->d_clusters;
@@ -467,6 +474,7 @@ extern "C" mpt_status mpt_agent_destroy(mpt_agent *ag) {
         if (!ag) return;
         if (ag->d_tris) (void)hipFree(ag->d_tris);
         if (ag->d_clusters) (void)hipFree(ag->d_clusters);
+        if (ag->d_etris) (void)hipFree(ag->d_etris);
         delete ag;
     });
 }
@@ -538,6 +546,12 @@ static void check_links(const mpt_env *env, const mpt_agent *const *links, int32
 extern "C" mpt_status mpt_collide_batch(const mpt_env *env, const mpt_agent *const *links, int32_t L,
                                         const double *poses, const int64_t *edge_pose_offsets, int64_t E,
                                         uint8_t *verdict_out, void *stream_) {
+    return mpt_collide_batch_ex(env, links, L, poses, edge_pose_offsets, E, 0, verdict_out, stream_);
+}
+
+extern "C" mpt_status mpt_collide_batch_ex(const mpt_env *env, const mpt_agent *const *links, int32_t L,
+                                           const double *poses, const int64_t *edge_pose_offsets, int64_t E,
+                                           int32_t check_self, uint8_t *verdict_out, void *stream_) {
     return guarded([&] {
         check_links(env, links, L);
         require(E >= 0 && (E == 0 || (edge_pose_offsets && verdict_out)), "bad edge arrays");
@@ -560,6 +574,11 @@ extern "C" mpt_status mpt_collide_batch(const mpt_env *env, const mpt_agent *con
             hip_check(hipMemcpyAsync(d_pe, pe.data(), sizeof(int32_t) * P, hipMemcpyHostToDevice, stream), "pe H2D");
         }
         collide_common(env, links, L, d_poses, d_pe, P, E, d_v, stream);
+        if (check_self && L > 1) {  // after the env pass, which zeroed the verdicts: OR
+            int32_t mc = 1;
+            const AgentDev *d_links = link_table(links, L, &mc);
+            launch_self_collide(d_links, L, d_poses, d_pe, P, d_v, stream);
+        }
         hip_check(hipMemcpyAsync(verdict_out, d_v, (size_t)E, hipMemcpyDeviceToHost, stream), "verdict D2H");
         hip_check(hipStreamSynchronize(stream), "collide sync");
     });

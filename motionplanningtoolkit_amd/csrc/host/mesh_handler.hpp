@@ -2,7 +2,7 @@
 // MeshHandler (utilities/meshhandler.hpp:16-243) and fcl_helpers::parseTransform
 // (utilities/fcl_helpers.hpp:16-25).  The FCL BVHModel<OBBRSS> + DynamicAABBTree managers
 // are replaced by device-resident meshes behind the C ABI (include/mpt.h); isInCollision
-// becomes one mpt_collide_batch call for the whole pose list.
+// becomes one mpt_collide_batch_ex call for the whole pose list (checkSelfCollision included).
 #pragma once
 #include <array>
 #include <memory>
@@ -102,8 +102,6 @@ public:
     static bool isInCollision(const StaticEnvironmentMeshHandler &environment,
                               const std::vector<const SimpleAgentMeshHandler *> &agent,
                               const std::vector<std::vector<Transform3f>> &poses, bool checkSelfCollision = false) {
-        if (checkSelfCollision)
-            throw std::runtime_error("self-collision checking is not implemented on the device yet");
         const int32_t L = (int32_t)agent.size();
         if (L == 0 || poses.empty()) return false;
         std::vector<double> buf;
@@ -123,8 +121,9 @@ public:
         for (int32_t l = 0; l < L; ++l) links[l] = agent[l]->handle();
         const int64_t off[2] = {0, P};
         uint8_t verdict = 0;
-        mpt_throw(mpt_collide_batch(environment.handle(), links.data(), L, buf.data(), off, 1, &verdict, nullptr),
-                  "mpt_collide_batch");
+        mpt_throw(mpt_collide_batch_ex(environment.handle(), links.data(), L, buf.data(), off, 1,
+                                       checkSelfCollision ? 1 : 0, &verdict, nullptr),
+                  "mpt_collide_batch_ex");
         return verdict != 0;
     }
 
@@ -132,7 +131,8 @@ public:
     // returns one verdict per edge (1 = contact).
     static std::vector<uint8_t> collideEdges(const StaticEnvironmentMeshHandler &environment,
                                              const std::vector<const SimpleAgentMeshHandler *> &agent,
-                                             const std::vector<std::vector<std::vector<Transform3f>>> &edges) {
+                                             const std::vector<std::vector<std::vector<Transform3f>>> &edges,
+                                             bool checkSelfCollision = false) {
         const int32_t L = (int32_t)agent.size();
         std::vector<uint8_t> verdict(edges.size(), 0);
         if (L == 0 || edges.empty()) return verdict;
@@ -153,9 +153,9 @@ public:
         }
         std::vector<const mpt_agent *> links(L);
         for (int32_t l = 0; l < L; ++l) links[l] = agent[l]->handle();
-        mpt_throw(mpt_collide_batch(environment.handle(), links.data(), L, buf.data(), off.data(),
-                                    (int64_t)edges.size(), verdict.data(), nullptr),
-                  "mpt_collide_batch");
+        mpt_throw(mpt_collide_batch_ex(environment.handle(), links.data(), L, buf.data(), off.data(),
+                                       (int64_t)edges.size(), checkSelfCollision ? 1 : 0, verdict.data(), nullptr),
+                  "mpt_collide_batch_ex");
         return verdict;
     }
 };

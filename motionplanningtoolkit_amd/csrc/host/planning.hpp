@@ -44,11 +44,12 @@ public:
     }
 
     // safeEdge over many edges in one device call (the batched form PRM construction uses).
-    std::vector<bool> safeEdges(const Agent &agent, const std::vector<Edge> &edges, double dt) const {
+    std::vector<bool> safeEdges(const Agent &agent, const std::vector<Edge> &edges, double dt,
+                                bool checkSelfCollision = false) const {
         std::vector<std::vector<std::vector<Transform3f>>> poses;
         poses.reserve(edges.size());
         for (const Edge &e : edges) poses.push_back(agent.getPoses(e, dt));
-        const std::vector<uint8_t> v = MeshHandler::collideEdges(mesh, agent.getMeshes(), poses);
+        const std::vector<uint8_t> v = MeshHandler::collideEdges(mesh, agent.getMeshes(), poses, checkSelfCollision);
         std::vector<bool> ok(v.size());
         for (size_t i = 0; i < v.size(); ++i) ok[i] = v[i] == 0;
         return ok;

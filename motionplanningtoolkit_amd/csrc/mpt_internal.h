@@ -46,6 +46,7 @@ struct AgentDev {
     int32_t n_clusters;
     int32_t n_tris;
     double bc[3], be[3];      // whole-link local box centre / half-extent
+    const EnvTri *etris;      // [T] the triangles as intersect_Triangle's P side (self-collision)
 };
 
 // Broad-phase env tree, 64 children per node so one wave tests a node's children with one
@@ -161,6 +162,11 @@ void launch_pose_edge(const int64_t *d_offsets, int64_t E, int32_t *d_pose_edge,
 void launch_collide_sweep(const EnvDev &env, const AgentDev *d_link, int32_t n_clusters, const double *poses,
                           const int64_t *poff, int64_t E, uint8_t *verdict, unsigned long long *stats,
                           hipStream_t stream);
+
+// Self-collision (self.hip, MeshHandler::isInCollision's checkSelfCollision branch): units
+// are (pose, link pair j < k); verdict[pose_edge[p]] = 1 when links j and k of pose p touch.
+void launch_self_collide(const AgentDev *d_links, int32_t L, const double *poses, const int32_t *pose_edge,
+                         int64_t n_poses, uint8_t *verdict, hipStream_t stream);
 
 // ---------------- distance (distance.hip) ----------------
 // Units are (pose, link) pairs as for collide mode A; best[E] receives the per-edge minimum

@@ -1304,3 +1304,32 @@ int64_t orc_prm_radius(const orc_bvh *env, const double env_tf[12], const double
     free(parent);
     return E;
 }
+
+/* ======================================================================
+ * Self-collision: MeshHandler::isInCollision's checkSelfCollision branch
+ * (utilities/meshhandler.hpp:205-219): every pair of distinct link objects of a pose.
+ * ====================================================================== */
+static int self_collide_pose(const double *agent_tris, const int64_t *off, int32_t L, const double *pose) {
+    for (int32_t j = 0; j < L; ++j)
+        for (int32_t k = j + 1; k < L; ++k) {
+            const double *pj = pose + 12 * j, *pk = pose + 12 * k;
+            double R[9], T[3], Qp[9];
+            orc_relative_transform(pj, pj + 9, pk, pk + 9, R, T);
+            for (int64_t b = off[k]; b < off[k + 1]; ++b) {
+                map_tri(R, T, agent_tris + 9 * b, Qp);
+                for (int64_t a = off[j]; a < off[j + 1]; ++a)
+                    if (tri_gate(agent_tris + 9 * a, Qp) && orc_tri_intersect(agent_tris + 9 * a, Qp)) return 1;
+            }
+        }
+    return 0;
+}
+
+void orc_self_collide_batch(const double *agent_tris, const int64_t *link_tri_off, int32_t L, const double *poses,
+                            const int64_t *edge_pose_offsets, int64_t E, uint8_t *verdict) {
+    for (int64_t e = 0; e < E; ++e) {
+        int hit = 0;
+        for (int64_t p = edge_pose_offsets[e]; p < edge_pose_offsets[e + 1] && !hit; ++p)
+            hit = self_collide_pose(agent_tris, link_tri_off, L, poses + 12 * L * p);
+        verdict[e] = (uint8_t)hit;
+    }
+}

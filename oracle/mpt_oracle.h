@@ -164,6 +164,12 @@ void orc_distance_batch(const double *env_tris, int64_t Te, const double env_tf[
                         const double *poses, const int64_t *edge_pose_offsets, int64_t E,
                         double *dist, int nthreads);
 
+/* Self-collision (utilities/meshhandler.hpp:205-219, checkSelfCollision): verdict[e] = 1 when
+ * two distinct links j < k of one of edge e's poses touch (link j = FCL's o1, all triangle
+ * pairs, tri_gate + intersect_Triangle).  poses [sumP][L][12]. */
+void orc_self_collide_batch(const double *agent_tris, const int64_t *link_tri_off, int32_t L, const double *poses,
+                            const int64_t *edge_pose_offsets, int64_t E, uint8_t *verdict);
+
 /* PRM roadmap with radius neighbours (config 4; prm.hpp:334-387 with kNearestWithin):
  * edges (i, j), j < i, squared L2 of the first three state variables < r2, sorted by (i, j);
  * verdict per edge over Omnidirectional::steer(key_i, key_j, 1000) + getPoses(cc_dt) with the

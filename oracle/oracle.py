@@ -70,6 +70,7 @@ def lib():
             "orc_engine_step": (I64, [I32, P, I32, P, D, D, U64, U64, I32, P, P, P, I64, P, P, I64, I64, P, P, C.c_int, C.c_int]),
             "orc_prm_build": (I64, [P, P, P, I64, P, I64, I32, I32, D, P, P, I64, P]),
             "orc_tri_distance": (D, [P, P]),
+            "orc_self_collide_batch": (None, [P, P, I32, P, P, I64, P]),
             "orc_prm_radius": (I64, [P, P, P, I64, P, I64, I32, D, D, P, P, I64, P, C.c_int]),
             "orc_distance_unit": (D, [P, I64, P, P, I64, P]),
             "orc_distance_batch": (None, [P, I64, P, P, P, I32, P, P, I64, P, C.c_int]),
@@ -135,6 +136,19 @@ def prm_radius(bvh: BVH, env_tf, agent_tris, states, r2: float, cc_dt: float, nt
     lib().orc_prm_radius(bvh.ptr, _p(_f64(env_tf)), _p(at), at.shape[0], _p(st), n, dim, r2, cc_dt, _p(edges),
                          _p(verdict), E, _p(comp), nthreads)
     return edges[:E], verdict[:E], comp[:n]
+
+
+def self_collide_batch(link_tris: list, poses, edge_offsets) -> np.ndarray:
+    """Link-vs-link verdicts per edge (checkSelfCollision branch)."""
+    agent = _f64(np.concatenate([np.asarray(t, np.float64).reshape(-1, 9) for t in link_tris]))
+    off = np.zeros(len(link_tris) + 1, np.int64)
+    off[1:] = np.cumsum([np.asarray(t).reshape(-1, 9).shape[0] for t in link_tris])
+    poses = _f64(poses)
+    eo = np.ascontiguousarray(edge_offsets, np.int64)
+    E = len(eo) - 1
+    out = np.zeros(E, np.uint8)
+    lib().orc_self_collide_batch(_p(agent), _p(off), len(link_tris), _p(poses), _p(eo), E, _p(out))
+    return out
 
 
 def tri_distance(S, T) -> float:

@@ -176,3 +176,62 @@ def test_empty_and_degenerate(mpt_gpu, oracle):
     # an empty environment never collides
     empty = mpt_gpu.Environment(np.zeros((0, 9)))
     assert mpt_gpu.collide_batch(empty, [ag], pose([0, 0, 0]).reshape(1, 1, 12), np.array([0, 1])).tolist() == [0]
+
+
+def test_self_collision_known_answers(mpt_gpu, oracle):
+    """checkSelfCollision (meshhandler.hpp:205-219): two box links of one pose, env far away."""
+    box = scenes.read_obj(scenes.mesh_path("agent_unit_box"), "last")
+    env_tf = pose([100.0, 0, 0])
+    env = mpt_gpu.Environment(box, env_tf)
+    ags = [mpt_gpu.AgentMesh(box), mpt_gpu.AgentMesh(box)]
+    ts = [1.5, 0.9, 1.0, 1.01]
+    poses = np.array([[pose([0, 0, 0]), pose([t, 0, 0])] for t in ts])
+    off = np.arange(len(ts) + 1)
+    got = mpt_gpu.collide_batch(env, ags, poses, off, check_self=True)
+    assert got.tolist() == [0, 1, 1, 0]
+    assert mpt_gpu.collide_batch(env, ags, poses, off).tolist() == [0, 0, 0, 0]
+    assert np.array_equal(got, oracle.self_collide_batch([box, box], poses, off))
+
+
+def test_self_collision_snake(mpt_gpu, oracle):
+    """Snake poses (11 box links, snake_trailers.hpp:411-459 verbatim) from random states and
+    controls in the corridor: verdict = env contact or link-vs-link contact."""
+    sc = scenes.snake_scenario("corridor")
+    rng = np.random.default_rng(17)
+    L = int(sc.prm[0]) + 1
+    E = 400
+    chunks, off = [], [0]
+    for _ in range(E):
+        st = rng.uniform(sc.ranges[:, 0], sc.ranges[:, 1])
+        st[0] = rng.uniform(-4, 4)
+        aw = [rng.uniform(-0.1, 1), rng.uniform(-math.pi / 18, math.pi / 18)]
+        p = oracle.snake_get_poses(sc.prm, st, aw, sc.steer_dt, sc.cc_dt)
+        chunks.append(p)
+        off.append(off[-1] + len(p))
+    poses = np.concatenate(chunks)
+    links = [sc.agent_tris] * L
+    env = mpt_gpu.Environment(sc.env_tris, sc.env_tf)
+    ags = [mpt_gpu.AgentMesh(sc.agent_tris)] * L
+    got = mpt_gpu.collide_batch(env, ags, poses, off, check_self=True)
+    ref = oracle.collide_batch(sc.env_tris, sc.env_tf, links, poses, off) | oracle.self_collide_batch(links, poses, off)
+    assert np.array_equal(got, ref), np.nonzero(got != ref)
+    # the reference poses every trailer at the same (-(Lt + Lh), Y, 0) (snake_trailers.hpp:434-456,
+    # not chained), so its trailers always overlap: with checkSelfCollision every snake edge collides
+    assert oracle.self_collide_batch(links, poses, off).all()
+
+
+def test_self_collision_random_chains(mpt_gpu, oracle):
+    """Four links (box, blimp submesh, box, box) at random relative poses: both outcomes."""
+    box = scenes.read_obj(scenes.mesh_path("agent_unit_box"), "last")
+    blimp = scenes.read_obj(scenes.mesh_path("agent_blimp"), "last")
+    links = [box, blimp, box, box]
+    rng = np.random.default_rng(23)
+    E, P = 300, 3
+    poses = np.array([[pose(rng.uniform(-4, 4, 3), random_rot(rng)) for _ in links] for _ in range(E * P)])
+    off = np.arange(0, E * P + 1, P)
+    env_t = scenes.read_obj(scenes.mesh_path("env_unit_box"))
+    env = mpt_gpu.Environment(env_t, pose([500.0, 0, 0]))
+    got = mpt_gpu.collide_batch(env, [mpt_gpu.AgentMesh(t) for t in links], poses, off, check_self=True)
+    ref = oracle.self_collide_batch(links, poses, off)
+    assert np.array_equal(got, ref), np.nonzero(got != ref)
+    assert 0 < ref.sum() < E

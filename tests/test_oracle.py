@@ -400,3 +400,16 @@ def test_oracle_prm_radius_is_consistent(oracle):
     for c in np.unique(lab):
         m = np.flatnonzero(lab == c)
         assert np.all(comp[m] == m.min())
+
+
+def test_oracle_self_collision_known_answers(oracle, unit_box):
+    """checkSelfCollision restatement: two unit boxes of one pose, touching counts."""
+    I = np.eye(3).ravel()
+    R = oracle.quat_to_rot([math.cos(math.pi / 8), 0, 0, math.sin(math.pi / 8)])  # 45 deg about z
+    poses = np.array([[np.r_[I, 0, 0, 0], np.r_[I, t, 0, 0]] for t in (0.5, 1.0, 1.000001, 3.0)]
+                     + [[np.r_[I, 0, 0, 0], np.r_[R, 1.2, 0, 0]], [np.r_[I, 0, 0, 0], np.r_[R, 1.22, 0, 0]]])
+    got = oracle.self_collide_batch([unit_box, unit_box], poses, np.arange(len(poses) + 1))
+    assert got.tolist() == [1, 1, 0, 0, 1, 0]
+    # three links: only the (0, 2) pair touches
+    p3 = np.array([[np.r_[I, 0, 0, 0], np.r_[I, 0, 5, 0], np.r_[I, 0.9, 0, 0]]])
+    assert oracle.self_collide_batch([unit_box] * 3, p3, [0, 1]).tolist() == [1]
