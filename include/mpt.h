@@ -136,6 +136,15 @@ mpt_status mpt_prm_connect(const mpt_env *env, const mpt_agent *agent, int32_t a
                            int64_t n, int32_t dim, double radius2, double cc_dt, int64_t cap, int32_t *edges,
                            uint8_t *verdict, int64_t *n_edges, int32_t *comp, float ms[4]);
 
+/* ---- workspace discretisation: PRMLite::generateEdges (discretizations/workspace/prmlite.hpp:128-164)
+ * All vertex pairs i < j, pair index e = row-major over i < j (E = V(V-1)/2).  vertices [V][12] =
+ * R | T with R = Quaternion3f::toRotation of the vertex's quaternion.  The edge's poses are
+ * PRMLite::interpolate (:181-203): steps = (unsigned)(|t_i - t_j| / step), each pose
+ * (t_j - t_i) / steps further than the previous one (accumulated), rotation of vertex i; an
+ * edge without poses is safe.  collides[e] = 1 when a pose is in collision (edge dropped). */
+mpt_status mpt_prmlite_edges(const mpt_env *env, const mpt_agent *agent, const double *vertices, int64_t V,
+                             double step, uint8_t *collides, void *stream);
+
 /* ---- NN: FLANN_KDTreeWrapper ---- */
 mpt_status mpt_nn_create(int32_t dim, int64_t capacity, mpt_nn **out);
 mpt_status mpt_nn_destroy(mpt_nn *nn);

@@ -39,6 +39,19 @@ mpt_status mpt_host_prm(const char *inst_path, const double *states, int64_t n, 
                         int64_t cap, int32_t *edges, double *costs, int64_t *n_edges, int64_t comp_cap,
                         int32_t *comp, int64_t *n_milestones, int32_t *solved, double *cost);
 
+/* GridDiscretization (discretizations/workspace/griddiscretization.hpp:6-189) over the .inst's
+ * workspace and agent: a cell is free when none of getRepresentivePosesForLocation(centre)
+ * collides.  free_out[cells], centers[cells][3] written up to cap. */
+mpt_status mpt_host_grid_discretization(const char *inst_path, const double sizes[3], int64_t cap, uint8_t *free_out,
+                                        double *centers, int64_t *n_cells);
+
+/* PRMLite (discretizations/workspace/prmlite.hpp:8-263): n_vertices collision-free random
+ * vertices (the reference's RNG stream), then every pair connected unless an interpolated pose
+ * collides (mpt_prmlite_edges).  verts[n_vertices][12] = R | T; edges[E][2] = (i, j), i < j,
+ * sorted; written up to cap. */
+mpt_status mpt_host_prmlite(const char *inst_path, int32_t n_vertices, double step, double *verts, int64_t cap,
+                            int32_t *edges, int64_t *n_edges);
+
 #ifdef __cplusplus
 }
 #endif

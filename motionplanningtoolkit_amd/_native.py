@@ -44,6 +44,7 @@ SIGNATURES = {
     "mpt_set_collide_mode": (I32, [I32]),
     "mpt_distance_batch": (I32, [P, P, I32, P, P, I64, P, P]),
     "mpt_prm_connect": (I32, [P, P, I32, P, I64, I32, D, D, I64, P, P, P, P, P]),
+    "mpt_prmlite_edges": (I32, [P, P, P, I64, D, P, P]),
     "mpt_distance_batch_device": (I32, [P, P, I32, P, P, I64, I64, P, P]),
     "mpt_last_collide_stats": (I32, [P]),
     "mpt_nn_create": (I32, [I32, I64, P]),
@@ -75,6 +76,8 @@ SIGNATURES = {
     "mpt_host_load_mesh": (I32, [C.c_char_p, I32, P, I64, P, P]),
     "mpt_host_rrt_inst": (I32, [C.c_char_p, I32, I64, P, P, P, P, P]),
     "mpt_host_prm": (I32, [C.c_char_p, P, I64, I32, I32, I64, P, P, P, I64, P, P, P, P]),
+    "mpt_host_grid_discretization": (I32, [C.c_char_p, P, I64, P, P, P]),
+    "mpt_host_prmlite": (I32, [C.c_char_p, I32, D, P, I64, P, P]),
 }
 
 

@@ -172,6 +172,16 @@ def prm_connect(env: Environment, agent: AgentMesh, kind: int, states, radius2: 
             "ms": dict(zip(["neighbours", "poses", "collision", "total"], ms.tolist()))}
 
 
+def prmlite_edges(env: Environment, agent: AgentMesh, vertices, step: float = 0.1) -> np.ndarray:
+    """PRMLite::generateEdges on the device: collides [V(V-1)/2] over the pairs i < j (row-major)
+    of vertices [V][12] (R | T)."""
+    v = _f64(vertices).reshape(-1, 12)
+    V = v.shape[0]
+    out = np.zeros(max(V * (V - 1) // 2, 0), np.uint8)
+    check(lib().mpt_prmlite_edges(env.handle, agent.handle, _p(v), V, step, _p(out), None), "mpt_prmlite_edges")
+    return out
+
+
 COLLIDE_MODES = {"split": 0, "fused": 1}
 
 
@@ -374,6 +384,30 @@ def prm(path: str, states=None, batch: int = 1, max_queries: int = 50):
                              ccap, _p(comp), C.byref(nm), C.byref(solved), C.byref(cost)), "mpt_host_prm", host=True)
     return {"edges": edges[: ne.value], "costs": costs[: ne.value], "comp": comp[: nm.value],
             "solved": bool(solved.value), "cost": cost.value}
+
+
+def grid_discretization(path: str, sizes) -> tuple:
+    """GridDiscretization of the .inst's workspace: (free [cells] bool, centers [cells][3])."""
+    sz = _f64(sizes)
+    n = C.c_int64()
+    check(lib().mpt_host_grid_discretization(path.encode(), _p(sz), 0, None, None, C.byref(n)),
+          "mpt_host_grid_discretization", host=True)
+    free = np.zeros(n.value, np.uint8)
+    centers = np.zeros((n.value, 3))
+    check(lib().mpt_host_grid_discretization(path.encode(), _p(sz), n.value, _p(free), _p(centers), C.byref(n)),
+          "mpt_host_grid_discretization", host=True)
+    return free.astype(bool), centers
+
+
+def prmlite(path: str, n_vertices: int, step: float = 0.1) -> tuple:
+    """PRMLite over the .inst's workspace and agent: (vertices [V][12], edges [E][2] i < j)."""
+    verts = np.zeros((n_vertices, 12))
+    cap = max(n_vertices * (n_vertices - 1) // 2, 1)
+    edges = np.zeros((cap, 2), np.int32)
+    ne = C.c_int64()
+    check(lib().mpt_host_prmlite(path.encode(), n_vertices, step, _p(verts), cap, _p(edges), C.byref(ne)),
+          "mpt_host_prmlite", host=True)
+    return verts, edges[: ne.value]
 
 
 def rrt_inst(path: str, iterations_at_a_time: int, cap: int = 1 << 16):

@@ -599,6 +599,30 @@ extern "C" mpt_status mpt_collide_batch_device(const mpt_env *env, const mpt_age
     });
 }
 
+// ---------------------------------------------------------------- PRMLite edges
+extern "C" mpt_status mpt_prmlite_edges(const mpt_env *env, const mpt_agent *agent, const double *vertices, int64_t V,
+                                        double step, uint8_t *collides, void *stream_) {
+    return guarded([&] {
+        require(env && agent, "null handle");
+        require(V >= 0 && (V == 0 || vertices), "bad vertices");
+        require(step > 0, "step must be > 0");
+        const int64_t E = V * (V - 1) / 2;
+        if (E == 0) return;
+        require(collides != nullptr, "null output");
+        hipStream_t stream = (hipStream_t)stream_;
+        int32_t mc = 1;
+        const mpt_agent *links[1] = {agent};
+        const AgentDev *d_link = link_table(links, 1, &mc);
+        auto *d_v = (double *)g_ws.poses.get(sizeof(double) * 12 * V);
+        auto *d_hit = (uint8_t *)g_ws.verdict.get((size_t)E);
+        hip_check(hipMemcpyAsync(d_v, vertices, sizeof(double) * 12 * V, hipMemcpyHostToDevice, stream), "verts H2D");
+        hip_check(hipMemsetAsync(d_hit, 0, (size_t)E, stream), "memset");
+        launch_prmlite_edges(env->dev, d_link, mc, d_v, V, step, d_hit, nullptr, stream);
+        hip_check(hipMemcpyAsync(collides, d_hit, (size_t)E, hipMemcpyDeviceToHost, stream), "D2H");
+        hip_check(hipStreamSynchronize(stream), "sync");
+    });
+}
+
 // ---------------------------------------------------------------- distance
 static void distance_common(const mpt_env *env, const mpt_agent *const *links, int32_t L, const double *d_poses,
                             const int32_t *d_pose_edge, int64_t total_poses, int64_t E, double *d_dist,

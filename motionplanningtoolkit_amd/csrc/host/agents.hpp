@@ -24,6 +24,20 @@
 namespace mpt_host {
 
 typedef std::vector<std::pair<double, double>> WorkspaceBounds;
+
+// getRepresentivePosesForLocation of the blimp and the snake (agents/blimp.hpp:194-217,
+// snake_trailers.hpp:220-244): 4 yaw rotations i * pi/8 at loc, rotation(0,0) = cos,
+// (0,1) = sin, (1,0) = -sin, (1,1) = cos; one single-link pose each.
+inline std::vector<std::vector<Transform3f>> rotated_location_poses(const std::vector<double> &loc) {
+    std::vector<std::vector<Transform3f>> ret;
+    const unsigned rotations = 4;
+    const double increment = M_PI / ((double)rotations * 2.);
+    for (unsigned i = 0; i < rotations; ++i) {
+        const double c = std::cos((double)i * increment), s = std::sin((double)i * increment);
+        ret.push_back({Transform3f({{c, s, 0, -s, c, 0, 0, 0, 1}}, {{loc[0], loc[1], loc[2]}})});
+    }
+    return ret;
+}
 typedef std::vector<std::pair<double, double>> StateVarRanges;
 typedef std::vector<double> StateVars;
 
@@ -122,6 +136,11 @@ public:
     }
 
     std::vector<const SimpleAgentMeshHandler *> getMeshes() const { return {&mesh}; }
+
+    // agents/omnidirectional.hpp:191-200: one pose, translation only
+    std::vector<std::vector<Transform3f>> getRepresentivePosesForLocation(const std::vector<double> &loc) const {
+        return {{Transform3f({{loc[0], loc[1], loc[2]}})}};
+    }
 
     std::vector<std::vector<Transform3f>> getPoses(const Edge &edge, double dt) const {
         std::vector<std::vector<Transform3f>> ret;
@@ -224,6 +243,11 @@ public:
     }
 
     std::vector<const SimpleAgentMeshHandler *> getMeshes() const { return {&mesh}; }
+
+    // agents/blimp.hpp:194-217 returns the 4 transforms as one list; each is a pose here
+    std::vector<std::vector<Transform3f>> getRepresentivePosesForLocation(const std::vector<double> &loc) const {
+        return rotated_location_poses(loc);
+    }
 
     std::vector<std::vector<Transform3f>> getPoses(const Edge &edge, double dt) const {
         std::vector<std::vector<Transform3f>> ret;
@@ -358,6 +382,11 @@ public:
 
     std::vector<const SimpleAgentMeshHandler *> getMeshes() const {
         return std::vector<const SimpleAgentMeshHandler *>(trailerCount + 1, &mesh);
+    }
+
+    // snake_trailers.hpp:220-244: 4 poses of one transform (the head link)
+    std::vector<std::vector<Transform3f>> getRepresentivePosesForLocation(const std::vector<double> &loc) const {
+        return rotated_location_poses(loc);
     }
 
     std::vector<std::vector<Transform3f>> getPoses(const Edge &edge, double dt) const {

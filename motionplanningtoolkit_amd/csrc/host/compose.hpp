@@ -9,6 +9,7 @@
 
 #include "agents.hpp"
 #include "planning.hpp"
+#include "discretizations.hpp"
 #include "prm.hpp"
 
 namespace mpt_host {
@@ -107,6 +108,69 @@ inline PrmResult run_prm_inst(const std::string &path, const double *states, int
     if (type == "Omnidirectional") return run_prm<Omnidirectional>(args, states, n, batch, max_queries);
     if (type == "Blimp") return run_prm<Blimp>(args, states, n, batch, max_queries);
     if (type == "Snake") return run_prm<SnakeTrailers>(args, states, n, batch, max_queries);
+    throw std::runtime_error("unrecognized Agent Type: " + type);
+}
+
+// Workspace discretisations over the .inst's workspace and agent (discretizations/workspace/).
+struct GridResult {
+    std::vector<uint8_t> free;
+    std::vector<double> centers;  // [cells][3]
+};
+template <class Agent>
+GridResult run_grid(const InstanceFileMap &args, const std::vector<double> &sizes) {
+    Agent agent(args);
+    Map3D<Agent> workspace(args);
+    GridDiscretization<Map3D<Agent>, Agent> grid(workspace, agent, sizes);
+    GridResult r;
+    for (unsigned int c = 0; c < grid.getCellCount(); ++c) {
+        r.free.push_back(grid.isFree(c) ? 1 : 0);
+        const auto p = grid.getGridCenter(c);
+        r.centers.insert(r.centers.end(), p.begin(), p.end());
+    }
+    return r;
+}
+
+struct LiteResult {
+    std::vector<double> verts;   // [V][12]
+    std::vector<int32_t> edges;  // [E][2], i < j, row-major order
+};
+template <class Agent>
+LiteResult run_prmlite(const InstanceFileMap &args, int32_t n_vertices, double step) {
+    Agent agent(args);
+    Map3D<Agent> workspace(args);
+    PRMLite<Map3D<Agent>, Agent> lite(workspace, agent, (unsigned)n_vertices, step);
+    LiteResult r;
+    for (const auto &v : lite.getVertices()) {
+        r.verts.insert(r.verts.end(), v.transform.R.begin(), v.transform.R.end());
+        r.verts.insert(r.verts.end(), v.transform.T.begin(), v.transform.T.end());
+    }
+    for (unsigned i = 0; i < lite.getCellCount(); ++i) {
+        auto nb = lite.getNeighboringCells(i);
+        std::sort(nb.begin(), nb.end());
+        for (unsigned j : nb)
+            if (j > i) {
+                r.edges.push_back((int32_t)i);
+                r.edges.push_back((int32_t)j);
+            }
+    }
+    return r;
+}
+
+inline GridResult run_grid_inst(const std::string &path, const std::vector<double> &sizes) {
+    InstanceFileMap args(path);
+    const std::string type = args.value("Agent Type");
+    if (type == "Omnidirectional") return run_grid<Omnidirectional>(args, sizes);
+    if (type == "Blimp") return run_grid<Blimp>(args, sizes);
+    if (type == "Snake") return run_grid<SnakeTrailers>(args, sizes);
+    throw std::runtime_error("unrecognized Agent Type: " + type);
+}
+
+inline LiteResult run_prmlite_inst(const std::string &path, int32_t n_vertices, double step) {
+    InstanceFileMap args(path);
+    const std::string type = args.value("Agent Type");
+    if (type == "Omnidirectional") return run_prmlite<Omnidirectional>(args, n_vertices, step);
+    if (type == "Blimp") return run_prmlite<Blimp>(args, n_vertices, step);
+    if (type == "Snake") return run_prmlite<SnakeTrailers>(args, n_vertices, step);
     throw std::runtime_error("unrecognized Agent Type: " + type);
 }
 

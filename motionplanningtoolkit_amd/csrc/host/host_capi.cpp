@@ -76,3 +76,29 @@ extern "C" mpt_status mpt_host_prm(const char *inst_path, const double *states, 
         if (comp && mc > 0) std::memcpy(comp, r.comp.data(), sizeof(int32_t) * mc);
     });
 }
+
+extern "C" mpt_status mpt_host_grid_discretization(const char *inst_path, const double sizes[3], int64_t cap,
+                                                   uint8_t *free_out, double *centers, int64_t *n_cells) {
+    return hguard([&] {
+        if (!inst_path || !sizes || !n_cells) throw std::invalid_argument("null pointer");
+        const auto r = mpt_host::run_grid_inst(inst_path, std::vector<double>(sizes, sizes + 3));
+        const int64_t n = (int64_t)r.free.size();
+        *n_cells = n;
+        const int64_t m = std::min<int64_t>(n, cap);
+        if (free_out && m > 0) std::memcpy(free_out, r.free.data(), (size_t)m);
+        if (centers && m > 0) std::memcpy(centers, r.centers.data(), sizeof(double) * 3 * m);
+    });
+}
+
+extern "C" mpt_status mpt_host_prmlite(const char *inst_path, int32_t n_vertices, double step, double *verts,
+                                       int64_t cap, int32_t *edges, int64_t *n_edges) {
+    return hguard([&] {
+        if (!inst_path || !n_edges || n_vertices < 0) throw std::invalid_argument("bad arguments");
+        const auto r = mpt_host::run_prmlite_inst(inst_path, n_vertices, step);
+        if (verts) std::memcpy(verts, r.verts.data(), sizeof(double) * r.verts.size());
+        const int64_t ne = (int64_t)r.edges.size() / 2;
+        *n_edges = ne;
+        const int64_t m = std::min<int64_t>(ne, cap);
+        if (edges && m > 0) std::memcpy(edges, r.edges.data(), sizeof(int32_t) * 2 * m);
+    });
+}

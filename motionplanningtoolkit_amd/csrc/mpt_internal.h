@@ -168,6 +168,10 @@ void launch_collide_sweep(const EnvDev &env, const AgentDev *d_link, int32_t n_c
 void launch_self_collide(const AgentDev *d_links, int32_t L, const double *poses, const int32_t *pose_edge,
                          int64_t n_poses, uint8_t *verdict, hipStream_t stream);
 
+// PRMLite edges (sweep.hip): all pairs i < j of verts [V][12] (R|T), hit[V(V-1)/2] zeroed.
+void launch_prmlite_edges(const EnvDev &env, const AgentDev *d_link, int32_t n_clusters, const double *verts, int64_t V,
+                          double step, uint8_t *hit, unsigned long long *stats, hipStream_t stream);
+
 // ---------------- distance (distance.hip) ----------------
 // Units are (pose, link) pairs as for collide mode A; best[E] receives the per-edge minimum
 // distance as the bit pattern of a double (DBL_MAX when the edge has no poses).

@@ -27,19 +27,24 @@ struct SweepCounters {
     uint32_t waves = 0, items = 0, pair_poses = 0, sat = 0;
 };
 
-__device__ __forceinline__ void sweep_wave(const EnvDev &env, const AgentDev &ag, const double *__restrict__ poses,
-                                           const int64_t *__restrict__ poff, int64_t e, int32_t cl, uint8_t *verdict,
-                                           int lane, int32_t *stk, SweepCounters &cnt) {
-    if (load_flag(verdict + e)) return;
-    const int64_t p0 = poff[e], p1 = poff[e + 1];
-    if (p1 <= p0) return;
+// fcl::relativeTransform's T for a world translation t (R1^T (t - T1), relative_transform()'s order)
+__device__ __forceinline__ void env_rel_t(const EnvDev &env, const double *t, double Tp[3]) {
+    const double d0 = t[0] - env.tf[9], d1 = t[1] - env.tf[10], d2 = t[2] - env.tf[11];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) Tp[i] = env.tf[0 * 3 + i] * d0 + env.tf[1 * 3 + i] * d1 + env.tf[2 * 3 + i] * d2;
+}
+
+// One (edge, cluster): Rw = the edge's world rotation, tf / tl = world translations of its
+// first and last pose, gen(f) calls f(world translation) for each pose in order and stops
+// when f returns true (a contact).
+template <class Gen>
+__device__ __forceinline__ void sweep_core(const EnvDev &env, const AgentDev &ag, int32_t cl, const double *Rw,
+                                           const double *tf, const double *tl, Gen gen, uint8_t *flag, int lane,
+                                           int32_t *stk, SweepCounters &cnt) {
     ++cnt.waves;
     double R[9], T0[3], TN[3];
-    unit_transform(env, poses + p0 * 12, R, T0);
-    {
-        double R2[9];
-        unit_transform(env, poses + (p1 - 1) * 12, R2, TN);
-    }
+    relative_transform(env.tf, env.tf + 9, Rw, tf, R, T0);
+    env_rel_t(env, tl, TN);
 #pragma unroll
     for (int i = 0; i < 9; ++i) R[i] = uniform_d(R[i]);
 #pragma unroll
@@ -103,29 +108,25 @@ __device__ __forceinline__ void sweep_wave(const EnvDev &env, const AgentDev &ag
                 const Item ti = env.items[t];  // level 0: item index = triangle index
                 const bool near = act && box_overlap(tlo, thi, ti.lo, ti.hi);
                 if (!__ballot(near)) continue;
-                if (load_flag(verdict + e)) return;
+                if (load_flag(flag)) return;
                 const EnvTri &E = env.tris[t];
                 bool hit = false;
                 if (near) {
-                    for (int64_t p = p0; p < p1 && !hit; ++p) {
-                        // T of fcl::relativeTransform: R1^T (T2 - T1), as relative_transform()
-                        const double *pt = poses + p * 12 + 9;
-                        const double d0 = pt[0] - env.tf[9], d1 = pt[1] - env.tf[10], d2 = pt[2] - env.tf[11];
+                    gen([&](const double *tw) {
                         double Tp[3];
-#pragma unroll
-                        for (int i = 0; i < 3; ++i)
-                            Tp[i] = env.tf[0 * 3 + i] * d0 + env.tf[1 * 3 + i] * d1 + env.tf[2 * 3 + i] * d2;
+                        env_rel_t(env, tw, Tp);
                         const v3 Q1 = mk(RQ[0].x + Tp[0], RQ[0].y + Tp[1], RQ[0].z + Tp[2]);
                         const v3 Q2 = mk(RQ[1].x + Tp[0], RQ[1].y + Tp[1], RQ[1].z + Tp[2]);
                         const v3 Q3 = mk(RQ[2].x + Tp[0], RQ[2].y + Tp[1], RQ[2].z + Tp[2]);
                         ++cnt.pair_poses;
-                        if (!tri_gate(E.lo, E.hi, Q1, Q2, Q3)) continue;
+                        if (!tri_gate(E.lo, E.hi, Q1, Q2, Q3)) return false;
                         ++cnt.sat;
                         hit = tri_intersect(E, Q1, Q2, Q3);
-                    }
+                        return hit;
+                    });
                 }
                 if (__ballot(hit)) {
-                    if (lane == 0) __hip_atomic_store(verdict + e, (uint8_t)1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    if (lane == 0) __hip_atomic_store(flag, (uint8_t)1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     return;
                 }
             }
@@ -153,6 +154,21 @@ __device__ __forceinline__ void sweep_wave(const EnvDev &env, const AgentDev &ag
     }
 }
 
+// edges given as pose ranges of a pose array (prm_connect.hip)
+__device__ __forceinline__ void sweep_wave(const EnvDev &env, const AgentDev &ag, const double *__restrict__ poses,
+                                           const int64_t *__restrict__ poff, int64_t e, int32_t cl, uint8_t *verdict,
+                                           int lane, int32_t *stk, SweepCounters &cnt) {
+    if (load_flag(verdict + e)) return;
+    const int64_t p0 = poff[e], p1 = poff[e + 1];
+    if (p1 <= p0) return;
+    sweep_core(env, ag, cl, poses + p0 * 12, poses + p0 * 12 + 9, poses + (p1 - 1) * 12 + 9,
+               [&](auto &&f) {
+                   for (int64_t p = p0; p < p1; ++p)
+                       if (f(poses + p * 12 + 9)) return;
+               },
+               verdict + e, lane, stk, cnt);
+}
+
 __global__ __launch_bounds__(kSweepWaves * 64) void k_sweep(EnvDev env, const AgentDev *__restrict__ link,
                                                             const double *__restrict__ poses,
                                                             const int64_t *__restrict__ poff, int64_t E,
@@ -172,6 +188,71 @@ __global__ __launch_bounds__(kSweepWaves * 64) void k_sweep(EnvDev env, const Ag
         atomicAdd(stats + 2, (unsigned long long)cnt.pair_poses);
         atomicAdd(stats + 3, (unsigned long long)cnt.sat);
     }
+}
+
+// PRMLite::generateEdges (discretizations/workspace/prmlite.hpp:128-164, interpolate :181-203):
+// pair e = (i, j), i < j row-major; steps = (unsigned)(|t_i - t_j| / step) poses, each one
+// vecStep = (t_j - t_i) / steps further (accumulated, as setTransform(q1, T + vecStep)), all
+// with vertex i's rotation; no poses = safe.
+__global__ __launch_bounds__(kSweepWaves * 64) void k_sweep_lite(EnvDev env, const AgentDev *__restrict__ link,
+                                                                 const double *__restrict__ verts, int64_t V,
+                                                                 double step, int64_t E, int32_t n_clusters,
+                                                                 uint8_t *hit, unsigned long long *stats) {
+    __shared__ int32_t s_stk[kSweepWaves][2 * kSweepStack];
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    const int64_t g = (int64_t)blockIdx.x * kSweepWaves + wave;
+    const int64_t e = g / n_clusters;
+    const int32_t cl = (int32_t)(g % n_clusters);
+    SweepCounters cnt;
+    if (e < E && !load_flag(hit + e)) {
+        // pair index -> (i, j): row i holds V - 1 - i pairs
+        const double b = 2.0 * (double)V - 1.0;
+        int64_t i = (int64_t)((b - sqrt(b * b - 8.0 * (double)e)) * 0.5);
+        if (i < 0) i = 0;
+        while (i > 0 && i * (2 * V - i - 1) / 2 > e) --i;
+        while ((i + 1) * (2 * V - i - 2) / 2 <= e) ++i;
+        const int64_t j = e - i * (2 * V - i - 1) / 2 + i + 1;
+        const double *ti = verts + i * 12, *tj = verts + j * 12;
+        const double *v1 = ti + 9, *v2 = tj + 9;
+        const double df[3] = {v1[0] - v2[0], v1[1] - v2[1], v1[2] - v2[2]};
+        const double dist = sqrt(df[0] * df[0] + df[1] * df[1] + df[2] * df[2]);
+        const double q = dist / step;
+        const unsigned steps = (q >= 4294967296.0 || !(q >= 0)) ? 0u : (unsigned)q;
+        if (steps > 0) {
+            const double vs[3] = {(v2[0] - v1[0]) / (double)steps, (v2[1] - v1[1]) / (double)steps,
+                                  (v2[2] - v1[2]) / (double)steps};
+            double tf[3] = {v1[0] + vs[0], v1[1] + vs[1], v1[2] + vs[2]}, tl[3] = {v1[0], v1[1], v1[2]};
+            for (unsigned s = 0; s < steps; ++s)
+                for (int k = 0; k < 3; ++k) tl[k] = tl[k] + vs[k];
+            sweep_core(env, link[0], cl, ti, tf, tl,
+                       [&](auto &&f) {
+                           double t[3] = {v1[0], v1[1], v1[2]};
+                           for (unsigned s = 0; s < steps; ++s) {
+                               for (int k = 0; k < 3; ++k) t[k] = t[k] + vs[k];
+                               if (f(t)) return;
+                           }
+                       },
+                       hit + e, lane, s_stk[wave], cnt);
+        }
+    }
+    if (stats && lane == 0 && cnt.waves) {
+        atomicAdd(stats + 0, (unsigned long long)cnt.waves);
+        atomicAdd(stats + 1, (unsigned long long)cnt.items);
+        atomicAdd(stats + 2, (unsigned long long)cnt.pair_poses);
+        atomicAdd(stats + 3, (unsigned long long)cnt.sat);
+    }
+}
+
+void launch_prmlite_edges(const EnvDev &env, const AgentDev *d_link, int32_t n_clusters, const double *verts, int64_t V,
+                          double step, uint8_t *hit, unsigned long long *stats, hipStream_t stream) {
+    const int64_t E = V * (V - 1) / 2;
+    if (E <= 0 || env.n_tris <= 0) return;
+    const int64_t blocks = (E * n_clusters + kSweepWaves - 1) / kSweepWaves;
+    if (blocks > 0x7fffffff) throw Error{5, "PRMLite batch too large"};
+    hipLaunchKernelGGL(k_sweep_lite, dim3((unsigned)blocks), dim3(kSweepWaves * 64), 0, stream, env, d_link, verts, V,
+                       step, E, n_clusters, hit, stats);
+    hip_check(hipGetLastError(), "k_sweep_lite launch");
 }
 
 void launch_collide_sweep(const EnvDev &env, const AgentDev *d_link, int32_t n_clusters, const double *poses,

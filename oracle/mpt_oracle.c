@@ -1333,3 +1333,77 @@ void orc_self_collide_batch(const double *agent_tris, const int64_t *link_tri_of
         verdict[e] = (uint8_t)hit;
     }
 }
+
+/* ======================================================================
+ * PRMLite::generateEdges (discretizations/workspace/prmlite.hpp:128-164) with
+ * PRMLite::interpolate (:181-203): translation steps accumulated from vertex i toward j, the
+ * rotation of vertex i, endpoints excluded; no steps = an edge without poses (kept).
+ * ====================================================================== */
+void orc_prmlite_edges(const orc_bvh *env, const double env_tf[12], const double *agent_tris, int64_t Ta,
+                       const double *verts, int64_t V, double step, uint8_t *collides, int nthreads) {
+#ifdef _OPENMP
+#pragma omp parallel for schedule(dynamic, 4) num_threads(nthreads > 0 ? nthreads : 1)
+#endif
+    for (int64_t i = 0; i < V; ++i) {
+        const int64_t row = i * (2 * V - i - 1) / 2;
+        double pose[12];
+        memcpy(pose, verts + 12 * i, 9 * sizeof(double));
+        for (int64_t j = i + 1; j < V; ++j) {
+            const double *v1 = verts + 12 * i + 9, *v2 = verts + 12 * j + 9;
+            double diff[3];
+            sub3(v1, v2, diff);
+            const double dist = sqrt(dot3(diff, diff));
+            const double q = dist / step;
+            const unsigned int steps = (q >= 4294967296.0 || !(q >= 0)) ? 0u : (unsigned int)q;
+            int hit = 0;
+            if (steps > 0) {
+                const double vs[3] = {(v2[0] - v1[0]) / (double)steps, (v2[1] - v1[1]) / (double)steps,
+                                      (v2[2] - v1[2]) / (double)steps};
+                pose[9] = v1[0]; pose[10] = v1[1]; pose[11] = v1[2];
+                for (unsigned int s = 0; s < steps && !hit; ++s) {
+                    for (int k = 0; k < 3; ++k) pose[9 + k] = pose[9 + k] + vs[k];
+                    hit = orc_collide_unit_bvh(env, env_tf, agent_tris, Ta, pose, NULL);
+                }
+            }
+            collides[row + (j - i - 1)] = (uint8_t)hit;
+        }
+    }
+    (void)nthreads;
+}
+
+/* ======================================================================
+ * GridDiscretization (discretizations/workspace/griddiscretization.hpp:9-36, getGridCenter
+ * :111-124 as written) with getRepresentivePosesForLocation (agents/omnidirectional.hpp:191-200,
+ * blimp.hpp:194-217, snake_trailers.hpp:220-244).
+ * ====================================================================== */
+int64_t orc_grid_discretization(const orc_bvh *env, const double env_tf[12], const double *agent_tris, int64_t Ta,
+                                const double bounds[6], const double sizes[3], int32_t n_rot, uint8_t *free_out,
+                                int64_t cap) {
+    unsigned int dims[3], cells = 1;
+    for (int i = 0; i < 3; ++i) {
+        const double range = fabs(bounds[2 * i] - bounds[2 * i + 1]);
+        dims[i] = range == 0 ? 1u : (unsigned int)ceil(range / sizes[i]);
+        cells *= dims[i];
+    }
+    for (unsigned int n = 0; n < cells && (int64_t)n < cap; ++n) {
+        double c[3];
+        c[0] = bounds[0] + (double)(n % dims[0]) * sizes[0] + sizes[0] * 0.5;
+        unsigned int prev = 1;
+        for (int i = 1; i < 3; ++i) {
+            prev *= dims[i];
+            c[i] = bounds[2 * i] + (double)(n / prev % dims[i]) * sizes[i] + sizes[1] * 0.5;
+        }
+        int hit = 0;
+        const double increment = M_PI / ((double)4 * 2.);
+        for (int r = 0; r < n_rot && !hit; ++r) {
+            double pose[12] = {1, 0, 0, 0, 1, 0, 0, 0, 1, c[0], c[1], c[2]};
+            if (n_rot > 1) {
+                const double cs = cos((double)r * increment), sn = sin((double)r * increment);
+                pose[0] = cs; pose[1] = sn; pose[3] = -sn; pose[4] = cs;
+            }
+            hit = orc_collide_unit_bvh(env, env_tf, agent_tris, Ta, pose, NULL);
+        }
+        free_out[n] = (uint8_t)!hit;
+    }
+    return (int64_t)cells;
+}

@@ -170,6 +170,19 @@ void orc_distance_batch(const double *env_tris, int64_t Te, const double env_tf[
 void orc_self_collide_batch(const double *agent_tris, const int64_t *link_tri_off, int32_t L, const double *poses,
                             const int64_t *edge_pose_offsets, int64_t E, uint8_t *verdict);
 
+/* GridDiscretization (discretizations/workspace/griddiscretization.hpp:9-36): cells over
+ * bounds [3][2] (lo, hi) of the given sizes; a cell is free when none of its representative
+ * poses collides: n_rot = 1 -> identity (Omnidirectional), 4 -> yaw i*pi/8 (Blimp, Snake head).
+ * Centres per getGridCenter as written.  Returns the cell count (free written up to cap). */
+int64_t orc_grid_discretization(const orc_bvh *env, const double env_tf[12], const double *agent_tris, int64_t Ta,
+                                const double bounds[6], const double sizes[3], int32_t n_rot, uint8_t *free_out,
+                                int64_t cap);
+
+/* PRMLite::generateEdges (discretizations/workspace/prmlite.hpp:128-164): collides[e] for all
+ * vertex pairs i < j (row-major), verts [V][12] = R | T, poses per PRMLite::interpolate. */
+void orc_prmlite_edges(const orc_bvh *env, const double env_tf[12], const double *agent_tris, int64_t Ta,
+                       const double *verts, int64_t V, double step, uint8_t *collides, int nthreads);
+
 /* PRM roadmap with radius neighbours (config 4; prm.hpp:334-387 with kNearestWithin):
  * edges (i, j), j < i, squared L2 of the first three state variables < r2, sorted by (i, j);
  * verdict per edge over Omnidirectional::steer(key_i, key_j, 1000) + getPoses(cc_dt) with the

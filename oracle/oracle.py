@@ -70,6 +70,8 @@ def lib():
             "orc_engine_step": (I64, [I32, P, I32, P, D, D, U64, U64, I32, P, P, P, I64, P, P, I64, I64, P, P, C.c_int, C.c_int]),
             "orc_prm_build": (I64, [P, P, P, I64, P, I64, I32, I32, D, P, P, I64, P]),
             "orc_tri_distance": (D, [P, P]),
+            "orc_grid_discretization": (I64, [P, P, P, I64, P, P, I32, P, I64]),
+            "orc_prmlite_edges": (None, [P, P, P, I64, P, I64, D, P, C.c_int]),
             "orc_self_collide_batch": (None, [P, P, I32, P, P, I64, P]),
             "orc_prm_radius": (I64, [P, P, P, I64, P, I64, I32, D, D, P, P, I64, P, C.c_int]),
             "orc_distance_unit": (D, [P, I64, P, P, I64, P]),
@@ -149,6 +151,24 @@ def self_collide_batch(link_tris: list, poses, edge_offsets) -> np.ndarray:
     out = np.zeros(E, np.uint8)
     lib().orc_self_collide_batch(_p(agent), _p(off), len(link_tris), _p(poses), _p(eo), E, _p(out))
     return out
+
+
+def prmlite_edges(bvh: BVH, env_tf, agent_tris, verts, step=0.1, nthreads=8) -> np.ndarray:
+    v = _f64(verts).reshape(-1, 12)
+    V = v.shape[0]
+    at = _f64(agent_tris).reshape(-1, 9)
+    out = np.zeros(max(V * (V - 1) // 2, 0), np.uint8)
+    lib().orc_prmlite_edges(bvh.ptr, _p(_f64(env_tf)), _p(at), at.shape[0], _p(v), V, step, _p(out), nthreads)
+    return out
+
+
+def grid_discretization(bvh: BVH, env_tf, agent_tris, bounds, sizes, n_rot) -> np.ndarray:
+    at = _f64(agent_tris).reshape(-1, 9)
+    b, s = _f64(bounds).ravel(), _f64(sizes)
+    n = lib().orc_grid_discretization(bvh.ptr, _p(_f64(env_tf)), _p(at), at.shape[0], _p(b), _p(s), n_rot, None, 0)
+    out = np.zeros(n, np.uint8)
+    lib().orc_grid_discretization(bvh.ptr, _p(_f64(env_tf)), _p(at), at.shape[0], _p(b), _p(s), n_rot, _p(out), n)
+    return out.astype(bool)
 
 
 def tri_distance(S, T) -> float:

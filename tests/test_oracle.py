@@ -413,3 +413,18 @@ def test_oracle_self_collision_known_answers(oracle, unit_box):
     # three links: only the (0, 2) pair touches
     p3 = np.array([[np.r_[I, 0, 0, 0], np.r_[I, 0, 5, 0], np.r_[I, 0.9, 0, 0]]])
     assert oracle.self_collide_batch([unit_box] * 3, p3, [0, 1]).tolist() == [1]
+
+
+def test_oracle_grid_discretization_centres(oracle):
+    """GridDiscretization's cell centres as written (griddiscretization.hpp:111-124): dims >= 1 use
+    the n / (prod of dimensions[1..i]) index and sizes[1] for the half-cell offset."""
+    box = scenes.read_obj(scenes.mesh_path("env_unit_box"))
+    free = oracle.grid_discretization(oracle.BVH(box), np.r_[np.eye(3).ravel(), 0, 0, 0], box,
+                                      [[-2, 2], [-2, 2], [-2, 2]], [1.0, 1.0, 1.0], 1)
+    assert len(free) == 64
+    # with these quirks cell n's centre is (x(n % 4), y(n / 4 % 4), z(n / 16 % 4)): the cells
+    # whose box is within 1 of the origin box in every axis collide
+    c = np.arange(-1.5, 2.0, 1.0)
+    want = np.array([not (abs(c[n % 4]) <= 1 and abs(c[n // 4 % 4]) <= 1 and abs(c[n // 16 % 4]) <= 1)
+                     for n in range(64)])
+    assert np.array_equal(free, want)
