@@ -39,6 +39,8 @@ def parse():
     ap.add_argument("--batch", type=int, default=65536, help="extensions per round (K)")
     ap.add_argument("--tree", type=int, default=100_000, help="tree nodes at the start of each round (N0)")
     ap.add_argument("--seed", type=int, default=1000)
+    ap.add_argument("--workload", default="blimp", choices=["blimp", "snake"],
+                    help="blimp = BASELINE config 2 (default); snake = config 3 (snake_trailers, 11 links, corridor)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample length")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--nn", default="auto", choices=["grid", "brute", "auto", "tree"], help="engine NN structure")
@@ -71,15 +73,19 @@ def cpu_baseline(sc, tree, K_gpu, seed, target_s):
                                   sc.agent_tris, nodes, par, n0, nthreads=threads, use_kdtree=True)
         return time.perf_counter() - t, n - n0
 
-    t0, _ = run(256, 1)
-    K = int(min(max(256 * target_s / max(t0, 1e-3), 256), K_gpu))
+    # per-round fixed cost (the kd-tree build) + per-extension cost, from two short runs
+    t_a, _ = run(256, 1)
+    t_b, _ = run(1024, 1)
+    per = max((t_b - t_a) / 768, 1e-7)
+    fixed = max(t_a - 256 * per, 0.0)
+    K = int(min(max((target_s - fixed) / per, 256), K_gpu))
     t1, valid1 = run(K, 1)
     threads = os.cpu_count() or 1
     threads = min(threads, 16)
     tn, validn = run(K, threads)
     return {
         "value": valid1 / t1, "unit": "valid extensions/s", "cores": 1, "kind": "port",
-        "sample": f"{K} extensions of the same blimp round (100k-node tree, kd-tree NN built per round, "
+        "sample": f"{K} extensions of the same {sc.name} round ({n0}-node tree, kd-tree NN built per round, "
                   f"AABB-tree + FCL tri-tri SAT), oracle/mpt_oracle.c, {t1:.2f} s",
         "all_cores": {"value": validn / tn, "cores": threads, "seconds": round(tn, 3)},
         "cpu": _cpu_model(),
@@ -292,7 +298,14 @@ def main():
             dist.destroy_process_group()
         return
 
-    sc = scenes.blimp_scenario("all")
+    if args.workload == "snake":
+        sc = scenes.snake_scenario("corridor")
+        workload = (f"snake.inst: snake_trailers ({sc.links} unit-box links, T=10) in the synthetic corridor "
+                    f"({sc.env_tris.shape[0]} tris), batched RRT round over a {args.tree}-node tree")
+    else:
+        sc = scenes.blimp_scenario("all")
+        workload = ("blimp.inst: blimp (1355 tris) vs single-room env (model.dae, 316 tris), "
+                    f"batched RRT round over a {args.tree}-node tree")
     seed = multiseed.rank_seed(args.seed, rank)
     rng = np.random.default_rng(seed)
     n0, K = args.tree, args.batch
@@ -357,9 +370,9 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "f64",
-        "data": "synthetic (uniform samples and tree states over Blimp::getStateVarRanges; meshes from the reference)",
-        "config": {"workload": "blimp.inst: blimp (1355 tris) vs single-room env (model.dae, 316 tris), "
-                               "batched RRT round over a 100k-node tree",
+        "data": f"synthetic (uniform samples and tree states over the {args.workload}'s getStateVarRanges; "
+                "meshes from the reference)",
+        "config": {"workload": workload,
                    "tree_nodes": n0, "extensions_per_round": K, "seed_base": args.seed, "nn_index": args.nn,
                    "parallelism": f"independent seeds x{world}"},
         "checked_per_s": checked / elapsed,
