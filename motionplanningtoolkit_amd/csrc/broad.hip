@@ -47,7 +47,8 @@ struct SplitArgs {
     Cand *cand;
     uint32_t *cand_count;
     Cand *spill;
-    uint32_t *ctl;
+    uint32_t *ctl;       // this launch's counters: [1] overflow units, [2] spill count
+    uint32_t *ctl_next;  // the other half, zeroed by k_pairs for the next launch
     int32_t *ovf_list;
     int64_t n_seg;
     int32_t pair_cap, cand_cap, spill_cap, n_clusters, n_cwaves;
@@ -152,12 +153,79 @@ __device__ __forceinline__ uint32_t walk_tree(const EnvDev &env, const Item *__r
     return tests;
 }
 
+// Per-(pose, cluster) record of a thread that survived the root cull, compacted in LDS so
+// the tree walks run on as few waves as possible (most clusters are culled at the root).
+struct PairRec {
+    float lo[3], hi[3];
+    int32_t unit, c, tfirst, tcount;
+};
+
 template <bool kTwo, bool kLds>
 __global__ __launch_bounds__(kPairThreads) void k_pairs(EnvDev env, const AgentDev *__restrict__ links,
                                                        CollideWork w, SplitArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    __shared__ uint32_t s_pc[kPairThreads / 64], s_hc[kPairThreads / 64];
+    __shared__ uint32_t s_pc[kPairThreads / 64], s_hc[kPairThreads / 64], s_live[kPairThreads / 64];
     __shared__ uint4 s_stk[kTwo ? 1 : kPairThreads * kStack];
+    __shared__ PairRec s_rec[kPairThreads];
+    if (blockIdx.x == 0) {  // stream-ordered resets instead of memset launches
+        if (threadIdx.x < 4) a.ctl_next[threadIdx.x] = 0u;
+        if (threadIdx.x == 0) a.hdr_count[a.n_seg] = 0u;  // the header scan's sentinel slot
+    }
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    const int64_t t = (int64_t)blockIdx.x * kPairThreads + threadIdx.x;
+    const int64_t seg = t >> 6;
+    // 1. thread per (pose, cluster): FCL relative transform, cluster box, root cull
+    {
+        const int64_t unit = t / a.n_clusters;
+        const int32_t c = (int32_t)(t % a.n_clusters);
+        bool live = unit < w.n_units;
+        int32_t link = 0;
+        int64_t slot = 0, edge = 0;
+        if (live) live = decode_unit(w, unit, link, slot, edge);
+        if (live) live = c < links[link].n_clusters;
+        const bool decoded = live;
+        PairRec r;
+        if (live) {
+            double R[9], T[3];
+            unit_transform(env, w.poses + (slot * w.L + link) * 12, R, T);
+            const Cluster &cl = links[link].clusters[c];
+            local_box(cl.c, cl.e, R, T, r.lo, r.hi);
+            r.unit = (int32_t)unit;
+            r.c = c;
+            r.tfirst = cl.first;
+            r.tcount = cl.count;
+            live = box_overlap(r.lo, r.hi, env.root_lo, env.root_hi);
+        }
+        const uint64_t m = __ballot(live);
+        if (lane == 0) {
+            s_live[wave] = (uint32_t)__popcll(m);
+            s_pc[wave] = 0;
+            s_hc[wave] = 0;
+        }
+        if (w.stats) {
+            const uint64_t dm = __ballot(decoded);
+            if (lane == 0) {
+                atomicAdd(w.stats + 1, (unsigned long long)__popcll(m));
+                atomicAdd(w.stats + 10, (unsigned long long)__popcll(dm));
+            }
+        }
+        __syncthreads();
+        if (live) {
+            uint32_t base = 0;
+            for (int v = 0; v < wave; ++v) base += s_live[v];
+            s_rec[base + (uint32_t)__popcll(m & ((1ull << lane) - 1))] = r;
+        }
+    }
+    uint32_t total = 0;
+    for (int v = 0; v < kPairThreads / 64; ++v) total += s_live[v];
+    if (total == 0) {  // block-uniform: nothing reaches the env tree
+        if (lane == 0 && seg < a.n_seg) {
+            a.hdr_count[seg] = 0;
+            a.pair_count[seg] = 0;
+        }
+        return;
+    }
     const Item *items = env.items;
     if (kLds) {
         Item *s_items = reinterpret_cast<Item *>(smem);
@@ -167,34 +235,12 @@ __global__ __launch_bounds__(kPairThreads) void k_pairs(EnvDev env, const AgentD
         for (int i = threadIdx.x; i < n * 2; i += blockDim.x) dst[i] = src[i];
         items = s_items;
     }
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int lane = threadIdx.x & 63;
-    if (lane == 0) {
-        s_pc[wave] = 0;
-        s_hc[wave] = 0;
-    }
     __syncthreads();
-    const int64_t t = (int64_t)blockIdx.x * kPairThreads + threadIdx.x;
-    const int64_t seg = t >> 6;
-    const int64_t unit = t / a.n_clusters;
-    const int32_t c = (int32_t)(t % a.n_clusters);
-    bool live = unit < w.n_units;
-    int32_t link = 0;
-    int64_t slot = 0, edge = 0;
-    if (live) live = decode_unit(w, unit, link, slot, edge);
-    if (live) live = c < links[link].n_clusters;
-    const bool decoded = live;
-    float lo[3] = {0, 0, 0}, hi[3] = {0, 0, 0};
-    int32_t tfirst = 0, tcount = 0;
-    if (live) {
-        double R[9], T[3];
-        unit_transform(env, w.poses + (slot * w.L + link) * 12, R, T);
-        const Cluster &cl = links[link].clusters[c];
-        local_box(cl.c, cl.e, R, T, lo, hi);
-        tfirst = cl.first;
-        tcount = cl.count;
-        live = box_overlap(lo, hi, env.root_lo, env.root_hi);
-    }
+    // 2. the surviving records, packed onto the first waves: walk the env tree; the pair
+    //    words and headers carry the (segment, lane) of the thread that walked
+    const bool live = threadIdx.x < total;
+    PairRec r;
+    if (live) r = s_rec[threadIdx.x];
     uint4 *stk = s_stk + (kTwo ? 0 : threadIdx.x * kStack);
     uint32_t np = 0, tests = 0;
     bool ovf = false;
@@ -202,7 +248,7 @@ __global__ __launch_bounds__(kPairThreads) void k_pairs(EnvDev env, const AgentD
     // one pass: each pair takes the next slot of the wave's segment (LDS atomic) as a
     // (lane, triangle) word; k_cands picks a header's pairs out by lane
     if (live)
-        tests = walk_tree<kTwo>(env, items, lo, hi, stk, [&](int32_t tri) {
+        tests = walk_tree<kTwo>(env, items, r.lo, r.hi, stk, [&](int32_t tri) {
             const uint32_t pos = atomicAdd(&s_pc[wave], 1u);
             if (pos < (uint32_t)a.pair_cap)
                 out[pos] = (int32_t)(((uint32_t)lane << kPairTriBits) | (uint32_t)tri);
@@ -212,17 +258,15 @@ __global__ __launch_bounds__(kPairThreads) void k_pairs(EnvDev env, const AgentD
         });
     if (np > 0 && !ovf) {
         const uint32_t h = atomicAdd(&s_hc[wave], 1u);
-        a.hdr[seg * kHdrCap + h] = PairHdr{(int32_t)unit, c, (int32_t)seg, (int32_t)np, tfirst, tcount, lane, 0};
+        a.hdr[seg * kHdrCap + h] = PairHdr{r.unit, r.c, (int32_t)seg, (int32_t)np, r.tfirst, r.tcount, lane, 0};
     }
-    if (ovf) a.ovf_list[atomicAdd(a.ctl + 1, 1u)] = (int32_t)unit;  // rare: fused re-run
+    if (ovf) a.ovf_list[atomicAdd(a.ctl + 1, 1u)] = r.unit;  // rare: fused re-run
     __builtin_amdgcn_wave_barrier();
     if (lane == 0 && seg < a.n_seg) {
         a.hdr_count[seg] = s_hc[wave];
         a.pair_count[seg] = s_pc[wave] < (uint32_t)a.pair_cap ? s_pc[wave] : (uint32_t)a.pair_cap;
     }
     if (w.stats) {
-        const uint64_t lm = __ballot(live);
-        const uint64_t dm = __ballot(decoded);
         uint32_t sum_tests = tests, sum_pairs = np;
 #pragma unroll
         for (int off = 32; off > 0; off >>= 1) {
@@ -230,8 +274,6 @@ __global__ __launch_bounds__(kPairThreads) void k_pairs(EnvDev env, const AgentD
             sum_pairs += __shfl_xor(sum_pairs, off);
         }
         if (lane == 0) {
-            atomicAdd(w.stats + 1, (unsigned long long)__popcll(lm));
-            atomicAdd(w.stats + 10, (unsigned long long)__popcll(dm));
             atomicAdd(w.stats + 2, (unsigned long long)sum_tests);
             atomicAdd(w.stats + 4, (unsigned long long)sum_pairs);
         }
@@ -405,7 +447,9 @@ void CollideScratch::ensure(int64_t n_units, int32_t max_clusters) {
         hip_check(hipMalloc(&cand, sizeof(Cand) * (size_t)n_cwaves * cand_cap), "alloc candidates");
         hip_check(hipMalloc(&cand_count, sizeof(uint32_t) * (size_t)n_cwaves), "alloc candidate counts");
         hip_check(hipMalloc(&spill, sizeof(Cand) * (size_t)spill_cap), "alloc spill");
-        hip_check(hipMalloc(&ctl, sizeof(uint32_t) * 4), "alloc collide ctl");
+        hip_check(hipMalloc(&ctl, sizeof(uint32_t) * 8), "alloc collide ctl");
+        hip_check(hipMemset(ctl, 0, sizeof(uint32_t) * 8), "zero collide ctl");
+        ctl_par = 0;
     }
     const int64_t segs = (n_units * (int64_t)(max_clusters > 0 ? max_clusters : 1) + 63) / 64;
     if (segs > n_seg) {
@@ -453,9 +497,13 @@ static void collide_split_chunk(const EnvDev &env, const AgentDev *d_links, int3
     if (threads >= (int64_t(1) << 31) || w.n_units > s.ovf_cap || segs > s.n_seg || !s.pairs)
         throw Error{5, "collide scratch not sized for this launch"};
     if (env.n_tris >= (1 << kPairTriBits)) throw Error{5, "env too large for the split collide path"};
-    SplitArgs a{s.pairs, s.hdr,   s.hdr_count, s.pair_count, s.hdr_off, s.hdr_dense, s.cand, s.cand_count, s.spill, s.ctl,
-                s.ovf_list, segs, s.pair_cap, s.cand_cap, s.spill_cap, C,           s.n_cwaves};
-    hip_check(hipMemsetAsync(s.ctl, 0, sizeof(uint32_t) * 4, stream), "collide ctl memset");
+    // ctl is double-buffered: this launch's half was zeroed by the previous launch's k_pairs
+    // (or at allocation), and this k_pairs zeroes the other half for the next launch
+    uint32_t *ctl = s.ctl + 4 * s.ctl_par, *ctl_next = s.ctl + 4 * (1 - s.ctl_par);
+    s.ctl_par ^= 1;
+    SplitArgs a{s.pairs,  s.hdr,      s.hdr_count, s.pair_count, s.hdr_off, s.hdr_dense, s.cand,    s.cand_count,
+                s.spill,  ctl,        ctl_next,    s.ovf_list,   segs,      s.pair_cap,  s.cand_cap, s.spill_cap,
+                C,        s.n_cwaves};
     const unsigned pblocks = (unsigned)((threads + kPairThreads - 1) / kPairThreads);
     const int32_t n_items = env.lev_off[env.n_levels];
     const bool lds = n_items <= kLdsItems;
@@ -477,8 +525,7 @@ static void collide_split_chunk(const EnvDev &env, const AgentDev *d_links, int3
     }
     hip_check(hipGetLastError(), "k_pairs launch");
     mark(0);
-    // count slot `segs` is the scan's sentinel (a larger earlier launch may have used it)
-    hip_check(hipMemsetAsync(s.hdr_count + segs, 0, sizeof(uint32_t), stream), "sentinel memset");
+    // count slot `segs` is the scan's sentinel (a larger earlier launch may have used it): k_pairs zeroed it
     size_t tb = s.scan_bytes;
     hip_check(hipcub::DeviceScan::ExclusiveSum(s.scan_tmp, tb, s.hdr_count, s.hdr_off, (int)(segs + 1), stream),
               "header scan");
@@ -500,7 +547,7 @@ static void collide_split_chunk(const EnvDev &env, const AgentDev *d_links, int3
     // path, list read on the device, a small grid so the usual empty launch costs little
     CollideWork f = w;
     f.unit_list = s.ovf_list;
-    f.unit_list_n = s.ctl + 1;
+    f.unit_list_n = ctl + 1;
     f.stats = nullptr;
     launch_collide(env, d_links, f, stream, 64);
 }

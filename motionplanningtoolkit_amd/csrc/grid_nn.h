@@ -42,6 +42,7 @@ public:
 private:
     GridParams g{};
     int64_t n_max = 0, pts_cap = 0, cells_cap = 0;
+    bool counts_zero = false;  // counts[] is all zero (true after every complete build)
     int32_t dim = 0;
     double *spts = nullptr;
     int32_t *sids = nullptr, *cell_of = nullptr, *counts = nullptr, *cell_start = nullptr;

@@ -50,7 +50,9 @@ __global__ void k_grid_scatter(const double *__restrict__ pts, int32_t d, int64_
     if (n_dev) n = *n_dev < n ? *n_dev : n;
     if (i >= n) return;
     const int32_t cell = cell_of[i];
-    const int64_t pos = cell_start[cell] + atomicAdd(cursor + cell, 1);
+    // the cursor counts the cell down from its size, so every count is zero again when the
+    // scatter ends and the next build needs no memset
+    const int64_t pos = cell_start[cell] + (atomicSub(cursor + cell, 1) - 1);
     for (int j = 0; j < d; ++j) spts[pos * d + j] = pts[i * d + j];
     sids[pos] = (int32_t)(i + 1);
 }
@@ -231,6 +233,10 @@ void GridIndex::reserve(int64_t cap_pts, int32_t d, int64_t ncells) {
         hip_check(hipMalloc(&counts, sizeof(int32_t) * (ncells + 1)), "grid counts");
         hip_check(hipMalloc(&cell_start, sizeof(int32_t) * (ncells + 1)), "grid starts");
         cells_cap = ncells + 1;
+        // every count starts at zero and each build leaves them so (k_grid_scatter counts
+        // down); a build with more cells than the last one relies on this
+        hip_check(hipMemset(counts, 0, sizeof(int32_t) * (size_t)cells_cap), "grid counts zero");
+        counts_zero = true;
         size_t tb = 0;
         hip_check(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, counts, cell_start, (int)(ncells + 1)), "scan size");
         if (tb > temp_bytes) {
@@ -253,7 +259,8 @@ void GridIndex::build(const double *pts, int64_t n_upper, const int64_t *n_dev, 
     reserve(n_upper, d, gp.ncells);
     g = gp;
     n_max = n_upper;
-    hip_check(hipMemsetAsync(counts, 0, sizeof(int32_t) * (g.ncells + 1), stream), "grid memset");
+    if (!counts_zero) hip_check(hipMemsetAsync(counts, 0, sizeof(int32_t) * (size_t)cells_cap, stream), "grid memset");
+    counts_zero = false;
     if (n_upper > 0) {
         const unsigned blocks = (unsigned)((n_upper + 255) / 256);
         hipLaunchKernelGGL(k_grid_count, dim3(blocks), dim3(256), 0, stream, g, pts, d, n_upper, n_dev, cell_of, counts);
@@ -262,12 +269,12 @@ void GridIndex::build(const double *pts, int64_t n_upper, const int64_t *n_dev, 
     size_t tb = temp_bytes;
     hip_check(hipcub::DeviceScan::ExclusiveSum(temp, tb, counts, cell_start, (int)(g.ncells + 1), stream), "scan");
     if (n_upper > 0) {
-        hip_check(hipMemsetAsync(counts, 0, sizeof(int32_t) * g.ncells, stream), "cursor memset");
         const unsigned blocks = (unsigned)((n_upper + 255) / 256);
         hipLaunchKernelGGL(k_grid_scatter, dim3(blocks), dim3(256), 0, stream, pts, d, n_upper, n_dev, cell_of,
                            cell_start, counts, spts, sids);
         hip_check(hipGetLastError(), "k_grid_scatter");
     }
+    counts_zero = true;  // k_grid_scatter counted every cell back down (nothing counted when n_upper == 0)
 }
 
 GridDev GridIndex::dev() const {
@@ -333,7 +340,10 @@ int32_t choose_grid_dims(int32_t d, const double *lohi, int32_t dims[3]) {
 // (d2, id) order by xor-shuffles before the ring bound test, which is group-uniform.
 // Sixteen times more waves than k_grid_knn, so the dependent cell_start -> point loads
 // are hidden by occupancy instead of exposed one query per lane.
-template <int D, int kGroup>
+// kFirst = the ring the walk starts at: with kFirst = 1 the centre cell and ring 1 (the 3^gd
+// block) are one pass, so the group spends one dependent cell -> point load chain less per
+// query (ring 0 alone keeps 15 of 16 lanes idle and seldom settles the query).
+template <int D, int kGroup, int kFirst>
 __global__ __launch_bounds__(256) void k_grid_nn1_group(GridDev G, int32_t d, const double *__restrict__ q,
                                                         int64_t nq, int32_t *__restrict__ out_ids,
                                                         double *__restrict__ out_d2) {
@@ -358,7 +368,7 @@ __global__ __launch_bounds__(256) void k_grid_nn1_group(GridDev G, int32_t d, co
     double bd = __builtin_huge_val();
     int32_t bi = -1;
     uint32_t n_pts = 0, n_cells = 0;
-    for (int r = 0;; ++r) {
+    for (int r = kFirst;; ++r) {
         const int side = 2 * r + 1;
         const int cube = g.gd == 3 ? side * side * side : (g.gd == 2 ? side * side : side);
         for (int c = sub; c < cube; c += kGroup) {
@@ -368,7 +378,7 @@ __global__ __launch_bounds__(256) void k_grid_nn1_group(GridDev G, int32_t d, co
                 rest /= side;
             }
             const int cheb = max(abs(o[0]), max(abs(o[1]), abs(o[2])));
-            if (cheb != r) continue;  // interior: visited in an earlier ring
+            if (cheb != r && r != kFirst) continue;  // interior: visited in an earlier ring
             int cc[3];
             bool inside = true;
             for (int j = 0; j < 3; ++j) {
@@ -440,18 +450,19 @@ static void grid_knn_d(const GridDev &G, int32_t d, const double *q, int64_t nq,
     const dim3 grid((unsigned)((nq + 255) / 256));
     static const bool per_lane = getenv("MPT_NN1_PER_LANE") != nullptr;  // experiment knob
     static const int group = getenv("MPT_NN1_GROUP") ? atoi(getenv("MPT_NN1_GROUP")) : 16;
-    if (k == 1 && !per_lane && group == 64)
-        hipLaunchKernelGGL((k_grid_nn1_group<D, 64>), dim3((unsigned)((nq * 64 + 255) / 256)), dim3(256), 0, stream, G,
-                           d, q, nq, ids, d2);
-    else if (k == 1 && !per_lane && group == 32)
-        hipLaunchKernelGGL((k_grid_nn1_group<D, 32>), dim3((unsigned)((nq * 32 + 255) / 256)), dim3(256), 0, stream, G,
-                           d, q, nq, ids, d2);
+    static const int first = getenv("MPT_NN1_FIRST_RING") ? atoi(getenv("MPT_NN1_FIRST_RING")) : 0;
+    if (k == 1 && !per_lane && group == 32)
+        hipLaunchKernelGGL((k_grid_nn1_group<D, 32, 1>), dim3((unsigned)((nq * 32 + 255) / 256)), dim3(256), 0, stream,
+                           G, d, q, nq, ids, d2);
     else if (k == 1 && !per_lane && group == 8)
-        hipLaunchKernelGGL((k_grid_nn1_group<D, 8>), dim3((unsigned)((nq * 8 + 255) / 256)), dim3(256), 0, stream, G,
+        hipLaunchKernelGGL((k_grid_nn1_group<D, 8, 0>), dim3((unsigned)((nq * 8 + 255) / 256)), dim3(256), 0, stream, G,
                            d, q, nq, ids, d2);
+    else if (k == 1 && !per_lane && first == 1)
+        hipLaunchKernelGGL((k_grid_nn1_group<D, 16, 1>), dim3((unsigned)((nq * 16 + 255) / 256)), dim3(256), 0, stream,
+                           G, d, q, nq, ids, d2);
     else if (k == 1 && !per_lane)
-        hipLaunchKernelGGL((k_grid_nn1_group<D, 16>), dim3((unsigned)((nq * 16 + 255) / 256)), dim3(256), 0, stream, G,
-                           d, q, nq, ids, d2);
+        hipLaunchKernelGGL((k_grid_nn1_group<D, 16, 0>), dim3((unsigned)((nq * 16 + 255) / 256)), dim3(256), 0, stream,
+                           G, d, q, nq, ids, d2);
     else if (k == 1)
         hipLaunchKernelGGL((k_grid_knn<D, 1>), grid, dim3(256), 0, stream, G, d, q, nq, k, ids, d2);
     else if (k <= 16)

@@ -133,7 +133,8 @@ struct CollideScratch {
     Cand *cand = nullptr;           // [n_cwaves][cand_cap]
     uint32_t *cand_count = nullptr; // [n_cwaves]
     Cand *spill = nullptr;          // [spill_cap] shared overflow of full candidate segments
-    uint32_t *ctl = nullptr;        // [1] overflow units, [2] spill count
+    uint32_t *ctl = nullptr;        // 2 x [4]: [1] overflow units, [2] spill count (double-buffered)
+    int32_t ctl_par = 0;            // the half the next launch uses
     int32_t *ovf_list = nullptr;    // [ovf_cap]
     int64_t ovf_cap = 0, n_seg = 0;
     int32_t pair_cap = 0, cand_cap = 0, spill_cap = 0, n_cwaves = 0;

@@ -131,9 +131,11 @@ __global__ void k_sample(EngineParams p, uint64_t ext_base, int32_t K, double *_
 // [k*pmax + i][L][12] and pcount[k].
 __global__ void k_steer(EngineParams p, uint64_t ext_base, int32_t K, const double *__restrict__ nodes,
                         const int32_t *__restrict__ nn, double *__restrict__ ends, double *__restrict__ poses,
-                        int32_t *__restrict__ pcount, unsigned long long *__restrict__ counters) {
+                        int32_t *__restrict__ pcount, uint8_t *__restrict__ verdict,
+                        unsigned long long *__restrict__ counters) {
     const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= K) return;
+    verdict[k] = 0;  // the collision stage only ever sets verdicts
     const uint64_t g = ext_base + (uint64_t)k;
     const int d = p.d;
     double from[kMaxDim], end[kMaxDim];
@@ -589,10 +591,9 @@ extern "C" mpt_status mpt_rrt_step(mpt_rrt *r, int32_t K, void *stream_) {
         }
         mark(3);
         hipLaunchKernelGGL(k_steer, dim3(kb), dim3(256), 0, stream, p, r->ext_base, K, r->d_nodes, r->d_nn, r->d_ends,
-                           r->d_poses, r->d_pcount, r->d_counters);
+                           r->d_poses, r->d_pcount, r->d_verdict, r->d_counters);
         hip_check(hipGetLastError(), "k_steer");
         mark(4);
-        hip_check(hipMemsetAsync(r->d_verdict, 0, (size_t)K, stream), "verdict memset");
         CollideWork cw{};
         cw.poses = r->d_poses;
         cw.pose_edge = nullptr;

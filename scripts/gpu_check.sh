@@ -11,7 +11,7 @@ run() {  # name timeout cmd...
   tail -4 "gpurun_out/$name.log"
   return $rc
 }
-run pytest_gpu 800 python -m pytest tests -m gpu -q -p no:cacheprovider -ra; rc=$?
+run pytest_gpu 800 python -u -m pytest tests -m gpu -x -q -p no:cacheprovider -ra --timeout 120 --timeout-method thread; rc=$?
 [ $rc -gt 1 ] && exit $rc
 run smoke 180 python -c "import __graft_entry__ as g; g.smoke()"; rc=$?
 [ $rc -gt 1 ] && exit $rc
