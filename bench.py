@@ -121,18 +121,24 @@ def stage_bytes(stage, c, K, n0, d, pmax):
     return None
 
 
+NN_KERNEL = {"grid": "k_grid_nn1_group", "tree": "k_tree_nn1", "brute": "k_knn1"}
+
+
 def roofline(per_launch, cst, K, n0, d, pmax, nn_mode, traffic_path):
     """Roofline of the round's dominant kernel: achieved = its algorithmic bytes per launch
     / its hipEvent-measured duration (per-stage events on the engine's stream); every
     stage's figure is listed under `stages`."""
     stages = {}
-    for s in STAGE_KERNEL:
+    kernels = dict(STAGE_KERNEL, nn_query=NN_KERNEL.get(nn_mode, STAGE_KERNEL["nn_query"]))
+    if nn_mode == "tree":
+        kernels["nn_build"] = "k_pt_gather"
+    for s in kernels:
         ms = per_launch.get(s, 0.0)
         b = stage_bytes(s, cst, K, n0, d, pmax)
         if ms <= 0 or b is None:
             continue
         gbs = b / (ms * 1e-3) / 1e9
-        stages[s] = {"kernel": STAGE_KERNEL[s], "ms": round(ms, 4), "bytes": int(b), "achieved_gbs": round(gbs, 1),
+        stages[s] = {"kernel": kernels[s], "ms": round(ms, 4), "bytes": int(b), "achieved_gbs": round(gbs, 1),
                      "frac": round(gbs / HBM_PEAK_GBS, 4)}
     dominant = max(stages, key=lambda s: stages[s]["ms"])
     st = stages[dominant]
@@ -241,7 +247,7 @@ def run_seeds(args, world, rank, dist, torch, mpt, multiseed, scenes):
     torch.cuda.synchronize()
     cst = e0.collide_stats(False)
     per_launch = e0.kernel_times()
-    roof = roofline(per_launch, cst, K, n_before, sc.dim, e0.info()["pmax"], args.nn, args.traffic)
+    roof = roofline(per_launch, cst, K, n_before, sc.dim, e0.info()["pmax"], e0.last_nn(), args.traffic)
     import hashlib
 
     all_digest = hashlib.sha256("".join(digests[i] for i in sorted(digests)).encode()).hexdigest()
@@ -356,7 +362,7 @@ def main():
     eng.collide_stats(True)
     round_()
     cst = eng.collide_stats(False)
-    roof = roofline(per_launch, cst, K, n0, sc.dim, eng.info()["pmax"], args.nn, args.traffic)
+    roof = roofline(per_launch, cst, K, n0, sc.dim, eng.info()["pmax"], eng.last_nn(), args.traffic)
 
     out = {
         "metric": "valid RRT edge extensions/sec (collision+NN) per node, 1/2/4/8 MI355X",

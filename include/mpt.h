@@ -211,6 +211,9 @@ mpt_status mpt_rrt_enable_timing(mpt_rrt *rrt, int32_t enable);
  * for trees that do not fill the sampling box), grid occupancy target (points per cell,
  * <= 0 keeps the current value, default 2).  Results are identical. */
 mpt_status mpt_rrt_set_nn(mpt_rrt *rrt, int32_t mode, double points_per_cell);
+/* NN structure the last round used (MPT_NN_BRUTE / _GRID / _TREE; what MPT_NN_AUTO chose),
+ * -1 before the first round. */
+mpt_status mpt_rrt_last_nn(const mpt_rrt *rrt, int32_t *mode);
 /* Collision work counters accumulated since the previous call (synchronises), then reset;
  * enable = 1 keeps counting in later rounds (atomics: off for timed runs).
  * out [16] (may be NULL): [0] (pose, link) units, [1] agent clusters past the root cull,

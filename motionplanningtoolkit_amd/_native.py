@@ -68,6 +68,7 @@ SIGNATURES = {
     "mpt_rrt_last_round": (I32, [P, P, P, P, P]),
     "mpt_rrt_last_poses": (I32, [P, P, P]),
     "mpt_rrt_info": (I32, [P, P]),
+    "mpt_rrt_last_nn": (I32, [P, P]),
     "mpt_rrt_enable_timing": (I32, [P, I32]),
     "mpt_rrt_set_nn": (I32, [P, I32, D]),
     "mpt_rrt_collide_stats": (I32, [P, I32, P]),

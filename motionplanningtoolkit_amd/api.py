@@ -318,6 +318,12 @@ class RRTEngine:
         check(lib().mpt_rrt_last_poses(self.handle, _p(poses), _p(counts)), "mpt_rrt_last_poses")
         return poses, counts
 
+    def last_nn(self) -> str:
+        """NN structure the last round used: 'brute' | 'grid' | 'tree' ('' before any round)."""
+        m = C.c_int32(-1)
+        check(lib().mpt_rrt_last_nn(self.handle, C.byref(m)), "mpt_rrt_last_nn")
+        return {1: "brute", 2: "grid", 3: "tree"}.get(m.value, "")
+
     def enable_timing(self, on: bool = True) -> None:
         check(lib().mpt_rrt_enable_timing(self.handle, 1 if on else 0), "mpt_rrt_enable_timing")
 

@@ -53,6 +53,7 @@ private:
 void launch_grid_knn(const GridDev &G, int32_t d, const double *q, int64_t nq, int32_t k, int32_t *ids, double *d2,
                      hipStream_t stream);
 
+
 // Per-dim [min, max] of pts[0, n) into d_out[2*d] (lo0, hi0, lo1, hi1, ...).
 void launch_bbox(const double *pts, int64_t n, int32_t d, double *d_out, hipStream_t stream);
 

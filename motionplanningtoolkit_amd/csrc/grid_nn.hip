@@ -343,16 +343,11 @@ int32_t choose_grid_dims(int32_t d, const double *lohi, int32_t dims[3]) {
 // kFirst = the ring the walk starts at: with kFirst = 1 the centre cell and ring 1 (the 3^gd
 // block) are one pass, so the group spends one dependent cell -> point load chain less per
 // query (ring 0 alone keeps 15 of 16 lanes idle and seldom settles the query).
+// One query qi for the kGroup lanes of a group (sub = lane in the group; group-uniform call).
 template <int D, int kGroup, int kFirst>
-__global__ __launch_bounds__(256) void k_grid_nn1_group(GridDev G, int32_t d, const double *__restrict__ q,
-                                                        int64_t nq, int32_t *__restrict__ out_ids,
-                                                        double *__restrict__ out_d2) {
+__device__ __forceinline__ void nn1_group_query(const GridDev &G, int32_t d, const double *__restrict__ q, int64_t qi,
+                                                int sub, int32_t *__restrict__ out_ids, double *__restrict__ out_d2) {
     constexpr int DD = D > 0 ? D : 16;
-    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const int64_t slot = t / kGroup;
-    const int sub = (int)(t % kGroup);
-    if (slot >= nq) return;  // whole groups leave together (nq is per group)
-    const int64_t qi = slot;
     const GridParams &g = G.g;
     const int dim = D > 0 ? D : d;
     double qq[DD];
@@ -444,31 +439,42 @@ __global__ __launch_bounds__(256) void k_grid_nn1_group(GridDev G, int32_t d, co
     }
 }
 
+template <int D, int kGroup, int kFirst>
+__global__ __launch_bounds__(256) void k_grid_nn1_group(GridDev G, int32_t d, const double *__restrict__ q,
+                                                        int64_t nq, int32_t *__restrict__ out_ids,
+                                                        double *__restrict__ out_d2) {
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t slot = t / kGroup;
+    if (slot >= nq) return;  // whole groups leave together (nq is per group)
+    nn1_group_query<D, kGroup, kFirst>(G, d, q, slot, (int)(t % kGroup), out_ids, out_d2);
+}
+
 template <int D>
 static void grid_knn_d(const GridDev &G, int32_t d, const double *q, int64_t nq, int32_t k, int32_t *ids, double *d2,
                        hipStream_t stream) {
     const dim3 grid((unsigned)((nq + 255) / 256));
     static const bool per_lane = getenv("MPT_NN1_PER_LANE") != nullptr;  // experiment knob
-    static const int group = getenv("MPT_NN1_GROUP") ? atoi(getenv("MPT_NN1_GROUP")) : 16;
-    static const int first = getenv("MPT_NN1_FIRST_RING") ? atoi(getenv("MPT_NN1_FIRST_RING")) : 0;
-    if (k == 1 && !per_lane && group == 32)
-        hipLaunchKernelGGL((k_grid_nn1_group<D, 32, 1>), dim3((unsigned)((nq * 32 + 255) / 256)), dim3(256), 0, stream,
-                           G, d, q, nq, ids, d2);
-    else if (k == 1 && !per_lane && group == 8)
-        hipLaunchKernelGGL((k_grid_nn1_group<D, 8, 0>), dim3((unsigned)((nq * 8 + 255) / 256)), dim3(256), 0, stream, G,
-                           d, q, nq, ids, d2);
-    else if (k == 1 && !per_lane && first == 1)
-        hipLaunchKernelGGL((k_grid_nn1_group<D, 16, 1>), dim3((unsigned)((nq * 16 + 255) / 256)), dim3(256), 0, stream,
-                           G, d, q, nq, ids, d2);
-    else if (k == 1 && !per_lane)
-        hipLaunchKernelGGL((k_grid_nn1_group<D, 16, 0>), dim3((unsigned)((nq * 16 + 255) / 256)), dim3(256), 0, stream,
-                           G, d, q, nq, ids, d2);
-    else if (k == 1)
+    // 32 lanes per query and rings 0 + 1 as the first pass (the 27 cells of the 3^3 block in one
+    // step): 12 % faster than 16 lanes from ring 0 on config 2 (MPT_NN1_GROUP / _FIRST_RING: A/B)
+    static const int group = getenv("MPT_NN1_GROUP") ? atoi(getenv("MPT_NN1_GROUP")) : 32;
+    static const int first = getenv("MPT_NN1_FIRST_RING") ? atoi(getenv("MPT_NN1_FIRST_RING")) : 1;
+#define MPT_NN1_GROUP_LAUNCH(GRP, FIRST)                                                                        \
+    hipLaunchKernelGGL((k_grid_nn1_group<D, GRP, FIRST>), dim3((unsigned)((nq * GRP + 255) / 256)), dim3(256), 0, \
+                       stream, G, d, q, nq, ids, d2)
+    if (k == 1 && !per_lane && group == 32) {
+        if (first) MPT_NN1_GROUP_LAUNCH(32, 1); else MPT_NN1_GROUP_LAUNCH(32, 0);
+    } else if (k == 1 && !per_lane && group == 8) {
+        MPT_NN1_GROUP_LAUNCH(8, 0);
+    } else if (k == 1 && !per_lane) {
+        if (first) MPT_NN1_GROUP_LAUNCH(16, 1); else MPT_NN1_GROUP_LAUNCH(16, 0);
+    } else if (k == 1) {
         hipLaunchKernelGGL((k_grid_knn<D, 1>), grid, dim3(256), 0, stream, G, d, q, nq, k, ids, d2);
-    else if (k <= 16)
+    } else if (k <= 16) {
         hipLaunchKernelGGL((k_grid_knn<D, 16>), grid, dim3(256), 0, stream, G, d, q, nq, k, ids, d2);
-    else
+    } else {
         hipLaunchKernelGGL((k_grid_knn<D, 32>), grid, dim3(256), 0, stream, G, d, q, nq, k, ids, d2);
+    }
+#undef MPT_NN1_GROUP_LAUNCH
 }
 
 void launch_grid_knn(const GridDev &G, int32_t d, const double *q, int64_t nq, int32_t k, int32_t *ids, double *d2,

@@ -297,20 +297,40 @@ __global__ void k_set_n(int64_t *n_dev, int64_t n, unsigned long long *counters)
 }
 
 // Spread of the live nodes over the spatial dims (for MPT_NN_AUTO): per-dim min / max as
-// order-preserving 64-bit keys, out[0..gd) = min, out[3..3+gd) = max (pre-set to ~0 / 0).
+// order-preserving 64-bit keys, out[0..3) = min, out[3..6) = max (unused dims: ~0 / 0).
 __device__ __forceinline__ unsigned long long order_key(double x) {
     const unsigned long long b = (unsigned long long)__double_as_longlong(x);
     return (b >> 63) ? ~b : (b | 0x8000000000000000ull);
 }
-__global__ __launch_bounds__(256) void k_spread(const double *__restrict__ nodes, const int64_t *__restrict__ n_dev,
-                                                int32_t d, int32_t gd, unsigned long long *__restrict__ out) {
-    __shared__ unsigned long long s_min[3], s_max[3];
-    if (threadIdx.x < 3) {
-        s_min[threadIdx.x] = ~0ull;
-        s_max[threadIdx.x] = 0ull;
+constexpr int kSpreadBlocks = 128;
+
+__device__ __forceinline__ unsigned long long wave_min_u64(unsigned long long v) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        const unsigned long long o = __shfl_xor(v, off);
+        v = o < v ? o : v;
     }
-    __syncthreads();
+    return v;
+}
+__device__ __forceinline__ unsigned long long wave_max_u64(unsigned long long v) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        const unsigned long long o = __shfl_xor(v, off);
+        v = o > v ? o : v;
+    }
+    return v;
+}
+
+// One launch, no memsets: each block reduces its stride of nodes (shuffles, then one LDS
+// slot per wave) into partial[block][6]; the last block to finish (ticket) folds the
+// partials, writes the result straight into mapped pinned host memory and re-arms the ticket.
+__global__ __launch_bounds__(256) void k_spread(const double *__restrict__ nodes, const int64_t *__restrict__ n_dev,
+                                                int32_t d, int32_t gd, unsigned long long *__restrict__ partial,
+                                                unsigned int *__restrict__ ticket, unsigned long long *host_out) {
+    __shared__ unsigned long long s_v[4][6];
+    __shared__ bool s_last;
     const int64_t n = *n_dev;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     unsigned long long mn[3] = {~0ull, ~0ull, ~0ull}, mx[3] = {0, 0, 0};
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
         for (int j = 0; j < gd; ++j) {
@@ -318,15 +338,41 @@ __global__ __launch_bounds__(256) void k_spread(const double *__restrict__ nodes
             mn[j] = k < mn[j] ? k : mn[j];
             mx[j] = k > mx[j] ? k : mx[j];
         }
-    for (int j = 0; j < gd; ++j) {
-        atomicMin(&s_min[j], mn[j]);
-        atomicMax(&s_max[j], mx[j]);
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+        mn[j] = wave_min_u64(mn[j]);
+        mx[j] = wave_max_u64(mx[j]);
     }
+    if (lane == 0)
+        for (int j = 0; j < 3; ++j) {
+            s_v[wave][j] = mn[j];
+            s_v[wave][3 + j] = mx[j];
+        }
     __syncthreads();
-    if (threadIdx.x < (unsigned)gd) {
-        atomicMin(out + threadIdx.x, s_min[threadIdx.x]);
-        atomicMax(out + 3 + threadIdx.x, s_max[threadIdx.x]);
+    if (threadIdx.x < 6) {
+        const int j = threadIdx.x;
+        unsigned long long v = s_v[0][j];
+        for (int w = 1; w < 4; ++w) v = j < 3 ? (s_v[w][j] < v ? s_v[w][j] : v) : (s_v[w][j] > v ? s_v[w][j] : v);
+        partial[blockIdx.x * 6 + j] = v;
     }
+    __threadfence();
+    __syncthreads();
+    if (threadIdx.x == 0) s_last = atomicAdd(ticket, 1u) == gridDim.x - 1;
+    __syncthreads();
+    if (!s_last) return;
+    __threadfence();
+    if (threadIdx.x < 6) {
+        const int j = threadIdx.x;
+        const volatile unsigned long long *pv = partial;
+        unsigned long long v = pv[j];
+        for (unsigned b = 1; b < gridDim.x; ++b) {
+            const unsigned long long o = pv[b * 6 + j];
+            v = j < 3 ? (o < v ? o : v) : (o > v ? o : v);
+        }
+        host_out[j] = v;
+    }
+    if (threadIdx.x == 0) *ticket = 0u;
+    __threadfence_system();
 }
 
 double key_value(unsigned long long k) {
@@ -368,9 +414,10 @@ struct mpt_rrt {
     // MPT_NN_AUTO feedback: the live nodes' spatial spread, copied back after each round and
     // read at a later round once its event has completed (never waited for; the NN choice
     // changes only speed, results are identical)
-    unsigned long long *d_spread = nullptr, *h_spread = nullptr;
+    unsigned long long *d_spread = nullptr, *h_spread = nullptr, *h_spread_dev = nullptr;
     hipEvent_t ev_spread = nullptr;
     bool spread_pending = false, auto_tree = false;
+    int32_t last_nn = -1;  // structure the last round used (mpt_rrt_last_nn)
     // optional collision work counters (k_collide atomics): units, clusters, node visits, tri tests
     bool stats_on = false;
     CollideScratch cscratch;
@@ -380,8 +427,9 @@ struct mpt_rrt {
 
 namespace {
 void rfree(mpt_rrt *r) {
-    void *ps[] = {r->d_links, r->d_nodes, r->d_parents, r->d_n,  r->d_counters, r->d_samples, r->d_ends, r->d_poses,
-                  r->d_nnd2,  r->d_nn,    r->d_pcount,  r->d_bcount, r->d_verdict, r->d_scratch, r->d_cstats};
+    void *ps[] = {r->d_links, r->d_nodes,   r->d_parents, r->d_n,       r->d_counters, r->d_samples,
+                  r->d_ends,  r->d_poses,   r->d_nnd2,    r->d_nn,      r->d_pcount,   r->d_bcount,
+                  r->d_verdict, r->d_scratch, r->d_cstats};
     for (void *p : ps)
         if (p) (void)hipFree(p);
     for (auto &e : r->ev)
@@ -533,10 +581,6 @@ extern "C" mpt_status mpt_rrt_step(mpt_rrt *r, int32_t K, void *stream_) {
         auto mark = [&](int i) {
             if (r->timing) hip_check(hipEventRecord(r->ev[i], stream), "event record");
         };
-        mark(0);
-        hipLaunchKernelGGL(k_sample, dim3(kb), dim3(256), 0, stream, p, r->ext_base, K, r->d_samples);
-        hip_check(hipGetLastError(), "k_sample");
-        mark(1);
         if (r->nn_mode == MPT_NN_AUTO && r->spread_pending && hipEventQuery(r->ev_spread) == hipSuccess) {
             // the tree fills less than a quarter of the sampling box: most samples are far
             // from every node, where the grid walks empty rings and the Morton tree does not
@@ -553,6 +597,11 @@ extern "C" mpt_status mpt_rrt_step(mpt_rrt *r, int32_t K, void *stream_) {
         const bool big = r->n_upper >= 4096;
         const bool use_tree = r->nn_mode == MPT_NN_TREE || (r->nn_mode == MPT_NN_AUTO && big && r->auto_tree);
         const bool use_grid = !use_tree && (r->nn_mode == MPT_NN_GRID || (r->nn_mode == MPT_NN_AUTO && big));
+        r->last_nn = use_tree ? MPT_NN_TREE : (use_grid ? MPT_NN_GRID : MPT_NN_BRUTE);
+        mark(0);
+        hipLaunchKernelGGL(k_sample, dim3(kb), dim3(256), 0, stream, p, r->ext_base, K, r->d_samples);
+        hip_check(hipGetLastError(), "k_sample");
+        mark(1);
         if (use_tree) {
             r->ptree->reserve(r->cap, p.d);  // once: no allocation (device sync) in later rounds
             r->ptree->build(r->d_nodes, r->n_upper, r->d_n, p.d, stream);
@@ -622,17 +671,20 @@ extern "C" mpt_status mpt_rrt_step(mpt_rrt *r, int32_t K, void *stream_) {
         mark(9);
         if (r->nn_mode == MPT_NN_AUTO && !r->spread_pending) {
             if (!r->d_spread) {
-                hip_check(hipMalloc(&r->d_spread, sizeof(unsigned long long) * 6), "alloc spread");
-                hip_check(hipHostMalloc(&r->h_spread, sizeof(unsigned long long) * 6), "alloc spread");
+                // partials [kSpreadBlocks][6] + the ticket; the result goes to mapped pinned memory
+                const size_t bytes = sizeof(unsigned long long) * (kSpreadBlocks * 6 + 1);
+                hip_check(hipMalloc(&r->d_spread, bytes), "alloc spread");
+                hip_check(hipMemset(r->d_spread, 0, bytes), "zero spread");
+                hip_check(hipHostMalloc(&r->h_spread, sizeof(unsigned long long) * 6,
+                                        hipHostMallocMapped | hipHostMallocCoherent), "alloc spread");
+                hip_check(hipHostGetDevicePointer(reinterpret_cast<void **>(&r->h_spread_dev), r->h_spread, 0),
+                          "spread device pointer");
                 hip_check(hipEventCreateWithFlags(&r->ev_spread, hipEventDisableTiming), "event");
             }
-            hip_check(hipMemsetAsync(r->d_spread, 0xff, sizeof(unsigned long long) * 3, stream), "spread memset");
-            hip_check(hipMemsetAsync(r->d_spread + 3, 0, sizeof(unsigned long long) * 3, stream), "spread memset");
-            hipLaunchKernelGGL(k_spread, dim3(64), dim3(256), 0, stream, r->d_nodes, r->d_n, p.d, r->grid_gd,
-                               r->d_spread);
+            hipLaunchKernelGGL(k_spread, dim3(kSpreadBlocks), dim3(256), 0, stream, r->d_nodes, r->d_n, p.d,
+                               r->grid_gd, r->d_spread,
+                               reinterpret_cast<unsigned int *>(r->d_spread + kSpreadBlocks * 6), r->h_spread_dev);
             hip_check(hipGetLastError(), "k_spread");
-            hip_check(hipMemcpyAsync(r->h_spread, r->d_spread, sizeof(unsigned long long) * 6, hipMemcpyDeviceToHost,
-                                     stream), "spread D2H");
             hip_check(hipEventRecord(r->ev_spread, stream), "spread event");
             r->spread_pending = true;
         }
@@ -686,6 +738,13 @@ extern "C" mpt_status mpt_rrt_last_poses(mpt_rrt *r, double *poses, int32_t *pos
                       "poses D2H");
         if (pose_counts)
             hip_check(hipMemcpy(pose_counts, r->d_pcount, sizeof(int32_t) * K, hipMemcpyDeviceToHost), "pcount D2H");
+    });
+}
+
+extern "C" mpt_status mpt_rrt_last_nn(const mpt_rrt *r, int32_t *mode) {
+    return guarded([&] {
+        if (!r || !mode) throw Error{MPT_ERR_INVALID, "null pointer"};
+        *mode = r->last_nn;
     });
 }
 
