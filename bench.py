@@ -44,7 +44,8 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample length")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--nn", default="auto", choices=["grid", "brute", "auto", "tree"], help="engine NN structure")
-    ap.add_argument("--ppc", type=float, default=2.0, help="grid points per cell")
+    ap.add_argument("--ppc", type=float, default=0.0,
+                    help="grid points per cell (0: the engine's default, 2 floored by the expected NN distance)")
     ap.add_argument("--traffic", default=None, help="pmc_summary.json (default: latest profiles/r*/)")
     ap.add_argument("--seeds", type=int, default=0,
                     help="config 5: this many independent blimp RRTs (seed_base + i) sharded over the ranks "
@@ -93,7 +94,7 @@ def cpu_baseline(sc, tree, K_gpu, seed, target_s):
 
 
 # Stage -> the kernel that does its work (kernel names as rocprofv3 reports them).
-STAGE_KERNEL = {"nn_query": "k_grid_nn1_group", "collide_pairs": "k_pairs", "collide_cands": "k_cands",
+STAGE_KERNEL = {"nn_query": "k_grid_nn1_runs", "collide_pairs": "k_pairs", "collide_cands": "k_cands",
                 "collide_narrow": "k_narrow", "nn_build": "k_grid_scatter", "steer": "k_steer",
                 "sample": "k_sample", "append": "k_append"}
 
@@ -121,7 +122,7 @@ def stage_bytes(stage, c, K, n0, d, pmax):
     return None
 
 
-NN_KERNEL = {"grid": "k_grid_nn1_group", "tree": "k_tree_nn1", "brute": "k_knn1"}
+NN_KERNEL = {"grid": "k_grid_nn1_runs", "tree": "k_tree_nn1", "brute": "k_knn1"}
 
 
 def roofline(per_launch, cst, K, n0, d, pmax, nn_mode, traffic_path):

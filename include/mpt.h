@@ -209,7 +209,8 @@ mpt_status mpt_rrt_info(const mpt_rrt *rrt, int64_t info[4]);
 mpt_status mpt_rrt_enable_timing(mpt_rrt *rrt, int32_t enable);
 /* NN structure of the rounds: MPT_NN_AUTO / _BRUTE / _GRID / _TREE (packed Morton tree,
  * for trees that do not fill the sampling box), grid occupancy target (points per cell,
- * <= 0 keeps the current value, default 2).  Results are identical. */
+ * <= 0: the default, 2 points per cell with the cell side floored at 0.4x the expected NN
+ * distance over all state dims).  Results are identical. */
 mpt_status mpt_rrt_set_nn(mpt_rrt *rrt, int32_t mode, double points_per_cell);
 /* NN structure the last round used (MPT_NN_BRUTE / _GRID / _TREE; what MPT_NN_AUTO chose),
  * -1 before the first round. */

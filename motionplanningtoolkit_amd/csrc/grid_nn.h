@@ -23,16 +23,49 @@ struct GridDev {
     unsigned long long *stats;  // optional [2]: points examined, cells visited (1-NN kernel)
 };
 
-// h chosen for about `ppc` points per cell, capped at 4 cells per point and 2^25 cells.
+// Optional by-product of an index build (the engine's MPT_NN_AUTO feedback): the live
+// points' min / max over up to three state dims as order-preserving 64-bit keys, written
+// to host_out[0..3) (min) and host_out[3..6) (max) -- mapped pinned memory -- by the build
+// itself, so no extra pass over the nodes.  Unused dims: ~0 / 0.
+struct SpreadOut {
+    int32_t gd = 0;
+    int32_t dims[3] = {0, 0, 0};
+    unsigned long long *partial = nullptr;  // [blocks][6] per-block partials (grid build), device
+    unsigned long long *host_out = nullptr; // [6], device pointer of mapped host memory
+};
+
+__host__ __device__ __forceinline__ unsigned long long order_key_u64(double x) {
+    unsigned long long b;
+    __builtin_memcpy(&b, &x, sizeof b);
+    return (b >> 63) ? ~b : (b | 0x8000000000000000ull);
+}
+__host__ __device__ __forceinline__ double key_value_u64(unsigned long long k) {
+    const unsigned long long b = (k >> 63) ? (k & 0x7fffffffffffffffull) : ~k;
+    double x;
+    __builtin_memcpy(&x, &b, sizeof x);
+    return x;
+}
+
+// h chosen for about `ppc` points per cell and at least h_min, capped at 4 cells per point
+// and 2^25 cells.
 GridParams make_grid_params(int32_t d, const int32_t *dims, int32_t gd, const double *lo, const double *hi, int64_t n,
-                            double ppc);
+                            double ppc, double h_min = 0.0);
+
+// Expected nearest-neighbour distance of n points uniform over the box [lo, hi]^d (dims of
+// zero width ignored): the radius r with n * vol(ball_r) = vol(box).  When many state dims
+// lie outside the grid (the snake: 13 of 15), r is far above the ppc-sized cell, and the
+// walk pays per-cell overhead for cells that never prune; the engine floors h at a fraction
+// of r.
+double expected_nn_distance(int32_t d, const double *lo, const double *hi, int64_t n);
 
 class GridIndex {
 public:
     ~GridIndex();
     // Index points [0, min(n_upper, *n_dev)) of pts [.][d]; stream-ordered, no host sync.
+    // spread (optional): also reduce the points' spread into spread->host_out (partial needs
+    // ceil(n_upper / 256) * 6 slots).
     void build(const double *pts, int64_t n_upper, const int64_t *n_dev, int32_t d, const GridParams &g,
-               hipStream_t stream);
+               hipStream_t stream, const SpreadOut *spread = nullptr);
     GridDev dev() const;
     const GridParams &params() const { return g; }
     // allocate for up to cap_pts points and ncells cells now (allocation synchronises the

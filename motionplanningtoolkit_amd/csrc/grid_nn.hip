@@ -16,6 +16,7 @@
 // scatter of coordinates and ids into cell order.  The in-cell order is arbitrary, which
 // cannot change any result (all ties resolve by id).
 #include <algorithm>
+#include <cstring>
 
 #include <hipcub/hipcub.hpp>
 
@@ -30,22 +31,106 @@ __device__ __forceinline__ int cell_coord(double x, double lo, double inv_h, int
     return (int)c;
 }
 
-__global__ void k_grid_count(GridParams g, const double *__restrict__ pts, int32_t d, int64_t n,
-                             const int64_t *__restrict__ n_dev, int32_t *__restrict__ cell_of,
-                             int32_t *__restrict__ counts) {
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (n_dev) n = *n_dev < n ? *n_dev : n;
-    if (i >= n) return;
-    int c[3] = {0, 0, 0};
-    for (int j = 0; j < g.gd; ++j) c[j] = cell_coord(pts[i * d + g.dims[j]], g.lo[j], g.inv_h, g.n[j]);
-    const int32_t cell = (c[0] * g.n[1] + c[1]) * g.n[2] + c[2];
-    cell_of[i] = cell;
-    atomicAdd(counts + cell, 1);
+__device__ __forceinline__ unsigned long long wave_min_u64(unsigned long long v) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        const unsigned long long o = __shfl_xor(v, off);
+        v = o < v ? o : v;
+    }
+    return v;
+}
+__device__ __forceinline__ unsigned long long wave_max_u64(unsigned long long v) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        const unsigned long long o = __shfl_xor(v, off);
+        v = o > v ? o : v;
+    }
+    return v;
 }
 
-__global__ void k_grid_scatter(const double *__restrict__ pts, int32_t d, int64_t n, const int64_t *__restrict__ n_dev,
-                               const int32_t *__restrict__ cell_of, const int32_t *__restrict__ cell_start,
-                               int32_t *__restrict__ cursor, double *__restrict__ spts, int32_t *__restrict__ sids) {
+// Block-wide fold of per-thread (min[3], max[3]) keys (blockDim.x == 256) into s_out[6],
+// visible to every thread of the block on return.
+__device__ __forceinline__ void block_fold_spread(unsigned long long (&mn)[3], unsigned long long (&mx)[3],
+                                                  unsigned long long (*s_v)[6], unsigned long long *s_out) {
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+        mn[j] = wave_min_u64(mn[j]);
+        mx[j] = wave_max_u64(mx[j]);
+    }
+    if (lane == 0)
+        for (int j = 0; j < 3; ++j) {
+            s_v[wave][j] = mn[j];
+            s_v[wave][3 + j] = mx[j];
+        }
+    __syncthreads();
+    if (threadIdx.x < 6) {
+        const int j = threadIdx.x;
+        unsigned long long v = s_v[0][j];
+        for (int w = 1; w < 4; ++w) v = j < 3 ? (s_v[w][j] < v ? s_v[w][j] : v) : (s_v[w][j] > v ? s_v[w][j] : v);
+        s_out[j] = v;
+    }
+    __syncthreads();
+}
+
+// Cell of every live point + histogram.  kSpread: the same pass also reduces the points'
+// spread (SpreadOut) into one partial per block (plain stores, no fence: the scatter kernel
+// that follows in the stream folds them).
+template <bool kSpread>
+__global__ __launch_bounds__(256) void k_grid_count(GridParams g, const double *__restrict__ pts, int32_t d,
+                                                    int64_t n, const int64_t *__restrict__ n_dev,
+                                                    int32_t *__restrict__ cell_of, int32_t *__restrict__ counts,
+                                                    SpreadOut sp) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (n_dev) n = *n_dev < n ? *n_dev : n;
+    if (i < n) {
+        int c[3] = {0, 0, 0};
+        for (int j = 0; j < g.gd; ++j) c[j] = cell_coord(pts[i * d + g.dims[j]], g.lo[j], g.inv_h, g.n[j]);
+        const int32_t cell = (c[0] * g.n[1] + c[1]) * g.n[2] + c[2];
+        cell_of[i] = cell;
+        atomicAdd(counts + cell, 1);
+    }
+    if constexpr (kSpread) {
+        __shared__ unsigned long long s_v[4][6], s_out[6];
+        unsigned long long mn[3] = {~0ull, ~0ull, ~0ull}, mx[3] = {0ull, 0ull, 0ull};
+        if (i < n) {
+#pragma unroll
+            for (int j = 0; j < 3; ++j)
+                if (j < sp.gd) mn[j] = mx[j] = order_key_u64(pts[i * d + sp.dims[j]]);
+        }
+        block_fold_spread(mn, mx, s_v, s_out);
+        if (threadIdx.x < 6) sp.partial[(int64_t)blockIdx.x * 6 + threadIdx.x] = s_out[threadIdx.x];
+    }
+}
+
+// Scatter into cell order.  kSpread: block 0 first folds k_grid_count's per-block spread
+// partials (n_part of them, all threads) and writes the result to mapped host memory.
+template <bool kSpread>
+__global__ __launch_bounds__(256) void k_grid_scatter(const double *__restrict__ pts, int32_t d, int64_t n,
+                                                      const int64_t *__restrict__ n_dev,
+                                                      const int32_t *__restrict__ cell_of,
+                                                      const int32_t *__restrict__ cell_start,
+                                                      int32_t *__restrict__ cursor, double *__restrict__ spts,
+                                                      int32_t *__restrict__ sids, SpreadOut sp, int32_t n_part) {
+    if constexpr (kSpread) {
+        if (blockIdx.x == 0) {
+            __shared__ unsigned long long s_v[4][6], s_out[6];
+            unsigned long long mn[3] = {~0ull, ~0ull, ~0ull}, mx[3] = {0ull, 0ull, 0ull};
+            for (int b = threadIdx.x; b < n_part; b += blockDim.x) {
+#pragma unroll
+                for (int j = 0; j < 3; ++j) {
+                    const unsigned long long lo = sp.partial[(int64_t)b * 6 + j];
+                    const unsigned long long hi = sp.partial[(int64_t)b * 6 + 3 + j];
+                    mn[j] = lo < mn[j] ? lo : mn[j];
+                    mx[j] = hi > mx[j] ? hi : mx[j];
+                }
+            }
+            block_fold_spread(mn, mx, s_v, s_out);
+            // fine-grained mapped memory: the stores go straight to the host; the event the
+            // engine records after the build orders them before the host reads
+            if (threadIdx.x < 6) sp.host_out[threadIdx.x] = s_out[threadIdx.x];
+        }
+    }
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (n_dev) n = *n_dev < n ? *n_dev : n;
     if (i >= n) return;
@@ -170,7 +255,7 @@ __global__ __launch_bounds__(256) void k_grid_knn(GridDev G, int32_t d, const do
 }
 
 GridParams make_grid_params(int32_t d, const int32_t *dims, int32_t gd, const double *lo, const double *hi, int64_t n,
-                            double ppc) {
+                            double ppc, double h_min) {
     GridParams g{};
     g.gd = gd;
     double vol = 1.0, span_max = 0.0;
@@ -188,6 +273,7 @@ GridParams make_grid_params(int32_t d, const int32_t *dims, int32_t gd, const do
     }
     const double cells_wanted = n > 0 ? (double)n / ppc : 1.0;
     double h = pow(vol / (cells_wanted > 1.0 ? cells_wanted : 1.0), 1.0 / gd);
+    h = h > h_min ? h : h_min;
     // cap the cell count (memory, scan length): at most 4 cells per point and 2^25 total
     for (;;) {
         double cells = 1.0;
@@ -254,7 +340,7 @@ GridIndex::~GridIndex() {
 }
 
 void GridIndex::build(const double *pts, int64_t n_upper, const int64_t *n_dev, int32_t d, const GridParams &gp,
-                      hipStream_t stream) {
+                      hipStream_t stream, const SpreadOut *spread) {
     if (gp.ncells >= (int64_t(1) << 31) - 1) throw Error{5, "grid too large"};
     reserve(n_upper, d, gp.ncells);
     g = gp;
@@ -263,15 +349,24 @@ void GridIndex::build(const double *pts, int64_t n_upper, const int64_t *n_dev, 
     counts_zero = false;
     if (n_upper > 0) {
         const unsigned blocks = (unsigned)((n_upper + 255) / 256);
-        hipLaunchKernelGGL(k_grid_count, dim3(blocks), dim3(256), 0, stream, g, pts, d, n_upper, n_dev, cell_of, counts);
+        if (spread)
+            hipLaunchKernelGGL(k_grid_count<true>, dim3(blocks), dim3(256), 0, stream, g, pts, d, n_upper, n_dev,
+                               cell_of, counts, *spread);
+        else
+            hipLaunchKernelGGL(k_grid_count<false>, dim3(blocks), dim3(256), 0, stream, g, pts, d, n_upper, n_dev,
+                               cell_of, counts, SpreadOut{});
         hip_check(hipGetLastError(), "k_grid_count");
     }
     size_t tb = temp_bytes;
     hip_check(hipcub::DeviceScan::ExclusiveSum(temp, tb, counts, cell_start, (int)(g.ncells + 1), stream), "scan");
     if (n_upper > 0) {
         const unsigned blocks = (unsigned)((n_upper + 255) / 256);
-        hipLaunchKernelGGL(k_grid_scatter, dim3(blocks), dim3(256), 0, stream, pts, d, n_upper, n_dev, cell_of,
-                           cell_start, counts, spts, sids);
+        if (spread)
+            hipLaunchKernelGGL(k_grid_scatter<true>, dim3(blocks), dim3(256), 0, stream, pts, d, n_upper, n_dev,
+                               cell_of, cell_start, counts, spts, sids, *spread, (int32_t)blocks);
+        else
+            hipLaunchKernelGGL(k_grid_scatter<false>, dim3(blocks), dim3(256), 0, stream, pts, d, n_upper, n_dev,
+                               cell_of, cell_start, counts, spts, sids, SpreadOut{}, 0);
         hip_check(hipGetLastError(), "k_grid_scatter");
     }
     counts_zero = true;  // k_grid_scatter counted every cell back down (nothing counted when n_upper == 0)
@@ -317,6 +412,19 @@ __global__ __launch_bounds__(256) void k_bbox(const double *__restrict__ pts, in
 void launch_bbox(const double *pts, int64_t n, int32_t d, double *d_out, hipStream_t stream) {
     hipLaunchKernelGGL(k_bbox, dim3((unsigned)d), dim3(256), 0, stream, pts, n, d, d_out);
     hip_check(hipGetLastError(), "k_bbox");
+}
+
+double expected_nn_distance(int32_t d, const double *lo, const double *hi, int64_t n) {
+    double log_v = 0.0;
+    int32_t de = 0;
+    for (int j = 0; j < d; ++j)
+        if (hi[j] > lo[j]) {
+            log_v += log(hi[j] - lo[j]);
+            ++de;
+        }
+    if (de == 0 || n < 1) return 0.0;
+    const double log_ball = 0.5 * de * log(M_PI) - lgamma(0.5 * de + 1.0);  // unit de-ball volume
+    return exp((log_v - log((double)n) - log_ball) / de);
 }
 
 int32_t choose_grid_dims(int32_t d, const double *lohi, int32_t dims[3]) {
@@ -449,6 +557,177 @@ __global__ __launch_bounds__(256) void k_grid_nn1_group(GridDev G, int32_t d, co
     nn1_group_query<D, kGroup, kFirst>(G, d, q, slot, (int)(t % kGroup), out_ids, out_d2);
 }
 
+// 1-NN over runs of cells.  Cells are laid out with the last grid dim contiguous, so the
+// cells of a pass that share their other coordinates form one run whose points are one
+// contiguous range [cell_start[first], cell_start[last + 1]):
+//   * first pass (r = 1, the 3^gd block): (2r+1)^(gd-1) runs of 2r+1 cells;
+//   * ring r >= 2: border columns give a full run of 2r+1 cells, interior columns only the
+//     two cells at +-r (two single-cell runs).
+// Each lane of the group takes run slots (2 per column), prunes a run whose box is farther
+// than its best so far, and loads the run's [start, end).  A shuffle scan of the run lengths
+// then spreads the pass's points evenly over the group, two per lane per step, both loads in
+// flight together (a lane no longer walks a whole cell point after point: the slowest lane
+// of the old cell-per-lane walk set every wave's time).  Merge, ring bound and (d2, id)
+// order as nn1_group_query, so results are identical bit for bit.
+template <int D, int kGroup, int kPts>
+__device__ __forceinline__ void nn1_runs_query(const GridDev &G, const double *__restrict__ q, int64_t qi, int sub,
+                                               int32_t *__restrict__ out_ids, double *__restrict__ out_d2) {
+    const GridParams &g = G.g;
+    double qq[D];
+#pragma unroll
+    for (int i = 0; i < D; ++i) qq[i] = q[qi * D + i];
+    double qg[3] = {0, 0, 0};
+    int cq[3] = {0, 0, 0};
+    const int gd = g.gd, zl = g.gd - 1;  // zl: the run (contiguous) dim
+    for (int j = 0; j < gd; ++j) {
+        const double x = q[qi * D + g.dims[j]];
+        qg[j] = x;
+        cq[j] = cell_coord(x, g.lo[j], g.inv_h, g.n[j]);
+    }
+    double bd = __builtin_huge_val();
+    int32_t bi = -1;
+    uint32_t n_pts = 0, n_cells = 0;
+    // box gap of cells [c0, c1] along grid dim j (border cells open outward), minus the slack
+    auto gap = [&](int j, int c0, int c1) {
+        const double clo = c0 == 0 ? -__builtin_huge_val() : g.lo[j] + (double)c0 * g.h;
+        const double chi = c1 == g.n[j] - 1 ? __builtin_huge_val() : g.lo[j] + (double)(c1 + 1) * g.h;
+        const double v = fmax(fmax(clo - qg[j], qg[j] - chi), 0.0) - g.slack;
+        return v > 0.0 ? v * v : 0.0;
+    };
+    for (int r = 1;; ++r) {
+        const int side = 2 * r + 1;
+        const int ncol = gd == 3 ? side * side : (gd == 2 ? side : 1);
+        for (int base = 0; base < 2 * ncol; base += kGroup) {
+            const int u = base + sub;
+            int32_t s = 0, len = 0;
+            if (u < 2 * ncol) {
+                const int col = u >> 1, part = u & 1;
+                int o0 = 0, o1 = 0;
+                if (gd == 3) {
+                    o0 = col / side - r;
+                    o1 = col % side - r;
+                } else if (gd == 2) {
+                    o0 = col - r;
+                }
+                const bool border = gd == 3 ? (abs(o0) == r || abs(o1) == r) : (gd == 2 ? abs(o0) == r : false);
+                const bool full = r == 1 || border;
+                bool ok = !(full && part);
+                int z0 = cq[zl] + (full ? -r : (part ? r : -r));
+                int z1 = cq[zl] + (full ? r : (part ? r : -r));
+                z0 = z0 < 0 ? 0 : z0;
+                z1 = z1 > g.n[zl] - 1 ? g.n[zl] - 1 : z1;
+                ok = ok && z0 <= z1;
+                int c0 = 0, c1 = 0;
+                if (gd >= 2) {
+                    c0 = cq[0] + o0;
+                    ok = ok && c0 >= 0 && c0 < g.n[0];
+                }
+                if (gd == 3) {
+                    c1 = cq[1] + o1;
+                    ok = ok && c1 >= 0 && c1 < g.n[1];
+                }
+                if (ok) {
+                    double lb2 = gap(zl, z0, z1);
+                    if (gd >= 2) lb2 += gap(0, c0, c0);
+                    if (gd == 3) lb2 += gap(1, c1, c1);
+                    // the 1e-12 shrink covers the different summation order of FLANN's distance
+                    if (lb2 * (1.0 - 1e-12) <= bd) {
+                        const int32_t cell0 = gd == 3 ? (c0 * g.n[1] + c1) * g.n[2] + z0 : (gd == 2 ? c0 * g.n[1] + z0 : z0);
+                        s = G.cell_start[cell0];
+                        len = G.cell_start[cell0 + (z1 - z0) + 1] - s;
+                        n_cells += (uint32_t)(z1 - z0 + 1);
+                    }
+                }
+            }
+            // inclusive scan of the lengths over the group
+            int32_t incl = len;
+#pragma unroll
+            for (int off = 1; off < kGroup; off <<= 1) {
+                const int32_t o = __shfl_up(incl, off, kGroup);
+                if (sub >= off) incl += o;
+            }
+            const int32_t total = __shfl(incl, kGroup - 1, kGroup);
+            const int32_t shift = s - (incl - len);  // point index = shift[run] + flat index
+            for (int32_t t = 0; t < total; t += kPts * kGroup) {
+                int32_t p[kPts];
+#pragma unroll
+                for (int h = 0; h < kPts; ++h) {
+                    const int32_t idx = t + h * kGroup + sub;
+                    // run of idx: the first lane whose inclusive prefix exceeds it
+                    int lo = 0, hi = kGroup - 1;
+#pragma unroll
+                    for (int step = kGroup; step > 1; step >>= 1) {
+                        const int mid = (lo + hi) >> 1;
+                        const int32_t v = __shfl(incl, mid, kGroup);
+                        if (v > idx) hi = mid;
+                        else lo = mid + 1;
+                    }
+                    // the shuffle runs on every lane of the group (a lane past the end still
+                    // serves as a source: ds_bpermute reads nothing from inactive lanes)
+                    const int32_t sh = __shfl(shift, lo, kGroup);
+                    p[h] = idx < total ? sh + idx : -1;
+                }
+                double dd[kPts];
+                int32_t id[kPts];
+#pragma unroll
+                for (int h = 0; h < kPts; ++h) {
+                    if (p[h] >= 0) {
+                        dd[h] = flann_l2<D>(qq, G.pts + (int64_t)p[h] * D);
+                        id[h] = G.ids[p[h]];
+                    }
+                }
+#pragma unroll
+                for (int h = 0; h < kPts; ++h) {
+                    if (p[h] < 0) continue;
+                    ++n_pts;
+                    if (G.removed && G.removed[id[h] - 1]) continue;
+                    if (nn_better(dd[h], id[h], bd, bi)) {
+                        bd = dd[h];
+                        bi = id[h];
+                    }
+                }
+            }
+        }
+#pragma unroll
+        for (int off = kGroup / 2; off > 0; off >>= 1) {
+            const double od = __shfl_xor(bd, off, kGroup);
+            const int32_t oi = __shfl_xor(bi, off, kGroup);
+            if (nn_better(od, oi, bd, bi)) {
+                bd = od;
+                bi = oi;
+            }
+        }
+        const double lb = ring_bound(g, qg, cq, r);
+        if (lb < 0.0) break;  // every cell visited
+        if (lb * lb > bd) break;
+    }
+    if (G.stats) {
+#pragma unroll
+        for (int off = kGroup / 2; off > 0; off >>= 1) {
+            n_pts += __shfl_xor(n_pts, off, kGroup);
+            n_cells += __shfl_xor(n_cells, off, kGroup);
+        }
+        if (sub == 0) {
+            atomicAdd(G.stats + 0, (unsigned long long)n_pts);
+            atomicAdd(G.stats + 1, (unsigned long long)n_cells);
+        }
+    }
+    if (sub == 0) {
+        out_ids[qi] = bi;
+        out_d2[qi] = bd;
+    }
+}
+
+// kPts: points per lane per step (loads in flight together)
+template <int D, int kGroup, int kPts>
+__global__ __launch_bounds__(256) void k_grid_nn1_runs(GridDev G, const double *__restrict__ q, int64_t nq,
+                                                       int32_t *__restrict__ out_ids, double *__restrict__ out_d2) {
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t slot = t / kGroup;
+    if (slot >= nq) return;  // whole groups leave together (nq is per group)
+    nn1_runs_query<D, kGroup, kPts>(G, q, slot, (int)(t % kGroup), out_ids, out_d2);
+}
+
 template <int D>
 static void grid_knn_d(const GridDev &G, int32_t d, const double *q, int64_t nq, int32_t k, int32_t *ids, double *d2,
                        hipStream_t stream) {
@@ -461,7 +740,25 @@ static void grid_knn_d(const GridDev &G, int32_t d, const double *q, int64_t nq,
 #define MPT_NN1_GROUP_LAUNCH(GRP, FIRST)                                                                        \
     hipLaunchKernelGGL((k_grid_nn1_group<D, GRP, FIRST>), dim3((unsigned)((nq * GRP + 255) / 256)), dim3(256), 0, \
                        stream, G, d, q, nq, ids, d2)
-    if (k == 1 && !per_lane && group == 32) {
+    // cell-run kernel (default); MPT_NN1_KERNEL=cells: the cell-per-lane walk (A/B)
+    static const bool cells = getenv("MPT_NN1_KERNEL") && !strcmp(getenv("MPT_NN1_KERNEL"), "cells");
+    if (k == 1 && !per_lane && !cells && D > 0) {
+        constexpr int DD = D > 0 ? D : 1;
+        // defaults from the A/B runs (scripts/measure_nnruns.sh): 16 lanes, one point per step
+        // for d <= 7 (config 2: 54.7 us vs 58.2 us at 32 x 2); 32 lanes, two points per step
+        // for the snake's d = 15 (0.85 ms vs 0.90 ms at 16 x 2)
+        static const int pts = getenv("MPT_NN1_PTS") ? atoi(getenv("MPT_NN1_PTS")) : (D >= 15 ? 2 : 1);
+        const int rgroup = getenv("MPT_NN1_GROUP") ? group : (D >= 15 ? 32 : 16);
+#define MPT_NN1_RUNS_LAUNCH(GRP, PTS)                                                                          \
+    hipLaunchKernelGGL((k_grid_nn1_runs<DD, GRP, PTS>), dim3((unsigned)((nq * GRP + 255) / 256)), dim3(256), 0, \
+                       stream, G, q, nq, ids, d2)
+        if (rgroup == 16) {
+            if (pts == 1) MPT_NN1_RUNS_LAUNCH(16, 1); else MPT_NN1_RUNS_LAUNCH(16, 2);
+        } else {
+            if (pts == 1) MPT_NN1_RUNS_LAUNCH(32, 1); else MPT_NN1_RUNS_LAUNCH(32, 2);
+        }
+#undef MPT_NN1_RUNS_LAUNCH
+    } else if (k == 1 && !per_lane && group == 32) {
         if (first) MPT_NN1_GROUP_LAUNCH(32, 1); else MPT_NN1_GROUP_LAUNCH(32, 0);
     } else if (k == 1 && !per_lane && group == 8) {
         MPT_NN1_GROUP_LAUNCH(8, 0);

@@ -24,7 +24,10 @@ public:
     ~PointTree();
     // Index rows [0, min(n_upper, *n_dev)) of pts [.][d]: bounding box and code plan on the
     // device, 30-bit codes over all dims, radix sort, boxes bottom-up.  Stream-ordered.
-    void build(const double *pts, int64_t n_upper, const int64_t *n_dev, int32_t d, hipStream_t stream);
+    // spread (optional, grid_nn.h): also write the live points' spread over spread->dims
+    // (from the build's bounding box) to spread->host_out.
+    void build(const double *pts, int64_t n_upper, const int64_t *n_dev, int32_t d, hipStream_t stream,
+               const struct SpreadOut *spread = nullptr);
     PointTreeDev dev() const { return t; }
     // allocate for up to n_upper points now (see GridIndex::reserve)
     void reserve(int64_t n_upper, int32_t d);

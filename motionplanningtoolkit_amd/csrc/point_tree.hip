@@ -19,6 +19,7 @@
 #include <hipcub/hipcub.hpp>
 
 #include "point_tree.h"
+#include "grid_nn.h"
 
 namespace mpt {
 
@@ -92,8 +93,16 @@ __global__ __launch_bounds__(256) void k_pt_bbox(const double *__restrict__ pts,
     }
 }
 
-__global__ void k_pt_plan(int32_t d, const unsigned long long *__restrict__ box, CodePlan *__restrict__ plan) {
+__global__ void k_pt_plan(int32_t d, const unsigned long long *__restrict__ box, CodePlan *__restrict__ plan,
+                          SpreadOut sp) {
     if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    if (sp.host_out) {  // the engine's MPT_NN_AUTO feedback (grid_nn.h SpreadOut)
+        for (int j = 0; j < 3; ++j) {
+            sp.host_out[j] = j < sp.gd ? box[sp.dims[j]] : ~0ull;
+            sp.host_out[3 + j] = j < sp.gd ? box[kPtMaxDim + sp.dims[j]] : 0ull;
+        }
+        __threadfence_system();
+    }
     double lo[kPtMaxDim], ext[kPtMaxDim], emax = 0.0;
     for (int j = 0; j < d; ++j) {
         lo[j] = key_value_pt(box[j]);
@@ -428,7 +437,8 @@ void PointTree::reserve(int64_t n_upper, int32_t d) {
     }
 }
 
-void PointTree::build(const double *pts, int64_t n_upper, const int64_t *n_dev, int32_t d, hipStream_t stream) {
+void PointTree::build(const double *pts, int64_t n_upper, const int64_t *n_dev, int32_t d, hipStream_t stream,
+                      const SpreadOut *spread) {
     if (d != 3 && d != 7 && d != 15) throw Error{1, "point tree: state dim must be 3, 7 or 15"};
     if (n_upper >= (int64_t(1) << 27)) throw Error{1, "point tree: too many points"};
     reserve(n_upper, d);
@@ -444,7 +454,7 @@ void PointTree::build(const double *pts, int64_t n_upper, const int64_t *n_dev, 
     hip_check(hipMemsetAsync(bbox, 0xff, sizeof(unsigned long long) * kPtMaxDim, stream), "bbox memset");
     hip_check(hipMemsetAsync(bbox + kPtMaxDim, 0, sizeof(unsigned long long) * kPtMaxDim, stream), "bbox memset");
     hipLaunchKernelGGL(k_pt_bbox, dim3(64), dim3(256), 0, stream, pts, d, n_upper, n_dev, bbox);
-    hipLaunchKernelGGL(k_pt_plan, dim3(1), dim3(64), 0, stream, d, bbox, plan);
+    hipLaunchKernelGGL(k_pt_plan, dim3(1), dim3(64), 0, stream, d, bbox, plan, spread ? *spread : SpreadOut{});
     hipLaunchKernelGGL(k_pt_morton, dim3(blocks), dim3(256), 0, stream, pts, d, n_upper, n_dev, plan, keys, vals);
     hip_check(hipGetLastError(), "k_pt_morton");
     size_t tb = temp_bytes;

@@ -36,6 +36,11 @@ namespace {
 
 constexpr int kMaxDim = 16;
 
+// grid cell floor = kGridHminK x the expected NN distance (make_grid_params h_min)
+constexpr double kGridHminK = 0.3;
+// MPT_NN_AUTO re-reads the nodes' spread at most every kSpreadEvery rounds
+constexpr int kSpreadEvery = 8;
+
 struct EngineParams {
     int32_t kind, d, L, pmax;
     double prm[7];
@@ -296,92 +301,6 @@ __global__ void k_set_n(int64_t *n_dev, int64_t n, unsigned long long *counters)
     counters[3] = (unsigned long long)n;
 }
 
-// Spread of the live nodes over the spatial dims (for MPT_NN_AUTO): per-dim min / max as
-// order-preserving 64-bit keys, out[0..3) = min, out[3..6) = max (unused dims: ~0 / 0).
-__device__ __forceinline__ unsigned long long order_key(double x) {
-    const unsigned long long b = (unsigned long long)__double_as_longlong(x);
-    return (b >> 63) ? ~b : (b | 0x8000000000000000ull);
-}
-constexpr int kSpreadBlocks = 128;
-
-__device__ __forceinline__ unsigned long long wave_min_u64(unsigned long long v) {
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) {
-        const unsigned long long o = __shfl_xor(v, off);
-        v = o < v ? o : v;
-    }
-    return v;
-}
-__device__ __forceinline__ unsigned long long wave_max_u64(unsigned long long v) {
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) {
-        const unsigned long long o = __shfl_xor(v, off);
-        v = o > v ? o : v;
-    }
-    return v;
-}
-
-// One launch, no memsets: each block reduces its stride of nodes (shuffles, then one LDS
-// slot per wave) into partial[block][6]; the last block to finish (ticket) folds the
-// partials, writes the result straight into mapped pinned host memory and re-arms the ticket.
-__global__ __launch_bounds__(256) void k_spread(const double *__restrict__ nodes, const int64_t *__restrict__ n_dev,
-                                                int32_t d, int32_t gd, unsigned long long *__restrict__ partial,
-                                                unsigned int *__restrict__ ticket, unsigned long long *host_out) {
-    __shared__ unsigned long long s_v[4][6];
-    __shared__ bool s_last;
-    const int64_t n = *n_dev;
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    unsigned long long mn[3] = {~0ull, ~0ull, ~0ull}, mx[3] = {0, 0, 0};
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
-        for (int j = 0; j < gd; ++j) {
-            const unsigned long long k = order_key(nodes[i * d + j]);
-            mn[j] = k < mn[j] ? k : mn[j];
-            mx[j] = k > mx[j] ? k : mx[j];
-        }
-#pragma unroll
-    for (int j = 0; j < 3; ++j) {
-        mn[j] = wave_min_u64(mn[j]);
-        mx[j] = wave_max_u64(mx[j]);
-    }
-    if (lane == 0)
-        for (int j = 0; j < 3; ++j) {
-            s_v[wave][j] = mn[j];
-            s_v[wave][3 + j] = mx[j];
-        }
-    __syncthreads();
-    if (threadIdx.x < 6) {
-        const int j = threadIdx.x;
-        unsigned long long v = s_v[0][j];
-        for (int w = 1; w < 4; ++w) v = j < 3 ? (s_v[w][j] < v ? s_v[w][j] : v) : (s_v[w][j] > v ? s_v[w][j] : v);
-        partial[blockIdx.x * 6 + j] = v;
-    }
-    __threadfence();
-    __syncthreads();
-    if (threadIdx.x == 0) s_last = atomicAdd(ticket, 1u) == gridDim.x - 1;
-    __syncthreads();
-    if (!s_last) return;
-    __threadfence();
-    if (threadIdx.x < 6) {
-        const int j = threadIdx.x;
-        const volatile unsigned long long *pv = partial;
-        unsigned long long v = pv[j];
-        for (unsigned b = 1; b < gridDim.x; ++b) {
-            const unsigned long long o = pv[b * 6 + j];
-            v = j < 3 ? (o < v ? o : v) : (o > v ? o : v);
-        }
-        host_out[j] = v;
-    }
-    if (threadIdx.x == 0) *ticket = 0u;
-    __threadfence_system();
-}
-
-double key_value(unsigned long long k) {
-    const unsigned long long b = (k >> 63) ? (k & 0x7fffffffffffffffull) : ~k;
-    double x;
-    std::memcpy(&x, &b, sizeof x);
-    return x;
-}
-
 }  // namespace
 
 struct mpt_rrt {
@@ -410,13 +329,15 @@ struct mpt_rrt {
     std::unique_ptr<GridIndex> grid;
     std::unique_ptr<PointTree> ptree;  // MPT_NN_TREE (point_tree.hip)
     int32_t grid_gd = 0, grid_dims[3] = {0, 0, 0};
-    double ppc = 2.0;
-    // MPT_NN_AUTO feedback: the live nodes' spatial spread, copied back after each round and
-    // read at a later round once its event has completed (never waited for; the NN choice
-    // changes only speed, results are identical)
+    double ppc = 0.0;  // grid points per cell; <= 0: 2, floored by the expected NN distance
+    // MPT_NN_AUTO feedback: the live nodes' spatial spread, a by-product of the round's index
+    // build (SpreadOut, grid_nn.h) written to mapped host memory and read at a later round once
+    // its event has completed (never waited for; the NN choice changes only speed, results
+    // are identical).  d_spread: the grid build's per-block partials.
     unsigned long long *d_spread = nullptr, *h_spread = nullptr, *h_spread_dev = nullptr;
     hipEvent_t ev_spread = nullptr;
-    bool spread_pending = false, auto_tree = false;
+    bool spread_pending = false, auto_tree = false, spread_seen = false;
+    int32_t rounds_since_spread = 0;
     int32_t last_nn = -1;  // structure the last round used (mpt_rrt_last_nn)
     // optional collision work counters (k_collide atomics): units, clusters, node visits, tri tests
     bool stats_on = false;
@@ -557,6 +478,7 @@ extern "C" mpt_status mpt_rrt_add_nodes(mpt_rrt *r, const double *states, const 
         hip_check(hipGetLastError(), "k_set_n");
         hip_check(hipDeviceSynchronize(), "sync");
         r->n_upper = nn;
+        r->spread_seen = false;  // bulk nodes: re-read the spread at the next index build
     });
 }
 
@@ -587,12 +509,13 @@ extern "C" mpt_status mpt_rrt_step(mpt_rrt *r, int32_t K, void *stream_) {
             double frac = 1.0;
             for (int j = 0; j < r->grid_gd; ++j) {
                 const int dj = r->grid_dims[j];
-                const double ext = key_value(r->h_spread[3 + j]) - key_value(r->h_spread[j]);
+                const double ext = key_value_u64(r->h_spread[3 + j]) - key_value_u64(r->h_spread[j]);
                 const double range = p.hi[dj] - p.lo[dj];
                 frac *= range > 0 ? std::min(1.0, std::max(0.0, ext / range)) : 1.0;
             }
             r->auto_tree = frac < 0.25;
             r->spread_pending = false;
+            r->spread_seen = true;
         }
         const bool big = r->n_upper >= 4096;
         const bool use_tree = r->nn_mode == MPT_NN_TREE || (r->nn_mode == MPT_NN_AUTO && big && r->auto_tree);
@@ -602,9 +525,30 @@ extern "C" mpt_status mpt_rrt_step(mpt_rrt *r, int32_t K, void *stream_) {
         hipLaunchKernelGGL(k_sample, dim3(kb), dim3(256), 0, stream, p, r->ext_base, K, r->d_samples);
         hip_check(hipGetLastError(), "k_sample");
         mark(1);
+        // the spread feedback rides on this round's index build when none is in flight
+        SpreadOut spread;
+        const bool want_spread = r->nn_mode == MPT_NN_AUTO && !r->spread_pending && (use_tree || use_grid) &&
+                                 (!r->spread_seen || r->rounds_since_spread >= kSpreadEvery);
+        ++r->rounds_since_spread;
+        if (want_spread) {
+            if (!r->d_spread) {
+                // the grid build's per-block partials [ceil(cap / 256)][6]
+                const int64_t blocks = (r->cap + 255) / 256;
+                hip_check(hipMalloc(&r->d_spread, sizeof(unsigned long long) * blocks * 6), "alloc spread");
+                hip_check(hipHostMalloc(&r->h_spread, sizeof(unsigned long long) * 6,
+                                        hipHostMallocMapped | hipHostMallocCoherent), "alloc spread");
+                hip_check(hipHostGetDevicePointer(reinterpret_cast<void **>(&r->h_spread_dev), r->h_spread, 0),
+                          "spread device pointer");
+                hip_check(hipEventCreateWithFlags(&r->ev_spread, hipEventDisableTiming), "event");
+            }
+            spread.gd = r->grid_gd;
+            for (int j = 0; j < 3; ++j) spread.dims[j] = r->grid_dims[j];
+            spread.partial = r->d_spread;
+            spread.host_out = r->h_spread_dev;
+        }
         if (use_tree) {
             r->ptree->reserve(r->cap, p.d);  // once: no allocation (device sync) in later rounds
-            r->ptree->build(r->d_nodes, r->n_upper, r->d_n, p.d, stream);
+            r->ptree->build(r->d_nodes, r->n_upper, r->d_n, p.d, stream, want_spread ? &spread : nullptr);
         } else if (use_grid) {
             // spatial dims of the agent's tree state: x, y, z (omni, blimp) or x, y (snake);
             // the grid spans the sampling ranges, nodes outside fall into the border cells
@@ -613,10 +557,21 @@ extern "C" mpt_status mpt_rrt_step(mpt_rrt *r, int32_t K, void *stream_) {
                 lo[j] = p.lo[r->grid_dims[j]];
                 hi[j] = p.hi[r->grid_dims[j]];
             }
-            const GridParams g = make_grid_params(p.d, r->grid_dims, r->grid_gd, lo, hi, r->n_upper, r->ppc);
-            const GridParams gcap = make_grid_params(p.d, r->grid_dims, r->grid_gd, lo, hi, r->cap, r->ppc);
+            // cells of ~2 points, but not much finer than the expected NN distance over all
+            // state dims (MPT_NN_HMIN_K: the fraction; A/B knob)
+            static const double hk = getenv("MPT_NN_HMIN_K") ? atof(getenv("MPT_NN_HMIN_K")) : kGridHminK;
+            const double ppc = r->ppc > 0 ? r->ppc : 2.0;
+            const double hmin_n = r->ppc > 0 ? 0.0 : hk * expected_nn_distance(p.d, p.lo, p.hi, r->n_upper);
+            const double hmin_c = r->ppc > 0 ? 0.0 : hk * expected_nn_distance(p.d, p.lo, p.hi, r->cap);
+            const GridParams g = make_grid_params(p.d, r->grid_dims, r->grid_gd, lo, hi, r->n_upper, ppc, hmin_n);
+            const GridParams gcap = make_grid_params(p.d, r->grid_dims, r->grid_gd, lo, hi, r->cap, ppc, hmin_c);
             r->grid->reserve(r->cap, p.d, std::max(g.ncells, gcap.ncells));  // once, as for the tree
-            r->grid->build(r->d_nodes, r->n_upper, r->d_n, p.d, g, stream);
+            r->grid->build(r->d_nodes, r->n_upper, r->d_n, p.d, g, stream, want_spread ? &spread : nullptr);
+        }
+        if (want_spread) {
+            hip_check(hipEventRecord(r->ev_spread, stream), "spread event");
+            r->spread_pending = true;
+            r->rounds_since_spread = 0;
         }
         mark(2);
         if (use_tree) {
@@ -669,25 +624,6 @@ extern "C" mpt_status mpt_rrt_step(mpt_rrt *r, int32_t K, void *stream_) {
                            r->d_counters);
         hip_check(hipGetLastError(), "append");
         mark(9);
-        if (r->nn_mode == MPT_NN_AUTO && !r->spread_pending) {
-            if (!r->d_spread) {
-                // partials [kSpreadBlocks][6] + the ticket; the result goes to mapped pinned memory
-                const size_t bytes = sizeof(unsigned long long) * (kSpreadBlocks * 6 + 1);
-                hip_check(hipMalloc(&r->d_spread, bytes), "alloc spread");
-                hip_check(hipMemset(r->d_spread, 0, bytes), "zero spread");
-                hip_check(hipHostMalloc(&r->h_spread, sizeof(unsigned long long) * 6,
-                                        hipHostMallocMapped | hipHostMallocCoherent), "alloc spread");
-                hip_check(hipHostGetDevicePointer(reinterpret_cast<void **>(&r->h_spread_dev), r->h_spread, 0),
-                          "spread device pointer");
-                hip_check(hipEventCreateWithFlags(&r->ev_spread, hipEventDisableTiming), "event");
-            }
-            hipLaunchKernelGGL(k_spread, dim3(kSpreadBlocks), dim3(256), 0, stream, r->d_nodes, r->d_n, p.d,
-                               r->grid_gd, r->d_spread,
-                               reinterpret_cast<unsigned int *>(r->d_spread + kSpreadBlocks * 6), r->h_spread_dev);
-            hip_check(hipGetLastError(), "k_spread");
-            hip_check(hipEventRecord(r->ev_spread, stream), "spread event");
-            r->spread_pending = true;
-        }
         r->ext_base += (uint64_t)K;
         r->n_upper = std::min<int64_t>(r->cap, r->n_upper + K);
         r->last_K = K;
@@ -780,7 +716,7 @@ extern "C" mpt_status mpt_rrt_set_nn(mpt_rrt *r, int32_t mode, double points_per
     return guarded([&] {
         if (!r || mode < MPT_NN_AUTO || mode > MPT_NN_TREE) throw Error{MPT_ERR_INVALID, "bad arguments"};
         r->nn_mode = mode;
-        if (points_per_cell > 0) r->ppc = points_per_cell;
+        r->ppc = points_per_cell > 0 ? points_per_cell : 0.0;
     });
 }
 
