@@ -7,7 +7,7 @@
 //   -> TreeInterface::insertIntoTree.
 // A round here performs K such extensions against the tree snapshot taken at the start
 // of the round (new nodes become visible to the next round), entirely on the device:
-//   k_sample -> k_knn1 (+ merge) -> k_steer -> k_collide -> k_count -> k_append -> k_commit
+//   k_sample -> NN index build + query -> k_steer -> collision -> k_append_commit
 // No host synchronisation inside a round; the node count lives in device memory.
 // The per-extension randomness comes from a counter-based generator (fcl_math.h
 // engine_uniform): extension g uses counters g*64 + j (sample dims) and g*64 + 32 + j
@@ -125,30 +125,39 @@ __device__ void snake_poses(const double *prm, int T, const double *s, double *o
     }
 }
 
-__global__ void k_sample(EngineParams p, uint64_t ext_base, int32_t K, double *__restrict__ samples) {
+// n_dev[1] = n_dev[0]: the round's starting node count, read by k_append_commit (which
+// overwrites n_dev[0] in the same launch)
+__global__ void k_sample(EngineParams p, uint64_t ext_base, int32_t K, double *__restrict__ samples,
+                         int64_t *__restrict__ n_dev) {
     const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k == 0) n_dev[1] = n_dev[0];
     if (k >= K) return;
     const uint64_t g = ext_base + (uint64_t)k;
     for (int j = 0; j < p.d; ++j) samples[k * p.d + j] = engine_uniform(p.seed, g * 64 + j, p.lo[j], p.hi[j]);
 }
 
 // randomSteer + getPoses per extension.  Writes the end state, the pose slots
-// [k*pmax + i][L][12] and pcount[k].
-__global__ void k_steer(EngineParams p, uint64_t ext_base, int32_t K, const double *__restrict__ nodes,
-                        const int32_t *__restrict__ nn, double *__restrict__ ends, double *__restrict__ poses,
-                        int32_t *__restrict__ pcount, uint8_t *__restrict__ verdict,
-                        unsigned long long *__restrict__ counters) {
+// [k*pmax + i][L][12] and pcount[k].  KIND fixes the state dim of the omnidirectional (3)
+// and blimp (7) agents at compile time, so their states stay in registers (the snake's
+// 5 + T is a run-time value).
+template <int KIND>
+__global__ __launch_bounds__(256) void k_steer(EngineParams p, uint64_t ext_base, int32_t K,
+                                               const double *__restrict__ nodes, const int32_t *__restrict__ nn,
+                                               double *__restrict__ ends, double *__restrict__ poses,
+                                               int32_t *__restrict__ pcount, uint8_t *__restrict__ verdict,
+                                               unsigned long long *__restrict__ counters) {
     const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= K) return;
     verdict[k] = 0;  // the collision stage only ever sets verdicts
     const uint64_t g = ext_base + (uint64_t)k;
-    const int d = p.d;
-    double from[kMaxDim], end[kMaxDim];
+    constexpr int DD = KIND == MPT_AGENT_OMNI ? 3 : (KIND == MPT_AGENT_BLIMP ? 7 : kMaxDim);
+    const int d = KIND == MPT_AGENT_SNAKE ? p.d : DD;
+    double from[DD], end[DD];
     const int64_t src = nn[k] - 1;  // nn ids are 1-based
     for (int j = 0; j < d; ++j) from[j] = nodes[src * d + j];
     double *ps = poses + (int64_t)k * p.pmax * p.L * 12;
     int32_t P = 0;
-    if (p.kind == MPT_AGENT_OMNI) {
+    if constexpr (KIND == MPT_AGENT_OMNI) {
         // Omnidirectional::randomSteer (agents/omnidirectional.hpp:168-184)
         const double rx = engine_uniform(p.seed, g * 64 + 32, -1.0, 1.0);
         const double ry = engine_uniform(p.seed, g * 64 + 33, -1.0, 1.0);
@@ -180,7 +189,7 @@ __global__ void k_steer(EngineParams p, uint64_t ext_base, int32_t K, const doub
                 ++P;
             }
         }
-    } else if (p.kind == MPT_AGENT_BLIMP) {
+    } else if constexpr (KIND == MPT_AGENT_BLIMP) {
         const double a = engine_uniform(p.seed, g * 64 + 32, -1.0, 1.0);
         const double w = engine_uniform(p.seed, g * 64 + 33, -0.1745, 0.1745);
         const double z = engine_uniform(p.seed, g * 64 + 34, -1.0, 1.0);
@@ -225,75 +234,57 @@ __global__ void k_steer(EngineParams p, uint64_t ext_base, int32_t K, const doub
     for (int j = 0; j < d; ++j) ends[k * d + j] = end[j];
 }
 
-// Per 256-extension block: number of collision-free extensions.
-__global__ __launch_bounds__(256) void k_count(const uint8_t *__restrict__ verdict, int32_t K,
-                                               int32_t *__restrict__ bcount) {
-    __shared__ int32_t s[4];
-    const int64_t k = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    const bool ok = k < K && verdict[k] == 0;
-    const int c = __popcll(__ballot(ok));
-    if ((threadIdx.x & 63) == 0) s[threadIdx.x >> 6] = c;
-    __syncthreads();
-    if (threadIdx.x == 0) bcount[blockIdx.x] = s[0] + s[1] + s[2] + s[3];
-}
-
-// Ordered append: extension k lands at n + (number of valid extensions before k).
-__global__ __launch_bounds__(256) void k_append(const uint8_t *__restrict__ verdict, int32_t K, int32_t d,
-                                                const double *__restrict__ ends, const int32_t *__restrict__ nn,
-                                                const int32_t *__restrict__ bcount, const int64_t *__restrict__ n_dev,
-                                                int64_t cap, double *__restrict__ nodes,
-                                                int32_t *__restrict__ parents) {
-    __shared__ int64_t s_red[256];
-    __shared__ int32_t s_wave[4];
-    const int tid = threadIdx.x;
-    int64_t acc = 0;
-    for (int64_t b = tid; b < blockIdx.x; b += 256) acc += bcount[b];
-    s_red[tid] = acc;
-    __syncthreads();
-    for (int st = 128; st > 0; st >>= 1) {
-        if (tid < st) s_red[tid] += s_red[tid + st];
-        __syncthreads();
+// Ordered append and commit in one launch: extension k lands at n0 + (number of valid
+// extensions before k).  Each block counts the valid extensions before it straight from the
+// verdict bytes (0 / 1, so 16 minus the popcount of every 16-byte load), so no block waits
+// on another; the last block also commits n and the counters.  n0 = n_dev[1] (k_sample).
+__global__ __launch_bounds__(256) void k_append_commit(const uint8_t *__restrict__ verdict, int32_t K, int32_t d,
+                                                       const double *__restrict__ ends,
+                                                       const int32_t *__restrict__ nn, int64_t *__restrict__ n_dev,
+                                                       int64_t cap, double *__restrict__ nodes,
+                                                       int32_t *__restrict__ parents,
+                                                       unsigned long long *__restrict__ counters) {
+    __shared__ int32_t s_wave[4], s_ones[4];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const uint4 *v4 = reinterpret_cast<const uint4 *>(verdict);
+    const int64_t nv4 = (int64_t)blockIdx.x * 16;  // 256 verdicts per block before this one
+    int32_t ones = 0;
+    for (int64_t i = tid; i < nv4; i += 256) {
+        const uint4 x = v4[i];
+        ones += __popc(x.x) + __popc(x.y) + __popc(x.z) + __popc(x.w);
     }
-    const int64_t base = *n_dev + s_red[0];
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) ones += __shfl_xor(ones, off);
     const int64_t k = (int64_t)blockIdx.x * 256 + tid;
     const bool ok = k < K && verdict[k] == 0;
     const uint64_t m = __ballot(ok);
-    const int lane = tid & 63, wave = tid >> 6;
-    const int before = __popcll(m & ((1ull << lane) - 1ull));
-    if (lane == 0) s_wave[wave] = __popcll(m);
+    if (lane == 0) {
+        s_ones[wave] = ones;
+        s_wave[wave] = __popcll(m);
+    }
     __syncthreads();
+    const int64_t before_block = nv4 * 16 - (int64_t)(s_ones[0] + s_ones[1] + s_ones[2] + s_ones[3]);
+    const int64_t n0 = n_dev[1];
     int wbase = 0;
     for (int w = 0; w < wave; ++w) wbase += s_wave[w];
-    if (!ok) return;
-    const int64_t idx = base + wbase + before;
-    if (idx >= cap) return;
-    for (int j = 0; j < d; ++j) nodes[idx * d + j] = ends[k * d + j];
-    parents[idx] = nn[k];
-}
-
-__global__ void k_commit(const int32_t *__restrict__ bcount, int32_t nblocks, int32_t K, int64_t *__restrict__ n_dev,
-                         int64_t cap, unsigned long long *__restrict__ counters) {
-    // one workgroup of 256: block sum of the per-block valid counts, then thread 0 commits
-    __shared__ int64_t s_red[256];
-    int64_t acc = 0;
-    for (int b = threadIdx.x; b < nblocks; b += 256) acc += bcount[b];
-    s_red[threadIdx.x] = acc;
-    __syncthreads();
-    for (int st = 128; st > 0; st >>= 1) {
-        if ((int)threadIdx.x < st) s_red[threadIdx.x] += s_red[threadIdx.x + st];
-        __syncthreads();
+    if (ok) {
+        const int64_t idx = n0 + before_block + wbase + __popcll(m & ((1ull << lane) - 1ull));
+        if (idx < cap) {
+            for (int j = 0; j < d; ++j) nodes[idx * d + j] = ends[k * d + j];
+            parents[idx] = nn[k];
+        }
     }
-    if (threadIdx.x != 0) return;
-    const int64_t tot = s_red[0];
-    const int64_t n = *n_dev;
-    const int64_t room = cap - n > 0 ? cap - n : 0;
-    const int64_t add = tot < room ? tot : room;
-    *n_dev = n + add;
-    counters[0] += 1;
-    counters[1] += (unsigned long long)K;
-    counters[2] += (unsigned long long)add;
-    counters[3] = (unsigned long long)(n + add);
-    counters[4] += (unsigned long long)(tot - add);
+    if (blockIdx.x == gridDim.x - 1 && tid == 0) {
+        const int64_t tot = before_block + s_wave[0] + s_wave[1] + s_wave[2] + s_wave[3];
+        const int64_t room = cap - n0 > 0 ? cap - n0 : 0;
+        const int64_t add = tot < room ? tot : room;
+        n_dev[0] = n0 + add;
+        counters[0] += 1;
+        counters[1] += (unsigned long long)K;
+        counters[2] += (unsigned long long)add;
+        counters[3] = (unsigned long long)(n0 + add);
+        counters[4] += (unsigned long long)(tot - add);
+    }
 }
 
 __global__ void k_set_n(int64_t *n_dev, int64_t n, unsigned long long *counters) {
@@ -315,7 +306,7 @@ struct mpt_rrt {
     unsigned long long *d_counters = nullptr;
     int32_t kcap = 0;
     double *d_samples = nullptr, *d_ends = nullptr, *d_poses = nullptr, *d_nnd2 = nullptr;
-    int32_t *d_nn = nullptr, *d_pcount = nullptr, *d_bcount = nullptr;
+    int32_t *d_nn = nullptr, *d_pcount = nullptr;
     uint8_t *d_verdict = nullptr;
     void *d_scratch = nullptr;
     size_t scratch_bytes = 0;
@@ -349,7 +340,7 @@ struct mpt_rrt {
 namespace {
 void rfree(mpt_rrt *r) {
     void *ps[] = {r->d_links, r->d_nodes,   r->d_parents, r->d_n,       r->d_counters, r->d_samples,
-                  r->d_ends,  r->d_poses,   r->d_nnd2,    r->d_nn,      r->d_pcount,   r->d_bcount,
+                  r->d_ends,  r->d_poses,   r->d_nnd2,    r->d_nn,      r->d_pcount,
                   r->d_verdict, r->d_scratch, r->d_cstats};
     for (void *p : ps)
         if (p) (void)hipFree(p);
@@ -363,7 +354,7 @@ void rfree(mpt_rrt *r) {
 void ensure_round_buffers(mpt_rrt *r, int32_t K) {
     const size_t need_scratch = nn_knn_scratch_bytes(K, std::max<int64_t>(r->cap, 1), 1);
     if (K > r->kcap) {
-        void *ps[] = {r->d_samples, r->d_ends, r->d_poses, r->d_nnd2, r->d_nn, r->d_pcount, r->d_bcount, r->d_verdict};
+        void *ps[] = {r->d_samples, r->d_ends, r->d_poses, r->d_nnd2, r->d_nn, r->d_pcount, r->d_verdict};
         for (void *p : ps)
             if (p) hip_check(hipFree(p), "hipFree");
         const int64_t d = r->p.d;
@@ -373,7 +364,6 @@ void ensure_round_buffers(mpt_rrt *r, int32_t K) {
         hip_check(hipMalloc(&r->d_nnd2, sizeof(double) * K), "alloc nnd2");
         hip_check(hipMalloc(&r->d_nn, sizeof(int32_t) * K), "alloc nn");
         hip_check(hipMalloc(&r->d_pcount, sizeof(int32_t) * K), "alloc pcount");
-        hip_check(hipMalloc(&r->d_bcount, sizeof(int32_t) * ((K + 255) / 256)), "alloc bcount");
         hip_check(hipMalloc(&r->d_verdict, (size_t)K), "alloc verdict");
         r->kcap = K;
         r->cscratch.ensure((int64_t)K * r->p.pmax * r->p.L, r->max_clusters);
@@ -432,8 +422,8 @@ extern "C" mpt_status mpt_rrt_create(const mpt_env *env, const mpt_agent *agent,
             r->cap = capacity;
             hip_check(hipMalloc(&r->d_nodes, sizeof(double) * dim * capacity), "alloc nodes");
             hip_check(hipMalloc(&r->d_parents, sizeof(int32_t) * capacity), "alloc parents");
-            hip_check(hipMalloc(&r->d_n, sizeof(int64_t)), "alloc n");
-            hip_check(hipMemset(r->d_n, 0, sizeof(int64_t)), "memset n");
+            hip_check(hipMalloc(&r->d_n, 2 * sizeof(int64_t)), "alloc n");  // [0] n, [1] round start
+            hip_check(hipMemset(r->d_n, 0, 2 * sizeof(int64_t)), "memset n");
             hip_check(hipMalloc(&r->d_counters, sizeof(unsigned long long) * 8), "alloc counters");
             hip_check(hipMemset(r->d_counters, 0, sizeof(unsigned long long) * 8), "memset counters");
             for (auto &e : r->ev) hip_check(hipEventCreate(&e), "event");
@@ -522,7 +512,7 @@ extern "C" mpt_status mpt_rrt_step(mpt_rrt *r, int32_t K, void *stream_) {
         const bool use_grid = !use_tree && (r->nn_mode == MPT_NN_GRID || (r->nn_mode == MPT_NN_AUTO && big));
         r->last_nn = use_tree ? MPT_NN_TREE : (use_grid ? MPT_NN_GRID : MPT_NN_BRUTE);
         mark(0);
-        hipLaunchKernelGGL(k_sample, dim3(kb), dim3(256), 0, stream, p, r->ext_base, K, r->d_samples);
+        hipLaunchKernelGGL(k_sample, dim3(kb), dim3(256), 0, stream, p, r->ext_base, K, r->d_samples, r->d_n);
         hip_check(hipGetLastError(), "k_sample");
         mark(1);
         // the spread feedback rides on this round's index build when none is in flight
@@ -594,7 +584,9 @@ extern "C" mpt_status mpt_rrt_step(mpt_rrt *r, int32_t K, void *stream_) {
             launch_knn(w, 1, r->d_nn, r->d_nnd2, r->d_scratch, stream);
         }
         mark(3);
-        hipLaunchKernelGGL(k_steer, dim3(kb), dim3(256), 0, stream, p, r->ext_base, K, r->d_nodes, r->d_nn, r->d_ends,
+        auto steer = p.kind == MPT_AGENT_OMNI ? k_steer<MPT_AGENT_OMNI>
+                     : (p.kind == MPT_AGENT_BLIMP ? k_steer<MPT_AGENT_BLIMP> : k_steer<MPT_AGENT_SNAKE>);
+        hipLaunchKernelGGL(steer, dim3(kb), dim3(256), 0, stream, p, r->ext_base, K, r->d_nodes, r->d_nn, r->d_ends,
                            r->d_poses, r->d_pcount, r->d_verdict, r->d_counters);
         hip_check(hipGetLastError(), "k_steer");
         mark(4);
@@ -617,11 +609,8 @@ extern "C" mpt_status mpt_rrt_step(mpt_rrt *r, int32_t K, void *stream_) {
                                  r->timing ? r->ev + 5 : nullptr);
         }
         mark(8);
-        hipLaunchKernelGGL(k_count, dim3(kb), dim3(256), 0, stream, r->d_verdict, K, r->d_bcount);
-        hipLaunchKernelGGL(k_append, dim3(kb), dim3(256), 0, stream, r->d_verdict, K, p.d, r->d_ends, r->d_nn,
-                           r->d_bcount, r->d_n, r->cap, r->d_nodes, r->d_parents);
-        hipLaunchKernelGGL(k_commit, dim3(1), dim3(256), 0, stream, r->d_bcount, (int32_t)kb, K, r->d_n, r->cap,
-                           r->d_counters);
+        hipLaunchKernelGGL(k_append_commit, dim3(kb), dim3(256), 0, stream, r->d_verdict, K, p.d, r->d_ends, r->d_nn,
+                           r->d_n, r->cap, r->d_nodes, r->d_parents, r->d_counters);
         hip_check(hipGetLastError(), "append");
         mark(9);
         r->ext_base += (uint64_t)K;
