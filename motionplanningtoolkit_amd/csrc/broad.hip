@@ -90,36 +90,49 @@ __device__ __forceinline__ uint32_t walk_tree(const EnvDev &env, const Item *__r
     const int32_t top_off = env.lev_off[top];
     const int32_t n_top = env.lev_off[top + 1] - top_off;
     uint32_t tests = (uint32_t)n_top;
-    auto tri_run = [&](int32_t first, int32_t count) {
-        int32_t k = first;
-        const int32_t end = first + count;
-        for (; k + 4 <= end; k += 4) {  // four independent loads in flight
-            const Item t0 = items[k], t1 = items[k + 1], t2 = items[k + 2], t3 = items[k + 3];
-            if (box_overlap(lo, hi, t0.lo, t0.hi)) sink(k);
-            if (box_overlap(lo, hi, t1.lo, t1.hi)) sink(k + 1);
-            if (box_overlap(lo, hi, t2.lo, t2.hi)) sink(k + 2);
-            if (box_overlap(lo, hi, t3.lo, t3.hi)) sink(k + 3);
+    // boxes of items [first, first + count) that overlap (lo, hi) as a bit mask; eight
+    // independent loads in flight per step (a one-at-a-time loop is a chain of dependent
+    // LDS round trips, which is what bounded the walk)
+    auto overlap_mask = [&](int32_t first, int32_t count) {
+        uint64_t M = 0;
+        for (int32_t i0 = 0; i0 < count; i0 += 8) {
+            float bl[8][3], bh[8][3];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const Item b = items[first + (i0 + j < count ? i0 + j : count - 1)];
+#pragma unroll
+                for (int x = 0; x < 3; ++x) {
+                    bl[j][x] = b.lo[x];
+                    bh[j][x] = b.hi[x];
+                }
+            }
+#pragma unroll
+            for (int j = 0; j < 8; ++j)
+                if (i0 + j < count && box_overlap(lo, hi, bl[j], bh[j])) M |= 1ull << (i0 + j);
         }
-        for (; k < end; ++k) {
-            const Item t = items[k];
-            if (box_overlap(lo, hi, t.lo, t.hi)) sink(k);
+        return M;
+    };
+    auto tri_run = [&](int32_t first, int32_t count) {
+        uint64_t M = overlap_mask(first, count);
+        while (M) {
+            const int j = __ffsll((unsigned long long)M) - 1;
+            M &= M - 1;
+            sink(first + j);
         }
     };
     if (kTwo) {
-        for (int32_t i = 0; i < n_top; ++i) {
+        uint64_t M = overlap_mask(top_off, n_top);
+        while (M) {
+            const int i = __ffsll((unsigned long long)M) - 1;
+            M &= M - 1;
             const Item b = items[top_off + i];
-            if (!box_overlap(lo, hi, b.lo, b.hi)) continue;
             tests += (uint32_t)b.count;
             tri_run(b.first, b.count);
         }
         return tests;
     }
     // general: DFS over (level, base, remaining-children mask)
-    uint64_t M = 0;
-    for (int32_t i = 0; i < n_top; ++i) {
-        const Item b = items[top_off + i];
-        if (box_overlap(lo, hi, b.lo, b.hi)) M |= 1ull << i;
-    }
+    uint64_t M = overlap_mask(top_off, n_top);
     int32_t lv = top, base = top_off, sp = 0;
     for (;;) {
         if (!M) {
@@ -139,11 +152,7 @@ __device__ __forceinline__ uint32_t walk_tree(const EnvDev &env, const Item *__r
             tri_run(it.first, it.count);
             continue;
         }
-        uint64_t Mc = 0;
-        for (int32_t c = 0; c < it.count; ++c) {
-            const Item ch = items[it.first + c];
-            if (box_overlap(lo, hi, ch.lo, ch.hi)) Mc |= 1ull << c;
-        }
+        const uint64_t Mc = overlap_mask(it.first, it.count);
         if (!Mc) continue;
         if (M) stk[sp++] = make_uint4((uint32_t)M, (uint32_t)(M >> 32), (uint32_t)base, (uint32_t)lv);
         M = Mc;
@@ -506,7 +515,9 @@ static void collide_split_chunk(const EnvDev &env, const AgentDev *d_links, int3
                 C,        s.n_cwaves};
     const unsigned pblocks = (unsigned)((threads + kPairThreads - 1) / kPairThreads);
     const int32_t n_items = env.lev_off[env.n_levels];
-    const bool lds = n_items <= kLdsItems;
+    // MPT_PAIRS_LDS=0: items read through the caches instead of staged in LDS (A/B knob)
+    static const bool lds_on = !(getenv("MPT_PAIRS_LDS") && atoi(getenv("MPT_PAIRS_LDS")) == 0);
+    const bool lds = lds_on && n_items <= kLdsItems;
     const size_t lds_bytes = lds ? sizeof(Item) * n_items : 0;
     if (env.n_levels <= 2) {
         if (lds)

@@ -1,22 +1,23 @@
 #!/bin/bash
-# Round-1 (third session): rocprofv3 passes of config 2 at HEAD, then config 3 (snake) NN
-# structure comparison.  Every GPU step has its own time limit; stops at the first failure.
-mkdir -p gpurun_out/m7
+# Round-1 (third session) measurements on one MI355X: config 2 / 3 / 5 bench lines, then the
+# rocprofv3 passes of config 2 (kernel trace + stats, FETCH_SIZE, WRITE_SIZE).  Every GPU step
+# has its own time limit; the script stops at the first failure.
+OUT=gpurun_out/m12
+mkdir -p $OUT
 run() {  # name timeout cmd...
   local name=$1 t=$2; shift 2
-  echo "== $name: $*" >> gpurun_out/m7/steps.log
-  timeout -k 10 "$t" "$@" > "gpurun_out/m7/$name.log" 2>&1
+  echo "== $name: $*" >> $OUT/steps.log
+  timeout -k 10 "$t" "$@" > "$OUT/$name.log" 2>&1
   local rc=$?
-  echo "== $name rc=$rc" >> gpurun_out/m7/steps.log
-  tail -c 300 "gpurun_out/m7/$name.log"; echo
+  echo "== $name rc=$rc" >> $OUT/steps.log
+  tail -c 300 "$OUT/$name.log"; echo
   [ $rc -ne 0 ] && exit $rc
   return 0
 }
+run c2 300 python bench.py --steps 30 --warmup 5 --cpu-seconds 15
+run c3 300 python bench.py --workload snake --steps 20 --warmup 3 --cpu-seconds 10
+run c5 300 python bench.py --seeds 256 --steps 5 --warmup 3 --no-cpu
 BENCH_ARGS="--steps 20 --warmup 3 --no-cpu" bash scripts/profile.sh r05 || exit $?
-python scripts/pmc_summary.py gpurun_out/prof_r05 gpurun_out/m7/r05 > gpurun_out/m7/pmc.log 2>&1
-S="python bench.py --workload snake --steps 10 --warmup 3 --no-cpu"
-run snake_auto 200 $S
-run snake_tree 200 $S --nn tree
-run snake_ppc8 200 $S --nn grid --ppc 8
-run snake_ppc32 200 $S --nn grid --ppc 32
+python scripts/pmc_summary.py gpurun_out/prof_r05 $OUT/r05 > $OUT/pmc.log 2>&1
+python scripts/trace_rounds.py gpurun_out/prof_r05/kt/run_kernel_trace.csv --warmup 3 --steps 20 --json $OUT/r05/timed_rounds.json > $OUT/rounds.txt 2>&1
 echo all done
