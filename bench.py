@@ -141,11 +141,18 @@ def roofline(per_launch, cst, K, n0, d, pmax, nn_mode, traffic_path):
         gbs = b / (ms * 1e-3) / 1e9
         stages[s] = {"kernel": kernels[s], "ms": round(ms, 4), "bytes": int(b), "achieved_gbs": round(gbs, 1),
                      "frac": round(gbs / HBM_PEAK_GBS, 4)}
+        t = pmc_traffic(traffic_path, kernels[s])
+        if t is not None:  # measured HBM bytes per launch (rocprofv3 PMC) over the same time
+            stages[s]["traffic"] = t
+            stages[s]["traffic_gbs"] = round(t / (ms * 1e-3) / 1e9, 1)
     dominant = max(stages, key=lambda s: stages[s]["ms"])
     st = stages[dominant]
     traffic = pmc_traffic(traffic_path, st["kernel"])
+    # achieved counts algorithmic bytes, which caches (LDS, L2, MALL) may serve;
+    # traffic_gbs is the measured HBM rate of the same launches, the honest distance to the roof
     out = {"bound": "hbm", "achieved": st["achieved_gbs"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
-           "frac": st["frac"], "traffic": traffic, "kernel": st["kernel"], "stage": dominant,
+           "frac": st["frac"], "traffic": traffic,
+           "traffic_gbs": st.get("traffic_gbs"), "kernel": st["kernel"], "stage": dominant,
            "ms_per_launch": st["ms"], "algorithmic_bytes": st["bytes"], "stages": stages, "work_per_round": cst}
     if dominant == "nn_query" and nn_mode == "brute":
         flops = float(K) * n0 * 3 * d  # 3*d*N FP64 ops per query (sub, mul, add)

@@ -458,6 +458,9 @@ void CollideScratch::ensure(int64_t n_units, int32_t max_clusters) {
         hip_check(hipMalloc(&spill, sizeof(Cand) * (size_t)spill_cap), "alloc spill");
         hip_check(hipMalloc(&ctl, sizeof(uint32_t) * 8), "alloc collide ctl");
         hip_check(hipMemset(ctl, 0, sizeof(uint32_t) * 8), "zero collide ctl");
+        // the null-stream memset is not ordered with the caller's (non-blocking) stream: wait
+        // for it, or the first k_narrow / fused re-run may read stale overflow and spill counts
+        hip_check(hipDeviceSynchronize(), "zero collide ctl sync");
         ctl_par = 0;
     }
     const int64_t segs = (n_units * (int64_t)(max_clusters > 0 ? max_clusters : 1) + 63) / 64;
@@ -475,6 +478,7 @@ void CollideScratch::ensure(int64_t n_units, int32_t max_clusters) {
         hip_check(hipMalloc(&hdr_off, sizeof(uint32_t) * (size_t)(segs + 1)), "alloc header offsets");
         hip_check(hipMalloc(&hdr_dense, sizeof(int32_t) * (size_t)segs * kHdrCap), "alloc dense headers");
         hip_check(hipMemset(hdr_count, 0, sizeof(uint32_t) * (size_t)(segs + 1)), "memset header counts");
+        hip_check(hipDeviceSynchronize(), "memset header counts sync");  // see ctl above
         scan_bytes = 0;
         hip_check(hipcub::DeviceScan::ExclusiveSum(nullptr, scan_bytes, hdr_count, hdr_off, (int)(segs + 1)),
                   "scan size");

@@ -322,6 +322,9 @@ void GridIndex::reserve(int64_t cap_pts, int32_t d, int64_t ncells) {
         // every count starts at zero and each build leaves them so (k_grid_scatter counts
         // down); a build with more cells than the last one relies on this
         hip_check(hipMemset(counts, 0, sizeof(int32_t) * (size_t)cells_cap), "grid counts zero");
+        // the null-stream memset is not ordered with the build's (non-blocking) stream: wait for
+        // it, or k_grid_count may add to stale counts and the scatter write past the points
+        hip_check(hipDeviceSynchronize(), "grid counts zero sync");
         counts_zero = true;
         size_t tb = 0;
         hip_check(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, counts, cell_start, (int)(ncells + 1)), "scan size");

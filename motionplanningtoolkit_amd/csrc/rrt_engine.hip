@@ -697,6 +697,7 @@ extern "C" mpt_status mpt_rrt_collide_stats(mpt_rrt *r, int32_t enable, uint64_t
             for (int i = 0; i < kCollideStats; ++i) out[i] = h[i];
         }
         hip_check(hipMemset(r->d_cstats, 0, sizeof(unsigned long long) * kCollideStats), "memset stats");
+        hip_check(hipDeviceSynchronize(), "memset stats sync");  // null stream vs the engine's stream
         r->stats_on = enable != 0;
     });
 }

@@ -14,9 +14,9 @@ run() {  # name timeout cmd...
   [ $rc -ne 0 ] && exit $rc
   return 0
 }
+run c5 300 python bench.py --seeds 256 --steps 5 --warmup 3 --no-cpu
 run c2 300 python bench.py --steps 30 --warmup 5 --cpu-seconds 15
 run c3 300 python bench.py --workload snake --steps 20 --warmup 3 --cpu-seconds 10
-run c5 300 python bench.py --seeds 256 --steps 5 --warmup 3 --no-cpu
 BENCH_ARGS="--steps 20 --warmup 3 --no-cpu" bash scripts/profile.sh r05 || exit $?
 python scripts/pmc_summary.py gpurun_out/prof_r05 $OUT/r05 > $OUT/pmc.log 2>&1
 python scripts/trace_rounds.py gpurun_out/prof_r05/kt/run_kernel_trace.csv --warmup 3 --steps 20 --json $OUT/r05/timed_rounds.json > $OUT/rounds.txt 2>&1

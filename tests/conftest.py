@@ -23,7 +23,12 @@ def pytest_configure(config):
 
 @pytest.fixture(scope="session")
 def mpt_gpu():
-    """libmpt initialised on device 0 -- fails loudly (no CPU fallback) without a gfx950."""
+    """libmpt initialised on device 0 -- fails loudly (no CPU fallback) without a gfx950.
+    torch's HIP runtime comes up first, as in bench.py, so tests that hand torch streams to
+    the library (config 5's engines on streams) run in the same process layout."""
+    import torch
+
+    torch.cuda.init()
     import motionplanningtoolkit_amd as mpt
 
     mpt.init(0)

@@ -176,6 +176,43 @@ def test_engine_tree_from_one_root(mpt_gpu, name):
         assert np.array_equal(trees[0][1], t[1])
 
 
+def test_engines_on_streams_match_one_stream(mpt_gpu):
+    """Config 5's execution model: many independent seeds, each its own engine grown from one
+    root, their rounds interleaved over several HIP streams (first-use allocations happen
+    while other engines' kernels run).  Every seed's tree must equal the one it grows alone
+    on the default stream, bit for bit."""
+    import torch
+
+    sc = scenes.blimp_scenario("all")
+    root = np.array([[88.6, 68.9, 57.1, 0, 0, 0, 0.0]])
+    env = mpt_gpu.Environment(sc.env_tris, sc.env_tf)
+    ag = mpt_gpu.AgentMesh(sc.agent_tris)
+    K, rounds, seeds = 2048, 5, list(range(300, 312))
+
+    def grow(streams):
+        engs = []
+        for s in seeds:
+            e = mpt_gpu.RRTEngine(env, ag, sc.kind, sc.prm, sc.ranges, sc.steer_dt, sc.cc_dt, 1 + rounds * K, s)
+            e.add_nodes(root)
+            engs.append(e)
+        for _ in range(rounds):
+            for j, e in enumerate(engs):
+                e.step(K, streams[j % len(streams)] if streams else None)
+        torch.cuda.synchronize()
+        out = []
+        for e in engs:
+            n = e.counters()["nodes"]
+            out.append(e.read_tree(n))
+            e.close()
+        return out
+
+    alone = grow(None)
+    mixed = grow([torch.cuda.Stream() for _ in range(4)])
+    for (sa, pa), (sb, pb) in zip(alone, mixed):
+        assert len(sa) > 1
+        assert np.array_equal(bits(sa), bits(sb)) and np.array_equal(pa, pb)
+
+
 def test_engine_set_size_and_capacity(mpt_gpu, oracle):
     sc = scenes.omni_scenario()
     eng, tree = make(mpt_gpu, sc, 100, 256, 5, cap_extra=50)
