@@ -731,6 +731,43 @@ __global__ __launch_bounds__(256) void k_grid_nn1_runs(GridDev G, const double *
     nn1_runs_query<D, kGroup, kPts>(G, q, slot, (int)(t % kGroup), out_ids, out_d2);
 }
 
+// XCD-aware variant.  The points are in cell order, x-major, so the cells of an x-slab
+// [s n0 / 8, (s + 1) n0 / 8) are one contiguous slice of the point array.  Workgroups are
+// dealt round-robin over the 8 XCDs, so workgroup b and b + 8 share an XCD (and its 4 MiB
+// L2): workgroup b serves slab b % 8 and scans the chunk b / 8 of kSlabChunk queries for
+// the ones whose cell lies in its slab.  Each XCD's L2 then holds about an eighth of the
+// tree (plus the neighbouring cells), instead of every XCD streaming the whole 5.6 MB tree
+// through its L2.  Queries whose walk leaves the slab are still exact (placement only
+// changes speed).  About 3/4 of the groups have a query per chunk (the chunk holds 6 NG
+// queries for NG groups; more than NG of one slab take a second turn).
+template <int D, int kGroup, int kPts>
+__global__ __launch_bounds__(256) void k_grid_nn1_runs_xcd(GridDev G, const double *__restrict__ q, int64_t nq,
+                                                           int32_t *__restrict__ out_ids,
+                                                           double *__restrict__ out_d2) {
+    constexpr int NG = 256 / kGroup;
+    constexpr int kChunk = 6 * NG;  // <= 96 queries: two waves scan them
+    __shared__ int32_t s_idx[kChunk];
+    __shared__ int32_t s_cnt[2];
+    const int slab = blockIdx.x & 7;
+    const int64_t base = (int64_t)(blockIdx.x >> 3) * kChunk;
+    const GridParams &g = G.g;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    bool mine = false;
+    if (threadIdx.x < kChunk && base + threadIdx.x < nq) {
+        const double x = q[(base + threadIdx.x) * D + g.dims[0]];
+        const int cx = cell_coord(x, g.lo[0], g.inv_h, g.n[0]);
+        mine = (cx * 8) / g.n[0] == slab;
+    }
+    const uint64_t m = __ballot(mine);
+    if (wave < 2 && lane == 0) s_cnt[wave] = (int32_t)__popcll(m);
+    __syncthreads();
+    if (mine) s_idx[(wave ? s_cnt[0] : 0) + (int)__popcll(m & ((1ull << lane) - 1ull))] = (int32_t)(base + threadIdx.x);
+    __syncthreads();
+    const int total = s_cnt[0] + (kChunk > 64 ? s_cnt[1] : 0);
+    const int grp = threadIdx.x / kGroup, sub = threadIdx.x % kGroup;
+    for (int i = grp; i < total; i += NG) nn1_runs_query<D, kGroup, kPts>(G, q, s_idx[i], sub, out_ids, out_d2);
+}
+
 template <int D>
 static void grid_knn_d(const GridDev &G, int32_t d, const double *q, int64_t nq, int32_t k, int32_t *ids, double *d2,
                        hipStream_t stream) {
@@ -752,13 +789,22 @@ static void grid_knn_d(const GridDev &G, int32_t d, const double *q, int64_t nq,
         // for the snake's d = 15 (0.85 ms vs 0.90 ms at 16 x 2)
         static const int pts = getenv("MPT_NN1_PTS") ? atoi(getenv("MPT_NN1_PTS")) : (D >= 15 ? 2 : 1);
         const int rgroup = getenv("MPT_NN1_GROUP") ? group : (D >= 15 ? 32 : 16);
-#define MPT_NN1_RUNS_LAUNCH(GRP, PTS)                                                                          \
-    hipLaunchKernelGGL((k_grid_nn1_runs<DD, GRP, PTS>), dim3((unsigned)((nq * GRP + 255) / 256)), dim3(256), 0, \
-                       stream, G, q, nq, ids, d2)
+        // XCD-slab variant for the snake's d = 15 (12 MB of points, three L2s' worth: NN 0.85 ->
+        // 0.72 ms); config 2's 5.6 MB tree gains less than the idle groups cost (54 -> 65 us).
+        // MPT_NN1_XCD=0/1 overrides (scripts/ab_nnxcd.sh)
+        static const bool xcd = getenv("MPT_NN1_XCD") ? atoi(getenv("MPT_NN1_XCD")) == 1 : D >= 15;
+#define MPT_NN1_RUNS_LAUNCH(GRP, PTS)                                                                            \
+    if (xcd)                                                                                                     \
+        hipLaunchKernelGGL((k_grid_nn1_runs_xcd<DD, GRP, PTS>),                                                  \
+                           dim3((unsigned)(((nq + 6 * (256 / GRP) - 1) / (6 * (256 / GRP))) * 8)), dim3(256), 0, \
+                           stream, G, q, nq, ids, d2);                                                           \
+    else                                                                                                         \
+        hipLaunchKernelGGL((k_grid_nn1_runs<DD, GRP, PTS>), dim3((unsigned)((nq * GRP + 255) / 256)), dim3(256), \
+                           0, stream, G, q, nq, ids, d2)
         if (rgroup == 16) {
-            if (pts == 1) MPT_NN1_RUNS_LAUNCH(16, 1); else MPT_NN1_RUNS_LAUNCH(16, 2);
+            if (pts == 1) { MPT_NN1_RUNS_LAUNCH(16, 1); } else { MPT_NN1_RUNS_LAUNCH(16, 2); }
         } else {
-            if (pts == 1) MPT_NN1_RUNS_LAUNCH(32, 1); else MPT_NN1_RUNS_LAUNCH(32, 2);
+            if (pts == 1) { MPT_NN1_RUNS_LAUNCH(32, 1); } else { MPT_NN1_RUNS_LAUNCH(32, 2); }
         }
 #undef MPT_NN1_RUNS_LAUNCH
     } else if (k == 1 && !per_lane && group == 32) {
