@@ -12,8 +12,8 @@
 //           (unit, cluster, triangle) pair.  Two passes (count, then write) give each thread
 //           a contiguous run of its wave's pair segment and one header; the reservations are
 //           LDS atomics.
-// scan      exclusive sum of the per-segment header counts (hipcub), k_expand writes the
-//           header slots densely.
+// scan      exclusive sum of the per-segment header counts whose epilogue writes the header
+//           slots densely (scan.h, one launch).
 // k_cands   one wave per header (grid-stride over the dense list): lanes = the cluster's
 //           agent triangles, mapped exactly (FP64) and boxed; lanes also fetch the header's
 //           env triangle boxes, which are then tested from registers; overlaps become
@@ -24,6 +24,7 @@
 #include <hipcub/hipcub.hpp>
 
 #include "collide_common.h"
+#include "scan.h"
 
 namespace mpt {
 
@@ -289,14 +290,15 @@ __global__ __launch_bounds__(kPairThreads) void k_pairs(EnvDev env, const AgentD
     }
 }
 
-// header slots in dense order: dense[off[seg] + h] = seg * kHdrCap + h
-__global__ void k_expand(const uint32_t *__restrict__ count, const uint32_t *__restrict__ off, int64_t n_seg,
-                         int32_t *__restrict__ dense) {
-    const int64_t seg = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (seg >= n_seg) return;
-    const uint32_t n = count[seg], o = off[seg];
-    for (uint32_t h = 0; h < n; ++h) dense[o + h] = (int32_t)(seg * kHdrCap + h);
-}
+// scan epilogue: header slots in dense order, dense[off[seg] + h] = seg * kHdrCap + h
+struct ExpandHeaders {
+    int32_t *dense;
+    int64_t n_seg;
+    __device__ void operator()(int64_t seg, uint32_t off, uint32_t n) const {
+        if (seg >= n_seg) return;  // the sentinel slot
+        for (uint32_t h = 0; h < n; ++h) dense[off + h] = (int32_t)(seg * kHdrCap + h);
+    }
+};
 
 // Append the lanes of h (ballot m) as candidates: to the wave's segment, or once that is
 // full to the shared spill list; false if both are full.  Called with all lanes active.
@@ -439,8 +441,7 @@ __global__ void k_count_units(CollideWork w) {
 }
 
 CollideScratch::~CollideScratch() {
-    void *ps[] = {pairs, hdr, hdr_count, pair_count, hdr_off, hdr_dense, scan_tmp, cand, cand_count, spill, ctl,
-                  ovf_list};
+    void *ps[] = {pairs, hdr, hdr_count, pair_count, hdr_off, hdr_dense, cand, cand_count, spill, ctl, ovf_list};
     for (void *p : ps)
         if (p) (void)hipFree(p);
 }
@@ -466,10 +467,9 @@ void CollideScratch::ensure(int64_t n_units, int32_t max_clusters) {
     const int64_t segs = (n_units * (int64_t)(max_clusters > 0 ? max_clusters : 1) + 63) / 64;
     if (segs > n_seg) {
         if (segs * kHdrCap >= (int64_t(1) << 31)) throw Error{5, "collide batch too large"};
-        void *ps[] = {pairs, hdr, hdr_count, pair_count, hdr_off, hdr_dense, scan_tmp};
+        void *ps[] = {pairs, hdr, hdr_count, pair_count, hdr_off, hdr_dense};
         for (void *p : ps)
             if (p) hip_check(hipFree(p), "hipFree");
-        scan_tmp = nullptr;
         pair_cap = kPairCap;
         hip_check(hipMalloc(&pairs, sizeof(int32_t) * (size_t)segs * pair_cap), "alloc pairs");
         hip_check(hipMalloc(&hdr, sizeof(PairHdr) * (size_t)segs * kHdrCap), "alloc headers");
@@ -479,10 +479,7 @@ void CollideScratch::ensure(int64_t n_units, int32_t max_clusters) {
         hip_check(hipMalloc(&hdr_dense, sizeof(int32_t) * (size_t)segs * kHdrCap), "alloc dense headers");
         hip_check(hipMemset(hdr_count, 0, sizeof(uint32_t) * (size_t)(segs + 1)), "memset header counts");
         hip_check(hipDeviceSynchronize(), "memset header counts sync");  // see ctl above
-        scan_bytes = 0;
-        hip_check(hipcub::DeviceScan::ExclusiveSum(nullptr, scan_bytes, hdr_count, hdr_off, (int)(segs + 1)),
-                  "scan size");
-        hip_check(hipMalloc(&scan_tmp, scan_bytes), "alloc scan temp");
+        hdr_scan.reserve(segs + 1);
         n_seg = segs;
     }
     if (n_units > ovf_cap) {
@@ -541,12 +538,7 @@ static void collide_split_chunk(const EnvDev &env, const AgentDev *d_links, int3
     hip_check(hipGetLastError(), "k_pairs launch");
     mark(0);
     // count slot `segs` is the scan's sentinel (a larger earlier launch may have used it): k_pairs zeroed it
-    size_t tb = s.scan_bytes;
-    hip_check(hipcub::DeviceScan::ExclusiveSum(s.scan_tmp, tb, s.hdr_count, s.hdr_off, (int)(segs + 1), stream),
-              "header scan");
-    hipLaunchKernelGGL(k_expand, dim3((unsigned)((segs + 255) / 256)), dim3(256), 0, stream, s.hdr_count, s.hdr_off,
-                       segs, s.hdr_dense);
-    hip_check(hipGetLastError(), "k_expand launch");
+    launch_scan_excl(s.hdr_scan, s.hdr_count, s.hdr_off, segs + 1, stream, ExpandHeaders{s.hdr_dense, segs});
     hipLaunchKernelGGL(k_cands, dim3((unsigned)((s.n_cwaves + 3) / 4)), dim3(256), 0, stream, env, d_links, w, a);
     hip_check(hipGetLastError(), "k_cands launch");
     mark(1);

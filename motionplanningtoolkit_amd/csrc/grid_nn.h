@@ -79,8 +79,7 @@ private:
     int32_t dim = 0;
     double *spts = nullptr;
     int32_t *sids = nullptr, *cell_of = nullptr, *counts = nullptr, *cell_start = nullptr;
-    void *temp = nullptr;
-    size_t temp_bytes = 0;
+    ScanState scan;  // counts -> cell_start, one launch
 };
 
 void launch_grid_knn(const GridDev &G, int32_t d, const double *q, int64_t nq, int32_t k, int32_t *ids, double *d2,

@@ -12,7 +12,7 @@
 //   * the walk stops once LB_safe^2 > worst-of-k (strict: exact ties are still visited and
 //     resolved by id), LB_safe = LB minus a slack far above the rounding of the cell
 //     assignment, so the result equals the brute-force result bit for bit.
-// Build per snapshot: cell id per point (atomic histogram) -> exclusive scan (hipcub) ->
+// Build per snapshot: cell id per point (atomic histogram) -> exclusive scan (scan.h) ->
 // scatter of coordinates and ids into cell order.  The in-cell order is arbitrary, which
 // cannot change any result (all ties resolve by id).
 #include <algorithm>
@@ -21,6 +21,7 @@
 #include <hipcub/hipcub.hpp>
 
 #include "grid_nn.h"
+#include "scan.h"
 
 namespace mpt {
 
@@ -326,18 +327,12 @@ void GridIndex::reserve(int64_t cap_pts, int32_t d, int64_t ncells) {
         // it, or k_grid_count may add to stale counts and the scatter write past the points
         hip_check(hipDeviceSynchronize(), "grid counts zero sync");
         counts_zero = true;
-        size_t tb = 0;
-        hip_check(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, counts, cell_start, (int)(ncells + 1)), "scan size");
-        if (tb > temp_bytes) {
-            if (temp) hip_check(hipFree(temp), "free");
-            hip_check(hipMalloc(&temp, tb), "scan temp");
-            temp_bytes = tb;
-        }
+        scan.reserve(ncells + 1);
     }
 }
 
 GridIndex::~GridIndex() {
-    void *ps[] = {spts, sids, cell_of, counts, cell_start, temp};
+    void *ps[] = {spts, sids, cell_of, counts, cell_start};
     for (void *p : ps)
         if (p) (void)hipFree(p);
 }
@@ -360,8 +355,8 @@ void GridIndex::build(const double *pts, int64_t n_upper, const int64_t *n_dev, 
                                cell_of, counts, SpreadOut{});
         hip_check(hipGetLastError(), "k_grid_count");
     }
-    size_t tb = temp_bytes;
-    hip_check(hipcub::DeviceScan::ExclusiveSum(temp, tb, counts, cell_start, (int)(g.ncells + 1), stream), "scan");
+    launch_scan_excl(scan, reinterpret_cast<const uint32_t *>(counts), reinterpret_cast<uint32_t *>(cell_start),
+                     g.ncells + 1, stream, NoEpilogue{});
     if (n_upper > 0) {
         const unsigned blocks = (unsigned)((n_upper + 255) / 256);
         if (spread)

@@ -118,6 +118,44 @@ struct PairHdr {
 };
 constexpr int kPairTriBits = 26;  // env triangles per env < 2^26 on the split path
 
+void hip_check(hipError_t e, const char *what);
+// Device state of a single-launch decoupled-look-back scan (scan.h): per-tile status words
+// (epoch-tagged, never reset) and a monotone tile ticket.
+constexpr int kScanTileItems = 2048;  // scan.h kScanTile
+struct ScanState {
+    unsigned long long *status = nullptr;  // [cap_tiles]
+    unsigned long long *ticket = nullptr;  // [1], monotone
+    int64_t cap_tiles = 0;
+    uint32_t epoch = 0;      // of the last launch (1..2^30-1)
+    uint64_t launched = 0;   // tickets handed out by earlier launches
+    ScanState() = default;
+    ScanState(const ScanState &) = delete;
+    ScanState &operator=(const ScanState &) = delete;
+    ~ScanState() {
+        if (status) (void)hipFree(status);
+        if (ticket) (void)hipFree(ticket);
+    }
+    // allocation-time zeroing is followed by a device sync (the null stream does not order
+    // with the caller's non-blocking stream)
+    void reserve(int64_t n) {
+        const int64_t tiles = (n + kScanTileItems - 1) / kScanTileItems;
+        if (!ticket) {
+            hip_check(hipMalloc(&ticket, sizeof(unsigned long long)), "scan ticket");
+            hip_check(hipMemset(ticket, 0, sizeof(unsigned long long)), "scan ticket zero");
+            hip_check(hipDeviceSynchronize(), "scan ticket sync");
+            launched = 0;
+        }
+        if (tiles > cap_tiles) {
+            if (status) hip_check(hipFree(status), "free");
+            cap_tiles = (tiles > 2 * cap_tiles ? tiles : 2 * cap_tiles);
+            hip_check(hipMalloc(&status, sizeof(unsigned long long) * cap_tiles), "scan status");
+            hip_check(hipMemset(status, 0, sizeof(unsigned long long) * cap_tiles), "scan status zero");
+            hip_check(hipDeviceSynchronize(), "scan status sync");
+            epoch = 0;
+        }
+    }
+};
+
 // Device scratch of the two-phase collide path (broad.hip).  Every stage writes to fixed
 // per-wave segments (no device-wide atomics on the hot path); what does not fit goes to
 // the shared spill list, and units that overflow even that are re-run by the fused kernel.
@@ -128,8 +166,7 @@ struct CollideScratch {
     uint32_t *pair_count = nullptr; // [n_seg] pairs written per segment
     uint32_t *hdr_off = nullptr;    // [n_seg + 1]
     int32_t *hdr_dense = nullptr;   // [n_seg * 64] header slots in dense order
-    void *scan_tmp = nullptr;
-    size_t scan_bytes = 0;
+    ScanState hdr_scan;             // header counts -> hdr_off + hdr_dense (one launch)
     Cand *cand = nullptr;           // [n_cwaves][cand_cap]
     uint32_t *cand_count = nullptr; // [n_cwaves]
     Cand *spill = nullptr;          // [spill_cap] shared overflow of full candidate segments
@@ -217,6 +254,7 @@ struct Error {
 };
 
 void hip_check(hipError_t e, const char *what);
+
 // per-thread message returned by mpt_last_error()
 std::string &last_error_ref();
 
