@@ -20,7 +20,8 @@
 //           candidates in the wave's segment (or the spill list).
 // k_narrow  one 64-lane workgroup per candidate segment (plus the spill list), one candidate
 //           per lane: exact transform, tri_gate, intersect_Triangle; verdict[edge] = 1.
-// Units whose pairs overflow a segment are re-run by the fused kernel (list mode).
+// Units whose pairs overflow a segment are re-run by k_narrow's last workgroups with the
+// fused kernel's per-unit walk (collide_common.h collide_unit).
 #include <hipcub/hipcub.hpp>
 
 #include "collide_common.h"
@@ -35,6 +36,7 @@ constexpr int kCandCap = 2048;      // candidates per k_cands wave (then the spi
 constexpr int64_t kSplitChunkUnits = 1 << 18;  // units per launch of the two-phase path
 constexpr int kSpillCap = 1 << 22;  // shared spill list (48 MiB)
 constexpr int kSpillBlocks = 256;   // k_narrow workgroups over the spill list
+constexpr int kOvfBlocks = 64;      // k_narrow workgroups re-running overflowed units
 constexpr int kLdsItems = 2048;     // env tree staged in LDS by k_pairs up to this size (64 KiB)
 constexpr int kStack = kMaxLevels;  // per-thread walk stack (general trees)
 
@@ -409,11 +411,24 @@ __device__ __forceinline__ void narrow_one(const EnvDev &env, const AgentDev *__
         __hip_atomic_store(w.verdict + edge, (uint8_t)1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// Workgroups [0, n_cwaves): one candidate segment each; the next kSpillBlocks: the spill list.
+// Workgroups [0, n_cwaves): one candidate segment each; the next kSpillBlocks: the spill list;
+// the last kOvfBlocks: the units that overflowed a pair segment or the spill list (none in
+// practice), each re-run whole by the fused walk (one wave per unit, BVH from global memory)
+// -- in this launch, so the usual empty case costs no launch of its own.
 __global__ __launch_bounds__(64) void k_narrow(EnvDev env, const AgentDev *__restrict__ links, CollideWork w,
                                                SplitArgs a) {
     const int32_t gw = blockIdx.x;
     uint32_t n_sat = 0;
+    if (gw >= a.n_cwaves + kSpillBlocks) {
+        __shared__ int32_t s_stk[kStackDepth];
+        const uint32_t n_ovf = __hip_atomic_load(a.ctl + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const bool shared_edges = w.pose_edge != nullptr || w.L > 1 || w.pmax > 1;
+        uint32_t nu = 0, nc = 0, nn = 0, ns = 0;
+        for (uint32_t i = (uint32_t)(gw - a.n_cwaves - kSpillBlocks); i < n_ovf; i += kOvfBlocks)
+            collide_unit(env, env.nodes, env.n_nodes, links, w, a.ovf_list[i], s_stk, (int)threadIdx.x, shared_edges,
+                         nc, nn, ns, nu);
+        return;
+    }
     if (gw < a.n_cwaves) {
         const uint32_t cnt = a.cand_count[gw];
         const Cand *seg = a.cand + (int64_t)gw * a.cand_cap;
@@ -542,7 +557,8 @@ static void collide_split_chunk(const EnvDev &env, const AgentDev *d_links, int3
     hipLaunchKernelGGL(k_cands, dim3((unsigned)((s.n_cwaves + 3) / 4)), dim3(256), 0, stream, env, d_links, w, a);
     hip_check(hipGetLastError(), "k_cands launch");
     mark(1);
-    hipLaunchKernelGGL(k_narrow, dim3((unsigned)(s.n_cwaves + kSpillBlocks)), dim3(64), 0, stream, env, d_links, w,
+    hipLaunchKernelGGL(k_narrow, dim3((unsigned)(s.n_cwaves + kSpillBlocks + kOvfBlocks)), dim3(64), 0, stream, env,
+                       d_links, w,
                        a);
     hip_check(hipGetLastError(), "k_narrow launch");
     mark(2);
@@ -550,13 +566,6 @@ static void collide_split_chunk(const EnvDev &env, const AgentDev *d_links, int3
         hipLaunchKernelGGL(k_count_units, dim3((unsigned)((w.n_units + 255) / 256)), dim3(256), 0, stream, w);
         hip_check(hipGetLastError(), "k_count_units launch");
     }
-    // units that overflowed a pair segment or the spill list (none in practice): fused
-    // path, list read on the device, a small grid so the usual empty launch costs little
-    CollideWork f = w;
-    f.unit_list = s.ovf_list;
-    f.unit_list_n = ctl + 1;
-    f.stats = nullptr;
-    launch_collide(env, d_links, f, stream, 64);
 }
 
 // Large batches run in chunks of whole edges (mode A: whole poses) of about kSplitChunkUnits

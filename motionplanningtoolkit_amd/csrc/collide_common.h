@@ -74,4 +74,126 @@ __device__ __forceinline__ bool box_overlap(const float alo[3], const float ahi[
            blo[2] <= ahi[2];
 }
 
+// --- the fused per-unit walk (collide.hip k_collide; broad.hip k_narrow's overflow re-run) ---
+// Uniform walk of the env BVH by one wave per (pose, link) unit; s_nodes is an LDS prefix of
+// env.nodes (or env.nodes itself with n_lds = n_nodes), the stack kStackDepth ints per wave.
+__device__ __forceinline__ bool box_hit(const float lo[3], const float hi[3], const BvhNode &n) {
+    return lo[0] <= n.hi[0] && n.lo[0] <= hi[0] && lo[1] <= n.hi[1] && n.lo[1] <= hi[1] &&
+           lo[2] <= n.hi[2] && n.lo[2] <= hi[2];
+}
+
+// Uniform walk of the env BVH for one cluster.  Returns true on a contact.
+__device__ inline bool walk_env(const BvhNode *__restrict__ s_nodes, int32_t n_lds, const BvhNode *__restrict__ nodes,
+                         const EnvTri *__restrict__ etris, int32_t *stk, bool act, v3 Q1, v3 Q2, v3 Q3,
+                         const float blo[3], const float bhi[3], uint32_t &n_nodes, uint32_t &n_sat) {
+    int sp = 0;
+    int32_t node = 0;
+    for (;;) {
+        // node is wave-uniform (SGPR): LDS prefix via ds_read, the rest via global loads
+        BvhNode nd;
+        if (node < n_lds) {
+            nd = s_nodes[node];
+        } else {
+            typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+            const u32x4 *g = reinterpret_cast<const u32x4 *>(nodes + node);
+            const u32x4 a = __builtin_nontemporal_load(g), b = __builtin_nontemporal_load(g + 1);
+            nd.lo[0] = __uint_as_float(a.x); nd.lo[1] = __uint_as_float(a.y); nd.lo[2] = __uint_as_float(a.z);
+            nd.a = (int32_t)a.w;
+            nd.hi[0] = __uint_as_float(b.x); nd.hi[1] = __uint_as_float(b.y); nd.hi[2] = __uint_as_float(b.z);
+            nd.b = (int32_t)b.w;
+        }
+        ++n_nodes;
+        const bool ov = act && box_hit(blo, bhi, nd);
+        const uint64_t m = __ballot(ov);
+        if (m) {
+            if (nd.b < 0) {
+                const EnvTri &E = etris[nd.a];
+                bool hit = false;
+                if (ov) hit = tri_gate(E.lo, E.hi, Q1, Q2, Q3) && tri_intersect(E, Q1, Q2, Q3);
+                n_sat += __popcll(m);
+                if (__ballot(hit)) return true;
+            } else {
+                if (sp < kStackDepth) stk[sp] = nd.b;
+                ++sp;
+                node = __builtin_amdgcn_readfirstlane(nd.a);
+                continue;
+            }
+        }
+        if (sp == 0) return false;
+        --sp;
+        node = __builtin_amdgcn_readfirstlane(stk[sp]);
+    }
+}
+
+__device__ inline void collide_unit(const EnvDev &env, const BvhNode *s_nodes, int32_t n_lds,
+                             const AgentDev *__restrict__ links, const CollideWork &w, int64_t unit, int32_t *stk,
+                             int lane, bool shared_edges, uint32_t &n_clusters, uint32_t &n_nodes,
+                             uint32_t &n_sat, uint32_t &n_units) {
+    int32_t link;
+    int64_t slot, edge;
+    if (!decode_unit(w, unit, link, slot, edge)) return;
+    const int32_t L = w.L;
+    if (shared_edges && load_flag(w.verdict + edge)) return;
+    ++n_units;
+
+    const double *pose = w.poses + (slot * L + link) * 12;
+    double R2[9], T2[3], R[9], T[3];
+#pragma unroll
+    for (int i = 0; i < 9; ++i) R2[i] = pose[i];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) T2[i] = pose[9 + i];
+    relative_transform(env.tf, env.tf + 9, R2, T2, R, T);
+
+    const AgentDev ag = links[link];
+    const BvhNode root = s_nodes[0];
+
+    for (int32_t cbase = 0; cbase < ag.n_clusters; cbase += kWave) {
+        const int32_t ci = cbase + lane;
+        bool ok = false;
+        if (ci < ag.n_clusters) {
+            const Cluster c = ag.clusters[ci];
+            const v3 cc = xform(R, T, mk(c.c[0], c.c[1], c.c[2]));
+            const double ccv[3] = {cc.x, cc.y, cc.z};
+            float lo[3], hi[3];
+#pragma unroll
+            for (int i = 0; i < 3; ++i) {
+                const double ex = fabs(R[i * 3 + 0]) * c.e[0] + fabs(R[i * 3 + 1]) * c.e[1] +
+                                  fabs(R[i * 3 + 2]) * c.e[2];
+                lo[i] = widen_lo(ccv[i] - ex);
+                hi[i] = widen_hi(ccv[i] + ex);
+            }
+            ok = box_hit(lo, hi, root);
+        }
+        uint64_t m = __ballot(ok);
+        while (m) {
+            const int j = __ffsll((unsigned long long)m) - 1;
+            m &= m - 1;
+            // another unit of this edge may already have found the contact
+            if (shared_edges && load_flag(w.verdict + edge)) return;
+            ++n_clusters;
+            const Cluster c = ag.clusters[cbase + j];
+            const bool act = lane < c.count;
+            v3 Q1 = mk(0, 0, 0), Q2 = Q1, Q3 = Q1;
+            float blo[3] = {0, 0, 0}, bhi[3] = {0, 0, 0};
+            if (act) {
+                const double *t = ag.tris + (int64_t)(c.first + lane) * 9;
+                Q1 = xform(R, T, mk(t[0], t[1], t[2]));
+                Q2 = xform(R, T, mk(t[3], t[4], t[5]));
+                Q3 = xform(R, T, mk(t[6], t[7], t[8]));
+                blo[0] = widen_lo(dmin(Q1.x, dmin(Q2.x, Q3.x)));
+                blo[1] = widen_lo(dmin(Q1.y, dmin(Q2.y, Q3.y)));
+                blo[2] = widen_lo(dmin(Q1.z, dmin(Q2.z, Q3.z)));
+                bhi[0] = widen_hi(dmax(Q1.x, dmax(Q2.x, Q3.x)));
+                bhi[1] = widen_hi(dmax(Q1.y, dmax(Q2.y, Q3.y)));
+                bhi[2] = widen_hi(dmax(Q1.z, dmax(Q2.z, Q3.z)));
+            }
+            if (walk_env(s_nodes, n_lds, env.nodes, env.tris, stk, act, Q1, Q2, Q3, blo, bhi, n_nodes, n_sat)) {
+                if (lane == 0)
+                    __hip_atomic_store(w.verdict + edge, (uint8_t)1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                return;
+            }
+        }
+    }
+}
+
 }  // namespace mpt

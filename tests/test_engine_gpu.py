@@ -114,6 +114,27 @@ def test_engine_rounds(mpt_gpu, oracle, name, nn_mode):
     tree, _ = check_round(mpt_gpu, oracle, sc, eng, tree, seed, K, K // 2 + 3)
 
 
+def test_engine_round_with_pair_overflow(mpt_gpu, oracle):
+    """The blimp against the blimp mesh itself as the environment, every pose within a few
+    units of it: clusters overlap far more env triangles than a pair segment holds, so units
+    overflow and k_narrow's last workgroups re-run them whole with the fused walk.  The round
+    must still match the oracle stage by stage, and the counters must show the re-runs."""
+    import dataclasses
+
+    base = scenes.blimp_scenario("all")
+    ranges = base.ranges.copy()
+    ranges[:3] = [-3.0, 3.0]
+    sc = dataclasses.replace(base, env_tris=base.agent_tris.copy(), env_tf=scenes.IDENTITY_TF.copy(), ranges=ranges)
+    seed, n0, K = 4321, 500, 256
+    eng, tree = make(mpt_gpu, sc, n0, K, seed)
+    eng.set_nn("brute")
+    eng.collide_stats(True)
+    _, v = check_round(mpt_gpu, oracle, sc, eng, tree, seed, 0, K)
+    st = eng.collide_stats(False)
+    assert st["fused_reruns"] > 0
+    assert v.sum() > 0
+
+
 @pytest.mark.parametrize("name", ["omni", "blimp", "snake"])
 def test_engine_rounds_fused_collide(mpt_gpu, oracle, name):
     """The same stage-by-stage parity with the fused collision kernel in the round."""
