@@ -339,16 +339,14 @@ def main():
         round_()
     torch.cuda.synchronize()
     c0 = eng.counters()
+    eng.kernel_times_sum()  # drop the warm-up rounds' stage times
 
-    ktimes = {}
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         round_()
-        for k, v in eng.kernel_times().items():  # hipEvents on the launch stream
-            ktimes[k] = ktimes.get(k, 0.0) + v
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
@@ -365,7 +363,10 @@ def main():
         return
 
     steps = args.steps
-    per_launch = {k: v / steps for k, v in ktimes.items()}
+    # hipEvents on the launch stream, recorded every timed round into the engine's event ring
+    # and read only now (no host sync inside the timed region)
+    ktimes, kt_rounds = eng.kernel_times_sum()
+    per_launch = {k: v / max(kt_rounds, 1) for k, v in ktimes.items()}
     # one more round, outside the timed region, with the collision work counters on
     eng.collide_stats(True)
     round_()

@@ -227,6 +227,10 @@ mpt_status mpt_rrt_collide_stats(mpt_rrt *rrt, int32_t enable, uint64_t out[16])
  * [sample, nn_build, nn_query, steer, collide_pairs, collide_cands, collide_narrow,
  *  collide_rest (memsets, fused re-run; the whole collide stage in fused mode), append]. */
 mpt_status mpt_rrt_kernel_times(mpt_rrt *rrt, float ms[9]);
+/* The same stages summed over every round recorded since the previous call, and the number
+ * of rounds (then reset).  Rounds record into a ring of 64 event sets, so timing a sequence
+ * of rounds needs no host synchronisation between them. */
+mpt_status mpt_rrt_kernel_times_sum(mpt_rrt *rrt, double ms[9], int64_t *rounds);
 
 #ifdef __cplusplus
 }

@@ -73,6 +73,7 @@ SIGNATURES = {
     "mpt_rrt_set_nn": (I32, [P, I32, D]),
     "mpt_rrt_collide_stats": (I32, [P, I32, P]),
     "mpt_rrt_kernel_times": (I32, [P, P]),
+    "mpt_rrt_kernel_times_sum": (I32, [P, P, P]),
     "mpt_host_last_error": (C.c_char_p, []),
     "mpt_host_load_mesh": (I32, [C.c_char_p, I32, P, I64, P, P]),
     "mpt_host_rrt_inst": (I32, [C.c_char_p, I32, I64, P, P, P, P, P]),

@@ -336,6 +336,17 @@ class RRTEngine:
         t["collide"] = t["collide_pairs"] + t["collide_cands"] + t["collide_narrow"] + t["collide_rest"]
         return t
 
+    def kernel_times_sum(self) -> tuple:
+        """(per-stage ms summed over the rounds recorded since the last call, rounds)."""
+        ms = np.zeros(9, np.float64)
+        n = np.zeros(1, np.int64)
+        check(lib().mpt_rrt_kernel_times_sum(self.handle, _p(ms), _p(n)), "mpt_rrt_kernel_times_sum")
+        names = ["sample", "nn_build", "nn_query", "steer", "collide_pairs", "collide_cands", "collide_narrow",
+                 "collide_rest", "append"]
+        t = dict(zip(names, ms.tolist()))
+        t["collide"] = t["collide_pairs"] + t["collide_cands"] + t["collide_narrow"] + t["collide_rest"]
+        return t, int(n[0])
+
     def collide_stats(self, enable: bool) -> dict:
         """Counters since the last call (then reset); enable keeps counting in later rounds."""
         out = np.zeros(16, np.uint64)

@@ -313,7 +313,11 @@ struct mpt_rrt {
     uint64_t ext_base = 0;
     int32_t last_K = 0;
     bool timing = false;
-    hipEvent_t ev[10] = {};
+    // stage timing: a ring of per-round event sets, so timed rounds need no host sync; the
+    // oldest set is folded into acc_ms only when the ring wraps (it completed long before)
+    std::vector<hipEvent_t> ring;  // [kTimingRing][10]
+    int64_t ring_next = 0, ring_done = 0, acc_rounds = 0;
+    double acc_ms[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
     float last_ms[6] = {0, 0, 0, 0, 0, 0};
     // NN structure over the round's snapshot (grid_nn.hip), rebuilt every round
     int32_t nn_mode = MPT_NN_AUTO;
@@ -344,11 +348,26 @@ void rfree(mpt_rrt *r) {
                   r->d_verdict, r->d_scratch, r->d_cstats};
     for (void *p : ps)
         if (p) (void)hipFree(p);
-    for (auto &e : r->ev)
+    for (auto &e : r->ring)
         if (e) (void)hipEventDestroy(e);
     if (r->d_spread) (void)hipFree(r->d_spread);
     if (r->h_spread) (void)hipHostFree(r->h_spread);
     if (r->ev_spread) (void)hipEventDestroy(r->ev_spread);
+}
+
+constexpr int kTimingRing = 64;
+
+// fold the oldest recorded round's stage times into acc_ms
+void timing_fold_one(mpt_rrt *r) {
+    hipEvent_t *e = r->ring.data() + (r->ring_done % kTimingRing) * 10;
+    hip_check(hipEventSynchronize(e[9]), "event sync");
+    for (int i = 0; i < 9; ++i) {
+        float ms = 0.f;
+        hip_check(hipEventElapsedTime(&ms, e[i], e[i + 1]), "elapsed");
+        r->acc_ms[i] += ms;
+    }
+    ++r->acc_rounds;
+    ++r->ring_done;
 }
 
 void ensure_round_buffers(mpt_rrt *r, int32_t K) {
@@ -426,7 +445,6 @@ extern "C" mpt_status mpt_rrt_create(const mpt_env *env, const mpt_agent *agent,
             hip_check(hipMemset(r->d_n, 0, 2 * sizeof(int64_t)), "memset n");
             hip_check(hipMalloc(&r->d_counters, sizeof(unsigned long long) * 8), "alloc counters");
             hip_check(hipMemset(r->d_counters, 0, sizeof(unsigned long long) * 8), "memset counters");
-            for (auto &e : r->ev) hip_check(hipEventCreate(&e), "event");
             r->grid.reset(new GridIndex());
             r->ptree.reset(new PointTree());
             r->grid_gd = agent_kind == MPT_AGENT_SNAKE ? 2 : 3;
@@ -490,8 +508,14 @@ extern "C" mpt_status mpt_rrt_step(mpt_rrt *r, int32_t K, void *stream_) {
         ensure_round_buffers(r, K);
         const EngineParams &p = r->p;
         const unsigned kb = (unsigned)((K + 255) / 256);
+        hipEvent_t *ev = nullptr;
+        if (r->timing) {
+            if (r->ring_next - r->ring_done >= kTimingRing) timing_fold_one(r);
+            ev = r->ring.data() + (r->ring_next % kTimingRing) * 10;
+            ++r->ring_next;
+        }
         auto mark = [&](int i) {
-            if (r->timing) hip_check(hipEventRecord(r->ev[i], stream), "event record");
+            if (ev) hip_check(hipEventRecord(ev[i], stream), "event record");
         };
         if (r->nn_mode == MPT_NN_AUTO && r->spread_pending && hipEventQuery(r->ev_spread) == hipSuccess) {
             // the tree fills less than a quarter of the sampling box: most samples are far
@@ -606,7 +630,7 @@ extern "C" mpt_status mpt_rrt_step(mpt_rrt *r, int32_t K, void *stream_) {
             mark(7);
         } else {
             launch_collide_split(r->env, r->d_links, r->max_clusters, cw, r->cscratch, stream,
-                                 r->timing ? r->ev + 5 : nullptr);
+                                 ev ? ev + 5 : nullptr);
         }
         mark(8);
         hipLaunchKernelGGL(k_append_commit, dim3(kb), dim3(256), 0, stream, r->d_verdict, K, p.d, r->d_ends, r->d_nn,
@@ -714,16 +738,34 @@ extern "C" mpt_status mpt_rrt_enable_timing(mpt_rrt *r, int32_t enable) {
     return guarded([&] {
         if (!r) throw Error{MPT_ERR_INVALID, "null pointer"};
         r->timing = enable != 0;
+        if (r->timing && r->ring.empty()) {
+            r->ring.assign((size_t)kTimingRing * 10, nullptr);
+            for (auto &e : r->ring) hip_check(hipEventCreate(&e), "event");
+        }
     });
 }
 
 extern "C" mpt_status mpt_rrt_kernel_times(mpt_rrt *r, float ms[9]) {
     return guarded([&] {
         if (!r || !ms) throw Error{MPT_ERR_INVALID, "null pointer"};
-        if (!r->timing) throw Error{MPT_ERR_INVALID, "timing not enabled"};
-        hip_check(hipEventSynchronize(r->ev[9]), "event sync");
+        if (!r->timing || r->ring_next == 0) throw Error{MPT_ERR_INVALID, "timing not enabled or no round yet"};
+        hipEvent_t *e = r->ring.data() + ((r->ring_next - 1) % kTimingRing) * 10;
+        hip_check(hipEventSynchronize(e[9]), "event sync");
         // [sample, nn_build, nn_query, steer, collide_pairs, collide_cands, collide_narrow,
         //  collide_rest, append]: consecutive event pairs
-        for (int i = 0; i < 9; ++i) hip_check(hipEventElapsedTime(&ms[i], r->ev[i], r->ev[i + 1]), "elapsed");
+        for (int i = 0; i < 9; ++i) hip_check(hipEventElapsedTime(&ms[i], e[i], e[i + 1]), "elapsed");
+    });
+}
+
+extern "C" mpt_status mpt_rrt_kernel_times_sum(mpt_rrt *r, double ms[9], int64_t *rounds) {
+    return guarded([&] {
+        if (!r || !ms || !rounds) throw Error{MPT_ERR_INVALID, "null pointer"};
+        while (r->ring_done < r->ring_next) timing_fold_one(r);
+        for (int i = 0; i < 9; ++i) {
+            ms[i] = r->acc_ms[i];
+            r->acc_ms[i] = 0.0;
+        }
+        *rounds = r->acc_rounds;
+        r->acc_rounds = 0;
     });
 }
