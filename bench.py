@@ -43,6 +43,9 @@ def parse():
                     help="blimp = BASELINE config 2 (default); snake = config 3 (snake_trailers, 11 links, corridor)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample length")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--stage-every", type=int, default=8,
+                    help="record the per-stage hipEvents on every n-th timed round (0: none); each recorded "
+                         "round pays ~34 us of event packets, so they sample the timed region")
     ap.add_argument("--nn", default="auto", choices=["grid", "brute", "auto", "tree"], help="engine NN structure")
     ap.add_argument("--ppc", type=float, default=0.0,
                     help="grid points per cell (0: the engine's default, 2 floored by the expected NN distance)")
@@ -145,6 +148,9 @@ def roofline(per_launch, cst, K, n0, d, pmax, nn_mode, traffic_path):
         if t is not None:  # measured HBM bytes per launch (rocprofv3 PMC) over the same time
             stages[s]["traffic"] = t
             stages[s]["traffic_gbs"] = round(t / (ms * 1e-3) / 1e9, 1)
+    if not stages:  # no stage timing recorded (--stage-every 0)
+        return {"bound": "hbm", "achieved": None, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": None,
+                "traffic": None, "stages": {}, "work_per_round": cst}
     dominant = max(stages, key=lambda s: stages[s]["ms"])
     st = stages[dominant]
     traffic = pmc_traffic(traffic_path, st["kernel"])
@@ -345,12 +351,15 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    for i in range(args.steps):
+        if args.stage_every != 1:
+            eng.enable_timing(args.stage_every > 0 and i % args.stage_every == 0)
         round_()
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    eng.enable_timing(True)
     c1 = eng.counters()
     valid = c1["valid"] - c0["valid"]
     checked = c1["checked"] - c0["checked"]
