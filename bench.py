@@ -402,6 +402,7 @@ def main():
         "checked_per_s": checked / elapsed,
         "valid_fraction": valid / max(checked, 1),
         "kernel_ms_per_round": {k: round(v, 4) for k, v in per_launch.items()},
+        "stage_timing": f"hipEvents on {kt_rounds} of the {steps} timed rounds (every {args.stage_every})",
         "roofline": roof,
     }
     if not args.no_cpu and world == 1:
