@@ -33,7 +33,7 @@ constexpr int kPairThreads = 256;   // k_pairs workgroup (4 waves)
 constexpr int kPairCap = 256;       // env triangles per k_pairs wave segment
 constexpr int kHdrCap = 64;         // headers per segment (one per lane at most)
 constexpr int kCandCap = 2048;      // candidates per k_cands wave (then the spill list)
-constexpr int64_t kSplitChunkUnits = 1 << 18;  // units per launch of the two-phase path
+constexpr int64_t kSplitChunkThreads = int64_t(1) << 22;  // (unit, cluster) threads per launch of the two-phase path
 constexpr int kSpillCap = 1 << 22;  // shared spill list (48 MiB)
 constexpr int kSpillBlocks = 256;   // k_narrow workgroups over the spill list
 constexpr int kOvfBlocks = 64;      // k_narrow workgroups re-running overflowed units
@@ -187,9 +187,13 @@ __global__ __launch_bounds__(kPairThreads) void k_pairs(EnvDev env, const AgentD
     const int lane = threadIdx.x & 63;
     const int64_t t = (int64_t)blockIdx.x * kPairThreads + threadIdx.x;
     const int64_t seg = t >> 6;
+    // 0. with a live-unit list, threads map to (live unit, cluster); workgroups past the list
+    //    only zero their segments' counts
+    const int64_t n_thr = w.live_units ? (int64_t)*w.n_live * a.n_clusters : w.n_units * a.n_clusters;
     // 1. thread per (pose, cluster): FCL relative transform, cluster box, root cull
     {
-        const int64_t unit = t / a.n_clusters;
+        const int64_t unit = t < n_thr ? (w.live_units ? (int64_t)w.live_units[t / a.n_clusters] : t / a.n_clusters)
+                                       : w.n_units;
         const int32_t c = (int32_t)(t % a.n_clusters);
         bool live = unit < w.n_units;
         int32_t link = 0;
@@ -461,8 +465,15 @@ CollideScratch::~CollideScratch() {
         if (p) (void)hipFree(p);
 }
 
+// units per chunk of the two-phase path: kSplitChunkThreads (unit, cluster) threads, so the
+// per-launch segments hold a chunk's pairs and candidates (the 11-link snake, one cluster per
+// link, runs a whole 720k-unit round in one launch; the 22-cluster blimp 190k units)
+static int64_t split_chunk_units(int32_t max_clusters) {
+    return kSplitChunkThreads / (max_clusters > 0 ? max_clusters : 1);
+}
+
 void CollideScratch::ensure(int64_t n_units, int32_t max_clusters) {
-    n_units = std::min<int64_t>(n_units, kSplitChunkUnits);  // launch_collide_split runs chunks
+    n_units = std::min<int64_t>(n_units, split_chunk_units(max_clusters));  // launch_collide_split runs chunks
     if (!ctl) {
         int dev = 0, cus = 256;
         if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
@@ -568,20 +579,22 @@ static void collide_split_chunk(const EnvDev &env, const AgentDev *d_links, int3
     }
 }
 
-// Large batches run in chunks of whole edges (mode A: whole poses) of about kSplitChunkUnits
+// Large batches run in chunks of whole edges (mode A: whole poses) of about split_chunk_units
 // units, by offsetting the pointers: the per-launch candidate segments and spill list then
 // hold a chunk's candidates instead of overflowing to the fused kernel (config 4's 21 M
 // poses overflowed 8 M units).  The scratch is sized for one chunk.
 void launch_collide_split(const EnvDev &env, const AgentDev *d_links, int32_t max_clusters, const CollideWork &w,
                           CollideScratch &s, hipStream_t stream, hipEvent_t *marks) {
     const int64_t g = w.pose_edge ? (int64_t)w.L : (int64_t)w.pmax * w.L;
-    const int64_t per = std::max<int64_t>(g, (kSplitChunkUnits / g) * g);
+    const int64_t per = std::max<int64_t>(g, (split_chunk_units(max_clusters) / g) * g);
     if (w.n_units <= per) {
         collide_split_chunk(env, d_links, max_clusters, w, s, stream, marks);
         return;
     }
     for (int64_t u0 = 0; u0 < w.n_units; u0 += per) {
         CollideWork c = w;
+        c.live_units = nullptr;  // absolute unit indices: not per chunk
+        c.n_live = nullptr;
         c.n_units = std::min(per, w.n_units - u0);
         if (w.pose_edge) {
             const int64_t p0 = u0 / w.L;

@@ -93,6 +93,11 @@ struct CollideWork {
     // fused kernel only: run just the units listed here (count read on the device)
     const int32_t *unit_list;
     const uint32_t *unit_list_n;
+    // two-phase path, optional: the units whose whole-link box meets the env root box
+    // (FCL's object-level AABB test, done by the producer of the poses); k_pairs then runs
+    // (live unit, cluster) threads only.  Any order; n_live read on the device.
+    const int32_t *live_units;
+    const uint32_t *n_live;
 };
 
 // Broad-phase candidate: (unit, agent triangle, env triangle) whose float boxes overlap.

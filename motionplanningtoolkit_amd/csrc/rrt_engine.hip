@@ -23,6 +23,7 @@
 #include "grid_nn.h"
 #include "point_tree.h"
 #include "mpt_internal.h"
+#include "collide_common.h"
 
 namespace mpt {
 const EnvDev &env_dev(const mpt_env *e);
@@ -128,9 +129,12 @@ __device__ void snake_poses(const double *prm, int T, const double *s, double *o
 // n_dev[1] = n_dev[0]: the round's starting node count, read by k_append_commit (which
 // overwrites n_dev[0] in the same launch)
 __global__ void k_sample(EngineParams p, uint64_t ext_base, int32_t K, double *__restrict__ samples,
-                         int64_t *__restrict__ n_dev) {
+                         int64_t *__restrict__ n_dev, uint32_t *__restrict__ n_live) {
     const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (k == 0) n_dev[1] = n_dev[0];
+    if (k == 0) {
+        n_dev[1] = n_dev[0];
+        if (n_live) *n_live = 0u;  // k_steer's live-unit list of this round
+    }
     if (k >= K) return;
     const uint64_t g = ext_base + (uint64_t)k;
     for (int j = 0; j < p.d; ++j) samples[k * p.d + j] = engine_uniform(p.seed, g * 64 + j, p.lo[j], p.hi[j]);
@@ -141,13 +145,11 @@ __global__ void k_sample(EngineParams p, uint64_t ext_base, int32_t K, double *_
 // and blimp (7) agents at compile time, so their states stay in registers (the snake's
 // 5 + T is a run-time value).
 template <int KIND>
-__global__ __launch_bounds__(256) void k_steer(EngineParams p, uint64_t ext_base, int32_t K,
-                                               const double *__restrict__ nodes, const int32_t *__restrict__ nn,
-                                               double *__restrict__ ends, double *__restrict__ poses,
-                                               int32_t *__restrict__ pcount, uint8_t *__restrict__ verdict,
-                                               unsigned long long *__restrict__ counters) {
-    const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (k >= K) return;
+__device__ __forceinline__ int32_t steer_one(const EngineParams &p, uint64_t ext_base, int64_t k,
+                                             const double *__restrict__ nodes, const int32_t *__restrict__ nn,
+                                             double *__restrict__ ends, double *__restrict__ poses,
+                                             int32_t *__restrict__ pcount, uint8_t *__restrict__ verdict,
+                                             unsigned long long *__restrict__ counters) {
     verdict[k] = 0;  // the collision stage only ever sets verdicts
     const uint64_t g = ext_base + (uint64_t)k;
     constexpr int DD = KIND == MPT_AGENT_OMNI ? 3 : (KIND == MPT_AGENT_BLIMP ? 7 : kMaxDim);
@@ -232,6 +234,63 @@ __global__ __launch_bounds__(256) void k_steer(EngineParams p, uint64_t ext_base
     }
     pcount[k] = P;
     for (int j = 0; j < d; ++j) ends[k * d + j] = end[j];
+    return P;
+}
+
+// The round's units whose whole-link box (AgentDev bc / be) under the pose meets the env
+// root box -- FCL's object-level AABB test before any BVH work; every cluster box lies inside
+// its link's box, so the units left out could only be culled by k_pairs' root test anyway.
+struct LiveOut {
+    int32_t *list;       // [K * pmax * L], or nullptr: no list this round
+    uint32_t *n_live;    // zeroed by k_sample
+    const AgentDev *links;
+    EnvDev env;
+};
+
+// randomSteer + getPoses, then the extension's live units appended to the round's list
+// (one device atomic per workgroup; the list order does not matter to any verdict).
+template <int KIND>
+__global__ __launch_bounds__(256) void k_steer(EngineParams p, uint64_t ext_base, int32_t K,
+                                               const double *__restrict__ nodes, const int32_t *__restrict__ nn,
+                                               double *__restrict__ ends, double *__restrict__ poses,
+                                               int32_t *__restrict__ pcount, uint8_t *__restrict__ verdict,
+                                               unsigned long long *__restrict__ counters, LiveOut lv) {
+    const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    int32_t P = 0;
+    if (k < K) P = steer_one<KIND>(p, ext_base, k, nodes, nn, ends, poses, pcount, verdict, counters);
+    if (!lv.list) return;  // kernel argument: uniform
+    const int32_t units = p.pmax * p.L;  // <= 64 (the launcher checks)
+    uint64_t mask = 0;
+    const double *ps = poses + k * units * 12;
+    for (int32_t i = 0; i < P; ++i)
+        for (int32_t l = 0; l < p.L; ++l) {
+            double R[9], T[3];
+            unit_transform(lv.env, ps + (i * p.L + l) * 12, R, T);
+            float blo[3], bhi[3];
+            local_box(lv.links[l].bc, lv.links[l].be, R, T, blo, bhi);
+            if (box_overlap(blo, bhi, lv.env.root_lo, lv.env.root_hi)) mask |= 1ull << (i * p.L + l);
+        }
+    __shared__ uint32_t s_wave[4];
+    __shared__ uint32_t s_base;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const uint32_t c = (uint32_t)__popcll(mask);
+    uint32_t incl = c;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const uint32_t o = __shfl_up(incl, off);
+        if (lane >= off) incl += o;
+    }
+    if (lane == 63) s_wave[wave] = incl;
+    __syncthreads();
+    if (threadIdx.x == 0) s_base = atomicAdd(lv.n_live, s_wave[0] + s_wave[1] + s_wave[2] + s_wave[3]);
+    __syncthreads();
+    uint32_t pos = s_base + incl - c;
+    for (int w = 0; w < wave; ++w) pos += s_wave[w];
+    while (mask) {
+        const int b = __ffsll((unsigned long long)mask) - 1;
+        mask &= mask - 1;
+        lv.list[pos++] = (int32_t)(k * units + b);
+    }
 }
 
 // Ordered append and commit in one launch: extension k lands at n0 + (number of valid
@@ -307,6 +366,8 @@ struct mpt_rrt {
     int32_t kcap = 0;
     double *d_samples = nullptr, *d_ends = nullptr, *d_poses = nullptr, *d_nnd2 = nullptr;
     int32_t *d_nn = nullptr, *d_pcount = nullptr;
+    int32_t *d_live = nullptr;     // k_steer's live-unit list [K * pmax * L] (two-phase collide)
+    uint32_t *d_nlive = nullptr;   // its length
     uint8_t *d_verdict = nullptr;
     void *d_scratch = nullptr;
     size_t scratch_bytes = 0;
@@ -345,7 +406,7 @@ namespace {
 void rfree(mpt_rrt *r) {
     void *ps[] = {r->d_links, r->d_nodes,   r->d_parents, r->d_n,       r->d_counters, r->d_samples,
                   r->d_ends,  r->d_poses,   r->d_nnd2,    r->d_nn,      r->d_pcount,
-                  r->d_verdict, r->d_scratch, r->d_cstats};
+                  r->d_verdict, r->d_scratch, r->d_cstats, r->d_live, r->d_nlive};
     for (void *p : ps)
         if (p) (void)hipFree(p);
     for (auto &e : r->ring)
@@ -373,7 +434,7 @@ void timing_fold_one(mpt_rrt *r) {
 void ensure_round_buffers(mpt_rrt *r, int32_t K) {
     const size_t need_scratch = nn_knn_scratch_bytes(K, std::max<int64_t>(r->cap, 1), 1);
     if (K > r->kcap) {
-        void *ps[] = {r->d_samples, r->d_ends, r->d_poses, r->d_nnd2, r->d_nn, r->d_pcount, r->d_verdict};
+        void *ps[] = {r->d_samples, r->d_ends, r->d_poses, r->d_nnd2, r->d_nn, r->d_pcount, r->d_verdict, r->d_live};
         for (void *p : ps)
             if (p) hip_check(hipFree(p), "hipFree");
         const int64_t d = r->p.d;
@@ -384,6 +445,8 @@ void ensure_round_buffers(mpt_rrt *r, int32_t K) {
         hip_check(hipMalloc(&r->d_nn, sizeof(int32_t) * K), "alloc nn");
         hip_check(hipMalloc(&r->d_pcount, sizeof(int32_t) * K), "alloc pcount");
         hip_check(hipMalloc(&r->d_verdict, (size_t)K), "alloc verdict");
+        hip_check(hipMalloc(&r->d_live, sizeof(int32_t) * (int64_t)K * r->p.pmax * r->p.L), "alloc live units");
+        if (!r->d_nlive) hip_check(hipMalloc(&r->d_nlive, sizeof(uint32_t)), "alloc live count");
         r->kcap = K;
         r->cscratch.ensure((int64_t)K * r->p.pmax * r->p.L, r->max_clusters);
     }
@@ -536,7 +599,10 @@ extern "C" mpt_status mpt_rrt_step(mpt_rrt *r, int32_t K, void *stream_) {
         const bool use_grid = !use_tree && (r->nn_mode == MPT_NN_GRID || (r->nn_mode == MPT_NN_AUTO && big));
         r->last_nn = use_tree ? MPT_NN_TREE : (use_grid ? MPT_NN_GRID : MPT_NN_BRUTE);
         mark(0);
-        hipLaunchKernelGGL(k_sample, dim3(kb), dim3(256), 0, stream, p, r->ext_base, K, r->d_samples, r->d_n);
+        // k_steer lists the live units for the two-phase collide (FCL's object-level AABB test)
+        const bool live_list = collide_mode() != MPT_COLLIDE_FUSED && p.pmax * p.L <= 64;
+        hipLaunchKernelGGL(k_sample, dim3(kb), dim3(256), 0, stream, p, r->ext_base, K, r->d_samples, r->d_n,
+                           live_list ? r->d_nlive : nullptr);
         hip_check(hipGetLastError(), "k_sample");
         mark(1);
         // the spread feedback rides on this round's index build when none is in flight
@@ -610,8 +676,9 @@ extern "C" mpt_status mpt_rrt_step(mpt_rrt *r, int32_t K, void *stream_) {
         mark(3);
         auto steer = p.kind == MPT_AGENT_OMNI ? k_steer<MPT_AGENT_OMNI>
                      : (p.kind == MPT_AGENT_BLIMP ? k_steer<MPT_AGENT_BLIMP> : k_steer<MPT_AGENT_SNAKE>);
+        LiveOut lv{live_list ? r->d_live : nullptr, r->d_nlive, r->d_links, r->env};
         hipLaunchKernelGGL(steer, dim3(kb), dim3(256), 0, stream, p, r->ext_base, K, r->d_nodes, r->d_nn, r->d_ends,
-                           r->d_poses, r->d_pcount, r->d_verdict, r->d_counters);
+                           r->d_poses, r->d_pcount, r->d_verdict, r->d_counters, lv);
         hip_check(hipGetLastError(), "k_steer");
         mark(4);
         CollideWork cw{};
@@ -623,6 +690,8 @@ extern "C" mpt_status mpt_rrt_step(mpt_rrt *r, int32_t K, void *stream_) {
         cw.n_units = (int64_t)K * p.pmax * p.L;
         cw.verdict = r->d_verdict;
         cw.stats = r->stats_on ? r->d_cstats : nullptr;
+        cw.live_units = live_list ? r->d_live : nullptr;
+        cw.n_live = live_list ? r->d_nlive : nullptr;
         if (collide_mode() == MPT_COLLIDE_FUSED) {
             launch_collide(r->env, r->d_links, cw, stream);
             mark(5);
