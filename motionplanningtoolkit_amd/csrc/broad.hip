@@ -505,7 +505,7 @@ void CollideScratch::ensure(int64_t n_units, int32_t max_clusters) {
         hip_check(hipMalloc(&hdr_dense, sizeof(int32_t) * (size_t)segs * kHdrCap), "alloc dense headers");
         hip_check(hipMemset(hdr_count, 0, sizeof(uint32_t) * (size_t)(segs + 1)), "memset header counts");
         hip_check(hipDeviceSynchronize(), "memset header counts sync");  // see ctl above
-        hdr_scan.reserve(segs + 1);
+        hdr_scan.reserve((segs + 1 + 255) / 256);
         n_seg = segs;
     }
     if (n_units > ovf_cap) {
@@ -564,7 +564,8 @@ static void collide_split_chunk(const EnvDev &env, const AgentDev *d_links, int3
     hip_check(hipGetLastError(), "k_pairs launch");
     mark(0);
     // count slot `segs` is the scan's sentinel (a larger earlier launch may have used it): k_pairs zeroed it
-    launch_scan_excl(s.hdr_scan, s.hdr_count, s.hdr_off, segs + 1, stream, ExpandHeaders{s.hdr_dense, segs});
+    // one segment per thread: the epilogue writes up to 64 header slots per segment
+    launch_scan_excl<1>(s.hdr_scan, s.hdr_count, s.hdr_off, segs + 1, stream, ExpandHeaders{s.hdr_dense, segs});
     hipLaunchKernelGGL(k_cands, dim3((unsigned)((s.n_cwaves + 3) / 4)), dim3(256), 0, stream, env, d_links, w, a);
     hip_check(hipGetLastError(), "k_cands launch");
     mark(1);

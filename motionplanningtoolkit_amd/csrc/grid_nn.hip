@@ -327,7 +327,7 @@ void GridIndex::reserve(int64_t cap_pts, int32_t d, int64_t ncells) {
         // it, or k_grid_count may add to stale counts and the scatter write past the points
         hip_check(hipDeviceSynchronize(), "grid counts zero sync");
         counts_zero = true;
-        scan.reserve(ncells + 1);
+        scan.reserve((ncells + 1 + 2047) / 2048);  // launch_scan_excl<8> tiles
     }
 }
 

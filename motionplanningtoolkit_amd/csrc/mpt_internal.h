@@ -126,7 +126,6 @@ constexpr int kPairTriBits = 26;  // env triangles per env < 2^26 on the split p
 void hip_check(hipError_t e, const char *what);
 // Device state of a single-launch decoupled-look-back scan (scan.h): per-tile status words
 // (epoch-tagged, never reset) and a monotone tile ticket.
-constexpr int kScanTileItems = 2048;  // scan.h kScanTile
 struct ScanState {
     unsigned long long *status = nullptr;  // [cap_tiles]
     unsigned long long *ticket = nullptr;  // [1], monotone
@@ -142,8 +141,7 @@ struct ScanState {
     }
     // allocation-time zeroing is followed by a device sync (the null stream does not order
     // with the caller's non-blocking stream)
-    void reserve(int64_t n) {
-        const int64_t tiles = (n + kScanTileItems - 1) / kScanTileItems;
+    void reserve(int64_t tiles) {
         if (!ticket) {
             hip_check(hipMalloc(&ticket, sizeof(unsigned long long)), "scan ticket");
             hip_check(hipMemset(ticket, 0, sizeof(unsigned long long)), "scan ticket zero");

@@ -4,7 +4,7 @@
 // hipcub's scan is two launches (look-back state init + scan) and the header scan needed a
 // third (k_expand); here each is one.
 //
-// Tile = 256 threads x 8 counts.  A workgroup takes a tile index from a monotone ticket
+// Tile = 256 threads x kItems counts.  A workgroup takes a tile index from a monotone ticket
 // (so tiles are claimed in dispatch order and a tile only ever waits on tiles already
 // running or done), publishes its aggregate, walks back over its predecessors' words until
 // it meets an inclusive prefix, then publishes its own inclusive prefix.  Each status word
@@ -17,9 +17,6 @@
 namespace mpt {
 
 constexpr int kScanThreads = 256;
-constexpr int kScanItems = 8;
-constexpr int kScanTile = kScanThreads * kScanItems;
-static_assert(kScanTile == kScanTileItems, "ScanState (mpt_internal.h) sizes tiles of kScanTileItems");
 
 struct NoEpilogue {
     __device__ void operator()(int64_t, uint32_t, uint32_t) const {}
@@ -29,8 +26,9 @@ __device__ __forceinline__ unsigned long long scan_word(uint32_t epoch, uint32_t
     return ((unsigned long long)epoch << 34) | ((unsigned long long)kind << 32) | v;
 }
 
-// out[i] = sum of in[0, i) for i < n; epi(i, out[i], in[i]) for every i < n.
-template <class Epi>
+// out[i] = sum of in[0, i) for i < n; epi(i, out[i], in[i]) for every i < n.  kItems counts
+// per thread (a tile of 256 kItems); an epilogue with work per element wants kItems = 1.
+template <class Epi, int kItems>
 __global__ __launch_bounds__(kScanThreads) void k_scan_excl(const uint32_t *__restrict__ in, uint32_t *__restrict__ out,
                                                             int64_t n, unsigned long long *__restrict__ status,
                                                             unsigned long long *__restrict__ ticket, uint64_t base,
@@ -41,10 +39,10 @@ __global__ __launch_bounds__(kScanThreads) void k_scan_excl(const uint32_t *__re
     if (threadIdx.x == 0) s_tile = (int64_t)(atomicAdd(ticket, 1ull) - base);
     __syncthreads();
     const int64_t tile = s_tile;
-    const int64_t i0 = tile * kScanTile + (int64_t)threadIdx.x * kScanItems;
-    uint32_t v[kScanItems], sum = 0;
+    const int64_t i0 = tile * (kScanThreads * kItems) + (int64_t)threadIdx.x * kItems;
+    uint32_t v[kItems], sum = 0;
 #pragma unroll
-    for (int k = 0; k < kScanItems; ++k) {
+    for (int k = 0; k < kItems; ++k) {
         v[k] = i0 + k < n ? in[i0 + k] : 0u;
         sum += v[k];
     }
@@ -106,7 +104,7 @@ __global__ __launch_bounds__(kScanThreads) void k_scan_excl(const uint32_t *__re
     __syncthreads();
     uint32_t run = s_prefix + wbase + (incl - sum);
 #pragma unroll
-    for (int k = 0; k < kScanItems; ++k) {
+    for (int k = 0; k < kItems; ++k) {
         if (i0 + k < n) {
             out[i0 + k] = run;
             epi(i0 + k, run, v[k]);
@@ -115,14 +113,14 @@ __global__ __launch_bounds__(kScanThreads) void k_scan_excl(const uint32_t *__re
     }
 }
 
-template <class Epi>
+template <int kItems = 8, class Epi>
 inline void launch_scan_excl(ScanState &s, const uint32_t *in, uint32_t *out, int64_t n, hipStream_t stream, Epi epi) {
     if (n <= 0) return;
-    s.reserve(n);
-    const int64_t tiles = (n + kScanTile - 1) / kScanTile;
+    const int64_t tiles = (n + kScanThreads * kItems - 1) / (kScanThreads * kItems);
+    s.reserve(tiles);
     s.epoch = s.epoch + 1 < (1u << 30) ? s.epoch + 1 : 1u;
-    hipLaunchKernelGGL((k_scan_excl<Epi>), dim3((unsigned)tiles), dim3(kScanThreads), 0, stream, in, out, n, s.status,
-                       s.ticket, (uint64_t)s.launched, s.epoch, epi);
+    hipLaunchKernelGGL((k_scan_excl<Epi, kItems>), dim3((unsigned)tiles), dim3(kScanThreads), 0, stream, in, out, n,
+                       s.status, s.ticket, (uint64_t)s.launched, s.epoch, epi);
     hip_check(hipGetLastError(), "k_scan_excl launch");
     s.launched += (uint64_t)tiles;
 }
