@@ -139,8 +139,14 @@ __global__ __launch_bounds__(256) void k_grid_scatter(const double *__restrict__
     // the cursor counts the cell down from its size, so every count is zero again when the
     // scatter ends and the next build needs no memset
     const int64_t pos = cell_start[cell] + (atomicSub(cursor + cell, 1) - 1);
-    for (int j = 0; j < d; ++j) spts[pos * d + j] = pts[i * d + j];
-    sids[pos] = (int32_t)(i + 1);
+    // record of d + 1 doubles: the coordinates, then the 1-based id in the pad slot, so a
+    // query reads a point and its id from one 32 / 64 / 128-B aligned record
+    double *rec = spts + pos * grid_stride(d);
+    for (int j = 0; j < d; ++j) rec[j] = pts[i * d + j];
+    if (grid_stride(d) > d)
+        rec[d] = __longlong_as_double((long long)(i + 1));
+    else
+        sids[pos] = (int32_t)(i + 1);
 }
 
 template <int KMAX>
@@ -225,9 +231,9 @@ __global__ __launch_bounds__(256) void k_grid_knn(GridDev G, int32_t d, const do
                     const int32_t cell = (cx * n1 + cy) * n2 + cz;
                     const int32_t s = G.cell_start[cell], e = G.cell_start[cell + 1];
                     for (int32_t p = s; p < e; ++p) {
-                        const double dd = D > 0 ? flann_l2<DD>(qq, G.pts + (int64_t)p * DD)
-                                                : flann_l2_dyn(qq, G.pts + (int64_t)p * dim, dim);
-                        const int32_t id = G.ids[p];
+                        const double *rec = G.pts + (int64_t)p * (D > 0 ? grid_stride(D) : G.stride);
+                        const double dd = D > 0 ? flann_l2<DD>(qq, rec) : flann_l2_dyn(qq, rec, dim);
+                        const int32_t id = grid_id<D>(G, rec, dim, p);
                         if (G.removed && G.removed[id - 1]) continue;
                         double kd = bd[0];
                         int32_t ki = bi[0];
@@ -306,10 +312,11 @@ void GridIndex::reserve(int64_t cap_pts, int32_t d, int64_t ncells) {
     if (cap_pts > pts_cap || d != dim) {
         if (spts) hip_check(hipFree(spts), "free");
         if (sids) hip_check(hipFree(sids), "free");
+        sids = nullptr;
         if (cell_of) hip_check(hipFree(cell_of), "free");
         const int64_t c = cap_pts > 0 ? cap_pts : 1;
-        hip_check(hipMalloc(&spts, sizeof(double) * c * d), "grid pts");
-        hip_check(hipMalloc(&sids, sizeof(int32_t) * c), "grid ids");
+        hip_check(hipMalloc(&spts, sizeof(double) * c * grid_stride(d)), "grid pts");
+        if (grid_stride(d) == d) hip_check(hipMalloc(&sids, sizeof(int32_t) * c), "grid ids");
         hip_check(hipMalloc(&cell_of, sizeof(int32_t) * c), "grid cell_of");
         pts_cap = c;
         dim = d;
@@ -376,6 +383,7 @@ GridDev GridIndex::dev() const {
     G.cell_start = cell_start;
     G.pts = spts;
     G.ids = sids;
+    G.stride = grid_stride(dim);
     G.removed = nullptr;
     G.stats = nullptr;
     return G;
@@ -505,9 +513,9 @@ __device__ __forceinline__ void nn1_group_query(const GridDev &G, int32_t d, con
             ++n_cells;
             n_pts += (uint32_t)(e - s);
             for (int32_t p = s; p < e; ++p) {
-                const double dd = D > 0 ? flann_l2<DD>(qq, G.pts + (int64_t)p * DD)
-                                        : flann_l2_dyn(qq, G.pts + (int64_t)p * dim, dim);
-                const int32_t id = G.ids[p];
+                const double *rec = G.pts + (int64_t)p * (D > 0 ? grid_stride(D) : G.stride);
+                const double dd = D > 0 ? flann_l2<DD>(qq, rec) : flann_l2_dyn(qq, rec, dim);
+                const int32_t id = grid_id<D>(G, rec, dim, p);
                 if (G.removed && G.removed[id - 1]) continue;
                 if (nn_better(dd, id, bd, bi)) {
                     bd = dd;
@@ -670,8 +678,9 @@ __device__ __forceinline__ void nn1_runs_query(const GridDev &G, const double *_
 #pragma unroll
                 for (int h = 0; h < kPts; ++h) {
                     if (p[h] >= 0) {
-                        dd[h] = flann_l2<D>(qq, G.pts + (int64_t)p[h] * D);
-                        id[h] = G.ids[p[h]];
+                        const double *rec = G.pts + (int64_t)p[h] * grid_stride(D);
+                        dd[h] = flann_l2<D>(qq, rec);
+                        id[h] = grid_id<D>(G, rec, D, p[h]);
                     }
                 }
 #pragma unroll
