@@ -134,6 +134,8 @@ def roofline(per_launch, cst, K, n0, d, pmax, nn_mode, traffic_path):
     stage's figure is listed under `stages`."""
     stages = {}
     kernels = dict(STAGE_KERNEL, nn_query=NN_KERNEL.get(nn_mode, STAGE_KERNEL["nn_query"]))
+    if nn_mode == "grid":  # the instantiation (its PMC row): the XCD-slab variant for d >= 15
+        kernels["nn_query"] = f"k_grid_nn1_runs_xcd<{d}," if d >= 15 else f"k_grid_nn1_runs<{d},"
     if nn_mode == "tree":
         kernels["nn_build"] = "k_pt_gather"
     for s in kernels:
