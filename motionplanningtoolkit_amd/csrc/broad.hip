@@ -477,8 +477,12 @@ void CollideScratch::ensure(int64_t n_units, int32_t max_clusters) {
     if (!ctl) {
         int dev = 0, cus = 256;
         if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-        n_cwaves = cus * 16;  // k_cands: a resident grid striding over the headers
-        cand_cap = kCandCap;
+        // k_cands: a resident grid striding over the headers; each header is a chain of
+        // dependent loads, so more waves in flight hide more of it (MPT_CANDS_WAVES_PER_CU: A/B)
+        const char *wpc = getenv("MPT_CANDS_WAVES_PER_CU");
+        const int per_cu = wpc && atoi(wpc) > 0 ? atoi(wpc) : 16;
+        n_cwaves = cus * per_cu;
+        cand_cap = (int32_t)std::max<int64_t>(256, (int64_t)kCandCap * 16 / per_cu);
         spill_cap = kSpillCap;
         hip_check(hipMalloc(&cand, sizeof(Cand) * (size_t)n_cwaves * cand_cap), "alloc candidates");
         hip_check(hipMalloc(&cand_count, sizeof(uint32_t) * (size_t)n_cwaves), "alloc candidate counts");

@@ -204,8 +204,15 @@ __device__ __forceinline__ int32_t steer_one(const EngineParams &p, uint64_t ext
         if (steps == 0) steps = 1;
         double s[7];
         for (int j = 0; j < 7; ++j) s[j] = from[j];
+        // one step of cc_dt == steer_dt is the end state itself (same inputs, same operations):
+        // reuse it instead of recomputing its cos / sin / tan
+        const bool same = steps == 1 && p.cc_dt == p.steer_dt;
         for (unsigned i = 0; i < steps; ++i) {
-            blimp_step(p.prm, s, a, w, z, p.cc_dt, s);
+            if (same) {
+                for (int j = 0; j < 7; ++j) s[j] = end[j];
+            } else {
+                blimp_step(p.prm, s, a, w, z, p.cc_dt, s);
+            }
             const double sv = sin(s[3]), cv = cos(s[3]);
             const double R[9] = {cv, sv, 0, -sv, cv, 0, 0, 0, 1};
             if (P < p.pmax) put_pose(ps + 12 * P, R, s[0], s[1], s[2]);
