@@ -55,6 +55,11 @@ def parse():
                          "(0 = config 2, one 100k-node tree per rank)")
     ap.add_argument("--seed-batch", type=int, default=4096, help="config 5: extensions per seed per round")
     ap.add_argument("--streams", type=int, default=32, help="config 5: HIP streams the seeds' rounds rotate over")
+    ap.add_argument("--no-joint-nn", action="store_true",
+                    help="config 5: each seed queries its own tree (default: one joint NN launch per round, "
+                         "mpt_rrt_step_many)")
+    ap.add_argument("--launch-threads", type=int, default=1,
+                    help="config 5: host threads issuing the seeds' rounds (thread t drives streams t, t+T, ...)")
     return ap.parse_args()
 
 
@@ -225,9 +230,34 @@ def run_seeds(args, world, rank, dist, torch, mpt, multiseed, scenes):
     if engines:
         engines[0].enable_timing(True)
 
+    # a seed round is ~25 small launches, so 256 seeds from one host thread are launch-bound;
+    # T threads each drive the engines of streams t, t + T, ... (ctypes drops the GIL)
+    T = max(1, min(args.launch_threads, len(streams)))
+    groups = [[(e, streams[j % len(streams)]) for j, e in enumerate(engines) if (j % len(streams)) % T == t]
+              for t in range(T)]
+
+    def drive(g):
+        for e, s in g:
+            e.step(K, s)
+
+    pool = None
+    if T > 1:
+        from concurrent.futures import ThreadPoolExecutor
+
+        dev = torch.cuda.current_device()
+        pool = ThreadPoolExecutor(T, initializer=torch.cuda.set_device, initargs=(dev,))
+
+    joint = torch.cuda.Stream()
+    eng_streams = [streams[j % len(streams)] for j in range(len(engines))]
+
     def round_():
-        for j, e in enumerate(engines):
-            e.step(K, streams[j % len(streams)])
+        if not args.no_joint_nn:
+            mpt.step_many(engines, K, eng_streams, joint)
+        elif pool is None:
+            drive(groups[0])
+        else:
+            for f in [pool.submit(drive, g) for g in groups]:
+                f.result()
 
     for _ in range(args.warmup):
         round_()
@@ -283,7 +313,8 @@ def run_seeds(args, world, rank, dist, torch, mpt, multiseed, scenes):
         "config": {"workload": f"config 5: {args.seeds} independent blimp RRTs (1355-tri blimp vs model.dae) "
                                f"grown from the start state, {K} extensions per seed per round",
                    "seeds": args.seeds, "seed_base": args.seed, "extensions_per_seed_round": K,
-                   "rounds_before_timing": args.warmup, "streams_per_gpu": len(streams),
+                   "rounds_before_timing": args.warmup, "streams_per_gpu": len(streams), "launch_threads": T,
+                   "joint_nn": not args.no_joint_nn,
                    "parallelism": f"seeds sharded over {world} GPU(s)"},
         "checked_per_s": checked / elapsed,
         "valid_fraction": valid / max(checked, 1),

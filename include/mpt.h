@@ -191,6 +191,11 @@ mpt_status mpt_rrt_set_size(mpt_rrt *rrt, int64_t n, void *stream);
 /* One batched round: K uniform samples -> exact 1-NN -> randomSteer -> getPoses ->
  * collision -> ordered append of the collision-free edges.  Asynchronous. */
 mpt_status mpt_rrt_step(mpt_rrt *rrt, int32_t K, void *stream);
+/* One round of n independent engines (BASELINE config 5: one engine per seed), engine i on
+ * streams[i].  Identical results to mpt_rrt_step per engine; the engines whose round uses the
+ * Morton-tree NN share one query launch on joint_stream (which waits for their sample + index
+ * build and is waited on by their steer + collide + append).  Asynchronous. */
+mpt_status mpt_rrt_step_many(mpt_rrt *const *rrts, int32_t n, int32_t K, void *const *streams, void *joint_stream);
 /* counters [8]: rounds, extensions checked, extensions valid, nodes, capacity drops,
  * pose overflow, reserved, reserved.  Synchronises. */
 mpt_status mpt_rrt_counters(mpt_rrt *rrt, uint64_t counters[8]);

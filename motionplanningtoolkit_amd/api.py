@@ -369,6 +369,16 @@ class RRTEngine:
 
 
 # ---------------------------------------------------------------- host planner (C++)
+
+def step_many(engines, K: int, streams, joint_stream=None) -> None:
+    """One round of several independent engines (mpt_rrt_step_many): engine i on streams[i],
+    the Morton-tree NN queries of all of them in one launch on joint_stream.  Results are
+    those of engines[i].step(K, streams[i]) for every i."""
+    n = len(engines)
+    hs = (C.c_void_p * n)(*[e.handle.value if isinstance(e.handle, C.c_void_p) else e.handle for e in engines])
+    ss = (C.c_void_p * n)(*[(_stream(s).value if s is not None else None) for s in streams])
+    check(lib().mpt_rrt_step_many(hs, n, K, ss, _stream(joint_stream)), "mpt_rrt_step_many")
+
 def load_mesh(path: str, which: str = "all") -> np.ndarray:
     """AssimpMeshLoader replacement: 'all' submeshes (environment) or 'last' (agent)."""
     w = 1 if which == "last" else 0

@@ -77,14 +77,14 @@ __global__ void k_pose_edge(const int64_t *__restrict__ off, int64_t E, int32_t 
 void launch_collide(const EnvDev &env, const AgentDev *d_links, const CollideWork &w, hipStream_t stream,
                     int cap_blocks) {
     if (w.n_units <= 0 || env.n_tris <= 0) return;
-    static int max_blocks = 0;
-    if (max_blocks == 0) {
+    // computed once (thread-safe static init: engines may step from several host threads)
+    static const int max_blocks = [] {
         int dev = 0, cus = 256;
         if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
         int per_cu = 6;  // ~2 workgroups per CU resident (VGPR-limited) x 3 rounds
         if (const char *s = getenv("MPT_COLLIDE_BLOCKS_PER_CU")) per_cu = atoi(s) > 0 ? atoi(s) : per_cu;
-        max_blocks = cus * per_cu;
-    }
+        return cus * per_cu;
+    }();
     const int32_t n_lds = env.n_nodes < kLdsNodes ? env.n_nodes : kLdsNodes;
     const size_t lds = sizeof(BvhNode) * n_lds + sizeof(int32_t) * kStackDepth * kCollideWaves;
     int64_t blocks = (w.n_units + kCollideWaves - 1) / kCollideWaves;

@@ -40,7 +40,8 @@ private:
     int32_t *vals = nullptr, *vals_sorted = nullptr, *sids = nullptr;
     double *spts = nullptr;
     float *boxes = nullptr;
-    unsigned long long *bbox = nullptr;  // [2][kPtMaxDim] order keys
+    unsigned long long *bbox = nullptr;  // [2][kPtMaxDim] order keys, then the box-build ticket
+    unsigned int *ticket = nullptr;
     struct CodePlan *plan = nullptr;
     void *temp = nullptr;
     size_t temp_bytes = 0;
@@ -57,6 +58,16 @@ inline int32_t pt_levels(int64_t n) {
     return L;
 }
 
+// One 1-NN job per tree: nq queries at q, results to ids / d2 (the joint launch of many engines).
+struct PtJob {
+    PointTreeDev T;
+    const double *q;
+    int32_t *ids;
+    double *d2;
+};
+constexpr int kXcds = 8;  // MI355X: workgroups are dealt round-robin over 8 XCDs
+// jobs: a device array [n_jobs], all trees of dim d, nq queries each
+void launch_tree_nn1_jobs(const PtJob *d_jobs, int32_t n_jobs, int32_t d, int64_t nq, hipStream_t stream);
 void launch_tree_nn1(const PointTreeDev &T, const double *q, int64_t nq, int32_t *ids, double *d2, hipStream_t stream);
 // Radius search (d2 < r2) over 3-dim keys: offsets == nullptr -> counts[qi]; else fill ids /
 // d2 of query qi from offsets[qi] on (traversal order).  below_only: ids <= qi only.

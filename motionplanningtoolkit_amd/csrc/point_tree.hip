@@ -5,11 +5,11 @@
 // lie far from every node, and a uniform grid over the sampling box walks many empty rings
 // for them.  Here the cost of a query depends on the tree's shape, not on where it lies.
 //
-// Build (every round, stream-ordered, no host sync): bounding box of the live nodes ->
-// code plan (below) -> 30-bit interleaved code per node -> hipcub radix sort -> coordinates
-// and ids gathered into code order -> leaves of 8 consecutive points and 8-ary levels above
-// them, each box the float-widened bounds over all state dims (a lower bound on FLANN's
-// squared L2).
+// Build (every round, stream-ordered, no host sync; five launches + the sort): bounding box
+// of the live nodes -> code plan (below) -> 30-bit interleaved code per node -> hipcub radix
+// sort -> coordinates and ids gathered into code order with the leaf boxes (8 consecutive
+// points) -> the 8-ary levels above them in one launch, each box the float-widened bounds over
+// all state dims (a lower bound on FLANN's squared L2).
 //
 // Query: 8 lanes per query walk the tree with a per-group LDS stack.  At an inner node the
 // lanes test its 8 children's boxes against the best distance so far and push the survivors
@@ -83,8 +83,17 @@ __global__ __launch_bounds__(256) void k_pt_bbox(const double *__restrict__ pts,
             mn = k < mn ? k : mn;
             mx = k > mx ? k : mx;
         }
-        atomicMin(&s_min[j], mn);
-        atomicMax(&s_max[j], mx);
+        // one LDS atomic per wave, not per lane (256 same-address 64-bit atomics serialise)
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) {
+            const unsigned long long omn = __shfl_xor(mn, off), omx = __shfl_xor(mx, off);
+            mn = omn < mn ? omn : mn;
+            mx = omx > mx ? omx : mx;
+        }
+        if ((threadIdx.x & 63) == 0) {
+            atomicMin(&s_min[j], mn);
+            atomicMax(&s_max[j], mx);
+        }
     }
     __syncthreads();
     if (threadIdx.x < (unsigned)d) {
@@ -93,53 +102,67 @@ __global__ __launch_bounds__(256) void k_pt_bbox(const double *__restrict__ pts,
     }
 }
 
-__global__ void k_pt_plan(int32_t d, const unsigned long long *__restrict__ box, CodePlan *__restrict__ plan,
-                          SpreadOut sp) {
-    if (threadIdx.x != 0 || blockIdx.x != 0) return;
-    if (sp.host_out) {  // the engine's MPT_NN_AUTO feedback (grid_nn.h SpreadOut)
+// One wave: lane k-1 sizes level k (h = emax / 2^k); the plan takes the finest level before
+// the first whose bit total exceeds the code.  The box is reset to empty for the next build.
+__global__ __launch_bounds__(64) void k_pt_plan(int32_t d, unsigned long long *__restrict__ box,
+                                                CodePlan *__restrict__ plan, SpreadOut sp) {
+    __shared__ double s_lo[kPtMaxDim], s_ext[kPtMaxDim];
+    __shared__ int32_t s_b[kPtMaxDim];
+    const int t = threadIdx.x;
+    if (t == 0 && sp.host_out) {  // the engine's MPT_NN_AUTO feedback (grid_nn.h SpreadOut)
         for (int j = 0; j < 3; ++j) {
             sp.host_out[j] = j < sp.gd ? box[sp.dims[j]] : ~0ull;
             sp.host_out[3 + j] = j < sp.gd ? box[kPtMaxDim + sp.dims[j]] : 0ull;
         }
         __threadfence_system();
     }
-    double lo[kPtMaxDim], ext[kPtMaxDim], emax = 0.0;
-    for (int j = 0; j < d; ++j) {
-        lo[j] = key_value_pt(box[j]);
-        const double hi = key_value_pt(box[kPtMaxDim + j]);
-        ext[j] = hi > lo[j] ? hi - lo[j] : 0.0;
-        emax = ext[j] > emax ? ext[j] : emax;
+    if (t < d) {
+        const double lo = key_value_pt(box[t]), hi = key_value_pt(box[kPtMaxDim + t]);
+        s_lo[t] = lo;
+        s_ext[t] = hi > lo ? hi - lo : 0.0;
     }
-    int32_t b[kPtMaxDim];
-    for (int j = 0; j < d; ++j) b[j] = 0;
-    if (emax > 0.0) {
-        // finest level k (h = emax / 2^k) whose bit total fits the code
-        for (int k = 1; k <= kCodeBits; ++k) {
-            const double h = ldexp(emax, -k);
-            int32_t bt[kPtMaxDim], tot = 0;
-            for (int j = 0; j < d; ++j) {
-                int32_t bj = 0;
-                while (bj < k && ldexp(h, bj) < ext[j]) ++bj;
-                bt[j] = bj;
-                tot += bj;
-            }
-            if (tot > kCodeBits) break;
-            for (int j = 0; j < d; ++j) b[j] = bt[j];
+    __syncthreads();
+    if (t < kPtMaxDim) {
+        box[t] = ~0ull;
+        box[kPtMaxDim + t] = 0ull;
+    }
+    double emax = 0.0;
+    for (int j = 0; j < d; ++j) emax = s_ext[j] > emax ? s_ext[j] : emax;
+    bool fail = false;
+    if (emax > 0.0 && t < kCodeBits) {
+        const int k = t + 1;
+        const double h = ldexp(emax, -k);
+        int32_t tot = 0;
+        for (int j = 0; j < d; ++j) {
+            int32_t bj = 0;
+            while (bj < k && ldexp(h, bj) < s_ext[j]) ++bj;
+            tot += bj;
         }
+        fail = tot > kCodeBits;
     }
+    const unsigned long long fm = __ballot(fail);
+    const int kstar = emax > 0.0 ? (fm ? __ffsll((long long)fm) - 1 : kCodeBits) : 0;
+    if (t < d) {
+        int32_t bj = 0;
+        if (kstar > 0) {
+            const double h = ldexp(emax, -kstar);
+            while (bj < kstar && ldexp(h, bj) < s_ext[t]) ++bj;
+        }
+        s_b[t] = bj;
+        plan->lo[t] = s_lo[t];
+        plan->qmax[t] = bj > 0 ? (1u << bj) - 1 : 0u;
+        plan->scale[t] = bj > 0 ? ldexp(1.0, bj) / s_ext[t] : 0.0;
+    }
+    __syncthreads();
+    if (t != 0) return;
     int32_t bmax = 0;
-    for (int j = 0; j < d; ++j) {
-        plan->lo[j] = lo[j];
-        plan->qmax[j] = b[j] > 0 ? (1u << b[j]) - 1 : 0u;
-        plan->scale[j] = b[j] > 0 ? ldexp(1.0, b[j]) / ext[j] : 0.0;
-        bmax = b[j] > bmax ? b[j] : bmax;
-    }
+    for (int j = 0; j < d; ++j) bmax = s_b[j] > bmax ? s_b[j] : bmax;
     int32_t n = 0;
-    for (int t = bmax - 1; t >= 0; --t)
+    for (int b = bmax - 1; b >= 0; --b)
         for (int j = 0; j < d; ++j)
-            if (b[j] > t) {
+            if (s_b[j] > b) {
                 plan->dim[n] = (int8_t)j;
-                plan->bit[n] = (int8_t)t;
+                plan->bit[n] = (int8_t)b;
                 ++n;
             }
     plan->n = n;
@@ -167,64 +190,106 @@ __global__ void k_pt_morton(const double *__restrict__ pts, int32_t d, int64_t n
     keys[i] = code;
 }
 
-__global__ void k_pt_gather(const double *__restrict__ pts, int32_t d, int64_t n_upper, const int64_t *__restrict__ n_dev,
-                            const int32_t *__restrict__ order, double *__restrict__ spts, int32_t *__restrict__ sids) {
+// Coordinates and ids into code order, and the level-1 boxes with them: a leaf is 8
+// consecutive sorted points, i.e. 8 consecutive lanes, so its bounds are an 8-lane reduction.
+__global__ __launch_bounds__(256) void k_pt_gather(const double *__restrict__ pts, int32_t d, int64_t n_upper,
+                                                   const int64_t *__restrict__ n_dev, const int32_t *__restrict__ order,
+                                                   double *__restrict__ spts, int32_t *__restrict__ sids,
+                                                   float *__restrict__ leaf_boxes) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int64_t n = *n_dev < n_upper ? *n_dev : n_upper;
-    if (i >= n) return;
-    const int32_t src = order[i];
-    for (int j = 0; j < d; ++j) spts[i * d + j] = pts[(int64_t)src * d + j];
-    sids[i] = src + 1;
-}
-
-// level-1 boxes: the widened bounds of 8 consecutive points over every dim
-__global__ void k_pt_leaf_boxes(PointTreeDev T, const double *__restrict__ spts, float *__restrict__ boxes) {
-    const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const int64_t n = live_n(T);
-    if (j >= lvl_size(n, 1)) return;
-    const int d = T.d;
-    float *b = boxes + j * 2 * d;
-    const int64_t p0 = j * kPtFan, p1 = p0 + kPtFan < n ? p0 + kPtFan : n;
-    for (int k = 0; k < d; ++k) {
-        double lo = spts[p0 * d + k], hi = lo;
-        for (int64_t p = p0 + 1; p < p1; ++p) {
-            const double x = spts[p * d + k];
-            lo = x < lo ? x : lo;
-            hi = x > hi ? x : hi;
+    const bool live = i < n;  // no early exit: the leaf reduction needs all 8 lanes
+    const int32_t src = live ? order[i] : 0;
+    if (live) sids[i] = src + 1;
+    for (int j = 0; j < d; ++j) {
+        const double x = live ? pts[(int64_t)src * d + j] : 0.0;
+        if (live) spts[i * d + j] = x;
+        double lo = live ? x : __builtin_huge_val(), hi = live ? x : -__builtin_huge_val();
+#pragma unroll
+        for (int off = kPtFan / 2; off > 0; off >>= 1) {
+            const double olo = __shfl_xor(lo, off, kPtFan), ohi = __shfl_xor(hi, off, kPtFan);
+            lo = olo < lo ? olo : lo;
+            hi = ohi > hi ? ohi : hi;
         }
-        b[k] = widen_lo(lo);
-        b[d + k] = widen_hi(hi);
+        if (live && (i & (kPtFan - 1)) == 0) {
+            float *b = leaf_boxes + (i / kPtFan) * 2 * d;
+            b[j] = widen_lo(lo);
+            b[d + j] = widen_hi(hi);
+        }
     }
 }
 
-__global__ void k_pt_up_boxes(PointTreeDev T, int l, float *__restrict__ boxes) {
-    const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const int64_t n = live_n(T);
-    if (j >= lvl_size(n, l)) return;
+// (box j, dim k) of level l >= 2: the bounds of its (up to) 8 children at level l - 1
+__device__ __forceinline__ void pt_up_box(const PointTreeDev &T, int64_t n, int l, float *__restrict__ boxes,
+                                          int64_t j, int k) {
     const int d = T.d;
     const float *child = boxes + lvl_off(T.n_upper, l - 1) * 2 * d;
     float *b = boxes + (lvl_off(T.n_upper, l) + j) * 2 * d;
     const int64_t c0 = j * kPtFan, nc = lvl_size(n, l - 1), c1 = c0 + kPtFan < nc ? c0 + kPtFan : nc;
-    for (int k = 0; k < d; ++k) {
-        float lo = child[c0 * 2 * d + k], hi = child[c0 * 2 * d + d + k];
-        for (int64_t c = c0 + 1; c < c1; ++c) {
-            lo = fminf(lo, child[c * 2 * d + k]);
-            hi = fmaxf(hi, child[c * 2 * d + d + k]);
-        }
-        b[k] = lo;
-        b[d + k] = hi;
+    float lo = child[c0 * 2 * d + k], hi = child[c0 * 2 * d + d + k];
+#pragma unroll
+    for (int c = 1; c < kPtFan; ++c) {  // independent loads; missing children repeat the first
+        const int64_t cc = c0 + c < c1 ? c0 + c : c0;
+        lo = fminf(lo, child[cc * 2 * d + k]);
+        hi = fmaxf(hi, child[cc * 2 * d + d + k]);
     }
+    b[k] = lo;
+    b[d + k] = hi;
+}
+
+// Box levels 2.. in one launch (k_pt_gather writes level 1).  Workgroup g builds the subtree
+// of points [g * 4096, + 4096): levels 2..4 above its 512 leaves (each level's children are its
+// own writes), one thread per (box, dim); the last workgroup to finish (ticket) builds levels
+// 5.. over everyone's level-4 boxes and resets the ticket for the next build.
+constexpr int kPtChunkLeaves = 512;  // 8^3: levels 1..4 inside a workgroup
+constexpr int kPtInBlockLevels = 4;
+
+__global__ __launch_bounds__(256) void k_pt_boxes(PointTreeDev T, float *__restrict__ boxes,
+                                                  unsigned int *__restrict__ ticket) {
+    const int64_t n = live_n(T);
+    const int64_t g = blockIdx.x;
+    const int top_in = T.n_levels < kPtInBlockLevels ? T.n_levels : kPtInBlockLevels;
+    for (int l = 2; l <= top_in; ++l) {
+        const int64_t per = (int64_t)kPtChunkLeaves >> (3 * (l - 1));
+        const int64_t j0 = g * per, nl = lvl_size(n, l), j1 = j0 + per < nl ? j0 + per : nl;
+        // one thread per (box, dim): short dependent chains at the small upper levels
+        for (int64_t it = threadIdx.x; it < (j1 - j0) * T.d; it += blockDim.x) {
+            const int64_t j = j0 + it / T.d;
+            const int k = (int)(it % T.d);
+            pt_up_box(T, n, l, boxes, j, k);
+        }
+        __threadfence_block();
+        __syncthreads();
+    }
+    if (T.n_levels <= kPtInBlockLevels) return;  // one workgroup: its level 4 is the root
+    __shared__ bool last;
+    __threadfence();
+    __syncthreads();
+    if (threadIdx.x == 0) last = atomicAdd(ticket, 1u) == gridDim.x - 1;
+    __syncthreads();
+    if (!last) return;
+    __threadfence();  // agent-scope acquire: this CU's L1 holds no stale copy of the others' boxes
+    for (int l = kPtInBlockLevels + 1; l <= T.n_levels; ++l) {
+        const int64_t nl = lvl_size(n, l);
+        for (int64_t it = threadIdx.x; it < nl * T.d; it += blockDim.x)
+            pt_up_box(T, n, l, boxes, it / T.d, (int)(it % T.d));
+        __threadfence_block();
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) *ticket = 0u;
 }
 
 constexpr int kPtGroupsPerBlock = 256 / kPtFan;
 constexpr int kPtStack = kPtFan * kPtMaxLevels;
 
-template <int D>
-__global__ __launch_bounds__(256) void k_tree_nn1(PointTreeDev T, const double *__restrict__ q, int64_t nq,
-                                                  int32_t *__restrict__ out_ids, double *__restrict__ out_d2) {
-    __shared__ int32_t s_node[kPtGroupsPerBlock][kPtStack];
-    __shared__ double s_lb[kPtGroupsPerBlock][kPtStack];
-    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+// queries [blk * BS / 8, + BS / 8) of one tree (a workgroup's share of k_tree_nn1 / _jobs)
+template <int D, int BS>
+__device__ __forceinline__ void tree_nn1_block(const PointTreeDev &T, const double *__restrict__ q, int64_t nq,
+                                               int32_t *__restrict__ out_ids, double *__restrict__ out_d2,
+                                               int64_t blk) {
+    __shared__ int32_t s_node[BS / kPtFan][kPtStack];
+    __shared__ double s_lb[BS / kPtFan][kPtStack];
+    const int64_t t = blk * BS + threadIdx.x;
     const int64_t slot = t / kPtFan;
     const int sub = (int)(t % kPtFan);
     const int grp = threadIdx.x / kPtFan;
@@ -318,6 +383,25 @@ __global__ __launch_bounds__(256) void k_tree_nn1(PointTreeDev T, const double *
         out_ids[slot] = bi;
         out_d2[slot] = bd;
     }
+}
+
+template <int D, int BS>
+__global__ __launch_bounds__(BS) void k_tree_nn1(PointTreeDev T, const double *__restrict__ q, int64_t nq,
+                                                 int32_t *__restrict__ out_ids, double *__restrict__ out_d2) {
+    tree_nn1_block<D, BS>(T, q, nq, out_ids, out_d2, blockIdx.x);
+}
+
+// Many trees in one launch (mpt_rrt_step_many: one engine per independent seed).  Jobs are
+// dealt to XCDs: workgroup b runs on XCD b % 8, so job j takes the workgroups of XCD j % 8
+// and its tree stays in that XCD's L2.
+template <int D, int BS>
+__global__ __launch_bounds__(BS) void k_tree_nn1_jobs(const PtJob *__restrict__ jobs, int32_t n_jobs, int64_t nq,
+                                                      int64_t blocks_per_job) {
+    const int64_t xcd = blockIdx.x % kXcds, slot = blockIdx.x / kXcds;
+    const int64_t job = xcd + kXcds * (slot / blocks_per_job);
+    if (job >= n_jobs) return;
+    const PtJob &J = jobs[job];
+    tree_nn1_block<D, BS>(J.T, J.q, nq, J.ids, J.d2, slot % blocks_per_job);
 }
 
 // Radius search (FLANN_KDTreeWrapper::kNearestWithin, utilities/flannkdtreewrapper.hpp:91-117:
@@ -417,8 +501,9 @@ void PointTree::reserve(int64_t n_upper, int32_t d) {
         cap = c;
         dim = d;
         size_t tb = 0;
-        hip_check(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, keys, keys_sorted, vals, vals_sorted, (int)c),
-                  "sort size");
+        hipcub::DoubleBuffer<uint32_t> kbuf(keys, keys_sorted);
+        hipcub::DoubleBuffer<int32_t> vbuf(vals, vals_sorted);
+        hip_check(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, kbuf, vbuf, (int)c), "sort size");
         if (tb > temp_bytes) {
             if (temp) hip_check(hipFree(temp), "free");
             hip_check(hipMalloc(&temp, tb), "sort temp");
@@ -427,7 +512,12 @@ void PointTree::reserve(int64_t n_upper, int32_t d) {
         box_cap = 0;
     }
     if (!bbox) {
-        hip_check(hipMalloc(&bbox, sizeof(unsigned long long) * 2 * kPtMaxDim), "pt bbox");
+        // [min keys][max keys] + the box ticket; set once here, reset by the build's own kernels
+        hip_check(hipMalloc(&bbox, sizeof(unsigned long long) * (2 * kPtMaxDim + 1)), "pt bbox");
+        hip_check(hipMemset(bbox, 0xff, sizeof(unsigned long long) * kPtMaxDim), "bbox init");
+        hip_check(hipMemset(bbox + kPtMaxDim, 0, sizeof(unsigned long long) * (kPtMaxDim + 1)), "bbox init");
+        hip_check(hipDeviceSynchronize(), "bbox init sync");  // null stream vs the caller's stream
+        ticket = reinterpret_cast<unsigned int *>(bbox + 2 * kPtMaxDim);
         hip_check(hipMalloc(&plan, sizeof(CodePlan)), "pt plan");
     }
     if (nb * 2 * d > box_cap) {
@@ -451,27 +541,23 @@ void PointTree::build(const double *pts, int64_t n_upper, const int64_t *n_dev, 
     t.ids = sids;
     if (n_upper <= 0) return;
     const unsigned blocks = (unsigned)((n_upper + 255) / 256);
-    hip_check(hipMemsetAsync(bbox, 0xff, sizeof(unsigned long long) * kPtMaxDim, stream), "bbox memset");
-    hip_check(hipMemsetAsync(bbox + kPtMaxDim, 0, sizeof(unsigned long long) * kPtMaxDim, stream), "bbox memset");
+    // bbox starts empty (reserve) and k_pt_plan resets it after reading it
     hipLaunchKernelGGL(k_pt_bbox, dim3(64), dim3(256), 0, stream, pts, d, n_upper, n_dev, bbox);
     hipLaunchKernelGGL(k_pt_plan, dim3(1), dim3(64), 0, stream, d, bbox, plan, spread ? *spread : SpreadOut{});
     hipLaunchKernelGGL(k_pt_morton, dim3(blocks), dim3(256), 0, stream, pts, d, n_upper, n_dev, plan, keys, vals);
     hip_check(hipGetLastError(), "k_pt_morton");
     size_t tb = temp_bytes;
-    hip_check(hipcub::DeviceRadixSort::SortPairs(temp, tb, keys, keys_sorted, vals, vals_sorted, (int)n_upper, 0,
-                                                 32, stream),
-              "radix sort");
-    hipLaunchKernelGGL(k_pt_gather, dim3(blocks), dim3(256), 0, stream, pts, d, n_upper, n_dev, vals_sorted, spts,
-                       sids);
+    // double-buffered: the sort ends in whichever buffer its last pass wrote (no copy back)
+    hipcub::DoubleBuffer<uint32_t> kbuf(keys, keys_sorted);
+    hipcub::DoubleBuffer<int32_t> vbuf(vals, vals_sorted);
+    hip_check(hipcub::DeviceRadixSort::SortPairs(temp, tb, kbuf, vbuf, (int)n_upper, 0, 32, stream), "radix sort");
+    hipLaunchKernelGGL(k_pt_gather, dim3(blocks), dim3(256), 0, stream, pts, d, n_upper, n_dev, vbuf.Current(), spts,
+                       sids, boxes);
     hip_check(hipGetLastError(), "k_pt_gather");
-    const int64_t m1 = lvl_size(n_upper, 1);
-    hipLaunchKernelGGL(k_pt_leaf_boxes, dim3((unsigned)((m1 + 255) / 256)), dim3(256), 0, stream, t, spts, boxes);
-    hip_check(hipGetLastError(), "k_pt_leaf_boxes");
-    for (int l = 2; l <= t.n_levels; ++l) {
-        const int64_t ml = lvl_size(n_upper, l);
-        hipLaunchKernelGGL(k_pt_up_boxes, dim3((unsigned)((ml + 255) / 256)), dim3(256), 0, stream, t, l, boxes);
-        hip_check(hipGetLastError(), "k_pt_up_boxes");
-    }
+    if (t.n_levels < 2) return;  // the gather's one leaf box is the root
+    const unsigned box_groups = (unsigned)((n_upper + kPtChunkLeaves * kPtFan - 1) / (kPtChunkLeaves * kPtFan));
+    hipLaunchKernelGGL(k_pt_boxes, dim3(box_groups), dim3(256), 0, stream, t, boxes, ticket);
+    hip_check(hipGetLastError(), "k_pt_boxes");
 }
 
 void launch_tree_radius(const PointTreeDev &T, const double *q, int64_t nq, double r2, bool below_only,
@@ -488,16 +574,43 @@ void launch_tree_radius(const PointTreeDev &T, const double *q, int64_t nq, doub
     hip_check(hipGetLastError(), "k_tree_radius launch");
 }
 
-void launch_tree_nn1(const PointTreeDev &T, const double *q, int64_t nq, int32_t *ids, double *d2, hipStream_t stream) {
-    if (nq <= 0) return;
-    const dim3 grid((unsigned)((nq * kPtFan + 255) / 256));
+template <int BS>
+static void launch_tree_nn1_bs(const PointTreeDev &T, const double *q, int64_t nq, int32_t *ids, double *d2,
+                               hipStream_t stream) {
+    const dim3 grid((unsigned)((nq * kPtFan + BS - 1) / BS));
     switch (T.d) {
-        case 3: hipLaunchKernelGGL(k_tree_nn1<3>, grid, dim3(256), 0, stream, T, q, nq, ids, d2); break;
-        case 7: hipLaunchKernelGGL(k_tree_nn1<7>, grid, dim3(256), 0, stream, T, q, nq, ids, d2); break;
-        case 15: hipLaunchKernelGGL(k_tree_nn1<15>, grid, dim3(256), 0, stream, T, q, nq, ids, d2); break;
+        case 3: hipLaunchKernelGGL((k_tree_nn1<3, BS>), grid, dim3(BS), 0, stream, T, q, nq, ids, d2); break;
+        case 7: hipLaunchKernelGGL((k_tree_nn1<7, BS>), grid, dim3(BS), 0, stream, T, q, nq, ids, d2); break;
+        case 15: hipLaunchKernelGGL((k_tree_nn1<15, BS>), grid, dim3(BS), 0, stream, T, q, nq, ids, d2); break;
         default: throw Error{1, "point tree: state dim must be 3, 7 or 15"};
     }
     hip_check(hipGetLastError(), "k_tree_nn1 launch");
+}
+
+void launch_tree_nn1(const PointTreeDev &T, const double *q, int64_t nq, int32_t *ids, double *d2, hipStream_t stream) {
+    if (nq <= 0) return;
+    // one-wave workgroups spread an engine round's few thousand queries over all CUs
+    // (MPT_PT_NN1_BLOCK=256: four waves per workgroup; A/B knob)
+    static const int bs = getenv("MPT_PT_NN1_BLOCK") ? atoi(getenv("MPT_PT_NN1_BLOCK")) : 64;
+    if (bs == 256)
+        launch_tree_nn1_bs<256>(T, q, nq, ids, d2, stream);
+    else
+        launch_tree_nn1_bs<64>(T, q, nq, ids, d2, stream);
+}
+
+void launch_tree_nn1_jobs(const PtJob *d_jobs, int32_t n_jobs, int32_t d, int64_t nq, hipStream_t stream) {
+    if (nq <= 0 || n_jobs <= 0) return;
+    constexpr int BS = 64;
+    const int64_t bpj = (nq * kPtFan + BS - 1) / BS;
+    const int64_t groups = (n_jobs + kXcds - 1) / kXcds;
+    const dim3 grid((unsigned)(kXcds * groups * bpj));
+    switch (d) {
+        case 3: hipLaunchKernelGGL((k_tree_nn1_jobs<3, BS>), grid, dim3(BS), 0, stream, d_jobs, n_jobs, nq, bpj); break;
+        case 7: hipLaunchKernelGGL((k_tree_nn1_jobs<7, BS>), grid, dim3(BS), 0, stream, d_jobs, n_jobs, nq, bpj); break;
+        case 15: hipLaunchKernelGGL((k_tree_nn1_jobs<15, BS>), grid, dim3(BS), 0, stream, d_jobs, n_jobs, nq, bpj); break;
+        default: throw Error{1, "point tree: state dim must be 3, 7 or 15"};
+    }
+    hip_check(hipGetLastError(), "k_tree_nn1_jobs launch");
 }
 
 }  // namespace mpt

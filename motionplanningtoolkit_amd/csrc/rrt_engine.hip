@@ -14,6 +14,7 @@
 // (controls), so results are independent of the launch geometry and of the GPU count.
 // K = 1 reference replay with the reference's own RNG streams is the host planner's job
 // (host/rrt.hpp over the same kernels).
+#include <algorithm>
 #include <cstring>
 #include <vector>
 
@@ -570,152 +571,282 @@ extern "C" mpt_status mpt_rrt_set_size(mpt_rrt *r, int64_t n, void *stream) {
     });
 }
 
+namespace {
+
+// One round is three phases so that many engines can share the NN launch (mpt_rrt_step_many):
+// head = sample + NN index build, nn = the NN query, tail = steer, collide, append.
+struct StepCtx {
+    hipEvent_t *ev = nullptr;  // this round's timing events (engine timing on) or null
+    unsigned kb = 0;
+    bool use_tree = false, use_grid = false, live_list = false;
+    void mark(int i, hipStream_t stream) const {
+        if (ev) hip_check(hipEventRecord(ev[i], stream), "event record");
+    }
+};
+
+StepCtx step_head(mpt_rrt *r, int32_t K, hipStream_t stream) {
+    StepCtx c;
+    if (r->n_upper < 1) throw Error{MPT_ERR_INVALID, "tree is empty: add a root first"};
+    ensure_round_buffers(r, K);
+    const EngineParams &p = r->p;
+    const unsigned kb = (unsigned)((K + 255) / 256);
+    hipEvent_t *ev = nullptr;
+    if (r->timing) {
+        if (r->ring_next - r->ring_done >= kTimingRing) timing_fold_one(r);
+        ev = r->ring.data() + (r->ring_next % kTimingRing) * 10;
+        ++r->ring_next;
+    }
+    c.ev = ev;
+    c.kb = kb;
+    if (r->nn_mode == MPT_NN_AUTO && r->spread_pending && hipEventQuery(r->ev_spread) == hipSuccess) {
+        // the tree fills less than a quarter of the sampling box: most samples are far
+        // from every node, where the grid walks empty rings and the Morton tree does not
+        double frac = 1.0;
+        for (int j = 0; j < r->grid_gd; ++j) {
+            const int dj = r->grid_dims[j];
+            const double ext = key_value_u64(r->h_spread[3 + j]) - key_value_u64(r->h_spread[j]);
+            const double range = p.hi[dj] - p.lo[dj];
+            frac *= range > 0 ? std::min(1.0, std::max(0.0, ext / range)) : 1.0;
+        }
+        r->auto_tree = frac < 0.25;
+        r->spread_pending = false;
+        r->spread_seen = true;
+    }
+    const bool big = r->n_upper >= 4096;
+    const bool use_tree = r->nn_mode == MPT_NN_TREE || (r->nn_mode == MPT_NN_AUTO && big && r->auto_tree);
+    const bool use_grid = !use_tree && (r->nn_mode == MPT_NN_GRID || (r->nn_mode == MPT_NN_AUTO && big));
+    r->last_nn = use_tree ? MPT_NN_TREE : (use_grid ? MPT_NN_GRID : MPT_NN_BRUTE);
+    c.mark(0, stream);
+    // k_steer lists the live units for the two-phase collide (FCL's object-level AABB test)
+    const bool live_list = collide_mode() != MPT_COLLIDE_FUSED && p.pmax * p.L <= 64;
+    hipLaunchKernelGGL(k_sample, dim3(kb), dim3(256), 0, stream, p, r->ext_base, K, r->d_samples, r->d_n,
+                       live_list ? r->d_nlive : nullptr);
+    hip_check(hipGetLastError(), "k_sample");
+    c.mark(1, stream);
+    // the spread feedback rides on this round's index build when none is in flight
+    SpreadOut spread;
+    const bool want_spread = r->nn_mode == MPT_NN_AUTO && !r->spread_pending && (use_tree || use_grid) &&
+                             (!r->spread_seen || r->rounds_since_spread >= kSpreadEvery);
+    ++r->rounds_since_spread;
+    if (want_spread) {
+        if (!r->d_spread) {
+            // the grid build's per-block partials [ceil(cap / 256)][6]
+            const int64_t blocks = (r->cap + 255) / 256;
+            hip_check(hipMalloc(&r->d_spread, sizeof(unsigned long long) * blocks * 6), "alloc spread");
+            hip_check(hipHostMalloc(&r->h_spread, sizeof(unsigned long long) * 6,
+                                    hipHostMallocMapped | hipHostMallocCoherent), "alloc spread");
+            hip_check(hipHostGetDevicePointer(reinterpret_cast<void **>(&r->h_spread_dev), r->h_spread, 0),
+                      "spread device pointer");
+            hip_check(hipEventCreateWithFlags(&r->ev_spread, hipEventDisableTiming), "event");
+        }
+        spread.gd = r->grid_gd;
+        for (int j = 0; j < 3; ++j) spread.dims[j] = r->grid_dims[j];
+        spread.partial = r->d_spread;
+        spread.host_out = r->h_spread_dev;
+    }
+    if (use_tree) {
+        r->ptree->reserve(r->cap, p.d);  // once: no allocation (device sync) in later rounds
+        r->ptree->build(r->d_nodes, r->n_upper, r->d_n, p.d, stream, want_spread ? &spread : nullptr);
+    } else if (use_grid) {
+        // spatial dims of the agent's tree state: x, y, z (omni, blimp) or x, y (snake);
+        // the grid spans the sampling ranges, nodes outside fall into the border cells
+        double lo[3], hi[3];
+        for (int j = 0; j < r->grid_gd; ++j) {
+            lo[j] = p.lo[r->grid_dims[j]];
+            hi[j] = p.hi[r->grid_dims[j]];
+        }
+        // cells of ~2 points, but not much finer than the expected NN distance over all
+        // state dims (MPT_NN_HMIN_K: the fraction; A/B knob)
+        static const double hk = getenv("MPT_NN_HMIN_K") ? atof(getenv("MPT_NN_HMIN_K")) : kGridHminK;
+        const double ppc = r->ppc > 0 ? r->ppc : 2.0;
+        const double hmin_n = r->ppc > 0 ? 0.0 : hk * expected_nn_distance(p.d, p.lo, p.hi, r->n_upper);
+        const double hmin_c = r->ppc > 0 ? 0.0 : hk * expected_nn_distance(p.d, p.lo, p.hi, r->cap);
+        const GridParams g = make_grid_params(p.d, r->grid_dims, r->grid_gd, lo, hi, r->n_upper, ppc, hmin_n);
+        const GridParams gcap = make_grid_params(p.d, r->grid_dims, r->grid_gd, lo, hi, r->cap, ppc, hmin_c);
+        r->grid->reserve(r->cap, p.d, std::max(g.ncells, gcap.ncells));  // once, as for the tree
+        r->grid->build(r->d_nodes, r->n_upper, r->d_n, p.d, g, stream, want_spread ? &spread : nullptr);
+    }
+    if (want_spread) {
+        hip_check(hipEventRecord(r->ev_spread, stream), "spread event");
+        r->spread_pending = true;
+        r->rounds_since_spread = 0;
+    }
+    c.mark(2, stream);
+    c.use_tree = use_tree;
+    c.use_grid = use_grid;
+    c.live_list = live_list;
+    return c;
+}
+
+void step_nn(mpt_rrt *r, int32_t K, hipStream_t stream, const StepCtx &c) {
+    const EngineParams &p = r->p;
+    const bool use_tree = c.use_tree, use_grid = c.use_grid;
+    if (use_tree) {
+        PointTreeDev T = r->ptree->dev();
+        T.stats = r->stats_on ? r->d_cstats + 8 : nullptr;
+        launch_tree_nn1(T, r->d_samples, K, r->d_nn, r->d_nnd2, stream);
+    } else if (use_grid) {
+        GridDev G = r->grid->dev();
+        G.stats = r->stats_on ? r->d_cstats + 8 : nullptr;
+        launch_grid_knn(G, p.d, r->d_samples, K, 1, r->d_nn, r->d_nnd2, stream);
+    } else {
+        NNWork w{};
+        w.pts = r->d_nodes;
+        w.removed = nullptr;
+        w.n = r->n_upper;
+        w.d = p.d;
+        w.q = r->d_samples;
+        w.nq = K;
+        w.n_dev = r->d_n;
+        launch_knn(w, 1, r->d_nn, r->d_nnd2, r->d_scratch, stream);
+    }
+    c.mark(3, stream);
+}
+
+void step_tail(mpt_rrt *r, int32_t K, hipStream_t stream, const StepCtx &c) {
+    const EngineParams &p = r->p;
+    const unsigned kb = c.kb;
+    const bool live_list = c.live_list;
+    hipEvent_t *ev = c.ev;
+    auto steer = p.kind == MPT_AGENT_OMNI ? k_steer<MPT_AGENT_OMNI>
+                 : (p.kind == MPT_AGENT_BLIMP ? k_steer<MPT_AGENT_BLIMP> : k_steer<MPT_AGENT_SNAKE>);
+    LiveOut lv{live_list ? r->d_live : nullptr, r->d_nlive, r->d_links, r->env};
+    hipLaunchKernelGGL(steer, dim3(kb), dim3(256), 0, stream, p, r->ext_base, K, r->d_nodes, r->d_nn, r->d_ends,
+                       r->d_poses, r->d_pcount, r->d_verdict, r->d_counters, lv);
+    hip_check(hipGetLastError(), "k_steer");
+    c.mark(4, stream);
+    CollideWork cw{};
+    cw.poses = r->d_poses;
+    cw.pose_edge = nullptr;
+    cw.pcount = r->d_pcount;
+    cw.pmax = p.pmax;
+    cw.L = p.L;
+    cw.n_units = (int64_t)K * p.pmax * p.L;
+    cw.verdict = r->d_verdict;
+    cw.stats = r->stats_on ? r->d_cstats : nullptr;
+    cw.live_units = live_list ? r->d_live : nullptr;
+    cw.n_live = live_list ? r->d_nlive : nullptr;
+    if (collide_mode() == MPT_COLLIDE_FUSED) {
+        launch_collide(r->env, r->d_links, cw, stream);
+        c.mark(5, stream);
+        c.mark(6, stream);
+        c.mark(7, stream);
+    } else {
+        launch_collide_split(r->env, r->d_links, r->max_clusters, cw, r->cscratch, stream,
+                             ev ? ev + 5 : nullptr);
+    }
+    c.mark(8, stream);
+    hipLaunchKernelGGL(k_append_commit, dim3(kb), dim3(256), 0, stream, r->d_verdict, K, p.d, r->d_ends, r->d_nn,
+                       r->d_n, r->cap, r->d_nodes, r->d_parents, r->d_counters);
+    hip_check(hipGetLastError(), "append");
+    c.mark(9, stream);
+    r->ext_base += (uint64_t)K;
+    r->n_upper = std::min<int64_t>(r->cap, r->n_upper + K);
+    r->last_K = K;
+}
+
+}  // namespace
+
 extern "C" mpt_status mpt_rrt_step(mpt_rrt *r, int32_t K, void *stream_) {
     return guarded([&] {
         if (!r || K < 1) throw Error{MPT_ERR_INVALID, "bad arguments"};
-        if (r->n_upper < 1) throw Error{MPT_ERR_INVALID, "tree is empty: add a root first"};
         hipStream_t stream = (hipStream_t)stream_;
-        ensure_round_buffers(r, K);
-        const EngineParams &p = r->p;
-        const unsigned kb = (unsigned)((K + 255) / 256);
-        hipEvent_t *ev = nullptr;
-        if (r->timing) {
-            if (r->ring_next - r->ring_done >= kTimingRing) timing_fold_one(r);
-            ev = r->ring.data() + (r->ring_next % kTimingRing) * 10;
-            ++r->ring_next;
+        const StepCtx c = step_head(r, K, stream);
+        step_nn(r, K, stream, c);
+        step_tail(r, K, stream, c);
+    });
+}
+
+namespace {
+
+// Host-side state of the joint NN launch (one per host thread): the job table is staged in a
+// ring of pinned buffers, so filling one never waits for a copy still in flight.
+constexpr int kJobRing = 4;
+struct JointNN {
+    PtJob *d_jobs = nullptr;
+    PtJob *h_jobs[kJobRing] = {};
+    hipEvent_t copied[kJobRing] = {};
+    int32_t cap = 0, next = 0;
+    std::vector<hipEvent_t> joins;
+    hipEvent_t done = nullptr;
+};
+thread_local JointNN g_joint;
+
+PtJob *joint_jobs(int32_t n, int *slot) {
+    JointNN &g = g_joint;
+    if (n > g.cap) {
+        hip_check(hipDeviceSynchronize(), "sync");  // buffers may still be in use
+        if (g.d_jobs) hip_check(hipFree(g.d_jobs), "free");
+        for (int i = 0; i < kJobRing; ++i)
+            if (g.h_jobs[i]) hip_check(hipHostFree(g.h_jobs[i]), "free");
+        const int32_t c = std::max(n, 2 * g.cap);
+        hip_check(hipMalloc(&g.d_jobs, sizeof(PtJob) * c), "jobs");
+        for (int i = 0; i < kJobRing; ++i) {
+            hip_check(hipHostMalloc(&g.h_jobs[i], sizeof(PtJob) * c), "jobs pinned");
+            if (!g.copied[i]) hip_check(hipEventCreateWithFlags(&g.copied[i], hipEventDisableTiming), "event");
         }
-        auto mark = [&](int i) {
-            if (ev) hip_check(hipEventRecord(ev[i], stream), "event record");
-        };
-        if (r->nn_mode == MPT_NN_AUTO && r->spread_pending && hipEventQuery(r->ev_spread) == hipSuccess) {
-            // the tree fills less than a quarter of the sampling box: most samples are far
-            // from every node, where the grid walks empty rings and the Morton tree does not
-            double frac = 1.0;
-            for (int j = 0; j < r->grid_gd; ++j) {
-                const int dj = r->grid_dims[j];
-                const double ext = key_value_u64(r->h_spread[3 + j]) - key_value_u64(r->h_spread[j]);
-                const double range = p.hi[dj] - p.lo[dj];
-                frac *= range > 0 ? std::min(1.0, std::max(0.0, ext / range)) : 1.0;
+        if (!g.done) hip_check(hipEventCreateWithFlags(&g.done, hipEventDisableTiming), "event");
+        g.cap = c;
+    }
+    *slot = g.next;
+    g.next = (g.next + 1) % kJobRing;
+    // the copy that last read this staging buffer was kJobRing calls ago
+    hip_check(hipEventSynchronize(g.copied[*slot]), "jobs staging");
+    return g.h_jobs[*slot];
+}
+
+}  // namespace
+
+extern "C" mpt_status mpt_rrt_step_many(mpt_rrt *const *rs, int32_t n, int32_t K, void *const *streams_,
+                                        void *joint_stream_) {
+    return guarded([&] {
+        if (!rs || n < 1 || K < 1 || !streams_) throw Error{MPT_ERR_INVALID, "bad arguments"};
+        for (int32_t i = 0; i < n; ++i)
+            if (!rs[i]) throw Error{MPT_ERR_INVALID, "null engine"};
+        auto stream_of = [&](int32_t i) { return (hipStream_t)streams_[i]; };
+        const hipStream_t joint = (hipStream_t)joint_stream_;
+        std::vector<StepCtx> cs(n);
+        for (int32_t i = 0; i < n; ++i) cs[i] = step_head(rs[i], K, stream_of(i));
+        // engines whose round uses the Morton tree (and the first such engine's state dim)
+        // share one NN launch; the rest query their own index on their own stream
+        std::vector<int32_t> J;
+        for (int32_t i = 0; i < n; ++i)
+            if (cs[i].use_tree && (J.empty() || rs[i]->p.d == rs[J[0]]->p.d)) J.push_back(i);
+        std::vector<char> joined(n, 0);
+        if (J.size() >= 2) {
+            JointNN &g = g_joint;
+            int slot = 0;
+            PtJob *h = joint_jobs((int32_t)J.size(), &slot);
+            for (size_t k = 0; k < J.size(); ++k) {
+                mpt_rrt *r = rs[J[k]];
+                PointTreeDev T = r->ptree->dev();
+                T.stats = r->stats_on ? r->d_cstats + 8 : nullptr;
+                h[k] = PtJob{T, r->d_samples, r->d_nn, r->d_nnd2};
+                joined[J[k]] = 1;
             }
-            r->auto_tree = frac < 0.25;
-            r->spread_pending = false;
-            r->spread_seen = true;
-        }
-        const bool big = r->n_upper >= 4096;
-        const bool use_tree = r->nn_mode == MPT_NN_TREE || (r->nn_mode == MPT_NN_AUTO && big && r->auto_tree);
-        const bool use_grid = !use_tree && (r->nn_mode == MPT_NN_GRID || (r->nn_mode == MPT_NN_AUTO && big));
-        r->last_nn = use_tree ? MPT_NN_TREE : (use_grid ? MPT_NN_GRID : MPT_NN_BRUTE);
-        mark(0);
-        // k_steer lists the live units for the two-phase collide (FCL's object-level AABB test)
-        const bool live_list = collide_mode() != MPT_COLLIDE_FUSED && p.pmax * p.L <= 64;
-        hipLaunchKernelGGL(k_sample, dim3(kb), dim3(256), 0, stream, p, r->ext_base, K, r->d_samples, r->d_n,
-                           live_list ? r->d_nlive : nullptr);
-        hip_check(hipGetLastError(), "k_sample");
-        mark(1);
-        // the spread feedback rides on this round's index build when none is in flight
-        SpreadOut spread;
-        const bool want_spread = r->nn_mode == MPT_NN_AUTO && !r->spread_pending && (use_tree || use_grid) &&
-                                 (!r->spread_seen || r->rounds_since_spread >= kSpreadEvery);
-        ++r->rounds_since_spread;
-        if (want_spread) {
-            if (!r->d_spread) {
-                // the grid build's per-block partials [ceil(cap / 256)][6]
-                const int64_t blocks = (r->cap + 255) / 256;
-                hip_check(hipMalloc(&r->d_spread, sizeof(unsigned long long) * blocks * 6), "alloc spread");
-                hip_check(hipHostMalloc(&r->h_spread, sizeof(unsigned long long) * 6,
-                                        hipHostMallocMapped | hipHostMallocCoherent), "alloc spread");
-                hip_check(hipHostGetDevicePointer(reinterpret_cast<void **>(&r->h_spread_dev), r->h_spread, 0),
-                          "spread device pointer");
-                hip_check(hipEventCreateWithFlags(&r->ev_spread, hipEventDisableTiming), "event");
+            // the joint stream waits for every engine stream's heads, the engines' tails for it
+            std::vector<hipStream_t> uniq;
+            for (int32_t i : J)
+                if (std::find(uniq.begin(), uniq.end(), stream_of(i)) == uniq.end()) uniq.push_back(stream_of(i));
+            while (g.joins.size() < uniq.size()) {
+                hipEvent_t e;
+                hip_check(hipEventCreateWithFlags(&e, hipEventDisableTiming), "event");
+                g.joins.push_back(e);
             }
-            spread.gd = r->grid_gd;
-            for (int j = 0; j < 3; ++j) spread.dims[j] = r->grid_dims[j];
-            spread.partial = r->d_spread;
-            spread.host_out = r->h_spread_dev;
-        }
-        if (use_tree) {
-            r->ptree->reserve(r->cap, p.d);  // once: no allocation (device sync) in later rounds
-            r->ptree->build(r->d_nodes, r->n_upper, r->d_n, p.d, stream, want_spread ? &spread : nullptr);
-        } else if (use_grid) {
-            // spatial dims of the agent's tree state: x, y, z (omni, blimp) or x, y (snake);
-            // the grid spans the sampling ranges, nodes outside fall into the border cells
-            double lo[3], hi[3];
-            for (int j = 0; j < r->grid_gd; ++j) {
-                lo[j] = p.lo[r->grid_dims[j]];
-                hi[j] = p.hi[r->grid_dims[j]];
+            for (size_t u = 0; u < uniq.size(); ++u) {
+                hip_check(hipEventRecord(g.joins[u], uniq[u]), "join record");
+                hip_check(hipStreamWaitEvent(joint, g.joins[u], 0), "join wait");
             }
-            // cells of ~2 points, but not much finer than the expected NN distance over all
-            // state dims (MPT_NN_HMIN_K: the fraction; A/B knob)
-            static const double hk = getenv("MPT_NN_HMIN_K") ? atof(getenv("MPT_NN_HMIN_K")) : kGridHminK;
-            const double ppc = r->ppc > 0 ? r->ppc : 2.0;
-            const double hmin_n = r->ppc > 0 ? 0.0 : hk * expected_nn_distance(p.d, p.lo, p.hi, r->n_upper);
-            const double hmin_c = r->ppc > 0 ? 0.0 : hk * expected_nn_distance(p.d, p.lo, p.hi, r->cap);
-            const GridParams g = make_grid_params(p.d, r->grid_dims, r->grid_gd, lo, hi, r->n_upper, ppc, hmin_n);
-            const GridParams gcap = make_grid_params(p.d, r->grid_dims, r->grid_gd, lo, hi, r->cap, ppc, hmin_c);
-            r->grid->reserve(r->cap, p.d, std::max(g.ncells, gcap.ncells));  // once, as for the tree
-            r->grid->build(r->d_nodes, r->n_upper, r->d_n, p.d, g, stream, want_spread ? &spread : nullptr);
+            hip_check(hipMemcpyAsync(g.d_jobs, h, sizeof(PtJob) * J.size(), hipMemcpyHostToDevice, joint), "jobs H2D");
+            hip_check(hipEventRecord(g.copied[slot], joint), "jobs copied");
+            launch_tree_nn1_jobs(g.d_jobs, (int32_t)J.size(), rs[J[0]]->p.d, K, joint);
+            hip_check(hipEventRecord(g.done, joint), "joint done");
+            for (hipStream_t s : uniq) hip_check(hipStreamWaitEvent(s, g.done, 0), "joint wait");
+            for (int32_t i : J) cs[i].mark(3, stream_of(i));
         }
-        if (want_spread) {
-            hip_check(hipEventRecord(r->ev_spread, stream), "spread event");
-            r->spread_pending = true;
-            r->rounds_since_spread = 0;
-        }
-        mark(2);
-        if (use_tree) {
-            PointTreeDev T = r->ptree->dev();
-            T.stats = r->stats_on ? r->d_cstats + 8 : nullptr;
-            launch_tree_nn1(T, r->d_samples, K, r->d_nn, r->d_nnd2, stream);
-        } else if (use_grid) {
-            GridDev G = r->grid->dev();
-            G.stats = r->stats_on ? r->d_cstats + 8 : nullptr;
-            launch_grid_knn(G, p.d, r->d_samples, K, 1, r->d_nn, r->d_nnd2, stream);
-        } else {
-            NNWork w{};
-            w.pts = r->d_nodes;
-            w.removed = nullptr;
-            w.n = r->n_upper;
-            w.d = p.d;
-            w.q = r->d_samples;
-            w.nq = K;
-            w.n_dev = r->d_n;
-            launch_knn(w, 1, r->d_nn, r->d_nnd2, r->d_scratch, stream);
-        }
-        mark(3);
-        auto steer = p.kind == MPT_AGENT_OMNI ? k_steer<MPT_AGENT_OMNI>
-                     : (p.kind == MPT_AGENT_BLIMP ? k_steer<MPT_AGENT_BLIMP> : k_steer<MPT_AGENT_SNAKE>);
-        LiveOut lv{live_list ? r->d_live : nullptr, r->d_nlive, r->d_links, r->env};
-        hipLaunchKernelGGL(steer, dim3(kb), dim3(256), 0, stream, p, r->ext_base, K, r->d_nodes, r->d_nn, r->d_ends,
-                           r->d_poses, r->d_pcount, r->d_verdict, r->d_counters, lv);
-        hip_check(hipGetLastError(), "k_steer");
-        mark(4);
-        CollideWork cw{};
-        cw.poses = r->d_poses;
-        cw.pose_edge = nullptr;
-        cw.pcount = r->d_pcount;
-        cw.pmax = p.pmax;
-        cw.L = p.L;
-        cw.n_units = (int64_t)K * p.pmax * p.L;
-        cw.verdict = r->d_verdict;
-        cw.stats = r->stats_on ? r->d_cstats : nullptr;
-        cw.live_units = live_list ? r->d_live : nullptr;
-        cw.n_live = live_list ? r->d_nlive : nullptr;
-        if (collide_mode() == MPT_COLLIDE_FUSED) {
-            launch_collide(r->env, r->d_links, cw, stream);
-            mark(5);
-            mark(6);
-            mark(7);
-        } else {
-            launch_collide_split(r->env, r->d_links, r->max_clusters, cw, r->cscratch, stream,
-                                 ev ? ev + 5 : nullptr);
-        }
-        mark(8);
-        hipLaunchKernelGGL(k_append_commit, dim3(kb), dim3(256), 0, stream, r->d_verdict, K, p.d, r->d_ends, r->d_nn,
-                           r->d_n, r->cap, r->d_nodes, r->d_parents, r->d_counters);
-        hip_check(hipGetLastError(), "append");
-        mark(9);
-        r->ext_base += (uint64_t)K;
-        r->n_upper = std::min<int64_t>(r->cap, r->n_upper + K);
-        r->last_K = K;
+        for (int32_t i = 0; i < n; ++i)
+            if (!joined[i]) step_nn(rs[i], K, stream_of(i), cs[i]);
+        for (int32_t i = 0; i < n; ++i) step_tail(rs[i], K, stream_of(i), cs[i]);
     });
 }
 

@@ -114,6 +114,25 @@ def test_engine_rounds(mpt_gpu, oracle, name, nn_mode):
     tree, _ = check_round(mpt_gpu, oracle, sc, eng, tree, seed, K, K // 2 + 3)
 
 
+def test_engine_tree_nn_large_blob(mpt_gpu, oracle):
+    """Morton-tree NN (config 5's structure) over a 40k-node RRT-like blob: more than 4096
+    points, so the box build spans several workgroups and the last one to finish builds
+    levels 5 and 6 (k_pt_boxes' ticket path); two rounds, the second after the ticket reset."""
+    sc = scenes.blimp_scenario("all")
+    rng = np.random.default_rng(77)
+    n0, K = 40_000, 2048
+    tree = rng.uniform(sc.ranges[:, 0], sc.ranges[:, 1], size=(n0, sc.dim))
+    tree[:, :3] = np.array([88.6, 68.9, 57.1]) + rng.normal(0.0, 6.0, size=(n0, 3))
+    env = mpt_gpu.Environment(sc.env_tris, sc.env_tf)
+    ag = mpt_gpu.AgentMesh(sc.agent_tris)
+    eng = mpt_gpu.RRTEngine(env, ag, sc.kind, sc.prm, sc.ranges, sc.steer_dt, sc.cc_dt, capacity=n0 + 4 * K,
+                            seed=4242)
+    eng.add_nodes(tree)
+    eng.set_nn("tree")
+    tree, _ = check_round(mpt_gpu, oracle, sc, eng, tree, 4242, 0, K)
+    tree, _ = check_round(mpt_gpu, oracle, sc, eng, tree, 4242, K, K)
+
+
 def test_engine_round_with_pair_overflow(mpt_gpu, oracle):
     """The blimp against the blimp mesh itself as the environment, every pose within a few
     units of it: clusters overlap far more env triangles than a pair segment holds, so units
@@ -231,6 +250,48 @@ def test_engines_on_streams_match_one_stream(mpt_gpu):
     mixed = grow([torch.cuda.Stream() for _ in range(4)])
     for (sa, pa), (sb, pb) in zip(alone, mixed):
         assert len(sa) > 1
+        assert np.array_equal(bits(sa), bits(sb)) and np.array_equal(pa, pb)
+
+
+def test_step_many_matches_single_steps(mpt_gpu):
+    """mpt_rrt_step_many (config 5's joint NN launch): twelve seeds over four streams, all but
+    one on the Morton tree (one launch of k_tree_nn1_jobs per round) and one on the grid (its
+    own query), must grow exactly the trees each seed grows alone with mpt_rrt_step."""
+    import torch
+
+    sc = scenes.blimp_scenario("all")
+    root = np.array([[88.6, 68.9, 57.1, 0, 0, 0, 0.0]])
+    env = mpt_gpu.Environment(sc.env_tris, sc.env_tf)
+    ag = mpt_gpu.AgentMesh(sc.agent_tris)
+    K, rounds, seeds = 2048, 4, list(range(500, 512))
+    modes = ["tree"] * (len(seeds) - 1) + ["grid"]
+
+    def grow(joint):
+        engs = []
+        for s, m in zip(seeds, modes):
+            e = mpt_gpu.RRTEngine(env, ag, sc.kind, sc.prm, sc.ranges, sc.steer_dt, sc.cc_dt, 1 + rounds * K, s)
+            e.add_nodes(root)
+            e.set_nn(m)
+            engs.append(e)
+        streams = [torch.cuda.Stream() for _ in range(4)]
+        for _ in range(rounds):
+            if joint:
+                mpt_gpu.step_many(engs, K, [streams[j % 4] for j in range(len(engs))], torch.cuda.Stream())
+            else:
+                for e in engs:
+                    e.step(K)
+        torch.cuda.synchronize()
+        out = []
+        for e in engs:
+            assert e.last_nn() == modes[len(out)]
+            out.append(e.read_tree(e.counters()["nodes"]))
+            e.close()
+        return out
+
+    alone = grow(False)
+    joint = grow(True)
+    for (sa, pa), (sb, pb) in zip(alone, joint):
+        assert len(sa) > 2048
         assert np.array_equal(bits(sa), bits(sb)) and np.array_equal(pa, pb)
 
 
