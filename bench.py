@@ -58,6 +58,9 @@ def parse():
     ap.add_argument("--no-joint-nn", action="store_true",
                     help="config 5: each seed queries its own tree (default: one joint NN launch per round, "
                          "mpt_rrt_step_many)")
+    ap.add_argument("--joint-groups", type=int, default=1,
+                    help="config 5: split the seeds into this many step_many groups, each on its own streams "
+                         "and joint stream, so one group's NN launch overlaps another's build / collide")
     ap.add_argument("--launch-threads", type=int, default=1,
                     help="config 5: host threads issuing the seeds' rounds (thread t drives streams t, t+T, ...)")
     return ap.parse_args()
@@ -107,12 +110,14 @@ STAGE_KERNEL = {"nn_query": "k_grid_nn1_runs", "collide_pairs": "k_pairs", "coll
                 "sample": "k_sample", "append": "k_append"}
 
 
-def stage_bytes(stage, c, K, n0, d, pmax):
+def stage_bytes(stage, c, K, n0, d, pmax, nn_mode="grid"):
     """Algorithmic bytes one launch of the stage must touch (DESIGN.md "Measurement"): the
     inputs it reads and outputs it writes, each counted once per use, from the counters
     of the round (c = RRTEngine.collide_stats)."""
     if stage == "nn_query":  # queries + results + examined points (coords, id) + cell ranges
-        return K * (8 * d + 12) + c["nn_points"] * (8 * d + 4) + c["nn_cells"] * 8
+        # grid: a cell's (start, count) pair; tree: a box's float lo / hi over d dims
+        per_cell = 8 * d if nn_mode == "tree" else 8
+        return K * (8 * d + 12) + c["nn_points"] * (8 * d + 4) + c["nn_cells"] * per_cell
     if stage == "collide_pairs":  # poses, cluster records, env tree items tested, pair words
         return c["units"] * 96 + c["cluster_threads"] * 64 + c["node_tests"] * 32 + c["pair_tests"] * 4
     if stage == "collide_cands":  # per header: header, pose, 64 agent triangles; pairs; candidates
@@ -145,7 +150,7 @@ def roofline(per_launch, cst, K, n0, d, pmax, nn_mode, traffic_path):
         kernels["nn_build"] = "k_pt_gather"
     for s in kernels:
         ms = per_launch.get(s, 0.0)
-        b = stage_bytes(s, cst, K, n0, d, pmax)
+        b = stage_bytes(s, cst, K, n0, d, pmax, nn_mode)
         if ms <= 0 or b is None:
             continue
         gbs = b / (ms * 1e-3) / 1e9
@@ -221,7 +226,7 @@ def run_seeds(args, world, rank, dist, torch, mpt, multiseed, scenes):
     start = np.array([[88.6, 68.9, 57.1, 0.0, 0.0, 0.0, 0.0]])
     engines = []
     for i in mine:
-        e = mpt.RRTEngine(env, agent, sc.kind, sc.prm, sc.ranges, sc.steer_dt, sc.cc_dt, 1 + (rounds + 1) * K,
+        e = mpt.RRTEngine(env, agent, sc.kind, sc.prm, sc.ranges, sc.steer_dt, sc.cc_dt, 1 + (rounds + 2) * K,
                           args.seed + i)
         e.add_nodes(start)
         e.set_nn(args.nn, args.ppc)
@@ -249,10 +254,21 @@ def run_seeds(args, world, rank, dist, torch, mpt, multiseed, scenes):
 
     joint = torch.cuda.Stream()
     eng_streams = [streams[j % len(streams)] for j in range(len(engines))]
+    # groups: contiguous slices of engines, group g on streams [g*S/G, (g+1)*S/G) + its own joint stream
+    G = max(1, min(args.joint_groups, len(streams), len(engines)))
+    gsz = -(-len(engines) // G)
+    spg = max(1, len(streams) // G)
+    jgroups = []
+    for g in range(G):
+        eg = engines[g * gsz:(g + 1) * gsz]
+        sg = streams[g * spg:(g + 1) * spg]
+        if eg:
+            jgroups.append((eg, [sg[j % len(sg)] for j in range(len(eg))], joint if g == 0 else torch.cuda.Stream()))
 
     def round_():
         if not args.no_joint_nn:
-            mpt.step_many(engines, K, eng_streams, joint)
+            for eg, ss, js in jgroups:
+                mpt.step_many(eg, K, ss, js)
         elif pool is None:
             drive(groups[0])
         else:
@@ -288,12 +304,42 @@ def run_seeds(args, world, rank, dist, torch, mpt, multiseed, scenes):
     # seed 0's engine: one more round with stage timing and work counters, outside the timed region
     e0 = engines[0]
     n_before = e0.counters()["nodes"]
-    e0.collide_stats(True)
-    e0.step(K, streams[0])
-    torch.cuda.synchronize()
-    cst = e0.collide_stats(False)
-    per_launch = e0.kernel_times()
-    roof = roofline(per_launch, cst, K, n_before, sc.dim, e0.info()["pmax"], e0.last_nn(), args.traffic)
+    if args.no_joint_nn:
+        e0.collide_stats(True)
+        e0.step(K, streams[0])
+        torch.cuda.synchronize()
+        cst = e0.collide_stats(False)
+        per_launch = e0.kernel_times()
+        roof = roofline(per_launch, cst, K, n_before, sc.dim, e0.info()["pmax"], e0.last_nn(), args.traffic)
+    else:
+        # all seeds: one round with work counters on (summed for the joint launch's bytes), then
+        # one with them off and the joint NN launch timed by hipEvents on its stream
+        for e in engines:
+            e.collide_stats(True)
+        mpt.step_many(engines, K, eng_streams, joint)
+        torch.cuda.synchronize()
+        csts = [e.collide_stats(False) for e in engines]
+        mpt.step_many(engines, K, eng_streams, joint)
+        torch.cuda.synchronize()
+        jms = mpt.joint_nn_ms()
+        cst = csts[0]
+        per_launch = dict(e0.kernel_times())
+        nn_bytes = sum(stage_bytes("nn_query", c, K, n_before, sc.dim, e0.info()["pmax"], "tree") for c in csts)
+        per_launch.pop("nn_query", None)
+        roof = roofline(per_launch, cst, K, n_before, sc.dim, e0.info()["pmax"], e0.last_nn(), args.traffic)
+        gbs = nn_bytes / (jms * 1e-3) / 1e9
+        nn = {"kernel": "k_tree_nn1_jobs<7,", "ms": round(jms, 4), "bytes": int(nn_bytes),
+              "achieved_gbs": round(gbs, 1), "frac": round(gbs / HBM_PEAK_GBS, 4),
+              "launch": f"one launch for all {len(engines)} seeds' {K} queries"}
+        t = pmc_traffic(args.traffic, nn["kernel"])
+        if t is not None:
+            nn["traffic"], nn["traffic_gbs"] = t, round(t / (jms * 1e-3) / 1e9, 1)
+        roof["stages"]["nn_query"] = nn
+        roof.update({"achieved": nn["achieved_gbs"], "frac": nn["frac"], "traffic": nn.get("traffic"),
+                     "traffic_gbs": nn.get("traffic_gbs"), "kernel": nn["kernel"], "stage": "nn_query",
+                     "ms_per_launch": nn["ms"], "algorithmic_bytes": nn["bytes"],
+                     "work_nn_all_seeds": {"nn_points": sum(c["nn_points"] for c in csts),
+                                           "nn_boxes": sum(c["nn_cells"] for c in csts)}})
     import hashlib
 
     all_digest = hashlib.sha256("".join(digests[i] for i in sorted(digests)).encode()).hexdigest()
@@ -314,7 +360,7 @@ def run_seeds(args, world, rank, dist, torch, mpt, multiseed, scenes):
                                f"grown from the start state, {K} extensions per seed per round",
                    "seeds": args.seeds, "seed_base": args.seed, "extensions_per_seed_round": K,
                    "rounds_before_timing": args.warmup, "streams_per_gpu": len(streams), "launch_threads": T,
-                   "joint_nn": not args.no_joint_nn,
+                   "joint_nn": not args.no_joint_nn, "joint_groups": G,
                    "parallelism": f"seeds sharded over {world} GPU(s)"},
         "checked_per_s": checked / elapsed,
         "valid_fraction": valid / max(checked, 1),

@@ -196,6 +196,9 @@ mpt_status mpt_rrt_step(mpt_rrt *rrt, int32_t K, void *stream);
  * Morton-tree NN share one query launch on joint_stream (which waits for their sample + index
  * build and is waited on by their steer + collide + append).  Asynchronous. */
 mpt_status mpt_rrt_step_many(mpt_rrt *const *rrts, int32_t n, int32_t K, void *const *streams, void *joint_stream);
+/* Duration (ms, hipEvents on joint_stream) of the calling thread's last joint NN launch of
+ * mpt_rrt_step_many that had an engine with timing enabled.  Synchronises on it. */
+mpt_status mpt_rrt_joint_nn_ms(float *ms);
 /* counters [8]: rounds, extensions checked, extensions valid, nodes, capacity drops,
  * pose overflow, reserved, reserved.  Synchronises. */
 mpt_status mpt_rrt_counters(mpt_rrt *rrt, uint64_t counters[8]);

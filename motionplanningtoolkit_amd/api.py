@@ -379,6 +379,13 @@ def step_many(engines, K: int, streams, joint_stream=None) -> None:
     ss = (C.c_void_p * n)(*[(_stream(s).value if s is not None else None) for s in streams])
     check(lib().mpt_rrt_step_many(hs, n, K, ss, _stream(joint_stream)), "mpt_rrt_step_many")
 
+
+def joint_nn_ms() -> float:
+    """hipEvent duration of this thread's last timed joint NN launch (step_many)."""
+    ms = C.c_float()
+    check(lib().mpt_rrt_joint_nn_ms(C.byref(ms)), "mpt_rrt_joint_nn_ms")
+    return ms.value
+
 def load_mesh(path: str, which: str = "all") -> np.ndarray:
     """AssimpMeshLoader replacement: 'all' submeshes (environment) or 'last' (agent)."""
     w = 1 if which == "last" else 0

@@ -66,46 +66,12 @@ __device__ __forceinline__ double key_value_pt(unsigned long long k) {
     return __longlong_as_double((long long)b);
 }
 
-// per-dim min / max of the live points as order keys: box[0..d) min, box[kPtMaxDim..) max
-__global__ __launch_bounds__(256) void k_pt_bbox(const double *__restrict__ pts, int32_t d, int64_t n_upper,
-                                                 const int64_t *__restrict__ n_dev, unsigned long long *__restrict__ box) {
-    __shared__ unsigned long long s_min[kPtMaxDim], s_max[kPtMaxDim];
-    if (threadIdx.x < kPtMaxDim) {
-        s_min[threadIdx.x] = ~0ull;
-        s_max[threadIdx.x] = 0ull;
-    }
-    __syncthreads();
-    const int64_t n = *n_dev < n_upper ? *n_dev : n_upper;
-    for (int j = 0; j < d; ++j) {
-        unsigned long long mn = ~0ull, mx = 0ull;
-        for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-            const unsigned long long k = order_key_pt(pts[i * d + j]);
-            mn = k < mn ? k : mn;
-            mx = k > mx ? k : mx;
-        }
-        // one LDS atomic per wave, not per lane (256 same-address 64-bit atomics serialise)
-#pragma unroll
-        for (int off = 32; off > 0; off >>= 1) {
-            const unsigned long long omn = __shfl_xor(mn, off), omx = __shfl_xor(mx, off);
-            mn = omn < mn ? omn : mn;
-            mx = omx > mx ? omx : mx;
-        }
-        if ((threadIdx.x & 63) == 0) {
-            atomicMin(&s_min[j], mn);
-            atomicMax(&s_max[j], mx);
-        }
-    }
-    __syncthreads();
-    if (threadIdx.x < (unsigned)d) {
-        atomicMin(box + threadIdx.x, s_min[threadIdx.x]);
-        atomicMax(box + kPtMaxDim + threadIdx.x, s_max[threadIdx.x]);
-    }
-}
-
-// One wave: lane k-1 sizes level k (h = emax / 2^k); the plan takes the finest level before
-// the first whose bit total exceeds the code.  The box is reset to empty for the next build.
-__global__ __launch_bounds__(64) void k_pt_plan(int32_t d, unsigned long long *__restrict__ box,
-                                                CodePlan *__restrict__ plan, SpreadOut sp) {
+// Code plan from the box (the first wave of the last k_pt_bbox workgroup): lane k-1 sizes
+// level k (h = emax / 2^k); the plan takes the finest level before the first whose bit total
+// exceeds the code.  The box is reset to empty for the next build.  All threads of the
+// workgroup must call it (barriers).
+__device__ void pt_plan(int32_t d, unsigned long long *__restrict__ box, CodePlan *__restrict__ plan,
+                        const SpreadOut &sp) {
     __shared__ double s_lo[kPtMaxDim], s_ext[kPtMaxDim];
     __shared__ int32_t s_b[kPtMaxDim];
     const int t = threadIdx.x;
@@ -166,6 +132,60 @@ __global__ __launch_bounds__(64) void k_pt_plan(int32_t d, unsigned long long *_
                 ++n;
             }
     plan->n = n;
+}
+
+// per-dim min / max of the live points as order keys: box[0..d) min, box[kPtMaxDim..) max
+__global__ __launch_bounds__(256) void k_pt_bbox(const double *__restrict__ pts, int32_t d, int64_t n_upper,
+                                                 const int64_t *__restrict__ n_dev, unsigned long long *__restrict__ box,
+                                                 unsigned int *__restrict__ ticket, CodePlan *__restrict__ plan,
+                                                 SpreadOut sp) {
+    __shared__ unsigned long long s_min[kPtMaxDim], s_max[kPtMaxDim];
+    if (threadIdx.x < kPtMaxDim) {
+        s_min[threadIdx.x] = ~0ull;
+        s_max[threadIdx.x] = 0ull;
+    }
+    __syncthreads();
+    const int64_t n = *n_dev < n_upper ? *n_dev : n_upper;
+    for (int j = 0; j < d; ++j) {
+        unsigned long long mn = ~0ull, mx = 0ull;
+        for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+            const unsigned long long k = order_key_pt(pts[i * d + j]);
+            mn = k < mn ? k : mn;
+            mx = k > mx ? k : mx;
+        }
+        // one LDS atomic per wave, not per lane (256 same-address 64-bit atomics serialise)
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) {
+            const unsigned long long omn = __shfl_xor(mn, off), omx = __shfl_xor(mx, off);
+            mn = omn < mn ? omn : mn;
+            mx = omx > mx ? omx : mx;
+        }
+        if ((threadIdx.x & 63) == 0) {
+            atomicMin(&s_min[j], mn);
+            atomicMax(&s_max[j], mx);
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x < (unsigned)d) {
+        atomicMin(box + threadIdx.x, s_min[threadIdx.x]);
+        atomicMax(box + kPtMaxDim + threadIdx.x, s_max[threadIdx.x]);
+    }
+    if (!plan) return;  // the plan runs as its own launch (k_pt_plan)
+    // the last workgroup to finish turns the box into the code plan (no separate launch)
+    __shared__ bool last;
+    __threadfence();
+    __syncthreads();
+    if (threadIdx.x == 0) last = atomicAdd(ticket, 1u) == gridDim.x - 1;
+    __syncthreads();
+    if (!last) return;
+    __threadfence();
+    if (threadIdx.x == 0) *ticket = 0u;
+    pt_plan(d, box, plan, sp);
+}
+
+__global__ __launch_bounds__(64) void k_pt_plan(int32_t d, unsigned long long *__restrict__ box,
+                                                CodePlan *__restrict__ plan, SpreadOut sp) {
+    pt_plan(d, box, plan, sp);
 }
 
 __global__ void k_pt_morton(const double *__restrict__ pts, int32_t d, int64_t n_upper, const int64_t *__restrict__ n_dev,
@@ -512,7 +532,8 @@ void PointTree::reserve(int64_t n_upper, int32_t d) {
         box_cap = 0;
     }
     if (!bbox) {
-        // [min keys][max keys] + the box ticket; set once here, reset by the build's own kernels
+        // [min keys][max keys] + the box-level and bbox tickets (two u32); set once here, reset
+        // by the build's own kernels
         hip_check(hipMalloc(&bbox, sizeof(unsigned long long) * (2 * kPtMaxDim + 1)), "pt bbox");
         hip_check(hipMemset(bbox, 0xff, sizeof(unsigned long long) * kPtMaxDim), "bbox init");
         hip_check(hipMemset(bbox + kPtMaxDim, 0, sizeof(unsigned long long) * (kPtMaxDim + 1)), "bbox init");
@@ -541,9 +562,13 @@ void PointTree::build(const double *pts, int64_t n_upper, const int64_t *n_dev, 
     t.ids = sids;
     if (n_upper <= 0) return;
     const unsigned blocks = (unsigned)((n_upper + 255) / 256);
-    // bbox starts empty (reserve) and k_pt_plan resets it after reading it
-    hipLaunchKernelGGL(k_pt_bbox, dim3(64), dim3(256), 0, stream, pts, d, n_upper, n_dev, bbox);
-    hipLaunchKernelGGL(k_pt_plan, dim3(1), dim3(64), 0, stream, d, bbox, plan, spread ? *spread : SpreadOut{});
+    // bbox starts empty (reserve) and the plan (in k_pt_bbox) resets it after reading it
+    // MPT_PT_PLAN_LAUNCH=1: the plan as a separate one-wave launch (A/B knob)
+    static const bool plan_launch = getenv("MPT_PT_PLAN_LAUNCH") && atoi(getenv("MPT_PT_PLAN_LAUNCH")) == 1;
+    const SpreadOut sp = spread ? *spread : SpreadOut{};
+    hipLaunchKernelGGL(k_pt_bbox, dim3(64), dim3(256), 0, stream, pts, d, n_upper, n_dev, bbox, ticket + 1,
+                       plan_launch ? nullptr : plan, sp);
+    if (plan_launch) hipLaunchKernelGGL(k_pt_plan, dim3(1), dim3(64), 0, stream, d, bbox, plan, sp);
     hipLaunchKernelGGL(k_pt_morton, dim3(blocks), dim3(256), 0, stream, pts, d, n_upper, n_dev, plan, keys, vals);
     hip_check(hipGetLastError(), "k_pt_morton");
     size_t tb = temp_bytes;

@@ -769,6 +769,8 @@ struct JointNN {
     int32_t cap = 0, next = 0;
     std::vector<hipEvent_t> joins;
     hipEvent_t done = nullptr;
+    hipEvent_t t0 = nullptr, t1 = nullptr;  // around the last joint launch (engine timing on)
+    bool timed = false;
 };
 thread_local JointNN g_joint;
 
@@ -839,7 +841,18 @@ extern "C" mpt_status mpt_rrt_step_many(mpt_rrt *const *rs, int32_t n, int32_t K
             }
             hip_check(hipMemcpyAsync(g.d_jobs, h, sizeof(PtJob) * J.size(), hipMemcpyHostToDevice, joint), "jobs H2D");
             hip_check(hipEventRecord(g.copied[slot], joint), "jobs copied");
+            bool timed = false;
+            for (int32_t i : J) timed = timed || rs[i]->timing;
+            if (timed) {
+                if (!g.t0) {
+                    hip_check(hipEventCreate(&g.t0), "event");
+                    hip_check(hipEventCreate(&g.t1), "event");
+                }
+                hip_check(hipEventRecord(g.t0, joint), "joint t0");
+            }
             launch_tree_nn1_jobs(g.d_jobs, (int32_t)J.size(), rs[J[0]]->p.d, K, joint);
+            if (timed) hip_check(hipEventRecord(g.t1, joint), "joint t1");
+            g.timed = timed;
             hip_check(hipEventRecord(g.done, joint), "joint done");
             for (hipStream_t s : uniq) hip_check(hipStreamWaitEvent(s, g.done, 0), "joint wait");
             for (int32_t i : J) cs[i].mark(3, stream_of(i));
@@ -847,6 +860,15 @@ extern "C" mpt_status mpt_rrt_step_many(mpt_rrt *const *rs, int32_t n, int32_t K
         for (int32_t i = 0; i < n; ++i)
             if (!joined[i]) step_nn(rs[i], K, stream_of(i), cs[i]);
         for (int32_t i = 0; i < n; ++i) step_tail(rs[i], K, stream_of(i), cs[i]);
+    });
+}
+
+extern "C" mpt_status mpt_rrt_joint_nn_ms(float *ms) {
+    return guarded([&] {
+        if (!ms) throw Error{MPT_ERR_INVALID, "null pointer"};
+        if (!g_joint.timed) throw Error{MPT_ERR_INVALID, "no timed joint NN launch on this thread"};
+        hip_check(hipEventSynchronize(g_joint.t1), "event sync");
+        hip_check(hipEventElapsedTime(ms, g_joint.t0, g_joint.t1), "elapsed");
     });
 }
 
