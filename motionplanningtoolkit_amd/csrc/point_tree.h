@@ -1,6 +1,7 @@
 // point_tree.h -- packed Morton tree for exact NN over a tree snapshot (see point_tree.hip).
 #pragma once
 #include "mpt_internal.h"
+#include "grid_nn.h"  // SpreadOut
 
 namespace mpt {
 
@@ -19,8 +20,42 @@ struct PointTreeDev {
     unsigned long long *stats; // optional [2]: points examined, boxes tested
 };
 
+// One tree of a joint build (mpt_rrt_step_many): the tree's own buffers, its points, and the
+// offset of its keys / values in the shared sort buffers.
+struct PtBuildJob {
+    PointTreeDev T;            // as PointTree::dev() after the build
+    const double *pts;         // [n_upper][d] input rows
+    int64_t off;               // into the shared key / value buffers
+    unsigned long long *bbox;  // the tree's box keys
+    unsigned int *ticket;      // [2]: box-level ticket, bbox ticket
+    struct CodePlan *plan;
+    double *spts;
+    int32_t *sids;
+    float *boxes;
+    SpreadOut sp;
+};
+
+// shared sort buffers of a joint build (grown on demand, owned by the caller)
+struct JointTreeScratch {
+    uint32_t *keys = nullptr, *keys_sorted = nullptr;
+    int32_t *vals = nullptr, *vals_sorted = nullptr;
+    int64_t cap = 0;
+    void *temp = nullptr;
+    size_t temp_bytes = 0;
+};
+
+// Build n trees of dim d in one launch per stage + one segmented sort.  d_jobs / h_jobs: the
+// same table on the device and the host; d_offsets: [n + 1] segment starts (int32) on the
+// device, total = its last entry.  Stream-ordered.
+void launch_tree_build_jobs(const PtBuildJob *d_jobs, const PtBuildJob *h_jobs, int32_t n, int32_t d,
+                            const int32_t *d_offsets, int64_t total, JointTreeScratch &S, hipStream_t stream);
+
 class PointTree {
 public:
+    // the host part of build(): reserve, lay out the levels, and describe the device work as
+    // a job of a joint build (launch_tree_build_jobs); dev() is valid once that has run
+    PtBuildJob prepare(const double *pts, int64_t n_upper, const int64_t *n_dev, int32_t d, int64_t off,
+                       const struct SpreadOut *spread);
     ~PointTree();
     // Index rows [0, min(n_upper, *n_dev)) of pts [.][d]: bounding box and code plan on the
     // device, 30-bit codes over all dims, radix sort, boxes bottom-up.  Stream-ordered.

@@ -135,10 +135,10 @@ __device__ void pt_plan(int32_t d, unsigned long long *__restrict__ box, CodePla
 }
 
 // per-dim min / max of the live points as order keys: box[0..d) min, box[kPtMaxDim..) max
-__global__ __launch_bounds__(256) void k_pt_bbox(const double *__restrict__ pts, int32_t d, int64_t n_upper,
-                                                 const int64_t *__restrict__ n_dev, unsigned long long *__restrict__ box,
-                                                 unsigned int *__restrict__ ticket, CodePlan *__restrict__ plan,
-                                                 SpreadOut sp) {
+__device__ __forceinline__ void pt_bbox(const double *__restrict__ pts, int32_t d, int64_t n_upper,
+                                        const int64_t *__restrict__ n_dev, unsigned long long *__restrict__ box,
+                                        unsigned int *__restrict__ ticket, CodePlan *__restrict__ plan,
+                                        const SpreadOut &sp, int64_t blk, int64_t nblk) {
     __shared__ unsigned long long s_min[kPtMaxDim], s_max[kPtMaxDim];
     if (threadIdx.x < kPtMaxDim) {
         s_min[threadIdx.x] = ~0ull;
@@ -148,7 +148,7 @@ __global__ __launch_bounds__(256) void k_pt_bbox(const double *__restrict__ pts,
     const int64_t n = *n_dev < n_upper ? *n_dev : n_upper;
     for (int j = 0; j < d; ++j) {
         unsigned long long mn = ~0ull, mx = 0ull;
-        for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        for (int64_t i = blk * blockDim.x + threadIdx.x; i < n; i += nblk * blockDim.x) {
             const unsigned long long k = order_key_pt(pts[i * d + j]);
             mn = k < mn ? k : mn;
             mx = k > mx ? k : mx;
@@ -175,7 +175,7 @@ __global__ __launch_bounds__(256) void k_pt_bbox(const double *__restrict__ pts,
     __shared__ bool last;
     __threadfence();
     __syncthreads();
-    if (threadIdx.x == 0) last = atomicAdd(ticket, 1u) == gridDim.x - 1;
+    if (threadIdx.x == 0) last = atomicAdd(ticket, 1u) == nblk - 1;
     __syncthreads();
     if (!last) return;
     __threadfence();
@@ -183,14 +183,22 @@ __global__ __launch_bounds__(256) void k_pt_bbox(const double *__restrict__ pts,
     pt_plan(d, box, plan, sp);
 }
 
+__global__ __launch_bounds__(256) void k_pt_bbox(const double *__restrict__ pts, int32_t d, int64_t n_upper,
+                                                 const int64_t *__restrict__ n_dev, unsigned long long *__restrict__ box,
+                                                 unsigned int *__restrict__ ticket, CodePlan *__restrict__ plan,
+                                                 SpreadOut sp) {
+    pt_bbox(pts, d, n_upper, n_dev, box, ticket, plan, sp, blockIdx.x, gridDim.x);
+}
+
 __global__ __launch_bounds__(64) void k_pt_plan(int32_t d, unsigned long long *__restrict__ box,
                                                 CodePlan *__restrict__ plan, SpreadOut sp) {
     pt_plan(d, box, plan, sp);
 }
 
-__global__ void k_pt_morton(const double *__restrict__ pts, int32_t d, int64_t n_upper, const int64_t *__restrict__ n_dev,
-                            const CodePlan *__restrict__ plan, uint32_t *__restrict__ keys, int32_t *__restrict__ vals) {
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+__device__ __forceinline__ void pt_morton(const double *__restrict__ pts, int32_t d, int64_t n_upper,
+                                          const int64_t *__restrict__ n_dev, const CodePlan *__restrict__ plan,
+                                          uint32_t *__restrict__ keys, int32_t *__restrict__ vals, int64_t blk) {
+    const int64_t i = blk * blockDim.x + threadIdx.x;
     if (i >= n_upper) return;
     const int64_t n = *n_dev < n_upper ? *n_dev : n_upper;
     vals[i] = (int32_t)i;
@@ -210,13 +218,18 @@ __global__ void k_pt_morton(const double *__restrict__ pts, int32_t d, int64_t n
     keys[i] = code;
 }
 
+__global__ void k_pt_morton(const double *__restrict__ pts, int32_t d, int64_t n_upper, const int64_t *__restrict__ n_dev,
+                            const CodePlan *__restrict__ plan, uint32_t *__restrict__ keys, int32_t *__restrict__ vals) {
+    pt_morton(pts, d, n_upper, n_dev, plan, keys, vals, blockIdx.x);
+}
+
 // Coordinates and ids into code order, and the level-1 boxes with them: a leaf is 8
 // consecutive sorted points, i.e. 8 consecutive lanes, so its bounds are an 8-lane reduction.
-__global__ __launch_bounds__(256) void k_pt_gather(const double *__restrict__ pts, int32_t d, int64_t n_upper,
-                                                   const int64_t *__restrict__ n_dev, const int32_t *__restrict__ order,
-                                                   double *__restrict__ spts, int32_t *__restrict__ sids,
-                                                   float *__restrict__ leaf_boxes) {
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+__device__ __forceinline__ void pt_gather(const double *__restrict__ pts, int32_t d, int64_t n_upper,
+                                          const int64_t *__restrict__ n_dev, const int32_t *__restrict__ order,
+                                          double *__restrict__ spts, int32_t *__restrict__ sids,
+                                          float *__restrict__ leaf_boxes, int64_t blk) {
+    const int64_t i = blk * blockDim.x + threadIdx.x;
     const int64_t n = *n_dev < n_upper ? *n_dev : n_upper;
     const bool live = i < n;  // no early exit: the leaf reduction needs all 8 lanes
     const int32_t src = live ? order[i] : 0;
@@ -237,6 +250,13 @@ __global__ __launch_bounds__(256) void k_pt_gather(const double *__restrict__ pt
             b[d + j] = widen_hi(hi);
         }
     }
+}
+
+__global__ __launch_bounds__(256) void k_pt_gather(const double *__restrict__ pts, int32_t d, int64_t n_upper,
+                                                   const int64_t *__restrict__ n_dev, const int32_t *__restrict__ order,
+                                                   double *__restrict__ spts, int32_t *__restrict__ sids,
+                                                   float *__restrict__ leaf_boxes) {
+    pt_gather(pts, d, n_upper, n_dev, order, spts, sids, leaf_boxes, blockIdx.x);
 }
 
 // (box j, dim k) of level l >= 2: the bounds of its (up to) 8 children at level l - 1
@@ -264,10 +284,9 @@ __device__ __forceinline__ void pt_up_box(const PointTreeDev &T, int64_t n, int 
 constexpr int kPtChunkLeaves = 512;  // 8^3: levels 1..4 inside a workgroup
 constexpr int kPtInBlockLevels = 4;
 
-__global__ __launch_bounds__(256) void k_pt_boxes(PointTreeDev T, float *__restrict__ boxes,
-                                                  unsigned int *__restrict__ ticket) {
+__device__ __forceinline__ void pt_boxes(const PointTreeDev &T, float *__restrict__ boxes,
+                                         unsigned int *__restrict__ ticket, int64_t g, int64_t ngroups) {
     const int64_t n = live_n(T);
-    const int64_t g = blockIdx.x;
     const int top_in = T.n_levels < kPtInBlockLevels ? T.n_levels : kPtInBlockLevels;
     for (int l = 2; l <= top_in; ++l) {
         const int64_t per = (int64_t)kPtChunkLeaves >> (3 * (l - 1));
@@ -285,7 +304,7 @@ __global__ __launch_bounds__(256) void k_pt_boxes(PointTreeDev T, float *__restr
     __shared__ bool last;
     __threadfence();
     __syncthreads();
-    if (threadIdx.x == 0) last = atomicAdd(ticket, 1u) == gridDim.x - 1;
+    if (threadIdx.x == 0) last = atomicAdd(ticket, 1u) == ngroups - 1;
     __syncthreads();
     if (!last) return;
     __threadfence();  // agent-scope acquire: this CU's L1 holds no stale copy of the others' boxes
@@ -297,6 +316,37 @@ __global__ __launch_bounds__(256) void k_pt_boxes(PointTreeDev T, float *__restr
         __syncthreads();
     }
     if (threadIdx.x == 0) *ticket = 0u;
+}
+
+__global__ __launch_bounds__(256) void k_pt_boxes(PointTreeDev T, float *__restrict__ boxes,
+                                                  unsigned int *__restrict__ ticket) {
+    pt_boxes(T, boxes, ticket, blockIdx.x, gridDim.x);
+}
+
+// ---- the same build for many trees at once (mpt_rrt_step_many): blockIdx.y = the tree; a
+// tree's keys / values live in shared buffers at its offset, sorted by one segmented sort
+__global__ __launch_bounds__(256) void k_pt_bbox_jobs(const PtBuildJob *__restrict__ jobs, int32_t d) {
+    const PtBuildJob &J = jobs[blockIdx.y];
+    pt_bbox(J.pts, d, J.T.n_upper, J.T.n_dev, J.bbox, J.ticket + 1, J.plan, J.sp, blockIdx.x, gridDim.x);
+}
+__global__ __launch_bounds__(256) void k_pt_morton_jobs(const PtBuildJob *__restrict__ jobs, int32_t d,
+                                                        uint32_t *__restrict__ keys, int32_t *__restrict__ vals) {
+    const PtBuildJob &J = jobs[blockIdx.y];
+    if ((int64_t)blockIdx.x * blockDim.x >= J.T.n_upper) return;
+    pt_morton(J.pts, d, J.T.n_upper, J.T.n_dev, J.plan, keys + J.off, vals + J.off, blockIdx.x);
+}
+__global__ __launch_bounds__(256) void k_pt_gather_jobs(const PtBuildJob *__restrict__ jobs, int32_t d,
+                                                        const int32_t *__restrict__ vals_sorted) {
+    const PtBuildJob &J = jobs[blockIdx.y];
+    if ((int64_t)blockIdx.x * blockDim.x >= J.T.n_upper) return;
+    pt_gather(J.pts, d, J.T.n_upper, J.T.n_dev, vals_sorted + J.off, J.spts, J.sids, J.boxes, blockIdx.x);
+}
+__global__ __launch_bounds__(256) void k_pt_boxes_jobs(const PtBuildJob *__restrict__ jobs) {
+    const PtBuildJob &J = jobs[blockIdx.y];
+    if (J.T.n_levels < 2) return;
+    const int64_t groups = (J.T.n_upper + kPtChunkLeaves * kPtFan - 1) / (kPtChunkLeaves * kPtFan);
+    if (blockIdx.x >= groups) return;  // before the ticket: only the tree's own groups count
+    pt_boxes(J.T, J.boxes, J.ticket, blockIdx.x, groups);
 }
 
 constexpr int kPtGroupsPerBlock = 256 / kPtFan;
@@ -583,6 +633,63 @@ void PointTree::build(const double *pts, int64_t n_upper, const int64_t *n_dev, 
     const unsigned box_groups = (unsigned)((n_upper + kPtChunkLeaves * kPtFan - 1) / (kPtChunkLeaves * kPtFan));
     hipLaunchKernelGGL(k_pt_boxes, dim3(box_groups), dim3(256), 0, stream, t, boxes, ticket);
     hip_check(hipGetLastError(), "k_pt_boxes");
+}
+
+PtBuildJob PointTree::prepare(const double *pts, int64_t n_upper, const int64_t *n_dev, int32_t d, int64_t off,
+                              const SpreadOut *spread) {
+    if (d != 3 && d != 7 && d != 15) throw Error{1, "point tree: state dim must be 3, 7 or 15"};
+    if (n_upper < 1 || n_upper >= (int64_t(1) << 27)) throw Error{1, "point tree: bad point count"};
+    reserve(n_upper, d);
+    t.d = d;
+    t.n_upper = n_upper;
+    t.n_levels = pt_levels(n_upper);
+    t.n_dev = n_dev;
+    t.boxes = boxes;
+    t.pts = spts;
+    t.ids = sids;
+    return PtBuildJob{t, pts, off, bbox, ticket, plan, spts, sids, boxes, spread ? *spread : SpreadOut{}};
+}
+
+void launch_tree_build_jobs(const PtBuildJob *d_jobs, const PtBuildJob *h_jobs, int32_t n, int32_t d,
+                            const int32_t *d_offsets, int64_t total, JointTreeScratch &S, hipStream_t stream) {
+    if (n <= 0) return;
+    int64_t max_n = 0, max_groups = 1;
+    for (int32_t j = 0; j < n; ++j) {
+        max_n = std::max(max_n, h_jobs[j].T.n_upper);
+        max_groups = std::max(max_groups, (h_jobs[j].T.n_upper + kPtChunkLeaves * kPtFan - 1) / (kPtChunkLeaves * kPtFan));
+    }
+    if (total > S.cap) {
+        hip_check(hipDeviceSynchronize(), "sync");  // the old buffers may still be in use
+        for (void *p : {(void *)S.keys, (void *)S.keys_sorted, (void *)S.vals, (void *)S.vals_sorted})
+            if (p) hip_check(hipFree(p), "free");
+        const int64_t c = std::max<int64_t>(total, 2 * S.cap);
+        hip_check(hipMalloc(&S.keys, sizeof(uint32_t) * c), "joint keys");
+        hip_check(hipMalloc(&S.keys_sorted, sizeof(uint32_t) * c), "joint keys");
+        hip_check(hipMalloc(&S.vals, sizeof(int32_t) * c), "joint vals");
+        hip_check(hipMalloc(&S.vals_sorted, sizeof(int32_t) * c), "joint vals");
+        S.cap = c;
+    }
+    size_t tb = 0;
+    hip_check(hipcub::DeviceSegmentedRadixSort::SortPairs(nullptr, tb, S.keys, S.keys_sorted, S.vals, S.vals_sorted,
+                                                          (int)total, n, d_offsets, d_offsets + 1, 0, 32, stream),
+              "segmented sort size");
+    if (tb > S.temp_bytes) {
+        hip_check(hipDeviceSynchronize(), "sync");
+        if (S.temp) hip_check(hipFree(S.temp), "free");
+        hip_check(hipMalloc(&S.temp, tb), "segmented sort temp");
+        S.temp_bytes = tb;
+    }
+    const unsigned bx = (unsigned)((max_n + 255) / 256);
+    hipLaunchKernelGGL(k_pt_bbox_jobs, dim3(64, n), dim3(256), 0, stream, d_jobs, d);
+    hipLaunchKernelGGL(k_pt_morton_jobs, dim3(bx, n), dim3(256), 0, stream, d_jobs, d, S.keys, S.vals);
+    hip_check(hipGetLastError(), "k_pt_morton_jobs");
+    tb = S.temp_bytes;
+    hip_check(hipcub::DeviceSegmentedRadixSort::SortPairs(S.temp, tb, S.keys, S.keys_sorted, S.vals, S.vals_sorted,
+                                                          (int)total, n, d_offsets, d_offsets + 1, 0, 32, stream),
+              "segmented sort");
+    hipLaunchKernelGGL(k_pt_gather_jobs, dim3(bx, n), dim3(256), 0, stream, d_jobs, d, S.vals_sorted);
+    hipLaunchKernelGGL(k_pt_boxes_jobs, dim3((unsigned)max_groups, n), dim3(256), 0, stream, d_jobs);
+    hip_check(hipGetLastError(), "k_pt_boxes_jobs");
 }
 
 void launch_tree_radius(const PointTreeDev &T, const double *q, int64_t nq, double r2, bool below_only,

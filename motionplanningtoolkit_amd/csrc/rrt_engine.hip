@@ -579,12 +579,14 @@ struct StepCtx {
     hipEvent_t *ev = nullptr;  // this round's timing events (engine timing on) or null
     unsigned kb = 0;
     bool use_tree = false, use_grid = false, live_list = false;
+    bool defer_tree = false, want_spread = false;  // tree build left to the caller (step_many)
+    SpreadOut spread{};
     void mark(int i, hipStream_t stream) const {
         if (ev) hip_check(hipEventRecord(ev[i], stream), "event record");
     }
 };
 
-StepCtx step_head(mpt_rrt *r, int32_t K, hipStream_t stream) {
+StepCtx step_head(mpt_rrt *r, int32_t K, hipStream_t stream, bool defer_tree = false) {
     StepCtx c;
     if (r->n_upper < 1) throw Error{MPT_ERR_INVALID, "tree is empty: add a root first"};
     ensure_round_buffers(r, K);
@@ -646,7 +648,13 @@ StepCtx step_head(mpt_rrt *r, int32_t K, hipStream_t stream) {
     }
     if (use_tree) {
         r->ptree->reserve(r->cap, p.d);  // once: no allocation (device sync) in later rounds
-        r->ptree->build(r->d_nodes, r->n_upper, r->d_n, p.d, stream, want_spread ? &spread : nullptr);
+        if (defer_tree) {
+            c.defer_tree = true;
+            c.want_spread = want_spread;
+            c.spread = spread;
+        } else {
+            r->ptree->build(r->d_nodes, r->n_upper, r->d_n, p.d, stream, want_spread ? &spread : nullptr);
+        }
     } else if (use_grid) {
         // spatial dims of the agent's tree state: x, y, z (omni, blimp) or x, y (snake);
         // the grid spans the sampling ranges, nodes outside fall into the border cells
@@ -667,7 +675,7 @@ StepCtx step_head(mpt_rrt *r, int32_t K, hipStream_t stream) {
         r->grid->build(r->d_nodes, r->n_upper, r->d_n, p.d, g, stream, want_spread ? &spread : nullptr);
     }
     if (want_spread) {
-        hip_check(hipEventRecord(r->ev_spread, stream), "spread event");
+        if (!c.defer_tree) hip_check(hipEventRecord(r->ev_spread, stream), "spread event");
         r->spread_pending = true;
         r->rounds_since_spread = 0;
     }
@@ -676,6 +684,12 @@ StepCtx step_head(mpt_rrt *r, int32_t K, hipStream_t stream) {
     c.use_grid = use_grid;
     c.live_list = live_list;
     return c;
+}
+
+// a deferred tree build that did not join a joint build: run it on the engine's stream
+void build_deferred(mpt_rrt *r, hipStream_t stream, const StepCtx &c) {
+    r->ptree->build(r->d_nodes, r->n_upper, r->d_n, r->p.d, stream, c.want_spread ? &c.spread : nullptr);
+    if (c.want_spread) hip_check(hipEventRecord(r->ev_spread, stream), "spread event");
 }
 
 void step_nn(mpt_rrt *r, int32_t K, hipStream_t stream, const StepCtx &c) {
@@ -763,28 +777,31 @@ namespace {
 // ring of pinned buffers, so filling one never waits for a copy still in flight.
 constexpr int kJobRing = 4;
 struct JointNN {
-    PtJob *d_jobs = nullptr;
-    PtJob *h_jobs[kJobRing] = {};
+    char *d_stage = nullptr;
+    char *h_stage[kJobRing] = {};
     hipEvent_t copied[kJobRing] = {};
-    int32_t cap = 0, next = 0;
+    size_t cap = 0;
+    int32_t next = 0;
     std::vector<hipEvent_t> joins;
     hipEvent_t done = nullptr;
     hipEvent_t t0 = nullptr, t1 = nullptr;  // around the last joint launch (engine timing on)
     bool timed = false;
+    JointTreeScratch trees;  // shared sort buffers of the joint tree build
 };
 thread_local JointNN g_joint;
 
-PtJob *joint_jobs(int32_t n, int *slot) {
+// a pinned staging buffer of at least `bytes` whose previous copy has completed
+char *joint_stage(size_t bytes, int *slot) {
     JointNN &g = g_joint;
-    if (n > g.cap) {
+    if (bytes > g.cap) {
         hip_check(hipDeviceSynchronize(), "sync");  // buffers may still be in use
-        if (g.d_jobs) hip_check(hipFree(g.d_jobs), "free");
+        if (g.d_stage) hip_check(hipFree(g.d_stage), "free");
         for (int i = 0; i < kJobRing; ++i)
-            if (g.h_jobs[i]) hip_check(hipHostFree(g.h_jobs[i]), "free");
-        const int32_t c = std::max(n, 2 * g.cap);
-        hip_check(hipMalloc(&g.d_jobs, sizeof(PtJob) * c), "jobs");
+            if (g.h_stage[i]) hip_check(hipHostFree(g.h_stage[i]), "free");
+        const size_t c = std::max(bytes, 2 * g.cap);
+        hip_check(hipMalloc(&g.d_stage, c), "stage");
         for (int i = 0; i < kJobRing; ++i) {
-            hip_check(hipHostMalloc(&g.h_jobs[i], sizeof(PtJob) * c), "jobs pinned");
+            hip_check(hipHostMalloc(&g.h_stage[i], c), "stage pinned");
             if (!g.copied[i]) hip_check(hipEventCreateWithFlags(&g.copied[i], hipEventDisableTiming), "event");
         }
         if (!g.done) hip_check(hipEventCreateWithFlags(&g.done, hipEventDisableTiming), "event");
@@ -794,7 +811,7 @@ PtJob *joint_jobs(int32_t n, int *slot) {
     g.next = (g.next + 1) % kJobRing;
     // the copy that last read this staging buffer was kJobRing calls ago
     hip_check(hipEventSynchronize(g.copied[*slot]), "jobs staging");
-    return g.h_jobs[*slot];
+    return g.h_stage[*slot];
 }
 
 }  // namespace
@@ -808,24 +825,42 @@ extern "C" mpt_status mpt_rrt_step_many(mpt_rrt *const *rs, int32_t n, int32_t K
         auto stream_of = [&](int32_t i) { return (hipStream_t)streams_[i]; };
         const hipStream_t joint = (hipStream_t)joint_stream_;
         std::vector<StepCtx> cs(n);
-        for (int32_t i = 0; i < n; ++i) cs[i] = step_head(rs[i], K, stream_of(i));
+        for (int32_t i = 0; i < n; ++i) cs[i] = step_head(rs[i], K, stream_of(i), true);
         // engines whose round uses the Morton tree (and the first such engine's state dim)
-        // share one NN launch; the rest query their own index on their own stream
+        // share one index build (a launch per stage + one segmented sort) and one NN launch;
+        // the rest query their own index on their own stream
         std::vector<int32_t> J;
         for (int32_t i = 0; i < n; ++i)
             if (cs[i].use_tree && (J.empty() || rs[i]->p.d == rs[J[0]]->p.d)) J.push_back(i);
+        if (J.size() < 2) J.clear();
         std::vector<char> joined(n, 0);
-        if (J.size() >= 2) {
+        for (int32_t i : J) joined[i] = 1;
+        for (int32_t i = 0; i < n; ++i)
+            if (cs[i].defer_tree && !joined[i]) build_deferred(rs[i], stream_of(i), cs[i]);
+        if (!J.empty()) {
             JointNN &g = g_joint;
+            const int32_t nj = (int32_t)J.size();
+            const size_t b_build = sizeof(PtBuildJob) * nj, b_nn = sizeof(PtJob) * nj;
+            const size_t b_off = sizeof(int32_t) * (nj + 1);
             int slot = 0;
-            PtJob *h = joint_jobs((int32_t)J.size(), &slot);
-            for (size_t k = 0; k < J.size(); ++k) {
+            char *h = joint_stage(b_build + b_nn + b_off, &slot);
+            PtBuildJob *hb = reinterpret_cast<PtBuildJob *>(h);
+            PtJob *hn = reinterpret_cast<PtJob *>(h + b_build);
+            int32_t *ho = reinterpret_cast<int32_t *>(h + b_build + b_nn);
+            int64_t total = 0;
+            for (int32_t k = 0; k < nj; ++k) {
                 mpt_rrt *r = rs[J[k]];
+                const StepCtx &c = cs[J[k]];
+                ho[k] = (int32_t)total;
+                hb[k] = r->ptree->prepare(r->d_nodes, r->n_upper, r->d_n, r->p.d, total,
+                                          c.want_spread ? &c.spread : nullptr);
+                total += r->n_upper;
+                if (total >= (int64_t(1) << 31)) throw Error{MPT_ERR_INVALID, "joint build: too many points"};
                 PointTreeDev T = r->ptree->dev();
                 T.stats = r->stats_on ? r->d_cstats + 8 : nullptr;
-                h[k] = PtJob{T, r->d_samples, r->d_nn, r->d_nnd2};
-                joined[J[k]] = 1;
+                hn[k] = PtJob{T, r->d_samples, r->d_nn, r->d_nnd2};
             }
+            ho[nj] = (int32_t)total;
             // the joint stream waits for every engine stream's heads, the engines' tails for it
             std::vector<hipStream_t> uniq;
             for (int32_t i : J)
@@ -839,8 +874,14 @@ extern "C" mpt_status mpt_rrt_step_many(mpt_rrt *const *rs, int32_t n, int32_t K
                 hip_check(hipEventRecord(g.joins[u], uniq[u]), "join record");
                 hip_check(hipStreamWaitEvent(joint, g.joins[u], 0), "join wait");
             }
-            hip_check(hipMemcpyAsync(g.d_jobs, h, sizeof(PtJob) * J.size(), hipMemcpyHostToDevice, joint), "jobs H2D");
+            hip_check(hipMemcpyAsync(g.d_stage, h, b_build + b_nn + b_off, hipMemcpyHostToDevice, joint), "jobs H2D");
             hip_check(hipEventRecord(g.copied[slot], joint), "jobs copied");
+            const PtBuildJob *db = reinterpret_cast<const PtBuildJob *>(g.d_stage);
+            const PtJob *dn = reinterpret_cast<const PtJob *>(g.d_stage + b_build);
+            const int32_t *doff = reinterpret_cast<const int32_t *>(g.d_stage + b_build + b_nn);
+            launch_tree_build_jobs(db, hb, nj, rs[J[0]]->p.d, doff, total, g.trees, joint);
+            for (int32_t i : J)
+                if (cs[i].want_spread) hip_check(hipEventRecord(rs[i]->ev_spread, joint), "spread event");
             bool timed = false;
             for (int32_t i : J) timed = timed || rs[i]->timing;
             if (timed) {
@@ -850,7 +891,7 @@ extern "C" mpt_status mpt_rrt_step_many(mpt_rrt *const *rs, int32_t n, int32_t K
                 }
                 hip_check(hipEventRecord(g.t0, joint), "joint t0");
             }
-            launch_tree_nn1_jobs(g.d_jobs, (int32_t)J.size(), rs[J[0]]->p.d, K, joint);
+            launch_tree_nn1_jobs(dn, nj, rs[J[0]]->p.d, K, joint);
             if (timed) hip_check(hipEventRecord(g.t1, joint), "joint t1");
             g.timed = timed;
             hip_check(hipEventRecord(g.done, joint), "joint done");
