@@ -146,23 +146,36 @@ __device__ __forceinline__ void pt_bbox(const double *__restrict__ pts, int32_t 
     }
     __syncthreads();
     const int64_t n = *n_dev < n_upper ? *n_dev : n_upper;
-    for (int j = 0; j < d; ++j) {
-        unsigned long long mn = ~0ull, mx = 0ull;
-        for (int64_t i = blk * blockDim.x + threadIdx.x; i < n; i += nblk * blockDim.x) {
-            const unsigned long long k = order_key_pt(pts[i * d + j]);
-            mn = k < mn ? k : mn;
-            mx = k > mx ? k : mx;
-        }
+    // one pass over each point's row (all dims at once: a per-dim pass re-reads every row d
+    // times, which the joint build's 256 trees cannot keep in L2)
+    unsigned long long mn[kPtMaxDim], mx[kPtMaxDim];
+#pragma unroll
+    for (int j = 0; j < kPtMaxDim; ++j) {
+        mn[j] = ~0ull;
+        mx[j] = 0ull;
+    }
+    for (int64_t i = blk * blockDim.x + threadIdx.x; i < n; i += nblk * blockDim.x) {
+#pragma unroll
+        for (int j = 0; j < kPtMaxDim; ++j)
+            if (j < d) {
+                const unsigned long long k = order_key_pt(pts[i * d + j]);
+                mn[j] = k < mn[j] ? k : mn[j];
+                mx[j] = k > mx[j] ? k : mx[j];
+            }
+    }
+#pragma unroll
+    for (int j = 0; j < kPtMaxDim; ++j) {
+        if (j >= d) break;
         // one LDS atomic per wave, not per lane (256 same-address 64-bit atomics serialise)
 #pragma unroll
         for (int off = 32; off > 0; off >>= 1) {
-            const unsigned long long omn = __shfl_xor(mn, off), omx = __shfl_xor(mx, off);
-            mn = omn < mn ? omn : mn;
-            mx = omx > mx ? omx : mx;
+            const unsigned long long omn = __shfl_xor(mn[j], off), omx = __shfl_xor(mx[j], off);
+            mn[j] = omn < mn[j] ? omn : mn[j];
+            mx[j] = omx > mx[j] ? omx : mx[j];
         }
         if ((threadIdx.x & 63) == 0) {
-            atomicMin(&s_min[j], mn);
-            atomicMax(&s_max[j], mx);
+            atomicMin(&s_min[j], mn[j]);
+            atomicMax(&s_max[j], mx[j]);
         }
     }
     __syncthreads();
@@ -327,7 +340,11 @@ __global__ __launch_bounds__(256) void k_pt_boxes(PointTreeDev T, float *__restr
 // tree's keys / values live in shared buffers at its offset, sorted by one segmented sort
 __global__ __launch_bounds__(256) void k_pt_bbox_jobs(const PtBuildJob *__restrict__ jobs, int32_t d) {
     const PtBuildJob &J = jobs[blockIdx.y];
-    pt_bbox(J.pts, d, J.T.n_upper, J.T.n_dev, J.bbox, J.ticket + 1, J.plan, J.sp, blockIdx.x, gridDim.x);
+    // ~2048 points per workgroup (at most gridDim.x): 64 workgroups for every small tree cost
+    // more in fences, atomics and tickets than the scan itself
+    const int64_t nblk = std::min<int64_t>(gridDim.x, std::max<int64_t>(1, (J.T.n_upper + 2047) / 2048));
+    if (blockIdx.x >= nblk) return;  // before the ticket: only the tree's own workgroups count
+    pt_bbox(J.pts, d, J.T.n_upper, J.T.n_dev, J.bbox, J.ticket + 1, J.plan, J.sp, blockIdx.x, nblk);
 }
 __global__ __launch_bounds__(256) void k_pt_morton_jobs(const PtBuildJob *__restrict__ jobs, int32_t d,
                                                         uint32_t *__restrict__ keys, int32_t *__restrict__ vals) {
