@@ -338,11 +338,13 @@ __global__ __launch_bounds__(256) void k_pt_boxes(PointTreeDev T, float *__restr
 
 // ---- the same build for many trees at once (mpt_rrt_step_many): blockIdx.y = the tree; a
 // tree's keys / values live in shared buffers at its offset, sorted by one segmented sort
-__global__ __launch_bounds__(256) void k_pt_bbox_jobs(const PtBuildJob *__restrict__ jobs, int32_t d) {
+__global__ __launch_bounds__(256) void k_pt_bbox_jobs(const PtBuildJob *__restrict__ jobs, int32_t d,
+                                                      int32_t bbox_points_per_group) {
     const PtBuildJob &J = jobs[blockIdx.y];
     // ~2048 points per workgroup (at most gridDim.x): 64 workgroups for every small tree cost
     // more in fences, atomics and tickets than the scan itself
-    const int64_t nblk = std::min<int64_t>(gridDim.x, std::max<int64_t>(1, (J.T.n_upper + 2047) / 2048));
+    const int64_t per = bbox_points_per_group;
+    const int64_t nblk = std::min<int64_t>(gridDim.x, std::max<int64_t>(1, (J.T.n_upper + per - 1) / per));
     if (blockIdx.x >= nblk) return;  // before the ticket: only the tree's own workgroups count
     pt_bbox(J.pts, d, J.T.n_upper, J.T.n_dev, J.bbox, J.ticket + 1, J.plan, J.sp, blockIdx.x, nblk);
 }
@@ -697,7 +699,10 @@ void launch_tree_build_jobs(const PtBuildJob *d_jobs, const PtBuildJob *h_jobs, 
         S.temp_bytes = tb;
     }
     const unsigned bx = (unsigned)((max_n + 255) / 256);
-    hipLaunchKernelGGL(k_pt_bbox_jobs, dim3(64, n), dim3(256), 0, stream, d_jobs, d);
+    // MPT_PT_BBOX_PTS: points per bbox workgroup of the joint build (A/B knob)
+    static const int per = getenv("MPT_PT_BBOX_PTS") && atoi(getenv("MPT_PT_BBOX_PTS")) > 0
+                               ? atoi(getenv("MPT_PT_BBOX_PTS")) : 2048;
+    hipLaunchKernelGGL(k_pt_bbox_jobs, dim3(64, n), dim3(256), 0, stream, d_jobs, d, per);
     hipLaunchKernelGGL(k_pt_morton_jobs, dim3(bx, n), dim3(256), 0, stream, d_jobs, d, S.keys, S.vals);
     hip_check(hipGetLastError(), "k_pt_morton_jobs");
     tb = S.temp_bytes;

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Joint tree build (one launch per stage + a segmented sort for all seeds): parity, then config 5.
 OUT=gpurun_out/ab5i; mkdir -p $OUT
-timeout -k 10 300 python -u -m pytest tests/test_engine_gpu.py -x -q -p no:cacheprovider --timeout 120 --timeout-method thread > $OUT/tests.log 2>&1 || { tail -30 $OUT/tests.log; exit 1; }
+timeout -k 10 300 python -u -m pytest tests/test_engine_gpu.py tests/test_prm_connect_gpu.py tests/test_nn_gpu.py -x -q -p no:cacheprovider --timeout 120 --timeout-method thread > $OUT/tests.log 2>&1 || { tail -30 $OUT/tests.log; exit 1; }
 tail -2 $OUT/tests.log
 for i in 1 2; do
   timeout -k 10 180 python bench.py --seeds 256 --steps 6 --warmup 3 --no-cpu > $OUT/c5_$i.log 2>&1 || { tail -20 $OUT/c5_$i.log; exit 1; }
