@@ -192,13 +192,19 @@ mpt_status mpt_rrt_set_size(mpt_rrt *rrt, int64_t n, void *stream);
  * collision -> ordered append of the collision-free edges.  Asynchronous. */
 mpt_status mpt_rrt_step(mpt_rrt *rrt, int32_t K, void *stream);
 /* One round of n independent engines (BASELINE config 5: one engine per seed), engine i on
- * streams[i].  Identical results to mpt_rrt_step per engine; the engines whose round uses the
- * Morton-tree NN share one query launch on joint_stream (which waits for their sample + index
- * build and is waited on by their steer + collide + append).  Asynchronous. */
+ * streams[i].  Identical results to mpt_rrt_step per engine.  The engines whose round uses the
+ * Morton-tree NN share one index build (a launch per stage + one segmented sort) and one query
+ * launch, both on joint_stream, which waits for their samples and is waited on by their
+ * steer + collide + append.  The job tables and sort buffers of the joint launches belong to
+ * joint_stream: calls with different joint streams (from one or several host threads) may
+ * overlap; calls on one joint stream are serialised.  Asynchronous. */
 mpt_status mpt_rrt_step_many(mpt_rrt *const *rrts, int32_t n, int32_t K, void *const *streams, void *joint_stream);
-/* Duration (ms, hipEvents on joint_stream) of the calling thread's last joint NN launch of
+/* Duration (ms, hipEvents on its joint stream) of the calling thread's last joint NN launch of
  * mpt_rrt_step_many that had an engine with timing enabled.  Synchronises on it. */
 mpt_status mpt_rrt_joint_nn_ms(float *ms);
+/* The last timed mpt_rrt_step_many on joint_stream: ms[0] = the joint tree build, ms[1] = the
+ * joint NN launch (hipEvents on joint_stream).  Synchronises on it. */
+mpt_status mpt_rrt_joint_times(void *joint_stream, float ms[2]);
 /* counters [8]: rounds, extensions checked, extensions valid, nodes, capacity drops,
  * pose overflow, reserved, reserved.  Synchronises. */
 mpt_status mpt_rrt_counters(mpt_rrt *rrt, uint64_t counters[8]);

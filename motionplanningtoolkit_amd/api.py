@@ -386,6 +386,14 @@ def joint_nn_ms() -> float:
     check(lib().mpt_rrt_joint_nn_ms(C.byref(ms)), "mpt_rrt_joint_nn_ms")
     return ms.value
 
+
+def joint_times(joint_stream) -> dict:
+    """The last timed step_many on joint_stream: {"build": ms of the joint tree build,
+    "nn": ms of the joint NN launch} (hipEvents on that stream)."""
+    ms = np.zeros(2, np.float32)
+    check(lib().mpt_rrt_joint_times(_stream(joint_stream), _p(ms)), "mpt_rrt_joint_times")
+    return {"build": float(ms[0]), "nn": float(ms[1])}
+
 def load_mesh(path: str, which: str = "all") -> np.ndarray:
     """AssimpMeshLoader replacement: 'all' submeshes (environment) or 'last' (agent)."""
     w = 1 if which == "last" else 0

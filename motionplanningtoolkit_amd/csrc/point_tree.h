@@ -35,7 +35,8 @@ struct PtBuildJob {
     SpreadOut sp;
 };
 
-// shared sort buffers of a joint build (grown on demand, owned by the caller)
+// shared sort buffers of a joint build (owned by the caller; reserve_tree_build_jobs sizes
+// them for the joined trees' capacities so later rounds never allocate)
 struct JointTreeScratch {
     uint32_t *keys = nullptr, *keys_sorted = nullptr;
     int32_t *vals = nullptr, *vals_sorted = nullptr;
@@ -49,6 +50,9 @@ struct JointTreeScratch {
 // device, total = its last entry.  Stream-ordered.
 void launch_tree_build_jobs(const PtBuildJob *d_jobs, const PtBuildJob *h_jobs, int32_t n, int32_t d,
                             const int32_t *d_offsets, int64_t total, JointTreeScratch &S, hipStream_t stream);
+// Size S for up to total_cap points in n_jobs segments (synchronises the device only when it
+// grows: call it before staging a round, not inside one).
+void reserve_tree_build_jobs(JointTreeScratch &S, int64_t total_cap, int32_t n_jobs);
 
 class PointTree {
 public:

@@ -669,6 +669,32 @@ PtBuildJob PointTree::prepare(const double *pts, int64_t n_upper, const int64_t 
     return PtBuildJob{t, pts, off, bbox, ticket, plan, spts, sids, boxes, spread ? *spread : SpreadOut{}};
 }
 
+void reserve_tree_build_jobs(JointTreeScratch &S, int64_t total_cap, int32_t n_jobs) {
+    if (total_cap >= (int64_t(1) << 31)) throw Error{1, "joint build: too many points"};
+    if (total_cap > S.cap) {
+        hip_check(hipDeviceSynchronize(), "sync");  // the old buffers may still be in use
+        for (void *p : {(void *)S.keys, (void *)S.keys_sorted, (void *)S.vals, (void *)S.vals_sorted})
+            if (p) hip_check(hipFree(p), "free");
+        const int64_t c = std::max<int64_t>(total_cap, 1024);
+        hip_check(hipMalloc(&S.keys, sizeof(uint32_t) * c), "joint keys");
+        hip_check(hipMalloc(&S.keys_sorted, sizeof(uint32_t) * c), "joint keys");
+        hip_check(hipMalloc(&S.vals, sizeof(int32_t) * c), "joint vals");
+        hip_check(hipMalloc(&S.vals_sorted, sizeof(int32_t) * c), "joint vals");
+        S.cap = c;
+    }
+    size_t tb = 0;
+    hip_check(hipcub::DeviceSegmentedRadixSort::SortPairs(nullptr, tb, S.keys, S.keys_sorted, S.vals, S.vals_sorted,
+                                                          (int)S.cap, n_jobs, (const int32_t *)nullptr,
+                                                          (const int32_t *)nullptr, 0, 32, (hipStream_t)0),
+              "segmented sort size");
+    if (tb > S.temp_bytes) {
+        hip_check(hipDeviceSynchronize(), "sync");
+        if (S.temp) hip_check(hipFree(S.temp), "free");
+        hip_check(hipMalloc(&S.temp, tb), "segmented sort temp");
+        S.temp_bytes = tb;
+    }
+}
+
 void launch_tree_build_jobs(const PtBuildJob *d_jobs, const PtBuildJob *h_jobs, int32_t n, int32_t d,
                             const int32_t *d_offsets, int64_t total, JointTreeScratch &S, hipStream_t stream) {
     if (n <= 0) return;

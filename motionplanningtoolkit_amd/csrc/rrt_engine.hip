@@ -16,9 +16,10 @@
 // (host/rrt.hpp over the same kernels).
 #include <algorithm>
 #include <cstring>
-#include <vector>
-
+#include <map>
 #include <memory>
+#include <mutex>
+#include <vector>
 
 #include "../../include/mpt.h"
 #include "grid_nn.h"
@@ -679,7 +680,8 @@ StepCtx step_head(mpt_rrt *r, int32_t K, hipStream_t stream, bool defer_tree = f
         r->spread_pending = true;
         r->rounds_since_spread = 0;
     }
-    c.mark(2, stream);
+    // a deferred build is marked where it runs (build_deferred, or after the joint build)
+    if (!c.defer_tree) c.mark(2, stream);
     c.use_tree = use_tree;
     c.use_grid = use_grid;
     c.live_list = live_list;
@@ -690,6 +692,7 @@ StepCtx step_head(mpt_rrt *r, int32_t K, hipStream_t stream, bool defer_tree = f
 void build_deferred(mpt_rrt *r, hipStream_t stream, const StepCtx &c) {
     r->ptree->build(r->d_nodes, r->n_upper, r->d_n, r->p.d, stream, c.want_spread ? &c.spread : nullptr);
     if (c.want_spread) hip_check(hipEventRecord(r->ev_spread, stream), "spread event");
+    c.mark(2, stream);
 }
 
 void step_nn(mpt_rrt *r, int32_t K, hipStream_t stream, const StepCtx &c) {
@@ -773,26 +776,46 @@ extern "C" mpt_status mpt_rrt_step(mpt_rrt *r, int32_t K, void *stream_) {
 
 namespace {
 
-// Host-side state of the joint NN launch (one per host thread): the job table is staged in a
-// ring of pinned buffers, so filling one never waits for a copy still in flight.
+// Host-side state of the joint build + NN launch, one per joint stream: the device job table
+// (d_stage) and the build's sort buffers are read by kernels on that stream, so only work
+// ordered on the same stream may overwrite them.  (Round 1 kept one per host thread: two
+// step_many groups on different joint streams then overwrote each other's job table and
+// sort keys while the other group's kernels still read them.)  The table is staged through
+// a ring of pinned buffers, so filling one never waits for a copy still in flight.
 constexpr int kJobRing = 4;
 struct JointNN {
+    std::mutex mu;  // one step_many at a time per joint stream (the ring and the tables)
     char *d_stage = nullptr;
     char *h_stage[kJobRing] = {};
     hipEvent_t copied[kJobRing] = {};
     size_t cap = 0;
     int32_t next = 0;
     std::vector<hipEvent_t> joins;
-    hipEvent_t done = nullptr;
-    hipEvent_t t0 = nullptr, t1 = nullptr;  // around the last joint launch (engine timing on)
+    hipEvent_t done = nullptr, built = nullptr;
+    // engine timing on: b0 -> t0 = the joint tree build, t0 -> t1 = the joint NN launch
+    hipEvent_t b0 = nullptr, t0 = nullptr, t1 = nullptr;
     bool timed = false;
     JointTreeScratch trees;  // shared sort buffers of the joint tree build
 };
-thread_local JointNN g_joint;
+std::mutex g_joints_mu;
+std::map<hipStream_t, std::unique_ptr<JointNN>> g_joints;
+thread_local JointNN *g_last_timed = nullptr;  // mpt_rrt_joint_nn_ms: this thread's last timed call
+
+JointNN &joint_state(hipStream_t s) {
+    std::lock_guard<std::mutex> lk(g_joints_mu);
+    std::unique_ptr<JointNN> &p = g_joints[s];
+    if (!p) p.reset(new JointNN());
+    return *p;
+}
+
+JointNN *joint_find(hipStream_t s) {
+    std::lock_guard<std::mutex> lk(g_joints_mu);
+    const auto it = g_joints.find(s);
+    return it == g_joints.end() ? nullptr : it->second.get();
+}
 
 // a pinned staging buffer of at least `bytes` whose previous copy has completed
-char *joint_stage(size_t bytes, int *slot) {
-    JointNN &g = g_joint;
+char *joint_stage(JointNN &g, size_t bytes, int *slot) {
     if (bytes > g.cap) {
         hip_check(hipDeviceSynchronize(), "sync");  // buffers may still be in use
         if (g.d_stage) hip_check(hipFree(g.d_stage), "free");
@@ -805,6 +828,7 @@ char *joint_stage(size_t bytes, int *slot) {
             if (!g.copied[i]) hip_check(hipEventCreateWithFlags(&g.copied[i], hipEventDisableTiming), "event");
         }
         if (!g.done) hip_check(hipEventCreateWithFlags(&g.done, hipEventDisableTiming), "event");
+        if (!g.built) hip_check(hipEventCreateWithFlags(&g.built, hipEventDisableTiming), "event");
         g.cap = c;
     }
     *slot = g.next;
@@ -838,12 +862,18 @@ extern "C" mpt_status mpt_rrt_step_many(mpt_rrt *const *rs, int32_t n, int32_t K
         for (int32_t i = 0; i < n; ++i)
             if (cs[i].defer_tree && !joined[i]) build_deferred(rs[i], stream_of(i), cs[i]);
         if (!J.empty()) {
-            JointNN &g = g_joint;
+            JointNN &g = joint_state(joint);
+            std::lock_guard<std::mutex> lk(g.mu);
             const int32_t nj = (int32_t)J.size();
+            // the shared sort buffers sized for the joined trees' capacities once, so no later
+            // round allocates (an allocation synchronises the device and stalls every stream)
+            int64_t cap_total = 0;
+            for (int32_t i : J) cap_total += rs[i]->cap;
+            reserve_tree_build_jobs(g.trees, cap_total, nj);
             const size_t b_build = sizeof(PtBuildJob) * nj, b_nn = sizeof(PtJob) * nj;
             const size_t b_off = sizeof(int32_t) * (nj + 1);
             int slot = 0;
-            char *h = joint_stage(b_build + b_nn + b_off, &slot);
+            char *h = joint_stage(g, b_build + b_nn + b_off, &slot);
             PtBuildJob *hb = reinterpret_cast<PtBuildJob *>(h);
             PtJob *hn = reinterpret_cast<PtJob *>(h + b_build);
             int32_t *ho = reinterpret_cast<int32_t *>(h + b_build + b_nn);
@@ -879,20 +909,31 @@ extern "C" mpt_status mpt_rrt_step_many(mpt_rrt *const *rs, int32_t n, int32_t K
             const PtBuildJob *db = reinterpret_cast<const PtBuildJob *>(g.d_stage);
             const PtJob *dn = reinterpret_cast<const PtJob *>(g.d_stage + b_build);
             const int32_t *doff = reinterpret_cast<const int32_t *>(g.d_stage + b_build + b_nn);
-            launch_tree_build_jobs(db, hb, nj, rs[J[0]]->p.d, doff, total, g.trees, joint);
-            for (int32_t i : J)
-                if (cs[i].want_spread) hip_check(hipEventRecord(rs[i]->ev_spread, joint), "spread event");
             bool timed = false;
             for (int32_t i : J) timed = timed || rs[i]->timing;
             if (timed) {
                 if (!g.t0) {
+                    hip_check(hipEventCreate(&g.b0), "event");
                     hip_check(hipEventCreate(&g.t0), "event");
                     hip_check(hipEventCreate(&g.t1), "event");
                 }
+                hip_check(hipEventRecord(g.b0, joint), "joint b0");
+            }
+            launch_tree_build_jobs(db, hb, nj, rs[J[0]]->p.d, doff, total, g.trees, joint);
+            for (int32_t i : J)
+                if (cs[i].want_spread) hip_check(hipEventRecord(rs[i]->ev_spread, joint), "spread event");
+            if (timed) {
                 hip_check(hipEventRecord(g.t0, joint), "joint t0");
+                // the engines' nn_build stage ends with the joint build
+                hip_check(hipEventRecord(g.built, joint), "joint built");
+                for (hipStream_t s : uniq) hip_check(hipStreamWaitEvent(s, g.built, 0), "built wait");
+                for (int32_t i : J) cs[i].mark(2, stream_of(i));
             }
             launch_tree_nn1_jobs(dn, nj, rs[J[0]]->p.d, K, joint);
-            if (timed) hip_check(hipEventRecord(g.t1, joint), "joint t1");
+            if (timed) {
+                hip_check(hipEventRecord(g.t1, joint), "joint t1");
+                g_last_timed = &g;
+            }
             g.timed = timed;
             hip_check(hipEventRecord(g.done, joint), "joint done");
             for (hipStream_t s : uniq) hip_check(hipStreamWaitEvent(s, g.done, 0), "joint wait");
@@ -907,9 +948,24 @@ extern "C" mpt_status mpt_rrt_step_many(mpt_rrt *const *rs, int32_t n, int32_t K
 extern "C" mpt_status mpt_rrt_joint_nn_ms(float *ms) {
     return guarded([&] {
         if (!ms) throw Error{MPT_ERR_INVALID, "null pointer"};
-        if (!g_joint.timed) throw Error{MPT_ERR_INVALID, "no timed joint NN launch on this thread"};
-        hip_check(hipEventSynchronize(g_joint.t1), "event sync");
-        hip_check(hipEventElapsedTime(ms, g_joint.t0, g_joint.t1), "elapsed");
+        JointNN *g = g_last_timed;
+        if (!g) throw Error{MPT_ERR_INVALID, "no timed joint NN launch on this thread"};
+        std::lock_guard<std::mutex> lk(g->mu);
+        hip_check(hipEventSynchronize(g->t1), "event sync");
+        hip_check(hipEventElapsedTime(ms, g->t0, g->t1), "elapsed");
+    });
+}
+
+extern "C" mpt_status mpt_rrt_joint_times(void *joint_stream, float ms[2]) {
+    return guarded([&] {
+        if (!ms) throw Error{MPT_ERR_INVALID, "null pointer"};
+        JointNN *g = joint_find((hipStream_t)joint_stream);
+        if (!g) throw Error{MPT_ERR_INVALID, "no joint launch on this stream"};
+        std::lock_guard<std::mutex> lk(g->mu);
+        if (!g->timed) throw Error{MPT_ERR_INVALID, "the last joint launch on this stream was not timed"};
+        hip_check(hipEventSynchronize(g->t1), "event sync");
+        hip_check(hipEventElapsedTime(&ms[0], g->b0, g->t0), "elapsed");
+        hip_check(hipEventElapsedTime(&ms[1], g->t0, g->t1), "elapsed");
     });
 }
 

@@ -147,6 +147,18 @@ def blimp_scenario(agent_submeshes: str = "all") -> Scenario:
                     np.array([1.0, 1.0, 1.0]), notes={"agent_submeshes": agent_submeshes})
 
 
+def blimp_room_scenario(agent_submeshes: str = "all") -> Scenario:
+    """The collision-heavy config-2 variant (BASELINE config 2 "with poses drawn
+    from the tree"): blimp.inst's agent and dynamics in model.dae, with the sampling box's
+    x, y, z ranges = the room's bounding box (0-177.2 x 0-137.8 x 0-114.2) instead of
+    blimp.inst:17's [-100, 100]^3, so every pose lies in the room and reaches the narrow phase."""
+    sc = blimp_scenario(agent_submeshes)
+    v = sc.env_tris.reshape(-1, 3)
+    sc.ranges = blimp_ranges(tuple(zip(v.min(0).tolist(), v.max(0).tolist())))
+    sc.name = "blimp-room"
+    return sc
+
+
 SNAKE_PRM = np.array([10, 1.0, 0.25, -1.0, 5.0, -0.785398, 0.785398])  # snake.inst:7-15
 
 

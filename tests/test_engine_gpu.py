@@ -295,6 +295,79 @@ def test_step_many_matches_single_steps(mpt_gpu):
         assert np.array_equal(bits(sa), bits(sb)) and np.array_equal(pa, pb)
 
 
+def test_step_many_groups_on_separate_joint_streams(mpt_gpu):
+    """Several step_many groups issued back to back from one host thread, each group on its own
+    engine streams and its own joint stream (bench.py --joint-groups): the joint job tables and
+    sort buffers belong to the joint stream, so one group's staging never overwrites what
+    another group's build and NN kernels still read (the round-1 race).  Group A: blimp seeds of
+    ragged sizes (one root; 3 000, 9 000 and 140 000 pre-added nodes: several bbox workgroups,
+    the box-level ticket path, more than 131 072 points); group B: blimp seeds from one root;
+    group C: the snake (d = 15, the 16-wide register rows).  Every tree must equal the one its
+    seed grows alone with mpt_rrt_step, bit for bit; the joint build / NN times are reported
+    per joint stream."""
+    import torch
+
+    blimp = scenes.blimp_scenario("all")
+    snake = scenes.snake_scenario("corridor")
+    root_b = np.array([[88.6, 68.9, 57.1, 0, 0, 0, 0.0]])
+    rng = np.random.default_rng(21)
+
+    def blob(n):
+        t = rng.uniform(blimp.ranges[:, 0], blimp.ranges[:, 1], size=(n, 7))
+        t[:, :3] = root_b[0, :3] + rng.normal(0.0, 8.0, size=(n, 3))
+        return t
+
+    K, rounds = 2048, 3
+    specs = []  # (scenario, seed, initial nodes, group)
+    for s, n in zip(range(700, 704), (1, 3000, 9000, 140_000)):
+        specs.append((blimp, s, root_b if n == 1 else blob(n), 0))
+    for s in range(710, 714):
+        specs.append((blimp, s, root_b, 1))
+    for s in range(720, 724):
+        specs.append((snake, s, np.asarray(snake.start, np.float64).reshape(1, -1), 2))
+    handles = {}
+    for sc in (blimp, snake):
+        handles[sc.name] = (mpt_gpu.Environment(sc.env_tris, sc.env_tf), mpt_gpu.AgentMesh(sc.agent_tris))
+    groups = [[j for j, sp in enumerate(specs) if sp[3] == g] for g in range(3)]
+
+    def grow(joint):
+        engs = []
+        for sc, s, init, _ in specs:
+            env, ag = handles[sc.name]
+            e = mpt_gpu.RRTEngine(env, ag, sc.kind, sc.prm, sc.ranges, sc.steer_dt, sc.cc_dt, len(init) + rounds * K, s)
+            e.add_nodes(init)
+            e.set_nn("tree")
+            engs.append(e)
+        streams = [[torch.cuda.Stream() for _ in range(2)] for _ in groups]
+        joints = [torch.cuda.Stream() for _ in groups]
+        times = None
+        for r in range(rounds):
+            if joint:
+                if r == rounds - 1:
+                    engs[groups[0][0]].enable_timing(True)
+                for g, idx in enumerate(groups):
+                    mpt_gpu.step_many([engs[j] for j in idx], K, [streams[g][k % 2] for k in range(len(idx))], joints[g])
+            else:
+                for e in engs:
+                    e.step(K)
+        torch.cuda.synchronize()
+        if joint:
+            times = mpt_gpu.joint_times(joints[0])
+        out = []
+        for e in engs:
+            assert e.last_nn() == "tree"
+            out.append(e.read_tree(e.counters()["nodes"]))
+            e.close()
+        return out, times
+
+    alone, _ = grow(False)
+    joint, times = grow(True)
+    for (sa, pa), (sb, pb) in zip(alone, joint):
+        assert len(sa) > K
+        assert np.array_equal(bits(sa), bits(sb)) and np.array_equal(pa, pb)
+    assert times["build"] > 0 and times["nn"] > 0
+
+
 def test_engine_set_size_and_capacity(mpt_gpu, oracle):
     sc = scenes.omni_scenario()
     eng, tree = make(mpt_gpu, sc, 100, 256, 5, cap_extra=50)

@@ -1,0 +1,174 @@
+"""GPU parity at the BASELINE configurations' full sizes.
+
+* Config 2: one engine round of the benchmark's exact shape -- 100 000-node blimp tree,
+  K = 65 536 extensions, blimp (1355 tris) vs the room (model.dae) -- NN ids of every query
+  against the oracle's exact kd-tree, collision verdicts of 4096 sampled extensions against
+  the oracle's AABB-tree collider (on the device's own poses), and the ordered append.
+* Config 2, collision-heavy variant (`bench.py --workload blimp-room`): tree and samples
+  inside the room, so every unit reaches the narrow phase.
+* Config 4: the 25 x 25-room environment (197 500 triangles, a four-level env tree that does
+  not fit the k_pairs LDS stage) with 100 000 milestones over the whole multi-room extent:
+  the roadmap of a milestone prefix against orc_prm_radius (edges, verdicts), the full edge
+  set against scipy's cKDTree (pairs within 1e-9 relative of the radius are excluded: FLANN's
+  summation order and cKDTree's differ there), the components against a host union-find, and
+  mpt_collide_batch against orc_collide_batch_bvh on 4096 poses spread over the rooms.
+Bars as everywhere: ids, verdicts, edge lists and components bit-exact.
+"""
+import math
+import os
+
+import numpy as np
+import pytest
+
+from motionplanningtoolkit_amd import scenes
+
+pytestmark = pytest.mark.gpu
+
+THREADS = min(16, len(os.sched_getaffinity(0)))
+I12 = np.r_[np.eye(3).ravel(), 0.0, 0.0, 0.0]
+
+
+def _engine_round_check(mpt, oracle, sc, tree, K, seed, n_sample=4096):
+    env = mpt.Environment(sc.env_tris, sc.env_tf)
+    ag = mpt.AgentMesh(sc.agent_tris)
+    n0 = len(tree)
+    eng = mpt.RRTEngine(env, ag, sc.kind, sc.prm, sc.ranges, sc.steer_dt, sc.cc_dt, n0 + K, seed)
+    eng.add_nodes(tree)
+    eng.step(K)
+    samples, nn, ends, verdict = eng.last_round(K)
+    poses, pcount = eng.last_poses(K)
+    # samples: the counter-based generator (spot check, pure +,-,* arithmetic)
+    for k in (0, 1, K // 2, K - 1):
+        exp = [oracle.engine_uniform(seed, k * 64 + j, lo, hi) for j, (lo, hi) in enumerate(sc.ranges)]
+        assert np.array_equal(samples[k], np.array(exp))
+    # NN ids of every query (exact kd-tree with FLANN's distance order, ties to the lowest id)
+    ref_ids, _ = oracle.KDTree(tree).knn(samples, 1, nthreads=THREADS)
+    assert np.array_equal(nn, ref_ids[:, 0])
+    # verdicts of a sample of extensions, on the device's own poses
+    rng = np.random.default_rng(seed)
+    idx = np.sort(rng.choice(K, size=min(n_sample, K), replace=False))
+    flat = np.concatenate([poses[k, :pcount[k]] for k in idx]).reshape(-1, 1, 12)
+    off = np.r_[0, np.cumsum(pcount[idx])]
+    ref_v = oracle.collide_batch_bvh(oracle.BVH(sc.env_tris), sc.env_tf, [sc.agent_tris], flat, off,
+                                     nthreads=THREADS)
+    assert np.array_equal(verdict[idx], ref_v)
+    # ordered append of the collision-free extensions
+    valid = np.nonzero(verdict == 0)[0]
+    c = eng.counters()
+    assert c["nodes"] == n0 + len(valid)
+    t2, par = eng.read_tree(n0 + len(valid))
+    assert np.array_equal(t2[:n0], tree)
+    assert np.array_equal(t2[n0:], ends[valid]) and np.array_equal(par[n0:], nn[valid])
+    return verdict
+
+
+def test_config2_full_round(mpt_gpu, oracle):
+    sc = scenes.blimp_scenario("all")
+    seed = 1000  # bench.py's rank-0 seed
+    tree = np.random.default_rng(seed).uniform(sc.ranges[:, 0], sc.ranges[:, 1], size=(100_000, sc.dim))
+    v = _engine_round_check(mpt_gpu, oracle, sc, tree, 65_536, seed)
+    assert 0 < v.sum() < len(v)
+
+
+def test_config2_room_full_round(mpt_gpu, oracle):
+    """The collision-heavy variant: every pose inside the room's box."""
+    sc = scenes.blimp_room_scenario()
+    seed = 1000
+    tree = np.random.default_rng(seed).uniform(sc.ranges[:, 0], sc.ranges[:, 1], size=(100_000, sc.dim))
+    v = _engine_round_check(mpt_gpu, oracle, sc, tree, 65_536, seed)
+    assert v.mean() > 0.05  # a real collision workload
+
+
+def rooms_prm_inputs(n=100_000, rooms=25, degree=10.0, seed=0):
+    """Config 4 milestones over the whole multi-room extent (scripts/bench_prm.py --bounds rooms)."""
+    sc = scenes.blimp_scenario("all")
+    env_t = scenes.rooms_env(rooms, rooms)
+    lo = env_t.reshape(-1, 3).min(0)
+    hi = env_t.reshape(-1, 3).max(0)
+    rng = np.random.default_rng(seed)
+    st = rng.uniform(sc.ranges[:, 0], sc.ranges[:, 1], size=(n, sc.dim))
+    st[:, :3] = rng.uniform(lo, hi, size=(n, 3))
+    vol = float(np.prod(hi - lo))
+    r = (degree * vol / (n * 4.0 / 3.0 * math.pi)) ** (1.0 / 3.0)
+    return sc, env_t, st, r * r
+
+
+def _components(n, edges, verdict):
+    parent = np.arange(n)
+
+    def find(a):
+        while parent[a] != a:
+            parent[a] = parent[parent[a]]
+            a = parent[a]
+        return a
+
+    for (i, j), v in zip(edges, verdict):
+        if v == 0:
+            a, b = find(int(i)), find(int(j))
+            if a != b:
+                parent[max(a, b)] = min(a, b)
+    return np.array([find(i) for i in range(n)], np.int32)
+
+
+def test_config4_rooms_at_size(mpt_gpu, oracle):
+    from scipy.spatial import cKDTree
+
+    sc, env_t, st, r2 = rooms_prm_inputs()
+    assert env_t.shape[0] == 197_500
+    env, ag = mpt_gpu.Environment(env_t, I12), mpt_gpu.AgentMesh(sc.agent_tris)
+    got = mpt_gpu.prm_connect(env, ag, 1, st, r2, sc.cc_dt)
+    edges, verdict = got["edges"], got["verdict"]
+    n = len(st)
+    assert len(edges) > 300_000 and 0 < verdict.sum() < len(verdict)
+    # (1) the whole edge set: pairs (i, j), j < i, of squared key distance < r2
+    keys = st[:, :3]
+    pairs = cKDTree(keys).query_pairs(math.sqrt(r2) * (1 + 1e-9), output_type="ndarray")
+    d2 = ((keys[pairs[:, 0]] - keys[pairs[:, 1]]) ** 2).sum(1)
+    clear = np.abs(d2 - r2) > 1e-9 * r2
+    exp = set(map(tuple, np.sort(pairs[clear & (d2 < r2)], axis=1)[:, ::-1].tolist()))
+    amb = set(map(tuple, np.sort(pairs[~clear], axis=1)[:, ::-1].tolist()))
+    got_set = set(map(tuple, edges.tolist()))
+    assert exp <= got_set and got_set - exp <= amb
+    # edges sorted by i, then j (the C ABI's order)
+    key = edges[:, 0].astype(np.int64) * n + edges[:, 1]
+    assert np.all(np.diff(key) > 0)
+    # (2) a milestone prefix against the oracle's restatement: edges and verdicts identical
+    #     (the oracle checks ~260 poses of the 1355-triangle blimp per edge: ~40 ms per edge)
+    k = 4_000
+    e_ref, v_ref, _ = oracle.prm_radius(oracle.BVH(env_t), I12, sc.agent_tris, st[:k], r2, sc.cc_dt,
+                                        nthreads=THREADS)
+    pre = edges[:, 0] < k
+    assert len(e_ref) > 400
+    assert np.array_equal(edges[pre], e_ref)
+    assert np.array_equal(verdict[pre], v_ref)
+    # (3) components over the free edges
+    assert np.array_equal(got["comp"], _components(n, edges, verdict))
+
+
+def test_config4_rooms_collide_batch(mpt_gpu, oracle):
+    """mpt_collide_batch in the 197 500-triangle env: 4096 single-pose edges (random yaw)
+    spread over the rooms, half of them near a wall."""
+    sc, env_t, _, _ = rooms_prm_inputs(n=10)
+    env, ag = mpt_gpu.Environment(env_t, I12), mpt_gpu.AgentMesh(sc.agent_tris)
+    rng = np.random.default_rng(11)
+    P = 4096
+    lo, hi = env_t.reshape(-1, 3).min(0), env_t.reshape(-1, 3).max(0)
+    xyz = rng.uniform(lo, hi, size=(P, 3))
+    # half of the poses within a few units of a random env vertex
+    v = env_t.reshape(-1, 3)[rng.integers(0, env_t.shape[0] * 3, size=P // 2)]
+    xyz[: P // 2] = v + rng.uniform(-6, 6, size=(P // 2, 3))
+    th = rng.uniform(0, 2 * math.pi, P)
+    poses = np.zeros((P, 12))
+    poses[:, 0], poses[:, 1], poses[:, 3], poses[:, 4], poses[:, 8] = np.cos(th), np.sin(th), -np.sin(th), np.cos(th), 1
+    poses[:, 9:] = xyz
+    off = np.arange(P + 1, dtype=np.int64)
+    for mode in ("split", "fused"):
+        mpt_gpu.set_collide_mode(mode)
+        try:
+            got = mpt_gpu.collide_batch(env, [ag], poses.reshape(P, 1, 12), off)
+        finally:
+            mpt_gpu.set_collide_mode("split")
+        ref = oracle.collide_batch_bvh(oracle.BVH(env_t), I12, [sc.agent_tris], poses.reshape(P, 1, 12), off,
+                                       nthreads=THREADS)
+        assert np.array_equal(got, ref), mode
+        assert 0.05 < got.mean() < 0.95
