@@ -7,18 +7,25 @@ Workload (one "step" = one batched RRT round on the device, motionplanningtoolki
   -> getPoses -> FCL-semantics collision -> ordered append of the collision-free edges.
   The tree is reset to its 100k base at the start of every round (inside the timed step)
   so every round does identical work.
+  --workload blimp-room: the same with the sampling box = the room's box, so every pose is
+  inside the room and reaches the narrow phase (the collision-heavy variant of config 2);
+  --workload snake: config 3; --seeds N: config 5 (N independent RRTs).
 
 Multi-GPU: one process per GPU (torchrun), each rank runs its own seed (independent
 trees, weak scaling); the only collective is the final max/sum reduction of timings and
 counters (RCCL), outside the data path.
 
-Prints ONE JSON line (rank 0).  See DESIGN.md "Measurement" for the roofline definition.
+Prints ONE JSON line (rank 0).  Roofline: per stage, compulsory bytes (every
+input and output of the launch once) / hipEvent time against the HBM peak, the measured HBM
+traffic of the same kernel (rocprofv3 FETCH_SIZE / WRITE_SIZE, profiles/<latest>/) against
+the same peak, their ratio, and the FP64 (collision kernels) or LDS (k_pairs) fraction.
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import subprocess
 import sys
 import time
 
@@ -27,8 +34,9 @@ import numpy as np
 REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
-FP64_PEAK_TFLOPS = 78.6   # MI355X FP64 (vector = matrix), AMD public spec; FMA counted as 2
-HBM_PEAK_GBS = 8000.0     # MI355X_MICROARCH.md: 8.0 TB/s spec
+FP64_PEAK_TFLOPS = 78.6   # MI355X FP64 vector peak (AMD public spec; FMA counted as 2)
+HBM_PEAK_GBS = 8000.0     # MI355X_MICROARCH.md §HBM: 8.0 TB/s spec
+LDS_PEAK_GBS = 150_000.0  # MI355X_MICROARCH.md §LDS: ~150 TB/s aggregate ds_read_b64/b128, every CU
 
 
 def parse():
@@ -39,8 +47,9 @@ def parse():
     ap.add_argument("--batch", type=int, default=65536, help="extensions per round (K)")
     ap.add_argument("--tree", type=int, default=100_000, help="tree nodes at the start of each round (N0)")
     ap.add_argument("--seed", type=int, default=1000)
-    ap.add_argument("--workload", default="blimp", choices=["blimp", "snake"],
-                    help="blimp = BASELINE config 2 (default); snake = config 3 (snake_trailers, 11 links, corridor)")
+    ap.add_argument("--workload", default="blimp", choices=["blimp", "blimp-room", "snake"],
+                    help="blimp = BASELINE config 2 (default); blimp-room = config 2 with every pose inside the room "
+                         "(collision-heavy); snake = config 3 (snake_trailers, 11 links, corridor)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample length")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--stage-every", type=int, default=8,
@@ -54,25 +63,66 @@ def parse():
                     help="config 5: this many independent blimp RRTs (seed_base + i) sharded over the ranks "
                          "(0 = config 2, one 100k-node tree per rank)")
     ap.add_argument("--seed-batch", type=int, default=4096, help="config 5: extensions per seed per round")
+    ap.add_argument("--seed-start", default="walls", choices=["walls", "centre"],
+                    help="config 5: start each seed near a wall of the room (default, so trees reach the walls "
+                         "and collide) or at the room's centre")
     ap.add_argument("--streams", type=int, default=32, help="config 5: HIP streams the seeds' rounds rotate over")
     ap.add_argument("--no-joint-nn", action="store_true",
-                    help="config 5: each seed queries its own tree (default: one joint NN launch per round, "
-                         "mpt_rrt_step_many)")
+                    help="config 5: each seed builds and queries its own tree (default: one joint build and one "
+                         "joint NN launch per round, mpt_rrt_step_many)")
     ap.add_argument("--joint-groups", type=int, default=1,
                     help="config 5: split the seeds into this many step_many groups, each on its own streams "
                          "and joint stream, so one group's NN launch overlaps another's build / collide")
     ap.add_argument("--launch-threads", type=int, default=1,
-                    help="config 5: host threads issuing the seeds' rounds (thread t drives streams t, t+T, ...)")
+                    help="config 5 with --no-joint-nn: host threads issuing the seeds' rounds")
     return ap.parse_args()
 
 
-def cpu_baseline(sc, tree, K_gpu, seed, target_s):
-    """The oracle (C port of the reference's FCL+FLANN semantics) on the host: the same
-    round on a bounded sample of extensions, 1 thread (the reference is single-threaded),
-    kd-tree NN built once per round (FLANN KDTreeSingleIndex-like), AABB-tree collision."""
+# ----------------------------------------------------------------------------- CPU baseline
+
+def cpu_cores():
+    """CPUs this job may use: the affinity set, capped by the cgroup CPU quota (the GPU box's
+    job gets a 16-CPU quota of a 256-CPU host; nproc there reports 16 via OMP_NUM_THREADS)."""
+    aff = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        q, p = open("/sys/fs/cgroup/cpu.max").read().split()
+        if q != "max":
+            quota = max(1, int(int(q) // int(p)))
+    except (OSError, ValueError):
+        pass
+    return (min(aff, quota) if quota else aff), {"affinity_cpus": aff, "cgroup_quota_cpus": quota,
+                                                 "host_cpus": os.cpu_count()}
+
+
+def _oracle_native():
+    """The oracle compiled for this host (-O3 -march=native) into a scratch directory; the
+    portable -O3 build if the compiler is missing."""
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import oracle as orc
 
+    out = os.path.join(os.environ.get("TMPDIR", "/tmp"), f"mpt_oracle_native_{os.getpid()}")
+    try:
+        path = orc.build_native(out)
+        orc.lib(path)
+        flags = "-O3 -march=native -ffp-contract=off -fopenmp"
+    except (OSError, subprocess.CalledProcessError):
+        orc.lib()
+        flags = "-O3 -ffp-contract=off -fopenmp (portable build; native build failed)"
+    return orc, flags
+
+
+def cpu_baseline(sc, tree, K_gpu, seed, target_s):
+    """The oracle (C restatement of the reference's FCL + FLANN semantics) on the host, timed
+    in the same run, three legs:
+      * all cores: the GPU's round on a bounded sample of its extensions (kd-tree NN built once
+        per round, AABB-tree + FCL tri-tri SAT collision), OpenMP over the extensions -- `value`;
+      * 1 core: the same sample single-threaded (the reference is single-threaded);
+      * FLANN 1.8.4 rebuild per insert: the reference's own loop, one extension at a time from
+        the same 100k-node tree, the kd-tree rebuilt after every insertion
+        (flannkdtreewrapper.hpp:35 addPoints -> buildIndex), 1 core."""
+    orc, flags = _oracle_native()
+    cores, core_info = cpu_cores()
     bvh = orc.BVH(sc.env_tris)
     n0 = tree.shape[0]
 
@@ -90,113 +140,28 @@ def cpu_baseline(sc, tree, K_gpu, seed, target_s):
     t_b, _ = run(1024, 1)
     per = max((t_b - t_a) / 768, 1e-7)
     fixed = max(t_a - 256 * per, 0.0)
-    K = int(min(max((target_s - fixed) / per, 256), K_gpu))
+    K = int(min(max((0.45 * target_s - fixed) / per, 256), K_gpu))
     t1, valid1 = run(K, 1)
-    threads = os.cpu_count() or 1
-    threads = min(threads, 16)
-    tn, validn = run(K, threads)
+    tn, validn = run(K, cores)
+    # the reference's sequential loop with FLANN 1.8.4's rebuild per insert, ~0.4 of the budget
+    nodes = np.zeros((n0 + 100_000, sc.dim))
+    nodes[:n0] = tree
+    par = np.zeros(nodes.shape[0], np.int32)
+    v_seq, tried, s_seq = orc.rrt_seq_rebuild(sc.kind, sc.prm, sc.ranges, sc.steer_dt, sc.cc_dt, seed, 0, bvh,
+                                              sc.env_tf, sc.agent_tris, nodes, par, n0, 100_000, 0.4 * target_s)
     return {
-        "value": valid1 / t1, "unit": "valid extensions/s", "cores": 1, "kind": "port",
+        "value": validn / tn, "unit": "valid extensions/s", "cores": cores, "kind": "port",
         "sample": f"{K} extensions of the same {sc.name} round ({n0}-node tree, kd-tree NN built per round, "
-                  f"AABB-tree + FCL tri-tri SAT), oracle/mpt_oracle.c, {t1:.2f} s",
-        "all_cores": {"value": validn / tn, "cores": threads, "seconds": round(tn, 3)},
-        "cpu": _cpu_model(),
+                  f"AABB-tree + FCL tri-tri SAT), oracle/mpt_oracle.c, OpenMP over {cores} cores, {tn:.2f} s",
+        "compile_flags": flags,
+        "cpu": _cpu_model(), **core_info,
+        "single_core": {"value": valid1 / t1, "cores": 1, "seconds": round(t1, 3)},
+        "flann_rebuild_per_insert": {
+            "value": v_seq / s_seq if s_seq > 0 else None, "cores": 1, "extensions": tried, "valid": v_seq,
+            "seconds": round(s_seq, 3),
+            "note": f"the reference's one-at-a-time loop from the same {n0}-node tree with a full kd-tree "
+                    "rebuild after every insertion (FLANN 1.8.4 addPoints, flannkdtreewrapper.hpp:35)"},
     }
-
-
-# Stage -> the kernel that does its work (kernel names as rocprofv3 reports them).
-STAGE_KERNEL = {"nn_query": "k_grid_nn1_runs", "collide_pairs": "k_pairs", "collide_cands": "k_cands",
-                "collide_narrow": "k_narrow", "nn_build": "k_grid_scatter", "steer": "k_steer",
-                "sample": "k_sample", "append": "k_append"}
-
-
-def stage_bytes(stage, c, K, n0, d, pmax, nn_mode="grid"):
-    """Algorithmic bytes one launch of the stage must touch (DESIGN.md "Measurement"): the
-    inputs it reads and outputs it writes, each counted once per use, from the counters
-    of the round (c = RRTEngine.collide_stats)."""
-    if stage == "nn_query":  # queries + results + examined points (coords, id) + cell ranges
-        # grid: a cell's (start, count) pair; tree: a box's float lo / hi over d dims
-        per_cell = 8 * d if nn_mode == "tree" else 8
-        return K * (8 * d + 12) + c["nn_points"] * (8 * d + 4) + c["nn_cells"] * per_cell
-    if stage == "collide_pairs":  # poses, cluster records, env tree items tested, pair words
-        return c["units"] * 96 + c["cluster_threads"] * 64 + c["node_tests"] * 32 + c["pair_tests"] * 4
-    if stage == "collide_cands":  # per header: header, pose, 64 agent triangles; pairs; candidates
-        return c["cluster_transforms"] * (32 + 96 + 64 * 72) + c["pair_tests"] * (4 + 32) + c["candidates"] * 12
-    if stage == "collide_narrow":  # per candidate: itself, pose, agent triangle, env triangle record
-        return c["candidates"] * (12 + 96 + 72 + 384)
-    if stage == "nn_build":  # read the tree, write it in cell order with ids, cell counts
-        return n0 * (2 * 8 * d + 12)
-    if stage == "steer":  # nn id, tree node, end state, poses
-        return K * (4 + 16 * d + 96 * pmax + 4)
-    if stage == "sample":
-        return K * 8 * d
-    if stage == "append":
-        return K * (1 + 8 * d + 4) * 2
-    return None
-
-
-NN_KERNEL = {"grid": "k_grid_nn1_runs", "tree": "k_tree_nn1", "brute": "k_knn1"}
-
-
-def roofline(per_launch, cst, K, n0, d, pmax, nn_mode, traffic_path):
-    """Roofline of the round's dominant kernel: achieved = its algorithmic bytes per launch
-    / its hipEvent-measured duration (per-stage events on the engine's stream); every
-    stage's figure is listed under `stages`."""
-    stages = {}
-    kernels = dict(STAGE_KERNEL, nn_query=NN_KERNEL.get(nn_mode, STAGE_KERNEL["nn_query"]))
-    if nn_mode == "grid":  # the instantiation (its PMC row): the XCD-slab variant for d >= 15
-        kernels["nn_query"] = f"k_grid_nn1_runs_xcd<{d}," if d >= 15 else f"k_grid_nn1_runs<{d},"
-    if nn_mode == "tree":
-        kernels["nn_build"] = "k_pt_gather"
-    for s in kernels:
-        ms = per_launch.get(s, 0.0)
-        b = stage_bytes(s, cst, K, n0, d, pmax, nn_mode)
-        if ms <= 0 or b is None:
-            continue
-        gbs = b / (ms * 1e-3) / 1e9
-        stages[s] = {"kernel": kernels[s], "ms": round(ms, 4), "bytes": int(b), "achieved_gbs": round(gbs, 1),
-                     "frac": round(gbs / HBM_PEAK_GBS, 4)}
-        t = pmc_traffic(traffic_path, kernels[s])
-        if t is not None:  # measured HBM bytes per launch (rocprofv3 PMC) over the same time
-            stages[s]["traffic"] = t
-            stages[s]["traffic_gbs"] = round(t / (ms * 1e-3) / 1e9, 1)
-    if not stages:  # no stage timing recorded (--stage-every 0)
-        return {"bound": "hbm", "achieved": None, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": None,
-                "traffic": None, "stages": {}, "work_per_round": cst}
-    dominant = max(stages, key=lambda s: stages[s]["ms"])
-    st = stages[dominant]
-    traffic = pmc_traffic(traffic_path, st["kernel"])
-    # achieved counts algorithmic bytes (SURVEY 8(d)), which caches (LDS, L2, MALL) may serve;
-    # traffic_gbs is the measured HBM rate of the same launches, the honest distance to the roof
-    out = {"bound": "hbm", "achieved": st["achieved_gbs"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
-           "frac": st["frac"], "traffic": traffic,
-           "traffic_gbs": st.get("traffic_gbs"), "kernel": st["kernel"], "stage": dominant,
-           "ms_per_launch": st["ms"], "algorithmic_bytes": st["bytes"], "stages": stages, "work_per_round": cst}
-    if dominant == "nn_query" and nn_mode == "brute":
-        flops = float(K) * n0 * 3 * d  # SURVEY 8(d): 3*d*N FP64 ops per query (sub, mul, add)
-        tf = flops / (st["ms"] * 1e-3) / 1e12
-        out.update({"bound": "mfma", "achieved": round(tf, 3), "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
-                    "frac": round(tf / FP64_PEAK_TFLOPS, 4), "kernel": "k_knn1",
-                    "note": "FP64 VALU (FLANN's L2 op order is not a dot product, so no MFMA)"})
-    return out
-
-
-def pmc_traffic(path, kernel):
-    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary
-    (scripts/profile.sh + scripts/pmc_summary.py), or None."""
-    if not path:
-        import glob
-
-        cands = sorted(glob.glob(os.path.join(REPO, "profiles", "r*", "pmc_summary.json")))
-        path = cands[-1] if cands else None
-    try:
-        summ = json.load(open(path))
-    except (OSError, ValueError, TypeError):
-        return None
-    for name, v in summ.items():
-        if kernel in name:
-            return v["hbm_bytes_per_launch"]
-    return None
 
 
 def _cpu_model():
@@ -209,34 +174,210 @@ def _cpu_model():
     return "unknown"
 
 
+# ----------------------------------------------------------------------------- roofline
+
+# Stage -> the kernel that does its work (names as rocprofv3 reports them).
+STAGE_KERNEL = {"nn_query": "k_grid_nn1_runs", "collide_pairs": "k_pairs", "collide_cands": "k_cands",
+                "collide_narrow": "k_narrow", "nn_build": "k_grid_scatter", "steer": "k_steer",
+                "sample": "k_sample", "append": "k_append"}
+NN_KERNEL = {"grid": "k_grid_nn1_runs", "tree": "k_tree_nn1", "brute": "k_knn1"}
+
+
+def geometry(sc, env):
+    """Sizes the compulsory-byte model needs: env / agent triangles, agent clusters (<= 64
+    triangles each, mpt_agent_create), env tree items (one per triangle + buckets of <= 16)."""
+    te = int(env.info()["triangles"])
+    ta = int(sc.agent_tris.shape[0])
+    return {"env_tris": te, "agent_tris": ta, "clusters": max(1, -(-ta // 64)), "env_items": te + -(-te // 8)}
+
+
+def compulsory_bytes(stage, c, K, n0, d, pmax, geo, nn_mode):
+    """Every input and output of one launch of the stage counted once (the HBM minimum);
+    c = RRTEngine.collide_stats of one round."""
+    rec = 8 * (d + 1) if d < 8 else 8 * d + 4  # grid point record (+ id)
+    live = c["cluster_threads"] / geo["clusters"]  # (pose, link) units past k_steer's object cull
+    if stage == "sample":
+        return K * 8 * d
+    if stage == "nn_build":
+        if nn_mode == "tree":  # read the nodes; codes, ids, sorted points, boxes
+            return n0 * (8 * d + 8 + 8 * d + 4) + (n0 // 7) * 8 * d
+        return n0 * (8 * d + rec + 8) + (n0 // 2) * 12  # nodes in, records out, cell ids, counts / starts
+    if stage == "nn_query":
+        index = n0 * rec + (n0 // 2) * 4 if nn_mode == "grid" else n0 * (8 * d + 4) + (n0 // 7) * 8 * d
+        return K * (8 * d + 12) + index
+    if stage == "steer":  # ids, neighbour rows, end states, poses, counts, verdict init, live list
+        return K * (4 + 8 * d + 8 * d + 4 + 1) + K * pmax * 96 + live * 4
+    if stage == "collide_pairs":  # live poses, clusters, env tree, pair words, headers
+        return live * 96 + geo["clusters"] * 64 + geo["env_items"] * 32 + c["pair_tests"] * 4 + c["cluster_transforms"] * 32
+    if stage == "collide_cands":  # headers, pair words, poses, agent triangles, env boxes, candidates
+        return (c["cluster_transforms"] * 32 + c["pair_tests"] * 4 + live * 96 + geo["agent_tris"] * 72
+                + geo["env_items"] * 32 + c["candidates"] * 12)
+    if stage == "collide_narrow":  # candidates, poses, agent triangles, env records, verdicts
+        return c["candidates"] * 12 + live * 96 + geo["agent_tris"] * 72 + geo["env_tris"] * 384 + K
+    if stage == "append":
+        return K * (1 + 8 * d + 4) * 2
+    return None
+
+
+def fp64_flops(stage, c, geo):
+    """FP64 work of the collision stages by SURVEY §8(d): 54 flops per agent triangle mapped
+    (Q' = R Q + T), 750 per exact triangle-pair test, + the relative transform and box of a
+    (unit, cluster) thread (~81)."""
+    if stage == "collide_narrow":
+        return 54.0 * c["candidates"] + 750.0 * c["tri_tests"]
+    if stage == "collide_cands":
+        return 54.0 * c["cluster_transforms"] * geo["agent_tris"] / geo["clusters"]
+    if stage == "collide_pairs":
+        return 81.0 * c["cluster_threads"]
+    return None
+
+
+def lds_bytes(stage, c, geo):
+    """k_pairs reads every env tree item it tests from LDS (32 B) after each workgroup stages
+    the tree (env_items * 32 B per 256-thread workgroup)."""
+    if stage != "collide_pairs":
+        return None
+    return c["node_tests"] * 32.0 + (c["cluster_threads"] / 256.0) * geo["env_items"] * 32.0
+
+
+def touched_bytes(stage, c, K, n0, d, pmax):
+    """Bytes the stage touches through any level of the hierarchy (round 1's figure, kept
+    for reference: examined points, tested tree items, candidate records)."""
+    if stage == "nn_query":
+        return K * (8 * d + 12) + c["nn_points"] * (8 * d + 4) + c["nn_cells"] * 8
+    if stage == "collide_pairs":
+        return c["units"] * 96 + c["cluster_threads"] * 64 + c["node_tests"] * 32 + c["pair_tests"] * 4
+    if stage == "collide_cands":
+        return c["cluster_transforms"] * (32 + 96 + 64 * 72) + c["pair_tests"] * (4 + 32) + c["candidates"] * 12
+    if stage == "collide_narrow":
+        return c["candidates"] * (12 + 96 + 72 + 384)
+    return None
+
+
+def pmc_summary(path):
+    if not path:
+        import glob
+
+        cands = sorted(glob.glob(os.path.join(REPO, "profiles", "r*", "pmc_summary.json")))
+        path = cands[-1] if cands else None
+    try:
+        return json.load(open(path)), os.path.relpath(path, REPO)
+    except (OSError, ValueError, TypeError):
+        return {}, None
+
+
+def pmc_traffic(summ, kernel):
+    """Measured HBM bytes per launch of `kernel`: (2 * FETCH_SIZE + WRITE_SIZE) * 1024 from the
+    committed rocprofv3 PMC summary (scripts/profile.sh + scripts/pmc_summary.py)."""
+    for name, v in summ.items():
+        if kernel in name:
+            return v["hbm_bytes_per_launch"]
+    return None
+
+
+def stage_table(per_launch, cst, K, n0, d, pmax, geo, nn_mode, kernels, summ):
+    stages = {}
+    for s, kern in kernels.items():
+        ms = per_launch.get(s, 0.0)
+        b = compulsory_bytes(s, cst, K, n0, d, pmax, geo, nn_mode)
+        if ms <= 0 or b is None:
+            continue
+        t = ms * 1e-3
+        st = {"kernel": kern, "ms": round(ms, 4), "compulsory_bytes": int(b),
+              "compulsory_gbs": round(b / t / 1e9, 1), "frac_hbm_compulsory": round(b / t / 1e9 / HBM_PEAK_GBS, 4)}
+        tr = pmc_traffic(summ, kern)
+        if tr is not None:
+            st.update({"traffic": int(tr), "traffic_gbs": round(tr / t / 1e9, 1),
+                       "frac_hbm_measured": round(tr / t / 1e9 / HBM_PEAK_GBS, 4),
+                       "traffic_over_compulsory": round(tr / b, 2)})
+        f = fp64_flops(s, cst, geo)
+        if f is not None:
+            st.update({"fp64_tflops": round(f / t / 1e12, 3), "frac_fp64": round(f / t / 1e12 / FP64_PEAK_TFLOPS, 4)})
+        lb = lds_bytes(s, cst, geo)
+        if lb is not None:
+            st.update({"lds_gbs": round(lb / t / 1e9, 1), "frac_lds": round(lb / t / 1e9 / LDS_PEAK_GBS, 4)})
+        tb = touched_bytes(s, cst, K, n0, d, pmax)
+        if tb is not None:
+            st["touched_bytes"] = int(tb)
+        stages[s] = st
+    return stages
+
+
+def roofline_of(stages, dominant, work, summ_path):
+    """The contract's roofline object for the dominant stage: HBM-bound unless its FP64
+    fraction is the larger one (then `mfma` = the FP64 VALU roof; no MFMA: FCL's operation
+    order is scalar FP64)."""
+    if not stages or dominant not in stages:
+        return {"bound": "hbm", "achieved": None, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": None, "traffic": None,
+                "stages": stages, "work_per_round": work}
+    st = stages[dominant]
+    out = {"bound": "hbm", "achieved": st["compulsory_gbs"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
+           "frac": st["frac_hbm_compulsory"], "traffic": st.get("traffic"), "traffic_gbs": st.get("traffic_gbs"),
+           "frac_hbm_measured": st.get("frac_hbm_measured"), "traffic_over_compulsory": st.get("traffic_over_compulsory"),
+           "kernel": st["kernel"], "stage": dominant, "ms_per_launch": st["ms"],
+           "algorithmic_bytes": st["compulsory_bytes"], "pmc_source": summ_path}
+    if st.get("frac_fp64", 0.0) > max(st["frac_hbm_compulsory"], st.get("frac_hbm_measured") or 0.0):
+        out.update({"bound": "mfma", "achieved": st["fp64_tflops"], "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
+                    "frac": st["frac_fp64"], "note": "FP64 VALU roof (FCL's scalar operation order; no MFMA)"})
+    out["definition"] = ("achieved = compulsory bytes (each input and output of the launch once) / hipEvent time; "
+                         "traffic = measured HBM bytes per launch (2*FETCH_SIZE + WRITE_SIZE, rocprofv3); "
+                         "per-stage FP64 and LDS fractions under stages")
+    out["stages"] = stages
+    out["work_per_round"] = work
+    return out
+
+
+# ----------------------------------------------------------------------------- config 5
+
+def seed_start(seed, env, agent, mpt, where):
+    """Config 5 start state of a seed: at rest, collision-free, either at the room's centre or
+    (default) 5.5-10 units from one of the room's four side walls (so the tree reaches walls
+    within a few rounds and extensions collide); deterministic per seed."""
+    if where == "centre":
+        return np.array([[88.6, 68.9, 57.1, 0.0, 0.0, 0.0, 0.0]])
+    rng = np.random.default_rng(seed)
+    lo, hi = np.array([0.0, 0.0, 0.0]), np.array([177.16, 137.80, 114.17])
+    for _ in range(64):
+        p = rng.uniform(lo + 12, hi - 12)
+        wall, dist = int(rng.integers(4)), rng.uniform(5.5, 10.0)
+        if wall == 0:
+            p[0] = lo[0] + dist
+        elif wall == 1:
+            p[0] = hi[0] - dist
+        elif wall == 2:
+            p[1] = lo[1] + dist
+        else:
+            p[1] = hi[1] - dist
+        th = rng.uniform(0, 2 * np.pi)
+        pose = np.r_[np.cos(th), np.sin(th), 0, -np.sin(th), np.cos(th), 0, 0, 0, 1, p].reshape(1, 1, 12)
+        if mpt.collide_batch(env, [agent], pose, np.array([0, 1]))[0] == 0:
+            return np.array([[p[0], p[1], p[2], th, 0.0, 0.0, 0.0]])
+    return np.array([[88.6, 68.9, 57.1, 0.0, 0.0, 0.0, 0.0]])
+
+
 def run_seeds(args, world, rank, dist, torch, mpt, multiseed, scenes):
     """BASELINE config 5: `args.seeds` independent blimp RRTs, each its own engine and tree grown
-    from the blimp start state, `args.seed_batch` extensions per seed per round; rank r runs
-    the contiguous shard multiseed.shard_seeds(seeds, world, r).  Total work is fixed as the
-    GPU count grows (strong scaling).  A seed's tree depends only on its seed (counter-based
-    RNG), so the digest of all trees is the same at every GPU count."""
+    from its start state, `args.seed_batch` extensions per seed per round; rank r runs the
+    contiguous shard multiseed.shard_seeds(seeds, world, r).  Total work is fixed as the GPU
+    count grows (strong scaling).  A seed's tree depends only on its seed (counter-based RNG),
+    so the digest of all trees is the same at every GPU count."""
     sc = scenes.blimp_scenario("all")
     env = mpt.Environment(sc.env_tris, sc.env_tf)
     agent = mpt.AgentMesh(sc.agent_tris)
     mine = list(multiseed.shard_seeds(args.seeds, world, rank))
     K = args.seed_batch
     rounds = args.warmup + args.steps
-    # collision-free start at rest in the middle of the room (model.dae spans (0,0,0)-(177,138,114);
-    # blimp.inst's start (0,0,0) is the room's corner, inside its walls)
-    start = np.array([[88.6, 68.9, 57.1, 0.0, 0.0, 0.0, 0.0]])
     engines = []
     for i in mine:
         e = mpt.RRTEngine(env, agent, sc.kind, sc.prm, sc.ranges, sc.steer_dt, sc.cc_dt, 1 + (rounds + 2) * K,
                           args.seed + i)
-        e.add_nodes(start)
+        e.add_nodes(seed_start(args.seed + i, env, agent, mpt, args.seed_start))
         e.set_nn(args.nn, args.ppc)
         engines.append(e)
     streams = [torch.cuda.Stream() for _ in range(max(1, min(args.streams, len(engines))))]
     if engines:
         engines[0].enable_timing(True)
 
-    # a seed round is ~25 small launches, so 256 seeds from one host thread are launch-bound;
-    # T threads each drive the engines of streams t, t + T, ... (ctypes drops the GIL)
     T = max(1, min(args.launch_threads, len(streams)))
     groups = [[(e, streams[j % len(streams)]) for j, e in enumerate(engines) if (j % len(streams)) % T == t]
               for t in range(T)]
@@ -252,9 +393,8 @@ def run_seeds(args, world, rank, dist, torch, mpt, multiseed, scenes):
         dev = torch.cuda.current_device()
         pool = ThreadPoolExecutor(T, initializer=torch.cuda.set_device, initargs=(dev,))
 
-    joint = torch.cuda.Stream()
-    eng_streams = [streams[j % len(streams)] for j in range(len(engines))]
-    # groups: contiguous slices of engines, group g on streams [g*S/G, (g+1)*S/G) + its own joint stream
+    # step_many groups: contiguous slices of engines, group g on streams [g*S/G, (g+1)*S/G) and
+    # its own joint stream (the joint job tables belong to the joint stream)
     G = max(1, min(args.joint_groups, len(streams), len(engines)))
     gsz = -(-len(engines) // G)
     spg = max(1, len(streams) // G)
@@ -263,7 +403,7 @@ def run_seeds(args, world, rank, dist, torch, mpt, multiseed, scenes):
         eg = engines[g * gsz:(g + 1) * gsz]
         sg = streams[g * spg:(g + 1) * spg]
         if eg:
-            jgroups.append((eg, [sg[j % len(sg)] for j in range(len(eg))], joint if g == 0 else torch.cuda.Stream()))
+            jgroups.append((eg, [sg[j % len(sg)] for j in range(len(eg))], torch.cuda.Stream()))
 
     def round_():
         if not args.no_joint_nn:
@@ -279,7 +419,6 @@ def run_seeds(args, world, rank, dist, torch, mpt, multiseed, scenes):
         round_()
     torch.cuda.synchronize()
     c0 = [e.counters() for e in engines]
-    ktimes = {}
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
@@ -301,48 +440,63 @@ def run_seeds(args, world, rank, dist, torch, mpt, multiseed, scenes):
     digests = multiseed.gather_digests(dist, digests)
     if rank != 0:
         return None
-    # seed 0's engine: one more round with stage timing and work counters, outside the timed region
+    summ, summ_path = pmc_summary(args.traffic)
+    geo = geometry(sc, env)
     e0 = engines[0]
     n_before = e0.counters()["nodes"]
+    pmax = e0.info()["pmax"]
     if args.no_joint_nn:
         e0.collide_stats(True)
         e0.step(K, streams[0])
         torch.cuda.synchronize()
         cst = e0.collide_stats(False)
         per_launch = e0.kernel_times()
-        roof = roofline(per_launch, cst, K, n_before, sc.dim, e0.info()["pmax"], e0.last_nn(), args.traffic)
+        nn_mode = e0.last_nn()
+        kernels = dict(STAGE_KERNEL, nn_query=NN_KERNEL.get(nn_mode, "k_grid_nn1_runs"))
+        if nn_mode == "tree":
+            kernels["nn_build"] = "k_pt_gather"
+        stages = stage_table(per_launch, cst, K, n_before, sc.dim, pmax, geo, nn_mode, kernels, summ)
+        roof = roofline_of(stages, max(stages, key=lambda s: stages[s]["ms"]) if stages else None, cst, summ_path)
     else:
-        # all seeds: one round with work counters on (summed for the joint launch's bytes), then
-        # one with them off and the joint NN launch timed by hipEvents on its stream
-        for e in engines:
+        # all seeds: one round with work counters on (summed for the joint launches' bytes), then
+        # one with them off and the joint build + NN launches timed by hipEvents on group 0's
+        # joint stream; engine 0's own stages for the per-seed kernels
+        eg0, ss0, js0 = jgroups[0]
+        for e in eg0:
             e.collide_stats(True)
-        mpt.step_many(engines, K, eng_streams, joint)
+        mpt.step_many(eg0, K, ss0, js0)
         torch.cuda.synchronize()
-        csts = [e.collide_stats(False) for e in engines]
-        mpt.step_many(engines, K, eng_streams, joint)
+        csts = [e.collide_stats(False) for e in eg0]
+        mpt.step_many(eg0, K, ss0, js0)
         torch.cuda.synchronize()
-        jms = mpt.joint_nn_ms()
+        jt = mpt.joint_times(js0)
         cst = csts[0]
         per_launch = dict(e0.kernel_times())
-        nn_bytes = sum(stage_bytes("nn_query", c, K, n_before, sc.dim, e0.info()["pmax"], "tree") for c in csts)
+        n_tot = sum(e.counters()["nodes"] for e in eg0) - len(eg0) * K  # nodes before the timed call (upper bound)
         per_launch.pop("nn_query", None)
-        roof = roofline(per_launch, cst, K, n_before, sc.dim, e0.info()["pmax"], e0.last_nn(), args.traffic)
-        gbs = nn_bytes / (jms * 1e-3) / 1e9
-        nn = {"kernel": "k_tree_nn1_jobs<7,", "ms": round(jms, 4), "bytes": int(nn_bytes),
-              "achieved_gbs": round(gbs, 1), "frac": round(gbs / HBM_PEAK_GBS, 4),
-              "launch": f"one launch for all {len(engines)} seeds' {K} queries"}
-        t = pmc_traffic(args.traffic, nn["kernel"])
-        if t is not None:
-            nn["traffic"], nn["traffic_gbs"] = t, round(t / (jms * 1e-3) / 1e9, 1)
-        roof["stages"]["nn_query"] = nn
-        roof.update({"achieved": nn["achieved_gbs"], "frac": nn["frac"], "traffic": nn.get("traffic"),
-                     "traffic_gbs": nn.get("traffic_gbs"), "kernel": nn["kernel"], "stage": "nn_query",
-                     "ms_per_launch": nn["ms"], "algorithmic_bytes": nn["bytes"],
-                     "work_nn_all_seeds": {"nn_points": sum(c["nn_points"] for c in csts),
-                                           "nn_boxes": sum(c["nn_cells"] for c in csts)}})
+        per_launch.pop("nn_build", None)
+        kernels = {s: k for s, k in STAGE_KERNEL.items() if s not in ("nn_query", "nn_build")}
+        stages = stage_table(per_launch, cst, K, n_before, sc.dim, pmax, geo, "tree", kernels, summ)
+        nj = len(eg0)
+        work_nn = {k: sum(c[k] for c in csts) for k in ("nn_points", "nn_cells")}
+        agg = dict(cst, **work_nn)
+        for s, kern, ms in (("nn_build", "k_pt_bbox_jobs", jt["build"]), ("nn_query", "k_tree_nn1_jobs<7,", jt["nn"])):
+            b = compulsory_bytes(s, agg, K * nj, max(n_tot, 1), sc.dim, pmax, geo, "tree")
+            t = ms * 1e-3
+            st = {"kernel": kern, "ms": round(ms, 4), "compulsory_bytes": int(b),
+                  "compulsory_gbs": round(b / t / 1e9, 1), "frac_hbm_compulsory": round(b / t / 1e9 / HBM_PEAK_GBS, 4),
+                  "launch": f"one joint launch{' chain' if s == 'nn_build' else ''} for {nj} seeds' {K} queries"}
+            tr = pmc_traffic(summ, kern)
+            if tr is not None:
+                st.update({"traffic": int(tr), "traffic_gbs": round(tr / t / 1e9, 1),
+                           "frac_hbm_measured": round(tr / t / 1e9 / HBM_PEAK_GBS, 4),
+                           "traffic_over_compulsory": round(tr / b, 2)})
+            stages[s] = st
+        roof = roofline_of(stages, "nn_query", dict(cst, work_nn_all_seeds=work_nn), summ_path)
     import hashlib
 
     all_digest = hashlib.sha256("".join(digests[i] for i in sorted(digests)).encode()).hexdigest()
+    n_local = len(mine)
     return {
         "metric": "valid RRT edge extensions/sec (collision+NN) per node, 1/2/4/8 MI355X",
         "value": valid / elapsed,
@@ -357,18 +511,21 @@ def run_seeds(args, world, rank, dist, torch, mpt, multiseed, scenes):
         "dtype": "f64",
         "data": "synthetic (uniform samples over Blimp::getStateVarRanges; meshes from the reference)",
         "config": {"workload": f"config 5: {args.seeds} independent blimp RRTs (1355-tri blimp vs model.dae) "
-                               f"grown from the start state, {K} extensions per seed per round",
-                   "seeds": args.seeds, "seed_base": args.seed, "extensions_per_seed_round": K,
-                   "rounds_before_timing": args.warmup, "streams_per_gpu": len(streams), "launch_threads": T,
-                   "joint_nn": not args.no_joint_nn, "joint_groups": G,
+                               f"grown from per-seed starts ({args.seed_start}), {K} extensions per seed per round",
+                   "seeds": args.seeds, "seeds_per_gpu": n_local, "seed_base": args.seed,
+                   "extensions_per_seed_round": K, "rounds_before_timing": args.warmup,
+                   "streams_per_gpu": len(streams), "joint_nn": not args.no_joint_nn, "joint_groups": G,
                    "parallelism": f"seeds sharded over {world} GPU(s)"},
         "checked_per_s": checked / elapsed,
         "valid_fraction": valid / max(checked, 1),
+        "per_seed_valid_per_s": valid / elapsed / max(args.seeds, 1),
         "seeds_digest": all_digest,
         "roofline": roof,
         "cpu_baseline": None,
     }
 
+
+# ----------------------------------------------------------------------------- main
 
 def main():
     args = parse()
@@ -401,6 +558,10 @@ def main():
         sc = scenes.snake_scenario("corridor")
         workload = (f"snake.inst: snake_trailers ({sc.links} unit-box links, T=10) in the synthetic corridor "
                     f"({sc.env_tris.shape[0]} tris), batched RRT round over a {args.tree}-node tree")
+    elif args.workload == "blimp-room":
+        sc = scenes.blimp_room_scenario()
+        workload = ("blimp.inst: blimp (1355 tris) vs single-room env (model.dae, 316 tris), tree and samples inside "
+                    f"the room's box (collision-heavy variant), batched RRT round over a {args.tree}-node tree")
     else:
         sc = scenes.blimp_scenario("all")
         workload = ("blimp.inst: blimp (1355 tris) vs single-room env (model.dae, 316 tris), "
@@ -451,15 +612,25 @@ def main():
         return
 
     steps = args.steps
-    # hipEvents on the launch stream, recorded every timed round into the engine's event ring
-    # and read only now (no host sync inside the timed region)
+    # hipEvents on the launch stream, recorded every n-th timed round into the engine's event
+    # ring and read only now (no host sync inside the timed region)
     ktimes, kt_rounds = eng.kernel_times_sum()
     per_launch = {k: v / max(kt_rounds, 1) for k, v in ktimes.items()}
     # one more round, outside the timed region, with the collision work counters on
     eng.collide_stats(True)
     round_()
     cst = eng.collide_stats(False)
-    roof = roofline(per_launch, cst, K, n0, sc.dim, eng.info()["pmax"], eng.last_nn(), args.traffic)
+    nn_mode = eng.last_nn()
+    d = sc.dim
+    kernels = dict(STAGE_KERNEL, nn_query=NN_KERNEL.get(nn_mode, "k_grid_nn1_runs"))
+    if nn_mode == "grid":  # the instantiation (its PMC row): the XCD-slab variant for d >= 15
+        kernels["nn_query"] = f"k_grid_nn1_runs_xcd<{d}," if d >= 15 else f"k_grid_nn1_runs<{d},"
+    if nn_mode == "tree":
+        kernels["nn_build"] = "k_pt_gather"
+    summ, summ_path = pmc_summary(args.traffic)
+    stages = stage_table(per_launch, cst, K, n0, d, eng.info()["pmax"], geometry(sc, env), nn_mode, kernels, summ)
+    dominant = max(stages, key=lambda s: stages[s]["ms"]) if stages else None
+    roof = roofline_of(stages, dominant, cst, summ_path)
 
     out = {
         "metric": "valid RRT edge extensions/sec (collision+NN) per node, 1/2/4/8 MI355X",

@@ -332,28 +332,31 @@ void walk3ds(const std::string &d, size_t off, size_t end, std::vector<std::stri
                 walk3ds(d, nx, cend, mats, objs, &objs.back());
                 break;
             }
+            // counts are clamped to what the chunk holds (a damaged file reads no further than
+            // its chunk; sanitize_host.cpp feeds truncated and flipped files)
             case 0x4110:
-                if (cur) {
-                    const uint16_t n = rd16(d, body);
-                    cur->verts.resize(3 * (size_t)n);
-                    std::memcpy(cur->verts.data(), d.data() + body + 2, sizeof(float) * 3 * n);
+                if (cur && body + 2 <= cend) {
+                    const size_t n = std::min<size_t>(rd16(d, body), (cend - body - 2) / 12);
+                    cur->verts.resize(3 * n);
+                    if (n) std::memcpy(cur->verts.data(), d.data() + body + 2, sizeof(float) * 3 * n);
                 }
                 break;
             case 0x4120:
-                if (cur) {
-                    const uint16_t n = rd16(d, body);
-                    cur->faces.resize(3 * (size_t)n);
-                    for (uint16_t f = 0; f < n; ++f)
+                if (cur && body + 2 <= cend) {
+                    const size_t n = std::min<size_t>(rd16(d, body), (cend - body - 2) / 8);
+                    cur->faces.resize(3 * n);
+                    for (size_t f = 0; f < n; ++f)
                         for (int k = 0; k < 3; ++k) cur->faces[3 * f + k] = rd16(d, body + 2 + 8 * f + 2 * k);
-                    walk3ds(d, body + 2 + 8 * (size_t)n, cend, mats, objs, cur);
+                    walk3ds(d, body + 2 + 8 * n, cend, mats, objs, cur);
                 }
                 break;
             case 0x4130:
                 if (cur) {
                     std::string name = rdstr(d, body, cend, nx);
-                    const uint16_t n = rd16(d, nx);
+                    if (nx + 2 > cend) break;
+                    const size_t n = std::min<size_t>(rd16(d, nx), (cend - nx - 2) / 2);
                     std::vector<uint16_t> fl(n);
-                    for (uint16_t f = 0; f < n; ++f) fl[f] = rd16(d, nx + 2 + 2 * f);
+                    for (size_t f = 0; f < n; ++f) fl[f] = rd16(d, nx + 2 + 2 * f);
                     cur->mats.emplace_back(name, std::move(fl));
                 }
                 break;
@@ -384,9 +387,11 @@ MeshFile load_3ds(const std::string &d) {
             sm.name = mi < mats.size() ? mats[mi] : "DefaultMaterial";
             for (size_t f = 0; f < nf; ++f) {
                 if (fmat[f] != mi) continue;
+                bool inside = true;  // a face naming a missing vertex (damaged file) is dropped whole
+                for (int k = 0; k < 3; ++k) inside = inside && 3 * (size_t)o.faces[3 * f + k] + 2 < o.verts.size();
+                if (!inside) continue;
                 for (int k = 0; k < 3; ++k) {
                     const size_t v = o.faces[3 * f + k];
-                    if (3 * v + 2 >= o.verts.size()) continue;
                     for (int c = 0; c < 3; ++c) sm.tris.push_back((double)o.verts[3 * v + c]);
                 }
             }

@@ -16,6 +16,7 @@
 #include <math.h>
 #include <stdlib.h>
 #include <string.h>
+#include <time.h>
 #ifdef _OPENMP
 #include <omp.h>
 #endif
@@ -439,14 +440,38 @@ struct orc_kdtree {
     int64_t *a, *b; /* inner: left,right ; leaf: first,count */
 };
 
-static const double *g_kd_pts;
-static int32_t g_kd_d, g_kd_dim;
-static int idx_cmp(const void *x, const void *y) {
-    const int64_t i = *(const int64_t *)x, j = *(const int64_t *)y;
-    const double a = g_kd_pts[i * g_kd_d + g_kd_dim], b = g_kd_pts[j * g_kd_d + g_kd_dim];
-    if (a < b) return -1;
-    if (a > b) return 1;
-    return (i < j) ? -1 : (i > j);
+/* (value along dim, index) total order of two points */
+static inline int kd_less(const double *src, int32_t d, int32_t dim, int64_t i, int64_t j) {
+    const double a = src[i * d + dim], b = src[j * d + dim];
+    return a < b || (a == b && i < j);
+}
+
+/* Quickselect: idx[first, first + n) reordered so that position h holds the h-th smallest
+ * point in (value, index) order, smaller ones before it, larger ones after (the median split
+ * in O(n), as FLANN's KDTreeSingleIndex::divideTree partitions instead of sorting). */
+static void kd_select(int64_t *idx, int64_t first, int64_t n, int64_t h, const double *src, int32_t d, int32_t dim) {
+    int64_t lo = first, hi = first + n - 1;
+    const int64_t k = first + h;
+    while (hi > lo) {
+        /* median of three as the pivot */
+        const int64_t mid = lo + (hi - lo) / 2;
+        if (kd_less(src, d, dim, idx[mid], idx[lo])) { int64_t s = idx[mid]; idx[mid] = idx[lo]; idx[lo] = s; }
+        if (kd_less(src, d, dim, idx[hi], idx[lo])) { int64_t s = idx[hi]; idx[hi] = idx[lo]; idx[lo] = s; }
+        if (kd_less(src, d, dim, idx[hi], idx[mid])) { int64_t s = idx[hi]; idx[hi] = idx[mid]; idx[mid] = s; }
+        const int64_t pv = idx[mid];
+        int64_t i = lo, j = hi;
+        while (i <= j) {
+            while (kd_less(src, d, dim, idx[i], pv)) ++i;
+            while (kd_less(src, d, dim, pv, idx[j])) --j;
+            if (i <= j) {
+                const int64_t s = idx[i]; idx[i] = idx[j]; idx[j] = s;
+                ++i; --j;
+            }
+        }
+        if (k <= j) hi = j;
+        else if (k >= i) lo = i;
+        else return;
+    }
 }
 
 static int64_t kd_rec(orc_kdtree *t, int64_t *idx, int64_t first, int64_t n, const double *src) {
@@ -467,9 +492,8 @@ static int64_t kd_rec(orc_kdtree *t, int64_t *idx, int64_t first, int64_t n, con
         }
         if (hi - lo > bw) { bw = hi - lo; best = k; }
     }
-    g_kd_pts = src; g_kd_d = t->d; g_kd_dim = best;
-    qsort(idx + first, (size_t)n, sizeof(int64_t), idx_cmp);
     const int64_t h = n / 2;
+    kd_select(idx, first, n, h, src, t->d, best);
     t->dim[node] = best;
     t->split[node] = src[idx[first + h] * t->d + best];
     t->a[node] = kd_rec(t, idx, first, h, src);
@@ -971,6 +995,79 @@ int64_t orc_engine_step(int32_t agent_kind, const double *prm, int32_t d, const 
     }
     free(samples); free(ends); free(d2);
     return n;
+}
+
+/* ======================================================================
+ * The reference's own sequential loop at a given tree size (CPU baseline leg): RRT::query
+ * (planners/rrt.hpp:42-94) one extension at a time against the current tree, with
+ * FLANN_KDTreeWrapper::insertPoint (utilities/flannkdtreewrapper.hpp:27-40) calling
+ * addPoints(point, 2) -> [upstream FLANN 1.8.4] KDTreeSingleIndex::buildIndex() over every point
+ * after each insertion.  Samples and controls come from the engine's counter-based streams
+ * (extension g = ext_base + i), so the first extensions equal the batched round's when no
+ * earlier one was inserted.  Stops after max_ext extensions or time_budget seconds.
+ * ====================================================================== */
+static double now_s(void) {
+    struct timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    return (double)ts.tv_sec + 1e-9 * (double)ts.tv_nsec;
+}
+
+int64_t orc_rrt_seq_rebuild(int32_t agent_kind, const double *prm, int32_t d, const double *ranges,
+                            double steer_dt, double cc_dt, uint64_t seed, uint64_t ext_base, int64_t max_ext,
+                            double time_budget, const orc_bvh *env, const double env_tf[12],
+                            const double *agent_tris, int64_t Ta, double *nodes, int32_t *parents,
+                            int64_t n_nodes, int64_t capacity, int64_t *ext_done, double *seconds) {
+    const int L = agent_kind == 2 ? (int)prm[0] + 1 : 1;
+    double sample[64], end[64], poses[12 * 64];
+    int64_t n = n_nodes, valid = 0, i = 0;
+    const double t0 = now_s();
+    orc_kdtree *t = orc_kdtree_build(nodes, n, d);
+    for (; i < max_ext && n < capacity; ++i) {
+        if (now_s() - t0 > time_budget) break;
+        const uint64_t g = ext_base + (uint64_t)i;
+        for (int32_t j = 0; j < d; ++j) sample[j] = orc_engine_uniform(seed, g * 64 + j, ranges[2 * j], ranges[2 * j + 1]);
+        int32_t id;
+        double d2;
+        orc_kdtree_knn(t, sample, 1, 1, &id, &d2, 1);
+        const double *from = nodes + (int64_t)(id - 1) * d;
+        int32_t P;
+        if (agent_kind == 0) {
+            double r[3];
+            for (int j = 0; j < 3; ++j) r[j] = orc_engine_uniform(seed, g * 64 + 32 + j, -1.0, 1.0);
+            omni_steer_from(r, from, end);
+            P = orc_omni_get_poses(from, end, cc_dt, poses, 64);
+        } else if (agent_kind == 1) {
+            double awz[3];
+            awz[0] = orc_engine_uniform(seed, g * 64 + 32, -1, 1);
+            awz[1] = orc_engine_uniform(seed, g * 64 + 33, -0.1745, 0.1745);
+            awz[2] = orc_engine_uniform(seed, g * 64 + 34, -1, 1);
+            orc_blimp_do_step(prm, from, awz[0], awz[1], awz[2], steer_dt, end);
+            P = orc_blimp_get_poses(prm, from, awz, steer_dt, cc_dt, poses, 64);
+        } else {
+            double aw[2];
+            aw[0] = orc_engine_uniform(seed, g * 64 + 32, -0.1, 1);
+            aw[1] = orc_engine_uniform(seed, g * 64 + 33, -M_PI / 18., M_PI / 18.);
+            orc_snake_do_step(prm, from, aw[0], aw[1], steer_dt, end);
+            P = orc_snake_get_poses(prm, from, aw, steer_dt, cc_dt, poses, 64 / L);
+        }
+        if (P > 64 / L) P = 64 / L;
+        int hit = 0;
+        for (int32_t p = 0; p < P && !hit; ++p)
+            for (int l = 0; l < L && !hit; ++l)
+                hit = orc_collide_unit_bvh(env, env_tf, agent_tris, Ta, poses + 12 * ((size_t)p * L + l), NULL);
+        if (hit) continue;
+        memcpy(nodes + n * d, end, sizeof(double) * (size_t)d);
+        parents[n] = id;
+        ++n;
+        ++valid;
+        /* insertPoint -> addPoints -> buildIndex over all n points */
+        orc_kdtree_free(t);
+        t = orc_kdtree_build(nodes, n, d);
+    }
+    orc_kdtree_free(t);
+    *ext_done = i;
+    *seconds = now_s() - t0;
+    return valid;
 }
 
 /* ======================================================================

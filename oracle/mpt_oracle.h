@@ -144,6 +144,17 @@ int64_t orc_engine_step(int32_t agent_kind, const double *prm, int32_t d, const 
                         double *nodes, int32_t *parents, int64_t n_nodes, int64_t capacity,
                         int32_t *nn_out, uint8_t *verdict_out, int nthreads, int use_kdtree);
 
+/* The reference's sequential loop at a tree size (CPU baseline leg): extensions one at a time
+ * on the engine's RNG streams (extension ext_base + i), kd-tree NN, collision, and after every
+ * insertion a full kd-tree rebuild, as FLANN 1.8.4's addPoints -> buildIndex
+ * (utilities/flannkdtreewrapper.hpp:35).  Stops after max_ext extensions or time_budget
+ * seconds; returns the extensions inserted, *ext_done = tried, *seconds = elapsed. */
+int64_t orc_rrt_seq_rebuild(int32_t agent_kind, const double *prm, int32_t d, const double *ranges,
+                            double steer_dt, double cc_dt, uint64_t seed, uint64_t ext_base, int64_t max_ext,
+                            double time_budget, const orc_bvh *env, const double env_tf[12],
+                            const double *agent_tris, int64_t Ta, double *nodes, int32_t *parents,
+                            int64_t n_nodes, int64_t capacity, int64_t *ext_done, double *seconds);
+
 /* PRM construction (planners/prm/prm.hpp:334-387) for the omnidirectional agent over
  * explicit milestones states[n][3]: edges[E][2] = (target, source), costs[E], comp[n] =
  * smallest milestone of each component.  Returns E, or -1 if E > cap. */

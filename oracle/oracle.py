@@ -30,14 +30,25 @@ def build() -> str:
     return _LIB_PATH
 
 
-def lib():
+def build_native(out_dir: str) -> str:
+    """The same restatement compiled for the host it runs on (-O3 -march=native): bench.py's
+    CPU-baseline leg builds it on the GPU box's own cores.  Returns the library path."""
+    subprocess.run(["make", "-s", "-C", _HERE, f"OUT={out_dir}", "OPT=-O3 -march=native"], check=True)
+    return os.path.join(out_dir, "libmpt_oracle.so")
+
+
+def lib(path: str | None = None):
+    """Load the oracle library (the portable -O3 build by default; `path` loads another
+    build of the same source, e.g. build_native's, and replaces the loaded one)."""
     global _lib
+    if path is not None and (_lib is None or _lib._name != path):
+        _lib = None
     if _lib is None:
-        if not os.path.exists(_LIB_PATH) or os.path.getmtime(_LIB_PATH) < os.path.getmtime(
+        if path is None and (not os.path.exists(_LIB_PATH) or os.path.getmtime(_LIB_PATH) < os.path.getmtime(
             os.path.join(_HERE, "mpt_oracle.c")
-        ):
+        )):
             build()
-        L = C.CDLL(_LIB_PATH)
+        L = C.CDLL(path or _LIB_PATH)
         sig = {
             "orc_quat_to_rot": (None, [P, P]),
             "orc_relative_transform": (None, [P, P, P, P, P, P]),
@@ -68,6 +79,7 @@ def lib():
             "orc_snake_get_poses": (I32, [P, P, P, D, D, P, I32]),
             "orc_rrt_run": (I64, [I32, P, I32, P, P, P, P, D, D, P, I64, P, P, I64, I64, I64, P, P, P, P]),
             "orc_engine_step": (I64, [I32, P, I32, P, D, D, U64, U64, I32, P, P, P, I64, P, P, I64, I64, P, P, C.c_int, C.c_int]),
+            "orc_rrt_seq_rebuild": (I64, [I32, P, I32, P, D, D, U64, U64, I64, D, P, P, P, I64, P, P, I64, I64, P, P]),
             "orc_prm_build": (I64, [P, P, P, I64, P, I64, I32, I32, D, P, P, I64, P]),
             "orc_tri_distance": (D, [P, P]),
             "orc_grid_discretization": (I64, [P, P, P, I64, P, P, I32, P, I64]),
@@ -359,6 +371,22 @@ def engine_step(kind, prm, ranges, steer_dt, cc_dt, seed, ext_base, K, bvh: BVH,
                               _p(_f64(env_tf)), _p(agent_tris), agent_tris.shape[0], _p(nodes), _p(parents),
                               n_nodes, nodes.shape[0], _p(nn), _p(verdict), nthreads, 1 if use_kdtree else 0)
     return n, nn, verdict
+
+
+def rrt_seq_rebuild(kind, prm, ranges, steer_dt, cc_dt, seed, ext_base, bvh: BVH, env_tf, agent_tris, nodes,
+                    parents, n_nodes, max_ext, time_budget):
+    """orc_rrt_seq_rebuild: the reference's one-extension-at-a-time loop with a kd-tree rebuild
+    per insertion (FLANN 1.8.4 addPoints).  Mutates nodes/parents; returns (valid, tried, s)."""
+    ranges = _f64(ranges).reshape(-1, 2)
+    d = ranges.shape[0]
+    assert nodes.dtype == np.float64 and nodes.flags.c_contiguous and nodes.shape[1] == d
+    agent_tris = _f64(agent_tris).reshape(-1, 9)
+    prm = _f64(prm if prm is not None else np.zeros(7))
+    done, secs = C.c_int64(), C.c_double()
+    valid = lib().orc_rrt_seq_rebuild(kind, _p(prm), d, _p(ranges), steer_dt, cc_dt, seed, ext_base, max_ext,
+                                      time_budget, bvh.ptr, _p(_f64(env_tf)), _p(agent_tris), agent_tris.shape[0],
+                                      _p(nodes), _p(parents), n_nodes, nodes.shape[0], C.byref(done), C.byref(secs))
+    return valid, done.value, secs.value
 
 
 def prm_build(bvh: BVH, env_tf, agent_tris, states, k=10, batch=1, cc_dt=0.1):

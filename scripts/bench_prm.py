@@ -34,6 +34,9 @@ def main():
     ap.add_argument("--cpu-n", type=int, default=3000)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--collide", default="split", choices=["split", "fused"])
+    ap.add_argument("--bounds", default="blimp", choices=["blimp", "rooms"],
+                    help="milestone x, y, z: blimp.inst's [-100, 100]^3 (one corner of the rooms) or the whole "
+                         "multi-room extent (every room's walls in play)")
     a = ap.parse_args()
 
     import motionplanningtoolkit_amd as mpt
@@ -46,7 +49,11 @@ def main():
     env, ag = mpt.Environment(env_t, sc.env_tf), mpt.AgentMesh(sc.agent_tris)
     rng = np.random.default_rng(0)
     st = rng.uniform(sc.ranges[:, 0], sc.ranges[:, 1], size=(a.n, sc.dim))
-    vol = float(np.prod(sc.ranges[:3, 1] - sc.ranges[:3, 0]))
+    lo, hi = sc.ranges[:3, 0], sc.ranges[:3, 1]
+    if a.bounds == "rooms":
+        lo, hi = env_t.reshape(-1, 3).min(0), env_t.reshape(-1, 3).max(0)
+        st[:, :3] = rng.uniform(lo, hi, size=(a.n, 3))
+    vol = float(np.prod(hi - lo))
     r = (a.degree * vol / (a.n * 4.0 / 3.0 * math.pi)) ** (1.0 / 3.0)
     r2 = r * r
     mpt.prm_connect(env, ag, 1, st[: min(a.n, 2000)], r2, sc.cc_dt)  # warm-up (allocations)
@@ -65,7 +72,8 @@ def main():
         "config": {"workload": f"blimp ({len(sc.agent_tris)} tris) PRM in {a.rooms}x{a.rooms} rooms "
                                f"({len(env_t)} tris)", "milestones": a.n, "radius": r, "edges": E,
                    "free_fraction": float(1.0 - res["verdict"].mean()) if E else None,
-                   "components": int(len(np.unique(res["comp"]))), "collide_mode": a.collide},
+                   "components": int(len(np.unique(res["comp"]))), "collide_mode": a.collide,
+                   "bounds": a.bounds},
     }
     if not a.no_cpu:
         sys.path.insert(0, os.path.join(REPO, "oracle"))

@@ -428,3 +428,34 @@ def test_oracle_grid_discretization_centres(oracle):
     want = np.array([not (abs(c[n % 4]) <= 1 and abs(c[n // 4 % 4]) <= 1 and abs(c[n // 16 % 4]) <= 1)
                      for n in range(64)])
     assert np.array_equal(free, want)
+
+
+def test_oracle_rebuild_loop_is_the_sequential_engine(oracle):
+    """bench.py's "FLANN 1.8.4 rebuild per insert" CPU leg (orc_rrt_seq_rebuild) is the
+    sequential loop: n extensions one at a time equal n engine rounds of K = 1 (each sees the
+    previous insertions), node for node; the per-insert kd-tree rebuild changes only time."""
+    import dataclasses
+
+    sc = scenes.omni_scenario()
+    # the omni box among the corridor's boxes, so some extensions collide
+    sc = dataclasses.replace(sc, env_tris=scenes.read_obj(scenes.mesh_path("env_corridor")),
+                             ranges=np.array([[-6.0, 6.0], [-52.0, 52.0], [-1.0, 1.0]]))
+    rng = np.random.default_rng(5)
+    n0, n_ext, seed = 500, 120, 31
+    base = rng.uniform(sc.ranges[:, 0], sc.ranges[:, 1], size=(n0, 3))
+    bvh = oracle.BVH(sc.env_tris)
+    a = np.zeros((n0 + n_ext, 3))
+    a[:n0] = base
+    pa = np.zeros(n0 + n_ext, np.int32)
+    valid, tried, _ = oracle.rrt_seq_rebuild(sc.kind, sc.prm, sc.ranges, sc.steer_dt, sc.cc_dt, seed, 0, bvh,
+                                             sc.env_tf, sc.agent_tris, a, pa, n0, n_ext, 60.0)
+    assert tried == n_ext and 0 < valid < n_ext
+    b = np.zeros((n0 + n_ext, 3))
+    b[:n0] = base
+    pb = np.zeros(n0 + n_ext, np.int32)
+    n = n0
+    for i in range(n_ext):
+        n, _, _ = oracle.engine_step(sc.kind, sc.prm, sc.ranges, sc.steer_dt, sc.cc_dt, seed, i, 1, bvh, sc.env_tf,
+                                     sc.agent_tris, b, pb, n)
+    assert n == n0 + valid
+    assert np.array_equal(a[:n], b[:n]) and np.array_equal(pa[:n], pb[:n])
