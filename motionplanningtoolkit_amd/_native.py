@@ -80,6 +80,7 @@ SIGNATURES = {
     "mpt_host_last_error": (C.c_char_p, []),
     "mpt_host_load_mesh": (I32, [C.c_char_p, I32, P, I64, P, P]),
     "mpt_host_rrt_inst": (I32, [C.c_char_p, I32, I64, P, P, P, P, P]),
+    "mpt_host_rrt_batched": (I32, [C.c_char_p, P, P, I64, P, P, P, P]),
     "mpt_host_prm": (I32, [C.c_char_p, P, I64, I32, I32, I64, P, P, P, I64, P, P, P, P]),
     "mpt_host_grid_discretization": (I32, [C.c_char_p, P, I64, P, P, P]),
     "mpt_host_prmlite": (I32, [C.c_char_p, I32, D, P, I64, P, P]),

@@ -464,3 +464,19 @@ def rrt_inst(path: str, iterations_at_a_time: int, cap: int = 1 << 16):
     d = dim.value
     m = min(n.value, cap)
     return starts[: m * d].reshape(m, d), ends[: m * d].reshape(m, d), bool(solved.value)
+
+
+def rrt_batched_inst(path: str, cap: int = 1 << 20) -> dict:
+    """Planner <file.inst> in its batched throughput mode (the file sets `Batch Size`; keys in
+    include/mpt_host.h mpt_host_rrt_batched): counters, wall time and tree 0."""
+    out = np.zeros(4, np.int64)
+    secs = C.c_double()
+    n = C.c_int64()
+    dim = C.c_int32()
+    states = np.zeros(cap * 16)
+    parents = np.zeros(cap, np.int32)
+    check(lib().mpt_host_rrt_batched(path.encode(), _p(out), C.byref(secs), cap, _p(states), _p(parents), C.byref(n),
+                                     C.byref(dim)), "mpt_host_rrt_batched", host=True)
+    d, m = dim.value, min(n.value, cap)
+    return {"rounds": int(out[0]), "checked": int(out[1]), "valid": int(out[2]), "solved_trees": int(out[3]),
+            "seconds": secs.value, "tree0": (states[: m * d].reshape(m, d), parents[:m])}

@@ -163,6 +163,14 @@ public:
         return ret;
     }
 
+    // the batched engine's view of the agent (include/mpt.h mpt_rrt_create)
+    static constexpr int32_t kEngineKind = MPT_AGENT_OMNI;
+    const double *params(double out[7]) const {
+        for (int i = 0; i < 7; ++i) out[i] = 0.0;
+        return out;
+    }
+    const SimpleAgentMeshHandler &agentMesh() const { return mesh; }
+
 private:
     SimpleAgentMeshHandler mesh;
     std::vector<double> goalThresholds;
@@ -296,6 +304,7 @@ public:
         return out;
     }
     const SimpleAgentMeshHandler &agentMesh() const { return mesh; }
+    static constexpr int32_t kEngineKind = MPT_AGENT_BLIMP;
 
 private:
     SimpleAgentMeshHandler mesh;
@@ -455,6 +464,7 @@ public:
         return out;
     }
     const SimpleAgentMeshHandler &agentMesh() const { return mesh; }
+    static constexpr int32_t kEngineKind = MPT_AGENT_SNAKE;
 
 private:
     SimpleAgentMeshHandler mesh;

@@ -3,6 +3,7 @@
 // reference (main.cpp:78-190, 202-207).  The typedef stack is the reference's with
 // FLANN_KDTreeWrapper replaced by GpuNN and Map3D/MeshHandler running on the GPU.
 #pragma once
+#include <chrono>
 #include <cstdlib>
 #include <string>
 #include <vector>
@@ -22,7 +23,9 @@ struct RunResult {
 
 template <class Agent>
 RunResult run_rrt(const InstanceFileMap &args, int iterationsAtATime) {
+    // main.cpp:39-55 with FLANN_KDTreeWrapper<KDTreeType, flann::L2<double>, Edge> -> GpuNN<Edge>
     typedef Map3D<Agent> Workspace;
+    typedef flann::KDTreeSingleIndexParams KDTreeType;
     typedef GpuNN<typename Agent::Edge> KDTree;
     typedef UniformSampler<Workspace, Agent, KDTree> Sampler;
     typedef TreeInterface<Agent, KDTree, Sampler> TreeIface;
@@ -32,7 +35,8 @@ RunResult run_rrt(const InstanceFileMap &args, int iterationsAtATime) {
     Workspace workspace(args);
     typename Agent::State start(parse_doubles(args.value("Agent Start Location")));
     typename Agent::State goal(parse_doubles(args.value("Agent Goal Location")));
-    KDTree kdtree(agent.getTreeStateSize());
+    KDTreeType kdtreeType;
+    KDTree kdtree(kdtreeType, agent.getTreeStateSize());
     Sampler sampler(workspace, agent, kdtree);
     TreeIface treeInterface(kdtree, sampler);
     Planner planner(workspace, agent, treeInterface, args);
@@ -171,6 +175,113 @@ inline LiteResult run_prmlite_inst(const std::string &path, int32_t n_vertices, 
     if (type == "Omnidirectional") return run_prmlite<Omnidirectional>(args, n_vertices, step);
     if (type == "Blimp") return run_prmlite<Blimp>(args, n_vertices, step);
     if (type == "Snake") return run_prmlite<SnakeTrailers>(args, n_vertices, step);
+    throw std::runtime_error("unrecognized Agent Type: " + type);
+}
+
+// Batched throughput mode of the `.inst` entry point (SURVEY §5 config keys): when the file
+// names `Batch Size ? K`, the planner runs the device engine (include/mpt.h mpt_rrt_*) instead
+// of the one-extension-at-a-time RRT::query:
+//   Batch Size ? K          extensions per round (per tree)
+//   Seed ? s                engine seed of the first tree (default 0)
+//   Seed Count ? n          independent trees, seeds s .. s + n - 1 (default 1), one
+//                           mpt_rrt_step_many round for all of them
+//   Rounds ? R              rounds to run (default: until Max Tree Size)
+//   Max Tree Size ? N       nodes per tree (default 1 + R * K; 100 000 without Rounds)
+//   NN Index ? auto|brute|grid|tree   (default auto)
+// Every tree grows from `Agent Start Location`; a tree is solved when one of its nodes is a
+// goal (Agent::isGoal against `Agent Goal Location`).
+struct BatchedResult {
+    int dim = 0;
+    int64_t rounds = 0, checked = 0, valid = 0;
+    double seconds = 0;
+    std::vector<int64_t> nodes;  // per tree
+    std::vector<int32_t> solved; // per tree: 1 when a node is a goal
+    std::vector<double> first;   // tree 0's states [nodes[0]][dim]
+    std::vector<int32_t> first_parents;
+};
+
+template <class Agent>
+BatchedResult run_batched(const InstanceFileMap &args) {
+    Agent agent(args);
+    Map3D<Agent> workspace(args);
+    typename Agent::State start(parse_doubles(args.value("Agent Start Location")));
+    typename Agent::State goal(parse_doubles(args.value("Agent Goal Location")));
+    const int32_t K = std::stoi(args.value("Batch Size"));
+    const uint64_t seed = std::stoull(args.value_or("Seed", "0"));
+    const int32_t n = std::stoi(args.value_or("Seed Count", "1"));
+    const int64_t R = std::stoll(args.value_or("Rounds", "-1"));
+    const int64_t cap = std::stoll(args.value_or("Max Tree Size", R > 0 ? std::to_string(1 + R * (int64_t)K) : "100000"));
+    const std::string nn = args.value_or("NN Index", "auto");
+    const int32_t nn_mode = nn == "brute" ? MPT_NN_BRUTE : nn == "grid" ? MPT_NN_GRID : nn == "tree" ? MPT_NN_TREE
+                                                                                                     : MPT_NN_AUTO;
+    if (K < 1 || n < 1 || cap < 1) throw std::runtime_error("Batch Size, Seed Count and Max Tree Size must be >= 1");
+    const unsigned d = agent.getTreeStateSize();
+    std::vector<double> ranges;
+    for (const auto &r : agent.getStateVarRanges(workspace.getBounds())) {
+        ranges.push_back(r.first);
+        ranges.push_back(r.second);
+    }
+    double prm[7];
+    agent.params(prm);
+    const double steer_dt = std::stod(args.value("Steering Delta t"));
+    const double cc_dt = std::stod(args.value("Collision Check Delta t"));
+    std::vector<mpt_rrt *> rs((size_t)n, nullptr);
+    struct Guard {
+        std::vector<mpt_rrt *> &rs;
+        ~Guard() {
+            for (mpt_rrt *r : rs)
+                if (r) mpt_rrt_destroy(r);
+        }
+    } guard{rs};
+    const std::vector<double> &sv = start.getStateVars();
+    for (int32_t i = 0; i < n; ++i) {
+        mpt_throw(mpt_rrt_create(workspace.environment().handle(), agent.agentMesh().handle(), Agent::kEngineKind, prm,
+                                 ranges.data(), (int32_t)d, steer_dt, cc_dt, cap, seed + (uint64_t)i, &rs[i]),
+                  "mpt_rrt_create");
+        mpt_throw(mpt_rrt_add_nodes(rs[i], sv.data(), nullptr, 1), "mpt_rrt_add_nodes");
+        mpt_throw(mpt_rrt_set_nn(rs[i], nn_mode, 0.0), "mpt_rrt_set_nn");
+    }
+    std::vector<void *> streams((size_t)n, nullptr);
+    BatchedResult r;
+    r.dim = (int)d;
+    const auto t0 = std::chrono::steady_clock::now();
+    const int64_t max_rounds = R > 0 ? R : (cap + K - 1) / K;
+    for (int64_t round = 0; round < max_rounds; ++round) {
+        if (n == 1)
+            mpt_throw(mpt_rrt_step(rs[0], K, nullptr), "mpt_rrt_step");
+        else
+            mpt_throw(mpt_rrt_step_many(rs.data(), n, K, streams.data(), nullptr), "mpt_rrt_step_many");
+        ++r.rounds;
+    }
+    mpt_throw(mpt_device_synchronize(), "mpt_device_synchronize");
+    r.seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    for (int32_t i = 0; i < n; ++i) {
+        uint64_t c[8];
+        mpt_throw(mpt_rrt_counters(rs[i], c), "mpt_rrt_counters");
+        r.checked += (int64_t)c[1];
+        r.valid += (int64_t)c[2];
+        r.nodes.push_back((int64_t)c[3]);
+        std::vector<double> st((size_t)c[3] * d);
+        std::vector<int32_t> par((size_t)c[3]);
+        mpt_throw(mpt_rrt_read_tree(rs[i], st.data(), par.data(), (int64_t)c[3]), "mpt_rrt_read_tree");
+        int32_t solved = 0;
+        for (uint64_t k = 0; k < c[3] && !solved; ++k)
+            solved = agent.isGoal(agent.buildState(StateVars(st.begin() + k * d, st.begin() + (k + 1) * d)), goal) ? 1 : 0;
+        r.solved.push_back(solved);
+        if (i == 0) {
+            r.first = std::move(st);
+            r.first_parents = std::move(par);
+        }
+    }
+    return r;
+}
+
+inline BatchedResult run_batched_inst(const std::string &path) {
+    InstanceFileMap args(path);
+    const std::string type = args.value("Agent Type");
+    if (type == "Omnidirectional") return run_batched<Omnidirectional>(args);
+    if (type == "Blimp") return run_batched<Blimp>(args);
+    if (type == "Snake") return run_batched<SnakeTrailers>(args);
     throw std::runtime_error("unrecognized Agent Type: " + type);
 }
 

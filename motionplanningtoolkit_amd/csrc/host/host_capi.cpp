@@ -56,6 +56,28 @@ extern "C" mpt_status mpt_host_rrt_inst(const char *inst_path, int32_t iteration
     });
 }
 
+extern "C" mpt_status mpt_host_rrt_batched(const char *inst_path, int64_t out[4], double *seconds, int64_t cap,
+                                           double *tree0_states, int32_t *tree0_parents, int64_t *tree0_nodes,
+                                           int32_t *dim) {
+    return hguard([&] {
+        if (!inst_path || !out) throw std::invalid_argument("null pointer");
+        const auto r = mpt_host::run_batched_inst(inst_path);
+        int64_t solved = 0;
+        for (int32_t s : r.solved) solved += s;
+        out[0] = r.rounds;
+        out[1] = r.checked;
+        out[2] = r.valid;
+        out[3] = solved;
+        if (seconds) *seconds = r.seconds;
+        if (dim) *dim = r.dim;
+        const int64_t n = r.nodes.empty() ? 0 : r.nodes[0];
+        if (tree0_nodes) *tree0_nodes = n;
+        const int64_t m = std::min<int64_t>(n, cap);
+        if (tree0_states && m > 0) std::memcpy(tree0_states, r.first.data(), sizeof(double) * r.dim * m);
+        if (tree0_parents && m > 0) std::memcpy(tree0_parents, r.first_parents.data(), sizeof(int32_t) * m);
+    });
+}
+
 extern "C" mpt_status mpt_host_prm(const char *inst_path, const double *states, int64_t n, int32_t batch,
                                    int32_t max_queries, int64_t cap, int32_t *edges, double *costs, int64_t *n_edges,
                                    int64_t comp_cap, int32_t *comp, int64_t *n_milestones, int32_t *solved,

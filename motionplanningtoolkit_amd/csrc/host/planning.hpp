@@ -69,6 +69,26 @@ private:
 };
 
 // ------------------------------------------------------------------ GpuNN
+// FLANN's index-parameter types as the reference's composition names them (main.cpp:41,
+// prm.hpp:145): tags only -- the device search is exact whichever is chosen, as FLANN's
+// KDTreeSingleIndex is with eps = 0 (KDTreeIndex's randomized approximation is not modelled,
+// DESIGN.md §2).
+namespace flann {
+struct KDTreeSingleIndexParams {
+    explicit KDTreeSingleIndexParams(int leaf_max_size = 10) : leaf_max_size(leaf_max_size) {}
+    int leaf_max_size;
+};
+struct KDTreeIndexParams {
+    explicit KDTreeIndexParams(int trees = 4) : trees(trees) {}
+    int trees;
+};
+template <class T>
+struct L2 {
+    typedef T ElementType;
+    typedef T ResultType;
+};
+}  // namespace flann
+
 // Same method set and result conventions as FLANN_KDTreeWrapper<KDTreeType, L2<double>, Element>:
 // ids start at 1, distances are squared L2, kNearestWithin's `radius` is compared with
 // squared distances (as the reference passes it straight to an L2<double> index).
@@ -84,6 +104,14 @@ public:
         mpt_nn *nn = nullptr;
         mpt_throw(mpt_nn_create((int32_t)dim, capacity_hint, &nn), "mpt_nn_create");
         nn_.reset(nn, [](mpt_nn *p) { mpt_nn_destroy(p); });
+    }
+
+    // FLANN_KDTreeWrapper(const KDTreeType &type, unsigned int dim, double epsilon = 0)
+    // (utilities/flannkdtreewrapper.hpp:21), so main.cpp:54-55's `KDTree kdtree(kdtreeType,
+    // agent.getTreeStateSize())` compiles unchanged; the search is exact (epsilon 0).
+    template <class KDTreeType>
+    GpuNN(const KDTreeType & /*type*/, unsigned int dim, double epsilon = 0) : GpuNN(dim) {
+        if (epsilon != 0) throw std::invalid_argument("GpuNN: approximate search (epsilon != 0) is not supported");
     }
 
     void insertPoint(Element *elem) {

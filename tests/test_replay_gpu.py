@@ -55,3 +55,23 @@ def test_replay_snake_corridor(mpt_gpu, oracle):
     sc = scenes.snake_scenario("corridor")
     sc.env_tris = scenes.read_obj(scenes.mesh_path("env_corridor"))
     compare(mpt_gpu, oracle, "snake_corridor.inst", sc, 600)
+
+
+def test_batched_inst_entry_point(mpt_gpu):
+    """The `.inst` entry point's batched throughput mode (`Batch Size`, `Seed`, `Seed Count`,
+    `Rounds`: compose.hpp run_batched, mpt_host_rrt_batched): tree 0 equals the same seed grown
+    through the Python engine API round for round, bit for bit, and the counters add up."""
+    r = mpt_gpu.rrt_batched_inst(inst("blimp_batched.inst"))
+    assert r["rounds"] == 5 and r["checked"] == 4 * 5 * 4096
+    assert 0 < r["valid"] <= r["checked"]
+    sc = scenes.blimp_scenario("all")
+    ranges = scenes.blimp_ranges(((0, 177.16), (0, 137.8), (0, 114.17)))
+    env, ag = mpt_gpu.Environment(sc.env_tris, sc.env_tf), mpt_gpu.AgentMesh(sc.agent_tris)
+    e = mpt_gpu.RRTEngine(env, ag, sc.kind, sc.prm, ranges, sc.steer_dt, sc.cc_dt, 1 + 5 * 4096, 1000)
+    e.add_nodes(np.array([[88.6, 68.9, 57.1, 1, 0, 0, 0]], np.float64))
+    for _ in range(5):
+        e.step(4096)
+    n = e.counters()["nodes"]
+    st, par = e.read_tree(n)
+    s0, p0 = r["tree0"]
+    assert np.array_equal(bits(st), bits(s0)) and np.array_equal(par, p0)
