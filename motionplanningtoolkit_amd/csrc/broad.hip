@@ -18,10 +18,10 @@
 //           agent triangles, mapped exactly (FP64) and boxed; lanes also fetch the header's
 //           env triangle boxes, which are then tested from registers; overlaps become
 //           candidates in the wave's segment (or the spill list).
-// k_narrow  one 64-lane workgroup per candidate segment (plus the spill list), one candidate
-//           per lane: exact transform, tri_gate, intersect_Triangle; verdict[edge] = 1.
-// Units whose pairs overflow a segment are re-run by k_narrow's last workgroups with the
-// fused kernel's per-unit walk (collide_common.h collide_unit).
+// k_narrow  one wave per candidate segment (plus the spill list), one candidate per lane:
+//           exact transform, tri_gate, intersect_Triangle; verdict[edge] = 1.
+// k_overflow  units whose pairs overflowed a segment are re-run with the fused kernel's
+//           per-unit walk (collide_common.h collide_unit).
 #include <hipcub/hipcub.hpp>
 
 #include "collide_common.h"
@@ -35,8 +35,6 @@ constexpr int kHdrCap = 64;         // headers per segment (one per lane at most
 constexpr int kCandCap = 2048;      // candidates per k_cands wave (then the spill list)
 constexpr int64_t kSplitChunkThreads = int64_t(1) << 22;  // (unit, cluster) threads per launch of the two-phase path
 constexpr int kSpillCap = 1 << 22;  // shared spill list (48 MiB)
-constexpr int kSpillBlocks = 256;   // k_narrow workgroups over the spill list
-constexpr int kOvfBlocks = 64;      // k_narrow workgroups re-running overflowed units
 constexpr int kLdsItems = 2048;     // env tree staged in LDS by k_pairs up to this size (64 KiB)
 constexpr int kStack = kMaxLevels;  // per-thread walk stack (general trees)
 
@@ -396,57 +394,133 @@ __global__ __launch_bounds__(256) void k_cands(EnvDev env, const AgentDev *__res
     }
 }
 
-__device__ __forceinline__ void narrow_one(const EnvDev &env, const AgentDev *__restrict__ links,
-                                           const CollideWork &w, const Cand cd, uint32_t &n_sat) {
-    int32_t link;
-    int64_t slot, edge;
-    decode_unit(w, cd.unit, link, slot, edge);
-    if (load_flag(w.verdict + edge)) return;
-    double R[9], T[3];
-    unit_transform(env, w.poses + (slot * w.L + link) * 12, R, T);
-    const double *t = links[link].tris + (int64_t)cd.atri * 9;
-    const v3 Q1 = xform(R, T, mk(t[0], t[1], t[2]));
-    const v3 Q2 = xform(R, T, mk(t[3], t[4], t[5]));
-    const v3 Q3 = xform(R, T, mk(t[6], t[7], t[8]));
-    const EnvTri &E = env.tris[cd.etri];
-    if (!tri_gate(E.lo, E.hi, Q1, Q2, Q3)) return;
-    ++n_sat;
-    if (tri_intersect(E, Q1, Q2, Q3))
-        __hip_atomic_store(w.verdict + edge, (uint8_t)1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+// One candidate per lane.  Every load a candidate needs (its edge's verdict flag, the pose, the
+// agent triangle and the env triangle) is issued before any of them is tested, so a
+// candidate costs one dependent round trip after its record instead of three; the next
+// record is fetched while this one computes.  kLds: the env triangles' vertices sit in LDS
+// and the P-side of intersect_Triangle is recomputed from them (tri_collide_verts, bitwise
+// make_env_tri's fields); otherwise the precomputed 384-B records are read (large envs).
+template <bool kLds>
+__device__ __forceinline__ void narrow_range(const EnvDev &env, const AgentDev *__restrict__ links,
+                                             const CollideWork &w, const Cand *__restrict__ cands, uint32_t i0,
+                                             uint32_t n, uint32_t stride, const double *__restrict__ s_verts,
+                                             uint32_t &n_sat) {
+    Cand next{};
+    if (i0 < n) next = cands[i0];
+    for (uint32_t i = i0; i < n; i += stride) {
+        const Cand cd = next;
+        if (i + stride < n) next = cands[i + stride];
+        int32_t link;
+        int64_t slot, edge;
+        decode_unit(w, cd.unit, link, slot, edge);
+        const uint8_t decided = load_flag(w.verdict + edge);
+        const double *pose = w.poses + (slot * w.L + link) * 12;
+        double P[12];
+#pragma unroll
+        for (int k = 0; k < 12; ++k) P[k] = pose[k];
+        const double *t = links[link].tris + (int64_t)cd.atri * 9;
+        double A[9];
+#pragma unroll
+        for (int k = 0; k < 9; ++k) A[k] = t[k];
+        if (decided) continue;  // another candidate of this edge already found the contact
+        double R[9], T[3];
+        relative_transform(env.tf, env.tf + 9, P, P + 9, R, T);
+        const v3 Q1 = xform(R, T, mk(A[0], A[1], A[2]));
+        const v3 Q2 = xform(R, T, mk(A[3], A[4], A[5]));
+        const v3 Q3 = xform(R, T, mk(A[6], A[7], A[8]));
+        bool hit;
+        if constexpr (kLds) {
+            hit = tri_collide_verts(s_verts + (int64_t)cd.etri * 9, Q1, Q2, Q3);
+        } else {
+            const EnvTri &E = env.tris[cd.etri];
+            hit = tri_gate(E.lo, E.hi, Q1, Q2, Q3) && tri_intersect(E, Q1, Q2, Q3);
+        }
+        if (w.stats) {
+            // SAT tests (the gate passed): recount with the cheap gate alone (stats runs only)
+            const double *tv = kLds ? s_verts + (int64_t)cd.etri * 9 : nullptr;
+            double lo[3], hi[3];
+#pragma unroll
+            for (int k = 0; k < 3; ++k) {
+                lo[k] = kLds ? dmin(tv[k], dmin(tv[3 + k], tv[6 + k])) : env.tris[cd.etri].lo[k];
+                hi[k] = kLds ? dmax(tv[k], dmax(tv[3 + k], tv[6 + k])) : env.tris[cd.etri].hi[k];
+            }
+            if (tri_gate(lo, hi, Q1, Q2, Q3)) ++n_sat;
+        }
+        if (hit) __hip_atomic_store(w.verdict + edge, (uint8_t)1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
 }
 
-// Workgroups [0, n_cwaves): one candidate segment each; the next kSpillBlocks: the spill list;
-// the last kOvfBlocks: the units that overflowed a pair segment or the spill list (none in
-// practice), each re-run whole by the fused walk (one wave per unit, BVH from global memory)
-// -- in this launch, so the usual empty case costs no launch of its own.
-__global__ __launch_bounds__(64) void k_narrow(EnvDev env, const AgentDev *__restrict__ links, CollideWork w,
-                                               SplitArgs a) {
-    const int32_t gw = blockIdx.x;
+// 256-thread workgroups, one wave per candidate segment: waves [0, n_cwaves) take segment
+// gw; the next kSpillWaves stride the spill list.  A workgroup whose segments hold at least
+// 4 * n_tris candidates (lds_ok: the env fits) first stages the env triangles' vertices
+// (72 B each) in LDS and recomputes their SAT fields -- below that the staging and the
+// recompute cost more than the 384-B records they save (A/B: blimp.inst, 2.1 candidates
+// per env tri per workgroup, 34 us global vs 36 us staged; blimp-room, 16: 174 vs 162 us).  The overflow re-run lives in
+// k_overflow: the fused walk's registers in this kernel cost a wave per SIMD (158 VGPRs).
+constexpr int kNarrowWaves = 4;
+constexpr int kSpillWaves = 256;
+constexpr int kOvfWaves = 64;
+constexpr int kNarrowLdsTris = 1024;  // env triangles staged in LDS up to this count (72 KiB)
+
+__global__ __launch_bounds__(kNarrowWaves * 64, 4) void k_narrow(EnvDev env, const AgentDev *__restrict__ links,
+                                                                 CollideWork w, SplitArgs a, int32_t lds_ok) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    __shared__ uint32_t s_cnt[kNarrowWaves];
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    const int32_t gw = (int32_t)blockIdx.x * kNarrowWaves + wave;
+    double *s_verts = reinterpret_cast<double *>(smem);
+    const uint32_t n_spill = a.ctl[2] < (uint32_t)a.spill_cap ? a.ctl[2] : (uint32_t)a.spill_cap;
+    const uint32_t cnt = gw < a.n_cwaves ? a.cand_count[gw] : 0;
+    bool lds = false;
+    if (lds_ok) {
+        if (lane == 0) s_cnt[wave] = gw < a.n_cwaves ? cnt : n_spill / kSpillWaves;
+        __syncthreads();
+        uint32_t tot = 0;
+#pragma unroll
+        for (int i = 0; i < kNarrowWaves; ++i) tot += s_cnt[i];
+        lds = tot >= (uint32_t)env.n_tris * 4u;
+        if (lds) {
+            // the vertices P1, P2, P3 of each EnvTri record, as given (fcl_math.h EnvTri)
+            for (int32_t i = threadIdx.x; i < env.n_tris * 9; i += blockDim.x) {
+                const int32_t tri = i / 9, k = i % 9;
+                const double *r = reinterpret_cast<const double *>(env.tris + tri);
+                s_verts[i] = k < 3 ? r[k] : (k < 6 ? r[41 + (k - 3)] : r[44 + (k - 6)]);
+            }
+            __syncthreads();
+        }
+    }
     uint32_t n_sat = 0;
-    if (gw >= a.n_cwaves + kSpillBlocks) {
-        __shared__ int32_t s_stk[kStackDepth];
-        const uint32_t n_ovf = __hip_atomic_load(a.ctl + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const bool shared_edges = w.pose_edge != nullptr || w.L > 1 || w.pmax > 1;
-        uint32_t nu = 0, nc = 0, nn = 0, ns = 0;
-        for (uint32_t i = (uint32_t)(gw - a.n_cwaves - kSpillBlocks); i < n_ovf; i += kOvfBlocks)
-            collide_unit(env, env.nodes, env.n_nodes, links, w, a.ovf_list[i], s_stk, (int)threadIdx.x, shared_edges,
-                         nc, nn, ns, nu);
-        return;
-    }
-    if (gw < a.n_cwaves) {
-        const uint32_t cnt = a.cand_count[gw];
-        const Cand *seg = a.cand + (int64_t)gw * a.cand_cap;
-        for (uint32_t i = threadIdx.x; i < cnt; i += 64) narrow_one(env, links, w, seg[i], n_sat);
-    } else {
-        const uint32_t n = a.ctl[2] < (uint32_t)a.spill_cap ? a.ctl[2] : (uint32_t)a.spill_cap;
-        for (uint32_t i = (uint32_t)(gw - a.n_cwaves) * 64 + threadIdx.x; i < n; i += kSpillBlocks * 64)
-            narrow_one(env, links, w, a.spill[i], n_sat);
-    }
+    const Cand *cands = gw < a.n_cwaves ? a.cand + (int64_t)gw * a.cand_cap : a.spill;
+    const uint32_t i0 = gw < a.n_cwaves ? (uint32_t)lane : (uint32_t)(gw - a.n_cwaves) * 64 + lane;
+    const uint32_t n = gw < a.n_cwaves ? cnt : n_spill;
+    const uint32_t stride = gw < a.n_cwaves ? 64u : (uint32_t)kSpillWaves * 64u;
+    if (lds)
+        narrow_range<true>(env, links, w, cands, i0, n, stride, s_verts, n_sat);
+    else
+        narrow_range<false>(env, links, w, cands, i0, n, stride, s_verts, n_sat);
     if (w.stats && n_sat) atomicAdd(w.stats + 3, (unsigned long long)n_sat);
-    if (w.stats && gw == 0 && threadIdx.x == 0) {
+    if (w.stats && gw == 0 && lane == 0) {
         atomicAdd(w.stats + 5, (unsigned long long)a.ctl[1]);
-        atomicAdd(w.stats + 7, (unsigned long long)(a.ctl[2] < (uint32_t)a.spill_cap ? a.ctl[2] : a.spill_cap));
+        atomicAdd(w.stats + 7, (unsigned long long)n_spill);
     }
+}
+
+// Units that overflowed a pair segment or the spill list (none in practice) are re-run whole
+// with the fused walk (one wave per unit, BVH from global memory).  Launched unconditionally:
+// the usual empty case is one read of the overflow count.
+__global__ __launch_bounds__(kNarrowWaves * 64) void k_overflow(EnvDev env, const AgentDev *__restrict__ links,
+                                                                CollideWork w, SplitArgs a) {
+    __shared__ int32_t s_stk[kNarrowWaves][kStackDepth];
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    const int32_t gw = (int32_t)blockIdx.x * kNarrowWaves + wave;
+    const uint32_t n_ovf = __hip_atomic_load(a.ctl + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const bool shared_edges = w.pose_edge != nullptr || w.L > 1 || w.pmax > 1;
+    uint32_t nu = 0, nc = 0, nn = 0, ns = 0;
+    for (uint32_t i = (uint32_t)gw; i < n_ovf; i += kOvfWaves)
+        collide_unit(env, env.nodes, env.n_nodes, links, w, a.ovf_list[i], s_stk[wave], lane, shared_edges, nc, nn, ns,
+                     nu);
 }
 
 // units decoded (stats only; the other stages count their own work)
@@ -573,10 +647,16 @@ static void collide_split_chunk(const EnvDev &env, const AgentDev *d_links, int3
     hipLaunchKernelGGL(k_cands, dim3((unsigned)((s.n_cwaves + 3) / 4)), dim3(256), 0, stream, env, d_links, w, a);
     hip_check(hipGetLastError(), "k_cands launch");
     mark(1);
-    hipLaunchKernelGGL(k_narrow, dim3((unsigned)(s.n_cwaves + kSpillBlocks + kOvfBlocks)), dim3(64), 0, stream, env,
-                       d_links, w,
-                       a);
+    const unsigned nblocks = (unsigned)((s.n_cwaves + kSpillWaves + kNarrowWaves - 1) / kNarrowWaves);
+    // MPT_NARROW_LDS=0: never stage the env in LDS (A/B knob)
+    static const bool narrow_lds = !(getenv("MPT_NARROW_LDS") && atoi(getenv("MPT_NARROW_LDS")) == 0);
+    const int32_t lds_ok = narrow_lds && env.n_tris <= kNarrowLdsTris;
+    hipLaunchKernelGGL(k_narrow, dim3(nblocks), dim3(kNarrowWaves * 64), lds_ok ? sizeof(double) * 9 * env.n_tris : 0,
+                       stream, env, d_links, w, a, lds_ok);
     hip_check(hipGetLastError(), "k_narrow launch");
+    hipLaunchKernelGGL(k_overflow, dim3(kOvfWaves / kNarrowWaves), dim3(kNarrowWaves * 64), 0, stream, env, d_links,
+                       w, a);
+    hip_check(hipGetLastError(), "k_overflow launch");
     mark(2);
     if (w.stats) {
         hipLaunchKernelGGL(k_count_units, dim3((unsigned)((w.n_units + 255) / 256)), dim3(256), 0, stream, w);

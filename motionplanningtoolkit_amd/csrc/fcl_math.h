@@ -192,6 +192,51 @@ MPT_HD bool tri_intersect(const ETri &E, v3 Q1, v3 Q2, v3 Q3) {
     return true;
 }
 
+// tri_gate + tri_intersect from the env triangle's three vertices t[9] alone: every P-side
+// quantity is recomputed with exactly make_env_tri's operations (so bitwise the record's
+// fields) at its point of use, so a kernel can keep only the 72-B vertices on chip (LDS)
+// and spend FP64 instead of dependent loads of the 384-B record.
+MPT_HD bool tri_collide_verts(const double *t, v3 Q1, v3 Q2, v3 Q3) {
+    double lo[3], hi[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        lo[k] = dmin(t[k], dmin(t[3 + k], t[6 + k]));
+        hi[k] = dmax(t[k], dmax(t[3 + k], t[6 + k]));
+    }
+    if (!tri_gate(lo, hi, Q1, Q2, Q3)) return false;
+    const v3 P1 = mk(t[0], t[1], t[2]), P2 = mk(t[3], t[4], t[5]), P3 = mk(t[6], t[7], t[8]);
+    const v3 p1 = sub(P1, P1), p2 = sub(P2, P1), p3 = sub(P3, P1);
+    const v3 e1 = sub(p2, p1), e2 = sub(p3, p2), e3 = sub(p1, p3);
+    // make_env_tri's proj(): min / max of {p1, p2, p3} . ax
+    auto proj_overlap = [&](v3 ax, v3 q1, v3 q2, v3 q3) {
+        const double a = dot(ax, p1), b = dot(ax, p2), c = dot(ax, p3);
+        return overlap_q(ax, dmin(a, dmin(b, c)), dmax(a, dmax(b, c)), q1, q2, q3);
+    };
+    const v3 q1 = sub(Q1, P1), q2 = sub(Q2, P1), q3 = sub(Q3, P1);
+    const v3 n1 = cross(e1, e2);
+    if (!proj_overlap(n1, q1, q2, q3)) return false;
+    const v3 f1 = sub(q2, q1), f2 = sub(q3, q2), f3 = sub(q1, q3);
+    const v3 m1 = cross(f1, f2);
+    // the record's p2 field holds e1 (make_env_tri); tri_intersect passes it as project6_p's p2
+    if (!project6_p(m1, e1, p3, q1, q2, q3)) return false;
+    if (!proj_overlap(cross(e1, n1), q1, q2, q3)) return false;
+    if (!proj_overlap(cross(e2, n1), q1, q2, q3)) return false;
+    if (!proj_overlap(cross(e3, n1), q1, q2, q3)) return false;
+    if (!project6_p(cross(e1, f1), e1, p3, q1, q2, q3)) return false;
+    if (!project6_p(cross(e1, f2), e1, p3, q1, q2, q3)) return false;
+    if (!project6_p(cross(e1, f3), e1, p3, q1, q2, q3)) return false;
+    if (!project6_p(cross(e2, f1), e1, p3, q1, q2, q3)) return false;
+    if (!project6_p(cross(e2, f2), e1, p3, q1, q2, q3)) return false;
+    if (!project6_p(cross(e2, f3), e1, p3, q1, q2, q3)) return false;
+    if (!project6_p(cross(e3, f1), e1, p3, q1, q2, q3)) return false;
+    if (!project6_p(cross(e3, f2), e1, p3, q1, q2, q3)) return false;
+    if (!project6_p(cross(e3, f3), e1, p3, q1, q2, q3)) return false;
+    if (!project6_p(cross(f1, m1), e1, p3, q1, q2, q3)) return false;
+    if (!project6_p(cross(f2, m1), e1, p3, q1, q2, q3)) return false;
+    if (!project6_p(cross(f3, m1), e1, p3, q1, q2, q3)) return false;
+    return true;
+}
+
 MPT_HD v3 add(v3 a, v3 b) { return v3{a.x + b.x, a.y + b.y, a.z + b.z}; }
 MPT_HD v3 scale(v3 a, double s) { return v3{a.x * s, a.y * s, a.z * s}; }
 
