@@ -254,11 +254,17 @@ def touched_bytes(stage, c, K, n0, d, pmax):
     return None
 
 
-def pmc_summary(path):
+# workload -> the subdirectory of profiles/r*/ that holds its own PMC summary (the same kernel
+# names move different bytes in each workload)
+PMC_SUBDIR = {"blimp": "", "blimp-room": "room", "snake": "snake", "seeds": "c5"}
+
+
+def pmc_summary(path, workload="blimp"):
     if not path:
         import glob
 
-        cands = sorted(glob.glob(os.path.join(REPO, "profiles", "r*", "pmc_summary.json")))
+        sub = PMC_SUBDIR.get(workload, "")
+        cands = sorted(glob.glob(os.path.join(REPO, "profiles", "r[0-9][0-9]", sub, "pmc_summary.json")))
         path = cands[-1] if cands else None
     try:
         return json.load(open(path)), os.path.relpath(path, REPO)
@@ -440,7 +446,7 @@ def run_seeds(args, world, rank, dist, torch, mpt, multiseed, scenes):
     digests = multiseed.gather_digests(dist, digests)
     if rank != 0:
         return None
-    summ, summ_path = pmc_summary(args.traffic)
+    summ, summ_path = pmc_summary(args.traffic, "seeds")
     geo = geometry(sc, env)
     e0 = engines[0]
     n_before = e0.counters()["nodes"]
@@ -623,11 +629,14 @@ def main():
     nn_mode = eng.last_nn()
     d = sc.dim
     kernels = dict(STAGE_KERNEL, nn_query=NN_KERNEL.get(nn_mode, "k_grid_nn1_runs"))
-    if nn_mode == "grid":  # the instantiation (its PMC row): the XCD-slab variant for d >= 15
-        kernels["nn_query"] = f"k_grid_nn1_runs_xcd<{d}," if d >= 15 else f"k_grid_nn1_runs<{d},"
+    if nn_mode == "grid":  # the instantiation (its PMC row)
+        if os.environ.get("MPT_NN_SORT", "1") != "0":
+            kernels["nn_query"] = f"k_grid_nn1_runs_sorted<{d},"  # queries bucketed by k_sample
+        else:
+            kernels["nn_query"] = f"k_grid_nn1_runs_xcd<{d}," if d >= 15 else f"k_grid_nn1_runs<{d},"
     if nn_mode == "tree":
         kernels["nn_build"] = "k_pt_gather"
-    summ, summ_path = pmc_summary(args.traffic)
+    summ, summ_path = pmc_summary(args.traffic, args.workload)
     stages = stage_table(per_launch, cst, K, n0, d, eng.info()["pmax"], geometry(sc, env), nn_mode, kernels, summ)
     dominant = max(stages, key=lambda s: stages[s]["ms"]) if stages else None
     roof = roofline_of(stages, dominant, cst, summ_path)

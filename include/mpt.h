@@ -186,7 +186,8 @@ mpt_status mpt_rrt_create(const mpt_env *env, const mpt_agent *agent, int32_t ag
 mpt_status mpt_rrt_destroy(mpt_rrt *rrt);
 /* Append n tree nodes [n][dim] with parent ids (NULL = 0). */
 mpt_status mpt_rrt_add_nodes(mpt_rrt *rrt, const double *states, const int32_t *parents, int64_t n);
-/* Set the node count (truncate) without a host sync. */
+/* Set the node count (truncate) without a host sync: applied by the next round on its own
+ * stream (`stream` is unused) or before mpt_rrt_counters / mpt_rrt_add_nodes read the count. */
 mpt_status mpt_rrt_set_size(mpt_rrt *rrt, int64_t n, void *stream);
 /* One batched round: K uniform samples -> exact 1-NN -> randomSteer -> getPoses ->
  * collision -> ordered append of the collision-free edges.  Asynchronous. */

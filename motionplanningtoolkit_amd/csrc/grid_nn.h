@@ -74,14 +74,49 @@ GridParams make_grid_params(int32_t d, const int32_t *dims, int32_t gd, const do
 // of r.
 double expected_nn_distance(int32_t d, const double *lo, const double *hi, int64_t n);
 
+// Queries bucketed by their coordinate along one state dim (the grid's first dim), written by
+// extra workgroups of the index build's count launch (GridIndex::build with a QueryBucketing:
+// block-aggregated atomics, so the order inside a bucket is arbitrary; the work overlaps the
+// point count instead of adding a dependent step to the round).  The sorted 1-NN launch deals the bucket-major query order to
+// the XCDs in eight contiguous slices of equal size: each XCD then walks an x-slab of the
+// points (plus the neighbouring cells) through its own L2 instead of every XCD streaming the
+// whole point array, and no workgroup idles (the slices are cut by query count, not by x).
+// Results are per query and exact, so the order changes only speed.
+struct QueryOrder {
+    int32_t *count = nullptr;  // [nb * kQCountStride] queries per bucket; zero before the producer runs
+    int32_t *list = nullptr;   // [nb][cap] query indices per bucket
+    int32_t nb = 0, cap = 0;
+    int32_t dim = 0;           // state dim that orders the queries
+    double lo = 0.0, inv_w = 0.0;  // bucket = clamp(floor((x - lo) * inv_w), 0, nb - 1)
+};
+constexpr int32_t kQueryBuckets = 32;
+// bucket b's count lives at count[b * kQCountStride]: one 128-B line per counter, so the
+// producer's device atomics on different buckets do not serialise on one line
+constexpr int32_t kQCountStride = 32;
+
+__host__ __device__ __forceinline__ int32_t query_bucket(const QueryOrder &o, double x) {
+    double b = floor((x - o.lo) * o.inv_w);
+    b = b < 0.0 ? 0.0 : b;
+    b = b > (double)(o.nb - 1) ? (double)(o.nb - 1) : b;
+    return (int32_t)b;
+}
+
+// what GridIndex::build buckets alongside its point count
+struct QueryBucketing {
+    const double *q = nullptr;  // [nq][d] queries (state dim d, as the points)
+    int64_t nq = 0;
+    QueryOrder o;
+};
+
 class GridIndex {
 public:
     ~GridIndex();
     // Index points [0, min(n_upper, *n_dev)) of pts [.][d]; stream-ordered, no host sync.
     // spread (optional): also reduce the points' spread into spread->host_out (partial needs
     // ceil(n_upper / 256) * 6 slots).
+    // qb (optional): also bucket qb->nq queries into qb->o (counts zero on entry).
     void build(const double *pts, int64_t n_upper, const int64_t *n_dev, int32_t d, const GridParams &g,
-               hipStream_t stream, const SpreadOut *spread = nullptr);
+               hipStream_t stream, const SpreadOut *spread = nullptr, const QueryBucketing *qb = nullptr);
     GridDev dev() const;
     const GridParams &params() const { return g; }
     // allocate for up to cap_pts points and ncells cells now (allocation synchronises the
@@ -100,6 +135,11 @@ private:
 
 void launch_grid_knn(const GridDev &G, int32_t d, const double *q, int64_t nq, int32_t k, int32_t *ids, double *d2,
                      hipStream_t stream);
+
+// 1-NN of the nq queries listed by o (every query in exactly one bucket), results by query
+// index as launch_grid_knn with k = 1.
+void launch_grid_nn1_sorted(const GridDev &G, int32_t d, const double *q, int64_t nq, const QueryOrder &o,
+                            int32_t *ids, double *d2, hipStream_t stream);
 
 
 // Per-dim [min, max] of pts[0, n) into d_out[2*d] (lo0, hi0, lo1, hi1, ...).

@@ -20,6 +20,7 @@
 
 #include <hipcub/hipcub.hpp>
 
+#include "../../include/mpt.h"
 #include "grid_nn.h"
 #include "scan.h"
 
@@ -77,19 +78,56 @@ __device__ __forceinline__ void block_fold_spread(unsigned long long (&mn)[3], u
 // Cell of every live point + histogram.  kSpread: the same pass also reduces the points'
 // spread (SpreadOut) into one partial per block (plain stores, no fence: the scatter kernel
 // that follows in the stream folds them).
+// One workgroup's kQueriesPerBlock queries into their buckets: an LDS histogram, then one
+// device atomic per (workgroup, bucket) for the bucket's base, then each query's slot.  The
+// device atomics on one bucket serialise, so a workgroup takes 1024 queries (64 atomics per
+// bucket for 65536 queries instead of 256).
+constexpr int kQueriesPerThread = 4, kQueriesPerBlock = 256 * kQueriesPerThread;
+__device__ __forceinline__ void bucket_queries(const QueryBucketing &qb, int32_t d, int64_t first) {
+    __shared__ int32_t s_cnt[kQueryBuckets], s_base[kQueryBuckets];
+    const QueryOrder &o = qb.o;
+    if (threadIdx.x < kQueryBuckets) s_cnt[threadIdx.x] = 0;
+    __syncthreads();
+    int32_t b[kQueriesPerThread], rank[kQueriesPerThread];
+#pragma unroll
+    for (int h = 0; h < kQueriesPerThread; ++h) {
+        const int64_t k = first + h * 256 + threadIdx.x;
+        b[h] = -1;
+        rank[h] = 0;
+        if (k < qb.nq) {
+            b[h] = query_bucket(o, qb.q[k * d + o.dim]);
+            rank[h] = atomicAdd(&s_cnt[b[h]], 1);
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x < o.nb && s_cnt[threadIdx.x] > 0)
+        s_base[threadIdx.x] = atomicAdd(o.count + threadIdx.x * kQCountStride, s_cnt[threadIdx.x]);
+    __syncthreads();
+#pragma unroll
+    for (int h = 0; h < kQueriesPerThread; ++h)
+        if (b[h] >= 0) o.list[(int64_t)b[h] * o.cap + s_base[b[h]] + rank[h]] = (int32_t)(first + h * 256 + threadIdx.x);
+}
+
+// n_pt_blocks: the workgroups that count points; those after them bucket queries (qb)
 template <bool kSpread>
 __global__ __launch_bounds__(256) void k_grid_count(GridParams g, const double *__restrict__ pts, int32_t d,
                                                     int64_t n, const int64_t *__restrict__ n_dev,
                                                     int32_t *__restrict__ cell_of, int32_t *__restrict__ counts,
-                                                    SpreadOut sp) {
+                                                    SpreadOut sp, uint32_t n_pt_blocks, QueryBucketing qb) {
+    if (blockIdx.x >= n_pt_blocks) {  // workgroup-uniform
+        bucket_queries(qb, d, (int64_t)(blockIdx.x - n_pt_blocks) * kQueriesPerBlock);
+        return;
+    }
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (n_dev) n = *n_dev < n ? *n_dev : n;
     if (i < n) {
         int c[3] = {0, 0, 0};
         for (int j = 0; j < g.gd; ++j) c[j] = cell_coord(pts[i * d + g.dims[j]], g.lo[j], g.inv_h, g.n[j]);
         const int32_t cell = (c[0] * g.n[1] + c[1]) * g.n[2] + c[2];
-        cell_of[i] = cell;
-        atomicAdd(counts + cell, 1);
+        // the point's rank in its cell (arbitrary order: every result resolves ties by id), so
+        // the scatter places it without an atomic of its own
+        const int32_t rank = atomicAdd(counts + cell, 1);
+        reinterpret_cast<int2 *>(cell_of)[i] = make_int2(cell, rank);
     }
     if constexpr (kSpread) {
         __shared__ unsigned long long s_v[4][6], s_out[6];
@@ -111,7 +149,7 @@ __global__ __launch_bounds__(256) void k_grid_scatter(const double *__restrict__
                                                       const int64_t *__restrict__ n_dev,
                                                       const int32_t *__restrict__ cell_of,
                                                       const int32_t *__restrict__ cell_start,
-                                                      int32_t *__restrict__ cursor, double *__restrict__ spts,
+                                                      double *__restrict__ spts,
                                                       int32_t *__restrict__ sids, SpreadOut sp, int32_t n_part) {
     if constexpr (kSpread) {
         if (blockIdx.x == 0) {
@@ -135,10 +173,8 @@ __global__ __launch_bounds__(256) void k_grid_scatter(const double *__restrict__
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (n_dev) n = *n_dev < n ? *n_dev : n;
     if (i >= n) return;
-    const int32_t cell = cell_of[i];
-    // the cursor counts the cell down from its size, so every count is zero again when the
-    // scatter ends and the next build needs no memset
-    const int64_t pos = cell_start[cell] + (atomicSub(cursor + cell, 1) - 1);
+    const int2 cr = reinterpret_cast<const int2 *>(cell_of)[i];
+    const int64_t pos = (int64_t)cell_start[cr.x] + cr.y;
     // record of d + 1 doubles: the coordinates, then the 1-based id in the pad slot, so a
     // query reads a point and its id from one 32 / 64 / 128-B aligned record
     double *rec = spts + pos * grid_stride(d);
@@ -148,6 +184,14 @@ __global__ __launch_bounds__(256) void k_grid_scatter(const double *__restrict__
     else
         sids[pos] = (int32_t)(i + 1);
 }
+
+// scan epilogue of the grid build: each count back to zero once scanned
+struct ZeroCounts {
+    uint32_t *counts;
+    __device__ void operator()(int64_t i, uint32_t, uint32_t v) const {
+        if (v) counts[i] = 0u;
+    }
+};
 
 template <int KMAX>
 __device__ __forceinline__ void grid_push(double (&bd)[KMAX], int32_t (&bi)[KMAX], int32_t k, double dd, int32_t id) {
@@ -317,7 +361,7 @@ void GridIndex::reserve(int64_t cap_pts, int32_t d, int64_t ncells) {
         const int64_t c = cap_pts > 0 ? cap_pts : 1;
         hip_check(hipMalloc(&spts, sizeof(double) * c * grid_stride(d)), "grid pts");
         if (grid_stride(d) == d) hip_check(hipMalloc(&sids, sizeof(int32_t) * c), "grid ids");
-        hip_check(hipMalloc(&cell_of, sizeof(int32_t) * c), "grid cell_of");
+        hip_check(hipMalloc(&cell_of, sizeof(int32_t) * 2 * c), "grid cell_of");  // (cell, rank) pairs
         pts_cap = c;
         dim = d;
     }
@@ -345,36 +389,39 @@ GridIndex::~GridIndex() {
 }
 
 void GridIndex::build(const double *pts, int64_t n_upper, const int64_t *n_dev, int32_t d, const GridParams &gp,
-                      hipStream_t stream, const SpreadOut *spread) {
+                      hipStream_t stream, const SpreadOut *spread, const QueryBucketing *qb) {
     if (gp.ncells >= (int64_t(1) << 31) - 1) throw Error{5, "grid too large"};
     reserve(n_upper, d, gp.ncells);
     g = gp;
     n_max = n_upper;
     if (!counts_zero) hip_check(hipMemsetAsync(counts, 0, sizeof(int32_t) * (size_t)cells_cap, stream), "grid memset");
     counts_zero = false;
-    if (n_upper > 0) {
+    const unsigned qblocks = qb ? (unsigned)((qb->nq + kQueriesPerBlock - 1) / kQueriesPerBlock) : 0u;
+    if (n_upper > 0 || qblocks > 0) {
         const unsigned blocks = (unsigned)((n_upper + 255) / 256);
+        const QueryBucketing q = qb ? *qb : QueryBucketing{};
         if (spread)
-            hipLaunchKernelGGL(k_grid_count<true>, dim3(blocks), dim3(256), 0, stream, g, pts, d, n_upper, n_dev,
-                               cell_of, counts, *spread);
+            hipLaunchKernelGGL(k_grid_count<true>, dim3(blocks + qblocks), dim3(256), 0, stream, g, pts, d, n_upper,
+                               n_dev, cell_of, counts, *spread, blocks, q);
         else
-            hipLaunchKernelGGL(k_grid_count<false>, dim3(blocks), dim3(256), 0, stream, g, pts, d, n_upper, n_dev,
-                               cell_of, counts, SpreadOut{});
+            hipLaunchKernelGGL(k_grid_count<false>, dim3(blocks + qblocks), dim3(256), 0, stream, g, pts, d, n_upper,
+                               n_dev, cell_of, counts, SpreadOut{}, blocks, q);
         hip_check(hipGetLastError(), "k_grid_count");
     }
+    // the scan leaves every count zero again, so the next build needs no memset
     launch_scan_excl(scan, reinterpret_cast<const uint32_t *>(counts), reinterpret_cast<uint32_t *>(cell_start),
-                     g.ncells + 1, stream, NoEpilogue{});
+                     g.ncells + 1, stream, ZeroCounts{reinterpret_cast<uint32_t *>(counts)});
     if (n_upper > 0) {
         const unsigned blocks = (unsigned)((n_upper + 255) / 256);
         if (spread)
             hipLaunchKernelGGL(k_grid_scatter<true>, dim3(blocks), dim3(256), 0, stream, pts, d, n_upper, n_dev,
-                               cell_of, cell_start, counts, spts, sids, *spread, (int32_t)blocks);
+                               cell_of, cell_start, spts, sids, *spread, (int32_t)blocks);
         else
             hipLaunchKernelGGL(k_grid_scatter<false>, dim3(blocks), dim3(256), 0, stream, pts, d, n_upper, n_dev,
-                               cell_of, cell_start, counts, spts, sids, SpreadOut{}, 0);
+                               cell_of, cell_start, spts, sids, SpreadOut{}, 0);
         hip_check(hipGetLastError(), "k_grid_scatter");
     }
-    counts_zero = true;  // k_grid_scatter counted every cell back down (nothing counted when n_upper == 0)
+    counts_zero = true;  // the scan zeroed every count it read
 }
 
 GridDev GridIndex::dev() const {
@@ -563,19 +610,90 @@ __global__ __launch_bounds__(256) void k_grid_nn1_group(GridDev G, int32_t d, co
     nn1_group_query<D, kGroup, kFirst>(G, d, q, slot, (int)(t % kGroup), out_ids, out_d2);
 }
 
+// Group primitives for the run kernels: a group is kGroup aligned lanes of a wave.  A 16-lane
+// group is one DPP row, so its scans and reductions are row-local DPP moves (VALU, no LDS
+// round trip: row_shr for the scan, row_ror for the all-reduce); wider groups use shuffles.
+template <int kGroup>
+__device__ __forceinline__ int32_t grp_incl_scan(int32_t v, int sub) {
+    if constexpr (kGroup == 16) {
+        (void)sub;
+        v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xf, 0xf, false);  // row_shr:1 (0 past the row start)
+        v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xf, 0xf, false);  // row_shr:2
+        v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xf, 0xf, false);  // row_shr:4
+        v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xf, 0xf, false);  // row_shr:8
+        return v;
+    } else {
+#pragma unroll
+        for (int off = 1; off < kGroup; off <<= 1) {
+            const int32_t o = __shfl_up(v, off, kGroup);
+            if (sub >= off) v += o;
+        }
+        return v;
+    }
+}
+
+template <int kGroup>
+__device__ __forceinline__ int32_t grp_last(int32_t v) {
+    if constexpr (kGroup == 16) return __builtin_amdgcn_update_dpp(0, v, 0x15F, 0xf, 0xf, false);  // row_newbcast:15
+    else return __shfl(v, kGroup - 1, kGroup);
+}
+
+template <int CTRL>
+__device__ __forceinline__ void dpp_merge_step(double &bd, int32_t &bi) {
+    const int32_t lo = __builtin_amdgcn_update_dpp(0, __double2loint(bd), CTRL, 0xf, 0xf, false);
+    const int32_t hi = __builtin_amdgcn_update_dpp(0, __double2hiint(bd), CTRL, 0xf, 0xf, false);
+    const int32_t oi = __builtin_amdgcn_update_dpp(0, bi, CTRL, 0xf, 0xf, false);
+    const double od = __hiloint2double(hi, lo);
+    if (nn_better(od, oi, bd, bi)) {
+        bd = od;
+        bi = oi;
+    }
+}
+
+// every lane of the group ends with the group's best (d2, id) in (d2, id) order
+template <int kGroup>
+__device__ __forceinline__ void grp_merge_best(double &bd, int32_t &bi) {
+    if constexpr (kGroup == 16) {
+        // rotations within the row: after ror 8, 4, 2, 1 each lane has seen all 16
+        dpp_merge_step<0x128>(bd, bi);
+        dpp_merge_step<0x124>(bd, bi);
+        dpp_merge_step<0x122>(bd, bi);
+        dpp_merge_step<0x121>(bd, bi);
+    } else {
+#pragma unroll
+        for (int off = kGroup / 2; off > 0; off >>= 1) {
+            const double od = __shfl_xor(bd, off, kGroup);
+            const int32_t oi = __shfl_xor(bi, off, kGroup);
+            if (nn_better(od, oi, bd, bi)) {
+                bd = od;
+                bi = oi;
+            }
+        }
+    }
+}
+
+// small non-negative integer quotient by a run-time divisor through f32 (exact while
+// a * side < 2^20: (a + 0.5) / side is at least 0.5 / side from an integer)
+__device__ __forceinline__ int small_div(int a, int side, float inv_side) {
+    (void)side;
+    return (int)(((float)a + 0.5f) * inv_side);
+}
+
 // 1-NN over runs of cells.  Cells are laid out with the last grid dim contiguous, so the
 // cells of a pass that share their other coordinates form one run whose points are one
 // contiguous range [cell_start[first], cell_start[last + 1]):
-//   * first pass (r = 1, the 3^gd block): (2r+1)^(gd-1) runs of 2r+1 cells;
+//   * first pass (r = 1, the 3^GD block): 3^(GD-1) runs of 3 cells, one step of the group;
 //   * ring r >= 2: border columns give a full run of 2r+1 cells, interior columns only the
 //     two cells at +-r (two single-cell runs).
-// Each lane of the group takes run slots (2 per column), prunes a run whose box is farther
-// than its best so far, and loads the run's [start, end).  A shuffle scan of the run lengths
-// then spreads the pass's points evenly over the group, two per lane per step, both loads in
-// flight together (a lane no longer walks a whole cell point after point: the slowest lane
-// of the old cell-per-lane walk set every wave's time).  Merge, ring bound and (d2, id)
-// order as nn1_group_query, so results are identical bit for bit.
-template <int D, int kGroup, int kPts>
+// Each lane of the group takes run slots, prunes a run whose box is farther than its best so
+// far (not in the first pass: nothing is known yet), and loads the run's [start, end).  A scan
+// of the run lengths then spreads the pass's points evenly over the group (a per-lane binary
+// search over the scanned prefixes maps a flat index to its run; the lane of the group's
+// longest run no longer sets every wave's time).  GD (the grid dims) is a template argument,
+// so every per-dim loop is unrolled and the query's grid coordinates come from registers.
+// The merge is in (d2, id) order and the stop test is the ring bound, so the result is the
+// brute-force result bit for bit.
+template <int D, int GD, int kGroup, int kPts>
 __device__ __forceinline__ void nn1_runs_query(const GridDev &G, const double *__restrict__ q, int64_t qi, int sub,
                                                int32_t *__restrict__ out_ids, double *__restrict__ out_d2) {
     const GridParams &g = G.g;
@@ -584,12 +702,18 @@ __device__ __forceinline__ void nn1_runs_query(const GridDev &G, const double *_
     for (int i = 0; i < D; ++i) qq[i] = q[qi * D + i];
     double qg[3] = {0, 0, 0};
     int cq[3] = {0, 0, 0};
-    const int gd = g.gd, zl = g.gd - 1;  // zl: the run (contiguous) dim
-    for (int j = 0; j < gd; ++j) {
-        const double x = q[qi * D + g.dims[j]];
+    constexpr int zl = GD - 1;  // the run (contiguous) dim
+#pragma unroll
+    for (int j = 0; j < GD; ++j) {
+        double x = qq[0];
+#pragma unroll
+        for (int i = 1; i < D; ++i)
+            if (i == g.dims[j]) x = qq[i];
         qg[j] = x;
         cq[j] = cell_coord(x, g.lo[j], g.inv_h, g.n[j]);
     }
+    // the lane's base address for ds_bpermute inside its group
+    const int grp_base = (int)((threadIdx.x & 63) & ~(kGroup - 1)) << 2;
     double bd = __builtin_huge_val();
     int32_t bi = -1;
     uint32_t n_pts = 0, n_cells = 0;
@@ -602,57 +726,69 @@ __device__ __forceinline__ void nn1_runs_query(const GridDev &G, const double *_
     };
     for (int r = 1;; ++r) {
         const int side = 2 * r + 1;
-        const int ncol = gd == 3 ? side * side : (gd == 2 ? side : 1);
-        for (int base = 0; base < 2 * ncol; base += kGroup) {
+        const float inv_side = 1.0f / (float)side, inv_in = r > 1 ? 1.0f / (float)(side - 2) : 0.f;
+        const int ncol = GD == 3 ? side * side : (GD == 2 ? side : 1);
+        // run slots: one per column (the full run of a border column, or of every column in
+        // the first pass; an interior column's -r cell), then one per interior column for its
+        // +r cell
+        const int nint = r == 1 ? 0 : (GD == 3 ? (side - 2) * (side - 2) : (GD == 2 ? side - 2 : 1));
+        const int nslot = ncol + nint;
+        for (int base = 0; base < nslot; base += kGroup) {
             const int u = base + sub;
             int32_t s = 0, len = 0;
-            if (u < 2 * ncol) {
-                const int col = u >> 1, part = u & 1;
+            if (u < nslot) {
+                const int part = u >= ncol ? 1 : 0;
                 int o0 = 0, o1 = 0;
-                if (gd == 3) {
-                    o0 = col / side - r;
-                    o1 = col % side - r;
-                } else if (gd == 2) {
-                    o0 = col - r;
+                if (!part) {
+                    if constexpr (GD == 3) {
+                        const int a = small_div(u, side, inv_side);
+                        o0 = a - r;
+                        o1 = u - a * side - r;
+                    } else if constexpr (GD == 2) {
+                        o0 = u - r;
+                    }
+                } else {
+                    const int v = u - ncol;  // interior column v
+                    if constexpr (GD == 3) {
+                        const int a = small_div(v, side - 2, inv_in);
+                        o0 = a + 1 - r;
+                        o1 = v - a * (side - 2) + 1 - r;
+                    } else if constexpr (GD == 2) {
+                        o0 = v + 1 - r;
+                    }
                 }
-                const bool border = gd == 3 ? (abs(o0) == r || abs(o1) == r) : (gd == 2 ? abs(o0) == r : false);
+                const bool border = GD == 3 ? (abs(o0) == r || abs(o1) == r) : (GD == 2 ? abs(o0) == r : false);
                 const bool full = r == 1 || border;
-                bool ok = !(full && part);
                 int z0 = cq[zl] + (full ? -r : (part ? r : -r));
                 int z1 = cq[zl] + (full ? r : (part ? r : -r));
                 z0 = z0 < 0 ? 0 : z0;
                 z1 = z1 > g.n[zl] - 1 ? g.n[zl] - 1 : z1;
-                ok = ok && z0 <= z1;
+                bool ok = z0 <= z1;
                 int c0 = 0, c1 = 0;
-                if (gd >= 2) {
+                if constexpr (GD >= 2) {
                     c0 = cq[0] + o0;
                     ok = ok && c0 >= 0 && c0 < g.n[0];
                 }
-                if (gd == 3) {
+                if constexpr (GD == 3) {
                     c1 = cq[1] + o1;
                     ok = ok && c1 >= 0 && c1 < g.n[1];
                 }
-                if (ok) {
+                if (ok && r > 1) {
                     double lb2 = gap(zl, z0, z1);
-                    if (gd >= 2) lb2 += gap(0, c0, c0);
-                    if (gd == 3) lb2 += gap(1, c1, c1);
+                    if constexpr (GD >= 2) lb2 += gap(0, c0, c0);
+                    if constexpr (GD == 3) lb2 += gap(1, c1, c1);
                     // the 1e-12 shrink covers the different summation order of FLANN's distance
-                    if (lb2 * (1.0 - 1e-12) <= bd) {
-                        const int32_t cell0 = gd == 3 ? (c0 * g.n[1] + c1) * g.n[2] + z0 : (gd == 2 ? c0 * g.n[1] + z0 : z0);
-                        s = G.cell_start[cell0];
-                        len = G.cell_start[cell0 + (z1 - z0) + 1] - s;
-                        n_cells += (uint32_t)(z1 - z0 + 1);
-                    }
+                    ok = lb2 * (1.0 - 1e-12) <= bd;
+                }
+                if (ok) {
+                    const int32_t cell0 = GD == 3 ? (c0 * g.n[1] + c1) * g.n[2] + z0 : (GD == 2 ? c0 * g.n[1] + z0 : z0);
+                    s = G.cell_start[cell0];
+                    len = G.cell_start[cell0 + (z1 - z0) + 1] - s;
+                    n_cells += (uint32_t)(z1 - z0 + 1);
                 }
             }
-            // inclusive scan of the lengths over the group
-            int32_t incl = len;
-#pragma unroll
-            for (int off = 1; off < kGroup; off <<= 1) {
-                const int32_t o = __shfl_up(incl, off, kGroup);
-                if (sub >= off) incl += o;
-            }
-            const int32_t total = __shfl(incl, kGroup - 1, kGroup);
+            const int32_t incl = grp_incl_scan<kGroup>(len, sub);
+            const int32_t total = grp_last<kGroup>(incl);
             const int32_t shift = s - (incl - len);  // point index = shift[run] + flat index
             for (int32_t t = 0; t < total; t += kPts * kGroup) {
                 int32_t p[kPts];
@@ -664,13 +800,13 @@ __device__ __forceinline__ void nn1_runs_query(const GridDev &G, const double *_
 #pragma unroll
                     for (int step = kGroup; step > 1; step >>= 1) {
                         const int mid = (lo + hi) >> 1;
-                        const int32_t v = __shfl(incl, mid, kGroup);
+                        const int32_t v = __builtin_amdgcn_ds_bpermute(grp_base + (mid << 2), incl);
                         if (v > idx) hi = mid;
                         else lo = mid + 1;
                     }
-                    // the shuffle runs on every lane of the group (a lane past the end still
+                    // every lane of the group runs the permute (a lane past the end still
                     // serves as a source: ds_bpermute reads nothing from inactive lanes)
-                    const int32_t sh = __shfl(shift, lo, kGroup);
+                    const int32_t sh = __builtin_amdgcn_ds_bpermute(grp_base + (lo << 2), shift);
                     p[h] = idx < total ? sh + idx : -1;
                 }
                 double dd[kPts];
@@ -695,17 +831,25 @@ __device__ __forceinline__ void nn1_runs_query(const GridDev &G, const double *_
                 }
             }
         }
+        grp_merge_best<kGroup>(bd, bi);
+        // lower bound on the distance (along the grid dims) from q to any cell outside the
+        // ring-r block; stop once it exceeds the best (or every cell has been visited)
+        double lb = __builtin_huge_val();
+        bool more = false;
 #pragma unroll
-        for (int off = kGroup / 2; off > 0; off >>= 1) {
-            const double od = __shfl_xor(bd, off, kGroup);
-            const int32_t oi = __shfl_xor(bi, off, kGroup);
-            if (nn_better(od, oi, bd, bi)) {
-                bd = od;
-                bi = oi;
+        for (int j = 0; j < GD; ++j) {
+            if (cq[j] - r > 0) {
+                more = true;
+                lb = fmin(lb, qg[j] - (g.lo[j] + (double)(cq[j] - r) * g.h));
+            }
+            if (cq[j] + r + 1 < g.n[j]) {
+                more = true;
+                lb = fmin(lb, g.lo[j] + (double)(cq[j] + r + 1) * g.h - qg[j]);
             }
         }
-        const double lb = ring_bound(g, qg, cq, r);
-        if (lb < 0.0) break;  // every cell visited
+        if (!more) break;  // every cell visited
+        lb -= g.slack;
+        lb = lb > 0.0 ? lb : 0.0;
         if (lb * lb > bd) break;
     }
     if (G.stats) {
@@ -726,13 +870,13 @@ __device__ __forceinline__ void nn1_runs_query(const GridDev &G, const double *_
 }
 
 // kPts: points per lane per step (loads in flight together)
-template <int D, int kGroup, int kPts>
+template <int D, int GD, int kGroup, int kPts>
 __global__ __launch_bounds__(256) void k_grid_nn1_runs(GridDev G, const double *__restrict__ q, int64_t nq,
                                                        int32_t *__restrict__ out_ids, double *__restrict__ out_d2) {
     const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int64_t slot = t / kGroup;
     if (slot >= nq) return;  // whole groups leave together (nq is per group)
-    nn1_runs_query<D, kGroup, kPts>(G, q, slot, (int)(t % kGroup), out_ids, out_d2);
+    nn1_runs_query<D, GD, kGroup, kPts>(G, q, slot, (int)(t % kGroup), out_ids, out_d2);
 }
 
 // XCD-aware variant.  The points are in cell order, x-major, so the cells of an x-slab
@@ -740,11 +884,12 @@ __global__ __launch_bounds__(256) void k_grid_nn1_runs(GridDev G, const double *
 // dealt round-robin over the 8 XCDs, so workgroup b and b + 8 share an XCD (and its 4 MiB
 // L2): workgroup b serves slab b % 8 and scans the chunk b / 8 of kSlabChunk queries for
 // the ones whose cell lies in its slab.  Each XCD's L2 then holds about an eighth of the
-// tree (plus the neighbouring cells), instead of every XCD streaming the whole 5.6 MB tree
+// tree (plus the neighbouring cells), instead of every XCD streaming the whole point array
 // through its L2.  Queries whose walk leaves the slab are still exact (placement only
 // changes speed).  About 3/4 of the groups have a query per chunk (the chunk holds 6 NG
-// queries for NG groups; more than NG of one slab take a second turn).
-template <int D, int kGroup, int kPts>
+// queries for NG groups; more than NG of one slab take a second turn).  The engine's
+// bucket-sorted launch (k_grid_nn1_runs_sorted) replaces it when the queries come bucketed.
+template <int D, int GD, int kGroup, int kPts>
 __global__ __launch_bounds__(256) void k_grid_nn1_runs_xcd(GridDev G, const double *__restrict__ q, int64_t nq,
                                                            int32_t *__restrict__ out_ids,
                                                            double *__restrict__ out_d2) {
@@ -769,7 +914,110 @@ __global__ __launch_bounds__(256) void k_grid_nn1_runs_xcd(GridDev G, const doub
     __syncthreads();
     const int total = s_cnt[0] + (kChunk > 64 ? s_cnt[1] : 0);
     const int grp = threadIdx.x / kGroup, sub = threadIdx.x % kGroup;
-    for (int i = grp; i < total; i += NG) nn1_runs_query<D, kGroup, kPts>(G, q, s_idx[i], sub, out_ids, out_d2);
+    for (int i = grp; i < total; i += NG) nn1_runs_query<D, GD, kGroup, kPts>(G, q, s_idx[i], sub, out_ids, out_d2);
+}
+
+// Bucket-sorted 1-NN (QueryOrder): workgroup b runs on XCD b % 8 and takes slice b % 8,
+// chunk b / 8 of the bucket-major query order; a query's index comes from its bucket's list.
+template <int D, int GD, int kGroup, int kPts>
+__global__ __launch_bounds__(256) void k_grid_nn1_runs_sorted(GridDev G, const double *__restrict__ q, int64_t nq,
+                                                              QueryOrder o, int32_t *__restrict__ out_ids,
+                                                              double *__restrict__ out_d2) {
+    __shared__ int32_t s_pre[kQueryBuckets + 1];
+    if (threadIdx.x < 64) {
+        const int lane = threadIdx.x;
+        int32_t incl = lane < o.nb ? o.count[lane * kQCountStride] : 0;
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+            const int32_t v = __shfl_up(incl, off);
+            if (lane >= off) incl += v;
+        }
+        if (lane < o.nb) s_pre[lane + 1] = incl;
+        if (lane == 0) s_pre[0] = 0;
+    }
+    __syncthreads();
+    constexpr int QPW = 256 / kGroup;  // queries per workgroup
+    const int64_t per_xcd = (int64_t)(gridDim.x >> 3);  // gridDim.x is a multiple of 8
+    const int64_t wg = (int64_t)(blockIdx.x & 7) * per_xcd + (blockIdx.x >> 3);
+    const int64_t pos = wg * QPW + threadIdx.x / kGroup;
+    if (pos >= nq) return;  // whole groups leave together
+    // bucket of pos: binary search over the prefix (nb <= 32: five LDS reads)
+    int lo = 0, hi = o.nb - 1;
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (s_pre[mid] <= pos) lo = mid;
+        else hi = mid - 1;
+    }
+    const int64_t qi = o.list[(int64_t)lo * o.cap + (pos - s_pre[lo])];
+    nn1_runs_query<D, GD, kGroup, kPts>(G, q, qi, (int)(threadIdx.x % kGroup), out_ids, out_d2);
+}
+
+// run-kernel group shape per state dim: 16 lanes x 1 point for d <= 7 (config 2: 54.7 us vs
+// 58.2 us at 32 x 2); 32 lanes x 2 points for the snake's d = 15 (0.85 ms vs 0.90 ms at 16 x 2)
+template <int D>
+struct RunShape {
+    static constexpr int kGroup = D >= 15 ? 32 : 16, kPts = D >= 15 ? 2 : 1;
+};
+
+template <int D, int GD>
+static void grid_nn1_sorted_dg(const GridDev &G, const double *q, int64_t nq, const QueryOrder &o, int32_t *ids,
+                               double *d2, hipStream_t stream) {
+    constexpr int GRP = RunShape<D>::kGroup, PTS = RunShape<D>::kPts;
+    constexpr int QPW = 256 / GRP;
+    int64_t wgs = (nq + QPW - 1) / QPW;
+    wgs = (wgs + 7) / 8 * 8;
+    hipLaunchKernelGGL((k_grid_nn1_runs_sorted<D, GD, GRP, PTS>), dim3((unsigned)wgs), dim3(256), 0, stream, G, q, nq,
+                       o, ids, d2);
+}
+
+template <int D>
+static void grid_nn1_sorted_d(const GridDev &G, const double *q, int64_t nq, const QueryOrder &o, int32_t *ids,
+                              double *d2, hipStream_t stream) {
+    switch (G.g.gd) {
+        case 1: grid_nn1_sorted_dg<D, 1>(G, q, nq, o, ids, d2, stream); break;
+        case 2: grid_nn1_sorted_dg<D, 2>(G, q, nq, o, ids, d2, stream); break;
+        default: grid_nn1_sorted_dg<D, 3>(G, q, nq, o, ids, d2, stream); break;
+    }
+}
+
+void launch_grid_nn1_sorted(const GridDev &G, int32_t d, const double *q, int64_t nq, const QueryOrder &o,
+                            int32_t *ids, double *d2, hipStream_t stream) {
+    if (nq <= 0) return;
+    if (o.nb < 1 || o.nb > kQueryBuckets || !o.count || !o.list) throw Error{MPT_ERR_INVALID, "bad query order"};
+    switch (d) {
+        case 3: grid_nn1_sorted_d<3>(G, q, nq, o, ids, d2, stream); break;
+        case 7: grid_nn1_sorted_d<7>(G, q, nq, o, ids, d2, stream); break;
+        case 15: grid_nn1_sorted_d<15>(G, q, nq, o, ids, d2, stream); break;
+        default: throw Error{MPT_ERR_INVALID, "sorted 1-NN: d must be 3, 7 or 15"};
+    }
+    hip_check(hipGetLastError(), "k_grid_nn1_runs_sorted launch");
+}
+
+// unsorted run-kernel launch; xcd: the slab variant (default for d = 15: the snake's 12 MB of
+// points are three L2s' worth, NN 0.85 -> 0.72 ms; config 2's tree gains less than the idle
+// groups cost, 54 -> 65 us).  MPT_NN1_XCD=0/1 overrides (scripts/ab.sh)
+template <int D, int GD>
+static void grid_nn1_runs_dg(const GridDev &G, const double *q, int64_t nq, int32_t *ids, double *d2,
+                             hipStream_t stream) {
+    constexpr int GRP = RunShape<D>::kGroup, PTS = RunShape<D>::kPts;
+    static const bool xcd = getenv("MPT_NN1_XCD") ? atoi(getenv("MPT_NN1_XCD")) == 1 : D >= 15;
+    if (xcd)
+        hipLaunchKernelGGL((k_grid_nn1_runs_xcd<D, GD, GRP, PTS>),
+                           dim3((unsigned)(((nq + 6 * (256 / GRP) - 1) / (6 * (256 / GRP))) * 8)), dim3(256), 0,
+                           stream, G, q, nq, ids, d2);
+    else
+        hipLaunchKernelGGL((k_grid_nn1_runs<D, GD, GRP, PTS>), dim3((unsigned)((nq * GRP + 255) / 256)), dim3(256), 0,
+                           stream, G, q, nq, ids, d2);
+}
+
+template <int D>
+static void grid_nn1_runs_d(const GridDev &G, const double *q, int64_t nq, int32_t *ids, double *d2,
+                            hipStream_t stream) {
+    switch (G.g.gd) {
+        case 1: grid_nn1_runs_dg<D, 1>(G, q, nq, ids, d2, stream); break;
+        case 2: grid_nn1_runs_dg<D, 2>(G, q, nq, ids, d2, stream); break;
+        default: grid_nn1_runs_dg<D, 3>(G, q, nq, ids, d2, stream); break;
+    }
 }
 
 template <int D>
@@ -786,32 +1034,13 @@ static void grid_knn_d(const GridDev &G, int32_t d, const double *q, int64_t nq,
                        stream, G, d, q, nq, ids, d2)
     // cell-run kernel (default); MPT_NN1_KERNEL=cells: the cell-per-lane walk (A/B)
     static const bool cells = getenv("MPT_NN1_KERNEL") && !strcmp(getenv("MPT_NN1_KERNEL"), "cells");
-    if (k == 1 && !per_lane && !cells && D > 0) {
-        constexpr int DD = D > 0 ? D : 1;
-        // defaults from the A/B runs (scripts/measure_nnruns.sh): 16 lanes, one point per step
-        // for d <= 7 (config 2: 54.7 us vs 58.2 us at 32 x 2); 32 lanes, two points per step
-        // for the snake's d = 15 (0.85 ms vs 0.90 ms at 16 x 2)
-        static const int pts = getenv("MPT_NN1_PTS") ? atoi(getenv("MPT_NN1_PTS")) : (D >= 15 ? 2 : 1);
-        const int rgroup = getenv("MPT_NN1_GROUP") ? group : (D >= 15 ? 32 : 16);
-        // XCD-slab variant for the snake's d = 15 (12 MB of points, three L2s' worth: NN 0.85 ->
-        // 0.72 ms); config 2's 5.6 MB tree gains less than the idle groups cost (54 -> 65 us).
-        // MPT_NN1_XCD=0/1 overrides (scripts/ab_nnxcd.sh)
-        static const bool xcd = getenv("MPT_NN1_XCD") ? atoi(getenv("MPT_NN1_XCD")) == 1 : D >= 15;
-#define MPT_NN1_RUNS_LAUNCH(GRP, PTS)                                                                            \
-    if (xcd)                                                                                                     \
-        hipLaunchKernelGGL((k_grid_nn1_runs_xcd<DD, GRP, PTS>),                                                  \
-                           dim3((unsigned)(((nq + 6 * (256 / GRP) - 1) / (6 * (256 / GRP))) * 8)), dim3(256), 0, \
-                           stream, G, q, nq, ids, d2);                                                           \
-    else                                                                                                         \
-        hipLaunchKernelGGL((k_grid_nn1_runs<DD, GRP, PTS>), dim3((unsigned)((nq * GRP + 255) / 256)), dim3(256), \
-                           0, stream, G, q, nq, ids, d2)
-        if (rgroup == 16) {
-            if (pts == 1) { MPT_NN1_RUNS_LAUNCH(16, 1); } else { MPT_NN1_RUNS_LAUNCH(16, 2); }
-        } else {
-            if (pts == 1) { MPT_NN1_RUNS_LAUNCH(32, 1); } else { MPT_NN1_RUNS_LAUNCH(32, 2); }
+    if constexpr (D > 0) {
+        if (k == 1 && !per_lane && !cells) {
+            grid_nn1_runs_d<D>(G, q, nq, ids, d2, stream);
+            return;
         }
-#undef MPT_NN1_RUNS_LAUNCH
-    } else if (k == 1 && !per_lane && group == 32) {
+    }
+    if (k == 1 && !per_lane && group == 32) {
         if (first) MPT_NN1_GROUP_LAUNCH(32, 1); else MPT_NN1_GROUP_LAUNCH(32, 0);
     } else if (k == 1 && !per_lane && group == 8) {
         MPT_NN1_GROUP_LAUNCH(8, 0);

@@ -130,10 +130,19 @@ __device__ void snake_poses(const double *prm, int T, const double *s, double *o
 
 // n_dev[1] = n_dev[0]: the round's starting node count, read by k_append_commit (which
 // overwrites n_dev[0] in the same launch)
+// n_dev[1] = n_dev[0]: the round's starting node count, read by k_append_commit (which
+// overwrites n_dev[0] in the same launch)
+// set_n >= 0: a truncation left by mpt_rrt_set_size, applied first (k_set_n folded into the
+// round's first launch)
 __global__ void k_sample(EngineParams p, uint64_t ext_base, int32_t K, double *__restrict__ samples,
-                         int64_t *__restrict__ n_dev, uint32_t *__restrict__ n_live) {
+                         int64_t *__restrict__ n_dev, uint32_t *__restrict__ n_live, int64_t set_n,
+                         unsigned long long *__restrict__ counters) {
     const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (k == 0) {
+        if (set_n >= 0) {
+            n_dev[0] = set_n;
+            counters[3] = (unsigned long long)set_n;
+        }
         n_dev[1] = n_dev[0];
         if (n_live) *n_live = 0u;  // k_steer's live-unit list of this round
     }
@@ -254,6 +263,8 @@ struct LiveOut {
     uint32_t *n_live;    // zeroed by k_sample
     const AgentDev *links;
     EnvDev env;
+    int32_t *q_count;    // the round's QueryOrder counts (read by the NN launch): zeroed here
+    int32_t q_nb;
 };
 
 // randomSteer + getPoses, then the extension's live units appended to the round's list
@@ -267,6 +278,7 @@ __global__ __launch_bounds__(256) void k_steer(EngineParams p, uint64_t ext_base
     const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     int32_t P = 0;
     if (k < K) P = steer_one<KIND>(p, ext_base, k, nodes, nn, ends, poses, pcount, verdict, counters);
+    if (lv.q_count && k < lv.q_nb) lv.q_count[k * kQCountStride] = 0;  // the NN launch has run: next round's k_sample counts
     if (!lv.list) return;  // kernel argument: uniform
     const int32_t units = p.pmax * p.L;  // <= 64 (the launcher checks)
     uint64_t mask = 0;
@@ -409,6 +421,12 @@ struct mpt_rrt {
     CollideScratch cscratch;
     int32_t max_clusters = 1;
     unsigned long long *d_cstats = nullptr;
+    // grid rounds: the samples bucketed along the grid's first dim (QueryOrder, grid_nn.h)
+    int32_t *d_qcount = nullptr, *d_qlist = nullptr;
+    int32_t q_cap = 0;
+    // mpt_rrt_set_size's node count, applied by the next round's k_sample (or by flush_size
+    // before the host reads the count); -1: none
+    int64_t pending_n = -1;
 };
 
 namespace {
@@ -421,6 +439,8 @@ void rfree(mpt_rrt *r) {
     for (auto &e : r->ring)
         if (e) (void)hipEventDestroy(e);
     if (r->d_spread) (void)hipFree(r->d_spread);
+    if (r->d_qcount) (void)hipFree(r->d_qcount);
+    if (r->d_qlist) (void)hipFree(r->d_qlist);
     if (r->h_spread) (void)hipHostFree(r->h_spread);
     if (r->ev_spread) (void)hipEventDestroy(r->ev_spread);
 }
@@ -539,10 +559,23 @@ extern "C" mpt_status mpt_rrt_destroy(mpt_rrt *r) {
     });
 }
 
+namespace {
+// apply a pending mpt_rrt_set_size before the host reads the node count or the counters
+void flush_size(mpt_rrt *r) {
+    hip_check(hipDeviceSynchronize(), "sync");
+    if (r->pending_n >= 0) {
+        hipLaunchKernelGGL(k_set_n, dim3(1), dim3(1), 0, 0, r->d_n, r->pending_n, r->d_counters);
+        hip_check(hipGetLastError(), "k_set_n");
+        hip_check(hipDeviceSynchronize(), "sync");
+        r->pending_n = -1;
+    }
+}
+}  // namespace
+
 extern "C" mpt_status mpt_rrt_add_nodes(mpt_rrt *r, const double *states, const int32_t *parents, int64_t n) {
     return guarded([&] {
         if (!r || n < 0 || (n > 0 && !states)) throw Error{MPT_ERR_INVALID, "bad arguments"};
-        hip_check(hipDeviceSynchronize(), "sync");
+        flush_size(r);
         int64_t cur = 0;
         hip_check(hipMemcpy(&cur, r->d_n, sizeof(int64_t), hipMemcpyDeviceToHost), "n D2H");
         if (cur + n > r->cap) throw Error{MPT_ERR_CAPACITY, "tree capacity exceeded"};
@@ -566,8 +599,10 @@ extern "C" mpt_status mpt_rrt_set_size(mpt_rrt *r, int64_t n, void *stream) {
     return guarded([&] {
         if (!r || n < 0 || n > r->cap) throw Error{MPT_ERR_INVALID, "bad size"};
         if (n > r->n_upper) throw Error{MPT_ERR_INVALID, "set_size can only truncate"};
-        hipLaunchKernelGGL(k_set_n, dim3(1), dim3(1), 0, (hipStream_t)stream, r->d_n, n, r->d_counters);
-        hip_check(hipGetLastError(), "k_set_n");
+        // applied by the next round's k_sample on its stream (no launch of its own: a round
+        // trip of one small kernel per reset in the bench's timed loop), or by flush_size
+        (void)stream;
+        r->pending_n = n;
         r->n_upper = n;
     });
 }
@@ -582,6 +617,7 @@ struct StepCtx {
     bool use_tree = false, use_grid = false, live_list = false;
     bool defer_tree = false, want_spread = false;  // tree build left to the caller (step_many)
     SpreadOut spread{};
+    QueryOrder qo{};  // qo.list: this round's samples are bucketed (sorted grid 1-NN)
     void mark(int i, hipStream_t stream) const {
         if (ev) hip_check(hipEventRecord(ev[i], stream), "event record");
     }
@@ -622,8 +658,35 @@ StepCtx step_head(mpt_rrt *r, int32_t K, hipStream_t stream, bool defer_tree = f
     c.mark(0, stream);
     // k_steer lists the live units for the two-phase collide (FCL's object-level AABB test)
     const bool live_list = collide_mode() != MPT_COLLIDE_FUSED && p.pmax * p.L <= 64;
+    // grid rounds: the index build also buckets the samples along the grid's first dim, so the
+    // 1-NN launch can deal them to the XCDs by x-slab (MPT_NN_SORT=0: the unsorted launch, A/B)
+    static const bool sort_q = !getenv("MPT_NN_SORT") || atoi(getenv("MPT_NN_SORT")) != 0;
+    if (use_grid && sort_q && (p.d == 3 || p.d == 7 || p.d == 15)) {
+        if (r->q_cap < K) {
+            if (r->d_qlist) hip_check(hipFree(r->d_qlist), "hipFree");
+            hip_check(hipMalloc(&r->d_qlist, sizeof(int32_t) * (size_t)kQueryBuckets * K), "alloc query lists");
+            r->q_cap = K;
+        }
+        if (!r->d_qcount) {
+            const size_t qc_bytes = sizeof(int32_t) * kQueryBuckets * kQCountStride;
+            hip_check(hipMalloc(&r->d_qcount, qc_bytes), "alloc query counts");
+            hip_check(hipMemset(r->d_qcount, 0, qc_bytes), "zero query counts");
+            // the null-stream memset is not ordered with the engine's stream
+            hip_check(hipDeviceSynchronize(), "query counts zero sync");
+        }
+        const int dj = r->grid_dims[0];
+        const double span = p.hi[dj] - p.lo[dj];
+        c.qo.count = r->d_qcount;
+        c.qo.list = r->d_qlist;
+        c.qo.nb = kQueryBuckets;
+        c.qo.cap = r->q_cap;
+        c.qo.dim = dj;
+        c.qo.lo = p.lo[dj];
+        c.qo.inv_w = span > 0 ? (double)kQueryBuckets / span : 0.0;
+    }
     hipLaunchKernelGGL(k_sample, dim3(kb), dim3(256), 0, stream, p, r->ext_base, K, r->d_samples, r->d_n,
-                       live_list ? r->d_nlive : nullptr);
+                       live_list ? r->d_nlive : nullptr, r->pending_n, r->d_counters);
+    r->pending_n = -1;
     hip_check(hipGetLastError(), "k_sample");
     c.mark(1, stream);
     // the spread feedback rides on this round's index build when none is in flight
@@ -673,7 +736,12 @@ StepCtx step_head(mpt_rrt *r, int32_t K, hipStream_t stream, bool defer_tree = f
         const GridParams g = make_grid_params(p.d, r->grid_dims, r->grid_gd, lo, hi, r->n_upper, ppc, hmin_n);
         const GridParams gcap = make_grid_params(p.d, r->grid_dims, r->grid_gd, lo, hi, r->cap, ppc, hmin_c);
         r->grid->reserve(r->cap, p.d, std::max(g.ncells, gcap.ncells));  // once, as for the tree
-        r->grid->build(r->d_nodes, r->n_upper, r->d_n, p.d, g, stream, want_spread ? &spread : nullptr);
+        QueryBucketing qb;
+        qb.q = r->d_samples;
+        qb.nq = K;
+        qb.o = c.qo;
+        r->grid->build(r->d_nodes, r->n_upper, r->d_n, p.d, g, stream, want_spread ? &spread : nullptr,
+                       c.qo.list ? &qb : nullptr);
     }
     if (want_spread) {
         if (!c.defer_tree) hip_check(hipEventRecord(r->ev_spread, stream), "spread event");
@@ -705,7 +773,10 @@ void step_nn(mpt_rrt *r, int32_t K, hipStream_t stream, const StepCtx &c) {
     } else if (use_grid) {
         GridDev G = r->grid->dev();
         G.stats = r->stats_on ? r->d_cstats + 8 : nullptr;
-        launch_grid_knn(G, p.d, r->d_samples, K, 1, r->d_nn, r->d_nnd2, stream);
+        if (c.qo.list)
+            launch_grid_nn1_sorted(G, p.d, r->d_samples, K, c.qo, r->d_nn, r->d_nnd2, stream);
+        else
+            launch_grid_knn(G, p.d, r->d_samples, K, 1, r->d_nn, r->d_nnd2, stream);
     } else {
         NNWork w{};
         w.pts = r->d_nodes;
@@ -727,7 +798,7 @@ void step_tail(mpt_rrt *r, int32_t K, hipStream_t stream, const StepCtx &c) {
     hipEvent_t *ev = c.ev;
     auto steer = p.kind == MPT_AGENT_OMNI ? k_steer<MPT_AGENT_OMNI>
                  : (p.kind == MPT_AGENT_BLIMP ? k_steer<MPT_AGENT_BLIMP> : k_steer<MPT_AGENT_SNAKE>);
-    LiveOut lv{live_list ? r->d_live : nullptr, r->d_nlive, r->d_links, r->env};
+    LiveOut lv{live_list ? r->d_live : nullptr, r->d_nlive, r->d_links, r->env, c.qo.count, c.qo.nb};
     hipLaunchKernelGGL(steer, dim3(kb), dim3(256), 0, stream, p, r->ext_base, K, r->d_nodes, r->d_nn, r->d_ends,
                        r->d_poses, r->d_pcount, r->d_verdict, r->d_counters, lv);
     hip_check(hipGetLastError(), "k_steer");
@@ -972,7 +1043,7 @@ extern "C" mpt_status mpt_rrt_joint_times(void *joint_stream, float ms[2]) {
 extern "C" mpt_status mpt_rrt_counters(mpt_rrt *r, uint64_t c[8]) {
     return guarded([&] {
         if (!r || !c) throw Error{MPT_ERR_INVALID, "null pointer"};
-        hip_check(hipDeviceSynchronize(), "sync");
+        flush_size(r);
         unsigned long long h[8];
         hip_check(hipMemcpy(h, r->d_counters, sizeof(h), hipMemcpyDeviceToHost), "counters");
         for (int i = 0; i < 8; ++i) c[i] = h[i];

@@ -13,5 +13,5 @@ for v in "$@"; do
   echo "== $name: $envs python bench.py $ARGS"
   env $envs timeout -k 10 300 python bench.py $ARGS > $OUT/$name.log 2>&1 || { tail -5 $OUT/$name.log; exit 1; }
   grep '^{' $OUT/$name.log > $OUT/$name.json
-  python -c "import json,sys; d=json.load(open(sys.argv[1])); print(sys.argv[2], round(d['value']/1e6,2), 'M/s', round(d['ms_per_step'],3), 'ms/step')" $OUT/$name.json $name
+  python -c "import json,sys; d=json.load(open(sys.argv[1])); k=d.get('kernel_ms_per_round') or {}; print(sys.argv[2], round(d['value']/1e6,2), 'M/s', round(d['ms_per_step'],3), 'ms/step', ' '.join('%s=%s' % kv for kv in k.items()))" $OUT/$name.json $name
 done
