@@ -29,6 +29,9 @@
 namespace mpt {
 
 constexpr int kDistWaves = 4;
+// a bucket's queued pairs are evaluated at its end once at least this many wait
+// (MPT_DIST_FLUSH: A/B; 1 = after every bucket: 4 % slower on the blimp in the room)
+__constant__ int32_t c_dist_flush = 32;
 constexpr int kDistStack = kMaxLevels * kWave;
 
 __device__ __forceinline__ double read_best(const unsigned long long *p) {
@@ -62,16 +65,18 @@ struct DistCounters {
     uint32_t clusters = 0, items = 0, tri_calls = 0, pair_tests = 0;
 };
 
-// Per-wave LDS: the cluster's mapped agent triangles, the pair queue and the DFS stack.
+// Per-wave LDS: the cluster's mapped agent triangles, the pair queue and the DFS stack
+// (9 KiB a wave: four 4-wave workgroups per CU, i.e. 4 waves per SIMD).
 struct DistLds {
     double q[kWave][9];        // Q' of the cluster's triangles, by lane
     int32_t queue[2 * kWave];  // pending (env tri << 6 | agent lane) pairs
-    int32_t stk_i[kDistStack];
-    int32_t stk_l[kDistStack];
+    int32_t stk_il[kDistStack];  // item << 3 | level (kMaxLevels <= 8)
     float stk_b[kDistStack];
 };
+static_assert(kMaxLevels <= 8, "stack entries pack the level in 3 bits");
 
 // Exact triangle distances of the queued pairs, one pair per lane; returns the new bound.
+template <int kOcc>
 __device__ __forceinline__ double flush_pairs(const EnvDev &env, DistLds &s, int n, int lane, double U,
                                               unsigned long long *bp, DistCounters &cnt) {
     double d = DBL_MAX;
@@ -81,7 +86,8 @@ __device__ __forceinline__ double flush_pairs(const EnvDev &env, DistLds &s, int
         const v3 Q[3] = {mk(qa[0], qa[1], qa[2]), mk(qa[3], qa[4], qa[5]), mk(qa[6], qa[7], qa[8])};
         const EnvTri &E = env.tris[e >> 6];
         const v3 S[3] = {mk(E.P1[0], E.P1[1], E.P1[2]), mk(E.P2[0], E.P2[1], E.P2[2]), mk(E.P3[0], E.P3[1], E.P3[2])};
-        d = tri_distance(S, E.lo, E.hi, Q);
+        // at 4 waves per SIMD the rolled form (128 VGPRs); else the unrolled one
+        d = tri_distance<kOcc >= 4 ? 1 : 3>(S, E.lo, E.hi, Q);
     }
     cnt.tri_calls += (uint32_t)n;
     const double wb = wave_min_d(d);
@@ -95,9 +101,10 @@ __device__ __forceinline__ double flush_pairs(const EnvDev &env, DistLds &s, int
 // Depth-first walk of the env tree for one agent cluster (box cblo/cbhi, lane's triangle
 // box qlo/qhi, Q' in s.q), nearest child first; pairs that survive the exact box-gap test
 // are queued and evaluated 64 at a time.  Returns the updated bound.
+template <int kOcc>
 __device__ double walk_cluster(const EnvDev &env, DistLds &s, const float cblo[3], const float cbhi[3], bool act,
-                               const double qlo[3], const double qhi[3], int lane, double U,
-                               unsigned long long *bp, DistCounters &cnt) {
+                               const double qlo[3], const double qhi[3], const double xlo[3], const double xhi[3],
+                               int lane, double U, unsigned long long *bp, DistCounters &cnt) {
     int sp = 0, qn = 0;
     int lev = env.n_levels - 1;
     int32_t first = env.lev_off[lev];
@@ -144,10 +151,31 @@ __device__ double walk_cluster(const EnvDev &env, DistLds &s, const float cblo[3
                     if (!act) seed_t = -1;
                     const uint64_t pm = __ballot(act);
                     if (act) s.queue[(int)__popcll(pm & ((1ull << lane) - 1))] = (seed_t << 6) | lane;
-                    U = flush_pairs(env, s, (int)__popcll(pm), lane, U, bp, cnt);
+                    U = flush_pairs<kOcc>(env, s, (int)__popcll(pm), lane, U, bp, cnt);
                     if (U == 0.0) return U;
                 }
-                for (int32_t t = bf; t < bf + bc; ++t) {
+                // the bucket's env triangles whose exact box is within the bound of the cluster's
+                // exact box (xlo / xhi: the union of the lanes' triangle boxes), one per lane; a
+                // pair of any other triangle has a box gap above the bound (no lane would pass)
+                uint64_t tm;
+                {
+                    const double thr = U * (1.0 + 1e-9) + 1e-9;
+                    bool near = false;
+                    if (lane < bc) {
+                        const EnvTri &E = env.tris[bf + lane];
+                        double g2 = 0.0;
+#pragma unroll
+                        for (int k = 0; k < 3; ++k) {
+                            const double g = dmax(dmax(E.lo[k] - xhi[k], xlo[k] - E.hi[k]), 0.0);
+                            g2 += g * g;
+                        }
+                        near = g2 <= thr * thr;
+                    }
+                    tm = __ballot(near);
+                }
+                while (tm) {
+                    const int32_t t = bf + __ffsll((unsigned long long)tm) - 1;
+                    tm &= tm - 1;
                     const EnvTri &E = env.tris[t];
                     const double thr = U * (1.0 + 1e-9) + 1e-9;
                     double g2 = 0.0;
@@ -162,14 +190,17 @@ __device__ double walk_cluster(const EnvDev &env, DistLds &s, const float cblo[3
                     qn += (int)__popcll(pm);
                     cnt.pair_tests += (uint32_t)__popcll(__ballot(act));
                     if (qn >= kWave) {
-                        U = flush_pairs(env, s, kWave, lane, U, bp, cnt);
+                        U = flush_pairs<kOcc>(env, s, kWave, lane, U, bp, cnt);
                         qn -= kWave;
                         if (lane < qn) s.queue[lane] = s.queue[kWave + lane];
                         if (U == 0.0) return U;
                     }
                 }
-                if (qn > 0) {
-                    U = flush_pairs(env, s, qn, lane, U, bp, cnt);
+                // a bucket's leftover pairs wait for the next bucket's (the walk flushes them at
+                // its end) unless c_dist_flush of them are queued: fewer part-empty flushes
+                // against a bound that is staler by at most one bucket
+                if (qn >= c_dist_flush) {
+                    U = flush_pairs<kOcc>(env, s, qn, lane, U, bp, cnt);
                     qn = 0;
                     if (U == 0.0) return U;
                 }
@@ -191,8 +222,7 @@ __device__ double walk_cluster(const EnvDev &env, DistLds &s, const float cblo[3
             const uint64_t rest = m & ~(1ull << j);
             if (keep && lane != j) {
                 const int pos = sp + (int)__popcll(rest & ((1ull << lane) - 1));
-                s.stk_i[pos] = first + lane;
-                s.stk_l[pos] = lev;
+                s.stk_il[pos] = ((first + lane) << 3) | lev;
                 s.stk_b[pos] = lb;
             }
             sp += (int)__popcll(rest);
@@ -207,20 +237,25 @@ __device__ double walk_cluster(const EnvDev &env, DistLds &s, const float cblo[3
         while (sp > 0) {
             --sp;
             if (s.stk_b[sp] <= Uf2p) {
-                const Item it = env.items[s.stk_i[sp]];
+                const int32_t il = s.stk_il[sp];
+                const Item it = env.items[il >> 3];
                 first = __builtin_amdgcn_readfirstlane(it.first);
                 count = __builtin_amdgcn_readfirstlane(it.count);
-                lev = __builtin_amdgcn_readfirstlane(s.stk_l[sp] - 1);
+                lev = __builtin_amdgcn_readfirstlane((il & 7) - 1);
                 found = true;
                 break;
             }
         }
-        if (!found) return U;
+        if (!found) {
+            if (qn > 0) U = flush_pairs<kOcc>(env, s, qn, lane, U, bp, cnt);
+            return U;
+        }
     }
 }
 
 // One wave per (pose, link) unit: clusters in increasing order of their lower bound over
 // the env tree's top level, each walked with the bound the earlier ones left.
+template <int kOcc>
 __device__ void distance_unit(const EnvDev &env, const AgentDev *__restrict__ links, const DistWork &w, int64_t unit,
                               int lane, DistLds &s, DistCounters &cnt) {
     const int32_t L = w.L;
@@ -298,20 +333,38 @@ __device__ void distance_unit(const EnvDev &env, const AgentDev *__restrict__ li
                 qhi[1] = dmax(Q[0].y, dmax(Q[1].y, Q[2].y));
                 qhi[2] = dmax(Q[0].z, dmax(Q[1].z, Q[2].z));
             }
-            U = walk_cluster(env, s, cblo, cbhi, act, qlo, qhi, lane, U, bp, cnt);
+            // the cluster's exact box: the union of its lanes' triangle boxes
+            double xlo[3], xhi[3];
+#pragma unroll
+            for (int k = 0; k < 3; ++k) {
+                double lo = act ? qlo[k] : DBL_MAX, hi = act ? qhi[k] : -DBL_MAX;
+#pragma unroll
+                for (int off = 32; off > 0; off >>= 1) {
+                    lo = fmin(lo, __shfl_xor(lo, off));
+                    hi = fmax(hi, __shfl_xor(hi, off));
+                }
+                xlo[k] = uniform_d(lo);
+                xhi[k] = uniform_d(hi);
+            }
+            U = walk_cluster<kOcc>(env, s, cblo, cbhi, act, qlo, qhi, xlo, xhi, lane, U, bp, cnt);
             if (U == 0.0) return;
         }
     }
 }
 
-__global__ __launch_bounds__(kDistWaves * 64) void k_distance(EnvDev env, const AgentDev *__restrict__ links,
-                                                              DistWork w) {
+// kOcc workgroups per CU.  2 (default): the unconstrained allocation with the unrolled
+// triDistance (242 VGPRs, 2 waves per SIMD).  4: at most 128 VGPRs with the rolled triDistance
+// (4 waves per SIMD; the LDS allows it, the registers spill ~100 dwords): 12-14 % slower on
+// the blimp in the room (MPT_DIST_OCC=4, scripts/measure_distance.sh).
+template <int kOcc>
+__global__ __launch_bounds__(kDistWaves * 64, kOcc) void k_distance(EnvDev env, const AgentDev *__restrict__ links,
+                                                                 DistWork w) {
     __shared__ DistLds s_lds[kDistWaves];
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
     const int64_t unit = (int64_t)blockIdx.x * kDistWaves + wave;
     DistCounters cnt;
-    if (unit < w.n_units) distance_unit(env, links, w, unit, lane, s_lds[wave], cnt);
+    if (unit < w.n_units) distance_unit<kOcc>(env, links, w, unit, lane, s_lds[wave], cnt);
     if (w.stats && lane == 0 && unit < w.n_units) {
         atomicAdd(w.stats + 0, (unsigned long long)cnt.clusters);
         atomicAdd(w.stats + 1, (unsigned long long)cnt.items);
@@ -335,7 +388,17 @@ void launch_distance(const EnvDev &env, const AgentDev *d_links, const DistWork 
     if (w.n_units <= 0 || env.n_tris <= 0) return;
     const int64_t blocks = (w.n_units + kDistWaves - 1) / kDistWaves;
     if (blocks > 0x7fffffff) throw Error{MPT_ERR_INVALID, "distance batch too large"};
-    hipLaunchKernelGGL(k_distance, dim3((unsigned)blocks), dim3(kDistWaves * 64), 0, stream, env, d_links, w);
+    static const int occ = getenv("MPT_DIST_OCC") ? atoi(getenv("MPT_DIST_OCC")) : 2;
+    static const bool flush_set = [] {
+        const int32_t f = getenv("MPT_DIST_FLUSH") ? atoi(getenv("MPT_DIST_FLUSH")) : 32;
+        hip_check(hipMemcpyToSymbol(HIP_SYMBOL(c_dist_flush), &f, sizeof f), "flush threshold");
+        return true;
+    }();
+    (void)flush_set;
+    if (occ == 2)
+        hipLaunchKernelGGL(k_distance<2>, dim3((unsigned)blocks), dim3(kDistWaves * 64), 0, stream, env, d_links, w);
+    else
+        hipLaunchKernelGGL(k_distance<4>, dim3((unsigned)blocks), dim3(kDistWaves * 64), 0, stream, env, d_links, w);
     hip_check(hipGetLastError(), "k_distance launch");
 }
 

@@ -330,39 +330,64 @@ MPT_HD bool face_vertex(const v3 S[3], const v3 Sv[3], v3 Sn, double Snl, const 
 // exact boxes of S and T overlap; otherwise the edge-pair minimum is returned.  For
 // non-degenerate triangles the two agree (overlapping triangles have overlapping boxes);
 // for collinear ones FCL's answer is 0 at any distance.
+// kUnroll = 1: rolled loops (about 100 fewer VGPRs); 3: fully unrolled (the rotations become
+// register renames).  The same operations in the same order either way.
+template <int kUnroll = 3>
 MPT_HD double tri_distance(const v3 S[3], const double slo[3], const double shi[3], const v3 T[3]) {
-    const v3 Sv[3] = {sub(S[1], S[0]), sub(S[2], S[1]), sub(S[0], S[2])};
-    const v3 Tv[3] = {sub(T[1], T[0]), sub(T[2], T[1]), sub(T[0], T[2])};
+    // The 9 edge pairs in triDistance's order (i over S's edges, j over T's), as rolled loops:
+    // the triangles are rotated one vertex per step, so edge i / j is always vertex 0 -> 1 of
+    // the rotated triple and the off-edge vertex is vertex 2 (S[(i+2)%3], T[(j+2)%3]); edge
+    // vectors are recomputed from the vertices by the same subtraction.  Unrolled, the nine
+    // segPoints kept ~220 VGPRs live (2 waves per SIMD); the values and their order of
+    // operations are unchanged, so results are bitwise those of the unrolled form.
     const v3 D0 = sub(S[0], T[0]);
     double mindd = dot(D0, D0) + 1;
     int shown_disjoint = 0;
-#pragma unroll
+    v3 s0 = S[0], s1 = S[1], s2 = S[2];
+#pragma unroll kUnroll
     for (int i = 0; i < 3; ++i) {
-#pragma unroll
+        const v3 sv = sub(s1, s0);
+        v3 t0 = T[0], t1 = T[1], t2 = T[2];
+#pragma unroll kUnroll
         for (int j = 0; j < 3; ++j) {
+            const v3 tv = sub(t1, t0);
             v3 VEC, P, Q;
-            seg_points(S[i], Sv[i], T[j], Tv[j], VEC, P, Q);
+            seg_points(s0, sv, t0, tv, VEC, P, Q);
             const v3 V = sub(Q, P);
             const double dd = dot(V, V);
             if (dd <= mindd) {
                 mindd = dd;
-                double a = dot(sub(S[(i + 2) % 3], P), VEC);
-                double b = dot(sub(T[(j + 2) % 3], Q), VEC);
+                double a = dot(sub(s2, P), VEC);
+                double b = dot(sub(t2, Q), VEC);
                 if (a <= 0 && b >= 0) return sqrt(dd);
                 const double p = dot(V, VEC);
                 if (a < 0) a = 0;
                 if (b > 0) b = 0;
                 if (p - a + b > 0) shown_disjoint = 1;
             }
+            const v3 tt = t0;
+            t0 = t1;
+            t1 = t2;
+            t2 = tt;
         }
+        const v3 ss = s0;
+        s0 = s1;
+        s1 = s2;
+        s2 = ss;
     }
     double d;
-    const v3 Sn = cross(Sv[0], Sv[1]);
-    const double Snl = dot(Sn, Sn);
-    if (Snl > 1e-15 && face_vertex(S, Sv, Sn, Snl, T, true, shown_disjoint, d)) return d;
-    const v3 Tn = cross(Tv[0], Tv[1]);
-    const double Tnl = dot(Tn, Tn);
-    if (Tnl > 1e-15 && face_vertex(T, Tv, Tn, Tnl, S, false, shown_disjoint, d)) return d;
+    {
+        const v3 Sv[3] = {sub(S[1], S[0]), sub(S[2], S[1]), sub(S[0], S[2])};
+        const v3 Sn = cross(Sv[0], Sv[1]);
+        const double Snl = dot(Sn, Sn);
+        if (Snl > 1e-15 && face_vertex(S, Sv, Sn, Snl, T, true, shown_disjoint, d)) return d;
+    }
+    {
+        const v3 Tv[3] = {sub(T[1], T[0]), sub(T[2], T[1]), sub(T[0], T[2])};
+        const v3 Tn = cross(Tv[0], Tv[1]);
+        const double Tnl = dot(Tn, Tn);
+        if (Tnl > 1e-15 && face_vertex(T, Tv, Tn, Tnl, S, false, shown_disjoint, d)) return d;
+    }
     if (shown_disjoint) return sqrt(mindd);
     const double tlo[3] = {dmin(T[0].x, dmin(T[1].x, T[2].x)), dmin(T[0].y, dmin(T[1].y, T[2].y)),
                            dmin(T[0].z, dmin(T[1].z, T[2].z))};
