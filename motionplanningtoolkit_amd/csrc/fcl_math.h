@@ -398,6 +398,129 @@ MPT_HD double tri_distance(const v3 S[3], const double slo[3], const double shi[
     return boxes ? 0.0 : sqrt(mindd);
 }
 
+// ---------------------------------------------------------------------------------------
+// Correctly rounded sin / cos / tan: the trigonometry of the batched engine's steering (blimp
+// doStep, snake doStep, their stateToFCLTransform rotations).  The reference calls std::sin /
+// cos / tan, i.e. the host libm; glibc's are not correctly rounded (about 0.15 % of sin / cos
+// and 0.23 % of tan arguments come out 1 ulp off) and differ between its FMA and SSE2
+// variants, so the engine uses the implementation-independent definition, the correctly
+// rounded value, which the oracle's engine round (orc_cr_sin / cos / tan) computes the same
+// way: engine trees are bitwise the oracle's.  x = k pi/2 + r with pi/2 in four parts (the
+// first three of 33 bits: k * P_i exact for |k| < 2^20), r in double-double, sin r / cos r by
+// Horner over r^2 in double-double (Taylor to r^29 / r^28), tan = sin / cos in double-double;
+// the double-double value (relative error < 2^-100) rounded to double.
+struct DD {
+    double h, l;
+};
+MPT_HD DD dd_two_sum(double a, double b) {
+    const double s = a + b, bb = s - a;
+    return DD{s, (a - (s - bb)) + (b - bb)};
+}
+MPT_HD DD dd_fast(double a, double b) {  // |a| >= |b| (or a == 0)
+    const double s = a + b;
+    return DD{s, b - (s - a)};
+}
+MPT_HD DD dd_prod(double a, double b) {
+    const double p = a * b;
+    return DD{p, fma(a, b, -p)};
+}
+MPT_HD DD dd_add(DD a, DD b) {
+    const DD s = dd_two_sum(a.h, b.h);
+    return dd_fast(s.h, s.l + (a.l + b.l));
+}
+MPT_HD DD dd_mul(DD a, DD b) {
+    const DD p = dd_prod(a.h, b.h);
+    return dd_fast(p.h, p.l + (a.h * b.l + a.l * b.h));
+}
+// exact 1/n! split hi + lo: sin r = r sum_n (-1)^n r^2n / (2n+1)!, cos r = sum_n (-1)^n r^2n / (2n)!
+#define MPT_CR_SIN_COEFFS                                                                                  \
+    {{0x1p+0, 0x0p+0}, {-0x1.5555555555555p-3, -0x1.5555555555555p-57},                                \
+     {0x1.1111111111111p-7, 0x1.1111111111111p-63}, {-0x1.a01a01a01a01ap-13, -0x1.a01a01a01a01ap-73},     \
+     {0x1.71de3a556c734p-19, -0x1.c154f8ddc6c00p-73}, {-0x1.ae64567f544e4p-26, 0x1.c062e06d1f209p-80},    \
+     {0x1.6124613a86d09p-33, 0x1.f28e0cc748ebep-87}, {-0x1.ae7f3e733b81fp-41, -0x1.1d8656b0ee8cbp-97},    \
+     {0x1.952c77030ad4ap-49, 0x1.ac981465ddc6cp-103}, {-0x1.2f49b46814157p-57, -0x1.2650f61dbdcb4p-112},  \
+     {0x1.71b8ef6dcf572p-66, -0x1.d043ae40c4647p-120}, {-0x1.761b41316381ap-75, 0x1.3423c7d91404fp-130},  \
+     {0x1.3f3ccdd165fa9p-84, -0x1.58ddadf344487p-139}, {-0x1.d1ab1c2dccea3p-94, -0x1.054d0c78aea14p-149}, \
+     {0x1.259f98b4358adp-103, 0x1.eaf8c39dd9bc5p-157}}
+#define MPT_CR_COS_COEFFS                                                                                  \
+    {{0x1p+0, 0x0p+0}, {-0x1p-1, 0x0p+0},                                                                \
+     {0x1.5555555555555p-5, 0x1.5555555555555p-59}, {-0x1.6c16c16c16c17p-10, 0x1.f49f49f49f49fp-65},      \
+     {0x1.a01a01a01a01ap-16, 0x1.a01a01a01a01ap-76}, {-0x1.27e4fb7789f5cp-22, -0x1.cbbc05b4fa99ap-76},    \
+     {0x1.1eed8eff8d898p-29, -0x1.2aec959e14c06p-83}, {-0x1.93974a8c07c9dp-37, -0x1.05d6f8a2efd1fp-92},   \
+     {0x1.ae7f3e733b81fp-45, 0x1.1d8656b0ee8cbp-101}, {-0x1.6827863b97d97p-53, -0x1.eec01221a8b0bp-107},  \
+     {0x1.e542ba4020225p-62, 0x1.ea72b4afe3c2fp-120}, {-0x1.0ce396db7f853p-70, 0x1.aebcdbd20331cp-124},   \
+     {0x1.f2cf01972f578p-80, -0x1.9ada5fcc1ab14p-135}, {-0x1.88e85fc6a4e5ap-89, 0x1.71c37ebd16540p-143},  \
+     {0x1.0a18a2635085dp-98, 0x1.b9e2e28e1aa54p-153}}
+
+// r = x - k pi/2 (double-double); returns k mod 4
+MPT_HD int cr_reduce(double x, DD &r) {
+    const double k = rint(x * 0x1.45f306dc9c883p-1);
+    const double t = x - k * 0x1.921fb54400000p+0;  // exact for |k| < 2^20
+    DD a = dd_two_sum(t, -(k * 0x1.0b4611a600000p-34));
+    a = dd_add(a, dd_prod(-k, 0x1.3198a2e000000p-69));
+    a = dd_add(a, dd_prod(-k, 0x1.b839a252049c1p-104));
+    r = a;
+    return (int)((long long)k & 3);
+}
+// sin r and cos r of a reduced argument
+MPT_HD void cr_sincos_r(DD r, DD &s, DD &c) {
+    constexpr double cs[15][2] = MPT_CR_SIN_COEFFS;
+    constexpr double cc[15][2] = MPT_CR_COS_COEFFS;
+    const DD z = dd_mul(r, r);
+    DD ps{cs[14][0], cs[14][1]}, pc{cc[14][0], cc[14][1]};
+#pragma unroll
+    for (int n = 13; n >= 0; --n) {
+        ps = dd_add(dd_mul(ps, z), DD{cs[n][0], cs[n][1]});
+        pc = dd_add(dd_mul(pc, z), DD{cc[n][0], cc[n][1]});
+    }
+    s = dd_mul(r, ps);
+    c = pc;
+}
+MPT_HD double cr_sin(double x) {
+    if (x == 0.0 || !isfinite(x)) return x == 0.0 ? x : x - x;
+    DD r, s, c;
+    const int q = cr_reduce(x, r);
+    cr_sincos_r(r, s, c);
+    const double v = (q & 1) ? c.h : s.h;
+    return (q & 2) ? -v : v;
+}
+MPT_HD double cr_cos(double x) {
+    if (!isfinite(x)) return x - x;
+    DD r, s, c;
+    const int q = cr_reduce(x, r);
+    cr_sincos_r(r, s, c);
+    const double v = (q & 1) ? s.h : c.h;
+    return ((q + 1) & 2) ? -v : v;
+}
+// both at once (one reduction): the pose rotations need sin and cos of the same angle
+MPT_HD void cr_sincos(double x, double &sv, double &cv) {
+    if (!isfinite(x)) {
+        sv = cv = x - x;
+        return;
+    }
+    DD r, s, c;
+    const int q = cr_reduce(x, r);
+    cr_sincos_r(r, s, c);
+    const double vs = (q & 1) ? c.h : s.h, vc = (q & 1) ? s.h : c.h;
+    sv = x == 0.0 ? x : ((q & 2) ? -vs : vs);
+    cv = ((q + 1) & 2) ? -vc : vc;
+}
+MPT_HD double cr_tan(double x) {
+    if (x == 0.0 || !isfinite(x)) return x == 0.0 ? x : x - x;
+    DD r, s, c;
+    const int q = cr_reduce(x, r);
+    cr_sincos_r(r, s, c);
+    DD n = s, d = c;  // tan = sin / cos, or -cos / sin in odd quadrants
+    if (q & 1) {
+        n = DD{-c.h, -c.l};
+        d = s;
+    }
+    const double q1 = n.h / d.h;
+    const DD p = dd_prod(q1, d.h);
+    const double rem = (((n.h - p.h) - p.l) + n.l) - q1 * d.l;
+    return dd_fast(q1, rem / d.h).h;
+}
+
 // FLANN 1.8.4 L2<double>::operator() accumulation order: groups of four
 // result += ((d0*d0 + d1*d1) + d2*d2) + d3*d3, then the tail one at a time.
 // The first group is stored instead of added to 0.0 (0.0 + t == t bit for bit, t >= 0).

@@ -60,9 +60,11 @@ __device__ __forceinline__ double normalize_theta(double t) {
 __device__ void blimp_step(const double *prm, const double *s, double a, double w, double z, double dt,
                            double *out) {
     double n[7];
-    n[0] = s[0] + cos(s[3]) * s[4] * dt;
-    n[1] = s[1] + sin(s[3]) * s[4] * dt;
-    n[3] = normalize_theta(s[3] + s[4] * tan(s[5]) / prm[0]);
+    double sv, cv;
+    cr_sincos(s[3], sv, cv);  // correctly rounded (fcl_math.h): bitwise the oracle's engine round
+    n[0] = s[0] + cv * s[4] * dt;
+    n[1] = s[1] + sv * s[4] * dt;
+    n[3] = normalize_theta(s[3] + s[4] * cr_tan(s[5]) / prm[0]);
     n[2] = s[2] + s[6] * dt;
     n[4] = s[4] + a * dt;
     n[5] = s[5] + w * dt;
@@ -78,9 +80,11 @@ __device__ void blimp_step(const double *prm, const double *s, double a, double 
 __device__ void snake_step(const double *prm, int T, const double *s, double a, double w, double dt, double *out) {
     const double Lt = prm[1], Lh = prm[2];
     double n[kMaxDim];
-    n[0] = s[0] + cos(s[4]) * s[2] * dt;
-    n[1] = s[1] + sin(s[4]) * s[2] * dt;
-    n[4] = normalize_theta(s[4] + s[2] * tan(s[3]) / Lt * dt);
+    double sv, cv;
+    cr_sincos(s[4], sv, cv);
+    n[0] = s[0] + cv * s[2] * dt;
+    n[1] = s[1] + sv * s[2] * dt;
+    n[4] = normalize_theta(s[4] + s[2] * cr_tan(s[3]) / Lt * dt);
     n[2] = s[2] + a * dt;
     n[3] = s[3] + w * dt;
     if (n[2] > prm[4]) n[2] = prm[4]; else if (n[2] < prm[3]) n[2] = prm[3];
@@ -88,8 +92,10 @@ __device__ void snake_step(const double *prm, int T, const double *s, double a, 
     double coeff = s[2] / (Lt + Lh);
     double prev = s[4];
     for (int i = 1; i < T + 1; ++i) {
-        n[4 + i] = normalize_theta(s[4 + i] + coeff * sin(prev - s[4 + i]) * dt);
-        coeff *= cos(prev - s[4 + i]);
+        double sd, cd;
+        cr_sincos(prev - s[4 + i], sd, cd);
+        n[4 + i] = normalize_theta(s[4 + i] + coeff * sd * dt);
+        coeff *= cd;
         prev = s[4 + i];
     }
     for (int i = 0; i < 5 + T; ++i) out[i] = n[i];
@@ -107,13 +113,14 @@ __device__ __forceinline__ void put_pose(double *p, const double R[9], double x,
 // trailers at (-(Lt + Lh), Y, 0), rotation = rotation * identity (x*1 + y*0 + z*0).
 __device__ void snake_poses(const double *prm, int T, const double *s, double *out /*[L][12]*/) {
     double R[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1};
-    double sv = sin(s[4]), cv = cos(s[4]);
+    double sv, cv;
+    cr_sincos(s[4], sv, cv);
     R[0] = cv; R[3] = -sv; R[1] = sv; R[4] = cv;
     put_pose(out, R, s[0], s[1], 0.0);
     const double px = -(prm[1] + prm[2]);
     for (int i = 1; i < T + 1; ++i) {
         const double t = s[4 + i] - s[4 + i - 1];
-        sv = sin(t); cv = cos(t);
+        cr_sincos(t, sv, cv);
         R[0] = cv; R[3] = -sv; R[1] = sv; R[4] = cv;
         double M[9];
 #pragma unroll
@@ -224,7 +231,8 @@ __device__ __forceinline__ int32_t steer_one(const EngineParams &p, uint64_t ext
             } else {
                 blimp_step(p.prm, s, a, w, z, p.cc_dt, s);
             }
-            const double sv = sin(s[3]), cv = cos(s[3]);
+            double sv, cv;
+            cr_sincos(s[3], sv, cv);
             const double R[9] = {cv, sv, 0, -sv, cv, 0, 0, 0, 1};
             if (P < p.pmax) put_pose(ps + 12 * P, R, s[0], s[1], s[2]);
             ++P;

@@ -693,20 +693,143 @@ int32_t orc_omni_get_poses(const double start[3], const double end[3], double dt
     return P;
 }
 
+/* ======================================================================
+ * Correctly rounded sin / cos / tan: the trigonometry contract of the batched engine round
+ * (orc_engine_step; the device's fcl_math.h cr_sin / cr_cos / cr_tan follow the same
+ * definition).  The reference calls std::sin / cos / tan, i.e. the host's libm; glibc 2.35's
+ * are not correctly rounded (about 0.15 % of sin / cos and 0.23 % of tan arguments in
+ * [-7, 7] / [-0.8, 0.8] are 1 ulp off, tests/test_oracle.py against libquadmath) and differ
+ * between its FMA and SSE2 variants, so no device code can be bitwise "libm"; the engine
+ * instead uses the one implementation-independent definition, the correctly rounded value.
+ * The sequential loops (orc_rrt_run, the K = 1 replay) keep the host libm, as the reference.
+ *
+ * Method: x = k pi/2 + r with pi/2 split into four parts (P1..P3 of 33 bits, so k * Pi is
+ * exact for |k| < 2^20), r in double-double; sin r and cos r by Horner over r^2 in
+ * double-double (Taylor series to r^29 / r^28, |r| <= pi/4 + 2^-30: truncation < 2^-110);
+ * tan = sin / cos in double-double.  The double-double result (relative error below
+ * 2^-100) rounded to double is the correctly rounded value unless the exact value lies
+ * within 2^-100 of a rounding boundary.  Coefficients: exact 1/n! split hi + lo.
+ * ====================================================================== */
+typedef struct { double h, l; } orc_dd;
+static inline orc_dd dd_two_sum(double a, double b) {
+    const double s = a + b, bb = s - a;
+    const orc_dd r = {s, (a - (s - bb)) + (b - bb)};
+    return r;
+}
+static inline orc_dd dd_fast(double a, double b) {  /* |a| >= |b| (or a == 0) */
+    const double s = a + b;
+    const orc_dd r = {s, b - (s - a)};
+    return r;
+}
+static inline orc_dd dd_prod(double a, double b) {
+    const double p = a * b;
+    const orc_dd r = {p, fma(a, b, -p)};
+    return r;
+}
+static inline orc_dd dd_add(orc_dd a, orc_dd b) {
+    const orc_dd s = dd_two_sum(a.h, b.h);
+    return dd_fast(s.h, s.l + (a.l + b.l));
+}
+static inline orc_dd dd_mul(orc_dd a, orc_dd b) {
+    const orc_dd p = dd_prod(a.h, b.h);
+    return dd_fast(p.h, p.l + (a.h * b.l + a.l * b.h));
+}
+
+static const double CR_SIN[15][2] = {
+    {0x1p+0, 0x0p+0}, {-0x1.5555555555555p-3, -0x1.5555555555555p-57},
+    {0x1.1111111111111p-7, 0x1.1111111111111p-63}, {-0x1.a01a01a01a01ap-13, -0x1.a01a01a01a01ap-73},
+    {0x1.71de3a556c734p-19, -0x1.c154f8ddc6c00p-73}, {-0x1.ae64567f544e4p-26, 0x1.c062e06d1f209p-80},
+    {0x1.6124613a86d09p-33, 0x1.f28e0cc748ebep-87}, {-0x1.ae7f3e733b81fp-41, -0x1.1d8656b0ee8cbp-97},
+    {0x1.952c77030ad4ap-49, 0x1.ac981465ddc6cp-103}, {-0x1.2f49b46814157p-57, -0x1.2650f61dbdcb4p-112},
+    {0x1.71b8ef6dcf572p-66, -0x1.d043ae40c4647p-120}, {-0x1.761b41316381ap-75, 0x1.3423c7d91404fp-130},
+    {0x1.3f3ccdd165fa9p-84, -0x1.58ddadf344487p-139}, {-0x1.d1ab1c2dccea3p-94, -0x1.054d0c78aea14p-149},
+    {0x1.259f98b4358adp-103, 0x1.eaf8c39dd9bc5p-157}};
+static const double CR_COS[15][2] = {
+    {0x1p+0, 0x0p+0}, {-0x1p-1, 0x0p+0},
+    {0x1.5555555555555p-5, 0x1.5555555555555p-59}, {-0x1.6c16c16c16c17p-10, 0x1.f49f49f49f49fp-65},
+    {0x1.a01a01a01a01ap-16, 0x1.a01a01a01a01ap-76}, {-0x1.27e4fb7789f5cp-22, -0x1.cbbc05b4fa99ap-76},
+    {0x1.1eed8eff8d898p-29, -0x1.2aec959e14c06p-83}, {-0x1.93974a8c07c9dp-37, -0x1.05d6f8a2efd1fp-92},
+    {0x1.ae7f3e733b81fp-45, 0x1.1d8656b0ee8cbp-101}, {-0x1.6827863b97d97p-53, -0x1.eec01221a8b0bp-107},
+    {0x1.e542ba4020225p-62, 0x1.ea72b4afe3c2fp-120}, {-0x1.0ce396db7f853p-70, 0x1.aebcdbd20331cp-124},
+    {0x1.f2cf01972f578p-80, -0x1.9ada5fcc1ab14p-135}, {-0x1.88e85fc6a4e5ap-89, 0x1.71c37ebd16540p-143},
+    {0x1.0a18a2635085dp-98, 0x1.b9e2e28e1aa54p-153}};
+
+/* r = x - k pi/2 in double-double; returns k mod 4 */
+static int cr_reduce(double x, orc_dd *r) {
+    const double k = nearbyint(x * 0x1.45f306dc9c883p-1);
+    const double t = x - k * 0x1.921fb54400000p+0;  /* exact for |k| < 2^20 */
+    orc_dd a = dd_two_sum(t, -(k * 0x1.0b4611a600000p-34));
+    a = dd_add(a, dd_prod(-k, 0x1.3198a2e000000p-69));
+    a = dd_add(a, dd_prod(-k, 0x1.b839a252049c1p-104));
+    *r = a;
+    return (int)((int64_t)k & 3);
+}
+static orc_dd cr_poly(const double c[15][2], orc_dd z) {
+    orc_dd acc = {c[14][0], c[14][1]};
+    for (int n = 13; n >= 0; --n) {
+        const orc_dd cn = {c[n][0], c[n][1]};
+        acc = dd_add(dd_mul(acc, z), cn);
+    }
+    return acc;
+}
+/* sin r and cos r of the reduced argument */
+static void cr_sincos_r(orc_dd r, orc_dd *s, orc_dd *c) {
+    const orc_dd z = dd_mul(r, r);
+    *s = dd_mul(r, cr_poly(CR_SIN, z));
+    *c = cr_poly(CR_COS, z);
+}
+double orc_cr_sin(double x) {
+    if (x == 0.0 || !isfinite(x)) return x == 0.0 ? x : x - x;
+    orc_dd r, s, c;
+    const int q = cr_reduce(x, &r);
+    cr_sincos_r(r, &s, &c);
+    const double v = (q & 1) ? c.h : s.h;
+    return (q & 2) ? -v : v;
+}
+double orc_cr_cos(double x) {
+    if (!isfinite(x)) return x - x;
+    orc_dd r, s, c;
+    const int q = cr_reduce(x, &r);
+    cr_sincos_r(r, &s, &c);
+    const double v = (q & 1) ? s.h : c.h;
+    return ((q + 1) & 2) ? -v : v;
+}
+double orc_cr_tan(double x) {
+    if (x == 0.0 || !isfinite(x)) return x == 0.0 ? x : x - x;
+    orc_dd r, s, c;
+    const int q = cr_reduce(x, &r);
+    cr_sincos_r(r, &s, &c);
+    orc_dd n = s, d = c;  /* tan = sin / cos, or -cos / sin in odd quadrants */
+    if (q & 1) {
+        n.h = -c.h; n.l = -c.l;
+        d = s;
+    }
+    const double q1 = n.h / d.h;
+    const orc_dd p = dd_prod(q1, d.h);
+    const double rem = (((n.h - p.h) - p.l) + n.l) - q1 * d.l;
+    return dd_fast(q1, rem / d.h).h;
+}
+
+/* the trigonometry a steering routine uses: the host libm (the reference's std::sin / cos /
+ * tan; the sequential loops) or the correctly rounded one (the batched engine round) */
+typedef struct { double (*sin)(double); double (*cos)(double); double (*tan)(double); } orc_trig;
+static const orc_trig TRIG_LIBM = {sin, cos, tan};
+static const orc_trig TRIG_CR = {orc_cr_sin, orc_cr_cos, orc_cr_tan};
+
 static double normalize_theta(double t) {
     /* Blimp/SnakeTrailers::normalizeTheta */
     return t - 2 * M_PI * floor((t + M_PI) / (2 * M_PI));
 }
 
 /* Blimp::doStep, agents/blimp.hpp:293-317 (theta update omits dt, as written) */
-void orc_blimp_do_step(const double prm[7], const double s[7], double a, double w, double z,
-                       double dt, double out[7]) {
+static void blimp_do_step_t(const orc_trig *tr, const double prm[7], const double s[7], double a, double w,
+                            double z, double dt, double out[7]) {
     const double L = prm[0], vmin = prm[1], vmax = prm[2], pmin = prm[3], pmax = prm[4];
     const double zmin = prm[5], zmax = prm[6];
     double n[7];
-    n[0] = s[0] + cos(s[3]) * s[4] * dt;
-    n[1] = s[1] + sin(s[3]) * s[4] * dt;
-    n[3] = normalize_theta(s[3] + s[4] * tan(s[5]) / L);
+    n[0] = s[0] + tr->cos(s[3]) * s[4] * dt;
+    n[1] = s[1] + tr->sin(s[3]) * s[4] * dt;
+    n[3] = normalize_theta(s[3] + s[4] * tr->tan(s[5]) / L);
     n[2] = s[2] + s[6] * dt;
     n[4] = s[4] + a * dt;
     n[5] = s[5] + w * dt;
@@ -715,6 +838,14 @@ void orc_blimp_do_step(const double prm[7], const double s[7], double a, double 
     if (n[5] > pmax) n[5] = pmax; else if (n[5] < pmin) n[5] = pmin;
     if (n[6] > zmax) n[6] = zmax; else if (n[6] < zmin) n[6] = zmin;
     memcpy(out, n, sizeof n);
+}
+void orc_blimp_do_step(const double prm[7], const double s[7], double a, double w, double z,
+                       double dt, double out[7]) {
+    blimp_do_step_t(&TRIG_LIBM, prm, s, a, w, z, dt, out);
+}
+void orc_blimp_do_step_cr(const double prm[7], const double s[7], double a, double w, double z,
+                          double dt, double out[7]) {
+    blimp_do_step_t(&TRIG_CR, prm, s, a, w, z, dt, out);
 }
 
 /* Blimp::randomSteer, agents/blimp.hpp:179-187: draws a, w, z in that order from
@@ -728,8 +859,8 @@ void orc_blimp_random_steer(const double prm[7], orc_minstd *g, const double sta
 }
 
 /* Blimp::stateToFCLTransform, agents/blimp.hpp:339-356 */
-static void blimp_pose(const double s[7], double *pose) {
-    const double sv = sin(s[3]), cv = cos(s[3]);
+static void blimp_pose(const orc_trig *tr, const double s[7], double *pose) {
+    const double sv = tr->sin(s[3]), cv = tr->cos(s[3]);
     const double R[9] = {cv, sv, 0, -sv, cv, 0, 0, 0, 1};
     memcpy(pose, R, sizeof R);
     pose[9] = s[0]; pose[10] = s[1]; pose[11] = s[2];
@@ -738,30 +869,38 @@ static void blimp_pose(const double s[7], double *pose) {
 /* Build-defined Blimp::getPoses (the reference's agents/blimp.hpp:219-223 returns one
  * empty pose list, i.e. never checks): the states after each of the
  * max(1, floor(edge_dt / dt)) doStep(dt) increments, end state included. */
-int32_t orc_blimp_get_poses(const double prm[7], const double start[7], const double awz[3],
-                            double edge_dt, double dt, double *poses_out, int32_t maxP) {
+static int32_t blimp_get_poses_t(const orc_trig *tr, const double prm[7], const double start[7],
+                                 const double awz[3], double edge_dt, double dt, double *poses_out, int32_t maxP) {
     const double q = edge_dt / dt;
     unsigned int steps = (q >= 4294967296.0 || !(q >= 0)) ? 0u : (unsigned int)q;
     if (steps == 0) steps = 1;
     double s[7];
     memcpy(s, start, sizeof s);
     for (unsigned int i = 0; i < steps; ++i) {
-        orc_blimp_do_step(prm, s, awz[0], awz[1], awz[2], dt, s);
-        if ((int32_t)i < maxP) blimp_pose(s, poses_out + 12 * i);
+        blimp_do_step_t(tr, prm, s, awz[0], awz[1], awz[2], dt, s);
+        if ((int32_t)i < maxP) blimp_pose(tr, s, poses_out + 12 * i);
     }
     return (int32_t)steps;
 }
+int32_t orc_blimp_get_poses(const double prm[7], const double start[7], const double awz[3],
+                            double edge_dt, double dt, double *poses_out, int32_t maxP) {
+    return blimp_get_poses_t(&TRIG_LIBM, prm, start, awz, edge_dt, dt, poses_out, maxP);
+}
+int32_t orc_blimp_get_poses_cr(const double prm[7], const double start[7], const double awz[3],
+                               double edge_dt, double dt, double *poses_out, int32_t maxP) {
+    return blimp_get_poses_t(&TRIG_CR, prm, start, awz, edge_dt, dt, poses_out, maxP);
+}
 
 /* SnakeTrailers::doStep, agents/snake_trailers.hpp:341-369 */
-void orc_snake_do_step(const double prm[7], const double *s, double a, double w, double dt,
-                       double *out) {
+static void snake_do_step_t(const orc_trig *tr, const double prm[7], const double *s, double a, double w,
+                            double dt, double *out) {
     const int T = (int)prm[0];
     const double Lt = prm[1], Lh = prm[2], vmin = prm[3], vmax = prm[4], pmin = prm[5], pmax = prm[6];
     enum { X = 0, Y = 1, V = 2, PSI = 3, THETA = 4 };
     double n[64];
-    n[X] = s[X] + cos(s[THETA]) * s[V] * dt;
-    n[Y] = s[Y] + sin(s[THETA]) * s[V] * dt;
-    n[THETA] = normalize_theta(s[THETA] + s[V] * tan(s[PSI]) / Lt * dt);
+    n[X] = s[X] + tr->cos(s[THETA]) * s[V] * dt;
+    n[Y] = s[Y] + tr->sin(s[THETA]) * s[V] * dt;
+    n[THETA] = normalize_theta(s[THETA] + s[V] * tr->tan(s[PSI]) / Lt * dt);
     n[V] = s[V] + a * dt;
     n[PSI] = s[PSI] + w * dt;
     if (n[V] > vmax) n[V] = vmax; else if (n[V] < vmin) n[V] = vmin;
@@ -769,11 +908,19 @@ void orc_snake_do_step(const double prm[7], const double *s, double a, double w,
     double coeff = s[V] / (Lt + Lh);
     double prev = s[THETA];
     for (int i = 1; i < T + 1; ++i) {
-        n[THETA + i] = normalize_theta(s[THETA + i] + coeff * sin(prev - s[THETA + i]) * dt);
-        coeff *= cos(prev - s[THETA + i]);
+        n[THETA + i] = normalize_theta(s[THETA + i] + coeff * tr->sin(prev - s[THETA + i]) * dt);
+        coeff *= tr->cos(prev - s[THETA + i]);
         prev = s[THETA + i];
     }
     memcpy(out, n, sizeof(double) * (size_t)(5 + T));
+}
+void orc_snake_do_step(const double prm[7], const double *s, double a, double w, double dt,
+                       double *out) {
+    snake_do_step_t(&TRIG_LIBM, prm, s, a, w, dt, out);
+}
+void orc_snake_do_step_cr(const double prm[7], const double *s, double a, double w, double dt,
+                          double *out) {
+    snake_do_step_t(&TRIG_CR, prm, s, a, w, dt, out);
 }
 
 /* SnakeTrailers::randomSteer, agents/snake_trailers.hpp:206-213: a ~ U(-0.1, 1),
@@ -787,20 +934,20 @@ void orc_snake_random_steer(const double prm[7], orc_minstd *g, const double *st
 
 /* SnakeTrailers::stateToFCLTransforms, agents/snake_trailers.hpp:411-459, verbatim:
  * trailer translations are (-(Lt+Lh), Y, 0), not chained. */
-static void snake_poses(const double prm[7], const double *s, double *poses /*[L][12]*/) {
+static void snake_poses(const orc_trig *tr, const double prm[7], const double *s, double *poses /*[L][12]*/) {
     const int T = (int)prm[0];
     const double Lt = prm[1], Lh = prm[2];
     enum { X = 0, Y = 1, THETA = 4 };
     double pose_t[3] = {s[X], s[Y], 0};
     double R[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1};
-    double sv = sin(s[THETA]), cv = cos(s[THETA]);
+    double sv = tr->sin(s[THETA]), cv = tr->cos(s[THETA]);
     R[0] = cv; R[3] = -sv; R[1] = sv; R[4] = cv;
     memcpy(poses, R, sizeof R);
     memcpy(poses + 9, pose_t, sizeof pose_t);
     for (int i = 1; i < T + 1; ++i) {
         pose_t[0] = -(Lt + Lh);
         const double t = s[THETA + i] - s[THETA + i - 1];
-        sv = sin(t); cv = cos(t);
+        sv = tr->sin(t); cv = tr->cos(t);
         R[0] = cv; R[3] = -sv; R[1] = sv; R[4] = cv;
         /* rotation = rotation * identity: Matrix3Data::operator* sums x*1 + y*0 + z*0 */
         double M[9];
@@ -816,8 +963,8 @@ static void snake_poses(const double prm[7], const double *s, double *poses /*[L
 }
 
 /* SnakeTrailers::getPoses, agents/snake_trailers.hpp:246-268 */
-int32_t orc_snake_get_poses(const double prm[7], const double *start, const double aw[2],
-                            double edge_dt, double dt, double *poses_out, int32_t maxP) {
+static int32_t snake_get_poses_t(const orc_trig *tr, const double prm[7], const double *start, const double aw[2],
+                                 double edge_dt, double dt, double *poses_out, int32_t maxP) {
     const int T = (int)prm[0];
     const int L = T + 1;
     const double q = edge_dt / dt;
@@ -826,10 +973,18 @@ int32_t orc_snake_get_poses(const double prm[7], const double *start, const doub
     double s[64];
     memcpy(s, start, sizeof(double) * (size_t)(5 + T));
     for (unsigned int i = 0; i < steps; ++i) {
-        if ((int32_t)i < maxP) snake_poses(prm, s, poses_out + (size_t)12 * L * i);
-        orc_snake_do_step(prm, s, aw[0], aw[1], dt, s);
+        if ((int32_t)i < maxP) snake_poses(tr, prm, s, poses_out + (size_t)12 * L * i);
+        snake_do_step_t(tr, prm, s, aw[0], aw[1], dt, s);
     }
     return (int32_t)steps;
+}
+int32_t orc_snake_get_poses(const double prm[7], const double *start, const double aw[2],
+                            double edge_dt, double dt, double *poses_out, int32_t maxP) {
+    return snake_get_poses_t(&TRIG_LIBM, prm, start, aw, edge_dt, dt, poses_out, maxP);
+}
+int32_t orc_snake_get_poses_cr(const double prm[7], const double *start, const double aw[2],
+                               double edge_dt, double dt, double *poses_out, int32_t maxP) {
+    return snake_get_poses_t(&TRIG_CR, prm, start, aw, edge_dt, dt, poses_out, maxP);
 }
 
 /* ======================================================================
@@ -969,14 +1124,14 @@ int64_t orc_engine_step(int32_t agent_kind, const double *prm, int32_t d, const 
             awz[0] = orc_engine_uniform(seed, g * 64 + 32, -1, 1);
             awz[1] = orc_engine_uniform(seed, g * 64 + 33, -0.1745, 0.1745);
             awz[2] = orc_engine_uniform(seed, g * 64 + 34, -1, 1);
-            orc_blimp_do_step(prm, from, awz[0], awz[1], awz[2], steer_dt, end);
-            P = orc_blimp_get_poses(prm, from, awz, steer_dt, cc_dt, poses, 64);
+            orc_blimp_do_step_cr(prm, from, awz[0], awz[1], awz[2], steer_dt, end);
+            P = orc_blimp_get_poses_cr(prm, from, awz, steer_dt, cc_dt, poses, 64);
         } else {
             double aw[2];
             aw[0] = orc_engine_uniform(seed, g * 64 + 32, -0.1, 1);
             aw[1] = orc_engine_uniform(seed, g * 64 + 33, -M_PI / 18., M_PI / 18.);
-            orc_snake_do_step(prm, from, aw[0], aw[1], steer_dt, end);
-            P = orc_snake_get_poses(prm, from, aw, steer_dt, cc_dt, poses, 64 / L);
+            orc_snake_do_step_cr(prm, from, aw[0], aw[1], steer_dt, end);
+            P = orc_snake_get_poses_cr(prm, from, aw, steer_dt, cc_dt, poses, 64 / L);
         }
         if (P > 64 / L) P = 64 / L;
         int hit = 0;
@@ -1041,14 +1196,14 @@ int64_t orc_rrt_seq_rebuild(int32_t agent_kind, const double *prm, int32_t d, co
             awz[0] = orc_engine_uniform(seed, g * 64 + 32, -1, 1);
             awz[1] = orc_engine_uniform(seed, g * 64 + 33, -0.1745, 0.1745);
             awz[2] = orc_engine_uniform(seed, g * 64 + 34, -1, 1);
-            orc_blimp_do_step(prm, from, awz[0], awz[1], awz[2], steer_dt, end);
-            P = orc_blimp_get_poses(prm, from, awz, steer_dt, cc_dt, poses, 64);
+            orc_blimp_do_step_cr(prm, from, awz[0], awz[1], awz[2], steer_dt, end);
+            P = orc_blimp_get_poses_cr(prm, from, awz, steer_dt, cc_dt, poses, 64);
         } else {
             double aw[2];
             aw[0] = orc_engine_uniform(seed, g * 64 + 32, -0.1, 1);
             aw[1] = orc_engine_uniform(seed, g * 64 + 33, -M_PI / 18., M_PI / 18.);
-            orc_snake_do_step(prm, from, aw[0], aw[1], steer_dt, end);
-            P = orc_snake_get_poses(prm, from, aw, steer_dt, cc_dt, poses, 64 / L);
+            orc_snake_do_step_cr(prm, from, aw[0], aw[1], steer_dt, end);
+            P = orc_snake_get_poses_cr(prm, from, aw, steer_dt, cc_dt, poses, 64 / L);
         }
         if (P > 64 / L) P = 64 / L;
         int hit = 0;

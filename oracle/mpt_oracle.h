@@ -119,6 +119,21 @@ void orc_snake_random_steer(const double prm[7], orc_minstd *g, const double *st
 int32_t orc_snake_get_poses(const double prm[7], const double *start, const double aw[2],
                             double edge_dt, double dt, double *poses_out, int32_t maxP);
 
+/* The batched engine round's trigonometry: correctly rounded sin / cos / tan (mpt_oracle.c
+ * explains why not the host libm), and the blimp / snake steering with it (the plain
+ * functions above use the host libm, as the reference's sequential loop). */
+double orc_cr_sin(double x);
+double orc_cr_cos(double x);
+double orc_cr_tan(double x);
+void orc_blimp_do_step_cr(const double prm[7], const double s[7], double a, double w, double z,
+                          double dt, double out[7]);
+int32_t orc_blimp_get_poses_cr(const double prm[7], const double start[7], const double awz[3],
+                               double edge_dt, double dt, double *poses_out, int32_t maxP);
+void orc_snake_do_step_cr(const double prm[7], const double *s, double a, double w, double dt,
+                          double *out);
+int32_t orc_snake_get_poses_cr(const double prm[7], const double *start, const double aw[2],
+                               double edge_dt, double dt, double *poses_out, int32_t maxP);
+
 /* ---------------- sequential RRT (planners/rrt.hpp, K = 1 replay) ---------------- */
 /* agent_kind: 0 omni, 1 blimp, 2 snake.  ranges [d][2] = getStateVarRanges(bounds).
  * iterations_at_a_time: RRT::query's argument (<= 0: run until solved or max_nodes).

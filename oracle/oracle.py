@@ -77,6 +77,13 @@ def lib(path: str | None = None):
             "orc_blimp_get_poses": (I32, [P, P, P, D, D, P, I32]),
             "orc_snake_do_step": (None, [P, P, D, D, D, P]),
             "orc_snake_get_poses": (I32, [P, P, P, D, D, P, I32]),
+            "orc_cr_sin": (D, [D]),
+            "orc_cr_cos": (D, [D]),
+            "orc_cr_tan": (D, [D]),
+            "orc_blimp_do_step_cr": (None, [P, P, D, D, D, D, P]),
+            "orc_blimp_get_poses_cr": (I32, [P, P, P, D, D, P, I32]),
+            "orc_snake_do_step_cr": (None, [P, P, D, D, D, P]),
+            "orc_snake_get_poses_cr": (I32, [P, P, P, D, D, P, I32]),
             "orc_rrt_run": (I64, [I32, P, I32, P, P, P, P, D, D, P, I64, P, P, I64, I64, I64, P, P, P, P]),
             "orc_engine_step": (I64, [I32, P, I32, P, D, D, U64, U64, I32, P, P, P, I64, P, P, I64, I64, P, P, C.c_int, C.c_int]),
             "orc_rrt_seq_rebuild": (I64, [I32, P, I32, P, D, D, U64, U64, I64, D, P, P, P, I64, P, P, I64, I64, P, P]),
@@ -312,29 +319,51 @@ def omni_get_poses(start, end, dt, maxP=4096):
     return out[: min(P, maxP)]
 
 
-def blimp_do_step(prm, s, a, w, z, dt):
+# trig: "libm" = the host libm (the reference's std::sin / cos / tan: the sequential loops);
+# "cr" = correctly rounded (the batched engine round's contract, orc_cr_sin / cos / tan)
+def _sfx(trig):
+    if trig not in ("libm", "cr"):
+        raise ValueError(trig)
+    return "_cr" if trig == "cr" else ""
+
+
+def cr_sin(x) -> float:
+    return lib().orc_cr_sin(float(x))
+
+
+def cr_cos(x) -> float:
+    return lib().orc_cr_cos(float(x))
+
+
+def cr_tan(x) -> float:
+    return lib().orc_cr_tan(float(x))
+
+
+def blimp_do_step(prm, s, a, w, z, dt, trig="libm"):
     out = np.zeros(7)
-    lib().orc_blimp_do_step(_p(_f64(prm)), _p(_f64(s)), a, w, z, dt, _p(out))
+    getattr(lib(), "orc_blimp_do_step" + _sfx(trig))(_p(_f64(prm)), _p(_f64(s)), a, w, z, dt, _p(out))
     return out
 
 
-def blimp_get_poses(prm, start, awz, edge_dt, dt, maxP=4096):
+def blimp_get_poses(prm, start, awz, edge_dt, dt, maxP=4096, trig="libm"):
     out = np.zeros((maxP, 12))
-    P = lib().orc_blimp_get_poses(_p(_f64(prm)), _p(_f64(start)), _p(_f64(awz)), edge_dt, dt, _p(out), maxP)
+    P = getattr(lib(), "orc_blimp_get_poses" + _sfx(trig))(_p(_f64(prm)), _p(_f64(start)), _p(_f64(awz)), edge_dt,
+                                                           dt, _p(out), maxP)
     return out[: min(P, maxP)]
 
 
-def snake_do_step(prm, s, a, w, dt):
+def snake_do_step(prm, s, a, w, dt, trig="libm"):
     s = _f64(s)
     out = np.zeros_like(s)
-    lib().orc_snake_do_step(_p(_f64(prm)), _p(s), a, w, dt, _p(out))
+    getattr(lib(), "orc_snake_do_step" + _sfx(trig))(_p(_f64(prm)), _p(s), a, w, dt, _p(out))
     return out
 
 
-def snake_get_poses(prm, start, aw, edge_dt, dt, maxP=64):
+def snake_get_poses(prm, start, aw, edge_dt, dt, maxP=64, trig="libm"):
     L = int(prm[0]) + 1
     out = np.zeros((maxP, L, 12))
-    P = lib().orc_snake_get_poses(_p(_f64(prm)), _p(_f64(start)), _p(_f64(aw)), edge_dt, dt, _p(out), maxP)
+    P = getattr(lib(), "orc_snake_get_poses" + _sfx(trig))(_p(_f64(prm)), _p(_f64(start)), _p(_f64(aw)), edge_dt, dt,
+                                                           _p(out), maxP)
     return out[: min(P, maxP)]
 
 

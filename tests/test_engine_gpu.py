@@ -1,10 +1,10 @@
 """GPU parity: one batched RRT round of the device engine (k_sample -> k_knn1 -> k_steer ->
 k_collide -> ordered append) checked stage by stage against the oracle.
 
-Bars: samples, NN ids, collision verdicts and the append order are bit-exact; the steer
-and pose stages use device sin/cos/tan (ROCm ocml) where the oracle uses glibc libm, so
-states and poses are compared within 1e-12 relative (they agree to the last ulp or two),
-and verdicts are then checked bit-exactly on the device's own poses."""
+Bars: every stage is bit-exact -- samples, NN ids, steered states and poses, collision
+verdicts and the append order.  The blimp / snake steering's sin / cos / tan are the
+correctly rounded values on both sides (fcl_math.h cr_*, oracle orc_cr_*; DESIGN.md §2 on
+why the engine contract is not the host libm)."""
 import math
 
 import numpy as np
@@ -13,9 +13,6 @@ import pytest
 from motionplanningtoolkit_amd import scenes
 
 pytestmark = pytest.mark.gpu
-
-RTOL = 1e-12
-
 
 def bits(a):
     return np.ascontiguousarray(a, np.float64).view(np.uint64)
@@ -54,7 +51,7 @@ def check_round(mpt, oracle, sc, eng, tree, seed, ext_base, K):
     # 2. nearest neighbours over the snapshot
     ri, _ = oracle.knn(tree, samples, 1)
     assert np.array_equal(nn, ri[:, 0])
-    # 3. steer + poses (transcendentals: tolerance)
+    # 3. steer + poses (correctly rounded trig on both sides: bit-exact)
     exp_end = np.zeros_like(ends)
     for k in range(K):
         g = ext_base + k
@@ -69,16 +66,16 @@ def check_round(mpt, oracle, sc, eng, tree, seed, ext_base, K):
             assert np.array_equal(bits(ends[k]), bits(exp_end[k]))  # no transcendentals
             assert np.array_equal(bits(poses[k, :pcount[k], 0]), bits(exp_p))
         elif sc.kind == 1:
-            exp_end[k] = oracle.blimp_do_step(sc.prm, frm, c[0], c[1], c[2], sc.steer_dt)
-            exp_p = oracle.blimp_get_poses(sc.prm, frm, c, sc.steer_dt, sc.cc_dt)
+            exp_end[k] = oracle.blimp_do_step(sc.prm, frm, c[0], c[1], c[2], sc.steer_dt, trig="cr")
+            exp_p = oracle.blimp_get_poses(sc.prm, frm, c, sc.steer_dt, sc.cc_dt, trig="cr")
             assert pcount[k] == len(exp_p)
-            np.testing.assert_allclose(poses[k, :pcount[k], 0], exp_p, rtol=RTOL, atol=1e-13)
+            assert np.array_equal(bits(poses[k, :pcount[k], 0]), bits(exp_p))
         else:
-            exp_end[k] = oracle.snake_do_step(sc.prm, frm, c[0], c[1], sc.steer_dt)
-            exp_p = oracle.snake_get_poses(sc.prm, frm, c, sc.steer_dt, sc.cc_dt)
+            exp_end[k] = oracle.snake_do_step(sc.prm, frm, c[0], c[1], sc.steer_dt, trig="cr")
+            exp_p = oracle.snake_get_poses(sc.prm, frm, c, sc.steer_dt, sc.cc_dt, trig="cr")
             assert pcount[k] == len(exp_p)
-            np.testing.assert_allclose(poses[k, :pcount[k]], exp_p, rtol=RTOL, atol=1e-13)
-    np.testing.assert_allclose(ends, exp_end, rtol=RTOL, atol=1e-13)
+            assert np.array_equal(bits(poses[k, :pcount[k]]), bits(exp_p))
+    assert np.array_equal(bits(ends), bits(exp_end))
     # 4. verdicts on the device's own poses: bit-exact
     flat = np.concatenate([poses[k, :pcount[k]] for k in range(K)]).reshape(-1, inf["links"], 12)
     off = np.r_[0, np.cumsum(pcount)]
@@ -187,6 +184,38 @@ def test_engine_grid_equals_brute_over_growing_rounds(mpt_gpu, oracle):
     for t in trees[1:]:
         assert np.array_equal(bits(trees[0][0]), bits(t[0]))
         assert np.array_equal(trees[0][1], t[1])
+
+
+@pytest.mark.parametrize("nn_mode", ["grid", "tree"])
+@pytest.mark.parametrize("name", ["blimp", "snake"])
+def test_engine_trees_equal_oracle_over_rounds(mpt_gpu, oracle, name, nn_mode):
+    """Whole trees, not stages: several rounds grown on the device (each round sees the
+    previous rounds' nodes) equal the oracle's engine rounds (orc_engine_step: kd-tree NN,
+    correctly rounded steering trig, AABB-tree + FCL SAT collision) node for node, states and
+    parents bitwise."""
+    if name == "blimp":
+        sc, n0, Ks = scenes.blimp_scenario("all"), 5000, (2048, 777, 2048)
+    else:
+        sc, n0, Ks = scenes.snake_scenario("corridor"), 5000, (1024, 333, 1024)
+    seed = 4242
+    eng, tree = make(mpt_gpu, sc, n0, max(Ks), seed, cap_extra=sum(Ks))
+    eng.set_nn(nn_mode)
+    for K in Ks:
+        eng.step(K)
+    n = eng.counters()["nodes"]
+    got, gpar = eng.read_tree(n)
+    ref = np.zeros((n0 + sum(Ks), sc.dim))
+    ref[:n0] = tree
+    rpar = np.zeros(n0 + sum(Ks), np.int32)
+    bvh = oracle.BVH(sc.env_tris)
+    m, base = n0, 0
+    for K in Ks:
+        m, _, _ = oracle.engine_step(sc.kind, sc.prm, sc.ranges, sc.steer_dt, sc.cc_dt, seed, base, K, bvh,
+                                     sc.env_tf, sc.agent_tris, ref, rpar, m, nthreads=8)
+        base += K
+    assert m == n and n > n0
+    assert np.array_equal(bits(got), bits(ref[:n]))
+    assert np.array_equal(gpar[n0:], rpar[n0:n])
 
 
 @pytest.mark.parametrize("name", ["blimp", "snake"])
