@@ -407,7 +407,8 @@ MPT_HD double tri_distance(const v3 S[3], const double slo[3], const double shi[
 // rounded value, which the oracle's engine round (orc_cr_sin / cos / tan) computes the same
 // way: engine trees are bitwise the oracle's.  x = k pi/2 + r with pi/2 in four parts (the
 // first three of 33 bits: k * P_i exact for |k| < 2^20), r in double-double, sin r / cos r by
-// Horner over r^2 in double-double (Taylor to r^29 / r^28), tan = sin / cos in double-double;
+// Horner over r^2 (Taylor to r^29 / r^28; the eight leading terms in double-double, the tail
+// in double), tan = sin / cos in double-double;
 // the double-double value (relative error < 2^-100) rounded to double.
 struct DD {
     double h, l;
@@ -467,9 +468,17 @@ MPT_HD void cr_sincos_r(DD r, DD &s, DD &c) {
     constexpr double cs[15][2] = MPT_CR_SIN_COEFFS;
     constexpr double cc[15][2] = MPT_CR_COS_COEFFS;
     const DD z = dd_mul(r, r);
-    DD ps{cs[14][0], cs[14][1]}, pc{cc[14][0], cc[14][1]};
+    // terms 14..8 (at most 2^-53 of the sum for |r| <= pi/4 + 2^-30) in plain double over z.h:
+    // their rounding stays below 2^-105 of the result; terms 7..0 in double-double
+    double ts = cs[14][0], tc = cc[14][0];
 #pragma unroll
-    for (int n = 13; n >= 0; --n) {
+    for (int n = 13; n >= 8; --n) {
+        ts = ts * z.h + cs[n][0];
+        tc = tc * z.h + cc[n][0];
+    }
+    DD ps{ts, 0.0}, pc{tc, 0.0};
+#pragma unroll
+    for (int n = 7; n >= 0; --n) {
         ps = dd_add(dd_mul(ps, z), DD{cs[n][0], cs[n][1]});
         pc = dd_add(dd_mul(pc, z), DD{cc[n][0], cc[n][1]});
     }

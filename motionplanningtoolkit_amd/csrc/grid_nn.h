@@ -101,11 +101,25 @@ __host__ __device__ __forceinline__ int32_t query_bucket(const QueryOrder &o, do
     return (int32_t)b;
 }
 
+// The engine's round start, folded into the grid count launch (one launch less per round):
+// the samples generated there instead of by a k_sample launch, and k_sample's bookkeeping.
+constexpr int kGenMaxDim = 16;
+struct SampleGen {
+    double *out = nullptr;  // [nq][d] samples written here (nullptr: the queries are given)
+    uint64_t seed = 0, ext_base = 0;
+    double lo[kGenMaxDim] = {}, hi[kGenMaxDim] = {};
+    int64_t *n_dev = nullptr;              // [0] node count, [1] the round's starting count
+    int64_t set_n = -1;                    // a pending truncation (mpt_rrt_set_size), or -1
+    unsigned long long *counters = nullptr;
+    uint32_t *n_live = nullptr;            // the round's live-unit count, zeroed
+};
+
 // what GridIndex::build buckets alongside its point count
 struct QueryBucketing {
     const double *q = nullptr;  // [nq][d] queries (state dim d, as the points)
     int64_t nq = 0;
     QueryOrder o;
+    SampleGen gen;  // gen.out: generate the queries (engine samples) instead of reading q
 };
 
 class GridIndex {

@@ -88,6 +88,17 @@ __device__ __forceinline__ void bucket_queries(const QueryBucketing &qb, int32_t
     const QueryOrder &o = qb.o;
     if (threadIdx.x < kQueryBuckets) s_cnt[threadIdx.x] = 0;
     __syncthreads();
+    const SampleGen &gen = qb.gen;
+    if (gen.out && first == 0 && threadIdx.x == 0) {
+        // the round's start (what k_sample's thread 0 does): the count kernel's point blocks
+        // take the pending truncation as an argument, so this write races with no reader
+        if (gen.set_n >= 0) {
+            gen.n_dev[0] = gen.set_n;
+            gen.counters[3] = (unsigned long long)gen.set_n;
+        }
+        gen.n_dev[1] = gen.set_n >= 0 ? gen.set_n : gen.n_dev[0];
+        if (gen.n_live) *gen.n_live = 0u;
+    }
     int32_t b[kQueriesPerThread], rank[kQueriesPerThread];
 #pragma unroll
     for (int h = 0; h < kQueriesPerThread; ++h) {
@@ -95,7 +106,20 @@ __device__ __forceinline__ void bucket_queries(const QueryBucketing &qb, int32_t
         b[h] = -1;
         rank[h] = 0;
         if (k < qb.nq) {
-            b[h] = query_bucket(o, qb.q[k * d + o.dim]);
+            double x;
+            if (gen.out) {
+                // the engine's sample k (rrt_engine.hip k_sample: counters g * 64 + j)
+                const uint64_t g = gen.ext_base + (uint64_t)k;
+                x = 0.0;
+                for (int j = 0; j < d; ++j) {
+                    const double v = engine_uniform(gen.seed, g * 64 + j, gen.lo[j], gen.hi[j]);
+                    gen.out[k * d + j] = v;
+                    if (j == o.dim) x = v;
+                }
+            } else {
+                x = qb.q[k * d + o.dim];
+            }
+            b[h] = query_bucket(o, x);
             rank[h] = atomicAdd(&s_cnt[b[h]], 1);
         }
     }
@@ -119,7 +143,10 @@ __global__ __launch_bounds__(256) void k_grid_count(GridParams g, const double *
         return;
     }
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (n_dev) n = *n_dev < n ? *n_dev : n;
+    if (qb.gen.out && qb.gen.set_n >= 0)
+        n = qb.gen.set_n < n ? qb.gen.set_n : n;  // applied to n_dev by the round-start block
+    else if (n_dev)
+        n = *n_dev < n ? *n_dev : n;
     if (i < n) {
         int c[3] = {0, 0, 0};
         for (int j = 0; j < g.gd; ++j) c[j] = cell_coord(pts[i * d + g.dims[j]], g.lo[j], g.inv_h, g.n[j]);

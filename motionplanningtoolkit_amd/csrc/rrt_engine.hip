@@ -692,10 +692,16 @@ StepCtx step_head(mpt_rrt *r, int32_t K, hipStream_t stream, bool defer_tree = f
         c.qo.lo = p.lo[dj];
         c.qo.inv_w = span > 0 ? (double)kQueryBuckets / span : 0.0;
     }
-    hipLaunchKernelGGL(k_sample, dim3(kb), dim3(256), 0, stream, p, r->ext_base, K, r->d_samples, r->d_n,
-                       live_list ? r->d_nlive : nullptr, r->pending_n, r->d_counters);
+    // grid rounds with bucketed samples generate them in the grid count launch (its extra
+    // workgroups, with k_sample's bookkeeping): one launch less per round
+    const bool fuse_sample = c.qo.list != nullptr;
+    const int64_t set_n = r->pending_n;
     r->pending_n = -1;
-    hip_check(hipGetLastError(), "k_sample");
+    if (!fuse_sample) {
+        hipLaunchKernelGGL(k_sample, dim3(kb), dim3(256), 0, stream, p, r->ext_base, K, r->d_samples, r->d_n,
+                           live_list ? r->d_nlive : nullptr, set_n, r->d_counters);
+        hip_check(hipGetLastError(), "k_sample");
+    }
     c.mark(1, stream);
     // the spread feedback rides on this round's index build when none is in flight
     SpreadOut spread;
@@ -748,6 +754,20 @@ StepCtx step_head(mpt_rrt *r, int32_t K, hipStream_t stream, bool defer_tree = f
         qb.q = r->d_samples;
         qb.nq = K;
         qb.o = c.qo;
+        if (fuse_sample) {
+            SampleGen &gen = qb.gen;
+            gen.out = r->d_samples;
+            gen.seed = p.seed;
+            gen.ext_base = r->ext_base;
+            for (int j = 0; j < p.d && j < kGenMaxDim; ++j) {
+                gen.lo[j] = p.lo[j];
+                gen.hi[j] = p.hi[j];
+            }
+            gen.n_dev = r->d_n;
+            gen.set_n = set_n;
+            gen.counters = r->d_counters;
+            gen.n_live = live_list ? r->d_nlive : nullptr;
+        }
         r->grid->build(r->d_nodes, r->n_upper, r->d_n, p.d, g, stream, want_spread ? &spread : nullptr,
                        c.qo.list ? &qb : nullptr);
     }

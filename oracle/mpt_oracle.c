@@ -705,7 +705,8 @@ int32_t orc_omni_get_poses(const double start[3], const double end[3], double dt
  *
  * Method: x = k pi/2 + r with pi/2 split into four parts (P1..P3 of 33 bits, so k * Pi is
  * exact for |k| < 2^20), r in double-double; sin r and cos r by Horner over r^2 in
- * double-double (Taylor series to r^29 / r^28, |r| <= pi/4 + 2^-30: truncation < 2^-110);
+ * double-double (Taylor series to r^29 / r^28, |r| <= pi/4 + 2^-30: truncation < 2^-110; the
+ * eight leading terms in double-double, the tail in double);
  * tan = sin / cos in double-double.  The double-double result (relative error below
  * 2^-100) rounded to double is the correctly rounded value unless the exact value lies
  * within 2^-100 of a rounding boundary.  Coefficients: exact 1/n! split hi + lo.
@@ -764,9 +765,13 @@ static int cr_reduce(double x, orc_dd *r) {
     *r = a;
     return (int)((int64_t)k & 3);
 }
+/* terms 14..8 (at most 2^-53 of the sum for |r| <= pi/4 + 2^-30) in double over z.h, their
+ * rounding below 2^-105 of the result; terms 7..0 in double-double */
 static orc_dd cr_poly(const double c[15][2], orc_dd z) {
-    orc_dd acc = {c[14][0], c[14][1]};
-    for (int n = 13; n >= 0; --n) {
+    double t = c[14][0];
+    for (int n = 13; n >= 8; --n) t = t * z.h + c[n][0];
+    orc_dd acc = {t, 0.0};
+    for (int n = 7; n >= 0; --n) {
         const orc_dd cn = {c[n][0], c[n][1]};
         acc = dd_add(dd_mul(acc, z), cn);
     }
