@@ -36,6 +36,7 @@ constexpr int kCandCap = 2048;      // candidates per k_cands wave (then the spi
 constexpr int64_t kSplitChunkThreads = int64_t(1) << 22;  // (unit, cluster) threads per launch of the two-phase path
 constexpr int kSpillCap = 1 << 22;  // shared spill list (48 MiB)
 constexpr int kLdsItems = 2048;     // env tree staged in LDS by k_pairs up to this size (64 KiB)
+constexpr int kCandsLdsItems = 1024;  // env triangle items staged in LDS by k_cands up to this count
 constexpr int kStack = kMaxLevels;  // per-thread walk stack (general trees)
 
 struct SplitArgs {
@@ -202,7 +203,7 @@ __global__ __launch_bounds__(kPairThreads) void k_pairs(EnvDev env, const AgentD
         PairRec r;
         if (live) {
             double R[9], T[3];
-            unit_transform(env, w.poses + (slot * w.L + link) * 12, R, T);
+            unit_rt(env, w, slot, link, R, T);
             const Cluster &cl = links[link].clusters[c];
             local_box(cl.c, cl.e, R, T, r.lo, r.hi);
             r.unit = (int32_t)unit;
@@ -323,23 +324,39 @@ __device__ __forceinline__ bool emit(bool h, uint64_t m, int32_t unit, int32_t a
     return true;
 }
 
+// lds_items: the env's triangle items [0, n_tris) staged in LDS (small envs), else read
+// through the caches.  A header's chain of dependent loads is dense slot -> header -> {pose,
+// agent triangles, pair words} -> env items; the next header's dense slot is fetched ahead.
 __global__ __launch_bounds__(256) void k_cands(EnvDev env, const AgentDev *__restrict__ links, CollideWork w,
-                                               SplitArgs a) {
+                                               SplitArgs a, int32_t lds_items) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
     const int32_t cw = (int32_t)blockIdx.x * 4 + wave;
     const uint32_t total = __builtin_amdgcn_readfirstlane(a.hdr_off[a.n_seg]);
+    const Item *items = env.items;
+    if (lds_items > 0) {
+        Item *s_items = reinterpret_cast<Item *>(smem);
+        const uint4 *src = reinterpret_cast<const uint4 *>(env.items);
+        uint4 *dst = reinterpret_cast<uint4 *>(s_items);
+        for (int i = threadIdx.x; i < lds_items * 2; i += blockDim.x) dst[i] = src[i];
+        __syncthreads();
+        items = s_items;
+    }
     Cand *cseg = a.cand + (int64_t)cw * a.cand_cap;
     uint32_t cnt = 0, n_xf = 0;
+    int32_t slot_next = (uint32_t)cw < total ? __builtin_amdgcn_readfirstlane(a.hdr_dense[cw]) : 0;
     for (uint32_t g = (uint32_t)cw; g < total; g += (uint32_t)a.n_cwaves) {
-        const int32_t slot_h = __builtin_amdgcn_readfirstlane(a.hdr_dense[g]);
+        const int32_t slot_h = slot_next;
         const PairHdr H = a.hdr[slot_h];
+        if (g + (uint32_t)a.n_cwaves < total)
+            slot_next = __builtin_amdgcn_readfirstlane(a.hdr_dense[g + (uint32_t)a.n_cwaves]);
         const int32_t unit = __builtin_amdgcn_readfirstlane(H.unit);
         const int32_t hseg = __builtin_amdgcn_readfirstlane(H.seg);
         const int32_t hlane = __builtin_amdgcn_readfirstlane(H.lane);
+        const int32_t hn = __builtin_amdgcn_readfirstlane(H.n);  // this header's pair words
         const int32_t tfirst = __builtin_amdgcn_readfirstlane(H.tfirst);
         const int32_t tcount = __builtin_amdgcn_readfirstlane(H.tcount);
-        const int32_t sp = __builtin_amdgcn_readfirstlane(a.pair_count[hseg]);
         const int32_t *spairs = a.pairs + (int64_t)hseg * a.pair_cap;
         int32_t link;
         int64_t slot, edge;
@@ -347,7 +364,7 @@ __global__ __launch_bounds__(256) void k_cands(EnvDev env, const AgentDev *__res
         const bool act = lane < tcount;
         const double *tri = links[link].tris + (int64_t)(tfirst + (act ? lane : 0)) * 9;
         double R[9], T[3];
-        unit_transform(env, w.poses + (slot * w.L + link) * 12, R, T);
+        unit_rt(env, w, slot, link, R, T);
 #pragma unroll
         for (int i = 0; i < 9; ++i) R[i] = uniform_d(R[i]);
 #pragma unroll
@@ -360,17 +377,30 @@ __global__ __launch_bounds__(256) void k_cands(EnvDev env, const AgentDev *__res
             tlo[k] = wave_min(act ? blo[k] : __builtin_huge_valf());
             thi[k] = wave_max(act ? bhi[k] : -__builtin_huge_valf());
         }
-        for (int32_t k0 = 0; k0 < sp; k0 += 64) {
-            // lanes scan 64 words of the segment; this header's are those of its lane
+        // lanes scan the segment 64 words at a time; this header's words are those of its lane,
+        // all hn of them in the segment (a thread whose pairs overflowed wrote no header), so
+        // the scan stops once it has seen hn: no read of the segment's count, and never a word
+        // past the last one written this round
+        for (int32_t k0 = 0, found = 0; found < hn && k0 < a.pair_cap; k0 += 64) {
             bool mine = false;
             int32_t etri = 0;
             Item e{};
-            if (k0 + lane < sp) {
+            if (k0 + lane < a.pair_cap) {
                 const uint32_t word = (uint32_t)spairs[k0 + lane];
                 mine = (int32_t)(word >> kPairTriBits) == hlane;
                 etri = (int32_t)(word & ((1u << kPairTriBits) - 1u));
-                if (mine) e = env.items[etri];
             }
+            found += (int32_t)__popcll(__ballot(mine));
+            // words past this header's last one may be stale (earlier rounds): keep only the
+            // first hn - (found before this block) of this block's matches
+            if (found > hn) {
+                const uint64_t mm = __ballot(mine);
+                const int keep = hn - (found - (int32_t)__popcll(mm));
+                const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(mm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mm, 0u));
+                if (mine && (int)rank >= keep) mine = false;
+                found = hn;
+            }
+            if (mine) e = items[etri];
             // env triangles that miss the union of the agent triangle boxes are dropped
             uint64_t M = __ballot(mine && box_overlap(tlo, thi, e.lo, e.hi));
             bool ok = true;
@@ -414,7 +444,8 @@ __device__ __forceinline__ void narrow_range(const EnvDev &env, const AgentDev *
         int64_t slot, edge;
         decode_unit(w, cd.unit, link, slot, edge);
         const uint8_t decided = load_flag(w.verdict + edge);
-        const double *pose = w.poses + (slot * w.L + link) * 12;
+        // the unit's relative transform (precomputed) or its pose
+        const double *pose = (w.unit_rt ? w.unit_rt : w.poses) + (slot * w.L + link) * 12;
         double P[12];
 #pragma unroll
         for (int k = 0; k < 12; ++k) P[k] = pose[k];
@@ -424,7 +455,14 @@ __device__ __forceinline__ void narrow_range(const EnvDev &env, const AgentDev *
         for (int k = 0; k < 9; ++k) A[k] = t[k];
         if (decided) continue;  // another candidate of this edge already found the contact
         double R[9], T[3];
-        relative_transform(env.tf, env.tf + 9, P, P + 9, R, T);
+        if (w.unit_rt) {
+#pragma unroll
+            for (int k = 0; k < 9; ++k) R[k] = P[k];
+#pragma unroll
+            for (int k = 0; k < 3; ++k) T[k] = P[9 + k];
+        } else {
+            relative_transform(env.tf, env.tf + 9, P, P + 9, R, T);
+        }
         const v3 Q1 = xform(R, T, mk(A[0], A[1], A[2]));
         const v3 Q2 = xform(R, T, mk(A[3], A[4], A[5]));
         const v3 Q3 = xform(R, T, mk(A[6], A[7], A[8]));
@@ -644,7 +682,12 @@ static void collide_split_chunk(const EnvDev &env, const AgentDev *d_links, int3
     // count slot `segs` is the scan's sentinel (a larger earlier launch may have used it): k_pairs zeroed it
     // one segment per thread: the epilogue writes up to 64 header slots per segment
     launch_scan_excl<1>(s.hdr_scan, s.hdr_count, s.hdr_off, segs + 1, stream, ExpandHeaders{s.hdr_dense, segs});
-    hipLaunchKernelGGL(k_cands, dim3((unsigned)((s.n_cwaves + 3) / 4)), dim3(256), 0, stream, env, d_links, w, a);
+    // the env's triangle items in LDS when they fit in 32 KiB (four workgroups per CU);
+    // MPT_CANDS_LDS=0: always through the caches (A/B knob)
+    static const bool cands_lds = !(getenv("MPT_CANDS_LDS") && atoi(getenv("MPT_CANDS_LDS")) == 0);
+    const int32_t cl_items = cands_lds && env.n_tris <= kCandsLdsItems ? env.n_tris : 0;
+    hipLaunchKernelGGL(k_cands, dim3((unsigned)((s.n_cwaves + 3) / 4)), dim3(256), sizeof(Item) * (size_t)cl_items,
+                       stream, env, d_links, w, a, cl_items);
     hip_check(hipGetLastError(), "k_cands launch");
     mark(1);
     const unsigned nblocks = (unsigned)((s.n_cwaves + kSpillWaves + kNarrowWaves - 1) / kNarrowWaves);
@@ -684,10 +727,12 @@ void launch_collide_split(const EnvDev &env, const AgentDev *d_links, int32_t ma
         if (w.pose_edge) {
             const int64_t p0 = u0 / w.L;
             c.poses = w.poses + p0 * w.L * 12;
+            if (w.unit_rt) c.unit_rt = w.unit_rt + p0 * w.L * 12;
             c.pose_edge = w.pose_edge + p0;
         } else {
             const int64_t e0 = u0 / g;
             c.poses = w.poses + e0 * g * 12;
+            if (w.unit_rt) c.unit_rt = w.unit_rt + e0 * g * 12;
             c.pcount = w.pcount + e0;
             c.verdict = w.verdict + e0;
         }

@@ -41,6 +41,21 @@ __device__ __forceinline__ void unit_transform(const EnvDev &env, const double *
     relative_transform(env.tf, env.tf + 9, R2, T2, R, T);
 }
 
+// The unit's relative transform: precomputed (w.unit_rt: bitwise unit_transform's result) or
+// computed from its pose.
+__device__ __forceinline__ void unit_rt(const EnvDev &env, const CollideWork &w, int64_t slot, int32_t link,
+                                        double R[9], double T[3]) {
+    const int64_t o = (slot * w.L + link) * 12;
+    if (w.unit_rt) {
+#pragma unroll
+        for (int i = 0; i < 9; ++i) R[i] = w.unit_rt[o + i];
+#pragma unroll
+        for (int i = 0; i < 3; ++i) T[i] = w.unit_rt[o + 9 + i];
+    } else {
+        unit_transform(env, w.poses + o, R, T);
+    }
+}
+
 // Agent triangle mapped exactly as FCL does (Q' = R Q + T) and its widened float box.
 __device__ __forceinline__ void agent_tri_box(const double *__restrict__ t, const double R[9], const double T[3],
                                               float blo[3], float bhi[3]) {

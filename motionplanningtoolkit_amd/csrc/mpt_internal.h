@@ -98,6 +98,10 @@ struct CollideWork {
     // (live unit, cluster) threads only.  Any order; n_live read on the device.
     const int32_t *live_units;
     const uint32_t *n_live;
+    // two-phase path, optional: each unit's FCL relative transform [slots][L][12] (R row-major,
+    // then T), computed by the producer of the poses exactly as unit_transform does, so the
+    // stages load it instead of recomputing it per (unit, cluster), header and candidate
+    const double *unit_rt;
 };
 
 // Broad-phase candidate: (unit, agent triangle, env triangle) whose float boxes overlap.

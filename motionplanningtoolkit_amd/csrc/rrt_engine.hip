@@ -273,6 +273,7 @@ struct LiveOut {
     EnvDev env;
     int32_t *q_count;    // the round's QueryOrder counts (read by the NN launch): zeroed here
     int32_t q_nb;
+    double *unit_rt;     // [K * pmax * L][12]: each unit's relative transform (CollideWork::unit_rt)
 };
 
 // randomSteer + getPoses, then the extension's live units appended to the round's list
@@ -295,6 +296,11 @@ __global__ __launch_bounds__(256) void k_steer(EngineParams p, uint64_t ext_base
         for (int32_t l = 0; l < p.L; ++l) {
             double R[9], T[3];
             unit_transform(lv.env, ps + (i * p.L + l) * 12, R, T);
+            double *rt = lv.unit_rt + (k * units + i * p.L + l) * 12;
+#pragma unroll
+            for (int j = 0; j < 9; ++j) rt[j] = R[j];
+#pragma unroll
+            for (int j = 0; j < 3; ++j) rt[9 + j] = T[j];
             float blo[3], bhi[3];
             local_box(lv.links[l].bc, lv.links[l].be, R, T, blo, bhi);
             if (box_overlap(blo, bhi, lv.env.root_lo, lv.env.root_hi)) mask |= 1ull << (i * p.L + l);
@@ -396,6 +402,7 @@ struct mpt_rrt {
     double *d_samples = nullptr, *d_ends = nullptr, *d_poses = nullptr, *d_nnd2 = nullptr;
     int32_t *d_nn = nullptr, *d_pcount = nullptr;
     int32_t *d_live = nullptr;     // k_steer's live-unit list [K * pmax * L] (two-phase collide)
+    double *d_rt = nullptr;        // k_steer's unit relative transforms [K * pmax * L][12] (two-phase)
     uint32_t *d_nlive = nullptr;   // its length
     uint8_t *d_verdict = nullptr;
     void *d_scratch = nullptr;
@@ -441,7 +448,7 @@ namespace {
 void rfree(mpt_rrt *r) {
     void *ps[] = {r->d_links, r->d_nodes,   r->d_parents, r->d_n,       r->d_counters, r->d_samples,
                   r->d_ends,  r->d_poses,   r->d_nnd2,    r->d_nn,      r->d_pcount,
-                  r->d_verdict, r->d_scratch, r->d_cstats, r->d_live, r->d_nlive};
+                  r->d_verdict, r->d_scratch, r->d_cstats, r->d_live, r->d_nlive, r->d_rt};
     for (void *p : ps)
         if (p) (void)hipFree(p);
     for (auto &e : r->ring)
@@ -471,7 +478,8 @@ void timing_fold_one(mpt_rrt *r) {
 void ensure_round_buffers(mpt_rrt *r, int32_t K) {
     const size_t need_scratch = nn_knn_scratch_bytes(K, std::max<int64_t>(r->cap, 1), 1);
     if (K > r->kcap) {
-        void *ps[] = {r->d_samples, r->d_ends, r->d_poses, r->d_nnd2, r->d_nn, r->d_pcount, r->d_verdict, r->d_live};
+        void *ps[] = {r->d_samples, r->d_ends, r->d_poses, r->d_nnd2, r->d_nn, r->d_pcount, r->d_verdict, r->d_live,
+                      r->d_rt};
         for (void *p : ps)
             if (p) hip_check(hipFree(p), "hipFree");
         const int64_t d = r->p.d;
@@ -483,6 +491,7 @@ void ensure_round_buffers(mpt_rrt *r, int32_t K) {
         hip_check(hipMalloc(&r->d_pcount, sizeof(int32_t) * K), "alloc pcount");
         hip_check(hipMalloc(&r->d_verdict, (size_t)K), "alloc verdict");
         hip_check(hipMalloc(&r->d_live, sizeof(int32_t) * (int64_t)K * r->p.pmax * r->p.L), "alloc live units");
+        hip_check(hipMalloc(&r->d_rt, sizeof(double) * 12 * (int64_t)K * r->p.pmax * r->p.L), "alloc unit transforms");
         if (!r->d_nlive) hip_check(hipMalloc(&r->d_nlive, sizeof(uint32_t)), "alloc live count");
         r->kcap = K;
         r->cscratch.ensure((int64_t)K * r->p.pmax * r->p.L, r->max_clusters);
@@ -826,7 +835,7 @@ void step_tail(mpt_rrt *r, int32_t K, hipStream_t stream, const StepCtx &c) {
     hipEvent_t *ev = c.ev;
     auto steer = p.kind == MPT_AGENT_OMNI ? k_steer<MPT_AGENT_OMNI>
                  : (p.kind == MPT_AGENT_BLIMP ? k_steer<MPT_AGENT_BLIMP> : k_steer<MPT_AGENT_SNAKE>);
-    LiveOut lv{live_list ? r->d_live : nullptr, r->d_nlive, r->d_links, r->env, c.qo.count, c.qo.nb};
+    LiveOut lv{live_list ? r->d_live : nullptr, r->d_nlive, r->d_links, r->env, c.qo.count, c.qo.nb, r->d_rt};
     hipLaunchKernelGGL(steer, dim3(kb), dim3(256), 0, stream, p, r->ext_base, K, r->d_nodes, r->d_nn, r->d_ends,
                        r->d_poses, r->d_pcount, r->d_verdict, r->d_counters, lv);
     hip_check(hipGetLastError(), "k_steer");
@@ -841,6 +850,7 @@ void step_tail(mpt_rrt *r, int32_t K, hipStream_t stream, const StepCtx &c) {
     cw.verdict = r->d_verdict;
     cw.stats = r->stats_on ? r->d_cstats : nullptr;
     cw.live_units = live_list ? r->d_live : nullptr;
+    cw.unit_rt = live_list ? r->d_rt : nullptr;  // k_steer writes them with the live list
     cw.n_live = live_list ? r->d_nlive : nullptr;
     if (collide_mode() == MPT_COLLIDE_FUSED) {
         launch_collide(r->env, r->d_links, cw, stream);
