@@ -495,6 +495,8 @@ __device__ __forceinline__ void narrow_range(const EnvDev &env, const AgentDev *
 // recompute cost more than the 384-B records they save (A/B: blimp.inst, 2.1 candidates
 // per env tri per workgroup, 34 us global vs 36 us staged; blimp-room, 16: 174 vs 162 us).  The overflow re-run lives in
 // k_overflow: the fused walk's registers in this kernel cost a wave per SIMD (158 VGPRs).
+// Not kept: a gate-first pass queueing survivors in LDS and running the SAT on full waves of
+// them (reloaded and re-transformed) -- room narrow 169 -> 181 us, config 2 33 -> 34 us.
 constexpr int kNarrowWaves = 4;
 constexpr int kSpillWaves = 256;
 constexpr int kOvfWaves = 64;

@@ -196,14 +196,24 @@ MPT_HD bool tri_intersect(const ETri &E, v3 Q1, v3 Q2, v3 Q3) {
 // quantity is recomputed with exactly make_env_tri's operations (so bitwise the record's
 // fields) at its point of use, so a kernel can keep only the 72-B vertices on chip (LDS)
 // and spend FP64 instead of dependent loads of the 384-B record.
-MPT_HD bool tri_collide_verts(const double *t, v3 Q1, v3 Q2, v3 Q3) {
-    double lo[3], hi[3];
+// the env triangle's exact vertex box from its vertices t[9] (make_env_tri's lo / hi)
+MPT_HD void tri_box_verts(const double *t, double lo[3], double hi[3]) {
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
         lo[k] = dmin(t[k], dmin(t[3 + k], t[6 + k]));
         hi[k] = dmax(t[k], dmax(t[3 + k], t[6 + k]));
     }
+}
+MPT_HD bool tri_sat_verts(const double *t, v3 Q1, v3 Q2, v3 Q3);
+MPT_HD bool tri_collide_verts(const double *t, v3 Q1, v3 Q2, v3 Q3) {
+    double lo[3], hi[3];
+    tri_box_verts(t, lo, hi);
     if (!tri_gate(lo, hi, Q1, Q2, Q3)) return false;
+    return tri_sat_verts(t, Q1, Q2, Q3);
+}
+// intersect_Triangle from the env triangle's vertices (the P-side fields recomputed as
+// make_env_tri does), without the box gate
+MPT_HD bool tri_sat_verts(const double *t, v3 Q1, v3 Q2, v3 Q3) {
     const v3 P1 = mk(t[0], t[1], t[2]), P2 = mk(t[3], t[4], t[5]), P3 = mk(t[6], t[7], t[8]);
     const v3 p1 = sub(P1, P1), p2 = sub(P2, P1), p3 = sub(P3, P1);
     const v3 e1 = sub(p2, p1), e2 = sub(p3, p2), e3 = sub(p1, p3);

@@ -8,6 +8,10 @@ TAG=$1; shift
 ARGS=${BENCH_ARGS:---steps 20 --warmup 3 --no-cpu}
 OUT=gpurun_out/ab_$TAG
 mkdir -p $OUT
+# a throw-away first run: the first bench process on a box ran a few % slow (clocks, caches)
+if [ -z "$NO_WARM" ]; then
+  timeout -k 10 300 python bench.py $ARGS > $OUT/warm.log 2>&1 || { tail -5 $OUT/warm.log; exit 1; }
+fi
 for v in "$@"; do
   name=${v%%:*}; envs=${v#*:}
   echo "== $name: $envs python bench.py $ARGS"
