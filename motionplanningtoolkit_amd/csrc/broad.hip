@@ -30,7 +30,7 @@
 namespace mpt {
 
 constexpr int kPairThreads = 256;   // k_pairs workgroup (4 waves)
-constexpr int kPairCap = 256;       // env triangles per k_pairs wave segment
+constexpr int kPairCap = 512;       // env triangles per k_pairs wave segment (256: the room overflowed units into k_overflow, 17-27 us a round)
 constexpr int kHdrCap = 64;         // headers per segment (one per lane at most)
 constexpr int kCandCap = 2048;      // candidates per k_cands wave (then the spill list)
 constexpr int64_t kSplitChunkThreads = int64_t(1) << 22;  // (unit, cluster) threads per launch of the two-phase path
@@ -614,7 +614,9 @@ void CollideScratch::ensure(int64_t n_units, int32_t max_clusters) {
         void *ps[] = {pairs, hdr, hdr_count, pair_count, hdr_off, hdr_dense};
         for (void *p : ps)
             if (p) hip_check(hipFree(p), "hipFree");
-        pair_cap = kPairCap;
+        // MPT_PAIR_CAP: pair words per k_pairs wave segment (A/B knob)
+        static const int32_t cap_env = getenv("MPT_PAIR_CAP") ? atoi(getenv("MPT_PAIR_CAP")) : 0;
+        pair_cap = cap_env >= 64 ? cap_env : kPairCap;
         hip_check(hipMalloc(&pairs, sizeof(int32_t) * (size_t)segs * pair_cap), "alloc pairs");
         hip_check(hipMalloc(&hdr, sizeof(PairHdr) * (size_t)segs * kHdrCap), "alloc headers");
         hip_check(hipMalloc(&hdr_count, sizeof(uint32_t) * (size_t)(segs + 1)), "alloc header counts");

@@ -282,10 +282,12 @@ def test_engines_on_streams_match_one_stream(mpt_gpu):
         assert np.array_equal(bits(sa), bits(sb)) and np.array_equal(pa, pb)
 
 
-def test_step_many_matches_single_steps(mpt_gpu):
+def test_step_many_matches_single_steps(mpt_gpu, oracle):
     """mpt_rrt_step_many (config 5's joint NN launch): twelve seeds over four streams, all but
     one on the Morton tree (one launch of k_tree_nn1_jobs per round) and one on the grid (its
-    own query), must grow exactly the trees each seed grows alone with mpt_rrt_step."""
+    own query), must grow exactly the trees each seed grows alone with mpt_rrt_step -- and, for
+    three of the seeds, exactly the oracle's engine rounds (orc_engine_step) from the same
+    root."""
     import torch
 
     sc = scenes.blimp_scenario("all")
@@ -322,6 +324,18 @@ def test_step_many_matches_single_steps(mpt_gpu):
     for (sa, pa), (sb, pb) in zip(alone, joint):
         assert len(sa) > 2048
         assert np.array_equal(bits(sa), bits(sb)) and np.array_equal(pa, pb)
+    bvh = oracle.BVH(sc.env_tris)
+    for j in (0, 5, len(seeds) - 1):
+        ref = np.zeros((1 + rounds * K, sc.dim))
+        ref[0] = root[0]
+        par = np.zeros(1 + rounds * K, np.int32)
+        n = 1
+        for r in range(rounds):
+            n, _, _ = oracle.engine_step(sc.kind, sc.prm, sc.ranges, sc.steer_dt, sc.cc_dt, seeds[j], r * K, K, bvh,
+                                         sc.env_tf, sc.agent_tris, ref, par, n, nthreads=8)
+        sb, pb = joint[j]
+        assert n == len(sb)
+        assert np.array_equal(bits(sb), bits(ref[:n])) and np.array_equal(pb, par[:n])
 
 
 def test_step_many_groups_on_separate_joint_streams(mpt_gpu):
