@@ -617,6 +617,9 @@ void CollideScratch::ensure(int64_t n_units, int32_t max_clusters) {
         // MPT_PAIR_CAP: pair words per k_pairs wave segment (A/B knob)
         static const int32_t cap_env = getenv("MPT_PAIR_CAP") ? atoi(getenv("MPT_PAIR_CAP")) : 0;
         pair_cap = cap_env >= 64 ? cap_env : kPairCap;
+        // Not kept: each thread's pairs as one contiguous run (staged in LDS, placed after a
+        // wave scan) so a k_cands header reads only its own words -- room k_pairs 119 -> 140 us
+        // (LDS staging, occupancy), k_cands unchanged (its pair scan was not what bounds it).
         hip_check(hipMalloc(&pairs, sizeof(int32_t) * (size_t)segs * pair_cap), "alloc pairs");
         hip_check(hipMalloc(&hdr, sizeof(PairHdr) * (size_t)segs * kHdrCap), "alloc headers");
         hip_check(hipMalloc(&hdr_count, sizeof(uint32_t) * (size_t)(segs + 1)), "alloc header counts");
