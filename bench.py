@@ -438,7 +438,7 @@ def run_seeds(args, world, rank, dist, torch, mpt, multiseed, scenes):
     c1 = [e.counters() for e in engines]
     valid = sum(b["valid"] - a["valid"] for a, b in zip(c0, c1))
     checked = sum(b["checked"] - a["checked"] for a, b in zip(c0, c1))
-    elapsed, (valid, checked) = multiseed.reduce_run(dist, elapsed, [valid, checked], "cuda")
+    elapsed, (valid, checked) = multiseed.reduce_run(dist, elapsed, [valid, checked], args.red_dev)
     digests = {}
     for i, e, c in zip(mine, engines, c1):
         st, par = e.read_tree(c["nodes"])
@@ -475,7 +475,10 @@ def run_seeds(args, world, rank, dist, torch, mpt, multiseed, scenes):
         csts = [e.collide_stats(False) for e in eg0]
         mpt.step_many(eg0, K, ss0, js0)
         torch.cuda.synchronize()
-        jt = mpt.joint_times(js0)
+        try:
+            jt = mpt.joint_times(js0)
+        except mpt.MptError:
+            jt = None  # no joint launch: every tree still below the Morton-tree size (small runs)
         cst = csts[0]
         per_launch = dict(e0.kernel_times())
         n_tot = sum(e.counters()["nodes"] for e in eg0) - len(eg0) * K  # nodes before the timed call (upper bound)
@@ -486,7 +489,8 @@ def run_seeds(args, world, rank, dist, torch, mpt, multiseed, scenes):
         nj = len(eg0)
         work_nn = {k: sum(c[k] for c in csts) for k in ("nn_points", "nn_cells")}
         agg = dict(cst, **work_nn)
-        for s, kern, ms in (("nn_build", "k_pt_bbox_jobs", jt["build"]), ("nn_query", "k_tree_nn1_jobs<7,", jt["nn"])):
+        joint_stages = (("nn_build", "k_pt_bbox_jobs", jt["build"]), ("nn_query", "k_tree_nn1_jobs<7,", jt["nn"])) if jt else ()
+        for s, kern, ms in joint_stages:
             b = compulsory_bytes(s, agg, K * nj, max(n_tot, 1), sc.dim, pmax, geo, "tree")
             t = ms * 1e-3
             st = {"kernel": kern, "ms": round(ms, 4), "compulsory_bytes": int(b),
@@ -498,7 +502,8 @@ def run_seeds(args, world, rank, dist, torch, mpt, multiseed, scenes):
                            "frac_hbm_measured": round(tr / t / 1e9 / HBM_PEAK_GBS, 4),
                            "traffic_over_compulsory": round(tr / b, 2)})
             stages[s] = st
-        roof = roofline_of(stages, "nn_query", dict(cst, work_nn_all_seeds=work_nn), summ_path)
+        dom = "nn_query" if "nn_query" in stages else (max(stages, key=lambda k: stages[k]["ms"]) if stages else None)
+        roof = roofline_of(stages, dom, dict(cst, work_nn_all_seeds=work_nn), summ_path)
     import hashlib
 
     all_digest = hashlib.sha256("".join(digests[i] for i in sorted(digests)).encode()).hexdigest()
@@ -540,12 +545,23 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # MPT_DIST_BACKEND=gloo + MPT_BENCH_DEVICE=0: several ranks on one GPU (the multi-rank path
+    # rehearsed on a one-GPU box, tests/test_bench_gpu.py); the driver's runs use RCCL, one
+    # rank per GPU
+    backend = os.environ.get("MPT_DIST_BACKEND", "nccl")
+    if os.environ.get("MPT_BENCH_DEVICE") is not None:
+        local = int(os.environ["MPT_BENCH_DEVICE"])
     dist = None
     if world > 1:
         import torch.distributed as dist
 
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
+    red_dev = "cuda" if backend == "nccl" else "cpu"
+    args.red_dev = red_dev
     import motionplanningtoolkit_amd as mpt
     from motionplanningtoolkit_amd import multiseed, scenes
 
@@ -610,7 +626,7 @@ def main():
     valid = c1["valid"] - c0["valid"]
     checked = c1["checked"] - c0["checked"]
 
-    elapsed, (valid, checked) = multiseed.reduce_run(dist, elapsed, [valid, checked], "cuda")
+    elapsed, (valid, checked) = multiseed.reduce_run(dist, elapsed, [valid, checked], red_dev)
 
     if rank != 0:
         if dist:

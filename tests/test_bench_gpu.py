@@ -1,0 +1,44 @@
+"""The bench's multi-rank path on the GPU: config 5 sharded over two ranks (torchrun, gloo for
+the collectives, both ranks on the box's one GPU -- the driver's 8-GPU runs use RCCL, one rank
+per GPU) must grow exactly the trees one rank grows for the same seeds: the seeds digest of the
+two-rank run equals the one-rank run's.  Each run is a subprocess with its own time limit."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _run(cmd, env):
+    r = subprocess.run(cmd, cwd=REPO, env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    return json.loads(lines[0])
+
+
+@pytest.mark.timeout(600)
+def test_two_ranks_shard_config5_like_one():
+    env = dict(os.environ, MPT_DIST_BACKEND="gloo", MPT_BENCH_DEVICE="0")
+    args = ["bench.py", "--seeds", "8", "--seed-batch", "4096", "--steps", "2", "--warmup", "2", "--no-cpu",
+            "--streams", "4"]
+    one = _run([sys.executable] + args, env)
+    two = _run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                "--master-addr", "127.0.0.1", "--master-port", str(_port())] + args + ["--gpus", "2"], env)
+    assert two["n_gpus"] == 2 and one["n_gpus"] == 1
+    assert two["seeds_digest"] == one["seeds_digest"]
+    assert two["valid_fraction"] == one["valid_fraction"]
