@@ -76,7 +76,7 @@ struct DistLds {
 static_assert(kMaxLevels <= 8, "stack entries pack the level in 3 bits");
 
 // Exact triangle distances of the queued pairs, one pair per lane; returns the new bound.
-template <int kOcc>
+template <int kOcc, bool kSel>
 __device__ __forceinline__ double flush_pairs(const EnvDev &env, DistLds &s, int n, int lane, double U,
                                               unsigned long long *bp, DistCounters &cnt) {
     double d = DBL_MAX;
@@ -87,7 +87,7 @@ __device__ __forceinline__ double flush_pairs(const EnvDev &env, DistLds &s, int
         const EnvTri &E = env.tris[e >> 6];
         const v3 S[3] = {mk(E.P1[0], E.P1[1], E.P1[2]), mk(E.P2[0], E.P2[1], E.P2[2]), mk(E.P3[0], E.P3[1], E.P3[2])};
         // at 4 waves per SIMD the rolled form (128 VGPRs); else the unrolled one
-        d = tri_distance<kOcc >= 4 ? 1 : 3>(S, E.lo, E.hi, Q);
+        d = tri_distance<kOcc >= 4 ? 1 : 3, kSel>(S, E.lo, E.hi, Q);
     }
     cnt.tri_calls += (uint32_t)n;
     const double wb = wave_min_d(d);
@@ -101,7 +101,7 @@ __device__ __forceinline__ double flush_pairs(const EnvDev &env, DistLds &s, int
 // Depth-first walk of the env tree for one agent cluster (box cblo/cbhi, lane's triangle
 // box qlo/qhi, Q' in s.q), nearest child first; pairs that survive the exact box-gap test
 // are queued and evaluated 64 at a time.  Returns the updated bound.
-template <int kOcc>
+template <int kOcc, bool kSel>
 __device__ double walk_cluster(const EnvDev &env, DistLds &s, const float cblo[3], const float cbhi[3], bool act,
                                const double qlo[3], const double qhi[3], const double xlo[3], const double xhi[3],
                                int lane, double U, unsigned long long *bp, DistCounters &cnt) {
@@ -151,7 +151,7 @@ __device__ double walk_cluster(const EnvDev &env, DistLds &s, const float cblo[3
                     if (!act) seed_t = -1;
                     const uint64_t pm = __ballot(act);
                     if (act) s.queue[(int)__popcll(pm & ((1ull << lane) - 1))] = (seed_t << 6) | lane;
-                    U = flush_pairs<kOcc>(env, s, (int)__popcll(pm), lane, U, bp, cnt);
+                    U = flush_pairs<kOcc, kSel>(env, s, (int)__popcll(pm), lane, U, bp, cnt);
                     if (U == 0.0) return U;
                 }
                 // the bucket's env triangles whose exact box is within the bound of the cluster's
@@ -190,7 +190,7 @@ __device__ double walk_cluster(const EnvDev &env, DistLds &s, const float cblo[3
                     qn += (int)__popcll(pm);
                     cnt.pair_tests += (uint32_t)__popcll(__ballot(act));
                     if (qn >= kWave) {
-                        U = flush_pairs<kOcc>(env, s, kWave, lane, U, bp, cnt);
+                        U = flush_pairs<kOcc, kSel>(env, s, kWave, lane, U, bp, cnt);
                         qn -= kWave;
                         if (lane < qn) s.queue[lane] = s.queue[kWave + lane];
                         if (U == 0.0) return U;
@@ -200,7 +200,7 @@ __device__ double walk_cluster(const EnvDev &env, DistLds &s, const float cblo[3
                 // its end) unless c_dist_flush of them are queued: fewer part-empty flushes
                 // against a bound that is staler by at most one bucket
                 if (qn >= c_dist_flush) {
-                    U = flush_pairs<kOcc>(env, s, qn, lane, U, bp, cnt);
+                    U = flush_pairs<kOcc, kSel>(env, s, qn, lane, U, bp, cnt);
                     qn = 0;
                     if (U == 0.0) return U;
                 }
@@ -247,7 +247,7 @@ __device__ double walk_cluster(const EnvDev &env, DistLds &s, const float cblo[3
             }
         }
         if (!found) {
-            if (qn > 0) U = flush_pairs<kOcc>(env, s, qn, lane, U, bp, cnt);
+            if (qn > 0) U = flush_pairs<kOcc, kSel>(env, s, qn, lane, U, bp, cnt);
             return U;
         }
     }
@@ -255,7 +255,7 @@ __device__ double walk_cluster(const EnvDev &env, DistLds &s, const float cblo[3
 
 // One wave per (pose, link) unit: clusters in increasing order of their lower bound over
 // the env tree's top level, each walked with the bound the earlier ones left.
-template <int kOcc>
+template <int kOcc, bool kSel>
 __device__ void distance_unit(const EnvDev &env, const AgentDev *__restrict__ links, const DistWork &w, int64_t unit,
                               int lane, DistLds &s, DistCounters &cnt) {
     const int32_t L = w.L;
@@ -346,7 +346,7 @@ __device__ void distance_unit(const EnvDev &env, const AgentDev *__restrict__ li
                 xlo[k] = uniform_d(lo);
                 xhi[k] = uniform_d(hi);
             }
-            U = walk_cluster<kOcc>(env, s, cblo, cbhi, act, qlo, qhi, xlo, xhi, lane, U, bp, cnt);
+            U = walk_cluster<kOcc, kSel>(env, s, cblo, cbhi, act, qlo, qhi, xlo, xhi, lane, U, bp, cnt);
             if (U == 0.0) return;
         }
     }
@@ -356,7 +356,7 @@ __device__ void distance_unit(const EnvDev &env, const AgentDev *__restrict__ li
 // triDistance (242 VGPRs, 2 waves per SIMD).  4: at most 128 VGPRs with the rolled triDistance
 // (4 waves per SIMD; the LDS allows it, the registers spill ~100 dwords): 12-14 % slower on
 // the blimp in the room (MPT_DIST_OCC=4, scripts/measure_distance.sh).
-template <int kOcc>
+template <int kOcc, bool kSel>
 __global__ __launch_bounds__(kDistWaves * 64, kOcc) void k_distance(EnvDev env, const AgentDev *__restrict__ links,
                                                                  DistWork w) {
     __shared__ DistLds s_lds[kDistWaves];
@@ -364,7 +364,7 @@ __global__ __launch_bounds__(kDistWaves * 64, kOcc) void k_distance(EnvDev env, 
     const int lane = threadIdx.x & 63;
     const int64_t unit = (int64_t)blockIdx.x * kDistWaves + wave;
     DistCounters cnt;
-    if (unit < w.n_units) distance_unit<kOcc>(env, links, w, unit, lane, s_lds[wave], cnt);
+    if (unit < w.n_units) distance_unit<kOcc, kSel>(env, links, w, unit, lane, s_lds[wave], cnt);
     if (w.stats && lane == 0 && unit < w.n_units) {
         atomicAdd(w.stats + 0, (unsigned long long)cnt.clusters);
         atomicAdd(w.stats + 1, (unsigned long long)cnt.items);
@@ -395,10 +395,17 @@ void launch_distance(const EnvDev &env, const AgentDev *d_links, const DistWork 
         return true;
     }();
     (void)flush_set;
-    if (occ == 2)
-        hipLaunchKernelGGL(k_distance<2>, dim3((unsigned)blocks), dim3(kDistWaves * 64), 0, stream, env, d_links, w);
-    else
-        hipLaunchKernelGGL(k_distance<4>, dim3((unsigned)blocks), dim3(kDistWaves * 64), 0, stream, env, d_links, w);
+    // the branch-free segPoints (seg_points_sel: the same values; blimp vs room 12.4 -> 10.1 ms);
+    // MPT_DIST_SEL=0: the branchy form (A/B)
+    static const bool sel = !(getenv("MPT_DIST_SEL") && atoi(getenv("MPT_DIST_SEL")) == 0);
+#define MPT_DIST_LAUNCH(OCC, SEL) \
+    hipLaunchKernelGGL((k_distance<OCC, SEL>), dim3((unsigned)blocks), dim3(kDistWaves * 64), 0, stream, env, d_links, w)
+    if (occ == 2) {
+        if (sel) MPT_DIST_LAUNCH(2, true); else MPT_DIST_LAUNCH(2, false);
+    } else {
+        if (sel) MPT_DIST_LAUNCH(4, true); else MPT_DIST_LAUNCH(4, false);
+    }
+#undef MPT_DIST_LAUNCH
     hip_check(hipGetLastError(), "k_distance launch");
 }
 

@@ -303,6 +303,38 @@ MPT_HD void seg_points(v3 P, v3 A, v3 Q, v3 B, v3 &VEC, v3 &X, v3 &Y) {
     }
 }
 
+// seg_points without branches (the same values: each case's result is computed by the same
+// operations and selected).  In a wave each lane takes its own case of the nested branches,
+// so the branchy form runs the cases one after another; this form runs every lane through
+// one straight path (three divisions and three cross-product chains).
+MPT_HD v3 sel3(bool c, v3 a, v3 b) { return v3{c ? a.x : b.x, c ? a.y : b.y, c ? a.z : b.z}; }
+MPT_HD void seg_points_sel(v3 P, v3 A, v3 Q, v3 B, v3 &VEC, v3 &X, v3 &Y) {
+    const v3 T = sub(Q, P);
+    const double AA = dot(A, A), BB = dot(B, B), AB = dot(A, B), AT = dot(A, T), BT = dot(B, T);
+    const double denom = AA * BB - AB * AB;
+    double t = (AT * BB - BT * AB) / denom;
+    if (t < 0 || isnan(t)) t = 0;
+    else if (t > 1) t = 1;
+    const double u = (t * AB - BT) / BB;
+    const bool u0 = u <= 0 || isnan(u), u1 = !u0 && u >= 1, ue = u0 || u1;
+    // u0 / u1: Y = Q or Q + B and t again from AT / AA or (AB + AT) / AA
+    const double tt = (u0 ? AT : AB + AT) / AA;
+    const v3 QB = add(Q, B), QBu = add(Q, scale(B, u));
+    Y = u0 ? Q : (u1 ? QB : QBu);
+    const double s = ue ? tt : t;  // the parameter X is placed at
+    const bool c0 = s <= 0 || isnan(s), c1 = !c0 && s >= 1;
+    const v3 PA = add(P, A), PAs = add(P, scale(A, s));
+    X = c0 ? P : (c1 ? PA : PAs);
+    // u0 / u1: Y - P, Y - X or A x ((Y - P) x A) (for u0, Y - P is T's subtraction);
+    // interior u: B x ((Q - X) x B) at t = 0 or 1 (Q - P is T's), else +-(A x B)
+    const v3 YP = sub(Y, P), YX = sub(Y, X), QX = sub(Q, X);
+    const v3 D = ue ? A : B, W = ue ? YP : QX;
+    const v3 VC = cross(D, cross(W, D));
+    v3 VAB = cross(A, B);
+    if (dot(VAB, T) < 0) VAB = scale(VAB, -1.0);
+    VEC = ue ? (c0 ? YP : (c1 ? YX : VC)) : ((c0 || c1) ? VC : VAB);
+}
+
 // One triangle's vertex projected onto the other's plane, if it lies inside that face
 // (the "case 1" test of TriangleDistance::triDistance).  Sn = normal of S, Snl = |Sn|^2,
 // Sv = S's edge vectors; Tp[i] = (S0 - T_i).Sn.  Returns true and the distance if found;
@@ -342,7 +374,7 @@ MPT_HD bool face_vertex(const v3 S[3], const v3 Sv[3], v3 Sn, double Snl, const 
 // for collinear ones FCL's answer is 0 at any distance.
 // kUnroll = 1: rolled loops (about 100 fewer VGPRs); 3: fully unrolled (the rotations become
 // register renames).  The same operations in the same order either way.
-template <int kUnroll = 3>
+template <int kUnroll = 3, bool kSel = false>
 MPT_HD double tri_distance(const v3 S[3], const double slo[3], const double shi[3], const v3 T[3]) {
     // The 9 edge pairs in triDistance's order (i over S's edges, j over T's), as rolled loops:
     // the triangles are rotated one vertex per step, so edge i / j is always vertex 0 -> 1 of
@@ -362,7 +394,8 @@ MPT_HD double tri_distance(const v3 S[3], const double slo[3], const double shi[
         for (int j = 0; j < 3; ++j) {
             const v3 tv = sub(t1, t0);
             v3 VEC, P, Q;
-            seg_points(s0, sv, t0, tv, VEC, P, Q);
+            if constexpr (kSel) seg_points_sel(s0, sv, t0, tv, VEC, P, Q);
+            else seg_points(s0, sv, t0, tv, VEC, P, Q);
             const v3 V = sub(Q, P);
             const double dd = dot(V, V);
             if (dd <= mindd) {
