@@ -1,6 +1,8 @@
 """CPU: the C-ABI library builds, loads and exports every declared symbol; host-side
 logic that needs no device (mesh loading) matches the fixtures."""
 import ctypes
+import shutil
+import subprocess
 import os
 import re
 
@@ -89,3 +91,53 @@ def test_synthetic_envs():
     assert np.array_equal(c, scenes.corridor_env(0))
     r = scenes.rooms_env(3, 2)
     assert r.shape == (6 * 316, 9)
+
+
+_SEG_PROBE = r"""
+#define __HIP_PLATFORM_AMD__ 1
+#include "fcl_math.h"
+#include <cstdio>
+#include <cstring>
+#include <random>
+using namespace mpt;
+static bool same(v3 a, v3 b) { return !memcmp(&a.x, &b.x, 8) && !memcmp(&a.y, &b.y, 8) && !memcmp(&a.z, &b.z, 8); }
+int main() {
+    std::mt19937_64 g(7);
+    std::uniform_real_distribution<double> U(-2, 2);
+    long bad = 0;
+    for (long it = 0; it < 2000000; ++it) {
+        v3 P = mk(U(g), U(g), U(g)), A = mk(U(g), U(g), U(g)), Q = mk(U(g), U(g), U(g)), B = mk(U(g), U(g), U(g));
+        switch (it % 8) {
+            case 1: B = scale(A, U(g)); break;                                 // parallel
+            case 2: A = mk(0, 0, 0); break;                                    // zero-length
+            case 3: B = mk(0, 0, 0); break;
+            case 4: Q = add(P, scale(A, U(g))); B = scale(A, U(g)); break;     // collinear
+            case 5: Q = P; break;
+            case 6: A = mk(1e-300, 0, 0); break;
+            default: break;
+        }
+        v3 V1, X1, Y1, V2, X2, Y2;
+        seg_points(P, A, Q, B, V1, X1, Y1);
+        seg_points_sel(P, A, Q, B, V2, X2, Y2);
+        if (!same(V1, V2) || !same(X1, X2) || !same(Y1, Y2)) ++bad;
+    }
+    printf("%ld\n", bad);
+    return 0;
+}
+"""
+
+
+@pytest.mark.skipif(shutil.which("g++") is None or not os.path.isdir("/opt/rocm/include"), reason="needs g++ and HIP headers")
+def test_seg_points_branch_free_matches_branchy(tmp_path):
+    """k_distance's branch-free segPoints (fcl_math.h seg_points_sel) returns the branchy
+    form's (seg_points, FCL's TriangleDistance::segPoints restated) points and direction bit for
+    bit, on 2 M random segment pairs with parallel, collinear and zero-length cases (the header
+    is host + device code; the host build checks the arithmetic, -ffp-contract=off as the
+    device build)."""
+    src, exe = tmp_path / "seg.cpp", tmp_path / "seg"
+    src.write_text(_SEG_PROBE)
+    csrc = os.path.join(REPO, "motionplanningtoolkit_amd", "csrc")
+    subprocess.run(["g++", "-O2", "-std=c++17", "-ffp-contract=off", "-I", csrc, "-I", "/opt/rocm/include", "-x",
+                    "c++", str(src), "-o", str(exe)], check=True)
+    out = subprocess.run([str(exe)], check=True, capture_output=True, text=True).stdout.strip()
+    assert out == "0"
