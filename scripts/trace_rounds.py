@@ -1,6 +1,7 @@
 """Per-round view of a rocprofv3 kernel trace of bench.py (scripts/profile.sh, `kt` pass).
 
-Rounds are delimited by the engine's k_sample launches.  For the timed rounds (after
+Rounds end at the engine's k_append_commit launch (grid rounds start with the grid count
+launch, which also generates the samples; tree rounds with k_sample).  For the timed rounds (after
 `--warmup`, `--steps` of them; the bench's extra untimed stats round is dropped) it prints
 each kernel's mean / median duration, the kernels' busy time per round and the round span
 (k_sample start to the next round's k_sample start), so the idle gaps between launches show.
@@ -27,11 +28,14 @@ def main():
     rounds, cur = [], None
     for r in rows:
         name = r["Kernel_Name"]
-        if "k_sample" in name:
+        if cur is None:
             cur = []
             rounds.append(cur)
-        if cur is not None:
-            cur.append((name, int(r["Start_Timestamp"]), int(r["End_Timestamp"])))
+        cur.append((name, int(r["Start_Timestamp"]), int(r["End_Timestamp"])))
+        if "k_append_commit" in name:
+            cur = None
+    if rounds and not any("k_append_commit" in n for n, _, _ in rounds[-1]):
+        rounds.pop()  # trailing kernels after the last round
     timed = rounds[a.warmup:a.warmup + a.steps]
     per = collections.defaultdict(list)
     busy, span = [], []
