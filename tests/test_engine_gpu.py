@@ -130,6 +130,30 @@ def test_engine_tree_nn_large_blob(mpt_gpu, oracle):
     tree, _ = check_round(mpt_gpu, oracle, sc, eng, tree, 4242, K, K)
 
 
+@pytest.mark.parametrize("name", ["omni", "blimp"])
+def test_engine_grid_blob_and_sparse(mpt_gpu, oracle, name):
+    """The grid 1-NN (bucketed run kernel) on a tree that is half a tight blob and half
+    sparse: the blob's few cells hold thousands of points each (one run spreads them over the
+    group's lanes for many steps), and in the sparse half the first pass often does not settle
+    a query (the walk continues with ring 2 and beyond).  NN ids and the whole round stay
+    bit-exact against the oracle."""
+    sc = scenes.blimp_scenario("all") if name == "blimp" else scenes.omni_scenario()
+    rng = np.random.default_rng(99)
+    n0, K = 6000, 4096
+    tree = rng.uniform(sc.ranges[:, 0], sc.ranges[:, 1], size=(n0, sc.dim))
+    ctr = 0.5 * (sc.ranges[:3, 0] + sc.ranges[:3, 1])
+    tree[: n0 // 2, :3] = ctr + rng.normal(0.0, 0.01 * (sc.ranges[0, 1] - sc.ranges[0, 0]), size=(n0 // 2, 3))
+    env = mpt_gpu.Environment(sc.env_tris, sc.env_tf)
+    ag = mpt_gpu.AgentMesh(sc.agent_tris)
+    eng = mpt_gpu.RRTEngine(env, ag, sc.kind, sc.prm, sc.ranges, sc.steer_dt, sc.cc_dt, capacity=n0 + 4 * K,
+                            seed=31)
+    eng.add_nodes(tree)
+    eng.set_nn("grid")
+    tree, _ = check_round(mpt_gpu, oracle, sc, eng, tree, 31, 0, K)
+    tree, _ = check_round(mpt_gpu, oracle, sc, eng, tree, 31, K, K // 2 + 5)
+    assert eng.last_nn() == "grid"
+
+
 def test_engine_round_with_pair_overflow(mpt_gpu, oracle):
     """The blimp against the blimp mesh itself as the environment, every pose within a few
     units of it: clusters overlap far more env triangles than a pair segment holds, so units
