@@ -642,7 +642,8 @@ void CollideScratch::ensure(int64_t n_units, int32_t max_clusters) {
 }
 
 static void collide_split_chunk(const EnvDev &env, const AgentDev *d_links, int32_t max_clusters,
-                                const CollideWork &w, CollideScratch &s, hipStream_t stream, hipEvent_t *marks) {
+                                const CollideWork &w, CollideScratch &s, hipStream_t stream, hipEvent_t *marks,
+                                OvfDefer *defer) {
     auto mark = [&](int i) {
         if (marks) hip_check(hipEventRecord(marks[i], stream), "event record");
     };
@@ -704,9 +705,17 @@ static void collide_split_chunk(const EnvDev &env, const AgentDev *d_links, int3
     hipLaunchKernelGGL(k_narrow, dim3(nblocks), dim3(kNarrowWaves * 64), lds_ok ? sizeof(double) * 9 * env.n_tris : 0,
                        stream, env, d_links, w, a, lds_ok);
     hip_check(hipGetLastError(), "k_narrow launch");
-    hipLaunchKernelGGL(k_overflow, dim3(kOvfWaves / kNarrowWaves), dim3(kNarrowWaves * 64), 0, stream, env, d_links,
-                       w, a);
-    hip_check(hipGetLastError(), "k_overflow launch");
+    if (defer) {
+        defer->env = env;
+        defer->links = d_links;
+        defer->w = w;
+        defer->n_ovf = a.ctl + 1;
+        defer->ovf_list = a.ovf_list;
+    } else {
+        hipLaunchKernelGGL(k_overflow, dim3(kOvfWaves / kNarrowWaves), dim3(kNarrowWaves * 64), 0, stream, env, d_links,
+                           w, a);
+        hip_check(hipGetLastError(), "k_overflow launch");
+    }
     mark(2);
     if (w.stats) {
         hipLaunchKernelGGL(k_count_units, dim3((unsigned)((w.n_units + 255) / 256)), dim3(256), 0, stream, w);
@@ -719,11 +728,12 @@ static void collide_split_chunk(const EnvDev &env, const AgentDev *d_links, int3
 // hold a chunk's candidates instead of overflowing to the fused kernel (config 4's 21 M
 // poses overflowed 8 M units).  The scratch is sized for one chunk.
 void launch_collide_split(const EnvDev &env, const AgentDev *d_links, int32_t max_clusters, const CollideWork &w,
-                          CollideScratch &s, hipStream_t stream, hipEvent_t *marks) {
+                          CollideScratch &s, hipStream_t stream, hipEvent_t *marks, OvfDefer *defer) {
+    if (defer) defer->n_ovf = nullptr;
     const int64_t g = w.pose_edge ? (int64_t)w.L : (int64_t)w.pmax * w.L;
     const int64_t per = std::max<int64_t>(g, (split_chunk_units(max_clusters) / g) * g);
     if (w.n_units <= per) {
-        collide_split_chunk(env, d_links, max_clusters, w, s, stream, marks);
+        collide_split_chunk(env, d_links, max_clusters, w, s, stream, marks, defer);
         return;
     }
     for (int64_t u0 = 0; u0 < w.n_units; u0 += per) {
@@ -743,7 +753,8 @@ void launch_collide_split(const EnvDev &env, const AgentDev *d_links, int32_t ma
             c.pcount = w.pcount + e0;
             c.verdict = w.verdict + e0;
         }
-        collide_split_chunk(env, d_links, max_clusters, c, s, stream, u0 + per >= w.n_units ? marks : nullptr);
+        collide_split_chunk(env, d_links, max_clusters, c, s, stream, u0 + per >= w.n_units ? marks : nullptr,
+                            nullptr);
     }
 }
 

@@ -197,8 +197,21 @@ void launch_collide(const EnvDev &env, const AgentDev *d_links, const CollideWor
 // Two-phase path (broad.hip): k_pairs -> k_cands -> k_narrow -> fused kernel over
 // overflowed units.  s.ensure(w.n_units, max_clusters) must have run with the same value.
 // marks (optional, 3 events): recorded after the pair, candidate and exact-test stages.
+// What the last stage of the two-phase path (the fused re-run of overflowed units, k_overflow)
+// needs, for a caller that runs it inside its own next launch instead (the engine's append:
+// one launch less per round; see rrt_engine.hip k_append_commit).
+struct OvfDefer {
+    EnvDev env{};
+    const AgentDev *links = nullptr;
+    CollideWork w{};
+    const uint32_t *n_ovf = nullptr;  // nullptr: nothing deferred
+    const int32_t *ovf_list = nullptr;
+};
+// defer (optional): filled instead of launching k_overflow when the batch runs in one chunk
+// (otherwise defer->n_ovf stays nullptr and k_overflow runs as usual).
 void launch_collide_split(const EnvDev &env, const AgentDev *d_links, int32_t max_clusters, const CollideWork &w,
-                          CollideScratch &s, hipStream_t stream, hipEvent_t *marks = nullptr);
+                          CollideScratch &s, hipStream_t stream, hipEvent_t *marks = nullptr,
+                          OvfDefer *defer = nullptr);
 void launch_pose_edge(const int64_t *d_offsets, int64_t E, int32_t *d_pose_edge, hipStream_t stream);
 
 // Edges whose poses share one rotation (sweep.hip): poses of edge e are [poff[e], poff[e+1]);

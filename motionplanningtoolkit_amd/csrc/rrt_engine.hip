@@ -26,6 +26,7 @@
 #include "point_tree.h"
 #include "mpt_internal.h"
 #include "collide_common.h"
+#include "collide_common.h"
 
 namespace mpt {
 const EnvDev &env_dev(const mpt_env *e);
@@ -332,33 +333,23 @@ __global__ __launch_bounds__(256) void k_steer(EngineParams p, uint64_t ext_base
 // extensions before k).  Each block counts the valid extensions before it straight from the
 // verdict bytes (0 / 1, so 16 minus the popcount of every 16-byte load), so no block waits
 // on another; the last block also commits n and the counters.  n0 = n_dev[1] (k_sample).
-__global__ __launch_bounds__(256) void k_append_commit(const uint8_t *__restrict__ verdict, int32_t K, int32_t d,
-                                                       const double *__restrict__ ends,
-                                                       const int32_t *__restrict__ nn, int64_t *__restrict__ n_dev,
-                                                       int64_t cap, double *__restrict__ nodes,
-                                                       int32_t *__restrict__ parents,
-                                                       unsigned long long *__restrict__ counters) {
-    __shared__ int32_t s_wave[4], s_ones[4];
+//
+// ov (two-phase collide, one chunk): the round's overflowed units (none in practice) are re-run
+// here first with the fused walk (k_overflow's work, one wave per unit).  Then no block may
+// read a verdict before every re-run has stored its own, and no block may wait for another
+// (a spinning block could hold the slot another needs): the blocks take a ticket, all but the
+// last one leave, and the last one appends every extension in order itself.  The usual empty
+// case costs one load; the k_overflow launch it replaces cost ~5 us a round.
+__device__ __forceinline__ void append_commit_tail(int64_t before_block, int32_t blk_ones, const uint8_t *verdict,
+                                                   int64_t k0, int32_t K, int32_t d, const double *ends,
+                                                   const int32_t *nn, int64_t n0, int64_t cap, double *nodes,
+                                                   int32_t *parents, int32_t (&s_wave)[4], int64_t *tot_out) {
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const uint4 *v4 = reinterpret_cast<const uint4 *>(verdict);
-    const int64_t nv4 = (int64_t)blockIdx.x * 16;  // 256 verdicts per block before this one
-    int32_t ones = 0;
-    for (int64_t i = tid; i < nv4; i += 256) {
-        const uint4 x = v4[i];
-        ones += __popc(x.x) + __popc(x.y) + __popc(x.z) + __popc(x.w);
-    }
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) ones += __shfl_xor(ones, off);
-    const int64_t k = (int64_t)blockIdx.x * 256 + tid;
+    const int64_t k = k0 + tid;
     const bool ok = k < K && verdict[k] == 0;
     const uint64_t m = __ballot(ok);
-    if (lane == 0) {
-        s_ones[wave] = ones;
-        s_wave[wave] = __popcll(m);
-    }
+    if (lane == 0) s_wave[wave] = __popcll(m);
     __syncthreads();
-    const int64_t before_block = nv4 * 16 - (int64_t)(s_ones[0] + s_ones[1] + s_ones[2] + s_ones[3]);
-    const int64_t n0 = n_dev[1];
     int wbase = 0;
     for (int w = 0; w < wave; ++w) wbase += s_wave[w];
     if (ok) {
@@ -368,17 +359,81 @@ __global__ __launch_bounds__(256) void k_append_commit(const uint8_t *__restrict
             parents[idx] = nn[k];
         }
     }
-    if (blockIdx.x == gridDim.x - 1 && tid == 0) {
-        const int64_t tot = before_block + s_wave[0] + s_wave[1] + s_wave[2] + s_wave[3];
-        const int64_t room = cap - n0 > 0 ? cap - n0 : 0;
-        const int64_t add = tot < room ? tot : room;
-        n_dev[0] = n0 + add;
-        counters[0] += 1;
-        counters[1] += (unsigned long long)K;
-        counters[2] += (unsigned long long)add;
-        counters[3] = (unsigned long long)(n0 + add);
-        counters[4] += (unsigned long long)(tot - add);
+    *tot_out = before_block + s_wave[0] + s_wave[1] + s_wave[2] + s_wave[3];
+    (void)blk_ones;
+}
+
+__device__ __forceinline__ void append_commit_counters(int64_t tot, int64_t n0, int64_t cap, int32_t K,
+                                                       int64_t *n_dev, unsigned long long *counters) {
+    const int64_t room = cap - n0 > 0 ? cap - n0 : 0;
+    const int64_t add = tot < room ? tot : room;
+    n_dev[0] = n0 + add;
+    counters[0] += 1;
+    counters[1] += (unsigned long long)K;
+    counters[2] += (unsigned long long)add;
+    counters[3] = (unsigned long long)(n0 + add);
+    counters[4] += (unsigned long long)(tot - add);
+}
+
+__global__ __launch_bounds__(256) void k_append_commit(const uint8_t *__restrict__ verdict, int32_t K, int32_t d,
+                                                       const double *__restrict__ ends,
+                                                       const int32_t *__restrict__ nn, int64_t *__restrict__ n_dev,
+                                                       int64_t cap, double *__restrict__ nodes,
+                                                       int32_t *__restrict__ parents,
+                                                       unsigned long long *__restrict__ counters, OvfDefer ov,
+                                                       uint32_t *__restrict__ ticket) {
+    __shared__ int32_t s_wave[4], s_ones[4];
+    __shared__ int32_t s_last;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    if (ov.n_ovf) {
+        const uint32_t n_ovf = __hip_atomic_load(ov.n_ovf, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (n_ovf > 0) {  // grid-uniform
+            __shared__ int32_t s_stk[4][kStackDepth];
+            const bool shared_edges = ov.w.pose_edge != nullptr || ov.w.L > 1 || ov.w.pmax > 1;
+            uint32_t nu = 0, nc = 0, nnod = 0, ns = 0;
+            const uint32_t nw = gridDim.x * 4;
+            for (uint32_t i = blockIdx.x * 4 + wave; i < n_ovf; i += nw)
+                collide_unit(ov.env, ov.env.nodes, ov.env.n_nodes, ov.links, ov.w, ov.ovf_list[i], s_stk[wave], lane,
+                             shared_edges, nc, nnod, ns, nu);
+            __threadfence();
+            __syncthreads();
+            if (tid == 0) s_last = atomicAdd(ticket, 1u) == gridDim.x - 1;
+            __syncthreads();
+            if (!s_last) return;  // block-uniform
+            __threadfence();
+            // the last block: every extension, in order, with a running count
+            const int64_t n0 = n_dev[1];
+            int64_t before = 0;
+            for (int64_t k0 = 0; k0 < K; k0 += 256) {
+                int64_t tot;
+                append_commit_tail(before, 0, verdict, k0, K, d, ends, nn, n0, cap, nodes, parents, s_wave, &tot);
+                before = tot;
+                __syncthreads();  // s_wave is reused
+            }
+            if (tid == 0) {
+                append_commit_counters(before, n0, cap, K, n_dev, counters);
+                *ticket = 0u;  // for the next round's launch (stream-ordered)
+            }
+            return;
+        }
     }
+    const uint4 *v4 = reinterpret_cast<const uint4 *>(verdict);
+    const int64_t nv4 = (int64_t)blockIdx.x * 16;  // 256 verdicts per block before this one
+    int32_t ones = 0;
+    for (int64_t i = tid; i < nv4; i += 256) {
+        const uint4 x = v4[i];
+        ones += __popc(x.x) + __popc(x.y) + __popc(x.z) + __popc(x.w);
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) ones += __shfl_xor(ones, off);
+    if (lane == 0) s_ones[wave] = ones;
+    __syncthreads();
+    const int64_t before_block = nv4 * 16 - (int64_t)(s_ones[0] + s_ones[1] + s_ones[2] + s_ones[3]);
+    const int64_t n0 = n_dev[1];
+    int64_t tot;
+    append_commit_tail(before_block, 0, verdict, (int64_t)blockIdx.x * 256, K, d, ends, nn, n0, cap, nodes, parents,
+                       s_wave, &tot);
+    if (blockIdx.x == gridDim.x - 1 && tid == 0) append_commit_counters(tot, n0, cap, K, n_dev, counters);
 }
 
 __global__ void k_set_n(int64_t *n_dev, int64_t n, unsigned long long *counters) {
@@ -405,6 +460,7 @@ struct mpt_rrt {
     double *d_rt = nullptr;        // k_steer's unit relative transforms [K * pmax * L][12] (two-phase)
     uint32_t *d_nlive = nullptr;   // its length
     uint8_t *d_verdict = nullptr;
+    uint32_t *d_bar = nullptr;  // k_append_commit's ticket (overflow re-run)
     void *d_scratch = nullptr;
     size_t scratch_bytes = 0;
     uint64_t ext_base = 0;
@@ -448,7 +504,7 @@ namespace {
 void rfree(mpt_rrt *r) {
     void *ps[] = {r->d_links, r->d_nodes,   r->d_parents, r->d_n,       r->d_counters, r->d_samples,
                   r->d_ends,  r->d_poses,   r->d_nnd2,    r->d_nn,      r->d_pcount,
-                  r->d_verdict, r->d_scratch, r->d_cstats, r->d_live, r->d_nlive, r->d_rt};
+                  r->d_verdict, r->d_scratch, r->d_cstats, r->d_live, r->d_nlive, r->d_rt, r->d_bar};
     for (void *p : ps)
         if (p) (void)hipFree(p);
     for (auto &e : r->ring)
@@ -852,18 +908,27 @@ void step_tail(mpt_rrt *r, int32_t K, hipStream_t stream, const StepCtx &c) {
     cw.live_units = live_list ? r->d_live : nullptr;
     cw.unit_rt = live_list ? r->d_rt : nullptr;  // k_steer writes them with the live list
     cw.n_live = live_list ? r->d_nlive : nullptr;
+    OvfDefer ovf{};
     if (collide_mode() == MPT_COLLIDE_FUSED) {
         launch_collide(r->env, r->d_links, cw, stream);
         c.mark(5, stream);
         c.mark(6, stream);
         c.mark(7, stream);
     } else {
-        launch_collide_split(r->env, r->d_links, r->max_clusters, cw, r->cscratch, stream,
-                             ev ? ev + 5 : nullptr);
+        // the overflow re-run moves into the append launch (MPT_OVF_IN_APPEND=0: its own
+        // k_overflow launch, A/B)
+        static const bool defer = !(getenv("MPT_OVF_IN_APPEND") && atoi(getenv("MPT_OVF_IN_APPEND")) == 0);
+        if (defer && !r->d_bar) {
+            hip_check(hipMalloc(&r->d_bar, sizeof(uint32_t)), "alloc append ticket");
+            hip_check(hipMemset(r->d_bar, 0, sizeof(uint32_t)), "zero append ticket");
+            hip_check(hipDeviceSynchronize(), "append ticket zero sync");  // null stream vs the engine's
+        }
+        launch_collide_split(r->env, r->d_links, r->max_clusters, cw, r->cscratch, stream, ev ? ev + 5 : nullptr,
+                             defer ? &ovf : nullptr);
     }
     c.mark(8, stream);
     hipLaunchKernelGGL(k_append_commit, dim3(kb), dim3(256), 0, stream, r->d_verdict, K, p.d, r->d_ends, r->d_nn,
-                       r->d_n, r->cap, r->d_nodes, r->d_parents, r->d_counters);
+                       r->d_n, r->cap, r->d_nodes, r->d_parents, r->d_counters, ovf, r->d_bar);
     hip_check(hipGetLastError(), "append");
     c.mark(9, stream);
     r->ext_base += (uint64_t)K;
