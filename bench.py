@@ -52,9 +52,10 @@ def parse():
                          "(collision-heavy); snake = config 3 (snake_trailers, 11 links, corridor)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample length")
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--stage-every", type=int, default=8,
-                    help="record the per-stage hipEvents on every n-th timed round (0: none); each recorded "
-                         "round pays ~34 us of event packets, so they sample the timed region")
+    ap.add_argument("--stage-every", type=int, default=16,
+                    help="record the per-stage hipEvents on every n-th timed round (0: none); a recorded round "
+                         "pays ~60-80 us of event packets (config 2: 170 us a round with none, "
+                         "scripts/host_rate.py, 178 us with every 8th), so they sample the timed region")
     ap.add_argument("--nn", default="auto", choices=["grid", "brute", "auto", "tree"], help="engine NN structure")
     ap.add_argument("--ppc", type=float, default=0.0,
                     help="grid points per cell (0: the engine's default, 2 floored by the expected NN distance)")
