@@ -23,6 +23,9 @@
 // k_overflow  units whose pairs overflowed a segment are re-run with the fused kernel's
 //           per-unit walk (collide_common.h collide_unit).
 #include <hipcub/hipcub.hpp>
+#include <cstdio>
+#include <type_traits>
+#include <vector>
 
 #include "collide_common.h"
 #include "scan.h"
@@ -54,7 +57,12 @@ struct SplitArgs {
     int32_t *ovf_list;
     int64_t n_seg;
     int32_t pair_cap, cand_cap, spill_cap, n_clusters, n_cwaves;
+    unsigned long long *dbg_ts;  // MPT_PHASE_DBG: per-workgroup phase timestamps (diagnostics only)
 };
+
+__device__ __forceinline__ void phase_ts(unsigned long long *ts, int i) {
+    if (ts && threadIdx.x == 0) ts[(int64_t)blockIdx.x * 8 + i] = __builtin_amdgcn_s_memrealtime();
+}
 
 // wave-uniform item load through the scalar cache (items are read-only in these kernels)
 __device__ __forceinline__ Item load_item_u(const Item *__restrict__ items, int64_t idx) {
@@ -95,23 +103,28 @@ __device__ __forceinline__ uint32_t walk_tree(const EnvDev &env, const Item *__r
     // boxes of items [first, first + count) that overlap (lo, hi) as a bit mask; eight
     // independent loads in flight per step (a one-at-a-time loop is a chain of dependent
     // LDS round trips, which is what bounded the walk)
+    // (batches of 8, then of 4 for the remainder: a 10-triangle bucket reads 12 boxes, not 16)
+    auto overlap_batch = [&](auto kB, int32_t first, int32_t count, int32_t i0, uint64_t &M) {
+        constexpr int B = decltype(kB)::value;
+        float bl[B][3], bh[B][3];
+#pragma unroll
+        for (int j = 0; j < B; ++j) {
+            const Item b = items[first + (i0 + j < count ? i0 + j : count - 1)];
+#pragma unroll
+            for (int x = 0; x < 3; ++x) {
+                bl[j][x] = b.lo[x];
+                bh[j][x] = b.hi[x];
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < B; ++j)
+            if (i0 + j < count && box_overlap(lo, hi, bl[j], bh[j])) M |= 1ull << (i0 + j);
+    };
     auto overlap_mask = [&](int32_t first, int32_t count) {
         uint64_t M = 0;
-        for (int32_t i0 = 0; i0 < count; i0 += 8) {
-            float bl[8][3], bh[8][3];
-#pragma unroll
-            for (int j = 0; j < 8; ++j) {
-                const Item b = items[first + (i0 + j < count ? i0 + j : count - 1)];
-#pragma unroll
-                for (int x = 0; x < 3; ++x) {
-                    bl[j][x] = b.lo[x];
-                    bh[j][x] = b.hi[x];
-                }
-            }
-#pragma unroll
-            for (int j = 0; j < 8; ++j)
-                if (i0 + j < count && box_overlap(lo, hi, bl[j], bh[j])) M |= 1ull << (i0 + j);
-        }
+        int32_t i0 = 0;
+        for (; i0 + 8 <= count; i0 += 8) overlap_batch(std::integral_constant<int, 8>{}, first, count, i0, M);
+        for (; i0 < count; i0 += 4) overlap_batch(std::integral_constant<int, 4>{}, first, count, i0, M);
         return M;
     };
     auto tri_run = [&](int32_t first, int32_t count) {
@@ -164,6 +177,77 @@ __device__ __forceinline__ uint32_t walk_tree(const EnvDev &env, const Item *__r
     return tests;
 }
 
+// The two-level walk on quantized boxes (EnvDev::qitems, staged in LDS): one 16-B read per
+// box instead of two 12-B ones, and the overlap test as 15-bit SWAR on 32-bit words (bit 15 of
+// each half of (a | 0x8000) - b is set iff a >= b).  The items were quantized outward on the
+// host, the query box is here with a margin of 0.02 quanta beyond the float rounding of its
+// grid coordinate (<= 0.01 quanta: two roundings of ~0.004 and the float scale's 0.002), so
+// every pair the float walk keeps is kept (a superset: k_cands tests the exact float boxes
+// again).  The walk is LDS-bandwidth bound: per-workgroup phase times (MPT_PHASE_DBG=1)
+// showed the cull + staging ~4 us and the walk ~16 us of a ~20-us lifetime; with these boxes
+// the walk takes ~11 us (config 2's k_pairs 31 -> 25 us, the room's 115 -> 90 us).
+struct QBox {
+    uint32_t lxy, hxy, lz, hz;  // query: lo.x | lo.y << 16, hi.x | hi.y << 16, lo.z, hi.z
+};
+__device__ __forceinline__ QBox quantize_box(const EnvDev &env, const float lo[3], const float hi[3]) {
+    uint32_t l[3], h[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        const float vl = floorf((lo[k] - env.q_org[k]) * env.q_scale[k] - 0.02f);
+        const float vh = ceilf((hi[k] - env.q_org[k]) * env.q_scale[k] + 0.02f);
+        l[k] = (uint32_t)fminf(fmaxf(vl, 0.0f), (float)kQMax);
+        h[k] = (uint32_t)fminf(fmaxf(vh, 0.0f), (float)kQMax);
+    }
+    return QBox{l[0] | l[1] << 16, h[0] | h[1] << 16, l[2], h[2]};
+}
+__device__ __forceinline__ bool qbox_overlap(const QBox &q, uint4 it) {
+    constexpr uint32_t H = 0x80008000u;
+    const uint32_t t1 = (q.hxy | H) - it.x;  // query hi >= item lo (x, y)
+    const uint32_t t2 = (it.y | H) - q.lxy;  // item hi >= query lo (x, y)
+    const uint32_t A = (it.z & 0xffff0000u) | q.hz, B = (it.z & 0x0000ffffu) | (q.lz << 16);
+    const uint32_t t3 = (A | H) - B;         // query hi.z >= item lo.z, item hi.z >= query lo.z
+    return (t1 & t2 & t3 & H) == H;
+}
+template <class Sink>
+__device__ __forceinline__ uint32_t walk_two_q(const EnvDev &env, const uint4 *__restrict__ qi, const QBox &q,
+                                               Sink &&sink) {
+    const int32_t top = env.n_levels - 1;
+    const int32_t top_off = env.lev_off[top];
+    const int32_t n_top = env.lev_off[top + 1] - top_off;
+    uint32_t tests = (uint32_t)n_top;
+    auto batch = [&](auto kB, int32_t first, int32_t count, int32_t i0, uint64_t &M) {
+        constexpr int B = decltype(kB)::value;
+        uint4 b[B];
+#pragma unroll
+        for (int j = 0; j < B; ++j) b[j] = qi[first + (i0 + j < count ? i0 + j : count - 1)];
+#pragma unroll
+        for (int j = 0; j < B; ++j)
+            if (i0 + j < count && qbox_overlap(q, b[j])) M |= 1ull << (i0 + j);
+    };
+    auto mask = [&](int32_t first, int32_t count) {
+        uint64_t M = 0;
+        int32_t i0 = 0;
+        for (; i0 + 8 <= count; i0 += 8) batch(std::integral_constant<int, 8>{}, first, count, i0, M);
+        for (; i0 < count; i0 += 4) batch(std::integral_constant<int, 4>{}, first, count, i0, M);
+        return M;
+    };
+    uint64_t M = mask(top_off, n_top);
+    while (M) {
+        const int i = __ffsll((unsigned long long)M) - 1;
+        M &= M - 1;
+        const uint32_t w = qi[top_off + i].w;
+        const int32_t first = (int32_t)(w & ((1u << 26) - 1u)), count = (int32_t)(w >> 26) + 1;
+        tests += (uint32_t)count;
+        uint64_t Mt = mask(first, count);
+        while (Mt) {
+            const int j = __ffsll((unsigned long long)Mt) - 1;
+            Mt &= Mt - 1;
+            sink(first + j);
+        }
+    }
+    return tests;
+}
+
 // Per-(pose, cluster) record of a thread that survived the root cull, compacted in LDS so
 // the tree walks run on as few waves as possible (most clusters are culled at the root).
 struct PairRec {
@@ -178,6 +262,7 @@ __global__ __launch_bounds__(kPairThreads) void k_pairs(EnvDev env, const AgentD
     __shared__ uint32_t s_pc[kPairThreads / 64], s_hc[kPairThreads / 64], s_live[kPairThreads / 64];
     __shared__ uint4 s_stk[kTwo ? 1 : kPairThreads * kStack];
     __shared__ PairRec s_rec[kPairThreads];
+    phase_ts(a.dbg_ts, 0);
     if (blockIdx.x == 0) {  // stream-ordered resets instead of memset launches
         if (threadIdx.x < 4) a.ctl_next[threadIdx.x] = 0u;
         if (threadIdx.x == 0) a.hdr_count[a.n_seg] = 0u;  // the header scan's sentinel slot
@@ -232,9 +317,13 @@ __global__ __launch_bounds__(kPairThreads) void k_pairs(EnvDev env, const AgentD
             s_rec[base + (uint32_t)__popcll(m & ((1ull << lane) - 1))] = r;
         }
     }
+    phase_ts(a.dbg_ts, 1);
     uint32_t total = 0;
     for (int v = 0; v < kPairThreads / 64; ++v) total += s_live[v];
+    if (a.dbg_ts && threadIdx.x == 0) a.dbg_ts[(int64_t)blockIdx.x * 8 + 5] = total;
     if (total == 0) {  // block-uniform: nothing reaches the env tree
+        phase_ts(a.dbg_ts, 2);
+        phase_ts(a.dbg_ts, 3);
         if (lane == 0 && seg < a.n_seg) {
             a.hdr_count[seg] = 0;
             a.pair_count[seg] = 0;
@@ -242,15 +331,25 @@ __global__ __launch_bounds__(kPairThreads) void k_pairs(EnvDev env, const AgentD
         return;
     }
     const Item *items = env.items;
+    // two-level trees in LDS walk the quantized boxes (env.qitems; 16 B an item)
+    const bool quant = kTwo && kLds && env.qitems != nullptr;
+    const uint4 *qitems = nullptr;
     if (kLds) {
-        Item *s_items = reinterpret_cast<Item *>(smem);
         const int32_t n = env.lev_off[env.n_levels];
-        const uint4 *src = reinterpret_cast<const uint4 *>(env.items);
-        uint4 *dst = reinterpret_cast<uint4 *>(s_items);
-        for (int i = threadIdx.x; i < n * 2; i += blockDim.x) dst[i] = src[i];
-        items = s_items;
+        if (quant) {
+            uint4 *dst = reinterpret_cast<uint4 *>(smem);
+            for (int i = threadIdx.x; i < n; i += blockDim.x) dst[i] = env.qitems[i];
+            qitems = dst;
+        } else {
+            Item *s_items = reinterpret_cast<Item *>(smem);
+            const uint4 *src = reinterpret_cast<const uint4 *>(env.items);
+            uint4 *dst = reinterpret_cast<uint4 *>(s_items);
+            for (int i = threadIdx.x; i < n * 2; i += blockDim.x) dst[i] = src[i];
+            items = s_items;
+        }
     }
     __syncthreads();
+    phase_ts(a.dbg_ts, 2);
     // 2. the surviving records, packed onto the first waves: walk the env tree; the pair
     //    words and headers carry the (segment, lane) of the thread that walked
     const bool live = threadIdx.x < total;
@@ -262,15 +361,18 @@ __global__ __launch_bounds__(kPairThreads) void k_pairs(EnvDev env, const AgentD
     int32_t *out = a.pairs + seg * a.pair_cap;
     // one pass: each pair takes the next slot of the wave's segment (LDS atomic) as a
     // (lane, triangle) word; k_cands picks a header's pairs out by lane
-    if (live)
-        tests = walk_tree<kTwo>(env, items, r.lo, r.hi, stk, [&](int32_t tri) {
-            const uint32_t pos = atomicAdd(&s_pc[wave], 1u);
-            if (pos < (uint32_t)a.pair_cap)
-                out[pos] = (int32_t)(((uint32_t)lane << kPairTriBits) | (uint32_t)tri);
-            else
-                ovf = true;
-            ++np;
-        });
+    auto emit_pair = [&](int32_t tri) {
+        const uint32_t pos = atomicAdd(&s_pc[wave], 1u);
+        if (pos < (uint32_t)a.pair_cap)
+            out[pos] = (int32_t)(((uint32_t)lane << kPairTriBits) | (uint32_t)tri);
+        else
+            ovf = true;
+        ++np;
+    };
+    if (live) {
+        if (quant) tests = walk_two_q(env, qitems, quantize_box(env, r.lo, r.hi), emit_pair);
+        else tests = walk_tree<kTwo>(env, items, r.lo, r.hi, stk, emit_pair);
+    }
     if (np > 0 && !ovf) {
         const uint32_t h = atomicAdd(&s_hc[wave], 1u);
         a.hdr[seg * kHdrCap + h] = PairHdr{r.unit, r.c, (int32_t)seg, (int32_t)np, r.tfirst, r.tcount, lane, 0};
@@ -280,6 +382,10 @@ __global__ __launch_bounds__(kPairThreads) void k_pairs(EnvDev env, const AgentD
     if (lane == 0 && seg < a.n_seg) {
         a.hdr_count[seg] = s_hc[wave];
         a.pair_count[seg] = s_pc[wave] < (uint32_t)a.pair_cap ? s_pc[wave] : (uint32_t)a.pair_cap;
+    }
+    if (a.dbg_ts) {
+        __syncthreads();
+        phase_ts(a.dbg_ts, 3);
     }
     if (w.stats) {
         uint32_t sum_tests = tests, sum_pairs = np;
@@ -661,9 +767,21 @@ static void collide_split_chunk(const EnvDev &env, const AgentDev *d_links, int3
     // (or at allocation), and this k_pairs zeroes the other half for the next launch
     uint32_t *ctl = s.ctl + 4 * s.ctl_par, *ctl_next = s.ctl + 4 * (1 - s.ctl_par);
     s.ctl_par ^= 1;
+    // MPT_PHASE_DBG=1 (diagnostics only: synchronises after k_pairs and prints its per-workgroup
+    // phase times -- transform + root cull, LDS staging, tree walk -- to stderr)
+    static const bool phase_dbg = getenv("MPT_PHASE_DBG") && atoi(getenv("MPT_PHASE_DBG")) == 1;
+    static unsigned long long *dbg_buf = nullptr;
+    static int64_t dbg_cap = 0;
+    const unsigned pblocks0 = (unsigned)((threads + kPairThreads - 1) / kPairThreads);
+    if (phase_dbg && (int64_t)pblocks0 > dbg_cap) {
+        if (dbg_buf) hip_check(hipFree(dbg_buf), "hipFree");
+        hip_check(hipMalloc(&dbg_buf, sizeof(unsigned long long) * 8 * pblocks0), "alloc phase dbg");
+        dbg_cap = pblocks0;
+    }
     SplitArgs a{s.pairs,  s.hdr,      s.hdr_count, s.pair_count, s.hdr_off, s.hdr_dense, s.cand,    s.cand_count,
                 s.spill,  ctl,        ctl_next,    s.ovf_list,   segs,      s.pair_cap,  s.cand_cap, s.spill_cap,
-                C,        s.n_cwaves};
+                C,        s.n_cwaves, phase_dbg ? dbg_buf : nullptr};
+    if (phase_dbg) hip_check(hipMemsetAsync(dbg_buf, 0, sizeof(unsigned long long) * 8 * pblocks0, stream), "dbg zero");
     const unsigned pblocks = (unsigned)((threads + kPairThreads - 1) / kPairThreads);
     const int32_t n_items = env.lev_off[env.n_levels];
     // MPT_PAIRS_LDS=0: items read through the caches instead of staged in LDS (A/B knob)
@@ -686,6 +804,33 @@ static void collide_split_chunk(const EnvDev &env, const AgentDev *d_links, int3
                                w, a);
     }
     hip_check(hipGetLastError(), "k_pairs launch");
+    if (phase_dbg) {
+        hip_check(hipStreamSynchronize(stream), "phase dbg sync");
+        std::vector<unsigned long long> h((size_t)pblocks * 8);
+        hip_check(hipMemcpy(h.data(), dbg_buf, sizeof(unsigned long long) * 8 * pblocks, hipMemcpyDeviceToHost), "dbg");
+        unsigned long long t0 = ~0ull, t1 = 0;
+        double sum[3] = {0, 0, 0}, life = 0, life_live = 0;
+        int64_t nb = 0, nlive = 0;
+        for (unsigned b = 0; b < pblocks; ++b) {
+            const unsigned long long *e = &h[(size_t)b * 8];
+            if (!e[0]) continue;
+            ++nb;
+            t0 = std::min(t0, e[0]);
+            t1 = std::max(t1, e[3]);
+            life += (double)(e[3] - e[0]);
+            if (e[5]) {
+                ++nlive;
+                life_live += (double)(e[3] - e[0]);
+                for (int k = 0; k < 3; ++k) sum[k] += (double)(e[k + 1] - e[k]);
+            }
+        }
+        // s_memrealtime ticks at 100 MHz
+        fprintf(stderr, "[phase k_pairs] blocks %lld (live %lld) span %.1f us, wg life %.2f us (live %.2f us); live: "
+                        "phase1 %.2f us, staging %.2f us, walk %.2f us\n",
+                (long long)nb, (long long)nlive, (t1 - t0) * 0.01, nb ? life / nb * 0.01 : 0.0,
+                nlive ? life_live / nlive * 0.01 : 0.0, nlive ? sum[0] / nlive * 0.01 : 0.0,
+                nlive ? sum[1] / nlive * 0.01 : 0.0, nlive ? sum[2] / nlive * 0.01 : 0.0);
+    }
     mark(0);
     // count slot `segs` is the scan's sentinel (a larger earlier launch may have used it): k_pairs zeroed it
     // one segment per thread: the epilogue writes up to 64 header slots per segment

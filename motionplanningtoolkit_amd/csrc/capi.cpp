@@ -2,6 +2,7 @@
 // and cluster construction for the environment and agent meshes.
 #include <algorithm>
 #include <atomic>
+#include <cfloat>
 #include <cmath>
 #include <cstring>
 #include <mutex>
@@ -77,6 +78,7 @@ struct mpt_env {
     EnvTri *d_tris = nullptr;
     BvhNode *d_nodes = nullptr;
     Item *d_items = nullptr;
+    uint4 *d_qitems = nullptr;
     int64_t n_tris = 0, n_nodes = 0, depth = 0;
 };
 
@@ -349,6 +351,47 @@ extern "C" mpt_status mpt_env_create(const double *tris, int64_t n_tris, const d
                           "H2D");
                 env->dev.n_levels = (int32_t)lev_off.size() - 1;
                 for (size_t l = 0; l < lev_off.size(); ++l) env->dev.lev_off[l] = lev_off[l];
+                // quantized copies (EnvDev::qitems) over the root box (= the top level's union)
+                {
+                    float rlo[3] = {FLT_MAX, FLT_MAX, FLT_MAX}, rhi[3] = {-FLT_MAX, -FLT_MAX, -FLT_MAX};
+                    for (int32_t i = lev_off[lev_off.size() - 2]; i < lev_off.back(); ++i)
+                        for (int k = 0; k < 3; ++k) {
+                            rlo[k] = std::min(rlo[k], items[i].lo[k]);
+                            rhi[k] = std::max(rhi[k], items[i].hi[k]);
+                        }
+                    double scale[3];
+                    for (int k = 0; k < 3; ++k) {
+                        const double ext = (double)rhi[k] - (double)rlo[k];
+                        scale[k] = ext > 0 ? (double)kQMax / ext : 0.0;
+                        env->dev.q_org[k] = rlo[k];
+                        env->dev.q_scale[k] = (float)scale[k];
+                    }
+                    // outward: floor / ceil of the exact grid coordinate (the 1e-6 covers the
+                    // double rounding of the product)
+                    auto qlo = [&](float x, int k) {
+                        const double v = std::floor(((double)x - (double)rlo[k]) * scale[k] - 1e-6);
+                        return (uint32_t)std::min<double>(kQMax, std::max(0.0, v));
+                    };
+                    auto qhi = [&](float x, int k) {
+                        const double v = std::ceil(((double)x - (double)rlo[k]) * scale[k] + 1e-6);
+                        return (uint32_t)std::min<double>(kQMax, std::max(0.0, v));
+                    };
+                    std::vector<uint4> q(items.size());
+                    bool packable = true;
+                    for (size_t i = 0; i < items.size(); ++i) {
+                        const Item &it = items[i];
+                        if (it.first < 0 || it.first >= (1 << 26) || it.count < 1 || it.count > 64) packable = false;
+                        q[i].x = qlo(it.lo[0], 0) | qlo(it.lo[1], 1) << 16;
+                        q[i].y = qhi(it.hi[0], 0) | qhi(it.hi[1], 1) << 16;
+                        q[i].z = qlo(it.lo[2], 2) | qhi(it.hi[2], 2) << 16;
+                        q[i].w = (uint32_t)it.first | (uint32_t)(it.count - 1) << 26;
+                    }
+                    if (packable) {
+                        hip_check(hipMalloc(&env->d_qitems, sizeof(uint4) * q.size()), "hipMalloc env qitems");
+                        hip_check(hipMemcpy(env->d_qitems, q.data(), sizeof(uint4) * q.size(), hipMemcpyHostToDevice),
+                                  "H2D");
+                    }
+                }
                 nodes = bfs_order(nodes);  // top levels first: the prefix k_collide stages in LDS
                 recs.resize(n_tris);
                 for (int64_t i = 0; i < n_tris; ++i) make_env_tri(tris + 9 * order[i], recs[i]);
@@ -363,6 +406,7 @@ extern "C" mpt_status mpt_env_create(const double *tris, int64_t n_tris, const d
                 }
             }
             env->dev.items = env->d_items;
+            env->dev.qitems = env->d_qitems;
             env->n_tris = n_tris;
             env->n_nodes = (int64_t)nodes.size();
             env->depth = depth;
@@ -385,6 +429,7 @@ extern "C" mpt_status mpt_env_destroy(mpt_env *env) {
         if (env->d_tris) (void)hipFree(env->d_tris);
         if (env->d_nodes) (void)hipFree(env->d_nodes);
         if (env->d_items) (void)hipFree(env->d_items);
+        if (env->d_qitems) (void)hipFree(env->d_qitems);
         delete env;
     });
 }

@@ -63,10 +63,18 @@ struct Item {
 static_assert(sizeof(Item) == 32, "Item layout");
 constexpr int kMaxLevels = 8;
 
+// An Item's box quantized to 15 bits per coordinate over the env root box, rounded outward
+// (a superset of the float box, so a test on it never drops a pair the float test keeps), and
+// its children packed: 16 B instead of 32, one LDS read per box (k_pairs' two-level walk).
+//   x = lo.x | lo.y << 16, y = hi.x | hi.y << 16, z = lo.z | hi.z << 16,
+//   w = first | (count - 1) << 26
+constexpr uint32_t kQMax = 32767u;
 struct EnvDev {
     const EnvTri *tris;
     const BvhNode *nodes;
     const Item *items;    // all levels, level l at [lev_off[l], lev_off[l+1])
+    const uint4 *qitems;  // the same items quantized (see kQMax), or nullptr
+    float q_org[3], q_scale[3];  // quantization frame: q = (x - q_org) * q_scale
     double tf[12];        // R1 (row-major) + T1: parseTransform of "Environment Location"
     float root_lo[3], root_hi[3];  // root box (float, widened)
     int32_t n_tris;
