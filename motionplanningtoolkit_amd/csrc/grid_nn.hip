@@ -80,9 +80,9 @@ __device__ __forceinline__ void block_fold_spread(unsigned long long (&mn)[3], u
 // that follows in the stream folds them).
 // One workgroup's kQueriesPerBlock queries into their buckets: an LDS histogram, then one
 // device atomic per (workgroup, bucket) for the bucket's base, then each query's slot.  The
-// device atomics on one bucket serialise, so a workgroup takes 1024 queries (64 atomics per
-// bucket for 65536 queries instead of 256).
-constexpr int kQueriesPerThread = 4, kQueriesPerBlock = 256 * kQueriesPerThread;
+// device atomics on one bucket serialise, so a workgroup takes 256 * kQueriesPerThread
+// queries (512 by default: 128 atomics per bucket for 65536 queries).
+template <int kQueriesPerThread>
 __device__ __forceinline__ void bucket_queries(const QueryBucketing &qb, int32_t d, int64_t first) {
     __shared__ int32_t s_cnt[kQueryBuckets], s_base[kQueryBuckets];
     const QueryOrder &o = qb.o;
@@ -132,24 +132,37 @@ __device__ __forceinline__ void bucket_queries(const QueryBucketing &qb, int32_t
         if (b[h] >= 0) o.list[(int64_t)b[h] * o.cap + s_base[b[h]] + rank[h]] = (int32_t)(first + h * 256 + threadIdx.x);
 }
 
-// n_pt_blocks: the workgroups that count points; those after them bucket queries (qb)
-template <bool kSpread>
+// n_pt_blocks: the workgroups that count points; q_lead: the query-bucketing workgroups (qb)
+// placed before them (0: after them)
+template <bool kSpread, int kQPT>
 __global__ __launch_bounds__(256) void k_grid_count(GridParams g, const double *__restrict__ pts, int32_t d,
                                                     int64_t n, const int64_t *__restrict__ n_dev,
                                                     int32_t *__restrict__ cell_of, int32_t *__restrict__ counts,
-                                                    SpreadOut sp, uint32_t n_pt_blocks, QueryBucketing qb) {
-    if (blockIdx.x >= n_pt_blocks) {  // workgroup-uniform
-        bucket_queries(qb, d, (int64_t)(blockIdx.x - n_pt_blocks) * kQueriesPerBlock);
+                                                    SpreadOut sp, uint32_t n_pt_blocks, uint32_t q_lead,
+                                                    QueryBucketing qb) {
+    if (blockIdx.x < q_lead) {  // workgroup-uniform
+        bucket_queries<kQPT>(qb, d, (int64_t)blockIdx.x * (256 * kQPT));
         return;
     }
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t pb = blockIdx.x - q_lead;
+    if (pb >= n_pt_blocks) {  // workgroup-uniform
+        bucket_queries<kQPT>(qb, d, (int64_t)(pb - n_pt_blocks) * (256 * kQPT));
+        return;
+    }
+    const int64_t i = (int64_t)pb * blockDim.x + threadIdx.x;
     if (qb.gen.out && qb.gen.set_n >= 0)
         n = qb.gen.set_n < n ? qb.gen.set_n : n;  // applied to n_dev by the round-start block
     else if (n_dev)
         n = *n_dev < n ? *n_dev : n;
     if (i < n) {
+        // the grid dims' coordinates loaded together (clamped, unconditional), then the cell
+        double x[3];
+#pragma unroll
+        for (int j = 0; j < 3; ++j) x[j] = pts[i * d + g.dims[j < g.gd ? j : 0]];
         int c[3] = {0, 0, 0};
-        for (int j = 0; j < g.gd; ++j) c[j] = cell_coord(pts[i * d + g.dims[j]], g.lo[j], g.inv_h, g.n[j]);
+#pragma unroll
+        for (int j = 0; j < 3; ++j)
+            if (j < g.gd) c[j] = cell_coord(x[j], g.lo[j], g.inv_h, g.n[j]);
         const int32_t cell = (c[0] * g.n[1] + c[1]) * g.n[2] + c[2];
         // the point's rank in its cell (arbitrary order: every result resolves ties by id), so
         // the scatter places it without an atomic of its own
@@ -165,7 +178,7 @@ __global__ __launch_bounds__(256) void k_grid_count(GridParams g, const double *
                 if (j < sp.gd) mn[j] = mx[j] = order_key_u64(pts[i * d + sp.dims[j]]);
         }
         block_fold_spread(mn, mx, s_v, s_out);
-        if (threadIdx.x < 6) sp.partial[(int64_t)blockIdx.x * 6 + threadIdx.x] = s_out[threadIdx.x];
+        if (threadIdx.x < 6) sp.partial[(int64_t)pb * 6 + threadIdx.x] = s_out[threadIdx.x];
     }
 }
 
@@ -423,16 +436,31 @@ void GridIndex::build(const double *pts, int64_t n_upper, const int64_t *n_dev, 
     n_max = n_upper;
     if (!counts_zero) hip_check(hipMemsetAsync(counts, 0, sizeof(int32_t) * (size_t)cells_cap, stream), "grid memset");
     counts_zero = false;
-    const unsigned qblocks = qb ? (unsigned)((qb->nq + kQueriesPerBlock - 1) / kQueriesPerBlock) : 0u;
+    // queries per bucketing thread (MPT_GRID_QPT 1 / 2 / 4) and whether those workgroups lead
+    // the launch (MPT_GRID_QFIRST), A/B knobs: config 2's build 28.2 (4) -> 27.0 (2) / 27.1 (1)
+    // us, 380 -> 383 M valid ext/s; leading workgroups no different
+    static const int qpt = getenv("MPT_GRID_QPT") ? atoi(getenv("MPT_GRID_QPT")) : 2;
+    static const bool qfirst = getenv("MPT_GRID_QFIRST") && atoi(getenv("MPT_GRID_QFIRST")) != 0;
+    const int qpb = 256 * (qpt == 1 || qpt == 2 ? qpt : 4);
+    const unsigned qblocks = qb ? (unsigned)((qb->nq + qpb - 1) / qpb) : 0u;
     if (n_upper > 0 || qblocks > 0) {
         const unsigned blocks = (unsigned)((n_upper + 255) / 256);
         const QueryBucketing q = qb ? *qb : QueryBucketing{};
-        if (spread)
-            hipLaunchKernelGGL(k_grid_count<true>, dim3(blocks + qblocks), dim3(256), 0, stream, g, pts, d, n_upper,
-                               n_dev, cell_of, counts, *spread, blocks, q);
-        else
-            hipLaunchKernelGGL(k_grid_count<false>, dim3(blocks + qblocks), dim3(256), 0, stream, g, pts, d, n_upper,
-                               n_dev, cell_of, counts, SpreadOut{}, blocks, q);
+        const unsigned lead = qfirst ? qblocks : 0u;
+        const SpreadOut sp = spread ? *spread : SpreadOut{};
+        auto go = [&](auto kern) {
+            hipLaunchKernelGGL(kern, dim3(blocks + qblocks), dim3(256), 0, stream, g, pts, d, n_upper, n_dev, cell_of,
+                               counts, sp, blocks, lead, q);
+        };
+        if (spread) {
+            if (qpb == 256) go(k_grid_count<true, 1>);
+            else if (qpb == 512) go(k_grid_count<true, 2>);
+            else go(k_grid_count<true, 4>);
+        } else {
+            if (qpb == 256) go(k_grid_count<false, 1>);
+            else if (qpb == 512) go(k_grid_count<false, 2>);
+            else go(k_grid_count<false, 4>);
+        }
         hip_check(hipGetLastError(), "k_grid_count");
     }
     // the scan leaves every count zero again, so the next build needs no memset
