@@ -27,7 +27,7 @@ struct GridDev {
 // Points are stored as records of d + 1 doubles with the 1-based id in the pad (32 / 64-B
 // aligned: a point and its id in one line) for d < 8; the snake's d = 15 keeps 15-double
 // records and an id array (its 128-B padded records measured 1.7x slower: 0.73 -> 1.22 ms).
-__host__ __device__ __forceinline__ int32_t grid_stride(int32_t d) { return d < 8 ? d + 1 : d; }
+__host__ __device__ __forceinline__ constexpr int32_t grid_stride(int32_t d) { return d < 8 ? d + 1 : d; }
 // D > 0: the layout is known at compile time; D = 0: the run-time dim d decides
 template <int D>
 __device__ __forceinline__ int32_t grid_id(const GridDev &G, const double *rec, int d, int64_t p) {

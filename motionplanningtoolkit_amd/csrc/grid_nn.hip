@@ -184,7 +184,7 @@ __global__ __launch_bounds__(256) void k_grid_count(GridParams g, const double *
 
 // Scatter into cell order.  kSpread: block 0 first folds k_grid_count's per-block spread
 // partials (n_part of them, all threads) and writes the result to mapped host memory.
-template <bool kSpread>
+template <bool kSpread, int D>
 __global__ __launch_bounds__(256) void k_grid_scatter(const double *__restrict__ pts, int32_t d, int64_t n,
                                                       const int64_t *__restrict__ n_dev,
                                                       const int32_t *__restrict__ cell_of,
@@ -213,16 +213,37 @@ __global__ __launch_bounds__(256) void k_grid_scatter(const double *__restrict__
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (n_dev) n = *n_dev < n ? *n_dev : n;
     if (i >= n) return;
-    const int2 cr = reinterpret_cast<const int2 *>(cell_of)[i];
-    const int64_t pos = (int64_t)cell_start[cr.x] + cr.y;
-    // record of d + 1 doubles: the coordinates, then the 1-based id in the pad slot, so a
-    // query reads a point and its id from one 32 / 64 / 128-B aligned record
-    double *rec = spts + pos * grid_stride(d);
-    for (int j = 0; j < d; ++j) rec[j] = pts[i * d + j];
-    if (grid_stride(d) > d)
-        rec[d] = __longlong_as_double((long long)(i + 1));
-    else
-        sids[pos] = (int32_t)(i + 1);
+    if constexpr (D > 0) {
+        // the point's row loaded alongside its (cell, rank), not after the cell start (a
+        // run-time-length copy loop would wait on each load in turn)
+        double v[grid_stride(D) + 1];
+#pragma unroll
+        for (int j = 0; j < D; ++j) v[j] = pts[i * D + j];
+        v[D] = __longlong_as_double((long long)(i + 1));
+        const int2 cr = reinterpret_cast<const int2 *>(cell_of)[i];
+        const int64_t pos = (int64_t)cell_start[cr.x] + cr.y;
+        double *rec = spts + pos * grid_stride(D);
+        if constexpr (grid_stride(D) > D) {  // even-length padded record: 16-B stores
+#pragma unroll
+            for (int j = 0; j < grid_stride(D) / 2; ++j)
+                reinterpret_cast<double2 *>(rec)[j] = make_double2(v[2 * j], v[2 * j + 1]);
+        } else {
+#pragma unroll
+            for (int j = 0; j < D; ++j) rec[j] = v[j];
+            sids[pos] = (int32_t)(i + 1);
+        }
+    } else {
+        const int2 cr = reinterpret_cast<const int2 *>(cell_of)[i];
+        const int64_t pos = (int64_t)cell_start[cr.x] + cr.y;
+        // record of d + 1 doubles: the coordinates, then the 1-based id in the pad slot, so a
+        // query reads a point and its id from one 32 / 64 / 128-B aligned record
+        double *rec = spts + pos * grid_stride(d);
+        for (int j = 0; j < d; ++j) rec[j] = pts[i * d + j];
+        if (grid_stride(d) > d)
+            rec[d] = __longlong_as_double((long long)(i + 1));
+        else
+            sids[pos] = (int32_t)(i + 1);
+    }
 }
 
 // scan epilogue of the grid build: each count back to zero once scanned
@@ -468,12 +489,27 @@ void GridIndex::build(const double *pts, int64_t n_upper, const int64_t *n_dev, 
                      g.ncells + 1, stream, ZeroCounts{reinterpret_cast<uint32_t *>(counts)});
     if (n_upper > 0) {
         const unsigned blocks = (unsigned)((n_upper + 255) / 256);
-        if (spread)
-            hipLaunchKernelGGL(k_grid_scatter<true>, dim3(blocks), dim3(256), 0, stream, pts, d, n_upper, n_dev,
-                               cell_of, cell_start, spts, sids, *spread, (int32_t)blocks);
-        else
-            hipLaunchKernelGGL(k_grid_scatter<false>, dim3(blocks), dim3(256), 0, stream, pts, d, n_upper, n_dev,
-                               cell_of, cell_start, spts, sids, SpreadOut{}, 0);
+        // the state dims the engines use get a compile-time row (MPT_GRID_SCATTER_D=0: the
+        // run-time copy loop, A/B)
+        static const bool fixed_d = !getenv("MPT_GRID_SCATTER_D") || atoi(getenv("MPT_GRID_SCATTER_D")) != 0;
+        const SpreadOut sp = spread ? *spread : SpreadOut{};
+        const int32_t n_part = spread ? (int32_t)blocks : 0;
+        auto go = [&](auto kern) {
+            hipLaunchKernelGGL(kern, dim3(blocks), dim3(256), 0, stream, pts, d, n_upper, n_dev, cell_of, cell_start,
+                               spts, sids, sp, n_part);
+        };
+        const int dd = fixed_d ? d : 0;
+        if (spread) {
+            if (dd == 3) go(k_grid_scatter<true, 3>);
+            else if (dd == 7) go(k_grid_scatter<true, 7>);
+            else if (dd == 15) go(k_grid_scatter<true, 15>);
+            else go(k_grid_scatter<true, 0>);
+        } else {
+            if (dd == 3) go(k_grid_scatter<false, 3>);
+            else if (dd == 7) go(k_grid_scatter<false, 7>);
+            else if (dd == 15) go(k_grid_scatter<false, 15>);
+            else go(k_grid_scatter<false, 0>);
+        }
         hip_check(hipGetLastError(), "k_grid_scatter");
     }
     counts_zero = true;  // the scan zeroed every count it read
