@@ -175,7 +175,14 @@ __device__ __forceinline__ int32_t steer_one(const EngineParams &p, uint64_t ext
     const int d = KIND == MPT_AGENT_SNAKE ? p.d : DD;
     double from[DD], end[DD];
     const int64_t src = nn[k] - 1;  // nn ids are 1-based
-    for (int j = 0; j < d; ++j) from[j] = nodes[src * d + j];
+    if constexpr (KIND == MPT_AGENT_SNAKE) {
+        // run-time d: the row loaded whole (clamped, unconditional), not one load at a time
+#pragma unroll
+        for (int j = 0; j < DD; ++j) from[j] = nodes[src * d + (j < d ? j : d - 1)];
+    } else {
+#pragma unroll
+        for (int j = 0; j < DD; ++j) from[j] = nodes[src * DD + j];
+    }
     double *ps = poses + (int64_t)k * p.pmax * p.L * 12;
     int32_t P = 0;
     if constexpr (KIND == MPT_AGENT_OMNI) {
@@ -355,7 +362,14 @@ __device__ __forceinline__ void append_commit_tail(int64_t before_block, int32_t
     if (ok) {
         const int64_t idx = n0 + before_block + wbase + __popcll(m & ((1ull << lane) - 1ull));
         if (idx < cap) {
-            for (int j = 0; j < d; ++j) nodes[idx * d + j] = ends[k * d + j];
+            // the row loaded whole before any store (clamped, unconditional: one round trip; a
+            // run-time-length copy loop waits on each load in turn)
+            double v[kMaxDim];
+#pragma unroll
+            for (int j = 0; j < kMaxDim; ++j) v[j] = ends[k * d + (j < d ? j : d - 1)];
+#pragma unroll
+            for (int j = 0; j < kMaxDim; ++j)
+                if (j < d) nodes[idx * d + j] = v[j];
             parents[idx] = nn[k];
         }
     }
@@ -420,9 +434,17 @@ __global__ __launch_bounds__(256) void k_append_commit(const uint8_t *__restrict
     const uint4 *v4 = reinterpret_cast<const uint4 *>(verdict);
     const int64_t nv4 = (int64_t)blockIdx.x * 16;  // 256 verdicts per block before this one
     int32_t ones = 0;
-    for (int64_t i = tid; i < nv4; i += 256) {
-        const uint4 x = v4[i];
-        ones += __popc(x.x) + __popc(x.y) + __popc(x.z) + __popc(x.w);
+    // eight 16-B loads in flight per thread (clamped, unconditional), not one round trip each
+    for (int64_t i0 = tid; i0 < nv4; i0 += 256 * 8) {
+        uint4 x[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int64_t i = i0 + u * 256;
+            x[u] = v4[i < nv4 ? i : 0];
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+            if (i0 + u * 256 < nv4) ones += __popc(x[u].x) + __popc(x[u].y) + __popc(x[u].z) + __popc(x[u].w);
     }
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) ones += __shfl_xor(ones, off);
