@@ -595,6 +595,40 @@ MPT_HD double flann_l2(const double *a, const double *b) {
     return result;
 }
 
+// flann_l2's first NG groups of four dims alone, and the sum continued from them:
+// flann_l2_rest<D, NG>(a, b, flann_l2_head<NG>(a, b)) == flann_l2<D>(a, b) bit for bit, and the
+// head never exceeds the full sum (every later term is non-negative, rounding is monotone)
+template <int NG>
+MPT_HD double flann_l2_head(const double *a, const double *b) {
+    double result = 0.0;
+#pragma unroll
+    for (int i = 0; i < 4 * NG; i += 4) {
+        const double d0 = a[i] - b[i], d1 = a[i + 1] - b[i + 1];
+        const double d2 = a[i + 2] - b[i + 2], d3 = a[i + 3] - b[i + 3];
+        const double t = d0 * d0 + d1 * d1 + d2 * d2 + d3 * d3;
+        result = (i == 0) ? t : result + t;
+    }
+    return result;
+}
+template <int D, int NG>
+MPT_HD double flann_l2_rest(const double *a, const double *b, double head) {
+    static_assert(D >= 4 * NG, "the head is whole groups of four");
+    double result = head;
+    int i = 4 * NG;
+#pragma unroll
+    for (; i + 3 < D; i += 4) {
+        const double d0 = a[i] - b[i], d1 = a[i + 1] - b[i + 1];
+        const double d2 = a[i + 2] - b[i + 2], d3 = a[i + 3] - b[i + 3];
+        result = result + (d0 * d0 + d1 * d1 + d2 * d2 + d3 * d3);
+    }
+#pragma unroll
+    for (; i < D; ++i) {
+        const double d0 = a[i] - b[i];
+        result += d0 * d0;
+    }
+    return result;
+}
+
 MPT_HD double flann_l2_dyn(const double *a, const double *b, int d) {
     double result = 0.0;
     int i = 0;

@@ -784,7 +784,7 @@ __device__ __forceinline__ int small_div(int a, int side, float inv_side) {
 // so every per-dim loop is unrolled and the query's grid coordinates come from registers.
 // The merge is in (d2, id) order and the stop test is the ring bound, so the result is the
 // brute-force result bit for bit.
-template <int D, int GD, int kGroup, int kPts>
+template <int D, int GD, int kGroup, int kPts, int kHeadScreen = 0>
 __device__ __forceinline__ void nn1_runs_query(const GridDev &G, const double *__restrict__ q, int64_t qi, int sub,
                                                int32_t *__restrict__ out_ids, double *__restrict__ out_d2) {
     const GridParams &g = G.g;
@@ -902,18 +902,42 @@ __device__ __forceinline__ void nn1_runs_query(const GridDev &G, const double *_
                 }
                 double dd[kPts];
                 int32_t id[kPts];
+                bool skip[kPts];
+                if constexpr (kHeadScreen > 0 && D >= 8) {
+                    // long records (the snake's 120 B): each point's first four dims first, the
+                    // rest and its id only when that head sum does not exceed the lane's best
+                    // (the full sum is at least the head, so a skipped point cannot be better)
+                    double head[kPts];
 #pragma unroll
-                for (int h = 0; h < kPts; ++h) {
-                    if (p[h] >= 0) {
-                        const double *rec = G.pts + (int64_t)p[h] * grid_stride(D);
-                        dd[h] = flann_l2<D>(qq, rec);
-                        id[h] = grid_id<D>(G, rec, D, p[h]);
+                    for (int h = 0; h < kPts; ++h) {
+                        head[h] = 0.0;
+                        if (p[h] >= 0) head[h] = flann_l2_head<kHeadScreen>(qq, G.pts + (int64_t)p[h] * grid_stride(D));
+                    }
+#pragma unroll
+                    for (int h = 0; h < kPts; ++h) {
+                        skip[h] = p[h] >= 0 && head[h] > bd;
+                        if (p[h] >= 0 && !skip[h]) {
+                            const double *rec = G.pts + (int64_t)p[h] * grid_stride(D);
+                            dd[h] = flann_l2_rest<D, kHeadScreen>(qq, rec, head[h]);
+                            id[h] = grid_id<D>(G, rec, D, p[h]);
+                        }
+                    }
+                } else {
+#pragma unroll
+                    for (int h = 0; h < kPts; ++h) {
+                        skip[h] = false;
+                        if (p[h] >= 0) {
+                            const double *rec = G.pts + (int64_t)p[h] * grid_stride(D);
+                            dd[h] = flann_l2<D>(qq, rec);
+                            id[h] = grid_id<D>(G, rec, D, p[h]);
+                        }
                     }
                 }
 #pragma unroll
                 for (int h = 0; h < kPts; ++h) {
                     if (p[h] < 0) continue;
                     ++n_pts;
+                    if (skip[h]) continue;
                     if (G.removed && G.removed[id[h] - 1]) continue;
                     if (nn_better(dd[h], id[h], bd, bi)) {
                         bd = dd[h];
@@ -1010,7 +1034,7 @@ __global__ __launch_bounds__(256) void k_grid_nn1_runs_xcd(GridDev G, const doub
 
 // Bucket-sorted 1-NN (QueryOrder): workgroup b runs on XCD b % 8 and takes slice b % 8,
 // chunk b / 8 of the bucket-major query order; a query's index comes from its bucket's list.
-template <int D, int GD, int kGroup, int kPts>
+template <int D, int GD, int kGroup, int kPts, int kHS>
 __global__ __launch_bounds__(256) void k_grid_nn1_runs_sorted(GridDev G, const double *__restrict__ q, int64_t nq,
                                                               QueryOrder o, int32_t *__restrict__ out_ids,
                                                               double *__restrict__ out_d2) {
@@ -1040,7 +1064,7 @@ __global__ __launch_bounds__(256) void k_grid_nn1_runs_sorted(GridDev G, const d
         else hi = mid - 1;
     }
     const int64_t qi = o.list[(int64_t)lo * o.cap + (pos - s_pre[lo])];
-    nn1_runs_query<D, GD, kGroup, kPts>(G, q, qi, (int)(threadIdx.x % kGroup), out_ids, out_d2);
+    nn1_runs_query<D, GD, kGroup, kPts, kHS>(G, q, qi, (int)(threadIdx.x % kGroup), out_ids, out_d2);
 }
 
 // run-kernel group shape per state dim: 16 lanes x 1 point for d <= 7 (config 2: 54.7 us vs
@@ -1057,8 +1081,19 @@ static void grid_nn1_sorted_dg(const GridDev &G, const double *q, int64_t nq, co
     constexpr int QPW = 256 / GRP;
     int64_t wgs = (nq + QPW - 1) / QPW;
     wgs = (wgs + 7) / 8 * 8;
-    hipLaunchKernelGGL((k_grid_nn1_runs_sorted<D, GD, GRP, PTS>), dim3((unsigned)wgs), dim3(256), 0, stream, G, q, nq,
-                       o, ids, d2);
+    // records of d >= 8 (the snake's 120 B) are screened by their first MPT_NN_HEAD groups of
+    // four dims (A/B on config 3's NN: 0.617 ms unscreened, 0.566 at one group, 0.472 at two,
+    // 0.533 at three)
+    static const int head = getenv("MPT_NN_HEAD") ? atoi(getenv("MPT_NN_HEAD")) : 2;
+    if (D >= 8 && head == 1)
+        hipLaunchKernelGGL((k_grid_nn1_runs_sorted<D, GD, GRP, PTS, 1>), dim3((unsigned)wgs), dim3(256), 0, stream,
+                           G, q, nq, o, ids, d2);
+    else if (D >= 8 && head == 2)
+        hipLaunchKernelGGL((k_grid_nn1_runs_sorted<D, GD, GRP, PTS, 2>), dim3((unsigned)wgs), dim3(256), 0, stream,
+                           G, q, nq, o, ids, d2);
+    else
+        hipLaunchKernelGGL((k_grid_nn1_runs_sorted<D, GD, GRP, PTS, 0>), dim3((unsigned)wgs), dim3(256), 0, stream,
+                           G, q, nq, o, ids, d2);
 }
 
 template <int D>

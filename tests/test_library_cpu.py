@@ -141,3 +141,49 @@ def test_seg_points_branch_free_matches_branchy(tmp_path):
                     "c++", str(src), "-o", str(exe)], check=True)
     out = subprocess.run([str(exe)], check=True, capture_output=True, text=True).stdout.strip()
     assert out == "0"
+
+
+_HEAD_PROBE = r"""
+#define __HIP_PLATFORM_AMD__ 1
+#include "fcl_math.h"
+#include <cstdio>
+#include <cstring>
+#include <random>
+using namespace mpt;
+template <int D, int NG>
+static long check(std::mt19937_64 &g) {
+    std::uniform_real_distribution<double> U(-50, 50);
+    long bad = 0;
+    double a[D], b[D];
+    for (long it = 0; it < 300000; ++it) {
+        for (int i = 0; i < D; ++i) {
+            a[i] = U(g);
+            b[i] = (it % 4 == 1 && i < 4 * NG) ? a[i] : U(g);  // head exactly zero
+        }
+        const double full = flann_l2<D>(a, b), head = flann_l2_head<NG>(a, b);
+        const double rest = flann_l2_rest<D, NG>(a, b, head);
+        if (memcmp(&full, &rest, 8) != 0 || head > full) ++bad;
+    }
+    return bad;
+}
+int main() {
+    std::mt19937_64 g(11);
+    printf("%ld\n", check<15, 1>(g) + check<15, 2>(g) + check<8, 1>(g) + check<8, 2>(g) + check<13, 3>(g));
+    return 0;
+}
+"""
+
+
+@pytest.mark.skipif(shutil.which("g++") is None or not os.path.isdir("/opt/rocm/include"), reason="needs g++ and HIP headers")
+def test_flann_l2_head_rest_split(tmp_path):
+    """The NN run kernel's head screen (grid_nn.hip, long records): FLANN's L2 sum split into its
+    first groups of four (fcl_math.h flann_l2_head) and the rest continued from them
+    (flann_l2_rest) equals flann_l2 bit for bit, and the head never exceeds the full sum, so a
+    point skipped because its head exceeds the best cannot be better."""
+    src, exe = tmp_path / "head.cpp", tmp_path / "head"
+    src.write_text(_HEAD_PROBE)
+    csrc = os.path.join(REPO, "motionplanningtoolkit_amd", "csrc")
+    subprocess.run(["g++", "-O2", "-std=c++17", "-ffp-contract=off", "-I", csrc, "-I", "/opt/rocm/include", "-x",
+                    "c++", str(src), "-o", str(exe)], check=True)
+    out = subprocess.run([str(exe)], check=True, capture_output=True, text=True).stdout.strip()
+    assert out == "0"
