@@ -991,7 +991,7 @@ __global__ __launch_bounds__(256) void k_grid_nn1_runs(GridDev G, const double *
     const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int64_t slot = t / kGroup;
     if (slot >= nq) return;  // whole groups leave together (nq is per group)
-    nn1_runs_query<D, GD, kGroup, kPts>(G, q, slot, (int)(t % kGroup), out_ids, out_d2);
+    nn1_runs_query<D, GD, kGroup, kPts, (D >= 8 ? 2 : 0)>(G, q, slot, (int)(t % kGroup), out_ids, out_d2);
 }
 
 // XCD-aware variant.  The points are in cell order, x-major, so the cells of an x-slab
@@ -1029,7 +1029,8 @@ __global__ __launch_bounds__(256) void k_grid_nn1_runs_xcd(GridDev G, const doub
     __syncthreads();
     const int total = s_cnt[0] + (kChunk > 64 ? s_cnt[1] : 0);
     const int grp = threadIdx.x / kGroup, sub = threadIdx.x % kGroup;
-    for (int i = grp; i < total; i += NG) nn1_runs_query<D, GD, kGroup, kPts>(G, q, s_idx[i], sub, out_ids, out_d2);
+    for (int i = grp; i < total; i += NG)
+        nn1_runs_query<D, GD, kGroup, kPts, (D >= 8 ? 2 : 0)>(G, q, s_idx[i], sub, out_ids, out_d2);
 }
 
 // Bucket-sorted 1-NN (QueryOrder): workgroup b runs on XCD b % 8 and takes slice b % 8,

@@ -46,12 +46,14 @@ def test_knn_k_exact(mpt_gpu, oracle, k, mode):
 
 
 @pytest.mark.parametrize("mode", MODES)
-def test_ties_resolve_to_lowest_id(mpt_gpu, oracle, mode):
+@pytest.mark.parametrize("d", [3, 15])
+def test_ties_resolve_to_lowest_id(mpt_gpu, oracle, mode, d):
+    # d = 15: the run kernel's head screen (first eight dims) on exact ties
     rng = np.random.default_rng(7)
-    base = rng.integers(-3, 4, size=(500, 3)).astype(np.float64)  # lattice: many exact ties
+    base = rng.integers(-3, 4, size=(500, d)).astype(np.float64)  # lattice: many exact ties
     pts = np.concatenate([base, base, base])
-    q = np.r_[rng.integers(-3, 4, size=(300, 3)).astype(np.float64) + 0.5, base[:50]]
-    nn = mpt_gpu.NearestNeighbors(3)
+    q = np.r_[rng.integers(-3, 4, size=(300, d)).astype(np.float64) + 0.5, base[:50]]
+    nn = mpt_gpu.NearestNeighbors(d)
     nn.set_index(mode)
     nn.append(pts)
     for k in (1, 4):
