@@ -135,10 +135,14 @@ __device__ void pt_plan(int32_t d, unsigned long long *__restrict__ box, CodePla
 }
 
 // per-dim min / max of the live points as order keys: box[0..d) min, box[kPtMaxDim..) max
-__device__ __forceinline__ void pt_bbox(const double *__restrict__ pts, int32_t d, int64_t n_upper,
+// D > 0: the state dim at compile time (rows loaded whole, several points in flight); D = 0:
+// the run-time d
+template <int D = 0>
+__device__ __forceinline__ void pt_bbox(const double *__restrict__ pts, int32_t d_rt, int64_t n_upper,
                                         const int64_t *__restrict__ n_dev, unsigned long long *__restrict__ box,
                                         unsigned int *__restrict__ ticket, CodePlan *__restrict__ plan,
                                         const SpreadOut &sp, int64_t blk, int64_t nblk) {
+    const int32_t d = D > 0 ? D : d_rt;
     __shared__ unsigned long long s_min[kPtMaxDim], s_max[kPtMaxDim];
     if (threadIdx.x < kPtMaxDim) {
         s_min[threadIdx.x] = ~0ull;
@@ -154,14 +158,38 @@ __device__ __forceinline__ void pt_bbox(const double *__restrict__ pts, int32_t 
         mn[j] = ~0ull;
         mx[j] = 0ull;
     }
-    for (int64_t i = blk * blockDim.x + threadIdx.x; i < n; i += nblk * blockDim.x) {
+    if constexpr (D > 0) {
+        // U rows loaded before any is reduced (a row past n repeats the first: min / max
+        // do not change), instead of one guarded load and its wait per coordinate
+        constexpr int U = D >= 15 ? 2 : 4;
+        const int64_t stride = nblk * blockDim.x;
+        for (int64_t i0 = blk * blockDim.x + threadIdx.x; i0 < n; i0 += U * stride) {
+            double v[U][D];
 #pragma unroll
-        for (int j = 0; j < kPtMaxDim; ++j)
-            if (j < d) {
-                const unsigned long long k = order_key_pt(pts[i * d + j]);
-                mn[j] = k < mn[j] ? k : mn[j];
-                mx[j] = k > mx[j] ? k : mx[j];
+            for (int u = 0; u < U; ++u) {
+                const int64_t i = i0 + u * stride < n ? i0 + u * stride : i0;
+#pragma unroll
+                for (int j = 0; j < D; ++j) v[u][j] = pts[i * D + j];
             }
+#pragma unroll
+            for (int u = 0; u < U; ++u)
+#pragma unroll
+                for (int j = 0; j < D; ++j) {
+                    const unsigned long long k = order_key_pt(v[u][j]);
+                    mn[j] = k < mn[j] ? k : mn[j];
+                    mx[j] = k > mx[j] ? k : mx[j];
+                }
+        }
+    } else {
+        for (int64_t i = blk * blockDim.x + threadIdx.x; i < n; i += nblk * blockDim.x) {
+#pragma unroll
+            for (int j = 0; j < kPtMaxDim; ++j)
+                if (j < d) {
+                    const unsigned long long k = order_key_pt(pts[i * d + j]);
+                    mn[j] = k < mn[j] ? k : mn[j];
+                    mx[j] = k > mx[j] ? k : mx[j];
+                }
+        }
     }
 #pragma unroll
     for (int j = 0; j < kPtMaxDim; ++j) {
@@ -208,7 +236,8 @@ __global__ __launch_bounds__(64) void k_pt_plan(int32_t d, unsigned long long *_
     pt_plan(d, box, plan, sp);
 }
 
-__device__ __forceinline__ void pt_morton(const double *__restrict__ pts, int32_t d, int64_t n_upper,
+template <int D = 0>
+__device__ __forceinline__ void pt_morton(const double *__restrict__ pts, int32_t d_rt, int64_t n_upper,
                                           const int64_t *__restrict__ n_dev, const CodePlan *__restrict__ plan,
                                           uint32_t *__restrict__ keys, int32_t *__restrict__ vals, int64_t blk) {
     const int64_t i = blk * blockDim.x + threadIdx.x;
@@ -219,15 +248,39 @@ __device__ __forceinline__ void pt_morton(const double *__restrict__ pts, int32_
         keys[i] = 0xffffffffu;  // past the live count: sorted to the end
         return;
     }
+    const int32_t d = D > 0 ? D : d_rt;
     uint32_t q[kPtMaxDim];
-    for (int j = 0; j < d; ++j) {
-        const double u = (pts[i * d + j] - plan->lo[j]) * plan->scale[j];
-        const uint32_t m = plan->qmax[j];
-        q[j] = u <= 0.0 ? 0u : (u >= (double)m ? m : (uint32_t)u);
+    if constexpr (D > 0) {
+        double x[D];  // the row loaded whole before any use
+#pragma unroll
+        for (int j = 0; j < D; ++j) x[j] = pts[i * D + j];
+#pragma unroll
+        for (int j = 0; j < D; ++j) {
+            const double u = (x[j] - plan->lo[j]) * plan->scale[j];
+            const uint32_t m = plan->qmax[j];
+            q[j] = u <= 0.0 ? 0u : (u >= (double)m ? m : (uint32_t)u);
+        }
+    } else {
+        for (int j = 0; j < d; ++j) {
+            const double u = (pts[i * d + j] - plan->lo[j]) * plan->scale[j];
+            const uint32_t m = plan->qmax[j];
+            q[j] = u <= 0.0 ? 0u : (u >= (double)m ? m : (uint32_t)u);
+        }
     }
     uint32_t code = 0;
     const int32_t nb = plan->n;
-    for (int k = 0; k < nb; ++k) code = (code << 1) | ((q[plan->dim[k]] >> plan->bit[k]) & 1u);
+    for (int k = 0; k < nb; ++k) {
+        const int32_t dk = plan->dim[k];
+        uint32_t v = q[0];
+        if constexpr (D > 0) {  // a select over the row instead of an indexed register read
+#pragma unroll
+            for (int j = 1; j < D; ++j)
+                if (j == dk) v = q[j];
+        } else {
+            v = q[dk];
+        }
+        code = (code << 1) | ((v >> plan->bit[k]) & 1u);
+    }
     keys[i] = code;
 }
 
@@ -238,17 +291,26 @@ __global__ void k_pt_morton(const double *__restrict__ pts, int32_t d, int64_t n
 
 // Coordinates and ids into code order, and the level-1 boxes with them: a leaf is 8
 // consecutive sorted points, i.e. 8 consecutive lanes, so its bounds are an 8-lane reduction.
-__device__ __forceinline__ void pt_gather(const double *__restrict__ pts, int32_t d, int64_t n_upper,
+template <int D = 0>
+__device__ __forceinline__ void pt_gather(const double *__restrict__ pts, int32_t d_rt, int64_t n_upper,
                                           const int64_t *__restrict__ n_dev, const int32_t *__restrict__ order,
                                           double *__restrict__ spts, int32_t *__restrict__ sids,
                                           float *__restrict__ leaf_boxes, int64_t blk) {
     const int64_t i = blk * blockDim.x + threadIdx.x;
     const int64_t n = *n_dev < n_upper ? *n_dev : n_upper;
     const bool live = i < n;  // no early exit: the leaf reduction needs all 8 lanes
+    const int32_t d = D > 0 ? D : d_rt;
     const int32_t src = live ? order[i] : 0;
     if (live) sids[i] = src + 1;
+    constexpr int DM = D > 0 ? D : 1;
+    double row[DM];
+    if constexpr (D > 0) {  // the source row loaded whole (row 0 stands in past the live count)
+#pragma unroll
+        for (int j = 0; j < D; ++j) row[j] = pts[(int64_t)src * D + j];
+    }
+#pragma unroll
     for (int j = 0; j < d; ++j) {
-        const double x = live ? pts[(int64_t)src * d + j] : 0.0;
+        const double x = D > 0 ? (live ? row[j < DM ? j : 0] : 0.0) : (live ? pts[(int64_t)src * d + j] : 0.0);
         if (live) spts[i * d + j] = x;
         double lo = live ? x : __builtin_huge_val(), hi = live ? x : -__builtin_huge_val();
 #pragma unroll
@@ -338,6 +400,7 @@ __global__ __launch_bounds__(256) void k_pt_boxes(PointTreeDev T, float *__restr
 
 // ---- the same build for many trees at once (mpt_rrt_step_many): blockIdx.y = the tree; a
 // tree's keys / values live in shared buffers at its offset, sorted by one segmented sort
+template <int D>
 __global__ __launch_bounds__(256) void k_pt_bbox_jobs(const PtBuildJob *__restrict__ jobs, int32_t d,
                                                       int32_t bbox_points_per_group) {
     const PtBuildJob &J = jobs[blockIdx.y];
@@ -346,19 +409,21 @@ __global__ __launch_bounds__(256) void k_pt_bbox_jobs(const PtBuildJob *__restri
     const int64_t per = bbox_points_per_group;
     const int64_t nblk = std::min<int64_t>(gridDim.x, std::max<int64_t>(1, (J.T.n_upper + per - 1) / per));
     if (blockIdx.x >= nblk) return;  // before the ticket: only the tree's own workgroups count
-    pt_bbox(J.pts, d, J.T.n_upper, J.T.n_dev, J.bbox, J.ticket + 1, J.plan, J.sp, blockIdx.x, nblk);
+    pt_bbox<D>(J.pts, d, J.T.n_upper, J.T.n_dev, J.bbox, J.ticket + 1, J.plan, J.sp, blockIdx.x, nblk);
 }
+template <int D>
 __global__ __launch_bounds__(256) void k_pt_morton_jobs(const PtBuildJob *__restrict__ jobs, int32_t d,
                                                         uint32_t *__restrict__ keys, int32_t *__restrict__ vals) {
     const PtBuildJob &J = jobs[blockIdx.y];
     if ((int64_t)blockIdx.x * blockDim.x >= J.T.n_upper) return;
-    pt_morton(J.pts, d, J.T.n_upper, J.T.n_dev, J.plan, keys + J.off, vals + J.off, blockIdx.x);
+    pt_morton<D>(J.pts, d, J.T.n_upper, J.T.n_dev, J.plan, keys + J.off, vals + J.off, blockIdx.x);
 }
+template <int D>
 __global__ __launch_bounds__(256) void k_pt_gather_jobs(const PtBuildJob *__restrict__ jobs, int32_t d,
                                                         const int32_t *__restrict__ vals_sorted) {
     const PtBuildJob &J = jobs[blockIdx.y];
     if ((int64_t)blockIdx.x * blockDim.x >= J.T.n_upper) return;
-    pt_gather(J.pts, d, J.T.n_upper, J.T.n_dev, vals_sorted + J.off, J.spts, J.sids, J.boxes, blockIdx.x);
+    pt_gather<D>(J.pts, d, J.T.n_upper, J.T.n_dev, vals_sorted + J.off, J.spts, J.sids, J.boxes, blockIdx.x);
 }
 __global__ __launch_bounds__(256) void k_pt_boxes_jobs(const PtBuildJob *__restrict__ jobs) {
     const PtBuildJob &J = jobs[blockIdx.y];
@@ -728,14 +793,21 @@ void launch_tree_build_jobs(const PtBuildJob *d_jobs, const PtBuildJob *h_jobs, 
     // MPT_PT_BBOX_PTS: points per bbox workgroup of the joint build (A/B knob)
     static const int per = getenv("MPT_PT_BBOX_PTS") && atoi(getenv("MPT_PT_BBOX_PTS")) > 0
                                ? atoi(getenv("MPT_PT_BBOX_PTS")) : 2048;
-    hipLaunchKernelGGL(k_pt_bbox_jobs, dim3(64, n), dim3(256), 0, stream, d_jobs, d, per);
-    hipLaunchKernelGGL(k_pt_morton_jobs, dim3(bx, n), dim3(256), 0, stream, d_jobs, d, S.keys, S.vals);
+    // compile-time rows for the engines' state dims (MPT_PT_FIXED_D=0: the run-time d, A/B)
+    static const bool fixed_d = !getenv("MPT_PT_FIXED_D") || atoi(getenv("MPT_PT_FIXED_D")) != 0;
+    const int dd = fixed_d && (d == 3 || d == 7 || d == 15) ? d : 0;
+    auto by_d = [&](auto k3, auto k7, auto k15, auto k0) { return dd == 3 ? k3 : dd == 7 ? k7 : dd == 15 ? k15 : k0; };
+    hipLaunchKernelGGL(by_d(k_pt_bbox_jobs<3>, k_pt_bbox_jobs<7>, k_pt_bbox_jobs<15>, k_pt_bbox_jobs<0>), dim3(64, n),
+                       dim3(256), 0, stream, d_jobs, d, per);
+    hipLaunchKernelGGL(by_d(k_pt_morton_jobs<3>, k_pt_morton_jobs<7>, k_pt_morton_jobs<15>, k_pt_morton_jobs<0>),
+                       dim3(bx, n), dim3(256), 0, stream, d_jobs, d, S.keys, S.vals);
     hip_check(hipGetLastError(), "k_pt_morton_jobs");
     tb = S.temp_bytes;
     hip_check(hipcub::DeviceSegmentedRadixSort::SortPairs(S.temp, tb, S.keys, S.keys_sorted, S.vals, S.vals_sorted,
                                                           (int)total, n, d_offsets, d_offsets + 1, 0, 32, stream),
               "segmented sort");
-    hipLaunchKernelGGL(k_pt_gather_jobs, dim3(bx, n), dim3(256), 0, stream, d_jobs, d, S.vals_sorted);
+    hipLaunchKernelGGL(by_d(k_pt_gather_jobs<3>, k_pt_gather_jobs<7>, k_pt_gather_jobs<15>, k_pt_gather_jobs<0>),
+                       dim3(bx, n), dim3(256), 0, stream, d_jobs, d, S.vals_sorted);
     hipLaunchKernelGGL(k_pt_boxes_jobs, dim3((unsigned)max_groups, n), dim3(256), 0, stream, d_jobs);
     hip_check(hipGetLastError(), "k_pt_boxes_jobs");
 }
