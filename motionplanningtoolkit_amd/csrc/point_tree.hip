@@ -359,6 +359,19 @@ __device__ __forceinline__ void pt_up_box(const PointTreeDev &T, int64_t n, int 
 constexpr int kPtChunkLeaves = 512;  // 8^3: levels 1..4 inside a workgroup
 constexpr int kPtInBlockLevels = 4;
 
+// levels 5.. of the tree over every group's level-4 boxes (one workgroup)
+__device__ __forceinline__ void pt_top_boxes(const PointTreeDev &T, float *__restrict__ boxes) {
+    const int64_t n = live_n(T);
+    for (int l = kPtInBlockLevels + 1; l <= T.n_levels; ++l) {
+        const int64_t nl = lvl_size(n, l);
+        for (int64_t it = threadIdx.x; it < nl * T.d; it += blockDim.x)
+            pt_up_box(T, n, l, boxes, it / T.d, (int)(it % T.d));
+        __threadfence_block();
+        __syncthreads();
+    }
+}
+
+// ticket == nullptr: levels 5.. are left to a launch of their own (k_pt_top_jobs)
 __device__ __forceinline__ void pt_boxes(const PointTreeDev &T, float *__restrict__ boxes,
                                          unsigned int *__restrict__ ticket, int64_t g, int64_t ngroups) {
     const int64_t n = live_n(T);
@@ -375,7 +388,7 @@ __device__ __forceinline__ void pt_boxes(const PointTreeDev &T, float *__restric
         __threadfence_block();
         __syncthreads();
     }
-    if (T.n_levels <= kPtInBlockLevels) return;  // one workgroup: its level 4 is the root
+    if (T.n_levels <= kPtInBlockLevels || !ticket) return;  // one workgroup: its level 4 is the root
     __shared__ bool last;
     __threadfence();
     __syncthreads();
@@ -383,13 +396,7 @@ __device__ __forceinline__ void pt_boxes(const PointTreeDev &T, float *__restric
     __syncthreads();
     if (!last) return;
     __threadfence();  // agent-scope acquire: this CU's L1 holds no stale copy of the others' boxes
-    for (int l = kPtInBlockLevels + 1; l <= T.n_levels; ++l) {
-        const int64_t nl = lvl_size(n, l);
-        for (int64_t it = threadIdx.x; it < nl * T.d; it += blockDim.x)
-            pt_up_box(T, n, l, boxes, it / T.d, (int)(it % T.d));
-        __threadfence_block();
-        __syncthreads();
-    }
+    pt_top_boxes(T, boxes);
     if (threadIdx.x == 0) *ticket = 0u;
 }
 
@@ -400,16 +407,24 @@ __global__ __launch_bounds__(256) void k_pt_boxes(PointTreeDev T, float *__restr
 
 // ---- the same build for many trees at once (mpt_rrt_step_many): blockIdx.y = the tree; a
 // tree's keys / values live in shared buffers at its offset, sorted by one segmented sort
+// plan_launch: the code plans come from k_pt_plan_jobs (one workgroup per tree) instead of
+// each tree's last bbox workgroup, so no bbox workgroup takes the ticket and its agent-scope
+// fences (an L2 write-back and invalidate per workgroup on gfx950)
 template <int D>
 __global__ __launch_bounds__(256) void k_pt_bbox_jobs(const PtBuildJob *__restrict__ jobs, int32_t d,
-                                                      int32_t bbox_points_per_group) {
+                                                      int32_t bbox_points_per_group, int32_t plan_launch) {
     const PtBuildJob &J = jobs[blockIdx.y];
     // ~2048 points per workgroup (at most gridDim.x): 64 workgroups for every small tree cost
     // more in fences, atomics and tickets than the scan itself
     const int64_t per = bbox_points_per_group;
     const int64_t nblk = std::min<int64_t>(gridDim.x, std::max<int64_t>(1, (J.T.n_upper + per - 1) / per));
     if (blockIdx.x >= nblk) return;  // before the ticket: only the tree's own workgroups count
-    pt_bbox<D>(J.pts, d, J.T.n_upper, J.T.n_dev, J.bbox, J.ticket + 1, J.plan, J.sp, blockIdx.x, nblk);
+    pt_bbox<D>(J.pts, d, J.T.n_upper, J.T.n_dev, J.bbox, J.ticket + 1, plan_launch ? nullptr : J.plan, J.sp,
+               blockIdx.x, nblk);
+}
+__global__ __launch_bounds__(64) void k_pt_plan_jobs(const PtBuildJob *__restrict__ jobs, int32_t d) {
+    const PtBuildJob &J = jobs[blockIdx.x];
+    pt_plan(d, J.bbox, J.plan, J.sp);
 }
 template <int D>
 __global__ __launch_bounds__(256) void k_pt_morton_jobs(const PtBuildJob *__restrict__ jobs, int32_t d,
@@ -425,12 +440,19 @@ __global__ __launch_bounds__(256) void k_pt_gather_jobs(const PtBuildJob *__rest
     if ((int64_t)blockIdx.x * blockDim.x >= J.T.n_upper) return;
     pt_gather<D>(J.pts, d, J.T.n_upper, J.T.n_dev, vals_sorted + J.off, J.spts, J.sids, J.boxes, blockIdx.x);
 }
-__global__ __launch_bounds__(256) void k_pt_boxes_jobs(const PtBuildJob *__restrict__ jobs) {
+// top_launch: levels 5.. come from k_pt_top_jobs (one workgroup per tree) instead of each
+// tree's last group, so no group takes the ticket and its agent-scope fences
+__global__ __launch_bounds__(256) void k_pt_boxes_jobs(const PtBuildJob *__restrict__ jobs, int32_t top_launch) {
     const PtBuildJob &J = jobs[blockIdx.y];
     if (J.T.n_levels < 2) return;
     const int64_t groups = (J.T.n_upper + kPtChunkLeaves * kPtFan - 1) / (kPtChunkLeaves * kPtFan);
     if (blockIdx.x >= groups) return;  // before the ticket: only the tree's own groups count
-    pt_boxes(J.T, J.boxes, J.ticket, blockIdx.x, groups);
+    pt_boxes(J.T, J.boxes, top_launch ? nullptr : J.ticket, blockIdx.x, groups);
+}
+__global__ __launch_bounds__(256) void k_pt_top_jobs(const PtBuildJob *__restrict__ jobs) {
+    const PtBuildJob &J = jobs[blockIdx.x];
+    if (J.T.n_levels <= kPtInBlockLevels) return;
+    pt_top_boxes(J.T, J.boxes);
 }
 
 constexpr int kPtGroupsPerBlock = 256 / kPtFan;
@@ -797,8 +819,11 @@ void launch_tree_build_jobs(const PtBuildJob *d_jobs, const PtBuildJob *h_jobs, 
     static const bool fixed_d = !getenv("MPT_PT_FIXED_D") || atoi(getenv("MPT_PT_FIXED_D")) != 0;
     const int dd = fixed_d && (d == 3 || d == 7 || d == 15) ? d : 0;
     auto by_d = [&](auto k3, auto k7, auto k15, auto k0) { return dd == 3 ? k3 : dd == 7 ? k7 : dd == 15 ? k15 : k0; };
+    // MPT_PT_PLAN_JOBS=0: each tree's last bbox workgroup computes its plan (ticket + fences), A/B
+    static const bool plan_jobs = !getenv("MPT_PT_PLAN_JOBS") || atoi(getenv("MPT_PT_PLAN_JOBS")) != 0;
     hipLaunchKernelGGL(by_d(k_pt_bbox_jobs<3>, k_pt_bbox_jobs<7>, k_pt_bbox_jobs<15>, k_pt_bbox_jobs<0>), dim3(64, n),
-                       dim3(256), 0, stream, d_jobs, d, per);
+                       dim3(256), 0, stream, d_jobs, d, per, plan_jobs ? 1 : 0);
+    if (plan_jobs) hipLaunchKernelGGL(k_pt_plan_jobs, dim3(n), dim3(64), 0, stream, d_jobs, d);
     hipLaunchKernelGGL(by_d(k_pt_morton_jobs<3>, k_pt_morton_jobs<7>, k_pt_morton_jobs<15>, k_pt_morton_jobs<0>),
                        dim3(bx, n), dim3(256), 0, stream, d_jobs, d, S.keys, S.vals);
     hip_check(hipGetLastError(), "k_pt_morton_jobs");
@@ -808,7 +833,8 @@ void launch_tree_build_jobs(const PtBuildJob *d_jobs, const PtBuildJob *h_jobs, 
               "segmented sort");
     hipLaunchKernelGGL(by_d(k_pt_gather_jobs<3>, k_pt_gather_jobs<7>, k_pt_gather_jobs<15>, k_pt_gather_jobs<0>),
                        dim3(bx, n), dim3(256), 0, stream, d_jobs, d, S.vals_sorted);
-    hipLaunchKernelGGL(k_pt_boxes_jobs, dim3((unsigned)max_groups, n), dim3(256), 0, stream, d_jobs);
+    hipLaunchKernelGGL(k_pt_boxes_jobs, dim3((unsigned)max_groups, n), dim3(256), 0, stream, d_jobs, plan_jobs ? 1 : 0);
+    if (plan_jobs) hipLaunchKernelGGL(k_pt_top_jobs, dim3(n), dim3(256), 0, stream, d_jobs);
     hip_check(hipGetLastError(), "k_pt_boxes_jobs");
 }
 
