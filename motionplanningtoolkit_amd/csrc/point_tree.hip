@@ -464,7 +464,9 @@ __device__ __forceinline__ void tree_nn1_block(const PointTreeDev &T, const doub
                                                int32_t *__restrict__ out_ids, double *__restrict__ out_d2,
                                                int64_t blk) {
     __shared__ int32_t s_node[BS / kPtFan][kPtStack];
-    __shared__ double s_lb[BS / kPtFan][kPtStack];
+    // stacked lower bounds as floats rounded down (still lower bounds: pruning stays exact),
+    // half the LDS of doubles, so more one-wave workgroups fit a CU
+    __shared__ float s_lb[BS / kPtFan][kPtStack];
     const int64_t t = blk * BS + threadIdx.x;
     const int64_t slot = t / kPtFan;
     const int sub = (int)(t % kPtFan);
@@ -481,13 +483,13 @@ __device__ __forceinline__ void tree_nn1_block(const PointTreeDev &T, const doub
         int sp = 1;
         if (sub == 0) {
             s_node[grp][0] = T.n_levels << 27;  // the root: level n_levels, index 0
-            s_lb[grp][0] = 0.0;
+            s_lb[grp][0] = 0.0f;
         }
         __builtin_amdgcn_wave_barrier();
         while (sp > 0) {
             --sp;
             const int32_t code = s_node[grp][sp];
-            const double lbs = s_lb[grp][sp];
+            const double lbs = (double)s_lb[grp][sp];
             __builtin_amdgcn_wave_barrier();
             // the 1e-12 shrink covers FLANN's summation order (as the grid kernel)
             if (lbs * (1.0 - 1e-12) > bd) continue;
@@ -537,7 +539,7 @@ __device__ __forceinline__ void tree_nn1_block(const PointTreeDev &T, const doub
                 }
                 if (keep) {
                     s_node[grp][sp + rank] = ((lev - 1) << 27) | (int32_t)c;
-                    s_lb[grp][sp + rank] = lb2;
+                    s_lb[grp][sp + rank] = __double2float_rd(lb2);
                 }
                 sp += __popc(gm);
                 __builtin_amdgcn_wave_barrier();
@@ -571,7 +573,7 @@ __global__ __launch_bounds__(BS) void k_tree_nn1(PointTreeDev T, const double *_
 // dealt to XCDs: workgroup b runs on XCD b % 8, so job j takes the workgroups of XCD j % 8
 // and its tree stays in that XCD's L2.
 template <int D, int BS>
-__global__ __launch_bounds__(BS) void k_tree_nn1_jobs(const PtJob *__restrict__ jobs, int32_t n_jobs, int64_t nq,
+__global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(8))) void k_tree_nn1_jobs(const PtJob *__restrict__ jobs, int32_t n_jobs, int64_t nq,
                                                       int64_t blocks_per_job) {
     const int64_t xcd = blockIdx.x % kXcds, slot = blockIdx.x / kXcds;
     const int64_t job = xcd + kXcds * (slot / blocks_per_job);
