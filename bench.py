@@ -42,8 +42,8 @@ LDS_PEAK_GBS = 150_000.0  # MI355X_MICROARCH.md §LDS: ~150 TB/s aggregate ds_re
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=30)
+    ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--batch", type=int, default=65536, help="extensions per round (K)")
     ap.add_argument("--tree", type=int, default=100_000, help="tree nodes at the start of each round (N0)")
     ap.add_argument("--seed", type=int, default=1000)
