@@ -572,9 +572,10 @@ __global__ __launch_bounds__(BS) void k_tree_nn1(PointTreeDev T, const double *_
 // Many trees in one launch (mpt_rrt_step_many: one engine per independent seed).  Jobs are
 // dealt to XCDs: workgroup b runs on XCD b % 8, so job j takes the workgroups of XCD j % 8
 // and its tree stays in that XCD's L2.
+// 8 waves per SIMD for d <= 7 (56 VGPRs, no spill); d = 15 would spill at 8, so 4 (108 VGPRs)
 template <int D, int BS>
-__global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(8))) void k_tree_nn1_jobs(const PtJob *__restrict__ jobs, int32_t n_jobs, int64_t nq,
-                                                      int64_t blocks_per_job) {
+__global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(D >= 15 ? 4 : 8))) void k_tree_nn1_jobs(
+    const PtJob *__restrict__ jobs, int32_t n_jobs, int64_t nq, int64_t blocks_per_job) {
     const int64_t xcd = blockIdx.x % kXcds, slot = blockIdx.x / kXcds;
     const int64_t job = xcd + kXcds * (slot / blocks_per_job);
     if (job >= n_jobs) return;
