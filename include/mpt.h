@@ -200,9 +200,16 @@ mpt_status mpt_rrt_step(mpt_rrt *rrt, int32_t K, void *stream);
  * joint_stream: calls with different joint streams (from one or several host threads) may
  * overlap; calls on one joint stream are serialised.  Asynchronous. */
 mpt_status mpt_rrt_step_many(mpt_rrt *const *rrts, int32_t n, int32_t K, void *const *streams, void *joint_stream);
-/* Duration (ms, hipEvents on its joint stream) of the calling thread's last joint NN launch of
- * mpt_rrt_step_many that had an engine with timing enabled.  Synchronises on it. */
+/* Duration (ms, hipEvents) of the most recent timed joint NN launch on the joint stream of the
+ * calling thread's last timed mpt_rrt_step_many (joint state is per joint stream: if other
+ * threads share that stream, their later launch is the one reported; mpt_rrt_joint_times
+ * names the stream explicitly).  Synchronises on it. */
 mpt_status mpt_rrt_joint_nn_ms(float *ms);
+/* Release the joint state of joint_stream (job-table staging ring, events, shared sort
+ * buffers), after synchronising on it.  Call before destroying or recycling a stream handle
+ * that mpt_rrt_step_many used as its joint stream: a recycled handle would otherwise inherit
+ * the old state.  No-op for a stream that holds none. */
+mpt_status mpt_rrt_joint_release(void *joint_stream);
 /* The last timed mpt_rrt_step_many on joint_stream: ms[0] = the joint tree build, ms[1] = the
  * joint NN launch (hipEvents on joint_stream).  Synchronises on it. */
 mpt_status mpt_rrt_joint_times(void *joint_stream, float ms[2]);
@@ -224,7 +231,7 @@ mpt_status mpt_rrt_info(const mpt_rrt *rrt, int64_t info[4]);
 mpt_status mpt_rrt_enable_timing(mpt_rrt *rrt, int32_t enable);
 /* NN structure of the rounds: MPT_NN_AUTO / _BRUTE / _GRID / _TREE (packed Morton tree,
  * for trees that do not fill the sampling box), grid occupancy target (points per cell,
- * <= 0: the default, 2 points per cell with the cell side floored at 0.4x the expected NN
+ * <= 0: the default, 2 points per cell with the cell side floored at 0.3x the expected NN
  * distance over all state dims).  Results are identical. */
 mpt_status mpt_rrt_set_nn(mpt_rrt *rrt, int32_t mode, double points_per_cell);
 /* NN structure the last round used (MPT_NN_BRUTE / _GRID / _TREE; what MPT_NN_AUTO chose),

@@ -23,18 +23,20 @@ mpt_status mpt_host_load_mesh(const char *path, int32_t which, double *tris, int
 
 /* Planner <file.inst> (main.cpp) with RRT::query(start, goal, iterations_at_a_time) on the GPU
  * collision + NN path.  Outputs the tree edges in insertion order (root first):
- * starts/ends [n][dim] (written up to cap edges). */
-mpt_status mpt_host_rrt_inst(const char *inst_path, int32_t iterations_at_a_time, int64_t cap, double *starts,
-                             double *ends, int64_t *n_edges, int32_t *dim, int32_t *solved);
+ * starts/ends [n][dim], each a buffer of state_cap doubles, written up to min(cap, state_cap / dim)
+ * edges (dim is an output: size the buffers for the largest agent, 16 doubles a state). */
+mpt_status mpt_host_rrt_inst(const char *inst_path, int32_t iterations_at_a_time, int64_t cap, int64_t state_cap,
+                             double *starts, double *ends, int64_t *n_edges, int32_t *dim, int32_t *solved);
 
 /* Batched throughput mode of Planner <file.inst>: the file sets `Batch Size ? K` (and optionally
  * `Seed`, `Seed Count`, `Rounds`, `Max Tree Size`, `NN Index`; motionplanningtoolkit_amd/csrc/host/
  * compose.hpp run_batched); Seed Count trees grow from `Agent Start Location` on the device engine
  * (mpt_rrt_step / mpt_rrt_step_many).  out[4] = {rounds, extensions checked, extensions valid,
- * trees with a goal node}; *seconds = device wall time of the rounds; tree 0's states [n][dim]
- * and parents [n] are written up to cap nodes (either may be NULL), *tree0_nodes = n. */
-mpt_status mpt_host_rrt_batched(const char *inst_path, int64_t out[4], double *seconds, int64_t cap, double *tree0_states,
-                                int32_t *tree0_parents, int64_t *tree0_nodes, int32_t *dim);
+ * trees with a goal node}; *seconds = device wall time of the rounds; tree 0's parents [n] are
+ * written up to cap nodes and its states [n][dim] up to the min(cap, state_cap / dim) rows a
+ * buffer of state_cap doubles holds (either may be NULL), *tree0_nodes = n. */
+mpt_status mpt_host_rrt_batched(const char *inst_path, int64_t out[4], double *seconds, int64_t cap, int64_t state_cap,
+                                double *tree0_states, int32_t *tree0_parents, int64_t *tree0_nodes, int32_t *dim);
 
 /* PRM (planners/prm/prm.hpp) with the .inst's agent and workspace.
  * states != NULL: addMilestone for states[n][dim] in order, `batch` at a time (1 = the

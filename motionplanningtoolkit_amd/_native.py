@@ -66,6 +66,7 @@ SIGNATURES = {
     "mpt_rrt_step_many": (I32, [P, I32, I32, P, P]),
     "mpt_rrt_joint_nn_ms": (I32, [P]),
     "mpt_rrt_joint_times": (I32, [P, P]),
+    "mpt_rrt_joint_release": (I32, [P]),
     "mpt_rrt_counters": (I32, [P, P]),
     "mpt_rrt_read_tree": (I32, [P, P, P, I64]),
     "mpt_rrt_last_round": (I32, [P, P, P, P, P]),
@@ -79,8 +80,8 @@ SIGNATURES = {
     "mpt_rrt_kernel_times_sum": (I32, [P, P, P]),
     "mpt_host_last_error": (C.c_char_p, []),
     "mpt_host_load_mesh": (I32, [C.c_char_p, I32, P, I64, P, P]),
-    "mpt_host_rrt_inst": (I32, [C.c_char_p, I32, I64, P, P, P, P, P]),
-    "mpt_host_rrt_batched": (I32, [C.c_char_p, P, P, I64, P, P, P, P]),
+    "mpt_host_rrt_inst": (I32, [C.c_char_p, I32, I64, I64, P, P, P, P, P]),
+    "mpt_host_rrt_batched": (I32, [C.c_char_p, P, P, I64, I64, P, P, P, P]),
     "mpt_host_prm": (I32, [C.c_char_p, P, I64, I32, I32, I64, P, P, P, I64, P, P, P, P]),
     "mpt_host_grid_discretization": (I32, [C.c_char_p, P, I64, P, P, P]),
     "mpt_host_prmlite": (I32, [C.c_char_p, I32, D, P, I64, P, P]),

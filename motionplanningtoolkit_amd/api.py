@@ -394,6 +394,11 @@ def joint_times(joint_stream) -> dict:
     check(lib().mpt_rrt_joint_times(_stream(joint_stream), _p(ms)), "mpt_rrt_joint_times")
     return {"build": float(ms[0]), "nn": float(ms[1])}
 
+
+def joint_release(joint_stream) -> None:
+    """Free the joint state step_many keeps for joint_stream (call before the stream goes)."""
+    check(lib().mpt_rrt_joint_release(_stream(joint_stream)), "mpt_rrt_joint_release")
+
 def load_mesh(path: str, which: str = "all") -> np.ndarray:
     """AssimpMeshLoader replacement: 'all' submeshes (environment) or 'last' (agent)."""
     w = 1 if which == "last" else 0
@@ -459,7 +464,7 @@ def rrt_inst(path: str, iterations_at_a_time: int, cap: int = 1 << 16):
     solved = C.c_int32()
     starts = np.zeros(cap * 16)
     ends = np.zeros(cap * 16)
-    check(lib().mpt_host_rrt_inst(path.encode(), iterations_at_a_time, cap, _p(starts), _p(ends), C.byref(n),
+    check(lib().mpt_host_rrt_inst(path.encode(), iterations_at_a_time, cap, starts.size, _p(starts), _p(ends), C.byref(n),
                                   C.byref(dim), C.byref(solved)), "mpt_host_rrt_inst", host=True)
     d = dim.value
     m = min(n.value, cap)
@@ -475,8 +480,8 @@ def rrt_batched_inst(path: str, cap: int = 1 << 20) -> dict:
     dim = C.c_int32()
     states = np.zeros(cap * 16)
     parents = np.zeros(cap, np.int32)
-    check(lib().mpt_host_rrt_batched(path.encode(), _p(out), C.byref(secs), cap, _p(states), _p(parents), C.byref(n),
-                                     C.byref(dim)), "mpt_host_rrt_batched", host=True)
+    check(lib().mpt_host_rrt_batched(path.encode(), _p(out), C.byref(secs), cap, states.size, _p(states), _p(parents),
+                                     C.byref(n), C.byref(dim)), "mpt_host_rrt_batched", host=True)
     d, m = dim.value, min(n.value, cap)
     return {"rounds": int(out[0]), "checked": int(out[1]), "valid": int(out[2]), "solved_trees": int(out[3]),
             "seconds": secs.value, "tree0": (states[: m * d].reshape(m, d), parents[:m])}

@@ -452,7 +452,13 @@ MPT_HD double tri_distance(const v3 S[3], const double slo[3], const double shi[
 // first three of 33 bits: k * P_i exact for |k| < 2^20), r in double-double, sin r / cos r by
 // Horner over r^2 (Taylor to r^29 / r^28; the eight leading terms in double-double, the tail
 // in double), tan = sin / cos in double-double;
-// the double-double value (relative error < 2^-100) rounded to double.
+// the double-double value (relative error < 2^-100) rounded to double.  The contract is this
+// deterministic implementation, shared bit for bit with the oracle and correctly rounded on the
+// pinned argument set (tests/test_oracle.py, against libquadmath) -- not a proof of correct
+// rounding for every double.  Domain: |x| <= 2^20 (the reduction's k * P_i products are exact
+// for |k| < 2^20); beyond it the result is NaN, loudly, instead of a silently inexact value (the
+// engine's angles are normalised to [-pi, pi) and its tan arguments are clamped turn rates).
+constexpr double kCrMaxArg = 0x1p20;
 struct DD {
     double h, l;
 };
@@ -530,6 +536,7 @@ MPT_HD void cr_sincos_r(DD r, DD &s, DD &c) {
 }
 MPT_HD double cr_sin(double x) {
     if (x == 0.0 || !isfinite(x)) return x == 0.0 ? x : x - x;
+    if (fabs(x) > kCrMaxArg) return __builtin_nan("");
     DD r, s, c;
     const int q = cr_reduce(x, r);
     cr_sincos_r(r, s, c);
@@ -538,6 +545,7 @@ MPT_HD double cr_sin(double x) {
 }
 MPT_HD double cr_cos(double x) {
     if (!isfinite(x)) return x - x;
+    if (fabs(x) > kCrMaxArg) return __builtin_nan("");
     DD r, s, c;
     const int q = cr_reduce(x, r);
     cr_sincos_r(r, s, c);
@@ -546,8 +554,8 @@ MPT_HD double cr_cos(double x) {
 }
 // both at once (one reduction): the pose rotations need sin and cos of the same angle
 MPT_HD void cr_sincos(double x, double &sv, double &cv) {
-    if (!isfinite(x)) {
-        sv = cv = x - x;
+    if (!isfinite(x) || fabs(x) > kCrMaxArg) {
+        sv = cv = isfinite(x) ? __builtin_nan("") : x - x;
         return;
     }
     DD r, s, c;
@@ -559,6 +567,7 @@ MPT_HD void cr_sincos(double x, double &sv, double &cv) {
 }
 MPT_HD double cr_tan(double x) {
     if (x == 0.0 || !isfinite(x)) return x == 0.0 ? x : x - x;
+    if (fabs(x) > kCrMaxArg) return __builtin_nan("");
     DD r, s, c;
     const int q = cr_reduce(x, r);
     cr_sincos_r(r, s, c);

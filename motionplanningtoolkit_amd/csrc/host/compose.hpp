@@ -185,7 +185,9 @@ inline LiteResult run_prmlite_inst(const std::string &path, int32_t n_vertices, 
 //   Seed ? s                engine seed of the first tree (default 0)
 //   Seed Count ? n          independent trees, seeds s .. s + n - 1 (default 1), one
 //                           mpt_rrt_step_many round for all of them
-//   Rounds ? R              rounds to run (default: until Max Tree Size)
+//   Rounds ? R              rounds to run (default: until every tree holds Max Tree Size
+//                           nodes, checked every 8 rounds; a check window in which no tree
+//                           grew ends the run too, so a fully blocked start terminates)
 //   Max Tree Size ? N       nodes per tree (default 1 + R * K; 100 000 without Rounds)
 //   NN Index ? auto|brute|grid|tree   (default auto)
 // Every tree grows from `Agent Start Location`; a tree is solved when one of its nodes is a
@@ -245,13 +247,26 @@ BatchedResult run_batched(const InstanceFileMap &args) {
     BatchedResult r;
     r.dim = (int)d;
     const auto t0 = std::chrono::steady_clock::now();
-    const int64_t max_rounds = R > 0 ? R : (cap + K - 1) / K;
-    for (int64_t round = 0; round < max_rounds; ++round) {
+    constexpr int64_t kCheckEvery = 8;
+    uint64_t last_total = 0;
+    for (int64_t round = 0; R > 0 ? round < R : true; ++round) {
         if (n == 1)
             mpt_throw(mpt_rrt_step(rs[0], K, nullptr), "mpt_rrt_step");
         else
             mpt_throw(mpt_rrt_step_many(rs.data(), n, K, streams.data(), nullptr), "mpt_rrt_step_many");
         ++r.rounds;
+        if (R <= 0 && (round + 1) % kCheckEvery == 0) {  // until Max Tree Size (a sync per check)
+            uint64_t total = 0;
+            bool full = true;
+            for (int32_t i = 0; i < n; ++i) {
+                uint64_t c[8];
+                mpt_throw(mpt_rrt_counters(rs[i], c), "mpt_rrt_counters");
+                total += c[3];
+                full = full && (int64_t)c[3] >= cap;
+            }
+            if (full || total == last_total) break;
+            last_total = total;
+        }
     }
     mpt_throw(mpt_device_synchronize(), "mpt_device_synchronize");
     r.seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();

@@ -41,8 +41,8 @@ extern "C" mpt_status mpt_host_load_mesh(const char *path, int32_t which, double
 }
 
 extern "C" mpt_status mpt_host_rrt_inst(const char *inst_path, int32_t iterations_at_a_time, int64_t cap,
-                                        double *starts, double *ends, int64_t *n_edges, int32_t *dim,
-                                        int32_t *solved) {
+                                        int64_t state_cap, double *starts, double *ends, int64_t *n_edges,
+                                        int32_t *dim, int32_t *solved) {
     return hguard([&] {
         if (!inst_path || !n_edges) throw std::invalid_argument("null pointer");
         const auto r = mpt_host::run_inst(inst_path, iterations_at_a_time);
@@ -50,15 +50,16 @@ extern "C" mpt_status mpt_host_rrt_inst(const char *inst_path, int32_t iteration
         *n_edges = n;
         if (dim) *dim = r.dim;
         if (solved) *solved = r.solved ? 1 : 0;
-        const int64_t m = std::min<int64_t>(n, cap);
+        // rows that fit both the edge cap and the state buffers (state_cap doubles each)
+        const int64_t m = std::min<int64_t>(n, std::min<int64_t>(cap, r.dim ? state_cap / r.dim : 0));
         if (starts && m > 0) std::memcpy(starts, r.starts.data(), sizeof(double) * r.dim * m);
         if (ends && m > 0) std::memcpy(ends, r.ends.data(), sizeof(double) * r.dim * m);
     });
 }
 
 extern "C" mpt_status mpt_host_rrt_batched(const char *inst_path, int64_t out[4], double *seconds, int64_t cap,
-                                           double *tree0_states, int32_t *tree0_parents, int64_t *tree0_nodes,
-                                           int32_t *dim) {
+                                           int64_t state_cap, double *tree0_states, int32_t *tree0_parents,
+                                           int64_t *tree0_nodes, int32_t *dim) {
     return hguard([&] {
         if (!inst_path || !out) throw std::invalid_argument("null pointer");
         const auto r = mpt_host::run_batched_inst(inst_path);
@@ -72,8 +73,10 @@ extern "C" mpt_status mpt_host_rrt_batched(const char *inst_path, int64_t out[4]
         if (dim) *dim = r.dim;
         const int64_t n = r.nodes.empty() ? 0 : r.nodes[0];
         if (tree0_nodes) *tree0_nodes = n;
+        // parents: up to cap nodes; states: up to the rows state_cap doubles hold
         const int64_t m = std::min<int64_t>(n, cap);
-        if (tree0_states && m > 0) std::memcpy(tree0_states, r.first.data(), sizeof(double) * r.dim * m);
+        const int64_t ms = std::min<int64_t>(m, r.dim ? state_cap / r.dim : 0);
+        if (tree0_states && ms > 0) std::memcpy(tree0_states, r.first.data(), sizeof(double) * r.dim * ms);
         if (tree0_parents && m > 0) std::memcpy(tree0_parents, r.first_parents.data(), sizeof(int32_t) * m);
     });
 }
@@ -117,7 +120,7 @@ extern "C" mpt_status mpt_host_prmlite(const char *inst_path, int32_t n_vertices
     return hguard([&] {
         if (!inst_path || !n_edges || n_vertices < 0) throw std::invalid_argument("bad arguments");
         const auto r = mpt_host::run_prmlite_inst(inst_path, n_vertices, step);
-        if (verts) std::memcpy(verts, r.verts.data(), sizeof(double) * r.verts.size());
+        if (verts) std::memcpy(verts, r.verts.data(), sizeof(double) * std::min<size_t>(r.verts.size(), (size_t)n_vertices * 12));
         const int64_t ne = (int64_t)r.edges.size() / 2;
         *n_edges = ne;
         const int64_t m = std::min<int64_t>(ne, cap);

@@ -26,7 +26,6 @@
 #include "point_tree.h"
 #include "mpt_internal.h"
 #include "collide_common.h"
-#include "collide_common.h"
 
 namespace mpt {
 const EnvDev &env_dev(const mpt_env *e);
@@ -136,8 +135,6 @@ __device__ void snake_poses(const double *prm, int T, const double *s, double *o
     }
 }
 
-// n_dev[1] = n_dev[0]: the round's starting node count, read by k_append_commit (which
-// overwrites n_dev[0] in the same launch)
 // n_dev[1] = n_dev[0]: the round's starting node count, read by k_append_commit (which
 // overwrites n_dev[0] in the same launch)
 // set_n >= 0: a truncation left by mpt_rrt_set_size, applied first (k_set_n folded into the
@@ -1162,6 +1159,33 @@ extern "C" mpt_status mpt_rrt_joint_times(void *joint_stream, float ms[2]) {
         hip_check(hipEventSynchronize(g->t1), "event sync");
         hip_check(hipEventElapsedTime(&ms[0], g->b0, g->t0), "elapsed");
         hip_check(hipEventElapsedTime(&ms[1], g->t0, g->t1), "elapsed");
+    });
+}
+
+extern "C" mpt_status mpt_rrt_joint_release(void *joint_stream) {
+    return guarded([&] {
+        std::unique_ptr<JointNN> g;
+        {
+            std::lock_guard<std::mutex> lk(g_joints_mu);
+            const auto it = g_joints.find((hipStream_t)joint_stream);
+            if (it == g_joints.end()) return;
+            g = std::move(it->second);
+            g_joints.erase(it);
+        }
+        std::lock_guard<std::mutex> lk(g->mu);  // no step_many of this stream is staging
+        hip_check(hipStreamSynchronize((hipStream_t)joint_stream), "joint stream sync");
+        if (g_last_timed == g.get()) g_last_timed = nullptr;
+        if (g->d_stage) hip_check(hipFree(g->d_stage), "free");
+        for (int i = 0; i < kJobRing; ++i) {
+            if (g->h_stage[i]) hip_check(hipHostFree(g->h_stage[i]), "free");
+            if (g->copied[i]) hip_check(hipEventDestroy(g->copied[i]), "event");
+        }
+        for (hipEvent_t e : g->joins) hip_check(hipEventDestroy(e), "event");
+        for (hipEvent_t e : {g->done, g->built, g->b0, g->t0, g->t1})
+            if (e) hip_check(hipEventDestroy(e), "event");
+        JointTreeScratch &S = g->trees;
+        for (void *p : {(void *)S.keys, (void *)S.keys_sorted, (void *)S.vals, (void *)S.vals_sorted, S.temp})
+            if (p) hip_check(hipFree(p), "free");
     });
 }
 

@@ -783,8 +783,11 @@ static void cr_sincos_r(orc_dd r, orc_dd *s, orc_dd *c) {
     *s = dd_mul(r, cr_poly(CR_SIN, z));
     *c = cr_poly(CR_COS, z);
 }
+/* domain |x| <= 2^20 (the reduction is exact for |k| < 2^20): NaN beyond it, as fcl_math.h */
+#define ORC_CR_MAX_ARG 0x1p20
 double orc_cr_sin(double x) {
     if (x == 0.0 || !isfinite(x)) return x == 0.0 ? x : x - x;
+    if (fabs(x) > ORC_CR_MAX_ARG) return NAN;
     orc_dd r, s, c;
     const int q = cr_reduce(x, &r);
     cr_sincos_r(r, &s, &c);
@@ -793,6 +796,7 @@ double orc_cr_sin(double x) {
 }
 double orc_cr_cos(double x) {
     if (!isfinite(x)) return x - x;
+    if (fabs(x) > ORC_CR_MAX_ARG) return NAN;
     orc_dd r, s, c;
     const int q = cr_reduce(x, &r);
     cr_sincos_r(r, &s, &c);
@@ -801,6 +805,7 @@ double orc_cr_cos(double x) {
 }
 double orc_cr_tan(double x) {
     if (x == 0.0 || !isfinite(x)) return x == 0.0 ? x : x - x;
+    if (fabs(x) > ORC_CR_MAX_ARG) return NAN;
     orc_dd r, s, c;
     const int q = cr_reduce(x, &r);
     cr_sincos_r(r, &s, &c);

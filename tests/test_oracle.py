@@ -524,6 +524,11 @@ def test_cr_trig_is_correctly_rounded(oracle, quad_probe):
     # signed zeros
     assert math.copysign(1.0, oracle.cr_sin(-0.0)) < 0 and math.copysign(1.0, oracle.cr_tan(-0.0)) < 0
     assert oracle.cr_cos(-0.0) == 1.0
+    # the domain edge: exact up to 2^20, NaN (loud, not silently inexact) beyond it
+    assert np.array_equal(np.array([oracle.cr_sin(2.0 ** 20), oracle.cr_cos(-(2.0 ** 20))]).view(np.uint64),
+                          quad_probe([2.0 ** 20, -(2.0 ** 20)])[:, :2].diagonal().view(np.uint64))
+    for f in (oracle.cr_sin, oracle.cr_cos, oracle.cr_tan):
+        assert math.isnan(f(2.0 ** 20 + 1.0)) and math.isnan(f(-3e7))
     # glibc misrounds a fraction of these (documented in DESIGN.md; not asserted exactly:
     # it depends on the host's glibc build and CPU features)
     miss = (ref[:, 3:] != ref[:, :3]).sum(axis=0)
