@@ -54,12 +54,69 @@ void launch_tree_build_jobs(const PtBuildJob *d_jobs, const PtBuildJob *h_jobs, 
 // grows: call it before staging a round, not inside one).
 void reserve_tree_build_jobs(JointTreeScratch &S, int64_t total_cap, int32_t n_jobs);
 
+// ---- incremental index (the engine's rounds; FLANN_KDTreeWrapper::insertPoint,
+// utilities/flannkdtreewrapper.hpp:27-40, adds points to a live index instead of rebuilding it)
+//
+// Codes come from a plan fixed by the sampling ranges (not the live box), so a point's code
+// never changes and last round's sorted order stays valid: a round sorts only its new points
+// (<= kPtIncSeg, in LDS) and merges them into the sorted arrays (merge path, one pass over
+// the tree), then rebuilds the boxes.  The same sort orders the round's queries by code, so
+// the groups of a wave walk neighbouring paths.  A full rebuild (first round, after a
+// truncation or a bulk insert, or more new points than kPtIncSeg) sorts every code with
+// hipcub and runs the same merge with no old points.
+constexpr int kPtIncSeg = 8192;   // new points / queries one round sorts in LDS
+constexpr int kPtIncBits = 63;    // code bits (64-bit keys)
+struct IncPlan {
+    double lo[kPtMaxDim], scale[kPtMaxDim];
+    uint32_t qmax[kPtMaxDim];
+    int32_t n;                               // code bits used
+    int8_t dim[kPtIncBits], bit[kPtIncBits]; // MSB first
+};
+// the fixed plan of the ranges [lo, hi] (host): one quantisation step h for every dim, the
+// smallest for which the bits sum to <= 63 (<= 31 per dim), widest dims split first
+IncPlan make_inc_plan(int32_t d, const double *lo, const double *hi);
+
+struct PtIncJob {
+    PointTreeDev T;               // the tree after this build (T.pts / T.ids = the out arrays)
+    const double *pts;            // [n_upper][d] node rows
+    const IncPlan *plan;          // device
+    const uint64_t *okeys;        // last build's sorted codes / ids / rows (old points)
+    const int32_t *oids;
+    const double *opts;
+    uint64_t *keys;               // out: sorted codes, ids, rows
+    int32_t *ids;
+    double *spts;
+    float *boxes;
+    uint64_t *nkeys;              // the new points' sorted codes and rows
+    int32_t *nvals;
+    int64_t *nidx;                // points the last build indexed; set to n by this build
+    unsigned long long *ibox;     // persistent box of the indexed points (order keys)
+    const double *q;              // queries [nq][d] to order by code, or nullptr
+    int64_t nq;
+    int32_t *qorder;              // out: query indices in code order [nq]
+    int32_t full;                 // 1: nkeys / nvals hold every point (hipcub-sorted), no old points
+    SpreadOut sp;
+};
+// the incremental build of n trees of dim d (stream-ordered): sort, merge, box levels.
+// d_jobs / h_jobs: the same table on the device and the host (n == 1: d_jobs unused)
+void launch_tree_inc_jobs(const PtIncJob *d_jobs, const PtIncJob *h_jobs, int32_t n, int32_t d, hipStream_t stream);
+
 class PointTree {
 public:
     // the host part of build(): reserve, lay out the levels, and describe the device work as
     // a job of a joint build (launch_tree_build_jobs); dev() is valid once that has run
     PtBuildJob prepare(const double *pts, int64_t n_upper, const int64_t *n_dev, int32_t d, int64_t off,
                        const struct SpreadOut *spread);
+    // The incremental index: the job of this round's build (launch_tree_inc_jobs), dev()
+    // valid once it has run.  full: rebuild from every point (its code + sort launches are
+    // issued on `stream` here); else the points past the last build's count are merged in
+    // (at most kPtIncSeg of them: the caller's bound).  q / nq: the round's queries to order
+    // (nq <= kPtIncSeg), or nullptr.  lo / hi: the sampling ranges (the code plan).
+    PtIncJob prepare_inc(const double *pts, int64_t n_upper, const int64_t *n_dev, int32_t d, const double *lo,
+                         const double *hi, const double *q, int64_t nq, bool full, hipStream_t stream,
+                         const struct SpreadOut *spread);
+    // the query order of the last prepare_inc (nullptr: none)
+    const int32_t *query_order() const { return iq_on ? iqorder : nullptr; }
     ~PointTree();
     // Index rows [0, min(n_upper, *n_dev)) of pts [.][d]: bounding box and code plan on the
     // device, 30-bit codes over all dims, radix sort, boxes bottom-up.  Stream-ordered.
@@ -70,6 +127,8 @@ public:
     PointTreeDev dev() const { return t; }
     // allocate for up to n_upper points now (see GridIndex::reserve)
     void reserve(int64_t n_upper, int32_t d);
+    // the same for the incremental index (prepare_inc)
+    void inc_reserve(int64_t cap, int32_t d);
 
 private:
     PointTreeDev t{};
@@ -84,6 +143,23 @@ private:
     struct CodePlan *plan = nullptr;
     void *temp = nullptr;
     size_t temp_bytes = 0;
+    void reserve_boxes(int64_t n_upper, int32_t d);
+    // incremental index (prepare_inc): two sets of sorted arrays, `icur` the last build's
+    int64_t icap = 0;
+    int32_t idim = 0, icur = 0;
+    bool iq_on = false;
+    uint64_t *ikeys[2] = {nullptr, nullptr};
+    int32_t *iids[2] = {nullptr, nullptr};
+    double *ipts[2] = {nullptr, nullptr};
+    uint64_t *inkeys = nullptr;
+    int32_t *invals = nullptr, *iqorder = nullptr;
+    int64_t *inidx = nullptr;
+    unsigned long long *ibox = nullptr;
+    IncPlan *iplan = nullptr;
+    double iplan_lo[kPtMaxDim] = {}, iplan_hi[kPtMaxDim] = {};
+    bool iplan_set = false;
+    void *itemp = nullptr;
+    size_t itemp_bytes = 0;
 };
 
 // box level sizes for a layout bound: level l (1-based) has ceil(n / 8^l) boxes
@@ -103,11 +179,14 @@ struct PtJob {
     const double *q;
     int32_t *ids;
     double *d2;
+    const int32_t *order;  // query indices in code order (prepare_inc), or nullptr: sample order
 };
 constexpr int kXcds = 8;  // MI355X: workgroups are dealt round-robin over 8 XCDs
 // jobs: a device array [n_jobs], all trees of dim d, nq queries each
 void launch_tree_nn1_jobs(const PtJob *d_jobs, int32_t n_jobs, int32_t d, int64_t nq, hipStream_t stream);
-void launch_tree_nn1(const PointTreeDev &T, const double *q, int64_t nq, int32_t *ids, double *d2, hipStream_t stream);
+// order (optional): the queries' processing order (a permutation of [0, nq)); results by query index
+void launch_tree_nn1(const PointTreeDev &T, const double *q, int64_t nq, int32_t *ids, double *d2, hipStream_t stream,
+                     const int32_t *order = nullptr);
 // Radius search (d2 < r2) over 3-dim keys: offsets == nullptr -> counts[qi]; else fill ids /
 // d2 of query qi from offsets[qi] on (traversal order).  below_only: ids <= qi only.
 void launch_tree_radius(const PointTreeDev &T, const double *q, int64_t nq, double r2, bool below_only,

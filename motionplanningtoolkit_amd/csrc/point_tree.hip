@@ -455,6 +455,288 @@ __global__ __launch_bounds__(256) void k_pt_top_jobs(const PtBuildJob *__restric
     pt_top_boxes(J.T, J.boxes);
 }
 
+// ---- incremental index (point_tree.h PtIncJob) ----
+
+// the job table on the device (a joint build), or one job passed in the kernel arguments
+struct IncJobs {
+    const PtIncJob *table;
+    PtIncJob one;
+    __device__ __forceinline__ const PtIncJob &at(int k) const { return table ? table[k] : one; }
+};
+
+// the point's 64-bit code under the fixed plan (row loaded whole)
+template <int D>
+__device__ __forceinline__ uint64_t inc_code(const IncPlan *__restrict__ P, const double (&x)[D]) {
+    uint32_t q[D];
+#pragma unroll
+    for (int j = 0; j < D; ++j) {
+        const double u = (x[j] - P->lo[j]) * P->scale[j];
+        const uint32_t m = P->qmax[j];
+        q[j] = u <= 0.0 ? 0u : (u >= (double)m ? m : (uint32_t)u);
+    }
+    uint64_t c = 0;
+    const int32_t nb = P->n;
+    for (int k = 0; k < nb; ++k) {
+        const int32_t dk = P->dim[k];
+        uint32_t v = q[0];
+#pragma unroll
+        for (int j = 1; j < D; ++j)
+            if (j == dk) v = q[j];
+        c = (c << 1) | (uint64_t)((v >> P->bit[k]) & 1u);
+    }
+    return c;
+}
+
+__device__ __forceinline__ bool inc_less(uint64_t ka, int32_t va, uint64_t kb, int32_t vb) {
+    return ka < kb || (ka == kb && va < vb);
+}
+
+constexpr int kIncSortThreads = 1024;
+
+// blockIdx.x = 0: the tree's new points [nidx, n) -> codes, bitonic sort in LDS, nkeys / nvals
+// (and their box into ibox); blockIdx.x = 1: the round's queries -> code order (qorder).
+// (code, row) pairs order totally, so the result does not depend on the sort.
+template <int D>
+__global__ __launch_bounds__(kIncSortThreads) void k_pt_inc_sort(IncJobs jobs) {
+    __shared__ uint64_t sk[kPtIncSeg];
+    __shared__ int32_t sv[kPtIncSeg];
+    __shared__ unsigned long long s_min[kPtMaxDim], s_max[kPtMaxDim];
+    const PtIncJob &J = jobs.at(blockIdx.y);
+    const int seg = blockIdx.x;
+    const int t = threadIdx.x;
+    int64_t m = 0, base = 0;
+    const double *src = nullptr;
+    if (seg == 0) {
+        if (J.full) return;  // nkeys / nvals already hold every point
+        const int64_t nd = *J.T.n_dev, n = nd < J.T.n_upper ? nd : J.T.n_upper;
+        base = *J.nidx;
+        m = n - base;
+        m = m < 0 ? 0 : (m > kPtIncSeg ? kPtIncSeg : m);  // the caller bounds it (host grow count)
+        src = J.pts;
+    } else {
+        if (!J.q) return;
+        m = J.nq < kPtIncSeg ? J.nq : kPtIncSeg;
+        src = J.q;
+    }
+    if (m == 0) return;
+    int size = 2;
+    while (size < m) size <<= 1;
+    if (t < kPtMaxDim) {
+        s_min[t] = ~0ull;
+        s_max[t] = 0ull;
+    }
+    unsigned long long mn[D], mx[D];
+#pragma unroll
+    for (int j = 0; j < D; ++j) {
+        mn[j] = ~0ull;
+        mx[j] = 0ull;
+    }
+    for (int i = t; i < size; i += kIncSortThreads) {
+        if (i < m) {
+            double x[D];
+            const int64_t row = base + i;
+#pragma unroll
+            for (int j = 0; j < D; ++j) x[j] = src[row * D + j];
+            sk[i] = inc_code<D>(J.plan, x);
+            sv[i] = (int32_t)row;
+            if (seg == 0) {
+#pragma unroll
+                for (int j = 0; j < D; ++j) {
+                    const unsigned long long k = order_key_pt(x[j]);
+                    mn[j] = k < mn[j] ? k : mn[j];
+                    mx[j] = k > mx[j] ? k : mx[j];
+                }
+            }
+        } else {
+            sk[i] = ~0ull;  // real codes use 63 bits
+            sv[i] = 0x7fffffff;
+        }
+    }
+    __syncthreads();
+    if (seg == 0) {  // the persistent box of the indexed points (MPT_NN_AUTO's spread)
+#pragma unroll
+        for (int j = 0; j < D; ++j) {
+#pragma unroll
+            for (int off = 32; off > 0; off >>= 1) {
+                const unsigned long long omn = __shfl_xor(mn[j], off), omx = __shfl_xor(mx[j], off);
+                mn[j] = omn < mn[j] ? omn : mn[j];
+                mx[j] = omx > mx[j] ? omx : mx[j];
+            }
+            if ((t & 63) == 0) {
+                atomicMin(&s_min[j], mn[j]);
+                atomicMax(&s_max[j], mx[j]);
+            }
+        }
+    }
+    for (int k = 2; k <= size; k <<= 1) {
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            for (int i = t; i < size; i += kIncSortThreads) {
+                const int l = i ^ j;
+                if (l > i) {
+                    const uint64_t ka = sk[i], kb = sk[l];
+                    const int32_t va = sv[i], vb = sv[l];
+                    const bool up = (i & k) == 0;
+                    if (up ? inc_less(kb, vb, ka, va) : inc_less(ka, va, kb, vb)) {
+                        sk[i] = kb;
+                        sk[l] = ka;
+                        sv[i] = vb;
+                        sv[l] = va;
+                    }
+                }
+            }
+            __syncthreads();
+        }
+    }
+    if (seg == 0) {
+        for (int i = t; i < m; i += kIncSortThreads) {
+            J.nkeys[i] = sk[i];
+            J.nvals[i] = sv[i];
+        }
+        if (t < D) {
+            atomicMin(J.ibox + t, s_min[t]);
+            atomicMax(J.ibox + kPtMaxDim + t, s_max[t]);
+        }
+    } else {
+        for (int i = t; i < m; i += kIncSortThreads) J.qorder[i] = sv[i];
+    }
+}
+
+// number of a's among the first p elements of merge(a, b), an a before a b of the same key
+template <class K>
+__device__ __forceinline__ int64_t merge_split(const K *a, int64_t na, const K *b, int64_t nb, int64_t p) {
+    int64_t lo = p > nb ? p - nb : 0, hi = p < na ? p : na;
+    while (lo < hi) {
+        const int64_t mid = (lo + hi) >> 1;
+        if (a[mid] <= b[p - 1 - mid]) lo = mid + 1;
+        else hi = mid;
+    }
+    return lo;
+}
+
+constexpr int kIncTile = 256;  // merged outputs per workgroup (one per thread)
+
+// Merge path: workgroup g writes outputs [g * 256, + 256) of merge(old, new): its split of
+// the old / new arrays by two binary searches, the tile's keys staged in LDS, each thread's
+// source by a search of its diagonal there; the row and id copied from the old sorted arrays
+// or the node rows; the leaf boxes (8 consecutive outputs) by an 8-lane reduction.
+template <int D>
+__global__ __launch_bounds__(kIncTile) void k_pt_inc_merge(IncJobs jobs) {
+    __shared__ uint64_t sa[kIncTile], sb[kIncTile];
+    __shared__ int64_t s_split[2];
+    const PtIncJob &J = jobs.at(blockIdx.y);
+    const int64_t nd = *J.T.n_dev, n = nd < J.T.n_upper ? nd : J.T.n_upper;
+    const int64_t p0 = (int64_t)blockIdx.x * kIncTile;
+    if (p0 >= n) return;
+    const int64_t n_old = J.full ? 0 : *J.nidx;
+    int64_t m = n - n_old;
+    if (!J.full) m = m < 0 ? 0 : (m > kPtIncSeg ? kPtIncSeg : m);
+    const int64_t p1 = p0 + kIncTile < n ? p0 + kIncTile : n;
+    const int t = threadIdx.x;
+    if (t < 2) s_split[t] = merge_split(J.okeys, n_old, J.nkeys, m, t == 0 ? p0 : p1);
+    __syncthreads();
+    const int64_t i0 = s_split[0], i1 = s_split[1];
+    const int na = (int)(i1 - i0), nb = (int)((p1 - p0) - na);
+    const int64_t j0 = p0 - i0;
+    if (t < na) sa[t] = J.okeys[i0 + t];
+    if (t < nb) sb[t] = J.nkeys[j0 + t];
+    __syncthreads();
+    const int64_t p = p0 + t;
+    const bool live = p < p1;
+    double row[D];
+    int32_t id = 0;
+    uint64_t key = 0;
+    if (live) {
+        const int a = (int)merge_split(sa, na, sb, nb, t), b = t - a;
+        if (a < na && (b >= nb || sa[a] <= sb[b])) {
+            const int64_t s = i0 + a;
+            key = sa[a];
+            id = J.oids[s];
+#pragma unroll
+            for (int j = 0; j < D; ++j) row[j] = J.opts[s * D + j];
+        } else {
+            const int64_t r = J.nvals[j0 + b];
+            key = sb[b];
+            id = (int32_t)r + 1;
+#pragma unroll
+            for (int j = 0; j < D; ++j) row[j] = J.pts[r * D + j];
+        }
+        J.keys[p] = key;
+        J.ids[p] = id;
+#pragma unroll
+        for (int j = 0; j < D; ++j) J.spts[p * D + j] = row[j];
+    }
+#pragma unroll
+    for (int j = 0; j < D; ++j) {
+        double lo = live ? row[j] : __builtin_huge_val(), hi = live ? row[j] : -__builtin_huge_val();
+#pragma unroll
+        for (int off = kPtFan / 2; off > 0; off >>= 1) {
+            const double olo = __shfl_xor(lo, off, kPtFan), ohi = __shfl_xor(hi, off, kPtFan);
+            lo = olo < lo ? olo : lo;
+            hi = ohi > hi ? ohi : hi;
+        }
+        if (live && (p & (kPtFan - 1)) == 0) {
+            float *bx = J.boxes + (p / kPtFan) * 2 * D;
+            bx[j] = widen_lo(lo);
+            bx[D + j] = widen_hi(hi);
+        }
+    }
+}
+
+__global__ __launch_bounds__(256) void k_pt_inc_boxes(IncJobs jobs) {
+    const PtIncJob &J = jobs.at(blockIdx.y);
+    if (J.T.n_levels < 2) return;
+    const int64_t groups = (J.T.n_upper + kPtChunkLeaves * kPtFan - 1) / (kPtChunkLeaves * kPtFan);
+    if (blockIdx.x >= groups) return;
+    pt_boxes(J.T, J.boxes, nullptr, blockIdx.x, groups);
+}
+
+// levels 5.. (one workgroup per tree), then the indexed count and the spread feedback
+__global__ __launch_bounds__(256) void k_pt_inc_top(IncJobs jobs) {
+    const PtIncJob &J = jobs.at(blockIdx.x);
+    if (J.T.n_levels > kPtInBlockLevels) pt_top_boxes(J.T, J.boxes);
+    if (threadIdx.x != 0) return;
+    *J.nidx = live_n(J.T);
+    const SpreadOut &sp = J.sp;
+    if (sp.host_out) {
+        for (int j = 0; j < 3; ++j) {
+            sp.host_out[j] = j < sp.gd ? J.ibox[sp.dims[j]] : ~0ull;
+            sp.host_out[3 + j] = j < sp.gd ? J.ibox[kPtMaxDim + sp.dims[j]] : 0ull;
+        }
+        __threadfence_system();
+    }
+}
+
+// full rebuild: the box of every live point (from empty)
+__global__ __launch_bounds__(64) void k_pt_inc_box_reset(unsigned long long *__restrict__ box) {
+    if (threadIdx.x < 2 * kPtMaxDim) box[threadIdx.x] = threadIdx.x < kPtMaxDim ? ~0ull : 0ull;
+}
+template <int D>
+__global__ __launch_bounds__(256) void k_pt_inc_bbox(const double *__restrict__ pts, int32_t d, int64_t n_upper,
+                                                     const int64_t *__restrict__ n_dev,
+                                                     unsigned long long *__restrict__ box) {
+    pt_bbox<D>(pts, d, n_upper, n_dev, box, nullptr, nullptr, SpreadOut{}, blockIdx.x, gridDim.x);
+}
+
+// full rebuild: every point's code (rows past the live count sort to the end)
+template <int D>
+__global__ __launch_bounds__(256) void k_pt_inc_codes(const double *__restrict__ pts, int64_t n_upper,
+                                                      const int64_t *__restrict__ n_dev,
+                                                      const IncPlan *__restrict__ plan, uint64_t *__restrict__ keys,
+                                                      int32_t *__restrict__ vals) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n_upper) return;
+    const int64_t n = *n_dev < n_upper ? *n_dev : n_upper;
+    vals[i] = (int32_t)i;
+    if (i >= n) {
+        keys[i] = ~0ull;
+        return;
+    }
+    double x[D];
+#pragma unroll
+    for (int j = 0; j < D; ++j) x[j] = pts[i * D + j];
+    keys[i] = inc_code<D>(plan, x);
+}
+
 constexpr int kPtGroupsPerBlock = 256 / kPtFan;
 constexpr int kPtStack = kPtFan * kPtMaxLevels;
 
@@ -462,7 +744,7 @@ constexpr int kPtStack = kPtFan * kPtMaxLevels;
 template <int D, int BS>
 __device__ __forceinline__ void tree_nn1_block(const PointTreeDev &T, const double *__restrict__ q, int64_t nq,
                                                int32_t *__restrict__ out_ids, double *__restrict__ out_d2,
-                                               int64_t blk) {
+                                               int64_t blk, const int32_t *__restrict__ order) {
     __shared__ int32_t s_node[BS / kPtFan][kPtStack];
     // stacked lower bounds as floats rounded down (still lower bounds: pruning stays exact),
     // half the LDS of doubles, so more one-wave workgroups fit a CU
@@ -472,9 +754,12 @@ __device__ __forceinline__ void tree_nn1_block(const PointTreeDev &T, const doub
     const int sub = (int)(t % kPtFan);
     const int grp = threadIdx.x / kPtFan;
     if (slot >= nq) return;  // whole groups leave together
+    // the query this group answers: in code order (neighbouring groups walk neighbouring
+    // paths) when the build sorted the queries, else in sample order
+    const int64_t qi = order ? (int64_t)order[slot] : slot;
     double qq[D];
 #pragma unroll
-    for (int i = 0; i < D; ++i) qq[i] = q[slot * D + i];
+    for (int i = 0; i < D; ++i) qq[i] = q[qi * D + i];
     const int64_t n = live_n(T);
     double bd = __builtin_huge_val();
     int32_t bi = -1;
@@ -558,15 +843,16 @@ __device__ __forceinline__ void tree_nn1_block(const PointTreeDev &T, const doub
         }
     }
     if (sub == 0) {
-        out_ids[slot] = bi;
-        out_d2[slot] = bd;
+        out_ids[qi] = bi;
+        out_d2[qi] = bd;
     }
 }
 
 template <int D, int BS>
 __global__ __launch_bounds__(BS) void k_tree_nn1(PointTreeDev T, const double *__restrict__ q, int64_t nq,
-                                                 int32_t *__restrict__ out_ids, double *__restrict__ out_d2) {
-    tree_nn1_block<D, BS>(T, q, nq, out_ids, out_d2, blockIdx.x);
+                                                 int32_t *__restrict__ out_ids, double *__restrict__ out_d2,
+                                                 const int32_t *__restrict__ order) {
+    tree_nn1_block<D, BS>(T, q, nq, out_ids, out_d2, blockIdx.x, order);
 }
 
 // Many trees in one launch (mpt_rrt_step_many: one engine per independent seed).  Jobs are
@@ -580,7 +866,7 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(D >= 15 ? 4 
     const int64_t job = xcd + kXcds * (slot / blocks_per_job);
     if (job >= n_jobs) return;
     const PtJob &J = jobs[job];
-    tree_nn1_block<D, BS>(J.T, J.q, nq, J.ids, J.d2, slot % blocks_per_job);
+    tree_nn1_block<D, BS>(J.T, J.q, nq, J.ids, J.d2, slot % blocks_per_job, J.order);
 }
 
 // Radius search (FLANN_KDTreeWrapper::kNearestWithin, utilities/flannkdtreewrapper.hpp:91-117:
@@ -662,11 +948,13 @@ PointTree::~PointTree() {
     for (void *p : {(void *)keys, (void *)keys_sorted, (void *)vals, (void *)vals_sorted, (void *)sids, (void *)spts,
                     (void *)boxes, temp, (void *)bbox, (void *)plan})
         if (p) (void)hipFree(p);
+    for (void *p : {(void *)ikeys[0], (void *)ikeys[1], (void *)iids[0], (void *)iids[1], (void *)ipts[0],
+                    (void *)ipts[1], (void *)inkeys, (void *)invals, (void *)iqorder, itemp, (void *)inidx,
+                    (void *)ibox, (void *)iplan})
+        if (p) (void)hipFree(p);
 }
 
 void PointTree::reserve(int64_t n_upper, int32_t d) {
-    const int32_t L = pt_levels(n_upper);
-    const int64_t nb = lvl_off(n_upper, L + 1);
     if (n_upper > cap || d != dim) {
         for (void *p : {(void *)keys, (void *)keys_sorted, (void *)vals, (void *)vals_sorted, (void *)sids, (void *)spts})
             if (p) hip_check(hipFree(p), "free");
@@ -700,6 +988,11 @@ void PointTree::reserve(int64_t n_upper, int32_t d) {
         ticket = reinterpret_cast<unsigned int *>(bbox + 2 * kPtMaxDim);
         hip_check(hipMalloc(&plan, sizeof(CodePlan)), "pt plan");
     }
+    reserve_boxes(n_upper, d);
+}
+
+void PointTree::reserve_boxes(int64_t n_upper, int32_t d) {
+    const int64_t nb = lvl_off(n_upper, pt_levels(n_upper) + 1);
     if (nb * 2 * d > box_cap) {
         if (boxes) hip_check(hipFree(boxes), "free");
         box_cap = std::max<int64_t>(nb * 2 * d, 2 * box_cap);
@@ -841,6 +1134,172 @@ void launch_tree_build_jobs(const PtBuildJob *d_jobs, const PtBuildJob *h_jobs, 
     hip_check(hipGetLastError(), "k_pt_boxes_jobs");
 }
 
+IncPlan make_inc_plan(int32_t d, const double *lo, const double *hi) {
+    IncPlan P{};
+    double ext[kPtMaxDim] = {}, emax = 0.0;
+    for (int j = 0; j < d; ++j) {
+        ext[j] = hi[j] > lo[j] ? hi[j] - lo[j] : 0.0;
+        emax = std::max(emax, ext[j]);
+    }
+    auto bits_of = [&](int j, double h, int k) {
+        int b = 0;
+        while (b < k && std::ldexp(h, b) < ext[j]) ++b;
+        return b;
+    };
+    int kstar = 0;
+    for (int k = 1; emax > 0.0 && k <= 31; ++k) {
+        const double h = std::ldexp(emax, -k);
+        int tot = 0;
+        for (int j = 0; j < d; ++j) tot += bits_of(j, h, k);
+        if (tot > kPtIncBits) break;
+        kstar = k;
+    }
+    int b[kPtMaxDim] = {}, bmax = 0;
+    for (int j = 0; j < d; ++j) {
+        b[j] = kstar > 0 ? bits_of(j, std::ldexp(emax, -kstar), kstar) : 0;
+        bmax = std::max(bmax, b[j]);
+        P.lo[j] = lo[j];
+        P.qmax[j] = b[j] > 0 ? (uint32_t)((1ull << b[j]) - 1) : 0u;
+        P.scale[j] = b[j] > 0 ? std::ldexp(1.0, b[j]) / ext[j] : 0.0;
+    }
+    int n = 0;
+    for (int l = bmax - 1; l >= 0; --l)
+        for (int j = 0; j < d; ++j)
+            if (b[j] > l) {
+                P.dim[n] = (int8_t)j;
+                P.bit[n] = (int8_t)l;
+                ++n;
+            }
+    P.n = n;
+    return P;
+}
+
+void PointTree::inc_reserve(int64_t c, int32_t d) {
+    if (c <= icap && d == idim) return;
+    hip_check(hipDeviceSynchronize(), "sync");  // the old buffers may still be in use
+    for (void *p : {(void *)ikeys[0], (void *)ikeys[1], (void *)iids[0], (void *)iids[1], (void *)ipts[0],
+                    (void *)ipts[1], (void *)inkeys, (void *)invals, (void *)iqorder, itemp})
+        if (p) hip_check(hipFree(p), "free");
+    c = std::max<int64_t>(c, 1024);
+    for (int b = 0; b < 2; ++b) {
+        hip_check(hipMalloc(&ikeys[b], sizeof(uint64_t) * c), "inc keys");
+        hip_check(hipMalloc(&iids[b], sizeof(int32_t) * c), "inc ids");
+        hip_check(hipMalloc(&ipts[b], sizeof(double) * d * c), "inc points");
+    }
+    hip_check(hipMalloc(&inkeys, sizeof(uint64_t) * c), "inc new keys");
+    hip_check(hipMalloc(&invals, sizeof(int32_t) * c), "inc new rows");
+    hip_check(hipMalloc(&iqorder, sizeof(int32_t) * kPtIncSeg), "inc query order");
+    size_t tb = 0;
+    hip_check(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, ikeys[0], inkeys, iids[0], invals, (int)c, 0,
+                                                  kPtIncBits),
+              "inc sort size");
+    hip_check(hipMalloc(&itemp, tb), "inc sort temp");
+    itemp_bytes = tb;
+    if (!inidx) {
+        hip_check(hipMalloc(&inidx, sizeof(int64_t)), "inc count");
+        hip_check(hipMemset(inidx, 0, sizeof(int64_t)), "inc count zero");
+        hip_check(hipMalloc(&ibox, sizeof(unsigned long long) * 2 * kPtMaxDim), "inc box");
+        hip_check(hipMalloc(&iplan, sizeof(IncPlan)), "inc plan");
+        hip_check(hipDeviceSynchronize(), "inc init sync");  // null stream vs the caller's stream
+    }
+    icap = c;
+    idim = d;
+    icur = 0;
+}
+
+PtIncJob PointTree::prepare_inc(const double *pts, int64_t n_upper, const int64_t *n_dev, int32_t d, const double *lo,
+                                const double *hi, const double *q, int64_t nq, bool full, hipStream_t stream,
+                                const SpreadOut *spread) {
+    if (d != 3 && d != 7 && d != 15) throw Error{1, "point tree: state dim must be 3, 7 or 15"};
+    if (n_upper < 1 || n_upper >= (int64_t(1) << 27)) throw Error{1, "point tree: bad point count"};
+    if (n_upper > icap || d != idim) {
+        inc_reserve(n_upper, d);
+        full = true;
+    }
+    reserve_boxes(icap, d);
+    bool same = iplan_set;
+    for (int j = 0; j < d && same; ++j) same = iplan_lo[j] == lo[j] && iplan_hi[j] == hi[j];
+    if (!same) {
+        const IncPlan P = make_inc_plan(d, lo, hi);
+        hip_check(hipMemcpy(iplan, &P, sizeof(P), hipMemcpyHostToDevice), "inc plan");
+        for (int j = 0; j < d; ++j) {
+            iplan_lo[j] = lo[j];
+            iplan_hi[j] = hi[j];
+        }
+        iplan_set = true;
+        full = true;
+    }
+    const int old = icur, nw = icur ^ 1;
+    if (full) {
+        // every point: box, codes, one radix sort into the new-point arrays; the old arrays
+        // are scratch (the merge reads no old point)
+        hipLaunchKernelGGL(k_pt_inc_box_reset, dim3(1), dim3(64), 0, stream, ibox);
+        hipLaunchKernelGGL(d == 3 ? k_pt_inc_bbox<3> : d == 7 ? k_pt_inc_bbox<7> : k_pt_inc_bbox<15>, dim3(64),
+                           dim3(256), 0, stream, pts, d, n_upper, n_dev, ibox);
+        const unsigned blocks = (unsigned)((n_upper + 255) / 256);
+        hipLaunchKernelGGL(d == 3 ? k_pt_inc_codes<3> : d == 7 ? k_pt_inc_codes<7> : k_pt_inc_codes<15>, dim3(blocks),
+                           dim3(256), 0, stream, pts, n_upper, n_dev, (const IncPlan *)iplan, ikeys[old], iids[old]);
+        hip_check(hipGetLastError(), "k_pt_inc_codes");
+        size_t tb = itemp_bytes;
+        hip_check(hipcub::DeviceRadixSort::SortPairs(itemp, tb, ikeys[old], inkeys, iids[old], invals, (int)n_upper, 0,
+                                                      kPtIncBits, stream),
+                  "inc full sort");
+    }
+    t.d = d;
+    t.n_upper = n_upper;
+    t.n_levels = pt_levels(n_upper);
+    t.n_dev = n_dev;
+    t.boxes = boxes;
+    t.pts = ipts[nw];
+    t.ids = iids[nw];
+    icur = nw;
+    // MPT_PT_QSORT=1: the queries in code order.  Measured slower (config 5, 32 seeds: joint
+    // NN 2.02 -> 2.70 ms for the same points and boxes examined), so sample order is the default
+    static const bool qsort = getenv("MPT_PT_QSORT") && atoi(getenv("MPT_PT_QSORT")) == 1;
+    iq_on = qsort && q && nq > 0 && nq <= kPtIncSeg;
+    PtIncJob J{};
+    J.T = t;
+    J.pts = pts;
+    J.plan = iplan;
+    J.okeys = ikeys[old];
+    J.oids = iids[old];
+    J.opts = ipts[old];
+    J.keys = ikeys[nw];
+    J.ids = iids[nw];
+    J.spts = ipts[nw];
+    J.boxes = boxes;
+    J.nkeys = inkeys;
+    J.nvals = invals;
+    J.nidx = inidx;
+    J.ibox = ibox;
+    J.q = iq_on ? q : nullptr;
+    J.nq = iq_on ? nq : 0;
+    J.qorder = iqorder;
+    J.full = full ? 1 : 0;
+    if (spread) J.sp = *spread;
+    return J;
+}
+
+void launch_tree_inc_jobs(const PtIncJob *d_jobs, const PtIncJob *h_jobs, int32_t n, int32_t d, hipStream_t stream) {
+    if (n <= 0) return;
+    // one job: passed in the kernel arguments (no staged table)
+    IncJobs js{n == 1 ? nullptr : d_jobs, h_jobs[0]};
+    int64_t max_n = 0;
+    for (int32_t j = 0; j < n; ++j) max_n = std::max(max_n, h_jobs[j].T.n_upper);
+    auto by_d = [&](auto k3, auto k7, auto k15) { return d == 3 ? k3 : d == 7 ? k7 : k15; };
+    if (d != 3 && d != 7 && d != 15) throw Error{1, "point tree: state dim must be 3, 7 or 15"};
+    hipLaunchKernelGGL(by_d(k_pt_inc_sort<3>, k_pt_inc_sort<7>, k_pt_inc_sort<15>), dim3(2, n), dim3(kIncSortThreads),
+                       0, stream, js);
+    hip_check(hipGetLastError(), "k_pt_inc_sort");
+    hipLaunchKernelGGL(by_d(k_pt_inc_merge<3>, k_pt_inc_merge<7>, k_pt_inc_merge<15>),
+                       dim3((unsigned)((max_n + kIncTile - 1) / kIncTile), n), dim3(kIncTile), 0, stream, js);
+    hip_check(hipGetLastError(), "k_pt_inc_merge");
+    const int64_t groups = (max_n + kPtChunkLeaves * kPtFan - 1) / (kPtChunkLeaves * kPtFan);
+    hipLaunchKernelGGL(k_pt_inc_boxes, dim3((unsigned)groups, n), dim3(256), 0, stream, js);
+    hipLaunchKernelGGL(k_pt_inc_top, dim3(n), dim3(256), 0, stream, js);
+    hip_check(hipGetLastError(), "k_pt_inc_top");
+}
+
 void launch_tree_radius(const PointTreeDev &T, const double *q, int64_t nq, double r2, bool below_only,
                         int32_t *counts, const int64_t *offsets, int32_t *ids, double *d2, hipStream_t stream) {
     if (nq <= 0) return;
@@ -857,26 +1316,27 @@ void launch_tree_radius(const PointTreeDev &T, const double *q, int64_t nq, doub
 
 template <int BS>
 static void launch_tree_nn1_bs(const PointTreeDev &T, const double *q, int64_t nq, int32_t *ids, double *d2,
-                               hipStream_t stream) {
+                               hipStream_t stream, const int32_t *order) {
     const dim3 grid((unsigned)((nq * kPtFan + BS - 1) / BS));
     switch (T.d) {
-        case 3: hipLaunchKernelGGL((k_tree_nn1<3, BS>), grid, dim3(BS), 0, stream, T, q, nq, ids, d2); break;
-        case 7: hipLaunchKernelGGL((k_tree_nn1<7, BS>), grid, dim3(BS), 0, stream, T, q, nq, ids, d2); break;
-        case 15: hipLaunchKernelGGL((k_tree_nn1<15, BS>), grid, dim3(BS), 0, stream, T, q, nq, ids, d2); break;
+        case 3: hipLaunchKernelGGL((k_tree_nn1<3, BS>), grid, dim3(BS), 0, stream, T, q, nq, ids, d2, order); break;
+        case 7: hipLaunchKernelGGL((k_tree_nn1<7, BS>), grid, dim3(BS), 0, stream, T, q, nq, ids, d2, order); break;
+        case 15: hipLaunchKernelGGL((k_tree_nn1<15, BS>), grid, dim3(BS), 0, stream, T, q, nq, ids, d2, order); break;
         default: throw Error{1, "point tree: state dim must be 3, 7 or 15"};
     }
     hip_check(hipGetLastError(), "k_tree_nn1 launch");
 }
 
-void launch_tree_nn1(const PointTreeDev &T, const double *q, int64_t nq, int32_t *ids, double *d2, hipStream_t stream) {
+void launch_tree_nn1(const PointTreeDev &T, const double *q, int64_t nq, int32_t *ids, double *d2, hipStream_t stream,
+                     const int32_t *order) {
     if (nq <= 0) return;
     // one-wave workgroups spread an engine round's few thousand queries over all CUs
     // (MPT_PT_NN1_BLOCK=256: four waves per workgroup; A/B knob)
     static const int bs = getenv("MPT_PT_NN1_BLOCK") ? atoi(getenv("MPT_PT_NN1_BLOCK")) : 64;
     if (bs == 256)
-        launch_tree_nn1_bs<256>(T, q, nq, ids, d2, stream);
+        launch_tree_nn1_bs<256>(T, q, nq, ids, d2, stream, order);
     else
-        launch_tree_nn1_bs<64>(T, q, nq, ids, d2, stream);
+        launch_tree_nn1_bs<64>(T, q, nq, ids, d2, stream, order);
 }
 
 void launch_tree_nn1_jobs(const PtJob *d_jobs, int32_t n_jobs, int32_t d, int64_t nq, hipStream_t stream) {

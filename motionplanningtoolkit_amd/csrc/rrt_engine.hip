@@ -517,6 +517,10 @@ struct mpt_rrt {
     // mpt_rrt_set_size's node count, applied by the next round's k_sample (or by flush_size
     // before the host reads the count); -1: none
     int64_t pending_n = -1;
+    // incremental Morton tree (point_tree.h prepare_inc): valid while nodes are only appended
+    // since its last build; pt_grow bounds the nodes appended since then (the K of each round)
+    bool pt_inc_ok = false;
+    int64_t pt_grow = 0;
 };
 
 namespace {
@@ -684,6 +688,7 @@ extern "C" mpt_status mpt_rrt_add_nodes(mpt_rrt *r, const double *states, const 
         hip_check(hipDeviceSynchronize(), "sync");
         r->n_upper = nn;
         r->spread_seen = false;  // bulk nodes: re-read the spread at the next index build
+        r->pt_inc_ok = false;
     });
 }
 
@@ -696,6 +701,7 @@ extern "C" mpt_status mpt_rrt_set_size(mpt_rrt *r, int64_t n, void *stream) {
         (void)stream;
         r->pending_n = n;
         r->n_upper = n;
+        r->pt_inc_ok = false;  // the index may hold truncated nodes
     });
 }
 
@@ -714,6 +720,25 @@ struct StepCtx {
         if (ev) hip_check(hipEventRecord(ev[i], stream), "event record");
     }
 };
+
+// the Morton-tree NN index is updated incrementally (MPT_PT_INC=0: rebuilt from scratch every
+// round with the live box's code plan, A/B)
+bool tree_incremental() {
+    static const bool inc = !getenv("MPT_PT_INC") || atoi(getenv("MPT_PT_INC")) != 0;
+    return inc;
+}
+
+// this round's incremental tree build (a full rebuild when the index is stale or more nodes
+// were appended since its last build than one round's sort holds); the queries (the round's
+// samples) are ordered by code for the NN launch
+PtIncJob tree_inc_job(mpt_rrt *r, int32_t K, hipStream_t stream, const SpreadOut *spread) {
+    const bool full = !r->pt_inc_ok || r->pt_grow > kPtIncSeg;
+    PtIncJob J = r->ptree->prepare_inc(r->d_nodes, r->n_upper, r->d_n, r->p.d, r->p.lo, r->p.hi, r->d_samples, K,
+                                       full, stream, spread);
+    r->pt_inc_ok = true;
+    r->pt_grow = 0;
+    return J;
+}
 
 StepCtx step_head(mpt_rrt *r, int32_t K, hipStream_t stream, bool defer_tree = false) {
     StepCtx c;
@@ -809,11 +834,16 @@ StepCtx step_head(mpt_rrt *r, int32_t K, hipStream_t stream, bool defer_tree = f
         spread.host_out = r->h_spread_dev;
     }
     if (use_tree) {
-        r->ptree->reserve(r->cap, p.d);  // once: no allocation (device sync) in later rounds
+        // once: no allocation (device sync) in later rounds
+        if (tree_incremental()) r->ptree->inc_reserve(r->cap, p.d);
+        else r->ptree->reserve(r->cap, p.d);
         if (defer_tree) {
             c.defer_tree = true;
             c.want_spread = want_spread;
             c.spread = spread;
+        } else if (tree_incremental()) {
+            PtIncJob J = tree_inc_job(r, K, stream, want_spread ? &spread : nullptr);
+            launch_tree_inc_jobs(nullptr, &J, 1, p.d, stream);
         } else {
             r->ptree->build(r->d_nodes, r->n_upper, r->d_n, p.d, stream, want_spread ? &spread : nullptr);
         }
@@ -869,8 +899,13 @@ StepCtx step_head(mpt_rrt *r, int32_t K, hipStream_t stream, bool defer_tree = f
 }
 
 // a deferred tree build that did not join a joint build: run it on the engine's stream
-void build_deferred(mpt_rrt *r, hipStream_t stream, const StepCtx &c) {
-    r->ptree->build(r->d_nodes, r->n_upper, r->d_n, r->p.d, stream, c.want_spread ? &c.spread : nullptr);
+void build_deferred(mpt_rrt *r, int32_t K, hipStream_t stream, const StepCtx &c) {
+    if (tree_incremental()) {
+        PtIncJob J = tree_inc_job(r, K, stream, c.want_spread ? &c.spread : nullptr);
+        launch_tree_inc_jobs(nullptr, &J, 1, r->p.d, stream);
+    } else {
+        r->ptree->build(r->d_nodes, r->n_upper, r->d_n, r->p.d, stream, c.want_spread ? &c.spread : nullptr);
+    }
     if (c.want_spread) hip_check(hipEventRecord(r->ev_spread, stream), "spread event");
     c.mark(2, stream);
 }
@@ -881,7 +916,8 @@ void step_nn(mpt_rrt *r, int32_t K, hipStream_t stream, const StepCtx &c) {
     if (use_tree) {
         PointTreeDev T = r->ptree->dev();
         T.stats = r->stats_on ? r->d_cstats + 8 : nullptr;
-        launch_tree_nn1(T, r->d_samples, K, r->d_nn, r->d_nnd2, stream);
+        launch_tree_nn1(T, r->d_samples, K, r->d_nn, r->d_nnd2, stream,
+                        tree_incremental() ? r->ptree->query_order() : nullptr);
     } else if (use_grid) {
         GridDev G = r->grid->dev();
         G.stats = r->stats_on ? r->d_cstats + 8 : nullptr;
@@ -952,6 +988,7 @@ void step_tail(mpt_rrt *r, int32_t K, hipStream_t stream, const StepCtx &c) {
     c.mark(9, stream);
     r->ext_base += (uint64_t)K;
     r->n_upper = std::min<int64_t>(r->cap, r->n_upper + K);
+    r->pt_grow += K;
     r->last_K = K;
 }
 
@@ -1053,38 +1090,27 @@ extern "C" mpt_status mpt_rrt_step_many(mpt_rrt *const *rs, int32_t n, int32_t K
         std::vector<char> joined(n, 0);
         for (int32_t i : J) joined[i] = 1;
         for (int32_t i = 0; i < n; ++i)
-            if (cs[i].defer_tree && !joined[i]) build_deferred(rs[i], stream_of(i), cs[i]);
+            if (cs[i].defer_tree && !joined[i]) build_deferred(rs[i], K, stream_of(i), cs[i]);
         if (!J.empty()) {
             JointNN &g = joint_state(joint);
             std::lock_guard<std::mutex> lk(g.mu);
             const int32_t nj = (int32_t)J.size();
+            const bool inc = tree_incremental();
             // the shared sort buffers sized for the joined trees' capacities once, so no later
             // round allocates (an allocation synchronises the device and stalls every stream)
             int64_t cap_total = 0;
             for (int32_t i : J) cap_total += rs[i]->cap;
-            reserve_tree_build_jobs(g.trees, cap_total, nj);
-            const size_t b_build = sizeof(PtBuildJob) * nj, b_nn = sizeof(PtJob) * nj;
+            if (!inc) reserve_tree_build_jobs(g.trees, cap_total, nj);
+            const size_t b_build = (inc ? sizeof(PtIncJob) : sizeof(PtBuildJob)) * nj, b_nn = sizeof(PtJob) * nj;
             const size_t b_off = sizeof(int32_t) * (nj + 1);
             int slot = 0;
             char *h = joint_stage(g, b_build + b_nn + b_off, &slot);
             PtBuildJob *hb = reinterpret_cast<PtBuildJob *>(h);
+            PtIncJob *hi = reinterpret_cast<PtIncJob *>(h);
             PtJob *hn = reinterpret_cast<PtJob *>(h + b_build);
             int32_t *ho = reinterpret_cast<int32_t *>(h + b_build + b_nn);
-            int64_t total = 0;
-            for (int32_t k = 0; k < nj; ++k) {
-                mpt_rrt *r = rs[J[k]];
-                const StepCtx &c = cs[J[k]];
-                ho[k] = (int32_t)total;
-                hb[k] = r->ptree->prepare(r->d_nodes, r->n_upper, r->d_n, r->p.d, total,
-                                          c.want_spread ? &c.spread : nullptr);
-                total += r->n_upper;
-                if (total >= (int64_t(1) << 31)) throw Error{MPT_ERR_INVALID, "joint build: too many points"};
-                PointTreeDev T = r->ptree->dev();
-                T.stats = r->stats_on ? r->d_cstats + 8 : nullptr;
-                hn[k] = PtJob{T, r->d_samples, r->d_nn, r->d_nnd2};
-            }
-            ho[nj] = (int32_t)total;
             // the joint stream waits for every engine stream's heads, the engines' tails for it
+            // (before the builds: a full incremental rebuild issues its launches here)
             std::vector<hipStream_t> uniq;
             for (int32_t i : J)
                 if (std::find(uniq.begin(), uniq.end(), stream_of(i)) == uniq.end()) uniq.push_back(stream_of(i));
@@ -1097,11 +1123,6 @@ extern "C" mpt_status mpt_rrt_step_many(mpt_rrt *const *rs, int32_t n, int32_t K
                 hip_check(hipEventRecord(g.joins[u], uniq[u]), "join record");
                 hip_check(hipStreamWaitEvent(joint, g.joins[u], 0), "join wait");
             }
-            hip_check(hipMemcpyAsync(g.d_stage, h, b_build + b_nn + b_off, hipMemcpyHostToDevice, joint), "jobs H2D");
-            hip_check(hipEventRecord(g.copied[slot], joint), "jobs copied");
-            const PtBuildJob *db = reinterpret_cast<const PtBuildJob *>(g.d_stage);
-            const PtJob *dn = reinterpret_cast<const PtJob *>(g.d_stage + b_build);
-            const int32_t *doff = reinterpret_cast<const int32_t *>(g.d_stage + b_build + b_nn);
             bool timed = false;
             for (int32_t i : J) timed = timed || rs[i]->timing;
             if (timed) {
@@ -1112,7 +1133,29 @@ extern "C" mpt_status mpt_rrt_step_many(mpt_rrt *const *rs, int32_t n, int32_t K
                 }
                 hip_check(hipEventRecord(g.b0, joint), "joint b0");
             }
-            launch_tree_build_jobs(db, hb, nj, rs[J[0]]->p.d, doff, total, g.trees, joint);
+            int64_t total = 0;
+            for (int32_t k = 0; k < nj; ++k) {
+                mpt_rrt *r = rs[J[k]];
+                const StepCtx &c = cs[J[k]];
+                ho[k] = (int32_t)total;
+                const SpreadOut *sp = c.want_spread ? &c.spread : nullptr;
+                if (inc) hi[k] = tree_inc_job(r, K, joint, sp);
+                else hb[k] = r->ptree->prepare(r->d_nodes, r->n_upper, r->d_n, r->p.d, total, sp);
+                total += r->n_upper;
+                if (total >= (int64_t(1) << 31)) throw Error{MPT_ERR_INVALID, "joint build: too many points"};
+                PointTreeDev T = r->ptree->dev();
+                T.stats = r->stats_on ? r->d_cstats + 8 : nullptr;
+                hn[k] = PtJob{T, r->d_samples, r->d_nn, r->d_nnd2, inc ? r->ptree->query_order() : nullptr};
+            }
+            ho[nj] = (int32_t)total;
+            hip_check(hipMemcpyAsync(g.d_stage, h, b_build + b_nn + b_off, hipMemcpyHostToDevice, joint), "jobs H2D");
+            hip_check(hipEventRecord(g.copied[slot], joint), "jobs copied");
+            const PtBuildJob *db = reinterpret_cast<const PtBuildJob *>(g.d_stage);
+            const PtIncJob *di = reinterpret_cast<const PtIncJob *>(g.d_stage);
+            const PtJob *dn = reinterpret_cast<const PtJob *>(g.d_stage + b_build);
+            const int32_t *doff = reinterpret_cast<const int32_t *>(g.d_stage + b_build + b_nn);
+            if (inc) launch_tree_inc_jobs(di, hi, nj, rs[J[0]]->p.d, joint);
+            else launch_tree_build_jobs(db, hb, nj, rs[J[0]]->p.d, doff, total, g.trees, joint);
             for (int32_t i : J)
                 if (cs[i].want_spread) hip_check(hipEventRecord(rs[i]->ev_spread, joint), "spread event");
             if (timed) {

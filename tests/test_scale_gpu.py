@@ -172,3 +172,59 @@ def test_config4_rooms_collide_batch(mpt_gpu, oracle):
                                        nthreads=THREADS)
         assert np.array_equal(got, ref), mode
         assert 0.05 < got.mean() < 0.95
+
+
+def test_config5_shard_shape(mpt_gpu, oracle):
+    """Config 5 at one GPU's shard (BASELINE config 5: 256 seeds, 32 per GPU): 32 blimp seeds
+    from wall starts (bench.py --seed-start walls), 4096 extensions per seed per round, 30
+    rounds through mpt_rrt_step_many (one joint Morton-tree build + NN launch per round; the
+    trees reach ~110k nodes and the index is updated incrementally), exactly as bench.py
+    --seeds 32 runs them.  Three seeds' trees are then grown by the oracle's engine rounds
+    (orc_engine_step: kd-tree NN, correctly rounded steering trig, AABB-tree + FCL SAT; the
+    reference's RRT::query loop, planners/rrt.hpp:42-94, batched) from the same starts and
+    must equal the device's node for node, states and parents bitwise."""
+    import sys
+
+    import torch
+
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+
+    sc = scenes.blimp_scenario("all")
+    env = mpt_gpu.Environment(sc.env_tris, sc.env_tf)
+    ag = mpt_gpu.AgentMesh(sc.agent_tris)
+    K, rounds, base = 4096, 30, 1000
+    seeds = [base + i for i in range(32)]
+    starts = {s: bench.seed_start(s, env, ag, mpt_gpu, "walls") for s in seeds}
+    engs = []
+    for s in seeds:
+        e = mpt_gpu.RRTEngine(env, ag, sc.kind, sc.prm, sc.ranges, sc.steer_dt, sc.cc_dt, 1 + rounds * K, s)
+        e.add_nodes(starts[s])
+        e.set_nn("auto")
+        engs.append(e)
+    streams = [torch.cuda.Stream() for _ in range(8)]
+    joint = torch.cuda.Stream()
+    for _ in range(rounds):
+        mpt_gpu.step_many(engs, K, [streams[j % 8] for j in range(len(engs))], joint)
+    torch.cuda.synchronize()
+    got = {}
+    for s, e in zip(seeds, engs):
+        assert e.last_nn() == "tree"
+        got[s] = e.read_tree(e.counters()["nodes"])
+        e.close()
+    mpt_gpu.joint_release(joint)
+    sizes = [len(got[s][0]) for s in seeds]
+    assert min(sizes) > 60_000, sizes
+    bvh = oracle.BVH(sc.env_tris)
+    for s in (seeds[0], seeds[13], seeds[31]):
+        ref = np.zeros((1 + rounds * K, sc.dim))
+        ref[0] = starts[s][0]
+        par = np.zeros(1 + rounds * K, np.int32)
+        n = 1
+        for r in range(rounds):
+            n, _, _ = oracle.engine_step(sc.kind, sc.prm, sc.ranges, sc.steer_dt, sc.cc_dt, s, r * K, K, bvh,
+                                         sc.env_tf, sc.agent_tris, ref, par, n, nthreads=THREADS)
+        st, pa = got[s]
+        assert n == len(st)
+        assert np.array_equal(st.view(np.uint64), ref[:n].view(np.uint64))
+        assert np.array_equal(pa, par[:n])
