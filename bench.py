@@ -67,7 +67,10 @@ def parse():
     ap.add_argument("--seed-start", default="walls", choices=["walls", "centre"],
                     help="config 5: start each seed near a wall of the room (default, so trees reach the walls "
                          "and collide) or at the room's centre")
-    ap.add_argument("--streams", type=int, default=32, help="config 5: HIP streams the seeds' rounds rotate over")
+    ap.add_argument("--streams", type=int, default=0,
+                    help="config 5: HIP streams the seeds' per-engine rounds rotate over (0, the default: every engine "
+                         "on its group's joint stream -- a joint round then joins no other stream; 32 streams cost "
+                         "~0.45 ms a round of event joins at 32 seeds)")
     ap.add_argument("--no-joint-nn", action="store_true",
                     help="config 5: each seed builds and queries its own tree (default: one joint build and one "
                          "joint NN launch per round, mpt_rrt_step_many)")
@@ -189,7 +192,18 @@ def geometry(sc, env):
     triangles each, mpt_agent_create), env tree items (one per triangle + buckets of <= 16)."""
     te = int(env.info()["triangles"])
     ta = int(sc.agent_tris.shape[0])
-    return {"env_tris": te, "agent_tris": ta, "clusters": max(1, -(-ta // 64)), "env_items": te + -(-te // 8)}
+    return {"env_tris": te, "agent_tris": ta, "clusters": max(1, -(-ta // 64)), "env_items": te + -(-te // 8),
+            "links": int(getattr(sc, "links", 1) or 1)}
+
+
+def inc_build_bytes(n, m, d):
+    """The incremental Morton-tree build of trees holding n points in total after it, m of them
+    new this round (point_tree.hip): the sort reads the new rows and writes their (code, row)
+    pairs; the merge reads the old sorted (code, id, row) records and the new pairs and rows,
+    and writes n sorted records and the leaf boxes; the box levels above read and write the
+    boxes (about n / 7 boxes of 2d floats in all)."""
+    rec = 8 + 4 + 8 * d
+    return m * (8 * d + 12) + (n - m) * rec + m * (12 + 8 * d) + n * rec + (n // 7) * 8 * d * 2
 
 
 def compulsory_bytes(stage, c, K, n0, d, pmax, geo, nn_mode):
@@ -200,14 +214,17 @@ def compulsory_bytes(stage, c, K, n0, d, pmax, geo, nn_mode):
     if stage == "sample":
         return K * 8 * d
     if stage == "nn_build":
-        if nn_mode == "tree":  # read the nodes; codes, ids, sorted points, boxes
-            return n0 * (8 * d + 8 + 8 * d + 4) + (n0 // 7) * 8 * d
+        if nn_mode == "tree":  # the incremental build (one round's K new points)
+            return inc_build_bytes(n0, min(K, n0), d)
         return n0 * (8 * d + rec + 8) + (n0 // 2) * 12  # nodes in, records out, cell ids, counts / starts
     if stage == "nn_query":
         index = n0 * rec + (n0 // 2) * 4 if nn_mode == "grid" else n0 * (8 * d + 4) + (n0 // 7) * 8 * d
         return K * (8 * d + 12) + index
-    if stage == "steer":  # ids, neighbour rows, end states, poses, counts, verdict init, live list
-        return K * (4 + 8 * d + 8 * d + 4 + 1) + K * pmax * 96 + live * 4
+    if stage == "steer":
+        # ids, neighbour rows, end states, counts, verdict init; every (pose, link) unit's pose
+        # and its FCL relative transform (96 B each, k_steer writes both); the live list
+        units = K * pmax * geo.get("links", 1)
+        return K * (4 + 8 * d + 8 * d + 4 + 1) + units * 96 * 2 + live * 4
     if stage == "collide_pairs":  # live poses, clusters, env tree, pair words, headers
         return live * 96 + geo["clusters"] * 64 + geo["env_items"] * 32 + c["pair_tests"] * 4 + c["cluster_transforms"] * 32
     if stage == "collide_cands":  # headers, pair words, poses, agent triangles, env boxes, candidates
@@ -257,14 +274,15 @@ def touched_bytes(stage, c, K, n0, d, pmax):
 
 # workload -> the subdirectory of profiles/r*/ that holds its own PMC summary (the same kernel
 # names move different bytes in each workload)
-PMC_SUBDIR = {"blimp": "", "blimp-room": "room", "snake": "snake", "seeds": "c5"}
+PMC_SUBDIR = {"blimp": "", "blimp-room": "room", "snake": "snake"}
 
 
 def pmc_summary(path, workload="blimp"):
     if not path:
         import glob
 
-        sub = PMC_SUBDIR.get(workload, "")
+        # config 5: the summary profiled at the same seed count (profiles/r*/c5_<seeds>/)
+        sub = f"c5_{workload[5:]}" if workload.startswith("seeds") else PMC_SUBDIR.get(workload, "")
         cands = sorted(glob.glob(os.path.join(REPO, "profiles", "r[0-9][0-9]", sub, "pmc_summary.json")))
         path = cands[-1] if cands else None
     try:
@@ -306,6 +324,57 @@ def stage_table(per_launch, cst, K, n0, d, pmax, geo, nn_mode, kernels, summ):
         tb = touched_bytes(s, cst, K, n0, d, pmax)
         if tb is not None:
             st["touched_bytes"] = int(tb)
+        stages[s] = st
+    return stages
+
+
+# config 5's joint round: stage -> the kernels of its launch chain (rocprofv3 names), whose
+# measured traffic per launch is summed (the collide chain runs once per collide sub-batch)
+JOINT_STAGE_KERNELS = {
+    "sample": ["k_sample_jobs"],
+    "nn_build": ["k_pt_inc_sort", "k_pt_inc_merge", "k_pt_inc_boxes", "k_pt_inc_top"],
+    "nn_query": ["k_tree_nn1_jobs"],
+    "steer": ["k_steer_jobs"],
+    "collide": ["k_pairs<", "k_scan_excl<mpt::ExpandHeaders", "k_cands", "k_narrow", "k_overflow"],
+    "append": ["k_append_jobs"],
+}
+
+
+def joint_stage_table(times, c, K, nj, n_tot, d, pmax, geo, summ):
+    """Per-stage roofline of one joint round of nj seeds (one launch per stage for all of
+    them): compulsory bytes of all seeds' work, the measured traffic of every kernel of the
+    stage's chain, FP64 of the collide stages; c = the seeds' summed work counters."""
+    units = K * pmax * geo.get("links", 1)
+    per_sub = max(1, (2 ** 22 // geo["clusters"]) // units)
+    n_sub = -(-nj // per_sub)
+    stages = {}
+    for s, ms in times.items():
+        if ms <= 0:
+            continue
+        if s == "collide":
+            b = sum(compulsory_bytes(x, c, K * nj, n_tot, d, pmax, geo, "tree")
+                    for x in ("collide_pairs", "collide_cands", "collide_narrow"))
+            f = sum(fp64_flops(x, c, geo) for x in ("collide_pairs", "collide_cands", "collide_narrow"))
+        else:
+            b = compulsory_bytes(s, c, K * nj, n_tot, d, pmax, geo, "tree")
+            f = None
+        if s == "nn_build":
+            b = inc_build_bytes(n_tot + K * nj, K * nj, d)
+        if b is None:
+            continue
+        t = ms * 1e-3
+        st = {"kernel": " + ".join(JOINT_STAGE_KERNELS.get(s, [])), "ms": round(ms, 4), "compulsory_bytes": int(b),
+              "compulsory_gbs": round(b / t / 1e9, 1), "frac_hbm_compulsory": round(b / t / 1e9 / HBM_PEAK_GBS, 4),
+              "launch": f"one joint launch per kernel for {nj} seeds x {K} extensions"
+                        + (f" ({n_sub} collide sub-batches)" if s == "collide" else "")}
+        trs = [pmc_traffic(summ, k) for k in JOINT_STAGE_KERNELS.get(s, [])]
+        if trs and all(x is not None for x in trs):
+            tr = sum(trs) * (n_sub if s == "collide" else 1)
+            st.update({"traffic": int(tr), "traffic_gbs": round(tr / t / 1e9, 1),
+                       "frac_hbm_measured": round(tr / t / 1e9 / HBM_PEAK_GBS, 4),
+                       "traffic_over_compulsory": round(tr / b, 2)})
+        if f:
+            st.update({"fp64_tflops": round(f / t / 1e12, 3), "frac_fp64": round(f / t / 1e12 / FP64_PEAK_TFLOPS, 4)})
         stages[s] = st
     return stages
 
@@ -381,7 +450,7 @@ def run_seeds(args, world, rank, dist, torch, mpt, multiseed, scenes):
         e.add_nodes(seed_start(args.seed + i, env, agent, mpt, args.seed_start))
         e.set_nn(args.nn, args.ppc)
         engines.append(e)
-    streams = [torch.cuda.Stream() for _ in range(max(1, min(args.streams, len(engines))))]
+    streams = [torch.cuda.Stream() for _ in range(max(1, min(max(args.streams, 1), len(engines))))]
     if engines:
         engines[0].enable_timing(True)
 
@@ -410,7 +479,10 @@ def run_seeds(args, world, rank, dist, torch, mpt, multiseed, scenes):
         eg = engines[g * gsz:(g + 1) * gsz]
         sg = streams[g * spg:(g + 1) * spg]
         if eg:
-            jgroups.append((eg, [sg[j % len(sg)] for j in range(len(eg))], torch.cuda.Stream()))
+            js = torch.cuda.Stream()
+            # --streams 0: every engine on its group's joint stream (a joint round then joins no
+            # other stream)
+            jgroups.append((eg, [sg[j % len(sg)] if args.streams > 0 else js for j in range(len(eg))], js))
 
     def round_():
         if not args.no_joint_nn:
@@ -430,8 +502,14 @@ def run_seeds(args, world, rank, dist, torch, mpt, multiseed, scenes):
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    host = 0.0
+    for i in range(args.steps):
+        if engines and args.stage_every != 1:
+            # the joint round's stage events on every n-th timed round only (as config 2)
+            engines[0].enable_timing(args.stage_every > 0 and i % args.stage_every == 0)
+        h0 = time.perf_counter()
         round_()
+        host += time.perf_counter() - h0
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
@@ -447,11 +525,12 @@ def run_seeds(args, world, rank, dist, torch, mpt, multiseed, scenes):
     digests = multiseed.gather_digests(dist, digests)
     if rank != 0:
         return None
-    summ, summ_path = pmc_summary(args.traffic, "seeds")
+    summ, summ_path = pmc_summary(args.traffic, f"seeds{args.seeds}")
     geo = geometry(sc, env)
     e0 = engines[0]
     n_before = e0.counters()["nodes"]
     pmax = e0.info()["pmax"]
+    scale = None
     if args.no_joint_nn:
         e0.collide_stats(True)
         e0.step(K, streams[0])
@@ -461,50 +540,58 @@ def run_seeds(args, world, rank, dist, torch, mpt, multiseed, scenes):
         nn_mode = e0.last_nn()
         kernels = dict(STAGE_KERNEL, nn_query=NN_KERNEL.get(nn_mode, "k_grid_nn1_runs"))
         if nn_mode == "tree":
-            kernels["nn_build"] = "k_pt_gather"
+            kernels["nn_build"] = "k_pt_inc_merge"
         stages = stage_table(per_launch, cst, K, n_before, sc.dim, pmax, geo, nn_mode, kernels, summ)
         roof = roofline_of(stages, max(stages, key=lambda s: stages[s]["ms"]) if stages else None, cst, summ_path)
     else:
-        # all seeds: one round with work counters on (summed for the joint launches' bytes), then
-        # one with them off and the joint build + NN launches timed by hipEvents on group 0's
-        # joint stream; engine 0's own stages for the per-seed kernels
+        # group 0: one round with the work counters on (each engine's own stages; summed over the
+        # group), then one timed round: a joint round reports every stage (one launch per stage
+        # for all the group's seeds, hipEvents on its joint stream), else the joint build + NN
         eg0, ss0, js0 = jgroups[0]
         for e in eg0:
             e.collide_stats(True)
         mpt.step_many(eg0, K, ss0, js0)
         torch.cuda.synchronize()
         csts = [e.collide_stats(False) for e in eg0]
+        e0.enable_timing(True)
         mpt.step_many(eg0, K, ss0, js0)
         torch.cuda.synchronize()
-        try:
-            jt = mpt.joint_times(js0)
-        except mpt.MptError:
-            jt = None  # no joint launch: every tree still below the Morton-tree size (small runs)
-        cst = csts[0]
-        per_launch = dict(e0.kernel_times())
-        n_tot = sum(e.counters()["nodes"] for e in eg0) - len(eg0) * K  # nodes before the timed call (upper bound)
-        per_launch.pop("nn_query", None)
-        per_launch.pop("nn_build", None)
-        kernels = {s: k for s, k in STAGE_KERNEL.items() if s not in ("nn_query", "nn_build")}
-        stages = stage_table(per_launch, cst, K, n_before, sc.dim, pmax, geo, "tree", kernels, summ)
         nj = len(eg0)
-        work_nn = {k: sum(c[k] for c in csts) for k in ("nn_points", "nn_cells")}
-        agg = dict(cst, **work_nn)
-        joint_stages = (("nn_build", "k_pt_bbox_jobs", jt["build"]), ("nn_query", "k_tree_nn1_jobs<7,", jt["nn"])) if jt else ()
-        for s, kern, ms in joint_stages:
-            b = compulsory_bytes(s, agg, K * nj, max(n_tot, 1), sc.dim, pmax, geo, "tree")
-            t = ms * 1e-3
-            st = {"kernel": kern, "ms": round(ms, 4), "compulsory_bytes": int(b),
-                  "compulsory_gbs": round(b / t / 1e9, 1), "frac_hbm_compulsory": round(b / t / 1e9 / HBM_PEAK_GBS, 4),
-                  "launch": f"one joint launch{' chain' if s == 'nn_build' else ''} for {nj} seeds' {K} queries"}
-            tr = pmc_traffic(summ, kern)
-            if tr is not None:
-                st.update({"traffic": int(tr), "traffic_gbs": round(tr / t / 1e9, 1),
-                           "frac_hbm_measured": round(tr / t / 1e9 / HBM_PEAK_GBS, 4),
-                           "traffic_over_compulsory": round(tr / b, 2)})
-            stages[s] = st
+        agg = {k: sum(c[k] for c in csts) for k in csts[0]}
+        n_tot = sum(e.counters()["nodes"] for e in eg0) - len(eg0) * K  # nodes before the timed call (upper bound)
+        try:
+            jst = mpt.joint_stage_times(js0)
+        except mpt.MptError:
+            jst = None
+        if jst is not None:
+            stages = joint_stage_table(jst, agg, K, nj, max(n_tot, 1), sc.dim, pmax, geo, summ)
+            # event-free stage times: a recorded round carries seven event packets; when the
+            # stages sum to more than a timed round, scale them to it
+            tot = sum(st["ms"] for st in stages.values())
+            scale = min(1.0, (1e3 * elapsed / args.steps) / tot) if tot > 0 else 1.0
+            for st in stages.values():
+                st["ms_event_free"] = round(st["ms"] * scale, 4)
+                for key in ("compulsory_gbs", "frac_hbm_compulsory", "traffic_gbs", "frac_hbm_measured",
+                            "fp64_tflops", "frac_fp64"):
+                    if key in st:
+                        st[key] = round(st[key] / scale, 4)
+        else:
+            try:
+                jt = mpt.joint_times(js0)
+            except mpt.MptError:
+                jt = None  # no joint launch: every tree still below the Morton-tree size (small runs)
+            per_launch = dict(e0.kernel_times())
+            per_launch.pop("nn_query", None)
+            per_launch.pop("nn_build", None)
+            kernels = {s: k for s, k in STAGE_KERNEL.items() if s not in ("nn_query", "nn_build")}
+            stages = stage_table(per_launch, csts[0], K, n_before, sc.dim, pmax, geo, "tree", kernels, summ)
+            if jt:
+                js = {"nn_build": jt["build"], "nn_query": jt["nn"]}
+                stages.update(joint_stage_table(js, agg, K, nj, max(n_tot, 1), sc.dim, pmax, geo, summ))
         dom = "nn_query" if "nn_query" in stages else (max(stages, key=lambda k: stages[k]["ms"]) if stages else None)
-        roof = roofline_of(stages, dom, dict(cst, work_nn_all_seeds=work_nn), summ_path)
+        roof = roofline_of(stages, dom, dict(agg, seeds_in_group=nj), summ_path)
+        if scale is not None:
+            roof["stage_time_scale"] = round(scale, 4)
     import hashlib
 
     all_digest = hashlib.sha256("".join(digests[i] for i in sorted(digests)).encode()).hexdigest()
@@ -531,6 +618,7 @@ def run_seeds(args, world, rank, dist, torch, mpt, multiseed, scenes):
         "checked_per_s": checked / elapsed,
         "valid_fraction": valid / max(checked, 1),
         "per_seed_valid_per_s": valid / elapsed / max(args.seeds, 1),
+        "host_enqueue_ms_per_step": 1e3 * host / args.steps,
         "seeds_digest": all_digest,
         "roofline": roof,
         "cpu_baseline": None,

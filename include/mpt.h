@@ -193,10 +193,15 @@ mpt_status mpt_rrt_set_size(mpt_rrt *rrt, int64_t n, void *stream);
  * collision -> ordered append of the collision-free edges.  Asynchronous. */
 mpt_status mpt_rrt_step(mpt_rrt *rrt, int32_t K, void *stream);
 /* One round of n independent engines (BASELINE config 5: one engine per seed), engine i on
- * streams[i].  Identical results to mpt_rrt_step per engine.  The engines whose round uses the
- * Morton-tree NN share one index build (a launch per stage + one segmented sort) and one query
- * launch, both on joint_stream, which waits for their samples and is waited on by their
- * steer + collide + append.  The job tables and sort buffers of the joint launches belong to
+ * streams[i].  Identical results to mpt_rrt_step per engine.  When every engine's round uses
+ * the Morton-tree NN and the engines share the env, the agent and every parameter but the
+ * seed (and K is a multiple of 16), the whole round is a joint round on joint_stream: one
+ * launch per stage (sample, incremental index build, NN, steer, collide, append) for all
+ * engines, after the engines' streams and before their next work; an engine's last-round
+ * buffers (mpt_rrt_last_round / _last_poses) are then the joint state's, valid until the next
+ * call on that joint stream.  Otherwise the engines whose round uses the Morton tree share
+ * one index build and one query launch on joint_stream, and the rest of each round runs on
+ * the engine's own stream.  The job tables and buffers of the joint launches belong to
  * joint_stream: calls with different joint streams (from one or several host threads) may
  * overlap; calls on one joint stream are serialised.  Asynchronous. */
 mpt_status mpt_rrt_step_many(mpt_rrt *const *rrts, int32_t n, int32_t K, void *const *streams, void *joint_stream);
@@ -213,6 +218,10 @@ mpt_status mpt_rrt_joint_release(void *joint_stream);
 /* The last timed mpt_rrt_step_many on joint_stream: ms[0] = the joint tree build, ms[1] = the
  * joint NN launch (hipEvents on joint_stream).  Synchronises on it. */
 mpt_status mpt_rrt_joint_times(void *joint_stream, float ms[2]);
+/* The last mpt_rrt_step_many on joint_stream if it was a timed joint round (an engine with
+ * timing on): ms = sample, index build, NN, steer, collide, append (hipEvents on
+ * joint_stream).  Synchronises on it. */
+mpt_status mpt_rrt_joint_stage_times(void *joint_stream, float ms[6]);
 /* counters [8]: rounds, extensions checked, extensions valid, nodes, capacity drops,
  * pose overflow, reserved, reserved.  Synchronises. */
 mpt_status mpt_rrt_counters(mpt_rrt *rrt, uint64_t counters[8]);

@@ -395,6 +395,14 @@ def joint_times(joint_stream) -> dict:
     return {"build": float(ms[0]), "nn": float(ms[1])}
 
 
+def joint_stage_times(joint_stream) -> dict:
+    """The last step_many on joint_stream when it ran as a timed joint round: ms of each stage
+    (one launch per stage for all engines, hipEvents on that stream)."""
+    ms = np.zeros(6, np.float32)
+    check(lib().mpt_rrt_joint_stage_times(_stream(joint_stream), _p(ms)), "mpt_rrt_joint_stage_times")
+    return dict(zip(["sample", "nn_build", "nn_query", "steer", "collide", "append"], ms.astype(float).tolist()))
+
+
 def joint_release(joint_stream) -> None:
     """Free the joint state step_many keeps for joint_stream (call before the stream goes)."""
     check(lib().mpt_rrt_joint_release(_stream(joint_stream)), "mpt_rrt_joint_release")

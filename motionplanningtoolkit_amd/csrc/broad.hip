@@ -691,6 +691,7 @@ CollideScratch::~CollideScratch() {
 static int64_t split_chunk_units(int32_t max_clusters) {
     return kSplitChunkThreads / (max_clusters > 0 ? max_clusters : 1);
 }
+int64_t collide_chunk_units(int32_t max_clusters) { return split_chunk_units(max_clusters); }
 
 void CollideScratch::ensure(int64_t n_units, int32_t max_clusters) {
     n_units = std::min<int64_t>(n_units, split_chunk_units(max_clusters));  // launch_collide_split runs chunks

@@ -217,6 +217,9 @@ struct OvfDefer {
 };
 // defer (optional): filled instead of launching k_overflow when the batch runs in one chunk
 // (otherwise defer->n_ovf stays nullptr and k_overflow runs as usual).
+// units one launch of the two-phase path takes (larger batches run in chunks, without the
+// live-unit list)
+int64_t collide_chunk_units(int32_t max_clusters);
 void launch_collide_split(const EnvDev &env, const AgentDev *d_links, int32_t max_clusters, const CollideWork &w,
                           CollideScratch &s, hipStream_t stream, hipEvent_t *marks = nullptr,
                           OvfDefer *defer = nullptr);

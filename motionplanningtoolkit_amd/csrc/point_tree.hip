@@ -1339,9 +1339,8 @@ void launch_tree_nn1(const PointTreeDev &T, const double *q, int64_t nq, int32_t
         launch_tree_nn1_bs<64>(T, q, nq, ids, d2, stream, order);
 }
 
-void launch_tree_nn1_jobs(const PtJob *d_jobs, int32_t n_jobs, int32_t d, int64_t nq, hipStream_t stream) {
-    if (nq <= 0 || n_jobs <= 0) return;
-    constexpr int BS = 64;
+template <int BS>
+static void launch_tree_nn1_jobs_bs(const PtJob *d_jobs, int32_t n_jobs, int32_t d, int64_t nq, hipStream_t stream) {
     const int64_t bpj = (nq * kPtFan + BS - 1) / BS;
     const int64_t groups = (n_jobs + kXcds - 1) / kXcds;
     const dim3 grid((unsigned)(kXcds * groups * bpj));
@@ -1352,6 +1351,15 @@ void launch_tree_nn1_jobs(const PtJob *d_jobs, int32_t n_jobs, int32_t d, int64_
         default: throw Error{1, "point tree: state dim must be 3, 7 or 15"};
     }
     hip_check(hipGetLastError(), "k_tree_nn1_jobs launch");
+}
+
+void launch_tree_nn1_jobs(const PtJob *d_jobs, int32_t n_jobs, int32_t d, int64_t nq, hipStream_t stream) {
+    if (nq <= 0 || n_jobs <= 0) return;
+    // MPT_PT_JOBS_BLOCK: threads per workgroup of the joint launch (64 / 128 / 256; A/B knob)
+    static const int bs = getenv("MPT_PT_JOBS_BLOCK") ? atoi(getenv("MPT_PT_JOBS_BLOCK")) : 64;
+    if (bs == 256) launch_tree_nn1_jobs_bs<256>(d_jobs, n_jobs, d, nq, stream);
+    else if (bs == 128) launch_tree_nn1_jobs_bs<128>(d_jobs, n_jobs, d, nq, stream);
+    else launch_tree_nn1_jobs_bs<64>(d_jobs, n_jobs, d, nq, stream);
 }
 
 }  // namespace mpt

@@ -15,6 +15,8 @@
 // K = 1 reference replay with the reference's own RNG streams is the host planner's job
 // (host/rrt.hpp over the same kernels).
 #include <algorithm>
+#include <chrono>
+#include <cstdio>
 #include <cstring>
 #include <map>
 #include <memory>
@@ -460,6 +462,143 @@ __global__ void k_set_n(int64_t *n_dev, int64_t n, unsigned long long *counters)
     counters[3] = (unsigned long long)n;
 }
 
+// ---- joint rounds (mpt_rrt_step_many): every engine's round in one launch per stage ----
+//
+// Engines that share the env, the agent links, the agent kind and the pose layout, and whose
+// rounds all use the Morton tree, run a round as one launch per stage on the joint stream:
+// sample -> incremental tree build -> NN -> steer -> collide (over every engine's units) ->
+// ordered append, each launch's blockIdx.y (or its unit range) naming the engine.  The round
+// buffers (samples, ends, poses, verdicts, live units) are the joint state's, engine j at
+// offset j * K.  An engine's randomness, NN, steering and append are its own (per-engine
+// seed, extension counter, nodes, count), so every tree equals the one the engine grows alone.
+struct EngineJob {
+    uint64_t seed, ext_base;
+    int64_t set_n;  // a pending mpt_rrt_set_size, or -1
+    int64_t cap;
+    double *nodes;
+    int32_t *parents;
+    int64_t *n_dev;
+    unsigned long long *counters;
+};
+
+__global__ void k_sample_jobs(EngineParams p, const EngineJob *__restrict__ jobs, int32_t K,
+                              double *__restrict__ samples, uint32_t *__restrict__ n_live, int32_t n_sub) {
+    const int job = blockIdx.y;
+    const EngineJob &J = jobs[job];
+    const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k == 0) {
+        if (J.set_n >= 0) {
+            J.n_dev[0] = J.set_n;
+            J.counters[3] = (unsigned long long)J.set_n;
+        }
+        J.n_dev[1] = J.n_dev[0];
+        if (job == 0)
+            for (int b = 0; b < n_sub; ++b) n_live[b] = 0u;  // the live-unit lists of this round
+    }
+    if (k >= K) return;
+    const uint64_t g = J.ext_base + (uint64_t)k;
+    double *out = samples + ((int64_t)job * K + k) * p.d;
+    for (int j = 0; j < p.d; ++j) out[j] = engine_uniform(J.seed, g * 64 + j, p.lo[j], p.hi[j]);
+}
+
+// k_steer for engine blockIdx.y: its extensions are joint edges job * K + k; the live units go
+// to the list of the engine's collide sub-batch (engines [b * per_sub, + per_sub)), indexed
+// from that sub-batch's first unit
+template <int KIND>
+__global__ __launch_bounds__(256) void k_steer_jobs(EngineParams p, const EngineJob *__restrict__ jobs, int32_t K,
+                                                    const int32_t *__restrict__ nn, double *__restrict__ ends,
+                                                    double *__restrict__ poses, int32_t *__restrict__ pcount,
+                                                    uint8_t *__restrict__ verdict, LiveOut lv, int32_t per_sub) {
+    const int job = blockIdx.y;
+    const EngineJob &J = jobs[job];
+    p.seed = J.seed;
+    const int32_t units = p.pmax * p.L;  // <= 64 (the launcher checks)
+    const int64_t e0 = (int64_t)job * K;  // this engine's first joint edge
+    const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    int32_t P = 0;
+    if (k < K)
+        P = steer_one<KIND>(p, J.ext_base, k, J.nodes, nn + e0, ends + e0 * p.d, poses + e0 * units * 12, pcount + e0,
+                            verdict + e0, J.counters);
+    const int sub = job / per_sub;
+    const int64_t sub_e0 = (int64_t)sub * per_sub * K;  // the sub-batch's first edge
+    int32_t *list = lv.list + sub_e0 * units;
+    uint64_t mask = 0;
+    const int64_t ge = e0 + k;  // joint edge
+    const double *ps = poses + ge * units * 12;
+    for (int32_t i = 0; i < P; ++i)
+        for (int32_t l = 0; l < p.L; ++l) {
+            double R[9], T[3];
+            unit_transform(lv.env, ps + (i * p.L + l) * 12, R, T);
+            double *rt = lv.unit_rt + (ge * units + i * p.L + l) * 12;
+#pragma unroll
+            for (int j = 0; j < 9; ++j) rt[j] = R[j];
+#pragma unroll
+            for (int j = 0; j < 3; ++j) rt[9 + j] = T[j];
+            float blo[3], bhi[3];
+            local_box(lv.links[l].bc, lv.links[l].be, R, T, blo, bhi);
+            if (box_overlap(blo, bhi, lv.env.root_lo, lv.env.root_hi)) mask |= 1ull << (i * p.L + l);
+        }
+    __shared__ uint32_t s_wave[4];
+    __shared__ uint32_t s_base;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const uint32_t c = (uint32_t)__popcll(mask);
+    uint32_t incl = c;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const uint32_t o = __shfl_up(incl, off);
+        if (lane >= off) incl += o;
+    }
+    if (lane == 63) s_wave[wave] = incl;
+    __syncthreads();
+    if (threadIdx.x == 0) s_base = atomicAdd(lv.n_live + sub, s_wave[0] + s_wave[1] + s_wave[2] + s_wave[3]);
+    __syncthreads();
+    uint32_t pos = s_base + incl - c;
+    for (int w = 0; w < wave; ++w) pos += s_wave[w];
+    const int64_t local_u0 = (ge - sub_e0) * units;
+    while (mask) {
+        const int b = __ffsll((unsigned long long)mask) - 1;
+        mask &= mask - 1;
+        list[pos++] = (int32_t)(local_u0 + b);
+    }
+}
+
+// k_append_commit for engine blockIdx.y over its K joint verdicts
+__global__ __launch_bounds__(256) void k_append_jobs(const EngineJob *__restrict__ jobs,
+                                                     const uint8_t *__restrict__ verdict, int32_t K, int32_t d,
+                                                     const double *__restrict__ ends, const int32_t *__restrict__ nn) {
+    __shared__ int32_t s_wave[4], s_ones[4];
+    const int job = blockIdx.y;
+    const EngineJob &J = jobs[job];
+    const int64_t e0 = (int64_t)job * K;
+    const uint8_t *vj = verdict + e0;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    // the engine's valid extensions before this block (K is a multiple of 16: the launcher checks)
+    const uint4 *v4 = reinterpret_cast<const uint4 *>(vj);
+    const int64_t nv4 = (int64_t)blockIdx.x * 16;
+    int32_t ones = 0;
+    for (int64_t i0 = tid; i0 < nv4; i0 += 256 * 8) {
+        uint4 x[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int64_t i = i0 + u * 256;
+            x[u] = v4[i < nv4 ? i : 0];
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+            if (i0 + u * 256 < nv4) ones += __popc(x[u].x) + __popc(x[u].y) + __popc(x[u].z) + __popc(x[u].w);
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) ones += __shfl_xor(ones, off);
+    if (lane == 0) s_ones[wave] = ones;
+    __syncthreads();
+    const int64_t before_block = nv4 * 16 - (int64_t)(s_ones[0] + s_ones[1] + s_ones[2] + s_ones[3]);
+    const int64_t n0 = J.n_dev[1];
+    int64_t tot;
+    append_commit_tail(before_block, 0, vj, (int64_t)blockIdx.x * 256, K, d, ends + e0 * d, nn + e0, n0, J.cap,
+                       J.nodes, J.parents, s_wave, &tot);
+    if (blockIdx.x == gridDim.x - 1 && tid == 0) append_commit_counters(tot, n0, J.cap, K, J.n_dev, J.counters);
+}
+
 }  // namespace
 
 struct mpt_rrt {
@@ -521,6 +660,15 @@ struct mpt_rrt {
     // since its last build; pt_grow bounds the nodes appended since then (the K of each round)
     bool pt_inc_ok = false;
     int64_t pt_grow = 0;
+    const mpt_agent *agent = nullptr;
+    // the last round ran in a joint round of mpt_rrt_step_many: its round buffers are the
+    // joint state's slices (valid until the next step_many on that joint stream)
+    bool last_joint = false;
+    struct {
+        const double *samples = nullptr, *ends = nullptr, *poses = nullptr;
+        const int32_t *nn = nullptr, *pcount = nullptr;
+        const uint8_t *verdict = nullptr;
+    } jv;
 };
 
 namespace {
@@ -622,6 +770,7 @@ extern "C" mpt_status mpt_rrt_create(const mpt_env *env, const mpt_agent *agent,
             }
             if ((int64_t)p.pmax * p.L > 4096) throw Error{MPT_ERR_INVALID, "too many poses per edge"};
             r->env = env_dev(env);
+            r->agent = agent;
             std::vector<AgentDev> links(p.L, agent_dev(agent));
             r->max_clusters = std::max(1, agent_dev(agent).n_clusters);
             hip_check(hipMalloc(&r->d_links, sizeof(AgentDev) * p.L), "alloc links");
@@ -731,29 +880,19 @@ bool tree_incremental() {
 // this round's incremental tree build (a full rebuild when the index is stale or more nodes
 // were appended since its last build than one round's sort holds); the queries (the round's
 // samples) are ordered by code for the NN launch
-PtIncJob tree_inc_job(mpt_rrt *r, int32_t K, hipStream_t stream, const SpreadOut *spread) {
+PtIncJob tree_inc_job(mpt_rrt *r, int32_t K, hipStream_t stream, const SpreadOut *spread,
+                      const double *samples = nullptr) {
     const bool full = !r->pt_inc_ok || r->pt_grow > kPtIncSeg;
-    PtIncJob J = r->ptree->prepare_inc(r->d_nodes, r->n_upper, r->d_n, r->p.d, r->p.lo, r->p.hi, r->d_samples, K,
-                                       full, stream, spread);
+    PtIncJob J = r->ptree->prepare_inc(r->d_nodes, r->n_upper, r->d_n, r->p.d, r->p.lo, r->p.hi,
+                                       samples ? samples : r->d_samples, K, full, stream, spread);
     r->pt_inc_ok = true;
     r->pt_grow = 0;
     return J;
 }
 
-StepCtx step_head(mpt_rrt *r, int32_t K, hipStream_t stream, bool defer_tree = false) {
-    StepCtx c;
-    if (r->n_upper < 1) throw Error{MPT_ERR_INVALID, "tree is empty: add a root first"};
-    ensure_round_buffers(r, K);
+// MPT_NN_AUTO: take up the spread a past round's index build left (never waited for)
+void refresh_auto(mpt_rrt *r) {
     const EngineParams &p = r->p;
-    const unsigned kb = (unsigned)((K + 255) / 256);
-    hipEvent_t *ev = nullptr;
-    if (r->timing) {
-        if (r->ring_next - r->ring_done >= kTimingRing) timing_fold_one(r);
-        ev = r->ring.data() + (r->ring_next % kTimingRing) * 10;
-        ++r->ring_next;
-    }
-    c.ev = ev;
-    c.kb = kb;
     if (r->nn_mode == MPT_NN_AUTO && r->spread_pending && hipEventQuery(r->ev_spread) == hipSuccess) {
         // the tree fills less than a quarter of the sampling box: most samples are far
         // from every node, where the grid walks empty rings and the Morton tree does not
@@ -768,8 +907,55 @@ StepCtx step_head(mpt_rrt *r, int32_t K, hipStream_t stream, bool defer_tree = f
         r->spread_pending = false;
         r->spread_seen = true;
     }
+}
+
+bool round_uses_tree(const mpt_rrt *r) {
     const bool big = r->n_upper >= 4096;
-    const bool use_tree = r->nn_mode == MPT_NN_TREE || (r->nn_mode == MPT_NN_AUTO && big && r->auto_tree);
+    return r->nn_mode == MPT_NN_TREE || (r->nn_mode == MPT_NN_AUTO && big && r->auto_tree);
+}
+
+// the spread feedback rides on this round's index build when none is in flight; true when
+// this round's build should write it (spread filled in)
+bool spread_request(mpt_rrt *r, bool indexed, SpreadOut &spread) {
+    const bool want = r->nn_mode == MPT_NN_AUTO && !r->spread_pending && indexed &&
+                      (!r->spread_seen || r->rounds_since_spread >= kSpreadEvery);
+    ++r->rounds_since_spread;
+    if (!want) return false;
+    if (!r->d_spread) {
+        // the grid build's per-block partials [ceil(cap / 256)][6]
+        const int64_t blocks = (r->cap + 255) / 256;
+        hip_check(hipMalloc(&r->d_spread, sizeof(unsigned long long) * blocks * 6), "alloc spread");
+        hip_check(hipHostMalloc(&r->h_spread, sizeof(unsigned long long) * 6,
+                                hipHostMallocMapped | hipHostMallocCoherent), "alloc spread");
+        hip_check(hipHostGetDevicePointer(reinterpret_cast<void **>(&r->h_spread_dev), r->h_spread, 0),
+                  "spread device pointer");
+        hip_check(hipEventCreateWithFlags(&r->ev_spread, hipEventDisableTiming), "event");
+    }
+    spread.gd = r->grid_gd;
+    for (int j = 0; j < 3; ++j) spread.dims[j] = r->grid_dims[j];
+    spread.partial = r->d_spread;
+    spread.host_out = r->h_spread_dev;
+    return true;
+}
+
+StepCtx step_head(mpt_rrt *r, int32_t K, hipStream_t stream, bool defer_tree = false) {
+    StepCtx c;
+    if (r->n_upper < 1) throw Error{MPT_ERR_INVALID, "tree is empty: add a root first"};
+    ensure_round_buffers(r, K);
+    r->last_joint = false;
+    const EngineParams &p = r->p;
+    const unsigned kb = (unsigned)((K + 255) / 256);
+    hipEvent_t *ev = nullptr;
+    if (r->timing) {
+        if (r->ring_next - r->ring_done >= kTimingRing) timing_fold_one(r);
+        ev = r->ring.data() + (r->ring_next % kTimingRing) * 10;
+        ++r->ring_next;
+    }
+    c.ev = ev;
+    c.kb = kb;
+    refresh_auto(r);
+    const bool big = r->n_upper >= 4096;
+    const bool use_tree = round_uses_tree(r);
     const bool use_grid = !use_tree && (r->nn_mode == MPT_NN_GRID || (r->nn_mode == MPT_NN_AUTO && big));
     r->last_nn = use_tree ? MPT_NN_TREE : (use_grid ? MPT_NN_GRID : MPT_NN_BRUTE);
     c.mark(0, stream);
@@ -812,27 +998,8 @@ StepCtx step_head(mpt_rrt *r, int32_t K, hipStream_t stream, bool defer_tree = f
         hip_check(hipGetLastError(), "k_sample");
     }
     c.mark(1, stream);
-    // the spread feedback rides on this round's index build when none is in flight
     SpreadOut spread;
-    const bool want_spread = r->nn_mode == MPT_NN_AUTO && !r->spread_pending && (use_tree || use_grid) &&
-                             (!r->spread_seen || r->rounds_since_spread >= kSpreadEvery);
-    ++r->rounds_since_spread;
-    if (want_spread) {
-        if (!r->d_spread) {
-            // the grid build's per-block partials [ceil(cap / 256)][6]
-            const int64_t blocks = (r->cap + 255) / 256;
-            hip_check(hipMalloc(&r->d_spread, sizeof(unsigned long long) * blocks * 6), "alloc spread");
-            hip_check(hipHostMalloc(&r->h_spread, sizeof(unsigned long long) * 6,
-                                    hipHostMallocMapped | hipHostMallocCoherent), "alloc spread");
-            hip_check(hipHostGetDevicePointer(reinterpret_cast<void **>(&r->h_spread_dev), r->h_spread, 0),
-                      "spread device pointer");
-            hip_check(hipEventCreateWithFlags(&r->ev_spread, hipEventDisableTiming), "event");
-        }
-        spread.gd = r->grid_gd;
-        for (int j = 0; j < 3; ++j) spread.dims[j] = r->grid_dims[j];
-        spread.partial = r->d_spread;
-        spread.host_out = r->h_spread_dev;
-    }
+    const bool want_spread = spread_request(r, use_tree || use_grid, spread);
     if (use_tree) {
         // once: no allocation (device sync) in later rounds
         if (tree_incremental()) r->ptree->inc_reserve(r->cap, p.d);
@@ -1012,7 +1179,7 @@ namespace {
 // step_many groups on different joint streams then overwrote each other's job table and
 // sort keys while the other group's kernels still read them.)  The table is staged through
 // a ring of pinned buffers, so filling one never waits for a copy still in flight.
-constexpr int kJobRing = 4;
+constexpr int kJobRing = 16;
 struct JointNN {
     std::mutex mu;  // one step_many at a time per joint stream (the ring and the tables)
     char *d_stage = nullptr;
@@ -1026,6 +1193,17 @@ struct JointNN {
     hipEvent_t b0 = nullptr, t0 = nullptr, t1 = nullptr;
     bool timed = false;
     JointTreeScratch trees;  // shared sort buffers of the joint tree build
+    // joint rounds (joint_round): the engines' round buffers, engine j at edge offset j * K
+    int64_t r_edges = 0, r_units = 0;
+    int32_t r_dim = 0, r_subs = 0;
+    double *j_samples = nullptr, *j_ends = nullptr, *j_poses = nullptr, *j_nnd2 = nullptr, *j_rt = nullptr;
+    int32_t *j_nn = nullptr, *j_pcount = nullptr, *j_live = nullptr;
+    uint8_t *j_verdict = nullptr;
+    uint32_t *j_nlive = nullptr;
+    CollideScratch cs;
+    // timed joint round: start, sample, build, NN, steer, collide, append
+    hipEvent_t st[7] = {};
+    bool round_timed = false;
 };
 std::mutex g_joints_mu;
 std::map<hipStream_t, std::unique_ptr<JointNN>> g_joints;
@@ -1068,6 +1246,239 @@ char *joint_stage(JointNN &g, size_t bytes, int *slot) {
     return g.h_stage[*slot];
 }
 
+void joint_free_round(JointNN &g) {
+    for (void *p : {(void *)g.j_samples, (void *)g.j_ends, (void *)g.j_poses, (void *)g.j_nnd2, (void *)g.j_rt,
+                    (void *)g.j_nn, (void *)g.j_pcount, (void *)g.j_live, (void *)g.j_verdict, (void *)g.j_nlive})
+        if (p) hip_check(hipFree(p), "free");
+    g.j_samples = g.j_ends = g.j_poses = g.j_nnd2 = g.j_rt = nullptr;
+    g.j_nn = g.j_pcount = g.j_live = nullptr;
+    g.j_verdict = nullptr;
+    g.j_nlive = nullptr;
+    g.r_edges = g.r_units = 0;
+}
+
+// Engines whose rounds can run as one joint round (see EngineJob): every round on the Morton
+// tree (incremental index), the same env, agent and engine parameters but the seed, the
+// two-phase collide with the live-unit list, no work counters, K a multiple of 16 (the
+// append's 16-byte verdict loads).  MPT_JOINT_ROUND=0: per-engine heads and tails (A/B).
+bool joint_round_ok(mpt_rrt *const *rs, int32_t n, int32_t K) {
+    static const bool on = !getenv("MPT_JOINT_ROUND") || atoi(getenv("MPT_JOINT_ROUND")) != 0;
+    if (!on || n < 2 || K < 16 || K % 16 != 0 || !tree_incremental() || collide_mode() == MPT_COLLIDE_FUSED)
+        return false;
+    const mpt_rrt *a = rs[0];
+    const EngineParams &p = a->p;
+    const int64_t units = (int64_t)p.pmax * p.L;
+    if (units > 64 || (int64_t)K * units > collide_chunk_units(a->max_clusters)) return false;
+    for (int32_t i = 0; i < n; ++i) {
+        mpt_rrt *r = rs[i];
+        if (r->stats_on || r->agent != a->agent || r->env.tris != a->env.tris || r->n_upper < 1) return false;
+        const EngineParams &q = r->p;
+        if (q.kind != p.kind || q.d != p.d || q.L != p.L || q.pmax != p.pmax || q.steer_dt != p.steer_dt ||
+            q.cc_dt != p.cc_dt || std::memcmp(q.prm, p.prm, sizeof(p.prm)) != 0 ||
+            std::memcmp(q.lo, p.lo, sizeof(p.lo)) != 0 || std::memcmp(q.hi, p.hi, sizeof(p.hi)) != 0)
+            return false;
+        refresh_auto(r);
+        if (!round_uses_tree(r)) return false;
+    }
+    return true;
+}
+
+// MPT_HOST_PROF=1: host time of the joint round's phases, printed every 32 calls (diagnostics)
+struct HostProf {
+    double acc[8] = {};
+    int64_t calls = 0;
+    std::chrono::steady_clock::time_point t;
+    void start() { t = std::chrono::steady_clock::now(); }
+    void lap(int i) {
+        const auto now = std::chrono::steady_clock::now();
+        acc[i] += std::chrono::duration<double, std::micro>(now - t).count();
+        t = now;
+    }
+    void done() {
+        if (++calls % 32) return;
+        fprintf(stderr, "[host joint round] us/call: stage %.1f engines %.1f joins %.1f sample %.1f build %.1f nn %.1f "
+                        "steer+collide+append %.1f tail %.1f\n",
+                acc[0] / 32, acc[1] / 32, acc[2] / 32, acc[3] / 32, acc[4] / 32, acc[5] / 32, acc[6] / 32, acc[7] / 32);
+        for (double &a : acc) a = 0;
+    }
+};
+
+void joint_round(mpt_rrt *const *rs, int32_t n, int32_t K, void *const *streams_, hipStream_t joint) {
+    static const bool prof = getenv("MPT_HOST_PROF") && atoi(getenv("MPT_HOST_PROF")) == 1;
+    static HostProf hp;
+    if (prof) hp.start();
+    JointNN &g = joint_state(joint);
+    std::lock_guard<std::mutex> lk(g.mu);
+    const mpt_rrt *a = rs[0];
+    const EngineParams &p = a->p;
+    const int32_t d = p.d;
+    const int64_t units = (int64_t)p.pmax * p.L;
+    // collide sub-batches: as many engines as one two-phase launch takes with the live list
+    const int32_t per_sub = (int32_t)std::max<int64_t>(1, collide_chunk_units(a->max_clusters) / ((int64_t)K * units));
+    const int32_t n_sub = (n + per_sub - 1) / per_sub;
+    const int64_t edges = (int64_t)n * K;
+    if (edges > g.r_edges || d != g.r_dim || units * edges > g.r_units || n_sub > g.r_subs) {
+        hip_check(hipDeviceSynchronize(), "sync");  // the old buffers may still be in use
+        joint_free_round(g);
+        hip_check(hipMalloc(&g.j_samples, sizeof(double) * edges * d), "joint samples");
+        hip_check(hipMalloc(&g.j_ends, sizeof(double) * edges * d), "joint ends");
+        hip_check(hipMalloc(&g.j_poses, sizeof(double) * 12 * edges * units), "joint poses");
+        hip_check(hipMalloc(&g.j_rt, sizeof(double) * 12 * edges * units), "joint unit transforms");
+        hip_check(hipMalloc(&g.j_nnd2, sizeof(double) * edges), "joint nn d2");
+        hip_check(hipMalloc(&g.j_nn, sizeof(int32_t) * edges), "joint nn");
+        hip_check(hipMalloc(&g.j_pcount, sizeof(int32_t) * edges), "joint pose counts");
+        hip_check(hipMalloc(&g.j_live, sizeof(int32_t) * edges * units), "joint live units");
+        hip_check(hipMalloc(&g.j_verdict, (size_t)edges), "joint verdicts");
+        hip_check(hipMalloc(&g.j_nlive, sizeof(uint32_t) * std::max(n_sub, 64)), "joint live counts");
+        g.r_edges = edges;
+        g.r_units = edges * units;
+        g.r_dim = d;
+        g.r_subs = std::max(n_sub, 64);
+    }
+    g.cs.ensure((int64_t)std::min(per_sub, n) * K * units, a->max_clusters);
+    // the engines' host bookkeeping and their job table
+    const size_t b_eng = sizeof(EngineJob) * n, b_inc = sizeof(PtIncJob) * n, b_nn = sizeof(PtJob) * n;
+    int slot = 0;
+    char *h = joint_stage(g, b_eng + b_inc + b_nn, &slot);
+    EngineJob *he = reinterpret_cast<EngineJob *>(h);
+    PtIncJob *hi = reinterpret_cast<PtIncJob *>(h + b_eng);
+    PtJob *hn = reinterpret_cast<PtJob *>(h + b_eng + b_inc);
+    const EngineJob *de = reinterpret_cast<const EngineJob *>(g.d_stage);
+    const PtIncJob *di = reinterpret_cast<const PtIncJob *>(g.d_stage + b_eng);
+    const PtJob *dn = reinterpret_cast<const PtJob *>(g.d_stage + b_eng + b_inc);
+    if (prof) hp.lap(0);
+    std::vector<SpreadOut> spreads(n);
+    std::vector<char> want(n, 0);
+    bool timed = false;
+    for (int32_t i = 0; i < n; ++i) {
+        mpt_rrt *r = rs[i];
+        he[i] = EngineJob{r->p.seed, r->ext_base, r->pending_n, r->cap, r->d_nodes, r->d_parents, r->d_n,
+                          r->d_counters};
+        r->pending_n = -1;
+        r->ptree->inc_reserve(r->cap, d);  // once: no allocation in later rounds
+        want[i] = spread_request(r, true, spreads[i]) ? 1 : 0;
+        timed = timed || r->timing;
+    }
+    if (prof) hp.lap(1);
+    // the joint stream waits for every engine stream's earlier work, the engines' streams
+    // for the joint round
+    std::vector<hipStream_t> uniq;
+    for (int32_t i = 0; i < n; ++i) {
+        const hipStream_t s = (hipStream_t)streams_[i];
+        if (s != joint && std::find(uniq.begin(), uniq.end(), s) == uniq.end()) uniq.push_back(s);
+    }
+    while (g.joins.size() < uniq.size()) {
+        hipEvent_t e;
+        hip_check(hipEventCreateWithFlags(&e, hipEventDisableTiming), "event");
+        g.joins.push_back(e);
+    }
+    for (size_t u = 0; u < uniq.size(); ++u) {
+        hip_check(hipEventRecord(g.joins[u], uniq[u]), "join record");
+        hip_check(hipStreamWaitEvent(joint, g.joins[u], 0), "join wait");
+    }
+    if (timed && !g.st[0]) {
+        for (hipEvent_t &e : g.st) hip_check(hipEventCreate(&e), "event");
+        if (!g.b0) {
+            hip_check(hipEventCreate(&g.b0), "event");
+            hip_check(hipEventCreate(&g.t0), "event");
+            hip_check(hipEventCreate(&g.t1), "event");
+        }
+    }
+    auto mark = [&](int i) {
+        if (timed) hip_check(hipEventRecord(g.st[i], joint), "joint stage event");
+    };
+    if (prof) hp.lap(2);
+    mark(0);
+    hip_check(hipMemcpyAsync(g.d_stage, he, b_eng, hipMemcpyHostToDevice, joint), "engine jobs H2D");
+    const unsigned kb = (unsigned)((K + 255) / 256);
+    hipLaunchKernelGGL(k_sample_jobs, dim3(kb, n), dim3(256), 0, joint, p, de, K, g.j_samples, g.j_nlive, n_sub);
+    hip_check(hipGetLastError(), "k_sample_jobs");
+    mark(1);
+    if (prof) hp.lap(3);
+    if (timed) hip_check(hipEventRecord(g.b0, joint), "joint b0");
+    // the index builds (a full rebuild issues its code and sort launches here, after the
+    // samples' launch applied any truncation) and the NN jobs
+    for (int32_t i = 0; i < n; ++i) {
+        mpt_rrt *r = rs[i];
+        hi[i] = tree_inc_job(r, K, joint, want[i] ? &spreads[i] : nullptr, g.j_samples + (int64_t)i * K * d);
+        PointTreeDev T = r->ptree->dev();
+        T.stats = nullptr;
+        hn[i] = PtJob{T, g.j_samples + (int64_t)i * K * d, g.j_nn + (int64_t)i * K, g.j_nnd2 + (int64_t)i * K,
+                      r->ptree->query_order()};
+    }
+    hip_check(hipMemcpyAsync(g.d_stage + b_eng, h + b_eng, b_inc + b_nn, hipMemcpyHostToDevice, joint), "jobs H2D");
+    hip_check(hipEventRecord(g.copied[slot], joint), "jobs copied");
+    launch_tree_inc_jobs(di, hi, n, d, joint);
+    for (int32_t i = 0; i < n; ++i)
+        if (want[i]) {
+            hip_check(hipEventRecord(rs[i]->ev_spread, joint), "spread event");
+            rs[i]->spread_pending = true;
+            rs[i]->rounds_since_spread = 0;
+        }
+    mark(2);
+    if (prof) hp.lap(4);
+    if (timed) hip_check(hipEventRecord(g.t0, joint), "joint t0");
+    launch_tree_nn1_jobs(dn, n, d, K, joint);
+    mark(3);
+    if (timed) hip_check(hipEventRecord(g.t1, joint), "joint t1");
+    if (prof) hp.lap(5);
+    auto steer = p.kind == MPT_AGENT_OMNI ? k_steer_jobs<MPT_AGENT_OMNI>
+                 : (p.kind == MPT_AGENT_BLIMP ? k_steer_jobs<MPT_AGENT_BLIMP> : k_steer_jobs<MPT_AGENT_SNAKE>);
+    LiveOut lv{g.j_live, g.j_nlive, a->d_links, a->env, nullptr, 0, g.j_rt};
+    hipLaunchKernelGGL(steer, dim3(kb, n), dim3(256), 0, joint, p, de, K, g.j_nn, g.j_ends, g.j_poses, g.j_pcount,
+                       g.j_verdict, lv, per_sub);
+    hip_check(hipGetLastError(), "k_steer_jobs");
+    mark(4);
+    for (int32_t b = 0; b < n_sub; ++b) {
+        const int64_t e0 = (int64_t)b * per_sub * K;
+        const int32_t ne = std::min(per_sub, n - b * per_sub);
+        CollideWork cw{};
+        cw.poses = g.j_poses + e0 * units * 12;
+        cw.pose_edge = nullptr;
+        cw.pcount = g.j_pcount + e0;
+        cw.pmax = p.pmax;
+        cw.L = p.L;
+        cw.n_units = (int64_t)ne * K * units;
+        cw.verdict = g.j_verdict + e0;
+        cw.stats = nullptr;
+        cw.live_units = g.j_live + e0 * units;
+        cw.n_live = g.j_nlive + b;
+        cw.unit_rt = g.j_rt + e0 * units * 12;
+        launch_collide_split(a->env, a->d_links, a->max_clusters, cw, g.cs, joint, nullptr, nullptr);
+    }
+    mark(5);
+    hipLaunchKernelGGL(k_append_jobs, dim3(kb, n), dim3(256), 0, joint, de, g.j_verdict, K, d, g.j_ends, g.j_nn);
+    hip_check(hipGetLastError(), "k_append_jobs");
+    mark(6);
+    if (prof) hp.lap(6);
+    g.timed = timed;
+    g.round_timed = timed;
+    if (timed) g_last_timed = &g;
+    if (!g.done) hip_check(hipEventCreateWithFlags(&g.done, hipEventDisableTiming), "event");
+    hip_check(hipEventRecord(g.done, joint), "joint done");
+    for (hipStream_t s : uniq) hip_check(hipStreamWaitEvent(s, g.done, 0), "joint wait");
+    for (int32_t i = 0; i < n; ++i) {
+        mpt_rrt *r = rs[i];
+        r->ext_base += (uint64_t)K;
+        r->n_upper = std::min<int64_t>(r->cap, r->n_upper + K);
+        r->pt_grow += K;
+        r->last_K = K;
+        r->last_nn = MPT_NN_TREE;
+        r->last_joint = true;
+        const int64_t e0 = (int64_t)i * K;
+        r->jv.samples = g.j_samples + e0 * d;
+        r->jv.ends = g.j_ends + e0 * d;
+        r->jv.poses = g.j_poses + e0 * units * 12;
+        r->jv.nn = g.j_nn + e0;
+        r->jv.pcount = g.j_pcount + e0;
+        r->jv.verdict = g.j_verdict + e0;
+    }
+    if (prof) {
+        hp.lap(7);
+        hp.done();
+    }
+}
+
 }  // namespace
 
 extern "C" mpt_status mpt_rrt_step_many(mpt_rrt *const *rs, int32_t n, int32_t K, void *const *streams_,
@@ -1078,6 +1489,10 @@ extern "C" mpt_status mpt_rrt_step_many(mpt_rrt *const *rs, int32_t n, int32_t K
             if (!rs[i]) throw Error{MPT_ERR_INVALID, "null engine"};
         auto stream_of = [&](int32_t i) { return (hipStream_t)streams_[i]; };
         const hipStream_t joint = (hipStream_t)joint_stream_;
+        if (joint_round_ok(rs, n, K)) {
+            joint_round(rs, n, K, streams_, joint);
+            return;
+        }
         std::vector<StepCtx> cs(n);
         for (int32_t i = 0; i < n; ++i) cs[i] = step_head(rs[i], K, stream_of(i), true);
         // engines whose round uses the Morton tree (and the first such engine's state dim)
@@ -1171,6 +1586,7 @@ extern "C" mpt_status mpt_rrt_step_many(mpt_rrt *const *rs, int32_t n, int32_t K
                 g_last_timed = &g;
             }
             g.timed = timed;
+            g.round_timed = false;
             hip_check(hipEventRecord(g.done, joint), "joint done");
             for (hipStream_t s : uniq) hip_check(hipStreamWaitEvent(s, g.done, 0), "joint wait");
             for (int32_t i : J) cs[i].mark(3, stream_of(i));
@@ -1205,6 +1621,18 @@ extern "C" mpt_status mpt_rrt_joint_times(void *joint_stream, float ms[2]) {
     });
 }
 
+extern "C" mpt_status mpt_rrt_joint_stage_times(void *joint_stream, float ms[6]) {
+    return guarded([&] {
+        if (!ms) throw Error{MPT_ERR_INVALID, "null pointer"};
+        JointNN *g = joint_find((hipStream_t)joint_stream);
+        if (!g) throw Error{MPT_ERR_INVALID, "no joint launch on this stream"};
+        std::lock_guard<std::mutex> lk(g->mu);
+        if (!g->round_timed) throw Error{MPT_ERR_INVALID, "the last step_many on this stream was not a timed joint round"};
+        hip_check(hipEventSynchronize(g->st[6]), "event sync");
+        for (int i = 0; i < 6; ++i) hip_check(hipEventElapsedTime(&ms[i], g->st[i], g->st[i + 1]), "elapsed");
+    });
+}
+
 extern "C" mpt_status mpt_rrt_joint_release(void *joint_stream) {
     return guarded([&] {
         std::unique_ptr<JointNN> g;
@@ -1229,6 +1657,9 @@ extern "C" mpt_status mpt_rrt_joint_release(void *joint_stream) {
         JointTreeScratch &S = g->trees;
         for (void *p : {(void *)S.keys, (void *)S.keys_sorted, (void *)S.vals, (void *)S.vals_sorted, S.temp})
             if (p) hip_check(hipFree(p), "free");
+        joint_free_round(*g);
+        for (hipEvent_t e : g->st)
+            if (e) hip_check(hipEventDestroy(e), "event");
     });
 }
 
@@ -1258,10 +1689,15 @@ extern "C" mpt_status mpt_rrt_last_round(mpt_rrt *r, double *samples, int32_t *n
         hip_check(hipDeviceSynchronize(), "sync");
         const int64_t K = r->last_K, d = r->p.d;
         if (K == 0) return;
-        if (samples) hip_check(hipMemcpy(samples, r->d_samples, sizeof(double) * K * d, hipMemcpyDeviceToHost), "");
-        if (nn_ids) hip_check(hipMemcpy(nn_ids, r->d_nn, sizeof(int32_t) * K, hipMemcpyDeviceToHost), "");
-        if (ends) hip_check(hipMemcpy(ends, r->d_ends, sizeof(double) * K * d, hipMemcpyDeviceToHost), "");
-        if (verdicts) hip_check(hipMemcpy(verdicts, r->d_verdict, (size_t)K, hipMemcpyDeviceToHost), "");
+        // a joint round's buffers are the joint state's slices (valid until its next step_many)
+        const bool j = r->last_joint;
+        const double *s = j ? r->jv.samples : r->d_samples, *e = j ? r->jv.ends : r->d_ends;
+        const int32_t *nn = j ? r->jv.nn : r->d_nn;
+        const uint8_t *v = j ? r->jv.verdict : r->d_verdict;
+        if (samples) hip_check(hipMemcpy(samples, s, sizeof(double) * K * d, hipMemcpyDeviceToHost), "");
+        if (nn_ids) hip_check(hipMemcpy(nn_ids, nn, sizeof(int32_t) * K, hipMemcpyDeviceToHost), "");
+        if (ends) hip_check(hipMemcpy(ends, e, sizeof(double) * K * d, hipMemcpyDeviceToHost), "");
+        if (verdicts) hip_check(hipMemcpy(verdicts, v, (size_t)K, hipMemcpyDeviceToHost), "");
     });
 }
 
@@ -1271,11 +1707,14 @@ extern "C" mpt_status mpt_rrt_last_poses(mpt_rrt *r, double *poses, int32_t *pos
         hip_check(hipDeviceSynchronize(), "sync");
         const int64_t K = r->last_K;
         if (K == 0) return;
+        const bool j = r->last_joint;
         if (poses)
-            hip_check(hipMemcpy(poses, r->d_poses, sizeof(double) * 12 * K * r->p.pmax * r->p.L, hipMemcpyDeviceToHost),
+            hip_check(hipMemcpy(poses, j ? r->jv.poses : r->d_poses, sizeof(double) * 12 * K * r->p.pmax * r->p.L,
+                                hipMemcpyDeviceToHost),
                       "poses D2H");
         if (pose_counts)
-            hip_check(hipMemcpy(pose_counts, r->d_pcount, sizeof(int32_t) * K, hipMemcpyDeviceToHost), "pcount D2H");
+            hip_check(hipMemcpy(pose_counts, j ? r->jv.pcount : r->d_pcount, sizeof(int32_t) * K, hipMemcpyDeviceToHost),
+                      "pcount D2H");
     });
 }
 

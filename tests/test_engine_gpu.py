@@ -445,3 +445,60 @@ def test_engine_set_size_and_capacity(mpt_gpu, oracle):
     assert eng.counters()["nodes"] == 100
     t, _ = eng.read_tree(100)
     assert np.array_equal(t, tree)
+
+
+def test_joint_round_matches_single_steps(mpt_gpu):
+    """mpt_rrt_step_many as a joint round (every engine on the Morton tree, one launch per stage
+    for all of them, engine j's round buffers at offset j * K of the joint state): six blimp
+    seeds, one of them truncated with set_size between rounds (applied by the joint sample
+    launch; the index then rebuilds from scratch), must grow exactly the trees each seed grows
+    alone, and an engine's last-round intermediates (samples, NN ids, end states, verdicts,
+    poses) must equal its solo round's."""
+    import torch
+
+    sc = scenes.blimp_scenario("all")
+    root = np.array([[88.6, 68.9, 57.1, 0, 0, 0, 0.0]])
+    env = mpt_gpu.Environment(sc.env_tris, sc.env_tf)
+    ag = mpt_gpu.AgentMesh(sc.agent_tris)
+    K, rounds, seeds = 1024, 5, list(range(900, 906))
+
+    def grow(joint):
+        engs = []
+        for s in seeds:
+            e = mpt_gpu.RRTEngine(env, ag, sc.kind, sc.prm, sc.ranges, sc.steer_dt, sc.cc_dt, 1 + rounds * K, s)
+            e.add_nodes(root)
+            e.set_nn("tree")
+            engs.append(e)
+        streams = [torch.cuda.Stream() for _ in range(3)]
+        js = torch.cuda.Stream()
+        for r in range(rounds):
+            if r == 3:
+                engs[2].set_size(500)
+            if joint:
+                engs[0].enable_timing(r == rounds - 1)
+                mpt_gpu.step_many(engs, K, [streams[j % 3] for j in range(len(engs))], js)
+            else:
+                for e in engs:
+                    e.step(K)
+        torch.cuda.synchronize()
+        times = mpt_gpu.joint_stage_times(js) if joint else None
+        out = []
+        for e in engs:
+            assert e.last_nn() == "tree"
+            out.append((e.read_tree(e.counters()["nodes"]), e.last_round(K), e.last_poses(K)))
+        for e in engs:
+            e.close()
+        if joint:
+            mpt_gpu.joint_release(js)
+        return out, times
+
+    alone, _ = grow(False)
+    joint, times = grow(True)
+    for (ta, ra, pa), (tb, rb, pb) in zip(alone, joint):
+        assert len(ta[0]) > K
+        assert np.array_equal(bits(ta[0]), bits(tb[0])) and np.array_equal(ta[1], tb[1])
+        for x, y in zip(ra, rb):
+            assert np.array_equal(np.asarray(x).view(np.uint8), np.asarray(y).view(np.uint8))
+        assert np.array_equal(bits(pa[0]), bits(pb[0])) and np.array_equal(pa[1], pb[1])
+    assert set(times) == {"sample", "nn_build", "nn_query", "steer", "collide", "append"}
+    assert all(v > 0 for v in times.values())
