@@ -52,6 +52,9 @@ def parse():
                          "(collision-heavy); snake = config 3 (snake_trailers, 11 links, corridor)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample length")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-variants", action="store_true",
+                    help="skip the secondary workloads' legs (config 2 at N=1 runs them by default, each in a "
+                         "process of its own, and reports them under `variants`)")
     ap.add_argument("--stage-every", type=int, default=16,
                     help="record the per-stage hipEvents on every n-th timed round (0: none); a recorded round "
                          "pays ~60-80 us of event packets (config 2: 170 us a round with none, "
@@ -625,6 +628,53 @@ def run_seeds(args, world, rank, dist, torch, mpt, multiseed, scenes):
     }
 
 
+# ----------------------------------------------------------------------------- variants
+
+# the secondary workloads measured in the same run as config 2 (one short leg each, in a
+# process of its own so one leg's device state never affects another's timing)
+VARIANTS = {
+    "blimp-room": ["--workload", "blimp-room", "--steps", "20", "--warmup", "3"],
+    "snake": ["--workload", "snake", "--steps", "10", "--warmup", "3"],
+    "seeds=32": ["--seeds", "32", "--steps", "20", "--warmup", "5"],
+    "seeds=256": ["--seeds", "256", "--steps", "10", "--warmup", "5"],
+}
+
+
+def run_variants():
+    """Each leg's bench line (no CPU baseline, no nested legs), condensed: value, ms_per_step,
+    the dominant stage's roofline, every stage's time and fractions, and (config 5) the seeds
+    digest; a leg that fails reports its error instead."""
+    out = {}
+    for name, extra in VARIANTS.items():
+        cmd = [sys.executable, os.path.abspath(__file__), "--no-cpu", "--no-variants"] + extra
+        t0 = time.perf_counter()
+        try:
+            p = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=dict(os.environ))
+            line = [x for x in p.stdout.splitlines() if x.startswith("{")]
+            if p.returncode != 0 or not line:
+                out[name] = {"error": f"rc={p.returncode}", "stderr_tail": p.stderr[-800:]}
+                continue
+            d = json.loads(line[-1])
+        except subprocess.TimeoutExpired:
+            out[name] = {"error": "timeout"}
+            continue
+        roof = d.get("roofline") or {}
+        leg = {k: d.get(k) for k in ("value", "unit", "ms_per_step", "steps", "warmup", "valid_fraction", "scaling",
+                                     "seeds_digest", "per_seed_valid_per_s", "host_enqueue_ms_per_step")
+               if d.get(k) is not None}
+        leg["config"] = d.get("config")
+        leg["roofline"] = {k: roof.get(k) for k in ("bound", "achieved", "peak", "unit", "frac", "traffic", "kernel",
+                                                    "stage", "ms_per_launch", "pmc_source", "stage_time_scale")
+                           if k in roof}
+        leg["stages"] = {s: {k: v for k, v in st.items()
+                             if k in ("ms", "ms_event_free", "frac_hbm_compulsory", "frac_hbm_measured",
+                                      "traffic_over_compulsory", "frac_fp64", "kernel")}
+                         for s, st in (roof.get("stages") or {}).items()}
+        leg["leg_wall_s"] = round(time.perf_counter() - t0, 1)
+        out[name] = leg
+    return out
+
+
 # ----------------------------------------------------------------------------- main
 
 def main():
@@ -773,6 +823,9 @@ def main():
         out["cpu_baseline"] = cpu_baseline(sc, tree, K, seed, args.cpu_seconds)
     else:
         out["cpu_baseline"] = None
+    if world == 1 and not args.no_variants and args.workload == "blimp":
+        del eng  # its device memory, before the legs' processes allocate theirs
+        out["variants"] = run_variants()
     print(json.dumps(out))
     if dist:
         dist.destroy_process_group()

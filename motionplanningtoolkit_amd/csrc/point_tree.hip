@@ -497,11 +497,12 @@ constexpr int kIncSortThreads = 1024;
 // (and their box into ibox); blockIdx.x = 1: the round's queries -> code order (qorder).
 // (code, row) pairs order totally, so the result does not depend on the sort.
 template <int D>
-__global__ __launch_bounds__(kIncSortThreads) void k_pt_inc_sort(IncJobs jobs) {
+__device__ __forceinline__ void pt_inc_sort(const PtIncJob &J) {
     __shared__ uint64_t sk[kPtIncSeg];
     __shared__ int32_t sv[kPtIncSeg];
     __shared__ unsigned long long s_min[kPtMaxDim], s_max[kPtMaxDim];
-    const PtIncJob &J = jobs.at(blockIdx.y);
+    // the plan in LDS: its fields were per-lane flat loads, each waited on, inside the code loop
+    __shared__ IncPlan s_plan;
     const int seg = blockIdx.x;
     const int t = threadIdx.x;
     int64_t m = 0, base = 0;
@@ -525,6 +526,10 @@ __global__ __launch_bounds__(kIncSortThreads) void k_pt_inc_sort(IncJobs jobs) {
         s_min[t] = ~0ull;
         s_max[t] = 0ull;
     }
+    static_assert(sizeof(IncPlan) % 4 == 0, "IncPlan copied as words");
+    for (int w = t; w < (int)(sizeof(IncPlan) / 4); w += kIncSortThreads)
+        reinterpret_cast<uint32_t *>(&s_plan)[w] = reinterpret_cast<const uint32_t *>(J.plan)[w];
+    __syncthreads();
     unsigned long long mn[D], mx[D];
 #pragma unroll
     for (int j = 0; j < D; ++j) {
@@ -537,7 +542,7 @@ __global__ __launch_bounds__(kIncSortThreads) void k_pt_inc_sort(IncJobs jobs) {
             const int64_t row = base + i;
 #pragma unroll
             for (int j = 0; j < D; ++j) x[j] = src[row * D + j];
-            sk[i] = inc_code<D>(J.plan, x);
+            sk[i] = inc_code<D>(&s_plan, x);
             sv[i] = (int32_t)row;
             if (seg == 0) {
 #pragma unroll
@@ -568,25 +573,82 @@ __global__ __launch_bounds__(kIncSortThreads) void k_pt_inc_sort(IncJobs jobs) {
             }
         }
     }
+    // bitonic sort of [0, size), 8 consecutive elements per thread in registers: partners fewer
+    // than 8 apart are in the thread's registers, fewer than 512 apart in its wave (lane
+    // shuffles), the rest exchanged through LDS (a 4096-element sort: 6 LDS stages of 78)
+    constexpr int E = kPtIncSeg / kIncSortThreads;
+    uint64_t key[E];
+    int32_t val[E];
+#pragma unroll
+    for (int a = 0; a < E; ++a) {
+        const int i = t * E + a;
+        key[a] = i < size ? sk[i] : ~0ull;
+        val[a] = i < size ? sv[i] : 0x7fffffff;
+    }
     for (int k = 2; k <= size; k <<= 1) {
         for (int j = k >> 1; j > 0; j >>= 1) {
-            for (int i = t; i < size; i += kIncSortThreads) {
-                const int l = i ^ j;
-                if (l > i) {
-                    const uint64_t ka = sk[i], kb = sk[l];
-                    const int32_t va = sv[i], vb = sv[l];
-                    const bool up = (i & k) == 0;
-                    if (up ? inc_less(kb, vb, ka, va) : inc_less(ka, va, kb, vb)) {
-                        sk[i] = kb;
-                        sk[l] = ka;
-                        sv[i] = vb;
-                        sv[l] = va;
+            if (j >= 64 * E) {  // block-uniform
+                __syncthreads();  // the last exchange's reads are done
+#pragma unroll
+                for (int a = 0; a < E; ++a) {
+                    sk[t * E + a] = key[a];
+                    sv[t * E + a] = val[a];
+                }
+                __syncthreads();
+#pragma unroll
+                for (int a = 0; a < E; ++a) {
+                    const int i = t * E + a, l = i ^ j;
+                    const uint64_t pk = sk[l];
+                    const int32_t pv = sv[l];
+                    const bool keep_min = (i < l) == ((i & k) == 0);
+                    if (keep_min ? inc_less(pk, pv, key[a], val[a]) : inc_less(key[a], val[a], pk, pv)) {
+                        key[a] = pk;
+                        val[a] = pv;
+                    }
+                }
+            } else if (j >= E) {
+                const int lm = j / E;
+                const bool lower = (t & lm) == 0;
+#pragma unroll
+                for (int a = 0; a < E; ++a) {
+                    const uint64_t pk = __shfl_xor(key[a], lm);
+                    const int32_t pv = __shfl_xor(val[a], lm);
+                    const bool keep_min = lower == (((t * E + a) & k) == 0);
+                    if (keep_min ? inc_less(pk, pv, key[a], val[a]) : inc_less(key[a], val[a], pk, pv)) {
+                        key[a] = pk;
+                        val[a] = pv;
+                    }
+                }
+            } else {
+                // partners within the thread's registers: j is 4, 2 or 1 (compile-time indices)
+#pragma unroll
+                for (int jj = E / 2; jj > 0; jj >>= 1) {
+                    if (jj != j) continue;
+#pragma unroll
+                    for (int a = 0; a < E; ++a) {
+                        const int b = a ^ jj;
+                        if (b < a) continue;
+                        const bool up = ((t * E + a) & k) == 0;
+                        if (up ? inc_less(key[b], val[b], key[a], val[a]) : inc_less(key[a], val[a], key[b], val[b])) {
+                            const uint64_t tk = key[a];
+                            const int32_t tv = val[a];
+                            key[a] = key[b];
+                            val[a] = val[b];
+                            key[b] = tk;
+                            val[b] = tv;
+                        }
                     }
                 }
             }
-            __syncthreads();
         }
     }
+    __syncthreads();
+#pragma unroll
+    for (int a = 0; a < E; ++a) {
+        sk[t * E + a] = key[a];
+        sv[t * E + a] = val[a];
+    }
+    __syncthreads();
     if (seg == 0) {
         for (int i = t; i < m; i += kIncSortThreads) {
             J.nkeys[i] = sk[i];
@@ -599,6 +661,12 @@ __global__ __launch_bounds__(kIncSortThreads) void k_pt_inc_sort(IncJobs jobs) {
     } else {
         for (int i = t; i < m; i += kIncSortThreads) J.qorder[i] = sv[i];
     }
+}
+
+template <int D>
+__global__ __launch_bounds__(kIncSortThreads) void k_pt_inc_sort(IncJobs jobs) {
+    if (jobs.table) pt_inc_sort<D>(jobs.table[blockIdx.y]);
+    else pt_inc_sort<D>(jobs.one);
 }
 
 // number of a's among the first p elements of merge(a, b), an a before a b of the same key
@@ -620,10 +688,9 @@ constexpr int kIncTile = 256;  // merged outputs per workgroup (one per thread)
 // source by a search of its diagonal there; the row and id copied from the old sorted arrays
 // or the node rows; the leaf boxes (8 consecutive outputs) by an 8-lane reduction.
 template <int D>
-__global__ __launch_bounds__(kIncTile) void k_pt_inc_merge(IncJobs jobs) {
+__device__ __forceinline__ void pt_inc_merge(const PtIncJob &J) {
     __shared__ uint64_t sa[kIncTile], sb[kIncTile];
     __shared__ int64_t s_split[2];
-    const PtIncJob &J = jobs.at(blockIdx.y);
     const int64_t nd = *J.T.n_dev, n = nd < J.T.n_upper ? nd : J.T.n_upper;
     const int64_t p0 = (int64_t)blockIdx.x * kIncTile;
     if (p0 >= n) return;
@@ -682,17 +749,26 @@ __global__ __launch_bounds__(kIncTile) void k_pt_inc_merge(IncJobs jobs) {
     }
 }
 
-__global__ __launch_bounds__(256) void k_pt_inc_boxes(IncJobs jobs) {
-    const PtIncJob &J = jobs.at(blockIdx.y);
+template <int D>
+__global__ __launch_bounds__(kIncTile) void k_pt_inc_merge(IncJobs jobs) {
+    if (jobs.table) pt_inc_merge<D>(jobs.table[blockIdx.y]);
+    else pt_inc_merge<D>(jobs.one);
+}
+
+__device__ __forceinline__ void pt_inc_boxes(const PtIncJob &J) {
     if (J.T.n_levels < 2) return;
     const int64_t groups = (J.T.n_upper + kPtChunkLeaves * kPtFan - 1) / (kPtChunkLeaves * kPtFan);
     if (blockIdx.x >= groups) return;
     pt_boxes(J.T, J.boxes, nullptr, blockIdx.x, groups);
 }
 
+__global__ __launch_bounds__(256) void k_pt_inc_boxes(IncJobs jobs) {
+    if (jobs.table) pt_inc_boxes(jobs.table[blockIdx.y]);
+    else pt_inc_boxes(jobs.one);
+}
+
 // levels 5.. (one workgroup per tree), then the indexed count and the spread feedback
-__global__ __launch_bounds__(256) void k_pt_inc_top(IncJobs jobs) {
-    const PtIncJob &J = jobs.at(blockIdx.x);
+__device__ __forceinline__ void pt_inc_top(const PtIncJob &J) {
     if (J.T.n_levels > kPtInBlockLevels) pt_top_boxes(J.T, J.boxes);
     if (threadIdx.x != 0) return;
     *J.nidx = live_n(J.T);
@@ -704,6 +780,11 @@ __global__ __launch_bounds__(256) void k_pt_inc_top(IncJobs jobs) {
         }
         __threadfence_system();
     }
+}
+
+__global__ __launch_bounds__(256) void k_pt_inc_top(IncJobs jobs) {
+    if (jobs.table) pt_inc_top(jobs.table[blockIdx.x]);
+    else pt_inc_top(jobs.one);
 }
 
 // full rebuild: the box of every live point (from empty)
@@ -848,25 +929,156 @@ __device__ __forceinline__ void tree_nn1_block(const PointTreeDev &T, const doub
     }
 }
 
+// The same exact search with two nodes expanded per step: 16 lanes per query, the stack's top
+// two entries popped together, each taken by one half of the group (a leaf's 8 points or an
+// inner node's 8 children); the halves' best (d2, id) merged over the 16 lanes, the children
+// re-tested against the merged bound, and the second entry's survivors pushed below the top
+// entry's (each half nearest-last), so the walk stays nearest-first.  Half the dependent
+// steps of the one-node walk for a few more nodes visited; the result is the same exact 1-NN
+// (any visiting order is: only boxes whose lower bound exceeds the best are skipped).  The
+// stack holds at most ~14 entries a level (two sibling blocks of 7) + 2: 2 * 8 * 10 entries.
+constexpr int kPtG2 = 2 * kPtFan;
+constexpr int kPtStack2 = 2 * kPtFan * kPtMaxLevels;
+constexpr int64_t kPtNnW2MaxQueries = 262144;  // the two-node walk up to this many queries a launch
+
 template <int D, int BS>
+__device__ __forceinline__ void tree_nn1_block2(const PointTreeDev &T, const double *__restrict__ q, int64_t nq,
+                                                int32_t *__restrict__ out_ids, double *__restrict__ out_d2,
+                                                int64_t blk, const int32_t *__restrict__ order) {
+    __shared__ int32_t s_node[BS / kPtG2][kPtStack2];
+    __shared__ float s_lb[BS / kPtG2][kPtStack2];
+    const int64_t t = blk * BS + threadIdx.x;
+    const int64_t slot = t / kPtG2;
+    const int sub = (int)(t % kPtG2);
+    const int half = sub / kPtFan;  // 0: the top entry, 1: the one below it
+    const int ls = sub % kPtFan;    // the child / point this lane takes
+    const int grp = threadIdx.x / kPtG2;
+    if (slot >= nq) return;  // whole groups leave together
+    const int64_t qi = order ? (int64_t)order[slot] : slot;
+    double qq[D];
+#pragma unroll
+    for (int i = 0; i < D; ++i) qq[i] = q[qi * D + i];
+    const int64_t n = live_n(T);
+    double bd = __builtin_huge_val();
+    int32_t bi = -1;
+    uint32_t n_pts = 0, n_box = 0;
+    if (n > 0) {
+        int sp = 1;
+        if (sub == 0) {
+            s_node[grp][0] = T.n_levels << 27;
+            s_lb[grp][0] = 0.0f;
+        }
+        __builtin_amdgcn_wave_barrier();
+        const int base = (threadIdx.x & 63) & ~(kPtG2 - 1);
+        while (sp > 0) {
+            const int np = sp >= 2 ? 2 : 1;
+            const bool have = half < np;
+            int32_t code = 0;
+            double lbs = 0.0;
+            if (have) {
+                code = s_node[grp][sp - 1 - half];
+                lbs = (double)s_lb[grp][sp - 1 - half];
+            }
+            sp -= np;
+            __builtin_amdgcn_wave_barrier();
+            const bool act = have && !(lbs * (1.0 - 1e-12) > bd);
+            const int lev = act ? code >> 27 : 0;
+            const int64_t idx = code & ((1 << 27) - 1);
+            bool keep = false;
+            double lb2 = 0.0;
+            int64_t c = 0;
+            if (lev == 1) {
+                const int64_t p = idx * kPtFan + ls;
+                if (p < n) {
+                    const double dd = flann_l2<D>(qq, T.pts + p * D);
+                    const int32_t id = T.ids[p];
+                    ++n_pts;
+                    if (nn_better(dd, id, bd, bi)) {
+                        bd = dd;
+                        bi = id;
+                    }
+                }
+            } else if (lev > 1) {
+                c = idx * kPtFan + ls;
+                if (c < lvl_size(n, lev - 1)) {
+                    const float *b = T.boxes + (lvl_off(T.n_upper, lev - 1) + c) * 2 * D;
+#pragma unroll
+                    for (int k = 0; k < D; ++k) {
+                        const double g = fmax(fmax((double)b[k] - qq[k], qq[k] - (double)b[D + k]), 0.0);
+                        lb2 += g * g;
+                    }
+                    keep = true;
+                    ++n_box;
+                }
+            }
+            // the two halves' best, then the survivors against it
+#pragma unroll
+            for (int off = kPtG2 / 2; off > 0; off >>= 1) {
+                const double od = __shfl_xor(bd, off, kPtG2);
+                const int32_t oi = __shfl_xor(bi, off, kPtG2);
+                if (nn_better(od, oi, bd, bi)) {
+                    bd = od;
+                    bi = oi;
+                }
+            }
+            keep = keep && lb2 * (1.0 - 1e-12) <= bd;
+            const uint32_t gm = (uint32_t)(__ballot(keep) >> base) & 0xffffu;
+            const uint32_t m1 = gm >> kPtFan, mine = half ? m1 : (gm & 0xffu);
+            int rank = 0;
+#pragma unroll
+            for (int j = 0; j < kPtFan; ++j) {
+                const double o = __shfl(lb2, half * kPtFan + j, kPtG2);
+                if (((mine >> j) & 1u) && (o > lb2 || (o == lb2 && j > ls))) ++rank;
+            }
+            if (keep) {
+                const int pos = sp + (half ? 0 : __popc(m1)) + rank;
+                s_node[grp][pos] = ((lev - 1) << 27) | (int32_t)c;
+                s_lb[grp][pos] = __double2float_rd(lb2);
+            }
+            sp += __popc(gm);
+            __builtin_amdgcn_wave_barrier();
+        }
+    }
+    if (T.stats) {
+#pragma unroll
+        for (int off = kPtG2 / 2; off > 0; off >>= 1) {
+            n_pts += __shfl_xor(n_pts, off, kPtG2);
+            n_box += __shfl_xor(n_box, off, kPtG2);
+        }
+        if (sub == 0) {
+            atomicAdd(T.stats + 0, (unsigned long long)n_pts);
+            atomicAdd(T.stats + 1, (unsigned long long)n_box);
+        }
+    }
+    if (sub == 0) {
+        out_ids[qi] = bi;
+        out_d2[qi] = bd;
+    }
+}
+
+template <int D, int BS, int W>
 __global__ __launch_bounds__(BS) void k_tree_nn1(PointTreeDev T, const double *__restrict__ q, int64_t nq,
                                                  int32_t *__restrict__ out_ids, double *__restrict__ out_d2,
                                                  const int32_t *__restrict__ order) {
-    tree_nn1_block<D, BS>(T, q, nq, out_ids, out_d2, blockIdx.x, order);
+    if constexpr (W >= 2) tree_nn1_block2<D, BS>(T, q, nq, out_ids, out_d2, blockIdx.x, order);
+    else tree_nn1_block<D, BS>(T, q, nq, out_ids, out_d2, blockIdx.x, order);
 }
 
 // Many trees in one launch (mpt_rrt_step_many: one engine per independent seed).  Jobs are
 // dealt to XCDs: workgroup b runs on XCD b % 8, so job j takes the workgroups of XCD j % 8
 // and its tree stays in that XCD's L2.
 // 8 waves per SIMD for d <= 7 (56 VGPRs, no spill); d = 15 would spill at 8, so 4 (108 VGPRs)
-template <int D, int BS>
-__global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(D >= 15 ? 4 : 8))) void k_tree_nn1_jobs(
+// W = 2: the two-node walk (tree_nn1_block2, 16 lanes per query), at 7 waves per SIMD for
+// d <= 7 (72 VGPRs: the 8-wave budget spilled 8 a lane and ran 9 % slower)
+template <int D, int BS, int W>
+__global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(D >= 15 ? 4 : (W >= 2 ? 7 : 8)))) void k_tree_nn1_jobs(
     const PtJob *__restrict__ jobs, int32_t n_jobs, int64_t nq, int64_t blocks_per_job) {
     const int64_t xcd = blockIdx.x % kXcds, slot = blockIdx.x / kXcds;
     const int64_t job = xcd + kXcds * (slot / blocks_per_job);
     if (job >= n_jobs) return;
     const PtJob &J = jobs[job];
-    tree_nn1_block<D, BS>(J.T, J.q, nq, J.ids, J.d2, slot % blocks_per_job, J.order);
+    if constexpr (W >= 2) tree_nn1_block2<D, BS>(J.T, J.q, nq, J.ids, J.d2, slot % blocks_per_job, J.order);
+    else tree_nn1_block<D, BS>(J.T, J.q, nq, J.ids, J.d2, slot % blocks_per_job, J.order);
 }
 
 // Radius search (FLANN_KDTreeWrapper::kNearestWithin, utilities/flannkdtreewrapper.hpp:91-117:
@@ -1314,14 +1526,14 @@ void launch_tree_radius(const PointTreeDev &T, const double *q, int64_t nq, doub
     hip_check(hipGetLastError(), "k_tree_radius launch");
 }
 
-template <int BS>
+template <int BS, int W>
 static void launch_tree_nn1_bs(const PointTreeDev &T, const double *q, int64_t nq, int32_t *ids, double *d2,
                                hipStream_t stream, const int32_t *order) {
-    const dim3 grid((unsigned)((nq * kPtFan + BS - 1) / BS));
+    const dim3 grid((unsigned)((nq * kPtFan * W + BS - 1) / BS));
     switch (T.d) {
-        case 3: hipLaunchKernelGGL((k_tree_nn1<3, BS>), grid, dim3(BS), 0, stream, T, q, nq, ids, d2, order); break;
-        case 7: hipLaunchKernelGGL((k_tree_nn1<7, BS>), grid, dim3(BS), 0, stream, T, q, nq, ids, d2, order); break;
-        case 15: hipLaunchKernelGGL((k_tree_nn1<15, BS>), grid, dim3(BS), 0, stream, T, q, nq, ids, d2, order); break;
+        case 3: hipLaunchKernelGGL((k_tree_nn1<3, BS, W>), grid, dim3(BS), 0, stream, T, q, nq, ids, d2, order); break;
+        case 7: hipLaunchKernelGGL((k_tree_nn1<7, BS, W>), grid, dim3(BS), 0, stream, T, q, nq, ids, d2, order); break;
+        case 15: hipLaunchKernelGGL((k_tree_nn1<15, BS, W>), grid, dim3(BS), 0, stream, T, q, nq, ids, d2, order); break;
         default: throw Error{1, "point tree: state dim must be 3, 7 or 15"};
     }
     hip_check(hipGetLastError(), "k_tree_nn1 launch");
@@ -1333,21 +1545,26 @@ void launch_tree_nn1(const PointTreeDev &T, const double *q, int64_t nq, int32_t
     // one-wave workgroups spread an engine round's few thousand queries over all CUs
     // (MPT_PT_NN1_BLOCK=256: four waves per workgroup; A/B knob)
     static const int bs = getenv("MPT_PT_NN1_BLOCK") ? atoi(getenv("MPT_PT_NN1_BLOCK")) : 64;
+    // nodes expanded per step: as the joint launch (MPT_PT_NN_W forces one)
+    static const int w_env = getenv("MPT_PT_NN_W") ? atoi(getenv("MPT_PT_NN_W")) : 0;
+    const int w = w_env > 0 ? w_env : (nq <= kPtNnW2MaxQueries ? 2 : 1);
     if (bs == 256)
-        launch_tree_nn1_bs<256>(T, q, nq, ids, d2, stream, order);
+        w == 1 ? launch_tree_nn1_bs<256, 1>(T, q, nq, ids, d2, stream, order)
+               : launch_tree_nn1_bs<256, 2>(T, q, nq, ids, d2, stream, order);
     else
-        launch_tree_nn1_bs<64>(T, q, nq, ids, d2, stream, order);
+        w == 1 ? launch_tree_nn1_bs<64, 1>(T, q, nq, ids, d2, stream, order)
+               : launch_tree_nn1_bs<64, 2>(T, q, nq, ids, d2, stream, order);
 }
 
-template <int BS>
+template <int BS, int W>
 static void launch_tree_nn1_jobs_bs(const PtJob *d_jobs, int32_t n_jobs, int32_t d, int64_t nq, hipStream_t stream) {
-    const int64_t bpj = (nq * kPtFan + BS - 1) / BS;
+    const int64_t bpj = (nq * kPtFan * (W >= 2 ? 2 : 1) + BS - 1) / BS;
     const int64_t groups = (n_jobs + kXcds - 1) / kXcds;
     const dim3 grid((unsigned)(kXcds * groups * bpj));
     switch (d) {
-        case 3: hipLaunchKernelGGL((k_tree_nn1_jobs<3, BS>), grid, dim3(BS), 0, stream, d_jobs, n_jobs, nq, bpj); break;
-        case 7: hipLaunchKernelGGL((k_tree_nn1_jobs<7, BS>), grid, dim3(BS), 0, stream, d_jobs, n_jobs, nq, bpj); break;
-        case 15: hipLaunchKernelGGL((k_tree_nn1_jobs<15, BS>), grid, dim3(BS), 0, stream, d_jobs, n_jobs, nq, bpj); break;
+        case 3: hipLaunchKernelGGL((k_tree_nn1_jobs<3, BS, W>), grid, dim3(BS), 0, stream, d_jobs, n_jobs, nq, bpj); break;
+        case 7: hipLaunchKernelGGL((k_tree_nn1_jobs<7, BS, W>), grid, dim3(BS), 0, stream, d_jobs, n_jobs, nq, bpj); break;
+        case 15: hipLaunchKernelGGL((k_tree_nn1_jobs<15, BS, W>), grid, dim3(BS), 0, stream, d_jobs, n_jobs, nq, bpj); break;
         default: throw Error{1, "point tree: state dim must be 3, 7 or 15"};
     }
     hip_check(hipGetLastError(), "k_tree_nn1_jobs launch");
@@ -1355,11 +1572,14 @@ static void launch_tree_nn1_jobs_bs(const PtJob *d_jobs, int32_t n_jobs, int32_t
 
 void launch_tree_nn1_jobs(const PtJob *d_jobs, int32_t n_jobs, int32_t d, int64_t nq, hipStream_t stream) {
     if (nq <= 0 || n_jobs <= 0) return;
-    // MPT_PT_JOBS_BLOCK: threads per workgroup of the joint launch (64 / 128 / 256; A/B knob)
-    static const int bs = getenv("MPT_PT_JOBS_BLOCK") ? atoi(getenv("MPT_PT_JOBS_BLOCK")) : 64;
-    if (bs == 256) launch_tree_nn1_jobs_bs<256>(d_jobs, n_jobs, d, nq, stream);
-    else if (bs == 128) launch_tree_nn1_jobs_bs<128>(d_jobs, n_jobs, d, nq, stream);
-    else launch_tree_nn1_jobs_bs<64>(d_jobs, n_jobs, d, nq, stream);
+    // The two-node walk halves a query's dependent steps for ~+15 % more nodes: it pays when
+    // the launch leaves the chip waiting on its slowest waves (config 5 at 32 seeds, 131 072
+    // queries: 1.96 -> 1.79 ms) and costs when the launch keeps every SIMD busy (256 seeds,
+    // 1 M queries: 8.98 -> 11.1 ms).  MPT_PT_NN_W = 1 / 2 forces one (A/B).
+    static const int w_env = getenv("MPT_PT_NN_W") ? atoi(getenv("MPT_PT_NN_W")) : 0;
+    const int w = w_env > 0 ? w_env : ((int64_t)n_jobs * nq <= kPtNnW2MaxQueries ? 2 : 1);
+    if (w == 1) launch_tree_nn1_jobs_bs<64, 1>(d_jobs, n_jobs, d, nq, stream);
+    else launch_tree_nn1_jobs_bs<64, 2>(d_jobs, n_jobs, d, nq, stream);
 }
 
 }  // namespace mpt
