@@ -22,6 +22,7 @@ from .api import (  # noqa: F401
     joint_nn_ms,
     joint_release,
     joint_stage_times,
+    prm_stats,
     joint_times,
     last_collide_stats,
     load_mesh,
@@ -41,6 +42,6 @@ from .api import (  # noqa: F401
 
 __all__ = [
     "AGENT_OMNI", "AGENT_BLIMP", "AGENT_SNAKE", "AgentMesh", "Environment", "NearestNeighbors", "RRTEngine",
-    "collide_batch", "collide_batch_device", "distance_batch", "distance_batch_device", "init", "joint_nn_ms", "joint_release", "joint_stage_times", "joint_times", "last_collide_stats", "load_mesh", "prm", "prm_connect", "prmlite_edges", "prmlite", "grid_discretization", "rrt_inst", "rrt_batched_inst",
+    "collide_batch", "collide_batch_device", "distance_batch", "distance_batch_device", "init", "joint_nn_ms", "joint_release", "joint_stage_times", "prm_stats", "joint_times", "last_collide_stats", "load_mesh", "prm", "prm_connect", "prmlite_edges", "prmlite", "grid_discretization", "rrt_inst", "rrt_batched_inst",
     "set_collide_mode", "set_collide_stats", "step_many", "synchronize", "transform_from_location", "build", "lib", "LIB_PATH", "MptError",
 ]

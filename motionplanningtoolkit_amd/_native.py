@@ -68,6 +68,7 @@ SIGNATURES = {
     "mpt_rrt_joint_times": (I32, [P, P]),
     "mpt_rrt_joint_release": (I32, [P]),
     "mpt_rrt_joint_stage_times": (I32, [P, P]),
+    "mpt_prm_stats": (I32, [I32, P]),
     "mpt_rrt_counters": (I32, [P, P]),
     "mpt_rrt_read_tree": (I32, [P, P, P, I64]),
     "mpt_rrt_last_round": (I32, [P, P, P, P, P]),

@@ -172,6 +172,14 @@ def prm_connect(env: Environment, agent: AgentMesh, kind: int, states, radius2: 
             "ms": dict(zip(["neighbours", "poses", "collision", "total"], ms.tolist()))}
 
 
+def prm_stats(enable: bool) -> dict:
+    """The sweep work counters of this thread's last prm_connect made with counters on; enable
+    turns them on (or off) for later calls (diagnostics: an atomic per wave)."""
+    out = np.zeros(6, np.uint64)
+    check(lib().mpt_prm_stats(1 if enable else 0, _p(out)), "mpt_prm_stats")
+    return dict(zip(["waves", "item_tests", "gate_tests", "sat_tests", "edges", "poses"], (int(x) for x in out)))
+
+
 def prmlite_edges(env: Environment, agent: AgentMesh, vertices, step: float = 0.1) -> np.ndarray:
     """PRMLite::generateEdges on the device: collides [V(V-1)/2] over the pairs i < j (row-major)
     of vertices [V][12] (R | T)."""

@@ -96,6 +96,7 @@ struct PtIncJob {
     int32_t *qorder;              // out: query indices in code order [nq]
     int32_t full;                 // 1: nkeys / nvals hold every point (hipcub-sorted), no old points
     SpreadOut sp;
+    unsigned long long *dbg;      // MPT_SORT_DBG=1: the sort's phase times [job][8] (diagnostics)
 };
 // the incremental build of n trees of dim d (stream-ordered): sort, merge, box levels.
 // d_jobs / h_jobs: the same table on the device and the host (n == 1: d_jobs unused)

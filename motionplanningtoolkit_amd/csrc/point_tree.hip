@@ -476,13 +476,28 @@ __device__ __forceinline__ uint64_t inc_code(const IncPlan *__restrict__ P, cons
     }
     uint64_t c = 0;
     const int32_t nb = P->n;
-    for (int k = 0; k < nb; ++k) {
-        const int32_t dk = P->dim[k];
-        uint32_t v = q[0];
+    // unrolled to the code width (d <= 7), so the plan's table reads issue together instead of
+    // one round trip per bit; the 15-dim select chain would not fit the registers unrolled
+    if constexpr (D <= 7) {
 #pragma unroll
-        for (int j = 1; j < D; ++j)
-            if (j == dk) v = q[j];
-        c = (c << 1) | (uint64_t)((v >> P->bit[k]) & 1u);
+        for (int k = 0; k < kPtIncBits; ++k) {
+            if (k >= nb) break;
+            const int32_t dk = P->dim[k];
+            uint32_t v = q[0];
+#pragma unroll
+            for (int j = 1; j < D; ++j)
+                if (j == dk) v = q[j];
+            c = (c << 1) | (uint64_t)((v >> P->bit[k]) & 1u);
+        }
+    } else {
+        for (int k = 0; k < nb; ++k) {
+            const int32_t dk = P->dim[k];
+            uint32_t v = q[0];
+#pragma unroll
+            for (int j = 1; j < D; ++j)
+                if (j == dk) v = q[j];
+            c = (c << 1) | (uint64_t)((v >> P->bit[k]) & 1u);
+        }
     }
     return c;
 }
@@ -526,10 +541,15 @@ __device__ __forceinline__ void pt_inc_sort(const PtIncJob &J) {
         s_min[t] = ~0ull;
         s_max[t] = 0ull;
     }
+    auto stamp = [&](int i) {
+        if (J.dbg && t == 0) J.dbg[blockIdx.y * 8 + i] = __builtin_amdgcn_s_memrealtime();
+    };
+    stamp(0);
     static_assert(sizeof(IncPlan) % 4 == 0, "IncPlan copied as words");
     for (int w = t; w < (int)(sizeof(IncPlan) / 4); w += kIncSortThreads)
         reinterpret_cast<uint32_t *>(&s_plan)[w] = reinterpret_cast<const uint32_t *>(J.plan)[w];
     __syncthreads();
+    stamp(1);
     unsigned long long mn[D], mx[D];
 #pragma unroll
     for (int j = 0; j < D; ++j) {
@@ -573,6 +593,7 @@ __device__ __forceinline__ void pt_inc_sort(const PtIncJob &J) {
             }
         }
     }
+    stamp(2);
     // bitonic sort of [0, size), 8 consecutive elements per thread in registers: partners fewer
     // than 8 apart are in the thread's registers, fewer than 512 apart in its wave (lane
     // shuffles), the rest exchanged through LDS (a 4096-element sort: 6 LDS stages of 78)
@@ -642,6 +663,7 @@ __device__ __forceinline__ void pt_inc_sort(const PtIncJob &J) {
             }
         }
     }
+    stamp(3);
     __syncthreads();
 #pragma unroll
     for (int a = 0; a < E; ++a) {
@@ -661,6 +683,7 @@ __device__ __forceinline__ void pt_inc_sort(const PtIncJob &J) {
     } else {
         for (int i = t; i < m; i += kIncSortThreads) J.qorder[i] = sv[i];
     }
+    stamp(4);
 }
 
 template <int D>
@@ -821,6 +844,36 @@ __global__ __launch_bounds__(256) void k_pt_inc_codes(const double *__restrict__
 constexpr int kPtGroupsPerBlock = 256 / kPtFan;
 constexpr int kPtStack = kPtFan * kPtMaxLevels;
 
+// A box's lower bound on FLANN's squared L2 from the query, as a float rounded down.  d <= 7:
+// computed in float (a quarter of the double box test's VALU work) from the query rounded
+// outward -- each gap at most (1 + u) over the exact one (u = 2^-24), its square and each
+// partial sum another (1 + u), so the float sum is at most (1 + u)^(D + 3) over the exact
+// bound, and the final scale by 1 - 2^-19 (itself rounded) brings it below it; d = 15: in
+// double (register budget) and rounded down.  Pruning on it keeps every box the exact bound
+// keeps.
+constexpr float kLbF32Shrink = 1.0f - 0x1p-19f;
+template <int D>
+__device__ __forceinline__ float box_lb(const float *__restrict__ b, const double (&qq)[D], const float (&qlo)[D],
+                                        const float (&qhi)[D]) {
+    if constexpr (D <= 7) {
+        float s = 0.0f;
+#pragma unroll
+        for (int k = 0; k < D; ++k) {
+            const float g = fmaxf(fmaxf(b[k] - qhi[k], qlo[k] - b[D + k]), 0.0f);
+            s = s + g * g;
+        }
+        return s * kLbF32Shrink;
+    } else {
+        double lb2 = 0.0;
+#pragma unroll
+        for (int k = 0; k < D; ++k) {
+            const double g = fmax(fmax((double)b[k] - qq[k], qq[k] - (double)b[D + k]), 0.0);
+            lb2 += g * g;
+        }
+        return __double2float_rd(lb2);
+    }
+}
+
 // queries [blk * BS / 8, + BS / 8) of one tree (a workgroup's share of k_tree_nn1 / _jobs)
 template <int D, int BS>
 __device__ __forceinline__ void tree_nn1_block(const PointTreeDev &T, const double *__restrict__ q, int64_t nq,
@@ -841,6 +894,12 @@ __device__ __forceinline__ void tree_nn1_block(const PointTreeDev &T, const doub
     double qq[D];
 #pragma unroll
     for (int i = 0; i < D; ++i) qq[i] = q[qi * D + i];
+    float qlo[D], qhi[D];  // the query rounded outward (box_lb, d <= 7)
+#pragma unroll
+    for (int i = 0; i < D; ++i) {
+        qlo[i] = __double2float_rd(qq[i]);
+        qhi[i] = __double2float_ru(qq[i]);
+    }
     const int64_t n = live_n(T);
     double bd = __builtin_huge_val();
     int32_t bi = -1;
@@ -884,15 +943,10 @@ __device__ __forceinline__ void tree_nn1_block(const PointTreeDev &T, const doub
             } else {
                 const int64_t c = idx * kPtFan + sub;
                 bool keep = false;
-                double lb2 = 0.0;
+                float lbf = 0.0f;
                 if (c < lvl_size(n, lev - 1)) {
-                    const float *b = T.boxes + (lvl_off(T.n_upper, lev - 1) + c) * 2 * D;
-#pragma unroll
-                    for (int k = 0; k < D; ++k) {
-                        const double g = fmax(fmax((double)b[k] - qq[k], qq[k] - (double)b[D + k]), 0.0);
-                        lb2 += g * g;
-                    }
-                    keep = lb2 * (1.0 - 1e-12) <= bd;
+                    lbf = box_lb<D>(T.boxes + (lvl_off(T.n_upper, lev - 1) + c) * 2 * D, qq, qlo, qhi);
+                    keep = (double)lbf * (1.0 - 1e-12) <= bd;
                     ++n_box;
                 }
                 const int base = (threadIdx.x & 63) & ~(kPtFan - 1);
@@ -900,12 +954,12 @@ __device__ __forceinline__ void tree_nn1_block(const PointTreeDev &T, const doub
                 int rank = 0;
 #pragma unroll
                 for (int j = 0; j < kPtFan; ++j) {
-                    const double o = __shfl(lb2, j, kPtFan);
-                    if (((gm >> j) & 1u) && (o > lb2 || (o == lb2 && j > sub))) ++rank;
+                    const float o = __shfl(lbf, j, kPtFan);
+                    if (((gm >> j) & 1u) && (o > lbf || (o == lbf && j > sub))) ++rank;
                 }
                 if (keep) {
                     s_node[grp][sp + rank] = ((lev - 1) << 27) | (int32_t)c;
-                    s_lb[grp][sp + rank] = __double2float_rd(lb2);
+                    s_lb[grp][sp + rank] = lbf;
                 }
                 sp += __popc(gm);
                 __builtin_amdgcn_wave_barrier();
@@ -958,6 +1012,12 @@ __device__ __forceinline__ void tree_nn1_block2(const PointTreeDev &T, const dou
     double qq[D];
 #pragma unroll
     for (int i = 0; i < D; ++i) qq[i] = q[qi * D + i];
+    float qlo[D], qhi[D];  // the query rounded outward (box_lb, d <= 7)
+#pragma unroll
+    for (int i = 0; i < D; ++i) {
+        qlo[i] = __double2float_rd(qq[i]);
+        qhi[i] = __double2float_ru(qq[i]);
+    }
     const int64_t n = live_n(T);
     double bd = __builtin_huge_val();
     int32_t bi = -1;
@@ -985,7 +1045,7 @@ __device__ __forceinline__ void tree_nn1_block2(const PointTreeDev &T, const dou
             const int lev = act ? code >> 27 : 0;
             const int64_t idx = code & ((1 << 27) - 1);
             bool keep = false;
-            double lb2 = 0.0;
+            float lbf = 0.0f;
             int64_t c = 0;
             if (lev == 1) {
                 const int64_t p = idx * kPtFan + ls;
@@ -1001,12 +1061,7 @@ __device__ __forceinline__ void tree_nn1_block2(const PointTreeDev &T, const dou
             } else if (lev > 1) {
                 c = idx * kPtFan + ls;
                 if (c < lvl_size(n, lev - 1)) {
-                    const float *b = T.boxes + (lvl_off(T.n_upper, lev - 1) + c) * 2 * D;
-#pragma unroll
-                    for (int k = 0; k < D; ++k) {
-                        const double g = fmax(fmax((double)b[k] - qq[k], qq[k] - (double)b[D + k]), 0.0);
-                        lb2 += g * g;
-                    }
+                    lbf = box_lb<D>(T.boxes + (lvl_off(T.n_upper, lev - 1) + c) * 2 * D, qq, qlo, qhi);
                     keep = true;
                     ++n_box;
                 }
@@ -1021,19 +1076,19 @@ __device__ __forceinline__ void tree_nn1_block2(const PointTreeDev &T, const dou
                     bi = oi;
                 }
             }
-            keep = keep && lb2 * (1.0 - 1e-12) <= bd;
+            keep = keep && (double)lbf * (1.0 - 1e-12) <= bd;
             const uint32_t gm = (uint32_t)(__ballot(keep) >> base) & 0xffffu;
             const uint32_t m1 = gm >> kPtFan, mine = half ? m1 : (gm & 0xffu);
             int rank = 0;
 #pragma unroll
             for (int j = 0; j < kPtFan; ++j) {
-                const double o = __shfl(lb2, half * kPtFan + j, kPtG2);
-                if (((mine >> j) & 1u) && (o > lb2 || (o == lb2 && j > ls))) ++rank;
+                const float o = __shfl(lbf, half * kPtFan + j, kPtG2);
+                if (((mine >> j) & 1u) && (o > lbf || (o == lbf && j > ls))) ++rank;
             }
             if (keep) {
                 const int pos = sp + (half ? 0 : __popc(m1)) + rank;
                 s_node[grp][pos] = ((lev - 1) << 27) | (int32_t)c;
-                s_lb[grp][pos] = __double2float_rd(lb2);
+                s_lb[grp][pos] = lbf;
             }
             sp += __popc(gm);
             __builtin_amdgcn_wave_barrier();
@@ -1487,6 +1542,10 @@ PtIncJob PointTree::prepare_inc(const double *pts, int64_t n_upper, const int64_
     J.q = iq_on ? q : nullptr;
     J.nq = iq_on ? nq : 0;
     J.qorder = iqorder;
+    static const bool dbg = getenv("MPT_SORT_DBG") && atoi(getenv("MPT_SORT_DBG")) == 1;
+    static unsigned long long *dbg_buf = nullptr;
+    if (dbg && !dbg_buf) hip_check(hipMalloc(&dbg_buf, sizeof(unsigned long long) * 8 * 4096), "sort dbg");
+    J.dbg = dbg ? dbg_buf : nullptr;
     J.full = full ? 1 : 0;
     if (spread) J.sp = *spread;
     return J;
@@ -1496,6 +1555,8 @@ void launch_tree_inc_jobs(const PtIncJob *d_jobs, const PtIncJob *h_jobs, int32_
     if (n <= 0) return;
     // one job: passed in the kernel arguments (no staged table)
     IncJobs js{n == 1 ? nullptr : d_jobs, h_jobs[0]};
+    static const bool dbg = getenv("MPT_SORT_DBG") && atoi(getenv("MPT_SORT_DBG")) == 1;
+    if (dbg && h_jobs[0].dbg) hip_check(hipMemsetAsync(h_jobs[0].dbg, 0, sizeof(unsigned long long) * 8 * n, stream), "dbg");
     int64_t max_n = 0;
     for (int32_t j = 0; j < n; ++j) max_n = std::max(max_n, h_jobs[j].T.n_upper);
     auto by_d = [&](auto k3, auto k7, auto k15) { return d == 3 ? k3 : d == 7 ? k7 : k15; };
@@ -1503,6 +1564,25 @@ void launch_tree_inc_jobs(const PtIncJob *d_jobs, const PtIncJob *h_jobs, int32_
     hipLaunchKernelGGL(by_d(k_pt_inc_sort<3>, k_pt_inc_sort<7>, k_pt_inc_sort<15>), dim3(2, n), dim3(kIncSortThreads),
                        0, stream, js);
     hip_check(hipGetLastError(), "k_pt_inc_sort");
+    if (dbg && h_jobs[0].dbg) {
+        std::vector<unsigned long long> h((size_t)8 * n);
+        hip_check(hipStreamSynchronize(stream), "dbg sync");
+        hip_check(hipMemcpy(h.data(), h_jobs[0].dbg, sizeof(unsigned long long) * 8 * n, hipMemcpyDeviceToHost), "dbg");
+        double ph[4] = {0, 0, 0, 0}, t0 = 1e300, t1 = 0;
+        int cnt = 0;
+        for (int j = 0; j < n; ++j) {
+            const unsigned long long *e = &h[(size_t)8 * j];
+            if (!e[0] || !e[4]) continue;
+            ++cnt;
+            for (int k = 0; k < 4; ++k) ph[k] += (double)(e[k + 1] - e[k]);
+            t0 = std::min(t0, (double)e[0]);
+            t1 = std::max(t1, (double)e[4]);
+        }
+        // s_memrealtime ticks at 100 MHz
+        if (cnt)
+            fprintf(stderr, "[sort dbg] %d trees: plan %.1f us, codes %.1f us, sort %.1f us, out %.1f us; span %.1f us\n",
+                    cnt, ph[0] / cnt * 0.01, ph[1] / cnt * 0.01, ph[2] / cnt * 0.01, ph[3] / cnt * 0.01, (t1 - t0) * 0.01);
+    }
     hipLaunchKernelGGL(by_d(k_pt_inc_merge<3>, k_pt_inc_merge<7>, k_pt_inc_merge<15>),
                        dim3((unsigned)((max_n + kIncTile - 1) / kIncTile), n), dim3(kIncTile), 0, stream, js);
     hip_check(hipGetLastError(), "k_pt_inc_merge");

@@ -177,6 +177,11 @@ int64_t scan_total(int64_t *d_in_out, int64_t n_plus_1, DBuf<char> &temp, hipStr
     return total;
 }
 
+// mpt_prm_stats: the sweep's work counters for the next mpt_prm_connect calls (one
+// same-address atomic per wave: diagnostics only, never in a timed call)
+thread_local bool g_prm_stats_on = false;
+thread_local uint64_t g_prm_stats[6] = {};
+
 int32_t uf_find(std::vector<int32_t> &p, int32_t x) {
     while (p[x] != x) {
         p[x] = p[p[x]];
@@ -186,6 +191,14 @@ int32_t uf_find(std::vector<int32_t> &p, int32_t x) {
 }
 
 }  // namespace
+
+extern "C" mpt_status mpt_prm_stats(int32_t enable, uint64_t out[6]) {
+    return guarded([&] {
+        if (out)
+            for (int i = 0; i < 6; ++i) out[i] = g_prm_stats[i];
+        g_prm_stats_on = enable != 0;
+    });
+}
 
 extern "C" mpt_status mpt_prm_connect(const mpt_env *env, const mpt_agent *agent, int32_t agent_kind,
                                       const double *states, int64_t n, int32_t dim, double radius2, double cc_dt,
@@ -273,7 +286,20 @@ extern "C" mpt_status mpt_prm_connect(const mpt_env *env, const mpt_agent *agent
             const int32_t mc = std::max(1, ag.n_clusters);
             static const char *path = getenv("MPT_PRM_COLLIDE");  // sweep (default) | split | fused
             if (!path || std::string(path) == "sweep") {
-                launch_collide_sweep(env_dev(env), d_link, mc, d_poses, d_poff, E, d_v, nullptr, stream);
+                unsigned long long *st = nullptr;
+                if (g_prm_stats_on) {
+                    st = reinterpret_cast<unsigned long long *>(S.temp.get(64) );
+                    hip_check(hipMemsetAsync(st, 0, sizeof(unsigned long long) * 4, stream), "stats zero");
+                }
+                launch_collide_sweep(env_dev(env), d_link, mc, d_poses, d_poff, E, d_v, st, stream);
+                if (st) {
+                    unsigned long long h[4];
+                    hip_check(hipMemcpyAsync(h, st, sizeof(h), hipMemcpyDeviceToHost, stream), "stats");
+                    hip_check(hipStreamSynchronize(stream), "stats sync");
+                    for (int i = 0; i < 4; ++i) g_prm_stats[i] = h[i];
+                    g_prm_stats[4] = (uint64_t)E;
+                    g_prm_stats[5] = (uint64_t)P;
+                }
             } else if (std::string(path) == "fused") {
                 launch_collide(env_dev(env), d_link, w, stream);
             } else {

@@ -25,6 +25,41 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, REPO)
 
 
+FP64_PEAK_TFLOPS = 78.6
+HBM_PEAK_GBS = 8000.0
+
+
+def sweep_roofline(w, ms, n_agent, n_env, traffic_path):
+    """k_sweep (the config-4 collision stage, one wave per (edge, agent cluster)): FP64 by
+    SURVEY §8(d)'s model -- 750 flops per exact triangle test, 27 per (pair, pose) gate (the
+    translated triangle's box and the overlap test), 45 per agent triangle rotated once per
+    wave (R Q, 64 lanes) -- and HBM: compulsory = the poses, pose offsets, verdicts, agent
+    triangles and the env tree items read once; measured = the kernel's rocprofv3 PMC traffic."""
+    t = ms * 1e-3
+    flops = 750.0 * w["sat_tests"] + 27.0 * w["gate_tests"] + 45.0 * 64 * w["waves"]
+    items = n_env + -(-n_env // 8)
+    comp = w["poses"] * 96 + (w["edges"] + 1) * 8 + w["edges"] + n_agent * 72 + items * 32
+    out = {"bound": "mfma", "kernel": "k_sweep", "achieved": round(flops / t / 1e12, 3), "peak": FP64_PEAK_TFLOPS,
+           "unit": "TFLOP/s", "frac": round(flops / t / 1e12 / FP64_PEAK_TFLOPS, 4),
+           "note": "FP64 VALU roof (FCL's scalar operation order; no MFMA)",
+           "compulsory_bytes": int(comp), "compulsory_gbs": round(comp / t / 1e9, 1),
+           "frac_hbm_compulsory": round(comp / t / 1e9 / HBM_PEAK_GBS, 4), "ms_per_launch": round(ms, 4),
+           "work": w, "traffic": None}
+    path = traffic_path or os.path.join(REPO, "profiles", "r15", "prm", "pmc_summary.json")
+    try:
+        summ = json.load(open(path))
+        tr = next(v["hbm_bytes_per_launch"] for k, v in summ.items() if "k_sweep" in k)
+        out.update({"traffic": int(tr), "traffic_gbs": round(tr / t / 1e9, 1),
+                    "frac_hbm_measured": round(tr / t / 1e9 / HBM_PEAK_GBS, 4),
+                    "traffic_over_compulsory": round(tr / comp, 2), "pmc_source": os.path.relpath(path, REPO)})
+    except (OSError, ValueError, StopIteration):
+        pass
+    if out["frac"] < max(out["frac_hbm_compulsory"], out.get("frac_hbm_measured") or 0.0):
+        out.update({"bound": "hbm", "achieved": out["compulsory_gbs"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": out["frac_hbm_compulsory"]})
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--n", type=int, default=100_000)
@@ -33,6 +68,7 @@ def main():
     ap.add_argument("--rooms", type=int, default=25)
     ap.add_argument("--cpu-n", type=int, default=3000)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--traffic", default=None, help="pmc_summary.json with k_sweep's traffic (default profiles/r15/prm)")
     ap.add_argument("--collide", default="split", choices=["split", "fused"])
     ap.add_argument("--bounds", default="blimp", choices=["blimp", "rooms"],
                     help="milestone x, y, z: blimp.inst's [-100, 100]^3 (one corner of the rooms) or the whole "
@@ -65,6 +101,11 @@ def main():
     E = len(res["edges"])
     ms = res["ms"]
     wall = min(walls)
+    # one more call with the sweep's work counters on (an atomic per wave: untimed)
+    mpt.prm_stats(True)
+    mpt.prm_connect(env, ag, 1, st, r2, sc.cc_dt)
+    work = mpt.prm_stats(False)
+    roof = sweep_roofline(work, ms["collision"], len(sc.agent_tris), int(env.info()["triangles"]), a.traffic)
     out = {
         "metric": "PRM roadmap construction (radius neighbours + edge collision checks), config 4",
         "value": a.n / wall, "unit": "milestones/s", "edges_checked_per_s": E / wall,
@@ -74,6 +115,7 @@ def main():
                    "free_fraction": float(1.0 - res["verdict"].mean()) if E else None,
                    "components": int(len(np.unique(res["comp"]))), "collide_mode": a.collide,
                    "bounds": a.bounds},
+        "roofline": roof,
     }
     if not a.no_cpu:
         sys.path.insert(0, os.path.join(REPO, "oracle"))
