@@ -991,20 +991,22 @@ __device__ __forceinline__ void tree_nn1_block(const PointTreeDev &T, const doub
 // steps of the one-node walk for a few more nodes visited; the result is the same exact 1-NN
 // (any visiting order is: only boxes whose lower bound exceeds the best are skipped).  The
 // stack holds at most ~14 entries a level (two sibling blocks of 7) + 2: 2 * 8 * 10 entries.
-constexpr int kPtG2 = 2 * kPtFan;
-constexpr int kPtStack2 = 2 * kPtFan * kPtMaxLevels;
-constexpr int64_t kPtNnW2MaxQueries = 262144;  // the two-node walk up to this many queries a launch
+constexpr int64_t kPtNnWideMaxQueries = 262144;  // the four-node walk up to this many queries a launch
 
-template <int D, int BS>
-__device__ __forceinline__ void tree_nn1_block2(const PointTreeDev &T, const double *__restrict__ q, int64_t nq,
+// NW nodes a step (2 or 4): 8 * NW lanes per query, the stack's top NW entries popped together
+template <int D, int BS, int NW>
+__device__ __forceinline__ void tree_nn1_blockn(const PointTreeDev &T, const double *__restrict__ q, int64_t nq,
                                                 int32_t *__restrict__ out_ids, double *__restrict__ out_d2,
                                                 int64_t blk, const int32_t *__restrict__ order) {
+    constexpr int kPtG2 = NW * kPtFan;                     // lanes per query
+    constexpr int kPtStack2 = NW * kPtFan * kPtMaxLevels;  // ~NW blocks of 7 a level
+    static_assert(kPtG2 <= 32, "ballot bits per group");
     __shared__ int32_t s_node[BS / kPtG2][kPtStack2];
     __shared__ float s_lb[BS / kPtG2][kPtStack2];
     const int64_t t = blk * BS + threadIdx.x;
     const int64_t slot = t / kPtG2;
     const int sub = (int)(t % kPtG2);
-    const int half = sub / kPtFan;  // 0: the top entry, 1: the one below it
+    const int half = sub / kPtFan;  // which popped entry: 0 the top, 1 the one below it, ...
     const int ls = sub % kPtFan;    // the child / point this lane takes
     const int grp = threadIdx.x / kPtG2;
     if (slot >= nq) return;  // whole groups leave together
@@ -1031,7 +1033,7 @@ __device__ __forceinline__ void tree_nn1_block2(const PointTreeDev &T, const dou
         __builtin_amdgcn_wave_barrier();
         const int base = (threadIdx.x & 63) & ~(kPtG2 - 1);
         while (sp > 0) {
-            const int np = sp >= 2 ? 2 : 1;
+            const int np = sp >= NW ? NW : sp;
             const bool have = half < np;
             int32_t code = 0;
             double lbs = 0.0;
@@ -1077,8 +1079,10 @@ __device__ __forceinline__ void tree_nn1_block2(const PointTreeDev &T, const dou
                 }
             }
             keep = keep && (double)lbf * (1.0 - 1e-12) <= bd;
-            const uint32_t gm = (uint32_t)(__ballot(keep) >> base) & 0xffffu;
-            const uint32_t m1 = gm >> kPtFan, mine = half ? m1 : (gm & 0xffu);
+            const uint32_t gm = (uint32_t)(__ballot(keep) >> base) & (uint32_t)((1ull << kPtG2) - 1);
+            const uint32_t mine = (gm >> (half * kPtFan)) & 0xffu;
+            // deeper entries' survivors go below: positions after every later half's
+            const int below = __popc(half + 1 < NW ? gm >> ((half + 1) * kPtFan) : 0u);
             int rank = 0;
 #pragma unroll
             for (int j = 0; j < kPtFan; ++j) {
@@ -1086,7 +1090,7 @@ __device__ __forceinline__ void tree_nn1_block2(const PointTreeDev &T, const dou
                 if (((mine >> j) & 1u) && (o > lbf || (o == lbf && j > ls))) ++rank;
             }
             if (keep) {
-                const int pos = sp + (half ? 0 : __popc(m1)) + rank;
+                const int pos = sp + below + rank;
                 s_node[grp][pos] = ((lev - 1) << 27) | (int32_t)c;
                 s_lb[grp][pos] = lbf;
             }
@@ -1115,7 +1119,7 @@ template <int D, int BS, int W>
 __global__ __launch_bounds__(BS) void k_tree_nn1(PointTreeDev T, const double *__restrict__ q, int64_t nq,
                                                  int32_t *__restrict__ out_ids, double *__restrict__ out_d2,
                                                  const int32_t *__restrict__ order) {
-    if constexpr (W >= 2) tree_nn1_block2<D, BS>(T, q, nq, out_ids, out_d2, blockIdx.x, order);
+    if constexpr (W >= 2) tree_nn1_blockn<D, BS, W>(T, q, nq, out_ids, out_d2, blockIdx.x, order);
     else tree_nn1_block<D, BS>(T, q, nq, out_ids, out_d2, blockIdx.x, order);
 }
 
@@ -1132,7 +1136,7 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(D >= 15 ? 4 
     const int64_t job = xcd + kXcds * (slot / blocks_per_job);
     if (job >= n_jobs) return;
     const PtJob &J = jobs[job];
-    if constexpr (W >= 2) tree_nn1_block2<D, BS>(J.T, J.q, nq, J.ids, J.d2, slot % blocks_per_job, J.order);
+    if constexpr (W >= 2) tree_nn1_blockn<D, BS, W>(J.T, J.q, nq, J.ids, J.d2, slot % blocks_per_job, J.order);
     else tree_nn1_block<D, BS>(J.T, J.q, nq, J.ids, J.d2, slot % blocks_per_job, J.order);
 }
 
@@ -1627,18 +1631,20 @@ void launch_tree_nn1(const PointTreeDev &T, const double *q, int64_t nq, int32_t
     static const int bs = getenv("MPT_PT_NN1_BLOCK") ? atoi(getenv("MPT_PT_NN1_BLOCK")) : 64;
     // nodes expanded per step: as the joint launch (MPT_PT_NN_W forces one)
     static const int w_env = getenv("MPT_PT_NN_W") ? atoi(getenv("MPT_PT_NN_W")) : 0;
-    const int w = w_env > 0 ? w_env : (nq <= kPtNnW2MaxQueries ? 2 : 1);
+    const int w = w_env > 0 ? w_env : (nq <= kPtNnWideMaxQueries ? 4 : 1);
     if (bs == 256)
         w == 1 ? launch_tree_nn1_bs<256, 1>(T, q, nq, ids, d2, stream, order)
-               : launch_tree_nn1_bs<256, 2>(T, q, nq, ids, d2, stream, order);
+               : (w == 2 ? launch_tree_nn1_bs<256, 2>(T, q, nq, ids, d2, stream, order)
+                         : launch_tree_nn1_bs<256, 4>(T, q, nq, ids, d2, stream, order));
     else
         w == 1 ? launch_tree_nn1_bs<64, 1>(T, q, nq, ids, d2, stream, order)
-               : launch_tree_nn1_bs<64, 2>(T, q, nq, ids, d2, stream, order);
+               : (w == 2 ? launch_tree_nn1_bs<64, 2>(T, q, nq, ids, d2, stream, order)
+                         : launch_tree_nn1_bs<64, 4>(T, q, nq, ids, d2, stream, order));
 }
 
 template <int BS, int W>
 static void launch_tree_nn1_jobs_bs(const PtJob *d_jobs, int32_t n_jobs, int32_t d, int64_t nq, hipStream_t stream) {
-    const int64_t bpj = (nq * kPtFan * (W >= 2 ? 2 : 1) + BS - 1) / BS;
+    const int64_t bpj = (nq * kPtFan * W + BS - 1) / BS;
     const int64_t groups = (n_jobs + kXcds - 1) / kXcds;
     const dim3 grid((unsigned)(kXcds * groups * bpj));
     switch (d) {
@@ -1652,13 +1658,15 @@ static void launch_tree_nn1_jobs_bs(const PtJob *d_jobs, int32_t n_jobs, int32_t
 
 void launch_tree_nn1_jobs(const PtJob *d_jobs, int32_t n_jobs, int32_t d, int64_t nq, hipStream_t stream) {
     if (nq <= 0 || n_jobs <= 0) return;
-    // The two-node walk halves a query's dependent steps for ~+15 % more nodes: it pays when
-    // the launch leaves the chip waiting on its slowest waves (config 5 at 32 seeds, 131 072
-    // queries: 1.96 -> 1.79 ms) and costs when the launch keeps every SIMD busy (256 seeds,
-    // 1 M queries: 8.98 -> 11.1 ms).  MPT_PT_NN_W = 1 / 2 forces one (A/B).
+    // The multi-node walk cuts a query's dependent steps (four nodes a step: a quarter) for more
+    // nodes visited: it pays when the launch leaves the chip waiting on its slowest waves and
+    // costs when the launch keeps every SIMD busy.  Config 5 round time by nodes a step (1 / 2 /
+    // 4): 32 seeds (131 072 queries) 3.24 / 2.75 / 2.26 ms, 64 seeds 5.27 / 4.65 / 4.07 ms, 256
+    // seeds (1 M queries) 13.66 / 13.86 / 13.97 ms.  MPT_PT_NN_W = 1 / 2 / 4 forces one (A/B).
     static const int w_env = getenv("MPT_PT_NN_W") ? atoi(getenv("MPT_PT_NN_W")) : 0;
-    const int w = w_env > 0 ? w_env : ((int64_t)n_jobs * nq <= kPtNnW2MaxQueries ? 2 : 1);
+    const int w = w_env > 0 ? w_env : ((int64_t)n_jobs * nq <= kPtNnWideMaxQueries ? 4 : 1);
     if (w == 1) launch_tree_nn1_jobs_bs<64, 1>(d_jobs, n_jobs, d, nq, stream);
+    else if (w == 4) launch_tree_nn1_jobs_bs<64, 4>(d_jobs, n_jobs, d, nq, stream);
     else launch_tree_nn1_jobs_bs<64, 2>(d_jobs, n_jobs, d, nq, stream);
 }
 
