@@ -221,8 +221,12 @@ def compulsory_bytes(stage, c, K, n0, d, pmax, geo, nn_mode):
             return inc_build_bytes(n0, min(K, n0), d)
         return n0 * (8 * d + rec + 8) + (n0 // 2) * 12  # nodes in, records out, cell ids, counts / starts
     if stage == "nn_query":
-        index = n0 * rec + (n0 // 2) * 4 if nn_mode == "grid" else n0 * (8 * d + 4) + (n0 // 7) * 8 * d
-        return K * (8 * d + 12) + index
+        if nn_mode != "grid":
+            # a pruned search over a tree that covers part of the sampling box (config 5: most
+            # samples lie far from the tree and touch its boundary leaves only) need not read the
+            # whole index: its queries and results (index bytes reported beside, index_bytes)
+            return K * (8 * d + 12)
+        return K * (8 * d + 12) + n0 * rec + (n0 // 2) * 4
     if stage == "steer":
         # ids, neighbour rows, end states, counts, verdict init; every (pose, link) unit's pose
         # and its FCL relative transform (96 B each, k_steer writes both); the live list
@@ -363,6 +367,7 @@ def joint_stage_table(times, c, K, nj, n_tot, d, pmax, geo, summ):
             f = None
         if s == "nn_build":
             b = inc_build_bytes(n_tot + K * nj, K * nj, d)
+        index_b = n_tot * (8 * d + 4) + (n_tot // 7) * 8 * d if s == "nn_query" else None
         if b is None:
             continue
         t = ms * 1e-3
@@ -370,6 +375,8 @@ def joint_stage_table(times, c, K, nj, n_tot, d, pmax, geo, summ):
               "compulsory_gbs": round(b / t / 1e9, 1), "frac_hbm_compulsory": round(b / t / 1e9 / HBM_PEAK_GBS, 4),
               "launch": f"one joint launch per kernel for {nj} seeds x {K} extensions"
                         + (f" ({n_sub} collide sub-batches)" if s == "collide" else "")}
+        if index_b:
+            st["index_bytes"] = int(index_b)
         trs = [pmc_traffic(summ, k) for k in JOINT_STAGE_KERNELS.get(s, [])]
         if trs and all(x is not None for x in trs):
             tr = sum(trs) * (n_sub if s == "collide" else 1)

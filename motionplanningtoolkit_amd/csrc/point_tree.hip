@@ -1000,7 +1000,7 @@ __device__ __forceinline__ void tree_nn1_blockn(const PointTreeDev &T, const dou
                                                 int64_t blk, const int32_t *__restrict__ order) {
     constexpr int kPtG2 = NW * kPtFan;                     // lanes per query
     constexpr int kPtStack2 = NW * kPtFan * kPtMaxLevels;  // ~NW blocks of 7 a level
-    static_assert(kPtG2 <= 32, "ballot bits per group");
+    static_assert(kPtG2 <= 64, "ballot bits per group");
     __shared__ int32_t s_node[BS / kPtG2][kPtStack2];
     __shared__ float s_lb[BS / kPtG2][kPtStack2];
     const int64_t t = blk * BS + threadIdx.x;
@@ -1079,10 +1079,10 @@ __device__ __forceinline__ void tree_nn1_blockn(const PointTreeDev &T, const dou
                 }
             }
             keep = keep && (double)lbf * (1.0 - 1e-12) <= bd;
-            const uint32_t gm = (uint32_t)(__ballot(keep) >> base) & (uint32_t)((1ull << kPtG2) - 1);
-            const uint32_t mine = (gm >> (half * kPtFan)) & 0xffu;
+            const uint64_t gm = (__ballot(keep) >> base) & (kPtG2 == 64 ? ~0ull : ((1ull << kPtG2) - 1));
+            const uint32_t mine = (uint32_t)(gm >> (half * kPtFan)) & 0xffu;
             // deeper entries' survivors go below: positions after every later half's
-            const int below = __popc(half + 1 < NW ? gm >> ((half + 1) * kPtFan) : 0u);
+            const int below = __popcll(half + 1 < NW ? gm >> ((half + 1) * kPtFan) : 0ull);
             int rank = 0;
 #pragma unroll
             for (int j = 0; j < kPtFan; ++j) {
@@ -1094,7 +1094,7 @@ __device__ __forceinline__ void tree_nn1_blockn(const PointTreeDev &T, const dou
                 s_node[grp][pos] = ((lev - 1) << 27) | (int32_t)c;
                 s_lb[grp][pos] = lbf;
             }
-            sp += __popc(gm);
+            sp += __popcll(gm);
             __builtin_amdgcn_wave_barrier();
         }
     }
@@ -1667,6 +1667,7 @@ void launch_tree_nn1_jobs(const PtJob *d_jobs, int32_t n_jobs, int32_t d, int64_
     const int w = w_env > 0 ? w_env : ((int64_t)n_jobs * nq <= kPtNnWideMaxQueries ? 4 : 1);
     if (w == 1) launch_tree_nn1_jobs_bs<64, 1>(d_jobs, n_jobs, d, nq, stream);
     else if (w == 4) launch_tree_nn1_jobs_bs<64, 4>(d_jobs, n_jobs, d, nq, stream);
+    else if (w == 8) launch_tree_nn1_jobs_bs<64, 8>(d_jobs, n_jobs, d, nq, stream);
     else launch_tree_nn1_jobs_bs<64, 2>(d_jobs, n_jobs, d, nq, stream);
 }
 

@@ -38,7 +38,10 @@ def sweep_roofline(w, ms, n_agent, n_env, traffic_path):
     t = ms * 1e-3
     flops = 750.0 * w["sat_tests"] + 27.0 * w["gate_tests"] + 45.0 * 64 * w["waves"]
     items = n_env + -(-n_env // 8)
-    comp = w["poses"] * 96 + (w["edges"] + 1) * 8 + w["edges"] + n_agent * 72 + items * 32
+    # an edge's poses share one rotation: its first pose whole (96 B), every other pose's
+    # translation (24 B; k_sweep reads no more of it)
+    comp = (w["edges"] * 96 + (w["poses"] - w["edges"]) * 24 + (w["edges"] + 1) * 8 + w["edges"] + n_agent * 72
+            + items * 32)
     out = {"bound": "mfma", "kernel": "k_sweep", "achieved": round(flops / t / 1e12, 3), "peak": FP64_PEAK_TFLOPS,
            "unit": "TFLOP/s", "frac": round(flops / t / 1e12 / FP64_PEAK_TFLOPS, 4),
            "note": "FP64 VALU roof (FCL's scalar operation order; no MFMA)",

@@ -4,7 +4,7 @@ HBM bytes per launch = (2 * FETCH_SIZE + WRITE_SIZE) * 1024, the correction
 /opt/skills/guides/MI355X_MICROARCH.md (§HBM) prescribes for gfx950: FETCH_SIZE reports
 half the bytes of a wide coalesced read.  The doubling is calibrated for 16-B-per-lane
 vector loads only; kernels whose reads are scalar (s_load) loads are marked as such in
-DESIGN.md.  Usage: python scripts/pmc_summary.py gpurun_out/prof_r01 profiles/r01
+DESIGN.md.  Usage: python scripts/pmc_summary.py gpurun_out/prof_r01 profiles/r01 [window-start window-end]
 """
 import collections
 import csv
@@ -14,13 +14,35 @@ import shutil
 import sys
 
 
-def main(src, dst):
+def window(rows, start, end):
+    """Dispatches from the first whose kernel name contains `start` ("last:<name>": the last
+    such) up to (not including) the first after it whose name contains `end` (or the end) --
+    e.g. config 5's last joint round only ("last:k_sample_jobs"): the round whose hipEvent stage
+    times bench.py reports, at the same tree sizes as its compulsory bytes (an average over the
+    run's growing trees does not match either)."""
+    rows = sorted(rows, key=lambda r: int(r["Dispatch_Id"]))
+    if start.startswith("last:"):  # from the last dispatch matching the marker
+        start = start[5:]
+        hits = [i for i, r in enumerate(rows) if start in r["Kernel_Name"]]
+        i0 = hits[-1] if hits else None
+    else:
+        i0 = next((i for i, r in enumerate(rows) if start in r["Kernel_Name"]), None)
+    if i0 is None:
+        return rows
+    i1 = next((i for i in range(i0, len(rows)) if end and end in rows[i]["Kernel_Name"]), len(rows))
+    return rows[i0:i1]
+
+
+def main(src, dst, start=None, end=None):
     os.makedirs(dst, exist_ok=True)
     out = {}
     for tag, cn in (("fetch", "FETCH_SIZE"), ("write", "WRITE_SIZE")):
         path = os.path.join(src, tag, "run_counter_collection.csv")
         agg = collections.defaultdict(list)
-        for r in csv.DictReader(open(path)):
+        rows = list(csv.DictReader(open(path)))
+        if start:
+            rows = window(rows, start, end)
+        for r in rows:
             agg[r["Kernel_Name"]].append(float(r["Counter_Value"]))
         for k, v in agg.items():
             out.setdefault(k, {})[cn] = sum(v) / len(v)
@@ -37,4 +59,5 @@ def main(src, dst):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1], sys.argv[2])
+    # optional: a dispatch window (see window()), e.g. k_sample_jobs "k_sample("
+    main(sys.argv[1], sys.argv[2], *(sys.argv[3:5]))
