@@ -89,6 +89,8 @@ struct PtIncJob {
     float *boxes;
     uint64_t *nkeys;              // the new points' sorted codes and rows
     int32_t *nvals;
+    uint64_t *ckeys;              // scratch [kPtIncSeg]: the new points sorted by chunks of 512
+    int32_t *cvals;
     int64_t *nidx;                // points the last build indexed; set to n by this build
     unsigned long long *ibox;     // persistent box of the indexed points (order keys)
     const double *q;              // queries [nq][d] to order by code, or nullptr
@@ -154,6 +156,8 @@ private:
     double *ipts[2] = {nullptr, nullptr};
     uint64_t *inkeys = nullptr;
     int32_t *invals = nullptr, *iqorder = nullptr;
+    uint64_t *ickeys = nullptr;
+    int32_t *icvals = nullptr;
     int64_t *inidx = nullptr;
     unsigned long long *ibox = nullptr;
     IncPlan *iplan = nullptr;

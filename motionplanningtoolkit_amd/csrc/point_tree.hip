@@ -502,8 +502,17 @@ __device__ __forceinline__ uint64_t inc_code(const IncPlan *__restrict__ P, cons
     return c;
 }
 
+// bitwise, not short-circuit: the && / || form compiled to divergent branches around every
+// compare-exchange of the sorts
 __device__ __forceinline__ bool inc_less(uint64_t ka, int32_t va, uint64_t kb, int32_t vb) {
-    return ka < kb || (ka == kb && va < vb);
+    return (ka < kb) | ((ka == kb) & (va < vb));
+}
+// compare-exchange against a partner: keep the smaller pair (keep_min) or the larger, by
+// selects.  Pairs are distinct but for padding, and swapping equal pairs changes nothing.
+__device__ __forceinline__ void inc_cx(uint64_t &k, int32_t &v, uint64_t pk, int32_t pv, bool keep_min) {
+    const bool sw = keep_min == inc_less(pk, pv, k, v);
+    k = sw ? pk : k;
+    v = sw ? pv : v;
 }
 
 constexpr int kIncSortThreads = 1024;
@@ -512,13 +521,12 @@ constexpr int kIncSortThreads = 1024;
 // (and their box into ibox); blockIdx.x = 1: the round's queries -> code order (qorder).
 // (code, row) pairs order totally, so the result does not depend on the sort.
 template <int D>
-__device__ __forceinline__ void pt_inc_sort(const PtIncJob &J) {
+__device__ __forceinline__ void pt_inc_sort(const PtIncJob &J, int seg) {
     __shared__ uint64_t sk[kPtIncSeg];
     __shared__ int32_t sv[kPtIncSeg];
     __shared__ unsigned long long s_min[kPtMaxDim], s_max[kPtMaxDim];
     // the plan in LDS: its fields were per-lane flat loads, each waited on, inside the code loop
     __shared__ IncPlan s_plan;
-    const int seg = blockIdx.x;
     const int t = threadIdx.x;
     int64_t m = 0, base = 0;
     const double *src = nullptr;
@@ -621,11 +629,7 @@ __device__ __forceinline__ void pt_inc_sort(const PtIncJob &J) {
                     const int i = t * E + a, l = i ^ j;
                     const uint64_t pk = sk[l];
                     const int32_t pv = sv[l];
-                    const bool keep_min = (i < l) == ((i & k) == 0);
-                    if (keep_min ? inc_less(pk, pv, key[a], val[a]) : inc_less(key[a], val[a], pk, pv)) {
-                        key[a] = pk;
-                        val[a] = pv;
-                    }
+                    inc_cx(key[a], val[a], pk, pv, (i < l) == ((i & k) == 0));
                 }
             } else if (j >= E) {
                 const int lm = j / E;
@@ -634,11 +638,7 @@ __device__ __forceinline__ void pt_inc_sort(const PtIncJob &J) {
                 for (int a = 0; a < E; ++a) {
                     const uint64_t pk = __shfl_xor(key[a], lm);
                     const int32_t pv = __shfl_xor(val[a], lm);
-                    const bool keep_min = lower == (((t * E + a) & k) == 0);
-                    if (keep_min ? inc_less(pk, pv, key[a], val[a]) : inc_less(key[a], val[a], pk, pv)) {
-                        key[a] = pk;
-                        val[a] = pv;
-                    }
+                    inc_cx(key[a], val[a], pk, pv, lower == (((t * E + a) & k) == 0));
                 }
             } else {
                 // partners within the thread's registers: j is 4, 2 or 1 (compile-time indices)
@@ -650,14 +650,13 @@ __device__ __forceinline__ void pt_inc_sort(const PtIncJob &J) {
                         const int b = a ^ jj;
                         if (b < a) continue;
                         const bool up = ((t * E + a) & k) == 0;
-                        if (up ? inc_less(key[b], val[b], key[a], val[a]) : inc_less(key[a], val[a], key[b], val[b])) {
-                            const uint64_t tk = key[a];
-                            const int32_t tv = val[a];
-                            key[a] = key[b];
-                            val[a] = val[b];
-                            key[b] = tk;
-                            val[b] = tv;
-                        }
+                        const bool sw = up == inc_less(key[b], val[b], key[a], val[a]);
+                        const uint64_t ka = key[a], kb = key[b];
+                        const int32_t va = val[a], vb = val[b];
+                        key[a] = sw ? kb : ka;
+                        val[a] = sw ? vb : va;
+                        key[b] = sw ? ka : kb;
+                        val[b] = sw ? va : vb;
                     }
                 }
             }
@@ -687,9 +686,203 @@ __device__ __forceinline__ void pt_inc_sort(const PtIncJob &J) {
 }
 
 template <int D>
-__global__ __launch_bounds__(kIncSortThreads) void k_pt_inc_sort(IncJobs jobs) {
-    if (jobs.table) pt_inc_sort<D>(jobs.table[blockIdx.y]);
-    else pt_inc_sort<D>(jobs.one);
+__global__ __launch_bounds__(kIncSortThreads) void k_pt_inc_sort(IncJobs jobs, int seg0) {
+    if (jobs.table) pt_inc_sort<D>(jobs.table[blockIdx.y], seg0 + (int)blockIdx.x);
+    else pt_inc_sort<D>(jobs.one, seg0 + (int)blockIdx.x);
+}
+
+// The new points' sort over many CUs: one workgroup per tree runs the 4096-element bitonic
+// network on one CU (~78 stages), which leaves most of the chip idle when there are few trees.
+// Instead: the codes one thread a point (k_pt_inc_ncodes); each wave sorts a chunk of 512 (8
+// elements a lane: partners 8+ apart by lane shuffles, closer ones in registers; no LDS, no
+// barriers); a third kernel places every element at its rank, its index in its own chunk plus,
+// per other chunk, the count of smaller (code, row) pairs there (a fixed-step binary search,
+// the chunks' searches interleaved).  (code, row) pairs are distinct, so the ranks are a
+// permutation and the result is the one total order any sort gives.
+constexpr int kIncChunk = 512;
+constexpr int kIncChunks = kPtIncSeg / kIncChunk;
+constexpr int kIncChunkWaves = 4;  // chunks a workgroup sorts
+constexpr int kIncCsortMaxTrees = 128;  // joint builds of fewer trees use the chunked sort
+static_assert(kIncChunks % kIncChunkWaves == 0, "whole workgroups");
+
+// the new points' codes and rows (one thread a point) into nkeys / nvals, in row order, and
+// their box into ibox
+template <int D>
+__device__ __forceinline__ void pt_inc_ncodes(const PtIncJob &J, const IncPlan &P) {
+    if (J.full) return;
+    const int64_t nd = *J.T.n_dev, n = nd < J.T.n_upper ? nd : J.T.n_upper;
+    const int64_t base = *J.nidx;
+    int64_t m = n - base;
+    m = m < 0 ? 0 : (m > kPtIncSeg ? kPtIncSeg : m);
+    const int i = (int)blockIdx.x * (int)blockDim.x + (int)threadIdx.x;
+    if ((int64_t)blockIdx.x * blockDim.x >= m) return;  // block-uniform
+    const bool live = i < m;
+    unsigned long long mn[D], mx[D];
+    if (live) {
+        double x[D];
+        const int64_t row = base + i;
+#pragma unroll
+        for (int j = 0; j < D; ++j) x[j] = J.pts[row * D + j];
+        J.nkeys[i] = inc_code<D>(&P, x);
+        J.nvals[i] = (int32_t)row;
+#pragma unroll
+        for (int j = 0; j < D; ++j) mn[j] = mx[j] = order_key_pt(x[j]);
+    } else {
+#pragma unroll
+        for (int j = 0; j < D; ++j) {
+            mn[j] = ~0ull;
+            mx[j] = 0ull;
+        }
+    }
+    // the persistent box of the indexed points (MPT_NN_AUTO's spread)
+#pragma unroll
+    for (int j = 0; j < D; ++j) {
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) {
+            const unsigned long long omn = __shfl_xor(mn[j], off), omx = __shfl_xor(mx[j], off);
+            mn[j] = omn < mn[j] ? omn : mn[j];
+            mx[j] = omx > mx[j] ? omx : mx[j];
+        }
+    }
+    if ((threadIdx.x & 63) == 0) {
+#pragma unroll
+        for (int j = 0; j < D; ++j) {
+            atomicMin(J.ibox + j, mn[j]);
+            atomicMax(J.ibox + kPtMaxDim + j, mx[j]);
+        }
+    }
+}
+
+template <int D>
+__global__ __launch_bounds__(256) void k_pt_inc_ncodes(IncJobs jobs) {
+    __shared__ IncPlan s_plan;
+    const PtIncJob &J = jobs.table ? jobs.table[blockIdx.y] : jobs.one;
+    for (int w = threadIdx.x; w < (int)(sizeof(IncPlan) / 4); w += blockDim.x)
+        reinterpret_cast<uint32_t *>(&s_plan)[w] = reinterpret_cast<const uint32_t *>(J.plan)[w];
+    __syncthreads();
+    if (jobs.table) pt_inc_ncodes<D>(jobs.table[blockIdx.y], s_plan);
+    else pt_inc_ncodes<D>(jobs.one, s_plan);
+}
+
+// one chunk of 512 (code, row) pairs a wave: nkeys / nvals -> ckeys / cvals
+__device__ __forceinline__ void pt_inc_csort(const PtIncJob &J) {
+    if (J.full) return;
+    const int64_t nd = *J.T.n_dev, n = nd < J.T.n_upper ? nd : J.T.n_upper;
+    int64_t m = n - *J.nidx;
+    m = m < 0 ? 0 : (m > kPtIncSeg ? kPtIncSeg : m);
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+    const int c0 = ((int)blockIdx.x * kIncChunkWaves + wave) * kIncChunk;
+    if (c0 >= m) return;
+    constexpr int E = kIncChunk / 64;
+    uint64_t key[E];
+    int32_t val[E];
+#pragma unroll
+    for (int a = 0; a < E; ++a) {
+        const int i = c0 + lane * E + a;
+        const bool live = i < m;
+        key[a] = live ? J.nkeys[i] : ~0ull;  // real codes use 63 bits: padding sorts last
+        val[a] = live ? J.nvals[i] : 0x7fffffff;
+    }
+#pragma unroll 1
+    for (int k = 2; k <= kIncChunk; k <<= 1) {
+#pragma unroll 1
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            if (j >= E) {
+                const int lm = j / E;
+                const bool lower = (lane & lm) == 0;
+#pragma unroll
+                for (int a = 0; a < E; ++a) {
+                    const uint64_t pk = __shfl_xor(key[a], lm);
+                    const int32_t pv = __shfl_xor(val[a], lm);
+                    inc_cx(key[a], val[a], pk, pv, lower == (((lane * E + a) & k) == 0));
+                }
+            } else {
+#pragma unroll
+                for (int jj = E / 2; jj > 0; jj >>= 1) {
+                    if (jj != j) continue;
+#pragma unroll
+                    for (int a = 0; a < E; ++a) {
+                        const int b = a ^ jj;
+                        if (b < a) continue;
+                        const bool up = ((lane * E + a) & k) == 0;
+                        const bool sw = up == inc_less(key[b], val[b], key[a], val[a]);
+                        const uint64_t ka = key[a], kb = key[b];
+                        const int32_t va = val[a], vb = val[b];
+                        key[a] = sw ? kb : ka;
+                        val[a] = sw ? vb : va;
+                        key[b] = sw ? ka : kb;
+                        val[b] = sw ? va : vb;
+                    }
+                }
+            }
+        }
+    }
+    // the whole chunk, padding included (the rank search reads 512 per chunk)
+#pragma unroll
+    for (int a = 0; a < E; ++a) {
+        J.ckeys[c0 + lane * E + a] = key[a];
+        J.cvals[c0 + lane * E + a] = val[a];
+    }
+}
+
+__global__ __launch_bounds__(64 * kIncChunkWaves) void k_pt_inc_csort(IncJobs jobs) {
+    if (jobs.table) pt_inc_csort(jobs.table[blockIdx.y]);
+    else pt_inc_csort(jobs.one);
+}
+
+__device__ __forceinline__ void pt_inc_crank(const PtIncJob &J) {
+    if (J.full) return;
+    const int64_t nd = *J.T.n_dev, n = nd < J.T.n_upper ? nd : J.T.n_upper;
+    int64_t m = n - *J.nidx;
+    m = m < 0 ? 0 : (m > kPtIncSeg ? kPtIncSeg : m);
+    const int e = (int)blockIdx.x * (int)blockDim.x + (int)threadIdx.x;
+    if (e >= m) return;
+    const int nch = (int)((m + kIncChunk - 1) / kIncChunk);
+    const uint64_t key = J.ckeys[e];
+    const int32_t val = J.cvals[e];
+    // per chunk: the count of its pairs below (key, val); for the element's own chunk that is
+    // its index there.  Fixed steps, the chunks' loads issued together.
+    int pos[kIncChunks];
+#pragma unroll
+    for (int c = 0; c < kIncChunks; ++c) pos[c] = 0;
+    // (every chunk's loads unconditional -- a branch per chunk made each load wait alone;
+    // chunks past nch read scratch and are masked out of the sum)
+    const uint64_t *__restrict__ ck = J.ckeys;
+    const int32_t *__restrict__ cv = J.cvals;
+#pragma unroll
+    for (int st = kIncChunk / 2; st > 0; st >>= 1) {
+        uint64_t pk[kIncChunks];
+        int32_t pv[kIncChunks];
+#pragma unroll
+        for (int c = 0; c < kIncChunks; ++c) {
+            const int q = c * kIncChunk + pos[c] + st - 1;
+            pk[c] = ck[q];
+            pv[c] = cv[q];
+        }
+#pragma unroll
+        for (int c = 0; c < kIncChunks; ++c) pos[c] += inc_less(pk[c], pv[c], key, val) ? st : 0;
+    }
+    int rank = 0;
+    {
+        uint64_t pk[kIncChunks];
+        int32_t pv[kIncChunks];
+#pragma unroll
+        for (int c = 0; c < kIncChunks; ++c) {
+            const int q = c * kIncChunk + pos[c];
+            pk[c] = ck[q];
+            pv[c] = cv[q];
+        }
+#pragma unroll
+        for (int c = 0; c < kIncChunks; ++c)
+            rank += c < nch ? pos[c] + (inc_less(pk[c], pv[c], key, val) ? 1 : 0) : 0;
+    }
+    J.nkeys[rank] = key;
+    J.nvals[rank] = val;
+}
+
+__global__ __launch_bounds__(256) void k_pt_inc_crank(IncJobs jobs) {
+    if (jobs.table) pt_inc_crank(jobs.table[blockIdx.y]);
+    else pt_inc_crank(jobs.one);
 }
 
 // number of a's among the first p elements of merge(a, b), an a before a b of the same key
@@ -1221,7 +1414,7 @@ PointTree::~PointTree() {
         if (p) (void)hipFree(p);
     for (void *p : {(void *)ikeys[0], (void *)ikeys[1], (void *)iids[0], (void *)iids[1], (void *)ipts[0],
                     (void *)ipts[1], (void *)inkeys, (void *)invals, (void *)iqorder, itemp, (void *)inidx,
-                    (void *)ibox, (void *)iplan})
+                    (void *)ibox, (void *)iplan, (void *)ickeys, (void *)icvals})
         if (p) (void)hipFree(p);
 }
 
@@ -1460,6 +1653,10 @@ void PointTree::inc_reserve(int64_t c, int32_t d) {
     hip_check(hipMalloc(&inkeys, sizeof(uint64_t) * c), "inc new keys");
     hip_check(hipMalloc(&invals, sizeof(int32_t) * c), "inc new rows");
     hip_check(hipMalloc(&iqorder, sizeof(int32_t) * kPtIncSeg), "inc query order");
+    if (!ickeys) {
+        hip_check(hipMalloc(&ickeys, sizeof(uint64_t) * kPtIncSeg), "inc chunk keys");
+        hip_check(hipMalloc(&icvals, sizeof(int32_t) * kPtIncSeg), "inc chunk rows");
+    }
     size_t tb = 0;
     hip_check(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, ikeys[0], inkeys, iids[0], invals, (int)c, 0,
                                                   kPtIncBits),
@@ -1541,6 +1738,8 @@ PtIncJob PointTree::prepare_inc(const double *pts, int64_t n_upper, const int64_
     J.boxes = boxes;
     J.nkeys = inkeys;
     J.nvals = invals;
+    J.ckeys = ickeys;
+    J.cvals = icvals;
     J.nidx = inidx;
     J.ibox = ibox;
     J.q = iq_on ? q : nullptr;
@@ -1565,9 +1764,29 @@ void launch_tree_inc_jobs(const PtIncJob *d_jobs, const PtIncJob *h_jobs, int32_
     for (int32_t j = 0; j < n; ++j) max_n = std::max(max_n, h_jobs[j].T.n_upper);
     auto by_d = [&](auto k3, auto k7, auto k15) { return d == 3 ? k3 : d == 7 ? k7 : k15; };
     if (d != 3 && d != 7 && d != 15) throw Error{1, "point tree: state dim must be 3, 7 or 15"};
-    hipLaunchKernelGGL(by_d(k_pt_inc_sort<3>, k_pt_inc_sort<7>, k_pt_inc_sort<15>), dim3(2, n), dim3(kIncSortThreads),
-                       0, stream, js);
-    hip_check(hipGetLastError(), "k_pt_inc_sort");
+    // the chunked sort while the one-workgroup sorts would leave most CUs idle: config 5 at 32
+    // trees 0.347 -> 0.294 ms a build; at 256 trees (one sort per CU) 1.74 -> 1.86 ms, the rank
+    // searches' loads costing more than the network they replace.  MPT_PT_CSORT=0 / 1 forces.
+    static const int csort_env = getenv("MPT_PT_CSORT") ? atoi(getenv("MPT_PT_CSORT")) : -1;
+    const bool csort = csort_env >= 0 ? csort_env == 1 : n < kIncCsortMaxTrees;
+    bool any_q = false;
+    for (int32_t j = 0; j < n; ++j) any_q = any_q || h_jobs[j].q;
+    if (csort) {
+        hipLaunchKernelGGL(by_d(k_pt_inc_ncodes<3>, k_pt_inc_ncodes<7>, k_pt_inc_ncodes<15>),
+                           dim3(kPtIncSeg / 256, n), dim3(256), 0, stream, js);
+        hip_check(hipGetLastError(), "k_pt_inc_ncodes");
+        hipLaunchKernelGGL(k_pt_inc_csort, dim3(kIncChunks / kIncChunkWaves, n), dim3(64 * kIncChunkWaves), 0, stream,
+                           js);
+        hip_check(hipGetLastError(), "k_pt_inc_csort");
+        hipLaunchKernelGGL(k_pt_inc_crank, dim3(kPtIncSeg / 256, n), dim3(256), 0, stream, js);
+        hip_check(hipGetLastError(), "k_pt_inc_crank");
+    }
+    if (!csort || any_q) {
+        // blockIdx.x + seg0: 0 = the new points, 1 = the queries
+        hipLaunchKernelGGL(by_d(k_pt_inc_sort<3>, k_pt_inc_sort<7>, k_pt_inc_sort<15>), dim3(csort ? 1 : 2, n),
+                           dim3(kIncSortThreads), 0, stream, js, csort ? 1 : 0);
+        hip_check(hipGetLastError(), "k_pt_inc_sort");
+    }
     if (dbg && h_jobs[0].dbg) {
         std::vector<unsigned long long> h((size_t)8 * n);
         hip_check(hipStreamSynchronize(stream), "dbg sync");
