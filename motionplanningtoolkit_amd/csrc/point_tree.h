@@ -91,6 +91,7 @@ struct PtIncJob {
     int32_t *nvals;
     uint64_t *ckeys;              // scratch [kPtIncSeg]: the new points sorted by chunks of 512
     int32_t *cvals;
+    int32_t *npos;                // scratch [kPtIncSeg]: the sorted new points' output places
     int64_t *nidx;                // points the last build indexed; set to n by this build
     unsigned long long *ibox;     // persistent box of the indexed points (order keys)
     const double *q;              // queries [nq][d] to order by code, or nullptr
@@ -157,7 +158,7 @@ private:
     uint64_t *inkeys = nullptr;
     int32_t *invals = nullptr, *iqorder = nullptr;
     uint64_t *ickeys = nullptr;
-    int32_t *icvals = nullptr;
+    int32_t *icvals = nullptr, *inpos = nullptr;
     int64_t *inidx = nullptr;
     unsigned long long *ibox = nullptr;
     IncPlan *iplan = nullptr;

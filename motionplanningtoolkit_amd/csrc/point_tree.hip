@@ -702,7 +702,6 @@ __global__ __launch_bounds__(kIncSortThreads) void k_pt_inc_sort(IncJobs jobs, i
 constexpr int kIncChunk = 512;
 constexpr int kIncChunks = kPtIncSeg / kIncChunk;
 constexpr int kIncChunkWaves = 4;  // chunks a workgroup sorts
-constexpr int kIncCsortMaxTrees = 128;  // joint builds of fewer trees use the chunked sort
 static_assert(kIncChunks % kIncChunkWaves == 0, "whole workgroups");
 
 // the new points' codes and rows (one thread a point) into nkeys / nvals, in row order, and
@@ -830,6 +829,52 @@ __global__ __launch_bounds__(64 * kIncChunkWaves) void k_pt_inc_csort(IncJobs jo
     else pt_inc_csort(jobs.one);
 }
 
+// NC: the chunks searched (the whole set: 16 only when more than 8 are live)
+template <int NC>
+__device__ __forceinline__ void pt_inc_crank_n(const PtIncJob &J, int64_t m, int e) {
+    const int nch = (int)((m + kIncChunk - 1) / kIncChunk);
+    const uint64_t key = J.ckeys[e];
+    const int32_t val = J.cvals[e];
+    // per chunk: the count of its pairs below (key, val); for the element's own chunk that is
+    // its index there.  Fixed steps, the chunks' loads issued together.
+    int pos[NC];
+#pragma unroll
+    for (int c = 0; c < NC; ++c) pos[c] = 0;
+    // (every chunk's loads unconditional -- a branch per chunk made each load wait alone;
+    // chunks past nch read scratch and are masked out of the sum)
+    const uint64_t *__restrict__ ck = J.ckeys;
+    const int32_t *__restrict__ cv = J.cvals;
+#pragma unroll
+    for (int st = kIncChunk / 2; st > 0; st >>= 1) {
+        uint64_t pk[NC];
+        int32_t pv[NC];
+#pragma unroll
+        for (int c = 0; c < NC; ++c) {
+            const int q = c * kIncChunk + pos[c] + st - 1;
+            pk[c] = ck[q];
+            pv[c] = cv[q];
+        }
+#pragma unroll
+        for (int c = 0; c < NC; ++c) pos[c] += inc_less(pk[c], pv[c], key, val) ? st : 0;
+    }
+    int rank = 0;
+    {
+        uint64_t pk[NC];
+        int32_t pv[NC];
+#pragma unroll
+        for (int c = 0; c < NC; ++c) {
+            const int q = c * kIncChunk + pos[c];
+            pk[c] = ck[q];
+            pv[c] = cv[q];
+        }
+#pragma unroll
+        for (int c = 0; c < NC; ++c)
+            rank += c < nch ? pos[c] + (inc_less(pk[c], pv[c], key, val) ? 1 : 0) : 0;
+    }
+    J.nkeys[rank] = key;
+    J.nvals[rank] = val;
+}
+
 __device__ __forceinline__ void pt_inc_crank(const PtIncJob &J) {
     if (J.full) return;
     const int64_t nd = *J.T.n_dev, n = nd < J.T.n_upper ? nd : J.T.n_upper;
@@ -837,47 +882,8 @@ __device__ __forceinline__ void pt_inc_crank(const PtIncJob &J) {
     m = m < 0 ? 0 : (m > kPtIncSeg ? kPtIncSeg : m);
     const int e = (int)blockIdx.x * (int)blockDim.x + (int)threadIdx.x;
     if (e >= m) return;
-    const int nch = (int)((m + kIncChunk - 1) / kIncChunk);
-    const uint64_t key = J.ckeys[e];
-    const int32_t val = J.cvals[e];
-    // per chunk: the count of its pairs below (key, val); for the element's own chunk that is
-    // its index there.  Fixed steps, the chunks' loads issued together.
-    int pos[kIncChunks];
-#pragma unroll
-    for (int c = 0; c < kIncChunks; ++c) pos[c] = 0;
-    // (every chunk's loads unconditional -- a branch per chunk made each load wait alone;
-    // chunks past nch read scratch and are masked out of the sum)
-    const uint64_t *__restrict__ ck = J.ckeys;
-    const int32_t *__restrict__ cv = J.cvals;
-#pragma unroll
-    for (int st = kIncChunk / 2; st > 0; st >>= 1) {
-        uint64_t pk[kIncChunks];
-        int32_t pv[kIncChunks];
-#pragma unroll
-        for (int c = 0; c < kIncChunks; ++c) {
-            const int q = c * kIncChunk + pos[c] + st - 1;
-            pk[c] = ck[q];
-            pv[c] = cv[q];
-        }
-#pragma unroll
-        for (int c = 0; c < kIncChunks; ++c) pos[c] += inc_less(pk[c], pv[c], key, val) ? st : 0;
-    }
-    int rank = 0;
-    {
-        uint64_t pk[kIncChunks];
-        int32_t pv[kIncChunks];
-#pragma unroll
-        for (int c = 0; c < kIncChunks; ++c) {
-            const int q = c * kIncChunk + pos[c];
-            pk[c] = ck[q];
-            pv[c] = cv[q];
-        }
-#pragma unroll
-        for (int c = 0; c < kIncChunks; ++c)
-            rank += c < nch ? pos[c] + (inc_less(pk[c], pv[c], key, val) ? 1 : 0) : 0;
-    }
-    J.nkeys[rank] = key;
-    J.nvals[rank] = val;
+    if (m <= (int64_t)kIncChunk * (kIncChunks / 2)) pt_inc_crank_n<kIncChunks / 2>(J, m, e);
+    else pt_inc_crank_n<kIncChunks>(J, m, e);
 }
 
 __global__ __launch_bounds__(256) void k_pt_inc_crank(IncJobs jobs) {
@@ -965,10 +971,127 @@ __device__ __forceinline__ void pt_inc_merge(const PtIncJob &J) {
     }
 }
 
+// An incremental merge with its split points precomputed: the output place of every new point
+// (k_pt_inc_npos: its index among the new plus the count of old codes <= its code, old first
+// on a tie as in merge_split) makes a tile's split a search of that short, cache-resident
+// array, and an output's source the count of the tile's new places below it.  The merge-path
+// form searched the whole old code array (17 dependent loads a workgroup, cold) and the
+// tile's keys in LDS per output.  A tile is kIncPer outputs a thread.
+constexpr int kIncPer = 4;
+constexpr int kIncTile2 = kIncTile * kIncPer;
+
+__device__ __forceinline__ void pt_inc_npos(const PtIncJob &J) {
+    if (J.full) return;
+    const int64_t nd = *J.T.n_dev, n = nd < J.T.n_upper ? nd : J.T.n_upper;
+    const int64_t n_old = *J.nidx;
+    int64_t m = n - n_old;
+    m = m < 0 ? 0 : (m > kPtIncSeg ? kPtIncSeg : m);
+    const int j = (int)blockIdx.x * (int)blockDim.x + (int)threadIdx.x;
+    if (j >= m) return;
+    const uint64_t key = J.nkeys[j];
+    int64_t lo = 0, hi = n_old;
+    while (lo < hi) {
+        const int64_t mid = (lo + hi) >> 1;
+        if (J.okeys[mid] <= key) lo = mid + 1;
+        else hi = mid;
+    }
+    J.npos[j] = (int32_t)(lo + j);
+}
+
+__global__ __launch_bounds__(256) void k_pt_inc_npos(IncJobs jobs) {
+    if (jobs.table) pt_inc_npos(jobs.table[blockIdx.y]);
+    else pt_inc_npos(jobs.one);
+}
+
 template <int D>
-__global__ __launch_bounds__(kIncTile) void k_pt_inc_merge(IncJobs jobs) {
-    if (jobs.table) pt_inc_merge<D>(jobs.table[blockIdx.y]);
-    else pt_inc_merge<D>(jobs.one);
+__device__ __forceinline__ void pt_inc_merge2(const PtIncJob &J) {
+    __shared__ int32_t s_np[kIncTile2];
+    __shared__ int32_t s_nb[2];
+    const int64_t nd = *J.T.n_dev, n = nd < J.T.n_upper ? nd : J.T.n_upper;
+    const int64_t p0 = (int64_t)blockIdx.x * kIncTile2;
+    if (p0 >= n) return;
+    const int64_t n_old = *J.nidx;
+    int64_t m = n - n_old;
+    m = m < 0 ? 0 : (m > kPtIncSeg ? kPtIncSeg : m);
+    const int64_t p1 = p0 + kIncTile2 < n ? p0 + kIncTile2 : n;
+    const int t = threadIdx.x;
+    if (t < 2) {  // new points placed before p0 / p1
+        const int64_t target = t == 0 ? p0 : p1;
+        int lo = 0, hi = (int)m;
+        while (lo < hi) {
+            const int mid = (lo + hi) >> 1;
+            if (J.npos[mid] < target) lo = mid + 1;
+            else hi = mid;
+        }
+        s_nb[t] = lo;
+    }
+    __syncthreads();
+    const int nb0 = s_nb[0], cnt = s_nb[1] - nb0;
+    for (int k = t; k < cnt; k += kIncTile) s_np[k] = J.npos[nb0 + k];
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < kIncPer; ++u) {
+        const int64_t p = p0 + u * kIncTile + t;
+        const bool live = p < p1;
+        double row[D];
+        if (live) {
+            int lo = 0, hi = cnt;  // the tile's new places below p
+            while (lo < hi) {
+                const int mid = (lo + hi) >> 1;
+                if (s_np[mid] < p) lo = mid + 1;
+                else hi = mid;
+            }
+            uint64_t key;
+            int32_t id;
+            if (lo < cnt && s_np[lo] == p) {
+                const int j = nb0 + lo;
+                const int64_t r = J.nvals[j];
+                key = J.nkeys[j];
+                id = (int32_t)r + 1;
+#pragma unroll
+                for (int k = 0; k < D; ++k) row[k] = J.pts[r * D + k];
+            } else {
+                const int64_t o = p - nb0 - lo;
+                key = J.okeys[o];
+                id = J.oids[o];
+#pragma unroll
+                for (int k = 0; k < D; ++k) row[k] = J.opts[o * D + k];
+            }
+            J.keys[p] = key;
+            J.ids[p] = id;
+#pragma unroll
+            for (int k = 0; k < D; ++k) J.spts[p * D + k] = row[k];
+        }
+#pragma unroll
+        for (int k = 0; k < D; ++k) {
+            double lo = live ? row[k] : __builtin_huge_val(), hi = live ? row[k] : -__builtin_huge_val();
+#pragma unroll
+            for (int off = kPtFan / 2; off > 0; off >>= 1) {
+                const double olo = __shfl_xor(lo, off, kPtFan), ohi = __shfl_xor(hi, off, kPtFan);
+                lo = olo < lo ? olo : lo;
+                hi = ohi > hi ? ohi : hi;
+            }
+            if (live && (p & (kPtFan - 1)) == 0) {
+                float *bx = J.boxes + (p / kPtFan) * 2 * D;
+                bx[k] = widen_lo(lo);
+                bx[D + k] = widen_hi(hi);
+            }
+        }
+    }
+}
+
+// merge2: the placed merge for incremental jobs (a full rebuild keeps the merge-path form;
+// its tiles are kIncTile outputs, so the grid is sized for those)
+template <int D>
+__global__ __launch_bounds__(kIncTile) void k_pt_inc_merge(IncJobs jobs, int merge2) {
+    const PtIncJob &J = jobs.table ? jobs.table[blockIdx.y] : jobs.one;
+    if (merge2 && !J.full) {
+        if (jobs.table) pt_inc_merge2<D>(jobs.table[blockIdx.y]);
+        else pt_inc_merge2<D>(jobs.one);
+    } else {
+        if (jobs.table) pt_inc_merge<D>(jobs.table[blockIdx.y]);
+        else pt_inc_merge<D>(jobs.one);
+    }
 }
 
 __device__ __forceinline__ void pt_inc_boxes(const PtIncJob &J) {
@@ -1414,7 +1537,7 @@ PointTree::~PointTree() {
         if (p) (void)hipFree(p);
     for (void *p : {(void *)ikeys[0], (void *)ikeys[1], (void *)iids[0], (void *)iids[1], (void *)ipts[0],
                     (void *)ipts[1], (void *)inkeys, (void *)invals, (void *)iqorder, itemp, (void *)inidx,
-                    (void *)ibox, (void *)iplan, (void *)ickeys, (void *)icvals})
+                    (void *)ibox, (void *)iplan, (void *)ickeys, (void *)icvals, (void *)inpos})
         if (p) (void)hipFree(p);
 }
 
@@ -1656,6 +1779,7 @@ void PointTree::inc_reserve(int64_t c, int32_t d) {
     if (!ickeys) {
         hip_check(hipMalloc(&ickeys, sizeof(uint64_t) * kPtIncSeg), "inc chunk keys");
         hip_check(hipMalloc(&icvals, sizeof(int32_t) * kPtIncSeg), "inc chunk rows");
+        hip_check(hipMalloc(&inpos, sizeof(int32_t) * kPtIncSeg), "inc new places");
     }
     size_t tb = 0;
     hip_check(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, ikeys[0], inkeys, iids[0], invals, (int)c, 0,
@@ -1740,6 +1864,7 @@ PtIncJob PointTree::prepare_inc(const double *pts, int64_t n_upper, const int64_
     J.nvals = invals;
     J.ckeys = ickeys;
     J.cvals = icvals;
+    J.npos = inpos;
     J.nidx = inidx;
     J.ibox = ibox;
     J.q = iq_on ? q : nullptr;
@@ -1764,11 +1889,9 @@ void launch_tree_inc_jobs(const PtIncJob *d_jobs, const PtIncJob *h_jobs, int32_
     for (int32_t j = 0; j < n; ++j) max_n = std::max(max_n, h_jobs[j].T.n_upper);
     auto by_d = [&](auto k3, auto k7, auto k15) { return d == 3 ? k3 : d == 7 ? k7 : k15; };
     if (d != 3 && d != 7 && d != 15) throw Error{1, "point tree: state dim must be 3, 7 or 15"};
-    // the chunked sort while the one-workgroup sorts would leave most CUs idle: config 5 at 32
-    // trees 0.347 -> 0.294 ms a build; at 256 trees (one sort per CU) 1.74 -> 1.86 ms, the rank
-    // searches' loads costing more than the network they replace.  MPT_PT_CSORT=0 / 1 forces.
-    static const int csort_env = getenv("MPT_PT_CSORT") ? atoi(getenv("MPT_PT_CSORT")) : -1;
-    const bool csort = csort_env >= 0 ? csort_env == 1 : n < kIncCsortMaxTrees;
+    // the chunked sort (config 5 builds, 32 / 64 / 256 trees: 0.366 / 0.545 / 1.759 ms with
+    // the one-workgroup sort, 0.297 / 0.515 / 1.761 ms chunked).  MPT_PT_CSORT=0: the former
+    static const bool csort = !(getenv("MPT_PT_CSORT") && atoi(getenv("MPT_PT_CSORT")) == 0);
     bool any_q = false;
     for (int32_t j = 0; j < n; ++j) any_q = any_q || h_jobs[j].q;
     if (csort) {
@@ -1806,8 +1929,15 @@ void launch_tree_inc_jobs(const PtIncJob *d_jobs, const PtIncJob *h_jobs, int32_
             fprintf(stderr, "[sort dbg] %d trees: plan %.1f us, codes %.1f us, sort %.1f us, out %.1f us; span %.1f us\n",
                     cnt, ph[0] / cnt * 0.01, ph[1] / cnt * 0.01, ph[2] / cnt * 0.01, ph[3] / cnt * 0.01, (t1 - t0) * 0.01);
     }
+    // MPT_PT_MERGE2=0: the merge-path form for every job (A/B)
+    static const bool merge2 = !(getenv("MPT_PT_MERGE2") && atoi(getenv("MPT_PT_MERGE2")) == 0);
+    if (merge2) {
+        hipLaunchKernelGGL(k_pt_inc_npos, dim3(kPtIncSeg / 256, n), dim3(256), 0, stream, js);
+        hip_check(hipGetLastError(), "k_pt_inc_npos");
+    }
     hipLaunchKernelGGL(by_d(k_pt_inc_merge<3>, k_pt_inc_merge<7>, k_pt_inc_merge<15>),
-                       dim3((unsigned)((max_n + kIncTile - 1) / kIncTile), n), dim3(kIncTile), 0, stream, js);
+                       dim3((unsigned)((max_n + kIncTile - 1) / kIncTile), n), dim3(kIncTile), 0, stream, js,
+                       merge2 ? 1 : 0);
     hip_check(hipGetLastError(), "k_pt_inc_merge");
     const int64_t groups = (max_n + kPtChunkLeaves * kPtFan - 1) / (kPtChunkLeaves * kPtFan);
     hipLaunchKernelGGL(k_pt_inc_boxes, dim3((unsigned)groups, n), dim3(256), 0, stream, js);
