@@ -83,8 +83,8 @@ __device__ __forceinline__ double flush_pairs(const EnvDev &env, DistLds &s, int
     if (lane < n) {
         const int32_t e = s.queue[lane];
         const double *qa = s.q[e & 63];
-        const v3 Q[3] = {mk(qa[0], qa[1], qa[2]), mk(qa[3], qa[4], qa[5]), mk(qa[6], qa[7], qa[8])};
         const EnvTri &E = env.tris[e >> 6];
+        const v3 Q[3] = {mk(qa[0], qa[1], qa[2]), mk(qa[3], qa[4], qa[5]), mk(qa[6], qa[7], qa[8])};
         const v3 S[3] = {mk(E.P1[0], E.P1[1], E.P1[2]), mk(E.P2[0], E.P2[1], E.P2[2]), mk(E.P3[0], E.P3[1], E.P3[2])};
         // at 4 waves per SIMD the rolled form (128 VGPRs); else the unrolled one
         d = tri_distance<kOcc >= 4 ? 1 : 3, kSel>(S, E.lo, E.hi, Q);
@@ -308,9 +308,9 @@ __device__ void distance_unit(const EnvDev &env, const AgentDev *__restrict__ li
             ++cnt.clusters;
             float cblo[3], cbhi[3];
 #pragma unroll
-            for (int k = 0; k < 3; ++k) {
-                cblo[k] = __shfl(clo[k], j);
-                cbhi[k] = __shfl(chi[k], j);
+            for (int k = 0; k < 3; ++k) {  // wave-uniform: scalar registers
+                cblo[k] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(clo[k]), j));
+                cbhi[k] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(chi[k]), j));
             }
             const Cluster c = ag.clusters[cbase + j];
             const bool act = lane < c.count;
@@ -352,10 +352,12 @@ __device__ void distance_unit(const EnvDev &env, const AgentDev *__restrict__ li
     }
 }
 
-// kOcc workgroups per CU.  2 (default): the unconstrained allocation with the unrolled
-// triDistance (242 VGPRs, 2 waves per SIMD).  4: at most 128 VGPRs with the rolled triDistance
-// (4 waves per SIMD; the LDS allows it, the registers spill ~100 dwords): 12-14 % slower on
-// the blimp in the room (MPT_DIST_OCC=4, scripts/measure_distance.sh).
+// kOcc workgroups per CU (MPT_DIST_OCC, scripts/measure_distance.sh).  3 (default): the
+// unrolled triDistance under 168 VGPRs, 3 waves per SIMD (5 dwords spilled): blimp in the room
+// 10.4 -> 7.8 ms against 2 (the unconstrained allocation, 178 VGPRs since triDistance no longer
+// holds S and T beside their rotating copies).  4: the rolled triDistance under 128 VGPRs
+// spills ~100 dwords and 51 scalars (the walk's state is ~55 VGPRs beside triDistance's 112):
+// 9.3 ms.
 template <int kOcc, bool kSel>
 __global__ __launch_bounds__(kDistWaves * 64, kOcc) void k_distance(EnvDev env, const AgentDev *__restrict__ links,
                                                                  DistWork w) {
@@ -388,7 +390,7 @@ void launch_distance(const EnvDev &env, const AgentDev *d_links, const DistWork 
     if (w.n_units <= 0 || env.n_tris <= 0) return;
     const int64_t blocks = (w.n_units + kDistWaves - 1) / kDistWaves;
     if (blocks > 0x7fffffff) throw Error{MPT_ERR_INVALID, "distance batch too large"};
-    static const int occ = getenv("MPT_DIST_OCC") ? atoi(getenv("MPT_DIST_OCC")) : 2;
+    static const int occ = getenv("MPT_DIST_OCC") ? atoi(getenv("MPT_DIST_OCC")) : 3;
     static const bool flush_set = [] {
         const int32_t f = getenv("MPT_DIST_FLUSH") ? atoi(getenv("MPT_DIST_FLUSH")) : 32;
         hip_check(hipMemcpyToSymbol(HIP_SYMBOL(c_dist_flush), &f, sizeof f), "flush threshold");
@@ -402,6 +404,8 @@ void launch_distance(const EnvDev &env, const AgentDev *d_links, const DistWork 
     hipLaunchKernelGGL((k_distance<OCC, SEL>), dim3((unsigned)blocks), dim3(kDistWaves * 64), 0, stream, env, d_links, w)
     if (occ == 2) {
         if (sel) MPT_DIST_LAUNCH(2, true); else MPT_DIST_LAUNCH(2, false);
+    } else if (occ == 3) {
+        if (sel) MPT_DIST_LAUNCH(3, true); else MPT_DIST_LAUNCH(3, false);
     } else {
         if (sel) MPT_DIST_LAUNCH(4, true); else MPT_DIST_LAUNCH(4, false);
     }

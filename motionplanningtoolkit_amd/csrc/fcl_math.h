@@ -385,11 +385,13 @@ MPT_HD double tri_distance(const v3 S[3], const double slo[3], const double shi[
     const v3 D0 = sub(S[0], T[0]);
     double mindd = dot(D0, D0) + 1;
     int shown_disjoint = 0;
+    // the rotating copies are the only vertex registers: three rotations bring each triple
+    // back, so after the loops they are S and T again (S / T themselves are not kept live)
     v3 s0 = S[0], s1 = S[1], s2 = S[2];
+    v3 t0 = T[0], t1 = T[1], t2 = T[2];
 #pragma unroll kUnroll
     for (int i = 0; i < 3; ++i) {
         const v3 sv = sub(s1, s0);
-        v3 t0 = T[0], t1 = T[1], t2 = T[2];
 #pragma unroll kUnroll
         for (int j = 0; j < 3; ++j) {
             const v3 tv = sub(t1, t0);
@@ -419,23 +421,24 @@ MPT_HD double tri_distance(const v3 S[3], const double slo[3], const double shi[
         s2 = ss;
     }
     double d;
+    const v3 Sx[3] = {s0, s1, s2}, Tx[3] = {t0, t1, t2};
     {
-        const v3 Sv[3] = {sub(S[1], S[0]), sub(S[2], S[1]), sub(S[0], S[2])};
+        const v3 Sv[3] = {sub(Sx[1], Sx[0]), sub(Sx[2], Sx[1]), sub(Sx[0], Sx[2])};
         const v3 Sn = cross(Sv[0], Sv[1]);
         const double Snl = dot(Sn, Sn);
-        if (Snl > 1e-15 && face_vertex(S, Sv, Sn, Snl, T, true, shown_disjoint, d)) return d;
+        if (Snl > 1e-15 && face_vertex(Sx, Sv, Sn, Snl, Tx, true, shown_disjoint, d)) return d;
     }
     {
-        const v3 Tv[3] = {sub(T[1], T[0]), sub(T[2], T[1]), sub(T[0], T[2])};
+        const v3 Tv[3] = {sub(Tx[1], Tx[0]), sub(Tx[2], Tx[1]), sub(Tx[0], Tx[2])};
         const v3 Tn = cross(Tv[0], Tv[1]);
         const double Tnl = dot(Tn, Tn);
-        if (Tnl > 1e-15 && face_vertex(T, Tv, Tn, Tnl, S, false, shown_disjoint, d)) return d;
+        if (Tnl > 1e-15 && face_vertex(Tx, Tv, Tn, Tnl, Sx, false, shown_disjoint, d)) return d;
     }
     if (shown_disjoint) return sqrt(mindd);
-    const double tlo[3] = {dmin(T[0].x, dmin(T[1].x, T[2].x)), dmin(T[0].y, dmin(T[1].y, T[2].y)),
-                           dmin(T[0].z, dmin(T[1].z, T[2].z))};
-    const double thi[3] = {dmax(T[0].x, dmax(T[1].x, T[2].x)), dmax(T[0].y, dmax(T[1].y, T[2].y)),
-                           dmax(T[0].z, dmax(T[1].z, T[2].z))};
+    const double tlo[3] = {dmin(Tx[0].x, dmin(Tx[1].x, Tx[2].x)), dmin(Tx[0].y, dmin(Tx[1].y, Tx[2].y)),
+                           dmin(Tx[0].z, dmin(Tx[1].z, Tx[2].z))};
+    const double thi[3] = {dmax(Tx[0].x, dmax(Tx[1].x, Tx[2].x)), dmax(Tx[0].y, dmax(Tx[1].y, Tx[2].y)),
+                           dmax(Tx[0].z, dmax(Tx[1].z, Tx[2].z))};
     const bool boxes = slo[0] <= thi[0] && tlo[0] <= shi[0] && slo[1] <= thi[1] && tlo[1] <= shi[1] &&
                        slo[2] <= thi[2] && tlo[2] <= shi[2];
     return boxes ? 0.0 : sqrt(mindd);
