@@ -1168,6 +1168,26 @@ constexpr int kPtStack = kPtFan * kPtMaxLevels;
 // double (register budget) and rounded down.  Pruning on it keeps every box the exact bound
 // keeps.
 constexpr float kLbF32Shrink = 1.0f - 0x1p-19f;
+
+// The walks' point rows, ids and boxes through address-space-1 pointers: the tree comes from a
+// job table, so the compiler cannot tell its pointers are global and emits flat loads, which
+// also count against the LDS counter (every lane-shuffle / stack wait then waits for them).
+using gdbl = const __attribute__((address_space(1))) double *;
+using gflt = const __attribute__((address_space(1))) float *;
+using gi32 = const __attribute__((address_space(1))) int32_t *;
+template <int D>
+__device__ __forceinline__ double leaf_l2(const double (&qq)[D], const PointTreeDev &T, int64_t p) {
+    double row[D];
+#pragma unroll
+    for (int k = 0; k < D; ++k) row[k] = ((gdbl)T.pts)[p * D + k];
+    return flann_l2<D>(qq, row);
+}
+__device__ __forceinline__ int32_t leaf_id(const PointTreeDev &T, int64_t p) { return ((gi32)T.ids)[p]; }
+template <int D>
+__device__ __forceinline__ void load_box(const PointTreeDev &T, int64_t box, float (&b)[2 * D]) {
+#pragma unroll
+    for (int k = 0; k < 2 * D; ++k) b[k] = ((gflt)T.boxes)[box * 2 * D + k];
+}
 template <int D>
 __device__ __forceinline__ float box_lb(const float *__restrict__ b, const double (&qq)[D], const float (&qlo)[D],
                                         const float (&qhi)[D]) {
@@ -1239,8 +1259,8 @@ __device__ __forceinline__ void tree_nn1_block(const PointTreeDev &T, const doub
             if (lev == 1) {
                 const int64_t p = idx * kPtFan + sub;
                 if (p < n) {
-                    const double dd = flann_l2<D>(qq, T.pts + p * D);
-                    const int32_t id = T.ids[p];
+                    const double dd = leaf_l2<D>(qq, T, p);
+                    const int32_t id = leaf_id(T, p);
                     ++n_pts;
                     if (nn_better(dd, id, bd, bi)) {
                         bd = dd;
@@ -1261,7 +1281,9 @@ __device__ __forceinline__ void tree_nn1_block(const PointTreeDev &T, const doub
                 bool keep = false;
                 float lbf = 0.0f;
                 if (c < lvl_size(n, lev - 1)) {
-                    lbf = box_lb<D>(T.boxes + (lvl_off(T.n_upper, lev - 1) + c) * 2 * D, qq, qlo, qhi);
+                    float bx[2 * D];
+                    load_box<D>(T, lvl_off(T.n_upper, lev - 1) + c, bx);
+                    lbf = box_lb<D>(bx, qq, qlo, qhi);
                     keep = (double)lbf * (1.0 - 1e-12) <= bd;
                     ++n_box;
                 }
@@ -1368,8 +1390,8 @@ __device__ __forceinline__ void tree_nn1_blockn(const PointTreeDev &T, const dou
             if (lev == 1) {
                 const int64_t p = idx * kPtFan + ls;
                 if (p < n) {
-                    const double dd = flann_l2<D>(qq, T.pts + p * D);
-                    const int32_t id = T.ids[p];
+                    const double dd = leaf_l2<D>(qq, T, p);
+                    const int32_t id = leaf_id(T, p);
                     ++n_pts;
                     if (nn_better(dd, id, bd, bi)) {
                         bd = dd;
@@ -1379,7 +1401,9 @@ __device__ __forceinline__ void tree_nn1_blockn(const PointTreeDev &T, const dou
             } else if (lev > 1) {
                 c = idx * kPtFan + ls;
                 if (c < lvl_size(n, lev - 1)) {
-                    lbf = box_lb<D>(T.boxes + (lvl_off(T.n_upper, lev - 1) + c) * 2 * D, qq, qlo, qhi);
+                    float bx[2 * D];
+                    load_box<D>(T, lvl_off(T.n_upper, lev - 1) + c, bx);
+                    lbf = box_lb<D>(bx, qq, qlo, qhi);
                     keep = true;
                     ++n_box;
                 }
