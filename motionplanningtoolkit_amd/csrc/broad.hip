@@ -330,22 +330,21 @@ __global__ __launch_bounds__(kPairThreads) void k_pairs(EnvDev env, const AgentD
         }
         return;
     }
-    const Item *items = env.items;
+    // the walk's items: in LDS (kLds) or global, decided at compile time -- a pointer that may
+    // be either compiles to flat instructions, slower for LDS and counted against the LDS
+    // counter for global
+    const Item *items = kLds ? reinterpret_cast<const Item *>(smem) : env.items;
     // two-level trees in LDS walk the quantized boxes (env.qitems; 16 B an item)
     const bool quant = kTwo && kLds && env.qitems != nullptr;
-    const uint4 *qitems = nullptr;
+    const uint4 *qitems = reinterpret_cast<const uint4 *>(smem);
     if (kLds) {
         const int32_t n = env.lev_off[env.n_levels];
+        uint4 *dst = reinterpret_cast<uint4 *>(smem);
         if (quant) {
-            uint4 *dst = reinterpret_cast<uint4 *>(smem);
             for (int i = threadIdx.x; i < n; i += blockDim.x) dst[i] = env.qitems[i];
-            qitems = dst;
         } else {
-            Item *s_items = reinterpret_cast<Item *>(smem);
             const uint4 *src = reinterpret_cast<const uint4 *>(env.items);
-            uint4 *dst = reinterpret_cast<uint4 *>(s_items);
             for (int i = threadIdx.x; i < n * 2; i += blockDim.x) dst[i] = src[i];
-            items = s_items;
         }
     }
     __syncthreads();
@@ -433,6 +432,9 @@ __device__ __forceinline__ bool emit(bool h, uint64_t m, int32_t unit, int32_t a
 // lds_items: the env's triangle items [0, n_tris) staged in LDS (small envs), else read
 // through the caches.  A header's chain of dependent loads is dense slot -> header -> {pose,
 // agent triangles, pair words} -> env items; the next header's dense slot is fetched ahead.
+// kLds: the items in LDS, a compile-time choice (a pointer that may be LDS or global compiles
+// to flat instructions)
+template <bool kLds>
 __global__ __launch_bounds__(256) void k_cands(EnvDev env, const AgentDev *__restrict__ links, CollideWork w,
                                                SplitArgs a, int32_t lds_items) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -440,14 +442,12 @@ __global__ __launch_bounds__(256) void k_cands(EnvDev env, const AgentDev *__res
     const int lane = threadIdx.x & 63;
     const int32_t cw = (int32_t)blockIdx.x * 4 + wave;
     const uint32_t total = __builtin_amdgcn_readfirstlane(a.hdr_off[a.n_seg]);
-    const Item *items = env.items;
-    if (lds_items > 0) {
-        Item *s_items = reinterpret_cast<Item *>(smem);
+    const Item *items = kLds ? reinterpret_cast<const Item *>(smem) : env.items;
+    if (kLds) {
         const uint4 *src = reinterpret_cast<const uint4 *>(env.items);
-        uint4 *dst = reinterpret_cast<uint4 *>(s_items);
+        uint4 *dst = reinterpret_cast<uint4 *>(smem);
         for (int i = threadIdx.x; i < lds_items * 2; i += blockDim.x) dst[i] = src[i];
         __syncthreads();
-        items = s_items;
     }
     Cand *cseg = a.cand + (int64_t)cw * a.cand_cap;
     uint32_t cnt = 0, n_xf = 0;
@@ -468,7 +468,8 @@ __global__ __launch_bounds__(256) void k_cands(EnvDev env, const AgentDev *__res
         int64_t slot, edge;
         decode_unit(w, unit, link, slot, edge);
         const bool act = lane < tcount;
-        const double *tri = links[link].tris + (int64_t)(tfirst + (act ? lane : 0)) * 9;
+        double tri[9];  // global loads (the agent's pointers are read from memory: flat otherwise)
+        load_global<9>(links[link].tris + (int64_t)(tfirst + (act ? lane : 0)) * 9, tri);
         double R[9], T[3];
         unit_rt(env, w, slot, link, R, T);
 #pragma unroll
@@ -555,10 +556,8 @@ __device__ __forceinline__ void narrow_range(const EnvDev &env, const AgentDev *
         double P[12];
 #pragma unroll
         for (int k = 0; k < 12; ++k) P[k] = pose[k];
-        const double *t = links[link].tris + (int64_t)cd.atri * 9;
         double A[9];
-#pragma unroll
-        for (int k = 0; k < 9; ++k) A[k] = t[k];
+        load_global<9>(links[link].tris + (int64_t)cd.atri * 9, A);
         if (decided) continue;  // another candidate of this edge already found the contact
         double R[9], T[3];
         if (w.unit_rt) {
@@ -840,8 +839,12 @@ static void collide_split_chunk(const EnvDev &env, const AgentDev *d_links, int3
     // MPT_CANDS_LDS=0: always through the caches (A/B knob)
     static const bool cands_lds = !(getenv("MPT_CANDS_LDS") && atoi(getenv("MPT_CANDS_LDS")) == 0);
     const int32_t cl_items = cands_lds && env.n_tris <= kCandsLdsItems ? env.n_tris : 0;
-    hipLaunchKernelGGL(k_cands, dim3((unsigned)((s.n_cwaves + 3) / 4)), dim3(256), sizeof(Item) * (size_t)cl_items,
-                       stream, env, d_links, w, a, cl_items);
+    if (cl_items > 0)
+        hipLaunchKernelGGL(k_cands<true>, dim3((unsigned)((s.n_cwaves + 3) / 4)), dim3(256),
+                           sizeof(Item) * (size_t)cl_items, stream, env, d_links, w, a, cl_items);
+    else
+        hipLaunchKernelGGL(k_cands<false>, dim3((unsigned)((s.n_cwaves + 3) / 4)), dim3(256), 0, stream, env, d_links, w,
+                           a, 0);
     hip_check(hipGetLastError(), "k_cands launch");
     mark(1);
     const unsigned nblocks = (unsigned)((s.n_cwaves + kSpillWaves + kNarrowWaves - 1) / kNarrowWaves);
