@@ -40,12 +40,15 @@ struct Cluster {
     int32_t count; // <= 64
 };
 
+// a pointer qualifier for global memory (address space 1)
+#define MPT_GLOBAL __attribute__((address_space(1)))
+
 // N doubles from p, which points to global memory, with global instructions: pointers read
 // from memory (job tables, AgentDev records) are otherwise accessed with flat instructions,
 // which also count against the LDS counter
 template <int N>
 __device__ __forceinline__ void load_global(const double *p, double (&out)[N]) {
-    const __attribute__((address_space(1))) double *g = (const __attribute__((address_space(1))) double *)p;
+    const MPT_GLOBAL double *g = (const MPT_GLOBAL double *)p;
 #pragma unroll
     for (int k = 0; k < N; ++k) out[k] = g[k];
 }

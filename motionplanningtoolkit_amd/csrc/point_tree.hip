@@ -720,10 +720,9 @@ __device__ __forceinline__ void pt_inc_ncodes(const PtIncJob &J, const IncPlan &
     if (live) {
         double x[D];
         const int64_t row = base + i;
-#pragma unroll
-        for (int j = 0; j < D; ++j) x[j] = J.pts[row * D + j];
-        J.nkeys[i] = inc_code<D>(&P, x);
-        J.nvals[i] = (int32_t)row;
+        load_global<D>(J.pts + row * D, x);
+        ((MPT_GLOBAL uint64_t *)J.nkeys)[i] = inc_code<D>(&P, x);
+        ((MPT_GLOBAL int32_t *)J.nvals)[i] = (int32_t)row;
 #pragma unroll
         for (int j = 0; j < D; ++j) mn[j] = mx[j] = order_key_pt(x[j]);
     } else {
@@ -779,8 +778,9 @@ __device__ __forceinline__ void pt_inc_csort(const PtIncJob &J) {
     for (int a = 0; a < E; ++a) {
         const int i = c0 + lane * E + a;
         const bool live = i < m;
-        key[a] = live ? J.nkeys[i] : ~0ull;  // real codes use 63 bits: padding sorts last
-        val[a] = live ? J.nvals[i] : 0x7fffffff;
+        // real codes use 63 bits: padding sorts last
+        key[a] = live ? ((const MPT_GLOBAL uint64_t *)J.nkeys)[i] : ~0ull;
+        val[a] = live ? ((const MPT_GLOBAL int32_t *)J.nvals)[i] : 0x7fffffff;
     }
 #pragma unroll 1
     for (int k = 2; k <= kIncChunk; k <<= 1) {
@@ -819,8 +819,8 @@ __device__ __forceinline__ void pt_inc_csort(const PtIncJob &J) {
     // the whole chunk, padding included (the rank search reads 512 per chunk)
 #pragma unroll
     for (int a = 0; a < E; ++a) {
-        J.ckeys[c0 + lane * E + a] = key[a];
-        J.cvals[c0 + lane * E + a] = val[a];
+        ((MPT_GLOBAL uint64_t *)J.ckeys)[c0 + lane * E + a] = key[a];
+        ((MPT_GLOBAL int32_t *)J.cvals)[c0 + lane * E + a] = val[a];
     }
 }
 
@@ -842,8 +842,8 @@ __device__ __forceinline__ void pt_inc_crank_n(const PtIncJob &J, int64_t m, int
     for (int c = 0; c < NC; ++c) pos[c] = 0;
     // (every chunk's loads unconditional -- a branch per chunk made each load wait alone;
     // chunks past nch read scratch and are masked out of the sum)
-    const uint64_t *__restrict__ ck = J.ckeys;
-    const int32_t *__restrict__ cv = J.cvals;
+    const MPT_GLOBAL uint64_t *ck = (const MPT_GLOBAL uint64_t *)J.ckeys;
+    const MPT_GLOBAL int32_t *cv = (const MPT_GLOBAL int32_t *)J.cvals;
 #pragma unroll
     for (int st = kIncChunk / 2; st > 0; st >>= 1) {
         uint64_t pk[NC];
@@ -1015,19 +1015,29 @@ __device__ __forceinline__ void pt_inc_merge2(const PtIncJob &J) {
     m = m < 0 ? 0 : (m > kPtIncSeg ? kPtIncSeg : m);
     const int64_t p1 = p0 + kIncTile2 < n ? p0 + kIncTile2 : n;
     const int t = threadIdx.x;
+    // the job's arrays through global pointers (read from the job table they are flat, and a
+    // flat access counts against the LDS counter: each LDS search would wait for the loads)
+    const MPT_GLOBAL int32_t *npos = (const MPT_GLOBAL int32_t *)J.npos;
+    const MPT_GLOBAL uint64_t *nkeys = (const MPT_GLOBAL uint64_t *)J.nkeys, *okeys = (const MPT_GLOBAL uint64_t *)J.okeys;
+    const MPT_GLOBAL int32_t *nvals = (const MPT_GLOBAL int32_t *)J.nvals, *oids = (const MPT_GLOBAL int32_t *)J.oids;
+    const MPT_GLOBAL double *pts = (const MPT_GLOBAL double *)J.pts, *opts = (const MPT_GLOBAL double *)J.opts;
+    MPT_GLOBAL uint64_t *keys = (MPT_GLOBAL uint64_t *)J.keys;
+    MPT_GLOBAL int32_t *ids = (MPT_GLOBAL int32_t *)J.ids;
+    MPT_GLOBAL double *spts = (MPT_GLOBAL double *)J.spts;
+    MPT_GLOBAL float *boxes = (MPT_GLOBAL float *)J.boxes;
     if (t < 2) {  // new points placed before p0 / p1
         const int64_t target = t == 0 ? p0 : p1;
         int lo = 0, hi = (int)m;
         while (lo < hi) {
             const int mid = (lo + hi) >> 1;
-            if (J.npos[mid] < target) lo = mid + 1;
+            if (npos[mid] < target) lo = mid + 1;
             else hi = mid;
         }
         s_nb[t] = lo;
     }
     __syncthreads();
     const int nb0 = s_nb[0], cnt = s_nb[1] - nb0;
-    for (int k = t; k < cnt; k += kIncTile) s_np[k] = J.npos[nb0 + k];
+    for (int k = t; k < cnt; k += kIncTile) s_np[k] = npos[nb0 + k];
     __syncthreads();
 #pragma unroll
     for (int u = 0; u < kIncPer; ++u) {
@@ -1045,22 +1055,22 @@ __device__ __forceinline__ void pt_inc_merge2(const PtIncJob &J) {
             int32_t id;
             if (lo < cnt && s_np[lo] == p) {
                 const int j = nb0 + lo;
-                const int64_t r = J.nvals[j];
-                key = J.nkeys[j];
+                const int64_t r = nvals[j];
+                key = nkeys[j];
                 id = (int32_t)r + 1;
 #pragma unroll
-                for (int k = 0; k < D; ++k) row[k] = J.pts[r * D + k];
+                for (int k = 0; k < D; ++k) row[k] = pts[r * D + k];
             } else {
                 const int64_t o = p - nb0 - lo;
-                key = J.okeys[o];
-                id = J.oids[o];
+                key = okeys[o];
+                id = oids[o];
 #pragma unroll
-                for (int k = 0; k < D; ++k) row[k] = J.opts[o * D + k];
+                for (int k = 0; k < D; ++k) row[k] = opts[o * D + k];
             }
-            J.keys[p] = key;
-            J.ids[p] = id;
+            keys[p] = key;
+            ids[p] = id;
 #pragma unroll
-            for (int k = 0; k < D; ++k) J.spts[p * D + k] = row[k];
+            for (int k = 0; k < D; ++k) spts[p * D + k] = row[k];
         }
 #pragma unroll
         for (int k = 0; k < D; ++k) {
@@ -1072,7 +1082,7 @@ __device__ __forceinline__ void pt_inc_merge2(const PtIncJob &J) {
                 hi = ohi > hi ? ohi : hi;
             }
             if (live && (p & (kPtFan - 1)) == 0) {
-                float *bx = J.boxes + (p / kPtFan) * 2 * D;
+                MPT_GLOBAL float *bx = boxes + (p / kPtFan) * 2 * D;
                 bx[k] = widen_lo(lo);
                 bx[D + k] = widen_hi(hi);
             }
