@@ -204,7 +204,8 @@ def inc_build_bytes(n, m, d):
     new this round (point_tree.hip): the sort reads the new rows and writes their (code, row)
     pairs; the merge reads the old sorted (code, id, row) records and the new pairs and rows,
     and writes n sorted records and the leaf boxes; the box levels above read and write the
-    boxes (about n / 7 boxes of 2d floats in all)."""
+    boxes (about n / 7 boxes of 2d floats in all).  The chunked sort's intermediate passes over
+    the m pairs (chunks, ranks, output places) are the algorithm's, not the minimum's."""
     rec = 8 + 4 + 8 * d
     return m * (8 * d + 12) + (n - m) * rec + m * (12 + 8 * d) + n * rec + (n // 7) * 8 * d * 2
 
@@ -339,7 +340,8 @@ def stage_table(per_launch, cst, K, n0, d, pmax, geo, nn_mode, kernels, summ):
 # measured traffic per launch is summed (the collide chain runs once per collide sub-batch)
 JOINT_STAGE_KERNELS = {
     "sample": ["k_sample_jobs"],
-    "nn_build": ["k_pt_inc_sort", "k_pt_inc_merge", "k_pt_inc_boxes", "k_pt_inc_top"],
+    "nn_build": ["k_pt_inc_ncodes", "k_pt_inc_csort", "k_pt_inc_crank", "k_pt_inc_npos", "k_pt_inc_merge",
+                 "k_pt_inc_boxes", "k_pt_inc_top"],
     "nn_query": ["k_tree_nn1_jobs"],
     "steer": ["k_steer_jobs"],
     "collide": ["k_pairs<", "k_scan_excl<mpt::ExpandHeaders", "k_cands", "k_narrow", "k_overflow"],
