@@ -7,6 +7,7 @@
 # workload's summary.  PART=c: config 5's passes (joint rounds only) and bench lines.  Every GPU step has
 # its own time limit; the script stops at the first failure.
 #   TAG=r16 PART=a bash scripts/measure_r3.sh && TAG=r16 PART=b bash scripts/measure_r3.sh
+# (C5=1 with PART=b: also config 5's bench lines, from part a's committed c5 summaries)
 TAG=${TAG:?set TAG}
 OUT=gpurun_out/m_$TAG
 P=$OUT/$TAG  # copied to profiles/$TAG afterwards
@@ -60,6 +61,12 @@ else
   run snake 300 python bench.py --workload snake --steps 20 --warmup 3 --cpu-seconds 15 --no-variants --traffic $R/snake/pmc_summary.json
   run prm 300 python scripts/bench_prm.py --traffic $P/prm/pmc_summary.json
   for c in c2 room snake prm; do grep '^{' $OUT/$c.log > $P/bench_$c.json; done
+  # config 5's lines from part a's summaries (PART=c re-profiles them instead)
+  if [ -n "$C5" ]; then
+    run c5_32 300 python bench.py --seeds 32 --traffic $R/c5_32/pmc_summary.json
+    run c5_256 300 python bench.py --seeds 256 --traffic $R/c5_256/pmc_summary.json
+    for c in c5_32 c5_256; do grep '^{' $OUT/$c.log > $P/bench_$c.json; done
+  fi
   echo part b done
 fi
 du -sh gpurun_out
