@@ -32,6 +32,10 @@ constexpr int kDistWaves = 4;
 // a bucket's queued pairs are evaluated at its end once at least this many wait
 // (MPT_DIST_FLUSH: A/B; 1 = after every bucket: 4 % slower on the blimp in the room)
 __constant__ int32_t c_dist_flush = 32;
+// the first pass's bound scale (MPT_DIST_ALPHA; 1 = one pass).  Blimp vs room, 65 536 poses,
+// alpha 1 / 0.7 / 0.5 / 0.3: 8.04 / 7.68 / 7.65 / 7.89 ms (triDistance calls 65.2 / 37.0 / 35.7
+// / 37.3 M); the reference's last submesh 3.81 / 2.43 / 2.38 / 2.55 ms
+__constant__ double c_dist_alpha = 0.5;
 constexpr int kDistStack = kMaxLevels * kWave;
 
 __device__ __forceinline__ double read_best(const unsigned long long *p) {
@@ -70,6 +74,7 @@ struct DistCounters {
 struct DistLds {
     double q[kWave][9];        // Q' of the cluster's triangles, by lane
     int32_t queue[2 * kWave];  // pending (env tri << 6 | agent lane) pairs
+    float qgap[2 * kWave];     // their squared box gaps, rounded down (re-tested at the flush)
     int32_t stk_il[kDistStack];  // item << 3 | level (kMaxLevels <= 8)
     float stk_b[kDistStack];
 };
@@ -80,7 +85,12 @@ template <int kOcc, bool kSel>
 __device__ __forceinline__ double flush_pairs(const EnvDev &env, DistLds &s, int n, int lane, double U,
                                               unsigned long long *bp, DistCounters &cnt) {
     double d = DBL_MAX;
-    if (lane < n) {
+    // a pair queued against an older bound is re-tested against the current one (its gap
+    // rounded down: never drops a pair the exact test keeps)
+    const double Un = uniform_d(dmin(U, read_best(bp)));
+    const double thr = Un * (1.0 + 1e-9) + 1e-9;
+    const bool ev = lane < n && (double)s.qgap[lane] <= thr * thr;
+    if (ev) {
         const int32_t e = s.queue[lane];
         const double *qa = s.q[e & 63];
         const EnvTri &E = env.tris[e >> 6];
@@ -89,7 +99,7 @@ __device__ __forceinline__ double flush_pairs(const EnvDev &env, DistLds &s, int
         // at 4 waves per SIMD the rolled form (128 VGPRs); else the unrolled one
         d = tri_distance<kOcc >= 4 ? 1 : 3, kSel>(S, E.lo, E.hi, Q);
     }
-    cnt.tri_calls += (uint32_t)n;
+    cnt.tri_calls += (uint32_t)__popcll(__ballot(ev));
     const double wb = wave_min_d(d);
     if (wb < U) {
         if (lane == 0) atomicMin(bp, (unsigned long long)__double_as_longlong(wb));
@@ -104,13 +114,14 @@ __device__ __forceinline__ double flush_pairs(const EnvDev &env, DistLds &s, int
 template <int kOcc, bool kSel>
 __device__ double walk_cluster(const EnvDev &env, DistLds &s, const float cblo[3], const float cbhi[3], bool act,
                                const double qlo[3], const double qhi[3], const double xlo[3], const double xhi[3],
-                               int lane, double U, unsigned long long *bp, DistCounters &cnt) {
+                               int lane, double U, unsigned long long *bp, DistCounters &cnt, double alpha,
+                               double lo2) {
     int sp = 0, qn = 0;
     int lev = env.n_levels - 1;
     int32_t first = env.lev_off[lev];
     int32_t count = env.lev_off[lev + 1] - first;
     for (;;) {
-        const float Uf2 = prune2(U);
+        const float Uf2 = prune2(alpha * U);
         float lb = __builtin_huge_valf();
         int32_t cf = 0, cc = 0;
         bool keep = false;
@@ -127,7 +138,7 @@ __device__ double walk_cluster(const EnvDev &env, DistLds &s, const float cblo[3
             while (m) {
                 const int j = __ffsll((unsigned long long)m) - 1;
                 m &= m - 1;
-                if (__shfl(lb, j) > prune2(U)) continue;
+                if (__shfl(lb, j) > prune2(alpha * U)) continue;
                 const int32_t bf = __builtin_amdgcn_readfirstlane(__shfl(cf, j));
                 const int32_t bc = __builtin_amdgcn_readfirstlane(__shfl(cc, j));
                 int32_t seed_t = -1;
@@ -150,7 +161,11 @@ __device__ double walk_cluster(const EnvDev &env, DistLds &s, const float cblo[3
                     }
                     if (!act) seed_t = -1;
                     const uint64_t pm = __ballot(act);
-                    if (act) s.queue[(int)__popcll(pm & ((1ull << lane) - 1))] = (seed_t << 6) | lane;
+                    if (act) {
+                        const int pos = (int)__popcll(pm & ((1ull << lane) - 1));
+                        s.queue[pos] = (seed_t << 6) | lane;
+                        s.qgap[pos] = 0.0f;
+                    }
                     U = flush_pairs<kOcc, kSel>(env, s, (int)__popcll(pm), lane, U, bp, cnt);
                     if (U == 0.0) return U;
                 }
@@ -159,7 +174,7 @@ __device__ double walk_cluster(const EnvDev &env, DistLds &s, const float cblo[3
                 // pair of any other triangle has a box gap above the bound (no lane would pass)
                 uint64_t tm;
                 {
-                    const double thr = U * (1.0 + 1e-9) + 1e-9;
+                    const double thr = alpha * U * (1.0 + 1e-9) + 1e-9;
                     bool near = false;
                     if (lane < bc) {
                         const EnvTri &E = env.tris[bf + lane];
@@ -177,22 +192,29 @@ __device__ double walk_cluster(const EnvDev &env, DistLds &s, const float cblo[3
                     const int32_t t = bf + __ffsll((unsigned long long)tm) - 1;
                     tm &= tm - 1;
                     const EnvTri &E = env.tris[t];
-                    const double thr = U * (1.0 + 1e-9) + 1e-9;
+                    const double thr = alpha * U * (1.0 + 1e-9) + 1e-9;
                     double g2 = 0.0;
 #pragma unroll
                     for (int k = 0; k < 3; ++k) {
                         const double g = dmax(dmax(E.lo[k] - qhi[k], qlo[k] - E.hi[k]), 0.0);
                         g2 += g * g;
                     }
-                    const bool pass = act && t != seed_t && g2 <= thr * thr;
+                    const bool pass = act && t != seed_t && g2 <= thr * thr && g2 > lo2;
                     const uint64_t pm = __ballot(pass);
-                    if (pass) s.queue[qn + (int)__popcll(pm & ((1ull << lane) - 1))] = (t << 6) | lane;
+                    if (pass) {
+                        const int pos = qn + (int)__popcll(pm & ((1ull << lane) - 1));
+                        s.queue[pos] = (t << 6) | lane;
+                        s.qgap[pos] = __double2float_rd(g2);
+                    }
                     qn += (int)__popcll(pm);
                     cnt.pair_tests += (uint32_t)__popcll(__ballot(act));
                     if (qn >= kWave) {
                         U = flush_pairs<kOcc, kSel>(env, s, kWave, lane, U, bp, cnt);
                         qn -= kWave;
-                        if (lane < qn) s.queue[lane] = s.queue[kWave + lane];
+                        if (lane < qn) {
+                            s.queue[lane] = s.queue[kWave + lane];
+                            s.qgap[lane] = s.qgap[kWave + lane];
+                        }
                         if (U == 0.0) return U;
                     }
                 }
@@ -232,7 +254,7 @@ __device__ double walk_cluster(const EnvDev &env, DistLds &s, const float cblo[3
             continue;
         }
         // pop the next pending subtree that can still hold the minimum
-        const float Uf2p = prune2(U);
+        const float Uf2p = prune2(alpha * U);
         bool found = false;
         while (sp > 0) {
             --sp;
@@ -288,6 +310,17 @@ __device__ void distance_unit(const EnvDev &env, const AgentDev *__restrict__ li
                 clb = fminf(clb, gap2f(clo, chi, it.lo, it.hi));
             }
         }
+        // Two passes (c_dist_alpha < 1): the first walks every cluster against alpha * U (its
+        // nodes pruned and its pairs queued on that tighter bound), so the pairs nearest to the
+        // unit are evaluated first and the bound falls to near its final value; the second walks
+        // against U for the pairs the first left, those with a gap above alpha * U_A (U_A the
+        // bound after the first; every pair the first queued had a gap at most alpha * U(t)
+        // with U(t) >= U_A, so none is skipped).  One pass evaluated ~5x the pairs whose gap is
+        // within the final distance, most of them against a bound still far from it.
+        const int npass = c_dist_alpha < 1.0 ? 2 : 1;
+        double lo2 = -1.0;
+        for (int pass = 0; pass < npass; ++pass) {
+        const double alpha = pass == 0 && npass == 2 ? c_dist_alpha : 1.0;
         uint64_t rem = __ballot(ci < ag.n_clusters);
         while (rem) {
             // nearest remaining cluster first
@@ -304,7 +337,7 @@ __device__ void distance_unit(const EnvDev &env, const AgentDev *__restrict__ li
             }
             const int j = __builtin_amdgcn_readfirstlane(idx);
             rem &= ~(1ull << j);
-            if (__shfl(clb, j) > prune2(U)) break;  // the rest are farther still
+            if (__shfl(clb, j) > prune2(alpha * U)) break;  // the rest are farther still
             ++cnt.clusters;
             float cblo[3], cbhi[3];
 #pragma unroll
@@ -346,8 +379,13 @@ __device__ void distance_unit(const EnvDev &env, const AgentDev *__restrict__ li
                 xlo[k] = uniform_d(lo);
                 xhi[k] = uniform_d(hi);
             }
-            U = walk_cluster<kOcc, kSel>(env, s, cblo, cbhi, act, qlo, qhi, xlo, xhi, lane, U, bp, cnt);
+            U = walk_cluster<kOcc, kSel>(env, s, cblo, cbhi, act, qlo, qhi, xlo, xhi, lane, U, bp, cnt, alpha, lo2);
             if (U == 0.0) return;
+        }
+        if (pass == 0 && npass == 2) {
+            const double ua = c_dist_alpha * U;
+            lo2 = ua * ua * (1.0 - 1e-12);  // below every first-pass threshold (rounding margin)
+        }
         }
     }
 }
@@ -394,6 +432,9 @@ void launch_distance(const EnvDev &env, const AgentDev *d_links, const DistWork 
     static const bool flush_set = [] {
         const int32_t f = getenv("MPT_DIST_FLUSH") ? atoi(getenv("MPT_DIST_FLUSH")) : 32;
         hip_check(hipMemcpyToSymbol(HIP_SYMBOL(c_dist_flush), &f, sizeof f), "flush threshold");
+        double al = getenv("MPT_DIST_ALPHA") ? atof(getenv("MPT_DIST_ALPHA")) : 0.5;
+        if (!(al > 0.0 && al <= 1.0)) al = 0.5;
+        hip_check(hipMemcpyToSymbol(HIP_SYMBOL(c_dist_alpha), &al, sizeof al), "first-pass scale");
         return true;
     }();
     (void)flush_set;
