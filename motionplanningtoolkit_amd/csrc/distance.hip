@@ -36,6 +36,10 @@ __constant__ int32_t c_dist_flush = 32;
 // alpha 1 / 0.7 / 0.5 / 0.3: 8.04 / 7.68 / 7.65 / 7.89 ms (triDistance calls 65.2 / 37.0 / 35.7
 // / 37.3 M); the reference's last submesh 3.81 / 2.43 / 2.38 / 2.55 ms
 __constant__ double c_dist_alpha = 0.5;
+// clusters the first pass walks at most (MPT_DIST_PASSA): the nearest one sets the bound nearly
+// as well as all of them, without their second walk (blimp: 1 / 2 / 4 / all: 6.45 / 6.54 / 6.65
+// / 7.65 ms, calls 36.4 / 36.4 / 36.3 / 35.7 M)
+__constant__ int32_t c_dist_passa = 1;
 constexpr int kDistStack = kMaxLevels * kWave;
 
 __device__ __forceinline__ double read_best(const unsigned long long *p) {
@@ -310,7 +314,7 @@ __device__ void distance_unit(const EnvDev &env, const AgentDev *__restrict__ li
                 clb = fminf(clb, gap2f(clo, chi, it.lo, it.hi));
             }
         }
-        // Two passes (c_dist_alpha < 1): the first walks every cluster against alpha * U (its
+        // Two passes (c_dist_alpha < 1): the first walks the nearest cluster(s) against alpha * U (its
         // nodes pruned and its pairs queued on that tighter bound), so the pairs nearest to the
         // unit are evaluated first and the bound falls to near its final value; the second walks
         // against U for the pairs the first left, those with a gap above alpha * U_A (U_A the
@@ -319,10 +323,14 @@ __device__ void distance_unit(const EnvDev &env, const AgentDev *__restrict__ li
         // within the final distance, most of them against a bound still far from it.
         const int npass = c_dist_alpha < 1.0 ? 2 : 1;
         double lo2 = -1.0;
+        uint64_t first_walked = 0;  // the clusters the first pass walked (only their pairs are excluded)
         for (int pass = 0; pass < npass; ++pass) {
         const double alpha = pass == 0 && npass == 2 ? c_dist_alpha : 1.0;
         uint64_t rem = __ballot(ci < ag.n_clusters);
+        int32_t walked = 0;
         while (rem) {
+            if (pass == 0 && npass == 2 && walked >= c_dist_passa) break;
+            ++walked;
             // nearest remaining cluster first
             float v = (rem >> lane) & 1 ? clb : __builtin_huge_valf();
             int idx = lane;
@@ -338,6 +346,7 @@ __device__ void distance_unit(const EnvDev &env, const AgentDev *__restrict__ li
             const int j = __builtin_amdgcn_readfirstlane(idx);
             rem &= ~(1ull << j);
             if (__shfl(clb, j) > prune2(alpha * U)) break;  // the rest are farther still
+            if (pass == 0) first_walked |= 1ull << j;
             ++cnt.clusters;
             float cblo[3], cbhi[3];
 #pragma unroll
@@ -379,7 +388,8 @@ __device__ void distance_unit(const EnvDev &env, const AgentDev *__restrict__ li
                 xlo[k] = uniform_d(lo);
                 xhi[k] = uniform_d(hi);
             }
-            U = walk_cluster<kOcc, kSel>(env, s, cblo, cbhi, act, qlo, qhi, xlo, xhi, lane, U, bp, cnt, alpha, lo2);
+            U = walk_cluster<kOcc, kSel>(env, s, cblo, cbhi, act, qlo, qhi, xlo, xhi, lane, U, bp, cnt, alpha,
+                                         pass == 1 && ((first_walked >> j) & 1) ? lo2 : -1.0);
             if (U == 0.0) return;
         }
         if (pass == 0 && npass == 2) {
@@ -435,6 +445,8 @@ void launch_distance(const EnvDev &env, const AgentDev *d_links, const DistWork 
         double al = getenv("MPT_DIST_ALPHA") ? atof(getenv("MPT_DIST_ALPHA")) : 0.5;
         if (!(al > 0.0 && al <= 1.0)) al = 0.5;
         hip_check(hipMemcpyToSymbol(HIP_SYMBOL(c_dist_alpha), &al, sizeof al), "first-pass scale");
+        const int32_t pa = getenv("MPT_DIST_PASSA") ? std::max(1, atoi(getenv("MPT_DIST_PASSA"))) : 1;
+        hip_check(hipMemcpyToSymbol(HIP_SYMBOL(c_dist_passa), &pa, sizeof pa), "first-pass clusters");
         return true;
     }();
     (void)flush_set;
