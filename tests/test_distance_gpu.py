@@ -117,6 +117,35 @@ def test_multi_room_env_deep_tree(mpt_gpu, oracle, nx, ny):
     check(mpt_gpu, oracle, env, pose([0, 0, 0]), [agent], poses, np.arange(n + 1))
 
 
+def test_agent_over_64_clusters(mpt_gpu, oracle):
+    """An agent of more than 64 clusters (four blimps side by side, 5420 triangles): the walk
+    takes its clusters 64 at a time, each chunk with its own two passes (the first over the
+    nearest cluster against half the bound, the second excluding only that cluster's pairs)."""
+    blimp = np.asarray(scenes.read_obj(scenes.mesh_path("agent_blimp"), "all"), np.float64).reshape(-1, 9)
+    shifts = [(0, 0, 0), (40, 0, 0), (0, 40, 0), (40, 40, 0)]
+    agent = np.concatenate([blimp + np.tile(np.asarray(d, np.float64), 3) for d in shifts])
+    assert len(agent) > 64 * 64
+    env = scenes.read_obj(scenes.mesh_path("env_model"))
+    rng = np.random.default_rng(41)
+    n = 120
+    ts = rng.uniform([-60, -60, -30], [200, 160, 140], size=(n, 3))
+    poses = np.array([pose(t, random_rot(rng)) for t in ts]).reshape(-1, 1, 12)
+    got = check(mpt_gpu, oracle, env, pose([0, 0, 0]), [agent], poses, np.arange(n + 1))
+    assert (got == 0).any() and (got > 1).any()
+
+
+@pytest.mark.parametrize("nx,ny", [(2, 2)])
+def test_multi_room_env_full_blimp(mpt_gpu, oracle, nx, ny):
+    """The deep env tree with the 22-cluster blimp: both passes over several clusters."""
+    env = scenes.rooms_env(nx, ny)
+    agent = scenes.read_obj(scenes.mesh_path("agent_blimp"), "all")
+    rng = np.random.default_rng(29)
+    n = 100
+    ts = rng.uniform([-10, -10, -10], [nx * 180 + 10, ny * 140 + 10, 125], size=(n, 3))
+    poses = np.array([pose(t, random_rot(rng)) for t in ts]).reshape(-1, 1, 12)
+    check(mpt_gpu, oracle, env, pose([0, 0, 0]), [agent], poses, np.arange(n + 1))
+
+
 def test_distance_agrees_with_collision(mpt_gpu):
     """Size-independent property at a larger batch: a colliding pose is at distance ~0 and a
     pose at a clear positive distance is collision free."""
