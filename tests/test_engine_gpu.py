@@ -111,13 +111,16 @@ def test_engine_rounds(mpt_gpu, oracle, name, nn_mode):
     tree, _ = check_round(mpt_gpu, oracle, sc, eng, tree, seed, K, K // 2 + 3)
 
 
-def test_engine_tree_nn_large_blob(mpt_gpu, oracle):
+@pytest.mark.parametrize("K", [2048, 6144])
+def test_engine_tree_nn_large_blob(mpt_gpu, oracle, K):
     """Morton-tree NN (config 5's structure) over a 40k-node RRT-like blob: more than 4096
     points, so the box build spans several workgroups and the last one to finish builds
-    levels 5 and 6 (k_pt_boxes' ticket path); two rounds, the second after the ticket reset."""
+    levels 5 and 6 (k_pt_boxes' ticket path); two rounds, the second after the ticket reset.
+    The second round's build is incremental: K = 6144 appends more than 4096 points, so the
+    chunked sort ranks across more than 8 chunks of 512."""
     sc = scenes.blimp_scenario("all")
     rng = np.random.default_rng(77)
-    n0, K = 40_000, 2048
+    n0 = 40_000
     tree = rng.uniform(sc.ranges[:, 0], sc.ranges[:, 1], size=(n0, sc.dim))
     tree[:, :3] = np.array([88.6, 68.9, 57.1]) + rng.normal(0.0, 6.0, size=(n0, 3))
     env = mpt_gpu.Environment(sc.env_tris, sc.env_tf)
