@@ -1339,7 +1339,14 @@ __device__ __forceinline__ void tree_nn1_block(const PointTreeDev &T, const doub
 // steps of the one-node walk for a few more nodes visited; the result is the same exact 1-NN
 // (any visiting order is: only boxes whose lower bound exceeds the best are skipped).  The
 // stack holds at most ~14 entries a level (two sibling blocks of 7) + 2: 2 * 8 * 10 entries.
-constexpr int64_t kPtNnWideMaxQueries = 262144;  // the four-node walk up to this many queries a launch
+constexpr int64_t kPtNnWideMaxQueries = 262144;  // d = 15: the four-node walk up to this many queries a launch
+
+// nodes a walk step by default: d <= 7 eight (one query a wave) at every launch size; d = 15 (its
+// registers) four up to kPtNnWideMaxQueries queries, else one
+inline int pt_nn_width(int32_t d, int64_t queries) {
+    if (d <= 7) return 8;
+    return queries <= kPtNnWideMaxQueries ? 4 : 1;
+}
 
 // NW nodes a step (2 or 4): 8 * NW lanes per query, the stack's top NW entries popped together
 template <int D, int BS, int NW>
@@ -1394,7 +1401,7 @@ __device__ __forceinline__ void tree_nn1_blockn(const PointTreeDev &T, const dou
             const bool act = have && !(lbs * (1.0 - 1e-12) > bd);
             const int lev = act ? code >> 27 : 0;
             const int64_t idx = code & ((1 << 27) - 1);
-            bool keep = false;
+            bool keep = false, leaf = false;
             float lbf = 0.0f;
             int64_t c = 0;
             if (lev == 1) {
@@ -1403,6 +1410,7 @@ __device__ __forceinline__ void tree_nn1_blockn(const PointTreeDev &T, const dou
                     const double dd = leaf_l2<D>(qq, T, p);
                     const int32_t id = leaf_id(T, p);
                     ++n_pts;
+                    leaf = true;
                     if (nn_better(dd, id, bd, bi)) {
                         bd = dd;
                         bi = id;
@@ -1418,26 +1426,33 @@ __device__ __forceinline__ void tree_nn1_blockn(const PointTreeDev &T, const dou
                     ++n_box;
                 }
             }
-            // the two halves' best, then the survivors against it
+            // the parts' best, then the survivors against it.  Wave-uniform skips: a group's
+            // lanes already share one best unless a lane examined a point this step, and with no
+            // survivor in the wave there is nothing to rank
+            if (__ballot(leaf)) {
 #pragma unroll
-            for (int off = kPtG2 / 2; off > 0; off >>= 1) {
-                const double od = __shfl_xor(bd, off, kPtG2);
-                const int32_t oi = __shfl_xor(bi, off, kPtG2);
-                if (nn_better(od, oi, bd, bi)) {
-                    bd = od;
-                    bi = oi;
+                for (int off = kPtG2 / 2; off > 0; off >>= 1) {
+                    const double od = __shfl_xor(bd, off, kPtG2);
+                    const int32_t oi = __shfl_xor(bi, off, kPtG2);
+                    if (nn_better(od, oi, bd, bi)) {
+                        bd = od;
+                        bi = oi;
+                    }
                 }
             }
             keep = keep && (double)lbf * (1.0 - 1e-12) <= bd;
-            const uint64_t gm = (__ballot(keep) >> base) & (kPtG2 == 64 ? ~0ull : ((1ull << kPtG2) - 1));
+            const uint64_t wm = __ballot(keep);
+            const uint64_t gm = (wm >> base) & (kPtG2 == 64 ? ~0ull : ((1ull << kPtG2) - 1));
             const uint32_t mine = (uint32_t)(gm >> (half * kPtFan)) & 0xffu;
             // deeper entries' survivors go below: positions after every later half's
             const int below = __popcll(half + 1 < NW ? gm >> ((half + 1) * kPtFan) : 0ull);
             int rank = 0;
+            if (wm) {
 #pragma unroll
-            for (int j = 0; j < kPtFan; ++j) {
-                const float o = __shfl(lbf, half * kPtFan + j, kPtG2);
-                if (((mine >> j) & 1u) && (o > lbf || (o == lbf && j > ls))) ++rank;
+                for (int j = 0; j < kPtFan; ++j) {
+                    const float o = __shfl(lbf, half * kPtFan + j, kPtG2);
+                    if (((mine >> j) & 1u) && (o > lbf || (o == lbf && j > ls))) ++rank;
+                }
             }
             if (keep) {
                 const int pos = sp + below + rank;
@@ -2014,15 +2029,17 @@ void launch_tree_nn1(const PointTreeDev &T, const double *q, int64_t nq, int32_t
     static const int bs = getenv("MPT_PT_NN1_BLOCK") ? atoi(getenv("MPT_PT_NN1_BLOCK")) : 64;
     // nodes expanded per step: as the joint launch (MPT_PT_NN_W forces one)
     static const int w_env = getenv("MPT_PT_NN_W") ? atoi(getenv("MPT_PT_NN_W")) : 0;
-    const int w = w_env > 0 ? w_env : (nq <= kPtNnWideMaxQueries ? 4 : 1);
+    const int w = w_env > 0 ? w_env : pt_nn_width(T.d, nq);
     if (bs == 256)
         w == 1 ? launch_tree_nn1_bs<256, 1>(T, q, nq, ids, d2, stream, order)
                : (w == 2 ? launch_tree_nn1_bs<256, 2>(T, q, nq, ids, d2, stream, order)
-                         : launch_tree_nn1_bs<256, 4>(T, q, nq, ids, d2, stream, order));
+                         : (w == 4 ? launch_tree_nn1_bs<256, 4>(T, q, nq, ids, d2, stream, order)
+                                   : launch_tree_nn1_bs<256, 8>(T, q, nq, ids, d2, stream, order)));
     else
         w == 1 ? launch_tree_nn1_bs<64, 1>(T, q, nq, ids, d2, stream, order)
                : (w == 2 ? launch_tree_nn1_bs<64, 2>(T, q, nq, ids, d2, stream, order)
-                         : launch_tree_nn1_bs<64, 4>(T, q, nq, ids, d2, stream, order));
+                         : (w == 4 ? launch_tree_nn1_bs<64, 4>(T, q, nq, ids, d2, stream, order)
+                                   : launch_tree_nn1_bs<64, 8>(T, q, nq, ids, d2, stream, order)));
 }
 
 template <int BS, int W>
@@ -2041,13 +2058,14 @@ static void launch_tree_nn1_jobs_bs(const PtJob *d_jobs, int32_t n_jobs, int32_t
 
 void launch_tree_nn1_jobs(const PtJob *d_jobs, int32_t n_jobs, int32_t d, int64_t nq, hipStream_t stream) {
     if (nq <= 0 || n_jobs <= 0) return;
-    // The multi-node walk cuts a query's dependent steps (four nodes a step: a quarter) for more
-    // nodes visited: it pays when the launch leaves the chip waiting on its slowest waves and
-    // costs when the launch keeps every SIMD busy.  Config 5 round time by nodes a step (1 / 2 /
-    // 4): 32 seeds (131 072 queries) 3.24 / 2.75 / 2.26 ms, 64 seeds 5.27 / 4.65 / 4.07 ms, 256
-    // seeds (1 M queries) 13.66 / 13.86 / 13.97 ms.  MPT_PT_NN_W = 1 / 2 / 4 forces one (A/B).
+    // The multi-node walk cuts a query's dependent steps (eight nodes a step: an eighth) for
+    // more nodes visited.  With the parts' best merged only on steps where a lane examined a
+    // point and the ranks skipped on steps without a survivor, the widest walk wins at every
+    // size: config 5 round time by nodes a step (1 / 2 / 4 / 8), 32 seeds (131 072 queries)
+    // - / - / 1.86 / 1.59 ms, 64 seeds - / - / 3.36 / 2.97 ms, 256 seeds (1 M queries) 12.83 /
+    // 12.53 / 11.26 / 10.80 ms.  MPT_PT_NN_W = 1 / 2 / 4 / 8 forces one (A/B).
     static const int w_env = getenv("MPT_PT_NN_W") ? atoi(getenv("MPT_PT_NN_W")) : 0;
-    const int w = w_env > 0 ? w_env : ((int64_t)n_jobs * nq <= kPtNnWideMaxQueries ? 4 : 1);
+    const int w = w_env > 0 ? w_env : pt_nn_width(d, (int64_t)n_jobs * nq);
     if (w == 1) launch_tree_nn1_jobs_bs<64, 1>(d_jobs, n_jobs, d, nq, stream);
     else if (w == 4) launch_tree_nn1_jobs_bs<64, 4>(d_jobs, n_jobs, d, nq, stream);
     else if (w == 8) launch_tree_nn1_jobs_bs<64, 8>(d_jobs, n_jobs, d, nq, stream);
