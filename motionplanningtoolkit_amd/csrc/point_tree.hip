@@ -1493,9 +1493,11 @@ __global__ __launch_bounds__(BS) void k_tree_nn1(PointTreeDev T, const double *_
 // and its tree stays in that XCD's L2.
 // 8 waves per SIMD for d <= 7 (56 VGPRs, no spill); d = 15 would spill at 8, so 4 (108 VGPRs)
 // W = 2: the two-node walk (tree_nn1_block2, 16 lanes per query), at 7 waves per SIMD for
-// d <= 7 (72 VGPRs: the 8-wave budget spilled 8 a lane and ran 9 % slower)
+// d <= 7 (72 VGPRs: the 8-wave budget spilled 8 a lane and ran 9 % slower); W = 8 (the default
+// eight-node walk, one query a wave) at 8 waves: 64 VGPRs with 2 spilled vs 66 at 7 waves, joint
+// NN 0.964 -> 0.945 ms (32 seeds), 7.36 -> 7.28 ms (256 seeds), profiles/r19/ab_c5/w8_summary.txt
 template <int D, int BS, int W>
-__global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(D >= 15 ? 4 : (W >= 2 ? 7 : 8)))) void k_tree_nn1_jobs(
+__global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(D >= 15 ? 4 : (W >= 2 && W < 8 ? 7 : 8)))) void k_tree_nn1_jobs(
     const PtJob *__restrict__ jobs, int32_t n_jobs, int64_t nq, int64_t blocks_per_job) {
     const int64_t xcd = blockIdx.x % kXcds, slot = blockIdx.x / kXcds;
     const int64_t job = xcd + kXcds * (slot / blocks_per_job);
