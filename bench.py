@@ -82,7 +82,18 @@ def parse():
                          "and joint stream, so one group's NN launch overlaps another's build / collide")
     ap.add_argument("--launch-threads", type=int, default=1,
                     help="config 5 with --no-joint-nn: host threads issuing the seeds' rounds")
+    ap.add_argument("--c5-seeds", type=int, default=256,
+                    help="the config-5 leg (every run without --seeds): seeds over all ranks (BASELINE config 5: "
+                         "256, contiguous shards, 32 per GPU at 8 GPUs)")
+    ap.add_argument("--c5-steps", type=int, default=C5_STEPS, help="the config-5 leg's timed rounds")
+    ap.add_argument("--c5-warmup", type=int, default=C5_WARMUP, help="the config-5 leg's untimed rounds before them")
     return ap.parse_args()
+
+
+# config 5 is measured at these rounds in every leg (the 32- and 256-seed legs of an N = 1 run,
+# the in-world leg of an N > 1 run, and the PMC profiles their traffic columns come from), so
+# their trees have the same sizes and their per-GPU ratio compares like with like
+C5_STEPS, C5_WARMUP = 25, 5
 
 
 # ----------------------------------------------------------------------------- CPU baseline
@@ -379,6 +390,11 @@ def joint_stage_table(times, c, K, nj, n_tot, d, pmax, geo, summ):
                         + (f" ({n_sub} collide sub-batches)" if s == "collide" else "")}
         if index_b:
             st["index_bytes"] = int(index_b)
+        if s == "nn_query" and c.get("nn_points"):
+            # work counters of the stats round (the same trees and queries): points examined and
+            # boxes tested per query
+            st["nn_points_per_query"] = round(c["nn_points"] / (K * nj), 2)
+            st["nn_boxes_per_query"] = round(c["nn_cells"] / (K * nj), 2)
         trs = [pmc_traffic(summ, k) for k in JOINT_STAGE_KERNELS.get(s, [])]
         if trs and all(x is not None for x in trs):
             tr = sum(trs) * (n_sub if s == "collide" else 1)
@@ -506,6 +522,12 @@ def run_seeds(args, world, rank, dist, torch, mpt, multiseed, scenes):
             for f in [pool.submit(drive, g) for g in groups]:
                 f.result()
 
+    # from scratch: every round from the seeds' start states (the first rounds' index
+    # reservations included), then the timed rounds continue the same trees
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t_scratch = time.perf_counter()
     for _ in range(args.warmup):
         round_()
     torch.cuda.synchronize()
@@ -525,11 +547,15 @@ def run_seeds(args, world, rank, dist, torch, mpt, multiseed, scenes):
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
-    elapsed = time.perf_counter() - t0
+    t1 = time.perf_counter()
+    elapsed = t1 - t0
+    scratch = t1 - t_scratch
     c1 = [e.counters() for e in engines]
     valid = sum(b["valid"] - a["valid"] for a, b in zip(c0, c1))
     checked = sum(b["checked"] - a["checked"] for a, b in zip(c0, c1))
+    valid_all = sum(b["valid"] for b in c1)
     elapsed, (valid, checked) = multiseed.reduce_run(dist, elapsed, [valid, checked], args.red_dev)
+    scratch, (valid_all,) = multiseed.reduce_run(dist, scratch, [valid_all], args.red_dev)
     digests = {}
     for i, e, c in zip(mine, engines, c1):
         st, par = e.read_tree(c["nodes"])
@@ -632,6 +658,11 @@ def run_seeds(args, world, rank, dist, torch, mpt, multiseed, scenes):
         "per_seed_valid_per_s": valid / elapsed / max(args.seeds, 1),
         "host_enqueue_ms_per_step": 1e3 * host / args.steps,
         "seeds_digest": all_digest,
+        "world_size": dist.get_world_size() if dist else 1,
+        "from_scratch": {"rounds": args.warmup + args.steps, "wall_s": round(scratch, 4),
+                         "valid_per_s": valid_all / scratch,
+                         "note": "wall time of every round from the seeds' start states (the warm-up rounds, "
+                                 "their first-use index reservations, and the timed rounds), max over ranks"},
         "roofline": roof,
         "cpu_baseline": None,
     }
@@ -640,22 +671,28 @@ def run_seeds(args, world, rank, dist, torch, mpt, multiseed, scenes):
 # ----------------------------------------------------------------------------- variants
 
 # the secondary workloads measured in the same run as config 2 (one short leg each, in a
-# process of its own so one leg's device state never affects another's timing)
+# process of its own so one leg's device state never affects another's timing): name ->
+# (script, arguments).  The two config-5 legs run the same rounds (C5_STEPS, C5_WARMUP).
+_C5 = ["--steps", str(C5_STEPS), "--warmup", str(C5_WARMUP)]
 VARIANTS = {
-    "blimp-room": ["--workload", "blimp-room", "--steps", "20", "--warmup", "3"],
-    "snake": ["--workload", "snake", "--steps", "10", "--warmup", "3"],
-    "seeds=32": ["--seeds", "32", "--steps", "20", "--warmup", "5"],
-    "seeds=256": ["--seeds", "256", "--steps", "10", "--warmup", "5"],
+    "blimp-room": ("bench.py", ["--workload", "blimp-room", "--steps", "20", "--warmup", "3"]),
+    "snake": ("bench.py", ["--workload", "snake", "--steps", "10", "--warmup", "3"]),
+    "seeds=32": ("bench.py", ["--seeds", "32"] + _C5),
+    "seeds=256": ("bench.py", ["--seeds", "256"] + _C5),
+    "prm": ("scripts/bench_prm.py", ["--reps", "3"]),
+    "distance": ("scripts/bench_distance.py", ["--steps", "10", "--warmup", "3"]),
 }
 
 
 def run_variants():
-    """Each leg's bench line (no CPU baseline, no nested legs), condensed: value, ms_per_step,
-    the dominant stage's roofline, every stage's time and fractions, and (config 5) the seeds
-    digest; a leg that fails reports its error instead."""
+    """Each leg's line (no CPU baseline, no nested legs), condensed: value, ms_per_step, the
+    dominant stage's roofline, every stage's time and fractions, and (config 5) the seeds
+    digest and from-scratch time; a leg that fails reports its error instead."""
     out = {}
-    for name, extra in VARIANTS.items():
-        cmd = [sys.executable, os.path.abspath(__file__), "--no-cpu", "--no-variants"] + extra
+    for name, (script, extra) in VARIANTS.items():
+        cmd = [sys.executable, os.path.join(REPO, script), "--no-cpu"] + extra
+        if script == "bench.py":
+            cmd.append("--no-variants")
         t0 = time.perf_counter()
         try:
             p = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=dict(os.environ))
@@ -667,20 +704,47 @@ def run_variants():
         except subprocess.TimeoutExpired:
             out[name] = {"error": "timeout"}
             continue
-        roof = d.get("roofline") or {}
-        leg = {k: d.get(k) for k in ("value", "unit", "ms_per_step", "steps", "warmup", "valid_fraction", "scaling",
-                                     "seeds_digest", "per_seed_valid_per_s", "host_enqueue_ms_per_step")
-               if d.get(k) is not None}
-        leg["config"] = d.get("config")
-        leg["roofline"] = {k: roof.get(k) for k in ("bound", "achieved", "peak", "unit", "frac", "traffic", "kernel",
-                                                    "stage", "ms_per_launch", "pmc_source", "stage_time_scale")
-                           if k in roof}
-        leg["stages"] = {s: {k: v for k, v in st.items()
-                             if k in ("ms", "ms_event_free", "frac_hbm_compulsory", "frac_hbm_measured",
-                                      "traffic_over_compulsory", "frac_fp64", "kernel")}
-                         for s, st in (roof.get("stages") or {}).items()}
-        leg["leg_wall_s"] = round(time.perf_counter() - t0, 1)
-        out[name] = leg
+        out[name] = condense(d)
+        out[name]["leg_wall_s"] = round(time.perf_counter() - t0, 1)
+    return out
+
+
+def condense(d):
+    roof = d.get("roofline") or {}
+    leg = {k: d.get(k) for k in ("metric", "value", "unit", "ms_per_step", "steps", "warmup", "valid_fraction",
+                                 "scaling", "seeds_digest", "per_seed_valid_per_s", "host_enqueue_ms_per_step",
+                                 "n_gpus", "world_size", "from_scratch", "edges_checked_per_s", "wall_ms",
+                                 "device_ms", "work_per_step", "parity_sample_bitexact")
+           if d.get(k) is not None}
+    leg["config"] = d.get("config")
+    leg["roofline"] = {k: roof.get(k) for k in ("bound", "achieved", "peak", "unit", "frac", "traffic", "kernel",
+                                                "stage", "ms_per_launch", "pmc_source", "stage_time_scale",
+                                                "frac_hbm_measured", "traffic_over_compulsory", "work")
+                       if k in roof}
+    leg["stages"] = {s: {k: v for k, v in st.items()
+                         if k in ("ms", "ms_event_free", "frac_hbm_compulsory", "frac_hbm_measured",
+                                  "traffic_over_compulsory", "frac_fp64", "kernel", "nn_points_per_query",
+                                  "nn_boxes_per_query")}
+                     for s, st in (roof.get("stages") or {}).items()}
+    return leg
+
+
+def config5_summary(c5_256, c5_32=None):
+    """The north-star scaling config in every line: the 256-seed run at this N (a leg of its
+    own at N = 1, the in-world leg at N > 1), and at N = 1 the 32-seed leg one GPU of eight
+    would run, at the same rounds: per-GPU ratio = v32 / v256, projected 8-GPU speed-up =
+    8 x v32 / v256 (the driver's own N = 8 run measures it when it gets a node)."""
+    if not c5_256 or "value" not in c5_256:
+        return {"error": "config-5 leg missing", "leg": c5_256}
+    out = {"seeds": 256, "value": c5_256["value"], "unit": c5_256.get("unit"), "ms_per_step": c5_256["ms_per_step"],
+           "steps": c5_256["steps"], "warmup": c5_256["warmup"], "n_gpus": c5_256.get("n_gpus"),
+           "world_size": c5_256.get("world_size"), "scaling": "strong", "seeds_digest": c5_256.get("seeds_digest"),
+           "from_scratch": c5_256.get("from_scratch")}
+    if c5_32 and "value" in c5_32:
+        same = (c5_32["steps"], c5_32["warmup"]) == (c5_256["steps"], c5_256["warmup"])
+        r = c5_32["value"] / c5_256["value"]
+        out.update({"seeds32_value": c5_32["value"], "same_rounds": same, "per_gpu_ratio": round(r, 4),
+                    "projected_8gpu_speedup": round(8 * r, 3)})
     return out
 
 
@@ -715,15 +779,33 @@ def main():
 
     mpt.init(local)
     torch.cuda.set_device(local)
-    stream = torch.cuda.current_stream()
     if args.seeds > 0:
         out = run_seeds(args, world, rank, dist, torch, mpt, multiseed, scenes)
-        if out is not None:
-            print(json.dumps(out))
-        if dist:
-            dist.destroy_process_group()
-        return
+    else:
+        out = run_tree(args, world, rank, dist, torch, mpt, multiseed, scenes)
+        if world > 1:
+            # BASELINE config 5 in the same torchrun world: args.c5_seeds seeds sharded
+            # contiguously over the ranks (32 per GPU at 8 GPUs), strong scaling; its seeds
+            # digest equals the N = 1 run's (the seeds=256 leg) for the same rounds
+            a5 = argparse.Namespace(**vars(args))
+            a5.seeds, a5.steps, a5.warmup = args.c5_seeds, args.c5_steps, args.c5_warmup
+            c5 = run_seeds(a5, world, rank, dist, torch, mpt, multiseed, scenes)
+            if out is not None:
+                out["config5"] = config5_summary(condense(c5) if c5 else None)
+        elif out is not None and not args.no_variants and args.workload == "blimp":
+            out["variants"] = run_variants()
+            out["config5"] = config5_summary(out["variants"].get("seeds=256"), out["variants"].get("seeds=32"))
+    if out is not None:
+        print(json.dumps(out))
+    if dist:
+        dist.destroy_process_group()
 
+
+def run_tree(args, world, rank, dist, torch, mpt, multiseed, scenes):
+    """BASELINE config 2 (or --workload's variant): one tree of args.tree nodes per rank, reset
+    to its base inside every timed round; returns the line on rank 0 (None elsewhere)."""
+    stream = torch.cuda.current_stream()
+    red_dev = args.red_dev
     if args.workload == "snake":
         sc = scenes.snake_scenario("corridor")
         workload = (f"snake.inst: snake_trailers ({sc.links} unit-box links, T=10) in the synthetic corridor "
@@ -777,9 +859,8 @@ def main():
     elapsed, (valid, checked) = multiseed.reduce_run(dist, elapsed, [valid, checked], red_dev)
 
     if rank != 0:
-        if dist:
-            dist.destroy_process_group()
-        return
+        eng.close()
+        return None
 
     steps = args.steps
     # hipEvents on the launch stream, recorded every n-th timed round into the engine's event
@@ -793,13 +874,10 @@ def main():
     nn_mode = eng.last_nn()
     d = sc.dim
     kernels = dict(STAGE_KERNEL, nn_query=NN_KERNEL.get(nn_mode, "k_grid_nn1_runs"))
-    if nn_mode == "grid":  # the instantiation (its PMC row)
-        if os.environ.get("MPT_NN_SORT", "1") != "0":
-            kernels["nn_query"] = f"k_grid_nn1_runs_sorted<{d},"  # queries bucketed by k_sample
-        else:
-            kernels["nn_query"] = f"k_grid_nn1_runs_xcd<{d}," if d >= 15 else f"k_grid_nn1_runs<{d},"
+    if nn_mode == "grid":  # the instantiation (its PMC row): queries bucketed by the grid count launch
+        kernels["nn_query"] = f"k_grid_nn1_runs_sorted<{d},"
     if nn_mode == "tree":
-        kernels["nn_build"] = "k_pt_gather"
+        kernels["nn_build"] = "k_pt_inc_merge"
     summ, summ_path = pmc_summary(args.traffic, args.workload)
     stages = stage_table(per_launch, cst, K, n0, d, eng.info()["pmax"], geometry(sc, env), nn_mode, kernels, summ)
     dominant = max(stages, key=lambda s: stages[s]["ms"]) if stages else None
@@ -822,6 +900,7 @@ def main():
         "config": {"workload": workload,
                    "tree_nodes": n0, "extensions_per_round": K, "seed_base": args.seed, "nn_index": args.nn,
                    "parallelism": f"independent seeds x{world}"},
+        "world_size": dist.get_world_size() if dist else 1,
         "checked_per_s": checked / elapsed,
         "valid_fraction": valid / max(checked, 1),
         "kernel_ms_per_round": {k: round(v, 4) for k, v in per_launch.items()},
@@ -832,12 +911,8 @@ def main():
         out["cpu_baseline"] = cpu_baseline(sc, tree, K, seed, args.cpu_seconds)
     else:
         out["cpu_baseline"] = None
-    if world == 1 and not args.no_variants and args.workload == "blimp":
-        del eng  # its device memory, before the legs' processes allocate theirs
-        out["variants"] = run_variants()
-    print(json.dumps(out))
-    if dist:
-        dist.destroy_process_group()
+    eng.close()  # its device memory, before the next leg allocates
+    return out
 
 
 if __name__ == "__main__":

@@ -204,7 +204,9 @@ mpt_status mpt_rrt_step(mpt_rrt *rrt, int32_t K, void *stream);
  * launch per stage (sample, incremental index build, NN, steer, collide, append) for all
  * engines, after the engines' streams and before their next work; an engine's last-round
  * buffers (mpt_rrt_last_round / _last_poses) are then the joint state's, valid until the next
- * call on that joint stream.  Otherwise the engines whose round uses the Morton tree share
+ * call on that joint stream (those two calls fail with MPT_ERR_INVALID once mpt_rrt_joint_release
+ * or a larger joint round has freed the buffers; stage times of a joint round come from
+ * mpt_rrt_joint_stage_times, and mpt_rrt_kernel_times fails after one).  Otherwise the engines whose round uses the Morton tree share
  * one index build and one query launch on joint_stream, and the rest of each round runs on
  * the engine's own stream.  The job tables and buffers of the joint launches belong to
  * joint_stream: calls with different joint streams (from one or several host threads) may

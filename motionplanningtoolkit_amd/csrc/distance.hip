@@ -29,17 +29,19 @@
 namespace mpt {
 
 constexpr int kDistWaves = 4;
-// a bucket's queued pairs are evaluated at its end once at least this many wait
-// (MPT_DIST_FLUSH: A/B; 1 = after every bucket: 4 % slower on the blimp in the room)
-__constant__ int32_t c_dist_flush = 32;
-// the first pass's bound scale (MPT_DIST_ALPHA; 1 = one pass).  Blimp vs room, 65 536 poses,
-// alpha 1 / 0.7 / 0.5 / 0.3: 8.04 / 7.68 / 7.65 / 7.89 ms (triDistance calls 65.2 / 37.0 / 35.7
-// / 37.3 M); the reference's last submesh 3.81 / 2.43 / 2.38 / 2.55 ms
-__constant__ double c_dist_alpha = 0.5;
-// clusters the first pass walks at most (MPT_DIST_PASSA): the nearest one sets the bound nearly
-// as well as all of them, without their second walk (blimp: 1 / 2 / 4 / all: 6.45 / 6.54 / 6.65
-// / 7.65 ms, calls 36.4 / 36.4 / 36.3 / 35.7 M)
-__constant__ int32_t c_dist_passa = 1;
+// Tuning constants (measured in round 3 with the run-time knobs since removed):
+// a bucket's queued pairs are evaluated at its end once at least this many wait (1 = after
+// every bucket: 4 % slower on the blimp in the room)
+constexpr int32_t c_dist_flush = 32;
+// the first pass's bound scale (1 = one pass).  Blimp vs room, 65 536 poses, alpha 1 / 0.7 /
+// 0.5 / 0.3: 8.04 / 7.68 / 7.65 / 7.89 ms (triDistance calls 65.2 / 37.0 / 35.7 / 37.3 M); the
+// reference's last submesh 3.81 / 2.43 / 2.38 / 2.55 ms.  Any value in (0, 1] is exact: see
+// flush_pairs for the one invariant the second pass relies on.
+constexpr double c_dist_alpha = 0.5;
+// clusters the first pass walks at most: the nearest one sets the bound nearly as well as all
+// of them, without their second walk (blimp: 1 / 2 / 4 / all: 6.45 / 6.54 / 6.65 / 7.65 ms,
+// calls 36.4 / 36.4 / 36.3 / 35.7 M)
+constexpr int32_t c_dist_passa = 1;
 constexpr int kDistStack = kMaxLevels * kWave;
 
 __device__ __forceinline__ double read_best(const unsigned long long *p) {
@@ -90,7 +92,10 @@ __device__ __forceinline__ double flush_pairs(const EnvDev &env, DistLds &s, int
                                               unsigned long long *bp, DistCounters &cnt) {
     double d = DBL_MAX;
     // a pair queued against an older bound is re-tested against the current one (its gap
-    // rounded down: never drops a pair the exact test keeps)
+    // rounded down: never drops a pair the exact test keeps).  This threshold must stay the
+    // full bound U, never alpha * U: the second pass (distance_unit) skips the first pass's
+    // pairs with a gap <= alpha * U_A on the grounds that the first pass evaluated every one of
+    // them, and a pair dropped here against alpha * U would then be lost.
     const double Un = uniform_d(dmin(U, read_best(bp)));
     const double thr = Un * (1.0 + 1e-9) + 1e-9;
     const bool ev = lane < n && (double)s.qgap[lane] <= thr * thr;
@@ -400,7 +405,7 @@ __device__ void distance_unit(const EnvDev &env, const AgentDev *__restrict__ li
     }
 }
 
-// kOcc workgroups per CU (MPT_DIST_OCC, scripts/measure_distance.sh).  3 (default): the
+// kOcc workgroups per CU.  3 (the one instantiated): the
 // unrolled triDistance under 168 VGPRs, 3 waves per SIMD (5 dwords spilled): blimp in the room
 // 10.4 -> 7.8 ms against 2 (the unconstrained allocation, 178 VGPRs since triDistance no longer
 // holds S and T beside their rotating copies).  4: the rolled triDistance under 128 VGPRs
@@ -438,31 +443,9 @@ void launch_distance(const EnvDev &env, const AgentDev *d_links, const DistWork 
     if (w.n_units <= 0 || env.n_tris <= 0) return;
     const int64_t blocks = (w.n_units + kDistWaves - 1) / kDistWaves;
     if (blocks > 0x7fffffff) throw Error{MPT_ERR_INVALID, "distance batch too large"};
-    static const int occ = getenv("MPT_DIST_OCC") ? atoi(getenv("MPT_DIST_OCC")) : 3;
-    static const bool flush_set = [] {
-        const int32_t f = getenv("MPT_DIST_FLUSH") ? atoi(getenv("MPT_DIST_FLUSH")) : 32;
-        hip_check(hipMemcpyToSymbol(HIP_SYMBOL(c_dist_flush), &f, sizeof f), "flush threshold");
-        double al = getenv("MPT_DIST_ALPHA") ? atof(getenv("MPT_DIST_ALPHA")) : 0.5;
-        if (!(al > 0.0 && al <= 1.0)) al = 0.5;
-        hip_check(hipMemcpyToSymbol(HIP_SYMBOL(c_dist_alpha), &al, sizeof al), "first-pass scale");
-        const int32_t pa = getenv("MPT_DIST_PASSA") ? std::max(1, atoi(getenv("MPT_DIST_PASSA"))) : 1;
-        hip_check(hipMemcpyToSymbol(HIP_SYMBOL(c_dist_passa), &pa, sizeof pa), "first-pass clusters");
-        return true;
-    }();
-    (void)flush_set;
-    // the branch-free segPoints (seg_points_sel: the same values; blimp vs room 12.4 -> 10.1 ms);
-    // MPT_DIST_SEL=0: the branchy form (A/B)
-    static const bool sel = !(getenv("MPT_DIST_SEL") && atoi(getenv("MPT_DIST_SEL")) == 0);
-#define MPT_DIST_LAUNCH(OCC, SEL) \
-    hipLaunchKernelGGL((k_distance<OCC, SEL>), dim3((unsigned)blocks), dim3(kDistWaves * 64), 0, stream, env, d_links, w)
-    if (occ == 2) {
-        if (sel) MPT_DIST_LAUNCH(2, true); else MPT_DIST_LAUNCH(2, false);
-    } else if (occ == 3) {
-        if (sel) MPT_DIST_LAUNCH(3, true); else MPT_DIST_LAUNCH(3, false);
-    } else {
-        if (sel) MPT_DIST_LAUNCH(4, true); else MPT_DIST_LAUNCH(4, false);
-    }
-#undef MPT_DIST_LAUNCH
+    // 3 workgroups per CU and the branch-free segPoints (seg_points_sel: the same values as the
+    // branchy form; blimp vs room 12.4 -> 10.1 ms)
+    hipLaunchKernelGGL((k_distance<3, true>), dim3((unsigned)blocks), dim3(kDistWaves * 64), 0, stream, env, d_links, w);
     hip_check(hipGetLastError(), "k_distance launch");
 }
 

@@ -1341,10 +1341,11 @@ __device__ __forceinline__ void tree_nn1_block(const PointTreeDev &T, const doub
 // stack holds at most ~14 entries a level (two sibling blocks of 7) + 2: 2 * 8 * 10 entries.
 constexpr int64_t kPtNnWideMaxQueries = 262144;  // d = 15: the four-node walk up to this many queries a launch
 
-// nodes a walk step by default: d <= 7 eight (one query a wave) at every launch size; d = 15 (its
-// registers) four up to kPtNnWideMaxQueries queries, else one
+// nodes a walk step by default: d = 7 (config 5, where it was measured) eight (one query a
+// wave) at every launch size; d = 3 and d = 15 (its registers) four up to kPtNnWideMaxQueries
+// queries, else one (the round-3 rule the eight-node walk replaced for d = 7 only)
 inline int pt_nn_width(int32_t d, int64_t queries) {
-    if (d <= 7) return 8;
+    if (d == 7) return 8;
     return queries <= kPtNnWideMaxQueries ? 4 : 1;
 }
 

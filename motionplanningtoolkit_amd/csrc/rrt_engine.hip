@@ -15,6 +15,7 @@
 // K = 1 reference replay with the reference's own RNG streams is the host planner's job
 // (host/rrt.hpp over the same kernels).
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cstdio>
 #include <cstring>
@@ -45,6 +46,10 @@ constexpr int kMaxDim = 16;
 constexpr double kGridHminK = 0.3;
 // MPT_NN_AUTO re-reads the nodes' spread at most every kSpreadEvery rounds
 constexpr int kSpreadEvery = 8;
+// MPT_NN_AUTO: the tree index when the nodes' spatial box covers less than this fraction of
+// the sampling box (most samples then lie far from every node, where the grid walks empty
+// rings and the tree does not)
+constexpr double kAutoTreeFrac = 0.25;
 
 struct EngineParams {
     int32_t kind, d, L, pmax;
@@ -669,6 +674,10 @@ struct mpt_rrt {
         const int32_t *nn = nullptr, *pcount = nullptr;
         const uint8_t *verdict = nullptr;
     } jv;
+    // the joint stream and the id of its round buffers the slices point into (a release or a
+    // reallocation of those buffers changes the id: last_round / last_poses then refuse)
+    hipStream_t jv_stream = nullptr;
+    uint64_t jv_id = 0;
 };
 
 namespace {
@@ -836,8 +845,30 @@ extern "C" mpt_status mpt_rrt_add_nodes(mpt_rrt *r, const double *states, const 
         hip_check(hipGetLastError(), "k_set_n");
         hip_check(hipDeviceSynchronize(), "sync");
         r->n_upper = nn;
-        r->spread_seen = false;  // bulk nodes: re-read the spread at the next index build
         r->pt_inc_ok = false;
+        if (cur == 0 && n > 0) {
+            // the first nodes: MPT_NN_AUTO's spread from the host copy, so the first indexed
+            // round already uses the right structure (a tree grown from one root would
+            // otherwise run one grid round over a clustered tree with samples over the whole
+            // box before the device spread came back)
+            double frac = 1.0;
+            for (int j = 0; j < r->grid_gd; ++j) {
+                const int dj = r->grid_dims[j];
+                double lo = states[dj], hi = states[dj];
+                for (int64_t i = 1; i < n; ++i) {
+                    lo = std::min(lo, states[i * d + dj]);
+                    hi = std::max(hi, states[i * d + dj]);
+                }
+                const double range = r->p.hi[dj] - r->p.lo[dj];
+                frac *= range > 0 ? std::min(1.0, std::max(0.0, (hi - lo) / range)) : 1.0;
+            }
+            r->auto_tree = frac < kAutoTreeFrac;
+            r->spread_seen = true;
+            r->spread_pending = false;
+            r->rounds_since_spread = 0;
+        } else {
+            r->spread_seen = false;  // bulk nodes: re-read the spread at the next index build
+        }
     });
 }
 
@@ -903,7 +934,7 @@ void refresh_auto(mpt_rrt *r) {
             const double range = p.hi[dj] - p.lo[dj];
             frac *= range > 0 ? std::min(1.0, std::max(0.0, ext / range)) : 1.0;
         }
-        r->auto_tree = frac < 0.25;
+        r->auto_tree = frac < kAutoTreeFrac;
         r->spread_pending = false;
         r->spread_seen = true;
     }
@@ -1200,6 +1231,7 @@ struct JointNN {
     int32_t *j_nn = nullptr, *j_pcount = nullptr, *j_live = nullptr;
     uint8_t *j_verdict = nullptr;
     uint32_t *j_nlive = nullptr;
+    uint64_t buf_id = 0;  // id of the round buffers above (0: none); engines' jv slices carry it
     CollideScratch cs;
     // timed joint round: start, sample, build, NN, steer, collide, append
     hipEvent_t st[7] = {};
@@ -1207,6 +1239,7 @@ struct JointNN {
 };
 std::mutex g_joints_mu;
 std::map<hipStream_t, std::unique_ptr<JointNN>> g_joints;
+std::atomic<uint64_t> g_joint_buf_ids{0};
 thread_local JointNN *g_last_timed = nullptr;  // mpt_rrt_joint_nn_ms: this thread's last timed call
 
 JointNN &joint_state(hipStream_t s) {
@@ -1255,6 +1288,7 @@ void joint_free_round(JointNN &g) {
     g.j_verdict = nullptr;
     g.j_nlive = nullptr;
     g.r_edges = g.r_units = 0;
+    g.buf_id = 0;
 }
 
 // Engines whose rounds can run as one joint round (see EngineJob): every round on the Morton
@@ -1334,6 +1368,7 @@ void joint_round(mpt_rrt *const *rs, int32_t n, int32_t K, void *const *streams_
         g.r_units = edges * units;
         g.r_dim = d;
         g.r_subs = std::max(n_sub, 64);
+        g.buf_id = ++g_joint_buf_ids;
     }
     g.cs.ensure((int64_t)std::min(per_sub, n) * K * units, a->max_clusters);
     // the engines' host bookkeeping and their job table
@@ -1465,6 +1500,8 @@ void joint_round(mpt_rrt *const *rs, int32_t n, int32_t K, void *const *streams_
         r->last_K = K;
         r->last_nn = MPT_NN_TREE;
         r->last_joint = true;
+        r->jv_stream = joint;
+        r->jv_id = g.buf_id;
         const int64_t e0 = (int64_t)i * K;
         r->jv.samples = g.j_samples + e0 * d;
         r->jv.ends = g.j_ends + e0 * d;
@@ -1597,6 +1634,16 @@ extern "C" mpt_status mpt_rrt_step_many(mpt_rrt *const *rs, int32_t n, int32_t K
     });
 }
 
+namespace {
+// an engine's last joint round slices are still the joint state's live buffers
+void joint_slices_check(const mpt_rrt *r) {
+    JointNN *g = joint_find(r->jv_stream);
+    if (!g || g->buf_id == 0 || g->buf_id != r->jv_id)
+        throw Error{MPT_ERR_INVALID, "the joint round's buffers were released or reallocated since this engine's "
+                                     "last round"};
+}
+}  // namespace
+
 extern "C" mpt_status mpt_rrt_joint_nn_ms(float *ms) {
     return guarded([&] {
         if (!ms) throw Error{MPT_ERR_INVALID, "null pointer"};
@@ -1691,6 +1738,7 @@ extern "C" mpt_status mpt_rrt_last_round(mpt_rrt *r, double *samples, int32_t *n
         if (K == 0) return;
         // a joint round's buffers are the joint state's slices (valid until its next step_many)
         const bool j = r->last_joint;
+        if (j) joint_slices_check(r);
         const double *s = j ? r->jv.samples : r->d_samples, *e = j ? r->jv.ends : r->d_ends;
         const int32_t *nn = j ? r->jv.nn : r->d_nn;
         const uint8_t *v = j ? r->jv.verdict : r->d_verdict;
@@ -1708,6 +1756,7 @@ extern "C" mpt_status mpt_rrt_last_poses(mpt_rrt *r, double *poses, int32_t *pos
         const int64_t K = r->last_K;
         if (K == 0) return;
         const bool j = r->last_joint;
+        if (j) joint_slices_check(r);
         if (poses)
             hip_check(hipMemcpy(poses, j ? r->jv.poses : r->d_poses, sizeof(double) * 12 * K * r->p.pmax * r->p.L,
                                 hipMemcpyDeviceToHost),
@@ -1777,6 +1826,9 @@ extern "C" mpt_status mpt_rrt_kernel_times(mpt_rrt *r, float ms[9]) {
     return guarded([&] {
         if (!r || !ms) throw Error{MPT_ERR_INVALID, "null pointer"};
         if (!r->timing || r->ring_next == 0) throw Error{MPT_ERR_INVALID, "timing not enabled or no round yet"};
+        if (r->last_joint)
+            throw Error{MPT_ERR_INVALID, "the last round ran in a joint round (mpt_rrt_step_many), which times its "
+                                         "stages on the joint stream: use mpt_rrt_joint_stage_times"};
         hipEvent_t *e = r->ring.data() + ((r->ring_next - 1) % kTimingRing) * 10;
         hip_check(hipEventSynchronize(e[9]), "event sync");
         // [sample, nn_build, nn_query, steer, collide_pairs, collide_cands, collide_narrow,

@@ -36,6 +36,35 @@ def blimp_poses(rng, n):
     return P
 
 
+HBM_PEAK_GBS = 8000.0
+
+
+def distance_roofline(out, a, n_agent, n_env, ms):
+    """k_distance: FP64 (TRI_DISTANCE_FLOPS per triDistance call) against the FP64 VALU roof;
+    compulsory HBM bytes = the poses (96 B), the edge offsets, the results, the agent
+    triangles (72 B) and the env records (384 B a triangle + 32 B a tree item) once; measured
+    traffic from the newest committed PMC summary (profiles/r*/distance/)."""
+    import glob
+
+    t = ms * 1e-3
+    comp = a.n * (96 + 8 + 8) + n_agent * 72 + n_env * (384 + 32)
+    roof = {"bound": "mfma", "kernel": "k_distance", "achieved": round(out["fp64"]["achieved_tflops"], 3),
+            "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": round(out["fp64"]["frac"], 4),
+            "note": "FP64 VALU roof (FCL's scalar operation order; no MFMA)", "ms_per_launch": round(ms, 4),
+            "compulsory_bytes": int(comp), "frac_hbm_compulsory": round(comp / t / 1e9 / HBM_PEAK_GBS, 4),
+            "traffic": None, "work": out["work_per_step"]}
+    c = sorted(glob.glob(os.path.join(REPO, "profiles", "r[0-9][0-9]", "distance", "pmc_summary.json")))
+    if c:
+        try:
+            summ = json.load(open(c[-1]))
+            tr = next(v["hbm_bytes_per_launch"] for k, v in summ.items() if "k_distance" in k)
+            roof.update({"traffic": int(tr), "frac_hbm_measured": round(tr / t / 1e9 / HBM_PEAK_GBS, 4),
+                         "traffic_over_compulsory": round(tr / comp, 2), "pmc_source": os.path.relpath(c[-1], REPO)})
+        except (OSError, ValueError, StopIteration):
+            pass
+    return roof
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--n", type=int, default=65536)
@@ -99,6 +128,7 @@ def main():
         "contact_fraction": float((d == 0).mean()),
     }
     out["fp64"]["frac"] = out["fp64"]["achieved_tflops"] / FP64_PEAK_TFLOPS
+    out["roofline"] = distance_roofline(out, a, len(agent_t), len(env_t), ms)
     if not a.no_cpu:
         sys.path.insert(0, os.path.join(REPO, "oracle"))
         import oracle as orc

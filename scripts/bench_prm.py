@@ -29,6 +29,14 @@ FP64_PEAK_TFLOPS = 78.6
 HBM_PEAK_GBS = 8000.0
 
 
+def latest_pmc(sub):
+    """The newest committed rocprofv3 PMC summary of this workload (profiles/r*/<sub>/)."""
+    import glob
+
+    c = sorted(glob.glob(os.path.join(REPO, "profiles", "r[0-9][0-9]", sub, "pmc_summary.json")))
+    return c[-1] if c else ""
+
+
 def sweep_roofline(w, ms, n_agent, n_env, traffic_path):
     """k_sweep (the config-4 collision stage, one wave per (edge, agent cluster)): FP64 by
     SURVEY §8(d)'s model -- 750 flops per exact triangle test, 27 per (pair, pose) gate (the
@@ -48,7 +56,7 @@ def sweep_roofline(w, ms, n_agent, n_env, traffic_path):
            "compulsory_bytes": int(comp), "compulsory_gbs": round(comp / t / 1e9, 1),
            "frac_hbm_compulsory": round(comp / t / 1e9 / HBM_PEAK_GBS, 4), "ms_per_launch": round(ms, 4),
            "work": w, "traffic": None}
-    path = traffic_path or os.path.join(REPO, "profiles", "r15", "prm", "pmc_summary.json")
+    path = traffic_path or latest_pmc("prm")
     try:
         summ = json.load(open(path))
         tr = next(v["hbm_bytes_per_launch"] for k, v in summ.items() if "k_sweep" in k)
@@ -71,7 +79,8 @@ def main():
     ap.add_argument("--rooms", type=int, default=25)
     ap.add_argument("--cpu-n", type=int, default=3000)
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--traffic", default=None, help="pmc_summary.json with k_sweep's traffic (default profiles/r15/prm)")
+    ap.add_argument("--traffic", default=None,
+                    help="pmc_summary.json with k_sweep's traffic (default: the newest profiles/r*/prm/)")
     ap.add_argument("--collide", default="split", choices=["split", "fused"])
     ap.add_argument("--bounds", default="blimp", choices=["blimp", "rooms"],
                     help="milestone x, y, z: blimp.inst's [-100, 100]^3 (one corner of the rooms) or the whole "

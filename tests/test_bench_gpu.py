@@ -1,7 +1,11 @@
 """The bench's multi-rank path on the GPU: config 5 sharded over two ranks (torchrun, gloo for
 the collectives, both ranks on the box's one GPU -- the driver's 8-GPU runs use RCCL, one rank
 per GPU) must grow exactly the trees one rank grows for the same seeds: the seeds digest of the
-two-rank run equals the one-rank run's.  Each run is a subprocess with its own time limit."""
+two-rank run equals the one-rank run's.  Each run is a subprocess with its own time limit.
+
+Two paths: `bench.py --seeds N` under torchrun, and the driver's own N > 1 command (no --seeds:
+config 2 per rank plus the mandatory config-5 leg in the same world, whose `config5` object
+must carry the world size and the one-rank digest)."""
 import json
 import os
 import socket
@@ -42,3 +46,24 @@ def test_two_ranks_shard_config5_like_one():
     assert two["n_gpus"] == 2 and one["n_gpus"] == 1
     assert two["seeds_digest"] == one["seeds_digest"]
     assert two["valid_fraction"] == one["valid_fraction"]
+
+
+@pytest.mark.timeout(600)
+def test_driver_multi_rank_line_carries_config5():
+    """`bench.py --gpus 2` as the driver launches it: the printed line is config 2 (weak, one
+    tree per rank) with the config-5 leg run in the same torchrun world (seeds sharded
+    contiguously over the ranks); its digest equals one rank's `--seeds` run at the same
+    rounds.  Sizes reduced (--tree, --batch, --c5-*) so the test stays short; the code path is
+    the driver's."""
+    env = dict(os.environ, MPT_DIST_BACKEND="gloo", MPT_BENCH_DEVICE="0")
+    c5 = ["--c5-seeds", "12", "--c5-steps", "2", "--c5-warmup", "3"]
+    two = _run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                "--master-addr", "127.0.0.1", "--master-port", str(_port()), "bench.py", "--gpus", "2", "--steps", "3",
+                "--warmup", "1", "--tree", "20000", "--batch", "4096", "--no-cpu"] + c5, env)
+    one = _run([sys.executable, "bench.py", "--seeds", "12", "--steps", "2", "--warmup", "3", "--no-cpu"], env)
+    assert two["n_gpus"] == 2 and two["world_size"] == 2 and two["scaling"] == "weak"
+    c = two["config5"]
+    assert c["world_size"] == 2 and c["n_gpus"] == 2 and c["scaling"] == "strong"
+    assert (c["steps"], c["warmup"]) == (2, 3)
+    assert c["seeds_digest"] == one["seeds_digest"]
+    assert c["from_scratch"]["rounds"] == 5 and c["from_scratch"]["wall_s"] > 0

@@ -489,10 +489,18 @@ def test_joint_round_matches_single_steps(mpt_gpu):
         for e in engs:
             assert e.last_nn() == "tree"
             out.append((e.read_tree(e.counters()["nodes"]), e.last_round(K), e.last_poses(K)))
+        if joint:
+            # a joint round's stage times live on the joint stream, not in the engine's ring
+            with pytest.raises(mpt_gpu.MptError):
+                engs[0].kernel_times()
+            mpt_gpu.joint_release(js)
+            # the slices an engine's last round points into are gone with the joint state
+            with pytest.raises(mpt_gpu.MptError):
+                engs[1].last_round(K)
+            with pytest.raises(mpt_gpu.MptError):
+                engs[1].last_poses(K)
         for e in engs:
             e.close()
-        if joint:
-            mpt_gpu.joint_release(js)
         return out, times
 
     alone, _ = grow(False)

@@ -2,8 +2,9 @@
 
 * Config 2: one engine round of the benchmark's exact shape -- 100 000-node blimp tree,
   K = 65 536 extensions, blimp (1355 tris) vs the room (model.dae) -- NN ids of every query
-  against the oracle's exact kd-tree, collision verdicts of 4096 sampled extensions against
-  the oracle's AABB-tree collider (on the device's own poses), and the ordered append.
+  against the oracle's exact kd-tree, collision verdicts of every extension against the
+  oracle's AABB-tree collider (on the device's own poses), and the ordered append.
+* Config 3: the same at the snake leg's shape (100 000-node 15-dim tree, 11 links, corridor).
 * Config 2, collision-heavy variant (`bench.py --workload blimp-room`): tree and samples
   inside the room, so every unit reaches the narrow phase.
 * Config 4: the 25 x 25-room environment (197 500 triangles, a four-level env tree that does
@@ -28,13 +29,15 @@ THREADS = min(16, len(os.sched_getaffinity(0)))
 I12 = np.r_[np.eye(3).ravel(), 0.0, 0.0, 0.0]
 
 
-def _engine_round_check(mpt, oracle, sc, tree, K, seed, n_sample=4096):
+def _engine_round_check(mpt, oracle, sc, tree, K, seed, n_sample=4096, nn_mode=None):
     env = mpt.Environment(sc.env_tris, sc.env_tf)
     ag = mpt.AgentMesh(sc.agent_tris)
     n0 = len(tree)
     eng = mpt.RRTEngine(env, ag, sc.kind, sc.prm, sc.ranges, sc.steer_dt, sc.cc_dt, n0 + K, seed)
     eng.add_nodes(tree)
     eng.step(K)
+    if nn_mode:
+        assert eng.last_nn() == nn_mode
     samples, nn, ends, verdict = eng.last_round(K)
     poses, pcount = eng.last_poses(K)
     # samples: the counter-based generator (spot check, pure +,-,* arithmetic)
@@ -47,9 +50,10 @@ def _engine_round_check(mpt, oracle, sc, tree, K, seed, n_sample=4096):
     # verdicts of a sample of extensions, on the device's own poses
     rng = np.random.default_rng(seed)
     idx = np.sort(rng.choice(K, size=min(n_sample, K), replace=False))
-    flat = np.concatenate([poses[k, :pcount[k]] for k in idx]).reshape(-1, 1, 12)
+    L = sc.links
+    flat = np.concatenate([poses[k, :pcount[k]] for k in idx]).reshape(-1, L, 12)
     off = np.r_[0, np.cumsum(pcount[idx])]
-    ref_v = oracle.collide_batch_bvh(oracle.BVH(sc.env_tris), sc.env_tf, [sc.agent_tris], flat, off,
+    ref_v = oracle.collide_batch_bvh(oracle.BVH(sc.env_tris), sc.env_tf, [sc.agent_tris] * L, flat, off,
                                      nthreads=THREADS)
     assert np.array_equal(verdict[idx], ref_v)
     # ordered append of the collision-free extensions
@@ -66,7 +70,21 @@ def test_config2_full_round(mpt_gpu, oracle):
     sc = scenes.blimp_scenario("all")
     seed = 1000  # bench.py's rank-0 seed
     tree = np.random.default_rng(seed).uniform(sc.ranges[:, 0], sc.ranges[:, 1], size=(100_000, sc.dim))
-    v = _engine_round_check(mpt_gpu, oracle, sc, tree, 65_536, seed)
+    v = _engine_round_check(mpt_gpu, oracle, sc, tree, 65_536, seed, n_sample=65_536, nn_mode="grid")
+    assert 0 < v.sum() < len(v)
+
+
+def test_config3_full_round(mpt_gpu, oracle):
+    """Config 3 at the bench's snake shape (`bench.py --workload snake`): snake_trailers (11
+    unit-box links, d = 15) in the synthetic corridor, a 100 000-node tree over the snake's
+    state ranges, K = 65 536 -- the grid NN over x, y with the head screen
+    (k_grid_nn1_runs_sorted<15, ...>).  Every NN id against the oracle's exact kd-tree, the
+    verdicts of all 65 536 extensions on the device's poses (all 11 links) against the oracle's
+    AABB-tree collider, and the ordered append (snake_trailers.hpp:170-183, 246-268)."""
+    sc = scenes.snake_scenario("corridor")
+    seed = 1000
+    tree = np.random.default_rng(seed).uniform(sc.ranges[:, 0], sc.ranges[:, 1], size=(100_000, sc.dim))
+    v = _engine_round_check(mpt_gpu, oracle, sc, tree, 65_536, seed, n_sample=65_536, nn_mode="grid")
     assert 0 < v.sum() < len(v)
 
 
