@@ -230,7 +230,9 @@ mpt_status mpt_rrt_joint_times(void *joint_stream, float ms[2]);
  * joint_stream).  Synchronises on it. */
 mpt_status mpt_rrt_joint_stage_times(void *joint_stream, float ms[6]);
 /* counters [8]: rounds, extensions checked, extensions valid, nodes, capacity drops,
- * pose overflow, reserved, reserved.  Synchronises. */
+ * pose overflow, index errors (an incremental tree build handed more new points than it
+ * merges: an internal bound broken; mpt_rrt_counters then fails with MPT_ERR_INTERNAL), reserved.
+ * Synchronises. */
 mpt_status mpt_rrt_counters(mpt_rrt *rrt, uint64_t counters[8]);
 /* Copy out the first n nodes and parents (1-based parent ids, 0 for roots). Synchronises. */
 mpt_status mpt_rrt_read_tree(mpt_rrt *rrt, double *states, int32_t *parents, int64_t n);

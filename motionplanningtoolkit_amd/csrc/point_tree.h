@@ -9,6 +9,15 @@ constexpr int kPtFan = 8;        // children per node, points per leaf
 constexpr int kPtMaxLevels = 10; // 8^10 points
 constexpr int kPtMaxDim = 16;
 
+// Seed points of a query's search (the incremental index): the tree's extreme points in
+// kPtHull directions -- the minimum and the maximum of every state dim, the rest spread over the
+// spatial dims' directions.  An RRT grows from its start while samples are uniform over the
+// ranges, so most queries lie far outside the tree and their nearest node sits on its hull: the
+// nearest seed bounds the search from its first step, where a walk from the root finds a tight
+// bound only after descending.  Any seed is an upper bound on the nearest distance, so the
+// result stays exact whichever points the seeds are.
+constexpr int kPtHull = 64;
+
 struct PointTreeDev {
     int32_t d;
     int32_t n_levels;          // box levels 1..n_levels (level n_levels = the root)
@@ -18,41 +27,9 @@ struct PointTreeDev {
     const double *pts;         // [n][d], Morton order
     const int32_t *ids;        // 1-based original ids
     unsigned long long *stats; // optional [2]: points examined, boxes tested
+    const double *hull_pts;    // optional [kPtHull][d]: seed points (ids in hull_ids, 0 = none)
+    const int32_t *hull_ids;
 };
-
-// One tree of a joint build (mpt_rrt_step_many): the tree's own buffers, its points, and the
-// offset of its keys / values in the shared sort buffers.
-struct PtBuildJob {
-    PointTreeDev T;            // as PointTree::dev() after the build
-    const double *pts;         // [n_upper][d] input rows
-    int64_t off;               // into the shared key / value buffers
-    unsigned long long *bbox;  // the tree's box keys
-    unsigned int *ticket;      // [2]: box-level ticket, bbox ticket
-    struct CodePlan *plan;
-    double *spts;
-    int32_t *sids;
-    float *boxes;
-    SpreadOut sp;
-};
-
-// shared sort buffers of a joint build (owned by the caller; reserve_tree_build_jobs sizes
-// them for the joined trees' capacities so later rounds never allocate)
-struct JointTreeScratch {
-    uint32_t *keys = nullptr, *keys_sorted = nullptr;
-    int32_t *vals = nullptr, *vals_sorted = nullptr;
-    int64_t cap = 0;
-    void *temp = nullptr;
-    size_t temp_bytes = 0;
-};
-
-// Build n trees of dim d in one launch per stage + one segmented sort.  d_jobs / h_jobs: the
-// same table on the device and the host; d_offsets: [n + 1] segment starts (int32) on the
-// device, total = its last entry.  Stream-ordered.
-void launch_tree_build_jobs(const PtBuildJob *d_jobs, const PtBuildJob *h_jobs, int32_t n, int32_t d,
-                            const int32_t *d_offsets, int64_t total, JointTreeScratch &S, hipStream_t stream);
-// Size S for up to total_cap points in n_jobs segments (synchronises the device only when it
-// grows: call it before staging a round, not inside one).
-void reserve_tree_build_jobs(JointTreeScratch &S, int64_t total_cap, int32_t n_jobs);
 
 // ---- incremental index (the engine's rounds; FLANN_KDTreeWrapper::insertPoint,
 // utilities/flannkdtreewrapper.hpp:27-40, adds points to a live index instead of rebuilding it)
@@ -64,17 +41,24 @@ void reserve_tree_build_jobs(JointTreeScratch &S, int64_t total_cap, int32_t n_j
 // the groups of a wave walk neighbouring paths.  A full rebuild (first round, after a
 // truncation or a bulk insert, or more new points than kPtIncSeg) sorts every code with
 // hipcub and runs the same merge with no old points.
-constexpr int kPtIncSeg = 8192;   // new points / queries one round sorts in LDS
+constexpr int kPtIncSeg = 8192;   // new points one round merges in
 constexpr int kPtIncBits = 63;    // code bits (64-bit keys)
 struct IncPlan {
     double lo[kPtMaxDim], scale[kPtMaxDim];
     uint32_t qmax[kPtMaxDim];
     int32_t n;                               // code bits used
     int8_t dim[kPtIncBits], bit[kPtIncBits]; // MSB first
+    // the seeds' directions: slot h keeps the point of the largest score, kind 0: hdir . (the
+    // first three state dims), kind 1: -x[hdim], kind 2: +x[hdim]
+    float hdir[kPtHull][3];
+    int8_t hkind[kPtHull], hdim[kPtHull];
+    int32_t n_hull;
+    int32_t pad;
 };
 // the fixed plan of the ranges [lo, hi] (host): one quantisation step h for every dim, the
-// smallest for which the bits sum to <= 63 (<= 31 per dim), widest dims split first
-IncPlan make_inc_plan(int32_t d, const double *lo, const double *hi);
+// smallest for which the bits sum to <= 63 (<= 31 per dim), widest dims split first; the seed
+// directions over the first `spatial` dims
+IncPlan make_inc_plan(int32_t d, const double *lo, const double *hi, int32_t spatial);
 
 struct PtIncJob {
     PointTreeDev T;               // the tree after this build (T.pts / T.ids = the out arrays)
@@ -94,12 +78,13 @@ struct PtIncJob {
     int32_t *npos;                // scratch [kPtIncSeg]: the sorted new points' output places
     int64_t *nidx;                // points the last build indexed; set to n by this build
     unsigned long long *ibox;     // persistent box of the indexed points (order keys)
-    const double *q;              // queries [nq][d] to order by code, or nullptr
-    int64_t nq;
-    int32_t *qorder;              // out: query indices in code order [nq]
+    unsigned long long *err;      // device error count (the engine's counters[6]): an incremental
+                                  // build found more than kPtIncSeg new points (host bound broken)
+    unsigned long long *hull_keys;// [kPtHull] (score key << 32 | row) of each seed slot's best point
+    double *hull_pts;             // out: [kPtHull][d] the seed rows, and their ids (0: empty slot)
+    int32_t *hull_ids;
     int32_t full;                 // 1: nkeys / nvals hold every point (hipcub-sorted), no old points
     SpreadOut sp;
-    unsigned long long *dbg;      // MPT_SORT_DBG=1: the sort's phase times [job][8] (diagnostics)
 };
 // the incremental build of n trees of dim d (stream-ordered): sort, merge, box levels.
 // d_jobs / h_jobs: the same table on the device and the host (n == 1: d_jobs unused)
@@ -107,20 +92,15 @@ void launch_tree_inc_jobs(const PtIncJob *d_jobs, const PtIncJob *h_jobs, int32_
 
 class PointTree {
 public:
-    // the host part of build(): reserve, lay out the levels, and describe the device work as
-    // a job of a joint build (launch_tree_build_jobs); dev() is valid once that has run
-    PtBuildJob prepare(const double *pts, int64_t n_upper, const int64_t *n_dev, int32_t d, int64_t off,
-                       const struct SpreadOut *spread);
     // The incremental index: the job of this round's build (launch_tree_inc_jobs), dev()
     // valid once it has run.  full: rebuild from every point (its code + sort launches are
     // issued on `stream` here); else the points past the last build's count are merged in
-    // (at most kPtIncSeg of them: the caller's bound).  q / nq: the round's queries to order
-    // (nq <= kPtIncSeg), or nullptr.  lo / hi: the sampling ranges (the code plan).
+    // (at most kPtIncSeg of them: the caller's bound, checked on the device too).  lo / hi:
+    // the sampling ranges (the code plan), spatial: the leading state dims the seed
+    // directions span.
     PtIncJob prepare_inc(const double *pts, int64_t n_upper, const int64_t *n_dev, int32_t d, const double *lo,
-                         const double *hi, const double *q, int64_t nq, bool full, hipStream_t stream,
+                         const double *hi, int32_t spatial, bool full, hipStream_t stream,
                          const struct SpreadOut *spread);
-    // the query order of the last prepare_inc (nullptr: none)
-    const int32_t *query_order() const { return iq_on ? iqorder : nullptr; }
     ~PointTree();
     // Index rows [0, min(n_upper, *n_dev)) of pts [.][d]: bounding box and code plan on the
     // device, 30-bit codes over all dims, radix sort, boxes bottom-up.  Stream-ordered.
@@ -151,12 +131,14 @@ private:
     // incremental index (prepare_inc): two sets of sorted arrays, `icur` the last build's
     int64_t icap = 0;
     int32_t idim = 0, icur = 0;
-    bool iq_on = false;
     uint64_t *ikeys[2] = {nullptr, nullptr};
     int32_t *iids[2] = {nullptr, nullptr};
     double *ipts[2] = {nullptr, nullptr};
     uint64_t *inkeys = nullptr;
-    int32_t *invals = nullptr, *iqorder = nullptr;
+    int32_t *invals = nullptr;
+    unsigned long long *ihull_keys = nullptr;
+    double *ihull_pts = nullptr;
+    int32_t *ihull_ids = nullptr;
     uint64_t *ickeys = nullptr;
     int32_t *icvals = nullptr, *inpos = nullptr;
     int64_t *inidx = nullptr;
@@ -185,14 +167,11 @@ struct PtJob {
     const double *q;
     int32_t *ids;
     double *d2;
-    const int32_t *order;  // query indices in code order (prepare_inc), or nullptr: sample order
 };
 constexpr int kXcds = 8;  // MI355X: workgroups are dealt round-robin over 8 XCDs
 // jobs: a device array [n_jobs], all trees of dim d, nq queries each
 void launch_tree_nn1_jobs(const PtJob *d_jobs, int32_t n_jobs, int32_t d, int64_t nq, hipStream_t stream);
-// order (optional): the queries' processing order (a permutation of [0, nq)); results by query index
-void launch_tree_nn1(const PointTreeDev &T, const double *q, int64_t nq, int32_t *ids, double *d2, hipStream_t stream,
-                     const int32_t *order = nullptr);
+void launch_tree_nn1(const PointTreeDev &T, const double *q, int64_t nq, int32_t *ids, double *d2, hipStream_t stream);
 // Radius search (d2 < r2) over 3-dim keys: offsets == nullptr -> counts[qi]; else fill ids /
 // d2 of query qi from offsets[qi] on (traversal order).  below_only: ids <= qi only.
 void launch_tree_radius(const PointTreeDev &T, const double *q, int64_t nq, double r2, bool below_only,

@@ -231,11 +231,6 @@ __global__ __launch_bounds__(256) void k_pt_bbox(const double *__restrict__ pts,
     pt_bbox(pts, d, n_upper, n_dev, box, ticket, plan, sp, blockIdx.x, gridDim.x);
 }
 
-__global__ __launch_bounds__(64) void k_pt_plan(int32_t d, unsigned long long *__restrict__ box,
-                                                CodePlan *__restrict__ plan, SpreadOut sp) {
-    pt_plan(d, box, plan, sp);
-}
-
 template <int D = 0>
 __device__ __forceinline__ void pt_morton(const double *__restrict__ pts, int32_t d_rt, int64_t n_upper,
                                           const int64_t *__restrict__ n_dev, const CodePlan *__restrict__ plan,
@@ -405,56 +400,6 @@ __global__ __launch_bounds__(256) void k_pt_boxes(PointTreeDev T, float *__restr
     pt_boxes(T, boxes, ticket, blockIdx.x, gridDim.x);
 }
 
-// ---- the same build for many trees at once (mpt_rrt_step_many): blockIdx.y = the tree; a
-// tree's keys / values live in shared buffers at its offset, sorted by one segmented sort
-// plan_launch: the code plans come from k_pt_plan_jobs (one workgroup per tree) instead of
-// each tree's last bbox workgroup, so no bbox workgroup takes the ticket and its agent-scope
-// fences (an L2 write-back and invalidate per workgroup on gfx950)
-template <int D>
-__global__ __launch_bounds__(256) void k_pt_bbox_jobs(const PtBuildJob *__restrict__ jobs, int32_t d,
-                                                      int32_t bbox_points_per_group, int32_t plan_launch) {
-    const PtBuildJob &J = jobs[blockIdx.y];
-    // ~2048 points per workgroup (at most gridDim.x): 64 workgroups for every small tree cost
-    // more in fences, atomics and tickets than the scan itself
-    const int64_t per = bbox_points_per_group;
-    const int64_t nblk = std::min<int64_t>(gridDim.x, std::max<int64_t>(1, (J.T.n_upper + per - 1) / per));
-    if (blockIdx.x >= nblk) return;  // before the ticket: only the tree's own workgroups count
-    pt_bbox<D>(J.pts, d, J.T.n_upper, J.T.n_dev, J.bbox, J.ticket + 1, plan_launch ? nullptr : J.plan, J.sp,
-               blockIdx.x, nblk);
-}
-__global__ __launch_bounds__(64) void k_pt_plan_jobs(const PtBuildJob *__restrict__ jobs, int32_t d) {
-    const PtBuildJob &J = jobs[blockIdx.x];
-    pt_plan(d, J.bbox, J.plan, J.sp);
-}
-template <int D>
-__global__ __launch_bounds__(256) void k_pt_morton_jobs(const PtBuildJob *__restrict__ jobs, int32_t d,
-                                                        uint32_t *__restrict__ keys, int32_t *__restrict__ vals) {
-    const PtBuildJob &J = jobs[blockIdx.y];
-    if ((int64_t)blockIdx.x * blockDim.x >= J.T.n_upper) return;
-    pt_morton<D>(J.pts, d, J.T.n_upper, J.T.n_dev, J.plan, keys + J.off, vals + J.off, blockIdx.x);
-}
-template <int D>
-__global__ __launch_bounds__(256) void k_pt_gather_jobs(const PtBuildJob *__restrict__ jobs, int32_t d,
-                                                        const int32_t *__restrict__ vals_sorted) {
-    const PtBuildJob &J = jobs[blockIdx.y];
-    if ((int64_t)blockIdx.x * blockDim.x >= J.T.n_upper) return;
-    pt_gather<D>(J.pts, d, J.T.n_upper, J.T.n_dev, vals_sorted + J.off, J.spts, J.sids, J.boxes, blockIdx.x);
-}
-// top_launch: levels 5.. come from k_pt_top_jobs (one workgroup per tree) instead of each
-// tree's last group, so no group takes the ticket and its agent-scope fences
-__global__ __launch_bounds__(256) void k_pt_boxes_jobs(const PtBuildJob *__restrict__ jobs, int32_t top_launch) {
-    const PtBuildJob &J = jobs[blockIdx.y];
-    if (J.T.n_levels < 2) return;
-    const int64_t groups = (J.T.n_upper + kPtChunkLeaves * kPtFan - 1) / (kPtChunkLeaves * kPtFan);
-    if (blockIdx.x >= groups) return;  // before the ticket: only the tree's own groups count
-    pt_boxes(J.T, J.boxes, top_launch ? nullptr : J.ticket, blockIdx.x, groups);
-}
-__global__ __launch_bounds__(256) void k_pt_top_jobs(const PtBuildJob *__restrict__ jobs) {
-    const PtBuildJob &J = jobs[blockIdx.x];
-    if (J.T.n_levels <= kPtInBlockLevels) return;
-    pt_top_boxes(J.T, J.boxes);
-}
-
 // ---- incremental index (point_tree.h PtIncJob) ----
 
 // the job table on the device (a joint build), or one job passed in the kernel arguments
@@ -515,182 +460,6 @@ __device__ __forceinline__ void inc_cx(uint64_t &k, int32_t &v, uint64_t pk, int
     v = sw ? pv : v;
 }
 
-constexpr int kIncSortThreads = 1024;
-
-// blockIdx.x = 0: the tree's new points [nidx, n) -> codes, bitonic sort in LDS, nkeys / nvals
-// (and their box into ibox); blockIdx.x = 1: the round's queries -> code order (qorder).
-// (code, row) pairs order totally, so the result does not depend on the sort.
-template <int D>
-__device__ __forceinline__ void pt_inc_sort(const PtIncJob &J, int seg) {
-    __shared__ uint64_t sk[kPtIncSeg];
-    __shared__ int32_t sv[kPtIncSeg];
-    __shared__ unsigned long long s_min[kPtMaxDim], s_max[kPtMaxDim];
-    // the plan in LDS: its fields were per-lane flat loads, each waited on, inside the code loop
-    __shared__ IncPlan s_plan;
-    const int t = threadIdx.x;
-    int64_t m = 0, base = 0;
-    const double *src = nullptr;
-    if (seg == 0) {
-        if (J.full) return;  // nkeys / nvals already hold every point
-        const int64_t nd = *J.T.n_dev, n = nd < J.T.n_upper ? nd : J.T.n_upper;
-        base = *J.nidx;
-        m = n - base;
-        m = m < 0 ? 0 : (m > kPtIncSeg ? kPtIncSeg : m);  // the caller bounds it (host grow count)
-        src = J.pts;
-    } else {
-        if (!J.q) return;
-        m = J.nq < kPtIncSeg ? J.nq : kPtIncSeg;
-        src = J.q;
-    }
-    if (m == 0) return;
-    int size = 2;
-    while (size < m) size <<= 1;
-    if (t < kPtMaxDim) {
-        s_min[t] = ~0ull;
-        s_max[t] = 0ull;
-    }
-    auto stamp = [&](int i) {
-        if (J.dbg && t == 0) J.dbg[blockIdx.y * 8 + i] = __builtin_amdgcn_s_memrealtime();
-    };
-    stamp(0);
-    static_assert(sizeof(IncPlan) % 4 == 0, "IncPlan copied as words");
-    for (int w = t; w < (int)(sizeof(IncPlan) / 4); w += kIncSortThreads)
-        reinterpret_cast<uint32_t *>(&s_plan)[w] = reinterpret_cast<const uint32_t *>(J.plan)[w];
-    __syncthreads();
-    stamp(1);
-    unsigned long long mn[D], mx[D];
-#pragma unroll
-    for (int j = 0; j < D; ++j) {
-        mn[j] = ~0ull;
-        mx[j] = 0ull;
-    }
-    for (int i = t; i < size; i += kIncSortThreads) {
-        if (i < m) {
-            double x[D];
-            const int64_t row = base + i;
-#pragma unroll
-            for (int j = 0; j < D; ++j) x[j] = src[row * D + j];
-            sk[i] = inc_code<D>(&s_plan, x);
-            sv[i] = (int32_t)row;
-            if (seg == 0) {
-#pragma unroll
-                for (int j = 0; j < D; ++j) {
-                    const unsigned long long k = order_key_pt(x[j]);
-                    mn[j] = k < mn[j] ? k : mn[j];
-                    mx[j] = k > mx[j] ? k : mx[j];
-                }
-            }
-        } else {
-            sk[i] = ~0ull;  // real codes use 63 bits
-            sv[i] = 0x7fffffff;
-        }
-    }
-    __syncthreads();
-    if (seg == 0) {  // the persistent box of the indexed points (MPT_NN_AUTO's spread)
-#pragma unroll
-        for (int j = 0; j < D; ++j) {
-#pragma unroll
-            for (int off = 32; off > 0; off >>= 1) {
-                const unsigned long long omn = __shfl_xor(mn[j], off), omx = __shfl_xor(mx[j], off);
-                mn[j] = omn < mn[j] ? omn : mn[j];
-                mx[j] = omx > mx[j] ? omx : mx[j];
-            }
-            if ((t & 63) == 0) {
-                atomicMin(&s_min[j], mn[j]);
-                atomicMax(&s_max[j], mx[j]);
-            }
-        }
-    }
-    stamp(2);
-    // bitonic sort of [0, size), 8 consecutive elements per thread in registers: partners fewer
-    // than 8 apart are in the thread's registers, fewer than 512 apart in its wave (lane
-    // shuffles), the rest exchanged through LDS (a 4096-element sort: 6 LDS stages of 78)
-    constexpr int E = kPtIncSeg / kIncSortThreads;
-    uint64_t key[E];
-    int32_t val[E];
-#pragma unroll
-    for (int a = 0; a < E; ++a) {
-        const int i = t * E + a;
-        key[a] = i < size ? sk[i] : ~0ull;
-        val[a] = i < size ? sv[i] : 0x7fffffff;
-    }
-    for (int k = 2; k <= size; k <<= 1) {
-        for (int j = k >> 1; j > 0; j >>= 1) {
-            if (j >= 64 * E) {  // block-uniform
-                __syncthreads();  // the last exchange's reads are done
-#pragma unroll
-                for (int a = 0; a < E; ++a) {
-                    sk[t * E + a] = key[a];
-                    sv[t * E + a] = val[a];
-                }
-                __syncthreads();
-#pragma unroll
-                for (int a = 0; a < E; ++a) {
-                    const int i = t * E + a, l = i ^ j;
-                    const uint64_t pk = sk[l];
-                    const int32_t pv = sv[l];
-                    inc_cx(key[a], val[a], pk, pv, (i < l) == ((i & k) == 0));
-                }
-            } else if (j >= E) {
-                const int lm = j / E;
-                const bool lower = (t & lm) == 0;
-#pragma unroll
-                for (int a = 0; a < E; ++a) {
-                    const uint64_t pk = __shfl_xor(key[a], lm);
-                    const int32_t pv = __shfl_xor(val[a], lm);
-                    inc_cx(key[a], val[a], pk, pv, lower == (((t * E + a) & k) == 0));
-                }
-            } else {
-                // partners within the thread's registers: j is 4, 2 or 1 (compile-time indices)
-#pragma unroll
-                for (int jj = E / 2; jj > 0; jj >>= 1) {
-                    if (jj != j) continue;
-#pragma unroll
-                    for (int a = 0; a < E; ++a) {
-                        const int b = a ^ jj;
-                        if (b < a) continue;
-                        const bool up = ((t * E + a) & k) == 0;
-                        const bool sw = up == inc_less(key[b], val[b], key[a], val[a]);
-                        const uint64_t ka = key[a], kb = key[b];
-                        const int32_t va = val[a], vb = val[b];
-                        key[a] = sw ? kb : ka;
-                        val[a] = sw ? vb : va;
-                        key[b] = sw ? ka : kb;
-                        val[b] = sw ? va : vb;
-                    }
-                }
-            }
-        }
-    }
-    stamp(3);
-    __syncthreads();
-#pragma unroll
-    for (int a = 0; a < E; ++a) {
-        sk[t * E + a] = key[a];
-        sv[t * E + a] = val[a];
-    }
-    __syncthreads();
-    if (seg == 0) {
-        for (int i = t; i < m; i += kIncSortThreads) {
-            J.nkeys[i] = sk[i];
-            J.nvals[i] = sv[i];
-        }
-        if (t < D) {
-            atomicMin(J.ibox + t, s_min[t]);
-            atomicMax(J.ibox + kPtMaxDim + t, s_max[t]);
-        }
-    } else {
-        for (int i = t; i < m; i += kIncSortThreads) J.qorder[i] = sv[i];
-    }
-    stamp(4);
-}
-
-template <int D>
-__global__ __launch_bounds__(kIncSortThreads) void k_pt_inc_sort(IncJobs jobs, int seg0) {
-    if (jobs.table) pt_inc_sort<D>(jobs.table[blockIdx.y], seg0 + (int)blockIdx.x);
-    else pt_inc_sort<D>(jobs.one, seg0 + (int)blockIdx.x);
-}
-
 // The new points' sort over many CUs: one workgroup per tree runs the 4096-element bitonic
 // network on one CU (~78 stages), which leaves most of the chip idle when there are few trees.
 // Instead: the codes one thread a point (k_pt_inc_ncodes); each wave sorts a chunk of 512 (8
@@ -704,21 +473,64 @@ constexpr int kIncChunks = kPtIncSeg / kIncChunk;
 constexpr int kIncChunkWaves = 4;  // chunks a workgroup sorts
 static_assert(kIncChunks % kIncChunkWaves == 0, "whole workgroups");
 
-// the new points' codes and rows (one thread a point) into nkeys / nvals, in row order, and
-// their box into ibox
+// Seed slots (point_tree.h kPtHull): lane h of a wave scores slot h over the wave's 64 points
+// (staged in LDS: every lane reads the same point at once, a broadcast) and offers its best to
+// the tree's slot with one 64-bit atomicMax of (score as an ordered float key << 32 | row).  Rows
+// of a wave are consecutive (row0 + lane).  The float rounding of the score only decides which
+// near-tie becomes the seed; any point is a valid seed.
+constexpr int kHullWaves = 4;  // waves of the workgroups that score (256 threads)
 template <int D>
-__device__ __forceinline__ void pt_inc_ncodes(const PtIncJob &J, const IncPlan &P) {
+__device__ __forceinline__ void hull_offer(const IncPlan &P, const double (&x)[D], bool live, int64_t row0,
+                                           double (*s_rows)[D], unsigned long long *__restrict__ keys) {
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int j = 0; j < D; ++j) s_rows[lane][j] = live ? x[j] : 0.0;
+    const uint64_t lm = __ballot(live);
+    __builtin_amdgcn_wave_barrier();
+    if (lane < P.n_hull) {
+        const int kind = P.hkind[lane], dm = P.hdim[lane];
+        const float u0 = P.hdir[lane][0], u1 = P.hdir[lane][1], u2 = P.hdir[lane][2];
+        unsigned long long best = 0;
+        for (uint64_t m = lm; m; m &= m - 1) {
+            const int j = __ffsll((long long)m) - 1;
+            double v;
+            if (kind == 0) {
+                v = (double)u0 * s_rows[j][0];
+                if (D > 1) v += (double)u1 * s_rows[j][D > 1 ? 1 : 0];
+                if (D > 2) v += (double)u2 * s_rows[j][D > 2 ? 2 : 0];
+            } else {
+                double xv = s_rows[j][0];
+#pragma unroll
+                for (int k = 1; k < D; ++k)
+                    if (k == dm) xv = s_rows[j][k];
+                v = kind == 1 ? -xv : xv;
+            }
+            const uint32_t b = __float_as_uint((float)v);
+            const uint32_t key = (b & 0x80000000u) ? ~b : (b | 0x80000000u);
+            const unsigned long long k64 = ((unsigned long long)key << 32) | (uint32_t)(row0 + j);
+            best = k64 > best ? k64 : best;
+        }
+        if (best) atomicMax(keys + lane, best);
+    }
+    __builtin_amdgcn_wave_barrier();
+}
+
+// the new points' codes and rows (one thread a point) into nkeys / nvals, in row order, their
+// box into ibox, and their offers to the seed slots
+template <int D>
+__device__ __forceinline__ void pt_inc_ncodes(const PtIncJob &J, const IncPlan &P, double (*s_rows)[D]) {
     if (J.full) return;
     const int64_t nd = *J.T.n_dev, n = nd < J.T.n_upper ? nd : J.T.n_upper;
     const int64_t base = *J.nidx;
     int64_t m = n - base;
+    if (m > kPtIncSeg && blockIdx.x == 0 && threadIdx.x == 0 && J.err) atomicAdd(J.err, 1ull);  // the host's bound broke
     m = m < 0 ? 0 : (m > kPtIncSeg ? kPtIncSeg : m);
     const int i = (int)blockIdx.x * (int)blockDim.x + (int)threadIdx.x;
     if ((int64_t)blockIdx.x * blockDim.x >= m) return;  // block-uniform
     const bool live = i < m;
     unsigned long long mn[D], mx[D];
+    double x[D];
     if (live) {
-        double x[D];
         const int64_t row = base + i;
         load_global<D>(J.pts + row * D, x);
         ((MPT_GLOBAL uint64_t *)J.nkeys)[i] = inc_code<D>(&P, x);
@@ -749,17 +561,20 @@ __device__ __forceinline__ void pt_inc_ncodes(const PtIncJob &J, const IncPlan &
             atomicMax(J.ibox + kPtMaxDim + j, mx[j]);
         }
     }
+    const int64_t row0 = base + (i & ~63);
+    hull_offer<D>(P, x, live, row0, s_rows, J.hull_keys);
 }
 
 template <int D>
-__global__ __launch_bounds__(256) void k_pt_inc_ncodes(IncJobs jobs) {
+__global__ __launch_bounds__(64 * kHullWaves) void k_pt_inc_ncodes(IncJobs jobs) {
     __shared__ IncPlan s_plan;
+    __shared__ double s_rows[kHullWaves][64][D];
     const PtIncJob &J = jobs.table ? jobs.table[blockIdx.y] : jobs.one;
     for (int w = threadIdx.x; w < (int)(sizeof(IncPlan) / 4); w += blockDim.x)
         reinterpret_cast<uint32_t *>(&s_plan)[w] = reinterpret_cast<const uint32_t *>(J.plan)[w];
     __syncthreads();
-    if (jobs.table) pt_inc_ncodes<D>(jobs.table[blockIdx.y], s_plan);
-    else pt_inc_ncodes<D>(jobs.one, s_plan);
+    if (jobs.table) pt_inc_ncodes<D>(jobs.table[blockIdx.y], s_plan, s_rows[threadIdx.x >> 6]);
+    else pt_inc_ncodes<D>(jobs.one, s_plan, s_rows[threadIdx.x >> 6]);
 }
 
 // one chunk of 512 (code, row) pairs a wave: nkeys / nvals -> ckeys / cvals
@@ -1090,12 +905,12 @@ __device__ __forceinline__ void pt_inc_merge2(const PtIncJob &J) {
     }
 }
 
-// merge2: the placed merge for incremental jobs (a full rebuild keeps the merge-path form;
-// its tiles are kIncTile outputs, so the grid is sized for those)
+// the placed merge for incremental jobs (a full rebuild keeps the merge-path form; its tiles
+// are kIncTile outputs, so the grid is sized for those)
 template <int D>
-__global__ __launch_bounds__(kIncTile) void k_pt_inc_merge(IncJobs jobs, int merge2) {
+__global__ __launch_bounds__(kIncTile) void k_pt_inc_merge(IncJobs jobs) {
     const PtIncJob &J = jobs.table ? jobs.table[blockIdx.y] : jobs.one;
-    if (merge2 && !J.full) {
+    if (!J.full) {
         if (jobs.table) pt_inc_merge2<D>(jobs.table[blockIdx.y]);
         else pt_inc_merge2<D>(jobs.one);
     } else {
@@ -1116,9 +931,18 @@ __global__ __launch_bounds__(256) void k_pt_inc_boxes(IncJobs jobs) {
     else pt_inc_boxes(jobs.one);
 }
 
-// levels 5.. (one workgroup per tree), then the indexed count and the spread feedback
+// levels 5.. (one workgroup per tree), the seed rows of the slots' best points, then the
+// indexed count and the spread feedback
 __device__ __forceinline__ void pt_inc_top(const PtIncJob &J) {
     if (J.T.n_levels > kPtInBlockLevels) pt_top_boxes(J.T, J.boxes);
+    const int d = J.T.d;
+    for (int it = threadIdx.x; it < kPtHull * d; it += blockDim.x) {
+        const int h = it / d, k = it - h * d;
+        const unsigned long long key = J.hull_keys[h];
+        const int64_t row = (int64_t)(uint32_t)key;
+        J.hull_pts[it] = key ? J.pts[row * d + k] : 0.0;
+        if (k == 0) J.hull_ids[h] = key ? (int32_t)row + 1 : 0;
+    }
     if (threadIdx.x != 0) return;
     *J.nidx = live_n(J.T);
     const SpreadOut &sp = J.sp;
@@ -1147,24 +971,32 @@ __global__ __launch_bounds__(256) void k_pt_inc_bbox(const double *__restrict__ 
     pt_bbox<D>(pts, d, n_upper, n_dev, box, nullptr, nullptr, SpreadOut{}, blockIdx.x, gridDim.x);
 }
 
-// full rebuild: every point's code (rows past the live count sort to the end)
+// full rebuild: every point's code (rows past the live count sort to the end) and its offers to
+// the seed slots (reset before this launch)
 template <int D>
-__global__ __launch_bounds__(256) void k_pt_inc_codes(const double *__restrict__ pts, int64_t n_upper,
-                                                      const int64_t *__restrict__ n_dev,
-                                                      const IncPlan *__restrict__ plan, uint64_t *__restrict__ keys,
-                                                      int32_t *__restrict__ vals) {
+__global__ __launch_bounds__(64 * kHullWaves) void k_pt_inc_codes(const double *__restrict__ pts, int64_t n_upper,
+                                                                  const int64_t *__restrict__ n_dev,
+                                                                  const IncPlan *__restrict__ plan,
+                                                                  uint64_t *__restrict__ keys,
+                                                                  int32_t *__restrict__ vals,
+                                                                  unsigned long long *__restrict__ hull_keys) {
+    __shared__ IncPlan s_plan;
+    __shared__ double s_rows[kHullWaves][64][D];
+    for (int w = threadIdx.x; w < (int)(sizeof(IncPlan) / 4); w += blockDim.x)
+        reinterpret_cast<uint32_t *>(&s_plan)[w] = reinterpret_cast<const uint32_t *>(plan)[w];
+    __syncthreads();
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n_upper) return;
+    if ((int64_t)blockIdx.x * blockDim.x >= n_upper) return;  // block-uniform
     const int64_t n = *n_dev < n_upper ? *n_dev : n_upper;
-    vals[i] = (int32_t)i;
-    if (i >= n) {
-        keys[i] = ~0ull;
-        return;
-    }
+    const bool live = i < n;
     double x[D];
 #pragma unroll
-    for (int j = 0; j < D; ++j) x[j] = pts[i * D + j];
-    keys[i] = inc_code<D>(plan, x);
+    for (int j = 0; j < D; ++j) x[j] = live ? pts[i * D + j] : 0.0;
+    if (i < n_upper) {
+        vals[i] = (int32_t)i;
+        keys[i] = live ? inc_code<D>(&s_plan, x) : ~0ull;
+    }
+    hull_offer<D>(s_plan, x, live, i & ~(int64_t)63, s_rows[threadIdx.x >> 6], hull_keys);
 }
 
 constexpr int kPtGroupsPerBlock = 256 / kPtFan;
@@ -1220,11 +1052,42 @@ __device__ __forceinline__ float box_lb(const float *__restrict__ b, const doubl
     }
 }
 
+// the seeds' best (d2, id) for the query, over a group of G lanes (point_tree.h kPtHull): lane
+// `sub` takes seeds sub, sub + G, ...; the group's best by xor-shuffles.  Leaves (bd, bi) at
+// +inf / -1 when the tree carries no seeds.
+template <int D, int G>
+__device__ __forceinline__ void hull_seed(const PointTreeDev &T, const double (&qq)[D], int sub, double &bd,
+                                          int32_t &bi, uint32_t &n_pts) {
+    if (!T.hull_ids) return;
+    for (int h = sub; h < kPtHull; h += G) {
+        const int32_t id = ((gi32)T.hull_ids)[h];
+        if (id <= 0) continue;
+        double row[D];
+#pragma unroll
+        for (int k = 0; k < D; ++k) row[k] = ((gdbl)T.hull_pts)[h * D + k];
+        const double dd = flann_l2<D>(qq, row);
+        ++n_pts;
+        if (nn_better(dd, id, bd, bi)) {
+            bd = dd;
+            bi = id;
+        }
+    }
+#pragma unroll
+    for (int off = G / 2; off > 0; off >>= 1) {
+        const double od = __shfl_xor(bd, off, G);
+        const int32_t oi = __shfl_xor(bi, off, G);
+        if (nn_better(od, oi, bd, bi)) {
+            bd = od;
+            bi = oi;
+        }
+    }
+}
+
 // queries [blk * BS / 8, + BS / 8) of one tree (a workgroup's share of k_tree_nn1 / _jobs)
 template <int D, int BS>
 __device__ __forceinline__ void tree_nn1_block(const PointTreeDev &T, const double *__restrict__ q, int64_t nq,
                                                int32_t *__restrict__ out_ids, double *__restrict__ out_d2,
-                                               int64_t blk, const int32_t *__restrict__ order) {
+                                               int64_t blk) {
     __shared__ int32_t s_node[BS / kPtFan][kPtStack];
     // stacked lower bounds as floats rounded down (still lower bounds: pruning stays exact),
     // half the LDS of doubles, so more one-wave workgroups fit a CU
@@ -1234,9 +1097,7 @@ __device__ __forceinline__ void tree_nn1_block(const PointTreeDev &T, const doub
     const int sub = (int)(t % kPtFan);
     const int grp = threadIdx.x / kPtFan;
     if (slot >= nq) return;  // whole groups leave together
-    // the query this group answers: in code order (neighbouring groups walk neighbouring
-    // paths) when the build sorted the queries, else in sample order
-    const int64_t qi = order ? (int64_t)order[slot] : slot;
+    const int64_t qi = slot;
     double qq[D];
 #pragma unroll
     for (int i = 0; i < D; ++i) qq[i] = q[qi * D + i];
@@ -1251,6 +1112,7 @@ __device__ __forceinline__ void tree_nn1_block(const PointTreeDev &T, const doub
     int32_t bi = -1;
     uint32_t n_pts = 0, n_box = 0;
     if (n > 0) {
+        hull_seed<D, kPtFan>(T, qq, sub, bd, bi, n_pts);
         int sp = 1;
         if (sub == 0) {
             s_node[grp][0] = T.n_levels << 27;  // the root: level n_levels, index 0
@@ -1353,7 +1215,7 @@ inline int pt_nn_width(int32_t d, int64_t queries) {
 template <int D, int BS, int NW>
 __device__ __forceinline__ void tree_nn1_blockn(const PointTreeDev &T, const double *__restrict__ q, int64_t nq,
                                                 int32_t *__restrict__ out_ids, double *__restrict__ out_d2,
-                                                int64_t blk, const int32_t *__restrict__ order) {
+                                                int64_t blk) {
     constexpr int kPtG2 = NW * kPtFan;                     // lanes per query
     constexpr int kPtStack2 = NW * kPtFan * kPtMaxLevels;  // ~NW blocks of 7 a level
     static_assert(kPtG2 <= 64, "ballot bits per group");
@@ -1366,7 +1228,7 @@ __device__ __forceinline__ void tree_nn1_blockn(const PointTreeDev &T, const dou
     const int ls = sub % kPtFan;    // the child / point this lane takes
     const int grp = threadIdx.x / kPtG2;
     if (slot >= nq) return;  // whole groups leave together
-    const int64_t qi = order ? (int64_t)order[slot] : slot;
+    const int64_t qi = slot;
     double qq[D];
 #pragma unroll
     for (int i = 0; i < D; ++i) qq[i] = q[qi * D + i];
@@ -1381,6 +1243,7 @@ __device__ __forceinline__ void tree_nn1_blockn(const PointTreeDev &T, const dou
     int32_t bi = -1;
     uint32_t n_pts = 0, n_box = 0;
     if (n > 0) {
+        hull_seed<D, kPtG2>(T, qq, sub, bd, bi, n_pts);
         int sp = 1;
         if (sub == 0) {
             s_node[grp][0] = T.n_levels << 27;
@@ -1483,10 +1346,9 @@ __device__ __forceinline__ void tree_nn1_blockn(const PointTreeDev &T, const dou
 
 template <int D, int BS, int W>
 __global__ __launch_bounds__(BS) void k_tree_nn1(PointTreeDev T, const double *__restrict__ q, int64_t nq,
-                                                 int32_t *__restrict__ out_ids, double *__restrict__ out_d2,
-                                                 const int32_t *__restrict__ order) {
-    if constexpr (W >= 2) tree_nn1_blockn<D, BS, W>(T, q, nq, out_ids, out_d2, blockIdx.x, order);
-    else tree_nn1_block<D, BS>(T, q, nq, out_ids, out_d2, blockIdx.x, order);
+                                                 int32_t *__restrict__ out_ids, double *__restrict__ out_d2) {
+    if constexpr (W >= 2) tree_nn1_blockn<D, BS, W>(T, q, nq, out_ids, out_d2, blockIdx.x);
+    else tree_nn1_block<D, BS>(T, q, nq, out_ids, out_d2, blockIdx.x);
 }
 
 // Many trees in one launch (mpt_rrt_step_many: one engine per independent seed).  Jobs are
@@ -1504,8 +1366,8 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(D >= 15 ? 4 
     const int64_t job = xcd + kXcds * (slot / blocks_per_job);
     if (job >= n_jobs) return;
     const PtJob &J = jobs[job];
-    if constexpr (W >= 2) tree_nn1_blockn<D, BS, W>(J.T, J.q, nq, J.ids, J.d2, slot % blocks_per_job, J.order);
-    else tree_nn1_block<D, BS>(J.T, J.q, nq, J.ids, J.d2, slot % blocks_per_job, J.order);
+    if constexpr (W >= 2) tree_nn1_blockn<D, BS, W>(J.T, J.q, nq, J.ids, J.d2, slot % blocks_per_job);
+    else tree_nn1_block<D, BS>(J.T, J.q, nq, J.ids, J.d2, slot % blocks_per_job);
 }
 
 // Radius search (FLANN_KDTreeWrapper::kNearestWithin, utilities/flannkdtreewrapper.hpp:91-117:
@@ -1588,8 +1450,9 @@ PointTree::~PointTree() {
                     (void *)boxes, temp, (void *)bbox, (void *)plan})
         if (p) (void)hipFree(p);
     for (void *p : {(void *)ikeys[0], (void *)ikeys[1], (void *)iids[0], (void *)iids[1], (void *)ipts[0],
-                    (void *)ipts[1], (void *)inkeys, (void *)invals, (void *)iqorder, itemp, (void *)inidx,
-                    (void *)ibox, (void *)iplan, (void *)ickeys, (void *)icvals, (void *)inpos})
+                    (void *)ipts[1], (void *)inkeys, (void *)invals, itemp, (void *)inidx, (void *)ibox, (void *)iplan,
+                    (void *)ickeys, (void *)icvals, (void *)inpos, (void *)ihull_keys, (void *)ihull_pts,
+                    (void *)ihull_ids})
         if (p) (void)hipFree(p);
 }
 
@@ -1651,15 +1514,14 @@ void PointTree::build(const double *pts, int64_t n_upper, const int64_t *n_dev, 
     t.boxes = boxes;
     t.pts = spts;
     t.ids = sids;
+    t.hull_pts = nullptr;
+    t.hull_ids = nullptr;
     if (n_upper <= 0) return;
     const unsigned blocks = (unsigned)((n_upper + 255) / 256);
-    // bbox starts empty (reserve) and the plan (in k_pt_bbox) resets it after reading it
-    // MPT_PT_PLAN_LAUNCH=1: the plan as a separate one-wave launch (A/B knob)
-    static const bool plan_launch = getenv("MPT_PT_PLAN_LAUNCH") && atoi(getenv("MPT_PT_PLAN_LAUNCH")) == 1;
+    // bbox starts empty (reserve) and the plan (in k_pt_bbox's last workgroup) resets it after
+    // reading it
     const SpreadOut sp = spread ? *spread : SpreadOut{};
-    hipLaunchKernelGGL(k_pt_bbox, dim3(64), dim3(256), 0, stream, pts, d, n_upper, n_dev, bbox, ticket + 1,
-                       plan_launch ? nullptr : plan, sp);
-    if (plan_launch) hipLaunchKernelGGL(k_pt_plan, dim3(1), dim3(64), 0, stream, d, bbox, plan, sp);
+    hipLaunchKernelGGL(k_pt_bbox, dim3(64), dim3(256), 0, stream, pts, d, n_upper, n_dev, bbox, ticket + 1, plan, sp);
     hipLaunchKernelGGL(k_pt_morton, dim3(blocks), dim3(256), 0, stream, pts, d, n_upper, n_dev, plan, keys, vals);
     hip_check(hipGetLastError(), "k_pt_morton");
     size_t tb = temp_bytes;
@@ -1676,104 +1538,7 @@ void PointTree::build(const double *pts, int64_t n_upper, const int64_t *n_dev, 
     hip_check(hipGetLastError(), "k_pt_boxes");
 }
 
-PtBuildJob PointTree::prepare(const double *pts, int64_t n_upper, const int64_t *n_dev, int32_t d, int64_t off,
-                              const SpreadOut *spread) {
-    if (d != 3 && d != 7 && d != 15) throw Error{1, "point tree: state dim must be 3, 7 or 15"};
-    if (n_upper < 1 || n_upper >= (int64_t(1) << 27)) throw Error{1, "point tree: bad point count"};
-    reserve(n_upper, d);
-    t.d = d;
-    t.n_upper = n_upper;
-    t.n_levels = pt_levels(n_upper);
-    t.n_dev = n_dev;
-    t.boxes = boxes;
-    t.pts = spts;
-    t.ids = sids;
-    return PtBuildJob{t, pts, off, bbox, ticket, plan, spts, sids, boxes, spread ? *spread : SpreadOut{}};
-}
-
-void reserve_tree_build_jobs(JointTreeScratch &S, int64_t total_cap, int32_t n_jobs) {
-    if (total_cap >= (int64_t(1) << 31)) throw Error{1, "joint build: too many points"};
-    if (total_cap > S.cap) {
-        hip_check(hipDeviceSynchronize(), "sync");  // the old buffers may still be in use
-        for (void *p : {(void *)S.keys, (void *)S.keys_sorted, (void *)S.vals, (void *)S.vals_sorted})
-            if (p) hip_check(hipFree(p), "free");
-        const int64_t c = std::max<int64_t>(total_cap, 1024);
-        hip_check(hipMalloc(&S.keys, sizeof(uint32_t) * c), "joint keys");
-        hip_check(hipMalloc(&S.keys_sorted, sizeof(uint32_t) * c), "joint keys");
-        hip_check(hipMalloc(&S.vals, sizeof(int32_t) * c), "joint vals");
-        hip_check(hipMalloc(&S.vals_sorted, sizeof(int32_t) * c), "joint vals");
-        S.cap = c;
-    }
-    size_t tb = 0;
-    hip_check(hipcub::DeviceSegmentedRadixSort::SortPairs(nullptr, tb, S.keys, S.keys_sorted, S.vals, S.vals_sorted,
-                                                          (int)S.cap, n_jobs, (const int32_t *)nullptr,
-                                                          (const int32_t *)nullptr, 0, 32, (hipStream_t)0),
-              "segmented sort size");
-    if (tb > S.temp_bytes) {
-        hip_check(hipDeviceSynchronize(), "sync");
-        if (S.temp) hip_check(hipFree(S.temp), "free");
-        hip_check(hipMalloc(&S.temp, tb), "segmented sort temp");
-        S.temp_bytes = tb;
-    }
-}
-
-void launch_tree_build_jobs(const PtBuildJob *d_jobs, const PtBuildJob *h_jobs, int32_t n, int32_t d,
-                            const int32_t *d_offsets, int64_t total, JointTreeScratch &S, hipStream_t stream) {
-    if (n <= 0) return;
-    int64_t max_n = 0, max_groups = 1;
-    for (int32_t j = 0; j < n; ++j) {
-        max_n = std::max(max_n, h_jobs[j].T.n_upper);
-        max_groups = std::max(max_groups, (h_jobs[j].T.n_upper + kPtChunkLeaves * kPtFan - 1) / (kPtChunkLeaves * kPtFan));
-    }
-    if (total > S.cap) {
-        hip_check(hipDeviceSynchronize(), "sync");  // the old buffers may still be in use
-        for (void *p : {(void *)S.keys, (void *)S.keys_sorted, (void *)S.vals, (void *)S.vals_sorted})
-            if (p) hip_check(hipFree(p), "free");
-        const int64_t c = std::max<int64_t>(total, 2 * S.cap);
-        hip_check(hipMalloc(&S.keys, sizeof(uint32_t) * c), "joint keys");
-        hip_check(hipMalloc(&S.keys_sorted, sizeof(uint32_t) * c), "joint keys");
-        hip_check(hipMalloc(&S.vals, sizeof(int32_t) * c), "joint vals");
-        hip_check(hipMalloc(&S.vals_sorted, sizeof(int32_t) * c), "joint vals");
-        S.cap = c;
-    }
-    size_t tb = 0;
-    hip_check(hipcub::DeviceSegmentedRadixSort::SortPairs(nullptr, tb, S.keys, S.keys_sorted, S.vals, S.vals_sorted,
-                                                          (int)total, n, d_offsets, d_offsets + 1, 0, 32, stream),
-              "segmented sort size");
-    if (tb > S.temp_bytes) {
-        hip_check(hipDeviceSynchronize(), "sync");
-        if (S.temp) hip_check(hipFree(S.temp), "free");
-        hip_check(hipMalloc(&S.temp, tb), "segmented sort temp");
-        S.temp_bytes = tb;
-    }
-    const unsigned bx = (unsigned)((max_n + 255) / 256);
-    // MPT_PT_BBOX_PTS: points per bbox workgroup of the joint build (A/B knob)
-    static const int per = getenv("MPT_PT_BBOX_PTS") && atoi(getenv("MPT_PT_BBOX_PTS")) > 0
-                               ? atoi(getenv("MPT_PT_BBOX_PTS")) : 2048;
-    // compile-time rows for the engines' state dims (MPT_PT_FIXED_D=0: the run-time d, A/B)
-    static const bool fixed_d = !getenv("MPT_PT_FIXED_D") || atoi(getenv("MPT_PT_FIXED_D")) != 0;
-    const int dd = fixed_d && (d == 3 || d == 7 || d == 15) ? d : 0;
-    auto by_d = [&](auto k3, auto k7, auto k15, auto k0) { return dd == 3 ? k3 : dd == 7 ? k7 : dd == 15 ? k15 : k0; };
-    // MPT_PT_PLAN_JOBS=0: each tree's last bbox workgroup computes its plan (ticket + fences), A/B
-    static const bool plan_jobs = !getenv("MPT_PT_PLAN_JOBS") || atoi(getenv("MPT_PT_PLAN_JOBS")) != 0;
-    hipLaunchKernelGGL(by_d(k_pt_bbox_jobs<3>, k_pt_bbox_jobs<7>, k_pt_bbox_jobs<15>, k_pt_bbox_jobs<0>), dim3(64, n),
-                       dim3(256), 0, stream, d_jobs, d, per, plan_jobs ? 1 : 0);
-    if (plan_jobs) hipLaunchKernelGGL(k_pt_plan_jobs, dim3(n), dim3(64), 0, stream, d_jobs, d);
-    hipLaunchKernelGGL(by_d(k_pt_morton_jobs<3>, k_pt_morton_jobs<7>, k_pt_morton_jobs<15>, k_pt_morton_jobs<0>),
-                       dim3(bx, n), dim3(256), 0, stream, d_jobs, d, S.keys, S.vals);
-    hip_check(hipGetLastError(), "k_pt_morton_jobs");
-    tb = S.temp_bytes;
-    hip_check(hipcub::DeviceSegmentedRadixSort::SortPairs(S.temp, tb, S.keys, S.keys_sorted, S.vals, S.vals_sorted,
-                                                          (int)total, n, d_offsets, d_offsets + 1, 0, 32, stream),
-              "segmented sort");
-    hipLaunchKernelGGL(by_d(k_pt_gather_jobs<3>, k_pt_gather_jobs<7>, k_pt_gather_jobs<15>, k_pt_gather_jobs<0>),
-                       dim3(bx, n), dim3(256), 0, stream, d_jobs, d, S.vals_sorted);
-    hipLaunchKernelGGL(k_pt_boxes_jobs, dim3((unsigned)max_groups, n), dim3(256), 0, stream, d_jobs, plan_jobs ? 1 : 0);
-    if (plan_jobs) hipLaunchKernelGGL(k_pt_top_jobs, dim3(n), dim3(256), 0, stream, d_jobs);
-    hip_check(hipGetLastError(), "k_pt_boxes_jobs");
-}
-
-IncPlan make_inc_plan(int32_t d, const double *lo, const double *hi) {
+IncPlan make_inc_plan(int32_t d, const double *lo, const double *hi, int32_t spatial) {
     IncPlan P{};
     double ext[kPtMaxDim] = {}, emax = 0.0;
     for (int j = 0; j < d; ++j) {
@@ -1810,6 +1575,37 @@ IncPlan make_inc_plan(int32_t d, const double *lo, const double *hi) {
                 ++n;
             }
     P.n = n;
+    // seed slots: every dim's minimum and maximum, then directions over the first `spatial`
+    // dims spread evenly (a Fibonacci lattice on the sphere; the circle for two dims)
+    int h = 0;
+    for (int j = 0; j < d && h + 1 < kPtHull; ++j) {
+        P.hkind[h] = 1;
+        P.hdim[h++] = (int8_t)j;
+        P.hkind[h] = 2;
+        P.hdim[h++] = (int8_t)j;
+    }
+    const int sd = std::max(1, std::min<int>(spatial, std::min(d, 3)));
+    const int nd = kPtHull - h;
+    for (int k = 0; k < nd; ++k, ++h) {
+        double u[3] = {0.0, 0.0, 0.0};
+        if (sd == 3) {
+            const double z = 1.0 - (2.0 * k + 1.0) / nd, r = std::sqrt(std::max(0.0, 1.0 - z * z));
+            const double phi = k * 2.399963229728653;  // the golden angle
+            u[0] = r * std::cos(phi);
+            u[1] = r * std::sin(phi);
+            u[2] = z;
+        } else if (sd == 2) {
+            const double a = 2.0 * M_PI * (k + 0.5) / nd;
+            u[0] = std::cos(a);
+            u[1] = std::sin(a);
+        } else {
+            u[0] = (k & 1) ? 1.0 : -1.0;
+        }
+        P.hkind[h] = 0;
+        P.hdim[h] = 0;
+        for (int j = 0; j < 3; ++j) P.hdir[h][j] = (float)u[j];
+    }
+    P.n_hull = h;
     return P;
 }
 
@@ -1817,7 +1613,7 @@ void PointTree::inc_reserve(int64_t c, int32_t d) {
     if (c <= icap && d == idim) return;
     hip_check(hipDeviceSynchronize(), "sync");  // the old buffers may still be in use
     for (void *p : {(void *)ikeys[0], (void *)ikeys[1], (void *)iids[0], (void *)iids[1], (void *)ipts[0],
-                    (void *)ipts[1], (void *)inkeys, (void *)invals, (void *)iqorder, itemp})
+                    (void *)ipts[1], (void *)inkeys, (void *)invals, itemp, (void *)ihull_pts})
         if (p) hip_check(hipFree(p), "free");
     c = std::max<int64_t>(c, 1024);
     for (int b = 0; b < 2; ++b) {
@@ -1827,7 +1623,11 @@ void PointTree::inc_reserve(int64_t c, int32_t d) {
     }
     hip_check(hipMalloc(&inkeys, sizeof(uint64_t) * c), "inc new keys");
     hip_check(hipMalloc(&invals, sizeof(int32_t) * c), "inc new rows");
-    hip_check(hipMalloc(&iqorder, sizeof(int32_t) * kPtIncSeg), "inc query order");
+    hip_check(hipMalloc(&ihull_pts, sizeof(double) * kPtHull * d), "inc seed rows");
+    if (!ihull_keys) {
+        hip_check(hipMalloc(&ihull_keys, sizeof(unsigned long long) * kPtHull), "inc seed keys");
+        hip_check(hipMalloc(&ihull_ids, sizeof(int32_t) * kPtHull), "inc seed ids");
+    }
     if (!ickeys) {
         hip_check(hipMalloc(&ickeys, sizeof(uint64_t) * kPtIncSeg), "inc chunk keys");
         hip_check(hipMalloc(&icvals, sizeof(int32_t) * kPtIncSeg), "inc chunk rows");
@@ -1852,7 +1652,7 @@ void PointTree::inc_reserve(int64_t c, int32_t d) {
 }
 
 PtIncJob PointTree::prepare_inc(const double *pts, int64_t n_upper, const int64_t *n_dev, int32_t d, const double *lo,
-                                const double *hi, const double *q, int64_t nq, bool full, hipStream_t stream,
+                                const double *hi, int32_t spatial, bool full, hipStream_t stream,
                                 const SpreadOut *spread) {
     if (d != 3 && d != 7 && d != 15) throw Error{1, "point tree: state dim must be 3, 7 or 15"};
     if (n_upper < 1 || n_upper >= (int64_t(1) << 27)) throw Error{1, "point tree: bad point count"};
@@ -1864,7 +1664,7 @@ PtIncJob PointTree::prepare_inc(const double *pts, int64_t n_upper, const int64_
     bool same = iplan_set;
     for (int j = 0; j < d && same; ++j) same = iplan_lo[j] == lo[j] && iplan_hi[j] == hi[j];
     if (!same) {
-        const IncPlan P = make_inc_plan(d, lo, hi);
+        const IncPlan P = make_inc_plan(d, lo, hi, spatial);
         hip_check(hipMemcpy(iplan, &P, sizeof(P), hipMemcpyHostToDevice), "inc plan");
         for (int j = 0; j < d; ++j) {
             iplan_lo[j] = lo[j];
@@ -1875,14 +1675,16 @@ PtIncJob PointTree::prepare_inc(const double *pts, int64_t n_upper, const int64_
     }
     const int old = icur, nw = icur ^ 1;
     if (full) {
-        // every point: box, codes, one radix sort into the new-point arrays; the old arrays
-        // are scratch (the merge reads no old point)
+        // every point: box, codes and seed offers, one radix sort into the new-point arrays; the
+        // old arrays are scratch (the merge reads no old point)
         hipLaunchKernelGGL(k_pt_inc_box_reset, dim3(1), dim3(64), 0, stream, ibox);
+        hip_check(hipMemsetAsync(ihull_keys, 0, sizeof(unsigned long long) * kPtHull, stream), "seed reset");
         hipLaunchKernelGGL(d == 3 ? k_pt_inc_bbox<3> : d == 7 ? k_pt_inc_bbox<7> : k_pt_inc_bbox<15>, dim3(64),
                            dim3(256), 0, stream, pts, d, n_upper, n_dev, ibox);
         const unsigned blocks = (unsigned)((n_upper + 255) / 256);
         hipLaunchKernelGGL(d == 3 ? k_pt_inc_codes<3> : d == 7 ? k_pt_inc_codes<7> : k_pt_inc_codes<15>, dim3(blocks),
-                           dim3(256), 0, stream, pts, n_upper, n_dev, (const IncPlan *)iplan, ikeys[old], iids[old]);
+                           dim3(64 * kHullWaves), 0, stream, pts, n_upper, n_dev, (const IncPlan *)iplan, ikeys[old],
+                           iids[old], ihull_keys);
         hip_check(hipGetLastError(), "k_pt_inc_codes");
         size_t tb = itemp_bytes;
         hip_check(hipcub::DeviceRadixSort::SortPairs(itemp, tb, ikeys[old], inkeys, iids[old], invals, (int)n_upper, 0,
@@ -1896,11 +1698,9 @@ PtIncJob PointTree::prepare_inc(const double *pts, int64_t n_upper, const int64_
     t.boxes = boxes;
     t.pts = ipts[nw];
     t.ids = iids[nw];
+    t.hull_pts = ihull_pts;
+    t.hull_ids = ihull_ids;
     icur = nw;
-    // MPT_PT_QSORT=1: the queries in code order.  Measured slower (config 5, 32 seeds: joint
-    // NN 2.02 -> 2.70 ms for the same points and boxes examined), so sample order is the default
-    static const bool qsort = getenv("MPT_PT_QSORT") && atoi(getenv("MPT_PT_QSORT")) == 1;
-    iq_on = qsort && q && nq > 0 && nq <= kPtIncSeg;
     PtIncJob J{};
     J.T = t;
     J.pts = pts;
@@ -1919,13 +1719,10 @@ PtIncJob PointTree::prepare_inc(const double *pts, int64_t n_upper, const int64_
     J.npos = inpos;
     J.nidx = inidx;
     J.ibox = ibox;
-    J.q = iq_on ? q : nullptr;
-    J.nq = iq_on ? nq : 0;
-    J.qorder = iqorder;
-    static const bool dbg = getenv("MPT_SORT_DBG") && atoi(getenv("MPT_SORT_DBG")) == 1;
-    static unsigned long long *dbg_buf = nullptr;
-    if (dbg && !dbg_buf) hip_check(hipMalloc(&dbg_buf, sizeof(unsigned long long) * 8 * 4096), "sort dbg");
-    J.dbg = dbg ? dbg_buf : nullptr;
+    J.err = nullptr;
+    J.hull_keys = ihull_keys;
+    J.hull_pts = ihull_pts;
+    J.hull_ids = ihull_ids;
     J.full = full ? 1 : 0;
     if (spread) J.sp = *spread;
     return J;
@@ -1935,61 +1732,24 @@ void launch_tree_inc_jobs(const PtIncJob *d_jobs, const PtIncJob *h_jobs, int32_
     if (n <= 0) return;
     // one job: passed in the kernel arguments (no staged table)
     IncJobs js{n == 1 ? nullptr : d_jobs, h_jobs[0]};
-    static const bool dbg = getenv("MPT_SORT_DBG") && atoi(getenv("MPT_SORT_DBG")) == 1;
-    if (dbg && h_jobs[0].dbg) hip_check(hipMemsetAsync(h_jobs[0].dbg, 0, sizeof(unsigned long long) * 8 * n, stream), "dbg");
     int64_t max_n = 0;
     for (int32_t j = 0; j < n; ++j) max_n = std::max(max_n, h_jobs[j].T.n_upper);
     auto by_d = [&](auto k3, auto k7, auto k15) { return d == 3 ? k3 : d == 7 ? k7 : k15; };
     if (d != 3 && d != 7 && d != 15) throw Error{1, "point tree: state dim must be 3, 7 or 15"};
-    // the chunked sort (config 5 builds, 32 / 64 / 256 trees: 0.366 / 0.545 / 1.759 ms with
-    // the one-workgroup sort, 0.297 / 0.515 / 1.761 ms chunked).  MPT_PT_CSORT=0: the former
-    static const bool csort = !(getenv("MPT_PT_CSORT") && atoi(getenv("MPT_PT_CSORT")) == 0);
-    bool any_q = false;
-    for (int32_t j = 0; j < n; ++j) any_q = any_q || h_jobs[j].q;
-    if (csort) {
-        hipLaunchKernelGGL(by_d(k_pt_inc_ncodes<3>, k_pt_inc_ncodes<7>, k_pt_inc_ncodes<15>),
-                           dim3(kPtIncSeg / 256, n), dim3(256), 0, stream, js);
-        hip_check(hipGetLastError(), "k_pt_inc_ncodes");
-        hipLaunchKernelGGL(k_pt_inc_csort, dim3(kIncChunks / kIncChunkWaves, n), dim3(64 * kIncChunkWaves), 0, stream,
-                           js);
-        hip_check(hipGetLastError(), "k_pt_inc_csort");
-        hipLaunchKernelGGL(k_pt_inc_crank, dim3(kPtIncSeg / 256, n), dim3(256), 0, stream, js);
-        hip_check(hipGetLastError(), "k_pt_inc_crank");
-    }
-    if (!csort || any_q) {
-        // blockIdx.x + seg0: 0 = the new points, 1 = the queries
-        hipLaunchKernelGGL(by_d(k_pt_inc_sort<3>, k_pt_inc_sort<7>, k_pt_inc_sort<15>), dim3(csort ? 1 : 2, n),
-                           dim3(kIncSortThreads), 0, stream, js, csort ? 1 : 0);
-        hip_check(hipGetLastError(), "k_pt_inc_sort");
-    }
-    if (dbg && h_jobs[0].dbg) {
-        std::vector<unsigned long long> h((size_t)8 * n);
-        hip_check(hipStreamSynchronize(stream), "dbg sync");
-        hip_check(hipMemcpy(h.data(), h_jobs[0].dbg, sizeof(unsigned long long) * 8 * n, hipMemcpyDeviceToHost), "dbg");
-        double ph[4] = {0, 0, 0, 0}, t0 = 1e300, t1 = 0;
-        int cnt = 0;
-        for (int j = 0; j < n; ++j) {
-            const unsigned long long *e = &h[(size_t)8 * j];
-            if (!e[0] || !e[4]) continue;
-            ++cnt;
-            for (int k = 0; k < 4; ++k) ph[k] += (double)(e[k + 1] - e[k]);
-            t0 = std::min(t0, (double)e[0]);
-            t1 = std::max(t1, (double)e[4]);
-        }
-        // s_memrealtime ticks at 100 MHz
-        if (cnt)
-            fprintf(stderr, "[sort dbg] %d trees: plan %.1f us, codes %.1f us, sort %.1f us, out %.1f us; span %.1f us\n",
-                    cnt, ph[0] / cnt * 0.01, ph[1] / cnt * 0.01, ph[2] / cnt * 0.01, ph[3] / cnt * 0.01, (t1 - t0) * 0.01);
-    }
-    // MPT_PT_MERGE2=0: the merge-path form for every job (A/B)
-    static const bool merge2 = !(getenv("MPT_PT_MERGE2") && atoi(getenv("MPT_PT_MERGE2")) == 0);
-    if (merge2) {
-        hipLaunchKernelGGL(k_pt_inc_npos, dim3(kPtIncSeg / 256, n), dim3(256), 0, stream, js);
-        hip_check(hipGetLastError(), "k_pt_inc_npos");
-    }
+    // the new points' chunked sort (config 5 builds, 32 / 64 / 256 trees: 0.366 / 0.545 / 1.759
+    // ms with the former one-workgroup sort, 0.297 / 0.515 / 1.761 ms chunked): codes and seed
+    // offers, 512-pair chunks a wave, ranks across chunks
+    hipLaunchKernelGGL(by_d(k_pt_inc_ncodes<3>, k_pt_inc_ncodes<7>, k_pt_inc_ncodes<15>),
+                       dim3(kPtIncSeg / (64 * kHullWaves), n), dim3(64 * kHullWaves), 0, stream, js);
+    hip_check(hipGetLastError(), "k_pt_inc_ncodes");
+    hipLaunchKernelGGL(k_pt_inc_csort, dim3(kIncChunks / kIncChunkWaves, n), dim3(64 * kIncChunkWaves), 0, stream, js);
+    hip_check(hipGetLastError(), "k_pt_inc_csort");
+    hipLaunchKernelGGL(k_pt_inc_crank, dim3(kPtIncSeg / 256, n), dim3(256), 0, stream, js);
+    hip_check(hipGetLastError(), "k_pt_inc_crank");
+    hipLaunchKernelGGL(k_pt_inc_npos, dim3(kPtIncSeg / 256, n), dim3(256), 0, stream, js);
+    hip_check(hipGetLastError(), "k_pt_inc_npos");
     hipLaunchKernelGGL(by_d(k_pt_inc_merge<3>, k_pt_inc_merge<7>, k_pt_inc_merge<15>),
-                       dim3((unsigned)((max_n + kIncTile - 1) / kIncTile), n), dim3(kIncTile), 0, stream, js,
-                       merge2 ? 1 : 0);
+                       dim3((unsigned)((max_n + kIncTile - 1) / kIncTile), n), dim3(kIncTile), 0, stream, js);
     hip_check(hipGetLastError(), "k_pt_inc_merge");
     const int64_t groups = (max_n + kPtChunkLeaves * kPtFan - 1) / (kPtChunkLeaves * kPtFan);
     hipLaunchKernelGGL(k_pt_inc_boxes, dim3((unsigned)groups, n), dim3(256), 0, stream, js);
@@ -2011,38 +1771,26 @@ void launch_tree_radius(const PointTreeDev &T, const double *q, int64_t nq, doub
     hip_check(hipGetLastError(), "k_tree_radius launch");
 }
 
-template <int BS, int W>
-static void launch_tree_nn1_bs(const PointTreeDev &T, const double *q, int64_t nq, int32_t *ids, double *d2,
-                               hipStream_t stream, const int32_t *order) {
+template <int W>
+static void launch_tree_nn1_w(const PointTreeDev &T, const double *q, int64_t nq, int32_t *ids, double *d2,
+                              hipStream_t stream) {
+    constexpr int BS = 64;  // one-wave workgroups spread an engine round's few thousand queries over all CUs
     const dim3 grid((unsigned)((nq * kPtFan * W + BS - 1) / BS));
     switch (T.d) {
-        case 3: hipLaunchKernelGGL((k_tree_nn1<3, BS, W>), grid, dim3(BS), 0, stream, T, q, nq, ids, d2, order); break;
-        case 7: hipLaunchKernelGGL((k_tree_nn1<7, BS, W>), grid, dim3(BS), 0, stream, T, q, nq, ids, d2, order); break;
-        case 15: hipLaunchKernelGGL((k_tree_nn1<15, BS, W>), grid, dim3(BS), 0, stream, T, q, nq, ids, d2, order); break;
+        case 3: hipLaunchKernelGGL((k_tree_nn1<3, BS, W>), grid, dim3(BS), 0, stream, T, q, nq, ids, d2); break;
+        case 7: hipLaunchKernelGGL((k_tree_nn1<7, BS, W>), grid, dim3(BS), 0, stream, T, q, nq, ids, d2); break;
+        case 15: hipLaunchKernelGGL((k_tree_nn1<15, BS, W>), grid, dim3(BS), 0, stream, T, q, nq, ids, d2); break;
         default: throw Error{1, "point tree: state dim must be 3, 7 or 15"};
     }
     hip_check(hipGetLastError(), "k_tree_nn1 launch");
 }
 
-void launch_tree_nn1(const PointTreeDev &T, const double *q, int64_t nq, int32_t *ids, double *d2, hipStream_t stream,
-                     const int32_t *order) {
+void launch_tree_nn1(const PointTreeDev &T, const double *q, int64_t nq, int32_t *ids, double *d2, hipStream_t stream) {
     if (nq <= 0) return;
-    // one-wave workgroups spread an engine round's few thousand queries over all CUs
-    // (MPT_PT_NN1_BLOCK=256: four waves per workgroup; A/B knob)
-    static const int bs = getenv("MPT_PT_NN1_BLOCK") ? atoi(getenv("MPT_PT_NN1_BLOCK")) : 64;
-    // nodes expanded per step: as the joint launch (MPT_PT_NN_W forces one)
-    static const int w_env = getenv("MPT_PT_NN_W") ? atoi(getenv("MPT_PT_NN_W")) : 0;
-    const int w = w_env > 0 ? w_env : pt_nn_width(T.d, nq);
-    if (bs == 256)
-        w == 1 ? launch_tree_nn1_bs<256, 1>(T, q, nq, ids, d2, stream, order)
-               : (w == 2 ? launch_tree_nn1_bs<256, 2>(T, q, nq, ids, d2, stream, order)
-                         : (w == 4 ? launch_tree_nn1_bs<256, 4>(T, q, nq, ids, d2, stream, order)
-                                   : launch_tree_nn1_bs<256, 8>(T, q, nq, ids, d2, stream, order)));
-    else
-        w == 1 ? launch_tree_nn1_bs<64, 1>(T, q, nq, ids, d2, stream, order)
-               : (w == 2 ? launch_tree_nn1_bs<64, 2>(T, q, nq, ids, d2, stream, order)
-                         : (w == 4 ? launch_tree_nn1_bs<64, 4>(T, q, nq, ids, d2, stream, order)
-                                   : launch_tree_nn1_bs<64, 8>(T, q, nq, ids, d2, stream, order)));
+    const int w = pt_nn_width(T.d, nq);
+    if (w == 8) launch_tree_nn1_w<8>(T, q, nq, ids, d2, stream);
+    else if (w == 4) launch_tree_nn1_w<4>(T, q, nq, ids, d2, stream);
+    else launch_tree_nn1_w<1>(T, q, nq, ids, d2, stream);
 }
 
 template <int BS, int W>
@@ -2066,13 +1814,11 @@ void launch_tree_nn1_jobs(const PtJob *d_jobs, int32_t n_jobs, int32_t d, int64_
     // point and the ranks skipped on steps without a survivor, the widest walk wins at every
     // size: config 5 round time by nodes a step (1 / 2 / 4 / 8), 32 seeds (131 072 queries)
     // - / - / 1.86 / 1.59 ms, 64 seeds - / - / 3.36 / 2.97 ms, 256 seeds (1 M queries) 12.83 /
-    // 12.53 / 11.26 / 10.80 ms.  MPT_PT_NN_W = 1 / 2 / 4 / 8 forces one (A/B).
-    static const int w_env = getenv("MPT_PT_NN_W") ? atoi(getenv("MPT_PT_NN_W")) : 0;
-    const int w = w_env > 0 ? w_env : pt_nn_width(d, (int64_t)n_jobs * nq);
-    if (w == 1) launch_tree_nn1_jobs_bs<64, 1>(d_jobs, n_jobs, d, nq, stream);
+    // 12.53 / 11.26 / 10.80 ms (round 3, before the seeds).
+    const int w = pt_nn_width(d, (int64_t)n_jobs * nq);
+    if (w == 8) launch_tree_nn1_jobs_bs<64, 8>(d_jobs, n_jobs, d, nq, stream);
     else if (w == 4) launch_tree_nn1_jobs_bs<64, 4>(d_jobs, n_jobs, d, nq, stream);
-    else if (w == 8) launch_tree_nn1_jobs_bs<64, 8>(d_jobs, n_jobs, d, nq, stream);
-    else launch_tree_nn1_jobs_bs<64, 2>(d_jobs, n_jobs, d, nq, stream);
+    else launch_tree_nn1_jobs_bs<64, 1>(d_jobs, n_jobs, d, nq, stream);
 }
 
 }  // namespace mpt

@@ -901,21 +901,14 @@ struct StepCtx {
     }
 };
 
-// the Morton-tree NN index is updated incrementally (MPT_PT_INC=0: rebuilt from scratch every
-// round with the live box's code plan, A/B)
-bool tree_incremental() {
-    static const bool inc = !getenv("MPT_PT_INC") || atoi(getenv("MPT_PT_INC")) != 0;
-    return inc;
-}
-
 // this round's incremental tree build (a full rebuild when the index is stale or more nodes
-// were appended since its last build than one round's sort holds); the queries (the round's
-// samples) are ordered by code for the NN launch
-PtIncJob tree_inc_job(mpt_rrt *r, int32_t K, hipStream_t stream, const SpreadOut *spread,
-                      const double *samples = nullptr) {
+// were appended since its last build than one round's merge takes: the host's bound, which the
+// build's first kernel checks on the device into counters[6])
+PtIncJob tree_inc_job(mpt_rrt *r, hipStream_t stream, const SpreadOut *spread) {
     const bool full = !r->pt_inc_ok || r->pt_grow > kPtIncSeg;
-    PtIncJob J = r->ptree->prepare_inc(r->d_nodes, r->n_upper, r->d_n, r->p.d, r->p.lo, r->p.hi,
-                                       samples ? samples : r->d_samples, K, full, stream, spread);
+    PtIncJob J = r->ptree->prepare_inc(r->d_nodes, r->n_upper, r->d_n, r->p.d, r->p.lo, r->p.hi, r->grid_gd, full,
+                                       stream, spread);
+    J.err = r->d_counters + 6;
     r->pt_inc_ok = true;
     r->pt_grow = 0;
     return J;
@@ -1032,18 +1025,14 @@ StepCtx step_head(mpt_rrt *r, int32_t K, hipStream_t stream, bool defer_tree = f
     SpreadOut spread;
     const bool want_spread = spread_request(r, use_tree || use_grid, spread);
     if (use_tree) {
-        // once: no allocation (device sync) in later rounds
-        if (tree_incremental()) r->ptree->inc_reserve(r->cap, p.d);
-        else r->ptree->reserve(r->cap, p.d);
+        r->ptree->inc_reserve(r->cap, p.d);  // once: no allocation (device sync) in later rounds
         if (defer_tree) {
             c.defer_tree = true;
             c.want_spread = want_spread;
             c.spread = spread;
-        } else if (tree_incremental()) {
-            PtIncJob J = tree_inc_job(r, K, stream, want_spread ? &spread : nullptr);
-            launch_tree_inc_jobs(nullptr, &J, 1, p.d, stream);
         } else {
-            r->ptree->build(r->d_nodes, r->n_upper, r->d_n, p.d, stream, want_spread ? &spread : nullptr);
+            PtIncJob J = tree_inc_job(r, stream, want_spread ? &spread : nullptr);
+            launch_tree_inc_jobs(nullptr, &J, 1, p.d, stream);
         }
     } else if (use_grid) {
         // spatial dims of the agent's tree state: x, y, z (omni, blimp) or x, y (snake);
@@ -1097,12 +1086,10 @@ StepCtx step_head(mpt_rrt *r, int32_t K, hipStream_t stream, bool defer_tree = f
 }
 
 // a deferred tree build that did not join a joint build: run it on the engine's stream
-void build_deferred(mpt_rrt *r, int32_t K, hipStream_t stream, const StepCtx &c) {
-    if (tree_incremental()) {
-        PtIncJob J = tree_inc_job(r, K, stream, c.want_spread ? &c.spread : nullptr);
+void build_deferred(mpt_rrt *r, hipStream_t stream, const StepCtx &c) {
+    {
+        PtIncJob J = tree_inc_job(r, stream, c.want_spread ? &c.spread : nullptr);
         launch_tree_inc_jobs(nullptr, &J, 1, r->p.d, stream);
-    } else {
-        r->ptree->build(r->d_nodes, r->n_upper, r->d_n, r->p.d, stream, c.want_spread ? &c.spread : nullptr);
     }
     if (c.want_spread) hip_check(hipEventRecord(r->ev_spread, stream), "spread event");
     c.mark(2, stream);
@@ -1114,8 +1101,7 @@ void step_nn(mpt_rrt *r, int32_t K, hipStream_t stream, const StepCtx &c) {
     if (use_tree) {
         PointTreeDev T = r->ptree->dev();
         T.stats = r->stats_on ? r->d_cstats + 8 : nullptr;
-        launch_tree_nn1(T, r->d_samples, K, r->d_nn, r->d_nnd2, stream,
-                        tree_incremental() ? r->ptree->query_order() : nullptr);
+        launch_tree_nn1(T, r->d_samples, K, r->d_nn, r->d_nnd2, stream);
     } else if (use_grid) {
         GridDev G = r->grid->dev();
         G.stats = r->stats_on ? r->d_cstats + 8 : nullptr;
@@ -1223,7 +1209,6 @@ struct JointNN {
     // engine timing on: b0 -> t0 = the joint tree build, t0 -> t1 = the joint NN launch
     hipEvent_t b0 = nullptr, t0 = nullptr, t1 = nullptr;
     bool timed = false;
-    JointTreeScratch trees;  // shared sort buffers of the joint tree build
     // joint rounds (joint_round): the engines' round buffers, engine j at edge offset j * K
     int64_t r_edges = 0, r_units = 0;
     int32_t r_dim = 0, r_subs = 0;
@@ -1297,7 +1282,7 @@ void joint_free_round(JointNN &g) {
 // append's 16-byte verdict loads).  MPT_JOINT_ROUND=0: per-engine heads and tails (A/B).
 bool joint_round_ok(mpt_rrt *const *rs, int32_t n, int32_t K) {
     static const bool on = !getenv("MPT_JOINT_ROUND") || atoi(getenv("MPT_JOINT_ROUND")) != 0;
-    if (!on || n < 2 || K < 16 || K % 16 != 0 || !tree_incremental() || collide_mode() == MPT_COLLIDE_FUSED)
+    if (!on || n < 2 || K < 16 || K % 16 != 0 || collide_mode() == MPT_COLLIDE_FUSED)
         return false;
     const mpt_rrt *a = rs[0];
     const EngineParams &p = a->p;
@@ -1435,11 +1420,10 @@ void joint_round(mpt_rrt *const *rs, int32_t n, int32_t K, void *const *streams_
     // samples' launch applied any truncation) and the NN jobs
     for (int32_t i = 0; i < n; ++i) {
         mpt_rrt *r = rs[i];
-        hi[i] = tree_inc_job(r, K, joint, want[i] ? &spreads[i] : nullptr, g.j_samples + (int64_t)i * K * d);
+        hi[i] = tree_inc_job(r, joint, want[i] ? &spreads[i] : nullptr);
         PointTreeDev T = r->ptree->dev();
         T.stats = nullptr;
-        hn[i] = PtJob{T, g.j_samples + (int64_t)i * K * d, g.j_nn + (int64_t)i * K, g.j_nnd2 + (int64_t)i * K,
-                      r->ptree->query_order()};
+        hn[i] = PtJob{T, g.j_samples + (int64_t)i * K * d, g.j_nn + (int64_t)i * K, g.j_nnd2 + (int64_t)i * K};
     }
     hip_check(hipMemcpyAsync(g.d_stage + b_eng, h + b_eng, b_inc + b_nn, hipMemcpyHostToDevice, joint), "jobs H2D");
     hip_check(hipEventRecord(g.copied[slot], joint), "jobs copied");
@@ -1542,25 +1526,16 @@ extern "C" mpt_status mpt_rrt_step_many(mpt_rrt *const *rs, int32_t n, int32_t K
         std::vector<char> joined(n, 0);
         for (int32_t i : J) joined[i] = 1;
         for (int32_t i = 0; i < n; ++i)
-            if (cs[i].defer_tree && !joined[i]) build_deferred(rs[i], K, stream_of(i), cs[i]);
+            if (cs[i].defer_tree && !joined[i]) build_deferred(rs[i], stream_of(i), cs[i]);
         if (!J.empty()) {
             JointNN &g = joint_state(joint);
             std::lock_guard<std::mutex> lk(g.mu);
             const int32_t nj = (int32_t)J.size();
-            const bool inc = tree_incremental();
-            // the shared sort buffers sized for the joined trees' capacities once, so no later
-            // round allocates (an allocation synchronises the device and stalls every stream)
-            int64_t cap_total = 0;
-            for (int32_t i : J) cap_total += rs[i]->cap;
-            if (!inc) reserve_tree_build_jobs(g.trees, cap_total, nj);
-            const size_t b_build = (inc ? sizeof(PtIncJob) : sizeof(PtBuildJob)) * nj, b_nn = sizeof(PtJob) * nj;
-            const size_t b_off = sizeof(int32_t) * (nj + 1);
+            const size_t b_build = sizeof(PtIncJob) * nj, b_nn = sizeof(PtJob) * nj;
             int slot = 0;
-            char *h = joint_stage(g, b_build + b_nn + b_off, &slot);
-            PtBuildJob *hb = reinterpret_cast<PtBuildJob *>(h);
+            char *h = joint_stage(g, b_build + b_nn, &slot);
             PtIncJob *hi = reinterpret_cast<PtIncJob *>(h);
             PtJob *hn = reinterpret_cast<PtJob *>(h + b_build);
-            int32_t *ho = reinterpret_cast<int32_t *>(h + b_build + b_nn);
             // the joint stream waits for every engine stream's heads, the engines' tails for it
             // (before the builds: a full incremental rebuild issues its launches here)
             std::vector<hipStream_t> uniq;
@@ -1585,29 +1560,19 @@ extern "C" mpt_status mpt_rrt_step_many(mpt_rrt *const *rs, int32_t n, int32_t K
                 }
                 hip_check(hipEventRecord(g.b0, joint), "joint b0");
             }
-            int64_t total = 0;
             for (int32_t k = 0; k < nj; ++k) {
                 mpt_rrt *r = rs[J[k]];
                 const StepCtx &c = cs[J[k]];
-                ho[k] = (int32_t)total;
-                const SpreadOut *sp = c.want_spread ? &c.spread : nullptr;
-                if (inc) hi[k] = tree_inc_job(r, K, joint, sp);
-                else hb[k] = r->ptree->prepare(r->d_nodes, r->n_upper, r->d_n, r->p.d, total, sp);
-                total += r->n_upper;
-                if (total >= (int64_t(1) << 31)) throw Error{MPT_ERR_INVALID, "joint build: too many points"};
+                hi[k] = tree_inc_job(r, joint, c.want_spread ? &c.spread : nullptr);
                 PointTreeDev T = r->ptree->dev();
                 T.stats = r->stats_on ? r->d_cstats + 8 : nullptr;
-                hn[k] = PtJob{T, r->d_samples, r->d_nn, r->d_nnd2, inc ? r->ptree->query_order() : nullptr};
+                hn[k] = PtJob{T, r->d_samples, r->d_nn, r->d_nnd2};
             }
-            ho[nj] = (int32_t)total;
-            hip_check(hipMemcpyAsync(g.d_stage, h, b_build + b_nn + b_off, hipMemcpyHostToDevice, joint), "jobs H2D");
+            hip_check(hipMemcpyAsync(g.d_stage, h, b_build + b_nn, hipMemcpyHostToDevice, joint), "jobs H2D");
             hip_check(hipEventRecord(g.copied[slot], joint), "jobs copied");
-            const PtBuildJob *db = reinterpret_cast<const PtBuildJob *>(g.d_stage);
             const PtIncJob *di = reinterpret_cast<const PtIncJob *>(g.d_stage);
             const PtJob *dn = reinterpret_cast<const PtJob *>(g.d_stage + b_build);
-            const int32_t *doff = reinterpret_cast<const int32_t *>(g.d_stage + b_build + b_nn);
-            if (inc) launch_tree_inc_jobs(di, hi, nj, rs[J[0]]->p.d, joint);
-            else launch_tree_build_jobs(db, hb, nj, rs[J[0]]->p.d, doff, total, g.trees, joint);
+            launch_tree_inc_jobs(di, hi, nj, rs[J[0]]->p.d, joint);
             for (int32_t i : J)
                 if (cs[i].want_spread) hip_check(hipEventRecord(rs[i]->ev_spread, joint), "spread event");
             if (timed) {
@@ -1701,9 +1666,6 @@ extern "C" mpt_status mpt_rrt_joint_release(void *joint_stream) {
         for (hipEvent_t e : g->joins) hip_check(hipEventDestroy(e), "event");
         for (hipEvent_t e : {g->done, g->built, g->b0, g->t0, g->t1})
             if (e) hip_check(hipEventDestroy(e), "event");
-        JointTreeScratch &S = g->trees;
-        for (void *p : {(void *)S.keys, (void *)S.keys_sorted, (void *)S.vals, (void *)S.vals_sorted, S.temp})
-            if (p) hip_check(hipFree(p), "free");
         joint_free_round(*g);
         for (hipEvent_t e : g->st)
             if (e) hip_check(hipEventDestroy(e), "event");
@@ -1717,6 +1679,7 @@ extern "C" mpt_status mpt_rrt_counters(mpt_rrt *r, uint64_t c[8]) {
         unsigned long long h[8];
         hip_check(hipMemcpy(h, r->d_counters, sizeof(h), hipMemcpyDeviceToHost), "counters");
         for (int i = 0; i < 8; ++i) c[i] = h[i];
+        if (h[6]) throw Error{MPT_ERR_INTERNAL, "incremental tree index: a build found more new points than it merges"};
     });
 }
 
