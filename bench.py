@@ -198,7 +198,7 @@ def _cpu_model():
 STAGE_KERNEL = {"nn_query": "k_grid_nn1_runs", "collide_pairs": "k_pairs", "collide_cands": "k_cands",
                 "collide_narrow": "k_narrow", "nn_build": "k_grid_scatter", "steer": "k_steer",
                 "sample": "k_sample", "append": "k_append"}
-NN_KERNEL = {"grid": "k_grid_nn1_runs", "tree": "k_tree_nn1", "brute": "k_knn1"}
+NN_KERNEL = {"grid": "k_grid_nn1_runs", "tree": "k_ct_nn1", "brute": "k_knn1"}
 
 
 def geometry(sc, env):
@@ -211,14 +211,16 @@ def geometry(sc, env):
 
 
 def inc_build_bytes(n, m, d):
-    """The incremental Morton-tree build of trees holding n points in total after it, m of them
-    new this round (point_tree.hip): the sort reads the new rows and writes their (code, row)
-    pairs; the merge reads the old sorted (code, id, row) records and the new pairs and rows,
-    and writes n sorted records and the leaf boxes; the box levels above read and write the
-    boxes (about n / 7 boxes of 2d floats in all).  The chunked sort's intermediate passes over
-    the m pairs (chunks, ranks, output places) are the algorithm's, not the minimum's."""
-    rec = 8 + 4 + 8 * d
-    return m * (8 * d + 12) + (n - m) * rec + m * (12 + 8 * d) + n * rec + (n // 7) * 8 * d * 2
+    """The cell tree's round (cell_tree.hip) over trees holding n points in total after it, m
+    of them new: the new rows read and their (code, row) pairs written and read back by the
+    sort; the touched buckets (at most m, 8 slots of row, id and 16-byte code each) read and
+    rewritten; the directory (about n / 4 entries: buckets hold 1..8 points) read and written
+    by the merge; the box levels above it (about n_dir * 8 / 7 nodes of 2d floats, a meta word
+    and a 16-byte code) written once and read once by the level above."""
+    slot = 8 * d + 4 + 16
+    n_dir = n // 4
+    nodes = n_dir * 8 // 7
+    return m * 8 * d + m * 24 * 2 + m * 8 * slot * 2 + n_dir * 20 * 2 + nodes * (8 * d + 4 + 16) * 2
 
 
 def compulsory_bytes(stage, c, K, n0, d, pmax, geo, nn_mode):
@@ -351,9 +353,9 @@ def stage_table(per_launch, cst, K, n0, d, pmax, geo, nn_mode, kernels, summ):
 # measured traffic per launch is summed (the collide chain runs once per collide sub-batch)
 JOINT_STAGE_KERNELS = {
     "sample": ["k_sample_jobs"],
-    "nn_build": ["k_pt_inc_ncodes", "k_pt_inc_csort", "k_pt_inc_crank", "k_pt_inc_npos", "k_pt_inc_merge",
-                 "k_pt_inc_boxes", "k_pt_inc_top"],
-    "nn_query": ["k_tree_nn1_jobs"],
+    "nn_build": ["k_ct_ncodes", "k_ct_csort", "k_ct_crank", "k_ct_locate", "k_ct_segments", "k_ct_apply",
+                 "k_ct_split_flags", "k_ct_split_scan", "k_ct_split_fill", "k_ct_dmerge", "k_ct_levels"],
+    "nn_query": ["k_ct_nn1_jobs"],
     "steer": ["k_steer_jobs"],
     "collide": ["k_pairs<", "k_scan_excl<mpt::ExpandHeaders", "k_cands", "k_narrow", "k_overflow"],
     "append": ["k_append_jobs"],
@@ -395,6 +397,7 @@ def joint_stage_table(times, c, K, nj, n_tot, d, pmax, geo, summ):
             # boxes tested per query
             st["nn_points_per_query"] = round(c["nn_points"] / (K * nj), 2)
             st["nn_boxes_per_query"] = round(c["nn_cells"] / (K * nj), 2)
+            st["nn_steps_per_query"] = round(c.get("nn_steps", 0) / (K * nj), 2)
         trs = [pmc_traffic(summ, k) for k in JOINT_STAGE_KERNELS.get(s, [])]
         if trs and all(x is not None for x in trs):
             tr = sum(trs) * (n_sub if s == "collide" else 1)
@@ -578,7 +581,7 @@ def run_seeds(args, world, rank, dist, torch, mpt, multiseed, scenes):
         nn_mode = e0.last_nn()
         kernels = dict(STAGE_KERNEL, nn_query=NN_KERNEL.get(nn_mode, "k_grid_nn1_runs"))
         if nn_mode == "tree":
-            kernels["nn_build"] = "k_pt_inc_merge"
+            kernels["nn_build"] = "k_ct_dmerge"
         stages = stage_table(per_launch, cst, K, n_before, sc.dim, pmax, geo, nn_mode, kernels, summ)
         roof = roofline_of(stages, max(stages, key=lambda s: stages[s]["ms"]) if stages else None, cst, summ_path)
     else:
@@ -724,7 +727,7 @@ def condense(d):
     leg["stages"] = {s: {k: v for k, v in st.items()
                          if k in ("ms", "ms_event_free", "frac_hbm_compulsory", "frac_hbm_measured",
                                   "traffic_over_compulsory", "frac_fp64", "kernel", "nn_points_per_query",
-                                  "nn_boxes_per_query")}
+                                  "nn_boxes_per_query", "nn_steps_per_query")}
                      for s, st in (roof.get("stages") or {}).items()}
     return leg
 
@@ -877,7 +880,7 @@ def run_tree(args, world, rank, dist, torch, mpt, multiseed, scenes):
     if nn_mode == "grid":  # the instantiation (its PMC row): queries bucketed by the grid count launch
         kernels["nn_query"] = f"k_grid_nn1_runs_sorted<{d},"
     if nn_mode == "tree":
-        kernels["nn_build"] = "k_pt_inc_merge"
+        kernels["nn_build"] = "k_ct_dmerge"
     summ, summ_path = pmc_summary(args.traffic, args.workload)
     stages = stage_table(per_launch, cst, K, n0, d, eng.info()["pmax"], geometry(sc, env), nn_mode, kernels, summ)
     dominant = max(stages, key=lambda s: stages[s]["ms"]) if stages else None

@@ -260,8 +260,8 @@ mpt_status mpt_rrt_last_nn(const mpt_rrt *rrt, int32_t *mode);
  * out [16] (may be NULL): [0] (pose, link) units, [1] agent clusters past the root cull,
  * [2] env tree node tests, [3] exact triangle tests, [4] (cluster, env triangle) pair tests,
  * [5] units re-run by the fused kernel, [6] agent cluster transforms, [7] broad-phase
- * candidates, [8] grid NN points examined, [9] grid NN cells visited, [10] (unit, cluster)
- * broad-phase threads, [11..15] reserved. */
+ * candidates, [8] NN points examined, [9] NN cells visited (grid) / boxes tested (tree), [10]
+ * (unit, cluster) broad-phase threads, [11] tree NN walk steps (all queries), [12..15] reserved. */
 mpt_status mpt_rrt_collide_stats(mpt_rrt *rrt, int32_t enable, uint64_t out[16]);
 /* hipEvent times (ms) of the last round's stages, after mpt_rrt_enable_timing(1):
  * [sample, nn_build, nn_query, steer, collide_pairs, collide_cands, collide_narrow,

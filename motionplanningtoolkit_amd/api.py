@@ -360,8 +360,8 @@ class RRTEngine:
         out = np.zeros(16, np.uint64)
         check(lib().mpt_rrt_collide_stats(self.handle, 1 if enable else 0, _p(out)), "mpt_rrt_collide_stats")
         names = ["units", "clusters", "node_tests", "tri_tests", "pair_tests", "fused_reruns", "cluster_transforms",
-                 "candidates", "nn_points", "nn_cells", "cluster_threads"]
-        return {k: int(v) for k, v in zip(names, out[:11])}
+                 "candidates", "nn_points", "nn_cells", "cluster_threads", "nn_steps"]
+        return {k: int(v) for k, v in zip(names, out[:12])}
 
     def set_nn(self, mode: str = "auto", points_per_cell: float = 0.0) -> None:
         """NN structure of the rounds: 'auto' | 'brute' | 'grid' | 'tree' (identical results)."""

@@ -57,12 +57,7 @@ struct SplitArgs {
     int32_t *ovf_list;
     int64_t n_seg;
     int32_t pair_cap, cand_cap, spill_cap, n_clusters, n_cwaves;
-    unsigned long long *dbg_ts;  // MPT_PHASE_DBG: per-workgroup phase timestamps (diagnostics only)
 };
-
-__device__ __forceinline__ void phase_ts(unsigned long long *ts, int i) {
-    if (ts && threadIdx.x == 0) ts[(int64_t)blockIdx.x * 8 + i] = __builtin_amdgcn_s_memrealtime();
-}
 
 // wave-uniform item load through the scalar cache (items are read-only in these kernels)
 __device__ __forceinline__ Item load_item_u(const Item *__restrict__ items, int64_t idx) {
@@ -262,7 +257,6 @@ __global__ __launch_bounds__(kPairThreads) void k_pairs(EnvDev env, const AgentD
     __shared__ uint32_t s_pc[kPairThreads / 64], s_hc[kPairThreads / 64], s_live[kPairThreads / 64];
     __shared__ uint4 s_stk[kTwo ? 1 : kPairThreads * kStack];
     __shared__ PairRec s_rec[kPairThreads];
-    phase_ts(a.dbg_ts, 0);
     if (blockIdx.x == 0) {  // stream-ordered resets instead of memset launches
         if (threadIdx.x < 4) a.ctl_next[threadIdx.x] = 0u;
         if (threadIdx.x == 0) a.hdr_count[a.n_seg] = 0u;  // the header scan's sentinel slot
@@ -317,13 +311,9 @@ __global__ __launch_bounds__(kPairThreads) void k_pairs(EnvDev env, const AgentD
             s_rec[base + (uint32_t)__popcll(m & ((1ull << lane) - 1))] = r;
         }
     }
-    phase_ts(a.dbg_ts, 1);
     uint32_t total = 0;
     for (int v = 0; v < kPairThreads / 64; ++v) total += s_live[v];
-    if (a.dbg_ts && threadIdx.x == 0) a.dbg_ts[(int64_t)blockIdx.x * 8 + 5] = total;
     if (total == 0) {  // block-uniform: nothing reaches the env tree
-        phase_ts(a.dbg_ts, 2);
-        phase_ts(a.dbg_ts, 3);
         if (lane == 0 && seg < a.n_seg) {
             a.hdr_count[seg] = 0;
             a.pair_count[seg] = 0;
@@ -348,7 +338,6 @@ __global__ __launch_bounds__(kPairThreads) void k_pairs(EnvDev env, const AgentD
         }
     }
     __syncthreads();
-    phase_ts(a.dbg_ts, 2);
     // 2. the surviving records, packed onto the first waves: walk the env tree; the pair
     //    words and headers carry the (segment, lane) of the thread that walked
     const bool live = threadIdx.x < total;
@@ -381,10 +370,6 @@ __global__ __launch_bounds__(kPairThreads) void k_pairs(EnvDev env, const AgentD
     if (lane == 0 && seg < a.n_seg) {
         a.hdr_count[seg] = s_hc[wave];
         a.pair_count[seg] = s_pc[wave] < (uint32_t)a.pair_cap ? s_pc[wave] : (uint32_t)a.pair_cap;
-    }
-    if (a.dbg_ts) {
-        __syncthreads();
-        phase_ts(a.dbg_ts, 3);
     }
     if (w.stats) {
         uint32_t sum_tests = tests, sum_pairs = np;
@@ -698,9 +683,9 @@ void CollideScratch::ensure(int64_t n_units, int32_t max_clusters) {
         int dev = 0, cus = 256;
         if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
         // k_cands: a resident grid striding over the headers; each header is a chain of
-        // dependent loads, so more waves in flight hide more of it (MPT_CANDS_WAVES_PER_CU: A/B)
-        const char *wpc = getenv("MPT_CANDS_WAVES_PER_CU");
-        const int per_cu = wpc && atoi(wpc) > 0 ? atoi(wpc) : 16;
+        // dependent loads, so more waves in flight hide more of it (8 / 24 a CU measured slower
+        // than 16 at the round-3 head)
+        const int per_cu = 16;
         n_cwaves = cus * per_cu;
         cand_cap = (int32_t)std::max<int64_t>(256, (int64_t)kCandCap * 16 / per_cu);
         spill_cap = kSpillCap;
@@ -720,9 +705,7 @@ void CollideScratch::ensure(int64_t n_units, int32_t max_clusters) {
         void *ps[] = {pairs, hdr, hdr_count, pair_count, hdr_off, hdr_dense};
         for (void *p : ps)
             if (p) hip_check(hipFree(p), "hipFree");
-        // MPT_PAIR_CAP: pair words per k_pairs wave segment (A/B knob)
-        static const int32_t cap_env = getenv("MPT_PAIR_CAP") ? atoi(getenv("MPT_PAIR_CAP")) : 0;
-        pair_cap = cap_env >= 64 ? cap_env : kPairCap;
+        pair_cap = kPairCap;  // pair words per k_pairs wave segment
         // Not kept: each thread's pairs as one contiguous run (staged in LDS, placed after a
         // wave scan) so a k_cands header reads only its own words -- room k_pairs 119 -> 140 us
         // (LDS staging, occupancy), k_cands unchanged (its pair scan was not what bounds it).
@@ -767,26 +750,12 @@ static void collide_split_chunk(const EnvDev &env, const AgentDev *d_links, int3
     // (or at allocation), and this k_pairs zeroes the other half for the next launch
     uint32_t *ctl = s.ctl + 4 * s.ctl_par, *ctl_next = s.ctl + 4 * (1 - s.ctl_par);
     s.ctl_par ^= 1;
-    // MPT_PHASE_DBG=1 (diagnostics only: synchronises after k_pairs and prints its per-workgroup
-    // phase times -- transform + root cull, LDS staging, tree walk -- to stderr)
-    static const bool phase_dbg = getenv("MPT_PHASE_DBG") && atoi(getenv("MPT_PHASE_DBG")) == 1;
-    static unsigned long long *dbg_buf = nullptr;
-    static int64_t dbg_cap = 0;
-    const unsigned pblocks0 = (unsigned)((threads + kPairThreads - 1) / kPairThreads);
-    if (phase_dbg && (int64_t)pblocks0 > dbg_cap) {
-        if (dbg_buf) hip_check(hipFree(dbg_buf), "hipFree");
-        hip_check(hipMalloc(&dbg_buf, sizeof(unsigned long long) * 8 * pblocks0), "alloc phase dbg");
-        dbg_cap = pblocks0;
-    }
     SplitArgs a{s.pairs,  s.hdr,      s.hdr_count, s.pair_count, s.hdr_off, s.hdr_dense, s.cand,    s.cand_count,
                 s.spill,  ctl,        ctl_next,    s.ovf_list,   segs,      s.pair_cap,  s.cand_cap, s.spill_cap,
-                C,        s.n_cwaves, phase_dbg ? dbg_buf : nullptr};
-    if (phase_dbg) hip_check(hipMemsetAsync(dbg_buf, 0, sizeof(unsigned long long) * 8 * pblocks0, stream), "dbg zero");
+                C,        s.n_cwaves};
     const unsigned pblocks = (unsigned)((threads + kPairThreads - 1) / kPairThreads);
     const int32_t n_items = env.lev_off[env.n_levels];
-    // MPT_PAIRS_LDS=0: items read through the caches instead of staged in LDS (A/B knob)
-    static const bool lds_on = !(getenv("MPT_PAIRS_LDS") && atoi(getenv("MPT_PAIRS_LDS")) == 0);
-    const bool lds = lds_on && n_items <= kLdsItems;
+    const bool lds = n_items <= kLdsItems;  // the env's tree items staged in LDS when they fit
     const size_t lds_bytes = lds ? sizeof(Item) * n_items : 0;
     if (env.n_levels <= 2) {
         if (lds)
@@ -804,41 +773,12 @@ static void collide_split_chunk(const EnvDev &env, const AgentDev *d_links, int3
                                w, a);
     }
     hip_check(hipGetLastError(), "k_pairs launch");
-    if (phase_dbg) {
-        hip_check(hipStreamSynchronize(stream), "phase dbg sync");
-        std::vector<unsigned long long> h((size_t)pblocks * 8);
-        hip_check(hipMemcpy(h.data(), dbg_buf, sizeof(unsigned long long) * 8 * pblocks, hipMemcpyDeviceToHost), "dbg");
-        unsigned long long t0 = ~0ull, t1 = 0;
-        double sum[3] = {0, 0, 0}, life = 0, life_live = 0;
-        int64_t nb = 0, nlive = 0;
-        for (unsigned b = 0; b < pblocks; ++b) {
-            const unsigned long long *e = &h[(size_t)b * 8];
-            if (!e[0]) continue;
-            ++nb;
-            t0 = std::min(t0, e[0]);
-            t1 = std::max(t1, e[3]);
-            life += (double)(e[3] - e[0]);
-            if (e[5]) {
-                ++nlive;
-                life_live += (double)(e[3] - e[0]);
-                for (int k = 0; k < 3; ++k) sum[k] += (double)(e[k + 1] - e[k]);
-            }
-        }
-        // s_memrealtime ticks at 100 MHz
-        fprintf(stderr, "[phase k_pairs] blocks %lld (live %lld) span %.1f us, wg life %.2f us (live %.2f us); live: "
-                        "phase1 %.2f us, staging %.2f us, walk %.2f us\n",
-                (long long)nb, (long long)nlive, (t1 - t0) * 0.01, nb ? life / nb * 0.01 : 0.0,
-                nlive ? life_live / nlive * 0.01 : 0.0, nlive ? sum[0] / nlive * 0.01 : 0.0,
-                nlive ? sum[1] / nlive * 0.01 : 0.0, nlive ? sum[2] / nlive * 0.01 : 0.0);
-    }
     mark(0);
     // count slot `segs` is the scan's sentinel (a larger earlier launch may have used it): k_pairs zeroed it
     // one segment per thread: the epilogue writes up to 64 header slots per segment
     launch_scan_excl<1>(s.hdr_scan, s.hdr_count, s.hdr_off, segs + 1, stream, ExpandHeaders{s.hdr_dense, segs});
-    // the env's triangle items in LDS when they fit in 32 KiB (four workgroups per CU);
-    // MPT_CANDS_LDS=0: always through the caches (A/B knob)
-    static const bool cands_lds = !(getenv("MPT_CANDS_LDS") && atoi(getenv("MPT_CANDS_LDS")) == 0);
-    const int32_t cl_items = cands_lds && env.n_tris <= kCandsLdsItems ? env.n_tris : 0;
+    // the env's triangle items in LDS when they fit in 32 KiB (four workgroups per CU)
+    const int32_t cl_items = env.n_tris <= kCandsLdsItems ? env.n_tris : 0;
     if (cl_items > 0)
         hipLaunchKernelGGL(k_cands<true>, dim3((unsigned)((s.n_cwaves + 3) / 4)), dim3(256),
                            sizeof(Item) * (size_t)cl_items, stream, env, d_links, w, a, cl_items);
@@ -848,9 +788,7 @@ static void collide_split_chunk(const EnvDev &env, const AgentDev *d_links, int3
     hip_check(hipGetLastError(), "k_cands launch");
     mark(1);
     const unsigned nblocks = (unsigned)((s.n_cwaves + kSpillWaves + kNarrowWaves - 1) / kNarrowWaves);
-    // MPT_NARROW_LDS=0: never stage the env in LDS (A/B knob)
-    static const bool narrow_lds = !(getenv("MPT_NARROW_LDS") && atoi(getenv("MPT_NARROW_LDS")) == 0);
-    const int32_t lds_ok = narrow_lds && env.n_tris <= kNarrowLdsTris;
+    const int32_t lds_ok = env.n_tris <= kNarrowLdsTris;  // k_narrow may stage the env's vertices in LDS
     hipLaunchKernelGGL(k_narrow, dim3(nblocks), dim3(kNarrowWaves * 64), lds_ok ? sizeof(double) * 9 * env.n_tris : 0,
                        stream, env, d_links, w, a, lds_ok);
     hip_check(hipGetLastError(), "k_narrow launch");

@@ -193,14 +193,8 @@ Range subtree_range(const std::vector<BvhNode> &pre, int32_t id, std::vector<Ran
 }
 // Bucket size of the broad-phase tree: small buckets keep bucket boxes tight for meshes of
 // large triangles (rooms), where a 64-triangle bucket spans several walls.
-int32_t env_bucket_size() {
-    static const int32_t s = [] {
-        const char *e = getenv("MPT_ENV_BUCKET");  // tuning knob
-        const int v = e ? atoi(e) : 0;
-        return v >= 1 && v <= kClusterMax ? v : 16;
-    }();
-    return s;
-}
+constexpr int32_t env_bucket_size() { return 16; }
+static_assert(env_bucket_size() <= kClusterMax, "bucket size");
 void collect_buckets(const std::vector<BvhNode> &pre, int32_t id, const std::vector<Range> &memo,
                      std::vector<Range> &out) {
     if (memo[id].count <= env_bucket_size()) {

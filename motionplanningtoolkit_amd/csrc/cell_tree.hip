@@ -1,0 +1,1554 @@
+// cell_tree.hip -- the engine's incremental exact 1-NN index (cell_tree.h).
+//
+// FLANN_KDTreeWrapper (utilities/flannkdtreewrapper.hpp:27-40) inserts each point into a live
+// kd-tree and FLANN 1.8.4 rebuilds it on every insert; a batched round here inserts its K new
+// points at once and touches only what they fall in.
+//
+// Codes.  A point's code interleaves its state dims quantised with one step h over the
+// sampling ranges (126 bits: the step is fine enough that distinct states get distinct codes,
+// where 63 bits left ~4 RRT nodes a cell), so a code never changes and code order is a fixed
+// space-filling order.
+//
+// Buckets.  The indexed points live in buckets of at most 8 (one lane each in the walk), each
+// the points of one interval [start, next start) of code space; the directory lists the
+// buckets by start.  A round sorts its new points by code, finds each one's bucket by a
+// binary search of the directory, and either appends them (the bucket still holds at most 8)
+// or splits the bucket: its old and new points, merged in code order, are cut into maximal
+// aligned code cells of at most 8 points -- points i - 1 and i share a bucket iff the smallest
+// cell holding both holds at most 8 of them -- and every bucket after the first gets a new
+// directory entry starting at the cell boundary.  Buckets are therefore cells of the code
+// space's binary trie, as a radix tree's leaves, and a round's work is its new points and the
+// buckets they touch.
+//
+// Boxes.  Above the directory an implicit 8-ary hierarchy (level 1 = each directory entry's
+// bucket box, level l = 8 consecutive level-(l - 1) boxes) is rebuilt each round from the
+// bucket boxes (~1/5 of a float box a point).  The walk is the Morton tree's (point_tree.hip):
+// 8 nodes a step, one query a wave, seeded by the tree's extreme points.
+//
+// Every result is exact whatever the buckets and boxes are (only boxes whose float lower bound
+// exceeds the best are skipped), so the layout decides speed only.
+#include <hipcub/hipcub.hpp>
+
+#include <algorithm>
+#include <cmath>
+
+#include "cell_tree.h"
+
+namespace mpt {
+
+namespace {
+
+// ---- 128-bit codes as (hi, lo) ----
+
+// (code, row) total order
+__device__ __forceinline__ bool cr_lt(uint64_t ah, uint64_t al, int32_t ar, uint64_t bh, uint64_t bl, int32_t br) {
+    return (ah < bh) | ((ah == bh) & ((al < bl) | ((al == bl) & (ar < br))));
+}
+// common prefix length of two codes (128: equal)
+__device__ __forceinline__ int c_cpl(uint64_t ah, uint64_t al, uint64_t bh, uint64_t bl) {
+    const uint64_t xh = ah ^ bh, xl = al ^ bl;
+    return xh ? __clzll((long long)xh) : (xl ? 64 + __clzll((long long)xl) : 128);
+}
+// the aligned cell boundary between two codes a < b: b with every bit below its first
+// difference from a cleared (the start of the cell of b's side)
+__device__ __forceinline__ void c_boundary(uint64_t ah, uint64_t al, uint64_t &bh, uint64_t &bl) {
+    const int k = c_cpl(ah, al, bh, bl);
+    if (k >= 127) return;     // equal, or differ in the last bit only: b itself
+    const int keep = k + 1;   // the common prefix and the differing bit
+    if (keep <= 64) {
+        bh &= keep == 64 ? ~0ull : ~(~0ull >> keep);
+        bl = 0;
+    } else {
+        bl &= ~(~0ull >> (keep - 64));
+    }
+}
+
+__device__ __forceinline__ unsigned long long okey(double x) {
+    const unsigned long long b = (unsigned long long)__double_as_longlong(x);
+    return (b >> 63) ? ~b : (b | 0x8000000000000000ull);
+}
+
+template <int D>
+__device__ __forceinline__ void ct_code(const CtPlan &P, const double (&x)[D], uint64_t &h, uint64_t &l) {
+    uint32_t q[D];
+#pragma unroll
+    for (int j = 0; j < D; ++j) {
+        const double u = (x[j] - P.lo[j]) * P.scale[j];
+        const uint32_t m = P.qmax[j];
+        q[j] = u <= 0.0 ? 0u : (u >= (double)m ? m : (uint32_t)u);
+    }
+    h = 0;
+    l = 0;
+    const int32_t nb = P.n;
+    for (int k = 0; k < nb; ++k) {
+        const int32_t dk = P.dim[k];
+        uint32_t v = q[0];
+#pragma unroll
+        for (int j = 1; j < D; ++j)
+            if (j == dk) v = q[j];
+        h = (h << 1) | (l >> 63);
+        l = (l << 1) | (uint64_t)((v >> P.bit[k]) & 1u);
+    }
+}
+
+// Seed slots (cell_tree.h kCtHull): lane h of a wave scores slot h over the wave's 64 points
+// (staged in LDS: every lane reads the same point at once, a broadcast) and offers its best to
+// the tree's slot with one 64-bit atomicMax of (score as an ordered float key << 32 | row).
+// Rows of a wave are consecutive (row0 + lane).  The float rounding of the score only decides
+// which near-tie becomes the seed; any point is a valid seed.
+constexpr int kCtWaves = 4;  // waves of the workgroups that stage rows (256 threads)
+template <int D>
+__device__ __forceinline__ void hull_offer(const CtPlan &P, const double (&x)[D], bool live, int64_t row0,
+                                           double (*s_rows)[D], unsigned long long *__restrict__ keys) {
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int j = 0; j < D; ++j) s_rows[lane][j] = live ? x[j] : 0.0;
+    const uint64_t lm = __ballot(live);
+    __builtin_amdgcn_wave_barrier();
+    if (lane < P.n_hull) {
+        const int kind = P.hkind[lane], dm = P.hdim[lane];
+        const float u0 = P.hdir[lane][0], u1 = P.hdir[lane][1], u2 = P.hdir[lane][2];
+        unsigned long long best = 0;
+        for (uint64_t m = lm; m; m &= m - 1) {
+            const int j = __ffsll((long long)m) - 1;
+            double v;
+            if (kind == 0) {
+                v = (double)u0 * s_rows[j][0];
+                if (D > 1) v += (double)u1 * s_rows[j][D > 1 ? 1 : 0];
+                if (D > 2) v += (double)u2 * s_rows[j][D > 2 ? 2 : 0];
+            } else {
+                double xv = s_rows[j][0];
+#pragma unroll
+                for (int k = 1; k < D; ++k)
+                    if (k == dm) xv = s_rows[j][k];
+                v = kind == 1 ? -xv : xv;
+            }
+            const uint32_t b = __float_as_uint((float)v);
+            const uint32_t key = (b & 0x80000000u) ? ~b : (b | 0x80000000u);
+            const unsigned long long k64 = ((unsigned long long)key << 32) | (uint32_t)(row0 + j);
+            best = k64 > best ? k64 : best;
+        }
+        if (best) atomicMax(keys + lane, best);
+    }
+    __builtin_amdgcn_wave_barrier();
+}
+
+// the box of rows (widened float bounds over every dim)
+template <int D>
+__device__ __forceinline__ void write_box(float *__restrict__ b, const double (&lo)[D], const double (&hi)[D]) {
+#pragma unroll
+    for (int k = 0; k < D; ++k) {
+        b[k] = widen_lo(lo[k]);
+        b[D + k] = widen_hi(hi[k]);
+    }
+}
+
+// the job table on the device (a joint build), or one job in the kernel arguments
+struct CtJobs {
+    const CtJob *table;
+    CtJob one;
+};
+#define CT_JOB(js) ((js).table ? (js).table[blockIdx.y] : (js).one)
+
+__device__ __forceinline__ int64_t ct_new_count(const CtJob &J) {
+    int64_t m = *J.T.n_dev - J.cnt->nidx;
+    return m < 0 ? 0 : (m > kCtSeg ? kCtSeg : m);
+}
+
+constexpr uint32_t kCtLeafBit = 0x80000000u;
+__device__ __forceinline__ uint32_t leaf_code(int32_t bucket, int32_t count) {
+    return kCtLeafBit | ((uint32_t)(count - 1) << 28) | (uint32_t)bucket;
+}
+__device__ __forceinline__ uint32_t inner_code(int64_t first, int32_t count) {
+    return ((uint32_t)(count - 1) << 28) | (uint32_t)first;
+}
+
+// ---- a round's new points ----
+
+// codes and rows of the new points [nidx, n) in row order, their box into ibox, their offers
+// to the seed slots
+template <int D>
+__global__ __launch_bounds__(64 * kCtWaves) void k_ct_ncodes(CtJobs js) {
+    __shared__ CtPlan s_plan;
+    __shared__ double s_rows[kCtWaves][64][D];
+    const CtJob J = CT_JOB(js);  // by value: the fields stay in registers across the stores
+    const int64_t base = J.cnt->nidx, mraw = *J.T.n_dev - base;
+    if ((mraw > kCtSeg || mraw > J.mb) && blockIdx.x == 0 && threadIdx.x == 0 && J.err)
+        atomicAdd(J.err, 1ull);  // the host's bound broken
+    const int64_t m = ct_new_count(J);
+    const int i = (int)blockIdx.x * (int)blockDim.x + (int)threadIdx.x;
+    if ((int64_t)blockIdx.x * blockDim.x >= m) return;  // block-uniform
+    for (int w = threadIdx.x; w < (int)(sizeof(CtPlan) / 4); w += blockDim.x)
+        reinterpret_cast<uint32_t *>(&s_plan)[w] = reinterpret_cast<const uint32_t *>(J.plan)[w];
+    __syncthreads();
+    const bool live = i < m;
+    double x[D];
+    unsigned long long mn[D], mx[D];
+    if (live) {
+        const int64_t row = base + i;
+        load_global<D>(J.pts + row * D, x);
+        uint64_t h, l;
+        ct_code<D>(s_plan, x, h, l);
+        J.ncode[2 * i] = h;
+        J.ncode[2 * i + 1] = l;
+        J.nrow[i] = (int32_t)row;
+#pragma unroll
+        for (int j = 0; j < D; ++j) mn[j] = mx[j] = okey(x[j]);
+    } else {
+#pragma unroll
+        for (int j = 0; j < D; ++j) {
+            x[j] = 0.0;
+            mn[j] = ~0ull;
+            mx[j] = 0ull;
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < D; ++j) {
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) {
+            const unsigned long long omn = __shfl_xor(mn[j], off), omx = __shfl_xor(mx[j], off);
+            mn[j] = omn < mn[j] ? omn : mn[j];
+            mx[j] = omx > mx[j] ? omx : mx[j];
+        }
+    }
+    if ((threadIdx.x & 63) == 0) {
+#pragma unroll
+        for (int j = 0; j < D; ++j) {
+            atomicMin(J.ibox + j, mn[j]);
+            atomicMax(J.ibox + kCtMaxDim + j, mx[j]);
+        }
+    }
+    hull_offer<D>(s_plan, x, live, base + (i & ~63), s_rows[threadIdx.x >> 6], J.hull_keys);
+}
+
+// (code, row) compare-exchange by selects (no divergent branches)
+__device__ __forceinline__ void cx3(uint64_t &h, uint64_t &l, int32_t &r, uint64_t ph, uint64_t pl, int32_t pr,
+                                    bool keep_min) {
+    const bool sw = keep_min == cr_lt(ph, pl, pr, h, l, r);
+    h = sw ? ph : h;
+    l = sw ? pl : l;
+    r = sw ? pr : r;
+}
+
+// The new points' sort over many CUs: each wave sorts a chunk of 512 (8 a lane: partners 8+
+// apart by lane shuffles, closer ones in registers); then every element's rank = its index in
+// its chunk + the count of smaller pairs in each other chunk (fixed-step binary searches).
+constexpr int kCtChunk = 512;
+constexpr int kCtChunks = kCtSeg / kCtChunk;
+constexpr int kCtChunkWaves = 4;
+
+__global__ __launch_bounds__(64 * kCtChunkWaves) void k_ct_csort(CtJobs js) {
+    const CtJob J = CT_JOB(js);  // by value: the fields stay in registers across the stores
+    const int64_t m = ct_new_count(J);
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+    const int c0 = ((int)blockIdx.x * kCtChunkWaves + wave) * kCtChunk;
+    if (c0 >= m) return;
+    constexpr int E = kCtChunk / 64;
+    uint64_t kh[E], kl[E];
+    int32_t kr[E];
+#pragma unroll
+    for (int a = 0; a < E; ++a) {
+        const int i = c0 + lane * E + a;
+        const bool live = i < m;
+        kh[a] = live ? J.ncode[2 * i] : ~0ull;  // padding sorts last (codes use 126 bits)
+        kl[a] = live ? J.ncode[2 * i + 1] : ~0ull;
+        kr[a] = live ? J.nrow[i] : 0x7fffffff;
+    }
+#pragma unroll 1
+    for (int k = 2; k <= kCtChunk; k <<= 1) {
+#pragma unroll 1
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            if (j >= E) {
+                const int lm = j / E;
+                const bool lower = (lane & lm) == 0;
+#pragma unroll
+                for (int a = 0; a < E; ++a) {
+                    const uint64_t ph = __shfl_xor(kh[a], lm), pl = __shfl_xor(kl[a], lm);
+                    const int32_t pr = __shfl_xor(kr[a], lm);
+                    cx3(kh[a], kl[a], kr[a], ph, pl, pr, lower == (((lane * E + a) & k) == 0));
+                }
+            } else {
+#pragma unroll
+                for (int jj = E / 2; jj > 0; jj >>= 1) {
+                    if (jj != j) continue;
+#pragma unroll
+                    for (int a = 0; a < E; ++a) {
+                        const int b = a ^ jj;
+                        if (b < a) continue;
+                        const bool up = ((lane * E + a) & k) == 0;
+                        const bool sw = up == cr_lt(kh[b], kl[b], kr[b], kh[a], kl[a], kr[a]);
+                        const uint64_t ah = kh[a], al = kl[a], bh = kh[b], bl = kl[b];
+                        const int32_t ar = kr[a], br = kr[b];
+                        kh[a] = sw ? bh : ah;
+                        kl[a] = sw ? bl : al;
+                        kr[a] = sw ? br : ar;
+                        kh[b] = sw ? ah : bh;
+                        kl[b] = sw ? al : bl;
+                        kr[b] = sw ? ar : br;
+                    }
+                }
+            }
+        }
+    }
+#pragma unroll
+    for (int a = 0; a < E; ++a) {
+        const int i = c0 + lane * E + a;
+        J.ccode[2 * i] = kh[a];
+        J.ccode[2 * i + 1] = kl[a];
+        J.crow[i] = kr[a];
+    }
+}
+
+template <int NC>
+__device__ __forceinline__ void ct_crank_n(const CtJob &J, int64_t m, int e) {
+    const int nch = (int)((m + kCtChunk - 1) / kCtChunk);
+    const uint64_t h = J.ccode[2 * e], l = J.ccode[2 * e + 1];
+    const int32_t r = J.crow[e];
+    int pos[NC];
+#pragma unroll
+    for (int c = 0; c < NC; ++c) pos[c] = 0;
+#pragma unroll
+    for (int st = kCtChunk / 2; st > 0; st >>= 1) {
+        uint64_t ph[NC], pl[NC];
+        int32_t pr[NC];
+#pragma unroll
+        for (int c = 0; c < NC; ++c) {
+            const int q = c * kCtChunk + pos[c] + st - 1;
+            ph[c] = J.ccode[2 * q];
+            pl[c] = J.ccode[2 * q + 1];
+            pr[c] = J.crow[q];
+        }
+#pragma unroll
+        for (int c = 0; c < NC; ++c) pos[c] += cr_lt(ph[c], pl[c], pr[c], h, l, r) ? st : 0;
+    }
+    int rank = 0;
+    {
+        uint64_t ph[NC], pl[NC];
+        int32_t pr[NC];
+#pragma unroll
+        for (int c = 0; c < NC; ++c) {
+            const int q = c * kCtChunk + pos[c];
+            ph[c] = J.ccode[2 * q];
+            pl[c] = J.ccode[2 * q + 1];
+            pr[c] = J.crow[q];
+        }
+#pragma unroll
+        for (int c = 0; c < NC; ++c) rank += c < nch ? pos[c] + (cr_lt(ph[c], pl[c], pr[c], h, l, r) ? 1 : 0) : 0;
+    }
+    J.ncode[2 * rank] = h;
+    J.ncode[2 * rank + 1] = l;
+    J.nrow[rank] = r;
+}
+
+__global__ __launch_bounds__(256) void k_ct_crank(CtJobs js) {
+    const CtJob J = CT_JOB(js);  // by value: the fields stay in registers across the stores
+    const int64_t m = ct_new_count(J);
+    const int e = (int)blockIdx.x * (int)blockDim.x + (int)threadIdx.x;
+    if (e >= m) return;
+    if (m <= (int64_t)kCtChunk * 4) ct_crank_n<4>(J, m, e);
+    else ct_crank_n<kCtChunks>(J, m, e);
+}
+
+// each sorted new point's directory position: the last entry whose start is <= its code
+__global__ __launch_bounds__(256) void k_ct_locate(CtJobs js) {
+    const CtJob J = CT_JOB(js);  // by value: the fields stay in registers across the stores
+    const int64_t m = ct_new_count(J);
+    const int j = (int)blockIdx.x * (int)blockDim.x + (int)threadIdx.x;
+    if (j >= m) return;
+    const uint64_t h = J.ncode[2 * j], l = J.ncode[2 * j + 1];
+    int lo = 0, hi = J.cnt->n_dir;  // entry 0 starts at code 0: the answer is in [0, n_dir)
+    while (hi - lo > 1) {
+        const int mid = (lo + hi) >> 1;
+        const uint64_t sh = J.odir_code[2 * mid], sl = J.odir_code[2 * mid + 1];
+        if (sh < h || (sh == h && sl <= l)) lo = mid;
+        else hi = mid;
+    }
+    J.npos[j] = lo;
+}
+
+// One workgroup a tree: the runs of equal directory positions (the touched buckets) become the
+// round's segments: segment s = (bucket, old count, new count, scratch offset j0 + 8 s); the
+// scratch positions no split element takes are marked -1 (every position of
+// [0, m + 8 * segments) is written: later kernels walk them all).
+constexpr int kCtSegThreads = 1024;
+constexpr int kCtSegPer = kCtSeg / kCtSegThreads;
+
+__global__ __launch_bounds__(kCtSegThreads) void k_ct_segments(CtJobs js) {
+    const CtJob J = CT_JOB(js);  // by value: the fields stay in registers across the stores
+    __shared__ int32_t s_sum[kCtSegThreads / 64];
+    __shared__ int32_t s_total;
+    __shared__ int32_t s_first[kCtSeg + 1];  // each segment's first new point
+    const int64_t m = ct_new_count(J);
+    const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+    int32_t pos[kCtSegPer];
+    int head[kCtSegPer];
+    int cnt = 0;
+#pragma unroll
+    for (int a = 0; a < kCtSegPer; ++a) {
+        const int j = t * kCtSegPer + a;
+        pos[a] = j < m ? J.npos[j] : -1;
+    }
+    const int32_t prev = (t * kCtSegPer > 0 && t * kCtSegPer - 1 < m) ? J.npos[t * kCtSegPer - 1] : -2;
+#pragma unroll
+    for (int a = 0; a < kCtSegPer; ++a) {
+        const int j = t * kCtSegPer + a;
+        const int32_t pv = a == 0 ? prev : pos[a - 1];
+        head[a] = (j < m && (j == 0 || pos[a] != pv)) ? 1 : 0;
+        cnt += head[a];
+    }
+    // block exclusive scan of the head counts
+    int incl = cnt;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const int o = __shfl_up(incl, off);
+        if (lane >= off) incl += o;
+    }
+    if (lane == 63) s_sum[wave] = incl;
+    __syncthreads();
+    if (t == 0) {
+        int acc = 0;
+        for (int w = 0; w < kCtSegThreads / 64; ++w) {
+            const int v = s_sum[w];
+            s_sum[w] = acc;
+            acc += v;
+        }
+        s_total = acc;
+        s_first[acc] = (int32_t)m;
+    }
+    __syncthreads();
+    const int s0 = s_sum[wave] + incl - cnt - 1;  // segment of the element before this thread's first
+    int s = s0;
+#pragma unroll
+    for (int a = 0; a < kCtSegPer; ++a) {
+        const int j = t * kCtSegPer + a;
+        if (j >= m) break;
+        s += head[a];
+        J.nseg[j] = s;
+        if (head[a]) s_first[s] = j;
+    }
+    __syncthreads();
+    s = s0;
+#pragma unroll
+    for (int a = 0; a < kCtSegPer; ++a) {
+        const int j = t * kCtSegPer + a;
+        if (j >= m) break;
+        s += head[a];
+        if (!head[a]) continue;
+        const int32_t b = J.odir_bk[pos[a]];
+        const int32_t c = J.bcnt[b];
+        const int32_t k = s_first[s + 1] - j;
+        const int32_t off = j + 8 * s;
+        J.seg[s] = make_int4(b, c, k, off);
+        J.seg_pos[s] = pos[a];
+        // scratch positions no split element takes: all of an append segment's, the 8 - c
+        // after a split segment's c + k elements
+        const int32_t from = c + k <= kCtCap ? off : off + c + k;
+        for (int e = from; e < off + k + 8; ++e) J.sseg[e] = -1;
+    }
+    if (t == 0) J.cnt->n_seg = s_total;
+}
+
+// Per sorted new point: appended to its bucket, or placed in its split segment's merged list
+// (the segment's first point also places the bucket's old points and, on append, sets the
+// bucket's count and box).
+template <int D>
+__global__ __launch_bounds__(256) void k_ct_apply(CtJobs js) {
+    const CtJob J = CT_JOB(js);  // by value: the fields stay in registers across the stores
+    const int64_t m = ct_new_count(J);
+    const int j = (int)blockIdx.x * (int)blockDim.x + (int)threadIdx.x;
+    if (j >= m) return;
+    const int s = J.nseg[j];
+    const int4 g = J.seg[s];
+    const int32_t b = g.x, c = g.y, k = g.z, off = g.w;
+    const int32_t j0 = off - 8 * s;
+    const uint64_t h = J.ncode[2 * j], l = J.ncode[2 * j + 1];
+    const int32_t row = J.nrow[j];
+    if (c + k <= kCtCap) {
+        const int64_t slot = (int64_t)b * kCtCap + c + (j - j0);
+        double x[D];
+        load_global<D>(J.pts + (int64_t)row * D, x);
+#pragma unroll
+        for (int q = 0; q < D; ++q) J.bpts[slot * D + q] = x[q];
+        J.bids[slot] = row + 1;
+        J.bcode[2 * slot] = h;
+        J.bcode[2 * slot + 1] = l;
+        if (j == j0) {
+            double lo[D], hi[D];
+            if (c > 0) {
+                const float *ob = J.bbox + (int64_t)b * 2 * D;
+#pragma unroll
+                for (int q = 0; q < D; ++q) {
+                    lo[q] = (double)ob[q];  // widened already: widening again only loosens it
+                    hi[q] = (double)ob[D + q];
+                }
+            } else {
+#pragma unroll
+                for (int q = 0; q < D; ++q) {
+                    lo[q] = __builtin_huge_val();
+                    hi[q] = -__builtin_huge_val();
+                }
+            }
+            for (int u = 0; u < k; ++u) {
+                double y[D];
+                load_global<D>(J.pts + (int64_t)J.nrow[j0 + u] * D, y);
+#pragma unroll
+                for (int q = 0; q < D; ++q) {
+                    lo[q] = y[q] < lo[q] ? y[q] : lo[q];
+                    hi[q] = y[q] > hi[q] ? y[q] : hi[q];
+                }
+            }
+            write_box<D>(J.bbox + (int64_t)b * 2 * D, lo, hi);
+            J.bcnt[b] = c + k;
+        }
+        return;
+    }
+    // split: this point's place in the merged list = its index among the new + the old points
+    // below it
+    int below = 0;
+    for (int o = 0; o < c; ++o) {
+        const int64_t os = (int64_t)b * kCtCap + o;
+        below += cr_lt(J.bcode[2 * os], J.bcode[2 * os + 1], J.bids[os] - 1, h, l, row) ? 1 : 0;
+    }
+    const int32_t e = off + (j - j0) + below;
+    J.scode[2 * e] = h;
+    J.scode[2 * e + 1] = l;
+    J.srow[e] = row;
+    J.sseg[e] = s;
+    if (j != j0) return;
+    for (int o = 0; o < c; ++o) {  // the old points' places
+        const int64_t os = (int64_t)b * kCtCap + o;
+        const uint64_t oh = J.bcode[2 * os], ol = J.bcode[2 * os + 1];
+        const int32_t orow = J.bids[os] - 1;
+        int ob = 0;
+        for (int o2 = 0; o2 < c; ++o2) {
+            const int64_t s2 = (int64_t)b * kCtCap + o2;
+            ob += cr_lt(J.bcode[2 * s2], J.bcode[2 * s2 + 1], J.bids[s2] - 1, oh, ol, orow) ? 1 : 0;
+        }
+        int lo = 0, hi = k;  // new points below it (sorted)
+        while (lo < hi) {
+            const int mid = (lo + hi) >> 1;
+            const int q = j0 + mid;
+            if (cr_lt(J.ncode[2 * q], J.ncode[2 * q + 1], J.nrow[q], oh, ol, orow)) lo = mid + 1;
+            else hi = mid;
+        }
+        const int32_t eo = off + ob + lo;
+        J.scode[2 * eo] = oh;
+        J.scode[2 * eo + 1] = ol;
+        J.srow[eo] = orow;
+        J.sseg[eo] = s;
+    }
+}
+
+// Do elements i - 1 and i of a sorted run [lo, hi) share a bucket?  Yes iff the smallest code
+// cell holding both holds at most 8 of the run's elements (a contiguous range around them);
+// equal codes that are more than 8 are grouped by row / 8 instead.  Leaves formed this way
+// hold at most 8: a leaf lies inside the largest of its pairs' cells.
+__device__ __forceinline__ bool ct_same(const uint64_t *__restrict__ code, const int32_t *__restrict__ row,
+                                        int64_t lo, int64_t hi, int64_t i) {
+    const uint64_t ah = code[2 * (i - 1)], al = code[2 * (i - 1) + 1];
+    const uint64_t bh = code[2 * i], bl = code[2 * i + 1];
+    const int k = c_cpl(ah, al, bh, bl);
+    int cnt = 2;
+    for (int64_t u = i - 2; u >= lo && cnt <= kCtCap; --u) {
+        if (c_cpl(code[2 * u], code[2 * u + 1], bh, bl) < k) break;
+        ++cnt;
+    }
+    for (int64_t u = i + 1; u < hi && cnt <= kCtCap; ++u) {
+        if (c_cpl(code[2 * u], code[2 * u + 1], bh, bl) < k) break;
+        ++cnt;
+    }
+    if (cnt <= kCtCap) return true;
+    if (k < 128) return false;
+    return row ? (row[i] >> 3) == (row[i - 1] >> 3) : ((i - lo) >> 3) == ((i - 1 - lo) >> 3);
+}
+
+__device__ __forceinline__ int64_t ct_scratch_total(const CtJob &J) {
+    return ct_new_count(J) + 8 * (int64_t)J.cnt->n_seg;
+}
+
+// leaf starts of the split segments: 1 the segment's first leaf (keeps the bucket), 2 a new leaf
+__global__ __launch_bounds__(256) void k_ct_split_flags(CtJobs js) {
+    const CtJob J = CT_JOB(js);  // by value: the fields stay in registers across the stores
+    const int64_t total = ct_scratch_total(J);
+    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
+        const int s = J.sseg[e];
+        int flag = 0;
+        if (s >= 0) {
+            const int4 g = J.seg[s];
+            const int64_t off = g.w, L = (int64_t)g.y + g.z;
+            if (e == off) flag = 1;
+            else if (!ct_same(J.scode, J.srow, off, off + L, e)) flag = 2;
+        }
+        J.slead[e] = flag;
+    }
+}
+
+// one workgroup a tree: each new leaf's rank among the round's new leaves (code order)
+constexpr int kCtScanThreads = 1024;
+__global__ __launch_bounds__(kCtScanThreads) void k_ct_split_scan(CtJobs js) {
+    const CtJob J = CT_JOB(js);  // by value: the fields stay in registers across the stores
+    __shared__ int32_t s_sum[kCtScanThreads / 64];
+    const int64_t total = ct_scratch_total(J);
+    const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+    const int64_t per = (total + kCtScanThreads - 1) / kCtScanThreads;
+    const int64_t e0 = t * per, e1 = e0 + per < total ? e0 + per : total;
+    int cnt = 0;
+    for (int64_t e = e0; e < e1; ++e) cnt += J.slead[e] == 2 ? 1 : 0;
+    int incl = cnt;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const int o = __shfl_up(incl, off);
+        if (lane >= off) incl += o;
+    }
+    if (lane == 63) s_sum[wave] = incl;
+    __syncthreads();
+    if (t == 0) {
+        int acc = 0;
+        for (int w = 0; w < kCtScanThreads / 64; ++w) {
+            const int v = s_sum[w];
+            s_sum[w] = acc;
+            acc += v;
+        }
+        J.cnt->n_new_dir = acc;
+    }
+    __syncthreads();
+    int r = s_sum[wave] + incl - cnt;
+    for (int64_t e = e0; e < e1; ++e) {
+        J.srank[e] = r;
+        r += J.slead[e] == 2 ? 1 : 0;
+    }
+}
+
+// a leaf start fills its bucket (the segment's first leaf: the split bucket; a new leaf: the
+// next free bucket by rank) and a new leaf records its directory entry
+template <int D>
+__device__ __forceinline__ void ct_fill_leaf(const CtJob &J, int64_t e, int flag) {
+    const int s = J.sseg[e];
+    const int4 g = J.seg[s];
+    const int64_t end = (int64_t)g.w + g.y + g.z;
+    int len = 1;
+    while (e + len < end && J.slead[e + len] == 0) ++len;
+    int32_t b = g.x;
+    if (flag == 2) {
+        const int32_t r = J.srank[e];
+        b = J.cnt->n_buckets + r;
+        if (b >= J.bcap || len > kCtCap) {
+            if (J.err) atomicAdd(J.err, 1ull);
+            return;
+        }
+        uint64_t bh = J.scode[2 * e], bl = J.scode[2 * e + 1];
+        c_boundary(J.scode[2 * (e - 1)], J.scode[2 * (e - 1) + 1], bh, bl);
+        J.edir_code[2 * r] = bh;
+        J.edir_code[2 * r + 1] = bl;
+        J.edir_bk[r] = b;
+        J.edir_pos[r] = J.seg_pos[s];
+    } else if (len > kCtCap) {
+        if (J.err) atomicAdd(J.err, 1ull);
+        return;
+    }
+    double lo[D], hi[D];
+#pragma unroll
+    for (int q = 0; q < D; ++q) {
+        lo[q] = __builtin_huge_val();
+        hi[q] = -__builtin_huge_val();
+    }
+    for (int u = 0; u < len; ++u) {
+        const int32_t row = J.srow[e + u];
+        double x[D];
+        load_global<D>(J.pts + (int64_t)row * D, x);
+        const int64_t slot = (int64_t)b * kCtCap + u;
+#pragma unroll
+        for (int q = 0; q < D; ++q) {
+            J.bpts[slot * D + q] = x[q];
+            lo[q] = x[q] < lo[q] ? x[q] : lo[q];
+            hi[q] = x[q] > hi[q] ? x[q] : hi[q];
+        }
+        J.bids[slot] = row + 1;
+        J.bcode[2 * slot] = J.scode[2 * (e + u)];
+        J.bcode[2 * slot + 1] = J.scode[2 * (e + u) + 1];
+    }
+    write_box<D>(J.bbox + (int64_t)b * 2 * D, lo, hi);
+    J.bcnt[b] = len;
+}
+
+template <int D>
+__global__ __launch_bounds__(256) void k_ct_split_fill(CtJobs js) {
+    const CtJob J = CT_JOB(js);  // by value: the fields stay in registers across the stores
+    const int64_t total = ct_scratch_total(J);
+    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
+        const int flag = J.slead[e];
+        if (flag) ct_fill_leaf<D>(J, e, flag);
+    }
+}
+
+// The new directory: old entry p goes to p + (new entries of segments before p), new entry r
+// (of the segment at directory position q) to q + 1 + r; with each entry its level-1 node (the
+// bucket's box and code).
+template <int D>
+__global__ __launch_bounds__(256) void k_ct_dmerge(CtJobs js) {
+    const CtJob J = CT_JOB(js);  // by value: the fields stay in registers across the stores
+    const int64_t n_old = J.cnt->n_dir, n_new = J.cnt->n_new_dir;
+    for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < n_old + n_new;
+         t += (int64_t)gridDim.x * blockDim.x) {
+    int64_t out;
+    uint64_t h, l;
+    int32_t b;
+    if (t < n_old) {
+        int64_t lo = 0, hi = n_new;  // new entries whose segment lies before t
+        while (lo < hi) {
+            const int64_t mid = (lo + hi) >> 1;
+            if (J.edir_pos[mid] < t) lo = mid + 1;
+            else hi = mid;
+        }
+        out = t + lo;
+        h = J.odir_code[2 * t];
+        l = J.odir_code[2 * t + 1];
+        b = J.odir_bk[t];
+    } else {
+        const int64_t r = t - n_old;
+        out = J.edir_pos[r] + 1 + r;
+        h = J.edir_code[2 * r];
+        l = J.edir_code[2 * r + 1];
+        b = J.edir_bk[r];
+    }
+    J.ndir_code[2 * out] = h;
+    J.ndir_code[2 * out + 1] = l;
+    J.ndir_bk[out] = b;
+    const int32_t cnt = J.bcnt[b];
+    J.nmeta[out] = leaf_code(b, cnt > 0 ? cnt : 1);
+#pragma unroll
+    for (int q = 0; q < 2 * D; ++q) J.nbox[out * 2 * D + q] = J.bbox[(int64_t)b * 2 * D + q];
+    }
+}
+
+// One workgroup a tree: the hierarchy above the directory, level after level -- consecutive
+// nodes grouped into maximal aligned code cells of at most 8 (ct_same over the nodes' codes: a
+// node's code is its first directory entry's start), or, when that would leave more than half as
+// many groups as nodes, runs of 8 (the depth stays logarithmic) -- then the counts, the seed
+// rows, the indexed count and the spread.
+constexpr int kCtLevelThreads = 1024;
+constexpr int kCtMaxLevels = 10;  // the walk's stack bound (ct_walk kStack); runs of 8 reach it below 8^9 entries
+
+__device__ __forceinline__ int ct_block_sum(int v, int32_t *s_w) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+    __syncthreads();
+    if (lane == 0) s_w[wave] = v;
+    __syncthreads();
+    int tot = 0;
+    for (int w = 0; w < kCtLevelThreads / 64; ++w) tot += s_w[w];
+    return tot;
+}
+
+template <int D>
+__global__ __launch_bounds__(kCtLevelThreads) void k_ct_levels(CtJobs js) {
+    const CtJob J = CT_JOB(js);  // by value: the fields stay in registers across the stores
+    __shared__ int32_t s_w[kCtLevelThreads / 64];
+    const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+    int64_t n = (int64_t)J.cnt->n_dir + J.cnt->n_new_dir, ls = 0;
+    int lev = 1;  // the level being grouped (the walk's stack holds ~7 entries a level a node of a step: <= 10 levels)
+    while (n > 1) {
+        const uint64_t *lc = ls == 0 ? J.ndir_code : J.ucode + 2 * ls;  // node i's code at lc[2 i]
+        int g = 0;
+        for (int64_t i = t; i < n; i += kCtLevelThreads) {
+            const int f = i == 0 || !ct_same(lc, nullptr, 0, n, i);
+            J.lflag[i] = f;
+            g += f;
+        }
+        int64_t G = ct_block_sum(g, s_w);
+        int need = lev + 1;  // levels if runs of 8 follow from the next one on
+        for (int64_t m = G; m > 1; m = (m + 7) / 8) ++need;
+        const bool fixed = G > n / 2 || need > kCtMaxLevels;
+        if (fixed) {
+            for (int64_t i = t; i < n; i += kCtLevelThreads) J.lflag[i] = (i & 7) == 0;
+            G = (n + 7) / 8;
+        }
+        __threadfence_block();
+        __syncthreads();
+        int64_t carry = 0;
+        for (int64_t c0 = 0; c0 < n; c0 += kCtLevelThreads) {
+            const int64_t i = c0 + t;
+            const int f = i < n ? J.lflag[i] : 0;
+            int incl = f;
+#pragma unroll
+            for (int off = 1; off < 64; off <<= 1) {
+                const int o = __shfl_up(incl, off);
+                if (lane >= off) incl += o;
+            }
+            __syncthreads();
+            if (lane == 63) s_w[wave] = incl;
+            __syncthreads();
+            int before = 0, tot = 0;
+            for (int w = 0; w < kCtLevelThreads / 64; ++w) {
+                before += w < wave ? s_w[w] : 0;
+                tot += s_w[w];
+            }
+            if (f) {
+                const int64_t grp = carry + before + incl - 1;
+                int len = 1;
+                while (i + len < n && len < kCtCap && !J.lflag[i + len]) ++len;
+                const int64_t first = ls + i, P = ls + n + grp;
+                float lo[D], hi[D];
+#pragma unroll
+                for (int q = 0; q < D; ++q) {
+                    lo[q] = J.nbox[first * 2 * D + q];
+                    hi[q] = J.nbox[first * 2 * D + D + q];
+                }
+                for (int u = 1; u < len; ++u)
+#pragma unroll
+                    for (int q = 0; q < D; ++q) {
+                        lo[q] = fminf(lo[q], J.nbox[(first + u) * 2 * D + q]);
+                        hi[q] = fmaxf(hi[q], J.nbox[(first + u) * 2 * D + D + q]);
+                    }
+#pragma unroll
+                for (int q = 0; q < D; ++q) {
+                    J.nbox[P * 2 * D + q] = lo[q];
+                    J.nbox[P * 2 * D + D + q] = hi[q];
+                }
+                J.nmeta[P] = inner_code(first, len);
+                J.ucode[2 * P] = lc[2 * i];
+                J.ucode[2 * P + 1] = lc[2 * i + 1];
+            }
+            carry += tot;
+        }
+        __threadfence_block();
+        __syncthreads();
+        ls += n;
+        n = G;
+        ++lev;
+    }
+    for (int it = t; it < kCtHull * D; it += kCtLevelThreads) {
+        const int h = it / D, k = it - h * D;
+        const unsigned long long key = J.hull_keys[h];
+        const int64_t row = (int64_t)(uint32_t)key;
+        J.hull_pts[it] = key ? J.pts[row * D + k] : 0.0;
+        if (k == 0) J.hull_ids[h] = key ? (int32_t)row + 1 : 0;
+    }
+    __syncthreads();
+    if (t != 0) return;
+    CtCounts *c = J.cnt;
+    const int32_t nn = c->n_new_dir;
+    c->root = (int32_t)ls;
+    c->n_dir += nn;
+    c->n_buckets += nn;
+    c->n_new_dir = 0;
+    c->n_seg = 0;
+    c->nidx = c->nidx + ct_new_count(J);
+    const SpreadOut &sp = J.sp;
+    if (sp.host_out) {
+        for (int j = 0; j < 3; ++j) {
+            sp.host_out[j] = j < sp.gd ? J.ibox[sp.dims[j]] : ~0ull;
+            sp.host_out[3 + j] = j < sp.gd ? J.ibox[kCtMaxDim + sp.dims[j]] : 0ull;
+        }
+        __threadfence_system();
+    }
+}
+
+// ---- full rebuild (prepare, full): every point sorted by (code, row), then cut into buckets ----
+
+template <int D>
+__global__ __launch_bounds__(64 * kCtWaves) void k_ct_codes_all(const double *__restrict__ pts, int64_t n_upper,
+                                                                const int64_t *__restrict__ n_dev,
+                                                                const CtPlan *__restrict__ plan,
+                                                                uint64_t *__restrict__ hi_out, uint64_t *__restrict__ lo_out,
+                                                                int32_t *__restrict__ rows,
+                                                                unsigned long long *__restrict__ hull_keys,
+                                                                unsigned long long *__restrict__ ibox) {
+    __shared__ CtPlan s_plan;
+    __shared__ double s_rows[kCtWaves][64][D];
+    for (int w = threadIdx.x; w < (int)(sizeof(CtPlan) / 4); w += blockDim.x)
+        reinterpret_cast<uint32_t *>(&s_plan)[w] = reinterpret_cast<const uint32_t *>(plan)[w];
+    __syncthreads();
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if ((int64_t)blockIdx.x * blockDim.x >= n_upper) return;  // block-uniform
+    const int64_t n = *n_dev < n_upper ? *n_dev : n_upper;
+    const bool live = i < n;
+    double x[D];
+#pragma unroll
+    for (int j = 0; j < D; ++j) x[j] = live ? pts[i * D + j] : 0.0;
+    if (i < n_upper) {
+        uint64_t h = ~0ull, l = ~0ull;  // rows past the live count sort last
+        if (live) ct_code<D>(s_plan, x, h, l);
+        hi_out[i] = h;
+        lo_out[i] = l;
+        rows[i] = (int32_t)i;
+    }
+    unsigned long long mn[D], mx[D];
+#pragma unroll
+    for (int j = 0; j < D; ++j) {
+        mn[j] = live ? okey(x[j]) : ~0ull;
+        mx[j] = live ? okey(x[j]) : 0ull;
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) {
+            const unsigned long long omn = __shfl_xor(mn[j], off), omx = __shfl_xor(mx[j], off);
+            mn[j] = omn < mn[j] ? omn : mn[j];
+            mx[j] = omx > mx[j] ? omx : mx[j];
+        }
+    }
+    if ((threadIdx.x & 63) == 0) {
+#pragma unroll
+        for (int j = 0; j < D; ++j) {
+            atomicMin(ibox + j, mn[j]);
+            atomicMax(ibox + kCtMaxDim + j, mx[j]);
+        }
+    }
+    hull_offer<D>(s_plan, x, live, i & ~(int64_t)63, s_rows[threadIdx.x >> 6], hull_keys);
+}
+
+// after the first (low-word) pass: the high words in that order, for the second pass
+__global__ void k_ct_gather_hi(const uint64_t *__restrict__ hi, const int32_t *__restrict__ order, int64_t n,
+                               uint64_t *__restrict__ out) {
+    const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j < n) out[j] = hi[order[j]];
+}
+
+// the sorted codes as (hi, lo) pairs (lo gathered by row) for the leaf rule
+__global__ void k_ct_pack(const uint64_t *__restrict__ hi_sorted, const uint64_t *__restrict__ lo_by_row,
+                          const int32_t *__restrict__ rows, int64_t n_upper, const int64_t *__restrict__ n_dev,
+                          uint64_t *__restrict__ code) {
+    const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t n = *n_dev < n_upper ? *n_dev : n_upper;
+    if (j >= n) return;
+    code[2 * j] = hi_sorted[j];
+    code[2 * j + 1] = lo_by_row[rows[j]];
+}
+
+__global__ void k_ct_bulk_flags(const uint64_t *__restrict__ code, const int32_t *__restrict__ rows, int64_t n_upper,
+                                const int64_t *__restrict__ n_dev, int32_t *__restrict__ flag) {
+    const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= n_upper) return;
+    const int64_t n = *n_dev < n_upper ? *n_dev : n_upper;
+    flag[j] = j < n && (j == 0 || !ct_same(code, rows, 0, n, j)) ? 1 : 0;
+}
+
+// leaf starts fill bucket r = their rank and directory entry r; an empty tree gets one empty
+// bucket (its box empty) starting at code 0
+template <int D>
+__global__ void k_ct_bulk_fill(const double *__restrict__ pts, const uint64_t *__restrict__ code,
+                               const int32_t *__restrict__ rows, const int32_t *__restrict__ flag,
+                               const int32_t *__restrict__ leaf, int64_t n_upper, const int64_t *__restrict__ n_dev,
+                               double *__restrict__ bpts, int32_t *__restrict__ bids, uint64_t *__restrict__ bcode,
+                               int32_t *__restrict__ bcnt, float *__restrict__ bbox, uint64_t *__restrict__ dir_code,
+                               int32_t *__restrict__ dir_bk, CtCounts *__restrict__ cnt) {
+    const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t n = *n_dev < n_upper ? *n_dev : n_upper;
+    if (n == 0) {
+        if (j == 0) {
+            bcnt[0] = 0;
+            for (int q = 0; q < D; ++q) {
+                bbox[q] = __builtin_huge_valf();
+                bbox[D + q] = -__builtin_huge_valf();
+            }
+            dir_code[0] = 0;
+            dir_code[1] = 0;
+            dir_bk[0] = 0;
+            cnt->n_dir = cnt->n_buckets = 1;
+            cnt->n_seg = cnt->n_new_dir = 0;
+            cnt->nidx = 0;
+        }
+        return;
+    }
+    if (j >= n) return;
+    if (j == n - 1) {
+        const int32_t nb = leaf[j] + flag[j];
+        cnt->n_dir = cnt->n_buckets = nb;
+        cnt->n_seg = cnt->n_new_dir = 0;
+        cnt->nidx = n;
+    }
+    if (!flag[j]) return;
+    const int32_t r = leaf[j];
+    int len = 1;
+    while (j + len < n && !flag[j + len]) ++len;
+    uint64_t sh = 0, sl = 0;
+    if (j > 0) {
+        sh = code[2 * j];
+        sl = code[2 * j + 1];
+        c_boundary(code[2 * (j - 1)], code[2 * (j - 1) + 1], sh, sl);
+    }
+    dir_code[2 * r] = sh;
+    dir_code[2 * r + 1] = sl;
+    dir_bk[r] = r;
+    double lo[D], hi[D];
+#pragma unroll
+    for (int q = 0; q < D; ++q) {
+        lo[q] = __builtin_huge_val();
+        hi[q] = -__builtin_huge_val();
+    }
+    for (int u = 0; u < len && u < kCtCap; ++u) {
+        const int32_t row = rows[j + u];
+        const int64_t slot = (int64_t)r * kCtCap + u;
+#pragma unroll
+        for (int q = 0; q < D; ++q) {
+            const double x = pts[(int64_t)row * D + q];
+            bpts[slot * D + q] = x;
+            lo[q] = x < lo[q] ? x : lo[q];
+            hi[q] = x > hi[q] ? x : hi[q];
+        }
+        bids[slot] = row + 1;
+        bcode[2 * slot] = code[2 * (j + u)];
+        bcode[2 * slot + 1] = code[2 * (j + u) + 1];
+    }
+    write_box<D>(bbox + (int64_t)r * 2 * D, lo, hi);
+    bcnt[r] = len < kCtCap ? len : kCtCap;
+}
+
+__global__ __launch_bounds__(64) void k_ct_box_reset(unsigned long long *__restrict__ box) {
+    if (threadIdx.x < 2 * kCtMaxDim) box[threadIdx.x] = threadIdx.x < kCtMaxDim ? ~0ull : 0ull;
+}
+
+// ---- the walk (point_tree.hip tree_nn1_blockn over the bucket hierarchy) ----
+
+using gdbl = const __attribute__((address_space(1))) double *;
+using gflt = const __attribute__((address_space(1))) float *;
+using gi32 = const __attribute__((address_space(1))) int32_t *;
+using gu32 = const __attribute__((address_space(1))) uint32_t *;
+
+// A box's lower bound on FLANN's squared L2 from the query, as a float rounded down (see
+// point_tree.hip box_lb: d <= 7 in float from the query rounded outward and scaled below the
+// exact bound, d = 15 in double rounded down).  Pruning on it keeps every box the exact bound
+// keeps.
+constexpr float kCtLbShrink = 1.0f - 0x1p-19f;
+template <int D>
+__device__ __forceinline__ float ct_box_lb(const float *__restrict__ b, const double (&qq)[D], const float (&qlo)[D],
+                                           const float (&qhi)[D]) {
+    if constexpr (D <= 7) {
+        float s = 0.0f;
+#pragma unroll
+        for (int k = 0; k < D; ++k) {
+            const float g = fmaxf(fmaxf(b[k] - qhi[k], qlo[k] - b[D + k]), 0.0f);
+            s = s + g * g;
+        }
+        return s * kCtLbShrink;
+    } else {
+        double lb2 = 0.0;
+#pragma unroll
+        for (int k = 0; k < D; ++k) {
+            const double g = fmax(fmax((double)b[k] - qq[k], qq[k] - (double)b[D + k]), 0.0);
+            lb2 += g * g;
+        }
+        return __double2float_rd(lb2);
+    }
+}
+
+// the seeds' best (d2, id) over a group of G lanes: lane `sub` takes seeds sub, sub + G, ...
+template <int D, int G>
+__device__ __forceinline__ void ct_seed(const CellTreeDev &T, const double (&qq)[D], int sub, double &bd, int32_t &bi,
+                                        uint32_t &n_pts) {
+    for (int h = sub; h < kCtHull; h += G) {
+        const int32_t id = ((gi32)T.hull_ids)[h];
+        if (id <= 0) continue;
+        double row[D];
+#pragma unroll
+        for (int k = 0; k < D; ++k) row[k] = ((gdbl)T.hull_pts)[h * D + k];
+        const double dd = flann_l2<D>(qq, row);
+        ++n_pts;
+        if (nn_better(dd, id, bd, bi)) {
+            bd = dd;
+            bi = id;
+        }
+    }
+#pragma unroll
+    for (int off = G / 2; off > 0; off >>= 1) {
+        const double od = __shfl_xor(bd, off, G);
+        const int32_t oi = __shfl_xor(bi, off, G);
+        if (nn_better(od, oi, bd, bi)) {
+            bd = od;
+            bi = oi;
+        }
+    }
+}
+
+// NW nodes a step: 8 * NW lanes per query, the stack's top NW entries popped together (each
+// taken by 8 lanes: a bucket's points or an inner box's 8 children); the parts' best merged,
+// the children re-tested against it, deeper entries' survivors pushed below the top's (each
+// part nearest-last), so the walk stays nearest-first.  The stack holds at most ~NW blocks of
+// 7 a level.
+template <int D, int BS, int NW>
+__device__ __forceinline__ void ct_walk(const CellTreeDev &T, const double *__restrict__ q, int64_t nq,
+                                        int32_t *__restrict__ out_ids, double *__restrict__ out_d2, int64_t blk) {
+    constexpr int G = NW * 8;        // lanes per query
+    constexpr int kStack = NW * 8 * kCtMaxLevels;  // ~NW blocks of 7 a level, <= 10 levels (k_ct_levels): 5 KiB for NW = 8
+    static_assert(G <= 64, "ballot bits per group");
+    __shared__ uint32_t s_code[BS / G][kStack];
+    __shared__ float s_lb[BS / G][kStack];
+    const int64_t t = blk * BS + threadIdx.x;
+    const int64_t qi = t / G;
+    const int sub = (int)(t % G);
+    const int part = sub / 8;  // which popped entry: 0 the top, 1 the one below it, ...
+    const int ls = sub % 8;    // the child / point this lane takes
+    const int grp = threadIdx.x / G;
+    if (qi >= nq) return;  // whole groups leave together
+    double qq[D];
+#pragma unroll
+    for (int i = 0; i < D; ++i) qq[i] = q[qi * D + i];
+    float qlo[D], qhi[D];
+#pragma unroll
+    for (int i = 0; i < D; ++i) {
+        qlo[i] = __double2float_rd(qq[i]);
+        qhi[i] = __double2float_ru(qq[i]);
+    }
+    double bd = __builtin_huge_val();
+    int32_t bi = -1;
+    uint32_t n_pts = 0, n_box = 0, n_steps = 1;  // the seeds' step
+    if (*T.n_dev > 0) {
+        ct_seed<D, G>(T, qq, sub, bd, bi, n_pts);
+        int sp = 1;
+        if (sub == 0) {
+            s_code[grp][0] = ((gu32)T.nmeta)[*T.root];
+            s_lb[grp][0] = 0.0f;
+        }
+        __builtin_amdgcn_wave_barrier();
+        const int base = (threadIdx.x & 63) & ~(G - 1);
+        while (sp > 0) {
+            const int np = sp >= NW ? NW : sp;
+            const bool have = part < np;
+            uint32_t code = 0;
+            double lbs = 0.0;
+            if (have) {
+                code = s_code[grp][sp - 1 - part];
+                lbs = (double)s_lb[grp][sp - 1 - part];
+            }
+            sp -= np;
+            ++n_steps;
+            __builtin_amdgcn_wave_barrier();
+            const bool act = have && !(lbs * (1.0 - 1e-12) > bd);
+            bool keep = false, leaf = false;
+            float lbf = 0.0f;
+            uint32_t child = 0;
+            if (act && (code & kCtLeafBit)) {
+                const int cnt = (int)((code >> 28) & 7u) + 1;
+                if (ls < cnt) {
+                    const int64_t p = (int64_t)(code & 0x0fffffffu) * kCtCap + ls;
+                    double row[D];
+#pragma unroll
+                    for (int k = 0; k < D; ++k) row[k] = ((gdbl)T.bpts)[p * D + k];
+                    const double dd = flann_l2<D>(qq, row);
+                    const int32_t id = ((gi32)T.bids)[p];
+                    ++n_pts;
+                    leaf = true;
+                    if (nn_better(dd, id, bd, bi)) {
+                        bd = dd;
+                        bi = id;
+                    }
+                }
+            } else if (act) {
+                const int cnt = (int)((code >> 28) & 7u) + 1;
+                if (ls < cnt) {
+                    const int64_t c = (int64_t)(code & 0x0fffffffu) + ls;
+                    float bx[2 * D];
+#pragma unroll
+                    for (int k = 0; k < 2 * D; ++k) bx[k] = ((gflt)T.nbox)[c * 2 * D + k];
+                    child = ((gu32)T.nmeta)[c];
+                    lbf = ct_box_lb<D>(bx, qq, qlo, qhi);
+                    keep = true;
+                    ++n_box;
+                }
+            }
+            // the parts' best, then the survivors against it.  Wave-uniform skips: a group's
+            // lanes already share one best unless a lane examined a point this step, and with no
+            // survivor in the wave there is nothing to rank
+            if (__ballot(leaf)) {
+#pragma unroll
+                for (int off = G / 2; off > 0; off >>= 1) {
+                    const double od = __shfl_xor(bd, off, G);
+                    const int32_t oi = __shfl_xor(bi, off, G);
+                    if (nn_better(od, oi, bd, bi)) {
+                        bd = od;
+                        bi = oi;
+                    }
+                }
+            }
+            keep = keep && (double)lbf * (1.0 - 1e-12) <= bd;
+            const uint64_t wm = __ballot(keep);
+            const uint64_t gm = (wm >> base) & (G == 64 ? ~0ull : ((1ull << G) - 1));
+            const uint32_t mine = (uint32_t)(gm >> (part * 8)) & 0xffu;
+            const int below = __popcll(part + 1 < NW ? gm >> ((part + 1) * 8) : 0ull);
+            int rank = 0;
+            if (wm) {
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    const float o = __shfl(lbf, part * 8 + j, G);
+                    if (((mine >> j) & 1u) && (o > lbf || (o == lbf && j > ls))) ++rank;
+                }
+            }
+            if (keep) {
+                const int pos = sp + below + rank;
+                s_code[grp][pos] = child;
+                s_lb[grp][pos] = lbf;
+            }
+            sp += __popcll(gm);
+            __builtin_amdgcn_wave_barrier();
+        }
+    }
+    if (T.stats) {
+#pragma unroll
+        for (int off = G / 2; off > 0; off >>= 1) {
+            n_pts += __shfl_xor(n_pts, off, G);
+            n_box += __shfl_xor(n_box, off, G);
+        }
+        if (sub == 0) {
+            atomicAdd(T.stats + 0, (unsigned long long)n_pts);
+            atomicAdd(T.stats + 1, (unsigned long long)n_box);
+            atomicAdd(T.stats + 3, (unsigned long long)n_steps);  // (+ 2: the collide counters' [10])
+        }
+    }
+    if (sub == 0) {
+        out_ids[qi] = bi;
+        out_d2[qi] = bd;
+    }
+}
+
+template <int D, int BS, int W>
+__global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(D >= 15 ? 4 : 8))) void k_ct_nn1(
+    CellTreeDev T, const double *__restrict__ q, int64_t nq, int32_t *__restrict__ out_ids, double *__restrict__ out_d2) {
+    ct_walk<D, BS, W>(T, q, nq, out_ids, out_d2, blockIdx.x);
+}
+
+// Many trees in one launch (mpt_rrt_step_many: one engine per independent seed).  Jobs are
+// dealt to XCDs: workgroup b runs on XCD b % 8, so job j takes the workgroups of XCD j % 8
+// and its tree stays in that XCD's L2.  8 waves per SIMD for d <= 7; d = 15 at 4 (registers).
+template <int D, int BS, int W>
+__global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(D >= 15 ? 4 : 8))) void k_ct_nn1_jobs(
+    const CtNnJob *__restrict__ jobs, int32_t n_jobs, int64_t nq, int64_t blocks_per_job) {
+    constexpr int kXcd = 8;
+    const int64_t xcd = blockIdx.x % kXcd, slot = blockIdx.x / kXcd;
+    const int64_t job = xcd + kXcd * (slot / blocks_per_job);
+    if (job >= n_jobs) return;
+    const CtNnJob &J = jobs[job];
+    ct_walk<D, BS, W>(J.T, J.q, nq, J.ids, J.d2, slot % blocks_per_job);
+}
+
+}  // namespace
+
+// ---- host ----
+
+CtPlan make_ct_plan(int32_t d, const double *lo, const double *hi, int32_t spatial) {
+    CtPlan P{};
+    double ext[kCtMaxDim] = {}, emax = 0.0;
+    for (int j = 0; j < d; ++j) {
+        ext[j] = hi[j] > lo[j] ? hi[j] - lo[j] : 0.0;
+        emax = std::max(emax, ext[j]);
+    }
+    auto bits_of = [&](int j, double h, int k) {
+        int b = 0;
+        while (b < k && std::ldexp(h, b) < ext[j]) ++b;
+        return b;
+    };
+    int kstar = 0;
+    for (int k = 1; emax > 0.0 && k <= 31; ++k) {
+        const double h = std::ldexp(emax, -k);
+        int tot = 0;
+        for (int j = 0; j < d; ++j) tot += bits_of(j, h, k);
+        if (tot > kCtBits) break;
+        kstar = k;
+    }
+    int b[kCtMaxDim] = {}, bmax = 0;
+    for (int j = 0; j < d; ++j) {
+        b[j] = kstar > 0 ? bits_of(j, std::ldexp(emax, -kstar), kstar) : 0;
+        bmax = std::max(bmax, b[j]);
+        P.lo[j] = lo[j];
+        P.qmax[j] = b[j] > 0 ? (uint32_t)((1ull << b[j]) - 1) : 0u;
+        P.scale[j] = b[j] > 0 ? std::ldexp(1.0, b[j]) / ext[j] : 0.0;
+    }
+    int n = 0;
+    for (int l = bmax - 1; l >= 0; --l)
+        for (int j = 0; j < d; ++j)
+            if (b[j] > l) {
+                P.dim[n] = (int8_t)j;
+                P.bit[n] = (int8_t)l;
+                ++n;
+            }
+    P.n = n;
+    // seed slots: every dim's minimum and maximum, then directions over the first `spatial`
+    // dims spread evenly (a Fibonacci lattice on the sphere; the circle for two dims)
+    int h = 0;
+    for (int j = 0; j < d && h + 1 < kCtHull; ++j) {
+        P.hkind[h] = 1;
+        P.hdim[h++] = (int8_t)j;
+        P.hkind[h] = 2;
+        P.hdim[h++] = (int8_t)j;
+    }
+    const int sd = std::max(1, std::min<int>(spatial, std::min(d, 3)));
+    const int nd = kCtHull - h;
+    for (int k = 0; k < nd; ++k, ++h) {
+        double u[3] = {0.0, 0.0, 0.0};
+        if (sd == 3) {
+            const double z = 1.0 - (2.0 * k + 1.0) / nd, r = std::sqrt(std::max(0.0, 1.0 - z * z));
+            const double phi = k * 2.399963229728653;  // the golden angle
+            u[0] = r * std::cos(phi);
+            u[1] = r * std::sin(phi);
+            u[2] = z;
+        } else if (sd == 2) {
+            const double a = 2.0 * M_PI * (k + 0.5) / nd;
+            u[0] = std::cos(a);
+            u[1] = std::sin(a);
+        } else {
+            u[0] = (k & 1) ? 1.0 : -1.0;
+        }
+        P.hkind[h] = 0;
+        P.hdim[h] = 0;
+        for (int j = 0; j < 3; ++j) P.hdir[h][j] = (float)u[j];
+    }
+    P.n_hull = h;
+    return P;
+}
+
+void CellTree::release() {
+    void *ps[] = {plan, cnt, bpts, bids, bcnt, bcode, bbox, nbox, nmeta, ucode, lflag, dir_code[0], dir_code[1], dir_bk[0], dir_bk[1],
+                  ncode, ccode, scode, edir_code, nrow, crow, npos, nseg, seg_pos, srow, sseg, slead, srank, edir_bk,
+                  edir_pos, seg, hull_keys, ibox, hull_pts, hull_ids, fhi, flo, fk0, fk1, fv0, fv1, fflag, fleaf, ftemp};
+    for (void *p : ps)
+        if (p) (void)hipFree(p);
+}
+
+CellTree::~CellTree() { release(); }
+
+void CellTree::reserve(int64_t c, int32_t d) {
+    if (c <= cap_ && d == dim) return;
+    if (d != 3 && d != 7 && d != 15) throw Error{1, "cell tree: state dim must be 3, 7 or 15"};
+    if (c >= (int64_t(1) << 26)) throw Error{1, "cell tree: capacity too large"};  // node indices < 2^28
+    hip_check(hipDeviceSynchronize(), "sync");  // the old buffers may still be in use
+    release();
+    *this = CellTree();
+    c = std::max<int64_t>(c, 64);
+    cap_ = c;
+    dim = d;
+    bcap = (int32_t)(c + 1);  // every bucket holds at least one point, an empty tree one bucket
+    const int64_t nodes = 2 * (int64_t)bcap + 64;  // each level at most half the one below, or runs of 8
+    auto al = [](void **p, size_t bytes, const char *what) { hip_check(hipMalloc(p, std::max<size_t>(bytes, 16)), what); };
+    al((void **)&plan, sizeof(CtPlan), "ct plan");
+    al((void **)&cnt, sizeof(CtCounts), "ct counts");
+    al((void **)&bpts, sizeof(double) * bcap * kCtCap * d, "ct bucket rows");
+    al((void **)&bids, sizeof(int32_t) * bcap * kCtCap, "ct bucket ids");
+    al((void **)&bcode, sizeof(uint64_t) * 2 * bcap * kCtCap, "ct bucket codes");
+    al((void **)&bcnt, sizeof(int32_t) * bcap, "ct bucket counts");
+    al((void **)&bbox, sizeof(float) * 2 * d * bcap, "ct bucket boxes");
+    al((void **)&nbox, sizeof(float) * 2 * d * nodes, "ct node boxes");
+    al((void **)&nmeta, sizeof(uint32_t) * nodes, "ct node codes");
+    al((void **)&ucode, sizeof(uint64_t) * 2 * nodes, "ct node cell codes");
+    al((void **)&lflag, sizeof(int32_t) * nodes, "ct level scratch");
+    for (int k = 0; k < 2; ++k) {
+        al((void **)&dir_code[k], sizeof(uint64_t) * 2 * bcap, "ct directory");
+        al((void **)&dir_bk[k], sizeof(int32_t) * bcap, "ct directory");
+    }
+    al((void **)&ncode, sizeof(uint64_t) * 2 * kCtSeg, "ct new codes");
+    al((void **)&ccode, sizeof(uint64_t) * 2 * kCtSeg, "ct chunk codes");
+    al((void **)&nrow, sizeof(int32_t) * kCtSeg, "ct new rows");
+    al((void **)&crow, sizeof(int32_t) * kCtSeg, "ct chunk rows");
+    al((void **)&npos, sizeof(int32_t) * kCtSeg, "ct positions");
+    al((void **)&nseg, sizeof(int32_t) * kCtSeg, "ct segments");
+    al((void **)&seg, sizeof(int4) * kCtSeg, "ct segments");
+    al((void **)&seg_pos, sizeof(int32_t) * kCtSeg, "ct segments");
+    al((void **)&scode, sizeof(uint64_t) * 2 * kCtScratch, "ct scratch");
+    al((void **)&srow, sizeof(int32_t) * kCtScratch, "ct scratch");
+    al((void **)&sseg, sizeof(int32_t) * kCtScratch, "ct scratch");
+    al((void **)&slead, sizeof(int32_t) * kCtScratch, "ct scratch");
+    al((void **)&srank, sizeof(int32_t) * kCtScratch, "ct scratch");
+    al((void **)&edir_code, sizeof(uint64_t) * 2 * kCtScratch, "ct new entries");
+    al((void **)&edir_bk, sizeof(int32_t) * kCtScratch, "ct new entries");
+    al((void **)&edir_pos, sizeof(int32_t) * kCtScratch, "ct new entries");
+    al((void **)&hull_keys, sizeof(unsigned long long) * kCtHull, "ct seeds");
+    al((void **)&hull_pts, sizeof(double) * kCtHull * d, "ct seeds");
+    al((void **)&hull_ids, sizeof(int32_t) * kCtHull, "ct seeds");
+    al((void **)&ibox, sizeof(unsigned long long) * 2 * kCtMaxDim, "ct box");
+    for (uint64_t **p : {&fhi, &flo, &fk0, &fk1}) al((void **)p, sizeof(uint64_t) * 2 * c, "ct full sort");
+    for (int32_t **p : {&fv0, &fv1, &fflag, &fleaf}) al((void **)p, sizeof(int32_t) * c, "ct full sort");
+    size_t tb = 0, tb2 = 0;
+    hip_check(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, flo, fk0, fv0, fv1, (int)c, 0, 64), "ct sort size");
+    hip_check(hipcub::DeviceScan::ExclusiveSum(nullptr, tb2, fflag, fleaf, (int)c), "ct scan size");
+    ftemp_bytes = std::max(tb, tb2);
+    al(&ftemp, ftemp_bytes, "ct sort temp");
+    hip_check(hipMemset(cnt, 0, sizeof(CtCounts)), "ct counts zero");
+    hip_check(hipDeviceSynchronize(), "ct init sync");  // the null stream vs the caller's stream
+}
+
+CtJob CellTree::prepare(const double *pts, int64_t n_upper, const int64_t *n_dev, int32_t d, const double *lo,
+                        const double *hi, int32_t spatial, bool full, int64_t grow, hipStream_t stream,
+                        const SpreadOut *spread, unsigned long long *err) {
+    if (d != dim || n_upper > cap_) throw Error{1, "cell tree: not reserved for this size"};
+    if (n_upper < 1) throw Error{1, "cell tree: empty layout"};
+    bool same = plan_set;
+    for (int j = 0; j < d && same; ++j) same = plan_lo[j] == lo[j] && plan_hi[j] == hi[j];
+    if (!same) {
+        const CtPlan P = make_ct_plan(d, lo, hi, spatial);
+        hip_check(hipMemcpy(plan, &P, sizeof(P), hipMemcpyHostToDevice), "ct plan");
+        for (int j = 0; j < d; ++j) {
+            plan_lo[j] = lo[j];
+            plan_hi[j] = hi[j];
+        }
+        plan_set = true;
+        full = true;
+    }
+    const int old = cur, nw = cur ^ 1;
+    if (full) {
+        // every point: box, codes and seed offers, a two-pass stable sort by (code, row), the
+        // leaf rule, the leaves' ranks, buckets and directory (into the round's old directory)
+        hipLaunchKernelGGL(k_ct_box_reset, dim3(1), dim3(64), 0, stream, ibox);
+        hip_check(hipMemsetAsync(hull_keys, 0, sizeof(unsigned long long) * kCtHull, stream), "seed reset");
+        const unsigned blocks = (unsigned)((n_upper + 255) / 256);
+        hipLaunchKernelGGL(d == 3 ? k_ct_codes_all<3> : d == 7 ? k_ct_codes_all<7> : k_ct_codes_all<15>, dim3(blocks),
+                           dim3(64 * kCtWaves), 0, stream, pts, n_upper, n_dev, (const CtPlan *)plan, fhi, flo, fv0,
+                           hull_keys, ibox);
+        hip_check(hipGetLastError(), "k_ct_codes_all");
+        size_t tb = ftemp_bytes;
+        hip_check(hipcub::DeviceRadixSort::SortPairs(ftemp, tb, flo, fk0, fv0, fv1, (int)n_upper, 0, 64, stream),
+                  "ct sort low");
+        hipLaunchKernelGGL(k_ct_gather_hi, dim3(blocks), dim3(256), 0, stream, fhi, fv1, n_upper, fk1);
+        tb = ftemp_bytes;
+        hip_check(hipcub::DeviceRadixSort::SortPairs(ftemp, tb, fk1, fk0, fv1, fv0, (int)n_upper, 0, 64, stream),
+                  "ct sort high");
+        // (hi, lo) pairs of the sorted order into fk1 (n_upper * 2 words: fk1 is sized 2c)
+        hipLaunchKernelGGL(k_ct_pack, dim3(blocks), dim3(256), 0, stream, fk0, flo, fv0, n_upper, n_dev, fk1);
+        hipLaunchKernelGGL(k_ct_bulk_flags, dim3(blocks), dim3(256), 0, stream, fk1, fv0, n_upper, n_dev, fflag);
+        tb = ftemp_bytes;
+        hip_check(hipcub::DeviceScan::ExclusiveSum(ftemp, tb, fflag, fleaf, (int)n_upper, stream), "ct leaf scan");
+        hipLaunchKernelGGL(d == 3 ? k_ct_bulk_fill<3> : d == 7 ? k_ct_bulk_fill<7> : k_ct_bulk_fill<15>, dim3(blocks),
+                           dim3(256), 0, stream, pts, fk1, fv0, fflag, fleaf, n_upper, n_dev, bpts, bids, bcode, bcnt,
+                           bbox, dir_code[old], dir_bk[old], cnt);
+        hip_check(hipGetLastError(), "k_ct_bulk_fill");
+    }
+    t.d = d;
+    t.n_bound = std::max<int64_t>(std::min<int64_t>(n_upper, bcap), 1);
+    t.n_dev = n_dev;
+    t.root = &cnt->root;
+    t.nmeta = nmeta;
+    t.nbox = nbox;
+    t.bpts = bpts;
+    t.bids = bids;
+    t.hull_pts = hull_pts;
+    t.hull_ids = hull_ids;
+    t.stats = nullptr;
+    cur = nw;
+    CtJob J{};
+    J.T = t;
+    J.pts = pts;
+    J.plan = plan;
+    J.cnt = cnt;
+    J.bcap = bcap;
+    J.mb = full ? 0 : (int32_t)std::min<int64_t>(std::max<int64_t>(grow, 0), kCtSeg);
+    J.bpts = bpts;
+    J.bids = bids;
+    J.bcode = bcode;
+    J.bcnt = bcnt;
+    J.bbox = bbox;
+    J.odir_code = dir_code[old];
+    J.odir_bk = dir_bk[old];
+    J.ndir_code = dir_code[nw];
+    J.ndir_bk = dir_bk[nw];
+    J.nmeta = nmeta;
+    J.nbox = nbox;
+    J.ucode = ucode;
+    J.lflag = lflag;
+    J.ncode = ncode;
+    J.nrow = nrow;
+    J.ccode = ccode;
+    J.crow = crow;
+    J.npos = npos;
+    J.nseg = nseg;
+    J.seg = seg;
+    J.seg_pos = seg_pos;
+    J.scode = scode;
+    J.srow = srow;
+    J.sseg = sseg;
+    J.slead = slead;
+    J.srank = srank;
+    J.edir_code = edir_code;
+    J.edir_bk = edir_bk;
+    J.edir_pos = edir_pos;
+    J.hull_keys = hull_keys;
+    J.hull_pts = hull_pts;
+    J.hull_ids = hull_ids;
+    J.ibox = ibox;
+    if (spread) J.sp = *spread;
+    J.err = err;
+    return J;
+}
+
+void launch_ct_jobs(const CtJob *d_jobs, const CtJob *h_jobs, int32_t n, int32_t d, hipStream_t stream) {
+    if (n <= 0) return;
+    if (d != 3 && d != 7 && d != 15) throw Error{1, "cell tree: state dim must be 3, 7 or 15"};
+    CtJobs js{n == 1 ? nullptr : d_jobs, h_jobs[0]};
+    // grids from the host's bounds (a workgroup that only learns on the device that it has
+    // nothing to do still pays its dependent count loads: sized by the real work, not the caps)
+    int64_t max_n = 0, mb = 0;
+    for (int32_t j = 0; j < n; ++j) {
+        max_n = std::max(max_n, h_jobs[j].T.n_bound);
+        mb = std::max<int64_t>(mb, h_jobs[j].mb);
+    }
+    auto by_d = [&](auto k3, auto k7, auto k15) { return d == 3 ? k3 : d == 7 ? k7 : k15; };
+    const unsigned yn = (unsigned)n;
+    if (mb > 0) {
+        const unsigned b256 = (unsigned)((mb + 255) / 256);
+        hipLaunchKernelGGL(by_d(k_ct_ncodes<3>, k_ct_ncodes<7>, k_ct_ncodes<15>), dim3(b256, yn), dim3(64 * kCtWaves), 0,
+                           stream, js);
+        hip_check(hipGetLastError(), "k_ct_ncodes");
+        const unsigned chunks = (unsigned)((mb + kCtChunk - 1) / kCtChunk);
+        hipLaunchKernelGGL(k_ct_csort, dim3((chunks + kCtChunkWaves - 1) / kCtChunkWaves, yn), dim3(64 * kCtChunkWaves), 0,
+                           stream, js);
+        hipLaunchKernelGGL(k_ct_crank, dim3(b256, yn), dim3(256), 0, stream, js);
+        hipLaunchKernelGGL(k_ct_locate, dim3(b256, yn), dim3(256), 0, stream, js);
+        hipLaunchKernelGGL(k_ct_segments, dim3(1, yn), dim3(kCtSegThreads), 0, stream, js);
+        hipLaunchKernelGGL(by_d(k_ct_apply<3>, k_ct_apply<7>, k_ct_apply<15>), dim3(b256, yn), dim3(256), 0, stream, js);
+        hip_check(hipGetLastError(), "k_ct_apply");
+        // the split elements (at most 9 a new point) strided over the new points' workgroups
+        hipLaunchKernelGGL(k_ct_split_flags, dim3(b256, yn), dim3(256), 0, stream, js);
+        hipLaunchKernelGGL(k_ct_split_scan, dim3(1, yn), dim3(kCtScanThreads), 0, stream, js);
+        hipLaunchKernelGGL(by_d(k_ct_split_fill<3>, k_ct_split_fill<7>, k_ct_split_fill<15>), dim3(b256, yn), dim3(256),
+                           0, stream, js);
+        hip_check(hipGetLastError(), "k_ct_split_fill");
+    }
+    // the directory (at most the indexed points' count of entries, ~1/5 of them in practice)
+    hipLaunchKernelGGL(by_d(k_ct_dmerge<3>, k_ct_dmerge<7>, k_ct_dmerge<15>),
+                       dim3((unsigned)std::max<int64_t>(1, (max_n + 2047) / 2048), yn), dim3(256), 0, stream, js);
+    hip_check(hipGetLastError(), "k_ct_dmerge");
+    hipLaunchKernelGGL(by_d(k_ct_levels<3>, k_ct_levels<7>, k_ct_levels<15>), dim3(1, yn), dim3(kCtLevelThreads), 0,
+                       stream, js);
+    hip_check(hipGetLastError(), "k_ct_levels");
+}
+
+template <int W>
+static void launch_ct_nn1_w(const CellTreeDev &T, const double *q, int64_t nq, int32_t *ids, double *d2,
+                            hipStream_t stream) {
+    constexpr int BS = 64;
+    const dim3 grid((unsigned)((nq * 8 * W + BS - 1) / BS));
+    switch (T.d) {
+        case 3: hipLaunchKernelGGL((k_ct_nn1<3, BS, W>), grid, dim3(BS), 0, stream, T, q, nq, ids, d2); break;
+        case 7: hipLaunchKernelGGL((k_ct_nn1<7, BS, W>), grid, dim3(BS), 0, stream, T, q, nq, ids, d2); break;
+        case 15: hipLaunchKernelGGL((k_ct_nn1<15, BS, W>), grid, dim3(BS), 0, stream, T, q, nq, ids, d2); break;
+        default: throw Error{1, "cell tree: state dim must be 3, 7 or 15"};
+    }
+    hip_check(hipGetLastError(), "k_ct_nn1 launch");
+}
+
+// nodes a walk step: eight (one query a wave) for d <= 7, four for d = 15 (its registers)
+static int ct_width(int32_t d) { return d <= 7 ? 8 : 4; }
+
+void launch_ct_nn1(const CellTreeDev &T, const double *q, int64_t nq, int32_t *ids, double *d2, hipStream_t stream) {
+    if (nq <= 0) return;
+    if (ct_width(T.d) == 8) launch_ct_nn1_w<8>(T, q, nq, ids, d2, stream);
+    else launch_ct_nn1_w<4>(T, q, nq, ids, d2, stream);
+}
+
+template <int W>
+static void launch_ct_nn1_jobs_w(const CtNnJob *d_jobs, int32_t n_jobs, int32_t d, int64_t nq, hipStream_t stream) {
+    constexpr int BS = 64;
+    const int64_t bpj = (nq * 8 * W + BS - 1) / BS;
+    const int64_t groups = (n_jobs + 7) / 8;
+    const dim3 grid((unsigned)(8 * groups * bpj));
+    switch (d) {
+        case 3: hipLaunchKernelGGL((k_ct_nn1_jobs<3, BS, W>), grid, dim3(BS), 0, stream, d_jobs, n_jobs, nq, bpj); break;
+        case 7: hipLaunchKernelGGL((k_ct_nn1_jobs<7, BS, W>), grid, dim3(BS), 0, stream, d_jobs, n_jobs, nq, bpj); break;
+        case 15: hipLaunchKernelGGL((k_ct_nn1_jobs<15, BS, W>), grid, dim3(BS), 0, stream, d_jobs, n_jobs, nq, bpj); break;
+        default: throw Error{1, "cell tree: state dim must be 3, 7 or 15"};
+    }
+    hip_check(hipGetLastError(), "k_ct_nn1_jobs launch");
+}
+
+void launch_ct_nn1_jobs(const CtNnJob *d_jobs, int32_t n_jobs, int32_t d, int64_t nq, hipStream_t stream) {
+    if (nq <= 0 || n_jobs <= 0) return;
+    if (ct_width(d) == 8) launch_ct_nn1_jobs_w<8>(d_jobs, n_jobs, d, nq, stream);
+    else launch_ct_nn1_jobs_w<4>(d_jobs, n_jobs, d, nq, stream);
+}
+
+}  // namespace mpt

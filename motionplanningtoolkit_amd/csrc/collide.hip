@@ -81,8 +81,7 @@ void launch_collide(const EnvDev &env, const AgentDev *d_links, const CollideWor
     static const int max_blocks = [] {
         int dev = 0, cus = 256;
         if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-        int per_cu = 6;  // ~2 workgroups per CU resident (VGPR-limited) x 3 rounds
-        if (const char *s = getenv("MPT_COLLIDE_BLOCKS_PER_CU")) per_cu = atoi(s) > 0 ? atoi(s) : per_cu;
+        const int per_cu = 6;  // ~2 workgroups per CU resident (VGPR-limited) x 3 rounds
         return cus * per_cu;
     }();
     const int32_t n_lds = env.n_nodes < kLdsNodes ? env.n_nodes : kLdsNodes;

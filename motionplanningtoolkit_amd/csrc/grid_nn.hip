@@ -457,31 +457,21 @@ void GridIndex::build(const double *pts, int64_t n_upper, const int64_t *n_dev, 
     n_max = n_upper;
     if (!counts_zero) hip_check(hipMemsetAsync(counts, 0, sizeof(int32_t) * (size_t)cells_cap, stream), "grid memset");
     counts_zero = false;
-    // queries per bucketing thread (MPT_GRID_QPT 1 / 2 / 4) and whether those workgroups lead
-    // the launch (MPT_GRID_QFIRST), A/B knobs: config 2's build 28.2 (4) -> 27.0 (2) / 27.1 (1)
-    // us, 380 -> 383 M valid ext/s; leading workgroups no different
-    static const int qpt = getenv("MPT_GRID_QPT") ? atoi(getenv("MPT_GRID_QPT")) : 2;
-    static const bool qfirst = getenv("MPT_GRID_QFIRST") && atoi(getenv("MPT_GRID_QFIRST")) != 0;
-    const int qpb = 256 * (qpt == 1 || qpt == 2 ? qpt : 4);
+    // two queries per bucketing thread, those workgroups after the points' (config 2's build
+    // 28.2 us with four, 27.0 with two, 27.1 with one; leading workgroups no different; round 3)
+    constexpr int kQpt = 2;
+    const int qpb = 256 * kQpt;
     const unsigned qblocks = qb ? (unsigned)((qb->nq + qpb - 1) / qpb) : 0u;
     if (n_upper > 0 || qblocks > 0) {
         const unsigned blocks = (unsigned)((n_upper + 255) / 256);
         const QueryBucketing q = qb ? *qb : QueryBucketing{};
-        const unsigned lead = qfirst ? qblocks : 0u;
         const SpreadOut sp = spread ? *spread : SpreadOut{};
         auto go = [&](auto kern) {
             hipLaunchKernelGGL(kern, dim3(blocks + qblocks), dim3(256), 0, stream, g, pts, d, n_upper, n_dev, cell_of,
-                               counts, sp, blocks, lead, q);
+                               counts, sp, blocks, 0u, q);
         };
-        if (spread) {
-            if (qpb == 256) go(k_grid_count<true, 1>);
-            else if (qpb == 512) go(k_grid_count<true, 2>);
-            else go(k_grid_count<true, 4>);
-        } else {
-            if (qpb == 256) go(k_grid_count<false, 1>);
-            else if (qpb == 512) go(k_grid_count<false, 2>);
-            else go(k_grid_count<false, 4>);
-        }
+        if (spread) go(k_grid_count<true, kQpt>);
+        else go(k_grid_count<false, kQpt>);
         hip_check(hipGetLastError(), "k_grid_count");
     }
     // the scan leaves every count zero again, so the next build needs no memset
@@ -489,16 +479,15 @@ void GridIndex::build(const double *pts, int64_t n_upper, const int64_t *n_dev, 
                      g.ncells + 1, stream, ZeroCounts{reinterpret_cast<uint32_t *>(counts)});
     if (n_upper > 0) {
         const unsigned blocks = (unsigned)((n_upper + 255) / 256);
-        // the state dims the engines use get a compile-time row (MPT_GRID_SCATTER_D=0: the
-        // run-time copy loop, A/B)
-        static const bool fixed_d = !getenv("MPT_GRID_SCATTER_D") || atoi(getenv("MPT_GRID_SCATTER_D")) != 0;
+        // the state dims the engines use get a compile-time row (the run-time copy loop waited
+        // on each coordinate)
         const SpreadOut sp = spread ? *spread : SpreadOut{};
         const int32_t n_part = spread ? (int32_t)blocks : 0;
         auto go = [&](auto kern) {
             hipLaunchKernelGGL(kern, dim3(blocks), dim3(256), 0, stream, pts, d, n_upper, n_dev, cell_of, cell_start,
                                spts, sids, sp, n_part);
         };
-        const int dd = fixed_d ? d : 0;
+        const int dd = d;
         if (spread) {
             if (dd == 3) go(k_grid_scatter<true, 3>);
             else if (dd == 7) go(k_grid_scatter<true, 7>);
@@ -1082,14 +1071,9 @@ static void grid_nn1_sorted_dg(const GridDev &G, const double *q, int64_t nq, co
     constexpr int QPW = 256 / GRP;
     int64_t wgs = (nq + QPW - 1) / QPW;
     wgs = (wgs + 7) / 8 * 8;
-    // records of d >= 8 (the snake's 120 B) are screened by their first MPT_NN_HEAD groups of
-    // four dims (A/B on config 3's NN: 0.617 ms unscreened, 0.566 at one group, 0.472 at two,
-    // 0.533 at three)
-    static const int head = getenv("MPT_NN_HEAD") ? atoi(getenv("MPT_NN_HEAD")) : 2;
-    if (D >= 8 && head == 1)
-        hipLaunchKernelGGL((k_grid_nn1_runs_sorted<D, GD, GRP, PTS, 1>), dim3((unsigned)wgs), dim3(256), 0, stream,
-                           G, q, nq, o, ids, d2);
-    else if (D >= 8 && head == 2)
+    // records of d >= 8 (the snake's 120 B) are screened by their first two groups of four dims
+    // (config 3's NN: 0.617 ms unscreened, 0.566 at one group, 0.472 at two, 0.533 at three)
+    if (D >= 8)
         hipLaunchKernelGGL((k_grid_nn1_runs_sorted<D, GD, GRP, PTS, 2>), dim3((unsigned)wgs), dim3(256), 0, stream,
                            G, q, nq, o, ids, d2);
     else
@@ -1120,15 +1104,14 @@ void launch_grid_nn1_sorted(const GridDev &G, int32_t d, const double *q, int64_
     hip_check(hipGetLastError(), "k_grid_nn1_runs_sorted launch");
 }
 
-// unsorted run-kernel launch; xcd: the slab variant (default for d = 15: the snake's 12 MB of
-// points are three L2s' worth, NN 0.85 -> 0.72 ms; config 2's tree gains less than the idle
-// groups cost, 54 -> 65 us).  MPT_NN1_XCD=0/1 overrides (scripts/ab.sh)
+// unsorted run-kernel launch; for d = 15 the XCD-slab variant (the snake's 12 MB of points are
+// three L2s' worth, NN 0.85 -> 0.72 ms; config 2's tree gains less than the idle groups cost,
+// 54 -> 65 us)
 template <int D, int GD>
 static void grid_nn1_runs_dg(const GridDev &G, const double *q, int64_t nq, int32_t *ids, double *d2,
                              hipStream_t stream) {
     constexpr int GRP = RunShape<D>::kGroup, PTS = RunShape<D>::kPts;
-    static const bool xcd = getenv("MPT_NN1_XCD") ? atoi(getenv("MPT_NN1_XCD")) == 1 : D >= 15;
-    if (xcd)
+    if (D >= 15)
         hipLaunchKernelGGL((k_grid_nn1_runs_xcd<D, GD, GRP, PTS>),
                            dim3((unsigned)(((nq + 6 * (256 / GRP) - 1) / (6 * (256 / GRP))) * 8)), dim3(256), 0,
                            stream, G, q, nq, ids, d2);
@@ -1151,36 +1134,22 @@ template <int D>
 static void grid_knn_d(const GridDev &G, int32_t d, const double *q, int64_t nq, int32_t k, int32_t *ids, double *d2,
                        hipStream_t stream) {
     const dim3 grid((unsigned)((nq + 255) / 256));
-    static const bool per_lane = getenv("MPT_NN1_PER_LANE") != nullptr;  // experiment knob
-    // 32 lanes per query and rings 0 + 1 as the first pass (the 27 cells of the 3^3 block in one
-    // step): 12 % faster than 16 lanes from ring 0 on config 2 (MPT_NN1_GROUP / _FIRST_RING: A/B)
-    static const int group = getenv("MPT_NN1_GROUP") ? atoi(getenv("MPT_NN1_GROUP")) : 32;
-    static const int first = getenv("MPT_NN1_FIRST_RING") ? atoi(getenv("MPT_NN1_FIRST_RING")) : 1;
-#define MPT_NN1_GROUP_LAUNCH(GRP, FIRST)                                                                        \
-    hipLaunchKernelGGL((k_grid_nn1_group<D, GRP, FIRST>), dim3((unsigned)((nq * GRP + 255) / 256)), dim3(256), 0, \
-                       stream, G, d, q, nq, ids, d2)
-    // cell-run kernel (default); MPT_NN1_KERNEL=cells: the cell-per-lane walk (A/B)
-    static const bool cells = getenv("MPT_NN1_KERNEL") && !strcmp(getenv("MPT_NN1_KERNEL"), "cells");
     if constexpr (D > 0) {
-        if (k == 1 && !per_lane && !cells) {
+        if (k == 1) {  // the cell-run kernel for the engines' state dims
             grid_nn1_runs_d<D>(G, q, nq, ids, d2, stream);
             return;
         }
     }
-    if (k == 1 && !per_lane && group == 32) {
-        if (first) MPT_NN1_GROUP_LAUNCH(32, 1); else MPT_NN1_GROUP_LAUNCH(32, 0);
-    } else if (k == 1 && !per_lane && group == 8) {
-        MPT_NN1_GROUP_LAUNCH(8, 0);
-    } else if (k == 1 && !per_lane) {
-        if (first) MPT_NN1_GROUP_LAUNCH(16, 1); else MPT_NN1_GROUP_LAUNCH(16, 0);
-    } else if (k == 1) {
-        hipLaunchKernelGGL((k_grid_knn<D, 1>), grid, dim3(256), 0, stream, G, d, q, nq, k, ids, d2);
+    if (k == 1) {
+        // any other d: 32 lanes per query and rings 0 + 1 as the first pass (the 27 cells of the
+        // 3^3 block in one step): 12 % faster than 16 lanes from ring 0 on config 2
+        hipLaunchKernelGGL((k_grid_nn1_group<D, 32, 1>), dim3((unsigned)((nq * 32 + 255) / 256)), dim3(256), 0, stream,
+                           G, d, q, nq, ids, d2);
     } else if (k <= 16) {
         hipLaunchKernelGGL((k_grid_knn<D, 16>), grid, dim3(256), 0, stream, G, d, q, nq, k, ids, d2);
     } else {
         hipLaunchKernelGGL((k_grid_knn<D, 32>), grid, dim3(256), 0, stream, G, d, q, nq, k, ids, d2);
     }
-#undef MPT_NN1_GROUP_LAUNCH
 }
 
 void launch_grid_knn(const GridDev &G, int32_t d, const double *q, int64_t nq, int32_t k, int32_t *ids, double *d2,

@@ -1816,7 +1816,8 @@ void launch_tree_nn1_jobs(const PtJob *d_jobs, int32_t n_jobs, int32_t d, int64_
     // - / - / 1.86 / 1.59 ms, 64 seeds - / - / 3.36 / 2.97 ms, 256 seeds (1 M queries) 12.83 /
     // 12.53 / 11.26 / 10.80 ms (round 3, before the seeds).
     const int w = pt_nn_width(d, (int64_t)n_jobs * nq);
-    if (w == 8) launch_tree_nn1_jobs_bs<64, 8>(d_jobs, n_jobs, d, nq, stream);
+    if (w == 2) launch_tree_nn1_jobs_bs<64, 2>(d_jobs, n_jobs, d, nq, stream);
+    else if (w == 8) launch_tree_nn1_jobs_bs<64, 8>(d_jobs, n_jobs, d, nq, stream);
     else if (w == 4) launch_tree_nn1_jobs_bs<64, 4>(d_jobs, n_jobs, d, nq, stream);
     else launch_tree_nn1_jobs_bs<64, 1>(d_jobs, n_jobs, d, nq, stream);
 }

@@ -284,8 +284,9 @@ extern "C" mpt_status mpt_prm_connect(const mpt_env *env, const mpt_agent *agent
             w.n_units = P;
             w.verdict = d_v;
             const int32_t mc = std::max(1, ag.n_clusters);
-            static const char *path = getenv("MPT_PRM_COLLIDE");  // sweep (default) | split | fused
-            if (!path || std::string(path) == "sweep") {
+            // the sweep collide (one launch over the edges' poses); mpt_set_collide_mode's
+            // FUSED: the one-kernel traversal
+            if (collide_mode() != MPT_COLLIDE_FUSED) {
                 unsigned long long *st = nullptr;
                 if (g_prm_stats_on) {
                     st = reinterpret_cast<unsigned long long *>(S.temp.get(64) );
@@ -300,11 +301,8 @@ extern "C" mpt_status mpt_prm_connect(const mpt_env *env, const mpt_agent *agent
                     g_prm_stats[4] = (uint64_t)E;
                     g_prm_stats[5] = (uint64_t)P;
                 }
-            } else if (std::string(path) == "fused") {
-                launch_collide(env_dev(env), d_link, w, stream);
             } else {
-                S.cs.ensure(P, mc);
-                launch_collide_split(env_dev(env), d_link, mc, w, S.cs, stream);
+                launch_collide(env_dev(env), d_link, w, stream);
             }
         }
         hip_check(hipEventRecord(ev[3], stream), "event");

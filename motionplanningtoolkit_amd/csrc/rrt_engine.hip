@@ -26,7 +26,7 @@
 
 #include "../../include/mpt.h"
 #include "grid_nn.h"
-#include "point_tree.h"
+#include "cell_tree.h"
 #include "mpt_internal.h"
 #include "collide_common.h"
 
@@ -638,7 +638,7 @@ struct mpt_rrt {
     // NN structure over the round's snapshot (grid_nn.hip), rebuilt every round
     int32_t nn_mode = MPT_NN_AUTO;
     std::unique_ptr<GridIndex> grid;
-    std::unique_ptr<PointTree> ptree;  // MPT_NN_TREE (point_tree.hip)
+    std::unique_ptr<CellTree> ctree;  // MPT_NN_TREE (cell_tree.hip)
     int32_t grid_gd = 0, grid_dims[3] = {0, 0, 0};
     double ppc = 0.0;  // grid points per cell; <= 0: 2, floored by the expected NN distance
     // MPT_NN_AUTO feedback: the live nodes' spatial spread, a by-product of the round's index
@@ -792,7 +792,7 @@ extern "C" mpt_status mpt_rrt_create(const mpt_env *env, const mpt_agent *agent,
             hip_check(hipMalloc(&r->d_counters, sizeof(unsigned long long) * 8), "alloc counters");
             hip_check(hipMemset(r->d_counters, 0, sizeof(unsigned long long) * 8), "memset counters");
             r->grid.reset(new GridIndex());
-            r->ptree.reset(new PointTree());
+            r->ctree.reset(new CellTree());
             r->grid_gd = agent_kind == MPT_AGENT_SNAKE ? 2 : 3;
             for (int j = 0; j < 3; ++j) r->grid_dims[j] = j;
         } catch (...) {
@@ -904,11 +904,10 @@ struct StepCtx {
 // this round's incremental tree build (a full rebuild when the index is stale or more nodes
 // were appended since its last build than one round's merge takes: the host's bound, which the
 // build's first kernel checks on the device into counters[6])
-PtIncJob tree_inc_job(mpt_rrt *r, hipStream_t stream, const SpreadOut *spread) {
-    const bool full = !r->pt_inc_ok || r->pt_grow > kPtIncSeg;
-    PtIncJob J = r->ptree->prepare_inc(r->d_nodes, r->n_upper, r->d_n, r->p.d, r->p.lo, r->p.hi, r->grid_gd, full,
-                                       stream, spread);
-    J.err = r->d_counters + 6;
+CtJob tree_inc_job(mpt_rrt *r, hipStream_t stream, const SpreadOut *spread) {
+    const bool full = !r->pt_inc_ok || r->pt_grow > kCtSeg;
+    CtJob J = r->ctree->prepare(r->d_nodes, r->n_upper, r->d_n, r->p.d, r->p.lo, r->p.hi, r->grid_gd, full,
+                                r->pt_grow, stream, spread, r->d_counters + 6);
     r->pt_inc_ok = true;
     r->pt_grow = 0;
     return J;
@@ -986,9 +985,8 @@ StepCtx step_head(mpt_rrt *r, int32_t K, hipStream_t stream, bool defer_tree = f
     // k_steer lists the live units for the two-phase collide (FCL's object-level AABB test)
     const bool live_list = collide_mode() != MPT_COLLIDE_FUSED && p.pmax * p.L <= 64;
     // grid rounds: the index build also buckets the samples along the grid's first dim, so the
-    // 1-NN launch can deal them to the XCDs by x-slab (MPT_NN_SORT=0: the unsorted launch, A/B)
-    static const bool sort_q = !getenv("MPT_NN_SORT") || atoi(getenv("MPT_NN_SORT")) != 0;
-    if (use_grid && sort_q && (p.d == 3 || p.d == 7 || p.d == 15)) {
+    // 1-NN launch can deal them to the XCDs by x-slab
+    if (use_grid && (p.d == 3 || p.d == 7 || p.d == 15)) {
         if (r->q_cap < K) {
             if (r->d_qlist) hip_check(hipFree(r->d_qlist), "hipFree");
             hip_check(hipMalloc(&r->d_qlist, sizeof(int32_t) * (size_t)kQueryBuckets * K), "alloc query lists");
@@ -1025,14 +1023,14 @@ StepCtx step_head(mpt_rrt *r, int32_t K, hipStream_t stream, bool defer_tree = f
     SpreadOut spread;
     const bool want_spread = spread_request(r, use_tree || use_grid, spread);
     if (use_tree) {
-        r->ptree->inc_reserve(r->cap, p.d);  // once: no allocation (device sync) in later rounds
+        r->ctree->reserve(r->cap, p.d);  // once: no allocation (device sync) in later rounds
         if (defer_tree) {
             c.defer_tree = true;
             c.want_spread = want_spread;
             c.spread = spread;
         } else {
-            PtIncJob J = tree_inc_job(r, stream, want_spread ? &spread : nullptr);
-            launch_tree_inc_jobs(nullptr, &J, 1, p.d, stream);
+            CtJob J = tree_inc_job(r, stream, want_spread ? &spread : nullptr);
+            launch_ct_jobs(nullptr, &J, 1, p.d, stream);
         }
     } else if (use_grid) {
         // spatial dims of the agent's tree state: x, y, z (omni, blimp) or x, y (snake);
@@ -1043,8 +1041,8 @@ StepCtx step_head(mpt_rrt *r, int32_t K, hipStream_t stream, bool defer_tree = f
             hi[j] = p.hi[r->grid_dims[j]];
         }
         // cells of ~2 points, but not much finer than the expected NN distance over all
-        // state dims (MPT_NN_HMIN_K: the fraction; A/B knob)
-        static const double hk = getenv("MPT_NN_HMIN_K") ? atof(getenv("MPT_NN_HMIN_K")) : kGridHminK;
+        // state dims (kGridHminK: the fraction)
+        const double hk = kGridHminK;
         const double ppc = r->ppc > 0 ? r->ppc : 2.0;
         const double hmin_n = r->ppc > 0 ? 0.0 : hk * expected_nn_distance(p.d, p.lo, p.hi, r->n_upper);
         const double hmin_c = r->ppc > 0 ? 0.0 : hk * expected_nn_distance(p.d, p.lo, p.hi, r->cap);
@@ -1088,8 +1086,8 @@ StepCtx step_head(mpt_rrt *r, int32_t K, hipStream_t stream, bool defer_tree = f
 // a deferred tree build that did not join a joint build: run it on the engine's stream
 void build_deferred(mpt_rrt *r, hipStream_t stream, const StepCtx &c) {
     {
-        PtIncJob J = tree_inc_job(r, stream, c.want_spread ? &c.spread : nullptr);
-        launch_tree_inc_jobs(nullptr, &J, 1, r->p.d, stream);
+        CtJob J = tree_inc_job(r, stream, c.want_spread ? &c.spread : nullptr);
+        launch_ct_jobs(nullptr, &J, 1, r->p.d, stream);
     }
     if (c.want_spread) hip_check(hipEventRecord(r->ev_spread, stream), "spread event");
     c.mark(2, stream);
@@ -1099,9 +1097,9 @@ void step_nn(mpt_rrt *r, int32_t K, hipStream_t stream, const StepCtx &c) {
     const EngineParams &p = r->p;
     const bool use_tree = c.use_tree, use_grid = c.use_grid;
     if (use_tree) {
-        PointTreeDev T = r->ptree->dev();
+        CellTreeDev T = r->ctree->dev();
         T.stats = r->stats_on ? r->d_cstats + 8 : nullptr;
-        launch_tree_nn1(T, r->d_samples, K, r->d_nn, r->d_nnd2, stream);
+        launch_ct_nn1(T, r->d_samples, K, r->d_nn, r->d_nnd2, stream);
     } else if (use_grid) {
         GridDev G = r->grid->dev();
         G.stats = r->stats_on ? r->d_cstats + 8 : nullptr;
@@ -1154,16 +1152,14 @@ void step_tail(mpt_rrt *r, int32_t K, hipStream_t stream, const StepCtx &c) {
         c.mark(6, stream);
         c.mark(7, stream);
     } else {
-        // the overflow re-run moves into the append launch (MPT_OVF_IN_APPEND=0: its own
-        // k_overflow launch, A/B)
-        static const bool defer = !(getenv("MPT_OVF_IN_APPEND") && atoi(getenv("MPT_OVF_IN_APPEND")) == 0);
-        if (defer && !r->d_bar) {
+        // the overflow re-run moves into the append launch (no k_overflow launch of its own)
+        if (!r->d_bar) {
             hip_check(hipMalloc(&r->d_bar, sizeof(uint32_t)), "alloc append ticket");
             hip_check(hipMemset(r->d_bar, 0, sizeof(uint32_t)), "zero append ticket");
             hip_check(hipDeviceSynchronize(), "append ticket zero sync");  // null stream vs the engine's
         }
         launch_collide_split(r->env, r->d_links, r->max_clusters, cw, r->cscratch, stream, ev ? ev + 5 : nullptr,
-                             defer ? &ovf : nullptr);
+                             &ovf);
     }
     c.mark(8, stream);
     hipLaunchKernelGGL(k_append_commit, dim3(kb), dim3(256), 0, stream, r->d_verdict, K, p.d, r->d_ends, r->d_nn,
@@ -1279,10 +1275,9 @@ void joint_free_round(JointNN &g) {
 // Engines whose rounds can run as one joint round (see EngineJob): every round on the Morton
 // tree (incremental index), the same env, agent and engine parameters but the seed, the
 // two-phase collide with the live-unit list, no work counters, K a multiple of 16 (the
-// append's 16-byte verdict loads).  MPT_JOINT_ROUND=0: per-engine heads and tails (A/B).
+// append's 16-byte verdict loads).
 bool joint_round_ok(mpt_rrt *const *rs, int32_t n, int32_t K) {
-    static const bool on = !getenv("MPT_JOINT_ROUND") || atoi(getenv("MPT_JOINT_ROUND")) != 0;
-    if (!on || n < 2 || K < 16 || K % 16 != 0 || collide_mode() == MPT_COLLIDE_FUSED)
+    if (n < 2 || K < 16 || K % 16 != 0 || collide_mode() == MPT_COLLIDE_FUSED)
         return false;
     const mpt_rrt *a = rs[0];
     const EngineParams &p = a->p;
@@ -1302,30 +1297,7 @@ bool joint_round_ok(mpt_rrt *const *rs, int32_t n, int32_t K) {
     return true;
 }
 
-// MPT_HOST_PROF=1: host time of the joint round's phases, printed every 32 calls (diagnostics)
-struct HostProf {
-    double acc[8] = {};
-    int64_t calls = 0;
-    std::chrono::steady_clock::time_point t;
-    void start() { t = std::chrono::steady_clock::now(); }
-    void lap(int i) {
-        const auto now = std::chrono::steady_clock::now();
-        acc[i] += std::chrono::duration<double, std::micro>(now - t).count();
-        t = now;
-    }
-    void done() {
-        if (++calls % 32) return;
-        fprintf(stderr, "[host joint round] us/call: stage %.1f engines %.1f joins %.1f sample %.1f build %.1f nn %.1f "
-                        "steer+collide+append %.1f tail %.1f\n",
-                acc[0] / 32, acc[1] / 32, acc[2] / 32, acc[3] / 32, acc[4] / 32, acc[5] / 32, acc[6] / 32, acc[7] / 32);
-        for (double &a : acc) a = 0;
-    }
-};
-
 void joint_round(mpt_rrt *const *rs, int32_t n, int32_t K, void *const *streams_, hipStream_t joint) {
-    static const bool prof = getenv("MPT_HOST_PROF") && atoi(getenv("MPT_HOST_PROF")) == 1;
-    static HostProf hp;
-    if (prof) hp.start();
     JointNN &g = joint_state(joint);
     std::lock_guard<std::mutex> lk(g.mu);
     const mpt_rrt *a = rs[0];
@@ -1357,16 +1329,15 @@ void joint_round(mpt_rrt *const *rs, int32_t n, int32_t K, void *const *streams_
     }
     g.cs.ensure((int64_t)std::min(per_sub, n) * K * units, a->max_clusters);
     // the engines' host bookkeeping and their job table
-    const size_t b_eng = sizeof(EngineJob) * n, b_inc = sizeof(PtIncJob) * n, b_nn = sizeof(PtJob) * n;
+    const size_t b_eng = sizeof(EngineJob) * n, b_inc = sizeof(CtJob) * n, b_nn = sizeof(CtNnJob) * n;
     int slot = 0;
     char *h = joint_stage(g, b_eng + b_inc + b_nn, &slot);
     EngineJob *he = reinterpret_cast<EngineJob *>(h);
-    PtIncJob *hi = reinterpret_cast<PtIncJob *>(h + b_eng);
-    PtJob *hn = reinterpret_cast<PtJob *>(h + b_eng + b_inc);
+    CtJob *hi = reinterpret_cast<CtJob *>(h + b_eng);
+    CtNnJob *hn = reinterpret_cast<CtNnJob *>(h + b_eng + b_inc);
     const EngineJob *de = reinterpret_cast<const EngineJob *>(g.d_stage);
-    const PtIncJob *di = reinterpret_cast<const PtIncJob *>(g.d_stage + b_eng);
-    const PtJob *dn = reinterpret_cast<const PtJob *>(g.d_stage + b_eng + b_inc);
-    if (prof) hp.lap(0);
+    const CtJob *di = reinterpret_cast<const CtJob *>(g.d_stage + b_eng);
+    const CtNnJob *dn = reinterpret_cast<const CtNnJob *>(g.d_stage + b_eng + b_inc);
     std::vector<SpreadOut> spreads(n);
     std::vector<char> want(n, 0);
     bool timed = false;
@@ -1375,11 +1346,10 @@ void joint_round(mpt_rrt *const *rs, int32_t n, int32_t K, void *const *streams_
         he[i] = EngineJob{r->p.seed, r->ext_base, r->pending_n, r->cap, r->d_nodes, r->d_parents, r->d_n,
                           r->d_counters};
         r->pending_n = -1;
-        r->ptree->inc_reserve(r->cap, d);  // once: no allocation in later rounds
+        r->ctree->reserve(r->cap, d);  // once: no allocation in later rounds
         want[i] = spread_request(r, true, spreads[i]) ? 1 : 0;
         timed = timed || r->timing;
     }
-    if (prof) hp.lap(1);
     // the joint stream waits for every engine stream's earlier work, the engines' streams
     // for the joint round
     std::vector<hipStream_t> uniq;
@@ -1407,27 +1377,25 @@ void joint_round(mpt_rrt *const *rs, int32_t n, int32_t K, void *const *streams_
     auto mark = [&](int i) {
         if (timed) hip_check(hipEventRecord(g.st[i], joint), "joint stage event");
     };
-    if (prof) hp.lap(2);
     mark(0);
     hip_check(hipMemcpyAsync(g.d_stage, he, b_eng, hipMemcpyHostToDevice, joint), "engine jobs H2D");
     const unsigned kb = (unsigned)((K + 255) / 256);
     hipLaunchKernelGGL(k_sample_jobs, dim3(kb, n), dim3(256), 0, joint, p, de, K, g.j_samples, g.j_nlive, n_sub);
     hip_check(hipGetLastError(), "k_sample_jobs");
     mark(1);
-    if (prof) hp.lap(3);
     if (timed) hip_check(hipEventRecord(g.b0, joint), "joint b0");
     // the index builds (a full rebuild issues its code and sort launches here, after the
     // samples' launch applied any truncation) and the NN jobs
     for (int32_t i = 0; i < n; ++i) {
         mpt_rrt *r = rs[i];
         hi[i] = tree_inc_job(r, joint, want[i] ? &spreads[i] : nullptr);
-        PointTreeDev T = r->ptree->dev();
+        CellTreeDev T = r->ctree->dev();
         T.stats = nullptr;
-        hn[i] = PtJob{T, g.j_samples + (int64_t)i * K * d, g.j_nn + (int64_t)i * K, g.j_nnd2 + (int64_t)i * K};
+        hn[i] = CtNnJob{T, g.j_samples + (int64_t)i * K * d, g.j_nn + (int64_t)i * K, g.j_nnd2 + (int64_t)i * K};
     }
     hip_check(hipMemcpyAsync(g.d_stage + b_eng, h + b_eng, b_inc + b_nn, hipMemcpyHostToDevice, joint), "jobs H2D");
     hip_check(hipEventRecord(g.copied[slot], joint), "jobs copied");
-    launch_tree_inc_jobs(di, hi, n, d, joint);
+    launch_ct_jobs(di, hi, n, d, joint);
     for (int32_t i = 0; i < n; ++i)
         if (want[i]) {
             hip_check(hipEventRecord(rs[i]->ev_spread, joint), "spread event");
@@ -1435,12 +1403,10 @@ void joint_round(mpt_rrt *const *rs, int32_t n, int32_t K, void *const *streams_
             rs[i]->rounds_since_spread = 0;
         }
     mark(2);
-    if (prof) hp.lap(4);
     if (timed) hip_check(hipEventRecord(g.t0, joint), "joint t0");
-    launch_tree_nn1_jobs(dn, n, d, K, joint);
+    launch_ct_nn1_jobs(dn, n, d, K, joint);
     mark(3);
     if (timed) hip_check(hipEventRecord(g.t1, joint), "joint t1");
-    if (prof) hp.lap(5);
     auto steer = p.kind == MPT_AGENT_OMNI ? k_steer_jobs<MPT_AGENT_OMNI>
                  : (p.kind == MPT_AGENT_BLIMP ? k_steer_jobs<MPT_AGENT_BLIMP> : k_steer_jobs<MPT_AGENT_SNAKE>);
     LiveOut lv{g.j_live, g.j_nlive, a->d_links, a->env, nullptr, 0, g.j_rt};
@@ -1469,7 +1435,6 @@ void joint_round(mpt_rrt *const *rs, int32_t n, int32_t K, void *const *streams_
     hipLaunchKernelGGL(k_append_jobs, dim3(kb, n), dim3(256), 0, joint, de, g.j_verdict, K, d, g.j_ends, g.j_nn);
     hip_check(hipGetLastError(), "k_append_jobs");
     mark(6);
-    if (prof) hp.lap(6);
     g.timed = timed;
     g.round_timed = timed;
     if (timed) g_last_timed = &g;
@@ -1493,10 +1458,6 @@ void joint_round(mpt_rrt *const *rs, int32_t n, int32_t K, void *const *streams_
         r->jv.nn = g.j_nn + e0;
         r->jv.pcount = g.j_pcount + e0;
         r->jv.verdict = g.j_verdict + e0;
-    }
-    if (prof) {
-        hp.lap(7);
-        hp.done();
     }
 }
 
@@ -1531,11 +1492,11 @@ extern "C" mpt_status mpt_rrt_step_many(mpt_rrt *const *rs, int32_t n, int32_t K
             JointNN &g = joint_state(joint);
             std::lock_guard<std::mutex> lk(g.mu);
             const int32_t nj = (int32_t)J.size();
-            const size_t b_build = sizeof(PtIncJob) * nj, b_nn = sizeof(PtJob) * nj;
+            const size_t b_build = sizeof(CtJob) * nj, b_nn = sizeof(CtNnJob) * nj;
             int slot = 0;
             char *h = joint_stage(g, b_build + b_nn, &slot);
-            PtIncJob *hi = reinterpret_cast<PtIncJob *>(h);
-            PtJob *hn = reinterpret_cast<PtJob *>(h + b_build);
+            CtJob *hi = reinterpret_cast<CtJob *>(h);
+            CtNnJob *hn = reinterpret_cast<CtNnJob *>(h + b_build);
             // the joint stream waits for every engine stream's heads, the engines' tails for it
             // (before the builds: a full incremental rebuild issues its launches here)
             std::vector<hipStream_t> uniq;
@@ -1564,15 +1525,15 @@ extern "C" mpt_status mpt_rrt_step_many(mpt_rrt *const *rs, int32_t n, int32_t K
                 mpt_rrt *r = rs[J[k]];
                 const StepCtx &c = cs[J[k]];
                 hi[k] = tree_inc_job(r, joint, c.want_spread ? &c.spread : nullptr);
-                PointTreeDev T = r->ptree->dev();
+                CellTreeDev T = r->ctree->dev();
                 T.stats = r->stats_on ? r->d_cstats + 8 : nullptr;
-                hn[k] = PtJob{T, r->d_samples, r->d_nn, r->d_nnd2};
+                hn[k] = CtNnJob{T, r->d_samples, r->d_nn, r->d_nnd2};
             }
             hip_check(hipMemcpyAsync(g.d_stage, h, b_build + b_nn, hipMemcpyHostToDevice, joint), "jobs H2D");
             hip_check(hipEventRecord(g.copied[slot], joint), "jobs copied");
-            const PtIncJob *di = reinterpret_cast<const PtIncJob *>(g.d_stage);
-            const PtJob *dn = reinterpret_cast<const PtJob *>(g.d_stage + b_build);
-            launch_tree_inc_jobs(di, hi, nj, rs[J[0]]->p.d, joint);
+            const CtJob *di = reinterpret_cast<const CtJob *>(g.d_stage);
+            const CtNnJob *dn = reinterpret_cast<const CtNnJob *>(g.d_stage + b_build);
+            launch_ct_jobs(di, hi, nj, rs[J[0]]->p.d, joint);
             for (int32_t i : J)
                 if (cs[i].want_spread) hip_check(hipEventRecord(rs[i]->ev_spread, joint), "spread event");
             if (timed) {
@@ -1582,7 +1543,7 @@ extern "C" mpt_status mpt_rrt_step_many(mpt_rrt *const *rs, int32_t n, int32_t K
                 for (hipStream_t s : uniq) hip_check(hipStreamWaitEvent(s, g.built, 0), "built wait");
                 for (int32_t i : J) cs[i].mark(2, stream_of(i));
             }
-            launch_tree_nn1_jobs(dn, nj, rs[J[0]]->p.d, K, joint);
+            launch_ct_nn1_jobs(dn, nj, rs[J[0]]->p.d, K, joint);
             if (timed) {
                 hip_check(hipEventRecord(g.t1, joint), "joint t1");
                 g_last_timed = &g;

@@ -133,6 +133,42 @@ def test_engine_tree_nn_large_blob(mpt_gpu, oracle, K):
     tree, _ = check_round(mpt_gpu, oracle, sc, eng, tree, 4242, K, K)
 
 
+def test_cell_tree_duplicates_truncation_bulk_and_overgrowth(mpt_gpu, oracle):
+    """The incremental cell tree (cell_tree.hip) through its edge cases, every round checked
+    stage by stage against the oracle: a full build over a blob holding 40 and 20 copies of two
+    states (equal codes, more than a bucket holds: grouped by row); incremental rounds that
+    append to and split buckets; a truncation (set_size: the next build starts over); a bulk
+    add_nodes of more copies; a round of K = 9000 (more new points than one round inserts, so the
+    next build is a full one); and the index error counter stays clear."""
+    sc = scenes.blimp_scenario("all")
+    rng = np.random.default_rng(5)
+    blob = rng.uniform(sc.ranges[:, 0], sc.ranges[:, 1], size=(3000, sc.dim))
+    blob[:, :3] = np.array([40.0, 60.0, 50.0]) + rng.normal(0.0, 4.0, size=(3000, 3))
+    dup_a, dup_b = blob[7].copy(), blob[1234].copy()
+    tree = np.concatenate([blob, np.tile(dup_a, (40, 1)), np.tile(dup_b, (20, 1))])
+    env = mpt_gpu.Environment(sc.env_tris, sc.env_tf)
+    ag = mpt_gpu.AgentMesh(sc.agent_tris)
+    eng = mpt_gpu.RRTEngine(env, ag, sc.kind, sc.prm, sc.ranges, sc.steer_dt, sc.cc_dt, capacity=40_000, seed=99)
+    eng.add_nodes(tree)
+    eng.set_nn("tree")
+    base = 0
+    for K in (1024, 1024):
+        tree, _ = check_round(mpt_gpu, oracle, sc, eng, tree, 99, base, K)
+        base += K
+    eng.set_size(2500)
+    tree = tree[:2500]
+    tree, _ = check_round(mpt_gpu, oracle, sc, eng, tree, 99, base, 700)
+    base += 700
+    more = np.concatenate([np.tile(dup_b, (30, 1)), rng.uniform(sc.ranges[:, 0], sc.ranges[:, 1], size=(500, sc.dim))])
+    eng.add_nodes(more)
+    tree = np.concatenate([tree, more])
+    for K in (1024, 9000, 512):
+        tree, _ = check_round(mpt_gpu, oracle, sc, eng, tree, 99, base, K)
+        base += K
+    assert eng.last_nn() == "tree"
+    assert eng.counters()["nodes"] == len(tree)
+
+
 @pytest.mark.parametrize("name", ["omni", "blimp"])
 def test_engine_grid_blob_and_sparse(mpt_gpu, oracle, name):
     """The grid 1-NN (bucketed run kernel) on a tree that is half a tight blob and half
