@@ -113,11 +113,11 @@ def test_engine_rounds(mpt_gpu, oracle, name, nn_mode):
 
 @pytest.mark.parametrize("K", [2048, 6144])
 def test_engine_tree_nn_large_blob(mpt_gpu, oracle, K):
-    """Morton-tree NN (config 5's structure) over a 40k-node RRT-like blob: more than 4096
-    points, so the box build spans several workgroups and the last one to finish builds
-    levels 5 and 6 (k_pt_boxes' ticket path); two rounds, the second after the ticket reset.
-    The second round's build is incremental: K = 6144 appends more than 4096 points, so the
-    chunked sort ranks across more than 8 chunks of 512."""
+    """Cell-tree NN (config 5's index, cell_tree.hip) over a 40k-node RRT-like blob: the first
+    round's full build (hipcub sort of every code, buckets of <= 8 points, a directory of
+    several thousand entries and box levels up to the root); the second round's build is
+    incremental: K = 6144 new points, so the chunked sort ranks across more than 8 chunks of
+    512, many buckets split, and the directory merge places entries across workgroups."""
     sc = scenes.blimp_scenario("all")
     rng = np.random.default_rng(77)
     n0 = 40_000
@@ -347,7 +347,7 @@ def test_engines_on_streams_match_one_stream(mpt_gpu):
 
 def test_step_many_matches_single_steps(mpt_gpu, oracle):
     """mpt_rrt_step_many (config 5's joint NN launch): twelve seeds over four streams, all but
-    one on the Morton tree (one launch of k_tree_nn1_jobs per round) and one on the grid (its
+    one on the cell tree (one launch of k_ct_nn1_jobs per round) and one on the grid (its
     own query), must grow exactly the trees each seed grows alone with mpt_rrt_step -- and, for
     three of the seeds, exactly the oracle's engine rounds (orc_engine_step) from the same
     root."""
