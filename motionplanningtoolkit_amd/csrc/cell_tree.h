@@ -17,6 +17,7 @@ constexpr int kCtBits = 126;       // code bits (two 64-bit words)
 constexpr int kCtSeg = 8192;       // new points one round inserts (the host bounds a round's growth)
 constexpr int kCtScratch = kCtSeg * (kCtCap + 1);  // a round's split elements (new + old of touched buckets)
 constexpr int kCtHull = 64;        // seed points (extreme points in fixed directions)
+constexpr int kCtL1Tile = 2048;    // level-1 entries a workgroup groups (k_ct_lflags / k_ct_lgroup)
 
 // the fixed code plan over the sampling ranges and the seed directions
 struct CtPlan {
@@ -43,7 +44,7 @@ struct CtCounts {
     int32_t n_seg;       // this round's touched buckets
     int32_t n_new_dir;   // this round's new directory entries
     int32_t root;        // the hierarchy's root node
-    int32_t pad;
+    int32_t n_l2;        // this round's level-2 node count (k_ct_lgroup)
     int64_t nidx;        // points indexed (rows [0, nidx) of the node array)
 };
 
@@ -90,6 +91,7 @@ struct CtJob {
     float *nbox;
     uint64_t *ucode;           // [nodes][2]
     int32_t *lflag;            // [nodes] scratch: the level's group starts
+    int32_t *lcount;           // [nodes / kCtL1Tile + 1] scratch: level 1's group starts a tile
     // new points: codes / rows in row order, then sorted; chunk scratch; directory positions
     uint64_t *ncode;           // [kCtSeg][2]
     int32_t *nrow;
@@ -147,7 +149,7 @@ private:
     uint64_t *bcode = nullptr, *ucode = nullptr;
     float *bbox = nullptr, *nbox = nullptr;
     uint32_t *nmeta = nullptr;
-    int32_t *lflag = nullptr;
+    int32_t *lflag = nullptr, *lcount = nullptr;
     uint64_t *dir_code[2] = {nullptr, nullptr};
     int32_t *dir_bk[2] = {nullptr, nullptr};
     uint64_t *ncode = nullptr, *ccode = nullptr, *scode = nullptr, *edir_code = nullptr;

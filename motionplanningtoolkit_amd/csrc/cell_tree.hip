@@ -683,139 +683,266 @@ __global__ __launch_bounds__(256) void k_ct_split_fill(CtJobs js) {
 
 // The new directory: old entry p goes to p + (new entries of segments before p), new entry r
 // (of the segment at directory position q) to q + 1 + r; with each entry its level-1 node (the
-// bucket's box and code).
+// bucket's box and code).  A workgroup takes 256 consecutive entries: two threads find the new
+// entries bounding its old ones, which are staged in LDS for the threads' searches.
 template <int D>
 __global__ __launch_bounds__(256) void k_ct_dmerge(CtJobs js) {
     const CtJob J = CT_JOB(js);  // by value: the fields stay in registers across the stores
+    __shared__ int32_t s_pos[256];
+    __shared__ int32_t s_lo[2];
     const int64_t n_old = J.cnt->n_dir, n_new = J.cnt->n_new_dir;
-    for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < n_old + n_new;
-         t += (int64_t)gridDim.x * blockDim.x) {
-    int64_t out;
-    uint64_t h, l;
-    int32_t b;
-    if (t < n_old) {
-        int64_t lo = 0, hi = n_new;  // new entries whose segment lies before t
-        while (lo < hi) {
-            const int64_t mid = (lo + hi) >> 1;
-            if (J.edir_pos[mid] < t) lo = mid + 1;
-            else hi = mid;
+    for (int64_t c0 = (int64_t)blockIdx.x * 256; c0 < n_old + n_new; c0 += (int64_t)gridDim.x * 256) {
+        const int64_t t = c0 + threadIdx.x;
+        int32_t lo_a = 0, lo_b = 0;
+        if (c0 < n_old) {  // block-uniform
+            if (threadIdx.x < 2) {  // new entries whose segment lies before c0 / before the chunk's end
+                const int64_t key = threadIdx.x == 0 ? c0 : (c0 + 256 < n_old ? c0 + 256 : n_old);
+                int64_t lo = 0, hi = n_new;
+                while (lo < hi) {
+                    const int64_t mid = (lo + hi) >> 1;
+                    if (J.edir_pos[mid] < key) lo = mid + 1;
+                    else hi = mid;
+                }
+                s_lo[threadIdx.x] = (int32_t)lo;
+            }
+            __syncthreads();
+            lo_a = s_lo[0];
+            lo_b = s_lo[1];
+            if (lo_b - lo_a <= 256 && threadIdx.x < lo_b - lo_a) s_pos[threadIdx.x] = J.edir_pos[lo_a + threadIdx.x];
+            __syncthreads();
         }
-        out = t + lo;
-        h = J.odir_code[2 * t];
-        l = J.odir_code[2 * t + 1];
-        b = J.odir_bk[t];
-    } else {
-        const int64_t r = t - n_old;
-        out = J.edir_pos[r] + 1 + r;
-        h = J.edir_code[2 * r];
-        l = J.edir_code[2 * r + 1];
-        b = J.edir_bk[r];
-    }
-    J.ndir_code[2 * out] = h;
-    J.ndir_code[2 * out + 1] = l;
-    J.ndir_bk[out] = b;
-    const int32_t cnt = J.bcnt[b];
-    J.nmeta[out] = leaf_code(b, cnt > 0 ? cnt : 1);
+        if (t < n_old + n_new) {
+            int64_t out;
+            uint64_t h, l;
+            int32_t b;
+            if (t < n_old) {
+                int32_t lo = lo_a, hi = lo_b;
+                if (lo_b - lo_a <= 256) {
+                    while (lo < hi) {
+                        const int32_t mid = (lo + hi) >> 1;
+                        if (s_pos[mid - lo_a] < t) lo = mid + 1;
+                        else hi = mid;
+                    }
+                } else {
+                    while (lo < hi) {
+                        const int32_t mid = (lo + hi) >> 1;
+                        if (J.edir_pos[mid] < t) lo = mid + 1;
+                        else hi = mid;
+                    }
+                }
+                out = t + lo;
+                h = J.odir_code[2 * t];
+                l = J.odir_code[2 * t + 1];
+                b = J.odir_bk[t];
+            } else {
+                const int64_t r = t - n_old;
+                out = J.edir_pos[r] + 1 + r;
+                h = J.edir_code[2 * r];
+                l = J.edir_code[2 * r + 1];
+                b = J.edir_bk[r];
+            }
+            J.ndir_code[2 * out] = h;
+            J.ndir_code[2 * out + 1] = l;
+            J.ndir_bk[out] = b;
+            const int32_t cnt = J.bcnt[b];
+            J.nmeta[out] = leaf_code(b, cnt > 0 ? cnt : 1);
 #pragma unroll
-    for (int q = 0; q < 2 * D; ++q) J.nbox[out * 2 * D + q] = J.bbox[(int64_t)b * 2 * D + q];
+            for (int q = 0; q < 2 * D; ++q) J.nbox[out * 2 * D + q] = J.bbox[(int64_t)b * 2 * D + q];
+        }
+        __syncthreads();  // s_lo / s_pos reused by the next chunk
     }
 }
 
-// One workgroup a tree: the hierarchy above the directory, level after level -- consecutive
-// nodes grouped into maximal aligned code cells of at most 8 (ct_same over the nodes' codes: a
-// node's code is its first directory entry's start), or, when that would leave more than half as
-// many groups as nodes, runs of 8 (the depth stays logarithmic) -- then the counts, the seed
-// rows, the indexed count and the spread.
+// The hierarchy above the directory: consecutive nodes of a level grouped into maximal aligned
+// code cells of at most 8 (ct_same over the nodes' codes: a node's code is its first directory
+// entry's start), or, when that would leave more than half as many groups as nodes or more
+// levels than the walk's stack allows, runs of 8 (the depth stays logarithmic).  Level 1 (the
+// directory, the big one) is grouped over many workgroups (k_ct_lflags, k_ct_lgroup), the levels
+// above it by one workgroup a tree (k_ct_levels), which also copies the seeds and closes the
+// round's counts.
 constexpr int kCtLevelThreads = 1024;
 constexpr int kCtMaxLevels = 10;  // the walk's stack bound (ct_walk kStack); runs of 8 reach it below 8^9 entries
+constexpr int kCtL1Per = kCtL1Tile / 256;
+static_assert(kCtL1Per == 8, "k_ct_lgroup: one run of 8 a thread when grouping by runs");
 
-__device__ __forceinline__ int ct_block_sum(int v, int32_t *s_w) {
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
-    __syncthreads();
-    if (lane == 0) s_w[wave] = v;
-    __syncthreads();
-    int tot = 0;
-    for (int w = 0; w < kCtLevelThreads / 64; ++w) tot += s_w[w];
-    return tot;
+// the levels a tree needs when level `lev` has G groups and runs of 8 follow
+__device__ __forceinline__ bool ct_fixed(int64_t n, int64_t G, int lev) {
+    int need = lev + 1;
+    for (int64_t m = G; m > 1; m = (m + 7) / 8) ++need;
+    return G > n / 2 || need > kCtMaxLevels;
 }
 
+// the parent of nodes [first, first + len) of a level at index P (box, meta, code)
+template <int D>
+__device__ __forceinline__ void ct_parent(const CtJob &J, const uint64_t *__restrict__ lc, int64_t first, int len,
+                                          int64_t P, int64_t i) {
+    float lo[D], hi[D];
+#pragma unroll
+    for (int q = 0; q < D; ++q) {
+        lo[q] = J.nbox[first * 2 * D + q];
+        hi[q] = J.nbox[first * 2 * D + D + q];
+    }
+    for (int u = 1; u < len; ++u)
+#pragma unroll
+        for (int q = 0; q < D; ++q) {
+            lo[q] = fminf(lo[q], J.nbox[(first + u) * 2 * D + q]);
+            hi[q] = fmaxf(hi[q], J.nbox[(first + u) * 2 * D + D + q]);
+        }
+#pragma unroll
+    for (int q = 0; q < D; ++q) {
+        J.nbox[P * 2 * D + q] = lo[q];
+        J.nbox[P * 2 * D + D + q] = hi[q];
+    }
+    J.nmeta[P] = inner_code(first, len);
+    J.ucode[2 * P] = lc[2 * i];
+    J.ucode[2 * P + 1] = lc[2 * i + 1];
+}
+
+__device__ __forceinline__ int ct_block_scan(int v, int32_t *s_w, int nthreads, int &total) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    int incl = v;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const int o = __shfl_up(incl, off);
+        if (lane >= off) incl += o;
+    }
+    __syncthreads();
+    if (lane == 63) s_w[wave] = incl;
+    __syncthreads();
+    int before = 0, tot = 0;
+    for (int w = 0; w < nthreads / 64; ++w) {
+        before += w < wave ? s_w[w] : 0;
+        tot += s_w[w];
+    }
+    total = tot;
+    return before + incl - v;  // exclusive
+}
+
+// level 1's group starts, kCtL1Per consecutive entries a thread; the tile's count
+__global__ __launch_bounds__(256) void k_ct_lflags(CtJobs js) {
+    const CtJob J = CT_JOB(js);  // by value: the fields stay in registers across the stores
+    __shared__ int32_t s_w[4];
+    const int64_t n = (int64_t)J.cnt->n_dir + J.cnt->n_new_dir;
+    const int64_t t0 = (int64_t)blockIdx.x * kCtL1Tile;
+    if (n <= 1 || t0 >= n) return;  // block-uniform
+    int c = 0;
+#pragma unroll
+    for (int a = 0; a < kCtL1Per; ++a) {
+        const int64_t i = t0 + threadIdx.x * kCtL1Per + a;
+        if (i < n) {
+            const int f = i == 0 || !ct_same(J.ndir_code, nullptr, 0, n, i);
+            J.lflag[i] = f;
+            c += f;
+        }
+    }
+    int tot;
+    (void)ct_block_scan(c, s_w, 256, tot);
+    if (threadIdx.x == 0) J.lcount[blockIdx.x] = tot;
+}
+
+// level 2: each tile's groups, numbered after the tiles before it
+template <int D>
+__global__ __launch_bounds__(256) void k_ct_lgroup(CtJobs js) {
+    const CtJob J = CT_JOB(js);  // by value: the fields stay in registers across the stores
+    __shared__ int32_t s_w[4];
+    __shared__ int64_t s_sum[2];
+    const int64_t n = (int64_t)J.cnt->n_dir + J.cnt->n_new_dir;
+    const int64_t t0 = (int64_t)blockIdx.x * kCtL1Tile;
+    if (n <= 1 || t0 >= n) return;  // block-uniform
+    const int64_t tiles = (n + kCtL1Tile - 1) / kCtL1Tile;
+    if (threadIdx.x < 64) {  // the groups of all tiles and of the tiles before this one
+        int64_t all = 0, before = 0;
+        for (int64_t b = threadIdx.x; b < tiles; b += 64) {
+            const int32_t v = J.lcount[b];
+            all += v;
+            before += b < (int64_t)blockIdx.x ? v : 0;
+        }
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) {
+            all += __shfl_xor(all, off);
+            before += __shfl_xor(before, off);
+        }
+        if (threadIdx.x == 0) {
+            s_sum[0] = all;
+            s_sum[1] = before;
+        }
+    }
+    __syncthreads();
+    const int64_t G = s_sum[0];
+    const bool fixed = ct_fixed(n, G, 1);
+    if (blockIdx.x == 0 && threadIdx.x == 0) J.cnt->n_l2 = (int32_t)(fixed ? (n + 7) / 8 : G);
+    const int64_t i0 = t0 + threadIdx.x * kCtL1Per;
+    if (fixed) {
+        if (i0 < n && (i0 & 7) == 0) {  // kCtL1Per == 8: one run a thread
+            const int len = n - i0 < 8 ? (int)(n - i0) : 8;
+            ct_parent<D>(J, J.ndir_code, i0, len, n + i0 / 8, i0);
+        }
+        return;
+    }
+    int f[kCtL1Per], c = 0;
+#pragma unroll
+    for (int a = 0; a < kCtL1Per; ++a) {
+        f[a] = i0 + a < n ? J.lflag[i0 + a] : 0;
+        c += f[a];
+    }
+    int tot;
+    int64_t g = s_sum[1] + ct_block_scan(c, s_w, 256, tot);
+#pragma unroll
+    for (int a = 0; a < kCtL1Per; ++a) {
+        if (!f[a]) continue;
+        const int64_t i = i0 + a;
+        int len = 1;
+        while (i + len < n && len < kCtCap && !J.lflag[i + len]) ++len;
+        ct_parent<D>(J, J.ndir_code, i, len, n + g, i);
+        ++g;
+    }
+}
+
+// one workgroup a tree: the levels above level 2 (a thread a run of consecutive nodes), then
+// the counts, the seed rows, the indexed count and the spread
 template <int D>
 __global__ __launch_bounds__(kCtLevelThreads) void k_ct_levels(CtJobs js) {
     const CtJob J = CT_JOB(js);  // by value: the fields stay in registers across the stores
     __shared__ int32_t s_w[kCtLevelThreads / 64];
-    const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
-    int64_t n = (int64_t)J.cnt->n_dir + J.cnt->n_new_dir, ls = 0;
-    int lev = 1;  // the level being grouped (the walk's stack holds ~7 entries a level a node of a step: <= 10 levels)
+    const int t = threadIdx.x;
+    const int64_t n1 = (int64_t)J.cnt->n_dir + J.cnt->n_new_dir;
+    int64_t ls = n1 > 1 ? n1 : 0, n = n1 > 1 ? J.cnt->n_l2 : n1;
+    int lev = 2;
     while (n > 1) {
-        const uint64_t *lc = ls == 0 ? J.ndir_code : J.ucode + 2 * ls;  // node i's code at lc[2 i]
-        int g = 0;
-        for (int64_t i = t; i < n; i += kCtLevelThreads) {
+        const uint64_t *lc = J.ucode + 2 * ls;  // node i's code at lc[2 i]
+        const int64_t per = (n + kCtLevelThreads - 1) / kCtLevelThreads;
+        const int64_t i0 = t * per, i1 = i0 + per < n ? i0 + per : n;
+        int c = 0;
+        for (int64_t i = i0; i < i1; ++i) {
             const int f = i == 0 || !ct_same(lc, nullptr, 0, n, i);
-            J.lflag[i] = f;
-            g += f;
+            J.lflag[ls + i] = f;
+            c += f;
         }
-        int64_t G = ct_block_sum(g, s_w);
-        int need = lev + 1;  // levels if runs of 8 follow from the next one on
-        for (int64_t m = G; m > 1; m = (m + 7) / 8) ++need;
-        const bool fixed = G > n / 2 || need > kCtMaxLevels;
-        if (fixed) {
-            for (int64_t i = t; i < n; i += kCtLevelThreads) J.lflag[i] = (i & 7) == 0;
-            G = (n + 7) / 8;
-        }
+        int G;
+        const int ex = ct_block_scan(c, s_w, kCtLevelThreads, G);
+        const bool fixed = ct_fixed(n, G, lev);
         __threadfence_block();
         __syncthreads();
-        int64_t carry = 0;
-        for (int64_t c0 = 0; c0 < n; c0 += kCtLevelThreads) {
-            const int64_t i = c0 + t;
-            const int f = i < n ? J.lflag[i] : 0;
-            int incl = f;
-#pragma unroll
-            for (int off = 1; off < 64; off <<= 1) {
-                const int o = __shfl_up(incl, off);
-                if (lane >= off) incl += o;
+        const int64_t nG = fixed ? (n + 7) / 8 : G;
+        int64_t g = ex;
+        for (int64_t i = i0; i < i1; ++i) {
+            int len = 0;
+            if (fixed) {
+                if ((i & 7) == 0) len = n - i < 8 ? (int)(n - i) : 8;
+                g = i / 8;
+            } else if (J.lflag[ls + i]) {
+                len = 1;
+                while (i + len < n && len < kCtCap && !J.lflag[ls + i + len]) ++len;
             }
-            __syncthreads();
-            if (lane == 63) s_w[wave] = incl;
-            __syncthreads();
-            int before = 0, tot = 0;
-            for (int w = 0; w < kCtLevelThreads / 64; ++w) {
-                before += w < wave ? s_w[w] : 0;
-                tot += s_w[w];
+            if (len) {
+                ct_parent<D>(J, lc, ls + i, len, ls + n + g, i);
+                ++g;
             }
-            if (f) {
-                const int64_t grp = carry + before + incl - 1;
-                int len = 1;
-                while (i + len < n && len < kCtCap && !J.lflag[i + len]) ++len;
-                const int64_t first = ls + i, P = ls + n + grp;
-                float lo[D], hi[D];
-#pragma unroll
-                for (int q = 0; q < D; ++q) {
-                    lo[q] = J.nbox[first * 2 * D + q];
-                    hi[q] = J.nbox[first * 2 * D + D + q];
-                }
-                for (int u = 1; u < len; ++u)
-#pragma unroll
-                    for (int q = 0; q < D; ++q) {
-                        lo[q] = fminf(lo[q], J.nbox[(first + u) * 2 * D + q]);
-                        hi[q] = fmaxf(hi[q], J.nbox[(first + u) * 2 * D + D + q]);
-                    }
-#pragma unroll
-                for (int q = 0; q < D; ++q) {
-                    J.nbox[P * 2 * D + q] = lo[q];
-                    J.nbox[P * 2 * D + D + q] = hi[q];
-                }
-                J.nmeta[P] = inner_code(first, len);
-                J.ucode[2 * P] = lc[2 * i];
-                J.ucode[2 * P + 1] = lc[2 * i + 1];
-            }
-            carry += tot;
         }
         __threadfence_block();
         __syncthreads();
         ls += n;
-        n = G;
+        n = nG;
         ++lev;
     }
     for (int it = t; it < kCtHull * D; it += kCtLevelThreads) {
@@ -1295,7 +1422,7 @@ CtPlan make_ct_plan(int32_t d, const double *lo, const double *hi, int32_t spati
 }
 
 void CellTree::release() {
-    void *ps[] = {plan, cnt, bpts, bids, bcnt, bcode, bbox, nbox, nmeta, ucode, lflag, dir_code[0], dir_code[1], dir_bk[0], dir_bk[1],
+    void *ps[] = {plan, cnt, bpts, bids, bcnt, bcode, bbox, nbox, nmeta, ucode, lflag, lcount, dir_code[0], dir_code[1], dir_bk[0], dir_bk[1],
                   ncode, ccode, scode, edir_code, nrow, crow, npos, nseg, seg_pos, srow, sseg, slead, srank, edir_bk,
                   edir_pos, seg, hull_keys, ibox, hull_pts, hull_ids, fhi, flo, fk0, fk1, fv0, fv1, fflag, fleaf, ftemp};
     for (void *p : ps)
@@ -1328,6 +1455,7 @@ void CellTree::reserve(int64_t c, int32_t d) {
     al((void **)&nmeta, sizeof(uint32_t) * nodes, "ct node codes");
     al((void **)&ucode, sizeof(uint64_t) * 2 * nodes, "ct node cell codes");
     al((void **)&lflag, sizeof(int32_t) * nodes, "ct level scratch");
+    al((void **)&lcount, sizeof(int32_t) * (bcap / kCtL1Tile + 1), "ct level scratch");
     for (int k = 0; k < 2; ++k) {
         al((void **)&dir_code[k], sizeof(uint64_t) * 2 * bcap, "ct directory");
         al((void **)&dir_bk[k], sizeof(int32_t) * bcap, "ct directory");
@@ -1440,6 +1568,7 @@ CtJob CellTree::prepare(const double *pts, int64_t n_upper, const int64_t *n_dev
     J.nbox = nbox;
     J.ucode = ucode;
     J.lflag = lflag;
+    J.lcount = lcount;
     J.ncode = ncode;
     J.nrow = nrow;
     J.ccode = ccode;
@@ -1502,6 +1631,10 @@ void launch_ct_jobs(const CtJob *d_jobs, const CtJob *h_jobs, int32_t n, int32_t
     hipLaunchKernelGGL(by_d(k_ct_dmerge<3>, k_ct_dmerge<7>, k_ct_dmerge<15>),
                        dim3((unsigned)std::max<int64_t>(1, (max_n + 2047) / 2048), yn), dim3(256), 0, stream, js);
     hip_check(hipGetLastError(), "k_ct_dmerge");
+    const unsigned tiles = (unsigned)std::max<int64_t>(1, (max_n + kCtL1Tile - 1) / kCtL1Tile);
+    hipLaunchKernelGGL(k_ct_lflags, dim3(tiles, yn), dim3(256), 0, stream, js);
+    hipLaunchKernelGGL(by_d(k_ct_lgroup<3>, k_ct_lgroup<7>, k_ct_lgroup<15>), dim3(tiles, yn), dim3(256), 0, stream,
+                       js);
     hipLaunchKernelGGL(by_d(k_ct_levels<3>, k_ct_levels<7>, k_ct_levels<15>), dim3(1, yn), dim3(kCtLevelThreads), 0,
                        stream, js);
     hip_check(hipGetLastError(), "k_ct_levels");
