@@ -30,6 +30,7 @@
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
+#include <type_traits>
 #include <cmath>
 
 #include "cell_tree.h"
@@ -1158,6 +1159,107 @@ __device__ __forceinline__ float ct_box_lb(const float *__restrict__ b, const do
     }
 }
 
+// ---- lane exchanges of the walk (DPP lane permutations and the gfx950 row / half swaps: no
+// LDS traffic, unlike ds_bpermute) ----
+constexpr int kDppXor1 = 0xB1;   // quad_perm [1,0,3,2]: lane i ^ 1
+constexpr int kDppXor2 = 0x4E;   // quad_perm [2,3,0,1]: lane i ^ 2
+constexpr int kDppRev4 = 0x1B;   // quad_perm [3,2,1,0]: lane i ^ 3
+constexpr int kDppRev8 = 0x141;  // row_half_mirror: lane i ^ 7 within 8
+constexpr int kDppRev16 = 0x140; // row_mirror: lane i ^ 15 within 16
+template <int CTRL>
+__device__ __forceinline__ uint32_t dpp_u(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, CTRL, 0xf, 0xf, true);  // every source lane is in range
+}
+// level L of a group reduction: each lane gets a lane of the other half of its 2L-lane block
+// (after the levels below L that half's lanes hold one value)
+template <int L>
+__device__ __forceinline__ uint32_t xchg(uint32_t v) {
+    if constexpr (L == 1) return dpp_u<kDppXor1>(v);
+    else if constexpr (L == 2) return dpp_u<kDppXor2>(v);
+    else if constexpr (L == 4) return dpp_u<kDppRev8>(v);
+    else if constexpr (L == 8) return dpp_u<kDppRev16>(v);
+    else if constexpr (L == 16) {  // rows 0 <-> 1, 2 <-> 3
+        const auto r = __builtin_amdgcn_permlane16_swap(v, v, false, false);
+        return (threadIdx.x & 16) ? r[0] : r[1];
+    } else {  // lanes 0..31 <-> 32..63
+        static_assert(L == 32, "xchg level");
+        const auto r = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+        return (threadIdx.x & 32) ? r[0] : r[1];
+    }
+}
+template <int L>
+__device__ __forceinline__ double xchg_d(double x) {
+    const uint32_t lo = (uint32_t)__double2loint(x), hi = (uint32_t)__double2hiint(x);
+    return __hiloint2double((int)xchg<L>(hi), (int)xchg<L>(lo));
+}
+template <int L, class F>
+__device__ __forceinline__ void each_level(F &&f) {
+    if constexpr (L >= 1) f(std::integral_constant<int, 1>{});
+    if constexpr (L >= 2) f(std::integral_constant<int, 2>{});
+    if constexpr (L >= 4) f(std::integral_constant<int, 4>{});
+    if constexpr (L >= 8) f(std::integral_constant<int, 8>{});
+    if constexpr (L >= 16) f(std::integral_constant<int, 16>{});
+    if constexpr (L >= 32) f(std::integral_constant<int, 32>{});
+}
+// (d2, id) take-better without branches (nn_better)
+__device__ __forceinline__ void nn_take(double &bd, int32_t &bi, double od, int32_t oi) {
+    const bool t = (od < bd) | ((od == bd) & (oi < bi));
+    bd = t ? od : bd;
+    bi = t ? oi : bi;
+}
+// The best (d2, id) of each G-lane group, in every lane of it (nn_better's order): the least
+// d2 first (one double a level), then the least id among the lanes holding it -- read from the
+// one such lane of a 64-lane group when it is alone (the common case), else reduced.
+template <int G>
+__device__ __forceinline__ void best_group(double &bd, int32_t &bi) {
+    double m = bd;
+    each_level<G / 2>([&](auto L) {
+        const double o = xchg_d<decltype(L)::value>(m);
+        m = o < m ? o : m;
+    });
+    const bool win = bd == m;
+    bd = m;
+    if constexpr (G == 64) {
+        const uint64_t wm = __ballot(win);
+        if (__popcll(wm) == 1) {
+            bi = __builtin_amdgcn_readlane(bi, __ffsll((long long)wm) - 1);
+            return;
+        }
+    }
+    int32_t c = win ? bi : 0x7fffffff;
+    each_level<G / 2>([&](auto L) {
+        const int32_t o = (int32_t)xchg<decltype(L)::value>((uint32_t)c);
+        c = o < c ? o : c;
+    });
+    bi = c;
+}
+// ascending sort of each 8-lane group by key (unique in the group: the lane index in its low
+// bits), the payload moved along: the bitonic network in its flip form (stage k: lane i against
+// i ^ (k - 1), then i ^ j for j = k / 4 .. 1; the lower lane keeps the smaller), every exchange
+// a DPP permutation
+template <int CTRL>
+__device__ __forceinline__ void cx8(uint32_t &k, uint32_t &p, bool upper) {
+    const uint32_t ok = dpp_u<CTRL>(k), op = dpp_u<CTRL>(p);
+    const bool t = (ok < k) != upper;
+    k = t ? ok : k;
+    p = t ? op : p;
+}
+__device__ __forceinline__ void sort8(uint32_t &k, uint32_t &p, int ls) {
+    const bool u1 = ls & 1, u2 = ls & 2, u4 = ls & 4;
+    cx8<kDppXor1>(k, p, u1);
+    cx8<kDppRev4>(k, p, u2);
+    cx8<kDppXor1>(k, p, u1);
+    cx8<kDppRev8>(k, p, u4);
+    cx8<kDppXor2>(k, p, u2);
+    cx8<kDppXor1>(k, p, u1);
+}
+// the smallest float >= x (x >= 0): the walk's pruning threshold in float (any box whose
+// lower bound is <= the best squared distance is <= it too)
+__device__ __forceinline__ float f32_up(double x) {
+    const float f = (float)x;
+    return (double)f < x ? __uint_as_float(__float_as_uint(f) + 1u) : f;
+}
+
 // the seeds' best (d2, id) over a group of G lanes: lane `sub` takes seeds sub, sub + G, ...
 template <int D, int G>
 __device__ __forceinline__ void ct_seed(const CellTreeDev &T, const double (&qq)[D], int sub, double &bd, int32_t &bi,
@@ -1170,20 +1272,9 @@ __device__ __forceinline__ void ct_seed(const CellTreeDev &T, const double (&qq)
         for (int k = 0; k < D; ++k) row[k] = ((gdbl)T.hull_pts)[h * D + k];
         const double dd = flann_l2<D>(qq, row);
         ++n_pts;
-        if (nn_better(dd, id, bd, bi)) {
-            bd = dd;
-            bi = id;
-        }
+        nn_take(bd, bi, dd, id);
     }
-#pragma unroll
-    for (int off = G / 2; off > 0; off >>= 1) {
-        const double od = __shfl_xor(bd, off, G);
-        const int32_t oi = __shfl_xor(bi, off, G);
-        if (nn_better(od, oi, bd, bi)) {
-            bd = od;
-            bi = oi;
-        }
-    }
+    best_group<G>(bd, bi);
 }
 
 // NW nodes a step: 8 * NW lanes per query, the stack's top NW entries popped together (each
@@ -1220,6 +1311,7 @@ __device__ __forceinline__ void ct_walk(const CellTreeDev &T, const double *__re
     uint32_t n_pts = 0, n_box = 0, n_steps = 1;  // the seeds' step
     if (*T.n_dev > 0) {
         ct_seed<D, G>(T, qq, sub, bd, bi, n_pts);
+        float bdf = f32_up(bd);
         int sp = 1;
         if (sub == 0) {
             s_code[grp][0] = ((gu32)T.nmeta)[*T.root];
@@ -1231,15 +1323,15 @@ __device__ __forceinline__ void ct_walk(const CellTreeDev &T, const double *__re
             const int np = sp >= NW ? NW : sp;
             const bool have = part < np;
             uint32_t code = 0;
-            double lbs = 0.0;
+            float lbs = 0.0f;
             if (have) {
                 code = s_code[grp][sp - 1 - part];
-                lbs = (double)s_lb[grp][sp - 1 - part];
+                lbs = s_lb[grp][sp - 1 - part];
             }
             sp -= np;
             ++n_steps;
             __builtin_amdgcn_wave_barrier();
-            const bool act = have && !(lbs * (1.0 - 1e-12) > bd);
+            const bool act = have && !(lbs > bdf);
             bool keep = false, leaf = false;
             float lbf = 0.0f;
             uint32_t child = 0;
@@ -1254,10 +1346,7 @@ __device__ __forceinline__ void ct_walk(const CellTreeDev &T, const double *__re
                     const int32_t id = ((gi32)T.bids)[p];
                     ++n_pts;
                     leaf = true;
-                    if (nn_better(dd, id, bd, bi)) {
-                        bd = dd;
-                        bi = id;
-                    }
+                    nn_take(bd, bi, dd, id);
                 }
             } else if (act) {
                 const int cnt = (int)((code >> 28) & 7u) + 1;
@@ -1276,33 +1365,25 @@ __device__ __forceinline__ void ct_walk(const CellTreeDev &T, const double *__re
             // lanes already share one best unless a lane examined a point this step, and with no
             // survivor in the wave there is nothing to rank
             if (__ballot(leaf)) {
-#pragma unroll
-                for (int off = G / 2; off > 0; off >>= 1) {
-                    const double od = __shfl_xor(bd, off, G);
-                    const int32_t oi = __shfl_xor(bi, off, G);
-                    if (nn_better(od, oi, bd, bi)) {
-                        bd = od;
-                        bi = oi;
-                    }
-                }
+                best_group<G>(bd, bi);
+                bdf = f32_up(bd);
             }
-            keep = keep && (double)lbf * (1.0 - 1e-12) <= bd;
+            keep = keep && lbf <= bdf;
             const uint64_t wm = __ballot(keep);
             const uint64_t gm = (wm >> base) & (G == 64 ? ~0ull : ((1ull << G) - 1));
-            const uint32_t mine = (uint32_t)(gm >> (part * 8)) & 0xffu;
+            const int c = __popc((uint32_t)(gm >> (part * 8)) & 0xffu);
             const int below = __popcll(part + 1 < NW ? gm >> ((part + 1) * 8) : 0ull);
-            int rank = 0;
             if (wm) {
-#pragma unroll
-                for (int j = 0; j < 8; ++j) {
-                    const float o = __shfl(lbf, part * 8 + j, G);
-                    if (((mine >> j) & 1u) && (o > lbf || (o == lbf && j > ls))) ++rank;
+                // each part's survivors sorted by lower bound, pushed nearest-last; the key's
+                // low 3 bits are the lane (unique keys), so the stored bound is rounded down by
+                // at most 7 ulp: still a lower bound
+                uint32_t key = (keep ? __float_as_uint(lbf) & ~7u : 0xfffffff8u) | (uint32_t)ls, pay = child;
+                sort8(key, pay, ls);
+                if (ls < c) {
+                    const int pos = sp + below + (c - 1 - ls);
+                    s_code[grp][pos] = pay;
+                    s_lb[grp][pos] = __uint_as_float(key & ~7u);
                 }
-            }
-            if (keep) {
-                const int pos = sp + below + rank;
-                s_code[grp][pos] = child;
-                s_lb[grp][pos] = lbf;
             }
             sp += __popcll(gm);
             __builtin_amdgcn_wave_barrier();
