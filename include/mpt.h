@@ -247,8 +247,8 @@ mpt_status mpt_rrt_info(const mpt_rrt *rrt, int64_t info[4]);
  * stream when timing is enabled: [sample, nn_build, nn_query, steer, collide, append]
  * (nn_build = grid index build, 0 in brute-force mode; nn_query includes the merge). */
 mpt_status mpt_rrt_enable_timing(mpt_rrt *rrt, int32_t enable);
-/* NN structure of the rounds: MPT_NN_AUTO / _BRUTE / _GRID / _TREE (packed Morton tree,
- * for trees that do not fill the sampling box), grid occupancy target (points per cell,
+/* NN structure of the rounds: MPT_NN_AUTO / _BRUTE / _GRID / _TREE (the incremental cell
+ * tree, for trees that do not fill the sampling box), grid occupancy target (points per cell,
  * <= 0: the default, 2 points per cell with the cell side floored at 0.3x the expected NN
  * distance over all state dims).  Results are identical. */
 mpt_status mpt_rrt_set_nn(mpt_rrt *rrt, int32_t mode, double points_per_cell);

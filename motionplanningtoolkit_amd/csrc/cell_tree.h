@@ -82,12 +82,15 @@ struct CtJob {
     uint64_t *bcode;           // [buckets][kCtCap][2] the slots' codes (hi, lo)
     int32_t *bcnt;
     float *bbox;               // [buckets][2d]
-    // directory (double-buffered: read odir, write ndir)
+    // The directory is the hierarchy's level 1 (node i = entry i: its start code, its bucket's
+    // meta and box), double-buffered: last round's in ocode / ometa / obox (the touched buckets'
+    // records updated in place), this round's written to ndir_code and the level-1 part of
+    // nmeta / nbox (T's arrays, the levels above following it)
     const uint64_t *odir_code; // [n_dir][2] interval start codes
-    const int32_t *odir_bk;
+    uint32_t *ometa;
+    float *obox;
     uint64_t *ndir_code;
-    int32_t *ndir_bk;
-    uint32_t *nmeta;           // the hierarchy (T.nmeta, T.nbox) and its nodes' codes above level 1
+    uint32_t *nmeta;
     float *nbox;
     uint64_t *ucode;           // [nodes][2]
     int32_t *lflag;            // [nodes] scratch: the level's group starts
@@ -147,11 +150,10 @@ private:
     double *bpts = nullptr;
     int32_t *bids = nullptr, *bcnt = nullptr;
     uint64_t *bcode = nullptr, *ucode = nullptr;
-    float *bbox = nullptr, *nbox = nullptr;
-    uint32_t *nmeta = nullptr;
+    float *bbox = nullptr, *nbox[2] = {nullptr, nullptr};
+    uint32_t *nmeta[2] = {nullptr, nullptr};
     int32_t *lflag = nullptr, *lcount = nullptr;
     uint64_t *dir_code[2] = {nullptr, nullptr};
-    int32_t *dir_bk[2] = {nullptr, nullptr};
     uint64_t *ncode = nullptr, *ccode = nullptr, *scode = nullptr, *edir_code = nullptr;
     int32_t *nrow = nullptr, *crow = nullptr, *npos = nullptr, *nseg = nullptr, *seg_pos = nullptr, *srow = nullptr,
             *sseg = nullptr, *slead = nullptr, *srank = nullptr, *edir_bk = nullptr, *edir_pos = nullptr;

@@ -435,7 +435,7 @@ __global__ __launch_bounds__(kCtSegThreads) void k_ct_segments(CtJobs js) {
         if (j >= m) break;
         s += head[a];
         if (!head[a]) continue;
-        const int32_t b = J.odir_bk[pos[a]];
+        const int32_t b = (int32_t)(J.ometa[pos[a]] & 0x0fffffffu);
         const int32_t c = J.bcnt[b];
         const int32_t k = s_first[s + 1] - j;
         const int32_t off = j + 8 * s;
@@ -500,6 +500,9 @@ __global__ __launch_bounds__(256) void k_ct_apply(CtJobs js) {
             }
             write_box<D>(J.bbox + (int64_t)b * 2 * D, lo, hi);
             J.bcnt[b] = c + k;
+            const int64_t dp = J.seg_pos[s];  // the bucket's record in last round's directory
+            write_box<D>(J.obox + dp * 2 * D, lo, hi);
+            J.ometa[dp] = leaf_code(b, c + k);
         }
         return;
     }
@@ -561,6 +564,25 @@ __device__ __forceinline__ bool ct_same(const uint64_t *__restrict__ code, const
     if (cnt <= kCtCap) return true;
     if (k < 128) return false;
     return row ? (row[i] >> 3) == (row[i - 1] >> 3) : ((i - lo) >> 3) == ((i - 1 - lo) >> 3);
+}
+
+// ct_same over adjacent prefix lengths a[u] = c_cpl(code u - 1, code u) (a window of them in
+// LDS): the cell of elements i - 1, i at prefix length k = a[i] extends left over u while
+// a[u] >= k and right likewise; equal codes (k = 128) that are more than 8 go by index / 8.
+__device__ __forceinline__ bool ct_same_a(const uint8_t *__restrict__ a, int64_t lo, int64_t hi, int64_t i) {
+    const int k = a[i];
+    int cnt = 2;
+    for (int64_t u = i - 1; u > lo && cnt <= kCtCap; --u) {
+        if (a[u] < k) break;
+        ++cnt;
+    }
+    for (int64_t u = i + 1; u < hi && cnt <= kCtCap; ++u) {
+        if (a[u] < k) break;
+        ++cnt;
+    }
+    if (cnt <= kCtCap) return true;
+    if (k < 128) return false;
+    return ((i - lo) >> 3) == ((i - 1 - lo) >> 3);
 }
 
 __device__ __forceinline__ int64_t ct_scratch_total(const CtJob &J) {
@@ -670,6 +692,11 @@ __device__ __forceinline__ void ct_fill_leaf(const CtJob &J, int64_t e, int flag
     }
     write_box<D>(J.bbox + (int64_t)b * 2 * D, lo, hi);
     J.bcnt[b] = len;
+    if (flag == 1) {  // the split bucket keeps its directory record: update it in place
+        const int64_t dp = J.seg_pos[s];
+        write_box<D>(J.obox + dp * 2 * D, lo, hi);
+        J.ometa[dp] = leaf_code(b, len);
+    }
 }
 
 template <int D>
@@ -684,8 +711,9 @@ __global__ __launch_bounds__(256) void k_ct_split_fill(CtJobs js) {
 
 // The new directory: old entry p goes to p + (new entries of segments before p), new entry r
 // (of the segment at directory position q) to q + 1 + r; with each entry its level-1 node (the
-// bucket's box and code).  A workgroup takes 256 consecutive entries: two threads find the new
-// entries bounding its old ones, which are staged in LDS for the threads' searches.
+// bucket's box and meta: a stream of last round's records, the new entries' from their
+// buckets).  A workgroup takes 256 consecutive entries: two threads find the new entries
+// bounding its old ones, which are staged in LDS for the threads' searches.
 template <int D>
 __global__ __launch_bounds__(256) void k_ct_dmerge(CtJobs js) {
     const CtJob J = CT_JOB(js);  // by value: the fields stay in registers across the stores
@@ -715,7 +743,6 @@ __global__ __launch_bounds__(256) void k_ct_dmerge(CtJobs js) {
         if (t < n_old + n_new) {
             int64_t out;
             uint64_t h, l;
-            int32_t b;
             if (t < n_old) {
                 int32_t lo = lo_a, hi = lo_b;
                 if (lo_b - lo_a <= 256) {
@@ -734,21 +761,21 @@ __global__ __launch_bounds__(256) void k_ct_dmerge(CtJobs js) {
                 out = t + lo;
                 h = J.odir_code[2 * t];
                 l = J.odir_code[2 * t + 1];
-                b = J.odir_bk[t];
+                J.nmeta[out] = J.ometa[t];
+#pragma unroll
+                for (int q = 0; q < 2 * D; ++q) J.nbox[out * 2 * D + q] = J.obox[t * 2 * D + q];
             } else {
                 const int64_t r = t - n_old;
                 out = J.edir_pos[r] + 1 + r;
                 h = J.edir_code[2 * r];
                 l = J.edir_code[2 * r + 1];
-                b = J.edir_bk[r];
+                const int32_t b = J.edir_bk[r];
+                J.nmeta[out] = leaf_code(b, J.bcnt[b]);
+#pragma unroll
+                for (int q = 0; q < 2 * D; ++q) J.nbox[out * 2 * D + q] = J.bbox[(int64_t)b * 2 * D + q];
             }
             J.ndir_code[2 * out] = h;
             J.ndir_code[2 * out + 1] = l;
-            J.ndir_bk[out] = b;
-            const int32_t cnt = J.bcnt[b];
-            J.nmeta[out] = leaf_code(b, cnt > 0 ? cnt : 1);
-#pragma unroll
-            for (int q = 0; q < 2 * D; ++q) J.nbox[out * 2 * D + q] = J.bbox[(int64_t)b * 2 * D + q];
         }
         __syncthreads();  // s_lo / s_pos reused by the next chunk
     }
@@ -762,6 +789,7 @@ __global__ __launch_bounds__(256) void k_ct_dmerge(CtJobs js) {
 // above it by one workgroup a tree (k_ct_levels), which also copies the seeds and closes the
 // round's counts.
 constexpr int kCtLevelThreads = 1024;
+constexpr int kCtLevelA = 16384;  // level sizes whose adjacent prefix lengths k_ct_levels keeps in LDS
 constexpr int kCtMaxLevels = 10;  // the walk's stack bound (ct_walk kStack); runs of 8 reach it below 8^9 entries
 constexpr int kCtL1Per = kCtL1Tile / 256;
 static_assert(kCtL1Per == 8, "k_ct_lgroup: one run of 8 a thread when grouping by runs");
@@ -819,19 +847,35 @@ __device__ __forceinline__ int ct_block_scan(int v, int32_t *s_w, int nthreads, 
     return before + incl - v;  // exclusive
 }
 
-// level 1's group starts, kCtL1Per consecutive entries a thread; the tile's count
+// level 1's group starts, kCtL1Per consecutive entries a thread; the tile's count.  The
+// adjacent prefix lengths of the tile and 8 entries either side go to LDS first (one coalesced
+// pass over the codes).
+constexpr int kCtHalo = kCtCap;
 __global__ __launch_bounds__(256) void k_ct_lflags(CtJobs js) {
     const CtJob J = CT_JOB(js);  // by value: the fields stay in registers across the stores
     __shared__ int32_t s_w[4];
+    __shared__ uint8_t s_a[kCtL1Tile + 2 * kCtHalo];
     const int64_t n = (int64_t)J.cnt->n_dir + J.cnt->n_new_dir;
     const int64_t t0 = (int64_t)blockIdx.x * kCtL1Tile;
     if (n <= 1 || t0 >= n) return;  // block-uniform
+    const int64_t a0 = t0 - kCtHalo;  // s_a[v] = a[a0 + v]
+    for (int v = threadIdx.x; v < kCtL1Tile + 2 * kCtHalo; v += 256) {
+        const int64_t u = a0 + v;
+        int cp = 0;
+        if (u >= 1 && u < n)
+            cp = c_cpl(J.ndir_code[2 * (u - 1)], J.ndir_code[2 * (u - 1) + 1], J.ndir_code[2 * u], J.ndir_code[2 * u + 1]);
+        s_a[v] = (uint8_t)cp;
+    }
+    __syncthreads();
+    // ct_same_a's window in tile coordinates: [max(0, a0), n) shifted by a0
+    const int64_t wlo = (a0 < 0 ? 0 : a0) - a0, whi = (n < a0 + kCtL1Tile + 2 * kCtHalo ? n : a0 + kCtL1Tile + 2 * kCtHalo) - a0;
     int c = 0;
 #pragma unroll
-    for (int a = 0; a < kCtL1Per; ++a) {
-        const int64_t i = t0 + threadIdx.x * kCtL1Per + a;
+    for (int q = 0; q < kCtL1Per; ++q) {
+        const int64_t i = t0 + threadIdx.x * kCtL1Per + q;
         if (i < n) {
-            const int f = i == 0 || !ct_same(J.ndir_code, nullptr, 0, n, i);
+            // the index / 8 rule counts from the run start 0: shift lo so (i - lo) keeps i's phase
+            const int f = i == 0 || !ct_same_a(s_a, wlo, whi, i - a0);
             J.lflag[i] = f;
             c += f;
         }
@@ -905,6 +949,7 @@ template <int D>
 __global__ __launch_bounds__(kCtLevelThreads) void k_ct_levels(CtJobs js) {
     const CtJob J = CT_JOB(js);  // by value: the fields stay in registers across the stores
     __shared__ int32_t s_w[kCtLevelThreads / 64];
+    __shared__ uint8_t s_a[kCtLevelA];
     const int t = threadIdx.x;
     const int64_t n1 = (int64_t)J.cnt->n_dir + J.cnt->n_new_dir;
     int64_t ls = n1 > 1 ? n1 : 0, n = n1 > 1 ? J.cnt->n_l2 : n1;
@@ -913,9 +958,15 @@ __global__ __launch_bounds__(kCtLevelThreads) void k_ct_levels(CtJobs js) {
         const uint64_t *lc = J.ucode + 2 * ls;  // node i's code at lc[2 i]
         const int64_t per = (n + kCtLevelThreads - 1) / kCtLevelThreads;
         const int64_t i0 = t * per, i1 = i0 + per < n ? i0 + per : n;
+        const bool in_lds = n <= kCtLevelA;  // block-uniform
+        if (in_lds) {
+            for (int64_t u = t; u < n; u += kCtLevelThreads)
+                s_a[u] = (uint8_t)(u == 0 ? 0 : c_cpl(lc[2 * (u - 1)], lc[2 * (u - 1) + 1], lc[2 * u], lc[2 * u + 1]));
+            __syncthreads();
+        }
         int c = 0;
         for (int64_t i = i0; i < i1; ++i) {
-            const int f = i == 0 || !ct_same(lc, nullptr, 0, n, i);
+            const int f = i == 0 || !(in_lds ? ct_same_a(s_a, 0, n, i) : ct_same(lc, nullptr, 0, n, i));
             J.lflag[ls + i] = f;
             c += f;
         }
@@ -1058,7 +1109,7 @@ __global__ void k_ct_bulk_fill(const double *__restrict__ pts, const uint64_t *_
                                const int32_t *__restrict__ leaf, int64_t n_upper, const int64_t *__restrict__ n_dev,
                                double *__restrict__ bpts, int32_t *__restrict__ bids, uint64_t *__restrict__ bcode,
                                int32_t *__restrict__ bcnt, float *__restrict__ bbox, uint64_t *__restrict__ dir_code,
-                               int32_t *__restrict__ dir_bk, CtCounts *__restrict__ cnt) {
+                               uint32_t *__restrict__ dir_meta, float *__restrict__ dir_box, CtCounts *__restrict__ cnt) {
     const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int64_t n = *n_dev < n_upper ? *n_dev : n_upper;
     if (n == 0) {
@@ -1070,7 +1121,11 @@ __global__ void k_ct_bulk_fill(const double *__restrict__ pts, const uint64_t *_
             }
             dir_code[0] = 0;
             dir_code[1] = 0;
-            dir_bk[0] = 0;
+            dir_meta[0] = leaf_code(0, 1);  // never walked: the walk skips an empty tree
+            for (int q = 0; q < D; ++q) {
+                dir_box[q] = __builtin_huge_valf();
+                dir_box[D + q] = -__builtin_huge_valf();
+            }
             cnt->n_dir = cnt->n_buckets = 1;
             cnt->n_seg = cnt->n_new_dir = 0;
             cnt->nidx = 0;
@@ -1096,7 +1151,6 @@ __global__ void k_ct_bulk_fill(const double *__restrict__ pts, const uint64_t *_
     }
     dir_code[2 * r] = sh;
     dir_code[2 * r + 1] = sl;
-    dir_bk[r] = r;
     double lo[D], hi[D];
 #pragma unroll
     for (int q = 0; q < D; ++q) {
@@ -1118,7 +1172,9 @@ __global__ void k_ct_bulk_fill(const double *__restrict__ pts, const uint64_t *_
         bcode[2 * slot + 1] = code[2 * (j + u) + 1];
     }
     write_box<D>(bbox + (int64_t)r * 2 * D, lo, hi);
+    write_box<D>(dir_box + (int64_t)r * 2 * D, lo, hi);
     bcnt[r] = len < kCtCap ? len : kCtCap;
+    dir_meta[r] = leaf_code(r, len < kCtCap ? len : kCtCap);
 }
 
 __global__ __launch_bounds__(64) void k_ct_box_reset(unsigned long long *__restrict__ box) {
@@ -1503,7 +1559,7 @@ CtPlan make_ct_plan(int32_t d, const double *lo, const double *hi, int32_t spati
 }
 
 void CellTree::release() {
-    void *ps[] = {plan, cnt, bpts, bids, bcnt, bcode, bbox, nbox, nmeta, ucode, lflag, lcount, dir_code[0], dir_code[1], dir_bk[0], dir_bk[1],
+    void *ps[] = {plan, cnt, bpts, bids, bcnt, bcode, bbox, nbox[0], nbox[1], nmeta[0], nmeta[1], ucode, lflag, lcount, dir_code[0], dir_code[1],
                   ncode, ccode, scode, edir_code, nrow, crow, npos, nseg, seg_pos, srow, sseg, slead, srank, edir_bk,
                   edir_pos, seg, hull_keys, ibox, hull_pts, hull_ids, fhi, flo, fk0, fk1, fv0, fv1, fflag, fleaf, ftemp};
     for (void *p : ps)
@@ -1532,14 +1588,15 @@ void CellTree::reserve(int64_t c, int32_t d) {
     al((void **)&bcode, sizeof(uint64_t) * 2 * bcap * kCtCap, "ct bucket codes");
     al((void **)&bcnt, sizeof(int32_t) * bcap, "ct bucket counts");
     al((void **)&bbox, sizeof(float) * 2 * d * bcap, "ct bucket boxes");
-    al((void **)&nbox, sizeof(float) * 2 * d * nodes, "ct node boxes");
-    al((void **)&nmeta, sizeof(uint32_t) * nodes, "ct node codes");
+    for (int k = 0; k < 2; ++k) {
+        al((void **)&nbox[k], sizeof(float) * 2 * d * nodes, "ct node boxes");
+        al((void **)&nmeta[k], sizeof(uint32_t) * nodes, "ct node codes");
+    }
     al((void **)&ucode, sizeof(uint64_t) * 2 * nodes, "ct node cell codes");
     al((void **)&lflag, sizeof(int32_t) * nodes, "ct level scratch");
     al((void **)&lcount, sizeof(int32_t) * (bcap / kCtL1Tile + 1), "ct level scratch");
     for (int k = 0; k < 2; ++k) {
         al((void **)&dir_code[k], sizeof(uint64_t) * 2 * bcap, "ct directory");
-        al((void **)&dir_bk[k], sizeof(int32_t) * bcap, "ct directory");
     }
     al((void **)&ncode, sizeof(uint64_t) * 2 * kCtSeg, "ct new codes");
     al((void **)&ccode, sizeof(uint64_t) * 2 * kCtSeg, "ct chunk codes");
@@ -1614,15 +1671,15 @@ CtJob CellTree::prepare(const double *pts, int64_t n_upper, const int64_t *n_dev
         hip_check(hipcub::DeviceScan::ExclusiveSum(ftemp, tb, fflag, fleaf, (int)n_upper, stream), "ct leaf scan");
         hipLaunchKernelGGL(d == 3 ? k_ct_bulk_fill<3> : d == 7 ? k_ct_bulk_fill<7> : k_ct_bulk_fill<15>, dim3(blocks),
                            dim3(256), 0, stream, pts, fk1, fv0, fflag, fleaf, n_upper, n_dev, bpts, bids, bcode, bcnt,
-                           bbox, dir_code[old], dir_bk[old], cnt);
+                           bbox, dir_code[old], nmeta[old], nbox[old], cnt);
         hip_check(hipGetLastError(), "k_ct_bulk_fill");
     }
     t.d = d;
     t.n_bound = std::max<int64_t>(std::min<int64_t>(n_upper, bcap), 1);
     t.n_dev = n_dev;
     t.root = &cnt->root;
-    t.nmeta = nmeta;
-    t.nbox = nbox;
+    t.nmeta = nmeta[nw];
+    t.nbox = nbox[nw];
     t.bpts = bpts;
     t.bids = bids;
     t.hull_pts = hull_pts;
@@ -1642,11 +1699,11 @@ CtJob CellTree::prepare(const double *pts, int64_t n_upper, const int64_t *n_dev
     J.bcnt = bcnt;
     J.bbox = bbox;
     J.odir_code = dir_code[old];
-    J.odir_bk = dir_bk[old];
+    J.ometa = nmeta[old];
+    J.obox = nbox[old];
     J.ndir_code = dir_code[nw];
-    J.ndir_bk = dir_bk[nw];
-    J.nmeta = nmeta;
-    J.nbox = nbox;
+    J.nmeta = nmeta[nw];
+    J.nbox = nbox[nw];
     J.ucode = ucode;
     J.lflag = lflag;
     J.lcount = lcount;

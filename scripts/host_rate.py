@@ -43,7 +43,7 @@ def main():
     torch.cuda.synchronize()
     t2 = time.perf_counter()
     print(f"enqueue {1e6 * (t1 - t0) / a.rounds:.1f} us/round, wall {1e6 * (t2 - t0) / a.rounds:.1f} us/round "
-          f"({a.rounds} rounds, split={os.environ.get('MPT_TAIL_SPLIT', 'default')})", flush=True)
+          f"({a.rounds} rounds)", flush=True)
 
 
 if __name__ == "__main__":

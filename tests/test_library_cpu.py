@@ -187,3 +187,12 @@ def test_flann_l2_head_rest_split(tmp_path):
                     "c++", str(src), "-o", str(exe)], check=True)
     out = subprocess.run([str(exe)], check=True, capture_output=True, text=True).stdout.strip()
     assert out == "0"
+
+
+def test_mesh_dir_override(tmp_path):
+    """MPT_MESH_DIR (the one path variable) redirects scenes.mesh_path."""
+    code = "from motionplanningtoolkit_amd import scenes; print(scenes.mesh_path('env_model'))"
+    env = dict(os.environ, MPT_MESH_DIR=str(tmp_path))
+    out = subprocess.run(["python", "-c", code], cwd=REPO, env=env, capture_output=True, text=True, timeout=120)
+    assert out.returncode == 0, out.stderr
+    assert out.stdout.strip().startswith(str(tmp_path))
