@@ -17,7 +17,7 @@ constexpr int kCtBits = 126;       // code bits (two 64-bit words)
 constexpr int kCtSeg = 8192;       // new points one round inserts (the host bounds a round's growth)
 constexpr int kCtScratch = kCtSeg * (kCtCap + 1);  // a round's split elements (new + old of touched buckets)
 constexpr int kCtHull = 64;        // seed points (extreme points in fixed directions)
-constexpr int kCtL1Tile = 2048;    // level-1 entries a workgroup groups (k_ct_lflags / k_ct_lgroup)
+constexpr int kCtL1Tile = 512;     // level-1 entries a workgroup groups (k_ct_lflags / k_ct_lgroup)
 
 // the fixed code plan over the sampling ranges and the seed directions
 struct CtPlan {

@@ -350,6 +350,54 @@ __global__ __launch_bounds__(256) void k_ct_crank(CtJobs js) {
     else ct_crank_n<kCtChunks>(J, m, e);
 }
 
+// Rounds of at most kCtLdsSort new points (the usual case: one round's K): one workgroup a tree
+// sorts them by (code, row) in LDS with a bitonic network (80 KiB: gfx950's 160 KiB LDS takes
+// it), instead of the chunk sort and the cross-chunk ranks.
+constexpr int kCtLdsSort = 4096;
+constexpr int kCtLdsSortThreads = 1024;
+__global__ __launch_bounds__(kCtLdsSortThreads) void k_ct_lsort(CtJobs js) {
+    const CtJob J = CT_JOB(js);  // by value: the fields stay in registers across the stores
+    __shared__ uint64_t s_h[kCtLdsSort], s_l[kCtLdsSort];
+    __shared__ int32_t s_r[kCtLdsSort];
+    // the host's bound (mb <= kCtLdsSort) chose this kernel; a broken bound is counted by
+    // k_ct_ncodes and must not write past the LDS arrays
+    const int m = (int)(ct_new_count(J) < kCtLdsSort ? ct_new_count(J) : kCtLdsSort);
+    if (m <= 1) return;
+    int P = 2;
+    while (P < m) P <<= 1;
+    for (int i = threadIdx.x; i < P; i += kCtLdsSortThreads) {
+        const bool live = i < m;
+        s_h[i] = live ? J.ncode[2 * i] : ~0ull;  // padding sorts last (codes use 126 bits)
+        s_l[i] = live ? J.ncode[2 * i + 1] : ~0ull;
+        s_r[i] = live ? J.nrow[i] : 0x7fffffff;
+    }
+    __syncthreads();
+    for (int k = 2; k <= P; k <<= 1) {
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            for (int p = threadIdx.x; p < P / 2; p += kCtLdsSortThreads) {
+                const int i = 2 * j * (p / j) + (p % j), q = i + j;
+                const uint64_t ah = s_h[i], al = s_l[i], bh = s_h[q], bl = s_l[q];
+                const int32_t ar = s_r[i], br = s_r[q];
+                const bool up = (i & k) == 0;
+                if (cr_lt(bh, bl, br, ah, al, ar) == up) {
+                    s_h[i] = bh;
+                    s_l[i] = bl;
+                    s_r[i] = br;
+                    s_h[q] = ah;
+                    s_l[q] = al;
+                    s_r[q] = ar;
+                }
+            }
+            __syncthreads();
+        }
+    }
+    for (int i = threadIdx.x; i < m; i += kCtLdsSortThreads) {
+        J.ncode[2 * i] = s_h[i];
+        J.ncode[2 * i + 1] = s_l[i];
+        J.nrow[i] = s_r[i];
+    }
+}
+
 // each sorted new point's directory position: the last entry whose start is <= its code
 __global__ __launch_bounds__(256) void k_ct_locate(CtJobs js) {
     const CtJob J = CT_JOB(js);  // by value: the fields stay in registers across the stores
@@ -712,72 +760,64 @@ __global__ __launch_bounds__(256) void k_ct_split_fill(CtJobs js) {
 // The new directory: old entry p goes to p + (new entries of segments before p), new entry r
 // (of the segment at directory position q) to q + 1 + r; with each entry its level-1 node (the
 // bucket's box and meta: a stream of last round's records, the new entries' from their
-// buckets).  A workgroup takes 256 consecutive entries: two threads find the new entries
-// bounding its old ones, which are staged in LDS for the threads' searches.
+// buckets).  A workgroup takes 256 consecutive old entries: two threads find the new entries
+// bounding them, which are staged in LDS for the threads' searches; the boxes then move as
+// 8-byte words, consecutive threads on consecutive words (coalesced both ways).
 template <int D>
 __global__ __launch_bounds__(256) void k_ct_dmerge(CtJobs js) {
     const CtJob J = CT_JOB(js);  // by value: the fields stay in registers across the stores
     __shared__ int32_t s_pos[256];
     __shared__ int32_t s_lo[2];
+    __shared__ int32_t s_shift[256];
     const int64_t n_old = J.cnt->n_dir, n_new = J.cnt->n_new_dir;
-    for (int64_t c0 = (int64_t)blockIdx.x * 256; c0 < n_old + n_new; c0 += (int64_t)gridDim.x * 256) {
+    for (int64_t c0 = (int64_t)blockIdx.x * 256; c0 < n_old; c0 += (int64_t)gridDim.x * 256) {
         const int64_t t = c0 + threadIdx.x;
-        int32_t lo_a = 0, lo_b = 0;
-        if (c0 < n_old) {  // block-uniform
-            if (threadIdx.x < 2) {  // new entries whose segment lies before c0 / before the chunk's end
-                const int64_t key = threadIdx.x == 0 ? c0 : (c0 + 256 < n_old ? c0 + 256 : n_old);
-                int64_t lo = 0, hi = n_new;
-                while (lo < hi) {
-                    const int64_t mid = (lo + hi) >> 1;
-                    if (J.edir_pos[mid] < key) lo = mid + 1;
-                    else hi = mid;
-                }
-                s_lo[threadIdx.x] = (int32_t)lo;
+        if (threadIdx.x < 2) {  // new entries whose segment lies before c0 / before the chunk's end
+            const int64_t key = threadIdx.x == 0 ? c0 : (c0 + 256 < n_old ? c0 + 256 : n_old);
+            int64_t lo = 0, hi = n_new;
+            while (lo < hi) {
+                const int64_t mid = (lo + hi) >> 1;
+                if (J.edir_pos[mid] < key) lo = mid + 1;
+                else hi = mid;
             }
-            __syncthreads();
-            lo_a = s_lo[0];
-            lo_b = s_lo[1];
-            if (lo_b - lo_a <= 256 && threadIdx.x < lo_b - lo_a) s_pos[threadIdx.x] = J.edir_pos[lo_a + threadIdx.x];
-            __syncthreads();
+            s_lo[threadIdx.x] = (int32_t)lo;
         }
-        if (t < n_old + n_new) {
-            int64_t out;
-            uint64_t h, l;
-            if (t < n_old) {
-                int32_t lo = lo_a, hi = lo_b;
-                if (lo_b - lo_a <= 256) {
-                    while (lo < hi) {
-                        const int32_t mid = (lo + hi) >> 1;
-                        if (s_pos[mid - lo_a] < t) lo = mid + 1;
-                        else hi = mid;
-                    }
-                } else {
-                    while (lo < hi) {
-                        const int32_t mid = (lo + hi) >> 1;
-                        if (J.edir_pos[mid] < t) lo = mid + 1;
-                        else hi = mid;
-                    }
-                }
-                out = t + lo;
-                h = J.odir_code[2 * t];
-                l = J.odir_code[2 * t + 1];
-                J.nmeta[out] = J.ometa[t];
-#pragma unroll
-                for (int q = 0; q < 2 * D; ++q) J.nbox[out * 2 * D + q] = J.obox[t * 2 * D + q];
-            } else {
-                const int64_t r = t - n_old;
-                out = J.edir_pos[r] + 1 + r;
-                h = J.edir_code[2 * r];
-                l = J.edir_code[2 * r + 1];
-                const int32_t b = J.edir_bk[r];
-                J.nmeta[out] = leaf_code(b, J.bcnt[b]);
-#pragma unroll
-                for (int q = 0; q < 2 * D; ++q) J.nbox[out * 2 * D + q] = J.bbox[(int64_t)b * 2 * D + q];
+        __syncthreads();
+        const int32_t lo_a = s_lo[0], lo_b = s_lo[1];
+        const bool staged = lo_b - lo_a <= 256;
+        if (staged && threadIdx.x < lo_b - lo_a) s_pos[threadIdx.x] = J.edir_pos[lo_a + threadIdx.x];
+        __syncthreads();
+        if (t < n_old) {
+            int32_t lo = lo_a, hi = lo_b;
+            while (lo < hi) {
+                const int32_t mid = (lo + hi) >> 1;
+                if ((staged ? s_pos[mid - lo_a] : J.edir_pos[mid]) < t) lo = mid + 1;
+                else hi = mid;
             }
-            J.ndir_code[2 * out] = h;
-            J.ndir_code[2 * out + 1] = l;
+            const int64_t out = t + lo;
+            s_shift[threadIdx.x] = lo;
+            J.ndir_code[2 * out] = J.odir_code[2 * t];
+            J.ndir_code[2 * out + 1] = J.odir_code[2 * t + 1];
+            J.nmeta[out] = J.ometa[t];
         }
-        __syncthreads();  // s_lo / s_pos reused by the next chunk
+        __syncthreads();
+        const int ne = (int)(n_old - c0 < 256 ? n_old - c0 : 256);
+        const uint2 *src = reinterpret_cast<const uint2 *>(J.obox) + c0 * D;  // a box = D words of 8 bytes
+        uint2 *dst = reinterpret_cast<uint2 *>(J.nbox);
+        for (int w = threadIdx.x; w < ne * D; w += 256) {
+            const int e = w / D;
+            dst[(c0 + e + s_shift[e]) * D + (w - e * D)] = src[w];
+        }
+        __syncthreads();  // s_lo / s_pos / s_shift reused by the next chunk
+    }
+    for (int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x; r < n_new; r += (int64_t)gridDim.x * 256) {
+        const int64_t out = J.edir_pos[r] + 1 + r;
+        const int32_t b = J.edir_bk[r];
+        J.ndir_code[2 * out] = J.edir_code[2 * r];
+        J.ndir_code[2 * out + 1] = J.edir_code[2 * r + 1];
+        J.nmeta[out] = leaf_code(b, J.bcnt[b]);
+#pragma unroll
+        for (int q = 0; q < 2 * D; ++q) J.nbox[out * 2 * D + q] = J.bbox[(int64_t)b * 2 * D + q];
     }
 }
 
@@ -791,8 +831,7 @@ __global__ __launch_bounds__(256) void k_ct_dmerge(CtJobs js) {
 constexpr int kCtLevelThreads = 1024;
 constexpr int kCtLevelA = 16384;  // level sizes whose adjacent prefix lengths k_ct_levels keeps in LDS
 constexpr int kCtMaxLevels = 10;  // the walk's stack bound (ct_walk kStack); runs of 8 reach it below 8^9 entries
-constexpr int kCtL1Per = kCtL1Tile / 256;
-static_assert(kCtL1Per == 8, "k_ct_lgroup: one run of 8 a thread when grouping by runs");
+constexpr int kCtL1Per = kCtL1Tile / 256;  // level-1 entries a thread of k_ct_lflags / k_ct_lgroup
 
 // the levels a tree needs when level `lev` has G groups and runs of 8 follow
 __device__ __forceinline__ bool ct_fixed(int64_t n, int64_t G, int lev) {
@@ -885,12 +924,16 @@ __global__ __launch_bounds__(256) void k_ct_lflags(CtJobs js) {
     if (threadIdx.x == 0) J.lcount[blockIdx.x] = tot;
 }
 
-// level 2: each tile's groups, numbered after the tiles before it
+// level 2: each tile's groups, numbered after the tiles before it.  The tile's boxes and flags
+// (and the 7 entries after it, where its last groups end) are staged in LDS with coalesced loads.
 template <int D>
 __global__ __launch_bounds__(256) void k_ct_lgroup(CtJobs js) {
     const CtJob J = CT_JOB(js);  // by value: the fields stay in registers across the stores
+    constexpr int kSpan = kCtL1Tile + kCtCap - 1;
     __shared__ int32_t s_w[4];
     __shared__ int64_t s_sum[2];
+    __shared__ uint2 s_box[kSpan * D];  // box e of the span: words [e * D, e * D + D)
+    __shared__ uint8_t s_f[kSpan];
     const int64_t n = (int64_t)J.cnt->n_dir + J.cnt->n_new_dir;
     const int64_t t0 = (int64_t)blockIdx.x * kCtL1Tile;
     if (n <= 1 || t0 >= n) return;  // block-uniform
@@ -912,33 +955,61 @@ __global__ __launch_bounds__(256) void k_ct_lgroup(CtJobs js) {
             s_sum[1] = before;
         }
     }
+    const int span = (int)(n - t0 < kSpan ? n - t0 : kSpan);
+    const uint2 *src = reinterpret_cast<const uint2 *>(J.nbox) + t0 * D;
+    for (int w = threadIdx.x; w < span * D; w += 256) s_box[w] = src[w];
+    for (int e = threadIdx.x; e < span; e += 256) s_f[e] = (uint8_t)J.lflag[t0 + e];
     __syncthreads();
     const int64_t G = s_sum[0];
     const bool fixed = ct_fixed(n, G, 1);
     if (blockIdx.x == 0 && threadIdx.x == 0) J.cnt->n_l2 = (int32_t)(fixed ? (n + 7) / 8 : G);
-    const int64_t i0 = t0 + threadIdx.x * kCtL1Per;
-    if (fixed) {
-        if (i0 < n && (i0 & 7) == 0) {  // kCtL1Per == 8: one run a thread
-            const int len = n - i0 < 8 ? (int)(n - i0) : 8;
-            ct_parent<D>(J, J.ndir_code, i0, len, n + i0 / 8, i0);
-        }
-        return;
-    }
+    const int e0 = threadIdx.x * kCtL1Per;  // this thread's entries [e0, e0 + kCtL1Per) of the tile
     int f[kCtL1Per], c = 0;
 #pragma unroll
     for (int a = 0; a < kCtL1Per; ++a) {
-        f[a] = i0 + a < n ? J.lflag[i0 + a] : 0;
+        const int e = e0 + a;
+        f[a] = t0 + e < n && (fixed ? ((t0 + e) & 7) == 0 : s_f[e] != 0);
         c += f[a];
     }
     int tot;
-    int64_t g = s_sum[1] + ct_block_scan(c, s_w, 256, tot);
+    const int64_t ex = ct_block_scan(c, s_w, 256, tot);
+    int64_t g = fixed ? 0 : s_sum[1] + ex;
 #pragma unroll
     for (int a = 0; a < kCtL1Per; ++a) {
         if (!f[a]) continue;
-        const int64_t i = i0 + a;
+        const int e = e0 + a;
+        const int64_t i = t0 + e;
         int len = 1;
-        while (i + len < n && len < kCtCap && !J.lflag[i + len]) ++len;
-        ct_parent<D>(J, J.ndir_code, i, len, n + g, i);
+        if (fixed) {
+            len = n - i < 8 ? (int)(n - i) : 8;
+            g = i / 8;
+        } else {
+            while (i + len < n && len < kCtCap && !s_f[e + len]) ++len;
+        }
+        float lo[D], hi[D];
+        const float *b0 = reinterpret_cast<const float *>(s_box + e * D);
+#pragma unroll
+        for (int q = 0; q < D; ++q) {
+            lo[q] = b0[q];
+            hi[q] = b0[D + q];
+        }
+        for (int u = 1; u < len; ++u) {
+            const float *bu = reinterpret_cast<const float *>(s_box + (e + u) * D);
+#pragma unroll
+            for (int q = 0; q < D; ++q) {
+                lo[q] = fminf(lo[q], bu[q]);
+                hi[q] = fmaxf(hi[q], bu[D + q]);
+            }
+        }
+        const int64_t P = n + g;
+#pragma unroll
+        for (int q = 0; q < D; ++q) {
+            J.nbox[P * 2 * D + q] = lo[q];
+            J.nbox[P * 2 * D + D + q] = hi[q];
+        }
+        J.nmeta[P] = inner_code(i, len);
+        J.ucode[2 * P] = J.ndir_code[2 * i];
+        J.ucode[2 * P + 1] = J.ndir_code[2 * i + 1];
         ++g;
     }
 }
@@ -1388,7 +1459,7 @@ __device__ __forceinline__ void ct_walk(const CellTreeDev &T, const double *__re
             ++n_steps;
             __builtin_amdgcn_wave_barrier();
             const bool act = have && !(lbs > bdf);
-            bool keep = false, leaf = false;
+            bool keep = false, better = false;
             float lbf = 0.0f;
             uint32_t child = 0;
             if (act && (code & kCtLeafBit)) {
@@ -1401,7 +1472,7 @@ __device__ __forceinline__ void ct_walk(const CellTreeDev &T, const double *__re
                     const double dd = flann_l2<D>(qq, row);
                     const int32_t id = ((gi32)T.bids)[p];
                     ++n_pts;
-                    leaf = true;
+                    better = (dd < bd) | ((dd == bd) & (id < bi));
                     nn_take(bd, bi, dd, id);
                 }
             } else if (act) {
@@ -1418,9 +1489,9 @@ __device__ __forceinline__ void ct_walk(const CellTreeDev &T, const double *__re
                 }
             }
             // the parts' best, then the survivors against it.  Wave-uniform skips: a group's
-            // lanes already share one best unless a lane examined a point this step, and with no
-            // survivor in the wave there is nothing to rank
-            if (__ballot(leaf)) {
+            // lanes already share one best unless a lane found a better point this step, and
+            // with no survivor in the wave there is nothing to rank
+            if (__ballot(better)) {
                 best_group<G>(bd, bi);
                 bdf = f32_up(bd);
             }
@@ -1750,10 +1821,14 @@ void launch_ct_jobs(const CtJob *d_jobs, const CtJob *h_jobs, int32_t n, int32_t
         hipLaunchKernelGGL(by_d(k_ct_ncodes<3>, k_ct_ncodes<7>, k_ct_ncodes<15>), dim3(b256, yn), dim3(64 * kCtWaves), 0,
                            stream, js);
         hip_check(hipGetLastError(), "k_ct_ncodes");
-        const unsigned chunks = (unsigned)((mb + kCtChunk - 1) / kCtChunk);
-        hipLaunchKernelGGL(k_ct_csort, dim3((chunks + kCtChunkWaves - 1) / kCtChunkWaves, yn), dim3(64 * kCtChunkWaves), 0,
-                           stream, js);
-        hipLaunchKernelGGL(k_ct_crank, dim3(b256, yn), dim3(256), 0, stream, js);
+        if (mb <= kCtLdsSort) {
+            hipLaunchKernelGGL(k_ct_lsort, dim3(1, yn), dim3(kCtLdsSortThreads), 0, stream, js);
+        } else {
+            const unsigned chunks = (unsigned)((mb + kCtChunk - 1) / kCtChunk);
+            hipLaunchKernelGGL(k_ct_csort, dim3((chunks + kCtChunkWaves - 1) / kCtChunkWaves, yn),
+                               dim3(64 * kCtChunkWaves), 0, stream, js);
+            hipLaunchKernelGGL(k_ct_crank, dim3(b256, yn), dim3(256), 0, stream, js);
+        }
         hipLaunchKernelGGL(k_ct_locate, dim3(b256, yn), dim3(256), 0, stream, js);
         hipLaunchKernelGGL(k_ct_segments, dim3(1, yn), dim3(kCtSegThreads), 0, stream, js);
         hipLaunchKernelGGL(by_d(k_ct_apply<3>, k_ct_apply<7>, k_ct_apply<15>), dim3(b256, yn), dim3(256), 0, stream, js);
