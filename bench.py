@@ -367,7 +367,7 @@ def joint_stage_table(times, c, K, nj, n_tot, d, pmax, geo, summ):
     them): compulsory bytes of all seeds' work, the measured traffic of every kernel of the
     stage's chain, FP64 of the collide stages; c = the seeds' summed work counters."""
     units = K * pmax * geo.get("links", 1)
-    per_sub = max(1, (2 ** 22 // geo["clusters"]) // units)
+    per_sub = max(1, (2 ** 25 // geo["clusters"]) // units)  # broad.hip kSplitChunkThreads
     n_sub = -(-nj // per_sub)
     stages = {}
     for s, ms in times.items():

@@ -35,9 +35,12 @@ namespace mpt {
 constexpr int kPairThreads = 256;   // k_pairs workgroup (4 waves)
 constexpr int kPairCap = 512;       // env triangles per k_pairs wave segment (256: the room overflowed units into k_overflow, 17-27 us a round)
 constexpr int kHdrCap = 64;         // headers per segment (one per lane at most)
-constexpr int kCandCap = 2048;      // candidates per k_cands wave (then the spill list)
-constexpr int64_t kSplitChunkThreads = int64_t(1) << 22;  // (unit, cluster) threads per launch of the two-phase path
-constexpr int kSpillCap = 1 << 22;  // shared spill list (48 MiB)
+constexpr int kCandCap = 8192;      // candidates per k_cands wave (then the spill list)
+// (unit, cluster) threads per launch of the two-phase path: a whole config-5 round of 256 blimp
+// seeds (1 M units x 22 clusters) in one chunk; its scratch (pair words, headers, candidates:
+// ~2 GiB) is small beside 288 GB of HBM, and one launch per kernel has one tail, not six
+constexpr int64_t kSplitChunkThreads = int64_t(1) << 25;
+constexpr int kSpillCap = 1 << 23;  // shared spill list (96 MiB)
 constexpr int kLdsItems = 2048;     // env tree staged in LDS by k_pairs up to this size (64 KiB)
 constexpr int kCandsLdsItems = 1024;  // env triangle items staged in LDS by k_cands up to this count
 constexpr int kStack = kMaxLevels;  // per-thread walk stack (general trees)

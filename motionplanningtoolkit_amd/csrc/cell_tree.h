@@ -25,6 +25,8 @@ struct CtPlan {
     uint32_t qmax[kCtMaxDim];
     int32_t n;                           // code bits used (<= kCtBits)
     int8_t dim[kCtBits], bit[kCtBits];   // MSB first
+    int8_t nb[kCtMaxDim];                // bits of each dim: level l (MSB first) takes the dims with nb > l
+    int32_t bmax;                        // levels (the most bits of a dim)
     // seed slot h keeps the indexed point of the largest score: kind 0: hdir . (the first three
     // state dims), kind 1: -x[hdim], kind 2: +x[hdim]
     float hdir[kCtHull][3];
@@ -32,6 +34,7 @@ struct CtPlan {
     int32_t n_hull;
     int32_t pad;
 };
+static_assert(sizeof(CtPlan) % 4 == 0, "the kernels copy the plan to LDS as 4-byte words");
 // one quantisation step h for every dim (cubic cells in raw state units, the units of FLANN's
 // L2), the smallest for which the bits sum to <= kCtBits (<= 31 a dim), widest dims split first;
 // seed directions over the first `spatial` dims
@@ -44,7 +47,9 @@ struct CtCounts {
     int32_t n_seg;       // this round's touched buckets
     int32_t n_new_dir;   // this round's new directory entries
     int32_t root;        // the hierarchy's root node
-    int32_t n_l2;        // this round's level-2 node count (k_ct_lgroup)
+    int32_t n_l2;        // this round's level-2 / level-3 node counts (k_ct_lgroup)
+    int32_t n_l3;
+    int32_t pad;
     int64_t nidx;        // points indexed (rows [0, nidx) of the node array)
 };
 

@@ -78,17 +78,21 @@ __device__ __forceinline__ void ct_code(const CtPlan &P, const double (&x)[D], u
         const uint32_t m = P.qmax[j];
         q[j] = u <= 0.0 ? 0u : (u >= (double)m ? m : (uint32_t)u);
     }
+    // level by level (MSB first): the level's bits of the dims that have one, gathered into a
+    // word and shifted in together (the plan's dim / bit order)
     h = 0;
     l = 0;
-    const int32_t nb = P.n;
-    for (int k = 0; k < nb; ++k) {
-        const int32_t dk = P.dim[k];
-        uint32_t v = q[0];
+    for (int lev = P.bmax - 1; lev >= 0; --lev) {
+        uint32_t w = 0;
+        int c = 0;
 #pragma unroll
-        for (int j = 1; j < D; ++j)
-            if (j == dk) v = q[j];
-        h = (h << 1) | (l >> 63);
-        l = (l << 1) | (uint64_t)((v >> P.bit[k]) & 1u);
+        for (int j = 0; j < D; ++j)
+            if (P.nb[j] > lev) {
+                w = (w << 1) | ((q[j] >> lev) & 1u);
+                ++c;
+            }
+        h = (h << c) | (l >> (64 - c));  // 1 <= c <= D: the widest dim has a bit at every level
+        l = (l << c) | w;
     }
 }
 
@@ -374,8 +378,9 @@ __global__ __launch_bounds__(kCtLdsSortThreads) void k_ct_lsort(CtJobs js) {
     __syncthreads();
     for (int k = 2; k <= P; k <<= 1) {
         for (int j = k >> 1; j > 0; j >>= 1) {
+            const int lj = __ffs(j) - 1;  // j = 2^lj
             for (int p = threadIdx.x; p < P / 2; p += kCtLdsSortThreads) {
-                const int i = 2 * j * (p / j) + (p % j), q = i + j;
+                const int i = ((p >> lj) << (lj + 1)) | (p & (j - 1)), q = i + j;
                 const uint64_t ah = s_h[i], al = s_l[i], bh = s_h[q], bl = s_l[q];
                 const int32_t ar = s_r[i], br = s_r[q];
                 const bool up = (i & k) == 0;
@@ -491,6 +496,195 @@ __global__ __launch_bounds__(kCtSegThreads) void k_ct_segments(CtJobs js) {
         J.seg_pos[s] = pos[a];
         // scratch positions no split element takes: all of an append segment's, the 8 - c
         // after a split segment's c + k elements
+        const int32_t from = c + k <= kCtCap ? off : off + c + k;
+        for (int e = from; e < off + k + 8; ++e) J.sseg[e] = -1;
+    }
+    if (t == 0) J.cnt->n_seg = s_total;
+}
+
+// A round of at most kCtLdsSort new points (the usual case: one round's K) in one workgroup a
+// tree, in place of k_ct_ncodes, k_ct_lsort, k_ct_locate and k_ct_segments: codes, box and
+// seed offers; the bitonic sort in LDS; each sorted point's directory position; the segments.
+constexpr int kCtFrontThreads = 512;  // 8 points a thread: their codes stay in registers (no spills)
+template <int D>
+__global__ __launch_bounds__(kCtFrontThreads) void k_ct_front(CtJobs js) {
+    constexpr int T = kCtFrontThreads, PER = kCtLdsSort / T;
+    const CtJob J = CT_JOB(js);  // by value: the fields stay in registers across the stores
+    __shared__ uint64_t s_hl[2 * kCtLdsSort];  // the codes' words (first: the seed offers' row staging)
+    __shared__ int32_t s_r[kCtLdsSort];
+    uint64_t *s_h = s_hl, *s_l = s_hl + kCtLdsSort;
+    __shared__ CtPlan s_plan;
+    __shared__ int32_t s_sum[T / 64];
+    __shared__ int32_t s_total;
+    static_assert(sizeof(double) * (T / 64) * 64 * D <= sizeof(s_hl), "row staging fits (d <= 7)");
+    const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+    const int64_t base = J.cnt->nidx, mraw = *J.T.n_dev - base;
+    if ((mraw > kCtSeg || mraw > J.mb) && t == 0 && J.err) atomicAdd(J.err, 1ull);  // the host's bound broken
+    const int m = (int)(mraw < 0 ? 0 : (mraw > kCtLdsSort ? kCtLdsSort : mraw));
+    for (int w = t; w < (int)(sizeof(CtPlan) / 4); w += T)
+        reinterpret_cast<uint32_t *>(&s_plan)[w] = reinterpret_cast<const uint32_t *>(J.plan)[w];
+    __syncthreads();
+    // 1. codes (kept in registers), the persistent box, the seed offers
+    uint64_t ch[PER], cl[PER];
+    double(*s_rows)[64][D] = reinterpret_cast<double(*)[64][D]>(s_hl);  // [wave][lane][dim]
+#pragma unroll
+    for (int a = 0; a < PER; ++a) {
+        const int i = a * T + t;  // wave-contiguous rows (hull_offer's row0 + lane)
+        const bool live = i < m;
+        double x[D];
+        unsigned long long mn[D], mx[D];
+        if (live) {
+            load_global<D>(J.pts + (base + i) * D, x);
+            ct_code<D>(s_plan, x, ch[a], cl[a]);
+#pragma unroll
+            for (int j = 0; j < D; ++j) mn[j] = mx[j] = okey(x[j]);
+        } else {
+            ch[a] = cl[a] = ~0ull;  // padding sorts last (codes use 126 bits)
+#pragma unroll
+            for (int j = 0; j < D; ++j) {
+                x[j] = 0.0;
+                mn[j] = ~0ull;
+                mx[j] = 0ull;
+            }
+        }
+        if (__ballot(live)) {  // wave-uniform
+#pragma unroll
+            for (int j = 0; j < D; ++j) {
+#pragma unroll
+                for (int off = 32; off > 0; off >>= 1) {
+                    const unsigned long long omn = __shfl_xor(mn[j], off), omx = __shfl_xor(mx[j], off);
+                    mn[j] = omn < mn[j] ? omn : mn[j];
+                    mx[j] = omx > mx[j] ? omx : mx[j];
+                }
+            }
+            if (lane == 0) {
+#pragma unroll
+                for (int j = 0; j < D; ++j) {
+                    atomicMin(J.ibox + j, mn[j]);
+                    atomicMax(J.ibox + kCtMaxDim + j, mx[j]);
+                }
+            }
+            hull_offer<D>(s_plan, x, live, base + a * T + wave * 64, s_rows[wave], J.hull_keys);
+        }
+    }
+    __syncthreads();  // the row staging is done with: the codes take its place
+    if (m == 0) return;  // block-uniform
+    int P = 2;
+    while (P < m) P <<= 1;
+#pragma unroll
+    for (int a = 0; a < PER; ++a) {
+        const int i = a * T + t;
+        if (i < P) {
+            s_h[i] = ch[a];
+            s_l[i] = cl[a];
+            s_r[i] = i < m ? (int32_t)(base + i) : 0x7fffffff;
+        }
+    }
+    __syncthreads();
+    // 2. the bitonic sort by (code, row)
+    for (int k = 2; k <= P; k <<= 1) {
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            const int lj = __ffs(j) - 1;  // j = 2^lj
+            for (int p = t; p < P / 2; p += T) {
+                const int i = ((p >> lj) << (lj + 1)) | (p & (j - 1)), q = i + j;
+                const uint64_t ah = s_h[i], al = s_l[i], bh = s_h[q], bl = s_l[q];
+                const int32_t ar = s_r[i], br = s_r[q];
+                const bool up = (i & k) == 0;
+                if (cr_lt(bh, bl, br, ah, al, ar) == up) {
+                    s_h[i] = bh;
+                    s_l[i] = bl;
+                    s_r[i] = br;
+                    s_h[q] = ah;
+                    s_l[q] = al;
+                    s_r[q] = ar;
+                }
+            }
+            __syncthreads();
+        }
+    }
+    // 3. the sorted points out (thread t: points [PER t, PER t + PER)) and their directory positions
+    int32_t pos[PER];
+    const int n_dir = J.cnt->n_dir;
+#pragma unroll
+    for (int a = 0; a < PER; ++a) {
+        const int j = t * PER + a;
+        pos[a] = -1;
+        if (j < m) {
+            const uint64_t h = s_h[j], l = s_l[j];
+            J.ncode[2 * j] = h;
+            J.ncode[2 * j + 1] = l;
+            J.nrow[j] = s_r[j];
+            int lo = 0, hi = n_dir;  // entry 0 starts at code 0: the answer is in [0, n_dir)
+            while (hi - lo > 1) {
+                const int mid = (lo + hi) >> 1;
+                const uint64_t sh = J.odir_code[2 * mid], sl = J.odir_code[2 * mid + 1];
+                if (sh < h || (sh == h && sl <= l)) lo = mid;
+                else hi = mid;
+            }
+            pos[a] = lo;
+        }
+    }
+    __syncthreads();  // the LDS arrays now hold the positions and the segments' first points
+    int32_t *s_pos = reinterpret_cast<int32_t *>(s_l);    // [kCtLdsSort]
+    int32_t *s_first = reinterpret_cast<int32_t *>(s_h);  // [kCtLdsSort + 1] (s_h holds 2 kCtLdsSort words)
+#pragma unroll
+    for (int a = 0; a < PER; ++a)
+        if (t * PER + a < m) s_pos[t * PER + a] = pos[a];
+    __syncthreads();
+    // 4. the segments (as k_ct_segments): runs of equal positions, segment s = (bucket, old
+    //    count, new count, scratch offset j0 + 8 s); scratch positions no split element takes -1
+    const int32_t prev = t > 0 && t * PER - 1 < m ? s_pos[t * PER - 1] : -2;
+    int head[PER], cnt = 0;
+#pragma unroll
+    for (int a = 0; a < PER; ++a) {
+        const int j = t * PER + a;
+        const int32_t pv = a == 0 ? prev : pos[a - 1];
+        head[a] = (j < m && (j == 0 || pos[a] != pv)) ? 1 : 0;
+        cnt += head[a];
+    }
+    int incl = cnt;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const int o = __shfl_up(incl, off);
+        if (lane >= off) incl += o;
+    }
+    if (lane == 63) s_sum[wave] = incl;
+    __syncthreads();
+    if (t == 0) {
+        int acc = 0;
+        for (int w = 0; w < T / 64; ++w) {
+            const int v = s_sum[w];
+            s_sum[w] = acc;
+            acc += v;
+        }
+        s_total = acc;
+        s_first[acc] = m;
+    }
+    __syncthreads();
+    const int s0 = s_sum[wave] + incl - cnt - 1;  // segment of the point before this thread's first
+    int sg = s0;
+#pragma unroll
+    for (int a = 0; a < PER; ++a) {
+        const int j = t * PER + a;
+        if (j >= m) break;
+        sg += head[a];
+        J.nseg[j] = sg;
+        if (head[a]) s_first[sg] = j;
+    }
+    __syncthreads();
+    sg = s0;
+#pragma unroll
+    for (int a = 0; a < PER; ++a) {
+        const int j = t * PER + a;
+        if (j >= m) break;
+        sg += head[a];
+        if (!head[a]) continue;
+        const int32_t b = (int32_t)(J.ometa[pos[a]] & 0x0fffffffu);
+        const int32_t c = J.bcnt[b];
+        const int32_t k = s_first[sg + 1] - j;
+        const int32_t off = j + 8 * sg;
+        J.seg[sg] = make_int4(b, c, k, off);
+        J.seg_pos[sg] = pos[a];
         const int32_t from = c + k <= kCtCap ? off : off + c + k;
         for (int e = from; e < off + k + 8; ++e) J.sseg[e] = -1;
     }
@@ -690,32 +884,28 @@ __global__ __launch_bounds__(kCtScanThreads) void k_ct_split_scan(CtJobs js) {
     }
 }
 
-// a leaf start fills its bucket (the segment's first leaf: the split bucket; a new leaf: the
-// next free bucket by rank) and a new leaf records its directory entry
+// A split leaf's bucket: the segment's first leaf keeps the split bucket, a new leaf takes the
+// next free bucket by its rank among the round's new leaves.
+__device__ __forceinline__ int32_t ct_leaf_bucket(const CtJob &J, int64_t st, int flag, const int4 &g) {
+    return flag == 1 ? g.x : J.cnt->n_buckets + J.srank[st];
+}
+
+// the leaf starting at split element e closes its bucket: count, box (from the rows), and the
+// directory (a new leaf: its entry; the split bucket: its record updated in place)
 template <int D>
-__device__ __forceinline__ void ct_fill_leaf(const CtJob &J, int64_t e, int flag) {
-    const int s = J.sseg[e];
-    const int4 g = J.seg[s];
-    const int64_t end = (int64_t)g.w + g.y + g.z;
-    int len = 1;
-    while (e + len < end && J.slead[e + len] == 0) ++len;
-    int32_t b = g.x;
+__device__ __forceinline__ void ct_leaf_close(const CtJob &J, int64_t e, int flag, int s, int32_t b, int len) {
+    if (b >= J.bcap || len > kCtCap) {
+        if (J.err) atomicAdd(J.err, 1ull);
+        return;
+    }
     if (flag == 2) {
         const int32_t r = J.srank[e];
-        b = J.cnt->n_buckets + r;
-        if (b >= J.bcap || len > kCtCap) {
-            if (J.err) atomicAdd(J.err, 1ull);
-            return;
-        }
         uint64_t bh = J.scode[2 * e], bl = J.scode[2 * e + 1];
         c_boundary(J.scode[2 * (e - 1)], J.scode[2 * (e - 1) + 1], bh, bl);
         J.edir_code[2 * r] = bh;
         J.edir_code[2 * r + 1] = bl;
         J.edir_bk[r] = b;
         J.edir_pos[r] = J.seg_pos[s];
-    } else if (len > kCtCap) {
-        if (J.err) atomicAdd(J.err, 1ull);
-        return;
     }
     double lo[D], hi[D];
 #pragma unroll
@@ -723,37 +913,75 @@ __device__ __forceinline__ void ct_fill_leaf(const CtJob &J, int64_t e, int flag
         lo[q] = __builtin_huge_val();
         hi[q] = -__builtin_huge_val();
     }
-    for (int u = 0; u < len; ++u) {
-        const int32_t row = J.srow[e + u];
-        double x[D];
-        load_global<D>(J.pts + (int64_t)row * D, x);
-        const int64_t slot = (int64_t)b * kCtCap + u;
 #pragma unroll
-        for (int q = 0; q < D; ++q) {
-            J.bpts[slot * D + q] = x[q];
-            lo[q] = x[q] < lo[q] ? x[q] : lo[q];
-            hi[q] = x[q] > hi[q] ? x[q] : hi[q];
+    for (int u = 0; u < kCtCap; ++u) {  // unrolled: the rows' loads are all in flight together
+        if (u < len) {
+            double x[D];
+            load_global<D>(J.pts + (int64_t)J.srow[e + u] * D, x);
+#pragma unroll
+            for (int q = 0; q < D; ++q) {
+                lo[q] = x[q] < lo[q] ? x[q] : lo[q];
+                hi[q] = x[q] > hi[q] ? x[q] : hi[q];
+            }
         }
-        J.bids[slot] = row + 1;
-        J.bcode[2 * slot] = J.scode[2 * (e + u)];
-        J.bcode[2 * slot + 1] = J.scode[2 * (e + u) + 1];
     }
     write_box<D>(J.bbox + (int64_t)b * 2 * D, lo, hi);
     J.bcnt[b] = len;
-    if (flag == 1) {  // the split bucket keeps its directory record: update it in place
+    if (flag == 1) {
         const int64_t dp = J.seg_pos[s];
         write_box<D>(J.obox + dp * 2 * D, lo, hi);
         J.ometa[dp] = leaf_code(b, len);
     }
 }
 
+// every split element copies its row into its leaf's bucket slot; each leaf's first element
+// also closes the leaf (ct_leaf_close).  A workgroup takes 256 consecutive elements, their
+// leaf flags and kCtCap either side staged in LDS for the walks to the leaf's ends.
 template <int D>
 __global__ __launch_bounds__(256) void k_ct_split_fill(CtJobs js) {
     const CtJob J = CT_JOB(js);  // by value: the fields stay in registers across the stores
+    __shared__ int8_t s_f[256 + 2 * kCtCap];  // flag of element c0 - kCtCap + v; -1 past the ends
     const int64_t total = ct_scratch_total(J);
-    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
-        const int flag = J.slead[e];
-        if (flag) ct_fill_leaf<D>(J, e, flag);
+    for (int64_t c0 = (int64_t)blockIdx.x * 256; c0 < total; c0 += (int64_t)gridDim.x * 256) {
+    for (int v = threadIdx.x; v < 256 + 2 * kCtCap; v += 256) {
+        const int64_t x = c0 - kCtCap + v;
+        s_f[v] = (int8_t)(x >= 0 && x < total ? J.slead[x] : -1);
+    }
+    __syncthreads();
+    const int64_t e = c0 + threadIdx.x;
+    const int s = e < total ? J.sseg[e] : -1;
+    if (s >= 0) {
+        const int ve = threadIdx.x + kCtCap;
+        int vs = ve;  // the leaf's first element (a segment's first element starts a leaf)
+        while (vs > 0 && s_f[vs] == 0) --vs;
+        int64_t st = c0 - kCtCap + vs;
+        if (s_f[vs] <= 0) {  // beyond the staged flags (a leaf longer than kCtCap: an index error)
+            st = st < 0 ? 0 : st;
+            while (st > 0 && J.slead[st] == 0) --st;
+        }
+        const int flag = J.slead[st];
+        const int4 g = J.seg[s];
+        const int32_t b = ct_leaf_bucket(J, st, flag, g);
+        const int64_t u = e - st;
+        if (b < J.bcap && u < kCtCap) {
+            const int32_t row = J.srow[e];
+            double x[D];
+            load_global<D>(J.pts + (int64_t)row * D, x);
+            const int64_t slot = (int64_t)b * kCtCap + u;
+#pragma unroll
+            for (int q = 0; q < D; ++q) J.bpts[slot * D + q] = x[q];
+            J.bids[slot] = row + 1;
+            J.bcode[2 * slot] = J.scode[2 * e];
+            J.bcode[2 * slot + 1] = J.scode[2 * e + 1];
+        }
+        if (e == st) {
+            const int64_t end = (int64_t)g.w + g.y + g.z;
+            int len = 1;
+            while (e + len < end && len <= kCtCap && s_f[ve + len] == 0) ++len;
+            ct_leaf_close<D>(J, e, flag, s, b, len);
+        }
+    }
+    __syncthreads();  // s_f reused by the next chunk
     }
 }
 
@@ -821,15 +1049,13 @@ __global__ __launch_bounds__(256) void k_ct_dmerge(CtJobs js) {
     }
 }
 
-// The hierarchy above the directory: consecutive nodes of a level grouped into maximal aligned
-// code cells of at most 8 (ct_same over the nodes' codes: a node's code is its first directory
-// entry's start), or, when that would leave more than half as many groups as nodes or more
-// levels than the walk's stack allows, runs of 8 (the depth stays logarithmic).  Level 1 (the
-// directory, the big one) is grouped over many workgroups (k_ct_lflags, k_ct_lgroup), the levels
-// above it by one workgroup a tree (k_ct_levels), which also copies the seeds and closes the
-// round's counts.
+// The hierarchy above the directory.  Levels 1 and 2 (the directory, the big one, and the one
+// above it) are grouped over many workgroups (k_ct_lflags, k_ct_lgroup): consecutive nodes into
+// maximal aligned code cells of at most 8 (ct_same over the nodes' codes: a node's code is its
+// first directory entry's start), or, when that would leave more than half as many groups as
+// nodes or more levels than the walk's stack allows, runs of 8.  Above level 3 one workgroup a
+// tree (k_ct_levels) groups runs of 8, then copies the seeds and closes the round's counts.
 constexpr int kCtLevelThreads = 1024;
-constexpr int kCtLevelA = 16384;  // level sizes whose adjacent prefix lengths k_ct_levels keeps in LDS
 constexpr int kCtMaxLevels = 10;  // the walk's stack bound (ct_walk kStack); runs of 8 reach it below 8^9 entries
 constexpr int kCtL1Per = kCtL1Tile / 256;  // level-1 entries a thread of k_ct_lflags / k_ct_lgroup
 
@@ -838,32 +1064,6 @@ __device__ __forceinline__ bool ct_fixed(int64_t n, int64_t G, int lev) {
     int need = lev + 1;
     for (int64_t m = G; m > 1; m = (m + 7) / 8) ++need;
     return G > n / 2 || need > kCtMaxLevels;
-}
-
-// the parent of nodes [first, first + len) of a level at index P (box, meta, code)
-template <int D>
-__device__ __forceinline__ void ct_parent(const CtJob &J, const uint64_t *__restrict__ lc, int64_t first, int len,
-                                          int64_t P, int64_t i) {
-    float lo[D], hi[D];
-#pragma unroll
-    for (int q = 0; q < D; ++q) {
-        lo[q] = J.nbox[first * 2 * D + q];
-        hi[q] = J.nbox[first * 2 * D + D + q];
-    }
-    for (int u = 1; u < len; ++u)
-#pragma unroll
-        for (int q = 0; q < D; ++q) {
-            lo[q] = fminf(lo[q], J.nbox[(first + u) * 2 * D + q]);
-            hi[q] = fmaxf(hi[q], J.nbox[(first + u) * 2 * D + D + q]);
-        }
-#pragma unroll
-    for (int q = 0; q < D; ++q) {
-        J.nbox[P * 2 * D + q] = lo[q];
-        J.nbox[P * 2 * D + D + q] = hi[q];
-    }
-    J.nmeta[P] = inner_code(first, len);
-    J.ucode[2 * P] = lc[2 * i];
-    J.ucode[2 * P + 1] = lc[2 * i + 1];
 }
 
 __device__ __forceinline__ int ct_block_scan(int v, int32_t *s_w, int nthreads, int &total) {
@@ -886,15 +1086,33 @@ __device__ __forceinline__ int ct_block_scan(int v, int32_t *s_w, int nthreads, 
     return before + incl - v;  // exclusive
 }
 
-// level 1's group starts, kCtL1Per consecutive entries a thread; the tile's count.  The
+// Level LEV (1: the directory, 2: the level above it) as the multi-workgroup kernels see it:
+// its nodes [base, base + n), their codes, where its tiles' counts go.
+template <int LEV>
+struct CtLevel {
+    int64_t base, n;
+    const uint64_t *code;
+    int32_t *lcount;
+};
+template <int LEV>
+__device__ __forceinline__ CtLevel<LEV> ct_level(const CtJob &J) {
+    const int64_t n1 = (int64_t)J.cnt->n_dir + J.cnt->n_new_dir;
+    if constexpr (LEV == 1) return {0, n1, J.ndir_code, J.lcount};
+    else return {n1, n1 > 1 ? (int64_t)J.cnt->n_l2 : 0, J.ucode + 2 * n1, J.lcount + J.bcap / kCtL1Tile + 1};
+}
+
+// a level's group starts, kCtL1Per consecutive nodes a thread; the tile's count.  The
 // adjacent prefix lengths of the tile and 8 entries either side go to LDS first (one coalesced
 // pass over the codes).
 constexpr int kCtHalo = kCtCap;
+template <int LEV>
 __global__ __launch_bounds__(256) void k_ct_lflags(CtJobs js) {
     const CtJob J = CT_JOB(js);  // by value: the fields stay in registers across the stores
     __shared__ int32_t s_w[4];
     __shared__ uint8_t s_a[kCtL1Tile + 2 * kCtHalo];
-    const int64_t n = (int64_t)J.cnt->n_dir + J.cnt->n_new_dir;
+    const CtLevel<LEV> V = ct_level<LEV>(J);
+    const int64_t n = V.n;
+    const uint64_t *__restrict__ code = V.code;
     const int64_t t0 = (int64_t)blockIdx.x * kCtL1Tile;
     if (n <= 1 || t0 >= n) return;  // block-uniform
     const int64_t a0 = t0 - kCtHalo;  // s_a[v] = a[a0 + v]
@@ -902,7 +1120,7 @@ __global__ __launch_bounds__(256) void k_ct_lflags(CtJobs js) {
         const int64_t u = a0 + v;
         int cp = 0;
         if (u >= 1 && u < n)
-            cp = c_cpl(J.ndir_code[2 * (u - 1)], J.ndir_code[2 * (u - 1) + 1], J.ndir_code[2 * u], J.ndir_code[2 * u + 1]);
+            cp = c_cpl(code[2 * (u - 1)], code[2 * (u - 1) + 1], code[2 * u], code[2 * u + 1]);
         s_a[v] = (uint8_t)cp;
     }
     __syncthreads();
@@ -915,18 +1133,18 @@ __global__ __launch_bounds__(256) void k_ct_lflags(CtJobs js) {
         if (i < n) {
             // the index / 8 rule counts from the run start 0: shift lo so (i - lo) keeps i's phase
             const int f = i == 0 || !ct_same_a(s_a, wlo, whi, i - a0);
-            J.lflag[i] = f;
+            J.lflag[V.base + i] = f;
             c += f;
         }
     }
     int tot;
     (void)ct_block_scan(c, s_w, 256, tot);
-    if (threadIdx.x == 0) J.lcount[blockIdx.x] = tot;
+    if (threadIdx.x == 0) V.lcount[blockIdx.x] = tot;
 }
 
 // level 2: each tile's groups, numbered after the tiles before it.  The tile's boxes and flags
 // (and the 7 entries after it, where its last groups end) are staged in LDS with coalesced loads.
-template <int D>
+template <int D, int LEV>
 __global__ __launch_bounds__(256) void k_ct_lgroup(CtJobs js) {
     const CtJob J = CT_JOB(js);  // by value: the fields stay in registers across the stores
     constexpr int kSpan = kCtL1Tile + kCtCap - 1;
@@ -934,14 +1152,15 @@ __global__ __launch_bounds__(256) void k_ct_lgroup(CtJobs js) {
     __shared__ int64_t s_sum[2];
     __shared__ uint2 s_box[kSpan * D];  // box e of the span: words [e * D, e * D + D)
     __shared__ uint8_t s_f[kSpan];
-    const int64_t n = (int64_t)J.cnt->n_dir + J.cnt->n_new_dir;
+    const CtLevel<LEV> V = ct_level<LEV>(J);
+    const int64_t n = V.n, base = V.base;
     const int64_t t0 = (int64_t)blockIdx.x * kCtL1Tile;
     if (n <= 1 || t0 >= n) return;  // block-uniform
     const int64_t tiles = (n + kCtL1Tile - 1) / kCtL1Tile;
     if (threadIdx.x < 64) {  // the groups of all tiles and of the tiles before this one
         int64_t all = 0, before = 0;
         for (int64_t b = threadIdx.x; b < tiles; b += 64) {
-            const int32_t v = J.lcount[b];
+            const int32_t v = V.lcount[b];
             all += v;
             before += b < (int64_t)blockIdx.x ? v : 0;
         }
@@ -956,13 +1175,13 @@ __global__ __launch_bounds__(256) void k_ct_lgroup(CtJobs js) {
         }
     }
     const int span = (int)(n - t0 < kSpan ? n - t0 : kSpan);
-    const uint2 *src = reinterpret_cast<const uint2 *>(J.nbox) + t0 * D;
+    const uint2 *src = reinterpret_cast<const uint2 *>(J.nbox) + (base + t0) * D;
     for (int w = threadIdx.x; w < span * D; w += 256) s_box[w] = src[w];
-    for (int e = threadIdx.x; e < span; e += 256) s_f[e] = (uint8_t)J.lflag[t0 + e];
+    for (int e = threadIdx.x; e < span; e += 256) s_f[e] = (uint8_t)J.lflag[base + t0 + e];
     __syncthreads();
     const int64_t G = s_sum[0];
-    const bool fixed = ct_fixed(n, G, 1);
-    if (blockIdx.x == 0 && threadIdx.x == 0) J.cnt->n_l2 = (int32_t)(fixed ? (n + 7) / 8 : G);
+    const bool fixed = ct_fixed(n, G, LEV);
+    if (blockIdx.x == 0 && threadIdx.x == 0) (LEV == 1 ? J.cnt->n_l2 : J.cnt->n_l3) = (int32_t)(fixed ? (n + 7) / 8 : G);
     const int e0 = threadIdx.x * kCtL1Per;  // this thread's entries [e0, e0 + kCtL1Per) of the tile
     int f[kCtL1Per], c = 0;
 #pragma unroll
@@ -1001,72 +1220,63 @@ __global__ __launch_bounds__(256) void k_ct_lgroup(CtJobs js) {
                 hi[q] = fmaxf(hi[q], bu[D + q]);
             }
         }
-        const int64_t P = n + g;
+        const int64_t P = base + n + g;
 #pragma unroll
         for (int q = 0; q < D; ++q) {
             J.nbox[P * 2 * D + q] = lo[q];
             J.nbox[P * 2 * D + D + q] = hi[q];
         }
-        J.nmeta[P] = inner_code(i, len);
-        J.ucode[2 * P] = J.ndir_code[2 * i];
-        J.ucode[2 * P + 1] = J.ndir_code[2 * i + 1];
+        J.nmeta[P] = inner_code(base + i, len);
+        J.ucode[2 * P] = V.code[2 * i];
+        J.ucode[2 * P + 1] = V.code[2 * i + 1];
         ++g;
     }
 }
 
-// one workgroup a tree: the levels above level 2 (a thread a run of consecutive nodes), then
-// the counts, the seed rows, the indexed count and the spread
+// one workgroup a tree: the levels above level 3, then the counts, the seed rows, the indexed
+// count and the spread
 template <int D>
 __global__ __launch_bounds__(kCtLevelThreads) void k_ct_levels(CtJobs js) {
     const CtJob J = CT_JOB(js);  // by value: the fields stay in registers across the stores
-    __shared__ int32_t s_w[kCtLevelThreads / 64];
-    __shared__ uint8_t s_a[kCtLevelA];
     const int t = threadIdx.x;
     const int64_t n1 = (int64_t)J.cnt->n_dir + J.cnt->n_new_dir;
-    int64_t ls = n1 > 1 ? n1 : 0, n = n1 > 1 ? J.cnt->n_l2 : n1;
-    int lev = 2;
+    // levels 1 and 2 were grouped by k_ct_lflags / k_ct_lgroup into levels 2 and 3
+    int64_t ls = 0, n = n1;
+    for (int k = 0; k < 2 && n > 1; ++k) {
+        ls += n;
+        n = k == 0 ? J.cnt->n_l2 : J.cnt->n_l3;
+    }
+    // above level 3: runs of 8 (boxes high in the tree prune little; what counts is how few
+    // levels a walk descends)
     while (n > 1) {
-        const uint64_t *lc = J.ucode + 2 * ls;  // node i's code at lc[2 i]
-        const int64_t per = (n + kCtLevelThreads - 1) / kCtLevelThreads;
-        const int64_t i0 = t * per, i1 = i0 + per < n ? i0 + per : n;
-        const bool in_lds = n <= kCtLevelA;  // block-uniform
-        if (in_lds) {
-            for (int64_t u = t; u < n; u += kCtLevelThreads)
-                s_a[u] = (uint8_t)(u == 0 ? 0 : c_cpl(lc[2 * (u - 1)], lc[2 * (u - 1) + 1], lc[2 * u], lc[2 * u + 1]));
-            __syncthreads();
-        }
-        int c = 0;
-        for (int64_t i = i0; i < i1; ++i) {
-            const int f = i == 0 || !(in_lds ? ct_same_a(s_a, 0, n, i) : ct_same(lc, nullptr, 0, n, i));
-            J.lflag[ls + i] = f;
-            c += f;
-        }
-        int G;
-        const int ex = ct_block_scan(c, s_w, kCtLevelThreads, G);
-        const bool fixed = ct_fixed(n, G, lev);
-        __threadfence_block();
-        __syncthreads();
-        const int64_t nG = fixed ? (n + 7) / 8 : G;
-        int64_t g = ex;
-        for (int64_t i = i0; i < i1; ++i) {
-            int len = 0;
-            if (fixed) {
-                if ((i & 7) == 0) len = n - i < 8 ? (int)(n - i) : 8;
-                g = i / 8;
-            } else if (J.lflag[ls + i]) {
-                len = 1;
-                while (i + len < n && len < kCtCap && !J.lflag[ls + i + len]) ++len;
+        const int64_t nG = (n + 7) / 8;
+        for (int64_t g = t; g < nG; g += kCtLevelThreads) {
+            const int64_t first = ls + 8 * g;
+            const int len = n - 8 * g < 8 ? (int)(n - 8 * g) : 8;
+            float lo[D], hi[D];
+#pragma unroll
+            for (int q = 0; q < D; ++q) {
+                lo[q] = J.nbox[first * 2 * D + q];
+                hi[q] = J.nbox[first * 2 * D + D + q];
             }
-            if (len) {
-                ct_parent<D>(J, lc, ls + i, len, ls + n + g, i);
-                ++g;
+            for (int u = 1; u < len; ++u)
+#pragma unroll
+                for (int q = 0; q < D; ++q) {
+                    lo[q] = fminf(lo[q], J.nbox[(first + u) * 2 * D + q]);
+                    hi[q] = fmaxf(hi[q], J.nbox[(first + u) * 2 * D + D + q]);
+                }
+            const int64_t P = ls + n + g;
+#pragma unroll
+            for (int q = 0; q < D; ++q) {
+                J.nbox[P * 2 * D + q] = lo[q];
+                J.nbox[P * 2 * D + D + q] = hi[q];
             }
+            J.nmeta[P] = inner_code(first, len);
         }
         __threadfence_block();
         __syncthreads();
         ls += n;
         n = nG;
-        ++lev;
     }
     for (int it = t; it < kCtHull * D; it += kCtLevelThreads) {
         const int h = it / D, k = it - h * D;
@@ -1583,6 +1793,7 @@ CtPlan make_ct_plan(int32_t d, const double *lo, const double *hi, int32_t spati
         b[j] = kstar > 0 ? bits_of(j, std::ldexp(emax, -kstar), kstar) : 0;
         bmax = std::max(bmax, b[j]);
         P.lo[j] = lo[j];
+        P.nb[j] = (int8_t)b[j];
         P.qmax[j] = b[j] > 0 ? (uint32_t)((1ull << b[j]) - 1) : 0u;
         P.scale[j] = b[j] > 0 ? std::ldexp(1.0, b[j]) / ext[j] : 0.0;
     }
@@ -1595,6 +1806,7 @@ CtPlan make_ct_plan(int32_t d, const double *lo, const double *hi, int32_t spati
                 ++n;
             }
     P.n = n;
+    P.bmax = bmax;
     // seed slots: every dim's minimum and maximum, then directions over the first `spatial`
     // dims spread evenly (a Fibonacci lattice on the sphere; the circle for two dims)
     int h = 0;
@@ -1665,7 +1877,7 @@ void CellTree::reserve(int64_t c, int32_t d) {
     }
     al((void **)&ucode, sizeof(uint64_t) * 2 * nodes, "ct node cell codes");
     al((void **)&lflag, sizeof(int32_t) * nodes, "ct level scratch");
-    al((void **)&lcount, sizeof(int32_t) * (bcap / kCtL1Tile + 1), "ct level scratch");
+    al((void **)&lcount, sizeof(int32_t) * (bcap / kCtL1Tile + bcap / (2 * kCtL1Tile) + 2), "ct level scratch");
     for (int k = 0; k < 2; ++k) {
         al((void **)&dir_code[k], sizeof(uint64_t) * 2 * bcap, "ct directory");
     }
@@ -1818,26 +2030,33 @@ void launch_ct_jobs(const CtJob *d_jobs, const CtJob *h_jobs, int32_t n, int32_t
     const unsigned yn = (unsigned)n;
     if (mb > 0) {
         const unsigned b256 = (unsigned)((mb + 255) / 256);
-        hipLaunchKernelGGL(by_d(k_ct_ncodes<3>, k_ct_ncodes<7>, k_ct_ncodes<15>), dim3(b256, yn), dim3(64 * kCtWaves), 0,
-                           stream, js);
-        hip_check(hipGetLastError(), "k_ct_ncodes");
-        if (mb <= kCtLdsSort) {
-            hipLaunchKernelGGL(k_ct_lsort, dim3(1, yn), dim3(kCtLdsSortThreads), 0, stream, js);
+        if (mb <= kCtLdsSort && d <= 7) {  // one workgroup a tree: codes, sort, positions, segments
+            hipLaunchKernelGGL(d == 3 ? k_ct_front<3> : k_ct_front<7>, dim3(1, yn), dim3(kCtFrontThreads), 0, stream,
+                               js);
+            hip_check(hipGetLastError(), "k_ct_front");
         } else {
-            const unsigned chunks = (unsigned)((mb + kCtChunk - 1) / kCtChunk);
-            hipLaunchKernelGGL(k_ct_csort, dim3((chunks + kCtChunkWaves - 1) / kCtChunkWaves, yn),
-                               dim3(64 * kCtChunkWaves), 0, stream, js);
-            hipLaunchKernelGGL(k_ct_crank, dim3(b256, yn), dim3(256), 0, stream, js);
+            hipLaunchKernelGGL(by_d(k_ct_ncodes<3>, k_ct_ncodes<7>, k_ct_ncodes<15>), dim3(b256, yn),
+                               dim3(64 * kCtWaves), 0, stream, js);
+            hip_check(hipGetLastError(), "k_ct_ncodes");
+            if (mb <= kCtLdsSort) {
+                hipLaunchKernelGGL(k_ct_lsort, dim3(1, yn), dim3(kCtLdsSortThreads), 0, stream, js);
+            } else {
+                const unsigned chunks = (unsigned)((mb + kCtChunk - 1) / kCtChunk);
+                hipLaunchKernelGGL(k_ct_csort, dim3((chunks + kCtChunkWaves - 1) / kCtChunkWaves, yn),
+                                   dim3(64 * kCtChunkWaves), 0, stream, js);
+                hipLaunchKernelGGL(k_ct_crank, dim3(b256, yn), dim3(256), 0, stream, js);
+            }
+            hipLaunchKernelGGL(k_ct_locate, dim3(b256, yn), dim3(256), 0, stream, js);
+            hipLaunchKernelGGL(k_ct_segments, dim3(1, yn), dim3(kCtSegThreads), 0, stream, js);
         }
-        hipLaunchKernelGGL(k_ct_locate, dim3(b256, yn), dim3(256), 0, stream, js);
-        hipLaunchKernelGGL(k_ct_segments, dim3(1, yn), dim3(kCtSegThreads), 0, stream, js);
         hipLaunchKernelGGL(by_d(k_ct_apply<3>, k_ct_apply<7>, k_ct_apply<15>), dim3(b256, yn), dim3(256), 0, stream, js);
         hip_check(hipGetLastError(), "k_ct_apply");
-        // the split elements (at most 9 a new point) strided over the new points' workgroups
+        // the split elements: at most 9 a new point, a thread each
+        const unsigned bsplit = (unsigned)((mb * (kCtCap + 1) + 255) / 256);
         hipLaunchKernelGGL(k_ct_split_flags, dim3(b256, yn), dim3(256), 0, stream, js);
         hipLaunchKernelGGL(k_ct_split_scan, dim3(1, yn), dim3(kCtScanThreads), 0, stream, js);
-        hipLaunchKernelGGL(by_d(k_ct_split_fill<3>, k_ct_split_fill<7>, k_ct_split_fill<15>), dim3(b256, yn), dim3(256),
-                           0, stream, js);
+        hipLaunchKernelGGL(by_d(k_ct_split_fill<3>, k_ct_split_fill<7>, k_ct_split_fill<15>), dim3(bsplit, yn),
+                           dim3(256), 0, stream, js);
         hip_check(hipGetLastError(), "k_ct_split_fill");
     }
     // the directory (at most the indexed points' count of entries, ~1/5 of them in practice)
@@ -1845,9 +2064,14 @@ void launch_ct_jobs(const CtJob *d_jobs, const CtJob *h_jobs, int32_t n, int32_t
                        dim3((unsigned)std::max<int64_t>(1, (max_n + 2047) / 2048), yn), dim3(256), 0, stream, js);
     hip_check(hipGetLastError(), "k_ct_dmerge");
     const unsigned tiles = (unsigned)std::max<int64_t>(1, (max_n + kCtL1Tile - 1) / kCtL1Tile);
-    hipLaunchKernelGGL(k_ct_lflags, dim3(tiles, yn), dim3(256), 0, stream, js);
-    hipLaunchKernelGGL(by_d(k_ct_lgroup<3>, k_ct_lgroup<7>, k_ct_lgroup<15>), dim3(tiles, yn), dim3(256), 0, stream,
-                       js);
+    // levels 1 and 2 over many workgroups (level 2 has at most half level 1's nodes)
+    hipLaunchKernelGGL(k_ct_lflags<1>, dim3(tiles, yn), dim3(256), 0, stream, js);
+    hipLaunchKernelGGL(by_d(k_ct_lgroup<3, 1>, k_ct_lgroup<7, 1>, k_ct_lgroup<15, 1>), dim3(tiles, yn), dim3(256), 0,
+                       stream, js);
+    const unsigned tiles2 = (tiles + 1) / 2;
+    hipLaunchKernelGGL(k_ct_lflags<2>, dim3(tiles2, yn), dim3(256), 0, stream, js);
+    hipLaunchKernelGGL(by_d(k_ct_lgroup<3, 2>, k_ct_lgroup<7, 2>, k_ct_lgroup<15, 2>), dim3(tiles2, yn), dim3(256), 0,
+                       stream, js);
     hipLaunchKernelGGL(by_d(k_ct_levels<3>, k_ct_levels<7>, k_ct_levels<15>), dim3(1, yn), dim3(kCtLevelThreads), 0,
                        stream, js);
     hip_check(hipGetLastError(), "k_ct_levels");

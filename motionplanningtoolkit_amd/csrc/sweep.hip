@@ -154,6 +154,145 @@ __device__ __forceinline__ void sweep_core(const EnvDev &env, const AgentDev &ag
     }
 }
 
+// One edge, every agent cluster (at most 64: lane c holds cluster c): the wave walks the env
+// tree once against the union of the clusters' swept boxes and fans out to the clusters only at
+// the env triangles that meet it -- the clusters whose swept box meets the triangle, each one's
+// triangles rotated then (lanes = its triangles) and tested over the poses as in sweep_core.
+// Same verdicts as sweep_core over every cluster: a contact is a contact whichever order finds it.
+template <class Gen>
+__device__ __forceinline__ void sweep_edge_core(const EnvDev &env, const AgentDev &ag, const double *Rw,
+                                                const double *tf, const double *tl, Gen gen, uint8_t *flag, int lane,
+                                                int32_t *stk, SweepCounters &cnt) {
+    ++cnt.waves;
+    double R[9], T0[3], TN[3];
+    relative_transform(env.tf, env.tf + 9, Rw, tf, R, T0);
+    env_rel_t(env, tl, TN);
+#pragma unroll
+    for (int i = 0; i < 9; ++i) R[i] = uniform_d(R[i]);
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        T0[i] = uniform_d(T0[i]);
+        TN[i] = uniform_d(TN[i]);
+    }
+    const int ncl = ag.n_clusters;
+    float clo[3] = {__builtin_huge_valf(), __builtin_huge_valf(), __builtin_huge_valf()};
+    float chi[3] = {-__builtin_huge_valf(), -__builtin_huge_valf(), -__builtin_huge_valf()};
+    if (lane < ncl) {  // lane c: cluster c's box swept along the edge
+        const Cluster c = ag.clusters[lane];
+        float alo[3], ahi[3], blo[3], bhi[3];
+        local_box(c.c, c.e, R, T0, alo, ahi);
+        local_box(c.c, c.e, R, TN, blo, bhi);
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            clo[k] = fminf(alo[k], blo[k]);
+            chi[k] = fmaxf(ahi[k], bhi[k]);
+        }
+    }
+    float ulo[3], uhi[3];  // their union (every lane)
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        ulo[k] = clo[k];
+        uhi[k] = chi[k];
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) {
+            ulo[k] = fminf(ulo[k], __shfl_xor(ulo[k], off));
+            uhi[k] = fmaxf(uhi[k], __shfl_xor(uhi[k], off));
+        }
+    }
+    int sp = 0;
+    int lev = env.n_levels - 1;
+    int32_t first = env.lev_off[lev];
+    int32_t count = env.lev_off[lev + 1] - first;
+    for (;;) {
+        bool keep = false;
+        int32_t cf = 0, cc = 0;
+        if (lane < count) {
+            const Item it = env.items[first + lane];
+            keep = box_overlap(ulo, uhi, it.lo, it.hi);
+            cf = it.first;
+            cc = it.count;
+        }
+        cnt.items += (uint32_t)count;
+        uint64_t m = __ballot(keep);
+        if (lev == 0) {
+            while (m) {  // env triangles meeting the union: fan out to the clusters meeting them
+                const int j = __ffsll((unsigned long long)m) - 1;
+                m &= m - 1;
+                const int32_t t = first + j;
+                const Item ti = env.items[t];  // level 0: item index = triangle index
+                uint64_t cm = __ballot(lane < ncl && box_overlap(clo, chi, ti.lo, ti.hi));
+                while (cm) {
+                    const int ci = __ffsll((unsigned long long)cm) - 1;
+                    cm &= cm - 1;
+                    if (load_flag(flag)) return;
+                    const Cluster c = ag.clusters[ci];
+                    const bool act = lane < c.count;
+                    v3 RQ[3] = {mk(0, 0, 0), mk(0, 0, 0), mk(0, 0, 0)};
+                    bool near = false;
+                    if (act) {  // the lane's triangle rotated once (R Q, xform's order before the + T)
+                        const double *tr = ag.tris + (int64_t)(c.first + lane) * 9;
+#pragma unroll
+                        for (int v = 0; v < 3; ++v) {
+                            const double x = tr[3 * v], y = tr[3 * v + 1], z = tr[3 * v + 2];
+                            RQ[v] = mk(R[0] * x + R[1] * y + R[2] * z, R[3] * x + R[4] * y + R[5] * z,
+                                       R[6] * x + R[7] * y + R[8] * z);
+                        }
+                        float tlo[3], thi[3];  // its box swept along the edge
+#pragma unroll
+                        for (int k = 0; k < 3; ++k) {
+                            const double a0 = (&RQ[0].x)[k], a1 = (&RQ[1].x)[k], a2 = (&RQ[2].x)[k];
+                            const double mn = dmin(a0, dmin(a1, a2)), mx = dmax(a0, dmax(a1, a2));
+                            tlo[k] = widen_lo(dmin(mn + T0[k], mn + TN[k]));
+                            thi[k] = widen_hi(dmax(mx + T0[k], mx + TN[k]));
+                        }
+                        near = box_overlap(tlo, thi, ti.lo, ti.hi);
+                    }
+                    if (!__ballot(near)) continue;
+                    const EnvTri &E = env.tris[t];
+                    bool hit = false;
+                    if (near) {
+                        gen([&](const double *tw) {
+                            double Tp[3];
+                            env_rel_t(env, tw, Tp);
+                            const v3 Q1 = mk(RQ[0].x + Tp[0], RQ[0].y + Tp[1], RQ[0].z + Tp[2]);
+                            const v3 Q2 = mk(RQ[1].x + Tp[0], RQ[1].y + Tp[1], RQ[1].z + Tp[2]);
+                            const v3 Q3 = mk(RQ[2].x + Tp[0], RQ[2].y + Tp[1], RQ[2].z + Tp[2]);
+                            ++cnt.pair_poses;
+                            if (!tri_gate(E.lo, E.hi, Q1, Q2, Q3)) return false;
+                            ++cnt.sat;
+                            hit = tri_intersect(E, Q1, Q2, Q3);
+                            return hit;
+                        });
+                    }
+                    if (__ballot(hit)) {
+                        if (lane == 0) __hip_atomic_store(flag, (uint8_t)1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        return;
+                    }
+                }
+            }
+        } else if (m) {
+            const int j = __ffsll((unsigned long long)m) - 1;
+            const uint64_t rest = m & (m - 1);
+            if (keep && lane != j) {
+                const int pos = sp + (int)__popcll(rest & ((1ull << lane) - 1));
+                stk[pos] = ((lev - 1) << 27) | cf;
+                stk[kSweepStack + pos] = cc;
+            }
+            sp += (int)__popcll(rest);
+            first = __builtin_amdgcn_readfirstlane(__shfl(cf, j));
+            count = __builtin_amdgcn_readfirstlane(__shfl(cc, j));
+            lev -= 1;
+            continue;
+        }
+        if (sp == 0) return;
+        --sp;
+        const int32_t code = __builtin_amdgcn_readfirstlane(stk[sp]);
+        count = __builtin_amdgcn_readfirstlane(stk[kSweepStack + sp]);
+        lev = code >> 27;
+        first = code & ((1 << 27) - 1);
+    }
+}
+
 // edges given as pose ranges of a pose array (prm_connect.hip)
 __device__ __forceinline__ void sweep_wave(const EnvDev &env, const AgentDev &ag, const double *__restrict__ poses,
                                            const int64_t *__restrict__ poff, int64_t e, int32_t cl, uint8_t *verdict,
@@ -169,6 +308,35 @@ __device__ __forceinline__ void sweep_wave(const EnvDev &env, const AgentDev &ag
                verdict + e, lane, stk, cnt);
 }
 
+// one wave an edge (agents of at most 64 clusters)
+__global__ __launch_bounds__(kSweepWaves * 64) void k_sweep_edge(EnvDev env, const AgentDev *__restrict__ link,
+                                                                 const double *__restrict__ poses,
+                                                                 const int64_t *__restrict__ poff, int64_t E,
+                                                                 uint8_t *verdict, unsigned long long *stats) {
+    __shared__ int32_t s_stk[kSweepWaves][2 * kSweepStack];
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    const int64_t e = (int64_t)blockIdx.x * kSweepWaves + wave;
+    SweepCounters cnt;
+    if (e < E && !load_flag(verdict + e)) {
+        const int64_t p0 = poff[e], p1 = poff[e + 1];
+        if (p1 > p0)
+            sweep_edge_core(env, link[0], poses + p0 * 12, poses + p0 * 12 + 9, poses + (p1 - 1) * 12 + 9,
+                            [&](auto &&f) {
+                                for (int64_t p = p0; p < p1; ++p)
+                                    if (f(poses + p * 12 + 9)) return;
+                            },
+                            verdict + e, lane, s_stk[wave], cnt);
+    }
+    if (stats && lane == 0 && cnt.waves) {
+        atomicAdd(stats + 0, (unsigned long long)cnt.waves);
+        atomicAdd(stats + 1, (unsigned long long)cnt.items);
+        atomicAdd(stats + 2, (unsigned long long)cnt.pair_poses);
+        atomicAdd(stats + 3, (unsigned long long)cnt.sat);
+    }
+}
+
+// one wave an (edge, cluster) (agents of more than 64 clusters)
 __global__ __launch_bounds__(kSweepWaves * 64) void k_sweep(EnvDev env, const AgentDev *__restrict__ link,
                                                             const double *__restrict__ poses,
                                                             const int64_t *__restrict__ poff, int64_t E,
@@ -260,6 +428,14 @@ void launch_collide_sweep(const EnvDev &env, const AgentDev *d_link, int32_t n_c
                           hipStream_t stream) {
     if (E <= 0 || env.n_tris <= 0) return;
     if (env.n_tris >= (1 << 27)) throw Error{5, "env too large for the sweep path"};
+    if (n_clusters <= 64) {
+        const int64_t blocks = (E + kSweepWaves - 1) / kSweepWaves;
+        if (blocks > 0x7fffffff) throw Error{5, "sweep batch too large"};
+        hipLaunchKernelGGL(k_sweep_edge, dim3((unsigned)blocks), dim3(kSweepWaves * 64), 0, stream, env, d_link, poses,
+                           poff, E, verdict, stats);
+        hip_check(hipGetLastError(), "k_sweep_edge launch");
+        return;
+    }
     const int64_t waves = E * n_clusters;
     const int64_t blocks = (waves + kSweepWaves - 1) / kSweepWaves;
     if (blocks > 0x7fffffff) throw Error{5, "sweep batch too large"};
