@@ -181,8 +181,8 @@ __device__ __forceinline__ uint32_t walk_tree(const EnvDev &env, const Item *__r
 // host, the query box is here with a margin of 0.02 quanta beyond the float rounding of its
 // grid coordinate (<= 0.01 quanta: two roundings of ~0.004 and the float scale's 0.002), so
 // every pair the float walk keeps is kept (a superset: k_cands tests the exact float boxes
-// again).  The walk is LDS-bandwidth bound: per-workgroup phase times (MPT_PHASE_DBG=1)
-// showed the cull + staging ~4 us and the walk ~16 us of a ~20-us lifetime; with these boxes
+// again).  The walk is LDS-bandwidth bound: per-workgroup phase times (a round-2 timer since
+// removed) showed the cull + staging ~4 us and the walk ~16 us of a ~20-us lifetime; with these boxes
 // the walk takes ~11 us (config 2's k_pairs 31 -> 25 us, the room's 115 -> 90 us).
 struct QBox {
     uint32_t lxy, hxy, lz, hz;  // query: lo.x | lo.y << 16, hi.x | hi.y << 16, lo.z, hi.z

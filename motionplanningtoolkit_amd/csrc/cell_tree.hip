@@ -2092,6 +2092,8 @@ static void launch_ct_nn1_w(const CellTreeDev &T, const double *q, int64_t nq, i
 }
 
 // nodes a walk step: eight (one query a wave) for d <= 7, four for d = 15 (its registers)
+// (round 4, config 5: four nodes a step with two queries a wave took 3.42 vs 2.62 ms at 256
+// seeds, 0.52 vs 0.42 ms at 32 -- more steps a query, 19.8 vs 13.4, and a wave waits for both)
 static int ct_width(int32_t d) { return d <= 7 ? 8 : 4; }
 
 void launch_ct_nn1(const CellTreeDev &T, const double *q, int64_t nq, int32_t *ids, double *d2, hipStream_t stream) {

@@ -269,7 +269,7 @@ extern "C" mpt_status mpt_prm_connect(const mpt_env *env, const mpt_agent *agent
             hipLaunchKernelGGL(k_edge_poses, dim3((unsigned)((E + 255) / 256)), dim3(256), 0, stream, d_keys, d_rot, d_src,
                                d_nbr, E, cc_dt, d_poff, d_poses, d_pe);
         hip_check(hipEventRecord(ev[2], stream), "event");
-        // collision verdicts (sweep path; MPT_PRM_COLLIDE=split|fused selects the per-pose paths)
+        // collision verdicts (the sweep path; mpt_set_collide_mode FUSED: the per-pose fused walk)
         uint8_t *d_v = S.verdict.get(E);
         if (E > 0) {
             hip_check(hipMemsetAsync(d_v, 0, (size_t)E, stream), "verdict memset");

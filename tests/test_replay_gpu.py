@@ -75,3 +75,22 @@ def test_batched_inst_entry_point(mpt_gpu):
     st, par = e.read_tree(n)
     s0, p0 = r["tree0"]
     assert np.array_equal(bits(st), bits(s0)) and np.array_equal(par, p0)
+
+
+def test_rrt_trace_opt_in(mpt_gpu):
+    """MPT_RRT_TRACE: the host RRT prints the reference's per-iteration
+    `RRT iter 2.1` line (planners/rrt.hpp:48) only when it is set."""
+    import subprocess
+    import sys
+
+    code = ("import motionplanningtoolkit_amd as m; m.init(0); "
+            f"m.rrt_inst({inst('omnidirectional.inst')!r}, 20)")
+    for on in (False, True):
+        env = dict(os.environ)
+        env.pop("MPT_RRT_TRACE", None)
+        if on:
+            env["MPT_RRT_TRACE"] = "1"
+        out = subprocess.run([sys.executable, "-c", code], cwd=REPO, env=env, capture_output=True, text=True,
+                             timeout=120)
+        assert out.returncode == 0, out.stderr[-2000:]
+        assert ("RRT iter 2.1" in out.stderr) == on
