@@ -49,7 +49,7 @@ struct CtCounts {
     int32_t root;        // the hierarchy's root node
     int32_t n_l2;        // this round's level-2 / level-3 node counts (k_ct_lgroup)
     int32_t n_l3;
-    int32_t pad;
+    int32_t n_scratch;   // this round's split elements (the split segments' old + new points)
     int64_t nidx;        // points indexed (rows [0, nidx) of the node array)
 };
 
@@ -107,9 +107,10 @@ struct CtJob {
     int32_t *crow;
     int32_t *npos;             // [kCtSeg] directory position of sorted new point j
     int32_t *nseg;             // [kCtSeg] its segment
-    int4 *seg;                 // [kCtSeg] (bucket, old count, new count, scratch offset)
+    int4 *seg;                 // [kCtSeg] (bucket, old count, new count, split scratch offset or -1)
     int32_t *seg_pos;          // [kCtSeg] the segment's directory position
-    // split scratch [kCtScratch]: merged (code, row) of each split segment, gaps marked -1
+    int32_t *seg_first;        // [kCtSeg] the segment's first sorted new point
+    // split scratch [kCtScratch]: merged (code, row) of each split segment, packed
     uint64_t *scode;           // [..][2]
     int32_t *srow;
     int32_t *sseg;
@@ -160,7 +161,8 @@ private:
     int32_t *lflag = nullptr, *lcount = nullptr;
     uint64_t *dir_code[2] = {nullptr, nullptr};
     uint64_t *ncode = nullptr, *ccode = nullptr, *scode = nullptr, *edir_code = nullptr;
-    int32_t *nrow = nullptr, *crow = nullptr, *npos = nullptr, *nseg = nullptr, *seg_pos = nullptr, *srow = nullptr,
+    int32_t *nrow = nullptr, *crow = nullptr, *npos = nullptr, *nseg = nullptr, *seg_pos = nullptr, *seg_first = nullptr,
+            *srow = nullptr,
             *sseg = nullptr, *slead = nullptr, *srank = nullptr, *edir_bk = nullptr, *edir_pos = nullptr;
     int4 *seg = nullptr;
     unsigned long long *hull_keys = nullptr, *ibox = nullptr;

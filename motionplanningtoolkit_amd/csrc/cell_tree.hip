@@ -242,23 +242,12 @@ constexpr int kCtChunk = 512;
 constexpr int kCtChunks = kCtSeg / kCtChunk;
 constexpr int kCtChunkWaves = 4;
 
-__global__ __launch_bounds__(64 * kCtChunkWaves) void k_ct_csort(CtJobs js) {
-    const CtJob J = CT_JOB(js);  // by value: the fields stay in registers across the stores
-    const int64_t m = ct_new_count(J);
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
-    const int c0 = ((int)blockIdx.x * kCtChunkWaves + wave) * kCtChunk;
-    if (c0 >= m) return;
-    constexpr int E = kCtChunk / 64;
-    uint64_t kh[E], kl[E];
-    int32_t kr[E];
-#pragma unroll
-    for (int a = 0; a < E; ++a) {
-        const int i = c0 + lane * E + a;
-        const bool live = i < m;
-        kh[a] = live ? J.ncode[2 * i] : ~0ull;  // padding sorts last (codes use 126 bits)
-        kl[a] = live ? J.ncode[2 * i + 1] : ~0ull;
-        kr[a] = live ? J.nrow[i] : 0x7fffffff;
-    }
+// a wave's 512 (code, row) pairs, 8 a lane (element lane * 8 + a), sorted ascending: bitonic,
+// partners 8+ apart by lane shuffles, closer ones in registers
+constexpr int kCtChunkE = kCtChunk / 64;
+__device__ __forceinline__ void ct_wave_sort512(uint64_t (&kh)[kCtChunkE], uint64_t (&kl)[kCtChunkE],
+                                                int32_t (&kr)[kCtChunkE], int lane) {
+    constexpr int E = kCtChunkE;
 #pragma unroll 1
     for (int k = 2; k <= kCtChunk; k <<= 1) {
 #pragma unroll 1
@@ -295,6 +284,26 @@ __global__ __launch_bounds__(64 * kCtChunkWaves) void k_ct_csort(CtJobs js) {
             }
         }
     }
+}
+
+__global__ __launch_bounds__(64 * kCtChunkWaves) void k_ct_csort(CtJobs js) {
+    const CtJob J = CT_JOB(js);  // by value: the fields stay in registers across the stores
+    const int64_t m = ct_new_count(J);
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+    const int c0 = ((int)blockIdx.x * kCtChunkWaves + wave) * kCtChunk;
+    if (c0 >= m) return;
+    constexpr int E = kCtChunkE;
+    uint64_t kh[E], kl[E];
+    int32_t kr[E];
+#pragma unroll
+    for (int a = 0; a < E; ++a) {
+        const int i = c0 + lane * E + a;
+        const bool live = i < m;
+        kh[a] = live ? J.ncode[2 * i] : ~0ull;  // padding sorts last (codes use 126 bits)
+        kl[a] = live ? J.ncode[2 * i + 1] : ~0ull;
+        kr[a] = live ? J.nrow[i] : 0x7fffffff;
+    }
+    ct_wave_sort512(kh, kl, kr, lane);
 #pragma unroll
     for (int a = 0; a < E; ++a) {
         const int i = c0 + lane * E + a;
@@ -355,11 +364,14 @@ __global__ __launch_bounds__(256) void k_ct_crank(CtJobs js) {
 }
 
 // Rounds of at most kCtLdsSort new points (the usual case: one round's K): one workgroup a tree
-// sorts them by (code, row) in LDS with a bitonic network (80 KiB: gfx950's 160 KiB LDS takes
-// it), instead of the chunk sort and the cross-chunk ranks.
+// sorts them by (code, row): each wave its 512 in registers (ct_wave_sort512), then the runs
+// merged pairwise in LDS (each element's place = its index in its run + its rank in the partner
+// run, found by binary search: stable, the left run's ties first) -- a fraction of a bitonic
+// network's LDS traffic.  80 KiB of LDS: gfx950's 160 KiB takes it.
 constexpr int kCtLdsSort = 4096;
-constexpr int kCtLdsSortThreads = 1024;
+constexpr int kCtLdsSortThreads = kCtLdsSort / kCtChunkE;  // 512: 8 waves of 512 pairs
 __global__ __launch_bounds__(kCtLdsSortThreads) void k_ct_lsort(CtJobs js) {
+    constexpr int E = kCtChunkE;
     const CtJob J = CT_JOB(js);  // by value: the fields stay in registers across the stores
     __shared__ uint64_t s_h[kCtLdsSort], s_l[kCtLdsSort];
     __shared__ int32_t s_r[kCtLdsSort];
@@ -367,39 +379,67 @@ __global__ __launch_bounds__(kCtLdsSortThreads) void k_ct_lsort(CtJobs js) {
     // k_ct_ncodes and must not write past the LDS arrays
     const int m = (int)(ct_new_count(J) < kCtLdsSort ? ct_new_count(J) : kCtLdsSort);
     if (m <= 1) return;
-    int P = 2;
-    while (P < m) P <<= 1;
-    for (int i = threadIdx.x; i < P; i += kCtLdsSortThreads) {
-        const bool live = i < m;
-        s_h[i] = live ? J.ncode[2 * i] : ~0ull;  // padding sorts last (codes use 126 bits)
-        s_l[i] = live ? J.ncode[2 * i + 1] : ~0ull;
-        s_r[i] = live ? J.nrow[i] : 0x7fffffff;
+    const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+    const int runs = (m + kCtChunk - 1) / kCtChunk;  // waves with points (block-uniform)
+    uint64_t kh[E], kl[E];
+    int32_t kr[E];
+    if (wave < runs) {
+#pragma unroll
+        for (int a = 0; a < E; ++a) {
+            const int i = wave * kCtChunk + lane * E + a;
+            const bool live = i < m;
+            kh[a] = live ? J.ncode[2 * i] : ~0ull;  // padding sorts last (codes use 126 bits)
+            kl[a] = live ? J.ncode[2 * i + 1] : ~0ull;
+            kr[a] = live ? J.nrow[i] : 0x7fffffff;
+        }
+        ct_wave_sort512(kh, kl, kr, lane);
     }
-    __syncthreads();
-    for (int k = 2; k <= P; k <<= 1) {
-        for (int j = k >> 1; j > 0; j >>= 1) {
-            const int lj = __ffs(j) - 1;  // j = 2^lj
-            for (int p = threadIdx.x; p < P / 2; p += kCtLdsSortThreads) {
-                const int i = ((p >> lj) << (lj + 1)) | (p & (j - 1)), q = i + j;
-                const uint64_t ah = s_h[i], al = s_l[i], bh = s_h[q], bl = s_l[q];
-                const int32_t ar = s_r[i], br = s_r[q];
-                const bool up = (i & k) == 0;
-                if (cr_lt(bh, bl, br, ah, al, ar) == up) {
-                    s_h[i] = bh;
-                    s_l[i] = bl;
-                    s_r[i] = br;
-                    s_h[q] = ah;
-                    s_l[q] = al;
-                    s_r[q] = ar;
-                }
+    const int P = runs * kCtChunk;  // sorted runs of 512 fill [0, P)
+    int R = kCtChunk;
+    // element e = wave * 512 + lane * 8 + a stays with its thread; only its place changes
+    int place[E];
+#pragma unroll
+    for (int a = 0; a < E; ++a) place[a] = wave * kCtChunk + lane * E + a;
+    for (; R < P; R <<= 1) {
+        __syncthreads();
+        if (wave < runs) {
+#pragma unroll
+            for (int a = 0; a < E; ++a) {
+                s_h[place[a]] = kh[a];
+                s_l[place[a]] = kl[a];
+                s_r[place[a]] = kr[a];
             }
-            __syncthreads();
+        }
+        __syncthreads();
+        if (wave < runs) {
+#pragma unroll
+            for (int a = 0; a < E; ++a) {
+                const int e = place[a], r = e / R, idx = e - r * R;
+                const int pr = r ^ 1, pb = pr * R;
+                const int plen = pb >= P ? 0 : (P - pb < R ? P - pb : R);
+                // rank in the partner run: elements below (left run: strictly; right run: or equal)
+                int lo = 0, hi = plen;
+                const bool left = (r & 1) == 0;
+                while (lo < hi) {
+                    const int mid = (lo + hi) >> 1, q = pb + mid;
+                    const bool below = left ? cr_lt(s_h[q], s_l[q], s_r[q], kh[a], kl[a], kr[a])
+                                            : !cr_lt(kh[a], kl[a], kr[a], s_h[q], s_l[q], s_r[q]);
+                    if (below) lo = mid + 1;
+                    else hi = mid;
+                }
+                place[a] = (r & ~1) * R + idx + lo;
+            }
         }
     }
-    for (int i = threadIdx.x; i < m; i += kCtLdsSortThreads) {
-        J.ncode[2 * i] = s_h[i];
-        J.ncode[2 * i + 1] = s_l[i];
-        J.nrow[i] = s_r[i];
+    __syncthreads();
+    if (wave < runs) {
+#pragma unroll
+        for (int a = 0; a < E; ++a)
+            if (place[a] < m) {
+                J.ncode[2 * place[a]] = kh[a];
+                J.ncode[2 * place[a] + 1] = kl[a];
+                J.nrow[place[a]] = kr[a];
+            }
     }
 }
 
@@ -420,10 +460,65 @@ __global__ __launch_bounds__(256) void k_ct_locate(CtJobs js) {
     J.npos[j] = lo;
 }
 
+// The segments' records (k_ct_segments, after its head scan): segment s =
+// (bucket, old count c, new count k, scratch offset), its directory position and first point.
+// Only split segments (c + k > kCtCap) take scratch -- their c + k merged elements, packed in
+// segment order -- so the split kernels visit live elements only.
+template <int PER, int T>
+__device__ __forceinline__ void ct_write_segments(const CtJob &J, int m, const int32_t (&pos)[PER],
+                                                  const int (&head)[PER], int s0, int s_total,
+                                                  const int32_t *s_first, int32_t *s_sum) {
+    const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+    int32_t b[PER], c[PER], k[PER];
+    int sz = 0, sg = s0;
+#pragma unroll
+    for (int a = 0; a < PER; ++a) {
+        const int j = t * PER + a;
+        b[a] = c[a] = k[a] = 0;
+        if (j >= m) continue;
+        sg += head[a];
+        if (!head[a]) continue;
+        b[a] = (int32_t)(J.ometa[pos[a]] & 0x0fffffffu);
+        c[a] = J.bcnt[b[a]];
+        k[a] = s_first[sg + 1] - j;
+        sz += c[a] + k[a] > kCtCap ? c[a] + k[a] : 0;
+    }
+    int incl = sz;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const int o = __shfl_up(incl, off);
+        if (lane >= off) incl += o;
+    }
+    __syncthreads();
+    if (lane == 63) s_sum[wave] = incl;
+    __syncthreads();
+    int before = 0, tot = 0;
+    for (int w = 0; w < T / 64; ++w) {
+        before += w < wave ? s_sum[w] : 0;
+        tot += s_sum[w];
+    }
+    int off = before + incl - sz;
+    sg = s0;
+#pragma unroll
+    for (int a = 0; a < PER; ++a) {
+        const int j = t * PER + a;
+        if (j >= m) break;
+        sg += head[a];
+        if (!head[a]) continue;
+        const bool split = c[a] + k[a] > kCtCap;
+        J.seg[sg] = make_int4(b[a], c[a], k[a], split ? off : -1);
+        J.seg_pos[sg] = pos[a];
+        J.seg_first[sg] = j;
+        off += split ? c[a] + k[a] : 0;
+    }
+    if (t == 0) {
+        J.cnt->n_seg = s_total;
+        J.cnt->n_scratch = tot;
+    }
+}
+
 // One workgroup a tree: the runs of equal directory positions (the touched buckets) become the
-// round's segments: segment s = (bucket, old count, new count, scratch offset j0 + 8 s); the
-// scratch positions no split element takes are marked -1 (every position of
-// [0, m + 8 * segments) is written: later kernels walk them all).
+// round's segments (ct_write_segments).
 constexpr int kCtSegThreads = 1024;
 constexpr int kCtSegPer = kCtSeg / kCtSegThreads;
 
@@ -481,214 +576,7 @@ __global__ __launch_bounds__(kCtSegThreads) void k_ct_segments(CtJobs js) {
         if (head[a]) s_first[s] = j;
     }
     __syncthreads();
-    s = s0;
-#pragma unroll
-    for (int a = 0; a < kCtSegPer; ++a) {
-        const int j = t * kCtSegPer + a;
-        if (j >= m) break;
-        s += head[a];
-        if (!head[a]) continue;
-        const int32_t b = (int32_t)(J.ometa[pos[a]] & 0x0fffffffu);
-        const int32_t c = J.bcnt[b];
-        const int32_t k = s_first[s + 1] - j;
-        const int32_t off = j + 8 * s;
-        J.seg[s] = make_int4(b, c, k, off);
-        J.seg_pos[s] = pos[a];
-        // scratch positions no split element takes: all of an append segment's, the 8 - c
-        // after a split segment's c + k elements
-        const int32_t from = c + k <= kCtCap ? off : off + c + k;
-        for (int e = from; e < off + k + 8; ++e) J.sseg[e] = -1;
-    }
-    if (t == 0) J.cnt->n_seg = s_total;
-}
-
-// A round of at most kCtLdsSort new points (the usual case: one round's K) in one workgroup a
-// tree, in place of k_ct_ncodes, k_ct_lsort, k_ct_locate and k_ct_segments: codes, box and
-// seed offers; the bitonic sort in LDS; each sorted point's directory position; the segments.
-constexpr int kCtFrontThreads = 512;  // 8 points a thread: their codes stay in registers (no spills)
-template <int D>
-__global__ __launch_bounds__(kCtFrontThreads) void k_ct_front(CtJobs js) {
-    constexpr int T = kCtFrontThreads, PER = kCtLdsSort / T;
-    const CtJob J = CT_JOB(js);  // by value: the fields stay in registers across the stores
-    __shared__ uint64_t s_hl[2 * kCtLdsSort];  // the codes' words (first: the seed offers' row staging)
-    __shared__ int32_t s_r[kCtLdsSort];
-    uint64_t *s_h = s_hl, *s_l = s_hl + kCtLdsSort;
-    __shared__ CtPlan s_plan;
-    __shared__ int32_t s_sum[T / 64];
-    __shared__ int32_t s_total;
-    static_assert(sizeof(double) * (T / 64) * 64 * D <= sizeof(s_hl), "row staging fits (d <= 7)");
-    const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
-    const int64_t base = J.cnt->nidx, mraw = *J.T.n_dev - base;
-    if ((mraw > kCtSeg || mraw > J.mb) && t == 0 && J.err) atomicAdd(J.err, 1ull);  // the host's bound broken
-    const int m = (int)(mraw < 0 ? 0 : (mraw > kCtLdsSort ? kCtLdsSort : mraw));
-    for (int w = t; w < (int)(sizeof(CtPlan) / 4); w += T)
-        reinterpret_cast<uint32_t *>(&s_plan)[w] = reinterpret_cast<const uint32_t *>(J.plan)[w];
-    __syncthreads();
-    // 1. codes (kept in registers), the persistent box, the seed offers
-    uint64_t ch[PER], cl[PER];
-    double(*s_rows)[64][D] = reinterpret_cast<double(*)[64][D]>(s_hl);  // [wave][lane][dim]
-#pragma unroll
-    for (int a = 0; a < PER; ++a) {
-        const int i = a * T + t;  // wave-contiguous rows (hull_offer's row0 + lane)
-        const bool live = i < m;
-        double x[D];
-        unsigned long long mn[D], mx[D];
-        if (live) {
-            load_global<D>(J.pts + (base + i) * D, x);
-            ct_code<D>(s_plan, x, ch[a], cl[a]);
-#pragma unroll
-            for (int j = 0; j < D; ++j) mn[j] = mx[j] = okey(x[j]);
-        } else {
-            ch[a] = cl[a] = ~0ull;  // padding sorts last (codes use 126 bits)
-#pragma unroll
-            for (int j = 0; j < D; ++j) {
-                x[j] = 0.0;
-                mn[j] = ~0ull;
-                mx[j] = 0ull;
-            }
-        }
-        if (__ballot(live)) {  // wave-uniform
-#pragma unroll
-            for (int j = 0; j < D; ++j) {
-#pragma unroll
-                for (int off = 32; off > 0; off >>= 1) {
-                    const unsigned long long omn = __shfl_xor(mn[j], off), omx = __shfl_xor(mx[j], off);
-                    mn[j] = omn < mn[j] ? omn : mn[j];
-                    mx[j] = omx > mx[j] ? omx : mx[j];
-                }
-            }
-            if (lane == 0) {
-#pragma unroll
-                for (int j = 0; j < D; ++j) {
-                    atomicMin(J.ibox + j, mn[j]);
-                    atomicMax(J.ibox + kCtMaxDim + j, mx[j]);
-                }
-            }
-            hull_offer<D>(s_plan, x, live, base + a * T + wave * 64, s_rows[wave], J.hull_keys);
-        }
-    }
-    __syncthreads();  // the row staging is done with: the codes take its place
-    if (m == 0) return;  // block-uniform
-    int P = 2;
-    while (P < m) P <<= 1;
-#pragma unroll
-    for (int a = 0; a < PER; ++a) {
-        const int i = a * T + t;
-        if (i < P) {
-            s_h[i] = ch[a];
-            s_l[i] = cl[a];
-            s_r[i] = i < m ? (int32_t)(base + i) : 0x7fffffff;
-        }
-    }
-    __syncthreads();
-    // 2. the bitonic sort by (code, row)
-    for (int k = 2; k <= P; k <<= 1) {
-        for (int j = k >> 1; j > 0; j >>= 1) {
-            const int lj = __ffs(j) - 1;  // j = 2^lj
-            for (int p = t; p < P / 2; p += T) {
-                const int i = ((p >> lj) << (lj + 1)) | (p & (j - 1)), q = i + j;
-                const uint64_t ah = s_h[i], al = s_l[i], bh = s_h[q], bl = s_l[q];
-                const int32_t ar = s_r[i], br = s_r[q];
-                const bool up = (i & k) == 0;
-                if (cr_lt(bh, bl, br, ah, al, ar) == up) {
-                    s_h[i] = bh;
-                    s_l[i] = bl;
-                    s_r[i] = br;
-                    s_h[q] = ah;
-                    s_l[q] = al;
-                    s_r[q] = ar;
-                }
-            }
-            __syncthreads();
-        }
-    }
-    // 3. the sorted points out (thread t: points [PER t, PER t + PER)) and their directory positions
-    int32_t pos[PER];
-    const int n_dir = J.cnt->n_dir;
-#pragma unroll
-    for (int a = 0; a < PER; ++a) {
-        const int j = t * PER + a;
-        pos[a] = -1;
-        if (j < m) {
-            const uint64_t h = s_h[j], l = s_l[j];
-            J.ncode[2 * j] = h;
-            J.ncode[2 * j + 1] = l;
-            J.nrow[j] = s_r[j];
-            int lo = 0, hi = n_dir;  // entry 0 starts at code 0: the answer is in [0, n_dir)
-            while (hi - lo > 1) {
-                const int mid = (lo + hi) >> 1;
-                const uint64_t sh = J.odir_code[2 * mid], sl = J.odir_code[2 * mid + 1];
-                if (sh < h || (sh == h && sl <= l)) lo = mid;
-                else hi = mid;
-            }
-            pos[a] = lo;
-        }
-    }
-    __syncthreads();  // the LDS arrays now hold the positions and the segments' first points
-    int32_t *s_pos = reinterpret_cast<int32_t *>(s_l);    // [kCtLdsSort]
-    int32_t *s_first = reinterpret_cast<int32_t *>(s_h);  // [kCtLdsSort + 1] (s_h holds 2 kCtLdsSort words)
-#pragma unroll
-    for (int a = 0; a < PER; ++a)
-        if (t * PER + a < m) s_pos[t * PER + a] = pos[a];
-    __syncthreads();
-    // 4. the segments (as k_ct_segments): runs of equal positions, segment s = (bucket, old
-    //    count, new count, scratch offset j0 + 8 s); scratch positions no split element takes -1
-    const int32_t prev = t > 0 && t * PER - 1 < m ? s_pos[t * PER - 1] : -2;
-    int head[PER], cnt = 0;
-#pragma unroll
-    for (int a = 0; a < PER; ++a) {
-        const int j = t * PER + a;
-        const int32_t pv = a == 0 ? prev : pos[a - 1];
-        head[a] = (j < m && (j == 0 || pos[a] != pv)) ? 1 : 0;
-        cnt += head[a];
-    }
-    int incl = cnt;
-#pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-        const int o = __shfl_up(incl, off);
-        if (lane >= off) incl += o;
-    }
-    if (lane == 63) s_sum[wave] = incl;
-    __syncthreads();
-    if (t == 0) {
-        int acc = 0;
-        for (int w = 0; w < T / 64; ++w) {
-            const int v = s_sum[w];
-            s_sum[w] = acc;
-            acc += v;
-        }
-        s_total = acc;
-        s_first[acc] = m;
-    }
-    __syncthreads();
-    const int s0 = s_sum[wave] + incl - cnt - 1;  // segment of the point before this thread's first
-    int sg = s0;
-#pragma unroll
-    for (int a = 0; a < PER; ++a) {
-        const int j = t * PER + a;
-        if (j >= m) break;
-        sg += head[a];
-        J.nseg[j] = sg;
-        if (head[a]) s_first[sg] = j;
-    }
-    __syncthreads();
-    sg = s0;
-#pragma unroll
-    for (int a = 0; a < PER; ++a) {
-        const int j = t * PER + a;
-        if (j >= m) break;
-        sg += head[a];
-        if (!head[a]) continue;
-        const int32_t b = (int32_t)(J.ometa[pos[a]] & 0x0fffffffu);
-        const int32_t c = J.bcnt[b];
-        const int32_t k = s_first[sg + 1] - j;
-        const int32_t off = j + 8 * sg;
-        J.seg[sg] = make_int4(b, c, k, off);
-        J.seg_pos[sg] = pos[a];
-        const int32_t from = c + k <= kCtCap ? off : off + c + k;
-        for (int e = from; e < off + k + 8; ++e) J.sseg[e] = -1;
-    }
-    if (t == 0) J.cnt->n_seg = s_total;
+    ct_write_segments<kCtSegPer, kCtSegThreads>(J, (int)m, pos, head, s0, s_total, s_first, s_sum);
 }
 
 // Per sorted new point: appended to its bucket, or placed in its split segment's merged list
@@ -703,7 +591,7 @@ __global__ __launch_bounds__(256) void k_ct_apply(CtJobs js) {
     const int s = J.nseg[j];
     const int4 g = J.seg[s];
     const int32_t b = g.x, c = g.y, k = g.z, off = g.w;
-    const int32_t j0 = off - 8 * s;
+    const int32_t j0 = J.seg_first[s];
     const uint64_t h = J.ncode[2 * j], l = J.ncode[2 * j + 1];
     const int32_t row = J.nrow[j];
     if (c + k <= kCtCap) {
@@ -827,9 +715,7 @@ __device__ __forceinline__ bool ct_same_a(const uint8_t *__restrict__ a, int64_t
     return ((i - lo) >> 3) == ((i - 1 - lo) >> 3);
 }
 
-__device__ __forceinline__ int64_t ct_scratch_total(const CtJob &J) {
-    return ct_new_count(J) + 8 * (int64_t)J.cnt->n_seg;
-}
+__device__ __forceinline__ int64_t ct_scratch_total(const CtJob &J) { return J.cnt->n_scratch; }
 
 // leaf starts of the split segments: 1 the segment's first leaf (keeps the bucket), 2 a new leaf
 __global__ __launch_bounds__(256) void k_ct_split_flags(CtJobs js) {
@@ -1294,6 +1180,7 @@ __global__ __launch_bounds__(kCtLevelThreads) void k_ct_levels(CtJobs js) {
     c->n_buckets += nn;
     c->n_new_dir = 0;
     c->n_seg = 0;
+    c->n_scratch = 0;
     c->nidx = c->nidx + ct_new_count(J);
     const SpreadOut &sp = J.sp;
     if (sp.host_out) {
@@ -1408,7 +1295,7 @@ __global__ void k_ct_bulk_fill(const double *__restrict__ pts, const uint64_t *_
                 dir_box[D + q] = -__builtin_huge_valf();
             }
             cnt->n_dir = cnt->n_buckets = 1;
-            cnt->n_seg = cnt->n_new_dir = 0;
+            cnt->n_seg = cnt->n_new_dir = cnt->n_scratch = 0;
             cnt->nidx = 0;
         }
         return;
@@ -1417,7 +1304,7 @@ __global__ void k_ct_bulk_fill(const double *__restrict__ pts, const uint64_t *_
     if (j == n - 1) {
         const int32_t nb = leaf[j] + flag[j];
         cnt->n_dir = cnt->n_buckets = nb;
-        cnt->n_seg = cnt->n_new_dir = 0;
+        cnt->n_seg = cnt->n_new_dir = cnt->n_scratch = 0;
         cnt->nidx = n;
     }
     if (!flag[j]) return;
@@ -1843,7 +1730,7 @@ CtPlan make_ct_plan(int32_t d, const double *lo, const double *hi, int32_t spati
 
 void CellTree::release() {
     void *ps[] = {plan, cnt, bpts, bids, bcnt, bcode, bbox, nbox[0], nbox[1], nmeta[0], nmeta[1], ucode, lflag, lcount, dir_code[0], dir_code[1],
-                  ncode, ccode, scode, edir_code, nrow, crow, npos, nseg, seg_pos, srow, sseg, slead, srank, edir_bk,
+                  ncode, ccode, scode, edir_code, nrow, crow, npos, nseg, seg_pos, seg_first, srow, sseg, slead, srank, edir_bk,
                   edir_pos, seg, hull_keys, ibox, hull_pts, hull_ids, fhi, flo, fk0, fk1, fv0, fv1, fflag, fleaf, ftemp};
     for (void *p : ps)
         if (p) (void)hipFree(p);
@@ -1889,6 +1776,7 @@ void CellTree::reserve(int64_t c, int32_t d) {
     al((void **)&nseg, sizeof(int32_t) * kCtSeg, "ct segments");
     al((void **)&seg, sizeof(int4) * kCtSeg, "ct segments");
     al((void **)&seg_pos, sizeof(int32_t) * kCtSeg, "ct segments");
+    al((void **)&seg_first, sizeof(int32_t) * kCtSeg, "ct segments");
     al((void **)&scode, sizeof(uint64_t) * 2 * kCtScratch, "ct scratch");
     al((void **)&srow, sizeof(int32_t) * kCtScratch, "ct scratch");
     al((void **)&sseg, sizeof(int32_t) * kCtScratch, "ct scratch");
@@ -1998,6 +1886,7 @@ CtJob CellTree::prepare(const double *pts, int64_t n_upper, const int64_t *n_dev
     J.nseg = nseg;
     J.seg = seg;
     J.seg_pos = seg_pos;
+    J.seg_first = seg_first;
     J.scode = scode;
     J.srow = srow;
     J.sseg = sseg;
@@ -2030,25 +1919,22 @@ void launch_ct_jobs(const CtJob *d_jobs, const CtJob *h_jobs, int32_t n, int32_t
     const unsigned yn = (unsigned)n;
     if (mb > 0) {
         const unsigned b256 = (unsigned)((mb + 255) / 256);
-        if (mb <= kCtLdsSort && d <= 7) {  // one workgroup a tree: codes, sort, positions, segments
-            hipLaunchKernelGGL(d == 3 ? k_ct_front<3> : k_ct_front<7>, dim3(1, yn), dim3(kCtFrontThreads), 0, stream,
-                               js);
-            hip_check(hipGetLastError(), "k_ct_front");
+        // (round 4: these four fused into one workgroup a tree ran 0.30-0.40 ms a round at 256
+        // seeds and 0.28-0.36 at 32, against 0.27 and 0.15 as separate launches: the codes and
+        // seed offers need the waves of many workgroups)
+        hipLaunchKernelGGL(by_d(k_ct_ncodes<3>, k_ct_ncodes<7>, k_ct_ncodes<15>), dim3(b256, yn), dim3(64 * kCtWaves), 0,
+                           stream, js);
+        hip_check(hipGetLastError(), "k_ct_ncodes");
+        if (mb <= kCtLdsSort) {
+            hipLaunchKernelGGL(k_ct_lsort, dim3(1, yn), dim3(kCtLdsSortThreads), 0, stream, js);
         } else {
-            hipLaunchKernelGGL(by_d(k_ct_ncodes<3>, k_ct_ncodes<7>, k_ct_ncodes<15>), dim3(b256, yn),
-                               dim3(64 * kCtWaves), 0, stream, js);
-            hip_check(hipGetLastError(), "k_ct_ncodes");
-            if (mb <= kCtLdsSort) {
-                hipLaunchKernelGGL(k_ct_lsort, dim3(1, yn), dim3(kCtLdsSortThreads), 0, stream, js);
-            } else {
-                const unsigned chunks = (unsigned)((mb + kCtChunk - 1) / kCtChunk);
-                hipLaunchKernelGGL(k_ct_csort, dim3((chunks + kCtChunkWaves - 1) / kCtChunkWaves, yn),
-                                   dim3(64 * kCtChunkWaves), 0, stream, js);
-                hipLaunchKernelGGL(k_ct_crank, dim3(b256, yn), dim3(256), 0, stream, js);
-            }
-            hipLaunchKernelGGL(k_ct_locate, dim3(b256, yn), dim3(256), 0, stream, js);
-            hipLaunchKernelGGL(k_ct_segments, dim3(1, yn), dim3(kCtSegThreads), 0, stream, js);
+            const unsigned chunks = (unsigned)((mb + kCtChunk - 1) / kCtChunk);
+            hipLaunchKernelGGL(k_ct_csort, dim3((chunks + kCtChunkWaves - 1) / kCtChunkWaves, yn),
+                               dim3(64 * kCtChunkWaves), 0, stream, js);
+            hipLaunchKernelGGL(k_ct_crank, dim3(b256, yn), dim3(256), 0, stream, js);
         }
+        hipLaunchKernelGGL(k_ct_locate, dim3(b256, yn), dim3(256), 0, stream, js);
+        hipLaunchKernelGGL(k_ct_segments, dim3(1, yn), dim3(kCtSegThreads), 0, stream, js);
         hipLaunchKernelGGL(by_d(k_ct_apply<3>, k_ct_apply<7>, k_ct_apply<15>), dim3(b256, yn), dim3(256), 0, stream, js);
         hip_check(hipGetLastError(), "k_ct_apply");
         // the split elements: at most 9 a new point, a thread each
