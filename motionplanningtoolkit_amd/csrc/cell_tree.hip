@@ -1647,7 +1647,7 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(D >= 15 ? 4 
     const int64_t xcd = blockIdx.x % kXcd, slot = blockIdx.x / kXcd;
     const int64_t job = xcd + kXcd * (slot / blocks_per_job);
     if (job >= n_jobs) return;
-    const CtNnJob &J = jobs[job];
+    const CtNnJob J = jobs[job];  // by value: the tree's pointers stay in SGPRs across the walk
     ct_walk<D, BS, W>(J.T, J.q, nq, J.ids, J.d2, slot % blocks_per_job);
 }
 
