@@ -321,6 +321,14 @@ def pmc_traffic(summ, kernel):
     return None
 
 
+def pmc_traffic_sum(summ, subs):
+    """Measured HBM bytes of a stage's launch chain: every summary entry whose kernel name
+    contains one of `subs` (each entry once; template instances of one kernel all count),
+    None when none is in the summary."""
+    hits = [v["hbm_bytes_per_launch"] for name, v in summ.items() if any(s in name for s in subs)]
+    return sum(hits) if hits else None
+
+
 def stage_table(per_launch, cst, K, n0, d, pmax, geo, nn_mode, kernels, summ):
     stages = {}
     for s, kern in kernels.items():
@@ -353,8 +361,8 @@ def stage_table(per_launch, cst, K, n0, d, pmax, geo, nn_mode, kernels, summ):
 # measured traffic per launch is summed (the collide chain runs once per collide sub-batch)
 JOINT_STAGE_KERNELS = {
     "sample": ["k_sample_jobs"],
-    "nn_build": ["k_ct_ncodes", "k_ct_csort", "k_ct_crank", "k_ct_locate", "k_ct_segments", "k_ct_apply",
-                 "k_ct_split_flags", "k_ct_split_scan", "k_ct_split_fill", "k_ct_dmerge", "k_ct_levels"],
+    "nn_build": ["k_ct_ncodes", "k_ct_lsort", "k_ct_csort", "k_ct_crank", "k_ct_locate", "k_ct_segments",
+                 "k_ct_apply", "k_ct_split_", "k_ct_dmerge", "k_ct_lflags", "k_ct_lgroup", "k_ct_levels"],
     "nn_query": ["k_ct_nn1_jobs"],
     "steer": ["k_steer_jobs"],
     "collide": ["k_pairs<", "k_scan_excl<mpt::ExpandHeaders", "k_cands", "k_narrow", "k_overflow"],
@@ -398,9 +406,10 @@ def joint_stage_table(times, c, K, nj, n_tot, d, pmax, geo, summ):
             st["nn_points_per_query"] = round(c["nn_points"] / (K * nj), 2)
             st["nn_boxes_per_query"] = round(c["nn_cells"] / (K * nj), 2)
             st["nn_steps_per_query"] = round(c.get("nn_steps", 0) / (K * nj), 2)
-        trs = [pmc_traffic(summ, k) for k in JOINT_STAGE_KERNELS.get(s, [])]
-        if trs and all(x is not None for x in trs):
-            tr = sum(trs) * (n_sub if s == "collide" else 1)
+        subs = JOINT_STAGE_KERNELS.get(s, [])
+        tr = pmc_traffic_sum(summ, subs) if subs else None
+        if tr is not None:
+            tr *= n_sub if s == "collide" else 1
             st.update({"traffic": int(tr), "traffic_gbs": round(tr / t / 1e9, 1),
                        "frac_hbm_measured": round(tr / t / 1e9 / HBM_PEAK_GBS, 4),
                        "traffic_over_compulsory": round(tr / b, 2)})
