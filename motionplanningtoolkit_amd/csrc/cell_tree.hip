@@ -360,87 +360,8 @@ __global__ __launch_bounds__(256) void k_ct_crank(CtJobs js) {
     const int e = (int)blockIdx.x * (int)blockDim.x + (int)threadIdx.x;
     if (e >= m) return;
     if (m <= (int64_t)kCtChunk * 4) ct_crank_n<4>(J, m, e);
+    else if (m <= (int64_t)kCtChunk * 8) ct_crank_n<8>(J, m, e);  // a round's K = 4096: 8 chunks
     else ct_crank_n<kCtChunks>(J, m, e);
-}
-
-// Rounds of at most kCtLdsSort new points (the usual case: one round's K): one workgroup a tree
-// sorts them by (code, row): each wave its 512 in registers (ct_wave_sort512), then the runs
-// merged pairwise in LDS (each element's place = its index in its run + its rank in the partner
-// run, found by binary search: stable, the left run's ties first) -- a fraction of a bitonic
-// network's LDS traffic.  80 KiB of LDS: gfx950's 160 KiB takes it.
-constexpr int kCtLdsSort = 4096;
-constexpr int kCtLdsSortThreads = kCtLdsSort / kCtChunkE;  // 512: 8 waves of 512 pairs
-__global__ __launch_bounds__(kCtLdsSortThreads) void k_ct_lsort(CtJobs js) {
-    constexpr int E = kCtChunkE;
-    const CtJob J = CT_JOB(js);  // by value: the fields stay in registers across the stores
-    __shared__ uint64_t s_h[kCtLdsSort], s_l[kCtLdsSort];
-    __shared__ int32_t s_r[kCtLdsSort];
-    // the host's bound (mb <= kCtLdsSort) chose this kernel; a broken bound is counted by
-    // k_ct_ncodes and must not write past the LDS arrays
-    const int m = (int)(ct_new_count(J) < kCtLdsSort ? ct_new_count(J) : kCtLdsSort);
-    if (m <= 1) return;
-    const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
-    const int runs = (m + kCtChunk - 1) / kCtChunk;  // waves with points (block-uniform)
-    uint64_t kh[E], kl[E];
-    int32_t kr[E];
-    if (wave < runs) {
-#pragma unroll
-        for (int a = 0; a < E; ++a) {
-            const int i = wave * kCtChunk + lane * E + a;
-            const bool live = i < m;
-            kh[a] = live ? J.ncode[2 * i] : ~0ull;  // padding sorts last (codes use 126 bits)
-            kl[a] = live ? J.ncode[2 * i + 1] : ~0ull;
-            kr[a] = live ? J.nrow[i] : 0x7fffffff;
-        }
-        ct_wave_sort512(kh, kl, kr, lane);
-    }
-    const int P = runs * kCtChunk;  // sorted runs of 512 fill [0, P)
-    int R = kCtChunk;
-    // element e = wave * 512 + lane * 8 + a stays with its thread; only its place changes
-    int place[E];
-#pragma unroll
-    for (int a = 0; a < E; ++a) place[a] = wave * kCtChunk + lane * E + a;
-    for (; R < P; R <<= 1) {
-        __syncthreads();
-        if (wave < runs) {
-#pragma unroll
-            for (int a = 0; a < E; ++a) {
-                s_h[place[a]] = kh[a];
-                s_l[place[a]] = kl[a];
-                s_r[place[a]] = kr[a];
-            }
-        }
-        __syncthreads();
-        if (wave < runs) {
-#pragma unroll
-            for (int a = 0; a < E; ++a) {
-                const int e = place[a], r = e / R, idx = e - r * R;
-                const int pr = r ^ 1, pb = pr * R;
-                const int plen = pb >= P ? 0 : (P - pb < R ? P - pb : R);
-                // rank in the partner run: elements below (left run: strictly; right run: or equal)
-                int lo = 0, hi = plen;
-                const bool left = (r & 1) == 0;
-                while (lo < hi) {
-                    const int mid = (lo + hi) >> 1, q = pb + mid;
-                    const bool below = left ? cr_lt(s_h[q], s_l[q], s_r[q], kh[a], kl[a], kr[a])
-                                            : !cr_lt(kh[a], kl[a], kr[a], s_h[q], s_l[q], s_r[q]);
-                    if (below) lo = mid + 1;
-                    else hi = mid;
-                }
-                place[a] = (r & ~1) * R + idx + lo;
-            }
-        }
-    }
-    __syncthreads();
-    if (wave < runs) {
-#pragma unroll
-        for (int a = 0; a < E; ++a)
-            if (place[a] < m) {
-                J.ncode[2 * place[a]] = kh[a];
-                J.ncode[2 * place[a] + 1] = kl[a];
-                J.nrow[place[a]] = kr[a];
-            }
-    }
 }
 
 // each sorted new point's directory position: the last entry whose start is <= its code
@@ -471,15 +392,24 @@ __device__ __forceinline__ void ct_write_segments(const CtJob &J, int m, const i
     const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
     int32_t b[PER], c[PER], k[PER];
     int sz = 0, sg = s0;
+    // the heads' buckets, then their counts: each pass's loads all in flight together
+#pragma unroll
+    for (int a = 0; a < PER; ++a) {
+        const bool h = t * PER + a < m && head[a];
+        b[a] = h ? (int32_t)(J.ometa[pos[a]] & 0x0fffffffu) : 0;
+    }
+#pragma unroll
+    for (int a = 0; a < PER; ++a) {
+        const bool h = t * PER + a < m && head[a];
+        c[a] = h ? J.bcnt[b[a]] : 0;
+    }
 #pragma unroll
     for (int a = 0; a < PER; ++a) {
         const int j = t * PER + a;
-        b[a] = c[a] = k[a] = 0;
+        k[a] = 0;
         if (j >= m) continue;
         sg += head[a];
         if (!head[a]) continue;
-        b[a] = (int32_t)(J.ometa[pos[a]] & 0x0fffffffu);
-        c[a] = J.bcnt[b[a]];
         k[a] = s_first[sg + 1] - j;
         sz += c[a] + k[a] > kCtCap ? c[a] + k[a] : 0;
     }
@@ -1925,14 +1855,13 @@ void launch_ct_jobs(const CtJob *d_jobs, const CtJob *h_jobs, int32_t n, int32_t
         hipLaunchKernelGGL(by_d(k_ct_ncodes<3>, k_ct_ncodes<7>, k_ct_ncodes<15>), dim3(b256, yn), dim3(64 * kCtWaves), 0,
                            stream, js);
         hip_check(hipGetLastError(), "k_ct_ncodes");
-        if (mb <= kCtLdsSort) {
-            hipLaunchKernelGGL(k_ct_lsort, dim3(1, yn), dim3(kCtLdsSortThreads), 0, stream, js);
-        } else {
-            const unsigned chunks = (unsigned)((mb + kCtChunk - 1) / kCtChunk);
-            hipLaunchKernelGGL(k_ct_csort, dim3((chunks + kCtChunkWaves - 1) / kCtChunkWaves, yn),
-                               dim3(64 * kCtChunkWaves), 0, stream, js);
-            hipLaunchKernelGGL(k_ct_crank, dim3(b256, yn), dim3(256), 0, stream, js);
-        }
+        // the sort over many CUs: chunks of 512 sorted by a wave each, then every pair's rank
+        // across the chunks (round 4: one workgroup a tree sorting in LDS took 0.12 ms a round
+        // at 256 seeds and 0.11 at 32 -- at 32 trees most CUs idle)
+        const unsigned chunks = (unsigned)((mb + kCtChunk - 1) / kCtChunk);
+        hipLaunchKernelGGL(k_ct_csort, dim3((chunks + kCtChunkWaves - 1) / kCtChunkWaves, yn), dim3(64 * kCtChunkWaves),
+                           0, stream, js);
+        hipLaunchKernelGGL(k_ct_crank, dim3(b256, yn), dim3(256), 0, stream, js);
         hipLaunchKernelGGL(k_ct_locate, dim3(b256, yn), dim3(256), 0, stream, js);
         hipLaunchKernelGGL(k_ct_segments, dim3(1, yn), dim3(kCtSegThreads), 0, stream, js);
         hipLaunchKernelGGL(by_d(k_ct_apply<3>, k_ct_apply<7>, k_ct_apply<15>), dim3(b256, yn), dim3(256), 0, stream, js);
