@@ -89,21 +89,6 @@ __device__ __forceinline__ bool box_overlap(const float alo[3], const float ahi[
            blo[2] <= ahi[2];
 }
 
-// Does a (pose, link) unit's whole-link box meet any of the env tree's top-level item boxes?
-// (A unit that meets none has no triangle pair: every cluster box lies inside the link box and
-// every triangle box inside its top-level item's.)  The live-unit list's cull in k_steer: FCL's
-// object-level AABB test, one tree level deeper than the root box.
-__device__ __forceinline__ bool env_top_overlap(const EnvDev &env, const float lo[3], const float hi[3]) {
-    if (!box_overlap(lo, hi, env.root_lo, env.root_hi)) return false;
-    const int lev = env.n_levels - 1;
-    const int32_t end = env.lev_off[lev + 1];
-    for (int32_t i = env.lev_off[lev]; i < end; ++i) {
-        const Item it = env.items[i];
-        if (box_overlap(lo, hi, it.lo, it.hi)) return true;
-    }
-    return false;
-}
-
 // --- the fused per-unit walk (collide.hip k_collide; broad.hip k_narrow's overflow re-run) ---
 // Uniform walk of the env BVH by one wave per (pose, link) unit; s_nodes is an LDS prefix of
 // env.nodes (or env.nodes itself with n_lds = n_nodes), the stack kStackDepth ints per wave.

@@ -315,7 +315,7 @@ __global__ __launch_bounds__(256) void k_steer(EngineParams p, uint64_t ext_base
             for (int j = 0; j < 3; ++j) rt[9 + j] = T[j];
             float blo[3], bhi[3];
             local_box(lv.links[l].bc, lv.links[l].be, R, T, blo, bhi);
-            if (env_top_overlap(lv.env, blo, bhi)) mask |= 1ull << (i * p.L + l);
+            if (box_overlap(blo, bhi, lv.env.root_lo, lv.env.root_hi)) mask |= 1ull << (i * p.L + l);
         }
     __shared__ uint32_t s_wave[4];
     __shared__ uint32_t s_base;
@@ -541,7 +541,7 @@ __global__ __launch_bounds__(256) void k_steer_jobs(EngineParams p, const Engine
             for (int j = 0; j < 3; ++j) rt[9 + j] = T[j];
             float blo[3], bhi[3];
             local_box(lv.links[l].bc, lv.links[l].be, R, T, blo, bhi);
-            if (env_top_overlap(lv.env, blo, bhi)) mask |= 1ull << (i * p.L + l);
+            if (box_overlap(blo, bhi, lv.env.root_lo, lv.env.root_hi)) mask |= 1ull << (i * p.L + l);
         }
     __shared__ uint32_t s_wave[4];
     __shared__ uint32_t s_base;
