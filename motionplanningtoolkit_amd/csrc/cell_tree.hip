@@ -567,38 +567,42 @@ __global__ __launch_bounds__(256) void k_ct_apply(CtJobs js) {
         return;
     }
     // split: this point's place in the merged list = its index among the new + the old points
-    // below it
-    int below = 0;
-    for (int o = 0; o < c; ++o) {
-        const int64_t os = (int64_t)b * kCtCap + o;
-        below += cr_lt(J.bcode[2 * os], J.bcode[2 * os + 1], J.bids[os] - 1, h, l, row) ? 1 : 0;
+    // below it.  The bucket's old (code, row) pairs into registers first (independent loads).
+    uint64_t oh[kCtCap], ol[kCtCap];
+    int32_t orw[kCtCap];
+#pragma unroll
+    for (int o = 0; o < kCtCap; ++o) {
+        const int64_t os = (int64_t)b * kCtCap + (o < c ? o : 0);
+        oh[o] = J.bcode[2 * os];
+        ol[o] = J.bcode[2 * os + 1];
+        orw[o] = J.bids[os] - 1;
     }
+    int below = 0;
+#pragma unroll
+    for (int o = 0; o < kCtCap; ++o) below += (o < c && cr_lt(oh[o], ol[o], orw[o], h, l, row)) ? 1 : 0;
     const int32_t e = off + (j - j0) + below;
     J.scode[2 * e] = h;
     J.scode[2 * e + 1] = l;
     J.srow[e] = row;
     J.sseg[e] = s;
     if (j != j0) return;
-    for (int o = 0; o < c; ++o) {  // the old points' places
-        const int64_t os = (int64_t)b * kCtCap + o;
-        const uint64_t oh = J.bcode[2 * os], ol = J.bcode[2 * os + 1];
-        const int32_t orow = J.bids[os] - 1;
+#pragma unroll
+    for (int o = 0; o < kCtCap; ++o) {  // the old points' places
+        if (o >= c) break;
         int ob = 0;
-        for (int o2 = 0; o2 < c; ++o2) {
-            const int64_t s2 = (int64_t)b * kCtCap + o2;
-            ob += cr_lt(J.bcode[2 * s2], J.bcode[2 * s2 + 1], J.bids[s2] - 1, oh, ol, orow) ? 1 : 0;
-        }
+#pragma unroll
+        for (int o2 = 0; o2 < kCtCap; ++o2) ob += (o2 < c && cr_lt(oh[o2], ol[o2], orw[o2], oh[o], ol[o], orw[o])) ? 1 : 0;
         int lo = 0, hi = k;  // new points below it (sorted)
         while (lo < hi) {
             const int mid = (lo + hi) >> 1;
             const int q = j0 + mid;
-            if (cr_lt(J.ncode[2 * q], J.ncode[2 * q + 1], J.nrow[q], oh, ol, orow)) lo = mid + 1;
+            if (cr_lt(J.ncode[2 * q], J.ncode[2 * q + 1], J.nrow[q], oh[o], ol[o], orw[o])) lo = mid + 1;
             else hi = mid;
         }
         const int32_t eo = off + ob + lo;
-        J.scode[2 * eo] = oh;
-        J.scode[2 * eo + 1] = ol;
-        J.srow[eo] = orow;
+        J.scode[2 * eo] = oh[o];
+        J.scode[2 * eo + 1] = ol[o];
+        J.srow[eo] = orw[o];
         J.sseg[eo] = s;
     }
 }
