@@ -1493,27 +1493,34 @@ __device__ __forceinline__ void ct_walk(const CellTreeDev &T, const double *__re
             bool keep = false, better = false;
             float lbf = 0.0f;
             uint32_t child = 0;
-            if (act && (code & kCtLeafBit)) {
-                const int cnt = (int)((code >> 28) & 7u) + 1;
-                if (ls < cnt) {
-                    const int64_t p = (int64_t)(code & 0x0fffffffu) * kCtCap + ls;
-                    double row[D];
+            const int cnt = (int)((code >> 28) & 7u) + 1;
+            if (act && ls < cnt) {
+                // one load for either kind: a bucket's point (D doubles, its id) and an inner
+                // node's child box (2D floats, its record) are the same 8D + 4 bytes, so a step
+                // whose entries mix buckets and inner nodes waits on memory once
+                const bool leaf = code & kCtLeafBit;
+                const int64_t e = leaf ? (int64_t)(code & 0x0fffffffu) * kCtCap + ls
+                                       : (int64_t)(code & 0x0fffffffu) + ls;
+                const gdbl src = leaf ? (gdbl)T.bpts : (gdbl)(const void *)T.nbox;
+                const gu32 msrc = leaf ? (gu32)(const void *)T.bids : (gu32)T.nmeta;
+                double row[D];
 #pragma unroll
-                    for (int k = 0; k < D; ++k) row[k] = ((gdbl)T.bpts)[p * D + k];
+                for (int k = 0; k < D; ++k) row[k] = src[e * D + k];
+                const uint32_t meta = msrc[e];
+                if (leaf) {
                     const double dd = flann_l2<D>(qq, row);
-                    const int32_t id = ((gi32)T.bids)[p];
+                    const int32_t id = (int32_t)meta;
                     ++n_pts;
                     better = (dd < bd) | ((dd == bd) & (id < bi));
                     nn_take(bd, bi, dd, id);
-                }
-            } else if (act) {
-                const int cnt = (int)((code >> 28) & 7u) + 1;
-                if (ls < cnt) {
-                    const int64_t c = (int64_t)(code & 0x0fffffffu) + ls;
+                } else {
                     float bx[2 * D];
 #pragma unroll
-                    for (int k = 0; k < 2 * D; ++k) bx[k] = ((gflt)T.nbox)[c * 2 * D + k];
-                    child = ((gu32)T.nmeta)[c];
+                    for (int k = 0; k < D; ++k) {
+                        bx[2 * k] = __int_as_float(__double2loint(row[k]));
+                        bx[2 * k + 1] = __int_as_float(__double2hiint(row[k]));
+                    }
+                    child = meta;
                     lbf = ct_box_lb<D>(bx, qq, qlo, qhi);
                     keep = true;
                     ++n_box;
