@@ -1321,7 +1321,6 @@ __device__ __forceinline__ float ct_box_lb(const float *__restrict__ b, const do
 // LDS traffic, unlike ds_bpermute) ----
 constexpr int kDppXor1 = 0xB1;   // quad_perm [1,0,3,2]: lane i ^ 1
 constexpr int kDppXor2 = 0x4E;   // quad_perm [2,3,0,1]: lane i ^ 2
-constexpr int kDppRev4 = 0x1B;   // quad_perm [3,2,1,0]: lane i ^ 3
 constexpr int kDppRev8 = 0x141;  // row_half_mirror: lane i ^ 7 within 8
 constexpr int kDppRev16 = 0x140; // row_mirror: lane i ^ 15 within 16
 template <int CTRL>
