@@ -235,78 +235,78 @@ __device__ __forceinline__ void cx3(uint64_t &h, uint64_t &l, int32_t &r, uint64
     r = sw ? pr : r;
 }
 
-// The new points' sort over many CUs: each wave sorts a chunk of 512 (8 a lane: partners 8+
-// apart by lane shuffles, closer ones in registers); then every element's rank = its index in
-// its chunk + the count of smaller pairs in each other chunk (fixed-step binary searches).
+// The new points' sort over many CUs: a 256-thread workgroup sorts a chunk of 512 (code, row)
+// pairs, 2 a thread (bitonic: the partner 1 apart in registers, 2..64 apart by lane shuffles in
+// the wave, 128+ apart through LDS); then every element's rank = its index in its chunk + the
+// count of smaller pairs in each other chunk (fixed-step binary searches).  (One wave a chunk,
+// 8 pairs a lane, ran 36 us at 32 seeds: one wave a SIMD and a long serial chain each.)
 constexpr int kCtChunk = 512;
 constexpr int kCtChunks = kCtSeg / kCtChunk;
-constexpr int kCtChunkWaves = 4;
+constexpr int kCtSortThreads = kCtChunk / 2;
 
-// a wave's 512 (code, row) pairs, 8 a lane (element lane * 8 + a), sorted ascending: bitonic,
-// partners 8+ apart by lane shuffles, closer ones in registers
-constexpr int kCtChunkE = kCtChunk / 64;
-__device__ __forceinline__ void ct_wave_sort512(uint64_t (&kh)[kCtChunkE], uint64_t (&kl)[kCtChunkE],
-                                                int32_t (&kr)[kCtChunkE], int lane) {
-    constexpr int E = kCtChunkE;
-#pragma unroll 1
-    for (int k = 2; k <= kCtChunk; k <<= 1) {
-#pragma unroll 1
-        for (int j = k >> 1; j > 0; j >>= 1) {
-            if (j >= E) {
-                const int lm = j / E;
-                const bool lower = (lane & lm) == 0;
-#pragma unroll
-                for (int a = 0; a < E; ++a) {
-                    const uint64_t ph = __shfl_xor(kh[a], lm), pl = __shfl_xor(kl[a], lm);
-                    const int32_t pr = __shfl_xor(kr[a], lm);
-                    cx3(kh[a], kl[a], kr[a], ph, pl, pr, lower == (((lane * E + a) & k) == 0));
-                }
-            } else {
-#pragma unroll
-                for (int jj = E / 2; jj > 0; jj >>= 1) {
-                    if (jj != j) continue;
-#pragma unroll
-                    for (int a = 0; a < E; ++a) {
-                        const int b = a ^ jj;
-                        if (b < a) continue;
-                        const bool up = ((lane * E + a) & k) == 0;
-                        const bool sw = up == cr_lt(kh[b], kl[b], kr[b], kh[a], kl[a], kr[a]);
-                        const uint64_t ah = kh[a], al = kl[a], bh = kh[b], bl = kl[b];
-                        const int32_t ar = kr[a], br = kr[b];
-                        kh[a] = sw ? bh : ah;
-                        kl[a] = sw ? bl : al;
-                        kr[a] = sw ? br : ar;
-                        kh[b] = sw ? ah : bh;
-                        kl[b] = sw ? al : bl;
-                        kr[b] = sw ? ar : br;
-                    }
-                }
-            }
-        }
-    }
-}
-
-__global__ __launch_bounds__(64 * kCtChunkWaves) void k_ct_csort(CtJobs js) {
+__global__ __launch_bounds__(kCtSortThreads) void k_ct_csort(CtJobs js) {
     const CtJob J = CT_JOB(js);  // by value: the fields stay in registers across the stores
+    __shared__ uint64_t s_h[kCtChunk], s_l[kCtChunk];
+    __shared__ int32_t s_r[kCtChunk];
     const int64_t m = ct_new_count(J);
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
-    const int c0 = ((int)blockIdx.x * kCtChunkWaves + wave) * kCtChunk;
-    if (c0 >= m) return;
-    constexpr int E = kCtChunkE;
-    uint64_t kh[E], kl[E];
-    int32_t kr[E];
+    const int c0 = (int)blockIdx.x * kCtChunk;
+    if (c0 >= m) return;  // block-uniform
+    const int t = threadIdx.x;
+    uint64_t kh[2], kl[2];
+    int32_t kr[2];
 #pragma unroll
-    for (int a = 0; a < E; ++a) {
-        const int i = c0 + lane * E + a;
+    for (int a = 0; a < 2; ++a) {
+        const int i = c0 + 2 * t + a;
         const bool live = i < m;
         kh[a] = live ? J.ncode[2 * i] : ~0ull;  // padding sorts last (codes use 126 bits)
         kl[a] = live ? J.ncode[2 * i + 1] : ~0ull;
         kr[a] = live ? J.nrow[i] : 0x7fffffff;
     }
-    ct_wave_sort512(kh, kl, kr, lane);
+#pragma unroll 1
+    for (int k = 2; k <= kCtChunk; k <<= 1) {
+#pragma unroll 1
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            const bool up = ((2 * t) & k) == 0;  // this thread's pairs sort ascending
+            if (j == 1) {
+                const bool sw = up == cr_lt(kh[1], kl[1], kr[1], kh[0], kl[0], kr[0]);
+                const uint64_t h0 = kh[0], l0 = kl[0];
+                const int32_t r0 = kr[0];
+                kh[0] = sw ? kh[1] : h0;
+                kl[0] = sw ? kl[1] : l0;
+                kr[0] = sw ? kr[1] : r0;
+                kh[1] = sw ? h0 : kh[1];
+                kl[1] = sw ? l0 : kl[1];
+                kr[1] = sw ? r0 : kr[1];
+            } else if (j < 128) {  // partner thread t ^ (j / 2), in this wave
+                const int lm = j >> 1;
+                const bool lower = (t & lm) == 0;
 #pragma unroll
-    for (int a = 0; a < E; ++a) {
-        const int i = c0 + lane * E + a;
+                for (int a = 0; a < 2; ++a) {
+                    const uint64_t ph = __shfl_xor(kh[a], lm), pl = __shfl_xor(kl[a], lm);
+                    const int32_t pr = __shfl_xor(kr[a], lm);
+                    cx3(kh[a], kl[a], kr[a], ph, pl, pr, lower == up);
+                }
+            } else {  // partner thread t ^ (j / 2) in another wave: through LDS
+                const bool lower = (t & (j >> 1)) == 0;
+                __syncthreads();
+#pragma unroll
+                for (int a = 0; a < 2; ++a) {
+                    s_h[2 * t + a] = kh[a];
+                    s_l[2 * t + a] = kl[a];
+                    s_r[2 * t + a] = kr[a];
+                }
+                __syncthreads();
+#pragma unroll
+                for (int a = 0; a < 2; ++a) {
+                    const int p = (2 * t + a) ^ j;
+                    cx3(kh[a], kl[a], kr[a], s_h[p], s_l[p], s_r[p], lower == up);
+                }
+            }
+        }
+    }
+#pragma unroll
+    for (int a = 0; a < 2; ++a) {
+        const int i = c0 + 2 * t + a;
         J.ccode[2 * i] = kh[a];
         J.ccode[2 * i + 1] = kl[a];
         J.crow[i] = kr[a];
@@ -1845,7 +1845,7 @@ void launch_ct_jobs(const CtJob *d_jobs, const CtJob *h_jobs, int32_t n, int32_t
         // across the chunks (round 4: one workgroup a tree sorting in LDS took 0.12 ms a round
         // at 256 seeds and 0.11 at 32 -- at 32 trees most CUs idle)
         const unsigned chunks = (unsigned)((mb + kCtChunk - 1) / kCtChunk);
-        hipLaunchKernelGGL(k_ct_csort, dim3((chunks + kCtChunkWaves - 1) / kCtChunkWaves, yn), dim3(64 * kCtChunkWaves),
+        hipLaunchKernelGGL(k_ct_csort, dim3(chunks, yn), dim3(kCtSortThreads),
                            0, stream, js);
         hipLaunchKernelGGL(k_ct_crank, dim3(b256, yn), dim3(256), 0, stream, js);
         hipLaunchKernelGGL(k_ct_locate, dim3(b256, yn), dim3(256), 0, stream, js);
