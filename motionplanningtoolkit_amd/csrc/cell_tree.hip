@@ -1426,8 +1426,7 @@ __device__ __forceinline__ void ct_walk(const CellTreeDev &T, const double *__re
     constexpr int G = NW * 8;        // lanes per query
     constexpr int kStack = NW * 8 * kCtMaxLevels;  // ~NW blocks of 7 a level, <= 10 levels (k_ct_levels): 5 KiB for NW = 8
     static_assert(G <= 64, "ballot bits per group");
-    __shared__ uint32_t s_code[BS / G][kStack];
-    __shared__ float s_lb[BS / G][kStack];
+    __shared__ uint2 s_stk[BS / G][kStack];  // (meta, lower bound's bits): one 8-byte access
     const int64_t t = blk * BS + threadIdx.x;
     const int64_t qi = t / G;
     const int sub = (int)(t % G);
@@ -1452,8 +1451,7 @@ __device__ __forceinline__ void ct_walk(const CellTreeDev &T, const double *__re
         float bdf = f32_up(bd);
         int sp = 1;
         if (sub == 0) {
-            s_code[grp][0] = ((gu32)T.nmeta)[*T.root];
-            s_lb[grp][0] = 0.0f;
+            s_stk[grp][0] = make_uint2(((gu32)T.nmeta)[*T.root], 0u);
         }
         __builtin_amdgcn_wave_barrier();
         const int base = (threadIdx.x & 63) & ~(G - 1);
@@ -1463,8 +1461,9 @@ __device__ __forceinline__ void ct_walk(const CellTreeDev &T, const double *__re
             uint32_t code = 0;
             float lbs = 0.0f;
             if (have) {
-                code = s_code[grp][sp - 1 - part];
-                lbs = s_lb[grp][sp - 1 - part];
+                const uint2 en = s_stk[grp][sp - 1 - part];
+                code = en.x;
+                lbs = __uint_as_float(en.y);
             }
             sp -= np;
             ++n_steps;
@@ -1522,8 +1521,7 @@ __device__ __forceinline__ void ct_walk(const CellTreeDev &T, const double *__re
                 const uint32_t pm = (uint32_t)(gm >> (part * 8)) & 0xffu;
                 const int r = __popc(pm & ((1u << ls) - 1u));
                 const int pos = sp + below + (c - 1 - r);
-                s_code[grp][pos] = child;
-                s_lb[grp][pos] = lbf;
+                s_stk[grp][pos] = make_uint2(child, __float_as_uint(lbf));
             }
             sp += __popcll(gm);
             __builtin_amdgcn_wave_barrier();
