@@ -124,7 +124,7 @@ struct CtJob {
     unsigned long long *hull_keys; // [kCtHull] (score key << 32 | row)
     double *hull_pts;
     int32_t *hull_ids;
-    unsigned long long *ibox;  // persistent box of the indexed points (order keys) [2][kCtMaxDim]
+    unsigned long long *ibox;  // persistent box of the indexed points (order keys) [2][kCtMaxDim]; rounds update dims 0..2 (the spread's)
     SpreadOut sp;
     unsigned long long *err;   // the engine's counters[6]: index errors (bounds the host broke)
 };

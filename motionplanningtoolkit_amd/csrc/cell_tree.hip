@@ -188,7 +188,6 @@ __global__ __launch_bounds__(64 * kCtWaves) void k_ct_ncodes(CtJobs js) {
     __syncthreads();
     const bool live = i < m;
     double x[D];
-    unsigned long long mn[D], mx[D];
     if (live) {
         const int64_t row = base + i;
         load_global<D>(J.pts + row * D, x);
@@ -197,30 +196,24 @@ __global__ __launch_bounds__(64 * kCtWaves) void k_ct_ncodes(CtJobs js) {
         J.ncode[2 * i] = h;
         J.ncode[2 * i + 1] = l;
         J.nrow[i] = (int32_t)row;
-#pragma unroll
-        for (int j = 0; j < D; ++j) mn[j] = mx[j] = okey(x[j]);
     } else {
 #pragma unroll
-        for (int j = 0; j < D; ++j) {
-            x[j] = 0.0;
-            mn[j] = ~0ull;
-            mx[j] = 0ull;
-        }
+        for (int j = 0; j < D; ++j) x[j] = 0.0;
     }
+    // the persistent box over dims 0..2 only: its one reader is k_ct_levels' copy for the
+    // engine's MPT_NN_AUTO spread, whose dims are the first two or three (rrt_engine grid_dims)
 #pragma unroll
-    for (int j = 0; j < D; ++j) {
+    for (int j = 0; j < (D < 3 ? D : 3); ++j) {
+        unsigned long long mn = live ? okey(x[j]) : ~0ull, mx = live ? okey(x[j]) : 0ull;
 #pragma unroll
         for (int off = 32; off > 0; off >>= 1) {
-            const unsigned long long omn = __shfl_xor(mn[j], off), omx = __shfl_xor(mx[j], off);
-            mn[j] = omn < mn[j] ? omn : mn[j];
-            mx[j] = omx > mx[j] ? omx : mx[j];
+            const unsigned long long omn = __shfl_xor(mn, off), omx = __shfl_xor(mx, off);
+            mn = omn < mn ? omn : mn;
+            mx = omx > mx ? omx : mx;
         }
-    }
-    if ((threadIdx.x & 63) == 0) {
-#pragma unroll
-        for (int j = 0; j < D; ++j) {
-            atomicMin(J.ibox + j, mn[j]);
-            atomicMax(J.ibox + kCtMaxDim + j, mx[j]);
+        if ((threadIdx.x & 63) == 0) {
+            atomicMin(J.ibox + j, mn);
+            atomicMax(J.ibox + kCtMaxDim + j, mx);
         }
     }
     hull_offer<D>(s_plan, x, live, base + (i & ~63), s_rows[threadIdx.x >> 6], J.hull_keys);
@@ -713,7 +706,8 @@ __device__ __forceinline__ int32_t ct_leaf_bucket(const CtJob &J, int64_t st, in
 // the leaf starting at split element e closes its bucket: count, box (from the rows), and the
 // directory (a new leaf: its entry; the split bucket: its record updated in place)
 template <int D>
-__device__ __forceinline__ void ct_leaf_close(const CtJob &J, int64_t e, int flag, int s, int32_t b, int len) {
+__device__ __forceinline__ void ct_leaf_close(const CtJob &J, int64_t e, int flag, int s, int32_t b, int len,
+                                              const double (*s_x)[D] = nullptr) {
     if (b >= J.bcap || len > kCtCap) {
         if (J.err) atomicAdd(J.err, 1ull);
         return;
@@ -737,7 +731,12 @@ __device__ __forceinline__ void ct_leaf_close(const CtJob &J, int64_t e, int fla
     for (int u = 0; u < kCtCap; ++u) {  // unrolled: the rows' loads are all in flight together
         if (u < len) {
             double x[D];
-            load_global<D>(J.pts + (int64_t)J.srow[e + u] * D, x);
+            if (s_x) {  // the leaf's rows as its elements' threads loaded them (LDS)
+#pragma unroll
+                for (int q = 0; q < D; ++q) x[q] = s_x[u][q];
+            } else {
+                load_global<D>(J.pts + (int64_t)J.srow[e + u] * D, x);
+            }
 #pragma unroll
             for (int q = 0; q < D; ++q) {
                 lo[q] = x[q] < lo[q] ? x[q] : lo[q];
@@ -761,6 +760,7 @@ template <int D>
 __global__ __launch_bounds__(256) void k_ct_split_fill(CtJobs js) {
     const CtJob J = CT_JOB(js);  // by value: the fields stay in registers across the stores
     __shared__ int8_t s_f[256 + 2 * kCtCap];  // flag of element c0 - kCtCap + v; -1 past the ends
+    __shared__ double s_x[256][D];             // the chunk's rows: a leaf inside it boxes from LDS
     const int64_t total = ct_scratch_total(J);
     for (int64_t c0 = (int64_t)blockIdx.x * 256; c0 < total; c0 += (int64_t)gridDim.x * 256) {
     for (int v = threadIdx.x; v < 256 + 2 * kCtCap; v += 256) {
@@ -770,8 +770,10 @@ __global__ __launch_bounds__(256) void k_ct_split_fill(CtJobs js) {
     __syncthreads();
     const int64_t e = c0 + threadIdx.x;
     const int s = e < total ? J.sseg[e] : -1;
+    const int ve = threadIdx.x + kCtCap;
+    int flag = 0, len = 0;
+    int32_t b = 0;
     if (s >= 0) {
-        const int ve = threadIdx.x + kCtCap;
         int vs = ve;  // the leaf's first element (a segment's first element starts a leaf)
         while (vs > 0 && s_f[vs] == 0) --vs;
         int64_t st = c0 - kCtCap + vs;
@@ -779,9 +781,9 @@ __global__ __launch_bounds__(256) void k_ct_split_fill(CtJobs js) {
             st = st < 0 ? 0 : st;
             while (st > 0 && J.slead[st] == 0) --st;
         }
-        const int flag = J.slead[st];
+        flag = J.slead[st];
         const int4 g = J.seg[s];
-        const int32_t b = ct_leaf_bucket(J, st, flag, g);
+        b = ct_leaf_bucket(J, st, flag, g);
         const int64_t u = e - st;
         if (b < J.bcap && u < kCtCap) {
             const int32_t row = J.srow[e];
@@ -789,19 +791,26 @@ __global__ __launch_bounds__(256) void k_ct_split_fill(CtJobs js) {
             load_global<D>(J.pts + (int64_t)row * D, x);
             const int64_t slot = (int64_t)b * kCtCap + u;
 #pragma unroll
-            for (int q = 0; q < D; ++q) J.bpts[slot * D + q] = x[q];
+            for (int q = 0; q < D; ++q) {
+                J.bpts[slot * D + q] = x[q];
+                s_x[threadIdx.x][q] = x[q];
+            }
             J.bids[slot] = row + 1;
             J.bcode[2 * slot] = J.scode[2 * e];
             J.bcode[2 * slot + 1] = J.scode[2 * e + 1];
         }
         if (e == st) {
             const int64_t end = (int64_t)g.w + g.y + g.z;
-            int len = 1;
+            len = 1;
             while (e + len < end && len <= kCtCap && s_f[ve + len] == 0) ++len;
-            ct_leaf_close<D>(J, e, flag, s, b, len);
         }
     }
-    __syncthreads();  // s_f reused by the next chunk
+    __syncthreads();  // s_x complete
+    if (len > 0) {  // this thread starts a leaf: close it
+        const bool in_chunk = threadIdx.x + len <= 256 && len <= kCtCap;
+        ct_leaf_close<D>(J, e, flag, s, b, len, in_chunk ? s_x + threadIdx.x : nullptr);
+    }
+    __syncthreads();  // s_f, s_x reused by the next chunk
     }
 }
 
