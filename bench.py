@@ -41,7 +41,13 @@ LDS_PEAK_GBS = 150_000.0  # MI355X_MICROARCH.md §LDS: ~150 TB/s aggregate ds_re
 
 def parse():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="ranks (one per GPU).  Without torchrun's WORLD_SIZE, N > 1 starts torch.distributed.run "
+                         "with N ranks as a child process (before any GPU call) and exits with its code; under "
+                         "torchrun it must equal WORLD_SIZE (default: WORLD_SIZE, else 1)")
+    ap.add_argument("--detail", default=os.path.join(REPO, "gpurun_out", "bench_detail.json"),
+                    help="where rank 0 writes the full line (every stage table, every leg); the printed line is "
+                         "the condensed one (empty: none)")
     ap.add_argument("--steps", type=int, default=30)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--batch", type=int, default=65536, help="extensions per round (K)")
@@ -361,7 +367,7 @@ def stage_table(per_launch, cst, K, n0, d, pmax, geo, nn_mode, kernels, summ):
 # measured traffic per launch is summed (the collide chain runs once per collide sub-batch)
 JOINT_STAGE_KERNELS = {
     "sample": ["k_sample_jobs"],
-    "nn_build": ["k_ct_ncodes", "k_ct_csort", "k_ct_crank", "k_ct_locate", "k_ct_segments",
+    "nn_build": ["k_ct_reset", "k_ct_csort", "k_ct_crank", "k_ct_locate", "k_ct_segments",
                  "k_ct_apply", "k_ct_split_", "k_ct_dmerge", "k_ct_lflags", "k_ct_lgroup", "k_ct_levels"],
     "nn_query": ["k_ct_nn1_jobs"],
     "steer": ["k_steer_jobs"],
@@ -419,9 +425,23 @@ def joint_stage_table(times, c, K, nj, n_tot, d, pmax, geo, summ):
     return stages
 
 
+def round_roof(stages, ms):
+    """The whole round against the HBM roof: every stage's compulsory bytes (and, where every
+    stage has a PMC row, its measured traffic) over the round's wall time per step."""
+    if not stages or ms <= 0:
+        return None
+    t = ms * 1e-3
+    b = sum(st["compulsory_bytes"] for st in stages.values())
+    out = {"ms": round(ms, 4), "compulsory_bytes": int(b), "frac_hbm_compulsory": round(b / t / 1e9 / HBM_PEAK_GBS, 4)}
+    tr = [st.get("traffic") for st in stages.values()]
+    if all(x is not None for x in tr):
+        out.update({"traffic": int(sum(tr)), "frac_hbm_measured": round(sum(tr) / t / 1e9 / HBM_PEAK_GBS, 4)})
+    return out
+
+
 def roofline_of(stages, dominant, work, summ_path):
     """The contract's roofline object for the dominant stage: HBM-bound unless its FP64
-    fraction is the larger one (then `mfma` = the FP64 VALU roof; no MFMA: FCL's operation
+    fraction is the larger one (then `fp64_valu` = the FP64 VALU roof; no MFMA: FCL's operation
     order is scalar FP64)."""
     if not stages or dominant not in stages:
         return {"bound": "hbm", "achieved": None, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": None, "traffic": None,
@@ -433,7 +453,7 @@ def roofline_of(stages, dominant, work, summ_path):
            "kernel": st["kernel"], "stage": dominant, "ms_per_launch": st["ms"],
            "algorithmic_bytes": st["compulsory_bytes"], "pmc_source": summ_path}
     if st.get("frac_fp64", 0.0) > max(st["frac_hbm_compulsory"], st.get("frac_hbm_measured") or 0.0):
-        out.update({"bound": "mfma", "achieved": st["fp64_tflops"], "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
+        out.update({"bound": "fp64_valu", "achieved": st["fp64_tflops"], "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
                     "frac": st["frac_fp64"], "note": "FP64 VALU roof (FCL's scalar operation order; no MFMA)"})
     out["definition"] = ("achieved = compulsory bytes (each input and output of the launch once) / hipEvent time; "
                          "traffic = measured HBM bytes per launch (2*FETCH_SIZE + WRITE_SIZE, rocprofv3); "
@@ -642,6 +662,7 @@ def run_seeds(args, world, rank, dist, torch, mpt, multiseed, scenes):
         roof = roofline_of(stages, dom, dict(agg, seeds_in_group=nj), summ_path)
         if scale is not None:
             roof["stage_time_scale"] = round(scale, 4)
+        roof["round"] = round_roof(stages, 1e3 * elapsed / args.steps)
     import hashlib
 
     all_digest = hashlib.sha256("".join(digests[i] for i in sorted(digests)).encode()).hexdigest()
@@ -691,20 +712,24 @@ VARIANTS = {
     "snake": ("bench.py", ["--workload", "snake", "--steps", "10", "--warmup", "3"]),
     "seeds=32": ("bench.py", ["--seeds", "32"] + _C5),
     "seeds=256": ("bench.py", ["--seeds", "256"] + _C5),
-    "prm": ("scripts/bench_prm.py", ["--reps", "3"]),
+    "prm": ("scripts/bench_prm.py", ["--reps", "3", "--bounds", "rooms"]),
     "distance": ("scripts/bench_distance.py", ["--steps", "10", "--warmup", "3"]),
 }
 
 
-def run_variants():
+def run_variants(detail=None):
     """Each leg's line (no CPU baseline, no nested legs), condensed: value, ms_per_step, the
     dominant stage's roofline, every stage's time and fractions, and (config 5) the seeds
-    digest and from-scratch time; a leg that fails reports its error instead."""
+    digest and from-scratch time; a leg that fails reports its error instead.  A bench.py leg
+    writes its full line to a detail file of its own, which is what is condensed here."""
     out = {}
+    ddir = os.path.dirname(detail) if detail else os.path.join(os.environ.get("TMPDIR", "/tmp"), f"mpt_{os.getpid()}")
     for name, (script, extra) in VARIANTS.items():
         cmd = [sys.executable, os.path.join(REPO, script), "--no-cpu"] + extra
+        leg_detail = None
         if script == "bench.py":
-            cmd.append("--no-variants")
+            leg_detail = os.path.join(ddir, f"bench_detail_{name.replace('=', '')}.json")
+            cmd += ["--no-variants", "--detail", leg_detail]
         t0 = time.perf_counter()
         try:
             p = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=dict(os.environ))
@@ -713,12 +738,80 @@ def run_variants():
                 out[name] = {"error": f"rc={p.returncode}", "stderr_tail": p.stderr[-800:]}
                 continue
             d = json.loads(line[-1])
+            if leg_detail:
+                try:
+                    d = json.load(open(leg_detail))
+                except (OSError, ValueError):
+                    pass
         except subprocess.TimeoutExpired:
             out[name] = {"error": "timeout"}
             continue
         out[name] = condense(d)
         out[name]["leg_wall_s"] = round(time.perf_counter() - t0, 1)
     return out
+
+
+# ----------------------------------------------------------------------------- the printed line
+
+# The printed line stays well inside the driver's 8 KB stdout tail: every leg's value, time,
+# dominant roofline and digest; the full stage tables go to the detail file (--detail).
+ROOF_KEYS = ("bound", "achieved", "peak", "unit", "frac", "traffic", "traffic_over_compulsory", "frac_hbm_measured",
+             "kernel", "stage", "ms_per_launch", "algorithmic_bytes", "pmc_source", "stage_time_scale")
+LEG_ROOF_KEYS = ("bound", "achieved", "unit", "frac", "traffic_over_compulsory", "kernel", "ms_per_launch", "pmc_source")
+
+
+def compact_roof(roof, keys=ROOF_KEYS, stages_ms=True):
+    r = {k: roof[k] for k in keys if roof.get(k) is not None}
+    st = roof.get("stages") or {}
+    if stages_ms and st:
+        r["stages_ms"] = {s: v.get("ms_event_free", v.get("ms")) for s, v in st.items()}
+    if roof.get("round"):
+        r["round"] = roof["round"]
+    return r
+
+
+def compact_leg(leg):
+    if "error" in leg:
+        return {"error": leg["error"], "stderr_tail": (leg.get("stderr_tail") or "")[-300:]}
+    out = {k: leg[k] for k in ("value", "unit", "ms_per_step", "wall_ms", "steps", "warmup", "valid_fraction",
+                               "seeds_digest", "world_size", "leg_wall_s") if leg.get(k) is not None}
+    if leg.get("from_scratch"):
+        fs = leg["from_scratch"]
+        out["from_scratch"] = {"rounds": fs.get("rounds"), "wall_s": fs.get("wall_s"),
+                               "valid_per_s": fs.get("valid_per_s")}
+    cfg = leg.get("config") or {}
+    for k in ("bounds", "free_fraction", "edges"):
+        if k in cfg:
+            out[k] = cfg[k]
+    out["roofline"] = compact_roof(leg.get("roofline") or {}, LEG_ROOF_KEYS, stages_ms=False)
+    return out
+
+
+def compact_line(out, detail):
+    line = {k: v for k, v in out.items() if k not in ("roofline", "variants", "config5", "config2", "cpu_baseline",
+                                                       "kernel_ms_per_round", "from_scratch")}
+    line["roofline"] = compact_roof(out.get("roofline") or {})
+    if out.get("from_scratch"):
+        fs = out["from_scratch"]
+        line["from_scratch"] = {k: fs.get(k) for k in ("rounds", "wall_s", "valid_per_s")}
+    cb = out.get("cpu_baseline")
+    if cb:
+        line["cpu_baseline"] = {k: cb.get(k) for k in ("value", "unit", "cores", "kind", "sample", "cpu")}
+        line["cpu_baseline"]["single_core"] = (cb.get("single_core") or {}).get("value")
+        line["cpu_baseline"]["flann_rebuild_per_insert"] = (cb.get("flann_rebuild_per_insert") or {}).get("value")
+    elif "cpu_baseline" in out:
+        line["cpu_baseline"] = None
+    if out.get("config2"):
+        line["config2"] = compact_leg(out["config2"])
+    if out.get("config5"):
+        line["config5"] = {k: v for k, v in out["config5"].items() if k != "from_scratch"}
+        fs = out["config5"].get("from_scratch") or {}
+        line["config5"]["from_scratch_valid_per_s"] = fs.get("valid_per_s")
+    if out.get("variants"):
+        line["variants"] = {k: compact_leg(v) for k, v in out["variants"].items()}
+    if detail:
+        line["detail"] = os.path.relpath(detail, REPO) if detail.startswith(REPO) else detail
+    return line
 
 
 def condense(d):
@@ -762,11 +855,36 @@ def config5_summary(c5_256, c5_32=None):
 
 # ----------------------------------------------------------------------------- main
 
+def free_port():
+    import socket
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def spawn_ranks(n):
+    """`bench.py --gpus N` without torchrun: the same command under torch.distributed.run with N
+    ranks on this node (127.0.0.1), started as a child process -- nothing here has touched the
+    GPU yet -- whose exit code is returned."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(free_port()), os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.run(cmd, env=dict(os.environ)).returncode
+
+
 def main():
     args = parse()
+    ws = os.environ.get("WORLD_SIZE")
+    if ws is None and args.gpus is not None and args.gpus > 1:
+        sys.exit(spawn_ranks(args.gpus))
+    if ws is not None and args.gpus is not None and int(ws) != args.gpus:
+        sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={ws}")
     import torch
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    world = int(ws or "1")
+    args.gpus = world
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     # MPT_DIST_BACKEND=gloo + MPT_BENCH_DEVICE=0: several ranks on one GPU (the multi-rank path
@@ -798,17 +916,33 @@ def main():
         if world > 1:
             # BASELINE config 5 in the same torchrun world: args.c5_seeds seeds sharded
             # contiguously over the ranks (32 per GPU at 8 GPUs), strong scaling; its seeds
-            # digest equals the N = 1 run's (the seeds=256 leg) for the same rounds
+            # digest equals the N = 1 run's (the seeds=256 leg) for the same rounds.  At N > 1
+            # it is the line's top level (the north star's scaling claim is over independent
+            # seeds), config 2's weak-scaled number nested under `config2`
             a5 = argparse.Namespace(**vars(args))
             a5.seeds, a5.steps, a5.warmup = args.c5_seeds, args.c5_steps, args.c5_warmup
             c5 = run_seeds(a5, world, rank, dist, torch, mpt, multiseed, scenes)
             if out is not None:
-                out["config5"] = config5_summary(condense(c5) if c5 else None)
+                c2 = out
+                out = dict(c5)
+                out["config2"] = condense(c2)
+                out["config2"]["cpu_baseline"] = c2.get("cpu_baseline")
+                out["scaling_note"] = (
+                    f"top level: config 5 ({args.c5_seeds} seeds over {world} GPUs, strong scaling); compare with "
+                    "the N = 1 line's config5.value (the same seeds and rounds on one GPU); config2: one 100k-node "
+                    "tree a rank (weak scaling)")
         elif out is not None and not args.no_variants and args.workload == "blimp":
-            out["variants"] = run_variants()
+            out["variants"] = run_variants(args.detail)
             out["config5"] = config5_summary(out["variants"].get("seeds=256"), out["variants"].get("seeds=32"))
     if out is not None:
-        print(json.dumps(out))
+        if args.detail:
+            try:
+                os.makedirs(os.path.dirname(args.detail), exist_ok=True)
+                with open(args.detail, "w") as f:
+                    json.dump(out, f, indent=1)
+            except OSError:
+                pass
+        print(json.dumps(compact_line(out, args.detail)))
     if dist:
         dist.destroy_process_group()
 
@@ -894,6 +1028,7 @@ def run_tree(args, world, rank, dist, torch, mpt, multiseed, scenes):
     stages = stage_table(per_launch, cst, K, n0, d, eng.info()["pmax"], geometry(sc, env), nn_mode, kernels, summ)
     dominant = max(stages, key=lambda s: stages[s]["ms"]) if stages else None
     roof = roofline_of(stages, dominant, cst, summ_path)
+    roof["round"] = round_roof(stages, 1e3 * elapsed / steps)
 
     out = {
         "metric": "valid RRT edge extensions/sec (collision+NN) per node, 1/2/4/8 MI355X",

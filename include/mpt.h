@@ -202,7 +202,8 @@ mpt_status mpt_rrt_step(mpt_rrt *rrt, int32_t K, void *stream);
  * the Morton-tree NN and the engines share the env, the agent and every parameter but the
  * seed (and K is a multiple of 16), the whole round is a joint round on joint_stream: one
  * launch per stage (sample, incremental index build, NN, steer, collide, append) for all
- * engines, after the engines' streams and before their next work; an engine's last-round
+ * engines, after the engines' streams and before their next work (a joint round indexes trees
+ * of any size, so engines grown from their start states are joint from their first round); an engine's last-round
  * buffers (mpt_rrt_last_round / _last_poses) are then the joint state's, valid until the next
  * call on that joint stream (those two calls fail with MPT_ERR_INVALID once mpt_rrt_joint_release
  * or a larger joint round has freed the buffers; stage times of a joint round come from
@@ -220,7 +221,9 @@ mpt_status mpt_rrt_joint_nn_ms(float *ms);
 /* Release the joint state of joint_stream (job-table staging ring, events, shared sort
  * buffers), after synchronising on it.  Call before destroying or recycling a stream handle
  * that mpt_rrt_step_many used as its joint stream: a recycled handle would otherwise inherit
- * the old state.  No-op for a stream that holds none. */
+ * the old state.  No-op for a stream that holds none.  Must not run at the same time as an
+ * mpt_rrt_step_many on the same joint stream (another host thread's mpt_rrt_last_round /
+ * _last_poses hold the state's lock through their copies and are safe). */
 mpt_status mpt_rrt_joint_release(void *joint_stream);
 /* The last timed mpt_rrt_step_many on joint_stream: ms[0] = the joint tree build, ms[1] = the
  * joint NN launch (hipEvents on joint_stream).  Synchronises on it. */

@@ -682,6 +682,7 @@ int64_t collide_chunk_units(int32_t max_clusters) { return split_chunk_units(max
 
 void CollideScratch::ensure(int64_t n_units, int32_t max_clusters) {
     n_units = std::min<int64_t>(n_units, split_chunk_units(max_clusters));  // launch_collide_split runs chunks
+    const int64_t threads = n_units * (int64_t)(max_clusters > 0 ? max_clusters : 1);
     if (!ctl) {
         int dev = 0, cus = 256;
         if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
@@ -690,17 +691,35 @@ void CollideScratch::ensure(int64_t n_units, int32_t max_clusters) {
         // than 16 at the round-3 head)
         const int per_cu = 16;
         n_cwaves = cus * per_cu;
-        cand_cap = (int32_t)std::max<int64_t>(256, (int64_t)kCandCap * 16 / per_cu);
-        spill_cap = kSpillCap;
-        hip_check(hipMalloc(&cand, sizeof(Cand) * (size_t)n_cwaves * cand_cap), "alloc candidates");
         hip_check(hipMalloc(&cand_count, sizeof(uint32_t) * (size_t)n_cwaves), "alloc candidate counts");
-        hip_check(hipMalloc(&spill, sizeof(Cand) * (size_t)spill_cap), "alloc spill");
         hip_check(hipMalloc(&ctl, sizeof(uint32_t) * 8), "alloc collide ctl");
         hip_check(hipMemset(ctl, 0, sizeof(uint32_t) * 8), "zero collide ctl");
         // the null-stream memset is not ordered with the caller's (non-blocking) stream: wait
         // for it, or the first k_narrow / fused re-run may read stale overflow and spill counts
         hip_check(hipDeviceSynchronize(), "zero collide ctl sync");
         ctl_par = 0;
+    }
+    // Candidate segments and the spill list sized by the launch's (unit, cluster) threads: ~16
+    // candidates a thread of a k_cands wave's share (config 2 and the room: ~350 threads a wave,
+    // 154 / 1214 candidates on average), at most kCandCap; the spill list 2 a thread, at most
+    // kSpillCap.  An engine's own K = 4096 round then takes ~25 MiB instead of ~480 (config 5's
+    // per-engine rounds); what overflows still reaches the fused re-run, so sizes change speed only.
+    const int64_t per_wave = (threads + n_cwaves - 1) / n_cwaves;
+    int64_t want_cand = 512, want_spill = int64_t(1) << 18;
+    while (want_cand < 16 * per_wave && want_cand < kCandCap) want_cand <<= 1;
+    while (want_spill < 2 * threads && want_spill < kSpillCap) want_spill <<= 1;
+    if (want_cand > cand_cap || want_spill > spill_cap) {
+        hip_check(hipDeviceSynchronize(), "sync");  // the old segments may still be in use
+        if (want_cand > cand_cap) {
+            if (cand) hip_check(hipFree(cand), "hipFree");
+            cand_cap = (int32_t)want_cand;
+            hip_check(hipMalloc(&cand, sizeof(Cand) * (size_t)n_cwaves * cand_cap), "alloc candidates");
+        }
+        if (want_spill > spill_cap) {
+            if (spill) hip_check(hipFree(spill), "hipFree");
+            spill_cap = (int32_t)want_spill;
+            hip_check(hipMalloc(&spill, sizeof(Cand) * (size_t)spill_cap), "alloc spill");
+        }
     }
     const int64_t segs = (n_units * (int64_t)(max_clusters > 0 ? max_clusters : 1) + 63) / 64;
     if (segs > n_seg) {

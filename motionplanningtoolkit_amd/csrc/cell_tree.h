@@ -51,6 +51,11 @@ struct CtCounts {
     int32_t n_l3;
     int32_t n_scratch;   // this round's split elements (the split segments' old + new points)
     int64_t nidx;        // points indexed (rows [0, nidx) of the node array)
+    // the walk's first entries: the root's children (the root itself when it is a leaf), so a
+    // query's first step tests the root's grandchildren -- one walk step fewer (k_ct_levels)
+    uint32_t top[8];
+    int32_t n_top;
+    int32_t pad;
 };
 
 // What the walk reads.  The hierarchy's nodes, level after level: level 1 = one node per
@@ -64,6 +69,8 @@ struct CellTreeDev {
     int64_t n_bound;           // host bound of the directory size (grid sizes)
     const int64_t *n_dev;      // live node count (0: empty tree)
     const int32_t *root;       // the root node (in the tree's CtCounts)
+    const uint32_t *top;       // the walk's first entries (CtCounts top / n_top)
+    const int32_t *n_top;
     const uint32_t *nmeta;     // [nodes]
     const float *nbox;         // [nodes][2d] widened float bounds: lo then hi
     const double *bpts;        // [buckets][kCtCap][d]
@@ -81,6 +88,8 @@ struct CtJob {
     CtCounts *cnt;
     int32_t bcap;              // bucket / directory capacity
     int32_t mb;                // host bound of this round's new points (0 after a full rebuild)
+    int32_t reset;             // 1: start from an empty index (k_ct_reset), then insert rows [0, n) as new
+    int32_t pad_;
     // buckets
     double *bpts;
     int32_t *bids;
@@ -134,8 +143,11 @@ public:
     // reserve for up to cap points of dim d (allocates and synchronises: call before the rounds)
     void reserve(int64_t cap, int32_t d);
     // This round's job.  full: rebuild the buckets from every point now (launches on stream);
-    // else the rows [nidx, n) are inserted by launch_ct_jobs (at most kCtSeg of them: the
-    // caller's bound, checked on the device).  lo / hi: the sampling ranges, spatial: the
+    // a full rebuild of at most kCtSeg rows instead starts from an empty index and inserts them
+    // all as the round's new points (no launches here: launch_ct_jobs resets and inserts, so a
+    // joint build of many young trees is one launch per stage); else the rows [nidx, n) are
+    // inserted by launch_ct_jobs (at most kCtSeg of them: the caller's bound, checked on the
+    // device).  lo / hi: the sampling ranges, spatial: the
     // leading state dims the seed directions span.  dev() is valid once the jobs have run.
     // grow: nodes appended since the last build (the host's bound of the new points).
     CtJob prepare(const double *pts, int64_t n_upper, const int64_t *n_dev, int32_t d, const double *lo,
@@ -173,6 +185,7 @@ private:
     int32_t *fv0 = nullptr, *fv1 = nullptr, *fflag = nullptr, *fleaf = nullptr;
     void *ftemp = nullptr;
     size_t ftemp_bytes = 0;
+    void *slab = nullptr;  // every buffer above is carved from it
 };
 
 // the round's build of n trees of dim d (stream-ordered): insert the new points, merge the new

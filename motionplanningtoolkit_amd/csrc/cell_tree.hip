@@ -155,9 +155,13 @@ struct CtJobs {
 };
 #define CT_JOB(js) ((js).table ? (js).table[blockIdx.y] : (js).one)
 
+// this round's new points: the rows past the indexed count, at most the host's bound mb (the
+// grids are sized by it; a device count beyond it -- a host bound broken, reported by
+// k_ct_csort into counters[6] -- leaves the rest for the next round instead of indexing rows
+// no kernel coded)
 __device__ __forceinline__ int64_t ct_new_count(const CtJob &J) {
-    int64_t m = *J.T.n_dev - J.cnt->nidx;
-    return m < 0 ? 0 : (m > kCtSeg ? kCtSeg : m);
+    const int64_t m = *J.T.n_dev - J.cnt->nidx, cap = J.mb < kCtSeg ? J.mb : kCtSeg;
+    return m < 0 ? 0 : (m > cap ? cap : m);
 }
 
 constexpr uint32_t kCtLeafBit = 0x80000000u;
@@ -169,55 +173,6 @@ __device__ __forceinline__ uint32_t inner_code(int64_t first, int32_t count) {
 }
 
 // ---- a round's new points ----
-
-// codes and rows of the new points [nidx, n) in row order, their box into ibox, their offers
-// to the seed slots
-template <int D>
-__global__ __launch_bounds__(64 * kCtWaves) void k_ct_ncodes(CtJobs js) {
-    __shared__ CtPlan s_plan;
-    __shared__ double s_rows[kCtWaves][64][D];
-    const CtJob J = CT_JOB(js);  // by value: the fields stay in registers across the stores
-    const int64_t base = J.cnt->nidx, mraw = *J.T.n_dev - base;
-    if ((mraw > kCtSeg || mraw > J.mb) && blockIdx.x == 0 && threadIdx.x == 0 && J.err)
-        atomicAdd(J.err, 1ull);  // the host's bound broken
-    const int64_t m = ct_new_count(J);
-    const int i = (int)blockIdx.x * (int)blockDim.x + (int)threadIdx.x;
-    if ((int64_t)blockIdx.x * blockDim.x >= m) return;  // block-uniform
-    for (int w = threadIdx.x; w < (int)(sizeof(CtPlan) / 4); w += blockDim.x)
-        reinterpret_cast<uint32_t *>(&s_plan)[w] = reinterpret_cast<const uint32_t *>(J.plan)[w];
-    __syncthreads();
-    const bool live = i < m;
-    double x[D];
-    if (live) {
-        const int64_t row = base + i;
-        load_global<D>(J.pts + row * D, x);
-        uint64_t h, l;
-        ct_code<D>(s_plan, x, h, l);
-        J.ncode[2 * i] = h;
-        J.ncode[2 * i + 1] = l;
-        J.nrow[i] = (int32_t)row;
-    } else {
-#pragma unroll
-        for (int j = 0; j < D; ++j) x[j] = 0.0;
-    }
-    // the persistent box over dims 0..2 only: its one reader is k_ct_levels' copy for the
-    // engine's MPT_NN_AUTO spread, whose dims are the first two or three (rrt_engine grid_dims)
-#pragma unroll
-    for (int j = 0; j < (D < 3 ? D : 3); ++j) {
-        unsigned long long mn = live ? okey(x[j]) : ~0ull, mx = live ? okey(x[j]) : 0ull;
-#pragma unroll
-        for (int off = 32; off > 0; off >>= 1) {
-            const unsigned long long omn = __shfl_xor(mn, off), omx = __shfl_xor(mx, off);
-            mn = omn < mn ? omn : mn;
-            mx = omx > mx ? omx : mx;
-        }
-        if ((threadIdx.x & 63) == 0) {
-            atomicMin(J.ibox + j, mn);
-            atomicMax(J.ibox + kCtMaxDim + j, mx);
-        }
-    }
-    hull_offer<D>(s_plan, x, live, base + (i & ~63), s_rows[threadIdx.x >> 6], J.hull_keys);
-}
 
 // (code, row) compare-exchange by selects (no divergent branches)
 __device__ __forceinline__ void cx3(uint64_t &h, uint64_t &l, int32_t &r, uint64_t ph, uint64_t pl, int32_t pr,
@@ -237,23 +192,72 @@ constexpr int kCtChunk = 512;
 constexpr int kCtChunks = kCtSeg / kCtChunk;
 constexpr int kCtSortThreads = kCtChunk / 2;
 
+// Codes and the chunk sort in one launch: a 256-thread workgroup takes 512 consecutive new
+// rows, two a thread -- rows c0 + a * 256 + t (consecutive within a wave: coalesced row loads,
+// the persistent box and the seed offers per wave of 64 rows) -- codes them, and sorts the
+// chunk's (code, row) pairs in LDS and registers (round 4: a launch of its own for the codes
+// wrote and re-read every pair).
+template <int D>
 __global__ __launch_bounds__(kCtSortThreads) void k_ct_csort(CtJobs js) {
     const CtJob J = CT_JOB(js);  // by value: the fields stay in registers across the stores
+    __shared__ CtPlan s_plan;
     __shared__ uint64_t s_h[kCtChunk], s_l[kCtChunk];
     __shared__ int32_t s_r[kCtChunk];
+    __shared__ double s_rows[kCtSortThreads / 64][64][D];
+    const int64_t base = J.cnt->nidx, mraw = *J.T.n_dev - base;
+    if ((mraw > kCtSeg || mraw > J.mb) && blockIdx.x == 0 && threadIdx.x == 0 && J.err)
+        atomicAdd(J.err, 1ull);  // the host's bound broken
     const int64_t m = ct_new_count(J);
     const int c0 = (int)blockIdx.x * kCtChunk;
     if (c0 >= m) return;  // block-uniform
     const int t = threadIdx.x;
+    for (int w = t; w < (int)(sizeof(CtPlan) / 4); w += blockDim.x)
+        reinterpret_cast<uint32_t *>(&s_plan)[w] = reinterpret_cast<const uint32_t *>(J.plan)[w];
+    __syncthreads();
+#pragma unroll
+    for (int a = 0; a < 2; ++a) {
+        const int i = c0 + a * kCtSortThreads + t;
+        const bool live = i < m;
+        double x[D];
+        uint64_t h = ~0ull, l = ~0ull;  // padding sorts last (codes use 126 bits)
+        if (live) {
+            load_global<D>(J.pts + (base + i) * D, x);
+            ct_code<D>(s_plan, x, h, l);
+        } else {
+#pragma unroll
+            for (int j = 0; j < D; ++j) x[j] = 0.0;
+        }
+        const int e = a * kCtSortThreads + t;
+        s_h[e] = h;
+        s_l[e] = l;
+        s_r[e] = live ? (int32_t)(base + i) : 0x7fffffff;
+        // the persistent box over dims 0..2 only: its one reader is k_ct_levels' copy for the
+        // engine's MPT_NN_AUTO spread, whose dims are the first two or three (rrt_engine grid_dims)
+#pragma unroll
+        for (int j = 0; j < (D < 3 ? D : 3); ++j) {
+            unsigned long long mn = live ? okey(x[j]) : ~0ull, mx = live ? okey(x[j]) : 0ull;
+#pragma unroll
+            for (int off = 32; off > 0; off >>= 1) {
+                const unsigned long long omn = __shfl_xor(mn, off), omx = __shfl_xor(mx, off);
+                mn = omn < mn ? omn : mn;
+                mx = omx > mx ? omx : mx;
+            }
+            if ((t & 63) == 0 && mn != ~0ull) {
+                atomicMin(J.ibox + j, mn);
+                atomicMax(J.ibox + kCtMaxDim + j, mx);
+            }
+        }
+        if ((int64_t)(c0 + a * kCtSortThreads + (t & ~63)) < m)  // wave-uniform: a live row in the wave
+            hull_offer<D>(s_plan, x, live, base + (i & ~63), s_rows[t >> 6], J.hull_keys);
+    }
+    __syncthreads();
     uint64_t kh[2], kl[2];
     int32_t kr[2];
 #pragma unroll
     for (int a = 0; a < 2; ++a) {
-        const int i = c0 + 2 * t + a;
-        const bool live = i < m;
-        kh[a] = live ? J.ncode[2 * i] : ~0ull;  // padding sorts last (codes use 126 bits)
-        kl[a] = live ? J.ncode[2 * i + 1] : ~0ull;
-        kr[a] = live ? J.nrow[i] : 0x7fffffff;
+        kh[a] = s_h[2 * t + a];
+        kl[a] = s_l[2 * t + a];
+        kr[a] = s_r[2 * t + a];
     }
 #pragma unroll 1
     for (int k = 2; k <= kCtChunk; k <<= 1) {
@@ -1115,6 +1119,12 @@ __global__ __launch_bounds__(kCtLevelThreads) void k_ct_levels(CtJobs js) {
         if (k == 0) J.hull_ids[h] = key ? (int32_t)row + 1 : 0;
     }
     __syncthreads();
+    if (t < 8) {  // the walk's first entries: the root's children, or the root when it is a leaf
+        const uint32_t rm = J.nmeta[ls];
+        const int nc = (rm & kCtLeafBit) ? 1 : (int)((rm >> 28) & 7u) + 1;
+        if (t < nc) J.cnt->top[t] = (rm & kCtLeafBit) ? rm : J.nmeta[(int64_t)(rm & 0x0fffffffu) + t];
+        if (t == 0) J.cnt->n_top = nc;
+    }
     if (t != 0) return;
     CtCounts *c = J.cnt;
     const int32_t nn = c->n_new_dir;
@@ -1132,6 +1142,35 @@ __global__ __launch_bounds__(kCtLevelThreads) void k_ct_levels(CtJobs js) {
             sp.host_out[3 + j] = j < sp.gd ? J.ibox[kCtMaxDim + sp.dims[j]] : 0ull;
         }
         __threadfence_system();
+    }
+}
+
+// An empty index (one empty bucket at code 0, as k_ct_bulk_fill makes for an empty tree), the
+// seeds and the persistent box cleared: the round then inserts rows [0, n) as new points.
+// One workgroup a job; jobs without the reset flag return.
+__global__ __launch_bounds__(64) void k_ct_reset(CtJobs js) {
+    const CtJob J = CT_JOB(js);
+    if (!J.reset) return;
+    const int t = threadIdx.x;
+    const int d = J.T.d;
+    J.hull_keys[t] = 0ull;  // kCtHull = 64 slots
+    if (t < 2 * kCtMaxDim) J.ibox[t] = t < kCtMaxDim ? ~0ull : 0ull;
+    if (t < 2 * d) {
+        const float v = t < d ? __builtin_huge_valf() : -__builtin_huge_valf();
+        J.bbox[t] = v;
+        J.obox[t] = v;
+    }
+    if (t == 0) {
+        J.bcnt[0] = 0;
+        uint64_t *dc = const_cast<uint64_t *>(J.odir_code);
+        dc[0] = 0;
+        dc[1] = 0;
+        J.ometa[0] = leaf_code(0, 1);  // the bucket's count is 0: the first round appends or splits it
+        CtCounts *c = J.cnt;
+        c->n_dir = c->n_buckets = 1;
+        c->n_seg = c->n_new_dir = c->n_scratch = 0;
+        c->root = 0;
+        c->nidx = 0;
     }
 }
 
@@ -1373,11 +1412,43 @@ __device__ __forceinline__ void nn_take(double &bd, int32_t &bi, double od, int3
     bd = t ? od : bd;
     bi = t ? oi : bi;
 }
+// The least u32 of the wave, uniform: the row butterflies (DPP), then rows 0 -> 1 and 2 -> 3
+// (row_bcast:15) and rows 0..1 -> 2..3 (row_bcast:31), so lane 63 holds it (7 instructions, no
+// LDS)
+constexpr int kDppBcast15 = 0x142;
+constexpr int kDppBcast31 = 0x143;
+__device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
+    v = min(v, dpp_u<kDppXor1>(v));
+    v = min(v, dpp_u<kDppXor2>(v));
+    v = min(v, dpp_u<kDppRev8>(v));
+    v = min(v, dpp_u<kDppRev16>(v));
+    v = min(v, (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, kDppBcast15, 0xa, 0xf, false));
+    v = min(v, (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, kDppBcast31, 0xc, 0xf, false));
+    return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
+}
+
 // The best (d2, id) of each G-lane group, in every lane of it (nn_better's order): the least
-// d2 first (one double a level), then the least id among the lanes holding it -- read from the
-// one such lane of a 64-lane group when it is alone (the common case), else reduced.
+// d2 first, then the least id among the lanes holding it -- read from the one such lane of a
+// 64-lane group when it is alone (the common case), else reduced.  A 64-lane group compares
+// the d2 bit patterns (non-negative doubles order as their bits): the least high word, then
+// the least low word among the lanes holding it, as two wave minimums of u32.
 template <int G>
 __device__ __forceinline__ void best_group(double &bd, int32_t &bi) {
+    if constexpr (G == 64) {
+        const uint32_t hi = (uint32_t)__double2hiint(bd), lo = (uint32_t)__double2loint(bd);
+        const uint32_t mh = wave_min_u32(hi);
+        const uint32_t ml = wave_min_u32(hi == mh ? lo : 0xffffffffu);
+        const bool win = (hi == mh) & (lo == ml);
+        bd = __hiloint2double((int)mh, (int)ml);
+        const uint64_t wm = __ballot(win);
+        if (__popcll(wm) == 1) {
+            bi = __builtin_amdgcn_readlane(bi, __ffsll((long long)wm) - 1);
+        } else {
+            const uint32_t c = win ? (uint32_t)bi ^ 0x80000000u : 0xffffffffu;  // signed order as u32
+            bi = (int32_t)(wave_min_u32(c) ^ 0x80000000u);
+        }
+        return;
+    }
     double m = bd;
     each_level<G / 2>([&](auto L) {
         const double o = xchg_d<decltype(L)::value>(m);
@@ -1385,13 +1456,6 @@ __device__ __forceinline__ void best_group(double &bd, int32_t &bi) {
     });
     const bool win = bd == m;
     bd = m;
-    if constexpr (G == 64) {
-        const uint64_t wm = __ballot(win);
-        if (__popcll(wm) == 1) {
-            bi = __builtin_amdgcn_readlane(bi, __ffsll((long long)wm) - 1);
-            return;
-        }
-    }
     int32_t c = win ? bi : 0x7fffffff;
     each_level<G / 2>([&](auto L) {
         const int32_t o = (int32_t)xchg<decltype(L)::value>((uint32_t)c);
@@ -1456,12 +1520,13 @@ __device__ __forceinline__ void ct_walk(const CellTreeDev &T, const double *__re
     int32_t bi = -1;
     uint32_t n_pts = 0, n_box = 0, n_steps = 1;  // the seeds' step
     if (*T.n_dev > 0) {
+        // the first entries (the root's children) loaded with the seeds: no dependent load
+        const int n_top = *(const __attribute__((address_space(1))) int32_t *)T.n_top;
+        const uint32_t top = sub < 8 ? ((gu32)T.top)[sub] : 0u;
         ct_seed<D, G>(T, qq, sub, bd, bi, n_pts);
         float bdf = f32_up(bd);
-        int sp = 1;
-        if (sub == 0) {
-            s_stk[grp][0] = make_uint2(((gu32)T.nmeta)[*T.root], 0u);
-        }
+        int sp = n_top;
+        if (sub < n_top) s_stk[grp][n_top - 1 - sub] = make_uint2(top, 0u);  // child 0 on top
         __builtin_amdgcn_wave_barrier();
         const int base = (threadIdx.x & 63) & ~(G - 1);
         while (sp > 0) {
@@ -1652,11 +1717,8 @@ CtPlan make_ct_plan(int32_t d, const double *lo, const double *hi, int32_t spati
 }
 
 void CellTree::release() {
-    void *ps[] = {plan, cnt, bpts, bids, bcnt, bcode, bbox, nbox[0], nbox[1], nmeta[0], nmeta[1], ucode, lflag, lcount, dir_code[0], dir_code[1],
-                  ncode, ccode, scode, edir_code, nrow, crow, npos, nseg, seg_pos, seg_first, srow, sseg, slead, srank, edir_bk,
-                  edir_pos, seg, hull_keys, ibox, hull_pts, hull_ids, fhi, flo, fk0, fk1, fv0, fv1, fflag, fleaf, ftemp};
-    for (void *p : ps)
-        if (p) (void)hipFree(p);
+    if (slab) (void)hipFree(slab);
+    slab = nullptr;
 }
 
 CellTree::~CellTree() { release(); }
@@ -1673,7 +1735,10 @@ void CellTree::reserve(int64_t c, int32_t d) {
     dim = d;
     bcap = (int32_t)(c + 1);  // every bucket holds at least one point, an empty tree one bucket
     const int64_t nodes = 2 * (int64_t)bcap + 64;  // each level at most half the one below, or runs of 8
-    auto al = [](void **p, size_t bytes, const char *what) { hip_check(hipMalloc(p, std::max<size_t>(bytes, 16)), what); };
+    // every buffer carved from one allocation (one hipMalloc an engine, not ~45: config 5
+    // reserves 256 trees in its first round)
+    std::vector<std::pair<void **, size_t>> bufs;
+    auto al = [&](void **p, size_t bytes, const char *) { bufs.emplace_back(p, std::max<size_t>(bytes, 16)); };
     al((void **)&plan, sizeof(CtPlan), "ct plan");
     al((void **)&cnt, sizeof(CtCounts), "ct counts");
     al((void **)&bpts, sizeof(double) * bcap * kCtCap * d, "ct bucket rows");
@@ -1719,6 +1784,14 @@ void CellTree::reserve(int64_t c, int32_t d) {
     hip_check(hipcub::DeviceScan::ExclusiveSum(nullptr, tb2, fflag, fleaf, (int)c), "ct scan size");
     ftemp_bytes = std::max(tb, tb2);
     al(&ftemp, ftemp_bytes, "ct sort temp");
+    size_t total = 0;
+    for (auto &b : bufs) total += (b.second + 255) & ~size_t(255);
+    hip_check(hipMalloc(&slab, total), "ct index");
+    char *at = static_cast<char *>(slab);
+    for (auto &b : bufs) {
+        *b.first = at;
+        at += (b.second + 255) & ~size_t(255);
+    }
     hip_check(hipMemset(cnt, 0, sizeof(CtCounts)), "ct counts zero");
     hip_check(hipDeviceSynchronize(), "ct init sync");  // the null stream vs the caller's stream
 }
@@ -1741,6 +1814,11 @@ CtJob CellTree::prepare(const double *pts, int64_t n_upper, const int64_t *n_dev
         full = true;
     }
     const int old = cur, nw = cur ^ 1;
+    const bool reset = full && n_upper <= kCtSeg;
+    if (reset) {
+        full = false;
+        grow = n_upper;
+    }
     if (full) {
         // every point: box, codes and seed offers, a two-pass stable sort by (code, row), the
         // leaf rule, the leaves' ranks, buckets and directory (into the round's old directory)
@@ -1772,6 +1850,8 @@ CtJob CellTree::prepare(const double *pts, int64_t n_upper, const int64_t *n_dev
     t.n_bound = std::max<int64_t>(std::min<int64_t>(n_upper, bcap), 1);
     t.n_dev = n_dev;
     t.root = &cnt->root;
+    t.top = cnt->top;
+    t.n_top = &cnt->n_top;
     t.nmeta = nmeta[nw];
     t.nbox = nbox[nw];
     t.bpts = bpts;
@@ -1787,6 +1867,7 @@ CtJob CellTree::prepare(const double *pts, int64_t n_upper, const int64_t *n_dev
     J.cnt = cnt;
     J.bcap = bcap;
     J.mb = full ? 0 : (int32_t)std::min<int64_t>(std::max<int64_t>(grow, 0), kCtSeg);
+    J.reset = reset ? 1 : 0;
     J.bpts = bpts;
     J.bids = bids;
     J.bcode = bcode;
@@ -1840,20 +1921,24 @@ void launch_ct_jobs(const CtJob *d_jobs, const CtJob *h_jobs, int32_t n, int32_t
     }
     auto by_d = [&](auto k3, auto k7, auto k15) { return d == 3 ? k3 : d == 7 ? k7 : k15; };
     const unsigned yn = (unsigned)n;
+    bool any_reset = false;
+    for (int32_t j = 0; j < n; ++j) any_reset = any_reset || h_jobs[j].reset;
+    if (any_reset) {
+        hipLaunchKernelGGL(k_ct_reset, dim3(1, yn), dim3(64), 0, stream, js);
+        hip_check(hipGetLastError(), "k_ct_reset");
+    }
     if (mb > 0) {
         const unsigned b256 = (unsigned)((mb + 255) / 256);
         // (round 4: these four fused into one workgroup a tree ran 0.30-0.40 ms a round at 256
         // seeds and 0.28-0.36 at 32, against 0.27 and 0.15 as separate launches: the codes and
         // seed offers need the waves of many workgroups)
-        hipLaunchKernelGGL(by_d(k_ct_ncodes<3>, k_ct_ncodes<7>, k_ct_ncodes<15>), dim3(b256, yn), dim3(64 * kCtWaves), 0,
-                           stream, js);
-        hip_check(hipGetLastError(), "k_ct_ncodes");
-        // the sort over many CUs: chunks of 512 sorted by a wave each, then every pair's rank
-        // across the chunks (round 4: one workgroup a tree sorting in LDS took 0.12 ms a round
-        // at 256 seeds and 0.11 at 32 -- at 32 trees most CUs idle)
+        // codes and the sort over many CUs: chunks of 512 coded and sorted by a workgroup each,
+        // then every pair's rank across the chunks (round 4: one workgroup a tree sorting in LDS
+        // took 0.12 ms a round at 256 seeds and 0.11 at 32 -- at 32 trees most CUs idle)
         const unsigned chunks = (unsigned)((mb + kCtChunk - 1) / kCtChunk);
-        hipLaunchKernelGGL(k_ct_csort, dim3(chunks, yn), dim3(kCtSortThreads),
+        hipLaunchKernelGGL(by_d(k_ct_csort<3>, k_ct_csort<7>, k_ct_csort<15>), dim3(chunks, yn), dim3(kCtSortThreads),
                            0, stream, js);
+        hip_check(hipGetLastError(), "k_ct_csort");
         hipLaunchKernelGGL(k_ct_crank, dim3(b256, yn), dim3(256), 0, stream, js);
         hipLaunchKernelGGL(k_ct_locate, dim3(b256, yn), dim3(256), 0, stream, js);
         hipLaunchKernelGGL(k_ct_segments, dim3(1, yn), dim3(kCtSegThreads), 0, stream, js);

@@ -245,6 +245,12 @@ void launch_collide_sweep(const EnvDev &env, const AgentDev *d_link, int32_t n_c
                           const int64_t *poff, int64_t E, uint8_t *verdict, unsigned long long *stats,
                           hipStream_t stream);
 
+// The same for PRM roadmap edges whose poses the sweep generates in-kernel from the milestones'
+// keys (prm_edges.h PrmEdges; no pose array).
+struct PrmEdges;
+void launch_collide_sweep_prm(const EnvDev &env, const AgentDev *d_link, int32_t n_clusters, const PrmEdges &edges,
+                              int64_t E, uint8_t *verdict, unsigned long long *stats, hipStream_t stream);
+
 // Self-collision (self.hip, MeshHandler::isInCollision's checkSelfCollision branch): units
 // are (pose, link pair j < k); verdict[pose_edge[p]] = 1 when links j and k of pose p touch.
 void launch_self_collide(const AgentDev *d_links, int32_t L, const double *poses, const int32_t *pose_edge,

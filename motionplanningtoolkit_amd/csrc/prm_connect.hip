@@ -26,6 +26,7 @@
 #include "../../include/mpt.h"
 #include "mpt_internal.h"
 #include "point_tree.h"
+#include "prm_edges.h"
 
 namespace mpt {
 const EnvDev &env_dev(const mpt_env *e);
@@ -61,81 +62,35 @@ __global__ void k_sort_segments(const int64_t *__restrict__ off, int64_t nq, int
     for (int64_t i = a; i < b; ++i) src[i] = (int32_t)q;
 }
 
-// Omnidirectional::steer(start, goal, 1000) (agents/omnidirectional.hpp:186-198, prm.hpp:366)
-__device__ __forceinline__ void steer_end(const double *s, const double *g, double *e) {
-    const double dx = g[0] - s[0], dy = g[1] - s[1], dz = g[2] - s[2];
-    const double dist = sqrt(dx * dx + dy * dy + dz * dz);
-    double fraction = 1000.0 / dist;
-    if (fraction > 1) fraction = 1;
-    e[0] = s[0] + dx * fraction;
-    e[1] = s[1] + dy * fraction;
-    e[2] = s[2] + dz * fraction;
-}
-
-// Omnidirectional::getPoses count (agents/omnidirectional.hpp:202-247)
-__device__ __forceinline__ int64_t omni_pose_count(const double *s, const double *e, double dt, double &dist,
-                                                   unsigned &it) {
-    const double dx = e[0] - s[0], dy = e[1] - s[1], dz = e[2] - s[2];
-    dist = sqrt(dx * dx + dy * dy + dz * dz);
-    const double q = dist / dt;
-    it = (q >= 4294967296.0 || !(q >= 0)) ? 0u : (unsigned)q;
-    if (it < 1) return 2;
-    return (int64_t)it + (((double)it * dt < dist) ? 1 : 0);
-}
-
-__global__ void k_edge_pose_count(const double *__restrict__ keys, const int32_t *__restrict__ src,
-                                  const int32_t *__restrict__ nbr, int64_t E, double dt, int64_t *__restrict__ pc) {
+__global__ void k_edge_pose_count(PrmEdges P, int64_t E, int64_t *__restrict__ pc) {
     const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (e > E) return;
     if (e == E) {
         pc[e] = 0;
         return;
     }
-    const double *s = keys + (int64_t)src[e] * 3;
-    double end[3], dist;
-    unsigned it;
-    steer_end(s, keys + (int64_t)(nbr[e] - 1) * 3, end);
-    pc[e] = omni_pose_count(s, end, dt, dist, it);
+    const PrmEdge g = prm_edge(P, e);
+    pc[e] = g.it < 1 ? 2 : (int64_t)g.it + (g.tail ? 1 : 0);
 }
 
-__device__ __forceinline__ void put_pose(double *o, const double *cs, double x, double y, double z) {
-    const double c = cs[0], s = cs[1];
-    o[0] = c; o[1] = s; o[2] = 0.0;
-    o[3] = -s; o[4] = c; o[5] = 0.0;
-    o[6] = 0.0; o[7] = 0.0; o[8] = 1.0;
-    o[9] = x; o[10] = y; o[11] = z;
-}
-
-__global__ void k_edge_poses(const double *__restrict__ keys, const double *__restrict__ rot,
-                             const int32_t *__restrict__ src, const int32_t *__restrict__ nbr, int64_t E, double dt,
-                             const int64_t *__restrict__ poff, double *__restrict__ poses, int32_t *__restrict__ pose_edge) {
+// the pose array (mpt_set_collide_mode FUSED: the per-pose walk reads it; the sweep generates
+// the same poses in-kernel instead, sweep.hip k_sweep_edge<PrmSrc>)
+__global__ void k_edge_poses(PrmEdges P, int64_t E, const int64_t *__restrict__ poff, double *__restrict__ poses,
+                             int32_t *__restrict__ pose_edge) {
     const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (e >= E) return;
-    const double *s = keys + (int64_t)src[e] * 3;
-    const double *cs = rot + (int64_t)src[e] * 2;
-    double end[3], dist;
-    unsigned it;
-    steer_end(s, keys + (int64_t)(nbr[e] - 1) * 3, end);
-    (void)omni_pose_count(s, end, dt, dist, it);
+    const PrmEdge g = prm_edge(P, e);
     int64_t p = poff[e];
-    const double dx = end[0] - s[0], dy = end[1] - s[1], dz = end[2] - s[2];
-    if (it < 1) {
-        put_pose(poses + 12 * p, cs, s[0], s[1], s[2]);
+    g.each([&](const double *t) {
+        double *o = poses + 12 * p;
+#pragma unroll
+        for (int k = 0; k < 9; ++k) o[k] = g.R[k];
+        o[9] = t[0];
+        o[10] = t[1];
+        o[11] = t[2];
         pose_edge[p++] = (int32_t)e;
-        put_pose(poses + 12 * p, cs, end[0], end[1], end[2]);
-        pose_edge[p++] = (int32_t)e;
-        return;
-    }
-    const double step = dt / dist;
-    for (unsigned i = 0; i < it; ++i) {
-        const double st = step * (double)i;
-        put_pose(poses + 12 * p, cs, s[0] + st * dx, s[1] + st * dy, s[2] + st * dz);
-        pose_edge[p++] = (int32_t)e;
-    }
-    if ((double)it * dt < dist) {
-        put_pose(poses + 12 * p, cs, end[0], end[1], end[2]);
-        pose_edge[p++] = (int32_t)e;
-    }
+        return false;
+    });
 }
 
 template <class T>
@@ -254,20 +209,28 @@ extern "C" mpt_status mpt_prm_connect(const mpt_env *env, const mpt_agent *agent
             hip_check(hipGetLastError(), "k_sort_segments");
         }
         hip_check(hipEventRecord(ev[1], stream), "event");
-        // poses of every edge
+        // the edges' poses: the sweep generates them where it tests them (no pose array); the
+        // fused per-pose walk (mpt_set_collide_mode FUSED) and the work counters (the pose
+        // count) need the count scan, the fused walk the array
+        const bool sweep = collide_mode() != MPT_COLLIDE_FUSED;
+        const PrmEdges PE{d_keys, d_rot, d_src, d_nbr, cc_dt};
         int64_t P = 0;
-        int64_t *d_poff = S.poff.get(E + 1);
-        if (E > 0) {
-            hipLaunchKernelGGL(k_edge_pose_count, dim3((unsigned)((E + 1 + 255) / 256)), dim3(256), 0, stream, d_keys,
-                               d_src, d_nbr, E, cc_dt, d_poff);
+        int64_t *d_poff = nullptr;
+        double *d_poses = nullptr;
+        int32_t *d_pe = nullptr;
+        if (E > 0 && (!sweep || g_prm_stats_on)) {
+            d_poff = S.poff.get(E + 1);
+            hipLaunchKernelGGL(k_edge_pose_count, dim3((unsigned)((E + 1 + 255) / 256)), dim3(256), 0, stream, PE, E,
+                               d_poff);
             P = scan_total(d_poff, E + 1, S.temp, stream);
+            if (P >= (int64_t(1) << 31)) throw Error{MPT_ERR_CAPACITY, "too many edge poses"};
         }
-        if (P >= (int64_t(1) << 31)) throw Error{MPT_ERR_CAPACITY, "too many edge poses"};
-        double *d_poses = S.poses.get(P * 12);
-        int32_t *d_pe = S.pose_edge.get(P);
-        if (E > 0)
-            hipLaunchKernelGGL(k_edge_poses, dim3((unsigned)((E + 255) / 256)), dim3(256), 0, stream, d_keys, d_rot, d_src,
-                               d_nbr, E, cc_dt, d_poff, d_poses, d_pe);
+        if (E > 0 && !sweep) {
+            d_poses = S.poses.get(P * 12);
+            d_pe = S.pose_edge.get(P);
+            hipLaunchKernelGGL(k_edge_poses, dim3((unsigned)((E + 255) / 256)), dim3(256), 0, stream, PE, E, d_poff,
+                               d_poses, d_pe);
+        }
         hip_check(hipEventRecord(ev[2], stream), "event");
         // collision verdicts (the sweep path; mpt_set_collide_mode FUSED: the per-pose fused walk)
         uint8_t *d_v = S.verdict.get(E);
@@ -276,23 +239,14 @@ extern "C" mpt_status mpt_prm_connect(const mpt_env *env, const mpt_agent *agent
             AgentDev *d_link = S.link.get(1);
             const AgentDev ag = agent_dev(agent);
             hip_check(hipMemcpy(d_link, &ag, sizeof(AgentDev), hipMemcpyHostToDevice), "link");
-            CollideWork w{};
-            w.poses = d_poses;
-            w.pose_edge = d_pe;
-            w.pmax = 1;
-            w.L = 1;
-            w.n_units = P;
-            w.verdict = d_v;
             const int32_t mc = std::max(1, ag.n_clusters);
-            // the sweep collide (one launch over the edges' poses); mpt_set_collide_mode's
-            // FUSED: the one-kernel traversal
-            if (collide_mode() != MPT_COLLIDE_FUSED) {
+            if (sweep) {
                 unsigned long long *st = nullptr;
                 if (g_prm_stats_on) {
-                    st = reinterpret_cast<unsigned long long *>(S.temp.get(64) );
+                    st = reinterpret_cast<unsigned long long *>(S.temp.get(64));
                     hip_check(hipMemsetAsync(st, 0, sizeof(unsigned long long) * 4, stream), "stats zero");
                 }
-                launch_collide_sweep(env_dev(env), d_link, mc, d_poses, d_poff, E, d_v, st, stream);
+                launch_collide_sweep_prm(env_dev(env), d_link, mc, PE, E, d_v, st, stream);
                 if (st) {
                     unsigned long long h[4];
                     hip_check(hipMemcpyAsync(h, st, sizeof(h), hipMemcpyDeviceToHost, stream), "stats");
@@ -302,6 +256,13 @@ extern "C" mpt_status mpt_prm_connect(const mpt_env *env, const mpt_agent *agent
                     g_prm_stats[5] = (uint64_t)P;
                 }
             } else {
+                CollideWork w{};
+                w.poses = d_poses;
+                w.pose_edge = d_pe;
+                w.pmax = 1;
+                w.L = 1;
+                w.n_units = P;
+                w.verdict = d_v;
                 launch_collide(env_dev(env), d_link, w, stream);
             }
         }

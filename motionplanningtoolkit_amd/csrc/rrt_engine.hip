@@ -937,6 +937,14 @@ bool round_uses_tree(const mpt_rrt *r) {
     return r->nn_mode == MPT_NN_TREE || (r->nn_mode == MPT_NN_AUTO && big && r->auto_tree);
 }
 
+// a joint round indexes every engine's tree in the cell tree whatever its size: a young tree
+// (<= kCtSeg nodes) starts from an empty index inside the joint build, so a planner run from
+// its start states is joint from its first round (no per-engine brute-force rounds, no
+// per-engine scratch, no per-seed full rebuilds)
+bool joint_uses_tree(const mpt_rrt *r) {
+    return r->nn_mode == MPT_NN_TREE || (r->nn_mode == MPT_NN_AUTO && r->auto_tree);
+}
+
 // the spread feedback rides on this round's index build when none is in flight; true when
 // this round's build should write it (spread filled in)
 bool spread_request(mpt_rrt *r, bool indexed, SpreadOut &spread) {
@@ -1219,13 +1227,13 @@ struct JointNN {
     bool round_timed = false;
 };
 std::mutex g_joints_mu;
-std::map<hipStream_t, std::unique_ptr<JointNN>> g_joints;
+std::map<hipStream_t, std::shared_ptr<JointNN>> g_joints;
 std::atomic<uint64_t> g_joint_buf_ids{0};
 thread_local JointNN *g_last_timed = nullptr;  // mpt_rrt_joint_nn_ms: this thread's last timed call
 
 JointNN &joint_state(hipStream_t s) {
     std::lock_guard<std::mutex> lk(g_joints_mu);
-    std::unique_ptr<JointNN> &p = g_joints[s];
+    std::shared_ptr<JointNN> &p = g_joints[s];
     if (!p) p.reset(new JointNN());
     return *p;
 }
@@ -1234,6 +1242,12 @@ JointNN *joint_find(hipStream_t s) {
     std::lock_guard<std::mutex> lk(g_joints_mu);
     const auto it = g_joints.find(s);
     return it == g_joints.end() ? nullptr : it->second.get();
+}
+
+std::shared_ptr<JointNN> joint_find_shared(hipStream_t s) {
+    std::lock_guard<std::mutex> lk(g_joints_mu);
+    const auto it = g_joints.find(s);
+    return it == g_joints.end() ? nullptr : it->second;
 }
 
 // a pinned staging buffer of at least `bytes` whose previous copy has completed
@@ -1292,7 +1306,7 @@ bool joint_round_ok(mpt_rrt *const *rs, int32_t n, int32_t K) {
             std::memcmp(q.lo, p.lo, sizeof(p.lo)) != 0 || std::memcmp(q.hi, p.hi, sizeof(p.hi)) != 0)
             return false;
         refresh_auto(r);
-        if (!round_uses_tree(r)) return false;
+        if (!joint_uses_tree(r)) return false;
     }
     return true;
 }
@@ -1561,12 +1575,22 @@ extern "C" mpt_status mpt_rrt_step_many(mpt_rrt *const *rs, int32_t n, int32_t K
 }
 
 namespace {
-// an engine's last joint round slices are still the joint state's live buffers
-void joint_slices_check(const mpt_rrt *r) {
-    JointNN *g = joint_find(r->jv_stream);
-    if (!g || g->buf_id == 0 || g->buf_id != r->jv_id)
+// an engine's last joint round slices are still the joint state's live buffers: the joint
+// state's lock, held by the caller through its copies (a step_many that reallocates the round
+// buffers or a joint_release on another host thread waits for it; the state itself stays alive
+// through the shared pointer)
+struct JointSlices {
+    std::shared_ptr<JointNN> g;
+    std::unique_lock<std::mutex> lk;
+};
+JointSlices joint_slices_lock(const mpt_rrt *r) {
+    JointSlices js;
+    js.g = joint_find_shared(r->jv_stream);
+    if (js.g) js.lk = std::unique_lock<std::mutex>(js.g->mu);
+    if (!js.g || js.g->buf_id == 0 || js.g->buf_id != r->jv_id)
         throw Error{MPT_ERR_INVALID, "the joint round's buffers were released or reallocated since this engine's "
                                      "last round"};
+    return js;
 }
 }  // namespace
 
@@ -1608,7 +1632,7 @@ extern "C" mpt_status mpt_rrt_joint_stage_times(void *joint_stream, float ms[6])
 
 extern "C" mpt_status mpt_rrt_joint_release(void *joint_stream) {
     return guarded([&] {
-        std::unique_ptr<JointNN> g;
+        std::shared_ptr<JointNN> g;
         {
             std::lock_guard<std::mutex> lk(g_joints_mu);
             const auto it = g_joints.find((hipStream_t)joint_stream);
@@ -1662,7 +1686,8 @@ extern "C" mpt_status mpt_rrt_last_round(mpt_rrt *r, double *samples, int32_t *n
         if (K == 0) return;
         // a joint round's buffers are the joint state's slices (valid until its next step_many)
         const bool j = r->last_joint;
-        if (j) joint_slices_check(r);
+        JointSlices lock;
+        if (j) lock = joint_slices_lock(r);
         const double *s = j ? r->jv.samples : r->d_samples, *e = j ? r->jv.ends : r->d_ends;
         const int32_t *nn = j ? r->jv.nn : r->d_nn;
         const uint8_t *v = j ? r->jv.verdict : r->d_verdict;
@@ -1680,7 +1705,8 @@ extern "C" mpt_status mpt_rrt_last_poses(mpt_rrt *r, double *poses, int32_t *pos
         const int64_t K = r->last_K;
         if (K == 0) return;
         const bool j = r->last_joint;
-        if (j) joint_slices_check(r);
+        JointSlices lock;
+        if (j) lock = joint_slices_lock(r);
         if (poses)
             hip_check(hipMemcpy(poses, j ? r->jv.poses : r->d_poses, sizeof(double) * 12 * K * r->p.pmax * r->p.L,
                                 hipMemcpyDeviceToHost),

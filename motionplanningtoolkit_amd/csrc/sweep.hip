@@ -17,6 +17,7 @@
 //      Q'_p = R Q + T_p, exact tri_gate, intersect_Triangle; a hit sets verdict[e] and every
 //      wave of the edge stops.
 #include "collide_common.h"
+#include "prm_edges.h"
 
 namespace mpt {
 
@@ -293,41 +294,52 @@ __device__ __forceinline__ void sweep_edge_core(const EnvDev &env, const AgentDe
     }
 }
 
-// edges given as pose ranges of a pose array (prm_connect.hip)
-__device__ __forceinline__ void sweep_wave(const EnvDev &env, const AgentDev &ag, const double *__restrict__ poses,
-                                           const int64_t *__restrict__ poff, int64_t e, int32_t cl, uint8_t *verdict,
-                                           int lane, int32_t *stk, SweepCounters &cnt) {
-    if (load_flag(verdict + e)) return;
-    const int64_t p0 = poff[e], p1 = poff[e + 1];
-    if (p1 <= p0) return;
-    sweep_core(env, ag, cl, poses + p0 * 12, poses + p0 * 12 + 9, poses + (p1 - 1) * 12 + 9,
-               [&](auto &&f) {
-                   for (int64_t p = p0; p < p1; ++p)
-                       if (f(poses + p * 12 + 9)) return;
-               },
-               verdict + e, lane, stk, cnt);
-}
+// Where an edge's poses come from.  A source's edge(e, core) calls core(Rw, tf, tl, gen) with
+// the edge's world rotation, its first and last pose's translation and the pose generator
+// (gen(f): f(world translation) for each pose in order until f returns true), or returns
+// without calling it when the edge has no poses.
+// A pose array: edge e's poses are [poff[e], poff[e + 1]) of poses [P][12] (R|T).
+struct PoseArraySrc {
+    const double *poses;
+    const int64_t *poff;
+    template <class Core>
+    __device__ __forceinline__ void edge(int64_t e, Core &&core) const {
+        const int64_t p0 = poff[e], p1 = poff[e + 1];
+        if (p1 <= p0) return;
+        core(poses + p0 * 12, poses + p0 * 12 + 9, poses + (p1 - 1) * 12 + 9, [&](auto &&f) {
+            for (int64_t p = p0; p < p1; ++p)
+                if (f(poses + p * 12 + 9)) return;
+        });
+    }
+};
+// A PRM roadmap edge (prm_edges.h): the poses generated from the two milestones' keys with the
+// pose stage's operations -- no pose array (config 4: ~20-130 M poses a roadmap)
+struct PrmSrc {
+    PrmEdges P;
+    template <class Core>
+    __device__ __forceinline__ void edge(int64_t e, Core &&core) const {
+        const PrmEdge g = prm_edge(P, e);
+        double tf[3], tl[3];
+        g.first(tf);
+        g.last(tl);
+        core(g.R, tf, tl, [&](auto &&f) { g.each(f); });
+    }
+};
 
 // one wave an edge (agents of at most 64 clusters)
+template <class Src>
 __global__ __launch_bounds__(kSweepWaves * 64) void k_sweep_edge(EnvDev env, const AgentDev *__restrict__ link,
-                                                                 const double *__restrict__ poses,
-                                                                 const int64_t *__restrict__ poff, int64_t E,
-                                                                 uint8_t *verdict, unsigned long long *stats) {
+                                                                 Src src, int64_t E, uint8_t *verdict,
+                                                                 unsigned long long *stats) {
     __shared__ int32_t s_stk[kSweepWaves][2 * kSweepStack];
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
     const int64_t e = (int64_t)blockIdx.x * kSweepWaves + wave;
     SweepCounters cnt;
-    if (e < E && !load_flag(verdict + e)) {
-        const int64_t p0 = poff[e], p1 = poff[e + 1];
-        if (p1 > p0)
-            sweep_edge_core(env, link[0], poses + p0 * 12, poses + p0 * 12 + 9, poses + (p1 - 1) * 12 + 9,
-                            [&](auto &&f) {
-                                for (int64_t p = p0; p < p1; ++p)
-                                    if (f(poses + p * 12 + 9)) return;
-                            },
-                            verdict + e, lane, s_stk[wave], cnt);
-    }
+    if (e < E && !load_flag(verdict + e))
+        src.edge(e, [&](const double *Rw, const double *tf, const double *tl, auto &&gen) {
+            sweep_edge_core(env, link[0], Rw, tf, tl, gen, verdict + e, lane, s_stk[wave], cnt);
+        });
     if (stats && lane == 0 && cnt.waves) {
         atomicAdd(stats + 0, (unsigned long long)cnt.waves);
         atomicAdd(stats + 1, (unsigned long long)cnt.items);
@@ -337,10 +349,9 @@ __global__ __launch_bounds__(kSweepWaves * 64) void k_sweep_edge(EnvDev env, con
 }
 
 // one wave an (edge, cluster) (agents of more than 64 clusters)
-__global__ __launch_bounds__(kSweepWaves * 64) void k_sweep(EnvDev env, const AgentDev *__restrict__ link,
-                                                            const double *__restrict__ poses,
-                                                            const int64_t *__restrict__ poff, int64_t E,
-                                                            int32_t n_clusters, uint8_t *verdict,
+template <class Src>
+__global__ __launch_bounds__(kSweepWaves * 64) void k_sweep(EnvDev env, const AgentDev *__restrict__ link, Src src,
+                                                            int64_t E, int32_t n_clusters, uint8_t *verdict,
                                                             unsigned long long *stats) {
     __shared__ int32_t s_stk[kSweepWaves][2 * kSweepStack];
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -349,8 +360,11 @@ __global__ __launch_bounds__(kSweepWaves * 64) void k_sweep(EnvDev env, const Ag
     const int64_t e = g / n_clusters;
     const int32_t cl = (int32_t)(g % n_clusters);
     SweepCounters cnt;
-    if (e < E) sweep_wave(env, link[0], poses, poff, e, cl, verdict, lane, s_stk[wave], cnt);
-    if (stats && lane == 0 && e < E) {
+    if (e < E && !load_flag(verdict + e))
+        src.edge(e, [&](const double *Rw, const double *tf, const double *tl, auto &&gen) {
+            sweep_core(env, link[0], cl, Rw, tf, tl, gen, verdict + e, lane, s_stk[wave], cnt);
+        });
+    if (stats && lane == 0 && cnt.waves) {
         atomicAdd(stats + 0, (unsigned long long)cnt.waves);
         atomicAdd(stats + 1, (unsigned long long)cnt.items);
         atomicAdd(stats + 2, (unsigned long long)cnt.pair_poses);
@@ -423,25 +437,36 @@ void launch_prmlite_edges(const EnvDev &env, const AgentDev *d_link, int32_t n_c
     hip_check(hipGetLastError(), "k_sweep_lite launch");
 }
 
-void launch_collide_sweep(const EnvDev &env, const AgentDev *d_link, int32_t n_clusters, const double *poses,
-                          const int64_t *poff, int64_t E, uint8_t *verdict, unsigned long long *stats,
-                          hipStream_t stream) {
+template <class Src>
+static void launch_sweep_src(const EnvDev &env, const AgentDev *d_link, int32_t n_clusters, const Src &src, int64_t E,
+                             uint8_t *verdict, unsigned long long *stats, hipStream_t stream) {
     if (E <= 0 || env.n_tris <= 0) return;
     if (env.n_tris >= (1 << 27)) throw Error{5, "env too large for the sweep path"};
     if (n_clusters <= 64) {
         const int64_t blocks = (E + kSweepWaves - 1) / kSweepWaves;
         if (blocks > 0x7fffffff) throw Error{5, "sweep batch too large"};
-        hipLaunchKernelGGL(k_sweep_edge, dim3((unsigned)blocks), dim3(kSweepWaves * 64), 0, stream, env, d_link, poses,
-                           poff, E, verdict, stats);
+        hipLaunchKernelGGL(k_sweep_edge<Src>, dim3((unsigned)blocks), dim3(kSweepWaves * 64), 0, stream, env, d_link,
+                           src, E, verdict, stats);
         hip_check(hipGetLastError(), "k_sweep_edge launch");
         return;
     }
     const int64_t waves = E * n_clusters;
     const int64_t blocks = (waves + kSweepWaves - 1) / kSweepWaves;
     if (blocks > 0x7fffffff) throw Error{5, "sweep batch too large"};
-    hipLaunchKernelGGL(k_sweep, dim3((unsigned)blocks), dim3(kSweepWaves * 64), 0, stream, env, d_link, poses, poff, E,
+    hipLaunchKernelGGL(k_sweep<Src>, dim3((unsigned)blocks), dim3(kSweepWaves * 64), 0, stream, env, d_link, src, E,
                        n_clusters, verdict, stats);
     hip_check(hipGetLastError(), "k_sweep launch");
+}
+
+void launch_collide_sweep(const EnvDev &env, const AgentDev *d_link, int32_t n_clusters, const double *poses,
+                          const int64_t *poff, int64_t E, uint8_t *verdict, unsigned long long *stats,
+                          hipStream_t stream) {
+    launch_sweep_src(env, d_link, n_clusters, PoseArraySrc{poses, poff}, E, verdict, stats, stream);
+}
+
+void launch_collide_sweep_prm(const EnvDev &env, const AgentDev *d_link, int32_t n_clusters, const PrmEdges &edges,
+                              int64_t E, uint8_t *verdict, unsigned long long *stats, hipStream_t stream) {
+    launch_sweep_src(env, d_link, n_clusters, PrmSrc{edges}, E, verdict, stats, stream);
 }
 
 }  // namespace mpt

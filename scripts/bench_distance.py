@@ -48,7 +48,7 @@ def distance_roofline(out, a, n_agent, n_env, ms):
 
     t = ms * 1e-3
     comp = a.n * (96 + 8 + 8) + n_agent * 72 + n_env * (384 + 32)
-    roof = {"bound": "mfma", "kernel": "k_distance", "achieved": round(out["fp64"]["achieved_tflops"], 3),
+    roof = {"bound": "fp64_valu", "kernel": "k_distance", "achieved": round(out["fp64"]["achieved_tflops"], 3),
             "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": round(out["fp64"]["frac"], 4),
             "note": "FP64 VALU roof (FCL's scalar operation order; no MFMA)", "ms_per_launch": round(ms, 4),
             "compulsory_bytes": int(comp), "frac_hbm_compulsory": round(comp / t / 1e9 / HBM_PEAK_GBS, 4),

@@ -2,8 +2,9 @@
 
 Workload: synthetic env = 25 x 25 copies of the model.dae room (197 500 triangles; the
 reference's apartment.dae is missing), blimp agent (all 1355 triangles of blimp.3ds),
-N milestones ~ U(Blimp::getStateVarRanges) (x, y, z in [-100, 100]), radius chosen for a mean
-of ~10 neighbours per milestone (counting both directions), cc_dt 0.1 (blimp.inst).  One call
+N milestones ~ U(Blimp::getStateVarRanges) with x, y, z over the whole multi-room extent
+(--bounds rooms, the default; --bounds blimp: blimp.inst's [-100, 100]^3), radius chosen for a
+mean of ~10 neighbours per milestone (counting both directions), cc_dt 0.1 (blimp.inst).  One call
 of mpt_prm_connect: point-tree radius search, edge poses, batched collision, components.
 Prints one JSON line: milestones/s, edges checked/s, per-stage device ms, and the oracle's
 single-core rate on a bounded sample of the same roadmap (its first milestones).
@@ -37,20 +38,19 @@ def latest_pmc(sub):
     return c[-1] if c else ""
 
 
-def sweep_roofline(w, ms, n_agent, n_env, traffic_path):
-    """k_sweep (the config-4 collision stage, one wave per (edge, agent cluster)): FP64 by
-    SURVEY §8(d)'s model -- 750 flops per exact triangle test, 27 per (pair, pose) gate (the
+def sweep_roofline(w, ms, n_agent, n_env, n_milestones, traffic_path):
+    """k_sweep (the config-4 collision stage, one wave per edge over the agent's clusters, the
+    edge's poses generated in the kernel from its two milestones, prm_edges.h): FP64 by SURVEY
+    §8(d)'s model -- 750 flops per exact triangle test, 27 per (pair, pose) gate (the
     translated triangle's box and the overlap test), 45 per agent triangle rotated once per
-    wave (R Q, 64 lanes) -- and HBM: compulsory = the poses, pose offsets, verdicts, agent
-    triangles and the env tree items read once; measured = the kernel's rocprofv3 PMC traffic."""
+    wave (R Q, 64 lanes) -- and HBM: compulsory = every input once -- the edges (source, target
+    id, verdict byte), the milestones' keys and yaw (40 B), the agent triangles, the env tree's
+    items and triangle records -- measured = the kernel's rocprofv3 PMC traffic."""
     t = ms * 1e-3
     flops = 750.0 * w["sat_tests"] + 27.0 * w["gate_tests"] + 45.0 * 64 * w["waves"]
     items = n_env + -(-n_env // 8)
-    # an edge's poses share one rotation: its first pose whole (96 B), every other pose's
-    # translation (24 B; k_sweep reads no more of it)
-    comp = (w["edges"] * 96 + (w["poses"] - w["edges"]) * 24 + (w["edges"] + 1) * 8 + w["edges"] + n_agent * 72
-            + items * 32)
-    out = {"bound": "mfma", "kernel": "k_sweep", "achieved": round(flops / t / 1e12, 3), "peak": FP64_PEAK_TFLOPS,
+    comp = w["edges"] * 9 + n_milestones * 40 + n_agent * 72 + items * 32 + n_env * 384
+    out = {"bound": "fp64_valu", "kernel": "k_sweep", "achieved": round(flops / t / 1e12, 3), "peak": FP64_PEAK_TFLOPS,
            "unit": "TFLOP/s", "frac": round(flops / t / 1e12 / FP64_PEAK_TFLOPS, 4),
            "note": "FP64 VALU roof (FCL's scalar operation order; no MFMA)",
            "compulsory_bytes": int(comp), "compulsory_gbs": round(comp / t / 1e9, 1),
@@ -82,9 +82,10 @@ def main():
     ap.add_argument("--traffic", default=None,
                     help="pmc_summary.json with k_sweep's traffic (default: the newest profiles/r*/prm/)")
     ap.add_argument("--collide", default="split", choices=["split", "fused"])
-    ap.add_argument("--bounds", default="blimp", choices=["blimp", "rooms"],
-                    help="milestone x, y, z: blimp.inst's [-100, 100]^3 (one corner of the rooms) or the whole "
-                         "multi-room extent (every room's walls in play)")
+    ap.add_argument("--bounds", default="rooms", choices=["blimp", "rooms"],
+                    help="milestone x, y, z: the whole multi-room extent (default: every room's walls in play, "
+                         "tests/test_scale_gpu.py test_config4_rooms_at_size) or blimp.inst's [-100, 100]^3 (one "
+                         "corner of the rooms)")
     a = ap.parse_args()
 
     import motionplanningtoolkit_amd as mpt
@@ -117,7 +118,7 @@ def main():
     mpt.prm_stats(True)
     mpt.prm_connect(env, ag, 1, st, r2, sc.cc_dt)
     work = mpt.prm_stats(False)
-    roof = sweep_roofline(work, ms["collision"], len(sc.agent_tris), int(env.info()["triangles"]), a.traffic)
+    roof = sweep_roofline(work, ms["collision"], len(sc.agent_tris), int(env.info()["triangles"]), a.n, a.traffic)
     out = {
         "metric": "PRM roadmap construction (radius neighbours + edge collision checks), config 4",
         "value": a.n / wall, "unit": "milestones/s", "edges_checked_per_s": E / wall,

@@ -1,0 +1,30 @@
+#!/bin/bash
+# Usage: TAG=x bash scripts/r21.sh [pytest files...]
+# On the GPU box: the given GPU tests, then config 5 at 32 / 256 seeds (25 + 5 rounds) and
+# config 4 at --bounds rooms; lines under gpurun_out/$TAG/.  Stops at the first failure.
+TAG=${TAG:?set TAG}
+O=gpurun_out/$TAG
+mkdir -p $O
+export TMPDIR=/tmp
+if [ $# -gt 0 ]; then
+  timeout -k 10 900 python -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu "$@" > $O/pytest.log 2>&1
+  rc=$?; tail -3 $O/pytest.log; [ $rc -ne 0 ] && exit $rc
+fi
+for n in 32 256; do
+  timeout -k 10 200 python bench.py --seeds $n --steps 25 --warmup 5 --no-cpu --detail $O/c5_${n}_detail.json > $O/c5_$n.json || exit 1
+done
+[ -n "$NO_PRM" ] || timeout -k 10 300 python scripts/bench_prm.py --reps 3 --no-cpu > $O/prm.json || exit 1
+python - $O <<'PY'
+import json, sys
+o = sys.argv[1]
+for n in (32, 256):
+    d = json.load(open(f"{o}/c5_{n}_detail.json"))
+    st = {k: round(v.get("ms_event_free", v["ms"]), 3) for k, v in d["roofline"]["stages"].items()}
+    print(n, round(d["value"] / 1e6, 1), "M/s", round(d["ms_per_step"], 3), "ms", d["seeds_digest"][:8],
+          "scratch", round(d["from_scratch"]["valid_per_s"] / 1e6, 1), st)
+try:
+    p = json.loads(open(f"{o}/prm.json").read().strip().splitlines()[-1])
+    print("prm", round(p["value"] / 1e6, 2), "M milestones/s", p["device_ms"], p["config"]["free_fraction"])
+except Exception as e:
+    print("prm", e)
+PY

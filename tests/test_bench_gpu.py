@@ -48,22 +48,40 @@ def test_two_ranks_shard_config5_like_one():
     assert two["valid_fraction"] == one["valid_fraction"]
 
 
+def _check_multi_rank_line(two, one):
+    """At N > 1 the line's top level is config 5 (strong scaling, seeds sharded contiguously
+    over the ranks) with config 2's weak-scaled line nested under `config2`."""
+    assert two["n_gpus"] == 2 and two["world_size"] == 2 and two["scaling"] == "strong"
+    assert (two["steps"], two["warmup"]) == (2, 3)
+    assert two["seeds_digest"] == one["seeds_digest"]
+    assert two["from_scratch"]["rounds"] == 5 and two["from_scratch"]["wall_s"] > 0
+    c2 = two["config2"]
+    assert c2["world_size"] == 2 and c2["value"] > 0
+    assert len(json.dumps(two)) < 8000
+
+
+C5_SMALL = ["--c5-seeds", "12", "--c5-steps", "2", "--c5-warmup", "3"]
+C2_SMALL = ["--steps", "3", "--warmup", "1", "--tree", "20000", "--batch", "4096", "--no-cpu"]
+
+
 @pytest.mark.timeout(600)
 def test_driver_multi_rank_line_carries_config5():
-    """`bench.py --gpus 2` as the driver launches it: the printed line is config 2 (weak, one
-    tree per rank) with the config-5 leg run in the same torchrun world (seeds sharded
-    contiguously over the ranks); its digest equals one rank's `--seeds` run at the same
-    rounds.  Sizes reduced (--tree, --batch, --c5-*) so the test stays short; the code path is
-    the driver's."""
+    """`bench.py --gpus 2` as the driver launches it (under torchrun).  Sizes reduced (--tree,
+    --batch, --c5-*) so the test stays short; the code path is the driver's."""
     env = dict(os.environ, MPT_DIST_BACKEND="gloo", MPT_BENCH_DEVICE="0")
-    c5 = ["--c5-seeds", "12", "--c5-steps", "2", "--c5-warmup", "3"]
     two = _run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
-                "--master-addr", "127.0.0.1", "--master-port", str(_port()), "bench.py", "--gpus", "2", "--steps", "3",
-                "--warmup", "1", "--tree", "20000", "--batch", "4096", "--no-cpu"] + c5, env)
+                "--master-addr", "127.0.0.1", "--master-port", str(_port()), "bench.py", "--gpus", "2"]
+               + C2_SMALL + C5_SMALL, env)
     one = _run([sys.executable, "bench.py", "--seeds", "12", "--steps", "2", "--warmup", "3", "--no-cpu"], env)
-    assert two["n_gpus"] == 2 and two["world_size"] == 2 and two["scaling"] == "weak"
-    c = two["config5"]
-    assert c["world_size"] == 2 and c["n_gpus"] == 2 and c["scaling"] == "strong"
-    assert (c["steps"], c["warmup"]) == (2, 3)
-    assert c["seeds_digest"] == one["seeds_digest"]
-    assert c["from_scratch"]["rounds"] == 5 and c["from_scratch"]["wall_s"] > 0
+    _check_multi_rank_line(two, one)
+
+
+@pytest.mark.timeout(600)
+def test_gpus_flag_spawns_ranks():
+    """`bench.py --gpus 2` with no torchrun around it starts the two ranks itself (a
+    torch.distributed.run child, before any GPU call) and prints the same line."""
+    env = dict(os.environ, MPT_DIST_BACKEND="gloo", MPT_BENCH_DEVICE="0")
+    env.pop("WORLD_SIZE", None)
+    two = _run([sys.executable, "bench.py", "--gpus", "2"] + C2_SMALL + C5_SMALL, env)
+    one = _run([sys.executable, "bench.py", "--seeds", "12", "--steps", "2", "--warmup", "3", "--no-cpu"], env)
+    _check_multi_rank_line(two, one)

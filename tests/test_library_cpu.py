@@ -196,3 +196,40 @@ def test_mesh_dir_override(tmp_path):
     out = subprocess.run(["python", "-c", code], cwd=REPO, env=env, capture_output=True, text=True, timeout=120)
     assert out.returncode == 0, out.stderr
     assert out.stdout.strip().startswith(str(tmp_path))
+
+
+def test_bench_line_fits_the_driver_tail():
+    """bench.py prints a condensed line (the full one goes to --detail): for a full round-4 line
+    with every leg (tests/golden/bench/full_line_r20.json, 17 KB) it stays under 8 KB -- the
+    driver keeps the last 8 KB of stdout -- and keeps every leg's value, time and roofline."""
+    import json
+    import sys
+
+    sys.path.insert(0, REPO)
+    import bench
+
+    full = json.load(open(os.path.join(REPO, "tests", "golden", "bench", "full_line_r20.json")))
+    line = bench.compact_line(full, os.path.join(REPO, "gpurun_out", "bench_detail.json"))
+    text = json.dumps(line)
+    assert len(text) < 6000, len(text)
+    assert line["value"] == full["value"] and line["roofline"]["frac"] == full["roofline"]["frac"]
+    for name, leg in full["variants"].items():
+        got = line["variants"][name]
+        assert got["value"] == leg["value"] and got.get("ms_per_step") == leg.get("ms_per_step")
+        assert got["roofline"]["frac"] == leg["roofline"]["frac"]
+    assert line["variants"]["seeds=256"]["seeds_digest"] == full["variants"]["seeds=256"]["seeds_digest"]
+    assert line["config5"]["per_gpu_ratio"] == full["config5"]["per_gpu_ratio"]
+
+
+def test_bench_gpus_must_match_world_size():
+    """Under torchrun, --gpus N must equal WORLD_SIZE (checked before anything is imported)."""
+    env = dict(os.environ, WORLD_SIZE="3", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys_executable(), os.path.join(REPO, "bench.py"), "--gpus", "2"], env=env,
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode != 0 and "WORLD_SIZE=3" in r.stderr
+
+
+def sys_executable():
+    import sys
+
+    return sys.executable

@@ -39,13 +39,34 @@ def test_omni_corridor(mpt_gpu, oracle):
 
 
 @pytest.mark.parametrize("agent_mode", ["last", "all"])
-def test_blimp_room(mpt_gpu, oracle, agent_mode):
+@pytest.mark.parametrize("mode", ["split", "fused"])
+def test_blimp_room(mpt_gpu, oracle, agent_mode, mode):
+    """split: the sweep with each edge's poses generated in the kernel (prm_edges.h, no pose
+    array); fused: the pose array and the per-pose walk -- the same verdicts."""
     sc = scenes.blimp_scenario(agent_mode)
     rng = np.random.default_rng(3)
     n = 1200
     st = rng.uniform(sc.ranges[:, 0], sc.ranges[:, 1], size=(n, 7))
     st[:, :3] = rng.uniform([-10, -10, -10], [190, 150, 125], size=(n, 3))
-    got = compare(mpt_gpu, oracle, sc.env_tris, sc.agent_tris, 1, st, 14.0 ** 2, sc.cc_dt)
+    mpt_gpu.set_collide_mode(mode)
+    try:
+        got = compare(mpt_gpu, oracle, sc.env_tris, sc.agent_tris, 1, st, 14.0 ** 2, sc.cc_dt)
+    finally:
+        mpt_gpu.set_collide_mode("split")
+    assert 0 < got["verdict"].sum() < len(got["verdict"])
+
+
+def test_agent_of_many_clusters(mpt_gpu, oracle):
+    """An agent of more than 64 clusters (four copies of the blimp, 5420 triangles, 85
+    clusters): the sweep's one-wave-an-(edge, cluster) form with in-kernel poses."""
+    sc = scenes.blimp_scenario("all")
+    ag = np.concatenate([sc.agent_tris + np.array([dx, 0, 0] * 3) for dx in (0.0, 3.0, 6.0, 9.0)])
+    assert len(ag) > 64 * 64  # clusters hold at most 64 triangles (mpt_agent_create)
+    rng = np.random.default_rng(8)
+    n = 300
+    st = rng.uniform(sc.ranges[:, 0], sc.ranges[:, 1], size=(n, 7))
+    st[:, :3] = rng.uniform([-10, -10, -10], [190, 150, 125], size=(n, 3))
+    got = compare(mpt_gpu, oracle, sc.env_tris, ag, 1, st, 20.0 ** 2, sc.cc_dt)
     assert 0 < got["verdict"].sum() < len(got["verdict"])
 
 

@@ -246,3 +246,71 @@ def test_config5_shard_shape(mpt_gpu, oracle):
         assert n == len(st)
         assert np.array_equal(st.view(np.uint64), ref[:n].view(np.uint64))
         assert np.array_equal(pa, par[:n])
+
+
+def test_config5_256_joint(mpt_gpu, oracle):
+    """The N = 1 north-star leg's shape (`bench.py --seeds 256`): 256 wall-start blimp seeds
+    in ONE step_many group from their start states -- every round a joint round (256 jobs dealt
+    over the XCDs in the joint NN launch, one collide chunk of ~1 M units x 22 clusters, the
+    young trees indexed from an empty cell tree inside the joint build) -- for 6 rounds of 4096
+    extensions.  Seeds 0, 127 and 255 node for node against orc_engine_step (the reference's
+    RRT::query loop, planners/rrt.hpp:42-94, batched), and the 256-seed digest equal to that of
+    eight separate 32-seed groups -- what each GPU of eight runs (multiseed.shard_seeds)."""
+    import hashlib
+    import sys
+
+    import torch
+
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    from motionplanningtoolkit_amd import multiseed
+
+    sc = scenes.blimp_scenario("all")
+    env = mpt_gpu.Environment(sc.env_tris, sc.env_tf)
+    ag = mpt_gpu.AgentMesh(sc.agent_tris)
+    K, rounds, base, n = 4096, 6, 1000, 256
+    seeds = [base + i for i in range(n)]
+    starts = {s: bench.seed_start(s, env, ag, mpt_gpu, "walls") for s in seeds}
+
+    def grow(group_seeds):
+        engs = []
+        for s in group_seeds:
+            e = mpt_gpu.RRTEngine(env, ag, sc.kind, sc.prm, sc.ranges, sc.steer_dt, sc.cc_dt, 1 + rounds * K, s)
+            e.add_nodes(starts[s])
+            e.set_nn("auto")
+            engs.append(e)
+        joint = torch.cuda.Stream()
+        for _ in range(rounds):
+            mpt_gpu.step_many(engs, K, [joint] * len(engs), joint)
+        torch.cuda.synchronize()
+        out = {}
+        for s, e in zip(group_seeds, engs):
+            assert e.last_nn() == "tree"
+            out[s] = e.read_tree(e.counters()["nodes"])
+            e.close()
+        mpt_gpu.joint_release(joint)
+        return out
+
+    def digest(trees):
+        return hashlib.sha256("".join(multiseed.tree_digest(*trees[s]) for s in sorted(trees)).encode()).hexdigest()
+
+    whole = grow(seeds)
+    sizes = [len(whole[s][0]) for s in seeds]
+    assert min(sizes) > 10_000, min(sizes)
+    shards = {}
+    for r in range(8):
+        shards.update(grow([seeds[i] for i in multiseed.shard_seeds(n, 8, r)]))
+    assert digest(whole) == digest(shards)
+    bvh = oracle.BVH(sc.env_tris)
+    for s in (seeds[0], seeds[127], seeds[255]):
+        ref = np.zeros((1 + rounds * K, sc.dim))
+        ref[0] = starts[s][0]
+        par = np.zeros(1 + rounds * K, np.int32)
+        m = 1
+        for r in range(rounds):
+            m, _, _ = oracle.engine_step(sc.kind, sc.prm, sc.ranges, sc.steer_dt, sc.cc_dt, s, r * K, K, bvh,
+                                         sc.env_tf, sc.agent_tris, ref, par, m, nthreads=THREADS)
+        st, pa = whole[s]
+        assert m == len(st)
+        assert np.array_equal(st.view(np.uint64), ref[:m].view(np.uint64))
+        assert np.array_equal(pa, par[:m])
