@@ -367,7 +367,7 @@ def stage_table(per_launch, cst, K, n0, d, pmax, geo, nn_mode, kernels, summ):
 # measured traffic per launch is summed (the collide chain runs once per collide sub-batch)
 JOINT_STAGE_KERNELS = {
     "sample": ["k_sample_jobs"],
-    "nn_build": ["k_ct_reset", "k_ct_csort", "k_ct_crank", "k_ct_locate", "k_ct_segments",
+    "nn_build": ["k_ct_reset", "k_ct_ncodes", "k_ct_csort", "k_ct_crank", "k_ct_locate", "k_ct_segments",
                  "k_ct_apply", "k_ct_split_", "k_ct_dmerge", "k_ct_lflags", "k_ct_lgroup", "k_ct_levels"],
     "nn_query": ["k_ct_nn1_jobs"],
     "steer": ["k_steer_jobs"],

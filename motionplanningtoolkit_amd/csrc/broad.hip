@@ -83,9 +83,6 @@ __device__ __forceinline__ float wave_max(float v) {
     for (int off = 32; off > 0; off >>= 1) v = fmaxf(v, __shfl_xor(v, off));
     return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v)));
 }
-__device__ __forceinline__ float lane_f(float v, int j) {
-    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), j));
-}
 
 // Per-thread walk of the env tree (items from LDS or global) with box (lo, hi);
 // sink(tri) for every overlapping triangle box; returns the number of item tests.
@@ -184,35 +181,15 @@ __device__ __forceinline__ uint32_t walk_tree(const EnvDev &env, const Item *__r
 // again).  The walk is LDS-bandwidth bound: per-workgroup phase times (a round-2 timer since
 // removed) showed the cull + staging ~4 us and the walk ~16 us of a ~20-us lifetime; with these boxes
 // the walk takes ~11 us (config 2's k_pairs 31 -> 25 us, the room's 115 -> 90 us).
-struct QBox {
-    uint32_t lxy, hxy, lz, hz;  // query: lo.x | lo.y << 16, hi.x | hi.y << 16, lo.z, hi.z
-};
-__device__ __forceinline__ QBox quantize_box(const EnvDev &env, const float lo[3], const float hi[3]) {
-    uint32_t l[3], h[3];
-#pragma unroll
-    for (int k = 0; k < 3; ++k) {
-        const float vl = floorf((lo[k] - env.q_org[k]) * env.q_scale[k] - 0.02f);
-        const float vh = ceilf((hi[k] - env.q_org[k]) * env.q_scale[k] + 0.02f);
-        l[k] = (uint32_t)fminf(fmaxf(vl, 0.0f), (float)kQMax);
-        h[k] = (uint32_t)fminf(fmaxf(vh, 0.0f), (float)kQMax);
-    }
-    return QBox{l[0] | l[1] << 16, h[0] | h[1] << 16, l[2], h[2]};
-}
-__device__ __forceinline__ bool qbox_overlap(const QBox &q, uint4 it) {
-    constexpr uint32_t H = 0x80008000u;
-    const uint32_t t1 = (q.hxy | H) - it.x;  // query hi >= item lo (x, y)
-    const uint32_t t2 = (it.y | H) - q.lxy;  // item hi >= query lo (x, y)
-    const uint32_t A = (it.z & 0xffff0000u) | q.hz, B = (it.z & 0x0000ffffu) | (q.lz << 16);
-    const uint32_t t3 = (A | H) - B;         // query hi.z >= item lo.z, item hi.z >= query lo.z
-    return (t1 & t2 & t3 & H) == H;
-}
+// sel: the top-level items to test (the unit's link-box mask, top_item_mask; all ones: every
+// one) -- the others cannot meet the cluster's box, which lies inside the link's
 template <class Sink>
 __device__ __forceinline__ uint32_t walk_two_q(const EnvDev &env, const uint4 *__restrict__ qi, const QBox &q,
-                                               Sink &&sink) {
+                                               uint64_t sel, Sink &&sink) {
     const int32_t top = env.n_levels - 1;
     const int32_t top_off = env.lev_off[top];
     const int32_t n_top = env.lev_off[top + 1] - top_off;
-    uint32_t tests = (uint32_t)n_top;
+    uint32_t tests = 0;
     auto batch = [&](auto kB, int32_t first, int32_t count, int32_t i0, uint64_t &M) {
         constexpr int B = decltype(kB)::value;
         uint4 b[B];
@@ -229,7 +206,30 @@ __device__ __forceinline__ uint32_t walk_two_q(const EnvDev &env, const uint4 *_
         for (; i0 < count; i0 += 4) batch(std::integral_constant<int, 4>{}, first, count, i0, M);
         return M;
     };
-    uint64_t M = mask(top_off, n_top);
+    uint64_t M = 0;
+    if (n_top > 64 || sel == ~0ull) {
+        M = mask(top_off, n_top);
+        tests = (uint32_t)n_top;
+    } else {
+        // the selected items, eight loads in flight a batch
+        for (uint64_t rem = sel & (n_top == 64 ? ~0ull : ((1ull << n_top) - 1)); rem;) {
+            int idx[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                idx[j] = rem ? __ffsll((unsigned long long)rem) - 1 : -1;
+                rem &= rem - 1;
+            }
+            uint4 b[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) b[j] = qi[top_off + (idx[j] >= 0 ? idx[j] : idx[0])];
+#pragma unroll
+            for (int j = 0; j < 8; ++j)
+                if (idx[j] >= 0) {
+                    ++tests;
+                    if (qbox_overlap(q, b[j])) M |= 1ull << idx[j];
+                }
+        }
+    }
     while (M) {
         const int i = __ffsll((unsigned long long)M) - 1;
         M &= M - 1;
@@ -251,6 +251,7 @@ __device__ __forceinline__ uint32_t walk_two_q(const EnvDev &env, const uint4 *_
 struct PairRec {
     float lo[3], hi[3];
     int32_t unit, c, tfirst, tcount;
+    uint64_t tmask;  // the unit's top-level item mask (CollideWork::unit_tmask), or all ones
 };
 
 template <bool kTwo, bool kLds>
@@ -292,6 +293,7 @@ __global__ __launch_bounds__(kPairThreads) void k_pairs(EnvDev env, const AgentD
             r.c = c;
             r.tfirst = cl.first;
             r.tcount = cl.count;
+            r.tmask = w.unit_tmask ? w.unit_tmask[unit] : ~0ull;
             live = box_overlap(r.lo, r.hi, env.root_lo, env.root_hi);
         }
         const uint64_t m = __ballot(live);
@@ -361,7 +363,7 @@ __global__ __launch_bounds__(kPairThreads) void k_pairs(EnvDev env, const AgentD
         ++np;
     };
     if (live) {
-        if (quant) tests = walk_two_q(env, qitems, quantize_box(env, r.lo, r.hi), emit_pair);
+        if (quant) tests = walk_two_q(env, qitems, quantize_box(env, r.lo, r.hi), r.tmask, emit_pair);
         else tests = walk_tree<kTwo>(env, items, r.lo, r.hi, stk, emit_pair);
     }
     if (np > 0 && !ovf) {
@@ -849,6 +851,7 @@ void launch_collide_split(const EnvDev &env, const AgentDev *d_links, int32_t ma
         CollideWork c = w;
         c.live_units = nullptr;  // absolute unit indices: not per chunk
         c.n_live = nullptr;
+        if (w.unit_tmask) c.unit_tmask = w.unit_tmask + u0;  // chunks hold whole edges: unit u0 first
         c.n_units = std::min(per, w.n_units - u0);
         if (w.pose_edge) {
             const int64_t p0 = u0 / w.L;

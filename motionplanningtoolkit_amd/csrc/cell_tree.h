@@ -154,6 +154,10 @@ public:
                   const double *hi, int32_t spatial, bool full, int64_t grow, hipStream_t stream,
                   const SpreadOut *spread, unsigned long long *err);
     CellTreeDev dev() const { return t; }
+    // the code plan for these sampling ranges, uploaded now (synchronous) unless it is the
+    // current one; true when it changed (the index must then be rebuilt).  prepare() calls it;
+    // calling it beforehand (mpt_rrt_set_nn) keeps the upload out of the rounds.
+    bool set_plan(const double *lo, const double *hi, int32_t spatial);
     ~CellTree();
 
 private:

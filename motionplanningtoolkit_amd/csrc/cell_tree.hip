@@ -157,7 +157,7 @@ struct CtJobs {
 
 // this round's new points: the rows past the indexed count, at most the host's bound mb (the
 // grids are sized by it; a device count beyond it -- a host bound broken, reported by
-// k_ct_csort into counters[6] -- leaves the rest for the next round instead of indexing rows
+// k_ct_ncodes into counters[6] -- leaves the rest for the next round instead of indexing rows
 // no kernel coded)
 __device__ __forceinline__ int64_t ct_new_count(const CtJob &J) {
     const int64_t m = *J.T.n_dev - J.cnt->nidx, cap = J.mb < kCtSeg ? J.mb : kCtSeg;
@@ -173,6 +173,55 @@ __device__ __forceinline__ uint32_t inner_code(int64_t first, int32_t count) {
 }
 
 // ---- a round's new points ----
+
+// codes and rows of the new points [nidx, n) in row order, their box into ibox, their offers
+// to the seed slots
+template <int D>
+__global__ __launch_bounds__(64 * kCtWaves) void k_ct_ncodes(CtJobs js) {
+    __shared__ CtPlan s_plan;
+    __shared__ double s_rows[kCtWaves][64][D];
+    const CtJob J = CT_JOB(js);  // by value: the fields stay in registers across the stores
+    const int64_t base = J.cnt->nidx, mraw = *J.T.n_dev - base;
+    if ((mraw > kCtSeg || mraw > J.mb) && blockIdx.x == 0 && threadIdx.x == 0 && J.err)
+        atomicAdd(J.err, 1ull);  // the host's bound broken
+    const int64_t m = ct_new_count(J);
+    const int i = (int)blockIdx.x * (int)blockDim.x + (int)threadIdx.x;
+    if ((int64_t)blockIdx.x * blockDim.x >= m) return;  // block-uniform
+    for (int w = threadIdx.x; w < (int)(sizeof(CtPlan) / 4); w += blockDim.x)
+        reinterpret_cast<uint32_t *>(&s_plan)[w] = reinterpret_cast<const uint32_t *>(J.plan)[w];
+    __syncthreads();
+    const bool live = i < m;
+    double x[D];
+    if (live) {
+        const int64_t row = base + i;
+        load_global<D>(J.pts + row * D, x);
+        uint64_t h, l;
+        ct_code<D>(s_plan, x, h, l);
+        J.ncode[2 * i] = h;
+        J.ncode[2 * i + 1] = l;
+        J.nrow[i] = (int32_t)row;
+    } else {
+#pragma unroll
+        for (int j = 0; j < D; ++j) x[j] = 0.0;
+    }
+    // the persistent box over dims 0..2 only: its one reader is k_ct_levels' copy for the
+    // engine's MPT_NN_AUTO spread, whose dims are the first two or three (rrt_engine grid_dims)
+#pragma unroll
+    for (int j = 0; j < (D < 3 ? D : 3); ++j) {
+        unsigned long long mn = live ? okey(x[j]) : ~0ull, mx = live ? okey(x[j]) : 0ull;
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) {
+            const unsigned long long omn = __shfl_xor(mn, off), omx = __shfl_xor(mx, off);
+            mn = omn < mn ? omn : mn;
+            mx = omx > mx ? omx : mx;
+        }
+        if ((threadIdx.x & 63) == 0) {
+            atomicMin(J.ibox + j, mn);
+            atomicMax(J.ibox + kCtMaxDim + j, mx);
+        }
+    }
+    hull_offer<D>(s_plan, x, live, base + (i & ~63), s_rows[threadIdx.x >> 6], J.hull_keys);
+}
 
 // (code, row) compare-exchange by selects (no divergent branches)
 __device__ __forceinline__ void cx3(uint64_t &h, uint64_t &l, int32_t &r, uint64_t ph, uint64_t pl, int32_t pr,
@@ -192,72 +241,23 @@ constexpr int kCtChunk = 512;
 constexpr int kCtChunks = kCtSeg / kCtChunk;
 constexpr int kCtSortThreads = kCtChunk / 2;
 
-// Codes and the chunk sort in one launch: a 256-thread workgroup takes 512 consecutive new
-// rows, two a thread -- rows c0 + a * 256 + t (consecutive within a wave: coalesced row loads,
-// the persistent box and the seed offers per wave of 64 rows) -- codes them, and sorts the
-// chunk's (code, row) pairs in LDS and registers (round 4: a launch of its own for the codes
-// wrote and re-read every pair).
-template <int D>
 __global__ __launch_bounds__(kCtSortThreads) void k_ct_csort(CtJobs js) {
     const CtJob J = CT_JOB(js);  // by value: the fields stay in registers across the stores
-    __shared__ CtPlan s_plan;
     __shared__ uint64_t s_h[kCtChunk], s_l[kCtChunk];
     __shared__ int32_t s_r[kCtChunk];
-    __shared__ double s_rows[kCtSortThreads / 64][64][D];
-    const int64_t base = J.cnt->nidx, mraw = *J.T.n_dev - base;
-    if ((mraw > kCtSeg || mraw > J.mb) && blockIdx.x == 0 && threadIdx.x == 0 && J.err)
-        atomicAdd(J.err, 1ull);  // the host's bound broken
     const int64_t m = ct_new_count(J);
     const int c0 = (int)blockIdx.x * kCtChunk;
     if (c0 >= m) return;  // block-uniform
     const int t = threadIdx.x;
-    for (int w = t; w < (int)(sizeof(CtPlan) / 4); w += blockDim.x)
-        reinterpret_cast<uint32_t *>(&s_plan)[w] = reinterpret_cast<const uint32_t *>(J.plan)[w];
-    __syncthreads();
-#pragma unroll
-    for (int a = 0; a < 2; ++a) {
-        const int i = c0 + a * kCtSortThreads + t;
-        const bool live = i < m;
-        double x[D];
-        uint64_t h = ~0ull, l = ~0ull;  // padding sorts last (codes use 126 bits)
-        if (live) {
-            load_global<D>(J.pts + (base + i) * D, x);
-            ct_code<D>(s_plan, x, h, l);
-        } else {
-#pragma unroll
-            for (int j = 0; j < D; ++j) x[j] = 0.0;
-        }
-        const int e = a * kCtSortThreads + t;
-        s_h[e] = h;
-        s_l[e] = l;
-        s_r[e] = live ? (int32_t)(base + i) : 0x7fffffff;
-        // the persistent box over dims 0..2 only: its one reader is k_ct_levels' copy for the
-        // engine's MPT_NN_AUTO spread, whose dims are the first two or three (rrt_engine grid_dims)
-#pragma unroll
-        for (int j = 0; j < (D < 3 ? D : 3); ++j) {
-            unsigned long long mn = live ? okey(x[j]) : ~0ull, mx = live ? okey(x[j]) : 0ull;
-#pragma unroll
-            for (int off = 32; off > 0; off >>= 1) {
-                const unsigned long long omn = __shfl_xor(mn, off), omx = __shfl_xor(mx, off);
-                mn = omn < mn ? omn : mn;
-                mx = omx > mx ? omx : mx;
-            }
-            if ((t & 63) == 0 && mn != ~0ull) {
-                atomicMin(J.ibox + j, mn);
-                atomicMax(J.ibox + kCtMaxDim + j, mx);
-            }
-        }
-        if ((int64_t)(c0 + a * kCtSortThreads + (t & ~63)) < m)  // wave-uniform: a live row in the wave
-            hull_offer<D>(s_plan, x, live, base + (i & ~63), s_rows[t >> 6], J.hull_keys);
-    }
-    __syncthreads();
     uint64_t kh[2], kl[2];
     int32_t kr[2];
 #pragma unroll
     for (int a = 0; a < 2; ++a) {
-        kh[a] = s_h[2 * t + a];
-        kl[a] = s_l[2 * t + a];
-        kr[a] = s_r[2 * t + a];
+        const int i = c0 + 2 * t + a;
+        const bool live = i < m;
+        kh[a] = live ? J.ncode[2 * i] : ~0ull;  // padding sorts last (codes use 126 bits)
+        kl[a] = live ? J.ncode[2 * i + 1] : ~0ull;
+        kr[a] = live ? J.nrow[i] : 0x7fffffff;
     }
 #pragma unroll 1
     for (int k = 2; k <= kCtChunk; k <<= 1) {
@@ -1347,11 +1347,13 @@ template <int D>
 __device__ __forceinline__ float ct_box_lb(const float *__restrict__ b, const double (&qq)[D], const float (&qlo)[D],
                                            const float (&qhi)[D]) {
     if constexpr (D <= 7) {
+        // fused multiply-adds: one rounding a term instead of two, still far inside the shrink
+        // (each gap and each step at most (1 + 2^-24) above the exact value: (1 + 2^-24)^9)
         float s = 0.0f;
 #pragma unroll
         for (int k = 0; k < D; ++k) {
             const float g = fmaxf(fmaxf(b[k] - qhi[k], qlo[k] - b[D + k]), 0.0f);
-            s = s + g * g;
+            s = __builtin_fmaf(g, g, s);
         }
         return s * kCtLbShrink;
     } else {
@@ -1463,6 +1465,22 @@ __device__ __forceinline__ void best_group(double &bd, int32_t &bi) {
     });
     bi = c;
 }
+// x rounded down / up to float (the largest float <= x, the smallest >= x) for finite x: the
+// nearest float, stepped one ulp when it lies on the wrong side -- 7 instructions where the
+// __double2float_rd / _ru library forms took ~14 each (14 conversions a query)
+__device__ __forceinline__ float f32_dn(double x) {
+    const float f = (float)x;
+    const uint32_t b = __float_as_uint(f);
+    const uint32_t nb = f > 0.0f ? b - 1u : (f < 0.0f ? b + 1u : 0x80000001u);
+    return (double)f > x ? __uint_as_float(nb) : f;
+}
+__device__ __forceinline__ float f32_up_any(double x) {
+    const float f = (float)x;
+    const uint32_t b = __float_as_uint(f);
+    const uint32_t nb = f > 0.0f ? b + 1u : (f < 0.0f ? b - 1u : 0x00000001u);
+    return (double)f < x ? __uint_as_float(nb) : f;
+}
+
 // the smallest float >= x (x >= 0): the walk's pruning threshold in float (any box whose
 // lower bound is <= the best squared distance is <= it too)
 __device__ __forceinline__ float f32_up(double x) {
@@ -1513,8 +1531,8 @@ __device__ __forceinline__ void ct_walk(const CellTreeDev &T, const double *__re
     float qlo[D], qhi[D];
 #pragma unroll
     for (int i = 0; i < D; ++i) {
-        qlo[i] = __double2float_rd(qq[i]);
-        qhi[i] = __double2float_ru(qq[i]);
+        qlo[i] = f32_dn(qq[i]);
+        qhi[i] = f32_up_any(qq[i]);
     }
     double bd = __builtin_huge_val();
     int32_t bi = -1;
@@ -1796,23 +1814,27 @@ void CellTree::reserve(int64_t c, int32_t d) {
     hip_check(hipDeviceSynchronize(), "ct init sync");  // the null stream vs the caller's stream
 }
 
+bool CellTree::set_plan(const double *lo, const double *hi, int32_t spatial) {
+    if (!plan) throw Error{1, "cell tree: not reserved"};
+    bool same = plan_set;
+    for (int j = 0; j < dim && same; ++j) same = plan_lo[j] == lo[j] && plan_hi[j] == hi[j];
+    if (same) return false;
+    const CtPlan P = make_ct_plan(dim, lo, hi, spatial);
+    hip_check(hipMemcpy(plan, &P, sizeof(P), hipMemcpyHostToDevice), "ct plan");
+    for (int j = 0; j < dim; ++j) {
+        plan_lo[j] = lo[j];
+        plan_hi[j] = hi[j];
+    }
+    plan_set = true;
+    return true;
+}
+
 CtJob CellTree::prepare(const double *pts, int64_t n_upper, const int64_t *n_dev, int32_t d, const double *lo,
                         const double *hi, int32_t spatial, bool full, int64_t grow, hipStream_t stream,
                         const SpreadOut *spread, unsigned long long *err) {
     if (d != dim || n_upper > cap_) throw Error{1, "cell tree: not reserved for this size"};
     if (n_upper < 1) throw Error{1, "cell tree: empty layout"};
-    bool same = plan_set;
-    for (int j = 0; j < d && same; ++j) same = plan_lo[j] == lo[j] && plan_hi[j] == hi[j];
-    if (!same) {
-        const CtPlan P = make_ct_plan(d, lo, hi, spatial);
-        hip_check(hipMemcpy(plan, &P, sizeof(P), hipMemcpyHostToDevice), "ct plan");
-        for (int j = 0; j < d; ++j) {
-            plan_lo[j] = lo[j];
-            plan_hi[j] = hi[j];
-        }
-        plan_set = true;
-        full = true;
-    }
+    if (set_plan(lo, hi, spatial)) full = true;
     const int old = cur, nw = cur ^ 1;
     const bool reset = full && n_upper <= kCtSeg;
     if (reset) {
@@ -1932,13 +1954,18 @@ void launch_ct_jobs(const CtJob *d_jobs, const CtJob *h_jobs, int32_t n, int32_t
         // (round 4: these four fused into one workgroup a tree ran 0.30-0.40 ms a round at 256
         // seeds and 0.28-0.36 at 32, against 0.27 and 0.15 as separate launches: the codes and
         // seed offers need the waves of many workgroups)
-        // codes and the sort over many CUs: chunks of 512 coded and sorted by a workgroup each,
-        // then every pair's rank across the chunks (round 4: one workgroup a tree sorting in LDS
-        // took 0.12 ms a round at 256 seeds and 0.11 at 32 -- at 32 trees most CUs idle)
+        hipLaunchKernelGGL(by_d(k_ct_ncodes<3>, k_ct_ncodes<7>, k_ct_ncodes<15>), dim3(b256, yn), dim3(64 * kCtWaves), 0,
+                           stream, js);
+        hip_check(hipGetLastError(), "k_ct_ncodes");
+        // the sort over many CUs: chunks of 512 sorted by a workgroup each, then every pair's
+        // rank across the chunks (round 4: one workgroup a tree sorting in LDS took 0.12 ms a
+        // round at 256 seeds and 0.11 at 32 -- at 32 trees most CUs idle).  Round 5, measured and
+        // not kept: the codes computed inside the sort's workgroups (one launch less: 36 -> 47 us
+        // at 32 seeds, half the threads coding; equal at 256), and the directory search folded
+        // into the rank kernel (23 -> 22 us at 32 seeds, 102 -> 129 us at 256: the searches in
+        // chunk order lose the sorted order's cache locality)
         const unsigned chunks = (unsigned)((mb + kCtChunk - 1) / kCtChunk);
-        hipLaunchKernelGGL(by_d(k_ct_csort<3>, k_ct_csort<7>, k_ct_csort<15>), dim3(chunks, yn), dim3(kCtSortThreads),
-                           0, stream, js);
-        hip_check(hipGetLastError(), "k_ct_csort");
+        hipLaunchKernelGGL(k_ct_csort, dim3(chunks, yn), dim3(kCtSortThreads), 0, stream, js);
         hipLaunchKernelGGL(k_ct_crank, dim3(b256, yn), dim3(256), 0, stream, js);
         hipLaunchKernelGGL(k_ct_locate, dim3(b256, yn), dim3(256), 0, stream, js);
         hipLaunchKernelGGL(k_ct_segments, dim3(1, yn), dim3(kCtSegThreads), 0, stream, js);

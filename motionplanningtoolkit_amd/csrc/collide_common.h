@@ -83,10 +83,61 @@ __device__ __forceinline__ void local_box(const double c[3], const double e[3], 
     }
 }
 
+// lane j's float, uniform
+__device__ __forceinline__ float lane_f(float v, int j) {
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), j));
+}
+
 __device__ __forceinline__ bool box_overlap(const float alo[3], const float ahi[3], const float *blo,
                                             const float *bhi) {
     return alo[0] <= bhi[0] && blo[0] <= ahi[0] && alo[1] <= bhi[1] && blo[1] <= ahi[1] && alo[2] <= bhi[2] &&
            blo[2] <= ahi[2];
+}
+
+// Quantized boxes (EnvDev::qitems): 15-bit coordinates over the env root box, rounded outward
+// on the host; a query box quantized outward with a margin of 0.02 quanta beyond its float
+// rounding (see broad.hip walk_two_q), so an overlap test on them keeps every pair the float
+// test keeps.
+struct QBox {
+    uint32_t lxy, hxy, lz, hz;  // query: lo.x | lo.y << 16, hi.x | hi.y << 16, lo.z, hi.z
+};
+__device__ __forceinline__ QBox quantize_box(const EnvDev &env, const float lo[3], const float hi[3]) {
+    uint32_t l[3], h[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        const float vl = floorf((lo[k] - env.q_org[k]) * env.q_scale[k] - 0.02f);
+        const float vh = ceilf((hi[k] - env.q_org[k]) * env.q_scale[k] + 0.02f);
+        l[k] = (uint32_t)fminf(fmaxf(vl, 0.0f), (float)kQMax);
+        h[k] = (uint32_t)fminf(fmaxf(vh, 0.0f), (float)kQMax);
+    }
+    return QBox{l[0] | l[1] << 16, h[0] | h[1] << 16, l[2], h[2]};
+}
+__device__ __forceinline__ bool qbox_overlap(const QBox &q, uint4 it) {
+    constexpr uint32_t H = 0x80008000u;
+    const uint32_t t1 = (q.hxy | H) - it.x;  // query hi >= item lo (x, y)
+    const uint32_t t2 = (it.y | H) - q.lxy;  // item hi >= query lo (x, y)
+    const uint32_t A = (it.z & 0xffff0000u) | q.hz, B = (it.z & 0x0000ffffu) | (q.lz << 16);
+    const uint32_t t3 = (A | H) - B;         // query hi.z >= item lo.z, item hi.z >= query lo.z
+    return (t1 & t2 & t3 & H) == H;
+}
+
+// The top-level items of a two-level quantized env tree (at most 64) that a box may meet: bit i
+// for item i -- k_steer's per-unit link-box mask, which k_pairs' cluster threads of the unit
+// start from instead of all top-level items (every cluster box lies inside its link's box)
+__device__ __forceinline__ uint64_t top_item_mask(const EnvDev &env, const float lo[3], const float hi[3]) {
+    const QBox q = quantize_box(env, lo, hi);
+    const int32_t top = env.n_levels - 1;
+    const int32_t first = env.lev_off[top], n = env.lev_off[top + 1] - first;
+    uint64_t M = 0;
+    for (int32_t i0 = 0; i0 < n; i0 += 8) {
+        uint4 b[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) b[j] = env.qitems[first + (i0 + j < n ? i0 + j : n - 1)];
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+            if (i0 + j < n && qbox_overlap(q, b[j])) M |= 1ull << (i0 + j);
+    }
+    return M;
 }
 
 // --- the fused per-unit walk (collide.hip k_collide; broad.hip k_narrow's overflow re-run) ---

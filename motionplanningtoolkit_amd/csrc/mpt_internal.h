@@ -123,6 +123,9 @@ struct CollideWork {
     // then T), computed by the producer of the poses exactly as unit_transform does, so the
     // stages load it instead of recomputing it per (unit, cluster), header and candidate
     const double *unit_rt;
+    // two-phase path, optional (with live_units, two-level quantized env trees): each unit's
+    // mask of the top-level items its whole-link box meets (top_item_mask), by unit index
+    const uint64_t *unit_tmask;
 };
 
 // Broad-phase candidate: (unit, agent triangle, env triangle) whose float boxes overlap.
@@ -238,15 +241,11 @@ void launch_collide_split(const EnvDev &env, const AgentDev *d_links, int32_t ma
                           OvfDefer *defer = nullptr);
 void launch_pose_edge(const int64_t *d_offsets, int64_t E, int32_t *d_pose_edge, hipStream_t stream);
 
-// Edges whose poses share one rotation (sweep.hip): poses of edge e are [poff[e], poff[e+1]);
-// one wave per (edge, cluster) of the single link d_link[0]; verdict[E] must be zeroed.
-// stats (optional [4]): waves, env item tests, (pair, pose) gate tests, SAT tests.
-void launch_collide_sweep(const EnvDev &env, const AgentDev *d_link, int32_t n_clusters, const double *poses,
-                          const int64_t *poff, int64_t E, uint8_t *verdict, unsigned long long *stats,
-                          hipStream_t stream);
-
-// The same for PRM roadmap edges whose poses the sweep generates in-kernel from the milestones'
-// keys (prm_edges.h PrmEdges; no pose array).
+// Edges whose poses share one rotation and translate along a segment (sweep.hip): PRM roadmap
+// edges, their poses generated in-kernel from the milestones' keys (prm_edges.h PrmEdges; no
+// pose array); one wave an edge (one an (edge, cluster) beyond 64 clusters) of the single link
+// d_link[0]; verdict[E] must be zeroed.  stats (optional [4]): waves, env item tests, (pair,
+// pose) gate tests, SAT tests.
 struct PrmEdges;
 void launch_collide_sweep_prm(const EnvDev &env, const AgentDev *d_link, int32_t n_clusters, const PrmEdges &edges,
                               int64_t E, uint8_t *verdict, unsigned long long *stats, hipStream_t stream);

@@ -74,20 +74,81 @@ struct PrmEdge {
             at(it - 1, t);
         }
     }
-    // f(world translation) for each pose in order until f returns true
+    // translation of pose q of the sequence: it < 1: the start then the end; else pose q of
+    // the main run, then the end (tail)
+    __device__ __forceinline__ void pose(unsigned q, double *t) const {
+        if (it >= 1 && q < it) {
+            at(q, t);
+        } else {
+            const double *src = (it < 1 && q == 0) ? s : end;
+            t[0] = src[0];
+            t[1] = src[1];
+            t[2] = src[2];
+        }
+    }
+    __device__ __forceinline__ unsigned count() const { return it < 1 ? 2u : it + (tail ? 1u : 0u); }
+
+    // f(world translation) for each pose in order until f returns true (one call site of f:
+    // the SAT it carries is inlined once)
     template <class F>
     __device__ __forceinline__ void each(F &&f) const {
-        if (it < 1) {
-            if (f(s)) return;
-            f(end);
-            return;
-        }
-        for (unsigned i = 0; i < it; ++i) {
+        const unsigned n = count();
+        for (unsigned q = 0; q < n; ++q) {
             double t[3];
-            at(i, t);
+            pose(q, t);
             if (f(t)) return;
         }
-        if (tail) f(end);
+    }
+
+    // The same for the poses whose gate with an env triangle can pass.  RQ: the agent triangle
+    // rotated (R Q, before + T); elo / ehi: the env triangle's exact box; env_tf: the env
+    // transform (R rows | T).  Pose i's env-relative translation is T'(i) = envT(s + (step * i)
+    // * dx), which in real arithmetic is T'(0) + i D', D' = step * R_env^T dx: the gate's box
+    // test along dim k then bounds i * D'_k between two numbers, an interval of i.  The interval
+    // is computed in float, widened by eps (1e-5 of the magnitudes involved: ~30x the rounding
+    // of the float and double terms) and by one index either side, so every pose outside it
+    // fails the exact gate; the poses inside run the exact test as before (bit-identical
+    // verdicts).  The per-pose loop over all ~260 poses of a config-4 edge (--bounds rooms: 1.1 G
+    // gate tests a roadmap) becomes a loop over the few poses that cross the env triangle's box.
+    template <class F, class V>
+    __device__ __forceinline__ void each_near(F &&f, const V *RQ, const double *elo, const double *ehi,
+                                              const double *env_tf) const {
+        unsigned q0 = 0, q1 = count();  // poses [q0, q1) of the sequence, then the tail
+        if (it >= 2) {
+            const float d0 = (float)(s[0] - env_tf[9]), d1 = (float)(s[1] - env_tf[10]), d2 = (float)(s[2] - env_tf[11]);
+            float lo = 0.0f, hi = (float)(it - 1);
+#pragma unroll
+            for (int k = 0; k < 3; ++k) {
+                const float rk0 = (float)env_tf[k], rk1 = (float)env_tf[3 + k], rk2 = (float)env_tf[6 + k];
+                const float T0 = rk0 * d0 + rk1 * d1 + rk2 * d2;
+                const float Dk = (float)step * (rk0 * (float)dx[0] + rk1 * (float)dx[1] + rk2 * (float)dx[2]);
+                const float a0 = (float)(&RQ[0].x)[k], a1 = (float)(&RQ[1].x)[k], a2 = (float)(&RQ[2].x)[k];
+                const float a = fminf(a0, fminf(a1, a2)), b = fmaxf(a0, fmaxf(a1, a2));
+                const float el = (float)elo[k], eh = (float)ehi[k];
+                const float eps = 1e-5f * (1.0f + fabsf(T0) + fabsf(Dk) * (float)it + fabsf(a) + fabsf(b) + fabsf(el) +
+                                           fabsf(eh) + fabsf(env_tf[9 + k]) + fabsf(rk0) + fabsf(rk1) + fabsf(rk2));
+                const float u = eh - a - T0 + eps;  // i * D'_k <= u
+                const float l = el - b - T0 - eps;  // i * D'_k >= l
+                if (Dk > 0.0f) {
+                    lo = fmaxf(lo, l / Dk);
+                    hi = fminf(hi, u / Dk);
+                } else if (Dk < 0.0f) {
+                    lo = fmaxf(lo, u / Dk);
+                    hi = fminf(hi, l / Dk);
+                } else if (l > 0.0f || u < 0.0f) {
+                    hi = -4.0f;  // this dim never overlaps
+                }
+            }
+            q0 = hi >= lo - 2.0f ? (unsigned)fmaxf(0.0f, floorf(lo) - 1.0f) : it;
+            q1 = hi >= lo - 2.0f ? (unsigned)fminf((float)it, ceilf(hi) + 2.0f) : it;
+            if (q1 < q0) q1 = q0;
+        }
+        const unsigned n = (q1 - q0) + (it >= 2 && tail ? 1u : 0u);
+        for (unsigned j = 0; j < n; ++j) {
+            double t[3];
+            pose(q0 + j < q1 ? q0 + j : it, t);  // past the run: the tail (index it)
+            if (f(t)) return;
+        }
     }
 };
 

@@ -286,7 +286,14 @@ struct LiveOut {
     int32_t *q_count;    // the round's QueryOrder counts (read by the NN launch): zeroed here
     int32_t q_nb;
     double *unit_rt;     // [K * pmax * L][12]: each unit's relative transform (CollideWork::unit_rt)
+    uint64_t *tmask;     // [K * pmax * L]: each unit's top-level item mask (CollideWork::unit_tmask), or nullptr
 };
+
+// the per-unit top-level masks apply: a two-level quantized env tree of at most 64 top items
+// (k_pairs' quantized LDS walk)
+inline bool tmask_applies(const EnvDev &env) {
+    return env.qitems != nullptr && env.n_levels <= 2 && env.lev_off[env.n_levels] - env.lev_off[env.n_levels - 1] <= 64;
+}
 
 // randomSteer + getPoses, then the extension's live units appended to the round's list
 // (one device atomic per workgroup; the list order does not matter to any verdict).
@@ -315,7 +322,11 @@ __global__ __launch_bounds__(256) void k_steer(EngineParams p, uint64_t ext_base
             for (int j = 0; j < 3; ++j) rt[9 + j] = T[j];
             float blo[3], bhi[3];
             local_box(lv.links[l].bc, lv.links[l].be, R, T, blo, bhi);
-            if (box_overlap(blo, bhi, lv.env.root_lo, lv.env.root_hi)) mask |= 1ull << (i * p.L + l);
+            const bool ov = box_overlap(blo, bhi, lv.env.root_lo, lv.env.root_hi);
+            if (ov) mask |= 1ull << (i * p.L + l);
+            // every unit's mask (a chunked collide walks units off the list too; a unit that
+            // misses the root box has no top-level item to meet)
+            if (lv.tmask) lv.tmask[k * units + i * p.L + l] = ov ? top_item_mask(lv.env, blo, bhi) : 0ull;
         }
     __shared__ uint32_t s_wave[4];
     __shared__ uint32_t s_base;
@@ -541,7 +552,11 @@ __global__ __launch_bounds__(256) void k_steer_jobs(EngineParams p, const Engine
             for (int j = 0; j < 3; ++j) rt[9 + j] = T[j];
             float blo[3], bhi[3];
             local_box(lv.links[l].bc, lv.links[l].be, R, T, blo, bhi);
-            if (box_overlap(blo, bhi, lv.env.root_lo, lv.env.root_hi)) mask |= 1ull << (i * p.L + l);
+            const bool ov = box_overlap(blo, bhi, lv.env.root_lo, lv.env.root_hi);
+            if (ov) mask |= 1ull << (i * p.L + l);
+            // every unit's mask (a chunked collide walks units off the list too; a unit that
+            // misses the root box has no top-level item to meet)
+            if (lv.tmask) lv.tmask[ge * units + i * p.L + l] = ov ? top_item_mask(lv.env, blo, bhi) : 0ull;
         }
     __shared__ uint32_t s_wave[4];
     __shared__ uint32_t s_base;
@@ -620,6 +635,7 @@ struct mpt_rrt {
     double *d_samples = nullptr, *d_ends = nullptr, *d_poses = nullptr, *d_nnd2 = nullptr;
     int32_t *d_nn = nullptr, *d_pcount = nullptr;
     int32_t *d_live = nullptr;     // k_steer's live-unit list [K * pmax * L] (two-phase collide)
+    uint64_t *d_tmask = nullptr;   // k_steer's per-unit top-level item masks [K * pmax * L]
     double *d_rt = nullptr;        // k_steer's unit relative transforms [K * pmax * L][12] (two-phase)
     uint32_t *d_nlive = nullptr;   // its length
     uint8_t *d_verdict = nullptr;
@@ -681,10 +697,42 @@ struct mpt_rrt {
 };
 
 namespace {
+// Mapped pinned slots for the engines' spread words (6 u64 each), carved from shared chunks:
+// one hipHostMalloc per 1024 engines instead of one per engine (config 5 starts 256 engines in
+// its first round; each pinned allocation costs far more than a round of kernels)
+struct PinnedSlots {
+    std::mutex mu;
+    std::vector<unsigned long long *> free_slots;
+    static constexpr int kSlotWords = 8, kSlots = 1024;
+    void take(unsigned long long **host, unsigned long long **dev) {
+        std::lock_guard<std::mutex> lk(mu);
+        if (free_slots.empty()) {
+            unsigned long long *chunk = nullptr;
+            hip_check(hipHostMalloc(&chunk, sizeof(unsigned long long) * kSlotWords * kSlots,
+                                    hipHostMallocMapped | hipHostMallocCoherent), "alloc spread slots");
+            for (int i = kSlots - 1; i >= 0; --i) free_slots.push_back(chunk + (size_t)i * kSlotWords);
+        }
+        *host = free_slots.back();
+        free_slots.pop_back();
+        hip_check(hipHostGetDevicePointer(reinterpret_cast<void **>(dev), *host, 0), "spread device pointer");
+    }
+    void give(unsigned long long *host) {
+        std::lock_guard<std::mutex> lk(mu);
+        free_slots.push_back(host);
+    }
+};
+PinnedSlots &pinned_slots() {
+    static PinnedSlots *p = new PinnedSlots();  // never freed: engines may outlive static destruction order
+    return *p;
+}
+
+}  // namespace
+
+namespace {
 void rfree(mpt_rrt *r) {
     void *ps[] = {r->d_links, r->d_nodes,   r->d_parents, r->d_n,       r->d_counters, r->d_samples,
                   r->d_ends,  r->d_poses,   r->d_nnd2,    r->d_nn,      r->d_pcount,
-                  r->d_verdict, r->d_scratch, r->d_cstats, r->d_live, r->d_nlive, r->d_rt, r->d_bar};
+                  r->d_verdict, r->d_scratch, r->d_cstats, r->d_live, r->d_nlive, r->d_rt, r->d_bar, r->d_tmask};
     for (void *p : ps)
         if (p) (void)hipFree(p);
     for (auto &e : r->ring)
@@ -692,7 +740,7 @@ void rfree(mpt_rrt *r) {
     if (r->d_spread) (void)hipFree(r->d_spread);
     if (r->d_qcount) (void)hipFree(r->d_qcount);
     if (r->d_qlist) (void)hipFree(r->d_qlist);
-    if (r->h_spread) (void)hipHostFree(r->h_spread);
+    if (r->h_spread) pinned_slots().give(r->h_spread);
     if (r->ev_spread) (void)hipEventDestroy(r->ev_spread);
 }
 
@@ -715,7 +763,7 @@ void ensure_round_buffers(mpt_rrt *r, int32_t K) {
     const size_t need_scratch = nn_knn_scratch_bytes(K, std::max<int64_t>(r->cap, 1), 1);
     if (K > r->kcap) {
         void *ps[] = {r->d_samples, r->d_ends, r->d_poses, r->d_nnd2, r->d_nn, r->d_pcount, r->d_verdict, r->d_live,
-                      r->d_rt};
+                      r->d_rt, r->d_tmask};
         for (void *p : ps)
             if (p) hip_check(hipFree(p), "hipFree");
         const int64_t d = r->p.d;
@@ -728,6 +776,7 @@ void ensure_round_buffers(mpt_rrt *r, int32_t K) {
         hip_check(hipMalloc(&r->d_verdict, (size_t)K), "alloc verdict");
         hip_check(hipMalloc(&r->d_live, sizeof(int32_t) * (int64_t)K * r->p.pmax * r->p.L), "alloc live units");
         hip_check(hipMalloc(&r->d_rt, sizeof(double) * 12 * (int64_t)K * r->p.pmax * r->p.L), "alloc unit transforms");
+        hip_check(hipMalloc(&r->d_tmask, sizeof(uint64_t) * (int64_t)K * r->p.pmax * r->p.L), "alloc unit masks");
         if (!r->d_nlive) hip_check(hipMalloc(&r->d_nlive, sizeof(uint32_t)), "alloc live count");
         r->kcap = K;
         r->cscratch.ensure((int64_t)K * r->p.pmax * r->p.L, r->max_clusters);
@@ -952,19 +1001,13 @@ bool spread_request(mpt_rrt *r, bool indexed, SpreadOut &spread) {
                       (!r->spread_seen || r->rounds_since_spread >= kSpreadEvery);
     ++r->rounds_since_spread;
     if (!want) return false;
-    if (!r->d_spread) {
-        // the grid build's per-block partials [ceil(cap / 256)][6]
-        const int64_t blocks = (r->cap + 255) / 256;
-        hip_check(hipMalloc(&r->d_spread, sizeof(unsigned long long) * blocks * 6), "alloc spread");
-        hip_check(hipHostMalloc(&r->h_spread, sizeof(unsigned long long) * 6,
-                                hipHostMallocMapped | hipHostMallocCoherent), "alloc spread");
-        hip_check(hipHostGetDevicePointer(reinterpret_cast<void **>(&r->h_spread_dev), r->h_spread, 0),
-                  "spread device pointer");
+    if (!r->h_spread) {
+        pinned_slots().take(&r->h_spread, &r->h_spread_dev);
         hip_check(hipEventCreateWithFlags(&r->ev_spread, hipEventDisableTiming), "event");
     }
     spread.gd = r->grid_gd;
     for (int j = 0; j < 3; ++j) spread.dims[j] = r->grid_dims[j];
-    spread.partial = r->d_spread;
+    spread.partial = r->d_spread;  // the grid build's per-block partials (step_head allocates them)
     spread.host_out = r->h_spread_dev;
     return true;
 }
@@ -1075,6 +1118,12 @@ StepCtx step_head(mpt_rrt *r, int32_t K, hipStream_t stream, bool defer_tree = f
             gen.counters = r->d_counters;
             gen.n_live = live_list ? r->d_nlive : nullptr;
         }
+        if (want_spread && !r->d_spread) {
+            // the grid build's per-block partials [ceil(cap / 256)][6]
+            const int64_t blocks = (r->cap + 255) / 256;
+            hip_check(hipMalloc(&r->d_spread, sizeof(unsigned long long) * blocks * 6), "alloc spread");
+            spread.partial = r->d_spread;
+        }
         r->grid->build(r->d_nodes, r->n_upper, r->d_n, p.d, g, stream, want_spread ? &spread : nullptr,
                        c.qo.list ? &qb : nullptr);
     }
@@ -1136,7 +1185,8 @@ void step_tail(mpt_rrt *r, int32_t K, hipStream_t stream, const StepCtx &c) {
     hipEvent_t *ev = c.ev;
     auto steer = p.kind == MPT_AGENT_OMNI ? k_steer<MPT_AGENT_OMNI>
                  : (p.kind == MPT_AGENT_BLIMP ? k_steer<MPT_AGENT_BLIMP> : k_steer<MPT_AGENT_SNAKE>);
-    LiveOut lv{live_list ? r->d_live : nullptr, r->d_nlive, r->d_links, r->env, c.qo.count, c.qo.nb, r->d_rt};
+    uint64_t *tm = live_list && tmask_applies(r->env) ? r->d_tmask : nullptr;
+    LiveOut lv{live_list ? r->d_live : nullptr, r->d_nlive, r->d_links, r->env, c.qo.count, c.qo.nb, r->d_rt, tm};
     hipLaunchKernelGGL(steer, dim3(kb), dim3(256), 0, stream, p, r->ext_base, K, r->d_nodes, r->d_nn, r->d_ends,
                        r->d_poses, r->d_pcount, r->d_verdict, r->d_counters, lv);
     hip_check(hipGetLastError(), "k_steer");
@@ -1152,6 +1202,7 @@ void step_tail(mpt_rrt *r, int32_t K, hipStream_t stream, const StepCtx &c) {
     cw.stats = r->stats_on ? r->d_cstats : nullptr;
     cw.live_units = live_list ? r->d_live : nullptr;
     cw.unit_rt = live_list ? r->d_rt : nullptr;  // k_steer writes them with the live list
+    cw.unit_tmask = tm;
     cw.n_live = live_list ? r->d_nlive : nullptr;
     OvfDefer ovf{};
     if (collide_mode() == MPT_COLLIDE_FUSED) {
@@ -1217,6 +1268,7 @@ struct JointNN {
     int64_t r_edges = 0, r_units = 0;
     int32_t r_dim = 0, r_subs = 0;
     double *j_samples = nullptr, *j_ends = nullptr, *j_poses = nullptr, *j_nnd2 = nullptr, *j_rt = nullptr;
+    uint64_t *j_tmask = nullptr;
     int32_t *j_nn = nullptr, *j_pcount = nullptr, *j_live = nullptr;
     uint8_t *j_verdict = nullptr;
     uint32_t *j_nlive = nullptr;
@@ -1255,12 +1307,14 @@ char *joint_stage(JointNN &g, size_t bytes, int *slot) {
     if (bytes > g.cap) {
         hip_check(hipDeviceSynchronize(), "sync");  // buffers may still be in use
         if (g.d_stage) hip_check(hipFree(g.d_stage), "free");
-        for (int i = 0; i < kJobRing; ++i)
-            if (g.h_stage[i]) hip_check(hipHostFree(g.h_stage[i]), "free");
+        if (g.h_stage[0]) hip_check(hipHostFree(g.h_stage[0]), "free");  // the ring's one allocation
         const size_t c = std::max(bytes, 2 * g.cap);
         hip_check(hipMalloc(&g.d_stage, c), "stage");
+        // the ring's buffers carved from one pinned allocation (one hipHostMalloc, not kJobRing)
+        char *ring = nullptr;
+        hip_check(hipHostMalloc(&ring, c * kJobRing), "stage pinned");
         for (int i = 0; i < kJobRing; ++i) {
-            hip_check(hipHostMalloc(&g.h_stage[i], c), "stage pinned");
+            g.h_stage[i] = ring + (size_t)i * c;
             if (!g.copied[i]) hip_check(hipEventCreateWithFlags(&g.copied[i], hipEventDisableTiming), "event");
         }
         if (!g.done) hip_check(hipEventCreateWithFlags(&g.done, hipEventDisableTiming), "event");
@@ -1276,9 +1330,11 @@ char *joint_stage(JointNN &g, size_t bytes, int *slot) {
 
 void joint_free_round(JointNN &g) {
     for (void *p : {(void *)g.j_samples, (void *)g.j_ends, (void *)g.j_poses, (void *)g.j_nnd2, (void *)g.j_rt,
-                    (void *)g.j_nn, (void *)g.j_pcount, (void *)g.j_live, (void *)g.j_verdict, (void *)g.j_nlive})
+                    (void *)g.j_nn, (void *)g.j_pcount, (void *)g.j_live, (void *)g.j_verdict, (void *)g.j_nlive,
+                    (void *)g.j_tmask})
         if (p) hip_check(hipFree(p), "free");
     g.j_samples = g.j_ends = g.j_poses = g.j_nnd2 = g.j_rt = nullptr;
+    g.j_tmask = nullptr;
     g.j_nn = g.j_pcount = g.j_live = nullptr;
     g.j_verdict = nullptr;
     g.j_nlive = nullptr;
@@ -1329,6 +1385,7 @@ void joint_round(mpt_rrt *const *rs, int32_t n, int32_t K, void *const *streams_
         hip_check(hipMalloc(&g.j_ends, sizeof(double) * edges * d), "joint ends");
         hip_check(hipMalloc(&g.j_poses, sizeof(double) * 12 * edges * units), "joint poses");
         hip_check(hipMalloc(&g.j_rt, sizeof(double) * 12 * edges * units), "joint unit transforms");
+        hip_check(hipMalloc(&g.j_tmask, sizeof(uint64_t) * edges * units), "joint unit masks");
         hip_check(hipMalloc(&g.j_nnd2, sizeof(double) * edges), "joint nn d2");
         hip_check(hipMalloc(&g.j_nn, sizeof(int32_t) * edges), "joint nn");
         hip_check(hipMalloc(&g.j_pcount, sizeof(int32_t) * edges), "joint pose counts");
@@ -1423,7 +1480,8 @@ void joint_round(mpt_rrt *const *rs, int32_t n, int32_t K, void *const *streams_
     if (timed) hip_check(hipEventRecord(g.t1, joint), "joint t1");
     auto steer = p.kind == MPT_AGENT_OMNI ? k_steer_jobs<MPT_AGENT_OMNI>
                  : (p.kind == MPT_AGENT_BLIMP ? k_steer_jobs<MPT_AGENT_BLIMP> : k_steer_jobs<MPT_AGENT_SNAKE>);
-    LiveOut lv{g.j_live, g.j_nlive, a->d_links, a->env, nullptr, 0, g.j_rt};
+    uint64_t *tm = tmask_applies(a->env) ? g.j_tmask : nullptr;
+    LiveOut lv{g.j_live, g.j_nlive, a->d_links, a->env, nullptr, 0, g.j_rt, tm};
     hipLaunchKernelGGL(steer, dim3(kb, n), dim3(256), 0, joint, p, de, K, g.j_nn, g.j_ends, g.j_poses, g.j_pcount,
                        g.j_verdict, lv, per_sub);
     hip_check(hipGetLastError(), "k_steer_jobs");
@@ -1443,6 +1501,7 @@ void joint_round(mpt_rrt *const *rs, int32_t n, int32_t K, void *const *streams_
         cw.live_units = g.j_live + e0 * units;
         cw.n_live = g.j_nlive + b;
         cw.unit_rt = g.j_rt + e0 * units * 12;
+        cw.unit_tmask = tm ? tm + e0 * units : nullptr;
         launch_collide_split(a->env, a->d_links, a->max_clusters, cw, g.cs, joint, nullptr, nullptr);
     }
     mark(5);
@@ -1644,10 +1703,9 @@ extern "C" mpt_status mpt_rrt_joint_release(void *joint_stream) {
         hip_check(hipStreamSynchronize((hipStream_t)joint_stream), "joint stream sync");
         if (g_last_timed == g.get()) g_last_timed = nullptr;
         if (g->d_stage) hip_check(hipFree(g->d_stage), "free");
-        for (int i = 0; i < kJobRing; ++i) {
-            if (g->h_stage[i]) hip_check(hipHostFree(g->h_stage[i]), "free");
+        if (g->h_stage[0]) hip_check(hipHostFree(g->h_stage[0]), "free");  // the ring's one allocation
+        for (int i = 0; i < kJobRing; ++i)
             if (g->copied[i]) hip_check(hipEventDestroy(g->copied[i]), "event");
-        }
         for (hipEvent_t e : g->joins) hip_check(hipEventDestroy(e), "event");
         for (hipEvent_t e : {g->done, g->built, g->b0, g->t0, g->t1})
             if (e) hip_check(hipEventDestroy(e), "event");
@@ -1758,6 +1816,13 @@ extern "C" mpt_status mpt_rrt_set_nn(mpt_rrt *r, int32_t mode, double points_per
         if (!r || mode < MPT_NN_AUTO || mode > MPT_NN_TREE) throw Error{MPT_ERR_INVALID, "bad arguments"};
         r->nn_mode = mode;
         r->ppc = points_per_cell > 0 ? points_per_cell : 0.0;
+        // the cell tree's memory for the engine's capacity, now rather than in a round (it
+        // allocates and synchronises the device): when its rounds will use the tree -- MPT_NN_TREE,
+        // or MPT_NN_AUTO once the first nodes' spread chose it (mpt_rrt_add_nodes)
+        if (mode == MPT_NN_TREE || (mode == MPT_NN_AUTO && r->spread_seen && r->auto_tree)) {
+            r->ctree->reserve(r->cap, r->p.d);
+            (void)r->ctree->set_plan(r->p.lo, r->p.hi, r->grid_gd);  // the first build then starts from it
+        }
     });
 }
 

@@ -36,8 +36,9 @@ __device__ __forceinline__ void env_rel_t(const EnvDev &env, const double *t, do
 }
 
 // One (edge, cluster): Rw = the edge's world rotation, tf / tl = world translations of its
-// first and last pose, gen(f) calls f(world translation) for each pose in order and stops
-// when f returns true (a contact).
+// first and last pose, gen(f, RQ, E, env) calls f(world translation) for each pose in order
+// whose gate with env triangle E may pass (every pose, or a superset of those) and stops when f
+// returns true (a contact).
 template <class Gen>
 __device__ __forceinline__ void sweep_core(const EnvDev &env, const AgentDev &ag, int32_t cl, const double *Rw,
                                            const double *tf, const double *tl, Gen gen, uint8_t *flag, int lane,
@@ -124,7 +125,7 @@ __device__ __forceinline__ void sweep_core(const EnvDev &env, const AgentDev &ag
                         ++cnt.sat;
                         hit = tri_intersect(E, Q1, Q2, Q3);
                         return hit;
-                    });
+                    }, RQ, E, env);
                 }
                 if (__ballot(hit)) {
                     if (lane == 0) __hip_atomic_store(flag, (uint8_t)1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -207,47 +208,63 @@ __device__ __forceinline__ void sweep_edge_core(const EnvDev &env, const AgentDe
     for (;;) {
         bool keep = false;
         int32_t cf = 0, cc = 0;
+        float ilo[3] = {0, 0, 0}, ihi[3] = {0, 0, 0};
         if (lane < count) {
             const Item it = env.items[first + lane];
             keep = box_overlap(ulo, uhi, it.lo, it.hi);
             cf = it.first;
             cc = it.count;
+#pragma unroll
+            for (int k = 0; k < 3; ++k) {
+                ilo[k] = it.lo[k];
+                ihi[k] = it.hi[k];
+            }
         }
         cnt.items += (uint32_t)count;
         uint64_t m = __ballot(keep);
         if (lev == 0) {
-            while (m) {  // env triangles meeting the union: fan out to the clusters meeting them
-                const int j = __ffsll((unsigned long long)m) - 1;
-                m &= m - 1;
-                const int32_t t = first + j;
-                const Item ti = env.items[t];  // level 0: item index = triangle index
-                uint64_t cm = __ballot(lane < ncl && box_overlap(clo, chi, ti.lo, ti.hi));
-                while (cm) {
-                    const int ci = __ffsll((unsigned long long)cm) - 1;
-                    cm &= cm - 1;
-                    if (load_flag(flag)) return;
-                    const Cluster c = ag.clusters[ci];
-                    const bool act = lane < c.count;
-                    v3 RQ[3] = {mk(0, 0, 0), mk(0, 0, 0), mk(0, 0, 0)};
-                    bool near = false;
-                    if (act) {  // the lane's triangle rotated once (R Q, xform's order before the + T)
-                        const double *tr = ag.tris + (int64_t)(c.first + lane) * 9;
+            // the bucket's env triangles meeting the union (lane j: triangle first + j): lane c
+            // (a cluster) collects those its swept box meets, then the wave visits each such
+            // cluster once -- its triangles rotated once for every triangle of the bucket it
+            // meets (round 4 rotated a cluster again for each env triangle, after a load of the
+            // edge's verdict flag no other wave writes here: one wave an edge)
+            uint64_t Tm = 0;
+            for (uint64_t mm = m; mm; mm &= mm - 1) {
+                const int j = __ffsll((unsigned long long)mm) - 1;
+                const float elo[3] = {lane_f(ilo[0], j), lane_f(ilo[1], j), lane_f(ilo[2], j)};
+                const float ehi[3] = {lane_f(ihi[0], j), lane_f(ihi[1], j), lane_f(ihi[2], j)};
+                if (lane < ncl && box_overlap(clo, chi, elo, ehi)) Tm |= 1ull << j;
+            }
+            for (uint64_t C = __ballot(Tm != 0); C; C &= C - 1) {
+                const int ci = __ffsll((unsigned long long)C) - 1;
+                uint64_t Tc = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(Tm >> 32), ci) << 32) |
+                              (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)Tm, ci);
+                const Cluster c = ag.clusters[ci];
+                const bool act = lane < c.count;
+                v3 RQ[3] = {mk(0, 0, 0), mk(0, 0, 0), mk(0, 0, 0)};
+                float tlo[3] = {0, 0, 0}, thi[3] = {0, 0, 0};
+                if (act) {  // the lane's triangle rotated once (R Q, xform's order before the + T)
+                    const double *tr = ag.tris + (int64_t)(c.first + lane) * 9;
 #pragma unroll
-                        for (int v = 0; v < 3; ++v) {
-                            const double x = tr[3 * v], y = tr[3 * v + 1], z = tr[3 * v + 2];
-                            RQ[v] = mk(R[0] * x + R[1] * y + R[2] * z, R[3] * x + R[4] * y + R[5] * z,
-                                       R[6] * x + R[7] * y + R[8] * z);
-                        }
-                        float tlo[3], thi[3];  // its box swept along the edge
-#pragma unroll
-                        for (int k = 0; k < 3; ++k) {
-                            const double a0 = (&RQ[0].x)[k], a1 = (&RQ[1].x)[k], a2 = (&RQ[2].x)[k];
-                            const double mn = dmin(a0, dmin(a1, a2)), mx = dmax(a0, dmax(a1, a2));
-                            tlo[k] = widen_lo(dmin(mn + T0[k], mn + TN[k]));
-                            thi[k] = widen_hi(dmax(mx + T0[k], mx + TN[k]));
-                        }
-                        near = box_overlap(tlo, thi, ti.lo, ti.hi);
+                    for (int v = 0; v < 3; ++v) {
+                        const double x = tr[3 * v], y = tr[3 * v + 1], z = tr[3 * v + 2];
+                        RQ[v] = mk(R[0] * x + R[1] * y + R[2] * z, R[3] * x + R[4] * y + R[5] * z,
+                                   R[6] * x + R[7] * y + R[8] * z);
                     }
+#pragma unroll
+                    for (int k = 0; k < 3; ++k) {  // its box swept along the edge
+                        const double a0 = (&RQ[0].x)[k], a1 = (&RQ[1].x)[k], a2 = (&RQ[2].x)[k];
+                        const double mn = dmin(a0, dmin(a1, a2)), mx = dmax(a0, dmax(a1, a2));
+                        tlo[k] = widen_lo(dmin(mn + T0[k], mn + TN[k]));
+                        thi[k] = widen_hi(dmax(mx + T0[k], mx + TN[k]));
+                    }
+                }
+                for (; Tc; Tc &= Tc - 1) {
+                    const int j = __ffsll((unsigned long long)Tc) - 1;
+                    const int32_t t = first + j;  // level 0: item index = triangle index
+                    const float elo[3] = {lane_f(ilo[0], j), lane_f(ilo[1], j), lane_f(ilo[2], j)};
+                    const float ehi[3] = {lane_f(ihi[0], j), lane_f(ihi[1], j), lane_f(ihi[2], j)};
+                    const bool near = act && box_overlap(tlo, thi, elo, ehi);
                     if (!__ballot(near)) continue;
                     const EnvTri &E = env.tris[t];
                     bool hit = false;
@@ -263,7 +280,7 @@ __device__ __forceinline__ void sweep_edge_core(const EnvDev &env, const AgentDe
                             ++cnt.sat;
                             hit = tri_intersect(E, Q1, Q2, Q3);
                             return hit;
-                        });
+                        }, RQ, E, env);
                     }
                     if (__ballot(hit)) {
                         if (lane == 0) __hip_atomic_store(flag, (uint8_t)1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -296,33 +313,36 @@ __device__ __forceinline__ void sweep_edge_core(const EnvDev &env, const AgentDe
 
 // Where an edge's poses come from.  A source's edge(e, core) calls core(Rw, tf, tl, gen) with
 // the edge's world rotation, its first and last pose's translation and the pose generator
-// (gen(f): f(world translation) for each pose in order until f returns true), or returns
+// (gen(f, RQ, E, env): f(world translation) for each pose in order until f returns true --
+// every pose whose translated triangle RQ + T may meet env triangle E's box), or returns
 // without calling it when the edge has no poses.
-// A pose array: edge e's poses are [poff[e], poff[e + 1]) of poses [P][12] (R|T).
-struct PoseArraySrc {
-    const double *poses;
-    const int64_t *poff;
-    template <class Core>
-    __device__ __forceinline__ void edge(int64_t e, Core &&core) const {
-        const int64_t p0 = poff[e], p1 = poff[e + 1];
-        if (p1 <= p0) return;
-        core(poses + p0 * 12, poses + p0 * 12 + 9, poses + (p1 - 1) * 12 + 9, [&](auto &&f) {
-            for (int64_t p = p0; p < p1; ++p)
-                if (f(poses + p * 12 + 9)) return;
-        });
-    }
-};
 // A PRM roadmap edge (prm_edges.h): the poses generated from the two milestones' keys with the
-// pose stage's operations -- no pose array (config 4: ~20-130 M poses a roadmap)
+// pose stage's operations -- no pose array (config 4: ~20-115 M poses a roadmap) -- and, for a
+// (triangle, env triangle) pair, only those whose gate can pass (PrmEdge::each_near)
 struct PrmSrc {
     PrmEdges P;
     template <class Core>
     __device__ __forceinline__ void edge(int64_t e, Core &&core) const {
-        const PrmEdge g = prm_edge(P, e);
+        PrmEdge g = prm_edge(P, e);
+        // one edge a wave: every field is wave-uniform -- scalar registers, not ~40 VGPRs held
+        // across the walk and the SAT
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            g.s[k] = uniform_d(g.s[k]);
+            g.end[k] = uniform_d(g.end[k]);
+            g.dx[k] = uniform_d(g.dx[k]);
+        }
+#pragma unroll
+        for (int k = 0; k < 9; ++k) g.R[k] = uniform_d(g.R[k]);
+        g.step = uniform_d(g.step);
+        g.it = __builtin_amdgcn_readfirstlane(g.it);
+        g.tail = __builtin_amdgcn_readfirstlane((int)g.tail) != 0;
         double tf[3], tl[3];
         g.first(tf);
         g.last(tl);
-        core(g.R, tf, tl, [&](auto &&f) { g.each(f); });
+        core(g.R, tf, tl, [&](auto &&f, const v3 *RQ, const EnvTri &E, const EnvDev &env) {
+            g.each_near(f, RQ, E.lo, E.hi, env.tf);
+        });
     }
 };
 
@@ -408,7 +428,7 @@ __global__ __launch_bounds__(kSweepWaves * 64) void k_sweep_lite(EnvDev env, con
             for (unsigned s = 0; s < steps; ++s)
                 for (int k = 0; k < 3; ++k) tl[k] = tl[k] + vs[k];
             sweep_core(env, link[0], cl, ti, tf, tl,
-                       [&](auto &&f) {
+                       [&](auto &&f, const v3 *, const EnvTri &, const EnvDev &) {
                            double t[3] = {v1[0], v1[1], v1[2]};
                            for (unsigned s = 0; s < steps; ++s) {
                                for (int k = 0; k < 3; ++k) t[k] = t[k] + vs[k];
@@ -456,12 +476,6 @@ static void launch_sweep_src(const EnvDev &env, const AgentDev *d_link, int32_t 
     hipLaunchKernelGGL(k_sweep<Src>, dim3((unsigned)blocks), dim3(kSweepWaves * 64), 0, stream, env, d_link, src, E,
                        n_clusters, verdict, stats);
     hip_check(hipGetLastError(), "k_sweep launch");
-}
-
-void launch_collide_sweep(const EnvDev &env, const AgentDev *d_link, int32_t n_clusters, const double *poses,
-                          const int64_t *poff, int64_t E, uint8_t *verdict, unsigned long long *stats,
-                          hipStream_t stream) {
-    launch_sweep_src(env, d_link, n_clusters, PoseArraySrc{poses, poff}, E, verdict, stats, stream);
 }
 
 void launch_collide_sweep_prm(const EnvDev &env, const AgentDev *d_link, int32_t n_clusters, const PrmEdges &edges,

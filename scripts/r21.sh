@@ -14,6 +14,21 @@ for n in 32 256; do
   timeout -k 10 200 python bench.py --seeds $n --steps 25 --warmup 5 --no-cpu --detail $O/c5_${n}_detail.json > $O/c5_$n.json || exit 1
 done
 [ -n "$NO_PRM" ] || timeout -k 10 300 python scripts/bench_prm.py --reps 3 --no-cpu > $O/prm.json || exit 1
+if [ -n "$SCRATCH" ]; then
+  for w in none stream group; do
+    for n in 32 256; do timeout -k 10 200 python scripts/scratch_rounds.py --seeds $n --warm $w > $O/scratch_${n}_$w.json || exit 1; cat $O/scratch_${n}_$w.json; done
+  done
+fi
+if [ -n "$HIPT" ]; then  # HIP API time of a run from the start states (first-round costs)
+  timeout -k 10 200 rocprofv3 --hip-trace --stats --output-format csv -d $O/hipt -o ht -- python scripts/scratch_rounds.py --seeds 32 --rounds 3 > $O/hipt.log 2>&1 || exit 1
+fi
+if [ -n "$KT" ]; then  # per-round kernel sums over rounds 10..19 of a kernel trace (scripts/kt_last.py)
+  for n in 32 256; do
+    timeout -k 10 200 rocprofv3 --kernel-trace --output-format csv -d $O/c$n -o kt -- python bench.py --seeds $n --steps 25 --warmup 5 --no-cpu --detail $O/kt_detail.json > $O/kt$n.log 2>&1 || exit 1
+    python scripts/kt_last.py $O/c$n/kt_kernel_trace.csv --rounds k_sample_jobs 10 20 > $O/rounds_$n.txt || exit 1
+    rm -f $O/c$n/kt_kernel_trace.csv
+  done
+fi
 python - $O <<'PY'
 import json, sys
 o = sys.argv[1]
