@@ -554,6 +554,31 @@ def run_seeds(args, world, rank, dist, torch, mpt, multiseed, scenes):
             for f in [pool.submit(drive, g) for g in groups]:
                 f.result()
 
+    # The process's one-time HIP start-up before it: the joint round's kernels launched once (a
+    # throwaway two-engine group on its own joint stream) and the streams' first work.  The first
+    # launch of each kernel in a process and a stream's first work cost ~13 ms (scripts/
+    # scratch_rounds.py: round 0 of 32 seeds 13.4 ms cold, 0.76 ms warm) -- once per process, not
+    # per planner run -- so from_scratch measures the planner's rounds, and process_warmup_s
+    # reports the start-up beside it.
+    t_warm = time.perf_counter()
+    for s_ in streams + [js for _, _, js in jgroups]:
+        with torch.cuda.stream(s_):
+            torch.zeros(1, device="cuda").add_(1)
+    if not args.no_joint_nn and engines:
+        tmp = []
+        for i in range(2):
+            e = mpt.RRTEngine(env, agent, sc.kind, sc.prm, sc.ranges, sc.steer_dt, sc.cc_dt, 1 + 2 * K, args.seed + i)
+            e.add_nodes(seed_start(args.seed + i, env, agent, mpt, args.seed_start))
+            e.set_nn(args.nn, args.ppc)
+            tmp.append(e)
+        ws = torch.cuda.Stream()
+        mpt.step_many(tmp, K, [ws] * 2, ws)
+        torch.cuda.synchronize()
+        for e in tmp:
+            e.close()
+        mpt.joint_release(ws)
+    torch.cuda.synchronize()
+    process_warmup = time.perf_counter() - t_warm
     # from scratch: every round from the seeds' start states (the first rounds' index
     # reservations included), then the timed rounds continue the same trees
     if dist:
@@ -693,9 +718,11 @@ def run_seeds(args, world, rank, dist, torch, mpt, multiseed, scenes):
         "seeds_digest": all_digest,
         "world_size": dist.get_world_size() if dist else 1,
         "from_scratch": {"rounds": args.warmup + args.steps, "wall_s": round(scratch, 4),
-                         "valid_per_s": valid_all / scratch,
+                         "valid_per_s": valid_all / scratch, "process_warmup_s": round(process_warmup, 4),
                          "note": "wall time of every round from the seeds' start states (the warm-up rounds, "
-                                 "their first-use index reservations, and the timed rounds), max over ranks"},
+                                 "their first-use reservations, and the timed rounds), max over ranks, in a "
+                                 "process whose HIP kernels and streams have run once (process_warmup_s: a "
+                                 "throwaway two-engine round and the streams' first work, before the clock)"},
         "roofline": roof,
         "cpu_baseline": None,
     }
@@ -778,7 +805,7 @@ def compact_leg(leg):
     if leg.get("from_scratch"):
         fs = leg["from_scratch"]
         out["from_scratch"] = {"rounds": fs.get("rounds"), "wall_s": fs.get("wall_s"),
-                               "valid_per_s": fs.get("valid_per_s")}
+                               "valid_per_s": fs.get("valid_per_s"), "process_warmup_s": fs.get("process_warmup_s")}
     cfg = leg.get("config") or {}
     for k in ("bounds", "free_fraction", "edges"):
         if k in cfg:
@@ -793,7 +820,7 @@ def compact_line(out, detail):
     line["roofline"] = compact_roof(out.get("roofline") or {})
     if out.get("from_scratch"):
         fs = out["from_scratch"]
-        line["from_scratch"] = {k: fs.get(k) for k in ("rounds", "wall_s", "valid_per_s")}
+        line["from_scratch"] = {k: fs.get(k) for k in ("rounds", "wall_s", "valid_per_s", "process_warmup_s")}
     cb = out.get("cpu_baseline")
     if cb:
         line["cpu_baseline"] = {k: cb.get(k) for k in ("value", "unit", "cores", "kind", "sample", "cpu")}

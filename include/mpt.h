@@ -137,9 +137,10 @@ mpt_status mpt_prm_connect(const mpt_env *env, const mpt_agent *agent, int32_t a
                            uint8_t *verdict, int64_t *n_edges, int32_t *comp, float ms[4]);
 /* Diagnostics: out (may be NULL) = the edge sweep's work counters of the calling thread's last
  * mpt_prm_connect made with counters on: waves, env item box tests, (pair, pose) gate tests,
- * exact triangle tests, edges, poses; enable switches the counters on for its later calls (one
- * same-address atomic per wave: not for timed calls). */
-mpt_status mpt_prm_stats(int32_t enable, uint64_t out[6]);
+ * exact triangle tests, edges, poses, (edge, triangle, triangle, pose range) candidates emitted,
+ * edges deferred to the single-kernel sweep; enable switches the counters on for its later
+ * calls (one same-address atomic per wave: not for timed calls). */
+mpt_status mpt_prm_stats(int32_t enable, uint64_t out[8]);
 
 /* ---- workspace discretisation: PRMLite::generateEdges (discretizations/workspace/prmlite.hpp:128-164)
  * All vertex pairs i < j, pair index e = row-major over i < j (E = V(V-1)/2).  vertices [V][12] =

@@ -175,9 +175,10 @@ def prm_connect(env: Environment, agent: AgentMesh, kind: int, states, radius2: 
 def prm_stats(enable: bool) -> dict:
     """The sweep work counters of this thread's last prm_connect made with counters on; enable
     turns them on (or off) for later calls (diagnostics: an atomic per wave)."""
-    out = np.zeros(6, np.uint64)
+    out = np.zeros(8, np.uint64)
     check(lib().mpt_prm_stats(1 if enable else 0, _p(out)), "mpt_prm_stats")
-    return dict(zip(["waves", "item_tests", "gate_tests", "sat_tests", "edges", "poses"], (int(x) for x in out)))
+    return dict(zip(["waves", "item_tests", "gate_tests", "sat_tests", "edges", "poses", "candidates",
+                     "deferred_edges"], (int(x) for x in out)))
 
 
 def prmlite_edges(env: Environment, agent: AgentMesh, vertices, step: float = 0.1) -> np.ndarray:

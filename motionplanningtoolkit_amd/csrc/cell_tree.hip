@@ -1646,6 +1646,9 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(D >= 15 ? 4 
 // Many trees in one launch (mpt_rrt_step_many: one engine per independent seed).  Jobs are
 // dealt to XCDs: workgroup b runs on XCD b % 8, so job j takes the workgroups of XCD j % 8
 // and its tree stays in that XCD's L2.  8 waves per SIMD for d <= 7; d = 15 at 4 (registers).
+// (Round 5, measured and not kept: a job split over two XCDs when an XCD holds fewer than 8
+// trees -- the mapping's 64-bit divisions pushed the walk past its 64-VGPR bound (12 bytes
+// spilled): NN 0.33 -> 0.37 ms at 32 seeds, 2.09 -> 2.60 at 256.)
 template <int D, int BS, int W>
 __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(D >= 15 ? 4 : 8))) void k_ct_nn1_jobs(
     const CtNnJob *__restrict__ jobs, int32_t n_jobs, int64_t nq, int64_t blocks_per_job) {

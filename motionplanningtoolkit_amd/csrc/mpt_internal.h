@@ -247,6 +247,8 @@ void launch_pose_edge(const int64_t *d_offsets, int64_t E, int32_t *d_pose_edge,
 // d_link[0]; verdict[E] must be zeroed.  stats (optional [4]): waves, env item tests, (pair,
 // pose) gate tests, SAT tests.
 struct PrmEdges;
+// the calling thread's last two-phase sweep: candidates emitted, edges deferred
+extern thread_local uint64_t last_sweep_counts[2];
 void launch_collide_sweep_prm(const EnvDev &env, const AgentDev *d_link, int32_t n_clusters, const PrmEdges &edges,
                               int64_t E, uint8_t *verdict, unsigned long long *stats, hipStream_t stream);
 

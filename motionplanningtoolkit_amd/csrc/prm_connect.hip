@@ -135,7 +135,7 @@ int64_t scan_total(int64_t *d_in_out, int64_t n_plus_1, DBuf<char> &temp, hipStr
 // mpt_prm_stats: the sweep's work counters for the next mpt_prm_connect calls (one
 // same-address atomic per wave: diagnostics only, never in a timed call)
 thread_local bool g_prm_stats_on = false;
-thread_local uint64_t g_prm_stats[6] = {};
+thread_local uint64_t g_prm_stats[8] = {};
 
 int32_t uf_find(std::vector<int32_t> &p, int32_t x) {
     while (p[x] != x) {
@@ -147,10 +147,10 @@ int32_t uf_find(std::vector<int32_t> &p, int32_t x) {
 
 }  // namespace
 
-extern "C" mpt_status mpt_prm_stats(int32_t enable, uint64_t out[6]) {
+extern "C" mpt_status mpt_prm_stats(int32_t enable, uint64_t out[8]) {
     return guarded([&] {
         if (out)
-            for (int i = 0; i < 6; ++i) out[i] = g_prm_stats[i];
+            for (int i = 0; i < 8; ++i) out[i] = g_prm_stats[i];
         g_prm_stats_on = enable != 0;
     });
 }
@@ -254,6 +254,8 @@ extern "C" mpt_status mpt_prm_connect(const mpt_env *env, const mpt_agent *agent
                     for (int i = 0; i < 4; ++i) g_prm_stats[i] = h[i];
                     g_prm_stats[4] = (uint64_t)E;
                     g_prm_stats[5] = (uint64_t)P;
+                    g_prm_stats[6] = last_sweep_counts[0];
+                    g_prm_stats[7] = last_sweep_counts[1];
                 }
             } else {
                 CollideWork w{};

@@ -110,40 +110,62 @@ struct PrmEdge {
     // fails the exact gate; the poses inside run the exact test as before (bit-identical
     // verdicts).  The per-pose loop over all ~260 poses of a config-4 edge (--bounds rooms: 1.1 G
     // gate tests a roadmap) becomes a loop over the few poses that cross the env triangle's box.
+    // The poses of the sequence [q0, q1), then the tail pose (index it) when tail_too, whose
+    // gate with env triangle box elo / ehi can pass for agent triangle RQ (see each_near)
+    template <class V>
+    __device__ __forceinline__ void near_range(const V *RQ, const double *elo, const double *ehi, const double *env_tf,
+                                               unsigned &q0, unsigned &q1, bool &tail_too) const {
+        q0 = 0;
+        q1 = count();
+        tail_too = false;
+        if (it < 2) return;
+        const float d0 = (float)(s[0] - env_tf[9]), d1 = (float)(s[1] - env_tf[10]), d2 = (float)(s[2] - env_tf[11]);
+        float lo = 0.0f, hi = (float)(it - 1);
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            const float rk0 = (float)env_tf[k], rk1 = (float)env_tf[3 + k], rk2 = (float)env_tf[6 + k];
+            const float T0 = rk0 * d0 + rk1 * d1 + rk2 * d2;
+            const float Dk = (float)step * (rk0 * (float)dx[0] + rk1 * (float)dx[1] + rk2 * (float)dx[2]);
+            const float a0 = (float)(&RQ[0].x)[k], a1 = (float)(&RQ[1].x)[k], a2 = (float)(&RQ[2].x)[k];
+            const float a = fminf(a0, fminf(a1, a2)), b = fmaxf(a0, fmaxf(a1, a2));
+            const float el = (float)elo[k], eh = (float)ehi[k];
+            const float eps = 1e-5f * (1.0f + fabsf(T0) + fabsf(Dk) * (float)it + fabsf(a) + fabsf(b) + fabsf(el) +
+                                       fabsf(eh) + fabsf((float)env_tf[9 + k]) + fabsf(rk0) + fabsf(rk1) + fabsf(rk2));
+            const float u = eh - a - T0 + eps;  // i * D'_k <= u
+            const float l = el - b - T0 - eps;  // i * D'_k >= l
+            if (Dk > 0.0f) {
+                lo = fmaxf(lo, l / Dk);
+                hi = fminf(hi, u / Dk);
+            } else if (Dk < 0.0f) {
+                lo = fmaxf(lo, u / Dk);
+                hi = fminf(hi, l / Dk);
+            } else if (l > 0.0f || u < 0.0f) {
+                hi = -4.0f;  // this dim never overlaps
+            }
+        }
+        q0 = hi >= lo - 2.0f ? (unsigned)fmaxf(0.0f, floorf(lo) - 1.0f) : it;
+        q1 = hi >= lo - 2.0f ? (unsigned)fminf((float)it, ceilf(hi) + 2.0f) : it;
+        if (q1 < q0) q1 = q0;
+        tail_too = tail;
+    }
+
+    // The same for the poses whose gate with an env triangle can pass.  RQ: the agent triangle
+    // rotated (R Q, before + T); elo / ehi: the env triangle's exact box; env_tf: the env
+    // transform (R rows | T).  Pose i's env-relative translation is T'(i) = envT(s + (step * i)
+    // * dx), which in real arithmetic is T'(0) + i D', D' = step * R_env^T dx: the gate's box
+    // test along dim k then bounds i * D'_k between two numbers, an interval of i.  The interval
+    // is computed in float, widened by eps (1e-5 of the magnitudes involved: ~30x the rounding
+    // of the float and double terms) and by one index either side, so every pose outside it
+    // fails the exact gate; the poses inside run the exact test as before (bit-identical
+    // verdicts).  The per-pose loop over all ~260 poses of a config-4 edge (--bounds rooms: 1.1 G
+    // gate tests a roadmap) becomes a loop over the few poses that cross the env triangle's box.
     template <class F, class V>
     __device__ __forceinline__ void each_near(F &&f, const V *RQ, const double *elo, const double *ehi,
                                               const double *env_tf) const {
-        unsigned q0 = 0, q1 = count();  // poses [q0, q1) of the sequence, then the tail
-        if (it >= 2) {
-            const float d0 = (float)(s[0] - env_tf[9]), d1 = (float)(s[1] - env_tf[10]), d2 = (float)(s[2] - env_tf[11]);
-            float lo = 0.0f, hi = (float)(it - 1);
-#pragma unroll
-            for (int k = 0; k < 3; ++k) {
-                const float rk0 = (float)env_tf[k], rk1 = (float)env_tf[3 + k], rk2 = (float)env_tf[6 + k];
-                const float T0 = rk0 * d0 + rk1 * d1 + rk2 * d2;
-                const float Dk = (float)step * (rk0 * (float)dx[0] + rk1 * (float)dx[1] + rk2 * (float)dx[2]);
-                const float a0 = (float)(&RQ[0].x)[k], a1 = (float)(&RQ[1].x)[k], a2 = (float)(&RQ[2].x)[k];
-                const float a = fminf(a0, fminf(a1, a2)), b = fmaxf(a0, fmaxf(a1, a2));
-                const float el = (float)elo[k], eh = (float)ehi[k];
-                const float eps = 1e-5f * (1.0f + fabsf(T0) + fabsf(Dk) * (float)it + fabsf(a) + fabsf(b) + fabsf(el) +
-                                           fabsf(eh) + fabsf(env_tf[9 + k]) + fabsf(rk0) + fabsf(rk1) + fabsf(rk2));
-                const float u = eh - a - T0 + eps;  // i * D'_k <= u
-                const float l = el - b - T0 - eps;  // i * D'_k >= l
-                if (Dk > 0.0f) {
-                    lo = fmaxf(lo, l / Dk);
-                    hi = fminf(hi, u / Dk);
-                } else if (Dk < 0.0f) {
-                    lo = fmaxf(lo, u / Dk);
-                    hi = fminf(hi, l / Dk);
-                } else if (l > 0.0f || u < 0.0f) {
-                    hi = -4.0f;  // this dim never overlaps
-                }
-            }
-            q0 = hi >= lo - 2.0f ? (unsigned)fmaxf(0.0f, floorf(lo) - 1.0f) : it;
-            q1 = hi >= lo - 2.0f ? (unsigned)fminf((float)it, ceilf(hi) + 2.0f) : it;
-            if (q1 < q0) q1 = q0;
-        }
-        const unsigned n = (q1 - q0) + (it >= 2 && tail ? 1u : 0u);
+        unsigned q0, q1;
+        bool tail_too;
+        near_range(RQ, elo, ehi, env_tf, q0, q1, tail_too);
+        const unsigned n = (q1 - q0) + (tail_too ? 1u : 0u);
         for (unsigned j = 0; j < n; ++j) {
             double t[3];
             pose(q0 + j < q1 ? q0 + j : it, t);  // past the run: the tail (index it)

@@ -446,6 +446,313 @@ __global__ __launch_bounds__(kSweepWaves * 64) void k_sweep_lite(EnvDev env, con
     }
 }
 
+// ---- PRM edges in two phases: the walk and fan-out emit (edge, agent triangle, env triangle,
+// pose range) candidates; a second launch runs the gate + SAT over each candidate's poses, one
+// candidate a lane.  The single-kernel sweep (k_sweep_edge) held the SAT's registers across its
+// walk (~200 VGPRs: 2 waves a SIMD for a latency-bound walk) and ran each SAT on a wave with a
+// few lanes active; split, the walk runs at more waves a SIMD and the SATs on full waves.
+// Verdicts are the same set: every (edge, agent triangle, env triangle, pose) the fused form
+// tests is in some candidate (same fan-out, same box tests, the same pose interval), and the
+// candidate's test is the same operations.
+
+struct SweepCand {
+    int32_t e, atri, etri;
+    uint32_t q0, q1t;  // poses [q0, q1) of the edge's sequence, then its tail pose when bit 31 of q1t is set
+};
+constexpr int kSweepStage = 128;  // a wave's candidates staged in LDS before one atomic reserves their slots
+constexpr int kSweepChunk = 8;    // poses a candidate covers at most
+
+struct SweepQueue {
+    SweepCand *c;
+    uint32_t *n;    // [0] candidates written (may pass cap), [1] overflow flag, [2] deferred edges
+    uint32_t cap;
+    int32_t *deferred;  // [E] edges whose walk stopped at kSweepEdgeCands candidates
+};
+// candidates an edge emits at most; an edge that reaches it stops its walk and is deferred to
+// the single-kernel sweep (after the SAT launch, if still undecided).  The fused sweep stops an
+// edge at its first contact; emitting every candidate of an edge that crosses a wall instead
+// (config 4 at --bounds rooms: tens of millions) cost a second a roadmap.
+constexpr int kSweepEdgeCands = 512;
+
+// false when the queue is full: the wave's edge is then deferred (the candidates that did fit
+// are tested all the same, which is harmless: a contact among them is a contact)
+__device__ __forceinline__ bool sweep_flush(SweepCand *buf, int nb, const SweepQueue &Q, int lane) {
+    if (nb <= 0) return true;
+    uint32_t base = 0;
+    if (lane == 0) base = atomicAdd(Q.n, (uint32_t)nb);
+    base = __builtin_amdgcn_readfirstlane(base);
+    for (int i = lane; i < nb; i += kWave)
+        if (base + (uint32_t)i < Q.cap) Q.c[base + i] = buf[i];
+    return base + (uint32_t)nb <= Q.cap;
+}
+
+// One wave an edge: sweep_edge_core's walk and fan-out (union of the clusters' swept boxes,
+// per-bucket cluster masks, each cluster rotated once a bucket), a candidate per lane whose
+// swept triangle box meets the env triangle's item box and whose pose interval is not empty
+__global__ __launch_bounds__(kSweepWaves * 64) void k_sweep_cands(EnvDev env, const AgentDev *__restrict__ link,
+                                                                  PrmEdges P, int64_t E, const uint8_t *verdict,
+                                                                  SweepQueue Q, unsigned long long *stats) {
+    __shared__ int32_t s_stk[kSweepWaves][2 * kSweepStack];
+    __shared__ SweepCand s_buf[kSweepWaves][kSweepStage];
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    const int64_t e = (int64_t)blockIdx.x * kSweepWaves + wave;
+    SweepCounters cnt;
+    SweepCand *buf = s_buf[wave];
+    int32_t *stk = s_stk[wave];
+    int nb = 0, n_edge = 0;
+    bool stop = false;
+    const AgentDev &ag = link[0];
+    if (e < E && !load_flag(verdict + e)) {
+        PrmEdge g = prm_edge(P, e);
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            g.s[k] = uniform_d(g.s[k]);
+            g.end[k] = uniform_d(g.end[k]);
+            g.dx[k] = uniform_d(g.dx[k]);
+        }
+#pragma unroll
+        for (int k = 0; k < 9; ++k) g.R[k] = uniform_d(g.R[k]);
+        g.step = uniform_d(g.step);
+        g.it = __builtin_amdgcn_readfirstlane(g.it);
+        g.tail = __builtin_amdgcn_readfirstlane((int)g.tail) != 0;
+        double tf[3], tl[3];
+        g.first(tf);
+        g.last(tl);
+        ++cnt.waves;
+        double R[9], T0[3], TN[3];
+        relative_transform(env.tf, env.tf + 9, g.R, tf, R, T0);
+        env_rel_t(env, tl, TN);
+#pragma unroll
+        for (int i = 0; i < 9; ++i) R[i] = uniform_d(R[i]);
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+            T0[i] = uniform_d(T0[i]);
+            TN[i] = uniform_d(TN[i]);
+        }
+        const int ncl = ag.n_clusters;
+        float clo[3] = {__builtin_huge_valf(), __builtin_huge_valf(), __builtin_huge_valf()};
+        float chi[3] = {-__builtin_huge_valf(), -__builtin_huge_valf(), -__builtin_huge_valf()};
+        if (lane < ncl) {  // lane c: cluster c's box swept along the edge
+            const Cluster c = ag.clusters[lane];
+            float alo[3], ahi[3], blo[3], bhi[3];
+            local_box(c.c, c.e, R, T0, alo, ahi);
+            local_box(c.c, c.e, R, TN, blo, bhi);
+#pragma unroll
+            for (int k = 0; k < 3; ++k) {
+                clo[k] = fminf(alo[k], blo[k]);
+                chi[k] = fmaxf(ahi[k], bhi[k]);
+            }
+        }
+        float ulo[3], uhi[3];  // their union (every lane)
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            ulo[k] = clo[k];
+            uhi[k] = chi[k];
+#pragma unroll
+            for (int off = 32; off > 0; off >>= 1) {
+                ulo[k] = fminf(ulo[k], __shfl_xor(ulo[k], off));
+                uhi[k] = fmaxf(uhi[k], __shfl_xor(uhi[k], off));
+            }
+        }
+        int sp = 0;
+        int lev = env.n_levels - 1;
+        int32_t first = env.lev_off[lev];
+        int32_t count = env.lev_off[lev + 1] - first;
+        for (;;) {
+            bool keep = false;
+            int32_t cf = 0, cc = 0;
+            float ilo[3] = {0, 0, 0}, ihi[3] = {0, 0, 0};
+            if (lane < count) {
+                const Item it = env.items[first + lane];
+                keep = box_overlap(ulo, uhi, it.lo, it.hi);
+                cf = it.first;
+                cc = it.count;
+#pragma unroll
+                for (int k = 0; k < 3; ++k) {
+                    ilo[k] = it.lo[k];
+                    ihi[k] = it.hi[k];
+                }
+            }
+            cnt.items += (uint32_t)count;
+            uint64_t m = __ballot(keep);
+            if (lev == 0) {
+                uint64_t Tm = 0;  // lane c: the bucket's triangles cluster c's swept box meets
+                for (uint64_t mm = m; mm; mm &= mm - 1) {
+                    const int j = __ffsll((unsigned long long)mm) - 1;
+                    const float elo[3] = {lane_f(ilo[0], j), lane_f(ilo[1], j), lane_f(ilo[2], j)};
+                    const float ehi[3] = {lane_f(ihi[0], j), lane_f(ihi[1], j), lane_f(ihi[2], j)};
+                    if (lane < ncl && box_overlap(clo, chi, elo, ehi)) Tm |= 1ull << j;
+                }
+                for (uint64_t C = __ballot(Tm != 0); C && !stop; C &= C - 1) {
+                    const int ci = __ffsll((unsigned long long)C) - 1;
+                    uint64_t Tc = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(Tm >> 32), ci) << 32) |
+                                  (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)Tm, ci);
+                    const Cluster c = ag.clusters[ci];
+                    const bool act = lane < c.count;
+                    v3 RQ[3] = {mk(0, 0, 0), mk(0, 0, 0), mk(0, 0, 0)};
+                    float tlo[3] = {0, 0, 0}, thi[3] = {0, 0, 0};
+                    if (act) {  // the lane's triangle rotated (R Q, xform's order before the + T)
+                        const double *tr = ag.tris + (int64_t)(c.first + lane) * 9;
+#pragma unroll
+                        for (int v = 0; v < 3; ++v) {
+                            const double x = tr[3 * v], y = tr[3 * v + 1], z = tr[3 * v + 2];
+                            RQ[v] = mk(R[0] * x + R[1] * y + R[2] * z, R[3] * x + R[4] * y + R[5] * z,
+                                       R[6] * x + R[7] * y + R[8] * z);
+                        }
+#pragma unroll
+                        for (int k = 0; k < 3; ++k) {  // its box swept along the edge
+                            const double a0 = (&RQ[0].x)[k], a1 = (&RQ[1].x)[k], a2 = (&RQ[2].x)[k];
+                            const double mn = dmin(a0, dmin(a1, a2)), mx = dmax(a0, dmax(a1, a2));
+                            tlo[k] = widen_lo(dmin(mn + T0[k], mn + TN[k]));
+                            thi[k] = widen_hi(dmax(mx + T0[k], mx + TN[k]));
+                        }
+                    }
+                    for (; Tc && !stop; Tc &= Tc - 1) {
+                        const int j = __ffsll((unsigned long long)Tc) - 1;
+                        const float elo[3] = {lane_f(ilo[0], j), lane_f(ilo[1], j), lane_f(ilo[2], j)};
+                        const float ehi[3] = {lane_f(ihi[0], j), lane_f(ihi[1], j), lane_f(ihi[2], j)};
+                        bool emit = false;
+                        unsigned q0 = 0, q1 = 0;
+                        bool tail_too = false;
+                        if (act && box_overlap(tlo, thi, elo, ehi)) {
+                            // the item box (widened floats) holds the triangle's exact box: its
+                            // interval holds the exact gate's poses
+                            const double elod[3] = {elo[0], elo[1], elo[2]}, ehid[3] = {ehi[0], ehi[1], ehi[2]};
+                            g.near_range(RQ, elod, ehid, env.tf, q0, q1, tail_too);
+                            emit = q1 > q0 || tail_too;
+                        }
+                        // a lane's poses go out in chunks of at most kSweepChunk (the tail pose
+                        // with the last): the SAT launch then runs equal short loops a lane
+                        // instead of each wave waiting for its longest interval
+                        for (uint64_t em = __ballot(emit); em && !stop; em = __ballot(emit)) {
+                            const int ne = __popcll(em);
+                            if (nb + ne > kSweepStage) {
+                                if (!sweep_flush(buf, nb, Q, lane)) stop = true;
+                                nb = 0;
+                                if (stop) break;
+                            }
+                            if (emit) {
+                                const int rank = __popcll(em & ((1ull << lane) - 1ull));
+                                const bool last = q1 - q0 <= (unsigned)kSweepChunk;
+                                const unsigned qe = last ? q1 : q0 + kSweepChunk;
+                                buf[nb + rank] = SweepCand{(int32_t)e, c.first + lane, first + j, q0,
+                                                           qe | (last && tail_too ? 0x80000000u : 0u)};
+                                q0 = qe;
+                                emit = !last;
+                            }
+                            nb += ne;
+                            n_edge += ne;
+                            if (n_edge >= kSweepEdgeCands) stop = true;  // wave-uniform: the edge is deferred
+                            __builtin_amdgcn_wave_barrier();
+                        }
+                    }
+                }
+            } else if (m) {
+                const int j = __ffsll((unsigned long long)m) - 1;
+                const uint64_t rest = m & (m - 1);
+                if (keep && lane != j) {
+                    const int pos = sp + (int)__popcll(rest & ((1ull << lane) - 1));
+                    stk[pos] = ((lev - 1) << 27) | cf;
+                    stk[kSweepStack + pos] = cc;
+                }
+                sp += (int)__popcll(rest);
+                first = __builtin_amdgcn_readfirstlane(__shfl(cf, j));
+                count = __builtin_amdgcn_readfirstlane(__shfl(cc, j));
+                lev -= 1;
+                continue;
+            }
+            if (sp == 0 || stop) break;
+            --sp;
+            const int32_t code = __builtin_amdgcn_readfirstlane(stk[sp]);
+            count = __builtin_amdgcn_readfirstlane(stk[kSweepStack + sp]);
+            lev = code >> 27;
+            first = code & ((1 << 27) - 1);
+        }
+    }
+    __builtin_amdgcn_wave_barrier();
+    if (!sweep_flush(buf, nb, Q, lane)) stop = true;
+    if (stop && lane == 0) Q.deferred[atomicAdd(Q.n + 2, 1u)] = (int32_t)e;
+    if (stats && lane == 0 && cnt.waves) {
+        atomicAdd(stats + 0, (unsigned long long)cnt.waves);
+        atomicAdd(stats + 1, (unsigned long long)cnt.items);
+    }
+}
+
+// the single-kernel sweep over a list of edges (the deferred ones; count on the device)
+__global__ __launch_bounds__(kSweepWaves * 64) void k_sweep_edge_list(EnvDev env, const AgentDev *__restrict__ link,
+                                                                      PrmSrc src, const int32_t *__restrict__ list,
+                                                                      const uint32_t *__restrict__ n_list,
+                                                                      uint8_t *verdict) {
+    __shared__ int32_t s_stk[kSweepWaves][2 * kSweepStack];
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    const uint32_t n = *n_list;
+    SweepCounters cnt;
+    for (uint32_t i = blockIdx.x * kSweepWaves + wave; i < n; i += gridDim.x * kSweepWaves) {
+        const int64_t e = list[i];
+        if (load_flag(verdict + e)) continue;
+        src.edge(e, [&](const double *Rw, const double *tf, const double *tl, auto &&gen) {
+            sweep_edge_core(env, link[0], Rw, tf, tl, gen, verdict + e, lane, s_stk[wave], cnt);
+        });
+    }
+}
+
+// One candidate a lane (a resident grid striding over them): the edge's rotation and its
+// poses regenerated (prm_edge: the same operations as the walk's), the agent triangle rotated
+// (R Q) and, over the candidate's poses, Q' = R Q + T', the exact gate and intersect_Triangle
+__global__ __launch_bounds__(256) void k_sweep_sat(EnvDev env, const AgentDev *__restrict__ link, PrmEdges P,
+                                                   SweepQueue Q, uint8_t *verdict, unsigned long long *stats) {
+    const uint32_t n = *Q.n < Q.cap ? *Q.n : Q.cap;
+    uint32_t n_gate = 0, n_sat = 0;
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+        const SweepCand cd = Q.c[i];
+        if (load_flag(verdict + cd.e)) continue;
+        const PrmEdge g = prm_edge(P, cd.e);
+        double tf[3], R[9], T0[3];
+        g.first(tf);
+        relative_transform(env.tf, env.tf + 9, g.R, tf, R, T0);
+        const double *tr = link[0].tris + (int64_t)cd.atri * 9;
+        v3 RQ[3];
+#pragma unroll
+        for (int v = 0; v < 3; ++v) {
+            const double x = tr[3 * v], y = tr[3 * v + 1], z = tr[3 * v + 2];
+            RQ[v] = mk(R[0] * x + R[1] * y + R[2] * z, R[3] * x + R[4] * y + R[5] * z, R[6] * x + R[7] * y + R[8] * z);
+        }
+        const EnvTri &E = env.tris[cd.etri];
+        const unsigned q1 = cd.q1t & 0x7fffffffu;
+        const unsigned np = (q1 - cd.q0) + (cd.q1t >> 31);
+        for (unsigned j = 0; j < np; ++j) {
+            double t[3], Tp[3];
+            if (j > 0 && load_flag(verdict + cd.e)) break;  // another lane found the edge's contact
+            g.pose(cd.q0 + j < q1 ? cd.q0 + j : g.it, t);
+            env_rel_t(env, t, Tp);
+            const v3 Q1 = mk(RQ[0].x + Tp[0], RQ[0].y + Tp[1], RQ[0].z + Tp[2]);
+            const v3 Q2 = mk(RQ[1].x + Tp[0], RQ[1].y + Tp[1], RQ[1].z + Tp[2]);
+            const v3 Q3 = mk(RQ[2].x + Tp[0], RQ[2].y + Tp[1], RQ[2].z + Tp[2]);
+            ++n_gate;
+            if (!tri_gate(E.lo, E.hi, Q1, Q2, Q3)) continue;
+            ++n_sat;
+            if (tri_intersect(E, Q1, Q2, Q3)) {
+                __hip_atomic_store(verdict + cd.e, (uint8_t)1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                break;
+            }
+        }
+    }
+    if (stats) {
+        uint32_t a = n_gate, b = n_sat;
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) {
+            a += __shfl_xor(a, off);
+            b += __shfl_xor(b, off);
+        }
+        if ((threadIdx.x & 63) == 0 && (a | b)) {
+            atomicAdd(stats + 2, (unsigned long long)a);
+            atomicAdd(stats + 3, (unsigned long long)b);
+        }
+    }
+}
+
 void launch_prmlite_edges(const EnvDev &env, const AgentDev *d_link, int32_t n_clusters, const double *verts, int64_t V,
                           double step, uint8_t *hit, unsigned long long *stats, hipStream_t stream) {
     const int64_t E = V * (V - 1) / 2;
@@ -478,9 +785,62 @@ static void launch_sweep_src(const EnvDev &env, const AgentDev *d_link, int32_t 
     hip_check(hipGetLastError(), "k_sweep launch");
 }
 
+thread_local uint64_t last_sweep_counts[2] = {0, 0};
+
 void launch_collide_sweep_prm(const EnvDev &env, const AgentDev *d_link, int32_t n_clusters, const PrmEdges &edges,
                               int64_t E, uint8_t *verdict, unsigned long long *stats, hipStream_t stream) {
-    launch_sweep_src(env, d_link, n_clusters, PrmSrc{edges}, E, verdict, stats, stream);
+    if (E <= 0 || env.n_tris <= 0) return;
+    if (n_clusters > 64 || env.n_tris >= (1 << 27)) {
+        launch_sweep_src(env, d_link, n_clusters, PrmSrc{edges}, E, verdict, stats, stream);
+        return;
+    }
+    // the candidate queue: 64 a edge (config 4 at --bounds rooms: ~? a edge), at least 4 M; one
+    // per thread of the caller's process (mpt_prm_connect is per thread); an overflow completes
+    // the verdicts with the single-kernel sweep (it skips the edges already decided)
+    struct Q {
+        SweepCand *c = nullptr;
+        int32_t *deferred = nullptr;
+        uint32_t *n = nullptr, *h = nullptr;
+        int64_t cap = 0, ecap = 0;
+        ~Q() {
+            if (c) (void)hipFree(c);
+            if (deferred) (void)hipFree(deferred);
+            if (n) (void)hipFree(n);
+            if (h) (void)hipHostFree(h);
+        }
+    };
+    static thread_local Q q;
+    // 32 a edge (config 4 at --bounds rooms: ~15 emitted a edge), at least 4 M: a full queue
+    // defers the edges that no longer fit
+    const int64_t want = std::min<int64_t>(std::max<int64_t>(int64_t(1) << 22, 32 * E), int64_t(1) << 31);
+    if (want > q.cap || E > q.ecap) {
+        hip_check(hipStreamSynchronize(stream), "sync");
+        if (q.c) hip_check(hipFree(q.c), "free");
+        if (q.deferred) hip_check(hipFree(q.deferred), "free");
+        hip_check(hipMalloc(&q.c, sizeof(SweepCand) * (size_t)want), "sweep candidates");
+        hip_check(hipMalloc(&q.deferred, sizeof(int32_t) * (size_t)E), "sweep deferred edges");
+        if (!q.n) hip_check(hipMalloc(&q.n, sizeof(uint32_t) * 4), "sweep counts");
+        if (!q.h) hip_check(hipHostMalloc(&q.h, sizeof(uint32_t) * 4), "sweep counts");
+        q.cap = want;
+        q.ecap = E;
+    }
+    hip_check(hipMemsetAsync(q.n, 0, sizeof(uint32_t) * 4, stream), "sweep counts zero");
+    const SweepQueue Qd{q.c, q.n, (uint32_t)std::min<int64_t>(q.cap, 0xffffffffLL), q.deferred};
+    const int64_t blocks = (E + kSweepWaves - 1) / kSweepWaves;
+    if (blocks > 0x7fffffff) throw Error{5, "sweep batch too large"};
+    hipLaunchKernelGGL(k_sweep_cands, dim3((unsigned)blocks), dim3(kSweepWaves * 64), 0, stream, env, d_link, edges, E,
+                       verdict, Qd, stats);
+    hip_check(hipGetLastError(), "k_sweep_cands launch");
+    hipLaunchKernelGGL(k_sweep_sat, dim3(4096), dim3(256), 0, stream, env, d_link, edges, Qd, verdict, stats);
+    hip_check(hipGetLastError(), "k_sweep_sat launch");
+    // the deferred edges that no candidate decided: the single-kernel sweep (stops at a contact)
+    hipLaunchKernelGGL(k_sweep_edge_list, dim3(4096), dim3(kSweepWaves * 64), 0, stream, env, d_link, PrmSrc{edges},
+                       q.deferred, q.n + 2, verdict);
+    hip_check(hipGetLastError(), "k_sweep_edge_list launch");
+    hip_check(hipMemcpyAsync(q.h, q.n, sizeof(uint32_t) * 4, hipMemcpyDeviceToHost, stream), "sweep counts");
+    hip_check(hipStreamSynchronize(stream), "sweep sync");
+    last_sweep_counts[0] = q.h[0];  // candidates emitted (may exceed the queue)
+    last_sweep_counts[1] = q.h[2];  // edges deferred to the single-kernel sweep
 }
 
 }  // namespace mpt

@@ -10,14 +10,21 @@ if [ $# -gt 0 ]; then
   timeout -k 10 900 python -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu "$@" > $O/pytest.log 2>&1
   rc=$?; tail -3 $O/pytest.log; [ $rc -ne 0 ] && exit $rc
 fi
+if [ -z "$NO_C5" ]; then
 for n in 32 256; do
   timeout -k 10 200 python bench.py --seeds $n --steps 25 --warmup 5 --no-cpu --detail $O/c5_${n}_detail.json > $O/c5_$n.json || exit 1
 done
+fi
 [ -n "$NO_PRM" ] || timeout -k 10 300 python scripts/bench_prm.py --reps 3 --no-cpu > $O/prm.json || exit 1
 if [ -n "$SCRATCH" ]; then
   for w in none stream group; do
     for n in 32 256; do timeout -k 10 200 python scripts/scratch_rounds.py --seeds $n --warm $w > $O/scratch_${n}_$w.json || exit 1; cat $O/scratch_${n}_$w.json; done
   done
+fi
+if [ -n "$PRMKT" ]; then  # config 4's kernels
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prmkt -o kt -- python scripts/bench_prm.py --reps 1 --no-cpu > $O/prmkt.log 2>&1 || exit 1
+  head -12 $O/prmkt/kt_kernel_stats.csv | cut -d, -f1-4
+  rm -f $O/prmkt/kt_kernel_trace.csv
 fi
 if [ -n "$HIPT" ]; then  # HIP API time of a run from the start states (first-round costs)
   timeout -k 10 200 rocprofv3 --hip-trace --stats --output-format csv -d $O/hipt -o ht -- python scripts/scratch_rounds.py --seeds 32 --rounds 3 > $O/hipt.log 2>&1 || exit 1
