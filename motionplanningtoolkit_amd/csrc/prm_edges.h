@@ -100,16 +100,6 @@ struct PrmEdge {
         }
     }
 
-    // The same for the poses whose gate with an env triangle can pass.  RQ: the agent triangle
-    // rotated (R Q, before + T); elo / ehi: the env triangle's exact box; env_tf: the env
-    // transform (R rows | T).  Pose i's env-relative translation is T'(i) = envT(s + (step * i)
-    // * dx), which in real arithmetic is T'(0) + i D', D' = step * R_env^T dx: the gate's box
-    // test along dim k then bounds i * D'_k between two numbers, an interval of i.  The interval
-    // is computed in float, widened by eps (1e-5 of the magnitudes involved: ~30x the rounding
-    // of the float and double terms) and by one index either side, so every pose outside it
-    // fails the exact gate; the poses inside run the exact test as before (bit-identical
-    // verdicts).  The per-pose loop over all ~260 poses of a config-4 edge (--bounds rooms: 1.1 G
-    // gate tests a roadmap) becomes a loop over the few poses that cross the env triangle's box.
     // The poses of the sequence [q0, q1), then the tail pose (index it) when tail_too, whose
     // gate with env triangle box elo / ehi can pass for agent triangle RQ (see each_near)
     template <class V>
@@ -166,10 +156,20 @@ struct PrmEdge {
         bool tail_too;
         near_range(RQ, elo, ehi, env_tf, q0, q1, tail_too);
         const unsigned n = (q1 - q0) + (tail_too ? 1u : 0u);
-        for (unsigned j = 0; j < n; ++j) {
-            double t[3];
-            pose(q0 + j < q1 ? q0 + j : it, t);  // past the run: the tail (index it)
-            if (f(t)) return;
+        // in step over the lanes that called it: the loop ends for all of them at the first
+        // lane's true (a contact decides the edge; a lane looping on past it only held the wave:
+        // config 4 at --bounds rooms, the colliding edges the sweep took ~180 iterations a lane,
+        // up to 7000)
+        bool done = false;
+        for (unsigned j = 0;; ++j) {
+            const bool more = j < n;
+            if (!__ballot(more)) return;
+            if (more) {
+                double t[3];
+                pose(q0 + j < q1 ? q0 + j : it, t);  // past the run: the tail (index it)
+                done = f(t);
+            }
+            if (__ballot(done)) return;
         }
     }
 };

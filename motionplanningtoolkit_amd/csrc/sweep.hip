@@ -464,15 +464,29 @@ constexpr int kSweepChunk = 8;    // poses a candidate covers at most
 
 struct SweepQueue {
     SweepCand *c;
-    uint32_t *n;    // [0] candidates written (may pass cap), [1] overflow flag, [2] deferred edges
+    uint32_t *n;  // [0] candidates written (may pass cap), [1] edges sent to the single-kernel sweep
     uint32_t cap;
-    int32_t *deferred;  // [E] edges whose walk stopped at kSweepEdgeCands candidates
+    int32_t *fused;       // [E] edges a full queue stopped (the single-kernel sweep decides them)
+    const int32_t *in_e;  // this pass's edges (null: every edge) and their resume indices
+    const uint32_t *in_r;
+    const uint32_t *n_in;
+    int32_t *out_e;  // the edges this pass capped: the next pass resumes them
+    uint32_t *out_r;
+    uint32_t *n_out;
+    uint32_t edge_cap;  // candidates an edge emits at most in this pass
 };
-// candidates an edge emits at most; an edge that reaches it stops its walk and is deferred to
-// the single-kernel sweep (after the SAT launch, if still undecided).  The fused sweep stops an
-// edge at its first contact; emitting every candidate of an edge that crosses a wall instead
-// (config 4 at --bounds rooms: tens of millions) cost a second a roadmap.
-constexpr int kSweepEdgeCands = 512;
+// The passes: each emits an edge's candidates from where its previous pass stopped (its resume
+// index: candidates are numbered in the walk's order, which is the same every pass) up to the
+// pass's per-edge cap, then the SAT launch decides what it can; an edge still undecided at the
+// cap goes to the next pass with a larger cap; after the last pass the single-kernel sweep takes
+// the edges still undecided.  Emitting every candidate of an edge at once (config 4 at --bounds
+// rooms: some edges emit thousands) cost a second a roadmap.  Config 4 at --bounds rooms,
+// collision ms by the number of passes (first cap 64, x4 a pass, as far as the queue holds):
+// 1: 47.5, 2: 52.0, 3: 52.9, 4: 60.2 -- the edges a pass leaves undecided mostly stay so over
+// hundreds more candidates, whose SATs a pass runs in parallel where the single-kernel sweep
+// stops at the edge's first contact; caps 512 / 2048 in one pass: 53 / 53.
+constexpr int kSweepEdgeCands = 64;  // the first pass's cap; x4 a pass
+constexpr int kSweepPasses = 1;      // then the single-kernel sweep takes what is left
 
 // false when the queue is full: the wave's edge is then deferred (the candidates that did fit
 // are tested all the same, which is harmless: a contact among them is a contact)
@@ -496,183 +510,198 @@ __global__ __launch_bounds__(kSweepWaves * 64) void k_sweep_cands(EnvDev env, co
     __shared__ SweepCand s_buf[kSweepWaves][kSweepStage];
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
-    const int64_t e = (int64_t)blockIdx.x * kSweepWaves + wave;
     SweepCounters cnt;
     SweepCand *buf = s_buf[wave];
     int32_t *stk = s_stk[wave];
-    int nb = 0, n_edge = 0;
-    bool stop = false;
     const AgentDev &ag = link[0];
-    if (e < E && !load_flag(verdict + e)) {
-        PrmEdge g = prm_edge(P, e);
-#pragma unroll
-        for (int k = 0; k < 3; ++k) {
-            g.s[k] = uniform_d(g.s[k]);
-            g.end[k] = uniform_d(g.end[k]);
-            g.dx[k] = uniform_d(g.dx[k]);
-        }
-#pragma unroll
-        for (int k = 0; k < 9; ++k) g.R[k] = uniform_d(g.R[k]);
-        g.step = uniform_d(g.step);
-        g.it = __builtin_amdgcn_readfirstlane(g.it);
-        g.tail = __builtin_amdgcn_readfirstlane((int)g.tail) != 0;
-        double tf[3], tl[3];
-        g.first(tf);
-        g.last(tl);
-        ++cnt.waves;
-        double R[9], T0[3], TN[3];
-        relative_transform(env.tf, env.tf + 9, g.R, tf, R, T0);
-        env_rel_t(env, tl, TN);
-#pragma unroll
-        for (int i = 0; i < 9; ++i) R[i] = uniform_d(R[i]);
-#pragma unroll
-        for (int i = 0; i < 3; ++i) {
-            T0[i] = uniform_d(T0[i]);
-            TN[i] = uniform_d(TN[i]);
-        }
-        const int ncl = ag.n_clusters;
-        float clo[3] = {__builtin_huge_valf(), __builtin_huge_valf(), __builtin_huge_valf()};
-        float chi[3] = {-__builtin_huge_valf(), -__builtin_huge_valf(), -__builtin_huge_valf()};
-        if (lane < ncl) {  // lane c: cluster c's box swept along the edge
-            const Cluster c = ag.clusters[lane];
-            float alo[3], ahi[3], blo[3], bhi[3];
-            local_box(c.c, c.e, R, T0, alo, ahi);
-            local_box(c.c, c.e, R, TN, blo, bhi);
-#pragma unroll
+    const int64_t n_list = Q.in_e ? (int64_t)*Q.n_in : E;
+    for (int64_t i = (int64_t)blockIdx.x * kSweepWaves + wave; i < n_list; i += (int64_t)gridDim.x * kSweepWaves) {
+        const int64_t e = Q.in_e ? Q.in_e[i] : i;
+        const uint32_t skip = Q.in_e ? __builtin_amdgcn_readfirstlane(Q.in_r[i]) : 0u;
+        const uint32_t upto = skip + Q.edge_cap;
+        uint32_t n_edge = 0;  // candidates numbered so far (those below skip were emitted by an earlier pass)
+        int nb = 0;
+        bool stop = false, full = false;
+        if (!load_flag(verdict + e)) {
+            PrmEdge g = prm_edge(P, e);
+    #pragma unroll
             for (int k = 0; k < 3; ++k) {
-                clo[k] = fminf(alo[k], blo[k]);
-                chi[k] = fmaxf(ahi[k], bhi[k]);
+                g.s[k] = uniform_d(g.s[k]);
+                g.end[k] = uniform_d(g.end[k]);
+                g.dx[k] = uniform_d(g.dx[k]);
             }
-        }
-        float ulo[3], uhi[3];  // their union (every lane)
-#pragma unroll
-        for (int k = 0; k < 3; ++k) {
-            ulo[k] = clo[k];
-            uhi[k] = chi[k];
-#pragma unroll
-            for (int off = 32; off > 0; off >>= 1) {
-                ulo[k] = fminf(ulo[k], __shfl_xor(ulo[k], off));
-                uhi[k] = fmaxf(uhi[k], __shfl_xor(uhi[k], off));
+    #pragma unroll
+            for (int k = 0; k < 9; ++k) g.R[k] = uniform_d(g.R[k]);
+            g.step = uniform_d(g.step);
+            g.it = __builtin_amdgcn_readfirstlane(g.it);
+            g.tail = __builtin_amdgcn_readfirstlane((int)g.tail) != 0;
+            double tf[3], tl[3];
+            g.first(tf);
+            g.last(tl);
+            ++cnt.waves;
+            double R[9], T0[3], TN[3];
+            relative_transform(env.tf, env.tf + 9, g.R, tf, R, T0);
+            env_rel_t(env, tl, TN);
+    #pragma unroll
+            for (int i = 0; i < 9; ++i) R[i] = uniform_d(R[i]);
+    #pragma unroll
+            for (int i = 0; i < 3; ++i) {
+                T0[i] = uniform_d(T0[i]);
+                TN[i] = uniform_d(TN[i]);
             }
-        }
-        int sp = 0;
-        int lev = env.n_levels - 1;
-        int32_t first = env.lev_off[lev];
-        int32_t count = env.lev_off[lev + 1] - first;
-        for (;;) {
-            bool keep = false;
-            int32_t cf = 0, cc = 0;
-            float ilo[3] = {0, 0, 0}, ihi[3] = {0, 0, 0};
-            if (lane < count) {
-                const Item it = env.items[first + lane];
-                keep = box_overlap(ulo, uhi, it.lo, it.hi);
-                cf = it.first;
-                cc = it.count;
-#pragma unroll
+            const int ncl = ag.n_clusters;
+            float clo[3] = {__builtin_huge_valf(), __builtin_huge_valf(), __builtin_huge_valf()};
+            float chi[3] = {-__builtin_huge_valf(), -__builtin_huge_valf(), -__builtin_huge_valf()};
+            if (lane < ncl) {  // lane c: cluster c's box swept along the edge
+                const Cluster c = ag.clusters[lane];
+                float alo[3], ahi[3], blo[3], bhi[3];
+                local_box(c.c, c.e, R, T0, alo, ahi);
+                local_box(c.c, c.e, R, TN, blo, bhi);
+    #pragma unroll
                 for (int k = 0; k < 3; ++k) {
-                    ilo[k] = it.lo[k];
-                    ihi[k] = it.hi[k];
+                    clo[k] = fminf(alo[k], blo[k]);
+                    chi[k] = fmaxf(ahi[k], bhi[k]);
                 }
             }
-            cnt.items += (uint32_t)count;
-            uint64_t m = __ballot(keep);
-            if (lev == 0) {
-                uint64_t Tm = 0;  // lane c: the bucket's triangles cluster c's swept box meets
-                for (uint64_t mm = m; mm; mm &= mm - 1) {
-                    const int j = __ffsll((unsigned long long)mm) - 1;
-                    const float elo[3] = {lane_f(ilo[0], j), lane_f(ilo[1], j), lane_f(ilo[2], j)};
-                    const float ehi[3] = {lane_f(ihi[0], j), lane_f(ihi[1], j), lane_f(ihi[2], j)};
-                    if (lane < ncl && box_overlap(clo, chi, elo, ehi)) Tm |= 1ull << j;
+            float ulo[3], uhi[3];  // their union (every lane)
+    #pragma unroll
+            for (int k = 0; k < 3; ++k) {
+                ulo[k] = clo[k];
+                uhi[k] = chi[k];
+    #pragma unroll
+                for (int off = 32; off > 0; off >>= 1) {
+                    ulo[k] = fminf(ulo[k], __shfl_xor(ulo[k], off));
+                    uhi[k] = fmaxf(uhi[k], __shfl_xor(uhi[k], off));
                 }
-                for (uint64_t C = __ballot(Tm != 0); C && !stop; C &= C - 1) {
-                    const int ci = __ffsll((unsigned long long)C) - 1;
-                    uint64_t Tc = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(Tm >> 32), ci) << 32) |
-                                  (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)Tm, ci);
-                    const Cluster c = ag.clusters[ci];
-                    const bool act = lane < c.count;
-                    v3 RQ[3] = {mk(0, 0, 0), mk(0, 0, 0), mk(0, 0, 0)};
-                    float tlo[3] = {0, 0, 0}, thi[3] = {0, 0, 0};
-                    if (act) {  // the lane's triangle rotated (R Q, xform's order before the + T)
-                        const double *tr = ag.tris + (int64_t)(c.first + lane) * 9;
-#pragma unroll
-                        for (int v = 0; v < 3; ++v) {
-                            const double x = tr[3 * v], y = tr[3 * v + 1], z = tr[3 * v + 2];
-                            RQ[v] = mk(R[0] * x + R[1] * y + R[2] * z, R[3] * x + R[4] * y + R[5] * z,
-                                       R[6] * x + R[7] * y + R[8] * z);
-                        }
-#pragma unroll
-                        for (int k = 0; k < 3; ++k) {  // its box swept along the edge
-                            const double a0 = (&RQ[0].x)[k], a1 = (&RQ[1].x)[k], a2 = (&RQ[2].x)[k];
-                            const double mn = dmin(a0, dmin(a1, a2)), mx = dmax(a0, dmax(a1, a2));
-                            tlo[k] = widen_lo(dmin(mn + T0[k], mn + TN[k]));
-                            thi[k] = widen_hi(dmax(mx + T0[k], mx + TN[k]));
-                        }
+            }
+            int sp = 0;
+            int lev = env.n_levels - 1;
+            int32_t first = env.lev_off[lev];
+            int32_t count = env.lev_off[lev + 1] - first;
+            for (;;) {
+                bool keep = false;
+                int32_t cf = 0, cc = 0;
+                float ilo[3] = {0, 0, 0}, ihi[3] = {0, 0, 0};
+                if (lane < count) {
+                    const Item it = env.items[first + lane];
+                    keep = box_overlap(ulo, uhi, it.lo, it.hi);
+                    cf = it.first;
+                    cc = it.count;
+    #pragma unroll
+                    for (int k = 0; k < 3; ++k) {
+                        ilo[k] = it.lo[k];
+                        ihi[k] = it.hi[k];
                     }
-                    for (; Tc && !stop; Tc &= Tc - 1) {
-                        const int j = __ffsll((unsigned long long)Tc) - 1;
+                }
+                cnt.items += (uint32_t)count;
+                uint64_t m = __ballot(keep);
+                if (lev == 0) {
+                    uint64_t Tm = 0;  // lane c: the bucket's triangles cluster c's swept box meets
+                    for (uint64_t mm = m; mm; mm &= mm - 1) {
+                        const int j = __ffsll((unsigned long long)mm) - 1;
                         const float elo[3] = {lane_f(ilo[0], j), lane_f(ilo[1], j), lane_f(ilo[2], j)};
                         const float ehi[3] = {lane_f(ihi[0], j), lane_f(ihi[1], j), lane_f(ihi[2], j)};
-                        bool emit = false;
-                        unsigned q0 = 0, q1 = 0;
-                        bool tail_too = false;
-                        if (act && box_overlap(tlo, thi, elo, ehi)) {
-                            // the item box (widened floats) holds the triangle's exact box: its
-                            // interval holds the exact gate's poses
-                            const double elod[3] = {elo[0], elo[1], elo[2]}, ehid[3] = {ehi[0], ehi[1], ehi[2]};
-                            g.near_range(RQ, elod, ehid, env.tf, q0, q1, tail_too);
-                            emit = q1 > q0 || tail_too;
+                        if (lane < ncl && box_overlap(clo, chi, elo, ehi)) Tm |= 1ull << j;
+                    }
+                    for (uint64_t C = __ballot(Tm != 0); C && !stop; C &= C - 1) {
+                        const int ci = __ffsll((unsigned long long)C) - 1;
+                        const uint32_t Th = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(Tm >> 32), ci);
+                        uint64_t Tc = ((uint64_t)Th << 32) | (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)Tm, ci);
+                        const Cluster c = ag.clusters[ci];
+                        const bool act = lane < c.count;
+                        v3 RQ[3] = {mk(0, 0, 0), mk(0, 0, 0), mk(0, 0, 0)};
+                        float tlo[3] = {0, 0, 0}, thi[3] = {0, 0, 0};
+                        if (act) {  // the lane's triangle rotated (R Q, xform's order before the + T)
+                            const double *tr = ag.tris + (int64_t)(c.first + lane) * 9;
+    #pragma unroll
+                            for (int v = 0; v < 3; ++v) {
+                                const double x = tr[3 * v], y = tr[3 * v + 1], z = tr[3 * v + 2];
+                                RQ[v] = mk(R[0] * x + R[1] * y + R[2] * z, R[3] * x + R[4] * y + R[5] * z,
+                                           R[6] * x + R[7] * y + R[8] * z);
+                            }
+    #pragma unroll
+                            for (int k = 0; k < 3; ++k) {  // its box swept along the edge
+                                const double a0 = (&RQ[0].x)[k], a1 = (&RQ[1].x)[k], a2 = (&RQ[2].x)[k];
+                                const double mn = dmin(a0, dmin(a1, a2)), mx = dmax(a0, dmax(a1, a2));
+                                tlo[k] = widen_lo(dmin(mn + T0[k], mn + TN[k]));
+                                thi[k] = widen_hi(dmax(mx + T0[k], mx + TN[k]));
+                            }
                         }
-                        // a lane's poses go out in chunks of at most kSweepChunk (the tail pose
-                        // with the last): the SAT launch then runs equal short loops a lane
-                        // instead of each wave waiting for its longest interval
-                        for (uint64_t em = __ballot(emit); em && !stop; em = __ballot(emit)) {
-                            const int ne = __popcll(em);
-                            if (nb + ne > kSweepStage) {
-                                if (!sweep_flush(buf, nb, Q, lane)) stop = true;
-                                nb = 0;
-                                if (stop) break;
+                        for (; Tc && !stop; Tc &= Tc - 1) {
+                            const int j = __ffsll((unsigned long long)Tc) - 1;
+                            const float elo[3] = {lane_f(ilo[0], j), lane_f(ilo[1], j), lane_f(ilo[2], j)};
+                            const float ehi[3] = {lane_f(ihi[0], j), lane_f(ihi[1], j), lane_f(ihi[2], j)};
+                            bool emit = false;
+                            unsigned q0 = 0, q1 = 0;
+                            bool tail_too = false;
+                            if (act && box_overlap(tlo, thi, elo, ehi)) {
+                                // the item box (widened floats) holds the triangle's exact box: its
+                                // interval holds the exact gate's poses
+                                const double elod[3] = {elo[0], elo[1], elo[2]}, ehid[3] = {ehi[0], ehi[1], ehi[2]};
+                                g.near_range(RQ, elod, ehid, env.tf, q0, q1, tail_too);
+                                emit = q1 > q0 || tail_too;
                             }
-                            if (emit) {
-                                const int rank = __popcll(em & ((1ull << lane) - 1ull));
-                                const bool last = q1 - q0 <= (unsigned)kSweepChunk;
-                                const unsigned qe = last ? q1 : q0 + kSweepChunk;
-                                buf[nb + rank] = SweepCand{(int32_t)e, c.first + lane, first + j, q0,
-                                                           qe | (last && tail_too ? 0x80000000u : 0u)};
-                                q0 = qe;
-                                emit = !last;
+                            // a lane's poses go out in chunks of at most kSweepChunk (the tail pose
+                            // with the last): the SAT launch then runs equal short loops a lane
+                            // instead of each wave waiting for its longest interval
+                            for (uint64_t em = __ballot(emit); em && !stop; em = __ballot(emit)) {
+                                const int ne = __popcll(em);
+                                const bool fresh = n_edge >= skip;  // a step boundary: all or none of it
+                                if (fresh && nb + ne > kSweepStage) {
+                                    if (!sweep_flush(buf, nb, Q, lane)) stop = full = true;
+                                    nb = 0;
+                                    if (stop) break;
+                                }
+                                if (emit) {
+                                    const int rank = __popcll(em & ((1ull << lane) - 1ull));
+                                    const bool last = q1 - q0 <= (unsigned)kSweepChunk;
+                                    const unsigned qe = last ? q1 : q0 + kSweepChunk;
+                                    if (fresh)
+                                        buf[nb + rank] = SweepCand{(int32_t)e, c.first + lane, first + j, q0,
+                                                                   qe | (last && tail_too ? 0x80000000u : 0u)};
+                                    q0 = qe;
+                                    emit = !last;
+                                }
+                                if (fresh) nb += ne;
+                                n_edge += (uint32_t)ne;
+                                if (n_edge >= upto) stop = true;  // wave-uniform: the next pass resumes here
+                                __builtin_amdgcn_wave_barrier();
                             }
-                            nb += ne;
-                            n_edge += ne;
-                            if (n_edge >= kSweepEdgeCands) stop = true;  // wave-uniform: the edge is deferred
-                            __builtin_amdgcn_wave_barrier();
                         }
                     }
+                } else if (m) {
+                    const int j = __ffsll((unsigned long long)m) - 1;
+                    const uint64_t rest = m & (m - 1);
+                    if (keep && lane != j) {
+                        const int pos = sp + (int)__popcll(rest & ((1ull << lane) - 1));
+                        stk[pos] = ((lev - 1) << 27) | cf;
+                        stk[kSweepStack + pos] = cc;
+                    }
+                    sp += (int)__popcll(rest);
+                    first = __builtin_amdgcn_readfirstlane(__shfl(cf, j));
+                    count = __builtin_amdgcn_readfirstlane(__shfl(cc, j));
+                    lev -= 1;
+                    continue;
                 }
-            } else if (m) {
-                const int j = __ffsll((unsigned long long)m) - 1;
-                const uint64_t rest = m & (m - 1);
-                if (keep && lane != j) {
-                    const int pos = sp + (int)__popcll(rest & ((1ull << lane) - 1));
-                    stk[pos] = ((lev - 1) << 27) | cf;
-                    stk[kSweepStack + pos] = cc;
-                }
-                sp += (int)__popcll(rest);
-                first = __builtin_amdgcn_readfirstlane(__shfl(cf, j));
-                count = __builtin_amdgcn_readfirstlane(__shfl(cc, j));
-                lev -= 1;
-                continue;
+                if (sp == 0 || stop) break;
+                --sp;
+                const int32_t code = __builtin_amdgcn_readfirstlane(stk[sp]);
+                count = __builtin_amdgcn_readfirstlane(stk[kSweepStack + sp]);
+                lev = code >> 27;
+                first = code & ((1 << 27) - 1);
             }
-            if (sp == 0 || stop) break;
-            --sp;
-            const int32_t code = __builtin_amdgcn_readfirstlane(stk[sp]);
-            count = __builtin_amdgcn_readfirstlane(stk[kSweepStack + sp]);
-            lev = code >> 27;
-            first = code & ((1 << 27) - 1);
         }
+        __builtin_amdgcn_wave_barrier();
+        if (!full && !sweep_flush(buf, nb, Q, lane)) stop = full = true;
+        if (lane == 0 && full) {
+            Q.fused[atomicAdd(Q.n + 1, 1u)] = (int32_t)e;
+        } else if (lane == 0 && stop) {
+            const uint32_t k = atomicAdd(Q.n_out, 1u);
+            Q.out_e[k] = (int32_t)e;
+            Q.out_r[k] = n_edge;
+        }
+        __builtin_amdgcn_wave_barrier();
     }
-    __builtin_amdgcn_wave_barrier();
-    if (!sweep_flush(buf, nb, Q, lane)) stop = true;
-    if (stop && lane == 0) Q.deferred[atomicAdd(Q.n + 2, 1u)] = (int32_t)e;
     if (stats && lane == 0 && cnt.waves) {
         atomicAdd(stats + 0, (unsigned long long)cnt.waves);
         atomicAdd(stats + 1, (unsigned long long)cnt.items);
@@ -683,7 +712,7 @@ __global__ __launch_bounds__(kSweepWaves * 64) void k_sweep_cands(EnvDev env, co
 __global__ __launch_bounds__(kSweepWaves * 64) void k_sweep_edge_list(EnvDev env, const AgentDev *__restrict__ link,
                                                                       PrmSrc src, const int32_t *__restrict__ list,
                                                                       const uint32_t *__restrict__ n_list,
-                                                                      uint8_t *verdict) {
+                                                                      uint8_t *verdict, unsigned long long *stats) {
     __shared__ int32_t s_stk[kSweepWaves][2 * kSweepStack];
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
@@ -695,6 +724,12 @@ __global__ __launch_bounds__(kSweepWaves * 64) void k_sweep_edge_list(EnvDev env
         src.edge(e, [&](const double *Rw, const double *tf, const double *tl, auto &&gen) {
             sweep_edge_core(env, link[0], Rw, tf, tl, gen, verdict + e, lane, s_stk[wave], cnt);
         });
+    }
+    if (stats && lane == 0 && cnt.waves) {
+        atomicAdd(stats + 0, (unsigned long long)cnt.waves);
+        atomicAdd(stats + 1, (unsigned long long)cnt.items);
+        atomicAdd(stats + 2, (unsigned long long)cnt.pair_poses);
+        atomicAdd(stats + 3, (unsigned long long)cnt.sat);
     }
 }
 
@@ -794,53 +829,88 @@ void launch_collide_sweep_prm(const EnvDev &env, const AgentDev *d_link, int32_t
         launch_sweep_src(env, d_link, n_clusters, PrmSrc{edges}, E, verdict, stats, stream);
         return;
     }
-    // the candidate queue: 64 a edge (config 4 at --bounds rooms: ~? a edge), at least 4 M; one
-    // per thread of the caller's process (mpt_prm_connect is per thread); an overflow completes
-    // the verdicts with the single-kernel sweep (it skips the edges already decided)
+    // the candidate queue and the pass lists, one set per thread of the caller's process
+    // (mpt_prm_connect is per thread)
     struct Q {
         SweepCand *c = nullptr;
-        int32_t *deferred = nullptr;
+        int32_t *fused = nullptr, *le[2] = {nullptr, nullptr};
+        uint32_t *lr[2] = {nullptr, nullptr};
         uint32_t *n = nullptr, *h = nullptr;
         int64_t cap = 0, ecap = 0;
         ~Q() {
-            if (c) (void)hipFree(c);
-            if (deferred) (void)hipFree(deferred);
-            if (n) (void)hipFree(n);
+            for (void *p : {(void *)c, (void *)fused, (void *)le[0], (void *)le[1], (void *)lr[0], (void *)lr[1],
+                            (void *)n})
+                if (p) (void)hipFree(p);
             if (h) (void)hipHostFree(h);
         }
     };
     static thread_local Q q;
-    // 32 a edge (config 4 at --bounds rooms: ~15 emitted a edge), at least 4 M: a full queue
-    // defers the edges that no longer fit
-    const int64_t want = std::min<int64_t>(std::max<int64_t>(int64_t(1) << 22, 32 * E), int64_t(1) << 31);
+    // 128 candidates an edge (the first pass: at most kSweepEdgeCands + 64 an edge, the cap being
+    // checked after each emission step), at least 4 M; later passes size their caps to it
+    const int64_t want = std::min<int64_t>(std::max<int64_t>(int64_t(1) << 22, 128 * E), int64_t(1) << 31);
     if (want > q.cap || E > q.ecap) {
         hip_check(hipStreamSynchronize(stream), "sync");
-        if (q.c) hip_check(hipFree(q.c), "free");
-        if (q.deferred) hip_check(hipFree(q.deferred), "free");
+        for (void *p : {(void *)q.c, (void *)q.fused, (void *)q.le[0], (void *)q.le[1], (void *)q.lr[0],
+                        (void *)q.lr[1]})
+            if (p) hip_check(hipFree(p), "free");
         hip_check(hipMalloc(&q.c, sizeof(SweepCand) * (size_t)want), "sweep candidates");
-        hip_check(hipMalloc(&q.deferred, sizeof(int32_t) * (size_t)E), "sweep deferred edges");
+        hip_check(hipMalloc(&q.fused, sizeof(int32_t) * (size_t)E), "sweep edge lists");
+        for (int k = 0; k < 2; ++k) {
+            hip_check(hipMalloc(&q.le[k], sizeof(int32_t) * (size_t)E), "sweep edge lists");
+            hip_check(hipMalloc(&q.lr[k], sizeof(uint32_t) * (size_t)E), "sweep edge lists");
+        }
         if (!q.n) hip_check(hipMalloc(&q.n, sizeof(uint32_t) * 4), "sweep counts");
         if (!q.h) hip_check(hipHostMalloc(&q.h, sizeof(uint32_t) * 4), "sweep counts");
         q.cap = want;
         q.ecap = E;
     }
+    // n: [0] queue, [1] fused list, [2 + k] list k
     hip_check(hipMemsetAsync(q.n, 0, sizeof(uint32_t) * 4, stream), "sweep counts zero");
-    const SweepQueue Qd{q.c, q.n, (uint32_t)std::min<int64_t>(q.cap, 0xffffffffLL), q.deferred};
-    const int64_t blocks = (E + kSweepWaves - 1) / kSweepWaves;
-    if (blocks > 0x7fffffff) throw Error{5, "sweep batch too large"};
-    hipLaunchKernelGGL(k_sweep_cands, dim3((unsigned)blocks), dim3(kSweepWaves * 64), 0, stream, env, d_link, edges, E,
-                       verdict, Qd, stats);
-    hip_check(hipGetLastError(), "k_sweep_cands launch");
-    hipLaunchKernelGGL(k_sweep_sat, dim3(4096), dim3(256), 0, stream, env, d_link, edges, Qd, verdict, stats);
-    hip_check(hipGetLastError(), "k_sweep_sat launch");
-    // the deferred edges that no candidate decided: the single-kernel sweep (stops at a contact)
-    hipLaunchKernelGGL(k_sweep_edge_list, dim3(4096), dim3(kSweepWaves * 64), 0, stream, env, d_link, PrmSrc{edges},
-                       q.deferred, q.n + 2, verdict);
-    hip_check(hipGetLastError(), "k_sweep_edge_list launch");
-    hip_check(hipMemcpyAsync(q.h, q.n, sizeof(uint32_t) * 4, hipMemcpyDeviceToHost, stream), "sweep counts");
+    uint64_t emitted = 0;
+    int64_t n_in = E;
+    uint32_t edge_cap = kSweepEdgeCands;
+    int last = -1;  // the list the last pass wrote
+    for (int pass = 0; pass < kSweepPasses && n_in > 0; ++pass) {
+        const int o = pass & 1;
+        if (pass > 0) hip_check(hipMemsetAsync(q.n, 0, sizeof(uint32_t), stream), "sweep counts zero");
+        hip_check(hipMemsetAsync(q.n + 2 + o, 0, sizeof(uint32_t), stream), "sweep counts zero");
+        SweepQueue Qd{q.c, q.n, (uint32_t)std::min<int64_t>(q.cap, 0xffffffffLL), q.fused,
+                      pass ? q.le[1 - o] : nullptr, pass ? q.lr[1 - o] : nullptr, q.n + 2 + (1 - o),
+                      q.le[o], q.lr[o], q.n + 2 + o, edge_cap};
+        const int64_t blocks = pass ? std::min<int64_t>(4096, (n_in + kSweepWaves - 1) / kSweepWaves)
+                                    : (E + kSweepWaves - 1) / kSweepWaves;
+        if (blocks > 0x7fffffff) throw Error{5, "sweep batch too large"};
+        hipLaunchKernelGGL(k_sweep_cands, dim3((unsigned)blocks), dim3(kSweepWaves * 64), 0, stream, env, d_link,
+                           edges, E, verdict, Qd, stats);
+        hip_check(hipGetLastError(), "k_sweep_cands launch");
+        hipLaunchKernelGGL(k_sweep_sat, dim3(4096), dim3(256), 0, stream, env, d_link, edges, Qd, verdict, stats);
+        hip_check(hipGetLastError(), "k_sweep_sat launch");
+        hip_check(hipMemcpyAsync(q.h, q.n, sizeof(uint32_t) * 4, hipMemcpyDeviceToHost, stream), "sweep counts");
+        hip_check(hipStreamSynchronize(stream), "sweep sync");
+        emitted += q.h[0];
+        n_in = q.h[2 + o];  // capped edges (some now decided: the next pass skips those)
+        last = o;
+        // the next cap: x4, as far as the queue holds every capped edge's share
+        const int64_t fit = n_in > 0 ? q.cap / n_in - kWave : 0;
+        edge_cap = (uint32_t)std::max<int64_t>(kSweepEdgeCands, std::min<int64_t>(int64_t(edge_cap) * 4, fit));
+    }
+    // what the passes left (capped at the last pass, or stopped by a full queue): the
+    // single-kernel sweep, which stops at a contact and skips the edges already decided
+    uint64_t to_fused = q.h[1];
+    if (n_in > 0 && last >= 0) {
+        hipLaunchKernelGGL(k_sweep_edge_list, dim3(4096), dim3(kSweepWaves * 64), 0, stream, env, d_link,
+                           PrmSrc{edges}, q.le[last], q.n + 2 + last, verdict, stats);
+        hip_check(hipGetLastError(), "k_sweep_edge_list launch");
+        to_fused += (uint64_t)n_in;
+    }
+    if (q.h[1] > 0) {
+        hipLaunchKernelGGL(k_sweep_edge_list, dim3(4096), dim3(kSweepWaves * 64), 0, stream, env, d_link,
+                           PrmSrc{edges}, q.fused, q.n + 1, verdict, stats);
+        hip_check(hipGetLastError(), "k_sweep_edge_list launch");
+    }
     hip_check(hipStreamSynchronize(stream), "sweep sync");
-    last_sweep_counts[0] = q.h[0];  // candidates emitted (may exceed the queue)
-    last_sweep_counts[1] = q.h[2];  // edges deferred to the single-kernel sweep
+    last_sweep_counts[0] = emitted;    // candidates emitted over the passes
+    last_sweep_counts[1] = to_fused;  // edges left to the single-kernel sweep
 }
 
 }  // namespace mpt

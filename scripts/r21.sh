@@ -40,13 +40,17 @@ python - $O <<'PY'
 import json, sys
 o = sys.argv[1]
 for n in (32, 256):
-    d = json.load(open(f"{o}/c5_{n}_detail.json"))
+    try:
+        d = json.load(open(f"{o}/c5_{n}_detail.json"))
+    except OSError:
+        continue
     st = {k: round(v.get("ms_event_free", v["ms"]), 3) for k, v in d["roofline"]["stages"].items()}
     print(n, round(d["value"] / 1e6, 1), "M/s", round(d["ms_per_step"], 3), "ms", d["seeds_digest"][:8],
           "scratch", round(d["from_scratch"]["valid_per_s"] / 1e6, 1), st)
 try:
     p = json.loads(open(f"{o}/prm.json").read().strip().splitlines()[-1])
-    print("prm", round(p["value"] / 1e6, 2), "M milestones/s", p["device_ms"], p["config"]["free_fraction"])
+    print("prm", round(p["value"] / 1e6, 2), "M milestones/s", p["device_ms"], p["config"]["free_fraction"],
+          p["roofline"].get("work"))
 except Exception as e:
     print("prm", e)
 PY
