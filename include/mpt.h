@@ -138,7 +138,7 @@ mpt_status mpt_prm_connect(const mpt_env *env, const mpt_agent *agent, int32_t a
 /* Diagnostics: out (may be NULL) = the edge sweep's work counters of the calling thread's last
  * mpt_prm_connect made with counters on: waves, env item box tests, (pair, pose) gate tests,
  * exact triangle tests, edges, poses, (edge, triangle, triangle, pose range) candidates emitted,
- * edges deferred to the single-kernel sweep; enable switches the counters on for its later
+ * edges the candidate pass capped (decided by k_sweep_prm); enable switches the counters on for its later
  * calls (one same-address atomic per wave: not for timed calls). */
 mpt_status mpt_prm_stats(int32_t enable, uint64_t out[8]);
 

@@ -74,7 +74,7 @@ __global__ void k_edge_pose_count(PrmEdges P, int64_t E, int64_t *__restrict__ p
 }
 
 // the pose array (mpt_set_collide_mode FUSED: the per-pose walk reads it; the sweep generates
-// the same poses in-kernel instead, sweep.hip k_sweep_edge<PrmSrc>)
+// the same poses in-kernel instead, sweep.hip PrmEdge)
 __global__ void k_edge_poses(PrmEdges P, int64_t E, const int64_t *__restrict__ poff, double *__restrict__ poses,
                              int32_t *__restrict__ pose_edge) {
     const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;

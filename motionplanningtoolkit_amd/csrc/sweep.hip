@@ -156,161 +156,6 @@ __device__ __forceinline__ void sweep_core(const EnvDev &env, const AgentDev &ag
     }
 }
 
-// One edge, every agent cluster (at most 64: lane c holds cluster c): the wave walks the env
-// tree once against the union of the clusters' swept boxes and fans out to the clusters only at
-// the env triangles that meet it -- the clusters whose swept box meets the triangle, each one's
-// triangles rotated then (lanes = its triangles) and tested over the poses as in sweep_core.
-// Same verdicts as sweep_core over every cluster: a contact is a contact whichever order finds it.
-template <class Gen>
-__device__ __forceinline__ void sweep_edge_core(const EnvDev &env, const AgentDev &ag, const double *Rw,
-                                                const double *tf, const double *tl, Gen gen, uint8_t *flag, int lane,
-                                                int32_t *stk, SweepCounters &cnt) {
-    ++cnt.waves;
-    double R[9], T0[3], TN[3];
-    relative_transform(env.tf, env.tf + 9, Rw, tf, R, T0);
-    env_rel_t(env, tl, TN);
-#pragma unroll
-    for (int i = 0; i < 9; ++i) R[i] = uniform_d(R[i]);
-#pragma unroll
-    for (int i = 0; i < 3; ++i) {
-        T0[i] = uniform_d(T0[i]);
-        TN[i] = uniform_d(TN[i]);
-    }
-    const int ncl = ag.n_clusters;
-    float clo[3] = {__builtin_huge_valf(), __builtin_huge_valf(), __builtin_huge_valf()};
-    float chi[3] = {-__builtin_huge_valf(), -__builtin_huge_valf(), -__builtin_huge_valf()};
-    if (lane < ncl) {  // lane c: cluster c's box swept along the edge
-        const Cluster c = ag.clusters[lane];
-        float alo[3], ahi[3], blo[3], bhi[3];
-        local_box(c.c, c.e, R, T0, alo, ahi);
-        local_box(c.c, c.e, R, TN, blo, bhi);
-#pragma unroll
-        for (int k = 0; k < 3; ++k) {
-            clo[k] = fminf(alo[k], blo[k]);
-            chi[k] = fmaxf(ahi[k], bhi[k]);
-        }
-    }
-    float ulo[3], uhi[3];  // their union (every lane)
-#pragma unroll
-    for (int k = 0; k < 3; ++k) {
-        ulo[k] = clo[k];
-        uhi[k] = chi[k];
-#pragma unroll
-        for (int off = 32; off > 0; off >>= 1) {
-            ulo[k] = fminf(ulo[k], __shfl_xor(ulo[k], off));
-            uhi[k] = fmaxf(uhi[k], __shfl_xor(uhi[k], off));
-        }
-    }
-    int sp = 0;
-    int lev = env.n_levels - 1;
-    int32_t first = env.lev_off[lev];
-    int32_t count = env.lev_off[lev + 1] - first;
-    for (;;) {
-        bool keep = false;
-        int32_t cf = 0, cc = 0;
-        float ilo[3] = {0, 0, 0}, ihi[3] = {0, 0, 0};
-        if (lane < count) {
-            const Item it = env.items[first + lane];
-            keep = box_overlap(ulo, uhi, it.lo, it.hi);
-            cf = it.first;
-            cc = it.count;
-#pragma unroll
-            for (int k = 0; k < 3; ++k) {
-                ilo[k] = it.lo[k];
-                ihi[k] = it.hi[k];
-            }
-        }
-        cnt.items += (uint32_t)count;
-        uint64_t m = __ballot(keep);
-        if (lev == 0) {
-            // the bucket's env triangles meeting the union (lane j: triangle first + j): lane c
-            // (a cluster) collects those its swept box meets, then the wave visits each such
-            // cluster once -- its triangles rotated once for every triangle of the bucket it
-            // meets (round 4 rotated a cluster again for each env triangle, after a load of the
-            // edge's verdict flag no other wave writes here: one wave an edge)
-            uint64_t Tm = 0;
-            for (uint64_t mm = m; mm; mm &= mm - 1) {
-                const int j = __ffsll((unsigned long long)mm) - 1;
-                const float elo[3] = {lane_f(ilo[0], j), lane_f(ilo[1], j), lane_f(ilo[2], j)};
-                const float ehi[3] = {lane_f(ihi[0], j), lane_f(ihi[1], j), lane_f(ihi[2], j)};
-                if (lane < ncl && box_overlap(clo, chi, elo, ehi)) Tm |= 1ull << j;
-            }
-            for (uint64_t C = __ballot(Tm != 0); C; C &= C - 1) {
-                const int ci = __ffsll((unsigned long long)C) - 1;
-                uint64_t Tc = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(Tm >> 32), ci) << 32) |
-                              (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)Tm, ci);
-                const Cluster c = ag.clusters[ci];
-                const bool act = lane < c.count;
-                v3 RQ[3] = {mk(0, 0, 0), mk(0, 0, 0), mk(0, 0, 0)};
-                float tlo[3] = {0, 0, 0}, thi[3] = {0, 0, 0};
-                if (act) {  // the lane's triangle rotated once (R Q, xform's order before the + T)
-                    const double *tr = ag.tris + (int64_t)(c.first + lane) * 9;
-#pragma unroll
-                    for (int v = 0; v < 3; ++v) {
-                        const double x = tr[3 * v], y = tr[3 * v + 1], z = tr[3 * v + 2];
-                        RQ[v] = mk(R[0] * x + R[1] * y + R[2] * z, R[3] * x + R[4] * y + R[5] * z,
-                                   R[6] * x + R[7] * y + R[8] * z);
-                    }
-#pragma unroll
-                    for (int k = 0; k < 3; ++k) {  // its box swept along the edge
-                        const double a0 = (&RQ[0].x)[k], a1 = (&RQ[1].x)[k], a2 = (&RQ[2].x)[k];
-                        const double mn = dmin(a0, dmin(a1, a2)), mx = dmax(a0, dmax(a1, a2));
-                        tlo[k] = widen_lo(dmin(mn + T0[k], mn + TN[k]));
-                        thi[k] = widen_hi(dmax(mx + T0[k], mx + TN[k]));
-                    }
-                }
-                for (; Tc; Tc &= Tc - 1) {
-                    const int j = __ffsll((unsigned long long)Tc) - 1;
-                    const int32_t t = first + j;  // level 0: item index = triangle index
-                    const float elo[3] = {lane_f(ilo[0], j), lane_f(ilo[1], j), lane_f(ilo[2], j)};
-                    const float ehi[3] = {lane_f(ihi[0], j), lane_f(ihi[1], j), lane_f(ihi[2], j)};
-                    const bool near = act && box_overlap(tlo, thi, elo, ehi);
-                    if (!__ballot(near)) continue;
-                    const EnvTri &E = env.tris[t];
-                    bool hit = false;
-                    if (near) {
-                        gen([&](const double *tw) {
-                            double Tp[3];
-                            env_rel_t(env, tw, Tp);
-                            const v3 Q1 = mk(RQ[0].x + Tp[0], RQ[0].y + Tp[1], RQ[0].z + Tp[2]);
-                            const v3 Q2 = mk(RQ[1].x + Tp[0], RQ[1].y + Tp[1], RQ[1].z + Tp[2]);
-                            const v3 Q3 = mk(RQ[2].x + Tp[0], RQ[2].y + Tp[1], RQ[2].z + Tp[2]);
-                            ++cnt.pair_poses;
-                            if (!tri_gate(E.lo, E.hi, Q1, Q2, Q3)) return false;
-                            ++cnt.sat;
-                            hit = tri_intersect(E, Q1, Q2, Q3);
-                            return hit;
-                        }, RQ, E, env);
-                    }
-                    if (__ballot(hit)) {
-                        if (lane == 0) __hip_atomic_store(flag, (uint8_t)1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                        return;
-                    }
-                }
-            }
-        } else if (m) {
-            const int j = __ffsll((unsigned long long)m) - 1;
-            const uint64_t rest = m & (m - 1);
-            if (keep && lane != j) {
-                const int pos = sp + (int)__popcll(rest & ((1ull << lane) - 1));
-                stk[pos] = ((lev - 1) << 27) | cf;
-                stk[kSweepStack + pos] = cc;
-            }
-            sp += (int)__popcll(rest);
-            first = __builtin_amdgcn_readfirstlane(__shfl(cf, j));
-            count = __builtin_amdgcn_readfirstlane(__shfl(cc, j));
-            lev -= 1;
-            continue;
-        }
-        if (sp == 0) return;
-        --sp;
-        const int32_t code = __builtin_amdgcn_readfirstlane(stk[sp]);
-        count = __builtin_amdgcn_readfirstlane(stk[kSweepStack + sp]);
-        lev = code >> 27;
-        first = code & ((1 << 27) - 1);
-    }
-}
-
 // Where an edge's poses come from.  A source's edge(e, core) calls core(Rw, tf, tl, gen) with
 // the edge's world rotation, its first and last pose's translation and the pose generator
 // (gen(f, RQ, E, env): f(world translation) for each pose in order until f returns true --
@@ -345,28 +190,6 @@ struct PrmSrc {
         });
     }
 };
-
-// one wave an edge (agents of at most 64 clusters)
-template <class Src>
-__global__ __launch_bounds__(kSweepWaves * 64) void k_sweep_edge(EnvDev env, const AgentDev *__restrict__ link,
-                                                                 Src src, int64_t E, uint8_t *verdict,
-                                                                 unsigned long long *stats) {
-    __shared__ int32_t s_stk[kSweepWaves][2 * kSweepStack];
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int lane = threadIdx.x & 63;
-    const int64_t e = (int64_t)blockIdx.x * kSweepWaves + wave;
-    SweepCounters cnt;
-    if (e < E && !load_flag(verdict + e))
-        src.edge(e, [&](const double *Rw, const double *tf, const double *tl, auto &&gen) {
-            sweep_edge_core(env, link[0], Rw, tf, tl, gen, verdict + e, lane, s_stk[wave], cnt);
-        });
-    if (stats && lane == 0 && cnt.waves) {
-        atomicAdd(stats + 0, (unsigned long long)cnt.waves);
-        atomicAdd(stats + 1, (unsigned long long)cnt.items);
-        atomicAdd(stats + 2, (unsigned long long)cnt.pair_poses);
-        atomicAdd(stats + 3, (unsigned long long)cnt.sat);
-    }
-}
 
 // one wave an (edge, cluster) (agents of more than 64 clusters)
 template <class Src>
@@ -446,14 +269,20 @@ __global__ __launch_bounds__(kSweepWaves * 64) void k_sweep_lite(EnvDev env, con
     }
 }
 
-// ---- PRM edges in two phases: the walk and fan-out emit (edge, agent triangle, env triangle,
-// pose range) candidates; a second launch runs the gate + SAT over each candidate's poses, one
-// candidate a lane.  The single-kernel sweep (k_sweep_edge) held the SAT's registers across its
-// walk (~200 VGPRs: 2 waves a SIMD for a latency-bound walk) and ran each SAT on a wave with a
-// few lanes active; split, the walk runs at more waves a SIMD and the SATs on full waves.
-// Verdicts are the same set: every (edge, agent triangle, env triangle, pose) the fused form
-// tests is in some candidate (same fan-out, same box tests, the same pose interval), and the
-// candidate's test is the same operations.
+// ---- PRM edges (mpt_prm_connect's sweep path), three launches over the roadmap:
+//  1. k_sweep_cands: one wave an edge walks the env tree (prm_walk) and emits (edge, agent
+//     triangle, env triangle, pose range) candidates, at most kSweepEdgeCands an edge: an edge
+//     that reaches the cap stops and is listed;
+//  2. k_sweep_sat: the gate + SAT over each candidate's poses, one candidate a lane (full waves
+//     at full occupancy; ~55 % of config 4's edges at --bounds rooms are decided here, free);
+//  3. k_sweep_prm over the listed edges (mostly colliding ones): the walk again, every
+//     kSweepCoarse-th pose of each pair's interval first (a contact with a wall lasts many
+//     poses: this pass finds nearly every colliding edge's), then the poses it skipped; the
+//     gate passes batched into SATs of 64 a wave, the edge ending at its first contact.
+// Verdicts are the same set: every (edge, agent triangle, env triangle, pose) the reference
+// tests either is in some candidate or in one of k_sweep_prm's two pose sets (same fan-out, same
+// box tests, the same pose interval), each with the same operations, and a contact found
+// anywhere is a contact.
 
 struct SweepCand {
     int32_t e, atri, etri;
@@ -464,9 +293,9 @@ constexpr int kSweepChunk = 8;    // poses a candidate covers at most
 
 struct SweepQueue {
     SweepCand *c;
-    uint32_t *n;  // [0] candidates written (may pass cap), [1] edges sent to the single-kernel sweep
+    uint32_t *n;  // [0] candidates written (may pass cap), [1] edges a full queue stopped
     uint32_t cap;
-    int32_t *fused;       // [E] edges a full queue stopped (the single-kernel sweep decides them)
+    int32_t *fused;       // [E] edges a full queue stopped (k_sweep_prm decides them)
     const int32_t *in_e;  // this pass's edges (null: every edge) and their resume indices
     const uint32_t *in_r;
     const uint32_t *n_in;
@@ -478,15 +307,20 @@ struct SweepQueue {
 // The passes: each emits an edge's candidates from where its previous pass stopped (its resume
 // index: candidates are numbered in the walk's order, which is the same every pass) up to the
 // pass's per-edge cap, then the SAT launch decides what it can; an edge still undecided at the
-// cap goes to the next pass with a larger cap; after the last pass the single-kernel sweep takes
-// the edges still undecided.  Emitting every candidate of an edge at once (config 4 at --bounds
-// rooms: some edges emit thousands) cost a second a roadmap.  Config 4 at --bounds rooms,
-// collision ms by the number of passes (first cap 64, x4 a pass, as far as the queue holds):
-// 1: 47.5, 2: 52.0, 3: 52.9, 4: 60.2 -- the edges a pass leaves undecided mostly stay so over
-// hundreds more candidates, whose SATs a pass runs in parallel where the single-kernel sweep
-// stops at the edge's first contact; caps 512 / 2048 in one pass: 53 / 53.
+// cap goes to the next pass with a larger cap; after the last pass k_sweep_prm takes the edges
+// still undecided.  Emitting every candidate of an edge at once (config 4 at --bounds rooms:
+// some edges emit thousands) cost a second a roadmap.  Config 4 at --bounds rooms, collision ms
+// by the number of passes (first cap 64, x4 a pass, as far as the queue holds; the tail then in
+// the round's first single-kernel sweep): 1: 47.5, 2: 52.0, 3: 52.9, 4: 60.2 -- an edge a pass
+// leaves undecided mostly stays so over hundreds more candidates, whose SATs a pass runs in
+// parallel where the walk kernels stop at the edge's first contact; caps 512 / 2048 in one
+// pass: 53 / 53.
 constexpr int kSweepEdgeCands = 64;  // the first pass's cap; x4 a pass
-constexpr int kSweepPasses = 1;      // then the single-kernel sweep takes what is left
+constexpr int kSweepPasses = 1;      // then k_sweep_prm takes what is left
+// k_sweep_prm's first pose stride (config 4 at --bounds rooms, collision ms: no coarse pass
+// 30.8, stride 4: 19.1, 8: 17.9, 16: 23.9; the coarse pass over every edge before the
+// candidates instead: 20.0, and over every edge with no candidates at all: 21.2)
+constexpr unsigned kSweepCoarse = 8;
 
 // false when the queue is full: the wave's edge is then deferred (the candidates that did fit
 // are tested all the same, which is harmless: a contact among them is a contact)
@@ -500,9 +334,166 @@ __device__ __forceinline__ bool sweep_flush(SweepCand *buf, int nb, const SweepQ
     return base + (uint32_t)nb <= Q.cap;
 }
 
-// One wave an edge: sweep_edge_core's walk and fan-out (union of the clusters' swept boxes,
-// per-bucket cluster masks, each cluster rotated once a bucket), a candidate per lane whose
-// swept triangle box meets the env triangle's item box and whose pose interval is not empty
+// A PRM edge for one wave: every field wave-uniform (scalar registers), and the env-relative
+// rotation R and translations T0 / TN of its first and last pose
+__device__ __forceinline__ PrmEdge prm_edge_uniform(const PrmEdges &P, int64_t e) {
+    PrmEdge g = prm_edge(P, e);
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        g.s[k] = uniform_d(g.s[k]);
+        g.end[k] = uniform_d(g.end[k]);
+        g.dx[k] = uniform_d(g.dx[k]);
+    }
+#pragma unroll
+    for (int k = 0; k < 9; ++k) g.R[k] = uniform_d(g.R[k]);
+    g.step = uniform_d(g.step);
+    g.it = __builtin_amdgcn_readfirstlane(g.it);
+    g.tail = __builtin_amdgcn_readfirstlane((int)g.tail) != 0;
+    return g;
+}
+
+__device__ __forceinline__ void prm_edge_frame(const EnvDev &env, const PrmEdge &g, double R[9], double T0[3],
+                                               double TN[3]) {
+    double tf[3], tl[3];
+    g.first(tf);
+    g.last(tl);
+    relative_transform(env.tf, env.tf + 9, g.R, tf, R, T0);
+    env_rel_t(env, tl, TN);
+#pragma unroll
+    for (int i = 0; i < 9; ++i) R[i] = uniform_d(R[i]);
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        T0[i] = uniform_d(T0[i]);
+        TN[i] = uniform_d(TN[i]);
+    }
+}
+
+// the agent triangle a rotated (R Q, xform's products and sums before the + T)
+__device__ __forceinline__ void rotate_tri(const AgentDev &ag, int32_t a, const double *R, v3 RQ[3]) {
+    const double *tr = ag.tris + (int64_t)a * 9;
+#pragma unroll
+    for (int v = 0; v < 3; ++v) {
+        const double x = tr[3 * v], y = tr[3 * v + 1], z = tr[3 * v + 2];
+        RQ[v] = mk(R[0] * x + R[1] * y + R[2] * z, R[3] * x + R[4] * y + R[5] * z, R[6] * x + R[7] * y + R[8] * z);
+    }
+}
+
+// One wave an edge, every agent cluster (at most 64: lane c holds cluster c): the wave walks the
+// env tree once against the union of the clusters' swept boxes and fans out to the clusters only
+// at the env triangles that meet it, each cluster rotated once a bucket.  visit(c, t, act, RQ, elo, ehi)
+// runs for each (cluster c, env triangle t) with a lane (act: one of c's triangles, rotated in
+// RQ) whose swept triangle box meets t's item box elo / ehi (near); a true from it (wave-uniform)
+// ends the walk.
+template <class Visit>
+__device__ __forceinline__ void prm_walk(const EnvDev &env, const AgentDev &ag, const double *R, const double *T0,
+                                         const double *TN, int lane, int32_t *stk, SweepCounters &cnt,
+                                         Visit &&visit) {
+    const int ncl = ag.n_clusters;
+    float clo[3] = {__builtin_huge_valf(), __builtin_huge_valf(), __builtin_huge_valf()};
+    float chi[3] = {-__builtin_huge_valf(), -__builtin_huge_valf(), -__builtin_huge_valf()};
+    if (lane < ncl) {  // lane c: cluster c's box swept along the edge
+        const Cluster c = ag.clusters[lane];
+        float alo[3], ahi[3], blo[3], bhi[3];
+        local_box(c.c, c.e, R, T0, alo, ahi);
+        local_box(c.c, c.e, R, TN, blo, bhi);
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            clo[k] = fminf(alo[k], blo[k]);
+            chi[k] = fmaxf(ahi[k], bhi[k]);
+        }
+    }
+    float ulo[3], uhi[3];  // their union (every lane)
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        ulo[k] = clo[k];
+        uhi[k] = chi[k];
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) {
+            ulo[k] = fminf(ulo[k], __shfl_xor(ulo[k], off));
+            uhi[k] = fmaxf(uhi[k], __shfl_xor(uhi[k], off));
+        }
+    }
+    bool stop = false;
+    int sp = 0;
+    int lev = env.n_levels - 1;
+    int32_t first = env.lev_off[lev];
+    int32_t count = env.lev_off[lev + 1] - first;
+    for (;;) {
+        bool keep = false;
+        int32_t cf = 0, cc = 0;
+        float ilo[3] = {0, 0, 0}, ihi[3] = {0, 0, 0};
+        if (lane < count) {
+            const Item it = env.items[first + lane];
+            keep = box_overlap(ulo, uhi, it.lo, it.hi);
+            cf = it.first;
+            cc = it.count;
+#pragma unroll
+            for (int k = 0; k < 3; ++k) {
+                ilo[k] = it.lo[k];
+                ihi[k] = it.hi[k];
+            }
+        }
+        cnt.items += (uint32_t)count;
+        uint64_t m = __ballot(keep);
+        if (lev == 0) {
+            uint64_t Tm = 0;  // lane c: the bucket's triangles cluster c's swept box meets
+            for (uint64_t mm = m; mm; mm &= mm - 1) {
+                const int j = __ffsll((unsigned long long)mm) - 1;
+                const float elo[3] = {lane_f(ilo[0], j), lane_f(ilo[1], j), lane_f(ilo[2], j)};
+                const float ehi[3] = {lane_f(ihi[0], j), lane_f(ihi[1], j), lane_f(ihi[2], j)};
+                if (lane < ncl && box_overlap(clo, chi, elo, ehi)) Tm |= 1ull << j;
+            }
+            for (uint64_t C = __ballot(Tm != 0); C && !stop; C &= C - 1) {
+                const int ci = __ffsll((unsigned long long)C) - 1;
+                const uint32_t Th = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(Tm >> 32), ci);
+                uint64_t Tc = ((uint64_t)Th << 32) | (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)Tm, ci);
+                const Cluster c = ag.clusters[ci];
+                const bool act = lane < c.count;
+                v3 RQ[3] = {mk(0, 0, 0), mk(0, 0, 0), mk(0, 0, 0)};
+                float tlo[3] = {0, 0, 0}, thi[3] = {0, 0, 0};
+                if (act) {
+                    rotate_tri(ag, c.first + lane, R, RQ);
+#pragma unroll
+                    for (int k = 0; k < 3; ++k) {  // its box swept along the edge
+                        const double a0 = (&RQ[0].x)[k], a1 = (&RQ[1].x)[k], a2 = (&RQ[2].x)[k];
+                        const double mn = dmin(a0, dmin(a1, a2)), mx = dmax(a0, dmax(a1, a2));
+                        tlo[k] = widen_lo(dmin(mn + T0[k], mn + TN[k]));
+                        thi[k] = widen_hi(dmax(mx + T0[k], mx + TN[k]));
+                    }
+                }
+                for (; Tc && !stop; Tc &= Tc - 1) {
+                    const int j = __ffsll((unsigned long long)Tc) - 1;
+                    const float elo[3] = {lane_f(ilo[0], j), lane_f(ilo[1], j), lane_f(ilo[2], j)};
+                    const float ehi[3] = {lane_f(ihi[0], j), lane_f(ihi[1], j), lane_f(ihi[2], j)};
+                    const bool near = act && box_overlap(tlo, thi, elo, ehi);
+                    if (!__ballot(near)) continue;
+                    stop = visit(c, first + j, near, RQ, elo, ehi);  // level 0: item index = triangle index
+                }
+            }
+        } else if (m) {
+            const int j = __ffsll((unsigned long long)m) - 1;
+            const uint64_t rest = m & (m - 1);
+            if (keep && lane != j) {
+                const int pos = sp + (int)__popcll(rest & ((1ull << lane) - 1));
+                stk[pos] = ((lev - 1) << 27) | cf;
+                stk[kSweepStack + pos] = cc;
+            }
+            sp += (int)__popcll(rest);
+            first = __builtin_amdgcn_readfirstlane(__shfl(cf, j));
+            count = __builtin_amdgcn_readfirstlane(__shfl(cc, j));
+            lev -= 1;
+            continue;
+        }
+        if (sp == 0 || stop) return;
+        --sp;
+        const int32_t code = __builtin_amdgcn_readfirstlane(stk[sp]);
+        count = __builtin_amdgcn_readfirstlane(stk[kSweepStack + sp]);
+        lev = code >> 27;
+        first = code & ((1 << 27) - 1);
+    }
+}
+
+// One wave an edge: prm_walk, a candidate per near lane whose pose interval is not empty
 __global__ __launch_bounds__(kSweepWaves * 64) void k_sweep_cands(EnvDev env, const AgentDev *__restrict__ link,
                                                                   PrmEdges P, int64_t E, const uint8_t *verdict,
                                                                   SweepQueue Q, unsigned long long *stats) {
@@ -512,8 +503,6 @@ __global__ __launch_bounds__(kSweepWaves * 64) void k_sweep_cands(EnvDev env, co
     const int lane = threadIdx.x & 63;
     SweepCounters cnt;
     SweepCand *buf = s_buf[wave];
-    int32_t *stk = s_stk[wave];
-    const AgentDev &ag = link[0];
     const int64_t n_list = Q.in_e ? (int64_t)*Q.n_in : E;
     for (int64_t i = (int64_t)blockIdx.x * kSweepWaves + wave; i < n_list; i += (int64_t)gridDim.x * kSweepWaves) {
         const int64_t e = Q.in_e ? Q.in_e[i] : i;
@@ -523,173 +512,49 @@ __global__ __launch_bounds__(kSweepWaves * 64) void k_sweep_cands(EnvDev env, co
         int nb = 0;
         bool stop = false, full = false;
         if (!load_flag(verdict + e)) {
-            PrmEdge g = prm_edge(P, e);
-    #pragma unroll
-            for (int k = 0; k < 3; ++k) {
-                g.s[k] = uniform_d(g.s[k]);
-                g.end[k] = uniform_d(g.end[k]);
-                g.dx[k] = uniform_d(g.dx[k]);
-            }
-    #pragma unroll
-            for (int k = 0; k < 9; ++k) g.R[k] = uniform_d(g.R[k]);
-            g.step = uniform_d(g.step);
-            g.it = __builtin_amdgcn_readfirstlane(g.it);
-            g.tail = __builtin_amdgcn_readfirstlane((int)g.tail) != 0;
-            double tf[3], tl[3];
-            g.first(tf);
-            g.last(tl);
+            const PrmEdge g = prm_edge_uniform(P, e);
             ++cnt.waves;
             double R[9], T0[3], TN[3];
-            relative_transform(env.tf, env.tf + 9, g.R, tf, R, T0);
-            env_rel_t(env, tl, TN);
-    #pragma unroll
-            for (int i = 0; i < 9; ++i) R[i] = uniform_d(R[i]);
-    #pragma unroll
-            for (int i = 0; i < 3; ++i) {
-                T0[i] = uniform_d(T0[i]);
-                TN[i] = uniform_d(TN[i]);
-            }
-            const int ncl = ag.n_clusters;
-            float clo[3] = {__builtin_huge_valf(), __builtin_huge_valf(), __builtin_huge_valf()};
-            float chi[3] = {-__builtin_huge_valf(), -__builtin_huge_valf(), -__builtin_huge_valf()};
-            if (lane < ncl) {  // lane c: cluster c's box swept along the edge
-                const Cluster c = ag.clusters[lane];
-                float alo[3], ahi[3], blo[3], bhi[3];
-                local_box(c.c, c.e, R, T0, alo, ahi);
-                local_box(c.c, c.e, R, TN, blo, bhi);
-    #pragma unroll
-                for (int k = 0; k < 3; ++k) {
-                    clo[k] = fminf(alo[k], blo[k]);
-                    chi[k] = fmaxf(ahi[k], bhi[k]);
-                }
-            }
-            float ulo[3], uhi[3];  // their union (every lane)
-    #pragma unroll
-            for (int k = 0; k < 3; ++k) {
-                ulo[k] = clo[k];
-                uhi[k] = chi[k];
-    #pragma unroll
-                for (int off = 32; off > 0; off >>= 1) {
-                    ulo[k] = fminf(ulo[k], __shfl_xor(ulo[k], off));
-                    uhi[k] = fmaxf(uhi[k], __shfl_xor(uhi[k], off));
-                }
-            }
-            int sp = 0;
-            int lev = env.n_levels - 1;
-            int32_t first = env.lev_off[lev];
-            int32_t count = env.lev_off[lev + 1] - first;
-            for (;;) {
-                bool keep = false;
-                int32_t cf = 0, cc = 0;
-                float ilo[3] = {0, 0, 0}, ihi[3] = {0, 0, 0};
-                if (lane < count) {
-                    const Item it = env.items[first + lane];
-                    keep = box_overlap(ulo, uhi, it.lo, it.hi);
-                    cf = it.first;
-                    cc = it.count;
-    #pragma unroll
-                    for (int k = 0; k < 3; ++k) {
-                        ilo[k] = it.lo[k];
-                        ihi[k] = it.hi[k];
-                    }
-                }
-                cnt.items += (uint32_t)count;
-                uint64_t m = __ballot(keep);
-                if (lev == 0) {
-                    uint64_t Tm = 0;  // lane c: the bucket's triangles cluster c's swept box meets
-                    for (uint64_t mm = m; mm; mm &= mm - 1) {
-                        const int j = __ffsll((unsigned long long)mm) - 1;
-                        const float elo[3] = {lane_f(ilo[0], j), lane_f(ilo[1], j), lane_f(ilo[2], j)};
-                        const float ehi[3] = {lane_f(ihi[0], j), lane_f(ihi[1], j), lane_f(ihi[2], j)};
-                        if (lane < ncl && box_overlap(clo, chi, elo, ehi)) Tm |= 1ull << j;
-                    }
-                    for (uint64_t C = __ballot(Tm != 0); C && !stop; C &= C - 1) {
-                        const int ci = __ffsll((unsigned long long)C) - 1;
-                        const uint32_t Th = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(Tm >> 32), ci);
-                        uint64_t Tc = ((uint64_t)Th << 32) | (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)Tm, ci);
-                        const Cluster c = ag.clusters[ci];
-                        const bool act = lane < c.count;
-                        v3 RQ[3] = {mk(0, 0, 0), mk(0, 0, 0), mk(0, 0, 0)};
-                        float tlo[3] = {0, 0, 0}, thi[3] = {0, 0, 0};
-                        if (act) {  // the lane's triangle rotated (R Q, xform's order before the + T)
-                            const double *tr = ag.tris + (int64_t)(c.first + lane) * 9;
-    #pragma unroll
-                            for (int v = 0; v < 3; ++v) {
-                                const double x = tr[3 * v], y = tr[3 * v + 1], z = tr[3 * v + 2];
-                                RQ[v] = mk(R[0] * x + R[1] * y + R[2] * z, R[3] * x + R[4] * y + R[5] * z,
-                                           R[6] * x + R[7] * y + R[8] * z);
-                            }
-    #pragma unroll
-                            for (int k = 0; k < 3; ++k) {  // its box swept along the edge
-                                const double a0 = (&RQ[0].x)[k], a1 = (&RQ[1].x)[k], a2 = (&RQ[2].x)[k];
-                                const double mn = dmin(a0, dmin(a1, a2)), mx = dmax(a0, dmax(a1, a2));
-                                tlo[k] = widen_lo(dmin(mn + T0[k], mn + TN[k]));
-                                thi[k] = widen_hi(dmax(mx + T0[k], mx + TN[k]));
-                            }
-                        }
-                        for (; Tc && !stop; Tc &= Tc - 1) {
-                            const int j = __ffsll((unsigned long long)Tc) - 1;
-                            const float elo[3] = {lane_f(ilo[0], j), lane_f(ilo[1], j), lane_f(ilo[2], j)};
-                            const float ehi[3] = {lane_f(ihi[0], j), lane_f(ihi[1], j), lane_f(ihi[2], j)};
-                            bool emit = false;
-                            unsigned q0 = 0, q1 = 0;
-                            bool tail_too = false;
-                            if (act && box_overlap(tlo, thi, elo, ehi)) {
-                                // the item box (widened floats) holds the triangle's exact box: its
-                                // interval holds the exact gate's poses
-                                const double elod[3] = {elo[0], elo[1], elo[2]}, ehid[3] = {ehi[0], ehi[1], ehi[2]};
-                                g.near_range(RQ, elod, ehid, env.tf, q0, q1, tail_too);
-                                emit = q1 > q0 || tail_too;
-                            }
-                            // a lane's poses go out in chunks of at most kSweepChunk (the tail pose
-                            // with the last): the SAT launch then runs equal short loops a lane
-                            // instead of each wave waiting for its longest interval
-                            for (uint64_t em = __ballot(emit); em && !stop; em = __ballot(emit)) {
-                                const int ne = __popcll(em);
-                                const bool fresh = n_edge >= skip;  // a step boundary: all or none of it
-                                if (fresh && nb + ne > kSweepStage) {
-                                    if (!sweep_flush(buf, nb, Q, lane)) stop = full = true;
-                                    nb = 0;
-                                    if (stop) break;
-                                }
-                                if (emit) {
-                                    const int rank = __popcll(em & ((1ull << lane) - 1ull));
-                                    const bool last = q1 - q0 <= (unsigned)kSweepChunk;
-                                    const unsigned qe = last ? q1 : q0 + kSweepChunk;
-                                    if (fresh)
-                                        buf[nb + rank] = SweepCand{(int32_t)e, c.first + lane, first + j, q0,
-                                                                   qe | (last && tail_too ? 0x80000000u : 0u)};
-                                    q0 = qe;
-                                    emit = !last;
-                                }
-                                if (fresh) nb += ne;
-                                n_edge += (uint32_t)ne;
-                                if (n_edge >= upto) stop = true;  // wave-uniform: the next pass resumes here
-                                __builtin_amdgcn_wave_barrier();
-                            }
-                        }
-                    }
-                } else if (m) {
-                    const int j = __ffsll((unsigned long long)m) - 1;
-                    const uint64_t rest = m & (m - 1);
-                    if (keep && lane != j) {
-                        const int pos = sp + (int)__popcll(rest & ((1ull << lane) - 1));
-                        stk[pos] = ((lev - 1) << 27) | cf;
-                        stk[kSweepStack + pos] = cc;
-                    }
-                    sp += (int)__popcll(rest);
-                    first = __builtin_amdgcn_readfirstlane(__shfl(cf, j));
-                    count = __builtin_amdgcn_readfirstlane(__shfl(cc, j));
-                    lev -= 1;
-                    continue;
-                }
-                if (sp == 0 || stop) break;
-                --sp;
-                const int32_t code = __builtin_amdgcn_readfirstlane(stk[sp]);
-                count = __builtin_amdgcn_readfirstlane(stk[kSweepStack + sp]);
-                lev = code >> 27;
-                first = code & ((1 << 27) - 1);
-            }
+            prm_edge_frame(env, g, R, T0, TN);
+            prm_walk(env, link[0], R, T0, TN, lane, s_stk[wave], cnt,
+                     [&](const Cluster &c, int32_t t, bool near, const v3 *RQ, const float *elo, const float *ehi) {
+                         unsigned q0 = 0, q1 = 0;
+                         bool tail_too = false, emit = false;
+                         if (near) {
+                             // the item box (widened floats) holds the triangle's exact box: its
+                             // interval holds the exact gate's poses
+                             const double elod[3] = {elo[0], elo[1], elo[2]}, ehid[3] = {ehi[0], ehi[1], ehi[2]};
+                             g.near_range(RQ, elod, ehid, env.tf, q0, q1, tail_too);
+                             emit = q1 > q0 || tail_too;
+                         }
+                         // a lane's poses go out in chunks of at most kSweepChunk (the tail pose
+                         // with the last): the SAT launch then runs equal short loops a lane
+                         // instead of each wave waiting for its longest interval
+                         for (uint64_t em = __ballot(emit); em && !stop; em = __ballot(emit)) {
+                             const int ne = __popcll(em);
+                             const bool fresh = n_edge >= skip;  // a step boundary: all or none of it
+                             if (fresh && nb + ne > kSweepStage) {
+                                 if (!sweep_flush(buf, nb, Q, lane)) stop = full = true;
+                                 nb = 0;
+                                 if (stop) break;
+                             }
+                             if (emit) {
+                                 const int rank = __popcll(em & ((1ull << lane) - 1ull));
+                                 const bool last = q1 - q0 <= (unsigned)kSweepChunk;
+                                 const unsigned qe = last ? q1 : q0 + kSweepChunk;
+                                 if (fresh)
+                                     buf[nb + rank] = SweepCand{(int32_t)e, c.first + lane, t, q0,
+                                                                qe | (last && tail_too ? 0x80000000u : 0u)};
+                                 q0 = qe;
+                                 emit = !last;
+                             }
+                             if (fresh) nb += ne;
+                             n_edge += (uint32_t)ne;
+                             if (n_edge >= upto) stop = true;  // wave-uniform: the next pass resumes here
+                             __builtin_amdgcn_wave_barrier();
+                         }
+                         return stop;
+                     });
         }
         __builtin_amdgcn_wave_barrier();
         if (!full && !sweep_flush(buf, nb, Q, lane)) stop = full = true;
@@ -708,22 +573,125 @@ __global__ __launch_bounds__(kSweepWaves * 64) void k_sweep_cands(EnvDev env, co
     }
 }
 
-// the single-kernel sweep over a list of edges (the deferred ones; count on the device)
-__global__ __launch_bounds__(kSweepWaves * 64) void k_sweep_edge_list(EnvDev env, const AgentDev *__restrict__ link,
-                                                                      PrmSrc src, const int32_t *__restrict__ list,
-                                                                      const uint32_t *__restrict__ n_list,
-                                                                      uint8_t *verdict, unsigned long long *stats) {
+// ---- k_sweep_prm: prm_walk, then for each near lane the poses of its interval in step over the
+// wave (every stride-th, or the ones a coarse pass at that stride skipped plus the tail), each
+// pose's exact gate; the (triangle, env triangle, pose) triples that pass go to a per-wave LDS
+// list, and each 64 of them run the SAT one a lane.  The round-5 single-kernel sweep (removed)
+// ran a SAT wherever any lane's gate passed: ~2.5 us of FP64 a wave for a lane or two, and at
+// config 4 --bounds rooms a colliding edge took up to 7000 of them before its contact (its tail
+// of ~105 k edges: 38 ms; batched: 24 ms; coarse poses first: 12 ms).  The edge stops at the
+// batch holding its first contact.  Same verdicts: every (pair, pose) whose gate passes is
+// tested, with the reference's operations (R Q recomputed from the triangle by the walk's
+// expression, the pose by PrmEdge::pose).
+struct SatTriple {
+    int32_t atri, etri;
+    uint32_t q;
+};
+constexpr int kSatBatch = 64;
+
+// the SATs of list[0, n) (n <= 64), one a lane; true: a contact
+__device__ __forceinline__ bool prm_sat_batch(const EnvDev &env, const AgentDev &ag, const PrmEdge &g, const double *R,
+                                              const SatTriple *list, int n, int lane) {
+    bool hit = false;
+    if (lane < n) {
+        const SatTriple s = list[lane];
+        v3 RQ[3];
+        rotate_tri(ag, s.atri, R, RQ);
+        double t[3], Tp[3];
+        g.pose(s.q, t);
+        env_rel_t(env, t, Tp);
+        const v3 Q1 = mk(RQ[0].x + Tp[0], RQ[0].y + Tp[1], RQ[0].z + Tp[2]);
+        const v3 Q2 = mk(RQ[1].x + Tp[0], RQ[1].y + Tp[1], RQ[1].z + Tp[2]);
+        const v3 Q3 = mk(RQ[2].x + Tp[0], RQ[2].y + Tp[1], RQ[2].z + Tp[2]);
+        hit = tri_intersect(env.tris[s.etri], Q1, Q2, Q3);
+    }
+    return __ballot(hit) != 0;
+}
+
+__global__ __launch_bounds__(kSweepWaves * 64) void k_sweep_prm(EnvDev env, const AgentDev *__restrict__ link,
+                                                                PrmEdges P, const int32_t *__restrict__ list,
+                                                                const uint32_t *__restrict__ n_list, int64_t E,
+                                                                unsigned stride, bool rest, uint8_t *verdict,
+                                                                unsigned long long *stats) {
     __shared__ int32_t s_stk[kSweepWaves][2 * kSweepStack];
+    __shared__ SatTriple s_sat[kSweepWaves][2 * kSatBatch];
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
-    const uint32_t n = *n_list;
     SweepCounters cnt;
-    for (uint32_t i = blockIdx.x * kSweepWaves + wave; i < n; i += gridDim.x * kSweepWaves) {
-        const int64_t e = list[i];
+    SatTriple *sat = s_sat[wave];
+    const AgentDev &ag = link[0];
+    const int64_t n = list ? (int64_t)*n_list : E;
+    for (int64_t i = (int64_t)blockIdx.x * kSweepWaves + wave; i < n; i += (int64_t)gridDim.x * kSweepWaves) {
+        const int64_t e = list ? list[i] : i;
         if (load_flag(verdict + e)) continue;
-        src.edge(e, [&](const double *Rw, const double *tf, const double *tl, auto &&gen) {
-            sweep_edge_core(env, link[0], Rw, tf, tl, gen, verdict + e, lane, s_stk[wave], cnt);
-        });
+        const PrmEdge g = prm_edge_uniform(P, e);
+        ++cnt.waves;
+        double R[9], T0[3], TN[3];
+        prm_edge_frame(env, g, R, T0, TN);
+        int ns = 0;  // triples listed
+        bool hit = false;
+        prm_walk(env, ag, R, T0, TN, lane, s_stk[wave], cnt,
+                 [&](const Cluster &c, int32_t t, bool near, const v3 *RQ, const float *, const float *) {
+                     const EnvTri &Et = env.tris[t];
+                     double elo[3], ehi[3];
+#pragma unroll
+                     for (int k = 0; k < 3; ++k) {
+                         elo[k] = uniform_d(Et.lo[k]);
+                         ehi[k] = uniform_d(Et.hi[k]);
+                     }
+                     unsigned q0 = 0, q1 = 0;
+                     bool tail_too = false;
+                     if (near) g.near_range(RQ, elo, ehi, env.tf, q0, q1, tail_too);
+                     // coarse (stride > 1): poses q0, q0 + stride, ... of the run; then the rest
+                     // (rest: the poses a coarse pass at that stride skipped, and the tail)
+                     const unsigned run = q1 - q0, coarse = (run + stride - 1) / stride;
+                     const unsigned nmain = rest ? run - coarse : coarse;
+                     const unsigned np = near ? nmain + (tail_too && (rest || stride == 1) ? 1u : 0u) : 0u;
+                     for (unsigned j = 0;; ++j) {
+                         const bool more = j < np;
+                         const uint64_t mm = __ballot(more);
+                         if (!mm) break;
+                         cnt.pair_poses += (uint32_t)__popcll(mm);
+                         bool pass = false;
+                         const unsigned jr = rest ? j + j / (stride - 1) + 1 : j * stride;
+                         const unsigned q = j < nmain ? q0 + jr : g.it;  // past the run: the tail
+                         if (more) {
+                             double tw[3], Tp[3];
+                             g.pose(q, tw);
+                             env_rel_t(env, tw, Tp);
+                             const v3 Q1 = mk(RQ[0].x + Tp[0], RQ[0].y + Tp[1], RQ[0].z + Tp[2]);
+                             const v3 Q2 = mk(RQ[1].x + Tp[0], RQ[1].y + Tp[1], RQ[1].z + Tp[2]);
+                             const v3 Q3 = mk(RQ[2].x + Tp[0], RQ[2].y + Tp[1], RQ[2].z + Tp[2]);
+                             pass = tri_gate(elo, ehi, Q1, Q2, Q3);
+                         }
+                         const uint64_t pm = __ballot(pass);
+                         if (!pm) continue;
+                         if (pass) sat[ns + __popcll(pm & ((1ull << lane) - 1ull))] = SatTriple{c.first + lane, t, q};
+                         ns += __popcll(pm);
+                         if (ns >= kSatBatch) {
+                             __builtin_amdgcn_wave_barrier();
+                             cnt.sat += kSatBatch;
+                             if (prm_sat_batch(env, ag, g, R, sat, kSatBatch, lane)) {
+                                 hit = true;
+                                 return true;
+                             }
+                             ns -= kSatBatch;  // < 64 left past the batch: to the front
+                             SatTriple rest{};
+                             if (lane < ns) rest = sat[kSatBatch + lane];
+                             __builtin_amdgcn_wave_barrier();
+                             if (lane < ns) sat[lane] = rest;
+                             __builtin_amdgcn_wave_barrier();
+                         }
+                     }
+                     return false;
+                 });
+        if (!hit && ns > 0) {
+            __builtin_amdgcn_wave_barrier();
+            cnt.sat += (uint32_t)ns;
+            hit = prm_sat_batch(env, ag, g, R, sat, ns, lane);
+        }
+        if (hit && lane == 0) __hip_atomic_store(verdict + e, (uint8_t)1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __builtin_amdgcn_wave_barrier();
     }
     if (stats && lane == 0 && cnt.waves) {
         atomicAdd(stats + 0, (unsigned long long)cnt.waves);
@@ -804,14 +772,6 @@ static void launch_sweep_src(const EnvDev &env, const AgentDev *d_link, int32_t 
                              uint8_t *verdict, unsigned long long *stats, hipStream_t stream) {
     if (E <= 0 || env.n_tris <= 0) return;
     if (env.n_tris >= (1 << 27)) throw Error{5, "env too large for the sweep path"};
-    if (n_clusters <= 64) {
-        const int64_t blocks = (E + kSweepWaves - 1) / kSweepWaves;
-        if (blocks > 0x7fffffff) throw Error{5, "sweep batch too large"};
-        hipLaunchKernelGGL(k_sweep_edge<Src>, dim3((unsigned)blocks), dim3(kSweepWaves * 64), 0, stream, env, d_link,
-                           src, E, verdict, stats);
-        hip_check(hipGetLastError(), "k_sweep_edge launch");
-        return;
-    }
     const int64_t waves = E * n_clusters;
     const int64_t blocks = (waves + kSweepWaves - 1) / kSweepWaves;
     if (blocks > 0x7fffffff) throw Error{5, "sweep batch too large"};
@@ -864,6 +824,11 @@ void launch_collide_sweep_prm(const EnvDev &env, const AgentDev *d_link, int32_t
         q.cap = want;
         q.ecap = E;
     }
+    auto prm_pass = [&](const int32_t *list, const uint32_t *n_list, unsigned stride, bool rest) {
+        hipLaunchKernelGGL(k_sweep_prm, dim3(4096), dim3(kSweepWaves * 64), 0, stream, env, d_link, edges, list,
+                           n_list, E, stride, rest, verdict, stats);
+        hip_check(hipGetLastError(), "k_sweep_prm launch");
+    };
     // n: [0] queue, [1] fused list, [2 + k] list k
     hip_check(hipMemsetAsync(q.n, 0, sizeof(uint32_t) * 4, stream), "sweep counts zero");
     uint64_t emitted = 0;
@@ -894,23 +859,18 @@ void launch_collide_sweep_prm(const EnvDev &env, const AgentDev *d_link, int32_t
         const int64_t fit = n_in > 0 ? q.cap / n_in - kWave : 0;
         edge_cap = (uint32_t)std::max<int64_t>(kSweepEdgeCands, std::min<int64_t>(int64_t(edge_cap) * 4, fit));
     }
-    // what the passes left (capped at the last pass, or stopped by a full queue): the
-    // single-kernel sweep, which stops at a contact and skips the edges already decided
+    // what the passes left (capped at the last pass, or stopped by a full queue): k_sweep_prm,
+    // which skips the edges already decided -- the coarse poses, then the rest
     uint64_t to_fused = q.h[1];
     if (n_in > 0 && last >= 0) {
-        hipLaunchKernelGGL(k_sweep_edge_list, dim3(4096), dim3(kSweepWaves * 64), 0, stream, env, d_link,
-                           PrmSrc{edges}, q.le[last], q.n + 2 + last, verdict, stats);
-        hip_check(hipGetLastError(), "k_sweep_edge_list launch");
+        prm_pass(q.le[last], q.n + 2 + last, kSweepCoarse, false);
+        prm_pass(q.le[last], q.n + 2 + last, kSweepCoarse, true);
         to_fused += (uint64_t)n_in;
     }
-    if (q.h[1] > 0) {
-        hipLaunchKernelGGL(k_sweep_edge_list, dim3(4096), dim3(kSweepWaves * 64), 0, stream, env, d_link,
-                           PrmSrc{edges}, q.fused, q.n + 1, verdict, stats);
-        hip_check(hipGetLastError(), "k_sweep_edge_list launch");
-    }
+    if (q.h[1] > 0) prm_pass(q.fused, q.n + 1, 1u, false);
     hip_check(hipStreamSynchronize(stream), "sweep sync");
     last_sweep_counts[0] = emitted;    // candidates emitted over the passes
-    last_sweep_counts[1] = to_fused;  // edges left to the single-kernel sweep
+    last_sweep_counts[1] = to_fused;  // edges left to k_sweep_prm
 }
 
 }  // namespace mpt

@@ -39,18 +39,20 @@ def latest_pmc(sub):
 
 
 def sweep_roofline(w, ms, n_agent, n_env, n_milestones, traffic_path):
-    """k_sweep (the config-4 collision stage, one wave per edge over the agent's clusters, the
-    edge's poses generated in the kernel from its two milestones, prm_edges.h): FP64 by SURVEY
-    §8(d)'s model -- 750 flops per exact triangle test, 27 per (pair, pose) gate (the
-    translated triangle's box and the overlap test), 45 per agent triangle rotated once per
-    wave (R Q, 64 lanes) -- and HBM: compulsory = every input once -- the edges (source, target
-    id, verdict byte), the milestones' keys and yaw (40 B), the agent triangles, the env tree's
-    items and triangle records -- measured = the kernel's rocprofv3 PMC traffic."""
+    """The config-4 collision stage (sweep.hip: k_sweep_cands, k_sweep_sat, k_sweep_prm twice --
+    one wave per edge over the agent's clusters, the edge's poses generated in the kernels from
+    its two milestones, prm_edges.h): FP64 by SURVEY §8(d)'s model -- 750 flops per exact
+    triangle test, 27 per (pair, pose) gate (the translated triangle's box and the overlap
+    test), 45 per agent triangle rotated once per wave (R Q, 64 lanes) -- and HBM: compulsory =
+    every input once -- the edges (source, target id, verdict byte), the milestones' keys and
+    yaw (40 B), the agent triangles, the env tree's items and triangle records -- measured = the
+    stage's rocprofv3 PMC traffic (every k_sweep* launch of one mpt_prm_connect call)."""
     t = ms * 1e-3
     flops = 750.0 * w["sat_tests"] + 27.0 * w["gate_tests"] + 45.0 * 64 * w["waves"]
     items = n_env + -(-n_env // 8)
     comp = w["edges"] * 9 + n_milestones * 40 + n_agent * 72 + items * 32 + n_env * 384
-    out = {"bound": "fp64_valu", "kernel": "k_sweep", "achieved": round(flops / t / 1e12, 3), "peak": FP64_PEAK_TFLOPS,
+    out = {"bound": "fp64_valu", "kernel": "k_sweep_cands + k_sweep_sat + k_sweep_prm",
+           "achieved": round(flops / t / 1e12, 3), "peak": FP64_PEAK_TFLOPS,
            "unit": "TFLOP/s", "frac": round(flops / t / 1e12 / FP64_PEAK_TFLOPS, 4),
            "note": "FP64 VALU roof (FCL's scalar operation order; no MFMA)",
            "compulsory_bytes": int(comp), "compulsory_gbs": round(comp / t / 1e9, 1),
@@ -59,7 +61,10 @@ def sweep_roofline(w, ms, n_agent, n_env, n_milestones, traffic_path):
     path = traffic_path or latest_pmc("prm")
     try:
         summ = json.load(open(path))
-        tr = next(v["hbm_bytes_per_launch"] for k, v in summ.items() if "k_sweep" in k)
+        parts = [v["hbm_bytes_per_launch"] * v.get("launches", 1) for k, v in summ.items() if "k_sweep" in k]
+        if not parts:
+            raise StopIteration
+        tr = sum(parts)
         out.update({"traffic": int(tr), "traffic_gbs": round(tr / t / 1e9, 1),
                     "frac_hbm_measured": round(tr / t / 1e9 / HBM_PEAK_GBS, 4),
                     "traffic_over_compulsory": round(tr / comp, 2), "pmc_source": os.path.relpath(path, REPO)})

@@ -46,11 +46,12 @@ def main(src, dst, start=None, end=None):
             agg[r["Kernel_Name"]].append(float(r["Counter_Value"]))
         for k, v in agg.items():
             out.setdefault(k, {})[cn] = sum(v) / len(v)
+            out[k]["launches"] = len(v)
     summ = {}
     for k, v in out.items():
         f, w = v.get("FETCH_SIZE", 0.0), v.get("WRITE_SIZE", 0.0)
         summ[k] = {"FETCH_SIZE_KB": round(f, 3), "WRITE_SIZE_KB": round(w, 3),
-                   "hbm_bytes_per_launch": round((2 * f + w) * 1024)}
+                   "hbm_bytes_per_launch": round((2 * f + w) * 1024), "launches": v.get("launches", 1)}
     json.dump(summ, open(os.path.join(dst, "pmc_summary.json"), "w"), indent=1)
     ks = os.path.join(src, "kt", "run_kernel_stats.csv")
     if os.path.exists(ks):
