@@ -386,7 +386,7 @@ __device__ __forceinline__ void rotate_tri(const AgentDev &ag, int32_t a, const 
 // ends the walk.
 template <class Visit>
 __device__ __forceinline__ void prm_walk(const EnvDev &env, const AgentDev &ag, const double *R, const double *T0,
-                                         const double *TN, int lane, int32_t *stk, SweepCounters &cnt,
+                                         const double *TN, int lane, int32_t *stk, SweepCounters &cnt, double *rq_lds,
                                          Visit &&visit) {
     const int ncl = ag.n_clusters;
     float clo[3] = {__builtin_huge_valf(), __builtin_huge_valf(), __builtin_huge_valf()};
@@ -460,7 +460,16 @@ __device__ __forceinline__ void prm_walk(const EnvDev &env, const AgentDev &ag, 
                         tlo[k] = widen_lo(dmin(mn + T0[k], mn + TN[k]));
                         thi[k] = widen_hi(dmax(mx + T0[k], mx + TN[k]));
                     }
+                    if (rq_lds) {  // the visitor reads it where it needs it (not held across its SATs)
+#pragma unroll
+                        for (int v = 0; v < 3; ++v) {
+                            rq_lds[lane * 9 + 3 * v] = RQ[v].x;
+                            rq_lds[lane * 9 + 3 * v + 1] = RQ[v].y;
+                            rq_lds[lane * 9 + 3 * v + 2] = RQ[v].z;
+                        }
+                    }
                 }
+                __builtin_amdgcn_wave_barrier();
                 for (; Tc && !stop; Tc &= Tc - 1) {
                     const int j = __ffsll((unsigned long long)Tc) - 1;
                     const float elo[3] = {lane_f(ilo[0], j), lane_f(ilo[1], j), lane_f(ilo[2], j)};
@@ -516,7 +525,7 @@ __global__ __launch_bounds__(kSweepWaves * 64) void k_sweep_cands(EnvDev env, co
             ++cnt.waves;
             double R[9], T0[3], TN[3];
             prm_edge_frame(env, g, R, T0, TN);
-            prm_walk(env, link[0], R, T0, TN, lane, s_stk[wave], cnt,
+            prm_walk(env, link[0], R, T0, TN, lane, s_stk[wave], cnt, nullptr,
                      [&](const Cluster &c, int32_t t, bool near, const v3 *RQ, const float *elo, const float *ehi) {
                          unsigned q0 = 0, q1 = 0;
                          bool tail_too = false, emit = false;
@@ -608,13 +617,17 @@ __device__ __forceinline__ bool prm_sat_batch(const EnvDev &env, const AgentDev 
     return __ballot(hit) != 0;
 }
 
-__global__ __launch_bounds__(kSweepWaves * 64) void k_sweep_prm(EnvDev env, const AgentDev *__restrict__ link,
+// 3 waves a SIMD: the lanes' rotated triangles live in LDS (prm_walk's copy, re-read each pose
+// step), 211 -> 164 VGPRs, no VGPR spill (config 4 at --bounds rooms: collision 17.9 -> 16.0 ms;
+// at 4 waves 24 VGPRs spill: 15.9 ms)
+__global__ __launch_bounds__(kSweepWaves * 64) __attribute__((amdgpu_waves_per_eu(3))) void k_sweep_prm(EnvDev env, const AgentDev *__restrict__ link,
                                                                 PrmEdges P, const int32_t *__restrict__ list,
                                                                 const uint32_t *__restrict__ n_list, int64_t E,
                                                                 unsigned stride, bool rest, uint8_t *verdict,
                                                                 unsigned long long *stats) {
     __shared__ int32_t s_stk[kSweepWaves][2 * kSweepStack];
     __shared__ SatTriple s_sat[kSweepWaves][2 * kSatBatch];
+    __shared__ double s_rq[kSweepWaves][kWave * 9];
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
     SweepCounters cnt;
@@ -630,8 +643,9 @@ __global__ __launch_bounds__(kSweepWaves * 64) void k_sweep_prm(EnvDev env, cons
         prm_edge_frame(env, g, R, T0, TN);
         int ns = 0;  // triples listed
         bool hit = false;
-        prm_walk(env, ag, R, T0, TN, lane, s_stk[wave], cnt,
-                 [&](const Cluster &c, int32_t t, bool near, const v3 *RQ, const float *, const float *) {
+        double *rq = s_rq[wave];
+        prm_walk(env, ag, R, T0, TN, lane, s_stk[wave], cnt, rq,
+                 [&](const Cluster &c, int32_t t, bool near, const v3 *, const float *, const float *) {
                      const EnvTri &Et = env.tris[t];
                      double elo[3], ehi[3];
 #pragma unroll
@@ -639,9 +653,20 @@ __global__ __launch_bounds__(kSweepWaves * 64) void k_sweep_prm(EnvDev env, cons
                          elo[k] = uniform_d(Et.lo[k]);
                          ehi[k] = uniform_d(Et.hi[k]);
                      }
+                     // the lane's rotated triangle from LDS (prm_walk's copy): read again in each
+                     // pose step, so no register holds it across the SAT batches
+                     auto rq_of = [&](v3 *RQ) {
+#pragma unroll
+                         for (int v = 0; v < 3; ++v)
+                             RQ[v] = mk(rq[lane * 9 + 3 * v], rq[lane * 9 + 3 * v + 1], rq[lane * 9 + 3 * v + 2]);
+                     };
                      unsigned q0 = 0, q1 = 0;
                      bool tail_too = false;
-                     if (near) g.near_range(RQ, elo, ehi, env.tf, q0, q1, tail_too);
+                     if (near) {
+                         v3 RQ[3];
+                         rq_of(RQ);
+                         g.near_range(RQ, elo, ehi, env.tf, q0, q1, tail_too);
+                     }
                      // coarse (stride > 1): poses q0, q0 + stride, ... of the run; then the rest
                      // (rest: the poses a coarse pass at that stride skipped, and the tail)
                      const unsigned run = q1 - q0, coarse = (run + stride - 1) / stride;
@@ -657,6 +682,9 @@ __global__ __launch_bounds__(kSweepWaves * 64) void k_sweep_prm(EnvDev env, cons
                          const unsigned q = j < nmain ? q0 + jr : g.it;  // past the run: the tail
                          if (more) {
                              double tw[3], Tp[3];
+                             v3 RQ[3];
+                             asm volatile("" ::: "memory");  // the LDS copy is read here, every step
+                             rq_of(RQ);
                              g.pose(q, tw);
                              env_rel_t(env, tw, Tp);
                              const v3 Q1 = mk(RQ[0].x + Tp[0], RQ[0].y + Tp[1], RQ[0].z + Tp[2]);
