@@ -1256,6 +1256,7 @@ struct JointNN {
     std::mutex mu;  // one step_many at a time per joint stream (the ring and the tables)
     char *d_stage = nullptr;
     char *h_stage[kJobRing] = {};
+    const char *hd_stage[kJobRing] = {};  // the same pinned buffers' device addresses
     hipEvent_t copied[kJobRing] = {};
     size_t cap = 0;
     int32_t next = 0;
@@ -1302,6 +1303,24 @@ std::shared_ptr<JointNN> joint_find_shared(hipStream_t s) {
     return it == g_joints.end() ? nullptr : it->second;
 }
 
+// The job tables go up by a kernel that reads the pinned ring over PCIe (a few KB), ordered on
+// the joint stream like any launch.  hipMemcpyAsync's DMA copy left the compute queue idle ~23 us
+// a round between k_sample_jobs and the build (config 5 at 32 seeds, kernel trace: the only
+// gap of the round besides ~6 us before the engine-table copy).
+__global__ void k_stage_copy(uint64_t *__restrict__ dst, const uint64_t *__restrict__ src, int64_t words) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < words; i += (int64_t)gridDim.x * blockDim.x)
+        dst[i] = src[i];
+}
+void stage_copy(JointNN &g, int slot, size_t off, size_t bytes, hipStream_t s) {
+    if (bytes == 0) return;
+    if (off % 8 || bytes % 8) throw Error{MPT_ERR_INTERNAL, "job tables: 8-byte records expected"};
+    const int64_t words = (int64_t)(bytes / 8);
+    const unsigned blocks = (unsigned)std::min<int64_t>(16, (words + 255) / 256);
+    hipLaunchKernelGGL(k_stage_copy, dim3(blocks), dim3(256), 0, s, reinterpret_cast<uint64_t *>(g.d_stage + off),
+                       reinterpret_cast<const uint64_t *>(g.hd_stage[slot] + off), words);
+    hip_check(hipGetLastError(), "k_stage_copy");
+}
+
 // a pinned staging buffer of at least `bytes` whose previous copy has completed
 char *joint_stage(JointNN &g, size_t bytes, int *slot) {
     if (bytes > g.cap) {
@@ -1313,8 +1332,11 @@ char *joint_stage(JointNN &g, size_t bytes, int *slot) {
         // the ring's buffers carved from one pinned allocation (one hipHostMalloc, not kJobRing)
         char *ring = nullptr;
         hip_check(hipHostMalloc(&ring, c * kJobRing), "stage pinned");
+        char *dring = nullptr;
+        hip_check(hipHostGetDevicePointer((void **)&dring, ring, 0), "stage pinned device address");
         for (int i = 0; i < kJobRing; ++i) {
             g.h_stage[i] = ring + (size_t)i * c;
+            g.hd_stage[i] = dring + (size_t)i * c;
             if (!g.copied[i]) hip_check(hipEventCreateWithFlags(&g.copied[i], hipEventDisableTiming), "event");
         }
         if (!g.done) hip_check(hipEventCreateWithFlags(&g.done, hipEventDisableTiming), "event");
@@ -1449,7 +1471,7 @@ void joint_round(mpt_rrt *const *rs, int32_t n, int32_t K, void *const *streams_
         if (timed) hip_check(hipEventRecord(g.st[i], joint), "joint stage event");
     };
     mark(0);
-    hip_check(hipMemcpyAsync(g.d_stage, he, b_eng, hipMemcpyHostToDevice, joint), "engine jobs H2D");
+    stage_copy(g, slot, 0, b_eng, joint);
     const unsigned kb = (unsigned)((K + 255) / 256);
     hipLaunchKernelGGL(k_sample_jobs, dim3(kb, n), dim3(256), 0, joint, p, de, K, g.j_samples, g.j_nlive, n_sub);
     hip_check(hipGetLastError(), "k_sample_jobs");
@@ -1464,7 +1486,7 @@ void joint_round(mpt_rrt *const *rs, int32_t n, int32_t K, void *const *streams_
         T.stats = nullptr;
         hn[i] = CtNnJob{T, g.j_samples + (int64_t)i * K * d, g.j_nn + (int64_t)i * K, g.j_nnd2 + (int64_t)i * K};
     }
-    hip_check(hipMemcpyAsync(g.d_stage + b_eng, h + b_eng, b_inc + b_nn, hipMemcpyHostToDevice, joint), "jobs H2D");
+    stage_copy(g, slot, b_eng, b_inc + b_nn, joint);
     hip_check(hipEventRecord(g.copied[slot], joint), "jobs copied");
     launch_ct_jobs(di, hi, n, d, joint);
     for (int32_t i = 0; i < n; ++i)
@@ -1602,7 +1624,7 @@ extern "C" mpt_status mpt_rrt_step_many(mpt_rrt *const *rs, int32_t n, int32_t K
                 T.stats = r->stats_on ? r->d_cstats + 8 : nullptr;
                 hn[k] = CtNnJob{T, r->d_samples, r->d_nn, r->d_nnd2};
             }
-            hip_check(hipMemcpyAsync(g.d_stage, h, b_build + b_nn, hipMemcpyHostToDevice, joint), "jobs H2D");
+            stage_copy(g, slot, 0, b_build + b_nn, joint);
             hip_check(hipEventRecord(g.copied[slot], joint), "jobs copied");
             const CtJob *di = reinterpret_cast<const CtJob *>(g.d_stage);
             const CtNnJob *dn = reinterpret_cast<const CtNnJob *>(g.d_stage + b_build);
