@@ -1643,21 +1643,21 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(D >= 15 ? 4 
     ct_walk<D, BS, W>(T, q, nq, out_ids, out_d2, blockIdx.x);
 }
 
-// Many trees in one launch (mpt_rrt_step_many: one engine per independent seed).  Jobs are
-// dealt to XCDs: workgroup b runs on XCD b % 8, so job j takes the workgroups of XCD j % 8
-// and its tree stays in that XCD's L2.  8 waves per SIMD for d <= 7; d = 15 at 4 (registers).
-// (Round 5, measured and not kept: a job split over two XCDs when an XCD holds fewer than 8
-// trees -- the mapping's 64-bit divisions pushed the walk past its 64-VGPR bound (12 bytes
-// spilled): NN 0.33 -> 0.37 ms at 32 seeds, 2.09 -> 2.60 at 256.)
+// Many trees in one launch (mpt_rrt_step_many: one engine per independent seed): job j takes
+// workgroups [j * bpj, (j + 1) * bpj), so consecutive workgroups of a job land on the 8 XCDs in
+// turn and every XCD gets an equal share of every job.  (Round 4 dealt whole jobs to XCDs --
+// job j on XCD j % 8, its tree in that XCD's L2 -- but a tree is larger than an XCD's 4 MB L2,
+// and with 4 jobs an XCD (32 seeds) the XCD with the costliest trees set the kernel's end:
+// round 5 measured NN 0.337 -> 0.284 ms at 32 seeds, 2.111 -> 2.079 at 256 for this mapping.
+// Also measured and not kept: a job split over two XCDs when an XCD holds fewer than 8 trees --
+// its 64-bit index math spilled the 64-VGPR walk: 0.33 -> 0.37 ms at 32 seeds.)
 template <int D, int BS, int W>
 __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(D >= 15 ? 4 : 8))) void k_ct_nn1_jobs(
-    const CtNnJob *__restrict__ jobs, int32_t n_jobs, int64_t nq, int64_t blocks_per_job) {
-    constexpr int kXcd = 8;
-    const int64_t xcd = blockIdx.x % kXcd, slot = blockIdx.x / kXcd;
-    const int64_t job = xcd + kXcd * (slot / blocks_per_job);
-    if (job >= n_jobs) return;
+    const CtNnJob *__restrict__ jobs, int32_t n_jobs, int64_t nq, int32_t blocks_per_job) {
+    const uint32_t job = blockIdx.x / (uint32_t)blocks_per_job, blk = blockIdx.x % (uint32_t)blocks_per_job;
+    if (job >= (uint32_t)n_jobs) return;
     const CtNnJob J = jobs[job];  // by value: the tree's pointers stay in SGPRs across the walk
-    ct_walk<D, BS, W>(J.T, J.q, nq, J.ids, J.d2, slot % blocks_per_job);
+    ct_walk<D, BS, W>(J.T, J.q, nq, J.ids, J.d2, blk);
 }
 
 }  // namespace
@@ -2029,12 +2029,13 @@ template <int W>
 static void launch_ct_nn1_jobs_w(const CtNnJob *d_jobs, int32_t n_jobs, int32_t d, int64_t nq, hipStream_t stream) {
     constexpr int BS = 64;
     const int64_t bpj = (nq * 8 * W + BS - 1) / BS;
-    const int64_t groups = (n_jobs + 7) / 8;
-    const dim3 grid((unsigned)(8 * groups * bpj));
+    if (bpj * n_jobs > 0x7fffffffLL) throw Error{1, "cell tree: joint NN launch too large"};
+    const dim3 grid((unsigned)(bpj * n_jobs));
+    const int32_t b = (int32_t)bpj;
     switch (d) {
-        case 3: hipLaunchKernelGGL((k_ct_nn1_jobs<3, BS, W>), grid, dim3(BS), 0, stream, d_jobs, n_jobs, nq, bpj); break;
-        case 7: hipLaunchKernelGGL((k_ct_nn1_jobs<7, BS, W>), grid, dim3(BS), 0, stream, d_jobs, n_jobs, nq, bpj); break;
-        case 15: hipLaunchKernelGGL((k_ct_nn1_jobs<15, BS, W>), grid, dim3(BS), 0, stream, d_jobs, n_jobs, nq, bpj); break;
+        case 3: hipLaunchKernelGGL((k_ct_nn1_jobs<3, BS, W>), grid, dim3(BS), 0, stream, d_jobs, n_jobs, nq, b); break;
+        case 7: hipLaunchKernelGGL((k_ct_nn1_jobs<7, BS, W>), grid, dim3(BS), 0, stream, d_jobs, n_jobs, nq, b); break;
+        case 15: hipLaunchKernelGGL((k_ct_nn1_jobs<15, BS, W>), grid, dim3(BS), 0, stream, d_jobs, n_jobs, nq, b); break;
         default: throw Error{1, "cell tree: state dim must be 3, 7 or 15"};
     }
     hip_check(hipGetLastError(), "k_ct_nn1_jobs launch");
