@@ -159,7 +159,24 @@ def test_config4_rooms_at_size(mpt_gpu, oracle):
     assert len(e_ref) > 400
     assert np.array_equal(edges[pre], e_ref)
     assert np.array_equal(verdict[pre], v_ref)
-    # (3) components over the free edges
+    # (3) 1 500 edges drawn from the whole roadmap (every stage of the sweep: the candidate pass,
+    #     its SAT launch, the capped edges' coarse and remaining poses): the oracle's verdict of
+    #     each, from one orc_prm_radius call over their endpoints in index order (an edge's poses
+    #     depend on its two milestones only; edges among the endpoints that were not drawn are
+    #     ignored)
+    rng = np.random.default_rng(7)
+    pick = rng.choice(len(edges), size=1500, replace=False)
+    ends = np.unique(edges[pick].ravel())
+    pos = np.full(n, -1, np.int64)
+    pos[ends] = np.arange(len(ends))
+    e_sub, v_sub, _ = oracle.prm_radius(oracle.BVH(env_t), I12, sc.agent_tris, st[ends], r2, sc.cc_dt,
+                                        nthreads=THREADS)
+    ref = {(int(a), int(b)): int(v) for (a, b), v in zip(e_sub.tolist(), v_sub.tolist())}
+    drawn = [(int(pos[i]), int(pos[j])) for i, j in edges[pick].tolist()]
+    assert all(d in ref for d in drawn)
+    assert np.array_equal(np.array([ref[d] for d in drawn], np.uint8), verdict[pick])
+    assert 0 < verdict[pick].sum() < len(pick)
+    # (4) components over the free edges
     assert np.array_equal(got["comp"], _components(n, edges, verdict))
 
 
