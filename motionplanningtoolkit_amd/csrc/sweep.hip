@@ -620,10 +620,11 @@ __device__ __forceinline__ bool prm_sat_batch(const EnvDev &env, const AgentDev 
 // 3 waves a SIMD: the lanes' rotated triangles live in LDS (prm_walk's copy, re-read each pose
 // step), 211 -> 164 VGPRs, no VGPR spill (config 4 at --bounds rooms: collision 17.9 -> 16.0 ms;
 // at 4 waves 24 VGPRs spill: 15.9 ms)
+template <unsigned stride>
 __global__ __launch_bounds__(kSweepWaves * 64) __attribute__((amdgpu_waves_per_eu(3))) void k_sweep_prm(EnvDev env, const AgentDev *__restrict__ link,
                                                                 PrmEdges P, const int32_t *__restrict__ list,
                                                                 const uint32_t *__restrict__ n_list, int64_t E,
-                                                                unsigned stride, bool rest, uint8_t *verdict,
+                                                                bool rest, uint8_t *verdict,
                                                                 unsigned long long *stats) {
     __shared__ int32_t s_stk[kSweepWaves][2 * kSweepStack];
     __shared__ SatTriple s_sat[kSweepWaves][2 * kSatBatch];
@@ -667,9 +668,12 @@ __global__ __launch_bounds__(kSweepWaves * 64) __attribute__((amdgpu_waves_per_e
                          rq_of(RQ);
                          g.near_range(RQ, elo, ehi, env.tf, q0, q1, tail_too);
                      }
-                     // coarse (stride > 1): poses q0, q0 + stride, ... of the run; then the rest
-                     // (rest: the poses a coarse pass at that stride skipped, and the tail)
-                     const unsigned run = q1 - q0, coarse = (run + stride - 1) / stride;
+                     // coarse (stride > 1): every stride-th pose of the run, its middle among them
+                     // (the run is the box-overlap interval widened a pose or two each side: with
+                     // q0 first, a run shorter than the stride tested only a widened end); then
+                     // the rest (rest: the poses a coarse pass at that stride skipped, and the tail)
+                     const unsigned run = q1 - q0, off = (run / 2) % stride;
+                     const unsigned coarse = run > off ? (run - off + stride - 1) / stride : 0u;
                      const unsigned nmain = rest ? run - coarse : coarse;
                      const unsigned np = near ? nmain + (tail_too && (rest || stride == 1) ? 1u : 0u) : 0u;
                      for (unsigned j = 0;; ++j) {
@@ -678,7 +682,8 @@ __global__ __launch_bounds__(kSweepWaves * 64) __attribute__((amdgpu_waves_per_e
                          if (!mm) break;
                          cnt.pair_poses += (uint32_t)__popcll(mm);
                          bool pass = false;
-                         const unsigned jr = rest ? j + j / (stride - 1) + 1 : j * stride;
+                         const unsigned jb = stride > 1 ? j / (stride - 1) : 0u, jo = j - jb * (stride - 1);
+                         const unsigned jr = rest ? jb * stride + (jo < off ? jo : jo + 1) : off + j * stride;
                          const unsigned q = j < nmain ? q0 + jr : g.it;  // past the run: the tail
                          if (more) {
                              double tw[3], Tp[3];
@@ -853,8 +858,12 @@ void launch_collide_sweep_prm(const EnvDev &env, const AgentDev *d_link, int32_t
         q.ecap = E;
     }
     auto prm_pass = [&](const int32_t *list, const uint32_t *n_list, unsigned stride, bool rest) {
-        hipLaunchKernelGGL(k_sweep_prm, dim3(4096), dim3(kSweepWaves * 64), 0, stream, env, d_link, edges, list,
-                           n_list, E, stride, rest, verdict, stats);
+        if (stride == kSweepCoarse)
+            hipLaunchKernelGGL(k_sweep_prm<kSweepCoarse>, dim3(4096), dim3(kSweepWaves * 64), 0, stream, env, d_link,
+                               edges, list, n_list, E, rest, verdict, stats);
+        else
+            hipLaunchKernelGGL(k_sweep_prm<1>, dim3(4096), dim3(kSweepWaves * 64), 0, stream, env, d_link, edges, list,
+                               n_list, E, false, verdict, stats);
         hip_check(hipGetLastError(), "k_sweep_prm launch");
     };
     // n: [0] queue, [1] fused list, [2 + k] list k
