@@ -275,10 +275,10 @@ __global__ __launch_bounds__(kSweepWaves * 64) void k_sweep_lite(EnvDev env, con
 //     that reaches the cap stops and is listed;
 //  2. k_sweep_sat: the gate + SAT over each candidate's poses, one candidate a lane (full waves
 //     at full occupancy; ~55 % of config 4's edges at --bounds rooms are decided here, free);
-//  3. k_sweep_prm over the listed edges (mostly colliding ones): the walk again, every
-//     kSweepCoarse-th pose of each pair's interval first (a contact with a wall lasts many
-//     poses: this pass finds nearly every colliding edge's), then the poses it skipped; the
-//     gate passes batched into SATs of 64 a wave, the edge ending at its first contact.
+//  3. k_sweep_prm over the listed edges (mostly colliding ones): the walk again, each pair's
+//     middle pose first (kSweepCoarse: a contact with a wall lasts many poses, so this pass finds
+//     nearly every colliding edge's), then the poses it skipped; the gate passes batched into
+//     SATs of 64 a wave, the edge ending at its first contact.
 // Verdicts are the same set: every (edge, agent triangle, env triangle, pose) the reference
 // tests either is in some candidate or in one of k_sweep_prm's two pose sets (same fan-out, same
 // box tests, the same pose interval), each with the same operations, and a contact found
@@ -317,10 +317,13 @@ struct SweepQueue {
 // pass: 53 / 53.
 constexpr int kSweepEdgeCands = 64;  // the first pass's cap; x4 a pass
 constexpr int kSweepPasses = 1;      // then k_sweep_prm takes what is left
-// k_sweep_prm's first pose stride (config 4 at --bounds rooms, collision ms: no coarse pass
-// 30.8, stride 4: 19.1, 8: 17.9, 16: 23.9; the coarse pass over every edge before the
-// candidates instead: 20.0, and over every edge with no candidates at all: 21.2)
-constexpr unsigned kSweepCoarse = 8;
+// k_sweep_prm's first pose stride, its poses centred on each pair's interval: 1024 exceeds
+// nearly every interval, so the first pass tests each pair's middle pose (config 4 at --bounds
+// rooms, collision ms on one box: stride 8: 14.8, 16: 14.3, 1024: 14.1; with the first pose at
+// the interval's start instead of its middle: no coarse pass 30.8, stride 4: 19.1, 8: 17.9, 16:
+// 23.9; the coarse pass over every edge before the candidates instead: 20.0, and over every
+// edge with no candidates at all: 21.2)
+constexpr unsigned kSweepCoarse = 1024;
 
 // false when the queue is full: the wave's edge is then deferred (the candidates that did fit
 // are tested all the same, which is harmless: a contact among them is a contact)
