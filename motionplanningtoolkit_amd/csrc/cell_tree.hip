@@ -138,13 +138,16 @@ __device__ __forceinline__ void hull_offer(const CtPlan &P, const double (&x)[D]
     __builtin_amdgcn_wave_barrier();
 }
 
-// the box of rows (widened float bounds over every dim)
+// the box of rows (widened float bounds over every dim).  A box is D (lo, -hi) float pairs,
+// dim by dim: pair k is one 8-byte word, so the walk's lower bound takes dim k's two gaps in
+// one packed addition (ct_box_lb), and a union of boxes is a minimum of both halves (an empty
+// box: (+inf, +inf))
 template <int D>
 __device__ __forceinline__ void write_box(float *__restrict__ b, const double (&lo)[D], const double (&hi)[D]) {
 #pragma unroll
     for (int k = 0; k < D; ++k) {
-        b[k] = widen_lo(lo[k]);
-        b[D + k] = widen_hi(hi[k]);
+        b[2 * k] = widen_lo(lo[k]);
+        b[2 * k + 1] = -widen_hi(hi[k]);
     }
 }
 
@@ -536,8 +539,8 @@ __global__ __launch_bounds__(256) void k_ct_apply(CtJobs js) {
                 const float *ob = J.bbox + (int64_t)b * 2 * D;
 #pragma unroll
                 for (int q = 0; q < D; ++q) {
-                    lo[q] = (double)ob[q];  // widened already: widening again only loosens it
-                    hi[q] = (double)ob[D + q];
+                    lo[q] = (double)ob[2 * q];  // widened already: widening again only loosens it
+                    hi[q] = -(double)ob[2 * q + 1];
                 }
             } else {
 #pragma unroll
@@ -1038,26 +1041,26 @@ __global__ __launch_bounds__(256) void k_ct_lgroup(CtJobs js) {
         } else {
             while (i + len < n && len < kCtCap && !s_f[e + len]) ++len;
         }
-        float lo[D], hi[D];
+        float lo[D], nhi[D];  // the union: (lo, -hi) pairs, a minimum of both
         const float *b0 = reinterpret_cast<const float *>(s_box + e * D);
 #pragma unroll
         for (int q = 0; q < D; ++q) {
-            lo[q] = b0[q];
-            hi[q] = b0[D + q];
+            lo[q] = b0[2 * q];
+            nhi[q] = b0[2 * q + 1];
         }
         for (int u = 1; u < len; ++u) {
             const float *bu = reinterpret_cast<const float *>(s_box + (e + u) * D);
 #pragma unroll
             for (int q = 0; q < D; ++q) {
-                lo[q] = fminf(lo[q], bu[q]);
-                hi[q] = fmaxf(hi[q], bu[D + q]);
+                lo[q] = fminf(lo[q], bu[2 * q]);
+                nhi[q] = fminf(nhi[q], bu[2 * q + 1]);
             }
         }
         const int64_t P = base + n + g;
 #pragma unroll
         for (int q = 0; q < D; ++q) {
-            J.nbox[P * 2 * D + q] = lo[q];
-            J.nbox[P * 2 * D + D + q] = hi[q];
+            J.nbox[P * 2 * D + 2 * q] = lo[q];
+            J.nbox[P * 2 * D + 2 * q + 1] = nhi[q];
         }
         J.nmeta[P] = inner_code(base + i, len);
         J.ucode[2 * P] = V.code[2 * i];
@@ -1086,23 +1089,23 @@ __global__ __launch_bounds__(kCtLevelThreads) void k_ct_levels(CtJobs js) {
         for (int64_t g = t; g < nG; g += kCtLevelThreads) {
             const int64_t first = ls + 8 * g;
             const int len = n - 8 * g < 8 ? (int)(n - 8 * g) : 8;
-            float lo[D], hi[D];
+            float lo[D], nhi[D];  // (lo, -hi) pairs: the union is a minimum of both
 #pragma unroll
             for (int q = 0; q < D; ++q) {
-                lo[q] = J.nbox[first * 2 * D + q];
-                hi[q] = J.nbox[first * 2 * D + D + q];
+                lo[q] = J.nbox[first * 2 * D + 2 * q];
+                nhi[q] = J.nbox[first * 2 * D + 2 * q + 1];
             }
             for (int u = 1; u < len; ++u)
 #pragma unroll
                 for (int q = 0; q < D; ++q) {
-                    lo[q] = fminf(lo[q], J.nbox[(first + u) * 2 * D + q]);
-                    hi[q] = fmaxf(hi[q], J.nbox[(first + u) * 2 * D + D + q]);
+                    lo[q] = fminf(lo[q], J.nbox[(first + u) * 2 * D + 2 * q]);
+                    nhi[q] = fminf(nhi[q], J.nbox[(first + u) * 2 * D + 2 * q + 1]);
                 }
             const int64_t P = ls + n + g;
 #pragma unroll
             for (int q = 0; q < D; ++q) {
-                J.nbox[P * 2 * D + q] = lo[q];
-                J.nbox[P * 2 * D + D + q] = hi[q];
+                J.nbox[P * 2 * D + 2 * q] = lo[q];
+                J.nbox[P * 2 * D + 2 * q + 1] = nhi[q];
             }
             J.nmeta[P] = inner_code(first, len);
         }
@@ -1156,7 +1159,7 @@ __global__ __launch_bounds__(64) void k_ct_reset(CtJobs js) {
     J.hull_keys[t] = 0ull;  // kCtHull = 64 slots
     if (t < 2 * kCtMaxDim) J.ibox[t] = t < kCtMaxDim ? ~0ull : 0ull;
     if (t < 2 * d) {
-        const float v = t < d ? __builtin_huge_valf() : -__builtin_huge_valf();
+        const float v = __builtin_huge_valf();  // the empty box: (lo, -hi) = (+inf, +inf)
         J.bbox[t] = v;
         J.obox[t] = v;
     }
@@ -1265,17 +1268,11 @@ __global__ void k_ct_bulk_fill(const double *__restrict__ pts, const uint64_t *_
     if (n == 0) {
         if (j == 0) {
             bcnt[0] = 0;
-            for (int q = 0; q < D; ++q) {
-                bbox[q] = __builtin_huge_valf();
-                bbox[D + q] = -__builtin_huge_valf();
-            }
+            for (int q = 0; q < 2 * D; ++q) bbox[q] = __builtin_huge_valf();  // empty: (+inf, +inf) pairs
             dir_code[0] = 0;
             dir_code[1] = 0;
             dir_meta[0] = leaf_code(0, 1);  // never walked: the walk skips an empty tree
-            for (int q = 0; q < D; ++q) {
-                dir_box[q] = __builtin_huge_valf();
-                dir_box[D + q] = -__builtin_huge_valf();
-            }
+            for (int q = 0; q < 2 * D; ++q) dir_box[q] = __builtin_huge_valf();
             cnt->n_dir = cnt->n_buckets = 1;
             cnt->n_seg = cnt->n_new_dir = cnt->n_scratch = 0;
             cnt->nidx = 0;
@@ -1347,12 +1344,18 @@ template <int D>
 __device__ __forceinline__ float ct_box_lb(const float *__restrict__ b, const double (&qq)[D], const float (&qlo)[D],
                                            const float (&qhi)[D]) {
     if constexpr (D <= 7) {
-        // fused multiply-adds: one rounding a term instead of two, still far inside the shrink
+        // dim k's two gaps (lo - qhi, qlo - hi) as one packed addition of the box's (lo, -hi)
+        // word and the query's (-qhi, qlo); then one max3 and one fused multiply-add: 3
+        // instructions a dim (4 unpacked).  One rounding a term, still far inside the shrink
         // (each gap and each step at most (1 + 2^-24) above the exact value: (1 + 2^-24)^9)
+        typedef float f2 __attribute__((ext_vector_type(2)));
         float s = 0.0f;
 #pragma unroll
         for (int k = 0; k < D; ++k) {
-            const float g = fmaxf(fmaxf(b[k] - qhi[k], qlo[k] - b[D + k]), 0.0f);
+            const f2 box = {b[2 * k], b[2 * k + 1]};
+            const f2 qry = {-qhi[k], qlo[k]};
+            const f2 gap = box + qry;
+            const float g = fmaxf(fmaxf(gap.x, gap.y), 0.0f);
             s = __builtin_fmaf(g, g, s);
         }
         return s * kCtLbShrink;
@@ -1360,7 +1363,7 @@ __device__ __forceinline__ float ct_box_lb(const float *__restrict__ b, const do
         double lb2 = 0.0;
 #pragma unroll
         for (int k = 0; k < D; ++k) {
-            const double g = fmax(fmax((double)b[k] - qq[k], qq[k] - (double)b[D + k]), 0.0);
+            const double g = fmax(fmax((double)b[2 * k] - qq[k], qq[k] + (double)b[2 * k + 1]), 0.0);
             lb2 += g * g;
         }
         return __double2float_rd(lb2);
