@@ -72,7 +72,7 @@ struct CellTreeDev {
     const uint32_t *top;       // the walk's first entries (CtCounts top / n_top)
     const int32_t *n_top;
     const uint32_t *nmeta;     // [nodes]
-    const float *nbox;         // [nodes][2d] widened float bounds: lo then hi
+    const float *nbox;         // [nodes][d][2] widened float bounds: (lo, -hi) a dim
     const double *bpts;        // [buckets][kCtCap][d]
     const int32_t *bids;       // [buckets][kCtCap] 1-based ids
     const double *hull_pts;    // [kCtHull][d] seed rows, ids in hull_ids (0: empty slot)
