@@ -254,7 +254,8 @@ mpt_status mpt_rrt_enable_timing(mpt_rrt *rrt, int32_t enable);
 /* NN structure of the rounds: MPT_NN_AUTO / _BRUTE / _GRID / _TREE (the incremental cell
  * tree, for trees that do not fill the sampling box), grid occupancy target (points per cell,
  * <= 0: the default, 2 points per cell with the cell side floored at 0.3x the expected NN
- * distance over all state dims).  Results are identical.  When the engine's rounds will use
+ * distance over all state dims; for 15-dim states 3 points per cell, no floor).  Results are
+ * identical.  When the engine's rounds will use
  * the tree (MPT_NN_TREE, or MPT_NN_AUTO after mpt_rrt_add_nodes' first nodes chose it), the
  * tree's memory for the engine's capacity is reserved here (allocates, synchronises). */
 mpt_status mpt_rrt_set_nn(mpt_rrt *rrt, int32_t mode, double points_per_cell);

@@ -1092,11 +1092,18 @@ StepCtx step_head(mpt_rrt *r, int32_t K, hipStream_t stream, bool defer_tree = f
             hi[j] = p.hi[r->grid_dims[j]];
         }
         // cells of ~2 points, but not much finer than the expected NN distance over all
-        // state dims (kGridHminK: the fraction)
+        // state dims (kGridHminK: the fraction).  A state of 15 dims (the snake: the grid
+        // spans x, y of them) takes cells of ~3 points with no floor: the floor from the
+        // 15-dim NN distance made cells so coarse that a query examined 1.51x the points any
+        // x, y index must (scripts/snake_floor.py: 1 100.6 vs 731.0); at 3 points a cell 1.29x
+        // (945.3), the round within its run-to-run spread (config 3 54.87 M before, 54.65 / 53.78
+        // M in two runs after; 2 points a cell: 1.26x but 51.1 M, the cells' overhead)
         const double hk = kGridHminK;
-        const double ppc = r->ppc > 0 ? r->ppc : 2.0;
-        const double hmin_n = r->ppc > 0 ? 0.0 : hk * expected_nn_distance(p.d, p.lo, p.hi, r->n_upper);
-        const double hmin_c = r->ppc > 0 ? 0.0 : hk * expected_nn_distance(p.d, p.lo, p.hi, r->cap);
+        const bool wide = p.d >= 15;
+        const double ppc = r->ppc > 0 ? r->ppc : (wide ? 3.0 : 2.0);
+        const bool floor_h = r->ppc <= 0 && !wide;
+        const double hmin_n = floor_h ? hk * expected_nn_distance(p.d, p.lo, p.hi, r->n_upper) : 0.0;
+        const double hmin_c = floor_h ? hk * expected_nn_distance(p.d, p.lo, p.hi, r->cap) : 0.0;
         const GridParams g = make_grid_params(p.d, r->grid_dims, r->grid_gd, lo, hi, r->n_upper, ppc, hmin_n);
         const GridParams gcap = make_grid_params(p.d, r->grid_dims, r->grid_gd, lo, hi, r->cap, ppc, hmin_c);
         r->grid->reserve(r->cap, p.d, std::max(g.ncells, gcap.ncells));  // once, as for the tree

@@ -28,6 +28,7 @@ def main():
     ap.add_argument("--batch", type=int, default=65536)
     ap.add_argument("--seed", type=int, default=1000)
     ap.add_argument("--chunk", type=int, default=512)
+    ap.add_argument("--ppc", type=float, default=0.0, help="grid points per cell (0: the engine's default)")
     a = ap.parse_args()
 
     import torch
@@ -45,7 +46,7 @@ def main():
     agent = mpt.AgentMesh(sc.agent_tris)
     eng = mpt.RRTEngine(env, agent, sc.kind, sc.prm, sc.ranges, sc.steer_dt, sc.cc_dt, n0 + K, seed)
     eng.add_nodes(tree)
-    eng.set_nn("auto", 0.0)
+    eng.set_nn("auto", a.ppc)
     eng.enable_timing(True)
     stream = torch.cuda.current_stream()
     for _ in range(3):  # the bench's warm-up rounds
@@ -81,7 +82,8 @@ def main():
     fl = floor.double().mean().item()
     out = {
         "metric": "config-3 NN points examined per query vs the x, y index floor",
-        "config": {"workload": "snake_trailers (11 links) in the corridor", "tree": n0, "queries": K, "seed": seed},
+        "config": {"workload": "snake_trailers (11 links) in the corridor", "tree": n0, "queries": K, "seed": seed,
+                   "ppc": a.ppc},
         "nn_structure": "grid over x, y (mpt_rrt_last_nn)",
         "examined_per_query": round(examined, 2),
         "floor_per_query": round(fl, 2),
