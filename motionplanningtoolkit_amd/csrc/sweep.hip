@@ -269,16 +269,18 @@ __global__ __launch_bounds__(kSweepWaves * 64) void k_sweep_lite(EnvDev env, con
     }
 }
 
-// ---- PRM edges (mpt_prm_connect's sweep path), three launches over the roadmap:
-//  1. k_sweep_cands: one wave an edge walks the env tree (prm_walk) and emits (edge, agent
-//     triangle, env triangle, pose range) candidates, at most kSweepEdgeCands an edge: an edge
-//     that reaches the cap stops and is listed;
+// ---- PRM edges (mpt_prm_connect's sweep path), four launches over the roadmap:
+//  0. k_sweep_prm over every edge, each (triangle, env triangle) pair at its middle pose only
+//     (kSweepCoarse): one wave an edge walks the env tree (prm_walk), the gate-passing triples
+//     go through the SAT 64 at a time, the edge ending at its first contact -- a contact with a
+//     wall lasts many poses, so this decides nearly every colliding edge (config 4 at --bounds
+//     rooms: 44 % of the edges collide);
+//  1. k_sweep_cands over the undecided edges: the walk again, (edge, agent triangle, env
+//     triangle, pose range) candidates, at most kSweepEdgeCands an edge: an edge that reaches
+//     the cap stops and is listed;
 //  2. k_sweep_sat: the gate + SAT over each candidate's poses, one candidate a lane (full waves
-//     at full occupancy; ~55 % of config 4's edges at --bounds rooms are decided here, free);
-//  3. k_sweep_prm over the listed edges (mostly colliding ones): the walk again, each pair's
-//     middle pose first (kSweepCoarse: a contact with a wall lasts many poses, so this pass finds
-//     nearly every colliding edge's), then the poses it skipped; the gate passes batched into
-//     SATs of 64 a wave, the edge ending at its first contact.
+//     at full occupancy): the free edges, ~430 k candidates a roadmap;
+//  3. k_sweep_prm over the listed edges (~5 000): the poses step 0 skipped.
 // Verdicts are the same set: every (edge, agent triangle, env triangle, pose) the reference
 // tests either is in some candidate or in one of k_sweep_prm's two pose sets (same fan-out, same
 // box tests, the same pose interval), each with the same operations, and a contact found
@@ -322,7 +324,8 @@ constexpr int kSweepPasses = 1;      // then k_sweep_prm takes what is left
 // rooms, collision ms on one box: stride 8: 14.8, 16: 14.3, 1024: 14.1; with the first pose at
 // the interval's start instead of its middle: no coarse pass 30.8, stride 4: 19.1, 8: 17.9, 16:
 // 23.9; the coarse pass over every edge before the candidates instead: 20.0, and over every
-// edge with no candidates at all: 21.2)
+// edge with no candidates at all: 21.2).  The middle-pose pass then went first, over every edge
+// (step 0 above): 13.9 -> 10.3 ms (without the candidate pass after it: 10.45)
 constexpr unsigned kSweepCoarse = 1024;
 
 // false when the queue is full: the wave's edge is then deferred (the candidates that did fit
@@ -869,6 +872,9 @@ void launch_collide_sweep_prm(const EnvDev &env, const AgentDev *d_link, int32_t
                                n_list, E, false, verdict, stats);
         hip_check(hipGetLastError(), "k_sweep_prm launch");
     };
+    // 0. every edge's pairs at their middle poses (k_sweep_prm): decides nearly every colliding
+    //    edge (a contact with a wall lasts many poses) before any candidate is queued
+    prm_pass(nullptr, nullptr, kSweepCoarse, false);
     // n: [0] queue, [1] fused list, [2 + k] list k
     hip_check(hipMemsetAsync(q.n, 0, sizeof(uint32_t) * 4, stream), "sweep counts zero");
     uint64_t emitted = 0;
@@ -903,8 +909,7 @@ void launch_collide_sweep_prm(const EnvDev &env, const AgentDev *d_link, int32_t
     // which skips the edges already decided -- the coarse poses, then the rest
     uint64_t to_fused = q.h[1];
     if (n_in > 0 && last >= 0) {
-        prm_pass(q.le[last], q.n + 2 + last, kSweepCoarse, false);
-        prm_pass(q.le[last], q.n + 2 + last, kSweepCoarse, true);
+        prm_pass(q.le[last], q.n + 2 + last, kSweepCoarse, true);  // their middle poses were step 0's
         to_fused += (uint64_t)n_in;
     }
     if (q.h[1] > 0) prm_pass(q.fused, q.n + 1, 1u, false);
