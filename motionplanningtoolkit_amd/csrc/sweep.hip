@@ -844,9 +844,11 @@ void launch_collide_sweep_prm(const EnvDev &env, const AgentDev *d_link, int32_t
         }
     };
     static thread_local Q q;
-    // 128 candidates an edge (the first pass: at most kSweepEdgeCands + 64 an edge, the cap being
-    // checked after each emission step), at least 4 M; later passes size their caps to it
-    const int64_t want = std::min<int64_t>(std::max<int64_t>(int64_t(1) << 22, 128 * E), int64_t(1) << 31);
+    // 16 candidates an edge, at least 4 M (after step 0 the candidate pass sees the free edges:
+    // config 4 at --bounds rooms queues ~1 an edge; an edge that finds the queue full goes to
+    // k_sweep_prm's full pass instead, so the size decides speed only); later passes size their
+    // caps to it
+    const int64_t want = std::min<int64_t>(std::max<int64_t>(int64_t(1) << 22, 16 * E), int64_t(1) << 31);
     if (want > q.cap || E > q.ecap) {
         hip_check(hipStreamSynchronize(stream), "sync");
         for (void *p : {(void *)q.c, (void *)q.fused, (void *)q.le[0], (void *)q.le[1], (void *)q.lr[0],
