@@ -630,7 +630,7 @@ template <unsigned stride>
 __global__ __launch_bounds__(kSweepWaves * 64) __attribute__((amdgpu_waves_per_eu(3))) void k_sweep_prm(EnvDev env, const AgentDev *__restrict__ link,
                                                                 PrmEdges P, const int32_t *__restrict__ list,
                                                                 const uint32_t *__restrict__ n_list, int64_t E,
-                                                                bool rest, uint8_t *verdict,
+                                                                bool rest, uint32_t *next, uint8_t *verdict,
                                                                 unsigned long long *stats) {
     __shared__ int32_t s_stk[kSweepWaves][2 * kSweepStack];
     __shared__ SatTriple s_sat[kSweepWaves][2 * kSatBatch];
@@ -641,7 +641,13 @@ __global__ __launch_bounds__(kSweepWaves * 64) __attribute__((amdgpu_waves_per_e
     SatTriple *sat = s_sat[wave];
     const AgentDev &ag = link[0];
     const int64_t n = list ? (int64_t)*n_list : E;
-    for (int64_t i = (int64_t)blockIdx.x * kSweepWaves + wave; i < n; i += (int64_t)gridDim.x * kSweepWaves) {
+    // edges taken one at a time from a shared counter (an edge's cost runs from a walk with no
+    // pair to thousands of gates: a fixed stride left waves with a run of costly ones last)
+    for (;;) {
+        uint32_t ni = 0;
+        if (lane == 0) ni = atomicAdd(next, 1u);
+        const int64_t i = (int64_t)__builtin_amdgcn_readfirstlane((int)ni);
+        if (i >= n) break;
         const int64_t e = list ? list[i] : i;
         if (load_flag(verdict + e)) continue;
         const PrmEdge g = prm_edge_uniform(P, e);
@@ -834,11 +840,11 @@ void launch_collide_sweep_prm(const EnvDev &env, const AgentDev *d_link, int32_t
         SweepCand *c = nullptr;
         int32_t *fused = nullptr, *le[2] = {nullptr, nullptr};
         uint32_t *lr[2] = {nullptr, nullptr};
-        uint32_t *n = nullptr, *h = nullptr;
+        uint32_t *n = nullptr, *h = nullptr, *next = nullptr;
         int64_t cap = 0, ecap = 0;
         ~Q() {
             for (void *p : {(void *)c, (void *)fused, (void *)le[0], (void *)le[1], (void *)lr[0], (void *)lr[1],
-                            (void *)n})
+                            (void *)n, (void *)next})
                 if (p) (void)hipFree(p);
             if (h) (void)hipHostFree(h);
         }
@@ -861,19 +867,23 @@ void launch_collide_sweep_prm(const EnvDev &env, const AgentDev *d_link, int32_t
             hip_check(hipMalloc(&q.lr[k], sizeof(uint32_t) * (size_t)E), "sweep edge lists");
         }
         if (!q.n) hip_check(hipMalloc(&q.n, sizeof(uint32_t) * 4), "sweep counts");
+        if (!q.next) hip_check(hipMalloc(&q.next, sizeof(uint32_t) * 8), "sweep edge counters");
         if (!q.h) hip_check(hipHostMalloc(&q.h, sizeof(uint32_t) * 4), "sweep counts");
         q.cap = want;
         q.ecap = E;
     }
+    int pass_no = 0;
     auto prm_pass = [&](const int32_t *list, const uint32_t *n_list, unsigned stride, bool rest) {
+        uint32_t *next = q.next + (pass_no++ & 7);  // a counter a launch (zeroed below, once a call)
         if (stride == kSweepCoarse)
             hipLaunchKernelGGL(k_sweep_prm<kSweepCoarse>, dim3(4096), dim3(kSweepWaves * 64), 0, stream, env, d_link,
-                               edges, list, n_list, E, rest, verdict, stats);
+                               edges, list, n_list, E, rest, next, verdict, stats);
         else
             hipLaunchKernelGGL(k_sweep_prm<1>, dim3(4096), dim3(kSweepWaves * 64), 0, stream, env, d_link, edges, list,
-                               n_list, E, false, verdict, stats);
+                               n_list, E, false, next, verdict, stats);
         hip_check(hipGetLastError(), "k_sweep_prm launch");
     };
+    hip_check(hipMemsetAsync(q.next, 0, sizeof(uint32_t) * 8, stream), "sweep counters zero");
     // 0. every edge's pairs at their middle poses (k_sweep_prm): decides nearly every colliding
     //    edge (a contact with a wall lasts many poses) before any candidate is queued
     prm_pass(nullptr, nullptr, kSweepCoarse, false);
