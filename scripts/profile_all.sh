@@ -21,7 +21,7 @@ prof room bench.py "--workload blimp-room --steps 5 --warmup 2 --no-cpu --no-var
 prof snake bench.py "--workload snake --steps 5 --warmup 2 --no-cpu --no-variants" || exit 1
 prof c5_32 bench.py "--seeds 32 --steps 25 --warmup 5 --no-cpu" last:k_sample_jobs || exit 1
 prof c5_256 bench.py "--seeds 256 --steps 25 --warmup 5 --no-cpu" last:k_sample_jobs || exit 1
-prof prm scripts/bench_prm.py "--reps 1 --no-cpu" last:k_sweep_cands || exit 1
+prof prm scripts/bench_prm.py "--reps 1 --no-cpu" last:k_sort_segments || exit 1
 prof distance scripts/bench_distance.py "--steps 3 --warmup 1 --no-cpu" || exit 1
 # the tree walk's instruction and wait counters (one pass: 5 SQ counters)
 timeout -s KILL 200 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_BUSY_CYCLES --output-format csv \
