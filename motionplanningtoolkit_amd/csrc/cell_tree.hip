@@ -114,24 +114,23 @@ __device__ __forceinline__ void hull_offer(const CtPlan &P, const double (&x)[D]
         const int kind = P.hkind[lane], dm = P.hdim[lane];
         const float u0 = P.hdir[lane][0], u1 = P.hdir[lane][1], u2 = P.hdir[lane][2];
         unsigned long long best = 0;
-        for (uint64_t m = lm; m; m &= m - 1) {
-            const int j = __ffsll((long long)m) - 1;
+        // every point of the wave, unrolled by 8 so the LDS reads overlap (a loop over the live
+        // mask's bits waited out each point's reads); dead points score key 0
+#pragma unroll 8
+        for (int j = 0; j < 64; ++j) {
             double v;
             if (kind == 0) {
                 v = (double)u0 * s_rows[j][0];
                 if (D > 1) v += (double)u1 * s_rows[j][D > 1 ? 1 : 0];
                 if (D > 2) v += (double)u2 * s_rows[j][D > 2 ? 2 : 0];
             } else {
-                double xv = s_rows[j][0];
-#pragma unroll
-                for (int k = 1; k < D; ++k)
-                    if (k == dm) xv = s_rows[j][k];
+                const double xv = s_rows[j][dm];
                 v = kind == 1 ? -xv : xv;
             }
             const uint32_t b = __float_as_uint((float)v);
             const uint32_t key = (b & 0x80000000u) ? ~b : (b | 0x80000000u);
             const unsigned long long k64 = ((unsigned long long)key << 32) | (uint32_t)(row0 + j);
-            best = k64 > best ? k64 : best;
+            best = ((lm >> j) & 1) && k64 > best ? k64 : best;
         }
         if (best) atomicMax(keys + lane, best);
     }
@@ -313,8 +312,14 @@ __global__ __launch_bounds__(kCtSortThreads) void k_ct_csort(CtJobs js) {
     }
 }
 
+// Every 8th element of each chunk (the last of each group of 8) is staged in LDS: the binary
+// search's steps of 256 .. 8 probe exactly those, so they run in LDS and only the steps of 4, 2
+// and 1 and the last probe read global memory (4 dependent loads, not 10).
+constexpr int kCtRankGroup = 8;
+constexpr int kCtRankSamples = kCtChunk / kCtRankGroup;  // 64 a chunk
 template <int NC>
-__device__ __forceinline__ void ct_crank_n(const CtJob &J, int64_t m, int e) {
+__device__ __forceinline__ void ct_crank_n(const CtJob &J, int64_t m, int e, const uint64_t *s_h, const uint64_t *s_l,
+                                           const int32_t *s_r) {
     const int nch = (int)((m + kCtChunk - 1) / kCtChunk);
     const uint64_t h = J.ccode[2 * e], l = J.ccode[2 * e + 1];
     const int32_t r = J.crow[e];
@@ -322,7 +327,15 @@ __device__ __forceinline__ void ct_crank_n(const CtJob &J, int64_t m, int e) {
 #pragma unroll
     for (int c = 0; c < NC; ++c) pos[c] = 0;
 #pragma unroll
-    for (int st = kCtChunk / 2; st > 0; st >>= 1) {
+    for (int st = kCtChunk / 2; st >= kCtRankGroup; st >>= 1) {
+#pragma unroll
+        for (int c = 0; c < NC; ++c) {
+            const int q = c * kCtRankSamples + (pos[c] + st) / kCtRankGroup - 1;  // element pos + st - 1
+            pos[c] += cr_lt(s_h[q], s_l[q], s_r[q], h, l, r) ? st : 0;
+        }
+    }
+#pragma unroll
+    for (int st = kCtRankGroup / 2; st > 0; st >>= 1) {
         uint64_t ph[NC], pl[NC];
         int32_t pr[NC];
 #pragma unroll
@@ -356,12 +369,26 @@ __device__ __forceinline__ void ct_crank_n(const CtJob &J, int64_t m, int e) {
 
 __global__ __launch_bounds__(256) void k_ct_crank(CtJobs js) {
     const CtJob J = CT_JOB(js);  // by value: the fields stay in registers across the stores
+    __shared__ uint64_t s_h[kCtChunks * kCtRankSamples], s_l[kCtChunks * kCtRankSamples];
+    __shared__ int32_t s_r[kCtChunks * kCtRankSamples];
     const int64_t m = ct_new_count(J);
+    if ((int64_t)blockIdx.x * blockDim.x >= m) return;  // block-uniform
+    const int nch = (int)((m + kCtChunk - 1) / kCtChunk);
+    const int NCs = m <= (int64_t)kCtChunk * 4 ? 4 : m <= (int64_t)kCtChunk * 8 ? 8 : kCtChunks;
+    for (int v = threadIdx.x; v < NCs * kCtRankSamples; v += blockDim.x) {
+        const int c = v / kCtRankSamples;
+        const int q = c * kCtChunk + (v - c * kCtRankSamples) * kCtRankGroup + kCtRankGroup - 1;
+        const bool in = c < nch;  // chunks past the last are never counted (their probes only steer)
+        s_h[v] = in ? J.ccode[2 * q] : ~0ull;
+        s_l[v] = in ? J.ccode[2 * q + 1] : ~0ull;
+        s_r[v] = in ? J.crow[q] : 0x7fffffff;
+    }
+    __syncthreads();
     const int e = (int)blockIdx.x * (int)blockDim.x + (int)threadIdx.x;
     if (e >= m) return;
-    if (m <= (int64_t)kCtChunk * 4) ct_crank_n<4>(J, m, e);
-    else if (m <= (int64_t)kCtChunk * 8) ct_crank_n<8>(J, m, e);  // a round's K = 4096: 8 chunks
-    else ct_crank_n<kCtChunks>(J, m, e);
+    if (NCs == 4) ct_crank_n<4>(J, m, e, s_h, s_l, s_r);
+    else if (NCs == 8) ct_crank_n<8>(J, m, e, s_h, s_l, s_r);  // a round's K = 4096: 8 chunks
+    else ct_crank_n<kCtChunks>(J, m, e, s_h, s_l, s_r);
 }
 
 // each sorted new point's directory position: the last entry whose start is <= its code
@@ -510,8 +537,8 @@ __global__ __launch_bounds__(kCtSegThreads) void k_ct_segments(CtJobs js) {
 }
 
 // Per sorted new point: appended to its bucket, or placed in its split segment's merged list
-// (the segment's first point also places the bucket's old points and, on append, sets the
-// bucket's count and box).
+// with the old points just below it (on append, the segment's first point sets the bucket's
+// count and box).
 template <int D>
 __global__ __launch_bounds__(256) void k_ct_apply(CtJobs js) {
     const CtJob J = CT_JOB(js);  // by value: the fields stay in registers across the stores
@@ -549,9 +576,16 @@ __global__ __launch_bounds__(256) void k_ct_apply(CtJobs js) {
                     hi[q] = -__builtin_huge_val();
                 }
             }
-            for (int u = 0; u < k; ++u) {
+            // the segment's k <= 8 rows, then their points: unconditional loads (slots past k
+            // repeat its last point), so each pass's loads are in flight together -- a loop over
+            // k waited out two dependent loads a point
+            int32_t rs[kCtCap];
+#pragma unroll
+            for (int u = 0; u < kCtCap; ++u) rs[u] = J.nrow[j0 + (u < k ? u : k - 1)];
+#pragma unroll
+            for (int u = 0; u < kCtCap; ++u) {
                 double y[D];
-                load_global<D>(J.pts + (int64_t)J.nrow[j0 + u] * D, y);
+                load_global<D>(J.pts + (int64_t)rs[u] * D, y);
 #pragma unroll
                 for (int q = 0; q < D; ++q) {
                     lo[q] = y[q] < lo[q] ? y[q] : lo[q];
@@ -577,29 +611,37 @@ __global__ __launch_bounds__(256) void k_ct_apply(CtJobs js) {
         ol[o] = J.bcode[2 * os + 1];
         orw[o] = J.bids[os] - 1;
     }
-    int below = 0;
+    // and the previous new point's (the segment's points are sorted, so `below` never falls)
+    const int jp = j > j0 ? j - 1 : j;
+    const uint64_t ph = J.ncode[2 * jp], pl = J.ncode[2 * jp + 1];
+    const int32_t pr = J.nrow[jp];
+    int below = 0, below_prev = 0;
 #pragma unroll
-    for (int o = 0; o < kCtCap; ++o) below += (o < c && cr_lt(oh[o], ol[o], orw[o], h, l, row)) ? 1 : 0;
+    for (int o = 0; o < kCtCap; ++o) {
+        below += (o < c && cr_lt(oh[o], ol[o], orw[o], h, l, row)) ? 1 : 0;
+        below_prev += (o < c && cr_lt(oh[o], ol[o], orw[o], ph, pl, pr)) ? 1 : 0;
+    }
+    if (j == j0) below_prev = 0;
     const int32_t e = off + (j - j0) + below;
     J.scode[2 * e] = h;
     J.scode[2 * e + 1] = l;
     J.srow[e] = row;
     J.sseg[e] = s;
-    if (j != j0) return;
+    // The old points of ranks [below_prev, below) lie between the previous new point and this
+    // one: j - j0 new points below them.  The segment's last point also places the old points
+    // above it (k new points below them).  Every old point is placed once, by the new point
+    // after it, with no searches (a segment's first point searching for all of them waited out
+    // up to 8 dependent binary searches).
+    const int r_hi = j == j0 + k - 1 ? c : below;
+    if (below_prev >= r_hi) return;
 #pragma unroll
-    for (int o = 0; o < kCtCap; ++o) {  // the old points' places
+    for (int o = 0; o < kCtCap; ++o) {
         if (o >= c) break;
-        int ob = 0;
+        int ob = 0;  // old point o's rank among the old points
 #pragma unroll
         for (int o2 = 0; o2 < kCtCap; ++o2) ob += (o2 < c && cr_lt(oh[o2], ol[o2], orw[o2], oh[o], ol[o], orw[o])) ? 1 : 0;
-        int lo = 0, hi = k;  // new points below it (sorted)
-        while (lo < hi) {
-            const int mid = (lo + hi) >> 1;
-            const int q = j0 + mid;
-            if (cr_lt(J.ncode[2 * q], J.ncode[2 * q + 1], J.nrow[q], oh[o], ol[o], orw[o])) lo = mid + 1;
-            else hi = mid;
-        }
-        const int32_t eo = off + ob + lo;
+        if (ob < below_prev || ob >= r_hi) continue;
+        const int32_t eo = off + ob + (ob < below ? j - j0 : k);
         J.scode[2 * eo] = oh[o];
         J.scode[2 * eo + 1] = ol[o];
         J.srow[eo] = orw[o];
@@ -652,19 +694,53 @@ __device__ __forceinline__ bool ct_same_a(const uint8_t *__restrict__ a, int64_t
 __device__ __forceinline__ int64_t ct_scratch_total(const CtJob &J) { return J.cnt->n_scratch; }
 
 // leaf starts of the split segments: 1 the segment's first leaf (keeps the bucket), 2 a new leaf
+// (ct_same over the adjacent prefix lengths of 256 elements and kCtCap either side, staged in
+// LDS by one coalesced pass: ct_same's neighbour loads waited out each other, up to 14 in a row)
 __global__ __launch_bounds__(256) void k_ct_split_flags(CtJobs js) {
     const CtJob J = CT_JOB(js);  // by value: the fields stay in registers across the stores
+    __shared__ uint8_t s_a[256 + 2 * kCtCap];  // s_a[v] = c_cpl(element u - 1, element u), u = c0 - kCtCap + v
     const int64_t total = ct_scratch_total(J);
-    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
-        const int s = J.sseg[e];
-        int flag = 0;
-        if (s >= 0) {
-            const int4 g = J.seg[s];
-            const int64_t off = g.w, L = (int64_t)g.y + g.z;
-            if (e == off) flag = 1;
-            else if (!ct_same(J.scode, J.srow, off, off + L, e)) flag = 2;
+    for (int64_t c0 = (int64_t)blockIdx.x * 256; c0 < total; c0 += (int64_t)gridDim.x * 256) {
+        for (int v = threadIdx.x; v < 256 + 2 * kCtCap; v += 256) {
+            const int64_t u = c0 - kCtCap + v;
+            int cp = 0;
+            if (u >= 1 && u < total)
+                cp = c_cpl(J.scode[2 * (u - 1)], J.scode[2 * (u - 1) + 1], J.scode[2 * u], J.scode[2 * u + 1]);
+            s_a[v] = (uint8_t)cp;
         }
-        J.slead[e] = flag;
+        __syncthreads();
+        const int64_t e = c0 + threadIdx.x;
+        if (e < total) {
+            const int s = J.sseg[e];
+            int flag = 0;
+            if (s >= 0) {
+                const int4 g = J.seg[s];
+                const int64_t off = g.w, L = (int64_t)g.y + g.z;
+                if (e == off) {
+                    flag = 1;
+                } else {
+                    // ct_same (row rule for equal codes) over the segment [off, off + L)
+                    const int i = (int)threadIdx.x + kCtCap;
+                    const int k = s_a[i];
+                    const int64_t lo = off - (c0 - kCtCap), hi = off + L - (c0 - kCtCap);
+                    int cnt = 2;
+                    for (int u = i - 1; u > lo && cnt <= kCtCap; --u) {
+                        if (s_a[u] < k) break;
+                        ++cnt;
+                    }
+                    for (int u = i + 1; u < hi && cnt <= kCtCap; ++u) {
+                        if (s_a[u] < k) break;
+                        ++cnt;
+                    }
+                    const bool same = cnt <= kCtCap ? true
+                                      : k < 128     ? false
+                                                    : (J.srow[e] >> 3) == (J.srow[e - 1] >> 3);
+                    flag = same ? 0 : 2;
+                }
+            }
+            J.slead[e] = flag;
+        }
+        __syncthreads();  // s_a reused by the next chunk
     }
 }
 
@@ -770,32 +846,37 @@ __global__ __launch_bounds__(256) void k_ct_split_fill(CtJobs js) {
     __shared__ double s_x[256][D];             // the chunk's rows: a leaf inside it boxes from LDS
     const int64_t total = ct_scratch_total(J);
     for (int64_t c0 = (int64_t)blockIdx.x * 256; c0 < total; c0 += (int64_t)gridDim.x * 256) {
+    // the element's own loads first, in flight with the flags' staging
+    const int64_t e = c0 + threadIdx.x;
+    const bool live = e < total;
+    const int s = live ? J.sseg[e] : -1;
+    const int32_t row = live ? J.srow[e] : 0;
+    const uint64_t eh = live ? J.scode[2 * e] : 0, el = live ? J.scode[2 * e + 1] : 0;
     for (int v = threadIdx.x; v < 256 + 2 * kCtCap; v += 256) {
         const int64_t x = c0 - kCtCap + v;
         s_f[v] = (int8_t)(x >= 0 && x < total ? J.slead[x] : -1);
     }
     __syncthreads();
-    const int64_t e = c0 + threadIdx.x;
-    const int s = e < total ? J.sseg[e] : -1;
     const int ve = threadIdx.x + kCtCap;
     int flag = 0, len = 0;
     int32_t b = 0;
     if (s >= 0) {
+        double x[D];
+        load_global<D>(J.pts + (int64_t)row * D, x);  // (its bucket is not needed to load it)
         int vs = ve;  // the leaf's first element (a segment's first element starts a leaf)
         while (vs > 0 && s_f[vs] == 0) --vs;
         int64_t st = c0 - kCtCap + vs;
         if (s_f[vs] <= 0) {  // beyond the staged flags (a leaf longer than kCtCap: an index error)
             st = st < 0 ? 0 : st;
             while (st > 0 && J.slead[st] == 0) --st;
+            flag = J.slead[st];
+        } else {
+            flag = s_f[vs];
         }
-        flag = J.slead[st];
         const int4 g = J.seg[s];
         b = ct_leaf_bucket(J, st, flag, g);
         const int64_t u = e - st;
         if (b < J.bcap && u < kCtCap) {
-            const int32_t row = J.srow[e];
-            double x[D];
-            load_global<D>(J.pts + (int64_t)row * D, x);
             const int64_t slot = (int64_t)b * kCtCap + u;
 #pragma unroll
             for (int q = 0; q < D; ++q) {
@@ -803,8 +884,8 @@ __global__ __launch_bounds__(256) void k_ct_split_fill(CtJobs js) {
                 s_x[threadIdx.x][q] = x[q];
             }
             J.bids[slot] = row + 1;
-            J.bcode[2 * slot] = J.scode[2 * e];
-            J.bcode[2 * slot + 1] = J.scode[2 * e + 1];
+            J.bcode[2 * slot] = eh;
+            J.bcode[2 * slot + 1] = el;
         }
         if (e == st) {
             const int64_t end = (int64_t)g.w + g.y + g.z;
@@ -819,6 +900,24 @@ __global__ __launch_bounds__(256) void k_ct_split_fill(CtJobs js) {
     }
     __syncthreads();  // s_f, s_x reused by the next chunk
     }
+}
+
+// The first index of a sorted a[0, n) whose value is >= key, by one wave: 64 probes a step
+// (a 64-ary search: 2 dependent loads for n <= 4096 where a binary search by one lane waits
+// out 12).  Every lane of the wave calls it and gets the answer.
+__device__ __forceinline__ int32_t wave_lower_bound(const int32_t *__restrict__ a, int32_t n, int64_t key) {
+    const int lane = threadIdx.x & 63;
+    int32_t lo = 0, hi = n;  // the answer is in [lo, hi]
+    while (lo < hi) {
+        const int32_t step = (hi - lo + 63) / 64;
+        const int32_t p = lo + (lane + 1) * step - 1;  // probe: is the answer past p?
+        const bool less = p < hi && a[p] < key;
+        const int32_t c = __popcll(__ballot(less));    // probes below key: lanes 0 .. c - 1
+        const int32_t nlo = lo + c * step, nhi = lo + (c + 1) * step - 1;
+        lo = nlo < hi ? nlo : hi;
+        hi = nhi < hi ? nhi : hi;
+    }
+    return lo;
 }
 
 // The new directory: old entry p goes to p + (new entries of segments before p), new entry r
@@ -836,15 +935,11 @@ __global__ __launch_bounds__(256) void k_ct_dmerge(CtJobs js) {
     const int64_t n_old = J.cnt->n_dir, n_new = J.cnt->n_new_dir;
     for (int64_t c0 = (int64_t)blockIdx.x * 256; c0 < n_old; c0 += (int64_t)gridDim.x * 256) {
         const int64_t t = c0 + threadIdx.x;
-        if (threadIdx.x < 2) {  // new entries whose segment lies before c0 / before the chunk's end
-            const int64_t key = threadIdx.x == 0 ? c0 : (c0 + 256 < n_old ? c0 + 256 : n_old);
-            int64_t lo = 0, hi = n_new;
-            while (lo < hi) {
-                const int64_t mid = (lo + hi) >> 1;
-                if (J.edir_pos[mid] < key) lo = mid + 1;
-                else hi = mid;
-            }
-            s_lo[threadIdx.x] = (int32_t)lo;
+        if (threadIdx.x < 128) {  // new entries whose segment lies before c0 / before the chunk's end
+            const int wv = threadIdx.x >> 6;  // wave 0: c0, wave 1: the chunk's end
+            const int64_t key = wv == 0 ? c0 : (c0 + 256 < n_old ? c0 + 256 : n_old);
+            const int32_t lo = wave_lower_bound(J.edir_pos, (int32_t)n_new, key);
+            if ((threadIdx.x & 63) == 0) s_lo[wv] = lo;
         }
         __syncthreads();
         const int32_t lo_a = s_lo[0], lo_b = s_lo[1];
@@ -1070,11 +1165,27 @@ __global__ __launch_bounds__(256) void k_ct_lgroup(CtJobs js) {
 }
 
 // one workgroup a tree: the levels above level 3, then the counts, the seed rows, the indexed
-// count and the spread
+// count and the spread.  Level 3 and everything above it fit in LDS for the trees the rounds
+// grow (a level's boxes are then read from LDS, not back from global memory after the level
+// below was stored and fenced); larger ones take the same steps in global memory.
+template <int D>
+constexpr int ct_level_lds_nodes() { return 98304 / (8 * D + 4); }  // 96 KiB of boxes and metas
 template <int D>
 __global__ __launch_bounds__(kCtLevelThreads) void k_ct_levels(CtJobs js) {
+    constexpr int kW = 2 * D;  // floats a box
+    constexpr int kNodes = ct_level_lds_nodes<D>();
+    __shared__ float s_box[kNodes * kW];
+    __shared__ uint32_t s_meta[kNodes];
     const CtJob J = CT_JOB(js);  // by value: the fields stay in registers across the stores
     const int t = threadIdx.x;
+    // the seed rows first: independent of the levels, so their loads overlap the levels' work
+    for (int it = t; it < kCtHull * D; it += kCtLevelThreads) {
+        const int h = it / D, k = it - h * D;
+        const unsigned long long key = J.hull_keys[h];
+        const int64_t row = (int64_t)(uint32_t)key;
+        J.hull_pts[it] = key ? J.pts[row * D + k] : 0.0;
+        if (k == 0) J.hull_ids[h] = key ? (int32_t)row + 1 : 0;
+    }
     const int64_t n1 = (int64_t)J.cnt->n_dir + J.cnt->n_new_dir;
     // levels 1 and 2 were grouped by k_ct_lflags / k_ct_lgroup into levels 2 and 3
     int64_t ls = 0, n = n1;
@@ -1084,48 +1195,59 @@ __global__ __launch_bounds__(kCtLevelThreads) void k_ct_levels(CtJobs js) {
     }
     // above level 3: runs of 8 (boxes high in the tree prune little; what counts is how few
     // levels a walk descends)
+    const int64_t lds0 = ls;  // the first node in LDS (level 3's)
+    const bool in_lds = n + (n + 6) / 7 + kCtMaxLevels <= kNodes;
+    if (in_lds) {
+        for (int64_t w = t; w < n * kW; w += kCtLevelThreads) s_box[w] = J.nbox[lds0 * kW + w];
+        for (int64_t w = t; w < n; w += kCtLevelThreads) s_meta[w] = J.nmeta[lds0 + w];
+        __syncthreads();
+    }
     while (n > 1) {
         const int64_t nG = (n + 7) / 8;
         for (int64_t g = t; g < nG; g += kCtLevelThreads) {
             const int64_t first = ls + 8 * g;
             const int len = n - 8 * g < 8 ? (int)(n - 8 * g) : 8;
+            const float *src = in_lds ? s_box + (first - lds0) * kW : J.nbox + first * kW;
             float lo[D], nhi[D];  // (lo, -hi) pairs: the union is a minimum of both
 #pragma unroll
             for (int q = 0; q < D; ++q) {
-                lo[q] = J.nbox[first * 2 * D + 2 * q];
-                nhi[q] = J.nbox[first * 2 * D + 2 * q + 1];
+                lo[q] = src[2 * q];
+                nhi[q] = src[2 * q + 1];
             }
             for (int u = 1; u < len; ++u)
 #pragma unroll
                 for (int q = 0; q < D; ++q) {
-                    lo[q] = fminf(lo[q], J.nbox[(first + u) * 2 * D + 2 * q]);
-                    nhi[q] = fminf(nhi[q], J.nbox[(first + u) * 2 * D + 2 * q + 1]);
+                    lo[q] = fminf(lo[q], src[u * kW + 2 * q]);
+                    nhi[q] = fminf(nhi[q], src[u * kW + 2 * q + 1]);
                 }
             const int64_t P = ls + n + g;
 #pragma unroll
             for (int q = 0; q < D; ++q) {
-                J.nbox[P * 2 * D + 2 * q] = lo[q];
-                J.nbox[P * 2 * D + 2 * q + 1] = nhi[q];
+                J.nbox[P * kW + 2 * q] = lo[q];
+                J.nbox[P * kW + 2 * q + 1] = nhi[q];
             }
-            J.nmeta[P] = inner_code(first, len);
+            const uint32_t meta = inner_code(first, len);
+            J.nmeta[P] = meta;
+            if (in_lds) {
+#pragma unroll
+                for (int q = 0; q < D; ++q) {
+                    s_box[(P - lds0) * kW + 2 * q] = lo[q];
+                    s_box[(P - lds0) * kW + 2 * q + 1] = nhi[q];
+                }
+                s_meta[P - lds0] = meta;
+            }
         }
-        __threadfence_block();
+        if (!in_lds) __threadfence_block();
         __syncthreads();
         ls += n;
         n = nG;
     }
-    for (int it = t; it < kCtHull * D; it += kCtLevelThreads) {
-        const int h = it / D, k = it - h * D;
-        const unsigned long long key = J.hull_keys[h];
-        const int64_t row = (int64_t)(uint32_t)key;
-        J.hull_pts[it] = key ? J.pts[row * D + k] : 0.0;
-        if (k == 0) J.hull_ids[h] = key ? (int32_t)row + 1 : 0;
-    }
     __syncthreads();
     if (t < 8) {  // the walk's first entries: the root's children, or the root when it is a leaf
-        const uint32_t rm = J.nmeta[ls];
+        auto meta_of = [&](int64_t i) { return in_lds && i >= lds0 ? s_meta[i - lds0] : J.nmeta[i]; };
+        const uint32_t rm = meta_of(ls);
         const int nc = (rm & kCtLeafBit) ? 1 : (int)((rm >> 28) & 7u) + 1;
-        if (t < nc) J.cnt->top[t] = (rm & kCtLeafBit) ? rm : J.nmeta[(int64_t)(rm & 0x0fffffffu) + t];
+        if (t < nc) J.cnt->top[t] = (rm & kCtLeafBit) ? rm : meta_of((int64_t)(rm & 0x0fffffffu) + t);
         if (t == 0) J.cnt->n_top = nc;
     }
     if (t != 0) return;
@@ -1977,8 +2099,10 @@ void launch_ct_jobs(const CtJob *d_jobs, const CtJob *h_jobs, int32_t n, int32_t
         hipLaunchKernelGGL(k_ct_segments, dim3(1, yn), dim3(kCtSegThreads), 0, stream, js);
         hipLaunchKernelGGL(by_d(k_ct_apply<3>, k_ct_apply<7>, k_ct_apply<15>), dim3(b256, yn), dim3(256), 0, stream, js);
         hip_check(hipGetLastError(), "k_ct_apply");
-        // the split elements: at most 9 a new point, a thread each
-        const unsigned bsplit = (unsigned)((mb * (kCtCap + 1) + 255) / 256);
+        // the split elements: at most 9 a new point, a thread each, in chunks of 256 over a grid
+        // of twice the new points' (rounds split ~1-2 new points' worth of elements a new point:
+        // a grid for the bound of 9 left most of its workgroups with nothing but their dispatch)
+        const unsigned bsplit = (unsigned)std::min<int64_t>((mb * (kCtCap + 1) + 255) / 256, 2 * (int64_t)b256);
         hipLaunchKernelGGL(k_ct_split_flags, dim3(b256, yn), dim3(256), 0, stream, js);
         hipLaunchKernelGGL(k_ct_split_scan, dim3(1, yn), dim3(kCtScanThreads), 0, stream, js);
         hipLaunchKernelGGL(by_d(k_ct_split_fill<3>, k_ct_split_fill<7>, k_ct_split_fill<15>), dim3(bsplit, yn),
@@ -1986,8 +2110,9 @@ void launch_ct_jobs(const CtJob *d_jobs, const CtJob *h_jobs, int32_t n, int32_t
         hip_check(hipGetLastError(), "k_ct_split_fill");
     }
     // the directory (at most the indexed points' count of entries, ~1/5 of them in practice)
+    // (a workgroup a chunk of 256 entries when a tree has ~1/4 as many entries as points)
     hipLaunchKernelGGL(by_d(k_ct_dmerge<3>, k_ct_dmerge<7>, k_ct_dmerge<15>),
-                       dim3((unsigned)std::max<int64_t>(1, (max_n + 2047) / 2048), yn), dim3(256), 0, stream, js);
+                       dim3((unsigned)std::max<int64_t>(1, (max_n + 1023) / 1024), yn), dim3(256), 0, stream, js);
     hip_check(hipGetLastError(), "k_ct_dmerge");
     const unsigned tiles = (unsigned)std::max<int64_t>(1, (max_n + kCtL1Tile - 1) / kCtL1Tile);
     // levels 1 and 2 over many workgroups (level 2 has at most half level 1's nodes)
