@@ -158,6 +158,12 @@ public:
     // current one; true when it changed (the index must then be rebuilt).  prepare() calls it;
     // calling it beforehand (mpt_rrt_set_nn) keeps the upload out of the rounds.
     bool set_plan(const double *lo, const double *hi, int32_t spatial);
+    // is the code plan the one for these ranges (set_plan would change nothing)?
+    bool plan_current(const double *lo, const double *hi) const {
+        bool same = plan_set;
+        for (int j = 0; j < dim && same; ++j) same = plan_lo[j] == lo[j] && plan_hi[j] == hi[j];
+        return same;
+    }
     ~CellTree();
 
 private:

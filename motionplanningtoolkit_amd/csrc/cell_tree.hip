@@ -79,15 +79,21 @@ __device__ __forceinline__ void ct_code(const CtPlan &P, const double (&x)[D], u
         q[j] = u <= 0.0 ? 0u : (u >= (double)m ? m : (uint32_t)u);
     }
     // level by level (MSB first): the level's bits of the dims that have one, gathered into a
-    // word and shifted in together (the plan's dim / bit order)
+    // word and shifted in together (the plan's dim / bit order).  The plan is the same for
+    // every lane: its bit counts go to scalar registers, so which dims a level takes and the
+    // shift amounts are scalar work, and the vector work is the bits themselves.
+    int nb[D];
+#pragma unroll
+    for (int j = 0; j < D; ++j) nb[j] = __builtin_amdgcn_readfirstlane(P.nb[j]);
+    const int bmax = __builtin_amdgcn_readfirstlane(P.bmax);
     h = 0;
     l = 0;
-    for (int lev = P.bmax - 1; lev >= 0; --lev) {
+    for (int lev = bmax - 1; lev >= 0; --lev) {
         uint32_t w = 0;
         int c = 0;
 #pragma unroll
         for (int j = 0; j < D; ++j)
-            if (P.nb[j] > lev) {
+            if (nb[j] > lev) {
                 w = (w << 1) | ((q[j] >> lev) & 1u);
                 ++c;
             }
@@ -97,7 +103,7 @@ __device__ __forceinline__ void ct_code(const CtPlan &P, const double (&x)[D], u
 }
 
 // Seed slots (cell_tree.h kCtHull): lane h of a wave scores slot h over the wave's 64 points
-// (staged in LDS: every lane reads the same point at once, a broadcast) and offers its best to
+// (staged in LDS: every lane reads the same point at once) and offers its best to
 // the tree's slot with one 64-bit atomicMax of (score as an ordered float key << 32 | row).
 // Rows of a wave are consecutive (row0 + lane).  The float rounding of the score only decides
 // which near-tie becomes the seed; any point is a valid seed.
@@ -111,22 +117,20 @@ __device__ __forceinline__ void hull_offer(const CtPlan &P, const double (&x)[D]
     const uint64_t lm = __ballot(live);
     __builtin_amdgcn_wave_barrier();
     if (lane < P.n_hull) {
+        // one form for every kind (no divergence between the lanes' kinds): c0 x[i0] + c1 x[i1]
+        // + c2 x[i2]; kind 1 / 2 is -1 / +1 times x[hdim] (the other terms 0 x[hdim])
         const int kind = P.hkind[lane], dm = P.hdim[lane];
-        const float u0 = P.hdir[lane][0], u1 = P.hdir[lane][1], u2 = P.hdir[lane][2];
+        const bool dir = kind == 0;
+        const int i0 = dir ? 0 : dm, i1 = dir ? (D > 1 ? 1 : 0) : dm, i2 = dir ? (D > 2 ? 2 : 0) : dm;
+        const double c0 = dir ? (double)P.hdir[lane][0] : (kind == 1 ? -1.0 : 1.0);
+        const double c1 = dir && D > 1 ? (double)P.hdir[lane][1] : 0.0;
+        const double c2 = dir && D > 2 ? (double)P.hdir[lane][2] : 0.0;
         unsigned long long best = 0;
         // every point of the wave, unrolled by 8 so the LDS reads overlap (a loop over the live
         // mask's bits waited out each point's reads); dead points score key 0
 #pragma unroll 8
         for (int j = 0; j < 64; ++j) {
-            double v;
-            if (kind == 0) {
-                v = (double)u0 * s_rows[j][0];
-                if (D > 1) v += (double)u1 * s_rows[j][D > 1 ? 1 : 0];
-                if (D > 2) v += (double)u2 * s_rows[j][D > 2 ? 2 : 0];
-            } else {
-                const double xv = s_rows[j][dm];
-                v = kind == 1 ? -xv : xv;
-            }
+            const double v = c0 * s_rows[j][i0] + c1 * s_rows[j][i1] + c2 * s_rows[j][i2];
             const uint32_t b = __float_as_uint((float)v);
             const uint32_t key = (b & 0x80000000u) ? ~b : (b | 0x80000000u);
             const unsigned long long k64 = ((unsigned long long)key << 32) | (uint32_t)(row0 + j);
@@ -182,15 +186,20 @@ template <int D>
 __global__ __launch_bounds__(64 * kCtWaves) void k_ct_ncodes(CtJobs js) {
     __shared__ CtPlan s_plan;
     __shared__ double s_rows[kCtWaves][64][D];
+    __shared__ unsigned long long s_keys[kCtHull], s_ibox[6];  // the workgroup's offers, then one global atomic each
     const CtJob J = CT_JOB(js);  // by value: the fields stay in registers across the stores
+    // the plan's loads in flight with the counts' (a workgroup past the new points still exits
+    // before its first barrier)
+    for (int w = threadIdx.x; w < (int)(sizeof(CtPlan) / 4); w += blockDim.x)
+        reinterpret_cast<uint32_t *>(&s_plan)[w] = reinterpret_cast<const uint32_t *>(J.plan)[w];
+    if (threadIdx.x < kCtHull) s_keys[threadIdx.x] = 0ull;
+    if (threadIdx.x < 6) s_ibox[threadIdx.x] = threadIdx.x < 3 ? ~0ull : 0ull;
     const int64_t base = J.cnt->nidx, mraw = *J.T.n_dev - base;
     if ((mraw > kCtSeg || mraw > J.mb) && blockIdx.x == 0 && threadIdx.x == 0 && J.err)
         atomicAdd(J.err, 1ull);  // the host's bound broken
     const int64_t m = ct_new_count(J);
     const int i = (int)blockIdx.x * (int)blockDim.x + (int)threadIdx.x;
     if ((int64_t)blockIdx.x * blockDim.x >= m) return;  // block-uniform
-    for (int w = threadIdx.x; w < (int)(sizeof(CtPlan) / 4); w += blockDim.x)
-        reinterpret_cast<uint32_t *>(&s_plan)[w] = reinterpret_cast<const uint32_t *>(J.plan)[w];
     __syncthreads();
     const bool live = i < m;
     double x[D];
@@ -218,11 +227,19 @@ __global__ __launch_bounds__(64 * kCtWaves) void k_ct_ncodes(CtJobs js) {
             mx = omx > mx ? omx : mx;
         }
         if ((threadIdx.x & 63) == 0) {
-            atomicMin(J.ibox + j, mn);
-            atomicMax(J.ibox + kCtMaxDim + j, mx);
+            atomicMin(s_ibox + j, mn);
+            atomicMax(s_ibox + 3 + j, mx);
         }
     }
-    hull_offer<D>(s_plan, x, live, base + (i & ~63), s_rows[threadIdx.x >> 6], J.hull_keys);
+    hull_offer<D>(s_plan, x, live, base + (i & ~63), s_rows[threadIdx.x >> 6], s_keys);
+    // one global atomic a slot a workgroup (not one a wave: the tree's offers to a slot are
+    // serialised at one address)
+    __syncthreads();
+    if (threadIdx.x < kCtHull && s_keys[threadIdx.x]) atomicMax(J.hull_keys + threadIdx.x, s_keys[threadIdx.x]);
+    if (threadIdx.x < (D < 3 ? D : 3)) {
+        atomicMin(J.ibox + threadIdx.x, s_ibox[threadIdx.x]);
+        atomicMax(J.ibox + kCtMaxDim + threadIdx.x, s_ibox[3 + threadIdx.x]);
+    }
 }
 
 // (code, row) compare-exchange by selects (no divergent branches)
@@ -986,7 +1003,6 @@ __global__ __launch_bounds__(256) void k_ct_dmerge(CtJobs js) {
 // first directory entry's start), or, when that would leave more than half as many groups as
 // nodes or more levels than the walk's stack allows, runs of 8.  Above level 3 one workgroup a
 // tree (k_ct_levels) groups runs of 8, then copies the seeds and closes the round's counts.
-constexpr int kCtLevelThreads = 1024;
 constexpr int kCtMaxLevels = 10;  // the walk's stack bound (ct_walk kStack); runs of 8 reach it below 8^9 entries
 constexpr int kCtL1Per = kCtL1Tile / 256;  // level-1 entries a thread of k_ct_lflags / k_ct_lgroup
 
@@ -1044,8 +1060,11 @@ __global__ __launch_bounds__(256) void k_ct_lflags(CtJobs js) {
     const CtLevel<LEV> V = ct_level<LEV>(J);
     const int64_t n = V.n;
     const uint64_t *__restrict__ code = V.code;
-    const int64_t t0 = (int64_t)blockIdx.x * kCtL1Tile;
-    if (n <= 1 || t0 >= n) return;  // block-uniform
+    if (n <= 1) return;  // block-uniform
+    // tiles over a grid sized by the level's typical size (a grid for the host's bound of it
+    // dispatched mostly empty workgroups)
+    for (int64_t tile = blockIdx.x; tile * kCtL1Tile < n; tile += gridDim.x) {
+    const int64_t t0 = tile * kCtL1Tile;
     const int64_t a0 = t0 - kCtHalo;  // s_a[v] = a[a0 + v]
     for (int v = threadIdx.x; v < kCtL1Tile + 2 * kCtHalo; v += 256) {
         const int64_t u = a0 + v;
@@ -1070,7 +1089,9 @@ __global__ __launch_bounds__(256) void k_ct_lflags(CtJobs js) {
     }
     int tot;
     (void)ct_block_scan(c, s_w, 256, tot);
-    if (threadIdx.x == 0) V.lcount[blockIdx.x] = tot;
+    if (threadIdx.x == 0) V.lcount[tile] = tot;
+    __syncthreads();  // s_a, s_w reused by the next tile
+    }
 }
 
 // level 2: each tile's groups, numbered after the tiles before it.  The tile's boxes and flags
@@ -1085,15 +1106,16 @@ __global__ __launch_bounds__(256) void k_ct_lgroup(CtJobs js) {
     __shared__ uint8_t s_f[kSpan];
     const CtLevel<LEV> V = ct_level<LEV>(J);
     const int64_t n = V.n, base = V.base;
-    const int64_t t0 = (int64_t)blockIdx.x * kCtL1Tile;
-    if (n <= 1 || t0 >= n) return;  // block-uniform
+    if (n <= 1) return;  // block-uniform
     const int64_t tiles = (n + kCtL1Tile - 1) / kCtL1Tile;
+    for (int64_t tile = blockIdx.x; tile < tiles; tile += gridDim.x) {  // (k_ct_lflags' grid)
+    const int64_t t0 = tile * kCtL1Tile;
     if (threadIdx.x < 64) {  // the groups of all tiles and of the tiles before this one
         int64_t all = 0, before = 0;
         for (int64_t b = threadIdx.x; b < tiles; b += 64) {
             const int32_t v = V.lcount[b];
             all += v;
-            before += b < (int64_t)blockIdx.x ? v : 0;
+            before += b < tile ? v : 0;
         }
 #pragma unroll
         for (int off = 32; off > 0; off >>= 1) {
@@ -1112,7 +1134,7 @@ __global__ __launch_bounds__(256) void k_ct_lgroup(CtJobs js) {
     __syncthreads();
     const int64_t G = s_sum[0];
     const bool fixed = ct_fixed(n, G, LEV);
-    if (blockIdx.x == 0 && threadIdx.x == 0) (LEV == 1 ? J.cnt->n_l2 : J.cnt->n_l3) = (int32_t)(fixed ? (n + 7) / 8 : G);
+    if (tile == 0 && threadIdx.x == 0) (LEV == 1 ? J.cnt->n_l2 : J.cnt->n_l3) = (int32_t)(fixed ? (n + 7) / 8 : G);
     const int e0 = threadIdx.x * kCtL1Per;  // this thread's entries [e0, e0 + kCtL1Per) of the tile
     int f[kCtL1Per], c = 0;
 #pragma unroll
@@ -1162,24 +1184,24 @@ __global__ __launch_bounds__(256) void k_ct_lgroup(CtJobs js) {
         J.ucode[2 * P + 1] = V.code[2 * i + 1];
         ++g;
     }
+    __syncthreads();  // s_sum, s_box, s_f reused by the next tile
+    }
 }
 
 // one workgroup a tree: the levels above level 3, then the counts, the seed rows, the indexed
-// count and the spread.  Level 3 and everything above it fit in LDS for the trees the rounds
-// grow (a level's boxes are then read from LDS, not back from global memory after the level
-// below was stored and fenced); larger ones take the same steps in global memory.
-template <int D>
-constexpr int ct_level_lds_nodes() { return 98304 / (8 * D + 4); }  // 96 KiB of boxes and metas
+// count and the spread.  Round 5, measured and not kept: the upper levels' boxes in LDS (14.4
+// us a round at 32 seeds either way); this work run by the last of k_ct_lgroup<2>'s workgroups
+// to finish a tree (a ticket: one launch less), which made k_ct_lgroup<2> 12.7 -> 58 us at 32
+// seeds and 39 -> 449 us at 256 -- every workgroup's device-scope fence before its ticket
+// writes back its XCD's L2.
+constexpr int kCtLevelThreads = 1024;
 template <int D>
 __global__ __launch_bounds__(kCtLevelThreads) void k_ct_levels(CtJobs js) {
-    constexpr int kW = 2 * D;  // floats a box
-    constexpr int kNodes = ct_level_lds_nodes<D>();
-    __shared__ float s_box[kNodes * kW];
-    __shared__ uint32_t s_meta[kNodes];
+    constexpr int NT = kCtLevelThreads;
     const CtJob J = CT_JOB(js);  // by value: the fields stay in registers across the stores
     const int t = threadIdx.x;
     // the seed rows first: independent of the levels, so their loads overlap the levels' work
-    for (int it = t; it < kCtHull * D; it += kCtLevelThreads) {
+    for (int it = t; it < kCtHull * D; it += NT) {
         const int h = it / D, k = it - h * D;
         const unsigned long long key = J.hull_keys[h];
         const int64_t row = (int64_t)(uint32_t)key;
@@ -1195,59 +1217,41 @@ __global__ __launch_bounds__(kCtLevelThreads) void k_ct_levels(CtJobs js) {
     }
     // above level 3: runs of 8 (boxes high in the tree prune little; what counts is how few
     // levels a walk descends)
-    const int64_t lds0 = ls;  // the first node in LDS (level 3's)
-    const bool in_lds = n + (n + 6) / 7 + kCtMaxLevels <= kNodes;
-    if (in_lds) {
-        for (int64_t w = t; w < n * kW; w += kCtLevelThreads) s_box[w] = J.nbox[lds0 * kW + w];
-        for (int64_t w = t; w < n; w += kCtLevelThreads) s_meta[w] = J.nmeta[lds0 + w];
-        __syncthreads();
-    }
     while (n > 1) {
         const int64_t nG = (n + 7) / 8;
-        for (int64_t g = t; g < nG; g += kCtLevelThreads) {
+        for (int64_t g = t; g < nG; g += NT) {
             const int64_t first = ls + 8 * g;
             const int len = n - 8 * g < 8 ? (int)(n - 8 * g) : 8;
-            const float *src = in_lds ? s_box + (first - lds0) * kW : J.nbox + first * kW;
             float lo[D], nhi[D];  // (lo, -hi) pairs: the union is a minimum of both
 #pragma unroll
             for (int q = 0; q < D; ++q) {
-                lo[q] = src[2 * q];
-                nhi[q] = src[2 * q + 1];
+                lo[q] = J.nbox[first * 2 * D + 2 * q];
+                nhi[q] = J.nbox[first * 2 * D + 2 * q + 1];
             }
             for (int u = 1; u < len; ++u)
 #pragma unroll
                 for (int q = 0; q < D; ++q) {
-                    lo[q] = fminf(lo[q], src[u * kW + 2 * q]);
-                    nhi[q] = fminf(nhi[q], src[u * kW + 2 * q + 1]);
+                    lo[q] = fminf(lo[q], J.nbox[(first + u) * 2 * D + 2 * q]);
+                    nhi[q] = fminf(nhi[q], J.nbox[(first + u) * 2 * D + 2 * q + 1]);
                 }
             const int64_t P = ls + n + g;
 #pragma unroll
             for (int q = 0; q < D; ++q) {
-                J.nbox[P * kW + 2 * q] = lo[q];
-                J.nbox[P * kW + 2 * q + 1] = nhi[q];
+                J.nbox[P * 2 * D + 2 * q] = lo[q];
+                J.nbox[P * 2 * D + 2 * q + 1] = nhi[q];
             }
-            const uint32_t meta = inner_code(first, len);
-            J.nmeta[P] = meta;
-            if (in_lds) {
-#pragma unroll
-                for (int q = 0; q < D; ++q) {
-                    s_box[(P - lds0) * kW + 2 * q] = lo[q];
-                    s_box[(P - lds0) * kW + 2 * q + 1] = nhi[q];
-                }
-                s_meta[P - lds0] = meta;
-            }
+            J.nmeta[P] = inner_code(first, len);
         }
-        if (!in_lds) __threadfence_block();
+        __threadfence_block();
         __syncthreads();
         ls += n;
         n = nG;
     }
     __syncthreads();
     if (t < 8) {  // the walk's first entries: the root's children, or the root when it is a leaf
-        auto meta_of = [&](int64_t i) { return in_lds && i >= lds0 ? s_meta[i - lds0] : J.nmeta[i]; };
-        const uint32_t rm = meta_of(ls);
+        const uint32_t rm = J.nmeta[ls];
         const int nc = (rm & kCtLeafBit) ? 1 : (int)((rm >> 28) & 7u) + 1;
-        if (t < nc) J.cnt->top[t] = (rm & kCtLeafBit) ? rm : meta_of((int64_t)(rm & 0x0fffffffu) + t);
+        if (t < nc) J.cnt->top[t] = (rm & kCtLeafBit) ? rm : J.nmeta[(int64_t)(rm & 0x0fffffffu) + t];
         if (t == 0) J.cnt->n_top = nc;
     }
     if (t != 0) return;
@@ -2114,12 +2118,14 @@ void launch_ct_jobs(const CtJob *d_jobs, const CtJob *h_jobs, int32_t n, int32_t
     hipLaunchKernelGGL(by_d(k_ct_dmerge<3>, k_ct_dmerge<7>, k_ct_dmerge<15>),
                        dim3((unsigned)std::max<int64_t>(1, (max_n + 1023) / 1024), yn), dim3(256), 0, stream, js);
     hip_check(hipGetLastError(), "k_ct_dmerge");
-    const unsigned tiles = (unsigned)std::max<int64_t>(1, (max_n + kCtL1Tile - 1) / kCtL1Tile);
-    // levels 1 and 2 over many workgroups (level 2 has at most half level 1's nodes)
+    // levels 1 and 2 over many workgroups, tiles in a grid-stride loop over a grid for a
+    // quarter of the host's bound (a tree has ~1/5 as many directory entries as points, level 2
+    // ~1/5 of those: the bound's grids dispatched ~5x as many workgroups as had a tile)
+    const unsigned tiles = (unsigned)std::max<int64_t>(1, (max_n / 4 + kCtL1Tile - 1) / kCtL1Tile);
     hipLaunchKernelGGL(k_ct_lflags<1>, dim3(tiles, yn), dim3(256), 0, stream, js);
     hipLaunchKernelGGL(by_d(k_ct_lgroup<3, 1>, k_ct_lgroup<7, 1>, k_ct_lgroup<15, 1>), dim3(tiles, yn), dim3(256), 0,
                        stream, js);
-    const unsigned tiles2 = (tiles + 1) / 2;
+    const unsigned tiles2 = (tiles + 3) / 4;
     hipLaunchKernelGGL(k_ct_lflags<2>, dim3(tiles2, yn), dim3(256), 0, stream, js);
     hipLaunchKernelGGL(by_d(k_ct_lgroup<3, 2>, k_ct_lgroup<7, 2>, k_ct_lgroup<15, 2>), dim3(tiles2, yn), dim3(256), 0,
                        stream, js);

@@ -583,15 +583,56 @@ __global__ __launch_bounds__(256) void k_steer_jobs(EngineParams p, const Engine
 }
 
 // k_append_commit for engine blockIdx.y over its K joint verdicts
+// kOvf: ov / ticket carry the joint collide's deferred overflow re-run, as k_append_commit
+// takes it (the last block then appends every engine's extensions in order).  The fused walk's
+// registers cost the kernel its occupancy (a 256-seed round's append 49 -> 63 us), so only
+// small joint rounds, whose append is a few latency-bound waves, take it (the launch it saves
+// is ~5 us); larger ones keep the k_overflow launch.
+template <bool kOvf>
 __global__ __launch_bounds__(256) void k_append_jobs(const EngineJob *__restrict__ jobs,
                                                      const uint8_t *__restrict__ verdict, int32_t K, int32_t d,
-                                                     const double *__restrict__ ends, const int32_t *__restrict__ nn) {
+                                                     const double *__restrict__ ends, const int32_t *__restrict__ nn,
+                                                     OvfDefer ov, uint32_t *__restrict__ ticket) {
     __shared__ int32_t s_wave[4], s_ones[4];
+    __shared__ int32_t s_last;
     const int job = blockIdx.y;
     const EngineJob &J = jobs[job];
     const int64_t e0 = (int64_t)job * K;
     const uint8_t *vj = verdict + e0;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    if (kOvf && ov.n_ovf) {
+        const uint32_t n_ovf = __hip_atomic_load(ov.n_ovf, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (n_ovf > 0) {  // grid-uniform
+            __shared__ int32_t s_stk[4][kStackDepth];
+            const bool shared_edges = ov.w.pose_edge != nullptr || ov.w.L > 1 || ov.w.pmax > 1;
+            uint32_t nu = 0, nc = 0, nnod = 0, ns = 0;
+            const uint32_t nblk = gridDim.x * gridDim.y, blk = blockIdx.y * gridDim.x + blockIdx.x;
+            for (uint32_t i = blk * 4 + wave; i < n_ovf; i += nblk * 4)
+                collide_unit(ov.env, ov.env.nodes, ov.env.n_nodes, ov.links, ov.w, ov.ovf_list[i], s_stk[wave], lane,
+                             shared_edges, nc, nnod, ns, nu);
+            __threadfence();
+            __syncthreads();
+            if (tid == 0) s_last = atomicAdd(ticket, 1u) == nblk - 1;
+            __syncthreads();
+            if (!s_last) return;  // block-uniform
+            __threadfence();
+            for (int32_t j = 0; j < (int32_t)gridDim.y; ++j) {  // every engine, every extension, in order
+                const EngineJob &Jj = jobs[j];
+                const int64_t n0 = Jj.n_dev[1];
+                int64_t before = 0;
+                for (int64_t k0 = 0; k0 < K; k0 += 256) {
+                    int64_t tot;
+                    append_commit_tail(before, 0, verdict + (int64_t)j * K, k0, K, d, ends + (int64_t)j * K * d,
+                                       nn + (int64_t)j * K, n0, Jj.cap, Jj.nodes, Jj.parents, s_wave, &tot);
+                    before = tot;
+                    __syncthreads();  // s_wave is reused
+                }
+                if (tid == 0) append_commit_counters(before, n0, Jj.cap, K, Jj.n_dev, Jj.counters);
+            }
+            if (tid == 0) *ticket = 0u;  // for the next round's launch (stream-ordered)
+            return;
+        }
+    }
     // the engine's valid extensions before this block (K is a multiple of 16: the launcher checks)
     const uint4 *v4 = reinterpret_cast<const uint4 *>(vj);
     const int64_t nv4 = (int64_t)blockIdx.x * 16;
@@ -953,6 +994,13 @@ struct StepCtx {
 // this round's incremental tree build (a full rebuild when the index is stale or more nodes
 // were appended since its last build than one round's merge takes: the host's bound, which the
 // build's first kernel checks on the device into counters[6])
+// does this round's tree_inc_job launch a full rebuild (CellTree::prepare: a full build, or a
+// new code plan, of more than kCtSeg rows; fewer restart the index inside launch_ct_jobs)?
+bool tree_inc_launches(const mpt_rrt *r) {
+    const bool full = !r->pt_inc_ok || r->pt_grow > kCtSeg || !r->ctree->plan_current(r->p.lo, r->p.hi);
+    return full && r->n_upper > kCtSeg;
+}
+
 CtJob tree_inc_job(mpt_rrt *r, hipStream_t stream, const SpreadOut *spread) {
     const bool full = !r->pt_inc_ok || r->pt_grow > kCtSeg;
     CtJob J = r->ctree->prepare(r->d_nodes, r->n_upper, r->d_n, r->p.d, r->p.lo, r->p.hi, r->grid_gd, full,
@@ -1282,6 +1330,7 @@ struct JointNN {
     uint32_t *j_nlive = nullptr;
     uint64_t buf_id = 0;  // id of the round buffers above (0: none); engines' jv slices carry it
     CollideScratch cs;
+    uint32_t *d_bar = nullptr;  // k_append_jobs' ticket (the deferred overflow re-run)
     // timed joint round: start, sample, build, NN, steer, collide, append
     hipEvent_t st[7] = {};
     bool round_timed = false;
@@ -1477,23 +1526,33 @@ void joint_round(mpt_rrt *const *rs, int32_t n, int32_t K, void *const *streams_
     auto mark = [&](int i) {
         if (timed) hip_check(hipEventRecord(g.st[i], joint), "joint stage event");
     };
+    // the index builds' jobs (a full rebuild issues its code and sort launches in
+    // tree_inc_job: those go after the samples' launch, which applies any truncation) and the
+    // NN jobs.  A round with no full rebuild fills them first and stages all three tables in
+    // one copy (one launch fewer a round).
+    bool rebuilds = false;
+    for (int32_t i = 0; i < n; ++i) rebuilds = rebuilds || tree_inc_launches(rs[i]);
+    auto fill_tree_jobs = [&]() {
+        for (int32_t i = 0; i < n; ++i) {
+            mpt_rrt *r = rs[i];
+            hi[i] = tree_inc_job(r, joint, want[i] ? &spreads[i] : nullptr);
+            CellTreeDev T = r->ctree->dev();
+            T.stats = nullptr;
+            hn[i] = CtNnJob{T, g.j_samples + (int64_t)i * K * d, g.j_nn + (int64_t)i * K, g.j_nnd2 + (int64_t)i * K};
+        }
+    };
+    if (!rebuilds) fill_tree_jobs();
     mark(0);
-    stage_copy(g, slot, 0, b_eng, joint);
+    stage_copy(g, slot, 0, rebuilds ? b_eng : b_eng + b_inc + b_nn, joint);
     const unsigned kb = (unsigned)((K + 255) / 256);
     hipLaunchKernelGGL(k_sample_jobs, dim3(kb, n), dim3(256), 0, joint, p, de, K, g.j_samples, g.j_nlive, n_sub);
     hip_check(hipGetLastError(), "k_sample_jobs");
     mark(1);
     if (timed) hip_check(hipEventRecord(g.b0, joint), "joint b0");
-    // the index builds (a full rebuild issues its code and sort launches here, after the
-    // samples' launch applied any truncation) and the NN jobs
-    for (int32_t i = 0; i < n; ++i) {
-        mpt_rrt *r = rs[i];
-        hi[i] = tree_inc_job(r, joint, want[i] ? &spreads[i] : nullptr);
-        CellTreeDev T = r->ctree->dev();
-        T.stats = nullptr;
-        hn[i] = CtNnJob{T, g.j_samples + (int64_t)i * K * d, g.j_nn + (int64_t)i * K, g.j_nnd2 + (int64_t)i * K};
+    if (rebuilds) {
+        fill_tree_jobs();
+        stage_copy(g, slot, b_eng, b_inc + b_nn, joint);
     }
-    stage_copy(g, slot, b_eng, b_inc + b_nn, joint);
     hip_check(hipEventRecord(g.copied[slot], joint), "jobs copied");
     launch_ct_jobs(di, hi, n, d, joint);
     for (int32_t i = 0; i < n; ++i)
@@ -1515,6 +1574,12 @@ void joint_round(mpt_rrt *const *rs, int32_t n, int32_t K, void *const *streams_
                        g.j_verdict, lv, per_sub);
     hip_check(hipGetLastError(), "k_steer_jobs");
     mark(4);
+    OvfDefer ovf{};
+    const bool fold_ovf = (int64_t)kb * n <= 1024;  // k_append_jobs<true>'s case (its comment)
+    if (fold_ovf && !g.d_bar) {
+        hip_check(hipMalloc(&g.d_bar, sizeof(uint32_t)), "alloc append ticket");
+        hip_check(hipMemsetAsync(g.d_bar, 0, sizeof(uint32_t), joint), "zero append ticket");
+    }
     for (int32_t b = 0; b < n_sub; ++b) {
         const int64_t e0 = (int64_t)b * per_sub * K;
         const int32_t ne = std::min(per_sub, n - b * per_sub);
@@ -1531,10 +1596,14 @@ void joint_round(mpt_rrt *const *rs, int32_t n, int32_t K, void *const *streams_
         cw.n_live = g.j_nlive + b;
         cw.unit_rt = g.j_rt + e0 * units * 12;
         cw.unit_tmask = tm ? tm + e0 * units : nullptr;
-        launch_collide_split(a->env, a->d_links, a->max_clusters, cw, g.cs, joint, nullptr, nullptr);
+        // a small round's last batch moves its overflow re-run into the append launch (when it
+        // ran in one chunk)
+        launch_collide_split(a->env, a->d_links, a->max_clusters, cw, g.cs, joint, nullptr,
+                             b == n_sub - 1 && fold_ovf ? &ovf : nullptr);
     }
     mark(5);
-    hipLaunchKernelGGL(k_append_jobs, dim3(kb, n), dim3(256), 0, joint, de, g.j_verdict, K, d, g.j_ends, g.j_nn);
+    hipLaunchKernelGGL(fold_ovf ? k_append_jobs<true> : k_append_jobs<false>, dim3(kb, n), dim3(256), 0, joint, de,
+                       g.j_verdict, K, d, g.j_ends, g.j_nn, ovf, g.d_bar);
     hip_check(hipGetLastError(), "k_append_jobs");
     mark(6);
     g.timed = timed;

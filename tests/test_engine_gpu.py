@@ -214,6 +214,54 @@ def test_engine_round_with_pair_overflow(mpt_gpu, oracle):
     assert v.sum() > 0
 
 
+def test_joint_rounds_with_pair_overflow(mpt_gpu):
+    """The overflow scene above in joint rounds: the joint collide's overflowed units are
+    re-run inside the joint append launch (k_append_jobs takes k_overflow's work, and its last
+    block appends every engine's extensions in order).  Three engines must grow exactly the
+    trees they grow alone, where the solo rounds count their fused re-runs."""
+    import dataclasses
+
+    import torch
+
+    base = scenes.blimp_scenario("all")
+    ranges = base.ranges.copy()
+    ranges[:3] = [-3.0, 3.0]
+    sc = dataclasses.replace(base, env_tris=base.agent_tris.copy(), env_tf=scenes.IDENTITY_TF.copy(), ranges=ranges)
+    env = mpt_gpu.Environment(sc.env_tris, sc.env_tf)
+    ag = mpt_gpu.AgentMesh(sc.agent_tris)
+    K, rounds, seeds, n0 = 256, 3, (71, 72, 73), 300
+
+    def grow(joint):
+        engs = []
+        for s in seeds:
+            e = mpt_gpu.RRTEngine(env, ag, sc.kind, sc.prm, sc.ranges, sc.steer_dt, sc.cc_dt, n0 + rounds * K, s)
+            e.add_nodes(np.random.default_rng(s).uniform(sc.ranges[:, 0], sc.ranges[:, 1], size=(n0, sc.dim)))
+            e.set_nn("tree")
+            engs.append(e)
+        reruns = 0
+        js = torch.cuda.Stream()
+        for _ in range(rounds):
+            if joint:
+                mpt_gpu.step_many(engs, K, [js] * len(engs), js)
+            else:
+                for e in engs:
+                    e.collide_stats(True)
+                    e.step(K)
+                    reruns += e.collide_stats(False)["fused_reruns"]
+        torch.cuda.synchronize()
+        out = [e.read_tree(e.counters()["nodes"]) for e in engs]
+        if joint:
+            mpt_gpu.joint_release(js)
+        return out, reruns
+
+    solo, reruns = grow(False)
+    joint, _ = grow(True)
+    assert reruns > 0
+    for (sa, pa), (sb, pb) in zip(solo, joint):
+        assert np.array_equal(bits(sa), bits(sb))
+        assert np.array_equal(pa, pb)
+
+
 @pytest.mark.parametrize("name", ["omni", "blimp", "snake"])
 def test_engine_rounds_fused_collide(mpt_gpu, oracle, name):
     """The same stage-by-stage parity with the fused collision kernel in the round."""
