@@ -527,16 +527,15 @@ __global__ __launch_bounds__(256) void k_cands(EnvDev env, const AgentDev *__res
 // record is fetched while this one computes.  kLds: the env triangles' vertices sit in LDS
 // and the P-side of intersect_Triangle is recomputed from them (tri_collide_verts, bitwise
 // make_env_tri's fields); otherwise the precomputed 384-B records are read (large envs).
-template <bool kLds>
+template <bool kLds, class Get>
 __device__ __forceinline__ void narrow_range(const EnvDev &env, const AgentDev *__restrict__ links,
-                                             const CollideWork &w, const Cand *__restrict__ cands, uint32_t i0,
-                                             uint32_t n, uint32_t stride, const double *__restrict__ s_verts,
-                                             uint32_t &n_sat) {
+                                             const CollideWork &w, Get cand_at, uint32_t i0, uint32_t n,
+                                             uint32_t stride, const double *__restrict__ s_verts, uint32_t &n_sat) {
     Cand next{};
-    if (i0 < n) next = cands[i0];
+    if (i0 < n) next = cand_at(i0);
     for (uint32_t i = i0; i < n; i += stride) {
         const Cand cd = next;
-        if (i + stride < n) next = cands[i + stride];
+        if (i + stride < n) next = cand_at(i + stride);
         int32_t link;
         int64_t slot, edge;
         decode_unit(w, cd.unit, link, slot, edge);
@@ -583,8 +582,10 @@ __device__ __forceinline__ void narrow_range(const EnvDev &env, const AgentDev *
     }
 }
 
-// 256-thread workgroups, one wave per candidate segment: waves [0, n_cwaves) take segment
-// gw; the next kSpillWaves stride the spill list.  A workgroup whose segments hold at least
+// 256-thread workgroups over the candidate segments, 4 a workgroup pooled into one list (one
+// wave a segment before: k_narrow 54.7 -> 46.7 us at 32 seeds, 181 -> 161 us at 256, the room
+// 112 -> 124 M valid ext/s; 8 segments in 512-thread workgroups: config 2 385 -> 374 M, the
+// rest unchanged); the next kSpillWaves waves stride the spill list.  A workgroup whose segments hold at least
 // 4 * n_tris candidates (lds_ok: the env fits) first stages the env triangles' vertices
 // (72 B each) in LDS and recomputes their SAT fields -- below that the staging and the
 // recompute cost more than the 384-B records they save (A/B: blimp.inst, 2.1 candidates
@@ -592,7 +593,8 @@ __device__ __forceinline__ void narrow_range(const EnvDev &env, const AgentDev *
 // k_overflow: the fused walk's registers in this kernel cost a wave per SIMD (158 VGPRs).
 // Not kept: a gate-first pass queueing survivors in LDS and running the SAT on full waves of
 // them (reloaded and re-transformed) -- room narrow 169 -> 181 us, config 2 33 -> 34 us.
-constexpr int kNarrowWaves = 4;
+constexpr int kNarrowWaves = 4;    // k_narrow's workgroup: its 4 segments pooled
+constexpr int kOvfBlockWaves = 4;  // k_overflow's workgroup
 constexpr int kSpillWaves = 256;
 constexpr int kOvfWaves = 64;
 constexpr int kNarrowLdsTris = 1024;  // env triangles staged in LDS up to this count (72 KiB)
@@ -626,14 +628,36 @@ __global__ __launch_bounds__(kNarrowWaves * 64, 4) void k_narrow(EnvDev env, con
         }
     }
     uint32_t n_sat = 0;
-    const Cand *cands = gw < a.n_cwaves ? a.cand + (int64_t)gw * a.cand_cap : a.spill;
-    const uint32_t i0 = gw < a.n_cwaves ? (uint32_t)lane : (uint32_t)(gw - a.n_cwaves) * 64 + lane;
-    const uint32_t n = gw < a.n_cwaves ? cnt : n_spill;
-    const uint32_t stride = gw < a.n_cwaves ? 64u : (uint32_t)kSpillWaves * 64u;
-    if (lds)
-        narrow_range<true>(env, links, w, cands, i0, n, stride, s_verts, n_sat);
-    else
-        narrow_range<false>(env, links, w, cands, i0, n, stride, s_verts, n_sat);
+    const int32_t gw0 = (int32_t)blockIdx.x * kNarrowWaves;  // (n_cwaves is a multiple of kNarrowWaves)
+    if (gw0 < a.n_cwaves) {
+        // the workgroup's kNarrowWaves segments as one list, strided over its threads: a
+        // segment's count follows the headers its k_cands wave happened to take, so at small
+        // batches one long segment held its wave (and the launch) long after the others
+        uint32_t pre[kNarrowWaves + 1];
+        pre[0] = 0;
+#pragma unroll
+        for (int i = 0; i < kNarrowWaves; ++i) pre[i + 1] = pre[i] + __builtin_amdgcn_readfirstlane(a.cand_count[gw0 + i]);
+        const Cand *seg0 = a.cand + (int64_t)gw0 * a.cand_cap;
+        const int64_t cap = a.cand_cap;
+        auto cand_at = [&](uint32_t i) {
+            int sgi = 0;
+#pragma unroll
+            for (int k = 1; k < kNarrowWaves; ++k) sgi += i >= pre[k] ? 1 : 0;
+            return seg0[sgi * cap + (i - pre[sgi])];
+        };
+        if (lds)
+            narrow_range<true>(env, links, w, cand_at, threadIdx.x, pre[kNarrowWaves], kNarrowWaves * 64, s_verts, n_sat);
+        else
+            narrow_range<false>(env, links, w, cand_at, threadIdx.x, pre[kNarrowWaves], kNarrowWaves * 64, s_verts, n_sat);
+    } else {
+        const Cand *cands = a.spill;
+        auto cand_at = [&](uint32_t i) { return cands[i]; };
+        const uint32_t i0 = (uint32_t)(gw - a.n_cwaves) * 64 + lane, stride = (uint32_t)kSpillWaves * 64u;
+        if (lds)
+            narrow_range<true>(env, links, w, cand_at, i0, n_spill, stride, s_verts, n_sat);
+        else
+            narrow_range<false>(env, links, w, cand_at, i0, n_spill, stride, s_verts, n_sat);
+    }
     if (w.stats && n_sat) atomicAdd(w.stats + 3, (unsigned long long)n_sat);
     if (w.stats && gw == 0 && lane == 0) {
         atomicAdd(w.stats + 5, (unsigned long long)a.ctl[1]);
@@ -644,12 +668,12 @@ __global__ __launch_bounds__(kNarrowWaves * 64, 4) void k_narrow(EnvDev env, con
 // Units that overflowed a pair segment or the spill list (none in practice) are re-run whole
 // with the fused walk (one wave per unit, BVH from global memory).  Launched unconditionally:
 // the usual empty case is one read of the overflow count.
-__global__ __launch_bounds__(kNarrowWaves * 64) void k_overflow(EnvDev env, const AgentDev *__restrict__ links,
+__global__ __launch_bounds__(kOvfBlockWaves * 64) void k_overflow(EnvDev env, const AgentDev *__restrict__ links,
                                                                 CollideWork w, SplitArgs a) {
-    __shared__ int32_t s_stk[kNarrowWaves][kStackDepth];
+    __shared__ int32_t s_stk[kOvfBlockWaves][kStackDepth];
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
-    const int32_t gw = (int32_t)blockIdx.x * kNarrowWaves + wave;
+    const int32_t gw = (int32_t)blockIdx.x * kOvfBlockWaves + wave;
     const uint32_t n_ovf = __hip_atomic_load(a.ctl + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const bool shared_edges = w.pose_edge != nullptr || w.L > 1 || w.pmax > 1;
     uint32_t nu = 0, nc = 0, nn = 0, ns = 0;
@@ -823,7 +847,7 @@ static void collide_split_chunk(const EnvDev &env, const AgentDev *d_links, int3
         defer->n_ovf = a.ctl + 1;
         defer->ovf_list = a.ovf_list;
     } else {
-        hipLaunchKernelGGL(k_overflow, dim3(kOvfWaves / kNarrowWaves), dim3(kNarrowWaves * 64), 0, stream, env, d_links,
+        hipLaunchKernelGGL(k_overflow, dim3(kOvfWaves / kOvfBlockWaves), dim3(kOvfBlockWaves * 64), 0, stream, env, d_links,
                            w, a);
         hip_check(hipGetLastError(), "k_overflow launch");
     }
