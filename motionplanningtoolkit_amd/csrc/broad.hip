@@ -423,7 +423,9 @@ __device__ __forceinline__ bool emit(bool h, uint64_t m, int32_t unit, int32_t a
 // through the caches.  A header's chain of dependent loads is dense slot -> header -> {pose,
 // agent triangles, pair words} -> env items; the next header's dense slot is fetched ahead.
 // kLds: the items in LDS, a compile-time choice (a pointer that may be LDS or global compiles
-// to flat instructions)
+// to flat instructions).  Round 5, measured and not kept: the workgroup's headers claimed from
+// an LDS counter instead of each wave's fixed stride (k_narrow's pooling, for the headers):
+// config 2 ~385 M, the room 126 vs 127 M, 32 seeds 131.2 vs 132.3 M -- no gain.
 template <bool kLds>
 __global__ __launch_bounds__(256) void k_cands(EnvDev env, const AgentDev *__restrict__ links, CollideWork w,
                                                SplitArgs a, int32_t lds_items) {
