@@ -1192,8 +1192,8 @@ __global__ __launch_bounds__(256) void k_ct_lgroup(CtJobs js) {
 // count and the spread.  Round 5, measured and not kept: the upper levels' boxes in LDS (14.4
 // us a round at 32 seeds either way); this work run by the last of k_ct_lgroup<2>'s workgroups
 // to finish a tree (a ticket: one launch less), which made k_ct_lgroup<2> 12.7 -> 58 us at 32
-// seeds and 39 -> 449 us at 256 -- every workgroup's device-scope fence before its ticket
-// writes back its XCD's L2.
+// seeds and 39 -> 449 us at 256 (every workgroup then fences at device scope before its
+// ticket: with one L2 an XCD, the likely cost).
 constexpr int kCtLevelThreads = 1024;
 template <int D>
 __global__ __launch_bounds__(kCtLevelThreads) void k_ct_levels(CtJobs js) {
