@@ -18,8 +18,9 @@
 //           agent triangles, mapped exactly (FP64) and boxed; lanes also fetch the header's
 //           env triangle boxes, which are then tested from registers; overlaps become
 //           candidates in the wave's segment (or the spill list).
-// k_narrow  one wave per candidate segment (plus the spill list), one candidate per lane:
-//           exact transform, tri_gate, intersect_Triangle; verdict[edge] = 1.
+// k_narrow  one workgroup per four candidate segments taken as one list (plus the spill
+//           list), one candidate per lane: exact transform, tri_gate, intersect_Triangle;
+//           verdict[edge] = 1.
 // k_overflow  units whose pairs overflowed a segment are re-run with the fused kernel's
 //           per-unit walk (collide_common.h collide_unit).
 #include <hipcub/hipcub.hpp>
