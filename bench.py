@@ -868,7 +868,7 @@ def config5_summary(c5_256, c5_32=None):
     8 x v32 / v256 (the driver's own N = 8 run measures it when it gets a node)."""
     if not c5_256 or "value" not in c5_256:
         return {"error": "config-5 leg missing", "leg": c5_256}
-    out = {"seeds": 256, "value": c5_256["value"], "unit": c5_256.get("unit"), "ms_per_step": c5_256["ms_per_step"],
+    out = {"seeds": (c5_256.get("config") or {}).get("seeds", 256), "value": c5_256["value"], "unit": c5_256.get("unit"), "ms_per_step": c5_256["ms_per_step"],
            "steps": c5_256["steps"], "warmup": c5_256["warmup"], "n_gpus": c5_256.get("n_gpus"),
            "world_size": c5_256.get("world_size"), "scaling": "strong", "seeds_digest": c5_256.get("seeds_digest"),
            "from_scratch": c5_256.get("from_scratch")}
@@ -877,6 +877,42 @@ def config5_summary(c5_256, c5_32=None):
         r = c5_32["value"] / c5_256["value"]
         out.update({"seeds32_value": c5_32["value"], "same_rounds": same, "per_gpu_ratio": round(r, 4),
                     "projected_8gpu_speedup": round(8 * r, 3)})
+    return out
+
+
+# The line's two scaling bases, the same keys at every N: `value` is config 2 (BASELINE configs[1],
+# one 100k-node tree a rank: weak scaling, value(N) = N ranks' valid extensions / max-over-ranks
+# time); `c5_*` is config 5 (BASELINE configs[4], the north star's scaling claim: 256 seeds
+# sharded contiguously over the N ranks, strong scaling, the same trees -- c5_seeds_digest -- at
+# every N).  At N = 1 c5_* is the seeds=256 leg, at N > 1 the leg run in the same world.
+SCALING_BASIS = ("value: config 2, one 100k-node blimp tree per rank (weak scaling); c5_value: config 5, "
+                 "256 seeds sharded over the N ranks (strong scaling; c5_seeds_digest equal at every N)")
+
+
+def c5_keys(leg):
+    """The config-5 quantities under one key set at every N (see SCALING_BASIS)."""
+    if not leg or "value" not in leg:
+        return {"c5_value": None, "c5_error": (leg or {}).get("error", "config-5 leg missing")}
+    return {"c5_value": leg["value"], "c5_ms_per_step": leg.get("ms_per_step"),
+            "c5_seeds": (leg.get("config") or {}).get("seeds"), "c5_seeds_digest": leg.get("seeds_digest"),
+            "c5_world_size": leg.get("world_size"), "c5_steps": leg.get("steps"), "c5_warmup": leg.get("warmup"),
+            "c5_scaling": "strong"}
+
+
+def attach_config5(out, c5_leg, variants=None):
+    """The config-5 part of the line at any N: c5_* keys and the `config5` summary; at N = 1
+    (variants: the legs run beside config 2) from the seeds=256 / seeds=32 legs, at N > 1
+    from the in-world leg (c5_leg)."""
+    if variants is not None:
+        out["variants"] = variants
+        c5_leg = variants.get("seeds=256")
+        out["config5"] = config5_summary(c5_leg, variants.get("seeds=32"))
+    else:
+        out["config5"] = config5_summary(c5_leg)
+        if isinstance((c5_leg or {}).get("roofline"), dict):
+            out["config5"]["roofline"] = compact_roof(c5_leg["roofline"], LEG_ROOF_KEYS, stages_ms=False)
+    out.update(c5_keys(c5_leg))
+    out["scaling_basis"] = SCALING_BASIS
     return out
 
 
@@ -943,24 +979,16 @@ def main():
         if world > 1:
             # BASELINE config 5 in the same torchrun world: args.c5_seeds seeds sharded
             # contiguously over the ranks (32 per GPU at 8 GPUs), strong scaling; its seeds
-            # digest equals the N = 1 run's (the seeds=256 leg) for the same rounds.  At N > 1
-            # it is the line's top level (the north star's scaling claim is over independent
-            # seeds), config 2's weak-scaled number nested under `config2`
+            # digest equals the N = 1 run's (the seeds=256 leg) for the same rounds.  The top
+            # level stays config 2 at every N (one basis for the driver's curve), config 5 goes
+            # under the c5_* keys (SCALING_BASIS)
             a5 = argparse.Namespace(**vars(args))
             a5.seeds, a5.steps, a5.warmup = args.c5_seeds, args.c5_steps, args.c5_warmup
             c5 = run_seeds(a5, world, rank, dist, torch, mpt, multiseed, scenes)
             if out is not None:
-                c2 = out
-                out = dict(c5)
-                out["config2"] = condense(c2)
-                out["config2"]["cpu_baseline"] = c2.get("cpu_baseline")
-                out["scaling_note"] = (
-                    f"top level: config 5 ({args.c5_seeds} seeds over {world} GPUs, strong scaling); compare with "
-                    "the N = 1 line's config5.value (the same seeds and rounds on one GPU); config2: one 100k-node "
-                    "tree a rank (weak scaling)")
+                attach_config5(out, c5)
         elif out is not None and not args.no_variants and args.workload == "blimp":
-            out["variants"] = run_variants(args.detail)
-            out["config5"] = config5_summary(out["variants"].get("seeds=256"), out["variants"].get("seeds=32"))
+            attach_config5(out, None, run_variants(args.detail))
     if out is not None:
         if args.detail:
             try:

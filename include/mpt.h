@@ -138,9 +138,19 @@ mpt_status mpt_prm_connect(const mpt_env *env, const mpt_agent *agent, int32_t a
 /* Diagnostics: out (may be NULL) = the edge sweep's work counters of the calling thread's last
  * mpt_prm_connect made with counters on: waves, env item box tests, (pair, pose) gate tests,
  * exact triangle tests, edges, poses, (edge, triangle, triangle, pose range) candidates emitted,
- * edges the candidate pass capped (decided by k_sweep_prm); enable switches the counters on for its later
- * calls (one same-address atomic per wave: not for timed calls). */
-mpt_status mpt_prm_stats(int32_t enable, uint64_t out[8]);
+ * edges the candidate pass capped (decided by k_sweep_prm); the first min(count, 8) of them are
+ * written (count: out's length; 8 since round 5, 6 before); enable switches the counters on for
+ * its later calls (one same-address atomic per wave: not for timed calls). */
+mpt_status mpt_prm_stats(int32_t enable, uint64_t *out, int32_t count);
+/* Diagnostics: the edges (indices into that call's edge list) the sweep of the calling thread's
+ * last mpt_prm_connect made with counters on sent to its per-edge pass (k_sweep_prm): first those
+ * its candidate pass capped, then those a full candidate queue deferred.  *n = their number, the
+ * first min(*n, cap) written to out (may be NULL). */
+mpt_status mpt_prm_deferred_edges(int32_t *out, int64_t cap, int64_t *n);
+/* Test hook: caps the PRM sweep's candidate queue at max_candidates (0 restores the sized
+ * queue, at least 4 M entries) so that a small roadmap drives the full-queue path (edges
+ * deferred to the per-edge sweep).  Process-wide; verdicts are unchanged by it. */
+mpt_status mpt_set_sweep_queue_cap(int64_t max_candidates);
 
 /* ---- workspace discretisation: PRMLite::generateEdges (discretizations/workspace/prmlite.hpp:128-164)
  * All vertex pairs i < j, pair index e = row-major over i < j (E = V(V-1)/2).  vertices [V][12] =
@@ -226,6 +236,12 @@ mpt_status mpt_rrt_joint_nn_ms(float *ms);
  * mpt_rrt_step_many on the same joint stream (another host thread's mpt_rrt_last_round /
  * _last_poses hold the state's lock through their copies and are safe). */
 mpt_status mpt_rrt_joint_release(void *joint_stream);
+/* Diagnostics: launch joint_stream's last joint NN launch again on that stream (same job table,
+ * queries and index; its outputs are rewritten with the same values), e.g. alone after an L2
+ * flush under rocprofv3 counters.  xcd_jobs = 1: every workgroup of a tree on one XCD (the
+ * round-4 mapping; trees a multiple of 8) instead of each tree's workgroups over all eight.
+ * Asynchronous. */
+mpt_status mpt_rrt_joint_replay_nn(void *joint_stream, int32_t xcd_jobs);
 /* The last timed mpt_rrt_step_many on joint_stream: ms[0] = the joint tree build, ms[1] = the
  * joint NN launch (hipEvents on joint_stream).  Synchronises on it. */
 mpt_status mpt_rrt_joint_times(void *joint_stream, float ms[2]);

@@ -67,8 +67,11 @@ SIGNATURES = {
     "mpt_rrt_joint_nn_ms": (I32, [P]),
     "mpt_rrt_joint_times": (I32, [P, P]),
     "mpt_rrt_joint_release": (I32, [P]),
+    "mpt_rrt_joint_replay_nn": (I32, [P, I32]),
     "mpt_rrt_joint_stage_times": (I32, [P, P]),
-    "mpt_prm_stats": (I32, [I32, P]),
+    "mpt_prm_stats": (I32, [I32, P, I32]),
+    "mpt_set_sweep_queue_cap": (I32, [I64]),
+    "mpt_prm_deferred_edges": (I32, [P, I64, P]),
     "mpt_rrt_counters": (I32, [P, P]),
     "mpt_rrt_read_tree": (I32, [P, P, P, I64]),
     "mpt_rrt_last_round": (I32, [P, P, P, P, P]),

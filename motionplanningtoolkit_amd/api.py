@@ -176,7 +176,7 @@ def prm_stats(enable: bool) -> dict:
     """The sweep work counters of this thread's last prm_connect made with counters on; enable
     turns them on (or off) for later calls (diagnostics: an atomic per wave)."""
     out = np.zeros(8, np.uint64)
-    check(lib().mpt_prm_stats(1 if enable else 0, _p(out)), "mpt_prm_stats")
+    check(lib().mpt_prm_stats(1 if enable else 0, _p(out), len(out)), "mpt_prm_stats")
     return dict(zip(["waves", "item_tests", "gate_tests", "sat_tests", "edges", "poses", "candidates",
                      "deferred_edges"], (int(x) for x in out)))
 
@@ -189,6 +189,22 @@ def prmlite_edges(env: Environment, agent: AgentMesh, vertices, step: float = 0.
     out = np.zeros(max(V * (V - 1) // 2, 0), np.uint8)
     check(lib().mpt_prmlite_edges(env.handle, agent.handle, _p(v), V, step, _p(out), None), "mpt_prmlite_edges")
     return out
+
+
+def prm_deferred_edges() -> np.ndarray:
+    """The edge indices this thread's last prm_connect made with counters on (prm_stats(True))
+    sent to the sweep's per-edge pass: the candidate pass's capped edges, then a full queue's."""
+    n = C.c_int64(0)
+    check(lib().mpt_prm_deferred_edges(None, 0, C.byref(n)), "mpt_prm_deferred_edges")
+    out = np.zeros(n.value, np.int32)
+    check(lib().mpt_prm_deferred_edges(_p(out), n.value, C.byref(n)), "mpt_prm_deferred_edges")
+    return out
+
+
+def set_sweep_queue_cap(max_candidates: int) -> None:
+    """Test hook: cap the PRM sweep's candidate queue (0 restores the sized queue), so that the
+    full-queue path (edges deferred to the per-edge sweep) runs on a small roadmap."""
+    check(lib().mpt_set_sweep_queue_cap(int(max_candidates)), "mpt_set_sweep_queue_cap")
 
 
 COLLIDE_MODES = {"split": 0, "fused": 1}
@@ -415,6 +431,11 @@ def joint_stage_times(joint_stream) -> dict:
 def joint_release(joint_stream) -> None:
     """Free the joint state step_many keeps for joint_stream (call before the stream goes)."""
     check(lib().mpt_rrt_joint_release(_stream(joint_stream)), "mpt_rrt_joint_release")
+
+def joint_replay_nn(joint_stream, xcd_jobs: bool = False) -> None:
+    """Diagnostics: joint_stream's last joint NN launch again (same jobs; same results)."""
+    check(lib().mpt_rrt_joint_replay_nn(_stream(joint_stream), 1 if xcd_jobs else 0), "mpt_rrt_joint_replay_nn")
+
 
 def load_mesh(path: str, which: str = "all") -> np.ndarray:
     """AssimpMeshLoader replacement: 'all' submeshes (environment) or 'last' (agent)."""

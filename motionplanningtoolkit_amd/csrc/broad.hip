@@ -30,6 +30,7 @@
 
 #include "collide_common.h"
 #include "scan.h"
+#include "wave_ops.h"
 
 namespace mpt {
 
@@ -72,17 +73,6 @@ __device__ __forceinline__ Item load_item_u(const Item *__restrict__ items, int6
 #else
     return items[idx];
 #endif
-}
-
-__device__ __forceinline__ float wave_min(float v) {
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) v = fminf(v, __shfl_xor(v, off));
-    return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v)));
-}
-__device__ __forceinline__ float wave_max(float v) {
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) v = fmaxf(v, __shfl_xor(v, off));
-    return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v)));
 }
 
 // Per-thread walk of the env tree (items from LDS or global) with box (lo, hi);
@@ -473,9 +463,9 @@ __global__ __launch_bounds__(256) void k_cands(EnvDev env, const AgentDev *__res
         if (act) agent_tri_box(tri, R, T, blo, bhi);
         ++n_xf;
 #pragma unroll
-        for (int k = 0; k < 3; ++k) {
-            tlo[k] = wave_min(act ? blo[k] : __builtin_huge_valf());
-            thi[k] = wave_max(act ? bhi[k] : -__builtin_huge_valf());
+        for (int k = 0; k < 3; ++k) {  // DPP / permlane levels (ds_bpermute: 36 LDS round trips a header)
+            tlo[k] = wave_min_dpp(act ? blo[k] : __builtin_huge_valf());
+            thi[k] = wave_max_dpp(act ? bhi[k] : -__builtin_huge_valf());
         }
         // lanes scan the segment 64 words at a time; this header's words are those of its lane,
         // all hn of them in the segment (a thread whose pairs overflowed wrote no header), so

@@ -1780,10 +1780,17 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(D >= 15 ? 4 
 // round 5 measured NN 0.337 -> 0.284 ms at 32 seeds, 2.111 -> 2.079 at 256 for this mapping.
 // Also measured and not kept: a job split over two XCDs when an XCD holds fewer than 8 trees --
 // its 64-bit index math spilled the 64-VGPR walk: 0.33 -> 0.37 ms at 32 seeds.)
+// xcd_jobs (diagnostics, mpt_rrt_joint_replay_nn; n_jobs a multiple of 8): round 4's mapping
+// instead, every workgroup of job j on XCD j % 8 (workgroup b runs on XCD b % 8).
 template <int D, int BS, int W>
 __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(D >= 15 ? 4 : 8))) void k_ct_nn1_jobs(
-    const CtNnJob *__restrict__ jobs, int32_t n_jobs, int64_t nq, int32_t blocks_per_job) {
-    const uint32_t job = blockIdx.x / (uint32_t)blocks_per_job, blk = blockIdx.x % (uint32_t)blocks_per_job;
+    const CtNnJob *__restrict__ jobs, int32_t n_jobs, int64_t nq, int32_t blocks_per_job, int32_t xcd_jobs) {
+    uint32_t job = blockIdx.x / (uint32_t)blocks_per_job, blk = blockIdx.x % (uint32_t)blocks_per_job;
+    if (xcd_jobs) {
+        const uint32_t k = blockIdx.x / 8u;
+        job = blockIdx.x % 8u + 8u * (k / (uint32_t)blocks_per_job);
+        blk = k % (uint32_t)blocks_per_job;
+    }
     if (job >= (uint32_t)n_jobs) return;
     const CtNnJob J = jobs[job];  // by value: the tree's pointers stay in SGPRs across the walk
     ct_walk<D, BS, W>(J.T, J.q, nq, J.ids, J.d2, blk);
@@ -2161,25 +2168,28 @@ void launch_ct_nn1(const CellTreeDev &T, const double *q, int64_t nq, int32_t *i
 }
 
 template <int W>
-static void launch_ct_nn1_jobs_w(const CtNnJob *d_jobs, int32_t n_jobs, int32_t d, int64_t nq, hipStream_t stream) {
+static void launch_ct_nn1_jobs_w(const CtNnJob *d_jobs, int32_t n_jobs, int32_t d, int64_t nq, hipStream_t stream,
+                                 int32_t xcd_jobs) {
     constexpr int BS = 64;
     const int64_t bpj = (nq * 8 * W + BS - 1) / BS;
     if (bpj * n_jobs > 0x7fffffffLL) throw Error{1, "cell tree: joint NN launch too large"};
     const dim3 grid((unsigned)(bpj * n_jobs));
     const int32_t b = (int32_t)bpj;
     switch (d) {
-        case 3: hipLaunchKernelGGL((k_ct_nn1_jobs<3, BS, W>), grid, dim3(BS), 0, stream, d_jobs, n_jobs, nq, b); break;
-        case 7: hipLaunchKernelGGL((k_ct_nn1_jobs<7, BS, W>), grid, dim3(BS), 0, stream, d_jobs, n_jobs, nq, b); break;
-        case 15: hipLaunchKernelGGL((k_ct_nn1_jobs<15, BS, W>), grid, dim3(BS), 0, stream, d_jobs, n_jobs, nq, b); break;
+        case 3: hipLaunchKernelGGL((k_ct_nn1_jobs<3, BS, W>), grid, dim3(BS), 0, stream, d_jobs, n_jobs, nq, b, xcd_jobs); break;
+        case 7: hipLaunchKernelGGL((k_ct_nn1_jobs<7, BS, W>), grid, dim3(BS), 0, stream, d_jobs, n_jobs, nq, b, xcd_jobs); break;
+        case 15: hipLaunchKernelGGL((k_ct_nn1_jobs<15, BS, W>), grid, dim3(BS), 0, stream, d_jobs, n_jobs, nq, b, xcd_jobs); break;
         default: throw Error{1, "cell tree: state dim must be 3, 7 or 15"};
     }
     hip_check(hipGetLastError(), "k_ct_nn1_jobs launch");
 }
 
-void launch_ct_nn1_jobs(const CtNnJob *d_jobs, int32_t n_jobs, int32_t d, int64_t nq, hipStream_t stream) {
+void launch_ct_nn1_jobs(const CtNnJob *d_jobs, int32_t n_jobs, int32_t d, int64_t nq, hipStream_t stream,
+                        int32_t xcd_jobs) {
     if (nq <= 0 || n_jobs <= 0) return;
-    if (ct_width(d) == 8) launch_ct_nn1_jobs_w<8>(d_jobs, n_jobs, d, nq, stream);
-    else launch_ct_nn1_jobs_w<4>(d_jobs, n_jobs, d, nq, stream);
+    if (xcd_jobs && n_jobs % 8 != 0) throw Error{1, "cell tree: whole jobs per XCD need a multiple of 8 jobs"};
+    if (ct_width(d) == 8) launch_ct_nn1_jobs_w<8>(d_jobs, n_jobs, d, nq, stream, xcd_jobs);
+    else launch_ct_nn1_jobs_w<4>(d_jobs, n_jobs, d, nq, stream, xcd_jobs);
 }
 
 }  // namespace mpt

@@ -15,6 +15,7 @@
 
 #include <exception>
 #include <string>
+#include <vector>
 
 #include "fcl_math.h"
 
@@ -249,6 +250,8 @@ void launch_pose_edge(const int64_t *d_offsets, int64_t E, int32_t *d_pose_edge,
 struct PrmEdges;
 // the calling thread's last two-phase sweep: candidates emitted, edges deferred
 extern thread_local uint64_t last_sweep_counts[2];
+extern thread_local std::vector<int32_t> last_sweep_deferred;
+extern int64_t sweep_queue_cap_limit;  // mpt_set_sweep_queue_cap (0: the sized queue)
 void launch_collide_sweep_prm(const EnvDev &env, const AgentDev *d_link, int32_t n_clusters, const PrmEdges &edges,
                               int64_t E, uint8_t *verdict, unsigned long long *stats, hipStream_t stream);
 

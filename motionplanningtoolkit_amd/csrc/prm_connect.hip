@@ -167,11 +167,27 @@ int32_t uf_find(std::vector<int32_t> &p, int32_t x) {
 
 }  // namespace
 
-extern "C" mpt_status mpt_prm_stats(int32_t enable, uint64_t out[8]) {
+extern "C" mpt_status mpt_prm_stats(int32_t enable, uint64_t *out, int32_t count) {
     return guarded([&] {
         if (out)
-            for (int i = 0; i < 8; ++i) out[i] = g_prm_stats[i];
+            for (int i = 0; i < 8 && i < count; ++i) out[i] = g_prm_stats[i];
         g_prm_stats_on = enable != 0;
+    });
+}
+
+extern "C" mpt_status mpt_prm_deferred_edges(int32_t *out, int64_t cap, int64_t *n) {
+    return guarded([&] {
+        if (!n) throw Error{MPT_ERR_INVALID, "mpt_prm_deferred_edges: n is NULL"};
+        *n = (int64_t)last_sweep_deferred.size();
+        if (out)
+            for (int64_t i = 0; i < *n && i < cap; ++i) out[i] = last_sweep_deferred[(size_t)i];
+    });
+}
+
+extern "C" mpt_status mpt_set_sweep_queue_cap(int64_t max_candidates) {
+    return guarded([&] {
+        if (max_candidates < 0) throw Error{MPT_ERR_INVALID, "mpt_set_sweep_queue_cap: negative"};
+        sweep_queue_cap_limit = max_candidates;
     });
 }
 

@@ -110,6 +110,11 @@ struct PrmEdge {
         tail_too = false;
         if (it < 2) return;
         const float d0 = (float)(s[0] - env_tf[9]), d1 = (float)(s[1] - env_tf[10]), d2 = (float)(s[2] - env_tf[11]);
+        // T0 and Dk below are float sums of rotated terms: their rounding follows the terms'
+        // magnitudes (|d|, step * it * |dx|), not the (possibly cancelled) sums, so eps carries
+        // both (|R| <= 1 entrywise bounds each term by them)
+        const float mag = fabsf(d0) + fabsf(d1) + fabsf(d2) +
+                          (float)step * (float)it * (float)(fabs(dx[0]) + fabs(dx[1]) + fabs(dx[2]));
         float lo = 0.0f, hi = (float)(it - 1);
 #pragma unroll
         for (int k = 0; k < 3; ++k) {
@@ -119,8 +124,9 @@ struct PrmEdge {
             const float a0 = (float)(&RQ[0].x)[k], a1 = (float)(&RQ[1].x)[k], a2 = (float)(&RQ[2].x)[k];
             const float a = fminf(a0, fminf(a1, a2)), b = fmaxf(a0, fmaxf(a1, a2));
             const float el = (float)elo[k], eh = (float)ehi[k];
-            const float eps = 1e-5f * (1.0f + fabsf(T0) + fabsf(Dk) * (float)it + fabsf(a) + fabsf(b) + fabsf(el) +
-                                       fabsf(eh) + fabsf((float)env_tf[9 + k]) + fabsf(rk0) + fabsf(rk1) + fabsf(rk2));
+            const float eps = 1e-5f * (1.0f + mag + fabsf(T0) + fabsf(Dk) * (float)it + fabsf(a) + fabsf(b) +
+                                       fabsf(el) + fabsf(eh) + fabsf((float)env_tf[9 + k]) + fabsf(rk0) +
+                                       fabsf(rk1) + fabsf(rk2));
             const float u = eh - a - T0 + eps;  // i * D'_k <= u
             const float l = el - b - T0 - eps;  // i * D'_k >= l
             if (Dk > 0.0f) {

@@ -1334,6 +1334,10 @@ struct JointNN {
     // timed joint round: start, sample, build, NN, steer, collide, append
     hipEvent_t st[7] = {};
     bool round_timed = false;
+    // the last joint NN launch (mpt_rrt_joint_replay_nn): its device job table and shape
+    const CtNnJob *nn_jobs = nullptr;
+    int32_t nn_n = 0, nn_d = 0;
+    int64_t nn_q = 0;
 };
 std::mutex g_joints_mu;
 std::map<hipStream_t, std::shared_ptr<JointNN>> g_joints;
@@ -1385,9 +1389,11 @@ char *joint_stage(JointNN &g, size_t bytes, int *slot) {
         if (g.h_stage[0]) hip_check(hipHostFree(g.h_stage[0]), "free");  // the ring's one allocation
         const size_t c = std::max(bytes, 2 * g.cap);
         hip_check(hipMalloc(&g.d_stage, c), "stage");
-        // the ring's buffers carved from one pinned allocation (one hipHostMalloc, not kJobRing)
+        // the ring's buffers carved from one pinned allocation (one hipHostMalloc, not kJobRing),
+        // mapped and coherent explicitly: k_stage_copy reads it through its device address
+        // (as PinnedSlots), independent of the runtime's default host-allocation flags
         char *ring = nullptr;
-        hip_check(hipHostMalloc(&ring, c * kJobRing), "stage pinned");
+        hip_check(hipHostMalloc(&ring, c * kJobRing, hipHostMallocMapped | hipHostMallocCoherent), "stage pinned");
         char *dring = nullptr;
         hip_check(hipHostGetDevicePointer((void **)&dring, ring, 0), "stage pinned device address");
         for (int i = 0; i < kJobRing; ++i) {
@@ -1564,6 +1570,10 @@ void joint_round(mpt_rrt *const *rs, int32_t n, int32_t K, void *const *streams_
     mark(2);
     if (timed) hip_check(hipEventRecord(g.t0, joint), "joint t0");
     launch_ct_nn1_jobs(dn, n, d, K, joint);
+    g.nn_jobs = dn;
+    g.nn_n = n;
+    g.nn_d = d;
+    g.nn_q = K;
     mark(3);
     if (timed) hip_check(hipEventRecord(g.t1, joint), "joint t1");
     auto steer = p.kind == MPT_AGENT_OMNI ? k_steer_jobs<MPT_AGENT_OMNI>
@@ -1715,6 +1725,10 @@ extern "C" mpt_status mpt_rrt_step_many(mpt_rrt *const *rs, int32_t n, int32_t K
                 for (int32_t i : J) cs[i].mark(2, stream_of(i));
             }
             launch_ct_nn1_jobs(dn, nj, rs[J[0]]->p.d, K, joint);
+            g.nn_jobs = dn;
+            g.nn_n = nj;
+            g.nn_d = rs[J[0]]->p.d;
+            g.nn_q = K;
             if (timed) {
                 hip_check(hipEventRecord(g.t1, joint), "joint t1");
                 g_last_timed = &g;
@@ -1784,6 +1798,18 @@ extern "C" mpt_status mpt_rrt_joint_stage_times(void *joint_stream, float ms[6])
         if (!g->round_timed) throw Error{MPT_ERR_INVALID, "the last step_many on this stream was not a timed joint round"};
         hip_check(hipEventSynchronize(g->st[6]), "event sync");
         for (int i = 0; i < 6; ++i) hip_check(hipEventElapsedTime(&ms[i], g->st[i], g->st[i + 1]), "elapsed");
+    });
+}
+
+// Diagnostics: the joint stream's last NN launch again, on that stream, over the same job table
+// (its queries, its trees' index as that round's build left it, its output slots: the results are
+// rewritten with the same values) -- the NN alone for rocprofv3 counters, e.g. after an L2 flush.
+extern "C" mpt_status mpt_rrt_joint_replay_nn(void *joint_stream, int32_t xcd_jobs) {
+    return guarded([&] {
+        std::shared_ptr<JointNN> g = joint_find_shared((hipStream_t)joint_stream);
+        if (!g || !g->nn_jobs) throw Error{MPT_ERR_INVALID, "no joint NN launch on this stream"};
+        std::lock_guard<std::mutex> lk(g->mu);
+        launch_ct_nn1_jobs(g->nn_jobs, g->nn_n, g->nn_d, g->nn_q, (hipStream_t)joint_stream, xcd_jobs);
     });
 }
 

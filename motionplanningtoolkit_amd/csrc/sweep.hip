@@ -332,12 +332,18 @@ constexpr unsigned kSweepCoarse = 1024;
 // are tested all the same, which is harmless: a contact among them is a contact)
 __device__ __forceinline__ bool sweep_flush(SweepCand *buf, int nb, const SweepQueue &Q, int lane) {
     if (nb <= 0) return true;
+    // a queue already full takes no more reservations, so the counter stays within cap plus
+    // one stage a running wave (no u32 wrap however many edges are deferred)
     uint32_t base = 0;
-    if (lane == 0) base = atomicAdd(Q.n, (uint32_t)nb);
+    if (lane == 0) {
+        base = __hip_atomic_load(Q.n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (base < Q.cap) base = atomicAdd(Q.n, (uint32_t)nb);
+    }
     base = __builtin_amdgcn_readfirstlane(base);
+    if (base >= Q.cap) return false;
     for (int i = lane; i < nb; i += kWave)
-        if (base + (uint32_t)i < Q.cap) Q.c[base + i] = buf[i];
-    return base + (uint32_t)nb <= Q.cap;
+        if ((uint64_t)base + (uint64_t)i < Q.cap) Q.c[base + i] = buf[i];
+    return (uint64_t)base + (uint64_t)nb <= Q.cap;
 }
 
 // A PRM edge for one wave: every field wave-uniform (scalar registers), and the env-relative
@@ -826,6 +832,8 @@ static void launch_sweep_src(const EnvDev &env, const AgentDev *d_link, int32_t 
 }
 
 thread_local uint64_t last_sweep_counts[2] = {0, 0};
+thread_local std::vector<int32_t> last_sweep_deferred;  // with counters on: the edges k_sweep_prm took
+int64_t sweep_queue_cap_limit = 0;  // mpt_set_sweep_queue_cap: a test hook (0: the sized queue)
 
 void launch_collide_sweep_prm(const EnvDev &env, const AgentDev *d_link, int32_t n_clusters, const PrmEdges &edges,
                               int64_t E, uint8_t *verdict, unsigned long long *stats, hipStream_t stream) {
@@ -872,6 +880,8 @@ void launch_collide_sweep_prm(const EnvDev &env, const AgentDev *d_link, int32_t
         q.cap = want;
         q.ecap = E;
     }
+    // the queue's capacity this call (a test shrinks it to drive the full-queue path)
+    const int64_t qcap = sweep_queue_cap_limit > 0 ? std::min<int64_t>(q.cap, sweep_queue_cap_limit) : q.cap;
     int pass_no = 0;
     auto prm_pass = [&](const int32_t *list, const uint32_t *n_list, unsigned stride, bool rest) {
         uint32_t *next = q.next + (pass_no++ & 7);  // a counter a launch (zeroed below, once a call)
@@ -897,7 +907,7 @@ void launch_collide_sweep_prm(const EnvDev &env, const AgentDev *d_link, int32_t
         const int o = pass & 1;
         if (pass > 0) hip_check(hipMemsetAsync(q.n, 0, sizeof(uint32_t), stream), "sweep counts zero");
         hip_check(hipMemsetAsync(q.n + 2 + o, 0, sizeof(uint32_t), stream), "sweep counts zero");
-        SweepQueue Qd{q.c, q.n, (uint32_t)std::min<int64_t>(q.cap, 0xffffffffLL), q.fused,
+        SweepQueue Qd{q.c, q.n, (uint32_t)std::min<int64_t>(qcap, 0xffffffffLL), q.fused,
                       pass ? q.le[1 - o] : nullptr, pass ? q.lr[1 - o] : nullptr, q.n + 2 + (1 - o),
                       q.le[o], q.lr[o], q.n + 2 + o, edge_cap};
         const int64_t blocks = pass ? std::min<int64_t>(4096, (n_in + kSweepWaves - 1) / kSweepWaves)
@@ -914,7 +924,7 @@ void launch_collide_sweep_prm(const EnvDev &env, const AgentDev *d_link, int32_t
         n_in = q.h[2 + o];  // capped edges (some now decided: the next pass skips those)
         last = o;
         // the next cap: x4, as far as the queue holds every capped edge's share
-        const int64_t fit = n_in > 0 ? q.cap / n_in - kWave : 0;
+        const int64_t fit = n_in > 0 ? qcap / n_in - kWave : 0;
         edge_cap = (uint32_t)std::max<int64_t>(kSweepEdgeCands, std::min<int64_t>(int64_t(edge_cap) * 4, fit));
     }
     // what the passes left (capped at the last pass, or stopped by a full queue): k_sweep_prm,
@@ -925,6 +935,16 @@ void launch_collide_sweep_prm(const EnvDev &env, const AgentDev *d_link, int32_t
         to_fused += (uint64_t)n_in;
     }
     if (q.h[1] > 0) prm_pass(q.fused, q.n + 1, 1u, false);
+    last_sweep_deferred.clear();
+    if (stats) {
+        // diagnostics (mpt_prm_deferred_edges): the capped edges, then the full queue's
+        const size_t a = (n_in > 0 && last >= 0) ? (size_t)n_in : 0, b = q.h[1];
+        last_sweep_deferred.resize(a + b);
+        if (a) hip_check(hipMemcpyAsync(last_sweep_deferred.data(), q.le[last], sizeof(int32_t) * a,
+                                        hipMemcpyDeviceToHost, stream), "deferred edges");
+        if (b) hip_check(hipMemcpyAsync(last_sweep_deferred.data() + a, q.fused, sizeof(int32_t) * b,
+                                        hipMemcpyDeviceToHost, stream), "deferred edges");
+    }
     hip_check(hipStreamSynchronize(stream), "sweep sync");
     last_sweep_counts[0] = emitted;    // candidates emitted over the passes
     last_sweep_counts[1] = to_fused;  // edges left to k_sweep_prm

@@ -49,14 +49,16 @@ def test_two_ranks_shard_config5_like_one():
 
 
 def _check_multi_rank_line(two, one):
-    """At N > 1 the line's top level is config 5 (strong scaling, seeds sharded contiguously
-    over the ranks) with config 2's weak-scaled line nested under `config2`."""
-    assert two["n_gpus"] == 2 and two["world_size"] == 2 and two["scaling"] == "strong"
-    assert (two["steps"], two["warmup"]) == (2, 3)
-    assert two["seeds_digest"] == one["seeds_digest"]
-    assert two["from_scratch"]["rounds"] == 5 and two["from_scratch"]["wall_s"] > 0
-    c2 = two["config2"]
-    assert c2["world_size"] == 2 and c2["value"] > 0
+    """At N > 1 the line's top level is config 2 as at N = 1 (weak scaling, one tree a rank:
+    one basis for the driver's curve) and config 5 (strong scaling, seeds sharded contiguously
+    over the ranks) sits under the same c5_* keys the N = 1 line carries, with the one-rank
+    digest (bench.SCALING_BASIS)."""
+    assert two["n_gpus"] == 2 and two["world_size"] == 2 and two["scaling"] == "weak" and two["value"] > 0
+    assert two["config"]["tree_nodes"] == 20000 and two["steps"] == 3
+    assert two["c5_world_size"] == 2 and two["c5_seeds"] == 12 and two["c5_value"] > 0
+    assert (two["c5_steps"], two["c5_warmup"]) == (2, 3)
+    assert two["c5_seeds_digest"] == one["seeds_digest"] == two["config5"]["seeds_digest"]
+    assert two["config5"]["from_scratch_valid_per_s"] > 0 and two["scaling_basis"]
     assert len(json.dumps(two)) < 8000
 
 

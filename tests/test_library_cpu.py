@@ -221,6 +221,38 @@ def test_bench_line_fits_the_driver_tail():
     assert line["config5"]["per_gpu_ratio"] == full["config5"]["per_gpu_ratio"]
 
 
+def test_bench_config5_keys_at_every_n():
+    """The c5_* keys carry config 5 under one name at N = 1 (from the seeds=256 leg run beside
+    config 2) and at N > 1 (the leg run in the same world), and survive the printed line; equal
+    trees give equal c5_seeds_digest."""
+    import copy
+    import json
+    import sys
+
+    sys.path.insert(0, REPO)
+    import bench
+
+    full = json.load(open(os.path.join(REPO, "tests", "golden", "bench", "full_line_r20.json")))
+    variants = full["variants"]
+    one = {k: full[k] for k in ("metric", "value", "unit", "n_gpus", "scaling")}
+    bench.attach_config5(one, None, variants)
+    leg = variants["seeds=256"]
+    two_leg = dict(copy.deepcopy(leg), world_size=2, n_gpus=2, value=2 * leg["value"])
+    two = dict(one, n_gpus=2)
+    for k in ("variants", "config5"):
+        two.pop(k)
+    bench.attach_config5(two, two_leg)
+    for line, ws in ((one, 1), (two, 2)):
+        printed = bench.compact_line(line, None)
+        assert printed["c5_value"] == line["c5_value"] and printed["c5_world_size"] == ws
+        assert printed["scaling_basis"] == bench.SCALING_BASIS and printed["c5_scaling"] == "strong"
+        assert printed["c5_seeds_digest"] == leg["seeds_digest"] == printed["config5"]["seeds_digest"]
+        assert printed["c5_ms_per_step"] == line["config5"]["ms_per_step"]
+    assert two["c5_value"] == 2 * one["c5_value"]
+    assert "per_gpu_ratio" in one["config5"] and "per_gpu_ratio" not in two["config5"]
+    assert bench.c5_keys(None)["c5_value"] is None
+
+
 def test_bench_gpus_must_match_world_size():
     """Under torchrun, --gpus N must equal WORLD_SIZE (checked before anything is imported)."""
     env = dict(os.environ, WORLD_SIZE="3", RANK="0", LOCAL_RANK="0")

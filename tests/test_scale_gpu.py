@@ -159,23 +159,40 @@ def test_config4_rooms_at_size(mpt_gpu, oracle):
     assert len(e_ref) > 400
     assert np.array_equal(edges[pre], e_ref)
     assert np.array_equal(verdict[pre], v_ref)
-    # (3) 1 500 edges drawn from the whole roadmap (every stage of the sweep: the candidate pass,
-    #     its SAT launch, the capped edges' coarse and remaining poses): the oracle's verdict of
-    #     each, from one orc_prm_radius call over their endpoints in index order (an edge's poses
-    #     depend on its two milestones only; edges among the endpoints that were not drawn are
-    #     ignored)
+    # (3) 10 000 edges drawn from the whole roadmap, up to half of them among the edges the
+    #     sweep's candidate pass capped or a full queue deferred (mpt_prm_deferred_edges: the
+    #     k_sweep_prm edges, the most candidates), the rest uniform: the oracle's verdict of each,
+    #     from orc_prm_radius calls over their endpoints in index order, 1 000 drawn edges a call
+    #     (an edge's poses depend on its two milestones only; edges among a call's endpoints that
+    #     were not drawn are ignored)
+    mpt_gpu.prm_stats(True)
+    try:
+        again = mpt_gpu.prm_connect(env, ag, 1, st, r2, sc.cc_dt)
+        deferred = mpt_gpu.prm_deferred_edges()
+    finally:
+        mpt_gpu.prm_stats(False)
+    assert np.array_equal(again["verdict"], verdict)
+    assert len(deferred) > 1000, len(deferred)
     rng = np.random.default_rng(7)
-    pick = rng.choice(len(edges), size=1500, replace=False)
-    ends = np.unique(edges[pick].ravel())
-    pos = np.full(n, -1, np.int64)
-    pos[ends] = np.arange(len(ends))
-    e_sub, v_sub, _ = oracle.prm_radius(oracle.BVH(env_t), I12, sc.agent_tris, st[ends], r2, sc.cc_dt,
-                                        nthreads=THREADS)
-    ref = {(int(a), int(b)): int(v) for (a, b), v in zip(e_sub.tolist(), v_sub.tolist())}
-    drawn = [(int(pos[i]), int(pos[j])) for i, j in edges[pick].tolist()]
-    assert all(d in ref for d in drawn)
-    assert np.array_equal(np.array([ref[d] for d in drawn], np.uint8), verdict[pick])
-    assert 0 < verdict[pick].sum() < len(pick)
+    hard = rng.choice(deferred, size=min(5000, len(deferred)), replace=False)
+    rest = np.setdiff1d(np.arange(len(edges)), hard)
+    pick = np.concatenate([hard, rng.choice(rest, size=10_000 - len(hard), replace=False)])
+    got_v = np.empty(len(pick), np.uint8)
+    ref_v = np.empty(len(pick), np.uint8)
+    bvh = oracle.BVH(env_t)
+    for c0 in range(0, len(pick), 1000):
+        sub = pick[c0:c0 + 1000]
+        ends = np.unique(edges[sub].ravel())
+        pos = np.full(n, -1, np.int64)
+        pos[ends] = np.arange(len(ends))
+        e_sub, v_sub, _ = oracle.prm_radius(bvh, I12, sc.agent_tris, st[ends], r2, sc.cc_dt, nthreads=THREADS)
+        ref = {(int(a), int(b)): int(v) for (a, b), v in zip(e_sub.tolist(), v_sub.tolist())}
+        drawn = [(int(pos[i]), int(pos[j])) for i, j in edges[sub].tolist()]
+        assert all(d in ref for d in drawn)
+        ref_v[c0:c0 + len(sub)] = [ref[d] for d in drawn]
+        got_v[c0:c0 + len(sub)] = verdict[sub]
+    assert np.array_equal(got_v, ref_v)
+    assert 0 < ref_v[:len(hard)].sum() < len(hard) and 0 < ref_v[len(hard):].sum() < len(pick) - len(hard)
     # (4) components over the free edges
     assert np.array_equal(got["comp"], _components(n, edges, verdict))
 
@@ -250,6 +267,14 @@ def test_config5_shard_shape(mpt_gpu, oracle):
     mpt_gpu.joint_release(joint)
     sizes = [len(got[s][0]) for s in seeds]
     assert min(sizes) > 60_000, sizes
+    # the driver line's seeds=32 digest (same seeds, rounds and starts)
+    import hashlib
+
+    from motionplanningtoolkit_amd import multiseed
+
+    assert rounds == bench.C5_WARMUP + bench.C5_STEPS
+    dg = hashlib.sha256("".join(multiseed.tree_digest(*got[s]) for s in seeds).encode()).hexdigest()
+    assert dg == _c5_golden()["seeds32"]
     bvh = oracle.BVH(sc.env_tris)
     for s in (seeds[0], seeds[13], seeds[31]):
         ref = np.zeros((1 + rounds * K, sc.dim))
@@ -265,14 +290,25 @@ def test_config5_shard_shape(mpt_gpu, oracle):
         assert np.array_equal(pa, par[:n])
 
 
+def _c5_golden():
+    import json
+
+    with open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "config5_digests.json")) as f:
+        return json.load(f)
+
+
 def test_config5_256_joint(mpt_gpu, oracle):
-    """The N = 1 north-star leg's shape (`bench.py --seeds 256`): 256 wall-start blimp seeds
-    in ONE step_many group from their start states -- every round a joint round (256 jobs dealt
-    over the XCDs in the joint NN launch, one collide chunk of ~1 M units x 22 clusters, the
-    young trees indexed from an empty cell tree inside the joint build) -- for 6 rounds of 4096
-    extensions.  Seeds 0, 127 and 255 node for node against orc_engine_step (the reference's
-    RRT::query loop, planners/rrt.hpp:42-94, batched), and the 256-seed digest equal to that of
-    eight separate 32-seed groups -- what each GPU of eight runs (multiseed.shard_seeds)."""
+    """The N = 1 north-star leg at the shape bench.py times it (`--seeds 256`, C5_WARMUP +
+    C5_STEPS = 30 rounds of 4096 extensions): 256 wall-start blimp seeds in ONE step_many group
+    from their start states -- every round a joint round (256 jobs dealt over the XCDs in the
+    joint NN launch, one collide chunk of ~1 M units x 22 clusters split at the kernel's chunk
+    boundary, the trees indexed from an empty cell tree inside the joint build and grown to ~110 k
+    nodes each, ~28 M nodes in the last rounds' joint index).  Asserted:
+    * the 256-seed digest equals that of eight separate 32-seed groups (what each GPU of eight
+      runs, multiseed.shard_seeds) and the driver line's seeds_digest (tests/golden/
+      config5_digests.json);
+    * seeds 0 and 255 equal orc_engine_step's trees node for node (the reference's RRT::query
+      loop, planners/rrt.hpp:42-94, batched), states and parents bitwise."""
     import hashlib
     import sys
 
@@ -282,14 +318,19 @@ def test_config5_256_joint(mpt_gpu, oracle):
     import bench
     from motionplanningtoolkit_amd import multiseed
 
+    gold = _c5_golden()
     sc = scenes.blimp_scenario("all")
     env = mpt_gpu.Environment(sc.env_tris, sc.env_tf)
     ag = mpt_gpu.AgentMesh(sc.agent_tris)
-    K, rounds, base, n = 4096, 6, 1000, 256
+    K, base, n = 4096, 1000, 256
+    rounds = bench.C5_WARMUP + bench.C5_STEPS
+    assert (rounds, K, base) == (gold["rounds"], gold["extensions_per_round"], gold["seed_base"])
     seeds = [base + i for i in range(n)]
     starts = {s: bench.seed_start(s, env, ag, mpt_gpu, "walls") for s in seeds}
+    keep = (seeds[0], seeds[255])
 
     def grow(group_seeds):
+        """per-tree digests of the group's seeds, and the kept seeds' trees"""
         engs = []
         for s in group_seeds:
             e = mpt_gpu.RRTEngine(env, ag, sc.kind, sc.prm, sc.ranges, sc.steer_dt, sc.cc_dt, 1 + rounds * K, s)
@@ -300,26 +341,30 @@ def test_config5_256_joint(mpt_gpu, oracle):
         for _ in range(rounds):
             mpt_gpu.step_many(engs, K, [joint] * len(engs), joint)
         torch.cuda.synchronize()
-        out = {}
+        dig, trees, sizes = {}, {}, []
         for s, e in zip(group_seeds, engs):
             assert e.last_nn() == "tree"
-            out[s] = e.read_tree(e.counters()["nodes"])
+            st, pa = e.read_tree(e.counters()["nodes"])
+            dig[s] = multiseed.tree_digest(st, pa)
+            sizes.append(len(st))
+            if s in keep:
+                trees[s] = (st, pa)
             e.close()
         mpt_gpu.joint_release(joint)
-        return out
+        return dig, trees, sizes
 
-    def digest(trees):
-        return hashlib.sha256("".join(multiseed.tree_digest(*trees[s]) for s in sorted(trees)).encode()).hexdigest()
+    def digest(d):
+        return hashlib.sha256("".join(d[s] for s in sorted(d)).encode()).hexdigest()
 
-    whole = grow(seeds)
-    sizes = [len(whole[s][0]) for s in seeds]
-    assert min(sizes) > 10_000, min(sizes)
+    whole, trees, sizes = grow(seeds)
+    assert min(sizes) > 10_000 and sum(sizes) > 20_000_000, (min(sizes), sum(sizes))
+    assert digest(whole) == gold["seeds256"]
     shards = {}
     for r in range(8):
-        shards.update(grow([seeds[i] for i in multiseed.shard_seeds(n, 8, r)]))
-    assert digest(whole) == digest(shards)
+        shards.update(grow([seeds[i] for i in multiseed.shard_seeds(n, 8, r)])[0])
+    assert shards == whole
     bvh = oracle.BVH(sc.env_tris)
-    for s in (seeds[0], seeds[127], seeds[255]):
+    for s in keep:
         ref = np.zeros((1 + rounds * K, sc.dim))
         ref[0] = starts[s][0]
         par = np.zeros(1 + rounds * K, np.int32)
@@ -327,7 +372,7 @@ def test_config5_256_joint(mpt_gpu, oracle):
         for r in range(rounds):
             m, _, _ = oracle.engine_step(sc.kind, sc.prm, sc.ranges, sc.steer_dt, sc.cc_dt, s, r * K, K, bvh,
                                          sc.env_tf, sc.agent_tris, ref, par, m, nthreads=THREADS)
-        st, pa = whole[s]
+        st, pa = trees[s]
         assert m == len(st)
         assert np.array_equal(st.view(np.uint64), ref[:m].view(np.uint64))
         assert np.array_equal(pa, par[:m])
