@@ -439,7 +439,16 @@ def round_roof(stages, ms):
     return out
 
 
-def roofline_of(stages, dominant, work, summ_path):
+def pmc_steady_us(summ, kernel):
+    """The dominant kernel's steady-state duration in the committed profile (scripts/pmc_summary.py
+    steady_us: the kernel trace of the same run as the counters, cold launches excluded)."""
+    for name, v in summ.items():
+        if kernel in name and v.get("steady_us"):
+            return v["steady_us"], v.get("steady_launches")
+    return None, None
+
+
+def roofline_of(stages, dominant, work, summ_path, summ=None):
     """The contract's roofline object for the dominant stage: HBM-bound unless its FP64
     fraction is the larger one (then `fp64_valu` = the FP64 VALU roof; no MFMA: FCL's operation
     order is scalar FP64)."""
@@ -455,6 +464,12 @@ def roofline_of(stages, dominant, work, summ_path):
     if st.get("frac_fp64", 0.0) > max(st["frac_hbm_compulsory"], st.get("frac_hbm_measured") or 0.0):
         out.update({"bound": "fp64_valu", "achieved": st["fp64_tflops"], "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
                     "frac": st["frac_fp64"], "note": "FP64 VALU roof (FCL's scalar operation order; no MFMA)"})
+    us, nl = pmc_steady_us(summ or {}, st["kernel"])
+    if us:
+        # the same fraction from the profile's own steady-state duration: the line's hipEvent
+        # time and the committed trace must agree
+        out.update({"profile_us_per_launch": us, "profile_launches": nl,
+                    "frac_from_profile": round(out["frac"] * st["ms"] * 1e3 / us, 4)})
     out["definition"] = ("achieved = compulsory bytes (each input and output of the launch once) / hipEvent time; "
                          "traffic = measured HBM bytes per launch (2*FETCH_SIZE + WRITE_SIZE, rocprofv3); "
                          "per-stage FP64 and LDS fractions under stages")
@@ -637,7 +652,8 @@ def run_seeds(args, world, rank, dist, torch, mpt, multiseed, scenes):
         if nn_mode == "tree":
             kernels["nn_build"] = "k_ct_dmerge"
         stages = stage_table(per_launch, cst, K, n_before, sc.dim, pmax, geo, nn_mode, kernels, summ)
-        roof = roofline_of(stages, max(stages, key=lambda s: stages[s]["ms"]) if stages else None, cst, summ_path)
+        roof = roofline_of(stages, max(stages, key=lambda s: stages[s]["ms"]) if stages else None, cst, summ_path,
+                           summ)
     else:
         # group 0: one round with the work counters on (each engine's own stages; summed over the
         # group), then one timed round: a joint round reports every stage (one launch per stage
@@ -684,7 +700,7 @@ def run_seeds(args, world, rank, dist, torch, mpt, multiseed, scenes):
                 js = {"nn_build": jt["build"], "nn_query": jt["nn"]}
                 stages.update(joint_stage_table(js, agg, K, nj, max(n_tot, 1), sc.dim, pmax, geo, summ))
         dom = "nn_query" if "nn_query" in stages else (max(stages, key=lambda k: stages[k]["ms"]) if stages else None)
-        roof = roofline_of(stages, dom, dict(agg, seeds_in_group=nj), summ_path)
+        roof = roofline_of(stages, dom, dict(agg, seeds_in_group=nj), summ_path, summ)
         if scale is not None:
             roof["stage_time_scale"] = round(scale, 4)
         roof["round"] = round_roof(stages, 1e3 * elapsed / args.steps)
@@ -783,8 +799,10 @@ def run_variants(detail=None):
 # The printed line stays well inside the driver's 8 KB stdout tail: every leg's value, time,
 # dominant roofline and digest; the full stage tables go to the detail file (--detail).
 ROOF_KEYS = ("bound", "achieved", "peak", "unit", "frac", "traffic", "traffic_over_compulsory", "frac_hbm_measured",
-             "kernel", "stage", "ms_per_launch", "algorithmic_bytes", "pmc_source", "stage_time_scale")
-LEG_ROOF_KEYS = ("bound", "achieved", "unit", "frac", "traffic_over_compulsory", "kernel", "ms_per_launch", "pmc_source")
+             "kernel", "stage", "ms_per_launch", "algorithmic_bytes", "pmc_source", "profile_us_per_launch",
+             "frac_from_profile", "stage_time_scale")
+LEG_ROOF_KEYS = ("bound", "achieved", "unit", "frac", "traffic_over_compulsory", "kernel", "ms_per_launch", "pmc_source",
+                 "profile_us_per_launch", "frac_from_profile")
 
 
 def compact_roof(roof, keys=ROOF_KEYS, stages_ms=True):
@@ -851,6 +869,7 @@ def condense(d):
     leg["config"] = d.get("config")
     leg["roofline"] = {k: roof.get(k) for k in ("bound", "achieved", "peak", "unit", "frac", "traffic", "kernel",
                                                 "stage", "ms_per_launch", "pmc_source", "stage_time_scale",
+                                                "profile_us_per_launch", "frac_from_profile",
                                                 "frac_hbm_measured", "traffic_over_compulsory", "work")
                        if k in roof}
     leg["stages"] = {s: {k: v for k, v in st.items()
@@ -1082,7 +1101,7 @@ def run_tree(args, world, rank, dist, torch, mpt, multiseed, scenes):
     summ, summ_path = pmc_summary(args.traffic, args.workload)
     stages = stage_table(per_launch, cst, K, n0, d, eng.info()["pmax"], geometry(sc, env), nn_mode, kernels, summ)
     dominant = max(stages, key=lambda s: stages[s]["ms"]) if stages else None
-    roof = roofline_of(stages, dominant, cst, summ_path)
+    roof = roofline_of(stages, dominant, cst, summ_path, summ)
     roof["round"] = round_roof(stages, 1e3 * elapsed / steps)
 
     out = {

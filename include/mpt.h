@@ -238,10 +238,11 @@ mpt_status mpt_rrt_joint_nn_ms(float *ms);
 mpt_status mpt_rrt_joint_release(void *joint_stream);
 /* Diagnostics: launch joint_stream's last joint NN launch again on that stream (same job table,
  * queries and index; its outputs are rewritten with the same values), e.g. alone after an L2
- * flush under rocprofv3 counters.  xcd_jobs = 1: every workgroup of a tree on one XCD (the
- * round-4 mapping; trees a multiple of 8) instead of each tree's workgroups over all eight.
+ * flush under rocprofv3 counters.  parts: how the launch maps trees to the 8 XCDs -- 0 = each
+ * tree's workgroups dealt over all eight; P > 0 = each tree cut into P contiguous runs of its
+ * queries, each run on one XCD (trees * P a multiple of 8; P = 1: whole trees per XCD).
  * Asynchronous. */
-mpt_status mpt_rrt_joint_replay_nn(void *joint_stream, int32_t xcd_jobs);
+mpt_status mpt_rrt_joint_replay_nn(void *joint_stream, int32_t parts);
 /* The last timed mpt_rrt_step_many on joint_stream: ms[0] = the joint tree build, ms[1] = the
  * joint NN launch (hipEvents on joint_stream).  Synchronises on it. */
 mpt_status mpt_rrt_joint_times(void *joint_stream, float ms[2]);

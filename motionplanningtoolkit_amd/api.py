@@ -432,9 +432,10 @@ def joint_release(joint_stream) -> None:
     """Free the joint state step_many keeps for joint_stream (call before the stream goes)."""
     check(lib().mpt_rrt_joint_release(_stream(joint_stream)), "mpt_rrt_joint_release")
 
-def joint_replay_nn(joint_stream, xcd_jobs: bool = False) -> None:
-    """Diagnostics: joint_stream's last joint NN launch again (same jobs; same results)."""
-    check(lib().mpt_rrt_joint_replay_nn(_stream(joint_stream), 1 if xcd_jobs else 0), "mpt_rrt_joint_replay_nn")
+def joint_replay_nn(joint_stream, parts: int = 0) -> None:
+    """Diagnostics: joint_stream's last joint NN launch again (same jobs; same results); parts:
+    0 = each tree over all eight XCDs, P > 0 = each tree in P contiguous runs, one XCD each."""
+    check(lib().mpt_rrt_joint_replay_nn(_stream(joint_stream), int(parts)), "mpt_rrt_joint_replay_nn")
 
 
 def load_mesh(path: str, which: str = "all") -> np.ndarray:

@@ -211,9 +211,10 @@ struct CtNnJob {
     double *d2;
 };
 // jobs: a device array [n_jobs], all trees of dim d, nq queries each
-// xcd_jobs: round 4's mapping, each job's workgroups on one XCD (diagnostics; n_jobs % 8 == 0)
+// parts: 0 = every job's workgroups dealt over all eight XCDs; P > 0 = each job in P contiguous
+// parts, each on one XCD (k_ct_nn1_jobs)
 void launch_ct_nn1_jobs(const CtNnJob *d_jobs, int32_t n_jobs, int32_t d, int64_t nq, hipStream_t stream,
-                        int32_t xcd_jobs = 0);
+                        int32_t parts = 0);
 void launch_ct_nn1(const CellTreeDev &T, const double *q, int64_t nq, int32_t *ids, double *d2, hipStream_t stream);
 
 }  // namespace mpt

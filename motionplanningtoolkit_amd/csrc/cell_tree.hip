@@ -1780,16 +1780,21 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(D >= 15 ? 4 
 // round 5 measured NN 0.337 -> 0.284 ms at 32 seeds, 2.111 -> 2.079 at 256 for this mapping.
 // Also measured and not kept: a job split over two XCDs when an XCD holds fewer than 8 trees --
 // its 64-bit index math spilled the 64-VGPR walk: 0.33 -> 0.37 ms at 32 seeds.)
-// xcd_jobs (diagnostics, mpt_rrt_joint_replay_nn; n_jobs a multiple of 8): round 4's mapping
-// instead, every workgroup of job j on XCD j % 8 (workgroup b runs on XCD b % 8).
+// parts > 0: each job cut into `parts` contiguous runs of its workgroups, run r of job j being
+// "part" v = j * parts + r, and part v's workgroups all on XCD v % 8 (workgroup b runs on XCD
+// b % 8; n_jobs * parts a multiple of 8, blocks_per_job a multiple of parts): a tree then lives
+// in at most `parts` XCDs' L2s, and its queries' and results' lines in
+// one XCD's.  parts = 0: workgroup b of job j on XCD b % 8 (every tree on all eight).
 template <int D, int BS, int W>
 __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(D >= 15 ? 4 : 8))) void k_ct_nn1_jobs(
-    const CtNnJob *__restrict__ jobs, int32_t n_jobs, int64_t nq, int32_t blocks_per_job, int32_t xcd_jobs) {
+    const CtNnJob *__restrict__ jobs, int32_t n_jobs, int64_t nq, int32_t blocks_per_job, int32_t parts) {
     uint32_t job = blockIdx.x / (uint32_t)blocks_per_job, blk = blockIdx.x % (uint32_t)blocks_per_job;
-    if (xcd_jobs) {
-        const uint32_t k = blockIdx.x / 8u;
-        job = blockIdx.x % 8u + 8u * (k / (uint32_t)blocks_per_job);
-        blk = k % (uint32_t)blocks_per_job;
+    if (parts > 0) {
+        const uint32_t bpp = (uint32_t)blocks_per_job / (uint32_t)parts;  // workgroups a part
+        const uint32_t k = blockIdx.x / 8u;                                // this XCD's k-th workgroup
+        const uint32_t v = blockIdx.x % 8u + 8u * (k / bpp);               // its part
+        job = v / (uint32_t)parts;
+        blk = (v % (uint32_t)parts) * bpp + k % bpp;
     }
     if (job >= (uint32_t)n_jobs) return;
     const CtNnJob J = jobs[job];  // by value: the tree's pointers stay in SGPRs across the walk
@@ -2169,27 +2174,32 @@ void launch_ct_nn1(const CellTreeDev &T, const double *q, int64_t nq, int32_t *i
 
 template <int W>
 static void launch_ct_nn1_jobs_w(const CtNnJob *d_jobs, int32_t n_jobs, int32_t d, int64_t nq, hipStream_t stream,
-                                 int32_t xcd_jobs) {
+                                 int32_t parts) {
     constexpr int BS = 64;
     const int64_t bpj = (nq * 8 * W + BS - 1) / BS;
     if (bpj * n_jobs > 0x7fffffffLL) throw Error{1, "cell tree: joint NN launch too large"};
     const dim3 grid((unsigned)(bpj * n_jobs));
     const int32_t b = (int32_t)bpj;
     switch (d) {
-        case 3: hipLaunchKernelGGL((k_ct_nn1_jobs<3, BS, W>), grid, dim3(BS), 0, stream, d_jobs, n_jobs, nq, b, xcd_jobs); break;
-        case 7: hipLaunchKernelGGL((k_ct_nn1_jobs<7, BS, W>), grid, dim3(BS), 0, stream, d_jobs, n_jobs, nq, b, xcd_jobs); break;
-        case 15: hipLaunchKernelGGL((k_ct_nn1_jobs<15, BS, W>), grid, dim3(BS), 0, stream, d_jobs, n_jobs, nq, b, xcd_jobs); break;
+        case 3: hipLaunchKernelGGL((k_ct_nn1_jobs<3, BS, W>), grid, dim3(BS), 0, stream, d_jobs, n_jobs, nq, b, parts); break;
+        case 7: hipLaunchKernelGGL((k_ct_nn1_jobs<7, BS, W>), grid, dim3(BS), 0, stream, d_jobs, n_jobs, nq, b, parts); break;
+        case 15: hipLaunchKernelGGL((k_ct_nn1_jobs<15, BS, W>), grid, dim3(BS), 0, stream, d_jobs, n_jobs, nq, b, parts); break;
         default: throw Error{1, "cell tree: state dim must be 3, 7 or 15"};
     }
     hip_check(hipGetLastError(), "k_ct_nn1_jobs launch");
 }
 
 void launch_ct_nn1_jobs(const CtNnJob *d_jobs, int32_t n_jobs, int32_t d, int64_t nq, hipStream_t stream,
-                        int32_t xcd_jobs) {
+                        int32_t parts) {
     if (nq <= 0 || n_jobs <= 0) return;
-    if (xcd_jobs && n_jobs % 8 != 0) throw Error{1, "cell tree: whole jobs per XCD need a multiple of 8 jobs"};
-    if (ct_width(d) == 8) launch_ct_nn1_jobs_w<8>(d_jobs, n_jobs, d, nq, stream, xcd_jobs);
-    else launch_ct_nn1_jobs_w<4>(d_jobs, n_jobs, d, nq, stream, xcd_jobs);
+    if (parts < 0 || parts > 64) throw Error{1, "cell tree: joint NN parts out of range"};
+    if (parts > 0) {
+        const int64_t bpj = (nq * 8 * ct_width(d) + 63) / 64;  // launch_ct_nn1_jobs_w's BS = 64
+        if ((int64_t)n_jobs * parts % 8 != 0 || bpj % parts != 0)
+            throw Error{1, "cell tree: joint NN parts need jobs * parts % 8 == 0 and a whole number of workgroups a part"};
+    }
+    if (ct_width(d) == 8) launch_ct_nn1_jobs_w<8>(d_jobs, n_jobs, d, nq, stream, parts);
+    else launch_ct_nn1_jobs_w<4>(d_jobs, n_jobs, d, nq, stream, parts);
 }
 
 }  // namespace mpt

@@ -25,6 +25,7 @@
 
 #include "../../include/mpt.h"
 #include "collide_common.h"
+#include "wave_ops.h"
 
 namespace mpt {
 
@@ -65,11 +66,9 @@ __device__ __forceinline__ float gap2f(const float alo[3], const float ahi[3], c
     return s;
 }
 
-__device__ __forceinline__ double wave_min_d(double v) {
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) v = fmin(v, __shfl_xor(v, off));
-    return v;
-}
+// the wave reductions below run on DPP / permlane exchanges (wave_ops.h): __shfl_xor's
+// ds_bpermute put an LDS round trip at each of their 6 levels, in the walk's hottest loops
+__device__ __forceinline__ double wave_min_d(double v) { return wave_min_f64_dpp(v); }
 
 struct DistCounters {
     uint32_t clusters = 0, items = 0, tri_calls = 0, pair_tests = 0;
@@ -147,9 +146,9 @@ __device__ double walk_cluster(const EnvDev &env, DistLds &s, const float cblo[3
             while (m) {
                 const int j = __ffsll((unsigned long long)m) - 1;
                 m &= m - 1;
-                if (__shfl(lb, j) > prune2(alpha * U)) continue;
-                const int32_t bf = __builtin_amdgcn_readfirstlane(__shfl(cf, j));
-                const int32_t bc = __builtin_amdgcn_readfirstlane(__shfl(cc, j));
+                if (lane_f(lb, j) > prune2(alpha * U)) continue;
+                const int32_t bf = __builtin_amdgcn_readlane(cf, j);
+                const int32_t bc = __builtin_amdgcn_readlane(cc, j);
                 int32_t seed_t = -1;
                 if (U == DBL_MAX) {
                     // first bucket of the edge: bound from one pair per agent triangle, its
@@ -240,15 +239,7 @@ __device__ double walk_cluster(const EnvDev &env, DistLds &s, const float cblo[3
             // enter the nearest surviving child now, push the others
             float v = keep ? lb : __builtin_huge_valf();
             int idx = lane;
-#pragma unroll
-            for (int off = 32; off > 0; off >>= 1) {
-                const float ov = __shfl_xor(v, off);
-                const int oi = __shfl_xor(idx, off);
-                if (ov < v || (ov == v && oi < idx)) {
-                    v = ov;
-                    idx = oi;
-                }
-            }
+            wave_argmin_f32_dpp(v, idx);
             const int j = __builtin_amdgcn_readfirstlane(idx);
             const uint64_t rest = m & ~(1ull << j);
             if (keep && lane != j) {
@@ -257,8 +248,8 @@ __device__ double walk_cluster(const EnvDev &env, DistLds &s, const float cblo[3
                 s.stk_b[pos] = lb;
             }
             sp += (int)__popcll(rest);
-            first = __builtin_amdgcn_readfirstlane(__shfl(cf, j));
-            count = __builtin_amdgcn_readfirstlane(__shfl(cc, j));
+            first = __builtin_amdgcn_readlane(cf, j);
+            count = __builtin_amdgcn_readlane(cc, j);
             lev -= 1;
             continue;
         }
@@ -339,18 +330,10 @@ __device__ void distance_unit(const EnvDev &env, const AgentDev *__restrict__ li
             // nearest remaining cluster first
             float v = (rem >> lane) & 1 ? clb : __builtin_huge_valf();
             int idx = lane;
-#pragma unroll
-            for (int off = 32; off > 0; off >>= 1) {
-                const float ov = __shfl_xor(v, off);
-                const int oi = __shfl_xor(idx, off);
-                if (ov < v || (ov == v && oi < idx)) {
-                    v = ov;
-                    idx = oi;
-                }
-            }
+            wave_argmin_f32_dpp(v, idx);
             const int j = __builtin_amdgcn_readfirstlane(idx);
             rem &= ~(1ull << j);
-            if (__shfl(clb, j) > prune2(alpha * U)) break;  // the rest are farther still
+            if (lane_f(clb, j) > prune2(alpha * U)) break;  // the rest are farther still
             if (pass == 0) first_walked |= 1ull << j;
             ++cnt.clusters;
             float cblo[3], cbhi[3];
@@ -384,14 +367,8 @@ __device__ void distance_unit(const EnvDev &env, const AgentDev *__restrict__ li
             double xlo[3], xhi[3];
 #pragma unroll
             for (int k = 0; k < 3; ++k) {
-                double lo = act ? qlo[k] : DBL_MAX, hi = act ? qhi[k] : -DBL_MAX;
-#pragma unroll
-                for (int off = 32; off > 0; off >>= 1) {
-                    lo = fmin(lo, __shfl_xor(lo, off));
-                    hi = fmax(hi, __shfl_xor(hi, off));
-                }
-                xlo[k] = uniform_d(lo);
-                xhi[k] = uniform_d(hi);
+                xlo[k] = uniform_d(wave_min_f64_dpp(act ? qlo[k] : DBL_MAX));
+                xhi[k] = uniform_d(wave_max_f64_dpp(act ? qhi[k] : -DBL_MAX));
             }
             U = walk_cluster<kOcc, kSel>(env, s, cblo, cbhi, act, qlo, qhi, xlo, xhi, lane, U, bp, cnt, alpha,
                                          pass == 1 && ((first_walked >> j) & 1) ? lo2 : -1.0);

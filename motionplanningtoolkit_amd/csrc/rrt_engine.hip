@@ -1804,12 +1804,12 @@ extern "C" mpt_status mpt_rrt_joint_stage_times(void *joint_stream, float ms[6])
 // Diagnostics: the joint stream's last NN launch again, on that stream, over the same job table
 // (its queries, its trees' index as that round's build left it, its output slots: the results are
 // rewritten with the same values) -- the NN alone for rocprofv3 counters, e.g. after an L2 flush.
-extern "C" mpt_status mpt_rrt_joint_replay_nn(void *joint_stream, int32_t xcd_jobs) {
+extern "C" mpt_status mpt_rrt_joint_replay_nn(void *joint_stream, int32_t parts) {
     return guarded([&] {
         std::shared_ptr<JointNN> g = joint_find_shared((hipStream_t)joint_stream);
         if (!g || !g->nn_jobs) throw Error{MPT_ERR_INVALID, "no joint NN launch on this stream"};
         std::lock_guard<std::mutex> lk(g->mu);
-        launch_ct_nn1_jobs(g->nn_jobs, g->nn_n, g->nn_d, g->nn_q, (hipStream_t)joint_stream, xcd_jobs);
+        launch_ct_nn1_jobs(g->nn_jobs, g->nn_n, g->nn_d, g->nn_q, (hipStream_t)joint_stream, parts);
     });
 }
 

@@ -18,6 +18,7 @@
 //      wave of the edge stops.
 #include "collide_common.h"
 #include "prm_edges.h"
+#include "wave_ops.h"
 
 namespace mpt {
 
@@ -142,8 +143,8 @@ __device__ __forceinline__ void sweep_core(const EnvDev &env, const AgentDev &ag
                 stk[kSweepStack + pos] = cc;
             }
             sp += (int)__popcll(rest);
-            first = __builtin_amdgcn_readfirstlane(__shfl(cf, j));
-            count = __builtin_amdgcn_readfirstlane(__shfl(cc, j));
+            first = __builtin_amdgcn_readlane(cf, j);  // j is uniform (a ballot's bit)
+            count = __builtin_amdgcn_readlane(cc, j);
             lev -= 1;
             continue;
         }
@@ -414,16 +415,11 @@ __device__ __forceinline__ void prm_walk(const EnvDev &env, const AgentDev &ag, 
             chi[k] = fmaxf(ahi[k], bhi[k]);
         }
     }
-    float ulo[3], uhi[3];  // their union (every lane)
+    float ulo[3], uhi[3];  // their union (uniform; DPP / permlane levels, wave_ops.h)
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
-        ulo[k] = clo[k];
-        uhi[k] = chi[k];
-#pragma unroll
-        for (int off = 32; off > 0; off >>= 1) {
-            ulo[k] = fminf(ulo[k], __shfl_xor(ulo[k], off));
-            uhi[k] = fmaxf(uhi[k], __shfl_xor(uhi[k], off));
-        }
+        ulo[k] = wave_min_dpp(clo[k]);
+        uhi[k] = wave_max_dpp(chi[k]);
     }
     bool stop = false;
     int sp = 0;
@@ -500,8 +496,8 @@ __device__ __forceinline__ void prm_walk(const EnvDev &env, const AgentDev &ag, 
                 stk[kSweepStack + pos] = cc;
             }
             sp += (int)__popcll(rest);
-            first = __builtin_amdgcn_readfirstlane(__shfl(cf, j));
-            count = __builtin_amdgcn_readfirstlane(__shfl(cc, j));
+            first = __builtin_amdgcn_readlane(cf, j);  // j is uniform (a ballot's bit)
+            count = __builtin_amdgcn_readlane(cc, j);
             lev -= 1;
             continue;
         }

@@ -45,4 +45,45 @@ __device__ __forceinline__ float wave_max_dpp(float v) {
     return wave_reduce_f32(v, [](float a, float b) { return fmaxf(a, b); });
 }
 
+template <int L>
+__device__ __forceinline__ double wave_xchg_f64(double x) {
+    const uint32_t lo = (uint32_t)__double2loint(x), hi = (uint32_t)__double2hiint(x);
+    return __hiloint2double((int)wave_xchg<L>(hi), (int)wave_xchg<L>(lo));
+}
+
+template <class Op>
+__device__ __forceinline__ double wave_reduce_f64(double v, Op op) {
+    v = op(v, wave_xchg_f64<1>(v));
+    v = op(v, wave_xchg_f64<2>(v));
+    v = op(v, wave_xchg_f64<4>(v));
+    v = op(v, wave_xchg_f64<8>(v));
+    v = op(v, wave_xchg_f64<16>(v));
+    v = op(v, wave_xchg_f64<32>(v));
+    return v;  // the same in every lane
+}
+__device__ __forceinline__ double wave_min_f64_dpp(double v) {
+    return wave_reduce_f64(v, [](double a, double b) { return fmin(a, b); });
+}
+__device__ __forceinline__ double wave_max_f64_dpp(double v) {
+    return wave_reduce_f64(v, [](double a, double b) { return fmax(a, b); });
+}
+
+// (v, idx) of the least v, ties to the least idx, in every lane
+template <int L>
+__device__ __forceinline__ void argmin_level(float &v, int &idx) {
+    const float ov = __uint_as_float(wave_xchg<L>(__float_as_uint(v)));
+    const int oi = (int)wave_xchg<L>((uint32_t)idx);
+    const bool t = ov < v || (ov == v && oi < idx);
+    v = t ? ov : v;
+    idx = t ? oi : idx;
+}
+__device__ __forceinline__ void wave_argmin_f32_dpp(float &v, int &idx) {
+    argmin_level<1>(v, idx);
+    argmin_level<2>(v, idx);
+    argmin_level<4>(v, idx);
+    argmin_level<8>(v, idx);
+    argmin_level<16>(v, idx);
+    argmin_level<32>(v, idx);
+}
+
 }  // namespace mpt

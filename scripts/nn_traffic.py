@@ -11,13 +11,12 @@ bracketed by hipEvents on the joint stream and separated by device syncs:
 
   replays (in dispatch order after the rounds' launches):
     after_round     right after the round (the round's last kernels: collide, append)
-    after_flush     after reading a 2 GiB buffer twice (L2 and the 256 MiB MALL hold clean,
-                    unrelated lines)
-    back_to_back    the same launch again at once (whatever the last launch left cached)
     after_writes    after writing 512 MiB (dirty lines of another buffer in L2 / MALL: their
                     write-back lands in whichever kernel evicts them)
-    xcd_after_flush after a flush, every workgroup of a tree on one XCD (round 4's mapping)
-    xcd_back_to_back
+    pP_flush        XCD mapping P (mpt_rrt_joint_replay_nn parts: 0 = every tree over all eight
+                    XCDs, P > 0 = each tree in P runs, one XCD each) after reading a 2 GiB buffer
+                    twice (L2 and the 256 MiB MALL hold clean, unrelated lines)
+    pP_b2b          the same launch again at once
 
 The ids and squared distances of the round are read before and after: identical.
 """
@@ -32,7 +31,13 @@ import numpy as np
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, REPO)
 
-LABELS = ["after_round", "after_flush", "back_to_back", "after_writes", "xcd_after_flush", "xcd_back_to_back"]
+
+def labels(seeds):
+    out = ["after_round", "after_writes"]
+    for p in (0, 1, 2, 4, 8):
+        if seeds * p % 8 == 0 and 4096 % max(p, 1) == 0:
+            out += [f"p{p}_flush", f"p{p}_b2b"]
+    return out
 
 
 def main():
@@ -79,15 +84,16 @@ def main():
             float(flush.sum())
 
     res = {}
+    LABELS = labels(len(engs))
     for label in LABELS:
-        if label in ("after_flush", "xcd_after_flush"):
+        if label.endswith("_flush"):
             do_flush()
         elif label == "after_writes":
             dirty.fill_(2.0)
         torch.cuda.synchronize()
         a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         a.record(joint)
-        mpt.joint_replay_nn(joint, xcd_jobs=label.startswith("xcd"))
+        mpt.joint_replay_nn(joint, parts=int(label[1:label.index("_")]) if label[0] == "p" else 0)
         b.record(joint)
         torch.cuda.synchronize()
         res[label] = round(a.elapsed_time(b), 4)

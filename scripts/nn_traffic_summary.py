@@ -7,7 +7,6 @@ import json
 import os
 import sys
 
-LABELS = ["after_round", "after_flush", "back_to_back", "after_writes", "xcd_after_flush", "xcd_back_to_back"]
 KERNEL = "k_ct_nn1_jobs"
 
 
@@ -33,11 +32,13 @@ def main(d):
         counters[name] = [float(r["Counter_Value"]) for r in rows if r["Counter_Name"] == name]
     n = len(dur)
     assert all(len(v) == n for v in counters.values()), (n, {k: len(v) for k, v in counters.items()})
+    meta = json.load(open(os.path.join(d, "replay_kt.json")))
+    LABELS = meta["replays_in_dispatch_order"]
     rounds = n - len(LABELS)
     names = [f"round_{rounds - 2}", f"round_{rounds - 1}"] + LABELS
     idx = [rounds - 2, rounds - 1] + list(range(rounds, n))
-    meta = json.load(open(os.path.join(d, "replay_kt.json")))
-    out = {"kernel": "k_ct_nn1_jobs<7, 64, 8>", "queries": meta["queries"], "nodes_indexed": meta["nodes_indexed"],
+    out = {"kernel": "k_ct_nn1_jobs<7, 64, 8>", "seeds": meta["seeds"], "queries": meta["queries"],
+           "nodes_indexed": meta["nodes_indexed"],
            "replay_ms_hipevent": meta["replay_ms"], "launches": {}}
     for name, i in zip(names, idx):
         f, w = counters["FETCH_SIZE"][i], counters["WRITE_SIZE"][i]

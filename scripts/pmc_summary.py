@@ -14,6 +14,29 @@ import shutil
 import sys
 
 
+def steady_durations(kt_csv, start=None, end=None, n_last=5):
+    """Per kernel, the mean kernel-trace duration (us) of its steady-state launches: in the
+    same dispatch window as the counters when one is given, else its last n_last launches
+    after the first (the first launch of a kernel in a process is cold: code object load,
+    first-touch of its buffers)."""
+    rows = list(csv.DictReader(open(kt_csv)))
+    for r in rows:
+        r.setdefault("Dispatch_Id", r.get("Correlation_Id", "0"))
+    rows.sort(key=lambda r: int(r["Start_Timestamp"]))
+    for i, r in enumerate(rows):
+        r["Dispatch_Id"] = str(i)  # trace order (window() sorts by it)
+    if start:
+        rows = window(rows, start, end)
+    per = collections.defaultdict(list)
+    for r in rows:
+        per[r["Kernel_Name"]].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
+    out = {}
+    for k, v in per.items():
+        use = v if start else (v[1:] if len(v) > 1 else v)[-n_last:]
+        out[k] = (round(sum(use) / len(use), 3), len(use))
+    return out
+
+
 def window(rows, start, end):
     """Dispatches from the first whose kernel name contains `start` ("last:<name>": the last
     such) up to (not including) the first after it whose name contains `end` (or the end) --
@@ -53,6 +76,13 @@ def main(src, dst, start=None, end=None):
         summ[k] = {"FETCH_SIZE_KB": round(f, 3), "WRITE_SIZE_KB": round(w, 3),
                    "hbm_bytes_per_launch": round((2 * f + w) * 1024), "launches": v.get("launches", 1)}
     json.dump(summ, open(os.path.join(dst, "pmc_summary.json"), "w"), indent=1)
+    kt = os.path.join(src, "kt", "run_kernel_trace.csv")
+    if os.path.exists(kt):
+        steady = steady_durations(kt, start, end)
+        for k, v in summ.items():
+            if k in steady:
+                v["steady_us"], v["steady_launches"] = steady[k]
+        json.dump(summ, open(os.path.join(dst, "pmc_summary.json"), "w"), indent=1)
     ks = os.path.join(src, "kt", "run_kernel_stats.csv")
     if os.path.exists(ks):
         shutil.copy(ks, os.path.join(dst, "kernel_stats.csv"))

@@ -23,28 +23,19 @@ prof c5_32 bench.py "--seeds 32 --steps 25 --warmup 5 --no-cpu" last:k_sample_jo
 prof c5_256 bench.py "--seeds 256 --steps 25 --warmup 5 --no-cpu" last:k_sample_jobs || exit 1
 prof prm scripts/bench_prm.py "--reps 1 --no-cpu" last:k_sort_segments || exit 1
 prof distance scripts/bench_distance.py "--steps 3 --warmup 1 --no-cpu" || exit 1
-# the tree walk's instruction and wait counters (one pass: 5 SQ counters)
-timeout -s KILL 200 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_BUSY_CYCLES --output-format csv \
-  -d $R/gpurun_out/prof_${TAG}_sq -o run -- python3 bench.py --seeds 256 --steps 25 --warmup 5 --no-cpu > $OUT/sq.log 2>&1 || exit 1
-python - $R/gpurun_out/prof_${TAG}_sq/run_counter_collection.csv $OUT/sq_ct_nn1_jobs.json <<'PY'
-import csv, json, sys, collections
-rows = [r for r in csv.DictReader(open(sys.argv[1])) if "k_ct_nn1_jobs" in r["Kernel_Name"]]
-rows.sort(key=lambda r: int(r["Dispatch_Id"]))
-last = max(int(r["Dispatch_Id"]) for r in rows)
-agg = collections.defaultdict(float)
-for r in rows:
-    if int(r["Dispatch_Id"]) == last:
-        agg[r["Counter_Name"]] += float(r["Counter_Value"])
-out = {"kernel": "k_ct_nn1_jobs<7, 64, 8> (the last joint round of bench.py --seeds 256 --steps 25 --warmup 5)",
-       "queries": 256 * 4096, **agg}
-q = out["queries"]
-if agg.get("SQ_INSTS_VALU"):
-    # SQ_INSTS_VALU counts wave instructions; one query is one wave
-    out["valu_instructions_per_query"] = agg["SQ_INSTS_VALU"] / q
-if agg.get("SQ_WAVE_CYCLES"):
-    out["wait_any_over_wave_cycles"] = agg.get("SQ_WAIT_ANY", 0) / agg["SQ_WAVE_CYCLES"]
-json.dump(out, open(sys.argv[2], "w"), indent=1)
-print(json.dumps(out))
-PY
-rm -f $R/gpurun_out/prof_${TAG}_sq/run_counter_collection.csv.bak
+# SQ counters of the kernels the verdict asks about (one pass each, 8 SQ counters): wait / issue
+# split (the guide: WAIT_ANY + WAIT_INST_ANY + ACTIVE_INST_ANY ~= WAVE_CYCLES)
+SQ="SQ_WAVES SQ_INSTS_VALU SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_BUSY_CYCLES"
+sq() {  # name kernel mode units script args...
+  local name=$1 kern=$2 mode=$3 units=$4 script=$5; shift 5
+  timeout -s KILL 240 rocprofv3 --pmc $SQ --output-format csv -d $R/gpurun_out/prof_${TAG}_sq_$name -o run -- python3 $R/$script "$@" > $OUT/sq_$name.log 2>&1 || return 1
+  python3 scripts/sq_summary.py $R/gpurun_out/prof_${TAG}_sq_$name/run_counter_collection.csv $OUT/sq_$name.json "$kern" $mode $units > /dev/null || return 1
+  rm -f $R/gpurun_out/prof_${TAG}_sq_$name/run_counter_collection.csv
+  echo "sq $name done"
+}
+sq ct_nn1_jobs k_ct_nn1_jobs last 1048576 bench.py --seeds 256 --steps 25 --warmup 5 --no-cpu || exit 1
+sq grid_nn1 k_grid_nn1_runs_sorted all 65536 bench.py --steps 5 --warmup 2 --no-cpu --no-variants || exit 1
+sq cands_room k_cands all "" bench.py --workload blimp-room --steps 5 --warmup 2 --no-cpu --no-variants || exit 1
+sq distance k_distance all 65536 scripts/bench_distance.py --steps 3 --warmup 1 --no-cpu || exit 1
+sq sweep_prm "k_sweep_prm<1024>" all "" scripts/bench_prm.py --reps 1 --no-cpu || exit 1
 echo profile_all done
