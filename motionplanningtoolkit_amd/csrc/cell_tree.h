@@ -211,10 +211,13 @@ struct CtNnJob {
     double *d2;
 };
 // jobs: a device array [n_jobs], all trees of dim d, nq queries each
-// parts: 0 = every job's workgroups dealt over all eight XCDs; P > 0 = each job in P contiguous
-// parts, each on one XCD (k_ct_nn1_jobs)
+// parts: 0 = every job's workgroups dealt over all eight XCDs one by one; P > 0 = each job in P
+// contiguous parts, each on one XCD (k_ct_nn1_jobs); kCtJointParts: the engine's choice
+constexpr int32_t kCtJointParts = 8;
 void launch_ct_nn1_jobs(const CtNnJob *d_jobs, int32_t n_jobs, int32_t d, int64_t nq, hipStream_t stream,
-                        int32_t parts = 0);
+                        int32_t parts);
+// kCtJointParts when the launch's shape allows it, else 0
+int32_t ct_joint_parts(int32_t n_jobs, int32_t d, int64_t nq);
 void launch_ct_nn1(const CellTreeDev &T, const double *q, int64_t nq, int32_t *ids, double *d2, hipStream_t stream);
 
 }  // namespace mpt

@@ -1773,18 +1773,22 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(D >= 15 ? 4 
 }
 
 // Many trees in one launch (mpt_rrt_step_many: one engine per independent seed): job j takes
-// workgroups [j * bpj, (j + 1) * bpj), so consecutive workgroups of a job land on the 8 XCDs in
-// turn and every XCD gets an equal share of every job.  (Round 4 dealt whole jobs to XCDs --
-// job j on XCD j % 8, its tree in that XCD's L2 -- but a tree is larger than an XCD's 4 MB L2,
-// and with 4 jobs an XCD (32 seeds) the XCD with the costliest trees set the kernel's end:
-// round 5 measured NN 0.337 -> 0.284 ms at 32 seeds, 2.111 -> 2.079 at 256 for this mapping.
-// Also measured and not kept: a job split over two XCDs when an XCD holds fewer than 8 trees --
-// its 64-bit index math spilled the 64-VGPR walk: 0.33 -> 0.37 ms at 32 seeds.)
-// parts > 0: each job cut into `parts` contiguous runs of its workgroups, run r of job j being
-// "part" v = j * parts + r, and part v's workgroups all on XCD v % 8 (workgroup b runs on XCD
-// b % 8; n_jobs * parts a multiple of 8, blocks_per_job a multiple of parts): a tree then lives
-// in at most `parts` XCDs' L2s, and its queries' and results' lines in
-// one XCD's.  parts = 0: workgroup b of job j on XCD b % 8 (every tree on all eight).
+// workgroups [j * bpj, (j + 1) * bpj) (one query a workgroup), and workgroup b runs on XCD b % 8.
+// parts = 0: consecutive workgroups of a job on the 8 XCDs in turn -- every XCD an equal share of
+// every tree, but each 64-B line of a job's queries and of its results touched by up to eight
+// XCDs' L2s.  parts = P > 0: job j cut into P contiguous runs of its workgroups, run r being part
+// v = j * P + r, part v's workgroups all on XCD v % 8: a tree then lives in P XCDs' L2s, its
+// queries' and results' lines in one (n_jobs * P a multiple of 8, bpj a multiple of P).  The
+// engine runs P = 8 (kCtJointParts): each XCD a contiguous eighth of every tree's queries.
+// Measured at the config-5 shape (scripts/nn_traffic.py: the last round's launch replayed alone,
+// 256 trees, 28.3 M points indexed, 1 M queries; kernel trace / HBM bytes 2 FETCH + WRITE):
+//   P = 0: 2.33 ms, 1271 MB (WRITE 68 MB for 12.6 MB of results);  P = 1 (round 4's whole
+//   trees per XCD): 2.27 ms, 267 MB;  P = 2: 2.22 ms, 409 MB;  P = 4: 2.16 ms, 651 MB;
+//   P = 8: 2.12 ms, 1078 MB (WRITE 13.4 MB)
+// -- what costs time is balance and the split lines, not the bytes (the trees' lines come
+// from the MALL).  Also measured (rounds 4-5) and not kept: P = 1 at 32 seeds (0.337 vs 0.284
+// ms: with 4 trees an XCD the costliest set the end), and a 64-bit form of the index math that
+// spilled the 64-VGPR walk.
 template <int D, int BS, int W>
 __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(D >= 15 ? 4 : 8))) void k_ct_nn1_jobs(
     const CtNnJob *__restrict__ jobs, int32_t n_jobs, int64_t nq, int32_t blocks_per_job, int32_t parts) {
@@ -2187,6 +2191,11 @@ static void launch_ct_nn1_jobs_w(const CtNnJob *d_jobs, int32_t n_jobs, int32_t 
         default: throw Error{1, "cell tree: state dim must be 3, 7 or 15"};
     }
     hip_check(hipGetLastError(), "k_ct_nn1_jobs launch");
+}
+
+int32_t ct_joint_parts(int32_t n_jobs, int32_t d, int64_t nq) {
+    const int64_t bpj = (nq * 8 * ct_width(d) + 63) / 64;
+    return ((int64_t)n_jobs * kCtJointParts % 8 == 0 && bpj % kCtJointParts == 0) ? kCtJointParts : 0;
 }
 
 void launch_ct_nn1_jobs(const CtNnJob *d_jobs, int32_t n_jobs, int32_t d, int64_t nq, hipStream_t stream,

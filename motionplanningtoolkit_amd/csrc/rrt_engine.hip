@@ -1569,7 +1569,7 @@ void joint_round(mpt_rrt *const *rs, int32_t n, int32_t K, void *const *streams_
         }
     mark(2);
     if (timed) hip_check(hipEventRecord(g.t0, joint), "joint t0");
-    launch_ct_nn1_jobs(dn, n, d, K, joint);
+    launch_ct_nn1_jobs(dn, n, d, K, joint, ct_joint_parts(n, d, K));
     g.nn_jobs = dn;
     g.nn_n = n;
     g.nn_d = d;
@@ -1724,7 +1724,7 @@ extern "C" mpt_status mpt_rrt_step_many(mpt_rrt *const *rs, int32_t n, int32_t K
                 for (hipStream_t s : uniq) hip_check(hipStreamWaitEvent(s, g.built, 0), "built wait");
                 for (int32_t i : J) cs[i].mark(2, stream_of(i));
             }
-            launch_ct_nn1_jobs(dn, nj, rs[J[0]]->p.d, K, joint);
+            launch_ct_nn1_jobs(dn, nj, rs[J[0]]->p.d, K, joint, ct_joint_parts(nj, rs[J[0]]->p.d, K));
             g.nn_jobs = dn;
             g.nn_n = nj;
             g.nn_d = rs[J[0]]->p.d;

@@ -597,3 +597,47 @@ def test_joint_round_matches_single_steps(mpt_gpu):
         assert np.array_equal(bits(pa[0]), bits(pb[0])) and np.array_equal(pa[1], pb[1])
     assert set(times) == {"sample", "nn_build", "nn_query", "steer", "collide", "append"}
     assert all(v > 0 for v in times.values())
+
+
+def test_joint_nn_xcd_mappings_same_ids(mpt_gpu, oracle):
+    """The joint NN launch under every XCD mapping (k_ct_nn1_jobs parts: 0 = each tree's
+    workgroups over all eight XCDs, P = 1, 2, 4, 8 = each tree in P contiguous runs, one XCD
+    each; mpt_rrt_joint_replay_nn) writes the same ids and squared distances -- which workgroup
+    answers a query changes nothing -- and they are the exact 1-NN of the oracle's kd-tree over
+    the index the round queried (flannkdtreewrapper.hpp:57-89)."""
+    import torch
+
+    sc = scenes.blimp_scenario("all")
+    root = np.array([[88.6, 68.9, 57.1, 0, 0, 0, 0.0]])
+    env = mpt_gpu.Environment(sc.env_tris, sc.env_tf)
+    ag = mpt_gpu.AgentMesh(sc.agent_tris)
+    K, rounds, n = 1024, 4, 16
+    engs = []
+    for s in range(700, 700 + n):
+        e = mpt_gpu.RRTEngine(env, ag, sc.kind, sc.prm, sc.ranges, sc.steer_dt, sc.cc_dt, 1 + rounds * K, s)
+        e.add_nodes(root)
+        e.set_nn("tree")
+        engs.append(e)
+    js = torch.cuda.Stream()
+    sizes = []
+    for r in range(rounds):
+        if r == rounds - 1:
+            torch.cuda.synchronize()
+            sizes = [e.counters()["nodes"] for e in engs]  # the last round's index
+        mpt_gpu.step_many(engs, K, [js] * n, js)
+    torch.cuda.synchronize()
+    base = [e.last_round(K) for e in engs]
+    for parts in (0, 1, 2, 4, 8, 0):
+        mpt_gpu.joint_replay_nn(js, parts)
+        torch.cuda.synchronize()
+        for e, b in zip(engs, base):
+            assert np.array_equal(e.last_round(K)[1], b[1]), parts
+    with pytest.raises(mpt_gpu.MptError):
+        mpt_gpu.joint_replay_nn(js, 3)  # a tree's 1024 workgroups do not split into 3 runs
+    for j in (0, n - 1):
+        tree, _ = engs[j].read_tree(sizes[j])
+        ref, _ = oracle.KDTree(tree).knn(base[j][0], 1)
+        assert np.array_equal(base[j][1], ref[:, 0])
+    for e in engs:
+        e.close()
+    mpt_gpu.joint_release(js)
