@@ -1712,6 +1712,9 @@ __device__ __forceinline__ void ct_walk(const CellTreeDev &T, const double *__re
                     const int32_t id = (int32_t)meta;
                     ++n_pts;
                     better = (dd < bd) | ((dd == bd) & (id < bi));
+                    // G = 64: the lane's own best may trail the wave's; only a point within the
+                    // shared bound can move it
+                    if constexpr (G == 64) better = better && dd <= (double)bdf;
                     nn_take(bd, bi, dd, id);
                 } else {
                     float bx[2 * D];
@@ -1730,8 +1733,18 @@ __device__ __forceinline__ void ct_walk(const CellTreeDev &T, const double *__re
             // lanes already share one best unless a lane found a better point this step, and
             // with no survivor in the wave there is nothing to rank
             if (__ballot(better)) {
-                best_group<G>(bd, bi);
-                bdf = f32_up(bd);
+                if constexpr (G == 64) {
+                    // one query a wave: each lane keeps its own exact best (bd, bi) and only the
+                    // pruning bound is shared -- the least of the lanes' bests rounded up to float,
+                    // which is f32_up of the wave's best (f32_up is monotone), the bound the full
+                    // (d2, id) merge gave: the same boxes are pruned, the same points examined,
+                    // and the exact merge runs once, after the walk (one wave minimum a step that
+                    // improves, where best_group took two plus the id's)
+                    bdf = __uint_as_float(wave_min_u32(__float_as_uint(f32_up(bd))));
+                } else {
+                    best_group<G>(bd, bi);
+                    bdf = f32_up(bd);
+                }
             }
             keep = keep && lbf <= bdf;
             const uint64_t wm = __ballot(keep);
@@ -1760,6 +1773,7 @@ __device__ __forceinline__ void ct_walk(const CellTreeDev &T, const double *__re
             atomicAdd(T.stats + 3, (unsigned long long)n_steps);  // (+ 2: the collide counters' [10])
         }
     }
+    if constexpr (G == 64) best_group<G>(bd, bi);  // the lanes' own bests (see the walk's merge)
     if (sub == 0) {
         out_ids[qi] = bi;
         out_d2[qi] = bd;

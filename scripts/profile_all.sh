@@ -1,5 +1,6 @@
 #!/bin/bash
-# Usage: TAG=r21 bash scripts/profile_all.sh
+# Usage: TAG=r21 bash scripts/profile_all.sh [steps...]   (steps: c2 room snake c5_32 c5_256 prm
+#        distance sq; default all -- split them over two calls to stay inside one call's limit)
 # On the GPU box: rocprofv3 kernel trace + FETCH_SIZE + WRITE_SIZE passes (scripts/profile.sh)
 # over every workload the bench line reports, summarised into gpurun_out/profiles_$TAG/<sub>/
 # (pmc_summary.json = HBM bytes per launch, kernel_stats.csv), plus the SQ counters of config
@@ -16,13 +17,16 @@ prof() {  # name script args window...
   rm -rf $R/gpurun_out/prof_${TAG}_$name/kt/*_kernel_trace.csv
   echo "$name done"
 }
-prof c2 bench.py "--steps 5 --warmup 2 --no-cpu --no-variants" || exit 1
-prof room bench.py "--workload blimp-room --steps 5 --warmup 2 --no-cpu --no-variants" || exit 1
-prof snake bench.py "--workload snake --steps 5 --warmup 2 --no-cpu --no-variants" || exit 1
-prof c5_32 bench.py "--seeds 32 --steps 25 --warmup 5 --no-cpu" last:k_sample_jobs || exit 1
-prof c5_256 bench.py "--seeds 256 --steps 25 --warmup 5 --no-cpu" last:k_sample_jobs || exit 1
-prof prm scripts/bench_prm.py "--reps 1 --no-cpu" last:k_sort_segments || exit 1
-prof distance scripts/bench_distance.py "--steps 3 --warmup 1 --no-cpu" || exit 1
+STEPS=("$@"); [ ${#STEPS[@]} -eq 0 ] && STEPS=(c2 room snake c5_32 c5_256 prm distance sq)
+want() { local x; for x in "${STEPS[@]}"; do [ "$x" = "$1" ] && return 0; done; return 1; }
+if want c2; then prof c2 bench.py "--steps 5 --warmup 2 --no-cpu --no-variants" || exit 1; fi
+if want room; then prof room bench.py "--workload blimp-room --steps 5 --warmup 2 --no-cpu --no-variants" || exit 1; fi
+if want snake; then prof snake bench.py "--workload snake --steps 5 --warmup 2 --no-cpu --no-variants" || exit 1; fi
+if want c5_32; then prof c5_32 bench.py "--seeds 32 --steps 25 --warmup 5 --no-cpu" last:k_sample_jobs || exit 1; fi
+if want c5_256; then prof c5_256 bench.py "--seeds 256 --steps 25 --warmup 5 --no-cpu" last:k_sample_jobs || exit 1; fi
+if want prm; then prof prm scripts/bench_prm.py "--reps 1 --no-cpu" last:k_sort_segments || exit 1; fi
+if want distance; then prof distance scripts/bench_distance.py "--steps 3 --warmup 1 --no-cpu" || exit 1; fi
+want sq || { echo profile_all done; exit 0; }
 # SQ counters of the kernels the verdict asks about (one pass each, 8 SQ counters): wait / issue
 # split (the guide: WAIT_ANY + WAIT_INST_ANY + ACTIVE_INST_ANY ~= WAVE_CYCLES)
 SQ="SQ_WAVES SQ_INSTS_VALU SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_BUSY_CYCLES"
