@@ -459,7 +459,7 @@ def roofline_of(stages, dominant, work, summ_path, summ=None):
     out = {"bound": "hbm", "achieved": st["compulsory_gbs"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
            "frac": st["frac_hbm_compulsory"], "traffic": st.get("traffic"), "traffic_gbs": st.get("traffic_gbs"),
            "frac_hbm_measured": st.get("frac_hbm_measured"), "traffic_over_compulsory": st.get("traffic_over_compulsory"),
-           "kernel": st["kernel"], "stage": dominant, "ms_per_launch": st.get("ms_event_free", st["ms"]),
+           "kernel": st["kernel"], "stage": dominant, "ms_per_launch": st["ms"],
            "algorithmic_bytes": st["compulsory_bytes"], "pmc_source": summ_path}
     if st.get("frac_fp64", 0.0) > max(st["frac_hbm_compulsory"], st.get("frac_hbm_measured") or 0.0):
         out.update({"bound": "fp64_valu", "achieved": st["fp64_tflops"], "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
@@ -469,7 +469,7 @@ def roofline_of(stages, dominant, work, summ_path, summ=None):
         # the same fraction from the profile's own steady-state duration: the line's hipEvent
         # time and the committed trace must agree
         out.update({"profile_us_per_launch": us, "profile_launches": nl,
-                    "frac_from_profile": round(out["frac"] * st.get("ms_event_free", st["ms"]) * 1e3 / us, 4)})
+                    "frac_from_profile": round(out["frac"] * st["ms"] * 1e3 / us, 4)})
     out["definition"] = ("achieved = compulsory bytes (each input and output of the launch once) / hipEvent time; "
                          "traffic = measured HBM bytes per launch (2*FETCH_SIZE + WRITE_SIZE, rocprofv3); "
                          "per-stage FP64 and LDS fractions under stages")
@@ -676,16 +676,14 @@ def run_seeds(args, world, rank, dist, torch, mpt, multiseed, scenes):
             jst = None
         if jst is not None:
             stages = joint_stage_table(jst, agg, K, nj, max(n_tot, 1), sc.dim, pmax, geo, summ)
-            # event-free stage times: a recorded round carries seven event packets; when the
-            # stages sum to more than a timed round, scale them to it
+            # event-free stage times (information only): a recorded round carries seven event
+            # packets; when the stages sum to more than a timed round, scaled to it.  The rates
+            # and fractions stay on the measured stage times -- the durations a kernel trace of
+            # the same round shows (the committed profiles' steady_us), so they can be checked
             tot = sum(st["ms"] for st in stages.values())
             scale = min(1.0, (1e3 * elapsed / args.steps) / tot) if tot > 0 else 1.0
             for st in stages.values():
                 st["ms_event_free"] = round(st["ms"] * scale, 4)
-                for key in ("compulsory_gbs", "frac_hbm_compulsory", "traffic_gbs", "frac_hbm_measured",
-                            "fp64_tflops", "frac_fp64"):
-                    if key in st:
-                        st[key] = round(st[key] / scale, 4)
         else:
             try:
                 jt = mpt.joint_times(js0)

@@ -1634,6 +1634,145 @@ __device__ __forceinline__ void ct_seed(const CellTreeDev &T, const double (&qq)
     best_group<G>(bd, bi);
 }
 
+// One query a wave (8 entries a step, 8 lanes an entry) over two stacks in the one LDS array:
+// inner entries growing up from slot 0, buckets growing down from the last slot.  A step pops
+// from one stack only -- buckets when 8 wait or no inner entry is left, else inner entries --
+// so every step runs one kind's code: a bucket step the points' exact distances (no push), an
+// inner step the children's float lower bounds and their pushes (no merge).  The one-stack walk
+// popped the top 8 entries whatever their kinds and ran both paths in most steps (SQ counters
+// at the config-5 shape: the walk issue-bound, ACTIVE_INST_VALU x 8 waves ~1.06 of a SIMD).
+// Bounds: an inner step pops <= 8 and pushes <= 64 inner children, so the inner stack holds
+// <= 8 + 56 a level over <= 9 inner levels (512); buckets are popped whenever 8 wait, so the
+// bucket stack holds < 8 + 64: together <= 584 of the 640 slots.  Which entries a step takes
+// changes the order of the walk only: every box whose float lower bound exceeds the shared bound
+// (f32_up of the best so far, an upper bound of the final best) is skipped, every other bucket's
+// points are examined, and the exact (d2, id) merge of the lanes' bests runs once at the end.
+constexpr int kCtSplitStack = 8 * 8 * kCtMaxLevels;
+constexpr bool kCtSplitWalk = true;  // ct_walk's 8-entry form (the one-stack walk otherwise)
+template <int D, int BS>
+__device__ __forceinline__ void ct_walk_split(const CellTreeDev &T, const double *__restrict__ q, int64_t nq,
+                                              int32_t *__restrict__ out_ids, double *__restrict__ out_d2,
+                                              int64_t blk) {
+    constexpr int G = 64;
+    constexpr int kStack = kCtSplitStack;
+    __shared__ uint2 s_stk[BS / G][kStack];  // (code, lower bound's bits)
+    const int64_t t = blk * BS + threadIdx.x;
+    const int64_t qi = t / G;
+    const int sub = (int)(t % G);
+    const int part = sub / 8;
+    const int ls = sub % 8;
+    const int grp = threadIdx.x / G;
+    if (qi >= nq) return;  // whole waves leave together
+    double qq[D];
+#pragma unroll
+    for (int i = 0; i < D; ++i) qq[i] = q[qi * D + i];
+    float qlo[D], qhi[D];
+#pragma unroll
+    for (int i = 0; i < D; ++i) {
+        qlo[i] = f32_dn(qq[i]);
+        qhi[i] = f32_up_any(qq[i]);
+    }
+    double bd = __builtin_huge_val();
+    int32_t bi = -1;
+    uint32_t n_pts = 0, n_box = 0, n_steps = 1;  // the seeds' step
+    uint2 *stk = s_stk[grp];
+    const uint64_t below_me = (1ull << sub) - 1ull;
+    if (*T.n_dev > 0) {
+        const int n_top = *(const __attribute__((address_space(1))) int32_t *)T.n_top;
+        const uint32_t top = sub < 8 ? ((gu32)T.top)[sub] : 0u;
+        ct_seed<D, G>(T, qq, sub, bd, bi, n_pts);
+        float bdf = f32_up(bd);
+        int isp = 0, lsp = 0;  // inner entries [0, isp), buckets [kStack - lsp, kStack)
+        {
+            const bool in = sub < n_top;
+            const bool lf = in && (top & kCtLeafBit);
+            const uint64_t ml = __ballot(lf), mi = __ballot(in && !lf);
+            if (lf) stk[kStack - 1 - __popcll(ml & below_me)] = make_uint2(top, 0u);
+            if (in && !lf) stk[__popcll(mi & below_me)] = make_uint2(top, 0u);
+            lsp = __popcll(ml);
+            isp = __popcll(mi);
+        }
+        __builtin_amdgcn_wave_barrier();
+        while (isp + lsp > 0) {
+            const bool leaves = lsp >= 8 || isp == 0;  // wave-uniform
+            const int avail = leaves ? lsp : isp;
+            const int np = avail >= 8 ? 8 : avail;
+            const bool have = part < np;
+            uint32_t code = 0;
+            float lbs = 0.0f;
+            if (have) {
+                const uint2 en = leaves ? stk[kStack - lsp + part] : stk[isp - 1 - part];
+                code = en.x;
+                lbs = __uint_as_float(en.y);
+            }
+            if (leaves) lsp -= np;
+            else isp -= np;
+            ++n_steps;
+            __builtin_amdgcn_wave_barrier();
+            const bool act = have && !(lbs > bdf) && ls < (int)((code >> 28) & 7u) + 1;
+            if (leaves) {
+                bool better = false;
+                if (act) {
+                    const int64_t e = (int64_t)(code & 0x0fffffffu) * kCtCap + ls;
+                    double row[D];
+#pragma unroll
+                    for (int k = 0; k < D; ++k) row[k] = ((gdbl)T.bpts)[e * D + k];
+                    const int32_t id = (int32_t)((gu32)(const void *)T.bids)[e];
+                    const double dd = flann_l2<D>(qq, row);
+                    ++n_pts;
+                    better = ((dd < bd) | ((dd == bd) & (id < bi))) && dd <= (double)bdf;
+                    nn_take(bd, bi, dd, id);
+                }
+                if (__ballot(better)) bdf = __uint_as_float(wave_min_u32(__float_as_uint(f32_up(bd))));
+            } else {
+                bool keep = false;
+                uint32_t child = 0;
+                float lbf = 0.0f;
+                if (act) {
+                    const int64_t e = (int64_t)(code & 0x0fffffffu) + ls;
+                    double row[D];
+#pragma unroll
+                    for (int k = 0; k < D; ++k) row[k] = ((gdbl)(const void *)T.nbox)[e * D + k];
+                    child = ((gu32)T.nmeta)[e];
+                    float bx[2 * D];
+#pragma unroll
+                    for (int k = 0; k < D; ++k) {
+                        bx[2 * k] = __int_as_float(__double2loint(row[k]));
+                        bx[2 * k + 1] = __int_as_float(__double2hiint(row[k]));
+                    }
+                    lbf = ct_box_lb<D>(bx, qq, qlo, qhi);
+                    keep = lbf <= bdf;
+                    ++n_box;
+                }
+                const bool kl = keep && (child & kCtLeafBit), ki = keep && !(child & kCtLeafBit);
+                const uint64_t ml = __ballot(kl), mi = __ballot(ki);
+                if (kl) stk[kStack - 1 - (lsp + __popcll(ml & below_me))] = make_uint2(child, __float_as_uint(lbf));
+                if (ki) stk[isp + __popcll(mi & below_me)] = make_uint2(child, __float_as_uint(lbf));
+                lsp += __popcll(ml);
+                isp += __popcll(mi);
+            }
+            __builtin_amdgcn_wave_barrier();
+        }
+    }
+    if (T.stats) {
+#pragma unroll
+        for (int off = G / 2; off > 0; off >>= 1) {
+            n_pts += __shfl_xor(n_pts, off, G);
+            n_box += __shfl_xor(n_box, off, G);
+        }
+        if (sub == 0) {
+            atomicAdd(T.stats + 0, (unsigned long long)n_pts);
+            atomicAdd(T.stats + 1, (unsigned long long)n_box);
+            atomicAdd(T.stats + 3, (unsigned long long)n_steps);
+        }
+    }
+    best_group<G>(bd, bi);  // the lanes' own bests
+    if (sub == 0) {
+        out_ids[qi] = bi;
+        out_d2[qi] = bd;
+    }
+}
+
 // NW nodes a step: 8 * NW lanes per query, the stack's top NW entries popped together (each
 // taken by 8 lanes: a bucket's points or an inner box's 8 children); the parts' best merged,
 // the children re-tested against it, deeper entries' survivors pushed below the top's (each
@@ -1643,6 +1782,10 @@ __device__ __forceinline__ void ct_seed(const CellTreeDev &T, const double (&qq)
 template <int D, int BS, int NW>
 __device__ __forceinline__ void ct_walk(const CellTreeDev &T, const double *__restrict__ q, int64_t nq,
                                         int32_t *__restrict__ out_ids, double *__restrict__ out_d2, int64_t blk) {
+    if constexpr (NW == 8 && D <= 7 && kCtSplitWalk) {
+        ct_walk_split<D, BS>(T, q, nq, out_ids, out_d2, blk);
+        return;
+    }
     constexpr int G = NW * 8;        // lanes per query
     constexpr int kStack = NW * 8 * kCtMaxLevels;  // ~NW blocks of 7 a level, <= 10 levels (k_ct_levels): 5 KiB for NW = 8
     static_assert(G <= 64, "ballot bits per group");

@@ -14,11 +14,12 @@ import shutil
 import sys
 
 
-def steady_durations(kt_csv, start=None, end=None, n_last=5):
-    """Per kernel, the mean kernel-trace duration (us) of its steady-state launches: in the
-    same dispatch window as the counters when one is given, else its last n_last launches
-    after the first (the first launch of a kernel in a process is cold: code object load,
-    first-touch of its buffers)."""
+def steady_durations(kt_csv, start=None, end=None):
+    """Per kernel, the kernel-trace duration (us) of its steady-state launches: the mean over
+    the same dispatch window as the counters when one is given (config 5: the last joint round),
+    else the median of its launches after the first -- the first launch of a kernel in a process
+    is cold (code object load, first touch of its buffers), and a bench's untimed work-counter
+    round (same-address atomics: config 2's grid NN 405 us against 34) is one outlier."""
     rows = list(csv.DictReader(open(kt_csv)))
     for r in rows:
         r.setdefault("Dispatch_Id", r.get("Correlation_Id", "0"))
@@ -32,8 +33,11 @@ def steady_durations(kt_csv, start=None, end=None, n_last=5):
         per[r["Kernel_Name"]].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
     out = {}
     for k, v in per.items():
-        use = v if start else (v[1:] if len(v) > 1 else v)[-n_last:]
-        out[k] = (round(sum(use) / len(use), 3), len(use))
+        if start:
+            out[k] = (round(sum(v) / len(v), 3), len(v))
+        else:
+            use = sorted(v[1:] if len(v) > 1 else v)
+            out[k] = (round(use[len(use) // 2], 3), len(use))
     return out
 
 

@@ -14,7 +14,6 @@ prof() {  # name script args window...
   local name=$1 script=$2 args=$3; shift 3
   SCRIPT=$script BENCH_ARGS="$args" bash scripts/profile.sh ${TAG}_$name || return 1
   python scripts/pmc_summary.py $R/gpurun_out/prof_${TAG}_$name $OUT/$name "$@" > /dev/null || return 1
-  rm -rf $R/gpurun_out/prof_${TAG}_$name/kt/*_kernel_trace.csv
   echo "$name done"
 }
 STEPS=("$@"); [ ${#STEPS[@]} -eq 0 ] && STEPS=(c2 room snake c5_32 c5_256 prm distance sq)
@@ -41,5 +40,5 @@ sq ct_nn1_jobs k_ct_nn1_jobs last 1048576 bench.py --seeds 256 --steps 25 --warm
 sq grid_nn1 k_grid_nn1_runs_sorted all 65536 bench.py --steps 5 --warmup 2 --no-cpu --no-variants || exit 1
 sq cands_room k_cands all "" bench.py --workload blimp-room --steps 5 --warmup 2 --no-cpu --no-variants || exit 1
 sq distance k_distance all 65536 scripts/bench_distance.py --steps 3 --warmup 1 --no-cpu || exit 1
-sq sweep_prm "k_sweep_prm<1024>" all "" scripts/bench_prm.py --reps 1 --no-cpu || exit 1
+sq sweep_prm "k_sweep_prm<1024" all "" scripts/bench_prm.py --reps 1 --no-cpu || exit 1
 echo profile_all done
