@@ -55,6 +55,10 @@ struct CtCounts {
     // query's first step tests the root's grandchildren -- one walk step fewer (k_ct_levels)
     uint32_t top[8];
     int32_t n_top;
+    // the two-stack walk's first entries: the nodes [lv_first, lv_first + lv_n) of the lowest
+    // level of at most 64 nodes, their boxes tested in the seeds' step (k_ct_levels)
+    int32_t lv_first;
+    int32_t lv_n;
     int32_t pad;
 };
 
@@ -71,6 +75,7 @@ struct CellTreeDev {
     const int32_t *root;       // the root node (in the tree's CtCounts)
     const uint32_t *top;       // the walk's first entries (CtCounts top / n_top)
     const int32_t *n_top;
+    const int32_t *lv;         // CtCounts lv_first, lv_n (the two-stack walk's first entries)
     const uint32_t *nmeta;     // [nodes]
     const float *nbox;         // [nodes][d][2] widened float bounds: (lo, -hi) a dim
     const double *bpts;        // [buckets][kCtCap][d]

@@ -1256,6 +1256,18 @@ __global__ __launch_bounds__(kCtLevelThreads) void k_ct_levels(CtJobs js) {
     }
     if (t != 0) return;
     CtCounts *c = J.cnt;
+    {
+        // the lowest level of at most 64 nodes (levels are contiguous: 1 = the directory, then
+        // levels 2 and 3 as k_ct_lgroup counted them, then runs of 8)
+        int64_t s = 0, m = n1;
+        for (int k = 0; m > 64; ++k) {
+            const int64_t next = k == 0 ? c->n_l2 : (k == 1 ? c->n_l3 : (m + 7) / 8);
+            s += m;
+            m = next;
+        }
+        c->lv_first = (int32_t)s;
+        c->lv_n = (int32_t)m;
+    }
     const int32_t nn = c->n_new_dir;
     c->root = (int32_t)ls;
     c->n_dir += nn;
@@ -1678,17 +1690,37 @@ __device__ __forceinline__ void ct_walk_split(const CellTreeDev &T, const double
     uint2 *stk = s_stk[grp];
     const uint64_t below_me = (1ull << sub) - 1ull;
     if (*T.n_dev > 0) {
-        const int n_top = *(const __attribute__((address_space(1))) int32_t *)T.n_top;
-        const uint32_t top = sub < 8 ? ((gu32)T.top)[sub] : 0u;
+        // the first entries: the nodes of the lowest level of at most 64 (lane sub: node
+        // lv_first + sub), their boxes loaded with the seeds and tested against the seeds' best
+        // -- no walk step for the narrow levels above it
+        const int lv_first = ((gi32)T.lv)[0], lv_n = ((gi32)T.lv)[1];
+        const bool in = sub < lv_n;
+        uint32_t code0 = 0;
+        float lb0 = 0.0f;
+        if (in) {
+            const int64_t e = (int64_t)lv_first + sub;
+            double row[D];
+#pragma unroll
+            for (int k = 0; k < D; ++k) row[k] = ((gdbl)(const void *)T.nbox)[e * D + k];
+            code0 = ((gu32)T.nmeta)[e];
+            float bx[2 * D];
+#pragma unroll
+            for (int k = 0; k < D; ++k) {
+                bx[2 * k] = __int_as_float(__double2loint(row[k]));
+                bx[2 * k + 1] = __int_as_float(__double2hiint(row[k]));
+            }
+            lb0 = ct_box_lb<D>(bx, qq, qlo, qhi);
+            ++n_box;
+        }
         ct_seed<D, G>(T, qq, sub, bd, bi, n_pts);
         float bdf = f32_up(bd);
         int isp = 0, lsp = 0;  // inner entries [0, isp), buckets [kStack - lsp, kStack)
         {
-            const bool in = sub < n_top;
-            const bool lf = in && (top & kCtLeafBit);
-            const uint64_t ml = __ballot(lf), mi = __ballot(in && !lf);
-            if (lf) stk[kStack - 1 - __popcll(ml & below_me)] = make_uint2(top, 0u);
-            if (in && !lf) stk[__popcll(mi & below_me)] = make_uint2(top, 0u);
+            const bool keep = in && lb0 <= bdf;
+            const bool lf = keep && (code0 & kCtLeafBit);
+            const uint64_t ml = __ballot(lf), mi = __ballot(keep && !lf);
+            if (lf) stk[kStack - 1 - __popcll(ml & below_me)] = make_uint2(code0, __float_as_uint(lb0));
+            if (keep && !lf) stk[__popcll(mi & below_me)] = make_uint2(code0, __float_as_uint(lb0));
             lsp = __popcll(ml);
             isp = __popcll(mi);
         }
@@ -2179,6 +2211,7 @@ CtJob CellTree::prepare(const double *pts, int64_t n_upper, const int64_t *n_dev
     t.root = &cnt->root;
     t.top = cnt->top;
     t.n_top = &cnt->n_top;
+    t.lv = &cnt->lv_first;
     t.nmeta = nmeta[nw];
     t.nbox = nbox[nw];
     t.bpts = bpts;
