@@ -902,8 +902,7 @@ def config5_summary(c5_256, c5_32=None):
 # time); `c5_*` is config 5 (BASELINE configs[4], the north star's scaling claim: 256 seeds
 # sharded contiguously over the N ranks, strong scaling, the same trees -- c5_seeds_digest -- at
 # every N).  At N = 1 c5_* is the seeds=256 leg, at N > 1 the leg run in the same world.
-SCALING_BASIS = ("value: config 2, one 100k-node blimp tree per rank (weak scaling); c5_value: config 5, "
-                 "256 seeds sharded over the N ranks (strong scaling; c5_seeds_digest equal at every N)")
+SCALING_BASIS = "value: config 2, a 100k tree a rank (weak); c5_*: config 5, 256 seeds over the ranks (strong)"
 
 
 def c5_keys(leg):
