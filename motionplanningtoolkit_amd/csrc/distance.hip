@@ -30,10 +30,11 @@
 namespace mpt {
 
 constexpr int kDistWaves = 4;
-// Tuning constants (measured in round 3 with the run-time knobs since removed):
-// a bucket's queued pairs are evaluated at its end once at least this many wait (1 = after
-// every bucket: 4 % slower on the blimp in the room)
-constexpr int32_t c_dist_flush = 32;
+// Tuning constants (measured in round 3 with the run-time knobs since removed).  Queued pairs
+// are evaluated when 64 wait, at a pass's end and at the seed; round 3 also flushed a bucket's
+// pairs at its end once 32 waited (1 = after every bucket: 4 % slower), which with the queue
+// carried over clusters costs more than it gains (blimp vs room: 16 / 32 / 48 / never: 5.96 /
+// 5.72 / 5.67 / 5.57 ms, profiles/r23/ab/distance_carried_queue.json).
 // the first pass's bound scale (1 = one pass).  Blimp vs room, 65 536 poses, alpha 1 / 0.7 /
 // 0.5 / 0.3: 8.04 / 7.68 / 7.65 / 7.89 ms (triDistance calls 65.2 / 37.0 / 35.7 / 37.3 M); the
 // reference's last submesh 3.81 / 2.43 / 2.38 / 2.55 ms.  Any value in (0, 1] is exact: see
@@ -74,11 +75,16 @@ struct DistCounters {
     uint32_t clusters = 0, items = 0, tri_calls = 0, pair_tests = 0;
 };
 
-// Per-wave LDS: the cluster's mapped agent triangles, the pair queue and the DFS stack
-// (9 KiB a wave: four 4-wave workgroups per CU, i.e. 4 waves per SIMD).
+// Per-wave LDS: the unit's transform, the pair queue and the DFS stack (5 KiB a wave).  The
+// queue holds (env, agent) triangle indices, not a cluster's mapped triangles, so its pairs
+// carry over from one cluster's walk to the next and a flush waits for 64 of them over the
+// clusters (blimp vs room: 10.6 flushes a pose instead of 11.9, one part-full at the end of each
+// cluster's walk; 5.77 vs 5.95 ms, profiles/r23/ab/distance_carried_queue.json); a flush maps
+// its agent triangles again (27 FMAs a lane beside triDistance's ~2000 instructions).
 struct DistLds {
-    double q[kWave][9];        // Q' of the cluster's triangles, by lane
-    int32_t queue[2 * kWave];  // pending (env tri << 6 | agent lane) pairs
+    double rt[12];             // the unit's R (row-major) and T
+    int32_t queue[2 * kWave];  // pending pairs: env triangle
+    int32_t qag[2 * kWave];    // and agent triangle (index into the link's triangles)
     float qgap[2 * kWave];     // their squared box gaps, rounded down (re-tested at the flush)
     int32_t stk_il[kDistStack];  // item << 3 | level (kMaxLevels <= 8)
     float stk_b[kDistStack];
@@ -87,8 +93,8 @@ static_assert(kMaxLevels <= 8, "stack entries pack the level in 3 bits");
 
 // Exact triangle distances of the queued pairs, one pair per lane; returns the new bound.
 template <int kOcc, bool kSel>
-__device__ __forceinline__ double flush_pairs(const EnvDev &env, DistLds &s, int n, int lane, double U,
-                                              unsigned long long *bp, DistCounters &cnt) {
+__device__ __forceinline__ double flush_pairs(const EnvDev &env, const double *atris, DistLds &s, int n, int lane,
+                                              double U, unsigned long long *bp, DistCounters &cnt) {
     double d = DBL_MAX;
     // a pair queued against an older bound is re-tested against the current one (its gap
     // rounded down: never drops a pair the exact test keeps).  This threshold must stay the
@@ -99,10 +105,12 @@ __device__ __forceinline__ double flush_pairs(const EnvDev &env, DistLds &s, int
     const double thr = Un * (1.0 + 1e-9) + 1e-9;
     const bool ev = lane < n && (double)s.qgap[lane] <= thr * thr;
     if (ev) {
-        const int32_t e = s.queue[lane];
-        const double *qa = s.q[e & 63];
-        const EnvTri &E = env.tris[e >> 6];
-        const v3 Q[3] = {mk(qa[0], qa[1], qa[2]), mk(qa[3], qa[4], qa[5]), mk(qa[6], qa[7], qa[8])};
+        const EnvTri &E = env.tris[s.queue[lane]];
+        const double *q = atris + (int64_t)s.qag[lane] * 9;
+        // Q' = R Q + T exactly as the walk mapped the triangle (and as FCL does)
+        const double *R = s.rt, *T = s.rt + 9;
+        const v3 Q[3] = {xform(R, T, mk(q[0], q[1], q[2])), xform(R, T, mk(q[3], q[4], q[5])),
+                         xform(R, T, mk(q[6], q[7], q[8]))};
         const v3 S[3] = {mk(E.P1[0], E.P1[1], E.P1[2]), mk(E.P2[0], E.P2[1], E.P2[2]), mk(E.P3[0], E.P3[1], E.P3[2])};
         // at 4 waves per SIMD the rolled form (128 VGPRs); else the unrolled one
         d = tri_distance<kOcc >= 4 ? 1 : 3, kSel>(S, E.lo, E.hi, Q);
@@ -116,15 +124,16 @@ __device__ __forceinline__ double flush_pairs(const EnvDev &env, DistLds &s, int
     return uniform_d(dmin(U, read_best(bp)));
 }
 
-// Depth-first walk of the env tree for one agent cluster (box cblo/cbhi, lane's triangle
-// box qlo/qhi, Q' in s.q), nearest child first; pairs that survive the exact box-gap test
-// are queued and evaluated 64 at a time.  Returns the updated bound.
+// Depth-first walk of the env tree for one agent cluster (box cblo/cbhi, lane's agent
+// triangle ai with box qlo/qhi), nearest child first; pairs that survive the exact box-gap
+// test are queued (qn pending, left for the next cluster's walk or the pass's end) and
+// evaluated 64 at a time.  Returns the updated bound.
 template <int kOcc, bool kSel>
-__device__ double walk_cluster(const EnvDev &env, DistLds &s, const float cblo[3], const float cbhi[3], bool act,
-                               const double qlo[3], const double qhi[3], const double xlo[3], const double xhi[3],
-                               int lane, double U, unsigned long long *bp, DistCounters &cnt, double alpha,
-                               double lo2) {
-    int sp = 0, qn = 0;
+__device__ double walk_cluster(const EnvDev &env, const double *atris, DistLds &s, int &qn, const float cblo[3],
+                               const float cbhi[3], bool act, int32_t ai, const double qlo[3], const double qhi[3],
+                               const double xlo[3], const double xhi[3], int lane, double U, unsigned long long *bp,
+                               DistCounters &cnt, double alpha, double lo2) {
+    int sp = 0;
     int lev = env.n_levels - 1;
     int32_t first = env.lev_off[lev];
     int32_t count = env.lev_off[lev + 1] - first;
@@ -171,10 +180,11 @@ __device__ double walk_cluster(const EnvDev &env, DistLds &s, const float cblo[3
                     const uint64_t pm = __ballot(act);
                     if (act) {
                         const int pos = (int)__popcll(pm & ((1ull << lane) - 1));
-                        s.queue[pos] = (seed_t << 6) | lane;
+                        s.queue[pos] = seed_t;
+                        s.qag[pos] = ai;
                         s.qgap[pos] = 0.0f;
                     }
-                    U = flush_pairs<kOcc, kSel>(env, s, (int)__popcll(pm), lane, U, bp, cnt);
+                    U = flush_pairs<kOcc, kSel>(env, atris, s, (int)__popcll(pm), lane, U, bp, cnt);
                     if (U == 0.0) return U;
                 }
                 // the bucket's env triangles whose exact box is within the bound of the cluster's
@@ -211,28 +221,22 @@ __device__ double walk_cluster(const EnvDev &env, DistLds &s, const float cblo[3
                     const uint64_t pm = __ballot(pass);
                     if (pass) {
                         const int pos = qn + (int)__popcll(pm & ((1ull << lane) - 1));
-                        s.queue[pos] = (t << 6) | lane;
+                        s.queue[pos] = t;
+                        s.qag[pos] = ai;
                         s.qgap[pos] = __double2float_rd(g2);
                     }
                     qn += (int)__popcll(pm);
                     cnt.pair_tests += (uint32_t)__popcll(__ballot(act));
                     if (qn >= kWave) {
-                        U = flush_pairs<kOcc, kSel>(env, s, kWave, lane, U, bp, cnt);
+                        U = flush_pairs<kOcc, kSel>(env, atris, s, kWave, lane, U, bp, cnt);
                         qn -= kWave;
                         if (lane < qn) {
                             s.queue[lane] = s.queue[kWave + lane];
+                            s.qag[lane] = s.qag[kWave + lane];
                             s.qgap[lane] = s.qgap[kWave + lane];
                         }
                         if (U == 0.0) return U;
                     }
-                }
-                // a bucket's leftover pairs wait for the next bucket's (the walk flushes them at
-                // its end) unless c_dist_flush of them are queued: fewer part-empty flushes
-                // against a bound that is staler by at most one bucket
-                if (qn >= c_dist_flush) {
-                    U = flush_pairs<kOcc, kSel>(env, s, qn, lane, U, bp, cnt);
-                    qn = 0;
-                    if (U == 0.0) return U;
                 }
             }
         } else if (m) {
@@ -268,10 +272,7 @@ __device__ double walk_cluster(const EnvDev &env, DistLds &s, const float cblo[3
                 break;
             }
         }
-        if (!found) {
-            if (qn > 0) U = flush_pairs<kOcc, kSel>(env, s, qn, lane, U, bp, cnt);
-            return U;
-        }
+        if (!found) return U;  // the pending pairs wait for the next cluster's
     }
 }
 
@@ -289,12 +290,19 @@ __device__ void distance_unit(const EnvDev &env, const AgentDev *__restrict__ li
     double U = uniform_d(read_best(bp));
     if (U == 0.0) return;  // defaultDistanceFunction stops at dist <= 0
 
-    double R[9], T[3];
-    unit_transform(env, w.poses + (slot * L + link) * 12, R, T);
+    {
+        double R[9], T[3];
+        unit_transform(env, w.poses + (slot * L + link) * 12, R, T);
+        if (lane == 0) {
 #pragma unroll
-    for (int i = 0; i < 9; ++i) R[i] = uniform_d(R[i]);
+            for (int i = 0; i < 9; ++i) s.rt[i] = R[i];
 #pragma unroll
-    for (int i = 0; i < 3; ++i) T[i] = uniform_d(T[i]);
+            for (int i = 0; i < 3; ++i) s.rt[9 + i] = T[i];
+        }
+    }
+    const double *R = s.rt, *T = s.rt + 9;
+    const double *atris = ag.tris;
+    int qn = 0;  // pending pairs, carried from one cluster's walk to the next
     const int top = env.n_levels - 1;
     const int32_t tfirst = env.lev_off[top], tcount = env.lev_off[top + 1] - tfirst;
 
@@ -344,18 +352,13 @@ __device__ void distance_unit(const EnvDev &env, const AgentDev *__restrict__ li
             }
             const Cluster c = ag.clusters[cbase + j];
             const bool act = lane < c.count;
+            const int32_t ai = c.first + lane;
             double qlo[3] = {0, 0, 0}, qhi[3] = {0, 0, 0};
             if (act) {
-                const double *t = ag.tris + (int64_t)(c.first + lane) * 9;
+                const double *t = ag.tris + (int64_t)ai * 9;
                 v3 Q[3];
 #pragma unroll
                 for (int k = 0; k < 3; ++k) Q[k] = xform(R, T, mk(t[3 * k], t[3 * k + 1], t[3 * k + 2]));
-#pragma unroll
-                for (int k = 0; k < 3; ++k) {
-                    s.q[lane][3 * k] = Q[k].x;
-                    s.q[lane][3 * k + 1] = Q[k].y;
-                    s.q[lane][3 * k + 2] = Q[k].z;
-                }
                 qlo[0] = dmin(Q[0].x, dmin(Q[1].x, Q[2].x));
                 qlo[1] = dmin(Q[0].y, dmin(Q[1].y, Q[2].y));
                 qlo[2] = dmin(Q[0].z, dmin(Q[1].z, Q[2].z));
@@ -370,8 +373,14 @@ __device__ void distance_unit(const EnvDev &env, const AgentDev *__restrict__ li
                 xlo[k] = uniform_d(wave_min_f64_dpp(act ? qlo[k] : DBL_MAX));
                 xhi[k] = uniform_d(wave_max_f64_dpp(act ? qhi[k] : -DBL_MAX));
             }
-            U = walk_cluster<kOcc, kSel>(env, s, cblo, cbhi, act, qlo, qhi, xlo, xhi, lane, U, bp, cnt, alpha,
-                                         pass == 1 && ((first_walked >> j) & 1) ? lo2 : -1.0);
+            U = walk_cluster<kOcc, kSel>(env, atris, s, qn, cblo, cbhi, act, ai, qlo, qhi, xlo, xhi, lane, U, bp, cnt,
+                                         alpha, pass == 1 && ((first_walked >> j) & 1) ? lo2 : -1.0);
+            if (U == 0.0) return;
+        }
+        // every pair of the pass evaluated before the next (the second pass's lo2 relies on it)
+        if (qn > 0) {
+            U = flush_pairs<kOcc, kSel>(env, atris, s, qn, lane, U, bp, cnt);
+            qn = 0;
             if (U == 0.0) return;
         }
         if (pass == 0 && npass == 2) {

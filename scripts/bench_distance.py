@@ -57,9 +57,14 @@ def distance_roofline(out, a, n_agent, n_env, ms):
     if c:
         try:
             summ = json.load(open(c[-1]))
-            tr = next(v["hbm_bytes_per_launch"] for k, v in summ.items() if "k_distance" in k)
+            kd = next(v for k, v in summ.items() if "k_distance" in k)
+            tr = kd["hbm_bytes_per_launch"]
             roof.update({"traffic": int(tr), "frac_hbm_measured": round(tr / t / 1e9 / HBM_PEAK_GBS, 4),
                          "traffic_over_compulsory": round(tr / comp, 2), "pmc_source": os.path.relpath(c[-1], REPO)})
+            if kd.get("steady_us"):
+                # the same fraction on the profile's own steady-state launch time
+                roof.update({"profile_us_per_launch": kd["steady_us"],
+                             "frac_from_profile": round(roof["frac"] * ms * 1e3 / kd["steady_us"], 4)})
         except (OSError, ValueError, StopIteration):
             pass
     return roof

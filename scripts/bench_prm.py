@@ -65,6 +65,11 @@ def sweep_roofline(w, ms, n_agent, n_env, n_milestones, traffic_path):
         if not parts:
             raise StopIteration
         tr = sum(parts)
+        # the stage's kernel time in the same profile (steady_us: the timed call's launches)
+        prof_us = sum(v["steady_us"] * v.get("steady_launches", 1) for k, v in summ.items()
+                      if "k_sweep" in k and v.get("steady_us"))
+        if prof_us > 0:
+            out["profile_us_per_launch"] = round(prof_us, 3)
         out.update({"traffic": int(tr), "traffic_gbs": round(tr / t / 1e9, 1),
                     "frac_hbm_measured": round(tr / t / 1e9 / HBM_PEAK_GBS, 4),
                     "traffic_over_compulsory": round(tr / comp, 2), "pmc_source": os.path.relpath(path, REPO)})
@@ -73,6 +78,9 @@ def sweep_roofline(w, ms, n_agent, n_env, n_milestones, traffic_path):
     if out["frac"] < max(out["frac_hbm_compulsory"], out.get("frac_hbm_measured") or 0.0):
         out.update({"bound": "hbm", "achieved": out["compulsory_gbs"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
                     "frac": out["frac_hbm_compulsory"]})
+    if out.get("profile_us_per_launch"):
+        # the same fraction on the profile's own kernel time (the line's is the stage's hipEvents)
+        out["frac_from_profile"] = round(out["frac"] * ms * 1e3 / out["profile_us_per_launch"], 4)
     return out
 
 
