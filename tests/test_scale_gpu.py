@@ -6,7 +6,7 @@
   oracle's AABB-tree collider (on the device's own poses), and the ordered append.
 * Config 3: the same at the snake leg's shape (100 000-node 15-dim tree, 11 links, corridor).
 * Config 2, collision-heavy variant (`bench.py --workload blimp-room`): tree and samples
-  inside the room, so every unit reaches the narrow phase.
+  inside the room, so every unit reaches the narrow phase; all 65 536 verdicts checked.
 * Config 4: the 25 x 25-room environment (197 500 triangles, a four-level env tree that does
   not fit the k_pairs LDS stage) with 100 000 milestones over the whole multi-room extent:
   the roadmap of a milestone prefix against orc_prm_radius (edges, verdicts), the full edge
@@ -89,11 +89,12 @@ def test_config3_full_round(mpt_gpu, oracle):
 
 
 def test_config2_room_full_round(mpt_gpu, oracle):
-    """The collision-heavy variant: every pose inside the room's box."""
+    """The collision-heavy variant: every pose inside the room's box; the verdicts of all
+    65 536 extensions against the oracle (every unit reaches the narrow phase here)."""
     sc = scenes.blimp_room_scenario()
     seed = 1000
     tree = np.random.default_rng(seed).uniform(sc.ranges[:, 0], sc.ranges[:, 1], size=(100_000, sc.dim))
-    v = _engine_round_check(mpt_gpu, oracle, sc, tree, 65_536, seed)
+    v = _engine_round_check(mpt_gpu, oracle, sc, tree, 65_536, seed, n_sample=65_536)
     assert v.mean() > 0.05  # a real collision workload
 
 
