@@ -162,3 +162,27 @@ def test_distance_agrees_with_collision(mpt_gpu):
     assert np.all(d[v == 1] <= 1e-9)
     assert np.all(v[d > 1e-6] == 0)
     assert 0.05 < v.mean() < 0.95
+
+
+def test_bench_shape_batch(mpt_gpu, oracle):
+    """The distance leg's own workload (scripts/bench_distance.py): the full blimp (1355 tris) at
+    65 536 poses (rotation about z, as Blimp::stateToFCLTransform makes them) in and around the
+    room, one pose an edge, in one batch; the first 16 384 distances against the oracle, bitwise."""
+    rng = np.random.default_rng(0)  # bench_distance.py's seed and pose generator
+    n = 65_536
+    t = rng.uniform([-30, -30, -30], [207, 168, 144], size=(n, 3))
+    th = rng.uniform(0, 2 * math.pi, n)
+    c, s = np.cos(th), np.sin(th)
+    P = np.zeros((n, 12))
+    P[:, 0], P[:, 1], P[:, 3], P[:, 4], P[:, 8] = c, s, -s, c, 1.0
+    P[:, 9:] = t
+    env_t = scenes.read_obj(scenes.mesh_path("env_model"))
+    agent_t = scenes.read_obj(scenes.mesh_path("agent_blimp"), "all")
+    env, ag = mpt_gpu.Environment(env_t), mpt_gpu.AgentMesh(agent_t)
+    got = mpt_gpu.distance_batch(env, [ag], P.reshape(-1, 1, 12), np.arange(n + 1))
+    k = 16_384
+    ref = oracle.distance_batch(env_t, pose([0, 0, 0]), [agent_t], P[:k].reshape(-1, 1, 12), np.arange(k + 1),
+                                nthreads=16)
+    bad = np.nonzero(bits(got[:k]) != bits(ref))[0]
+    assert bad.size == 0, (bad[:10], got[bad[:10]], ref[bad[:10]])
+    assert (got == 0).any() and (got > 1).any() and np.isfinite(got).all()
