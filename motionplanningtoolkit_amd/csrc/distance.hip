@@ -299,6 +299,7 @@ __device__ void distance_unit(const EnvDev &env, const AgentDev *__restrict__ li
 #pragma unroll
             for (int i = 0; i < 3; ++i) s.rt[9 + i] = T[i];
         }
+        __builtin_amdgcn_wave_barrier();  // lane 0's stores before every lane's reads (one wave's LDS)
     }
     const double *R = s.rt, *T = s.rt + 9;
     const double *atris = ag.tris;
